@@ -1,0 +1,96 @@
+"""Loader for libpcabi.so, the MI355X adapter-alignment engine (C ABI: include/pcabi.h).
+
+There is deliberately no CPU fallback: if the library or a gfx950 device is missing, compute
+entry points raise PcabiError. The CPU restatement under oracle/ is test infrastructure only.
+
+HIP runtime sharing: PyTorch-ROCm wheels bundle their own libamdhip64.so.7. If torch is already
+imported (the multi-GPU path uses torch.distributed/RCCL), loading libpcabi.so after it binds
+to the SAME runtime (identical SONAME), so one process never holds two HIP runtimes. Import
+torch before this module whenever both are used (bench.py and parallel.py do).
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('PCABI_LIB', os.path.join(_HERE, 'libpcabi.so'))
+
+NFIELDS = 8
+F_RS, F_RE, F_AS, F_AE, F_SCORE, F_M, F_L1, F_L2 = range(8)
+
+
+class PcabiError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Return the loaded ctypes library (loads and declares signatures on first use)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.isfile(LIB_PATH):
+        raise PcabiError('libpcabi.so not found at %s - run __graft_entry__.build() '
+                         '(hipcc --offload-arch=gfx950)' % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    c_int, c_i64, c_p, c_d = ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_double
+    sig = {
+        'adapterAlignment': ([ctypes.c_char_p, ctypes.c_char_p, c_int, c_int, c_int, c_int], c_p),
+        'freeCString': ([c_p], None),
+        'pcabi_last_error': ([], ctypes.c_char_p),
+        'pcabi_version': ([], c_int),
+        'pcabi_device_count': ([], c_int),
+        'pcabi_max_adapter_len': ([], c_int),
+        'pcabi_max_window_len': ([], c_int),
+        'pcabi_encode_dna5': ([c_p, c_p, c_i64], None),
+        'pcabi_pid6_host': ([c_p, c_p, c_i64, c_p], None),
+        'pcabi_align_host': ([c_int, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_p, ctypes.c_int32,
+                              c_p, c_p, c_i64, c_int, c_int, c_int, c_int, c_p], c_int),
+        'pcabi_dev_set': ([c_int], c_int),
+        'pcabi_dev_malloc': ([ctypes.POINTER(c_p), c_i64], c_int),
+        'pcabi_dev_free': ([c_p], c_int),
+        'pcabi_dev_h2d': ([c_p, c_p, c_i64], c_int),
+        'pcabi_dev_d2h': ([c_p, c_p, c_i64], c_int),
+        'pcabi_dev_memset': ([c_p, c_int, c_i64], c_int),
+        'pcabi_dev_sync': ([], c_int),
+        'pcabi_stream_create': ([ctypes.POINTER(c_p)], c_int),
+        'pcabi_stream_destroy': ([c_p], c_int),
+        'pcabi_stream_sync': ([c_p], c_int),
+        'pcabi_event_create': ([ctypes.POINTER(c_p)], c_int),
+        'pcabi_event_destroy': ([c_p], c_int),
+        'pcabi_event_record': ([c_p, c_p], c_int),
+        'pcabi_event_elapsed_ms': ([ctypes.POINTER(ctypes.c_float), c_p, c_p], c_int),
+        'pcabi_adapters_create': ([c_p, c_p, c_p, ctypes.c_int32, ctypes.POINTER(c_p)], c_int),
+        'pcabi_adapters_destroy': ([c_p], None),
+        'pcabi_align_cross_dev': ([c_p, c_p, c_p, c_i64, c_p, c_int, c_int, c_int, c_int, c_p, c_i64,
+                                   c_p], c_int),
+        'pcabi_end_trim_dev': ([c_p, c_i64, ctypes.c_int32, c_p, c_i64, ctypes.c_int32, c_i64, c_int,
+                                c_int, c_d, c_int, c_p, c_p, c_p, c_p, c_p], c_int),
+        'pcabi_best_full_identity_dev': ([c_p, c_i64, c_i64, ctypes.c_int32, c_p, c_p], c_int),
+    }
+    for name, (argtypes, restype) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = argtypes
+        fn.restype = restype
+    _lib = L
+    return L
+
+
+def exported_symbols():
+    """Names every ABI entry point declared in include/pcabi.h (checked by tests)."""
+    lib()
+    return ['adapterAlignment', 'freeCString', 'pcabi_last_error', 'pcabi_version',
+            'pcabi_device_count', 'pcabi_max_adapter_len', 'pcabi_max_window_len',
+            'pcabi_encode_dna5', 'pcabi_pid6_host', 'pcabi_align_host', 'pcabi_dev_set',
+            'pcabi_dev_malloc', 'pcabi_dev_free', 'pcabi_dev_h2d', 'pcabi_dev_d2h',
+            'pcabi_dev_memset', 'pcabi_dev_sync', 'pcabi_stream_create', 'pcabi_stream_destroy',
+            'pcabi_stream_sync', 'pcabi_event_create', 'pcabi_event_destroy', 'pcabi_event_record',
+            'pcabi_event_elapsed_ms', 'pcabi_adapters_create', 'pcabi_adapters_destroy',
+            'pcabi_align_cross_dev', 'pcabi_end_trim_dev', 'pcabi_best_full_identity_dev']
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().pcabi_last_error()
+        raise PcabiError('%s failed (%d): %s' % (what, rc, msg.decode() if msg else ''))

@@ -1,0 +1,313 @@
+// pcabi_dp.h -- per-lane semi-global Gotoh DP with forward traceback-attribute propagation.
+//
+// This is the arithmetic core of the MI355X adapter-alignment engine. One invocation aligns ONE
+// read window (horizontal sequence, columns j = 1..n) against ONE adapter (vertical sequence,
+// rows i = 1..L) and produces exactly the integers the reference's ScoredAlignment derives from
+// its gapped rows (porechop_abi/src/alignment.cpp:6-110), WITHOUT a trace matrix and WITHOUT a
+// traceback walk:
+//
+//   * The reference runs SeqAn globalAlignment with free end gaps on all four sides
+//     (porechop_abi/src/adapter_align.cpp:26-27), Gotoh when gap_open != gap_extend and linear
+//     otherwise (S/align/global_alignment_unbanded.h:213-221), then walks the trace matrix back
+//     from the first maximum of the last row / last column (S/align/dp_scout.h:175,
+//     S/align/dp_traceback_impl.h:379-548).
+//   * The walk's predecessor of every (cell, state) is a LOCAL function of that cell's trace bits
+//     (D / V-ext / V-open / H-ext / H-open / MAX_FROM_V|H, tie rules of S/align/dp_formula.h:153-163).
+//     So every state can carry forward the few attributes of "the path the traceback would take
+//     from here": its start cell (i0, j0), its match count m and its diagonal count nD. They are
+//     packed in one 32-bit word and selected with the same predicates that select the scores.
+//   * The end-of-path details (trailing gap run length and whether a diagonal precedes it) only
+//     matter in the last row / last column and are kept as O(1) running values there.
+//   * ScoredAlignment's st/en/a0/a1/identities reduce to closed forms of those values
+//     (finish(), documented in DESIGN.md §3 and fuzzed against the oracle in tests/).
+//
+// The code is plain C++ usable on the host (tests fuzz it against oracle/) and on the device,
+// where one wave64 lane owns one (window, adapter) pair and the adapter is wave-uniform
+// (SGPR-resident), so every instruction is a full-width VALU op with no cross-lane traffic.
+//
+// (S/ = porechop_abi/include/seqan/ of the reference.)
+#pragma once
+
+#include <stdint.h>
+
+#ifdef __HIPCC__
+#define PCABI_HD __host__ __device__ __forceinline__
+#else
+#define PCABI_HD inline
+#endif
+
+namespace pcabi {
+
+// SeqAn's DPCellDefaultInfinity is INT_MIN/2 (S/align/dp_cell.h:144-145). Any value far below
+// every reachable score behaves identically under max/compare: a NEG-derived candidate never
+// wins and never ties (|scores| <= 2^20 for all supported sizes).
+constexpr int NEG = -(1 << 28);
+
+// Attribute word: [ c + CBIAS : 16 ][ m : 8 ][ nD : 8 ]
+//   c  = j0 - i0  (path start cell; at least one of i0, j0 is zero)
+//   m  = matching diagonal columns on the path, nD = diagonal columns on the path
+constexpr int ATTR_B = 8;
+constexpr uint32_t ATTR_MASK = (1u << ATTR_B) - 1u;
+constexpr int ATTR_CSH = 2 * ATTR_B;
+constexpr int ATTR_CBIAS = 255;            // c >= -L >= -255
+constexpr int MAX_ADAPTER_LEN = 255;       // m, nD <= L fit 8 bits
+constexpr int MAX_WINDOW_LEN = 65535 - ATTR_CBIAS;
+constexpr uint32_t INC_D = 1u;                           // mismatching diagonal
+constexpr uint32_t INC_M = (1u << ATTR_B) + 1u;          // matching diagonal
+
+PCABI_HD uint32_t attr_start(int c) { return (uint32_t)(c + ATTR_CBIAS) << ATTR_CSH; }
+
+// last-column types of a path
+enum : int { LT_NONE = 0, LT_D = 1, LT_V = 2, LT_H = 3 };
+
+struct Scoring {
+    int ma, mi, go, ge;  // match, mismatch, gap open, gap extend (Python order)
+};
+
+// What the scout keeps for the current best end cell.
+struct Best {
+    int score;
+    int bi, bj;      // end cell (row in adapter coordinates 0..L, column 0..n)
+    uint32_t attr;   // attributes of the path of the corrected end state
+    int ltype;       // last path column type (LT_*)
+    int trail;       // length of the trailing gap run (only meaningful when it is used)
+    int precd;       // 1 if the column before the trailing run is diagonal
+};
+
+// Final integers, same meaning as ScoredAlignment + the two identity fractions m/l1, m/l2.
+struct Result {
+    int rs, re, as, ae, score, m, l1, l2;
+};
+
+// Closed forms of ScoredAlignment (porechop_abi/src/alignment.cpp:27-109) in terms of the path.
+// Derivation in DESIGN.md §3. bi/bj: end cell, L/n: sequence lengths.
+PCABI_HD Result finish(const Best &b, int L, int n) {
+    Result r;
+    const int c = (int)(b.attr >> ATTR_CSH) - ATTR_CBIAS;
+    const int m = (int)((b.attr >> ATTR_B) & ATTR_MASK);
+    const int nd = (int)(b.attr & ATTR_MASK);
+    const int i0 = c < 0 ? -c : 0;
+    const int j0 = c > 0 ? c : 0;
+    const int h = i0 + j0;                             // head length == first path column
+    const int K = (b.bi - i0) + (b.bj - j0) - nd;      // path columns
+    const bool tailA = b.bi < L;                       // adapter tail after the path
+    const bool tailR = b.bj < n;                       // read tail after the path
+    const int trailV = b.ltype == LT_V ? b.trail : 0;
+    const int trailH = b.ltype == LT_H ? b.trail : 0;
+    const int lastD = b.ltype == LT_D ? 1 : 0;
+    const int kR = K - 1 - trailV;                     // last path column holding a read base
+    const int kA = K - 1 - trailH;                     // last path column holding an adapter base
+    bool readSide;
+    if (tailA) readSide = true;
+    else if (tailR) readSide = false;
+    else readSide = (kR <= kA);
+    int ek;
+    if (readSide) {
+        ek = kR;
+        r.re = b.bj - 1;
+        r.ae = b.bi - trailV - (trailV > 0 ? b.precd : lastD);
+    } else {
+        ek = kA;
+        r.ae = b.bi - 1;
+        r.re = b.bj - trailH - (trailH > 0 ? b.precd : lastD);
+    }
+    r.rs = j0;
+    r.as = i0;
+    r.score = b.score;
+    r.m = m;
+    r.l1 = ek + 1;
+    const int a0 = j0 > 0 ? h : 0;
+    const int a1 = tailA ? (h + K + (L - b.bi) - 1) : (h + kA);
+    r.l2 = a1 - a0 + 1;
+    return r;
+}
+
+// The reference prints 100.0*m/l with "%f" (std::to_string, porechop_abi/src/alignment.cpp:118-119)
+// and Python parses it back (porechop_abi/nanopore_read.py:497-498). pid6 returns the same
+// double: d = (100.0*m)/l (IEEE, as in alignment.cpp:82,89), round d*1e6 to an integer with
+// round-half-even on its EXACT value (fma residual), then q/1e6 correctly rounded -- which is
+// what both printf and Python's float() do. l == 0 -> NaN (the reference's "-nan").
+PCABI_HD double pid6(int m, int l) {
+    if (l == 0) return __builtin_nan("");
+    const double d = (100.0 * (double)m) / (double)l;
+    const double p = d * 1e6;
+    const double e = __builtin_fma(d, 1e6, -p);   // d*1e6 == p + e exactly
+    double k = __builtin_rint(p);                 // half-even on p
+    const double f = p - k;                       // exact
+    if (f == 0.5 && e > 0.0) k += 1.0;
+    else if (f == -0.5 && e < 0.0) k -= 1.0;
+    return k / 1e6;
+}
+
+// Trailing-run bookkeeping when a gap state opens from an S-state whose last column type is
+// `slt` (and whose own trailing run of the same gap kind is (t, p) when slt == same kind).
+PCABI_HD void open_run(int slt, int same_kind, int t_prev, int p_prev, int &t, int &p) {
+    if (slt == same_kind) { t = t_prev + 1; p = p_prev; }
+    else { t = 1; p = (slt == LT_D) ? 1 : 0; }
+}
+
+// ------------------------------------------------------------------------------------------
+// align_lane<RPL, AFFINE>: rows live in registers (RPL compile-time slots). The adapter occupies
+// slots off+1..RPL (off = RPL - L, "top padding"): slots <= off are skipped by a branch that is
+// uniform across a wave (all lanes share the adapter), and the running "up" values entering
+// slot off+1 are exactly the free-end-gap boundary row, so padding costs nothing.
+//
+//   rd(j)  : read code at column j (1-based), 0..4
+//   adp[s] : adapter code of slot s (1-based; slots off+1..RPL), 0..4
+// ------------------------------------------------------------------------------------------
+template <int RPL, bool AFFINE, typename ReadFn, typename AdpFn>
+PCABI_HD Result align_lane(ReadFn rd, int n, AdpFn adp, int L, const Scoring sc) {
+    const int off = RPL - L;
+    int S[RPL + 1], H[RPL + 1];
+    uint32_t SA[RPL + 1], HA[RPL + 1];
+#pragma unroll
+    for (int s = 1; s <= RPL; ++s) {
+        S[s] = 0;
+        H[s] = NEG;
+        SA[s] = attr_start(-(s - off));
+        HA[s] = 0;
+    }
+
+    Best best;
+    best.score = 0;          // first scouted cell: (L, 0), S = 0 (S/align/dp_meta_info.h:204-216)
+    best.bi = L;
+    best.bj = 0;
+    best.attr = attr_start(-L);
+    best.ltype = LT_NONE;
+    best.trail = 0;
+    best.precd = 0;
+
+    // last-row running state: S-state last type of (L, j-1) and H-state trailing run (t, p)
+    int slt_last = LT_NONE, ht_last = 0, hp_last = 0;
+
+    for (int j = 1; j <= n; ++j) {
+        const int r = rd(j);
+        const bool lastcol = (j == n);
+        int sup = 0, vup = NEG, sdg = 0;
+        uint32_t saup = attr_start(j), vaup = 0, sadg = attr_start(j - 1);
+        // last-column running state: S-state last type of (i-1, n), V-state run (t, p)
+        int slt_up = LT_NONE, vt_up = 0, vp_up = 0;
+        // last-row cell products, kept for the row-L scout / running state
+        int lv = NEG, lh = NEG, ls = 0, lt_type = LT_NONE;
+        bool l_hext = false;
+        uint32_t lva = 0, lha = 0, lsa = 0;
+#pragma unroll
+        for (int s = 1; s <= RPL; ++s) {
+            if (s > off) {
+                const bool match = (r == adp(s));
+                const int diag = sdg + (match ? sc.ma : sc.mi);
+                const uint32_t da = sadg + (match ? INC_M : INC_D);
+                int hn, vn, g, sn;
+                uint32_t han, van, ga, san;
+                bool hext, vext, fromv, isd;
+                if (AFFINE) {
+                    const int hx = H[s] + sc.ge, ho = S[s] + sc.go;
+                    hext = !(hx < ho);
+                    hn = hext ? hx : ho;
+                    han = hext ? HA[s] : SA[s];
+                    const int vx = vup + sc.ge, vo = sup + sc.go;
+                    vext = !(vx < vo);
+                    vn = vext ? vx : vo;
+                    van = vext ? vaup : saup;
+                    fromv = !(vn < hn);
+                    g = fromv ? vn : hn;
+                    ga = fromv ? van : han;
+                } else {
+                    hext = false;
+                    vext = false;
+                    const int vv = sup + sc.ge, hh = S[s] + sc.ge;
+                    fromv = !(vv < hh);
+                    g = fromv ? vv : hh;
+                    ga = fromv ? saup : SA[s];
+                    hn = NEG; vn = NEG; han = 0; van = 0;
+                }
+                isd = !(diag < g);
+                sn = isd ? diag : g;
+                san = isd ? da : ga;
+                const int slt = isd ? LT_D : (fromv ? LT_V : LT_H);
+
+                if (lastcol) {
+                    // V run of this cell's V-state (affine) / S-state-from-V (linear)
+                    int vt, vp;
+                    if (AFFINE) {
+                        if (vext) { vt = vt_up + 1; vp = vp_up; }
+                        else open_run(slt_up, LT_V, vt_up, vp_up, vt, vp);
+                    } else {
+                        open_run(slt_up, LT_V, vt_up, vp_up, vt, vp);
+                    }
+                    if (s < RPL && sn > best.score) {   // last column, rows 1..L-1
+                        best.score = sn; best.bi = s - off; best.bj = n;
+                        if (AFFINE) {
+                            if (vn == sn)      { best.attr = van; best.ltype = LT_V; best.trail = vt; best.precd = vp; }
+                            else if (hn == sn) { best.attr = han; best.ltype = LT_H; best.trail = 0; best.precd = 0; }
+                            else               { best.attr = san; best.ltype = LT_D; best.trail = 0; best.precd = 0; }
+                        } else {
+                            best.attr = san; best.ltype = slt;
+                            best.trail = (slt == LT_V) ? vt : 0; best.precd = (slt == LT_V) ? vp : 0;
+                        }
+                    }
+                    // running V-run state for the next row: V-state (affine) or S-state (linear)
+                    if (AFFINE) {
+                        // S-state of this cell, as seen by an opening V below it:
+                        //   slt == LT_V: S path == V path -> carries (vt, vp)
+                        vt_up = vt; vp_up = vp;
+                    } else {
+                        if (slt == LT_V) { vt_up = vt; vp_up = vp; }
+                        else { vt_up = 0; vp_up = 0; }
+                    }
+                    slt_up = slt;
+                }
+                if (s == RPL) {
+                    lv = vn; lh = hn; ls = sn; lva = van; lha = han; lsa = san;
+                    lt_type = slt; l_hext = hext;
+                }
+                sdg = S[s];
+                sadg = SA[s];
+                S[s] = sn;
+                H[s] = hn;
+                SA[s] = san;
+                HA[s] = han;
+                sup = sn;
+                vup = vn;
+                saup = san;
+                vaup = van;
+                // In the AFFINE V-run chain the next row needs the V-state run of THIS cell
+                // (vt_up/vp_up above) and this cell's S type (slt_up): an extending V continues
+                // the V-state run, an opening V starts from the S-state (same run iff slt==V).
+            }
+        }
+
+        // ---- row L (the adapter's last row): H-state run and scout ----
+        int ht, hp;
+        if (AFFINE) {
+            if (l_hext) { ht = ht_last + 1; hp = hp_last; }
+            else open_run(slt_last, LT_H, ht_last, hp_last, ht, hp);
+        } else {
+            open_run(slt_last, LT_H, ht_last, hp_last, ht, hp);
+        }
+        if (ls > best.score) {   // last row, columns 1..n-1 in order; (L, n) ends the last column
+            best.score = ls; best.bi = L; best.bj = j;
+            int vt = 0, vp = 0;
+            if (lastcol) { vt = vt_up; vp = vp_up; }
+            if (AFFINE) {
+                if (lv == ls)      { best.attr = lva; best.ltype = LT_V; best.trail = vt; best.precd = vp; }
+                else if (lh == ls) { best.attr = lha; best.ltype = LT_H; best.trail = ht; best.precd = hp; }
+                else               { best.attr = lsa; best.ltype = LT_D; best.trail = 0; best.precd = 0; }
+            } else {
+                best.attr = lsa; best.ltype = lt_type;
+                best.trail = (lt_type == LT_V) ? vt : (lt_type == LT_H ? ht : 0);
+                best.precd = (lt_type == LT_V) ? vp : (lt_type == LT_H ? hp : 0);
+            }
+        }
+        if (AFFINE) {
+            ht_last = ht; hp_last = hp;
+        } else {
+            if (lt_type == LT_H) { ht_last = ht; hp_last = hp; }
+            else { ht_last = 0; hp_last = 0; }
+        }
+        slt_last = lt_type;
+    }
+    return finish(best, L, n);
+}
+
+}  // namespace pcabi

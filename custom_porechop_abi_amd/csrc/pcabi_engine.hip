@@ -1,0 +1,657 @@
+// pcabi_engine.hip -- gfx950 kernels + C ABI of the adapter-alignment engine (include/pcabi.h).
+//
+// Kernel map:
+//   k_align_cross<RPL, AFFINE>  one wave64 = 64 windows x ONE adapter (wave-uniform, SGPRs);
+//                               one lane = one (window, adapter) DP, rows in VGPRs
+//                               (pcabi_dp.h). VALU-bound integer work, no LDS, no shuffles.
+//   k_align_pairs<RPL, AFFINE>  same, work given as explicit (window, adapter) pairs grouped
+//                               by adapter into waves on the host.
+//   k_end_trim                  per-read decision epilogue (nanopore_read.py:175-217).
+//   k_best_full_id              per-adapter max of the full-adapter identity
+//                               (nanopore_read.py:158-173), deterministic (max is exact).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/pcabi.h"
+#include "pcabi_dp.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            return fail(PCABI_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+// Register buckets: adapters of length L run in the smallest bucket RPL >= L.
+constexpr int kBuckets[] = {8, 16, 24, 32, 48, 64, 96, 128};
+constexpr int kNumBuckets = sizeof(kBuckets) / sizeof(kBuckets[0]);
+constexpr int kMaxRPL = 128;
+
+int bucket_of(int L) {
+    for (int b = 0; b < kNumBuckets; ++b)
+        if (L <= kBuckets[b]) return b;
+    return -1;
+}
+
+struct KParams {
+    const uint8_t *codes;
+    const int64_t *win_off;
+    const int32_t *win_len;
+    int64_t n_win;
+    // bucket-local adapter table: RPL bytes per adapter, top padded (slot s-1 <-> byte s-1)
+    const uint32_t *adp_pad;
+    const int32_t *adp_len;
+    const int32_t *adp_id;     // global adapter index (result row in cross mode)
+    int32_t n_adp;
+    // pairs mode
+    const int32_t *task_win;   // [n_waves*64], -1 = idle lane
+    const int32_t *task_out;   // [n_waves*64] result index
+    const int32_t *wave_adp;   // [n_waves] bucket-local adapter
+    int64_t n_waves;
+    int32_t *out;
+    int64_t out_stride;
+    pcabi::Scoring sc;
+};
+
+// Streams one window's Dna5 codes 4 bytes at a time (window offsets are 4-byte aligned).
+struct WindowReader {
+    const uint32_t *p;
+    uint32_t cur, nxt;
+    __device__ __forceinline__ explicit WindowReader(const uint8_t *base) {
+        p = reinterpret_cast<const uint32_t *>(base);
+        cur = 0;
+        nxt = p[0];
+    }
+    __device__ __forceinline__ int operator()(int j) {
+        const int k = j - 1;
+        if ((k & 3) == 0) {
+            cur = nxt;
+            nxt = p[(k >> 2) + 1];   // prefetch; buffers carry >= 16 bytes of padding
+        }
+        return (int)((cur >> (8 * (k & 3))) & 0xFFu);
+    }
+};
+
+template <int RPL>
+struct AdapterRegs {
+    uint32_t w[RPL / 4];
+    __device__ __forceinline__ void load(const uint32_t *src) {
+#pragma unroll
+        for (int k = 0; k < RPL / 4; ++k) w[k] = __builtin_amdgcn_readfirstlane(src[k]);
+    }
+    __device__ __forceinline__ int operator()(int s) const {   // s: 1-based slot, compile-time
+        return (int)((w[(s - 1) >> 2] >> (8 * ((s - 1) & 3))) & 0xFFu);
+    }
+};
+
+__device__ __forceinline__ void store_result(int32_t *out, int64_t stride, int64_t idx,
+                                             const pcabi::Result &r) {
+    out[0 * stride + idx] = r.rs;
+    out[1 * stride + idx] = r.re;
+    out[2 * stride + idx] = r.as;
+    out[3 * stride + idx] = r.ae;
+    out[4 * stride + idx] = r.score;
+    out[5 * stride + idx] = r.m;
+    out[6 * stride + idx] = r.l1;
+    out[7 * stride + idx] = r.l2;
+}
+
+__device__ __forceinline__ pcabi::Result empty_result() {
+    pcabi::Result r;
+    r.rs = -1; r.re = 0; r.as = -1; r.ae = 0;
+    r.score = (int)0x80000000; r.m = 0; r.l1 = 0; r.l2 = 0;
+    return r;
+}
+
+template <int RPL, bool AFFINE>
+__device__ __forceinline__ void run_lane(const KParams &p, int a_local, int64_t w, int64_t out_idx) {
+    AdapterRegs<RPL> adp;
+    adp.load(p.adp_pad + (int64_t)a_local * (RPL / 4));
+    const int L = __builtin_amdgcn_readfirstlane(p.adp_len[a_local]);
+    if (w < 0) return;
+    const int n = p.win_len[w];
+    pcabi::Result r;
+    if (n <= 0) {
+        r = empty_result();
+    } else {
+        WindowReader rd(p.codes + p.win_off[w]);
+        r = pcabi::align_lane<RPL, AFFINE>(rd, n, adp, L, p.sc);
+    }
+    store_result(p.out, p.out_stride, out_idx, r);
+}
+
+// grid: x = ceil(n_win / 256) window blocks (4 waves x 64 windows), y = bucket adapters
+template <int RPL, bool AFFINE>
+__global__ __launch_bounds__(256) void k_align_cross(KParams p) {
+    const int a_local = blockIdx.y;
+    const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int a_glob = p.adp_id[a_local];
+    const int64_t out_idx = (int64_t)a_glob * p.n_win + w;
+    run_lane<RPL, AFFINE>(p, a_local, w < p.n_win ? w : -1, out_idx);
+}
+
+// grid: x = ceil(n_waves / 4); each wave one adapter, lanes = tasks
+template <int RPL, bool AFFINE>
+__global__ __launch_bounds__(256) void k_align_pairs(KParams p) {
+    const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (wave >= p.n_waves) return;
+    const int64_t slot = wave * 64 + (threadIdx.x & 63);
+    const int a_local = __builtin_amdgcn_readfirstlane(p.wave_adp[wave]);
+    const int32_t tw = p.task_win[slot];
+    run_lane<RPL, AFFINE>(p, a_local, tw, tw >= 0 ? p.task_out[slot] : 0);
+}
+
+// ---- decision epilogues --------------------------------------------------------------------
+
+__global__ __launch_bounds__(256) void k_end_trim(const int32_t *sres, int64_t sstride, int32_t n_sa,
+                                                  const int32_t *eres, int64_t estride, int32_t n_ea,
+                                                  int64_t n_read, int end_size, int extra,
+                                                  double thr, int min_trim,
+                                                  int32_t *start_trim, int32_t *end_trim,
+                                                  uint8_t *shit, uint8_t *ehit) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_read) return;
+    // find_start_trim (nanopore_read.py:175-195)
+    int st = 0;
+    for (int a = 0; a < n_sa; ++a) {
+        const int64_t i = (int64_t)a * n_read + r;
+        const int rs = sres[0 * sstride + i];
+        int re1, hit = 0;
+        double partial;
+        if (rs == -1) { re1 = 0; partial = 0.0; }
+        else { re1 = sres[1 * sstride + i] + 1; partial = pcabi::pid6(sres[5 * sstride + i], sres[6 * sstride + i]); }
+        if (partial > thr && re1 != end_size && re1 - rs >= min_trim) {
+            st = max(st, re1 + extra);
+            hit = 1;
+        }
+        if (shit) shit[i] = (uint8_t)hit;
+    }
+    // find_end_trim (nanopore_read.py:197-217)
+    int et = 0;
+    for (int a = 0; a < n_ea; ++a) {
+        const int64_t i = (int64_t)a * n_read + r;
+        const int rs = eres[0 * estride + i];
+        int re1, hit = 0;
+        double partial;
+        if (rs == -1) { re1 = 0; partial = 0.0; }
+        else { re1 = eres[1 * estride + i] + 1; partial = pcabi::pid6(eres[5 * estride + i], eres[6 * estride + i]); }
+        if (partial > thr && rs != 0 && re1 - rs >= min_trim) {
+            et = max(et, (end_size - rs) + extra);
+            hit = 1;
+        }
+        if (ehit) ehit[i] = (uint8_t)hit;
+    }
+    start_trim[r] = st;
+    end_trim[r] = et;
+}
+
+// best[a] = max(best[a], max_w pid2): one block per adapter, uint64 ordering of non-negative
+// doubles == numeric ordering, so the max is exact and order independent.
+__global__ __launch_bounds__(256) void k_best_full_id(const int32_t *res, int64_t stride, int64_t n_win,
+                                                      double *best) {
+    const int a = blockIdx.x;
+    __shared__ unsigned long long red[256];
+    unsigned long long mx = 0;
+    for (int64_t w = threadIdx.x; w < n_win; w += 256) {
+        const int64_t i = (int64_t)a * n_win + w;
+        const int rs = res[0 * stride + i];
+        const double full = (rs == -1) ? 0.0 : pcabi::pid6(res[5 * stride + i], res[7 * stride + i]);
+        const unsigned long long b = (unsigned long long)__double_as_longlong(full);
+        mx = b > mx ? b : mx;
+    }
+    red[threadIdx.x] = mx;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] = red[threadIdx.x] > red[threadIdx.x + s] ? red[threadIdx.x] : red[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const unsigned long long cur = (unsigned long long)__double_as_longlong(best[a]);
+        best[a] = __longlong_as_double((long long)(red[0] > cur ? red[0] : cur));
+    }
+}
+
+// ---- launch plumbing -------------------------------------------------------------------------
+
+template <int RPL>
+void launch_cross(const KParams &p, bool affine, int64_t n_win, hipStream_t st) {
+    dim3 grid((unsigned)((n_win + 255) / 256), (unsigned)p.n_adp);
+    if (affine) hipLaunchKernelGGL((k_align_cross<RPL, true>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((k_align_cross<RPL, false>), grid, dim3(256), 0, st, p);
+}
+
+template <int RPL>
+void launch_pairs(const KParams &p, bool affine, hipStream_t st) {
+    dim3 grid((unsigned)((p.n_waves + 3) / 4));
+    if (affine) hipLaunchKernelGGL((k_align_pairs<RPL, true>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((k_align_pairs<RPL, false>), grid, dim3(256), 0, st, p);
+}
+
+void dispatch_cross(int b, const KParams &p, bool affine, int64_t n_win, hipStream_t st) {
+    switch (kBuckets[b]) {
+    case 8: launch_cross<8>(p, affine, n_win, st); break;
+    case 16: launch_cross<16>(p, affine, n_win, st); break;
+    case 24: launch_cross<24>(p, affine, n_win, st); break;
+    case 32: launch_cross<32>(p, affine, n_win, st); break;
+    case 48: launch_cross<48>(p, affine, n_win, st); break;
+    case 64: launch_cross<64>(p, affine, n_win, st); break;
+    case 96: launch_cross<96>(p, affine, n_win, st); break;
+    case 128: launch_cross<128>(p, affine, n_win, st); break;
+    }
+}
+
+void dispatch_pairs(int b, const KParams &p, bool affine, hipStream_t st) {
+    switch (kBuckets[b]) {
+    case 8: launch_pairs<8>(p, affine, st); break;
+    case 16: launch_pairs<16>(p, affine, st); break;
+    case 24: launch_pairs<24>(p, affine, st); break;
+    case 32: launch_pairs<32>(p, affine, st); break;
+    case 48: launch_pairs<48>(p, affine, st); break;
+    case 64: launch_pairs<64>(p, affine, st); break;
+    case 96: launch_pairs<96>(p, affine, st); break;
+    case 128: launch_pairs<128>(p, affine, st); break;
+    }
+}
+
+// Host-side layout of a bucket's adapter table.
+struct BucketHost {
+    std::vector<uint8_t> pad;   // n * RPL bytes
+    std::vector<int32_t> len, id;
+};
+
+void build_buckets(const uint8_t *adp_codes, const int32_t *adp_off, const int32_t *adp_len,
+                   int32_t n_adp, BucketHost (&bk)[kNumBuckets]) {
+    for (int a = 0; a < n_adp; ++a) {
+        const int L = adp_len[a];
+        const int b = bucket_of(L);
+        const int R = kBuckets[b];
+        BucketHost &h = bk[b];
+        const size_t base = h.pad.size();
+        h.pad.resize(base + R, 0xFF);
+        const int off = R - L;
+        for (int k = 0; k < L; ++k) h.pad[base + off + k] = adp_codes[adp_off[a] + k];
+        h.len.push_back(L);
+        h.id.push_back(a);
+    }
+}
+
+}  // namespace
+
+// ---- prepared adapter tables (device) ---------------------------------------------------------
+struct pcabi_adapters {
+    int32_t n_adp = 0;
+    int32_t count[kNumBuckets] = {};
+    uint32_t *pad[kNumBuckets] = {};
+    int32_t *len[kNumBuckets] = {};
+    int32_t *id[kNumBuckets] = {};
+};
+
+namespace {
+
+struct DeviceBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(bytes, 1 << 16);
+        if (hipMalloc(&p, want) != hipSuccess) return fail(PCABI_E_NOMEM, "hipMalloc failed");
+        cap = want;
+        return 0;
+    }
+};
+
+// Per-device state for the host-buffer API (serialised by a mutex: the legacy ABI is called
+// concurrently from the reference's ThreadPool workers, porechop_abi.py:228,418,504).
+struct Engine {
+    std::mutex mu;
+    bool init = false;
+    hipStream_t stream = nullptr;
+    DeviceBuf codes, woff, wlen, out, tasks_win, tasks_out, wave_adp;
+    DeviceBuf pad[kNumBuckets], len[kNumBuckets], id[kNumBuckets];
+};
+
+Engine g_engines[16];
+
+int engine_init(Engine &e, int device) {
+    if (e.init) return 0;
+    HIP_TRY(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(PCABI_E_DEVICE, std::string("device is ") + prop.gcnArchName + ", kernels are built for gfx950");
+    HIP_TRY(hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking));
+    e.init = true;
+    return 0;
+}
+
+int check_common(const int32_t *adp_len, int32_t n_adp) {
+    for (int a = 0; a < n_adp; ++a)
+        if (adp_len[a] < 1 || adp_len[a] > kMaxRPL)
+            return fail(PCABI_E_ARG, "adapter length " + std::to_string(adp_len[a]) + " outside 1.." +
+                                         std::to_string(kMaxRPL));
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *pcabi_last_error(void) { return g_err.c_str(); }
+int pcabi_version(void) { return 1; }
+int pcabi_max_adapter_len(void) { return kMaxRPL; }
+int pcabi_max_window_len(void) { return pcabi::MAX_WINDOW_LEN; }
+
+int pcabi_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+void pcabi_encode_dna5(const char *ascii, uint8_t *codes, int64_t n) {
+    static uint8_t tab[256];
+    static bool built = false;
+    if (!built) {
+        for (int c = 0; c < 256; ++c) tab[c] = 4;
+        tab['A'] = tab['a'] = 0;
+        tab['C'] = tab['c'] = 1;
+        tab['G'] = tab['g'] = 2;
+        tab['T'] = tab['t'] = tab['U'] = tab['u'] = 3;
+        built = true;
+    }
+    for (int64_t i = 0; i < n; ++i) codes[i] = tab[(unsigned char)ascii[i]];
+}
+
+void pcabi_pid6_host(const int32_t *m, const int32_t *l, int64_t n, double *out) {
+    for (int64_t k = 0; k < n; ++k) out[k] = pcabi::pid6(m[k], l[k]);
+}
+
+int pcabi_align_host(int device, const uint8_t *codes, int64_t codes_len, const int64_t *win_off,
+                     const int32_t *win_len, int64_t n_win, const uint8_t *adp_codes,
+                     const int32_t *adp_off, const int32_t *adp_len, int32_t n_adp,
+                     const int32_t *task_win, const int32_t *task_adp, int64_t n_task, int match,
+                     int mismatch, int gap_open, int gap_extend, int32_t *out) {
+    if (device < 0 || device >= 16) return fail(PCABI_E_ARG, "bad device index");
+    if (n_win < 0 || n_adp < 0 || n_task < 0) return fail(PCABI_E_ARG, "negative count");
+    if (int rc = check_common(adp_len, n_adp)) return rc;
+    for (int64_t w = 0; w < n_win; ++w) {
+        if (win_len[w] < 0 || win_len[w] > pcabi::MAX_WINDOW_LEN)
+            return fail(PCABI_E_ARG, "window length out of range");
+        if (win_len[w] > 0 && ((win_off[w] & 3) != 0 || win_off[w] < 0 || win_off[w] + win_len[w] + 16 > codes_len))
+            return fail(PCABI_E_ARG, "window offset misaligned or buffer not padded by 16 bytes");
+    }
+    const int64_t n_res = task_win ? n_task : (int64_t)n_adp * n_win;
+    if (task_win)
+        for (int64_t t = 0; t < n_task; ++t)
+            if (task_win[t] < 0 || task_win[t] >= n_win || task_adp[t] < 0 || task_adp[t] >= n_adp)
+                return fail(PCABI_E_ARG, "task index out of range");
+    if (n_res == 0) return 0;
+
+    Engine &e = g_engines[device];
+    std::lock_guard<std::mutex> lock(e.mu);
+    if (int rc = engine_init(e, device)) return rc;
+    HIP_TRY(hipSetDevice(device));
+
+    BucketHost bk[kNumBuckets];
+    build_buckets(adp_codes, adp_off, adp_len, n_adp, bk);
+
+    if (int rc = e.codes.ensure((size_t)codes_len)) return rc;
+    if (int rc = e.woff.ensure(sizeof(int64_t) * (size_t)std::max<int64_t>(n_win, 1))) return rc;
+    if (int rc = e.wlen.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(n_win, 1))) return rc;
+    if (int rc = e.out.ensure(sizeof(int32_t) * PCABI_NFIELDS * (size_t)n_res)) return rc;
+    HIP_TRY(hipMemcpyAsync(e.codes.p, codes, (size_t)codes_len, hipMemcpyHostToDevice, e.stream));
+    HIP_TRY(hipMemcpyAsync(e.woff.p, win_off, sizeof(int64_t) * (size_t)n_win, hipMemcpyHostToDevice, e.stream));
+    HIP_TRY(hipMemcpyAsync(e.wlen.p, win_len, sizeof(int32_t) * (size_t)n_win, hipMemcpyHostToDevice, e.stream));
+
+    KParams p{};
+    p.codes = (const uint8_t *)e.codes.p;
+    p.win_off = (const int64_t *)e.woff.p;
+    p.win_len = (const int32_t *)e.wlen.p;
+    p.n_win = n_win;
+    p.out = (int32_t *)e.out.p;
+    p.out_stride = n_res;
+    p.sc = pcabi::Scoring{match, mismatch, gap_open, gap_extend};
+    const bool affine = gap_open != gap_extend;
+
+    // host-side pair grouping (pairs mode): per bucket, per adapter, runs padded to 64 lanes
+    std::vector<std::vector<int32_t>> per_adp;
+    if (task_win) {
+        per_adp.resize(n_adp);
+        for (int64_t t = 0; t < n_task; ++t) per_adp[task_adp[t]].push_back((int32_t)t);
+    }
+    std::vector<int32_t> tw, to, wa;
+    for (int b = 0; b < kNumBuckets; ++b) {
+        BucketHost &h = bk[b];
+        if (h.len.empty()) continue;
+        const int nb = (int)h.len.size();
+        if (int rc = e.pad[b].ensure(h.pad.size())) return rc;
+        if (int rc = e.len[b].ensure(sizeof(int32_t) * nb)) return rc;
+        if (int rc = e.id[b].ensure(sizeof(int32_t) * nb)) return rc;
+        HIP_TRY(hipMemcpyAsync(e.pad[b].p, h.pad.data(), h.pad.size(), hipMemcpyHostToDevice, e.stream));
+        HIP_TRY(hipMemcpyAsync(e.len[b].p, h.len.data(), sizeof(int32_t) * nb, hipMemcpyHostToDevice, e.stream));
+        HIP_TRY(hipMemcpyAsync(e.id[b].p, h.id.data(), sizeof(int32_t) * nb, hipMemcpyHostToDevice, e.stream));
+        p.adp_pad = (const uint32_t *)e.pad[b].p;
+        p.adp_len = (const int32_t *)e.len[b].p;
+        p.adp_id = (const int32_t *)e.id[b].p;
+        p.n_adp = nb;
+        if (!task_win) {
+            if (n_win > 0) dispatch_cross(b, p, affine, n_win, e.stream);
+        } else {
+            tw.clear(); to.clear(); wa.clear();
+            for (int k = 0; k < nb; ++k) {
+                const std::vector<int32_t> &ts = per_adp[h.id[k]];
+                for (size_t s = 0; s < ts.size(); s += 64) {
+                    wa.push_back(k);
+                    for (size_t q = 0; q < 64; ++q) {
+                        if (s + q < ts.size()) { tw.push_back(task_win[ts[s + q]]); to.push_back(ts[s + q]); }
+                        else { tw.push_back(-1); to.push_back(0); }
+                    }
+                }
+            }
+            if (wa.empty()) continue;
+            // the per-bucket task arrays must stay alive until the kernel has read them
+            if (int rc = e.tasks_win.ensure(sizeof(int32_t) * tw.size())) return rc;
+            if (int rc = e.tasks_out.ensure(sizeof(int32_t) * to.size())) return rc;
+            if (int rc = e.wave_adp.ensure(sizeof(int32_t) * wa.size())) return rc;
+            HIP_TRY(hipMemcpyAsync(e.tasks_win.p, tw.data(), sizeof(int32_t) * tw.size(), hipMemcpyHostToDevice, e.stream));
+            HIP_TRY(hipMemcpyAsync(e.tasks_out.p, to.data(), sizeof(int32_t) * to.size(), hipMemcpyHostToDevice, e.stream));
+            HIP_TRY(hipMemcpyAsync(e.wave_adp.p, wa.data(), sizeof(int32_t) * wa.size(), hipMemcpyHostToDevice, e.stream));
+            p.task_win = (const int32_t *)e.tasks_win.p;
+            p.task_out = (const int32_t *)e.tasks_out.p;
+            p.wave_adp = (const int32_t *)e.wave_adp.p;
+            p.n_waves = (int64_t)wa.size();
+            dispatch_pairs(b, p, affine, e.stream);
+            // host vectors are reused by the next bucket: drain before overwriting
+            HIP_TRY(hipStreamSynchronize(e.stream));
+        }
+        HIP_TRY(hipGetLastError());
+        // bucket buffers are reused across calls only; keep them distinct per bucket
+    }
+    HIP_TRY(hipMemcpyAsync(out, e.out.p, sizeof(int32_t) * PCABI_NFIELDS * (size_t)n_res,
+                           hipMemcpyDeviceToHost, e.stream));
+    HIP_TRY(hipStreamSynchronize(e.stream));
+    return 0;
+}
+
+// ---- legacy drop-in --------------------------------------------------------------------------
+
+static int fmt_pid(char *buf, size_t cap, int m, int l) {
+    if (l == 0) return std::snprintf(buf, cap, "-nan");
+    return std::snprintf(buf, cap, "%f", 100.0 * m / l);
+}
+
+char *adapterAlignment(char *readSeq, char *adapterSeq, int matchScore, int mismatchScore,
+                       int gapOpenScore, int gapExtensionScore) {
+    const int64_t n = (int64_t)std::strlen(readSeq);
+    const int32_t L = (int32_t)std::strlen(adapterSeq);
+    char *s = (char *)std::malloc(256);
+    if (!s) return nullptr;
+    if (n == 0 || L == 0) {
+        std::snprintf(s, 256, "-1,0,-1,0,%d,0.000000,0.000000", (int)0x80000000);
+        return s;
+    }
+    std::vector<uint8_t> codes((size_t)((n + 3) & ~3LL) + 16, 4);
+    pcabi_encode_dna5(readSeq, codes.data(), n);
+    std::vector<uint8_t> ac((size_t)L);
+    pcabi_encode_dna5(adapterSeq, ac.data(), L);
+    const int64_t woff = 0;
+    const int32_t wlen = (int32_t)n;
+    const int32_t aoff = 0;
+    int32_t out[PCABI_NFIELDS];
+    int device = 0;
+    (void)hipGetDevice(&device);
+    int rc = pcabi_align_host(device, codes.data(), (int64_t)codes.size(), &woff, &wlen, 1, ac.data(), &aoff,
+                              &L, 1, nullptr, nullptr, 0, matchScore, mismatchScore, gapOpenScore,
+                              gapExtensionScore, out);
+    if (rc != 0) {
+        std::fprintf(stderr, "libpcabi: adapterAlignment failed: %s\n", pcabi_last_error());
+        std::snprintf(s, 256, "-1,0,-1,0,%d,0.000000,0.000000", (int)0x80000000);
+        return s;
+    }
+    char p1[64], p2[64];
+    fmt_pid(p1, sizeof p1, out[PCABI_F_M], out[PCABI_F_L1]);
+    fmt_pid(p2, sizeof p2, out[PCABI_F_M], out[PCABI_F_L2]);
+    std::snprintf(s, 256, "%d,%d,%d,%d,%d,%s,%s", out[0], out[1], out[2], out[3], out[4], p1, p2);
+    return s;
+}
+
+void freeCString(char *p) { std::free(p); }
+
+// ---- device-resident interface ----------------------------------------------------------------
+
+int pcabi_dev_set(int device) { HIP_TRY(hipSetDevice(device)); return 0; }
+int pcabi_dev_malloc(void **ptr, int64_t bytes) { HIP_TRY(hipMalloc(ptr, (size_t)bytes)); return 0; }
+int pcabi_dev_free(void *ptr) { HIP_TRY(hipFree(ptr)); return 0; }
+int pcabi_dev_h2d(void *dst, const void *src, int64_t bytes) {
+    HIP_TRY(hipMemcpy(dst, src, (size_t)bytes, hipMemcpyHostToDevice)); return 0;
+}
+int pcabi_dev_d2h(void *dst, const void *src, int64_t bytes) {
+    HIP_TRY(hipMemcpy(dst, src, (size_t)bytes, hipMemcpyDeviceToHost)); return 0;
+}
+int pcabi_dev_memset(void *dst, int value, int64_t bytes) { HIP_TRY(hipMemset(dst, value, (size_t)bytes)); return 0; }
+int pcabi_dev_sync(void) { HIP_TRY(hipDeviceSynchronize()); return 0; }
+int pcabi_stream_create(void **stream) {
+    hipStream_t s;
+    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *stream = (void *)s;
+    return 0;
+}
+int pcabi_stream_destroy(void *stream) { HIP_TRY(hipStreamDestroy((hipStream_t)stream)); return 0; }
+int pcabi_stream_sync(void *stream) { HIP_TRY(hipStreamSynchronize((hipStream_t)stream)); return 0; }
+int pcabi_event_create(void **ev) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreate(&e));
+    *ev = (void *)e;
+    return 0;
+}
+int pcabi_event_destroy(void *ev) { HIP_TRY(hipEventDestroy((hipEvent_t)ev)); return 0; }
+int pcabi_event_record(void *ev, void *stream) { HIP_TRY(hipEventRecord((hipEvent_t)ev, (hipStream_t)stream)); return 0; }
+int pcabi_event_elapsed_ms(float *ms, void *start, void *stop) {
+    HIP_TRY(hipEventSynchronize((hipEvent_t)stop));
+    HIP_TRY(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop));
+    return 0;
+}
+
+int pcabi_adapters_create(const uint8_t *adp_codes, const int32_t *adp_off, const int32_t *adp_len,
+                          int32_t n_adp, pcabi_adapters **out) {
+    if (int rc = check_common(adp_len, n_adp)) return rc;
+    BucketHost bk[kNumBuckets];
+    build_buckets(adp_codes, adp_off, adp_len, n_adp, bk);
+    pcabi_adapters *a = new pcabi_adapters();
+    a->n_adp = n_adp;
+    for (int b = 0; b < kNumBuckets; ++b) {
+        const int nb = (int)bk[b].len.size();
+        a->count[b] = nb;
+        if (!nb) continue;
+        if (hipMalloc((void **)&a->pad[b], bk[b].pad.size()) != hipSuccess ||
+            hipMalloc((void **)&a->len[b], sizeof(int32_t) * nb) != hipSuccess ||
+            hipMalloc((void **)&a->id[b], sizeof(int32_t) * nb) != hipSuccess) {
+            pcabi_adapters_destroy(a);
+            return fail(PCABI_E_NOMEM, "hipMalloc failed for adapter table");
+        }
+        (void)hipMemcpy(a->pad[b], bk[b].pad.data(), bk[b].pad.size(), hipMemcpyHostToDevice);
+        (void)hipMemcpy(a->len[b], bk[b].len.data(), sizeof(int32_t) * nb, hipMemcpyHostToDevice);
+        (void)hipMemcpy(a->id[b], bk[b].id.data(), sizeof(int32_t) * nb, hipMemcpyHostToDevice);
+    }
+    *out = a;
+    return 0;
+}
+
+void pcabi_adapters_destroy(pcabi_adapters *a) {
+    if (!a) return;
+    for (int b = 0; b < kNumBuckets; ++b) {
+        if (a->pad[b]) (void)hipFree(a->pad[b]);
+        if (a->len[b]) (void)hipFree(a->len[b]);
+        if (a->id[b]) (void)hipFree(a->id[b]);
+    }
+    delete a;
+}
+
+int pcabi_align_cross_dev(const uint8_t *codes, const int64_t *win_off, const int32_t *win_len,
+                          int64_t n_win, const pcabi_adapters *adps, int match, int mismatch,
+                          int gap_open, int gap_extend, int32_t *out, int64_t out_stride, void *stream) {
+    if (!adps || n_win < 0) return fail(PCABI_E_ARG, "bad arguments");
+    if (n_win == 0) return 0;
+    KParams p{};
+    p.codes = codes;
+    p.win_off = win_off;
+    p.win_len = win_len;
+    p.n_win = n_win;
+    p.out = out;
+    p.out_stride = out_stride;
+    p.sc = pcabi::Scoring{match, mismatch, gap_open, gap_extend};
+    const bool affine = gap_open != gap_extend;
+    for (int b = 0; b < kNumBuckets; ++b) {
+        if (!adps->count[b]) continue;
+        p.adp_pad = adps->pad[b];
+        p.adp_len = adps->len[b];
+        p.adp_id = adps->id[b];
+        p.n_adp = adps->count[b];
+        dispatch_cross(b, p, affine, n_win, (hipStream_t)stream);
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int pcabi_end_trim_dev(const int32_t *start_res, int64_t start_stride, int32_t n_sa,
+                       const int32_t *end_res, int64_t end_stride, int32_t n_ea, int64_t n_read,
+                       int end_size, int extra_trim, double end_threshold, int min_trim_size,
+                       int32_t *start_trim, int32_t *end_trim, uint8_t *start_hit, uint8_t *end_hit,
+                       void *stream) {
+    if (n_read <= 0) return 0;
+    const unsigned blocks = (unsigned)((n_read + 255) / 256);
+    hipLaunchKernelGGL(k_end_trim, dim3(blocks), dim3(256), 0, (hipStream_t)stream, start_res, start_stride,
+                       n_sa, end_res, end_stride, n_ea, n_read, end_size, extra_trim, end_threshold,
+                       min_trim_size, start_trim, end_trim, start_hit, end_hit);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int pcabi_best_full_identity_dev(const int32_t *res, int64_t stride, int64_t n_win, int32_t n_adp,
+                                 double *best, void *stream) {
+    if (n_adp <= 0 || n_win <= 0) return 0;
+    hipLaunchKernelGGL(k_best_full_id, dim3((unsigned)n_adp), dim3(256), 0, (hipStream_t)stream, res, stride,
+                       n_win, best);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+}  // extern "C"

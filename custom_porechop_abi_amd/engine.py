@@ -1,0 +1,167 @@
+"""Batched host interface to the MI355X adapter-alignment engine (libpcabi.so).
+
+Sequences travel as Dna5 codes (A=0 C=1 G=2 T/U=3 other=4; the table of
+S/basic/alphabet_residue_tabs.h:113-140 in the reference's vendored SeqAn) packed in one
+byte buffer. A *window* is an (offset, length) view into that buffer; offsets are 4-byte
+aligned and the buffer carries 16 bytes of padding, as libpcabi requires (include/pcabi.h).
+
+The reference encodes each Python str with UTF-8 before handing it to SeqAn
+(porechop_abi/cpp_function_wrappers.py:52), so a non-ASCII character becomes several N codes;
+``encode_seq`` reproduces that byte-for-byte.
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import NFIELDS, check, lib
+
+DNA5 = np.full(256, 4, dtype=np.uint8)
+for _c, _v in (('A', 0), ('C', 1), ('G', 2), ('T', 3), ('U', 3)):
+    DNA5[ord(_c)] = _v
+    DNA5[ord(_c.lower())] = _v
+
+PAD = 16
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def encode_seq(seq):
+    """str -> Dna5 codes (uint8 array), byte-exact with the reference's UTF-8 marshalling."""
+    return DNA5[np.frombuffer(seq.encode('utf-8'), dtype=np.uint8)]
+
+
+class SeqPack(object):
+    """Sequences packed back to back (4-aligned starts, 16 bytes tail padding)."""
+
+    def __init__(self, seqs):
+        parts = []
+        offs = np.zeros(len(seqs), dtype=np.int64)
+        lens = np.zeros(len(seqs), dtype=np.int32)
+        pos = 0
+        for k, s in enumerate(seqs):
+            b = s.encode('utf-8') if isinstance(s, str) else bytes(s)
+            n = len(b)
+            offs[k] = pos
+            lens[k] = n
+            pad = (-n) & 3
+            parts.append(b)
+            if pad:
+                parts.append(b'N' * pad)
+            pos += n + pad
+        parts.append(b'N' * PAD)
+        raw = np.frombuffer(b''.join(parts), dtype=np.uint8)
+        self.codes = np.ascontiguousarray(DNA5[raw])
+        self.offsets = offs
+        self.lengths = lens
+
+    def __len__(self):
+        return len(self.lengths)
+
+    def views(self, starts, lengths, index=None):
+        """Window views [start, start+len) of packed sequences (start relative to each sequence).
+        Starts that are not 4-aligned are re-packed (copied) so the kernel's dword reads stay
+        aligned; returns (codes, offsets, lengths)."""
+        idx = np.arange(len(self.lengths)) if index is None else np.asarray(index)
+        starts = np.asarray(starts, dtype=np.int64)
+        lengths = np.asarray(lengths, dtype=np.int32)
+        abs_off = self.offsets[idx] + starts
+        if np.all((abs_off & 3) == 0):
+            return self.codes, abs_off, lengths
+        # re-pack: one copy of every window at an aligned slot
+        stride_off = np.zeros(len(idx), dtype=np.int64)
+        padded = (lengths.astype(np.int64) + 3) & ~3
+        stride_off[1:] = np.cumsum(padded)[:-1]
+        total = int(padded.sum()) + PAD
+        out = np.full(total, 4, dtype=np.uint8)
+        for k in range(len(idx)):
+            n = int(lengths[k])
+            if n:
+                out[stride_off[k]:stride_off[k] + n] = self.codes[abs_off[k]:abs_off[k] + n]
+        return out, stride_off, lengths
+
+
+def start_end_windows(pack, end_size):
+    """(start windows, end windows) exactly as seq[:end_size] and seq[-end_size:]
+    (porechop_abi/nanopore_read.py:164,169,181,203), as packed views."""
+    n = pack.lengths.astype(np.int64)
+    e = int(end_size)
+    s_len = np.minimum(n, e) if e >= 0 else np.maximum(n + e, 0)
+    if e > 0:
+        e_start = np.maximum(n - e, 0)
+    elif e == 0:
+        e_start = np.zeros_like(n)          # seq[-0:] is the whole sequence
+    else:
+        e_start = np.minimum(-e, n)
+    e_len = n - e_start
+    sw = pack.views(np.zeros_like(n), s_len.astype(np.int32))
+    ew = pack.views(e_start, e_len.astype(np.int32))
+    return sw, ew
+
+
+def encode_adapters(adapter_seqs):
+    b = [encode_seq(s) for s in adapter_seqs]
+    lens = np.array([len(x) for x in b], dtype=np.int32)
+    offs = np.zeros(len(b), dtype=np.int32)
+    if len(b) > 1:
+        offs[1:] = np.cumsum(lens)[:-1]
+    codes = np.concatenate(b + [np.zeros(PAD, np.uint8)]).astype(np.uint8)
+    return codes, offs, lens
+
+
+def align(windows, adapter_seqs, scoring_scheme_vals, pairs=None, device=0):
+    """Align windows against adapters on the GPU.
+
+    windows: (codes uint8, offsets int64, lengths int32) as from SeqPack.views.
+    pairs=None -> cross product, result column a*n_win + w; else (win_idx, adp_idx) arrays.
+    Returns int32 array (8, n_results): rs, re, as, ae, score, m, l1, l2 (pcabi.h field order).
+    """
+    codes, offs, lens = windows
+    codes = np.ascontiguousarray(codes, dtype=np.uint8)
+    offs = np.ascontiguousarray(offs, dtype=np.int64)
+    lens = np.ascontiguousarray(lens, dtype=np.int32)
+    acodes, aoffs, alens = encode_adapters(adapter_seqs)
+    n_win = len(lens)
+    n_adp = len(alens)
+    if pairs is None:
+        tw = ta = None
+        n_task = 0
+        n_res = n_win * n_adp
+    else:
+        tw = np.ascontiguousarray(pairs[0], dtype=np.int32)
+        ta = np.ascontiguousarray(pairs[1], dtype=np.int32)
+        n_task = len(tw)
+        n_res = n_task
+    out = np.zeros((NFIELDS, n_res), dtype=np.int32)
+    if n_res == 0:
+        return out
+    m, mm, go, ge = (int(x) for x in scoring_scheme_vals[:4])
+    rc = lib().pcabi_align_host(device, _ptr(codes), codes.size, _ptr(offs), _ptr(lens), n_win,
+                                _ptr(acodes), _ptr(aoffs), _ptr(alens), n_adp,
+                                _ptr(tw), _ptr(ta), n_task, m, mm, go, ge, _ptr(out))
+    check(rc, 'pcabi_align_host')
+    return out
+
+
+def pid6(m, l):
+    """float('%f' % (100*m/l)) elementwise (NaN where l == 0), the reference's identity text
+    round trip (porechop_abi/src/alignment.cpp:118-119, porechop_abi/nanopore_read.py:497-498)."""
+    m = np.ascontiguousarray(m, dtype=np.int32)
+    l = np.ascontiguousarray(l, dtype=np.int32)
+    out = np.empty(m.shape, dtype=np.float64)
+    lib().pcabi_pid6_host(_ptr(m), _ptr(l), m.size, _ptr(out))
+    return out
+
+
+def identities(res):
+    """(full_adapter_identity, aligned_region_identity, read_start, read_end_exclusive) arrays,
+    the tuple align_adapter returns (porechop_abi/nanopore_read.py:485-500)."""
+    rs = res[0]
+    failed = rs == -1
+    full = pid6(res[5], res[7])
+    part = pid6(res[5], res[6])
+    full[failed] = 0.0
+    part[failed] = 0.0
+    read_end = np.where(failed, 0, res[1] + 1).astype(np.int64)
+    return full, part, rs.astype(np.int64), read_end

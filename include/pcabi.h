@@ -1,0 +1,163 @@
+/*
+ * pcabi.h -- C ABI of the MI355X adapter-alignment engine (libpcabi.so).
+ *
+ * Two layers:
+ *
+ *  1. Drop-in legacy symbols, byte-compatible with the reference's cpp_functions.so
+ *     (porechop_abi/include/adapter_align.h:12-16, bound by ctypes in
+ *     porechop_abi/cpp_function_wrappers.py:25-39):
+ *        char *adapterAlignment(char *readSeq, char *adapterSeq,
+ *                               int matchScore, int mismatchScore,
+ *                               int gapOpenScore, int gapExtensionScore);
+ *        void  freeCString(char *p);
+ *     Same argument order (Python passes match, mismatch, gap_open, gap_extend:
+ *     cpp_function_wrappers.py:46-51), same malloc'd "rs,re,as,ae,score,pid1,pid2" result
+ *     (porechop_abi/src/alignment.cpp:113-120), caller frees with freeCString. Each call runs
+ *     on the GPU (one lane); concurrent callers are serialised per device.
+ *
+ *  2. Batch ABI used by the batched phase drivers (replacing the per-read ThreadPool loops of
+ *     porechop_abi/porechop_abi.py:200-245, 359-438, 457-522). Sequences are Dna5 codes
+ *     (A=0 C=1 G=2 T/U=3 anything else=4, S/basic/alphabet_residue_tabs.h:113-140) packed in
+ *     one byte buffer; a "window" is an (offset, length) view into it, offsets multiple of 4,
+ *     buffer padded with >= 16 readable bytes past the last window. Results are SoA int32,
+ *     8 fields x n_results, field order PCABI_F_*.
+ *
+ * Errors: functions return 0 on success, a negative PCABI_E_* code otherwise;
+ * pcabi_last_error() returns a thread-local message. No exceptions cross the ABI.
+ * There is no CPU fallback: without a usable gfx950 device every compute entry point fails
+ * (the legacy adapterAlignment then returns a string whose first field is -1 and sets
+ * pcabi_last_error()).
+ */
+#ifndef PCABI_H
+#define PCABI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- result field order (SoA rows) -------------------------------------------------- */
+enum {
+    PCABI_F_RS = 0,     /* read start (ScoredAlignment::m_readStartPos), -1 = no alignment */
+    PCABI_F_RE = 1,     /* read end, inclusive                                          */
+    PCABI_F_AS = 2,     /* adapter start                                                */
+    PCABI_F_AE = 3,     /* adapter end, inclusive                                       */
+    PCABI_F_SCORE = 4,  /* raw DP score                                                 */
+    PCABI_F_M = 5,      /* matching columns (numerator of both identities)              */
+    PCABI_F_L1 = 6,     /* aligned-region length: pid1 = 100*m/l1 (NaN when l1 == 0)     */
+    PCABI_F_L2 = 7,     /* full-adapter span length: pid2 = 100*m/l2                     */
+    PCABI_NFIELDS = 8
+};
+
+enum {
+    PCABI_OK = 0,
+    PCABI_E_ARG = -1,      /* bad argument / unsupported size                   */
+    PCABI_E_DEVICE = -2,   /* no usable gfx950 device / HIP runtime error       */
+    PCABI_E_NOMEM = -3
+};
+
+/* ---- legacy drop-in ------------------------------------------------------------------ */
+char *adapterAlignment(char *readSeq, char *adapterSeq, int matchScore, int mismatchScore,
+                       int gapOpenScore, int gapExtensionScore);
+void freeCString(char *p);
+
+/* ---- housekeeping -------------------------------------------------------------------- */
+const char *pcabi_last_error(void);
+int pcabi_version(void);                 /* ABI version, currently 1                     */
+int pcabi_device_count(void);            /* visible HIP devices (0 if none)              */
+int pcabi_max_adapter_len(void);         /* longest adapter the kernels accept           */
+int pcabi_max_window_len(void);          /* longest window / read the kernels accept     */
+
+/* ASCII -> Dna5 codes (host, table lookup). n bytes. */
+void pcabi_encode_dna5(const char *ascii, uint8_t *codes, int64_t n);
+
+/* Identity exactly as Python holds it after the reference's text round trip
+ * (alignment.cpp:118-119 "%f", nanopore_read.py:497-498 float()): out[k] = pid6(m[k], l[k]),
+ * NaN when l[k] == 0. Host-side formatting helper, same code as the device epilogues. */
+void pcabi_pid6_host(const int32_t *m, const int32_t *l, int64_t n, double *out);
+
+/* ---- batch alignment, host buffers ---------------------------------------------------- */
+/*
+ * Align windows against adapters on `device`.
+ *   codes[codes_len]            : Dna5 codes holding every window (padding rules above)
+ *   win_off[n_win], win_len[n_win]
+ *   adp_codes, adp_off[n_adp], adp_len[n_adp] : adapters (Dna5 codes, any alignment)
+ * Work:
+ *   task_win == NULL  -> cross product: result (a, w) at index a*n_win + w
+ *   task_win != NULL  -> n_task explicit pairs (task_win[t], task_adp[t]); result at index t
+ * out: int32[PCABI_NFIELDS * n_results], row f holds field f for every result.
+ */
+int pcabi_align_host(int device,
+                     const uint8_t *codes, int64_t codes_len,
+                     const int64_t *win_off, const int32_t *win_len, int64_t n_win,
+                     const uint8_t *adp_codes, const int32_t *adp_off, const int32_t *adp_len,
+                     int32_t n_adp,
+                     const int32_t *task_win, const int32_t *task_adp, int64_t n_task,
+                     int match, int mismatch, int gap_open, int gap_extend,
+                     int32_t *out);
+
+/* ---- device-resident interface (bench / multi-GPU shards) ------------------------------ */
+/* Thin HIP wrappers so hosts without a GPU framework can keep inputs resident in HBM. */
+int pcabi_dev_set(int device);
+int pcabi_dev_malloc(void **ptr, int64_t bytes);
+int pcabi_dev_free(void *ptr);
+int pcabi_dev_h2d(void *dst, const void *src, int64_t bytes);
+int pcabi_dev_d2h(void *dst, const void *src, int64_t bytes);
+int pcabi_dev_memset(void *dst, int value, int64_t bytes);
+int pcabi_dev_sync(void);
+int pcabi_stream_create(void **stream);
+int pcabi_stream_destroy(void *stream);
+int pcabi_stream_sync(void *stream);
+int pcabi_event_create(void **ev);
+int pcabi_event_destroy(void *ev);
+int pcabi_event_record(void *ev, void *stream);
+int pcabi_event_elapsed_ms(float *ms, void *start, void *stop);
+
+/*
+ * Prepared adapter table: adapters re-laid out per register bucket (top-padded, packed codes).
+ * Build once per adapter list; reuse across batches.
+ */
+typedef struct pcabi_adapters pcabi_adapters;
+int pcabi_adapters_create(const uint8_t *adp_codes, const int32_t *adp_off, const int32_t *adp_len,
+                          int32_t n_adp, pcabi_adapters **out);   /* uploads to current device */
+void pcabi_adapters_destroy(pcabi_adapters *a);
+
+/*
+ * Cross-product alignment, every pointer a DEVICE pointer, asynchronous on `stream`:
+ * result (a, w) -> out[f * out_stride + a * n_win + w].
+ */
+int pcabi_align_cross_dev(const uint8_t *codes, const int64_t *win_off, const int32_t *win_len,
+                          int64_t n_win, const pcabi_adapters *adps,
+                          int match, int mismatch, int gap_open, int gap_extend,
+                          int32_t *out, int64_t out_stride, void *stream);
+
+/*
+ * End-trim decision epilogue (porechop_abi/nanopore_read.py:175-217), device pointers:
+ *   start results: cross product of n_read start windows x n_sa start adapters (layout above)
+ *   end results  : cross product of n_read end windows   x n_ea end adapters
+ * Identities are compared exactly as the reference does after its text round trip
+ * (alignment.cpp:118-119 prints "%f", nanopore_read.py:497-498 parses it back): the device
+ * rounds 100*m/l to 6 decimals with round-half-even on the exact double, then to the nearest
+ * double (pcabi::pid6, checked against Python's '%f' in tests/).
+ * Writes start_trim[n_read], end_trim[n_read] (amounts, same integers as
+ * NanoporeRead.start_trim_amount / end_trim_amount) and, when non-NULL, per-pair
+ * "alignment recorded" flags (uint8, same layout as the results).
+ */
+int pcabi_end_trim_dev(const int32_t *start_res, int64_t start_stride, int32_t n_sa,
+                       const int32_t *end_res, int64_t end_stride, int32_t n_ea,
+                       int64_t n_read, int end_size, int extra_trim, double end_threshold, int min_trim_size,
+                       int32_t *start_trim, int32_t *end_trim,
+                       uint8_t *start_hit, uint8_t *end_hit, void *stream);
+
+/*
+ * Adapter-set discovery reduction (porechop_abi/nanopore_read.py:158-173): for each adapter a
+ * of a cross-product result block, best[a] = max(best[a], max_w pid2(a, w)).
+ */
+int pcabi_best_full_identity_dev(const int32_t *res, int64_t stride, int64_t n_win, int32_t n_adp,
+                                 double *best, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PCABI_H */

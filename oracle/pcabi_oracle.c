@@ -1,0 +1,263 @@
+/*
+ * pcabi_oracle.c -- CPU ORACLE (test infrastructure only; see pcabi_oracle.h).
+ *
+ * A straightforward restatement of what the reference computes for one (read, adapter)
+ * pair, written from the reference sources, step by step:
+ *
+ *   1. Dna5 mapping ........ S/basic/alphabet_residue_tabs.h:113-140
+ *   2. Unbanded DP, free end gaps on all four sides (AlignConfig<1,1,1,1>,
+ *      porechop_abi/src/adapter_align.cpp:26-27), Gotoh affine recurrences
+ *      (S/align/dp_formula_affine.h:66-125) or linear when open == extend
+ *      (S/align/global_alignment_unbanded.h:213-221, S/align/dp_formula_linear.h:65-105);
+ *      ties resolved by _maxScore "left unless left < right" (S/align/dp_formula.h:153-163).
+ *   3. Max scout over the last row then the last column, strict '>'
+ *      (S/align/dp_meta_info.h:187-216, S/align/dp_scout.h:175).
+ *   4. Start correction of the trace value (S/align/dp_algorithm_impl.h:1170-1186).
+ *   5. GapsLeft traceback with Gotoh run-to-open loops
+ *      (S/align/dp_traceback_impl.h:197-370, 379-455, 497-548).
+ *   6. Gapped rows -> ScoredAlignment fields (porechop_abi/src/alignment.cpp:6-110)
+ *      and "%d,%d,%d,%d,%d,%f,%f" text (alignment.cpp:113-120).
+ *
+ * Full (n+1)x(l+1) matrices; O(n*l) memory, intended for checking, not speed.
+ * (S/ = porechop_abi/include/seqan/ under /root/reference.)
+ */
+#include "pcabi_oracle.h"
+
+#include <limits.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* trace bits (our own encoding of SeqAn's TraceBitMap_ roles) */
+enum { T_NONE = 0, T_D = 1, T_H = 2, T_HO = 4, T_V = 8, T_VO = 16, T_MAXV = 32, T_MAXH = 64 };
+
+#define NEG (INT_MIN / 2) /* DPCellDefaultInfinity, S/align/dp_cell.h:144-145 */
+
+static int dna5(unsigned char c) {
+    switch (c) {
+    case 'A': case 'a': return 0;
+    case 'C': case 'c': return 1;
+    case 'G': case 'g': return 2;
+    case 'T': case 't': case 'U': case 'u': return 3;
+    default: return 4;
+    }
+}
+static const char DNA5_CHARS[5] = {'A', 'C', 'G', 'T', 'N'};
+
+void pcabi_oracle_align(const char *read, int n, const char *adapter, int l,
+                        int ma, int mi, int go, int ge, pcabi_oracle_result *out) {
+    memset(out, 0, sizeof(*out));
+    out->rs = -1;
+    out->re = -1;
+    out->as = -1;
+    out->ae = -1;
+    if (n <= 0 || l <= 0) {            /* _isValidDPSettings: empty sequence -> no alignment */
+        out->score = INT_MIN;
+        return;
+    }
+    const int affine = (go != ge);
+    const int W = n + 1;
+    const size_t cells = (size_t)(l + 1) * (size_t)W;
+    int *S = (int *)malloc(cells * sizeof(int));
+    int *H = (int *)malloc(cells * sizeof(int));
+    int *V = (int *)malloc(cells * sizeof(int));
+    unsigned char *T = (unsigned char *)calloc(cells, 1);
+    unsigned char *rc = (unsigned char *)malloc((size_t)n);
+    unsigned char *ac = (unsigned char *)malloc((size_t)l);
+    for (int j = 0; j < n; ++j) rc[j] = (unsigned char)dna5((unsigned char)read[j]);
+    for (int i = 0; i < l; ++i) ac[i] = (unsigned char)dna5((unsigned char)adapter[i]);
+#define IDX(i, j) ((size_t)(i) * (size_t)W + (size_t)(j))
+
+    /* free end gaps: first row and column are RecursionDirectionZero */
+    for (int j = 0; j <= n; ++j) { S[IDX(0, j)] = 0; H[IDX(0, j)] = NEG; V[IDX(0, j)] = NEG; }
+    for (int i = 0; i <= l; ++i) { S[IDX(i, 0)] = 0; H[IDX(i, 0)] = NEG; V[IDX(i, 0)] = NEG; }
+
+    for (int j = 1; j <= n; ++j) {
+        for (int i = 1; i <= l; ++i) {
+            int sub = (rc[j - 1] == ac[i - 1]) ? ma : mi;
+            int diag = S[IDX(i - 1, j - 1)] + sub;
+            unsigned char tv;
+            int s;
+            if (affine) {
+                int hx = H[IDX(i, j - 1)] + ge, ho = S[IDX(i, j - 1)] + go;
+                int h = (hx < ho) ? ho : hx;
+                unsigned char hb = (hx < ho) ? T_HO : T_H;
+                int vx = V[IDX(i - 1, j)] + ge, vo = S[IDX(i - 1, j)] + go;
+                int v = (vx < vo) ? vo : vx;
+                unsigned char vb = (vx < vo) ? T_VO : T_V;
+                int g = (v < h) ? h : v;
+                unsigned char gb = (v < h) ? T_MAXH : T_MAXV;
+                if (diag < g) { s = g; tv = (unsigned char)(gb | hb | vb); }
+                else          { s = diag; tv = (unsigned char)(T_D | hb | vb); }
+                H[IDX(i, j)] = h;
+                V[IDX(i, j)] = v;
+            } else {
+                int v = S[IDX(i - 1, j)] + ge, h = S[IDX(i, j - 1)] + ge;
+                int g = (v < h) ? h : v;
+                unsigned char gb = (v < h) ? (T_H | T_MAXH) : (T_V | T_MAXV);
+                if (diag < g) { s = g; tv = gb; }
+                else          { s = diag; tv = T_D; }
+                H[IDX(i, j)] = NEG;
+                V[IDX(i, j)] = NEG;
+            }
+            S[IDX(i, j)] = s;
+            T[IDX(i, j)] = tv;
+        }
+    }
+
+    /* scout: last row j = 0..n-1, then last column rows 0..l; strict '>' */
+    int best = NEG, bi = 0, bj = 0;
+    for (int j = 0; j < n; ++j)
+        if (S[IDX(l, j)] > best) { best = S[IDX(l, j)]; bi = l; bj = j; }
+    for (int i = 0; i <= l; ++i)
+        if (S[IDX(i, n)] > best) { best = S[IDX(i, n)]; bi = i; bj = n; }
+    out->score = best;
+
+    /* traceback (GapsLeft). path columns are collected in reverse: type 'D','V','H' */
+    char *path = (char *)malloc((size_t)(n + l + 2));
+    int plen = 0;
+    int i = bi, j = bj;
+    if (i > 0 && j > 0) {
+        unsigned char tv = T[IDX(i, j)];
+        if (affine) {
+            if (V[IDX(i, j)] == best)      { tv = (unsigned char)((tv & ~T_D) | T_MAXV); }
+            else if (H[IDX(i, j)] == best) { tv = (unsigned char)((tv & ~T_D) | T_MAXH); }
+        }
+        while (i > 0 && j > 0 && tv != T_NONE) {
+            if (tv & T_D) {
+                path[plen++] = 'D';
+                --i; --j;
+                tv = T[IDX(i, j)];
+            } else if ((tv & T_MAXV) && (tv & T_V)) {
+                if (affine) {
+                    while ((!(tv & T_VO) || (tv & T_V)) && i != 1) {
+                        path[plen++] = 'V';
+                        --i;
+                        tv = T[IDX(i, j)];
+                    }
+                }
+                path[plen++] = 'V';
+                --i;
+                tv = T[IDX(i, j)];
+            } else if ((tv & T_MAXV) && (tv & T_VO)) {
+                path[plen++] = 'V';
+                --i;
+                tv = T[IDX(i, j)];
+            } else if ((tv & T_MAXH) && (tv & T_H)) {
+                if (affine) {
+                    while ((!(tv & T_HO) || (tv & T_H)) && j != 1) {
+                        path[plen++] = 'H';
+                        --j;
+                        tv = T[IDX(i, j)];
+                    }
+                }
+                path[plen++] = 'H';
+                --j;
+                tv = T[IDX(i, j)];
+            } else if ((tv & T_MAXH) && (tv & T_HO)) {
+                path[plen++] = 'H';
+                --j;
+                tv = T[IDX(i, j)];
+            } else {
+                break; /* NONE */
+            }
+        }
+    }
+    const int i0 = i, j0 = j;
+
+    /* gapped rows: head + path + tail (S/align/dp_traceback_impl.h:523-545) */
+    const int cap = n + l + 2;
+    char *rr = (char *)malloc((size_t)cap);
+    char *ar = (char *)malloc((size_t)cap);
+    int len = 0;
+    if (i0 != 0) {
+        for (int k = 0; k < i0; ++k) { rr[len] = '-'; ar[len] = DNA5_CHARS[ac[k]]; ++len; }
+    } else if (j0 != 0) {
+        for (int k = 0; k < j0; ++k) { rr[len] = DNA5_CHARS[rc[k]]; ar[len] = '-'; ++len; }
+    }
+    {
+        int ci = i0, cj = j0;
+        for (int k = plen - 1; k >= 0; --k) {
+            if (path[k] == 'D') { rr[len] = DNA5_CHARS[rc[cj]]; ar[len] = DNA5_CHARS[ac[ci]]; ++ci; ++cj; }
+            else if (path[k] == 'V') { rr[len] = '-'; ar[len] = DNA5_CHARS[ac[ci]]; ++ci; }
+            else { rr[len] = DNA5_CHARS[rc[cj]]; ar[len] = '-'; ++cj; }
+            ++len;
+        }
+    }
+    if (bi != l) {
+        for (int k = bi; k < l; ++k) { rr[len] = '-'; ar[len] = DNA5_CHARS[ac[k]]; ++len; }
+    }
+    if (bj != n) {
+        for (int k = bj; k < n; ++k) { rr[len] = DNA5_CHARS[rc[k]]; ar[len] = '-'; ++len; }
+    }
+
+    /* ScoredAlignment (porechop_abi/src/alignment.cpp:27-109) */
+    int st = -1, en = -1, a0 = -1, a1 = -1;
+    { int r = 0, a = 0;
+      for (int c = 0; c < len; ++c) { if (rr[c] != '-') r = 1; if (ar[c] != '-') a = 1; if (r && a) { st = c; break; } } }
+    { int r = 0, a = 0;
+      for (int c = len - 1; c >= 0; --c) { if (rr[c] != '-') r = 1; if (ar[c] != '-') a = 1; if (r && a) { en = c; break; } } }
+    if (st >= 0 && en >= 0) {
+        for (int c = 0; c < len; ++c) if (ar[c] != '-') { a0 = c; break; }
+        for (int c = len - 1; c >= 0; --c) if (ar[c] != '-') { a1 = c; break; }
+        int m1 = 0, m2 = 0;
+        for (int c = st; c < en + 1; ++c) if (ar[c] == rr[c]) ++m1;
+        for (int c = a0; c < a1 + 1; ++c) if (ar[c] == rr[c]) ++m2;
+        int rb = 0, ab = 0;
+        for (int c = 0; c < len; ++c) {
+            if (c == st) { out->rs = rb; out->as = ab; }
+            if (c == en) { out->re = rb; out->ae = ab; }
+            if (rr[c] != '-') ++rb;
+            if (ar[c] != '-') ++ab;
+        }
+        /* both identity numerators are the same set of D-match columns;
+         * keep them separate here so the restatement stays literal. */
+        out->m = m1;
+        out->l1 = en - st + 1;
+        out->l2 = a1 - a0 + 1;
+        if (m1 != m2) out->m = -1000000 - m2; /* never happens; flags a broken assumption */
+    }
+    free(rr); free(ar); free(path);
+    free(S); free(H); free(V); free(T); free(rc); free(ac);
+#undef IDX
+}
+
+static int fmt_pid(char *buf, size_t cap, int m, int l) {
+    if (l == 0) return snprintf(buf, cap, "-nan"); /* 0.0/0 on x86-64 is the negative default NaN */
+    double d = 100.0 * m / l;
+    return snprintf(buf, cap, "%f", d);
+}
+
+char *pcabi_oracle_adapter_alignment(const char *read, const char *adapter,
+                                     int ma, int mi, int go, int ge) {
+    pcabi_oracle_result r;
+    pcabi_oracle_align(read, (int)strlen(read), adapter, (int)strlen(adapter), ma, mi, go, ge, &r);
+    char p1[64], p2[64];
+    char *s = (char *)malloc(256);
+    if (r.rs == -1) {
+        /* reference leaves the remaining fields uninitialised; only field 0 is defined */
+        snprintf(s, 256, "-1,0,-1,0,%d,0.000000,0.000000", r.score);
+        return s;
+    }
+    fmt_pid(p1, sizeof p1, r.m, r.l1);
+    fmt_pid(p2, sizeof p2, r.m, r.l2);
+    snprintf(s, 256, "%d,%d,%d,%d,%d,%s,%s", r.rs, r.re, r.as, r.ae, r.score, p1, p2);
+    return s;
+}
+
+void pcabi_oracle_free(char *p) { free(p); }
+
+void pcabi_oracle_align_batch(const char *reads, const long long *read_off, const int *read_len,
+                              const char *adapters, const int *adp_off, const int *adp_len,
+                              const int *adp_idx, long long n_pairs,
+                              int ma, int mi, int go, int ge, int *results) {
+    for (long long p = 0; p < n_pairs; ++p) {
+        pcabi_oracle_result r;
+        int a = adp_idx[p];
+        pcabi_oracle_align(reads + read_off[p], read_len[p], adapters + adp_off[a], adp_len[a],
+                           ma, mi, go, ge, &r);
+        int *o = results + 8 * p;
+        o[0] = r.rs; o[1] = r.re; o[2] = r.as; o[3] = r.ae;
+        o[4] = r.score; o[5] = r.m; o[6] = r.l1; o[7] = r.l2;
+    }
+}

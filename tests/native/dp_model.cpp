@@ -1,0 +1,36 @@
+// Host build of the device DP core (custom_porechop_abi_amd/csrc/pcabi_dp.h) for CPU-side
+// fuzzing against oracle/. TEST-ONLY: the product never runs this; it exists so the exact
+// per-lane algorithm the HIP kernels execute can be checked exhaustively without a GPU.
+#include "../../custom_porechop_abi_amd/csrc/pcabi_dp.h"
+#include <cstring>
+
+static int dna5(unsigned char c) {
+    switch (c) { case 'A': case 'a': return 0; case 'C': case 'c': return 1; case 'G': case 'g': return 2;
+                 case 'T': case 't': case 'U': case 'u': return 3; default: return 4; }
+}
+
+template <int RPL>
+static void run(const char *read, int n, const char *adp, int L, pcabi::Scoring sc, int *out) {
+    const int off = RPL - L;
+    auto rd = [&](int j) { return dna5((unsigned char)read[j - 1]); };
+    auto ad = [&](int s) { return dna5((unsigned char)adp[s - off - 1]); };
+    pcabi::Result r = (sc.go != sc.ge) ? pcabi::align_lane<RPL, true>(rd, n, ad, L, sc)
+                                       : pcabi::align_lane<RPL, false>(rd, n, ad, L, sc);
+    out[0] = r.rs; out[1] = r.re; out[2] = r.as; out[3] = r.ae;
+    out[4] = r.score; out[5] = r.m; out[6] = r.l1; out[7] = r.l2;
+}
+
+extern "C" int pcabi_model_align(const char *read, int n, const char *adp, int L,
+                                 int ma, int mi, int go, int ge, int *out) {
+    pcabi::Scoring sc{ma, mi, go, ge};
+    if (L <= 0 || n <= 0) return -1;
+    if (L <= 8) run<8>(read, n, adp, L, sc, out);
+    else if (L <= 16) run<16>(read, n, adp, L, sc, out);
+    else if (L <= 32) run<32>(read, n, adp, L, sc, out);
+    else if (L <= 64) run<64>(read, n, adp, L, sc, out);
+    else if (L <= 128) run<128>(read, n, adp, L, sc, out);
+    else return -2;
+    return 0;
+}
+
+extern "C" double pcabi_model_pid6(int m, int l) { return pcabi::pid6(m, l); }

@@ -1,0 +1,78 @@
+"""ctypes access to the CPU oracle (oracle/pcabi_oracle.c). TEST INFRASTRUCTURE ONLY."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SO = os.path.join(ROOT, 'oracle', 'liboracle.so')
+
+
+class Result(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_int) for k in ('rs', 're', 'as_', 'ae', 'score', 'm', 'l1', 'l2')]
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    src = os.path.join(ROOT, 'oracle', 'pcabi_oracle.c')
+    if not os.path.isfile(SO) or os.path.getmtime(SO) < os.path.getmtime(src):
+        subprocess.check_call(['make', '-s', '-C', os.path.join(ROOT, 'oracle')])
+    L = ctypes.CDLL(SO)
+    L.pcabi_oracle_align.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int] + \
+        [ctypes.c_int] * 4 + [ctypes.POINTER(Result)]
+    L.pcabi_oracle_adapter_alignment.argtypes = [ctypes.c_char_p, ctypes.c_char_p] + [ctypes.c_int] * 4
+    L.pcabi_oracle_adapter_alignment.restype = ctypes.c_void_p
+    L.pcabi_oracle_free.argtypes = [ctypes.c_void_p]
+    L.pcabi_oracle_align_batch.argtypes = [ctypes.c_void_p] * 7 + [ctypes.c_longlong] + \
+        [ctypes.c_int] * 4 + [ctypes.c_void_p]
+    _lib = L
+    return L
+
+
+def align(read, adapter, scoring):
+    """8 ints (rs, re, as, ae, score, m, l1, l2) for one pair; read/adapter are str."""
+    L = load()
+    r = Result()
+    rb, ab = read.encode('utf-8'), adapter.encode('utf-8')
+    L.pcabi_oracle_align(rb, len(rb), ab, len(ab), *scoring[:4], ctypes.byref(r))
+    return [r.rs, r.re, r.as_, r.ae, r.score, r.m, r.l1, r.l2]
+
+
+def result_string(read, adapter, scoring):
+    L = load()
+    p = L.pcabi_oracle_adapter_alignment(read.encode('utf-8'), adapter.encode('utf-8'), *scoring[:4])
+    s = ctypes.cast(p, ctypes.c_char_p).value.decode()
+    L.pcabi_oracle_free(p)
+    return s
+
+
+def align_many(reads, adapters, pairs, scoring):
+    """(8, n_pairs) int32 for explicit (read_idx, adapter_idx) pairs."""
+    L = load()
+    rb = [r.encode('utf-8') for r in reads]
+    ab = [a.encode('utf-8') for a in adapters]
+    rbuf = b''.join(rb) + b'\0'
+    abuf = b''.join(ab) + b'\0'
+    roff = np.zeros(len(rb), np.int64)
+    roff[1:] = np.cumsum([len(x) for x in rb])[:-1] if len(rb) > 1 else []
+    rlen = np.array([len(x) for x in rb], np.int32)
+    aoff = np.zeros(len(ab), np.int32)
+    aoff[1:] = np.cumsum([len(x) for x in ab])[:-1] if len(ab) > 1 else []
+    alen = np.array([len(x) for x in ab], np.int32)
+    pr = np.asarray(pairs[0], np.int64)
+    pa = np.ascontiguousarray(pairs[1], np.int32)
+    off_p = np.ascontiguousarray(roff[pr])
+    len_p = np.ascontiguousarray(rlen[pr])
+    out = np.zeros((len(pr), 8), np.int32)
+    rbufa = np.frombuffer(rbuf, np.uint8)
+    abufa = np.frombuffer(abuf, np.uint8)
+    vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    L.pcabi_oracle_align_batch(vp(rbufa), vp(off_p), vp(len_p), vp(abufa), vp(aoff), vp(alen), vp(pa),
+                               len(pr), *scoring[:4], vp(out))
+    return out.T.copy()

@@ -1,0 +1,142 @@
+"""GPU parity: libpcabi.so (HIP, gfx950) vs the CPU oracle, bit-exact on every integer field.
+
+Oracle = oracle/pcabi_oracle.c, itself pinned to the reference's own outputs by
+tests/test_oracle_golden.py. Sizes are chosen so the oracle finishes in seconds.
+"""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+from tests import oracle_lib
+
+SCHEMES = [(3, -6, -5, -2),   # reference default (arg_parser.py:178-180)
+           (2, -1, -1, -1),   # linear gaps (open == extend)
+           (1, -1, -3, -1),
+           (3, -6, -2, -5),   # open cheaper than extend
+           (5, -4, -8, -6)]
+
+
+def _rand_seq(rng, n, alph):
+    return ''.join(rng.choice(alph) for _ in range(n))
+
+
+def _mutate(rng, s, rate):
+    out = []
+    for c in s:
+        x = rng.random()
+        if x < rate / 3:
+            out.append(rng.choice('ACGT'))
+        elif x < 2 * rate / 3:
+            continue
+        elif x < rate:
+            out.append(c)
+            out.append(rng.choice('ACGT'))
+        else:
+            out.append(c)
+    return ''.join(out)
+
+
+def _case_set(seed, n_reads, n_adp, max_read, max_adp):
+    rng = random.Random(seed)
+    alph = rng.choice(['ACGT', 'ACGTN', 'AT', 'A', 'ACGT-'])
+    adps = [_rand_seq(rng, rng.choice([1, 2, 5, 8, 22, 24, 28, 32, 33, 50, rng.randint(1, max_adp)]), 'ACGT')
+            for _ in range(n_adp)]
+    reads = []
+    for _ in range(n_reads):
+        n = rng.choice([0, 1, 3, 17, 150, rng.randint(0, max_read)])
+        r = _rand_seq(rng, n, alph)
+        if n > 30 and rng.random() < 0.5:
+            a = _mutate(rng, rng.choice(adps), 0.1)
+            p = rng.randint(0, max(0, n - len(a)))
+            r = r[:p] + a + r[p + len(a):]
+        reads.append(r)
+    return reads, adps
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('scheme', SCHEMES)
+def test_cross_product_parity(gpu_lib, scheme):
+    from custom_porechop_abi_amd import engine
+    for seed in range(3):
+        reads, adps = _case_set(1000 * seed + hash(scheme) % 997, 96, 9, 260, 128)
+        pack = engine.SeqPack(reads)
+        got = engine.align(pack.views(np.zeros(len(reads), np.int64), pack.lengths), adps, scheme)
+        n = len(reads)
+        pr = np.tile(np.arange(n), len(adps))
+        pa = np.repeat(np.arange(len(adps)), n)
+        exp = oracle_lib.align_many(reads, adps, (pr, pa), scheme)
+        ok = exp[0] != -1
+        # rs == -1 (empty input): only field 0 is defined by the reference
+        assert np.array_equal(got[0], exp[0])
+        assert np.array_equal(got[:, ok], exp[:, ok]), _first_diff(got, exp, reads, adps, n)
+
+
+def _first_diff(got, exp, reads, adps, n):
+    bad = np.nonzero(np.any(got != exp, axis=0))[0]
+    k = int(bad[0])
+    return 'pair %d read=%r adapter=%r got=%s exp=%s' % (k, reads[k % n], adps[k // n], got[:, k], exp[:, k])
+
+
+@pytest.mark.gpu
+def test_pairs_mode_and_windows(gpu_lib):
+    """Explicit pairs + start/end windows of longer reads (the end-trim layout)."""
+    from custom_porechop_abi_amd import engine
+    rng = random.Random(7)
+    reads, adps = _case_set(77, 200, 12, 1200, 64)
+    pack = engine.SeqPack(reads)
+    sw, ew = engine.start_end_windows(pack, 150)
+    sc = (3, -6, -5, -2)
+    pr = np.array([rng.randrange(len(reads)) for _ in range(3000)], np.int32)
+    pa = np.array([rng.randrange(len(adps)) for _ in range(3000)], np.int32)
+    for win, slicer in ((sw, lambda s: s[:150]), (ew, lambda s: s[-150:])):
+        got = engine.align(win, adps, sc, pairs=(pr, pa))
+        exp = oracle_lib.align_many([slicer(r) for r in reads], adps, (pr, pa), sc)
+        ok = exp[0] != -1
+        assert np.array_equal(got[0], exp[0])
+        assert np.array_equal(got[:, ok], exp[:, ok])
+
+
+@pytest.mark.gpu
+def test_legacy_string_abi(gpu_lib):
+    """adapterAlignment()/freeCString() return the reference's exact text."""
+    from custom_porechop_abi_amd import cpp_function_wrappers as w
+    known = [('ACGTACGTAC', 'GTAC', '2,5,0,3,12,100.000000,100.000000'),
+             ('AAAAAAAAAA', 'AAAA', '0,3,0,3,12,100.000000,100.000000'),
+             ('AAAA', 'AAAAAAAAAA', '0,3,0,3,12,100.000000,40.000000'),
+             ('GGGGGGGG', 'TTTT', '0,0,4,3,0,-nan,0.000000'),
+             ('A', 'C', '0,0,1,0,0,-nan,0.000000'),
+             ('AC--GT', 'ACGT', '0,5,0,3,5,66.666667,66.666667')]
+    for r, a, s in known:
+        assert w.adapter_alignment(r, a, [3, -6, -5, -2]) == s
+    assert w.adapter_alignment('', 'ACGT', [3, -6, -5, -2]).split(',')[0] == '-1'
+    rng = random.Random(3)
+    for _ in range(60):
+        sc = rng.choice(SCHEMES)
+        r = _rand_seq(rng, rng.randint(1, 400), 'ACGTN')
+        a = _rand_seq(rng, rng.randint(1, 100), 'ACGT')
+        assert w.adapter_alignment(r, a, list(sc)) == oracle_lib.result_string(r, a, sc)
+
+
+@pytest.mark.gpu
+def test_long_reads_middle_shape(gpu_lib):
+    """Whole-read alignments (the middle-adapter scan shape): reads of several kb."""
+    from custom_porechop_abi_amd import engine
+    rng = random.Random(11)
+    adps = ['AATGTACTTCGTTCAGTTACGTATTGCT', 'GCAATACGTAACTGAACGAAGT', 'ACGTTTAGGCAT']
+    reads = []
+    for k in range(70):
+        n = rng.randint(1000, 9000)
+        r = _rand_seq(rng, n, 'ACGT')
+        if k % 3 == 0:
+            a = _mutate(rng, adps[k % 2], 0.05)
+            p = rng.randint(0, n - len(a))
+            r = r[:p] + a + r[p + len(a):]
+        reads.append(r)
+    pack = engine.SeqPack(reads)
+    sc = (3, -6, -5, -2)
+    got = engine.align(pack.views(np.zeros(len(reads), np.int64), pack.lengths), adps, sc)
+    n = len(reads)
+    exp = oracle_lib.align_many(reads, adps, (np.tile(np.arange(n), 3), np.repeat(np.arange(3), n)), sc)
+    assert np.array_equal(got, exp)
