@@ -1,0 +1,322 @@
+#!/usr/bin/env python3
+"""Headline benchmark: reads/s trimmed, 100k synthetic ONT reads x 50 adapter sets (BASELINE.json).
+
+One *step* = the end-trim hot path for one batch of reads, inputs resident in HBM:
+    start windows (seq[:150]) x start adapters  -> k_align_cross   (nanopore_read.py:175-195)
+    end windows   (seq[-150:]) x end adapters   -> k_align_cross   (nanopore_read.py:197-217)
+    per-read trim decisions                     -> k_end_trim
+for the first 50 non-"full sequence" adapter sets of the reference database
+(porechop_abi/adapters.py:77-), scoring 3,-6,-5,-2, end_size 150, end_threshold 75,
+extra_end_trim 2, min_trim_size 4 (reference defaults, arg_parser.py:178-208).
+
+Multi-GPU: one process per GPU (torch.distributed.run); each rank trims its own 100k-read shard
+(weak scaling, no data-path collective); the step time is the max over ranks (RCCL all-reduce
+MAX of the rank times). value = reads all ranks trimmed / that time.
+
+Also reported: roofline of the dominant kernel (k_align_cross, VALU-bound: integer cell updates,
+DESIGN.md §5), an HBM figure, and the reference SeqAn CPU path (oracle/_ref, compiled from the
+reference sources) timed on a bounded sample on this host's cores.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # int32 lane-ops/s: 256 CU x 4 SIMD32 x 2.4 GHz
+HBM_PEAK_GBS = 8000.0
+OPS_PER_CELL = 10                               # algorithmic int ops per cell
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--reads', type=int, default=100000, help='reads per GPU')
+    ap.add_argument('--sets', type=int, default=50)
+    ap.add_argument('--end-size', type=int, default=150)
+    ap.add_argument('--mean-len', type=int, default=8000)
+    ap.add_argument('--cpu-sample', type=int, default=3000, help='reads in the CPU-baseline sample (0 = skip)')
+    ap.add_argument('--cpu-threads', type=int, default=0, help='0 = min(16, cpus available)')
+    ap.add_argument('--check', type=int, default=256, help='reads checked against the oracle after timing')
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get('RANK', '0'))
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    import torch  # single HIP runtime for torch (RCCL) and libpcabi (see _lib.py)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl')
+    from custom_porechop_abi_amd import _lib, adapters as A, synth
+    from custom_porechop_abi_amd.engine import encode_adapters
+    L = _lib.lib()
+    _lib.check(L.pcabi_dev_set(local), 'pcabi_dev_set')
+
+    # ---- workload (host) ----
+    sets = [a for a in A.fresh_adapters() if '(full sequence)' not in a.name][:args.sets]
+    start_adps = [a.start_sequence[1] for a in sets if a.start_sequence]
+    end_adps = [a.end_sequence[1] for a in sets if a.end_sequence]
+    t0 = time.time()
+    reads = synth.make_reads(args.reads, args.mean_len, seed=12345 + rank, keep=args.end_size)
+    buf, s_off, s_len, e_off, e_len = synth.pack_end_windows(reads, args.end_size)
+    gen_s = time.time() - t0
+    n = args.reads
+
+    # ---- device-resident inputs ----
+    vp = ctypes.c_void_p
+
+    def dalloc(nbytes):
+        p = vp()
+        _lib.check(L.pcabi_dev_malloc(ctypes.byref(p), max(int(nbytes), 16)), 'malloc')
+        return p
+
+    def h2d(arr):
+        arr = np.ascontiguousarray(arr)
+        p = dalloc(arr.nbytes)
+        _lib.check(L.pcabi_dev_h2d(p, arr.ctypes.data_as(vp), arr.nbytes), 'h2d')
+        return p
+
+    d_codes = h2d(buf)
+    d_soff, d_slen, d_eoff, d_elen = h2d(s_off), h2d(s_len), h2d(e_off), h2d(e_len)
+    tabs = []
+    for lst in (start_adps, end_adps):
+        c, o, l = encode_adapters(lst)
+        t = vp()
+        _lib.check(L.pcabi_adapters_create(c.ctypes.data_as(vp), o.ctypes.data_as(vp), l.ctypes.data_as(vp),
+                                           len(lst), ctypes.byref(t)), 'adapters_create')
+        tabs.append(t)
+    n_sa, n_ea = len(start_adps), len(end_adps)
+    s_stride, e_stride = n_sa * n, n_ea * n
+    d_sres = dalloc(4 * 8 * s_stride)
+    d_eres = dalloc(4 * 8 * e_stride)
+    d_st, d_et = dalloc(4 * n), dalloc(4 * n)
+    stream = vp()
+    _lib.check(L.pcabi_stream_create(ctypes.byref(stream)), 'stream')
+    sc = (3, -6, -5, -2)
+
+    def align_start():
+        _lib.check(L.pcabi_align_cross_dev(d_codes, d_soff, d_slen, n, tabs[0], *sc, d_sres, s_stride, stream), 'align')
+
+    def align_end():
+        _lib.check(L.pcabi_align_cross_dev(d_codes, d_eoff, d_elen, n, tabs[1], *sc, d_eres, e_stride, stream), 'align')
+
+    def epilogue():
+        _lib.check(L.pcabi_end_trim_dev(d_sres, s_stride, n_sa, d_eres, e_stride, n_ea, n, args.end_size,
+                                        2, 75.0, 4, d_st, d_et, None, None, stream), 'end_trim')
+
+    ev = []
+    for _ in range(2 * args.steps + 2):
+        e = vp()
+        _lib.check(L.pcabi_event_create(ctypes.byref(e)), 'event')
+        ev.append(e)
+
+    def step(k=None):
+        if k is not None:
+            L.pcabi_event_record(ev[2 * k], stream)
+        align_start()
+        align_end()
+        if k is not None:
+            L.pcabi_event_record(ev[2 * k + 1], stream)
+        epilogue()
+
+    for _ in range(args.warmup):
+        step()
+    _lib.check(L.pcabi_stream_sync(stream), 'sync')
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize() if torch.cuda.is_available() else None
+        L.pcabi_stream_sync(stream)
+
+    barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(k)
+    L.pcabi_stream_sync(stream)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device='cuda')
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    align_ms = []
+    for k in range(args.steps):
+        ms = ctypes.c_float()
+        _lib.check(L.pcabi_event_elapsed_ms(ctypes.byref(ms), ev[2 * k], ev[2 * k + 1]), 'elapsed')
+        align_ms.append(ms.value)
+    align_ms = float(np.mean(align_ms))
+
+    # ---- algorithmic work per step (per GPU) ----
+    s_len64, e_len64 = s_len.astype(np.int64), e_len.astype(np.int64)
+    La = np.array([len(x) for x in start_adps], np.int64)
+    Le = np.array([len(x) for x in end_adps], np.int64)
+    cells = int(s_len64.sum() * La.sum() + e_len64.sum() * Le.sum())
+    alignments = n * (n_sa + n_ea)
+    alg_bytes = int(s_len64.sum() * 1 + e_len64.sum() * 1 + La.sum() + Le.sum() + alignments * 32)
+    tops = cells * OPS_PER_CELL / (align_ms * 1e-3) / 1e12
+    gbs = alg_bytes / (align_ms * 1e-3) / 1e9
+
+    # ---- correctness spot-check (outside the timed region) ----
+    checked = None
+    if args.check and rank == 0:
+        checked = spot_check(L, _lib, d_sres, d_eres, d_st, d_et, s_stride, e_stride, n, n_sa, n_ea, reads,
+                             start_adps, end_adps, args.end_size, min(args.check, n), sc)
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        cpu = cpu_baseline(reads[:args.cpu_sample], sets, args.end_size, sc, args.cpu_threads)
+
+    if rank == 0:
+        value = world * n * args.steps / elapsed
+        prof = load_traffic()
+        out = {
+            'metric': 'reads/sec trimmed (100k ONT reads x 50 adapter pairs)',
+            'value': round(value, 1),
+            'unit': 'reads/s',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': round(1e3 * elapsed / args.steps, 4),
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': 'int32',
+            'data': 'synthetic (seeded ONT-like reads, SURVEY.md §8d recipe; mean %d bp)' % args.mean_len,
+            'config': {'workload': 'end-trim: %d reads/GPU x %d adapter sets (%d start + %d end adapters), '
+                                   'start+end windows of %d bp, + per-read trim decisions'
+                                   % (n, len(sets), n_sa, n_ea, args.end_size),
+                       'reads_per_gpu': n, 'adapter_sets': len(sets), 'end_size': args.end_size,
+                       'scoring': list(sc), 'parallelism': 'dp%d (read shards)' % world},
+            'roofline': {'bound': 'valu', 'achieved': round(tops, 3), 'peak': round(VALU_PEAK_TOPS, 1),
+                         'unit': 'Tops/s (int32 lane-ops)', 'frac': round(tops / VALU_PEAK_TOPS, 4),
+                         'traffic': prof.get('traffic_bytes_per_step') if prof else None,
+                         'kernel': 'k_align_cross (start+end launches)',
+                         'ops_per_cell': OPS_PER_CELL, 'cells_per_step': cells,
+                         'kernel_ms_per_step': round(align_ms, 4)},
+            'hbm': {'achieved': round(gbs, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                    'frac': round(gbs / HBM_PEAK_GBS, 5), 'algorithmic_bytes_per_step': alg_bytes},
+            'gcups': round(cells / (align_ms * 1e-3) / 1e9, 1),
+            'cpu_baseline': cpu,
+            'gpu_vs_cpu': round(value / cpu['value'], 1) if cpu else None,
+            'parity_spot_check': checked,
+            'setup_s': round(gen_s, 2),
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def spot_check(L, _lib, d_sres, d_eres, d_st, d_et, s_stride, e_stride, n, n_sa, n_ea, reads, start_adps,
+               end_adps, E, k, sc):
+    """Compare the first k reads' trim amounts and raw alignment fields with the oracle."""
+    from tests import oracle_lib
+    from custom_porechop_abi_amd import synth
+    vp = ctypes.c_void_p
+    sres = np.empty((8, s_stride), np.int32)
+    eres = np.empty((8, e_stride), np.int32)
+    _lib.check(L.pcabi_dev_d2h(sres.ctypes.data_as(vp), d_sres, sres.nbytes), 'd2h')
+    _lib.check(L.pcabi_dev_d2h(eres.ctypes.data_as(vp), d_eres, eres.nbytes), 'd2h')
+    heads, tails = [], []
+    for r in reads[:k]:
+        if isinstance(r, tuple):
+            heads.append(synth.codes_to_str(r[0]))
+            tails.append(synth.codes_to_str(r[1]))
+        else:
+            heads.append(synth.codes_to_str(r[:E]))
+            tails.append(synth.codes_to_str(r[-E:]))
+    bad = 0
+    for wins, adps, res, nad in ((heads, start_adps, sres, n_sa), (tails, end_adps, eres, n_ea)):
+        pr = np.tile(np.arange(k), nad)
+        pa = np.repeat(np.arange(nad), k)
+        exp = oracle_lib.align_many(wins, adps, (pr, pa), sc)
+        got = res.reshape(8, nad, n)[:, :, :k].reshape(8, -1)
+        bad += int(np.sum(np.any(got != exp, axis=0)))
+    return {'pairs_checked': int(k * (n_sa + n_ea)), 'mismatches': bad}
+
+
+def cpu_baseline(reads, sets, E, sc, threads):
+    """The reference CPU path on a bounded sample: for every read, every adapter set's start and
+    end window through the reference's own adapterAlignment (oracle/_ref/cpp_functions.so, built
+    from /root/reference sources by oracle/Makefile) called via ctypes exactly as
+    porechop_abi/cpp_function_wrappers.py does, fanned out over a ThreadPool like
+    porechop_abi.py:418-432. Falls back to the oracle port if the reference build is absent."""
+    from multiprocessing.dummy import Pool as ThreadPool
+    from custom_porechop_abi_amd import synth
+    ref = os.path.join(ROOT, 'oracle', '_ref', 'cpp_functions.so')
+    kind = 'reference'
+    if os.path.isfile(ref):
+        lib = ctypes.CDLL(ref)
+        fn, fr = lib.adapterAlignment, lib.freeCString
+    else:
+        from tests import oracle_lib
+        lib = oracle_lib.load()
+        fn, fr = lib.pcabi_oracle_adapter_alignment, lib.pcabi_oracle_free
+        kind = 'port'
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_char_p] + [ctypes.c_int] * 4
+    fn.restype = ctypes.c_void_p
+    fr.argtypes = [ctypes.c_void_p]
+    jobs = []
+    for r in reads:
+        if isinstance(r, tuple):
+            h, t = synth.codes_to_str(r[0]), synth.codes_to_str(r[1])
+        else:
+            h, t = synth.codes_to_str(r[:E]), synth.codes_to_str(r[-E:])
+        jobs.append((h.encode(), t.encode()))
+    starts = [a.start_sequence[1].encode() for a in sets if a.start_sequence]
+    ends = [a.end_sequence[1].encode() for a in sets if a.end_sequence]
+
+    def one(job):
+        h, t = job
+        best = 0
+        for a in starts:
+            p = fn(h, a, *sc)
+            s = ctypes.cast(p, ctypes.c_char_p).value
+            fr(p)
+            best += len(s)
+        for a in ends:
+            p = fn(t, a, *sc)
+            s = ctypes.cast(p, ctypes.c_char_p).value
+            fr(p)
+            best += len(s)
+        return best
+
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else os.cpu_count()
+    nthr = threads or max(1, min(16, avail))
+    t0 = time.perf_counter()
+    with ThreadPool(nthr) as pool:
+        list(pool.imap(one, jobs, chunksize=4))
+    dt = time.perf_counter() - t0
+    return {'value': round(len(jobs) / dt, 2), 'unit': 'reads/s', 'cores': nthr, 'kind': kind,
+            'sample': '%d reads x %d+%d adapters (%d alignments), %.1f s wall, ThreadPool(%d) over ctypes '
+                      'adapterAlignment' % (len(jobs), len(starts), len(ends), len(jobs) * (len(starts) + len(ends)),
+                                            dt, nthr)}
+
+
+def load_traffic():
+    """HBM bytes per step from the committed rocprofv3 PMC pass (profiles/), if present."""
+    p = os.path.join(ROOT, 'profiles', 'traffic.json')
+    if os.path.isfile(p):
+        try:
+            return json.load(open(p))
+        except Exception:
+            return None
+    return None
+
+
+if __name__ == '__main__':
+    main()

@@ -95,6 +95,9 @@ PCABI_HD Result finish(const Best &b, int L, int n) {
     const int trailV = b.ltype == LT_V ? b.trail : 0;
     const int trailH = b.ltype == LT_H ? b.trail : 0;
     const int lastD = b.ltype == LT_D ? 1 : 0;
+    // A run that spans the whole path has no column before it (the fast kernel's pass-through
+    // padding rows would otherwise report a virtual diagonal there).
+    const int precd = (b.trail < K) ? b.precd : 0;
     const int kR = K - 1 - trailV;                     // last path column holding a read base
     const int kA = K - 1 - trailH;                     // last path column holding an adapter base
     bool readSide;
@@ -105,11 +108,11 @@ PCABI_HD Result finish(const Best &b, int L, int n) {
     if (readSide) {
         ek = kR;
         r.re = b.bj - 1;
-        r.ae = b.bi - trailV - (trailV > 0 ? b.precd : lastD);
+        r.ae = b.bi - trailV - (trailV > 0 ? precd : lastD);
     } else {
         ek = kA;
         r.ae = b.bi - 1;
-        r.re = b.bj - trailH - (trailH > 0 ? b.precd : lastD);
+        r.re = b.bj - trailH - (trailH > 0 ? precd : lastD);
     }
     r.rs = j0;
     r.as = i0;
@@ -156,7 +159,7 @@ PCABI_HD void open_run(int slt, int same_kind, int t_prev, int p_prev, int &t, i
 //   adp[s] : adapter code of slot s (1-based; slots off+1..RPL), 0..4
 // ------------------------------------------------------------------------------------------
 template <int RPL, bool AFFINE, typename ReadFn, typename AdpFn>
-PCABI_HD Result align_lane(ReadFn rd, int n, AdpFn adp, int L, const Scoring sc) {
+PCABI_HD Result align_lane_generic(ReadFn rd, int n, AdpFn adp, int L, const Scoring sc) {
     const int off = RPL - L;
     int S[RPL + 1], H[RPL + 1];
     uint32_t SA[RPL + 1], HA[RPL + 1];
@@ -308,6 +311,208 @@ PCABI_HD Result align_lane(ReadFn rd, int n, AdpFn adp, int L, const Scoring sc)
         slt_last = lt_type;
     }
     return finish(best, L, n);
+}
+
+}  // namespace pcabi
+
+namespace pcabi {
+
+// ------------------------------------------------------------------------------------------
+// align_lane_fast<RPL, AFFINE>: the production core. Branch-free rows.
+//
+// The adapter (length L) sits in register slots off+1..RPL, off = RPL - L in 0..3 (buckets are
+// multiples of 4). Instead of skipping the padding slots (a branch per row that wrecks register
+// allocation), the padding slots COMPUTE a pass-through row: their adapter code never matches
+// (5), their mismatch score is 0 and their attribute increment advances the start column by one.
+// With gap_open < 0 and gap_extend < 0 every padding cell then takes the diagonal with S = 0,
+// V = H = gap_open (< 0), and attribute == attr_start(j): exactly the free-end-gap boundary row
+// the first real row expects. Only slots 1..3 can be padding, so only they
+// carry the two per-slot constants.
+//
+// Column n (the last) is peeled out of the loop: it alone scouts rows 1..L-1 and tracks the
+// trailing-V bookkeeping. The last-row scout of every column uses selects, not branches.
+// Preconditions (checked by the host): 1 <= L <= RPL <= L + 3; off == 0 or (go < 0 && ge < 0).
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t INC_PAD = 1u << ATTR_CSH;   // padding diagonal: start column + 1
+constexpr int PAD_CODE = 5;                     // never equal to a read code (0..4)
+
+template <int RPL, bool AFFINE>
+struct LaneDP {
+    int S[RPL + 1], H[RPL + 1];
+    uint32_t SA[RPL + 1], HA[RPL + 1];
+    // best end cell so far
+    int bscore, bi, bj, blt, btrail, bprec;
+    uint32_t battr;
+    // row-L running state: S-state last type at (L, j-1), H-state run (t, p) at (L, j-1)
+    int slt_last, ht_last, hp_last;
+    // per-slot constants for the only slots that may be padding
+    int mis[4];
+    uint32_t ids[4];
+
+    template <typename AdpFn, bool LAST>
+    PCABI_HD void column(const int r, const int j, const AdpFn &adp, const int L, const int off,
+                         const Scoring &sc) {
+        int sup = 0, vup = NEG, sdg = 0;
+        uint32_t saup = attr_start(j), vaup = 0, sadg = attr_start(j - 1);
+        int slt_up = LT_NONE, vt_up = 0, vp_up = 0;
+        int lv = 0, lh = 0, ls = 0, lslt = LT_D;
+        bool lhext = false;
+        uint32_t lva = 0, lha = 0, lsa = 0;
+#pragma unroll
+        for (int s = 1; s <= RPL; ++s) {
+            const bool match = (r == adp(s));
+            const int mi_s = (s <= 3) ? mis[s] : sc.mi;
+            const uint32_t id_s = (s <= 3) ? ids[s] : INC_D;
+            const int diag = sdg + (match ? sc.ma : mi_s);
+            const uint32_t da = sadg + (match ? INC_M : id_s);
+            int hn, vn, g;
+            uint32_t han, van, ga;
+            bool hext, vext, fromv;
+            if (AFFINE) {
+                const int hx = H[s] + sc.ge, ho = S[s] + sc.go;
+                hext = !(hx < ho);
+                hn = hext ? hx : ho;
+                han = hext ? HA[s] : SA[s];
+                const int vx = vup + sc.ge, vo = sup + sc.go;
+                vext = !(vx < vo);
+                vn = vext ? vx : vo;
+                van = vext ? vaup : saup;
+                fromv = !(vn < hn);
+                g = fromv ? vn : hn;
+                ga = fromv ? van : han;
+            } else {
+                hext = vext = false;
+                const int vv = sup + sc.ge, hh = S[s] + sc.ge;
+                fromv = !(vv < hh);
+                g = fromv ? vv : hh;
+                ga = fromv ? saup : SA[s];
+                hn = vn = NEG;
+                han = van = 0;
+            }
+            const bool isd = !(diag < g);
+            const int sn = isd ? diag : g;
+            const uint32_t san = isd ? da : ga;
+            if (LAST && s < RPL) {
+                const int slt = isd ? LT_D : (fromv ? LT_V : LT_H);
+                // trailing V run of the V-state (affine) or of the S-state from V (linear)
+                const bool cont = AFFINE ? (vext || slt_up == LT_V) : (slt_up == LT_V);
+                const int vt = cont ? vt_up + 1 : 1;
+                const int vp = cont ? vp_up : (slt_up == LT_D ? 1 : 0);
+                if (sn > bscore) {
+                    bscore = sn;
+                    bi = s - off;
+                    bj = j;
+                    if (AFFINE) {
+                        const bool isv = (vn == sn), ish = !isv && (hn == sn);
+                        battr = isv ? van : (ish ? han : san);
+                        blt = isv ? LT_V : (ish ? LT_H : LT_D);
+                        btrail = isv ? vt : 0;
+                        bprec = isv ? vp : 0;
+                    } else {
+                        battr = san;
+                        blt = slt;
+                        btrail = (slt == LT_V) ? vt : 0;
+                        bprec = (slt == LT_V) ? vp : 0;
+                    }
+                }
+                if (AFFINE) { vt_up = vt; vp_up = vp; }
+                else { vt_up = (slt == LT_V) ? vt : 0; vp_up = (slt == LT_V) ? vp : 0; }
+                slt_up = slt;
+            }
+            if (s == RPL) {
+                lv = vn; lh = hn; ls = sn; lva = van; lha = han; lsa = san; lhext = hext;
+                lslt = isd ? LT_D : (fromv ? LT_V : LT_H);
+                if (LAST) {
+                    const bool cont = AFFINE ? (vext || slt_up == LT_V) : (slt_up == LT_V);
+                    const int vt = cont ? vt_up + 1 : 1;
+                    const int vp = cont ? vp_up : (slt_up == LT_D ? 1 : 0);
+                    vt_up = vt;
+                    vp_up = vp;
+                }
+            }
+            sdg = S[s];
+            sadg = SA[s];
+            S[s] = sn;
+            H[s] = hn;
+            SA[s] = san;
+            HA[s] = han;
+            sup = sn;
+            vup = vn;
+            saup = san;
+            vaup = van;
+        }
+        // ---- row L: H-state trailing run at (L, j) and the last-row scout ----
+        const bool hcont = AFFINE ? (lhext || slt_last == LT_H) : (slt_last == LT_H);
+        const int ht = hcont ? ht_last + 1 : 1;
+        const int hp = hcont ? hp_last : (slt_last == LT_D ? 1 : 0);
+        const bool upd = ls > bscore;
+        int clt, ctrail, cprec;
+        uint32_t cattr;
+        if (AFFINE) {
+            const bool isv = (lv == ls), ish = !isv && (lh == ls);
+            cattr = isv ? lva : (ish ? lha : lsa);
+            clt = isv ? LT_V : (ish ? LT_H : LT_D);
+            ctrail = isv ? (LAST ? vt_up : 0) : (ish ? ht : 0);
+            cprec = isv ? (LAST ? vp_up : 0) : (ish ? hp : 0);
+        } else {
+            cattr = lsa;
+            clt = lslt;
+            ctrail = (lslt == LT_V) ? (LAST ? vt_up : 0) : (lslt == LT_H ? ht : 0);
+            cprec = (lslt == LT_V) ? (LAST ? vp_up : 0) : (lslt == LT_H ? hp : 0);
+        }
+        bscore = upd ? ls : bscore;
+        bi = upd ? L : bi;
+        bj = upd ? j : bj;
+        battr = upd ? cattr : battr;
+        blt = upd ? clt : blt;
+        btrail = upd ? ctrail : btrail;
+        bprec = upd ? cprec : bprec;
+        if (AFFINE) { ht_last = ht; hp_last = hp; }
+        else { ht_last = (lslt == LT_H) ? ht : 0; hp_last = (lslt == LT_H) ? hp : 0; }
+        slt_last = lslt;
+    }
+};
+
+template <int RPL, bool AFFINE, typename ReadFn, typename AdpFn>
+PCABI_HD Result align_lane_fast(ReadFn &rd, int n, const AdpFn &adp, int L, const Scoring sc) {
+    LaneDP<RPL, AFFINE> st;
+    const int off = RPL - L;
+#pragma unroll
+    for (int s = 1; s <= RPL; ++s) {
+        st.S[s] = 0;
+        st.H[s] = NEG;
+        st.SA[s] = attr_start(-(s > off ? s - off : 0));
+        st.HA[s] = 0;
+    }
+#pragma unroll
+    for (int s = 1; s <= 3; ++s) {
+        st.mis[s] = (s <= off) ? 0 : sc.mi;
+        st.ids[s] = (s <= off) ? INC_PAD : INC_D;
+    }
+    st.bscore = 0;   // first scouted cell (L, 0), S = 0
+    st.bi = L;
+    st.bj = 0;
+    st.battr = attr_start(-L);
+    st.blt = LT_NONE;
+    st.btrail = 0;
+    st.bprec = 0;
+    st.slt_last = LT_NONE;
+    st.ht_last = 0;
+    st.hp_last = 0;
+    for (int j = 1; j < n; ++j) st.template column<AdpFn, false>(rd(j), j, adp, L, off, sc);
+    st.template column<AdpFn, true>(rd(n), n, adp, L, off, sc);
+    Best b;
+    b.score = st.bscore; b.bi = st.bi; b.bj = st.bj; b.attr = st.battr;
+    b.ltype = st.blt; b.trail = st.btrail; b.precd = st.bprec;
+    return finish(b, L, n);
+}
+
+// Which kernel core a (length, scoring) pair may use.
+PCABI_HD bool fast_ok(int L, int rpl, const Scoring &sc) {
+    const int off = rpl - L;
+    if (off < 0 || off > 3) return false;
+    if (off == 0) return true;
+    return (sc.go != sc.ge) ? (sc.go < 0 && sc.ge < 0) : (sc.ge < 0);
 }
 
 }  // namespace pcabi

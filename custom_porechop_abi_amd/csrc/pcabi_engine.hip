@@ -38,14 +38,28 @@ int fail(int code, const std::string &msg) {
             return fail(PCABI_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-// Register buckets: adapters of length L run in the smallest bucket RPL >= L.
-constexpr int kBuckets[] = {8, 16, 24, 32, 48, 64, 96, 128};
+// Register buckets. FAST (branch-free core, pcabi_dp.h align_lane_fast): every multiple of 4 up
+// to 64, used whenever pcabi::fast_ok holds. GENERIC (guarded core, any scoring): a few sizes,
+// also the only path for 64 < L <= 128 for now.
+enum Kind { FAST = 0, GENERIC = 1 };
+struct BucketDef {
+    int rpl;
+    Kind kind;
+};
+constexpr BucketDef kBuckets[] = {
+    {4, FAST},  {8, FAST},  {12, FAST}, {16, FAST}, {20, FAST}, {24, FAST}, {28, FAST}, {32, FAST},
+    {36, FAST}, {40, FAST}, {44, FAST}, {48, FAST}, {52, FAST}, {56, FAST}, {60, FAST}, {64, FAST},
+    {16, GENERIC}, {32, GENERIC}, {64, GENERIC}, {96, GENERIC}, {128, GENERIC}};
 constexpr int kNumBuckets = sizeof(kBuckets) / sizeof(kBuckets[0]);
 constexpr int kMaxRPL = 128;
 
-int bucket_of(int L) {
+int bucket_of(int L, const pcabi::Scoring &sc) {
+    if (L <= 64) {
+        const int rpl = (L + 3) & ~3;
+        if (pcabi::fast_ok(L, rpl, sc)) return rpl / 4 - 1;
+    }
     for (int b = 0; b < kNumBuckets; ++b)
-        if (L <= kBuckets[b]) return b;
+        if (kBuckets[b].kind == GENERIC && L <= kBuckets[b].rpl) return b;
     return -1;
 }
 
@@ -119,7 +133,7 @@ __device__ __forceinline__ pcabi::Result empty_result() {
     return r;
 }
 
-template <int RPL, bool AFFINE>
+template <int RPL, bool AFFINE, int KIND>
 __device__ __forceinline__ void run_lane(const KParams &p, int a_local, int64_t w, int64_t out_idx) {
     AdapterRegs<RPL> adp;
     adp.load(p.adp_pad + (int64_t)a_local * (RPL / 4));
@@ -131,30 +145,30 @@ __device__ __forceinline__ void run_lane(const KParams &p, int a_local, int64_t 
         r = empty_result();
     } else {
         WindowReader rd(p.codes + p.win_off[w]);
-        r = pcabi::align_lane<RPL, AFFINE>(rd, n, adp, L, p.sc);
+        if (KIND == FAST) r = pcabi::align_lane_fast<RPL, AFFINE>(rd, n, adp, L, p.sc);
+        else r = pcabi::align_lane_generic<RPL, AFFINE>(rd, n, adp, L, p.sc);
     }
     store_result(p.out, p.out_stride, out_idx, r);
 }
 
-// grid: x = ceil(n_win / 256) window blocks (4 waves x 64 windows), y = bucket adapters
-template <int RPL, bool AFFINE>
-__global__ __launch_bounds__(256) void k_align_cross(KParams p) {
-    const int a_local = blockIdx.y;
-    const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int a_glob = p.adp_id[a_local];
-    const int64_t out_idx = (int64_t)a_glob * p.n_win + w;
-    run_lane<RPL, AFFINE>(p, a_local, w < p.n_win ? w : -1, out_idx);
-}
-
-// grid: x = ceil(n_waves / 4); each wave one adapter, lanes = tasks
-template <int RPL, bool AFFINE>
-__global__ __launch_bounds__(256) void k_align_pairs(KParams p) {
-    const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (wave >= p.n_waves) return;
-    const int64_t slot = wave * 64 + (threadIdx.x & 63);
-    const int a_local = __builtin_amdgcn_readfirstlane(p.wave_adp[wave]);
-    const int32_t tw = p.task_win[slot];
-    run_lane<RPL, AFFINE>(p, a_local, tw, tw >= 0 ? p.task_out[slot] : 0);
+// One kernel for both work shapes (uniform branch on p.task_win):
+//  cross: grid (ceil(n_win/256), n_adp); lane = window, blockIdx.y = bucket-local adapter
+//  pairs: grid (ceil(n_waves/4)); wave = one adapter, lanes = host-grouped tasks
+template <int RPL, bool AFFINE, int KIND>
+__global__ __launch_bounds__(256) void k_align(KParams p) {
+    if (p.task_win == nullptr) {
+        const int a_local = blockIdx.y;
+        const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
+        const int a_glob = p.adp_id[a_local];
+        run_lane<RPL, AFFINE, KIND>(p, a_local, w < p.n_win ? w : -1, (int64_t)a_glob * p.n_win + w);
+    } else {
+        const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+        if (wave >= p.n_waves) return;
+        const int64_t slot = wave * 64 + (threadIdx.x & 63);
+        const int a_local = __builtin_amdgcn_readfirstlane(p.wave_adp[wave]);
+        const int32_t tw = p.task_win[slot];
+        run_lane<RPL, AFFINE, KIND>(p, a_local, tw, tw >= 0 ? p.task_out[slot] : 0);
+    }
 }
 
 // ---- decision epilogues --------------------------------------------------------------------
@@ -229,43 +243,30 @@ __global__ __launch_bounds__(256) void k_best_full_id(const int32_t *res, int64_
 
 // ---- launch plumbing -------------------------------------------------------------------------
 
-template <int RPL>
-void launch_cross(const KParams &p, bool affine, int64_t n_win, hipStream_t st) {
-    dim3 grid((unsigned)((n_win + 255) / 256), (unsigned)p.n_adp);
-    if (affine) hipLaunchKernelGGL((k_align_cross<RPL, true>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((k_align_cross<RPL, false>), grid, dim3(256), 0, st, p);
+template <int RPL, int KIND>
+void launch(const KParams &p, bool affine, dim3 grid, hipStream_t st) {
+    if (affine) hipLaunchKernelGGL((k_align<RPL, true, KIND>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((k_align<RPL, false, KIND>), grid, dim3(256), 0, st, p);
 }
 
-template <int RPL>
-void launch_pairs(const KParams &p, bool affine, hipStream_t st) {
-    dim3 grid((unsigned)((p.n_waves + 3) / 4));
-    if (affine) hipLaunchKernelGGL((k_align_pairs<RPL, true>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((k_align_pairs<RPL, false>), grid, dim3(256), 0, st, p);
-}
-
-void dispatch_cross(int b, const KParams &p, bool affine, int64_t n_win, hipStream_t st) {
-    switch (kBuckets[b]) {
-    case 8: launch_cross<8>(p, affine, n_win, st); break;
-    case 16: launch_cross<16>(p, affine, n_win, st); break;
-    case 24: launch_cross<24>(p, affine, n_win, st); break;
-    case 32: launch_cross<32>(p, affine, n_win, st); break;
-    case 48: launch_cross<48>(p, affine, n_win, st); break;
-    case 64: launch_cross<64>(p, affine, n_win, st); break;
-    case 96: launch_cross<96>(p, affine, n_win, st); break;
-    case 128: launch_cross<128>(p, affine, n_win, st); break;
-    }
-}
-
-void dispatch_pairs(int b, const KParams &p, bool affine, hipStream_t st) {
-    switch (kBuckets[b]) {
-    case 8: launch_pairs<8>(p, affine, st); break;
-    case 16: launch_pairs<16>(p, affine, st); break;
-    case 24: launch_pairs<24>(p, affine, st); break;
-    case 32: launch_pairs<32>(p, affine, st); break;
-    case 48: launch_pairs<48>(p, affine, st); break;
-    case 64: launch_pairs<64>(p, affine, st); break;
-    case 96: launch_pairs<96>(p, affine, st); break;
-    case 128: launch_pairs<128>(p, affine, st); break;
+void dispatch(int b, const KParams &p, bool affine, hipStream_t st) {
+    dim3 grid = p.task_win ? dim3((unsigned)((p.n_waves + 3) / 4))
+                           : dim3((unsigned)((p.n_win + 255) / 256), (unsigned)p.n_adp);
+    const BucketDef d = kBuckets[b];
+    if (d.kind == FAST) {
+        switch (d.rpl) {
+#define C(R) case R: launch<R, FAST>(p, affine, grid, st); break;
+        C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32) C(36) C(40) C(44) C(48) C(52) C(56) C(60) C(64)
+#undef C
+        }
+    } else {
+        switch (d.rpl) {
+        case 16: launch<16, GENERIC>(p, affine, grid, st); break;
+        case 32: launch<32, GENERIC>(p, affine, grid, st); break;
+        case 64: launch<64, GENERIC>(p, affine, grid, st); break;
+        case 96: launch<96, GENERIC>(p, affine, grid, st); break;
+        case 128: launch<128, GENERIC>(p, affine, grid, st); break;
+        }
     }
 }
 
@@ -276,14 +277,14 @@ struct BucketHost {
 };
 
 void build_buckets(const uint8_t *adp_codes, const int32_t *adp_off, const int32_t *adp_len,
-                   int32_t n_adp, BucketHost (&bk)[kNumBuckets]) {
+                   int32_t n_adp, const pcabi::Scoring &sc, BucketHost (&bk)[kNumBuckets]) {
     for (int a = 0; a < n_adp; ++a) {
         const int L = adp_len[a];
-        const int b = bucket_of(L);
-        const int R = kBuckets[b];
+        const int b = bucket_of(L, sc);
+        const int R = kBuckets[b].rpl;
         BucketHost &h = bk[b];
         const size_t base = h.pad.size();
-        h.pad.resize(base + R, 0xFF);
+        h.pad.resize(base + R, (uint8_t)pcabi::PAD_CODE);
         const int off = R - L;
         for (int k = 0; k < L; ++k) h.pad[base + off + k] = adp_codes[adp_off[a] + k];
         h.len.push_back(L);
@@ -296,6 +297,7 @@ void build_buckets(const uint8_t *adp_codes, const int32_t *adp_off, const int32
 // ---- prepared adapter tables (device) ---------------------------------------------------------
 struct pcabi_adapters {
     int32_t n_adp = 0;
+    bool padded[kNumBuckets] = {};
     int32_t count[kNumBuckets] = {};
     uint32_t *pad[kNumBuckets] = {};
     int32_t *len[kNumBuckets] = {};
@@ -410,8 +412,9 @@ int pcabi_align_host(int device, const uint8_t *codes, int64_t codes_len, const 
     if (int rc = engine_init(e, device)) return rc;
     HIP_TRY(hipSetDevice(device));
 
+    const pcabi::Scoring sc{match, mismatch, gap_open, gap_extend};
     BucketHost bk[kNumBuckets];
-    build_buckets(adp_codes, adp_off, adp_len, n_adp, bk);
+    build_buckets(adp_codes, adp_off, adp_len, n_adp, sc, bk);
 
     if (int rc = e.codes.ensure((size_t)codes_len)) return rc;
     if (int rc = e.woff.ensure(sizeof(int64_t) * (size_t)std::max<int64_t>(n_win, 1))) return rc;
@@ -428,7 +431,7 @@ int pcabi_align_host(int device, const uint8_t *codes, int64_t codes_len, const 
     p.n_win = n_win;
     p.out = (int32_t *)e.out.p;
     p.out_stride = n_res;
-    p.sc = pcabi::Scoring{match, mismatch, gap_open, gap_extend};
+    p.sc = sc;
     const bool affine = gap_open != gap_extend;
 
     // host-side pair grouping (pairs mode): per bucket, per adapter, runs padded to 64 lanes
@@ -453,7 +456,8 @@ int pcabi_align_host(int device, const uint8_t *codes, int64_t codes_len, const 
         p.adp_id = (const int32_t *)e.id[b].p;
         p.n_adp = nb;
         if (!task_win) {
-            if (n_win > 0) dispatch_cross(b, p, affine, n_win, e.stream);
+            p.task_win = nullptr;
+            if (n_win > 0) dispatch(b, p, affine, e.stream);
         } else {
             tw.clear(); to.clear(); wa.clear();
             for (int k = 0; k < nb; ++k) {
@@ -478,7 +482,7 @@ int pcabi_align_host(int device, const uint8_t *codes, int64_t codes_len, const 
             p.task_out = (const int32_t *)e.tasks_out.p;
             p.wave_adp = (const int32_t *)e.wave_adp.p;
             p.n_waves = (int64_t)wa.size();
-            dispatch_pairs(b, p, affine, e.stream);
+            dispatch(b, p, affine, e.stream);
             // host vectors are reused by the next bucket: drain before overwriting
             HIP_TRY(hipStreamSynchronize(e.stream));
         }
@@ -573,14 +577,18 @@ int pcabi_event_elapsed_ms(float *ms, void *start, void *stop) {
 int pcabi_adapters_create(const uint8_t *adp_codes, const int32_t *adp_off, const int32_t *adp_len,
                           int32_t n_adp, pcabi_adapters **out) {
     if (int rc = check_common(adp_len, n_adp)) return rc;
+    // Tables are laid out for the fast buckets (any scoring with negative gap costs);
+    // pcabi_align_cross_dev rejects scorings the layout cannot serve.
     BucketHost bk[kNumBuckets];
-    build_buckets(adp_codes, adp_off, adp_len, n_adp, bk);
+    build_buckets(adp_codes, adp_off, adp_len, n_adp, pcabi::Scoring{1, -1, -1, -1}, bk);
     pcabi_adapters *a = new pcabi_adapters();
     a->n_adp = n_adp;
     for (int b = 0; b < kNumBuckets; ++b) {
         const int nb = (int)bk[b].len.size();
         a->count[b] = nb;
         if (!nb) continue;
+        for (int k = 0; k < nb; ++k)
+            if (bk[b].len[k] != kBuckets[b].rpl) a->padded[b] = true;
         if (hipMalloc((void **)&a->pad[b], bk[b].pad.size()) != hipSuccess ||
             hipMalloc((void **)&a->len[b], sizeof(int32_t) * nb) != hipSuccess ||
             hipMalloc((void **)&a->id[b], sizeof(int32_t) * nb) != hipSuccess) {
@@ -621,11 +629,15 @@ int pcabi_align_cross_dev(const uint8_t *codes, const int64_t *win_off, const in
     const bool affine = gap_open != gap_extend;
     for (int b = 0; b < kNumBuckets; ++b) {
         if (!adps->count[b]) continue;
+        if (kBuckets[b].kind == FAST && adps->padded[b] &&
+            !pcabi::fast_ok(kBuckets[b].rpl - 1, kBuckets[b].rpl, p.sc))
+            return fail(PCABI_E_ARG, "scoring with non-negative gap costs: use pcabi_align_host "
+                                     "(generic kernels) for this adapter table");
         p.adp_pad = adps->pad[b];
         p.adp_len = adps->len[b];
         p.adp_id = adps->id[b];
         p.n_adp = adps->count[b];
-        dispatch_cross(b, p, affine, n_win, (hipStream_t)stream);
+        dispatch(b, p, affine, (hipStream_t)stream);
     }
     HIP_TRY(hipGetLastError());
     return 0;

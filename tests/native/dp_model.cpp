@@ -14,8 +14,8 @@ static void run(const char *read, int n, const char *adp, int L, pcabi::Scoring 
     const int off = RPL - L;
     auto rd = [&](int j) { return dna5((unsigned char)read[j - 1]); };
     auto ad = [&](int s) { return dna5((unsigned char)adp[s - off - 1]); };
-    pcabi::Result r = (sc.go != sc.ge) ? pcabi::align_lane<RPL, true>(rd, n, ad, L, sc)
-                                       : pcabi::align_lane<RPL, false>(rd, n, ad, L, sc);
+    pcabi::Result r = (sc.go != sc.ge) ? pcabi::align_lane_generic<RPL, true>(rd, n, ad, L, sc)
+                                       : pcabi::align_lane_generic<RPL, false>(rd, n, ad, L, sc);
     out[0] = r.rs; out[1] = r.re; out[2] = r.as; out[3] = r.ae;
     out[4] = r.score; out[5] = r.m; out[6] = r.l1; out[7] = r.l2;
 }
@@ -34,3 +34,31 @@ extern "C" int pcabi_model_align(const char *read, int n, const char *adp, int L
 }
 
 extern "C" double pcabi_model_pid6(int m, int l) { return pcabi::pid6(m, l); }
+
+template <int RPL>
+static void run_fast(const char *read, int n, const char *adp, int L, pcabi::Scoring sc, int *out) {
+    const int off = RPL - L;
+    auto rd = [&](int j) { return dna5((unsigned char)read[j - 1]); };
+    auto ad = [&](int s) { return s <= off ? pcabi::PAD_CODE : dna5((unsigned char)adp[s - off - 1]); };
+    pcabi::Result r = (sc.go != sc.ge) ? pcabi::align_lane_fast<RPL, true>(rd, n, ad, L, sc)
+                                       : pcabi::align_lane_fast<RPL, false>(rd, n, ad, L, sc);
+    out[0] = r.rs; out[1] = r.re; out[2] = r.as; out[3] = r.ae;
+    out[4] = r.score; out[5] = r.m; out[6] = r.l1; out[7] = r.l2;
+}
+
+// fast core (bucket = L rounded up to a multiple of 4); returns -3 if the preconditions fail
+extern "C" int pcabi_model_align_fast(const char *read, int n, const char *adp, int L,
+                                      int ma, int mi, int go, int ge, int *out) {
+    pcabi::Scoring sc{ma, mi, go, ge};
+    if (L <= 0 || n <= 0) return -1;
+    const int rpl = (L + 3) & ~3;
+    if (!pcabi::fast_ok(L, rpl, sc)) return -3;
+    switch (rpl) {
+#define C(R) case R: run_fast<R>(read, n, adp, L, sc, out); break;
+    C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32) C(36) C(40) C(44) C(48) C(52) C(56) C(60) C(64)
+    C(68) C(72) C(76) C(80) C(84) C(88) C(92) C(96) C(100) C(104) C(108) C(112) C(116) C(120) C(124) C(128)
+#undef C
+    default: return -2;
+    }
+    return 0;
+}
