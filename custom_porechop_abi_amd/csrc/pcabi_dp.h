@@ -43,19 +43,35 @@ namespace pcabi {
 // wins and never ties (|scores| <= 2^20 for all supported sizes).
 constexpr int NEG = -(1 << 28);
 
-// Attribute word: [ c + CBIAS : 16 ][ m : 8 ][ nD : 8 ]
+// Attribute word: [ (c + CBIAS) mod 2^16 : 16 ][ m : 8 ][ nD : 8 ]
 //   c  = j0 - i0  (path start cell; at least one of i0, j0 is zero)
 //   m  = matching diagonal columns on the path, nD = diagonal columns on the path
+// The c field WRAPS (uint32 arithmetic, top field): every live path spans fewer than
+// span_bound() < 2^15 columns (gap costs < 0 bound its horizontal moves), so c is recovered
+// exactly from the end column in finish(). Reads of any length are therefore supported.
 constexpr int ATTR_B = 8;
 constexpr uint32_t ATTR_MASK = (1u << ATTR_B) - 1u;
 constexpr int ATTR_CSH = 2 * ATTR_B;
 constexpr int ATTR_CBIAS = 255;            // c >= -L >= -255
 constexpr int MAX_ADAPTER_LEN = 255;       // m, nD <= L fit 8 bits
-constexpr int MAX_WINDOW_LEN = 65535 - ATTR_CBIAS;
+constexpr int MAX_WINDOW_LEN = 1 << 30;
 constexpr uint32_t INC_D = 1u;                           // mismatching diagonal
 constexpr uint32_t INC_M = (1u << ATTR_B) + 1u;          // matching diagonal
 
 PCABI_HD uint32_t attr_start(int c) { return (uint32_t)(c + ATTR_CBIAS) << ATTR_CSH; }
+
+// Upper bound on the columns spanned by any path the DP keeps (S-, H- or V-state). A path
+// ending at row i scores >= i*mi (the all-diagonal path is always available) and <= i*ma minus
+// the cost of its horizontal moves, each costing >= g = min(|go|, |ge|); a trailing H run is
+// bounded the same way. Returns -1 if gap costs are not both negative (no bound).
+PCABI_HD int span_bound(int L, int ma, int mi, int go, int ge) {
+    if (go >= 0 || ge >= 0) return -1;
+    const int g = (-go < -ge) ? -go : -ge;
+    const int d = (ma > mi ? ma - mi : 0) + 1;
+    const long long t = ((long long)L * d + g - 1) / g + 2;
+    const long long b = (long long)L + 2 * t + 4;
+    return b > (1 << 30) ? (1 << 30) : (int)b;
+}
 
 // last-column types of a path
 enum : int { LT_NONE = 0, LT_D = 1, LT_V = 2, LT_H = 3 };
@@ -83,7 +99,9 @@ struct Result {
 // Derivation in DESIGN.md §3. bi/bj: end cell, L/n: sequence lengths.
 PCABI_HD Result finish(const Best &b, int L, int n) {
     Result r;
-    const int c = (int)(b.attr >> ATTR_CSH) - ATTR_CBIAS;
+    // c lies in [bj - span, bj] with span < 2^15: undo the mod-2^16 wrap
+    const int u = (int)(b.attr >> ATTR_CSH) - ATTR_CBIAS;
+    const int c = b.bj - ((b.bj - u) & 0xFFFF);
     const int m = (int)((b.attr >> ATTR_B) & ATTR_MASK);
     const int nd = (int)(b.attr & ATTR_MASK);
     const int i0 = c < 0 ? -c : 0;

@@ -353,6 +353,15 @@ int check_common(const int32_t *adp_len, int32_t n_adp) {
     return 0;
 }
 
+// The wrapped start-column field needs a bounded path span unless every window is short.
+int check_span(const pcabi::Scoring &sc, int max_L, int64_t max_win) {
+    if (max_win < 32768 - 256) return 0;
+    const int b = pcabi::span_bound(max_L, sc.ma, sc.mi, sc.go, sc.ge);
+    if (b < 0 || b + max_L >= 32768)
+        return fail(PCABI_E_ARG, "windows longer than 32k need negative gap costs with a bounded path span");
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -413,6 +422,13 @@ int pcabi_align_host(int device, const uint8_t *codes, int64_t codes_len, const 
     HIP_TRY(hipSetDevice(device));
 
     const pcabi::Scoring sc{match, mismatch, gap_open, gap_extend};
+    {
+        int max_L = 0;
+        int64_t max_w = 0;
+        for (int a = 0; a < n_adp; ++a) max_L = std::max(max_L, (int)adp_len[a]);
+        for (int64_t w = 0; w < n_win; ++w) max_w = std::max<int64_t>(max_w, win_len[w]);
+        if (int rc = check_span(sc, max_L, max_w)) return rc;
+    }
     BucketHost bk[kNumBuckets];
     build_buckets(adp_codes, adp_off, adp_len, n_adp, sc, bk);
 
@@ -439,6 +455,11 @@ int pcabi_align_host(int device, const uint8_t *codes, int64_t codes_len, const 
     if (task_win) {
         per_adp.resize(n_adp);
         for (int64_t t = 0; t < n_task; ++t) per_adp[task_adp[t]].push_back((int32_t)t);
+        // longest windows first: lanes of a wave then run near-equal column counts
+        for (auto &v : per_adp)
+            std::stable_sort(v.begin(), v.end(), [&](int32_t x, int32_t y) {
+                return win_len[task_win[x]] > win_len[task_win[y]];
+            });
     }
     std::vector<int32_t> tw, to, wa;
     for (int b = 0; b < kNumBuckets; ++b) {

@@ -1,0 +1,189 @@
+"""Per-read adapter logic (mirror of porechop_abi/nanopore_read.py for the hot path).
+
+Same class name, attribute names and method signatures as the reference, so the phase drivers
+and the reference's own per-read call pattern work unchanged:
+  * NanoporeRead.align_adapter_set   -- porechop_abi/nanopore_read.py:158-173
+  * NanoporeRead.find_start_trim     -- :175-195
+  * NanoporeRead.find_end_trim       -- :197-217
+  * NanoporeRead.find_middle_adapters-- :219-252
+  * NanoporeRead.determine_barcode   -- :408-482
+  * align_adapter()                  -- :485-500
+Every alignment runs on the GPU through cpp_function_wrappers.adapter_alignment (one pair per
+call). The batched drivers in porechop_abi.py do the same work in bulk and then apply the SAME
+decision rules through the _apply_* helpers below, so both paths share one implementation of
+the trimming logic.
+
+Output formatting (colourised windows, FASTA/FASTQ writers) is outside the hot path and is not
+mirrored here.
+"""
+from .cpp_function_wrappers import adapter_alignment
+
+
+class NanoporeRead(object):
+
+    def __init__(self, name, seq, quals):
+        self.name = name
+        seq_u = seq.upper()
+        self.rna = seq_u.count('U') > seq_u.count('T')
+        self.seq = seq_u.replace('U', 'T') if self.rna else seq_u
+        self.quals = quals if len(quals) >= len(seq) else quals + '+' * (len(seq) - len(quals))
+
+        self.start_trim_amount = 0
+        self.end_trim_amount = 0
+        self.start_adapter_alignments = []
+        self.end_adapter_alignments = []
+
+        self.middle_adapter_positions = set()
+        self.middle_trim_positions = set()
+        self.middle_hit_str = ''
+
+        self.start_barcode_scores = {}
+        self.end_barcode_scores = {}
+        self.best_start_barcode = ('none', 0.0)
+        self.best_end_barcode = ('none', 0.0)
+        self.second_best_start_barcode = ('none', 0.0)
+        self.second_best_end_barcode = ('none', 0.0)
+        self.barcode_call = 'none'
+        self.albacore_barcode_call = None
+
+    # --- sequence views -------------------------------------------------------------------
+    def adapters_found(self):
+        """Fork filter (porechop_abi/nanopore_read.py:22-30): start AND end alignments found."""
+        return bool(self.start_adapter_alignments) and bool(self.end_adapter_alignments)
+
+    def get_seq_with_start_end_adapters_trimmed(self):
+        if not self.start_trim_amount and not self.end_trim_amount:
+            return self.seq
+        return self.seq[self.start_trim_amount:len(self.seq) - self.end_trim_amount]
+
+    def seq_length_with_start_end_adapters_trimmed(self):
+        return len(self.get_seq_with_start_end_adapters_trimmed())
+
+    # --- hot path, one alignment per call --------------------------------------------------
+    def align_adapter_set(self, adapter_set, end_size, scoring_scheme_vals):
+        """Adapter-set discovery: raise the set's best start/end full-adapter identity."""
+        if adapter_set.start_sequence:
+            full = align_adapter(self.seq[:end_size], adapter_set.start_sequence[1], scoring_scheme_vals)[0]
+            adapter_set.best_start_score = max(adapter_set.best_start_score, full)
+        if adapter_set.end_sequence:
+            full = align_adapter(self.seq[-end_size:], adapter_set.end_sequence[1], scoring_scheme_vals)[0]
+            adapter_set.best_end_score = max(adapter_set.best_end_score, full)
+
+    def find_start_trim(self, adapters, end_size, extra_trim_size, end_threshold,
+                        scoring_scheme_vals, min_trim_size, check_barcodes, forward_or_reverse):
+        window = self.seq[:end_size]
+        for adapter in adapters:
+            if not adapter.start_sequence:
+                continue
+            hit = align_adapter(window, adapter.start_sequence[1], scoring_scheme_vals)
+            self._apply_start_hit(adapter, hit, end_size, extra_trim_size, end_threshold,
+                                  min_trim_size, check_barcodes, forward_or_reverse)
+
+    def find_end_trim(self, adapters, end_size, extra_trim_size, end_threshold,
+                      scoring_scheme_vals, min_trim_size, check_barcodes, forward_or_reverse):
+        window = self.seq[-end_size:]
+        for adapter in adapters:
+            if not adapter.end_sequence:
+                continue
+            hit = align_adapter(window, adapter.end_sequence[1], scoring_scheme_vals)
+            self._apply_end_hit(adapter, hit, end_size, extra_trim_size, end_threshold,
+                                min_trim_size, check_barcodes, forward_or_reverse)
+
+    def find_middle_adapters(self, adapters, middle_threshold, extra_middle_trim_good_side,
+                             extra_middle_trim_bad_side, scoring_scheme_vals,
+                             start_sequence_names, end_sequence_names):
+        """Whole-read scan, re-aligning the same adapter after masking each strong hit."""
+        masked = self.get_seq_with_start_end_adapters_trimmed()
+        for adapter_name, adapter_seq in adapters:
+            while True:
+                full, _, read_start, read_end = align_adapter(masked, adapter_seq, scoring_scheme_vals)
+                if full < middle_threshold:
+                    break
+                masked = masked[:read_start] + '-' * (read_end - read_start) + masked[read_end:]
+                self._apply_middle_hit(adapter_name, full, read_start, read_end,
+                                       extra_middle_trim_good_side, extra_middle_trim_bad_side,
+                                       start_sequence_names, end_sequence_names)
+
+    # --- decision rules shared with the batched drivers -------------------------------------
+    def _apply_start_hit(self, adapter, hit, end_size, extra_trim_size, end_threshold, min_trim_size,
+                         check_barcodes, forward_or_reverse):
+        full, partial, read_start, read_end = hit
+        if partial > end_threshold and read_end != end_size and read_end - read_start >= min_trim_size:
+            self.start_trim_amount = max(self.start_trim_amount, read_end + extra_trim_size)
+            self.start_adapter_alignments.append((adapter, full, partial, read_start, read_end))
+        if check_barcodes and adapter.is_barcode() and adapter.barcode_direction() == forward_or_reverse:
+            self.start_barcode_scores[adapter.get_barcode_name()] = full
+
+    def _apply_end_hit(self, adapter, hit, end_size, extra_trim_size, end_threshold, min_trim_size,
+                       check_barcodes, forward_or_reverse):
+        full, partial, read_start, read_end = hit
+        if partial > end_threshold and read_start != 0 and read_end - read_start >= min_trim_size:
+            self.end_trim_amount = max(self.end_trim_amount, (end_size - read_start) + extra_trim_size)
+            self.end_adapter_alignments.append((adapter, full, partial, read_start, read_end))
+        if check_barcodes and adapter.is_barcode() and adapter.barcode_direction() == forward_or_reverse:
+            self.end_barcode_scores[adapter.get_barcode_name()] = full
+
+    def _apply_middle_hit(self, adapter_name, full, read_start, read_end, good_side, bad_side,
+                          start_sequence_names, end_sequence_names):
+        self.middle_adapter_positions.update(range(read_start, read_end))
+        self.middle_hit_str += '  %s (read coords: %d-%d, identity: %.1f%%)\n' % (
+            adapter_name, read_start, read_end, full)
+        trim_start = read_start - (bad_side if adapter_name in start_sequence_names else good_side)
+        trim_end = read_end + (bad_side if adapter_name in end_sequence_names else good_side)
+        self.middle_trim_positions.update(range(trim_start, trim_end))
+
+    def determine_barcode(self, barcode_threshold, barcode_diff, require_two_barcodes):
+        """Barcode call from the start/end full-adapter identities (stable sorts: ties keep
+        insertion order, i.e. adapter order, exactly like the reference)."""
+        starts = sorted(self.start_barcode_scores.items(), reverse=True, key=lambda x: x[1])
+        ends = sorted(self.end_barcode_scores.items(), reverse=True, key=lambda x: x[1])
+        if starts:
+            self.best_start_barcode = starts[0]
+        if len(starts) > 1:
+            self.second_best_start_barcode = starts[1]
+        if ends:
+            self.best_end_barcode = ends[0]
+        if len(ends) > 1:
+            self.second_best_end_barcode = ends[1]
+
+        call = 'none'
+        if require_two_barcodes:
+            bs, be = self.best_start_barcode, self.best_end_barcode
+            if (bs[1] >= barcode_threshold and be[1] >= barcode_threshold and
+                    bs[1] >= self.second_best_start_barcode[1] + barcode_diff and
+                    be[1] >= self.second_best_end_barcode[1] + barcode_diff and bs[0] == be[0]):
+                call = bs[0]
+        else:
+            merged, seen = [], set()
+            for name, score in sorted(starts + ends, reverse=True, key=lambda x: x[1]):
+                if name not in seen:
+                    merged.append((name, score))
+                    seen.add(name)
+            best = merged[0] if merged else ('none', 0.0)
+            second = merged[1] if len(merged) > 1 else ('none', 0.0)
+            if best[1] >= barcode_threshold and best[1] >= second[1] + barcode_diff:
+                call = best[0]
+        self.barcode_call = call
+        if self.albacore_barcode_call is not None and self.barcode_call != self.albacore_barcode_call:
+            self.barcode_call = 'none'
+
+
+def parse_alignment_result(result_string):
+    """The reference's parse of "rs,re,as,ae,score,pid1,pid2" (nanopore_read.py:485-500)."""
+    parts = result_string.split(',')
+    read_start = int(parts[0])
+    if read_start == -1:
+        return 0.0, 0.0, -1, 0
+    return float(parts[6]), float(parts[5]), read_start, int(parts[1]) + 1
+
+
+def align_adapter(read_seq, adapter_seq, scoring_scheme_vals):
+    """(full_adapter_identity, aligned_region_identity, read_start, read_end_exclusive)."""
+    return parse_alignment_result(adapter_alignment(read_seq, adapter_seq, scoring_scheme_vals))
+
+
+def add_number_to_read_name(read_name, number):
+    for sep in ('\t', ' '):
+        if sep in read_name:
+            return read_name.replace(sep, '_%d%s' % (number, sep), 1)
+    return '%s_%d' % (read_name, number)

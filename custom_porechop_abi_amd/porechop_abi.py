@@ -1,0 +1,326 @@
+"""Batched phase drivers (mirror of the hot-path drivers in porechop_abi/porechop_abi.py).
+
+The reference fans every read (or read x adapter-set pair) out over a ThreadPool that calls
+the per-pair C++ aligner once per alignment (porechop_abi.py:200-245, 359-438, 457-522). Here
+each phase packs its windows once, runs ALL alignments of the phase as one GPU batch
+(engine.align -> libpcabi k_align), and then applies the reference's per-read decision rules
+(NanoporeRead._apply_* -- the same code the per-read methods use) in the reference's order.
+Signatures are unchanged; `threads` is accepted and ignored (the GPU is the parallelism).
+
+Middle-adapter scan (porechop_abi.py:457-522 / nanopore_read.py:219-252): the reference masks
+every strong hit with '-' and re-aligns the SAME adapter, and the mask carries over to the
+following adapters. The batched scan reproduces that order exactly in rounds: round 1 aligns
+every read against every adapter on the unmasked read; for each read the first adapter (in
+list order) with a hit is final for all adapters before it; the hit is masked and the read
+re-enters the next round from that adapter on. Rounds repeat until no read has a hit.
+"""
+import sys
+
+import numpy as np
+
+from . import adapters as _adapters
+from .adapters import make_full_native_barcode_adapter, make_new_full_rapid_barcode_adapter, \
+    make_old_full_rapid_barcode_adapter
+from . import engine
+from .engine import SeqPack, identities, start_end_windows
+
+END_FORMATTING = '\033[0m'
+BOLD = '\033[1m'
+UNDERLINE = '\033[4m'
+
+
+def int_to_str(num, max_num=0):
+    s = 'n/a' if num is None else '{:,}'.format(num)
+    return s.rjust(len('{:,}'.format(int(max_num))))
+
+
+def bold_underline(text):
+    return BOLD + UNDERLINE + text + END_FORMATTING
+
+
+def output_progress_line(completed, total, print_dest, end_newline=False, step=10):
+    if step > 1 and completed % step != 0 and completed != total:
+        return
+    pct = 100.0 * completed / total if total > 0 else 0.0
+    line = '\r%s / %s (%.1f%%)' % (int_to_str(completed), int_to_str(total), pct)
+    print(line, end='\n' if end_newline else '', flush=True, file=print_dest)
+
+
+def _unique(seqs):
+    """Deduplicate adapter sequences: (unique list, index of each input in it)."""
+    pos, uniq, idx = {}, [], []
+    for s in seqs:
+        if s not in pos:
+            pos[s] = len(uniq)
+            uniq.append(s)
+        idx.append(pos[s])
+    return uniq, np.array(idx, dtype=np.int64)
+
+
+def _window_hits(windows, seqs, scoring_scheme_vals):
+    """Cross product windows x seqs on the GPU -> (full, partial, rs, re_excl), each (n_seq, n_win)."""
+    n_win = len(windows[2])
+    uniq, idx = _unique(seqs)
+    if not uniq or n_win == 0:
+        z = np.zeros((len(seqs), n_win))
+        return z, z.copy(), z.astype(np.int64), z.astype(np.int64)
+    res = engine.align(windows, uniq, scoring_scheme_vals)
+    full, part, rs, re_ = (x.reshape(len(uniq), n_win)[idx] for x in identities(res))
+    return full, part, rs, re_
+
+
+# ---------------------------------------------------------------------------------------------
+def find_matching_adapter_sets(check_reads, verbosity, end_size, scoring_scheme_vals, print_dest,
+                               adapter_threshold, threads, adapter_sets=None):
+    """Adapter-set discovery over the check reads (porechop_abi.py:200-245): every non-"full
+    sequence" set's start/end sequence against every check read's start/end window; keeps the
+    sets whose best start-or-end full-adapter identity reaches adapter_threshold."""
+    if adapter_sets is None:
+        adapter_sets = _adapters.ADAPTERS
+    read_count = len(check_reads)
+    if verbosity > 0:
+        print(bold_underline('Looking for known adapter sets'), flush=True, file=print_dest)
+        output_progress_line(0, read_count, print_dest)
+    search = [a for a in adapter_sets if '(full sequence)' not in a.name]
+    if check_reads:
+        pack = SeqPack([r.seq for r in check_reads])
+        sw, ew = start_end_windows(pack, end_size)
+        starts = [a for a in search if a.start_sequence]
+        ends = [a for a in search if a.end_sequence]
+        sfull = _window_hits(sw, [a.start_sequence[1] for a in starts], scoring_scheme_vals)[0]
+        efull = _window_hits(ew, [a.end_sequence[1] for a in ends], scoring_scheme_vals)[0]
+        for a, row in zip(starts, sfull):
+            a.best_start_score = max(a.best_start_score, float(row.max()))
+        for a, row in zip(ends, efull):
+            a.best_end_score = max(a.best_end_score, float(row.max()))
+    if verbosity > 0:
+        output_progress_line(read_count, read_count, print_dest, end_newline=True)
+    return [a for a in search if a.best_start_or_end_score() >= adapter_threshold]
+
+
+def fix_up_1d2_sets(matching_sets):
+    """porechop_abi.py:283-304. Note the reference compares against 'SQK-MAP006 Short' while
+    the database names the set 'SQK-MAP006 short', so this never fires there; kept verbatim."""
+    names = [x.name for x in matching_sets]
+    if '1D^2 part 1' in names and '1D^2 part 2' in names and 'SQK-MAP006 Short' in names:
+        score = {x.name: x.best_start_or_end_score() for x in matching_sets}
+        if score['1D^2 part 1'] >= score['SQK-MAP006 Short'] and \
+                score['1D^2 part 2'] >= score['SQK-MAP006 Short']:
+            matching_sets = [x for x in matching_sets if x.name != 'SQK-MAP006 Short']
+    return matching_sets
+
+
+def choose_barcoding_kit(adapter_sets, verbosity, print_dest):
+    """porechop_abi.py:248-280: pick forward or reverse barcodes from the discovery scores
+    (best start-or-end first, then start+end sums). Exits like the reference when undecidable."""
+    fwd_or = rev_or = fwd_and = rev_and = 0
+    for s in adapter_sets:
+        low = s.name.lower()
+        if 'barcode' not in low:
+            continue
+        if '(forward)' in low:
+            fwd_or += s.best_start_or_end_score()
+            fwd_and += s.best_start_score + s.best_end_score
+        elif '(reverse)' in low:
+            rev_or += s.best_start_or_end_score()
+            rev_and += s.best_start_score + s.best_end_score
+    if fwd_or == 0 and rev_or == 0:
+        sys.exit('Error: no barcodes were found, so Porechop cannot perform barcode demultiplexing')
+    if fwd_or != rev_or:
+        orientation = 'forward' if fwd_or > rev_or else 'reverse'
+    elif fwd_and != rev_and:
+        orientation = 'forward' if fwd_and > rev_and else 'reverse'
+    else:
+        sys.exit('Error: Porechop could not determine barcode orientation')
+    if verbosity > 0:
+        print('\nBarcodes determined to be in ' + orientation + ' orientation', file=print_dest)
+    return orientation
+
+
+def add_full_barcode_adapter_sets(matching_sets):
+    """porechop_abi.py:324-348: add full native / rapid barcode adapters for found barcodes."""
+    names = [x.name for x in matching_sets]
+    for i in range(1, 97):
+        if 'SQK-NSK007' in names and 'Barcode %d (reverse)' % i in names:
+            matching_sets.append(make_full_native_barcode_adapter(i))
+        if 'Rapid' in names and 'Barcode %d (forward)' % i in names:
+            if 'RBK004_upstream' in names:
+                matching_sets.append(make_new_full_rapid_barcode_adapter(i))
+            elif 'SQK-NSK007' in names:
+                matching_sets.append(make_old_full_rapid_barcode_adapter(i))
+    return matching_sets
+
+
+# ---------------------------------------------------------------------------------------------
+def find_adapters_at_read_ends(reads, matching_sets, verbosity, end_size, extra_trim_size,
+                               end_threshold, scoring_scheme_vals, print_dest, min_trim_size,
+                               threads, check_barcodes, barcode_threshold, barcode_diff,
+                               require_two_barcodes, forward_or_reverse_barcodes):
+    """End trimming (porechop_abi.py:359-438): start window x start sequences and end window x
+    end sequences of the matching sets for every read, then the per-read decisions of
+    find_start_trim / find_end_trim / determine_barcode."""
+    if verbosity > 0:
+        print(bold_underline('Trimming adapters from read ends'), file=print_dest)
+        name_len = max(max(len(x.start_sequence[0]) if x.start_sequence else 0 for x in matching_sets),
+                       max(len(x.end_sequence[0]) if x.end_sequence else 0 for x in matching_sets))
+        for s in matching_sets:
+            for seq in (s.start_sequence, s.end_sequence):
+                if seq:
+                    print('  ' + seq[0].rjust(name_len) + ': ' + '\033[31m' + seq[1] + END_FORMATTING,
+                          file=print_dest)
+        print('', file=print_dest)
+    read_count = len(reads)
+    if verbosity == 1:
+        output_progress_line(0, read_count, print_dest)
+    if reads:
+        pack = SeqPack([r.seq for r in reads])
+        sw, ew = start_end_windows(pack, end_size)
+        starts = [a for a in matching_sets if a.start_sequence]
+        ends = [a for a in matching_sets if a.end_sequence]
+        s_hits = _window_hits(sw, [a.start_sequence[1] for a in starts], scoring_scheme_vals)
+        e_hits = _window_hits(ew, [a.end_sequence[1] for a in ends], scoring_scheme_vals)
+        _apply_end_decisions(reads, starts, s_hits, ends, e_hits, end_size, extra_trim_size, end_threshold,
+                             min_trim_size, check_barcodes, forward_or_reverse_barcodes)
+        if check_barcodes:
+            for r in reads:
+                r.determine_barcode(barcode_threshold, barcode_diff, require_two_barcodes)
+    if verbosity == 1:
+        output_progress_line(read_count, read_count, print_dest, end_newline=True)
+    if verbosity > 0:
+        print('', file=print_dest)
+
+
+def _apply_end_decisions(reads, starts, s_hits, ends, e_hits, end_size, extra, thr, min_trim,
+                         check_barcodes, fwd_rev):
+    """Vectorised trim amounts + the reference's per-read alignment lists, in adapter order."""
+    for side, sets, hits in (('start', starts, s_hits), ('end', ends, e_hits)):
+        full, part, rs, re_ = hits
+        if not sets:
+            continue
+        if side == 'start':
+            ok = (part > thr) & (re_ != end_size) & (re_ - rs >= min_trim)
+            amount = np.where(ok, re_ + extra, 0)
+        else:
+            ok = (part > thr) & (rs != 0) & (re_ - rs >= min_trim)
+            amount = np.where(ok, (end_size - rs) + extra, 0)
+        best = amount.max(axis=0)
+        hit_reads, hit_adps = np.nonzero(ok.T)          # read-major, adapter order within a read
+        bc = [k for k, a in enumerate(sets)
+              if check_barcodes and a.is_barcode() and a.barcode_direction() == fwd_rev]
+        bc_names = [sets[k].get_barcode_name() for k in bc]
+        for i, r in enumerate(reads):
+            if side == 'start':
+                r.start_trim_amount = max(r.start_trim_amount, int(best[i]))
+            else:
+                r.end_trim_amount = max(r.end_trim_amount, int(best[i]))
+        lst_attr = 'start_adapter_alignments' if side == 'start' else 'end_adapter_alignments'
+        for i, k in zip(hit_reads.tolist(), hit_adps.tolist()):
+            getattr(reads[i], lst_attr).append((sets[k], float(full[k, i]), float(part[k, i]),
+                                                int(rs[k, i]), int(re_[k, i])))
+        if bc:
+            fb = full[bc]
+            for i, r in enumerate(reads):
+                d = r.start_barcode_scores if side == 'start' else r.end_barcode_scores
+                for name, v in zip(bc_names, fb[:, i].tolist()):
+                    d[name] = v
+
+
+# ---------------------------------------------------------------------------------------------
+def middle_adapter_list(matching_sets):
+    """porechop_abi.py:465-479: start sequences, plus end sequences that differ from their
+    set's start sequence; and the start / end sequence-name sets."""
+    adapters = []
+    for s in matching_sets:
+        if s.start_sequence:
+            adapters.append(s.start_sequence)
+        if s.end_sequence and (not s.start_sequence or s.end_sequence[1] != s.start_sequence[1]):
+            adapters.append(s.end_sequence)
+    start_names = {s.start_sequence[0] for s in matching_sets if s.start_sequence}
+    end_names = {s.end_sequence[0] for s in matching_sets if s.end_sequence}
+    return adapters, start_names, end_names
+
+
+def scan_middles(seqs, adapter_seqs, middle_threshold, scoring_scheme_vals, device=0):
+    """Exact batched equivalent of the reference's masked re-alignment loop.
+
+    Returns, per read, the ordered list of hits (adapter_index, full_identity, read_start,
+    read_end) that nanopore_read.find_middle_adapters would record."""
+    n = len(seqs)
+    hits = [[] for _ in range(n)]
+    if n == 0 or not adapter_seqs:
+        return hits
+    pack = SeqPack(seqs)
+    views = pack.views(np.zeros(n, np.int64), pack.lengths)
+    n_adp = len(adapter_seqs)
+    next_adp = np.zeros(n, dtype=np.int64)
+    active = np.arange(n)
+    while len(active):
+        # pairs: every active read against adapters next_adp[read]..end, adapter-major
+        reps = (n_adp - next_adp[active]).astype(np.int64)
+        pr = np.repeat(active, reps)
+        first = np.repeat(next_adp[active], reps)
+        offs = np.arange(len(pr)) - np.repeat(np.cumsum(reps) - reps, reps)
+        pa = first + offs
+        res = engine.align(views, adapter_seqs, scoring_scheme_vals, pairs=(pr, pa), device=device)
+        full, _, rs, re_ = identities(res)
+        strong = full >= middle_threshold
+        nxt = []
+        start = 0
+        if np.all(reps == reps[0]):
+            # uniform rows (round 1): only reads with a hit need Python work
+            m2 = strong.reshape(len(active), int(reps[0]))
+            rows = np.nonzero(m2.any(axis=1))[0]
+            qs = rows * int(reps[0]) + np.argmax(m2[rows], axis=1)
+            for k, q in zip(rows.tolist(), qs.tolist()):
+                r = int(active[k])
+                a, s0, e0 = int(pa[q]), int(rs[q]), int(re_[q])
+                hits[r].append((a, float(full[q]), s0, e0))
+                pack.codes[pack.offsets[r] + s0:pack.offsets[r] + e0] = 4   # '-' -> Dna5 N
+                next_adp[r] = a
+                nxt.append(r)
+            active = np.array(nxt, dtype=np.int64)
+            continue
+        for k, r in enumerate(active.tolist()):
+            cnt = int(reps[k])
+            seg = strong[start:start + cnt]
+            if seg.any():
+                q = start + int(np.argmax(seg))
+                a, s0, e0 = int(pa[q]), int(rs[q]), int(re_[q])
+                hits[r].append((a, float(full[q]), s0, e0))
+                pack.codes[pack.offsets[r] + s0:pack.offsets[r] + e0] = 4   # '-' -> Dna5 N
+                next_adp[r] = a
+                nxt.append(r)
+            start += cnt
+        active = np.array(nxt, dtype=np.int64)
+    return hits
+
+
+def find_adapters_in_read_middles(reads, matching_sets, verbosity, middle_threshold,
+                                  extra_trim_good_side, extra_trim_bad_side, scoring_scheme_vals,
+                                  print_dest, threads, discard_middle):
+    """Middle-adapter split scan (porechop_abi.py:457-522)."""
+    if verbosity > 0:
+        verb = 'Discarding' if discard_middle else 'Splitting'
+        print(bold_underline(verb + ' reads containing middle adapters'), file=print_dest)
+    adapters, start_names, end_names = middle_adapter_list(matching_sets)
+    read_count = len(reads)
+    if verbosity == 1:
+        output_progress_line(0, read_count, print_dest)
+    seqs = [r.get_seq_with_start_end_adapters_trimmed() for r in reads]
+    all_hits = scan_middles(seqs, [a[1] for a in adapters], middle_threshold, scoring_scheme_vals)
+    for r, hits in zip(reads, all_hits):
+        for a, full, s0, e0 in hits:
+            r._apply_middle_hit(adapters[a][0], full, s0, e0, extra_trim_good_side, extra_trim_bad_side,
+                                start_names, end_names)
+        if r.middle_adapter_positions and verbosity > 1:
+            print(r.name + '\n' + r.middle_hit_str, file=print_dest, flush=True)
+    if verbosity == 1:
+        output_progress_line(read_count, read_count, print_dest, end_newline=True)
+        print('', flush=True, file=print_dest)
+
+
+def filter_reads_by_adapter(reads, print_dest=sys.stdout):
+    """The fork's filter (porechop_abi.py:36-39): keep reads with start AND end alignments."""
+    kept = [r for r in reads if r.adapters_found()]
+    print('Filtered reads: %d' % len(kept), file=print_dest)
+    return kept

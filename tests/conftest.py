@@ -28,3 +28,13 @@ def gpu_lib():
     if L.pcabi_device_count() < 1:
         pytest.fail('no HIP device visible but test is marked gpu')
     return L
+
+
+@pytest.fixture(scope='session', autouse=True)
+def _built_library():
+    """libpcabi.so is a build artefact (git-ignored): build it once if this tree lacks it."""
+    so = os.path.join(ROOT, 'custom_porechop_abi_amd', 'libpcabi.so')
+    if not os.path.isfile(so):
+        import __graft_entry__
+        __graft_entry__.build_lib()
+    yield

@@ -76,3 +76,22 @@ def align_many(reads, adapters, pairs, scoring):
     L.pcabi_oracle_align_batch(vp(rbufa), vp(off_p), vp(len_p), vp(abufa), vp(aoff), vp(alen), vp(pa),
                                len(pr), *scoring[:4], vp(out))
     return out.T.copy()
+
+
+_LETTERS = np.frombuffer(b'ACGTNNNN', dtype=np.uint8)
+
+
+def align_windows(windows, adapter_seqs, scoring, pairs=None, device=0):
+    """Drop-in for custom_porechop_abi_amd.engine.align computed by the oracle (CPU).
+    Used by tests to exercise the batched host logic without a GPU."""
+    codes, offs, lens = windows
+    reads = [_LETTERS[codes[o:o + l]].tobytes().decode() for o, l in zip(offs.tolist(), lens.tolist())]
+    n_win, n_adp = len(reads), len(adapter_seqs)
+    if pairs is None:
+        pr = np.tile(np.arange(n_win), n_adp)
+        pa = np.repeat(np.arange(n_adp), n_win)
+    else:
+        pr, pa = np.asarray(pairs[0]), np.asarray(pairs[1])
+    if len(pr) == 0:
+        return np.zeros((8, 0), np.int32)
+    return align_many(reads, list(adapter_seqs), (pr, pa), scoring)

@@ -1,0 +1,84 @@
+"""C ABI of libpcabi.so (include/pcabi.h): the library loads without a GPU, exports every entry
+point the header declares (the two legacy symbols of porechop_abi/include/adapter_align.h:12-16
+included), and its host helpers are exact. No compute call needs a GPU here."""
+import ctypes
+import math
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    src = open(os.path.join(ROOT, 'include', 'pcabi.h')).read()
+    src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+    names = re.findall(r'^\s*(?:const\s+)?[A-Za-z_][\w]*\s*\**\s*\**\s*([A-Za-z_]\w*)\s*\(', src, flags=re.M)
+    return sorted(set(n for n in names if n not in ('if', 'while', 'sizeof')))
+
+
+def test_header_declares_legacy_symbols():
+    names = declared_functions()
+    assert 'adapterAlignment' in names and 'freeCString' in names
+    assert len(names) >= 25
+
+
+def test_library_exports_every_declared_symbol():
+    from custom_porechop_abi_amd import _lib
+    L = _lib.lib()
+    so = ctypes.CDLL(_lib.LIB_PATH)
+    for name in declared_functions():
+        assert hasattr(so, name), name
+    assert set(_lib.exported_symbols()) == set(declared_functions())
+    assert L.pcabi_version() == 1
+    assert L.pcabi_max_adapter_len() >= 111       # full rapid barcode adapters
+
+
+def test_encode_dna5_matches_seqan_table():
+    from custom_porechop_abi_amd import _lib, engine
+    L = _lib.lib()
+    src = bytes(range(256))
+    out = np.zeros(256, np.uint8)
+    L.pcabi_encode_dna5(ctypes.c_char_p(src), out.ctypes.data_as(ctypes.c_void_p), 256)
+    exp = np.full(256, 4, np.uint8)
+    for c, v in zip('ACGTUacgtu', [0, 1, 2, 3, 3, 0, 1, 2, 3, 3]):
+        exp[ord(c)] = v
+    assert np.array_equal(out, exp)
+    assert np.array_equal(engine.DNA5, exp)
+
+
+def test_pid6_host_exact():
+    from custom_porechop_abi_amd import engine
+    l = np.repeat(np.arange(1, 400), np.arange(2, 401)).astype(np.int32)
+    m = np.concatenate([np.arange(0, k + 1) for k in range(1, 400)]).astype(np.int32)
+    got = engine.pid6(m, l)
+    exp = np.array([float('%f' % (100.0 * a / b)) for a, b in zip(m.tolist(), l.tolist())])
+    assert np.array_equal(got, exp)
+    assert math.isnan(engine.pid6(np.array([0], np.int32), np.array([0], np.int32))[0])
+
+
+def test_compute_fails_loudly_without_device():
+    from custom_porechop_abi_amd import _lib, cpp_function_wrappers as w, engine
+    L = _lib.lib()
+    if L.pcabi_device_count() > 0:
+        pytest.skip('a GPU is visible')
+    # no CPU fallback: batch API raises, legacy ABI returns the no-alignment sentinel
+    pack = engine.SeqPack(['ACGTACGTAC'])
+    with pytest.raises(_lib.PcabiError):
+        engine.align(pack.views([0], pack.lengths), ['GTAC'], [3, -6, -5, -2])
+    assert w.adapter_alignment('ACGTACGTAC', 'GTAC', [3, -6, -5, -2]).split(',')[0] == '-1'
+
+
+def test_window_views_match_python_slices():
+    from custom_porechop_abi_amd import engine
+    seqs = ['', 'A', 'ACGTN' * 50, 'acgu' * 100, 'GATTACA' * 7]
+    pack = engine.SeqPack(seqs)
+    for E in (150, 1, 0, 400):
+        sw, ew = engine.start_end_windows(pack, E)
+        for k, s in enumerate(seqs):
+            for (codes, off, ln), sl in ((sw, s[:E]), (ew, s[-E:])):
+                got = codes[off[k]:off[k] + ln[k]]
+                assert off[k] % 4 == 0
+                assert np.array_equal(got, engine.encode_seq(sl))

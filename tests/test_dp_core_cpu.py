@@ -1,0 +1,96 @@
+"""The device DP core (custom_porechop_abi_amd/csrc/pcabi_dp.h), compiled for the HOST with g++,
+against the oracle and the reference's golden vectors. This checks the exact arithmetic the
+HIP kernels run (same source) without a GPU: the forward traceback-attribute propagation,
+the pass-through padding rows of the fast core, the wrapped start-column field (reads longer
+than 65 kb) and the exact "%f" identity rounding (pid6)."""
+import ctypes
+import os
+import random
+import subprocess
+import tempfile
+
+import pytest
+
+from tests import golden_lib, oracle_lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope='module')
+def model():
+    out = os.path.join(tempfile.mkdtemp(prefix='pcabi_model_'), 'dp_model.so')
+    subprocess.check_call(['g++', '-std=c++17', '-O2', '-shared', '-fPIC', '-o', out,
+                           os.path.join(ROOT, 'tests', 'native', 'dp_model.cpp')])
+    L = ctypes.CDLL(out)
+    for fn in ('pcabi_model_align', 'pcabi_model_align_fast'):
+        getattr(L, fn).argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int] + \
+            [ctypes.c_int] * 4 + [ctypes.c_void_p]
+    L.pcabi_model_pid6.restype = ctypes.c_double
+    L.pcabi_model_pid6.argtypes = [ctypes.c_int, ctypes.c_int]
+    return L
+
+
+def _run(model, fn, r, a, sc):
+    out = (ctypes.c_int * 8)()
+    rb, ab = r.encode(), a.encode()
+    rc = getattr(model, fn)(rb, len(rb), ab, len(ab), *sc, out)
+    return rc, list(out)
+
+
+def _fmt(res):
+    rs, re_, as_, ae, score, m, l1, l2 = res
+    p1 = '-nan' if l1 == 0 else '%f' % (100.0 * m / l1)
+    p2 = '-nan' if l2 == 0 else '%f' % (100.0 * m / l2)
+    return '%d,%d,%d,%d,%d,%s,%s' % (rs, re_, as_, ae, score, p1, p2)
+
+
+@pytest.mark.parametrize('fn', ['pcabi_model_align_fast', 'pcabi_model_align'])
+def test_core_vs_reference_golden(model, fn):
+    n_checked = 0
+    for sc, r, a, exp in golden_lib.g1_rows():
+        if not r or not a or len(a) > 128:
+            continue
+        rc, res = _run(model, fn, r, a, sc)
+        if rc == -3:
+            continue
+        assert rc == 0
+        assert _fmt(res) == exp, (sc, r, a, exp, res)
+        n_checked += 1
+    assert n_checked > 15000
+
+
+@pytest.mark.parametrize('fn', ['pcabi_model_align_fast', 'pcabi_model_align'])
+def test_core_fuzz_vs_oracle(model, fn):
+    rng = random.Random(42)
+    schemes = [(3, -6, -5, -2), (2, -1, -1, -1), (1, -1, -3, -1), (3, -6, -2, -5), (5, -4, -8, -6)]
+    for _ in range(3000):
+        sc = rng.choice(schemes)
+        al = rng.choice(['A', 'AT', 'ACGT', 'ACGTN'])
+        L = rng.randint(1, 128)
+        a = ''.join(rng.choice(al) for _ in range(L))
+        r = ''.join(rng.choice(al) for _ in range(rng.randint(1, 260)))
+        rc, res = _run(model, fn, r, a, sc)
+        if rc == -3:
+            continue
+        assert res == oracle_lib.align(r, a, sc), (sc, r, a)
+
+
+def test_core_long_reads_wrapped_start_column(model):
+    """Reads longer than the 16-bit start-column field: adapters placed past 65,536."""
+    rng = random.Random(9)
+    for k in range(4):
+        n = 70000 + 30000 * k
+        a = ''.join(rng.choice('ACGT') for _ in range(24))
+        r = [rng.choice('ACGT') for _ in range(n)]
+        p = n - 5000 if k % 2 else 66000
+        r[p:p + 24] = list(a)
+        r = ''.join(r)
+        for sc in [(3, -6, -5, -2), (2, -1, -1, -1)]:
+            rc, res = _run(model, 'pcabi_model_align_fast', r, a, sc)
+            assert rc == 0 and res == oracle_lib.align(r, a, sc)
+
+
+def test_pid6_matches_text_round_trip(model):
+    for l in range(1, 700):
+        for m in range(0, l + 1):
+            assert model.pcabi_model_pid6(m, l) == float('%f' % (100.0 * m / l))

@@ -1,0 +1,141 @@
+"""Batched phase drivers + NanoporeRead decision rules vs the reference's OWN drivers.
+
+tests/golden/g2_decisions.json.gz holds, for the reference's test FASTQs and a seeded synthetic
+set, what porechop_abi.porechop_abi (reference Python, reference SeqAn .so) decided for every
+read: matching adapter sets and their discovery scores, trim amounts, recorded start/end
+alignments, middle-adapter hits/trim positions and barcode scores/calls
+(tools/make_golden_g2.py). Two backends run the same host logic:
+  * 'oracle' (CPU, not gpu): engine.align replaced by the CPU oracle -- checks the host logic;
+  * 'gpu'   : the real HIP kernels through libpcabi.so.
+"""
+import io
+
+import pytest
+
+from tests import golden_lib, oracle_lib
+
+G2 = golden_lib.g2()
+CASES = [c['case'] for c in G2['cases']]
+
+
+def _records(case):
+    if case['input'] == 'synthetic_reads':
+        return [tuple(x) for x in G2['synthetic_reads']]
+    return golden_lib.load_records(case['input'])
+
+
+def _ranges(positions):
+    out = []
+    for p in sorted(positions):
+        if out and out[-1][1] == p:
+            out[-1][1] = p + 1
+        else:
+            out.append([p, p + 1])
+    return out
+
+
+def run_pipeline(case):
+    from custom_porechop_abi_amd import adapters as A, porechop_abi as P
+    from custom_porechop_abi_amd.nanopore_read import NanoporeRead
+    opts = case['opts']
+    sink = io.StringIO()
+    sets = A.fresh_adapters()
+    reads = [NanoporeRead(n, s, q) for n, s, q in _records(case)]
+    sc = opts['scoring']
+    check = reads[:opts.get('check_reads', 10000)]
+    matching = P.find_matching_adapter_sets(check, 0, opts['end_size'], sc, sink, opts['adapter_threshold'], 1,
+                                            adapter_sets=sets)
+    matching = P.fix_up_1d2_sets(matching)
+    fr = P.choose_barcoding_kit(matching, 0, sink) if opts['barcodes'] else None
+    set_scores = [[a.name, a.best_start_score, a.best_end_score] for a in sets if '(full sequence)' not in a.name]
+    matching = P.add_full_barcode_adapter_sets(matching)
+    if matching:
+        P.find_adapters_at_read_ends(reads, matching, 0, opts['end_size'], opts['extra_end_trim'],
+                                     opts['end_threshold'], sc, sink, opts['min_trim_size'], 1, opts['barcodes'],
+                                     75.0, 5.0, opts.get('require_two', False), fr)
+        P.find_adapters_in_read_middles(reads, matching, 0, opts['middle_threshold'], 10, 100, sc, sink, 1, False)
+    return matching, fr, set_scores, reads
+
+
+def check_case(case):
+    matching, fr, set_scores, reads = run_pipeline(case)
+    assert [a.name for a in matching] == case['matching']
+    assert fr == case['forward_or_reverse']
+    assert set_scores == case['set_scores']
+    assert len(reads) == len(case['reads'])
+    for r, exp in zip(reads, case['reads']):
+        got = {
+            'name': r.name,
+            'start_trim': r.start_trim_amount, 'end_trim': r.end_trim_amount,
+            'start_alns': [[a[0].name, a[1], a[2], a[3], a[4]] for a in r.start_adapter_alignments],
+            'end_alns': [[a[0].name, a[1], a[2], a[3], a[4]] for a in r.end_adapter_alignments],
+            'middle_pos': _ranges(r.middle_adapter_positions),
+            'middle_trim': _ranges(r.middle_trim_positions),
+            'middle_hit_str': r.middle_hit_str,
+            'start_bc': [list(x) for x in r.start_barcode_scores.items()],
+            'end_bc': [list(x) for x in r.end_barcode_scores.items()],
+            'barcode_call': r.barcode_call,
+        }
+        assert got == exp, r.name
+
+
+@pytest.mark.parametrize('case_name', CASES)
+def test_drivers_match_reference_with_oracle_backend(case_name, monkeypatch):
+    from custom_porechop_abi_amd import engine
+    monkeypatch.setattr(engine, 'align', oracle_lib.align_windows)
+    check_case([c for c in G2['cases'] if c['case'] == case_name][0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case_name', CASES)
+def test_drivers_match_reference_on_gpu(gpu_lib, case_name):
+    check_case([c for c in G2['cases'] if c['case'] == case_name][0])
+
+
+def test_reference_test_expectations_one_adapter_set(monkeypatch):
+    """test/test_one_adapter_set.py:51-69 (verbosity 1/2 output): 4 of 9 reads start-trimmed,
+    3 of 9 end-trimmed -- on the G2 decisions and through our drivers."""
+    from custom_porechop_abi_amd import engine
+    monkeypatch.setattr(engine, 'align', oracle_lib.align_windows)
+    case = [c for c in G2['cases'] if c['case'] == 'one_adapter_set'][0]
+    _, _, _, reads = run_pipeline(case)
+    assert sum(1 for r in reads if r.start_trim_amount) == 4
+    assert sum(1 for r in reads if r.end_trim_amount) == 3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case_name', ['one_adapter_set', 'barcodes', 'two_adapter_sets'])
+def test_per_read_methods_on_gpu(gpu_lib, case_name):
+    """The unbatched reference call pattern (one adapterAlignment per alignment through the
+    legacy C ABI, porechop_abi.py:366-378 / 476-484 single-thread loops) gives the same
+    decisions."""
+    from custom_porechop_abi_amd import adapters as A, porechop_abi as P
+    from custom_porechop_abi_amd.nanopore_read import NanoporeRead
+    case = [c for c in G2['cases'] if c['case'] == case_name][0]
+    opts = case['opts']
+    sc = opts['scoring']
+    sets = A.fresh_adapters()
+    reads = [NanoporeRead(n, s, q) for n, s, q in _records(case)]
+    for r in reads:
+        for s in sets:
+            if '(full sequence)' not in s.name:
+                r.align_adapter_set(s, opts['end_size'], sc)
+    search = [a for a in sets if '(full sequence)' not in a.name]
+    assert [[a.name, a.best_start_score, a.best_end_score] for a in search] == case['set_scores']
+    matching = [a for a in search if a.best_start_or_end_score() >= opts['adapter_threshold']]
+    matching = P.fix_up_1d2_sets(matching)
+    fr = P.choose_barcoding_kit(matching, 0, io.StringIO()) if opts['barcodes'] else None
+    matching = P.add_full_barcode_adapter_sets(matching)
+    adapters, start_names, end_names = P.middle_adapter_list(matching)
+    for r, exp in zip(reads, case['reads']):
+        r.find_start_trim(matching, opts['end_size'], opts['extra_end_trim'], opts['end_threshold'], sc,
+                          opts['min_trim_size'], opts['barcodes'], fr)
+        r.find_end_trim(matching, opts['end_size'], opts['extra_end_trim'], opts['end_threshold'], sc,
+                        opts['min_trim_size'], opts['barcodes'], fr)
+        if opts['barcodes']:
+            r.determine_barcode(75.0, 5.0, opts.get('require_two', False))
+        r.find_middle_adapters(adapters, opts['middle_threshold'], 10, 100, sc, start_names, end_names)
+        assert (r.start_trim_amount, r.end_trim_amount, r.barcode_call) == \
+            (exp['start_trim'], exp['end_trim'], exp['barcode_call'])
+        assert _ranges(r.middle_trim_positions) == exp['middle_trim']
+        assert r.middle_hit_str == exp['middle_hit_str']
