@@ -108,10 +108,10 @@ def main():
     sc = (3, -6, -5, -2)
 
     def align_start():
-        _lib.check(L.pcabi_align_cross_dev(d_codes, d_soff, d_slen, n, tabs[0], *sc, d_sres, s_stride, stream), 'align')
+        _lib.check(L.pcabi_align_cross_dev(d_codes, d_soff, d_slen, n, int(s_len.max()), tabs[0], *sc, d_sres, s_stride, stream), 'align')
 
     def align_end():
-        _lib.check(L.pcabi_align_cross_dev(d_codes, d_eoff, d_elen, n, tabs[1], *sc, d_eres, e_stride, stream), 'align')
+        _lib.check(L.pcabi_align_cross_dev(d_codes, d_eoff, d_elen, n, int(e_len.max()), tabs[1], *sc, d_eres, e_stride, stream), 'align')
 
     def epilogue():
         _lib.check(L.pcabi_end_trim_dev(d_sres, s_stride, n_sa, d_eres, e_stride, n_ea, n, args.end_size,

@@ -63,8 +63,8 @@ def lib():
         'pcabi_event_elapsed_ms': ([ctypes.POINTER(ctypes.c_float), c_p, c_p], c_int),
         'pcabi_adapters_create': ([c_p, c_p, c_p, ctypes.c_int32, ctypes.POINTER(c_p)], c_int),
         'pcabi_adapters_destroy': ([c_p], None),
-        'pcabi_align_cross_dev': ([c_p, c_p, c_p, c_i64, c_p, c_int, c_int, c_int, c_int, c_p, c_i64,
-                                   c_p], c_int),
+        'pcabi_align_cross_dev': ([c_p, c_p, c_p, c_i64, ctypes.c_int32, c_p, c_int, c_int, c_int, c_int,
+                                   c_p, c_i64, c_p], c_int),
         'pcabi_end_trim_dev': ([c_p, c_i64, ctypes.c_int32, c_p, c_i64, ctypes.c_int32, c_i64, c_int,
                                 c_int, c_d, c_int, c_p, c_p, c_p, c_p, c_p], c_int),
         'pcabi_best_full_identity_dev': ([c_p, c_i64, c_i64, ctypes.c_int32, c_p, c_p], c_int),

@@ -28,6 +28,15 @@
 // (S/ = porechop_abi/include/seqan/ of the reference.)
 #pragma once
 
+// Scheduling fence every N rows in the fast cores (0 = none); see DESIGN.md §5.
+#ifndef PCABI_ROW_FENCE
+#define PCABI_ROW_FENCE 1
+#endif
+
+
+
+
+
 #include <stdint.h>
 
 #ifdef __HIPCC__
@@ -43,7 +52,7 @@ namespace pcabi {
 // wins and never ties (|scores| <= 2^20 for all supported sizes).
 constexpr int NEG = -(1 << 28);
 
-// Attribute word: [ (c + CBIAS) mod 2^16 : 16 ][ m : 8 ][ nD : 8 ]
+// Attribute word: [ (c + CBIAS) mod 2^16 : 16 ][ nD : 8 ][ m : 8 ]
 //   c  = j0 - i0  (path start cell; at least one of i0, j0 is zero)
 //   m  = matching diagonal columns on the path, nD = diagonal columns on the path
 // The c field WRAPS (uint32 arithmetic, top field): every live path spans fewer than
@@ -55,8 +64,8 @@ constexpr int ATTR_CSH = 2 * ATTR_B;
 constexpr int ATTR_CBIAS = 255;            // c >= -L >= -255
 constexpr int MAX_ADAPTER_LEN = 255;       // m, nD <= L fit 8 bits
 constexpr int MAX_WINDOW_LEN = 1 << 30;
-constexpr uint32_t INC_D = 1u;                           // mismatching diagonal
-constexpr uint32_t INC_M = (1u << ATTR_B) + 1u;          // matching diagonal
+constexpr uint32_t INC_D = 1u << ATTR_B;                 // mismatching diagonal: nD + 1
+constexpr uint32_t INC_M = INC_D + 1u;                   // matching diagonal: nD + 1, m + 1
 
 PCABI_HD uint32_t attr_start(int c) { return (uint32_t)(c + ATTR_CBIAS) << ATTR_CSH; }
 
@@ -102,8 +111,8 @@ PCABI_HD Result finish(const Best &b, int L, int n) {
     // c lies in [bj - span, bj] with span < 2^15: undo the mod-2^16 wrap
     const int u = (int)(b.attr >> ATTR_CSH) - ATTR_CBIAS;
     const int c = b.bj - ((b.bj - u) & 0xFFFF);
-    const int m = (int)((b.attr >> ATTR_B) & ATTR_MASK);
-    const int nd = (int)(b.attr & ATTR_MASK);
+    const int m = (int)(b.attr & ATTR_MASK);
+    const int nd = (int)((b.attr >> ATTR_B) & ATTR_MASK);
     const int i0 = c < 0 ? -c : 0;
     const int j0 = c > 0 ? c : 0;
     const int h = i0 + j0;                             // head length == first path column
@@ -352,6 +361,11 @@ namespace pcabi {
 // Preconditions (checked by the host): 1 <= L <= RPL <= L + 3; off == 0 or (go < 0 && ge < 0).
 // ------------------------------------------------------------------------------------------
 constexpr uint32_t INC_PAD = 1u << ATTR_CSH;   // padding diagonal: start column + 1
+
+PCABI_HD int max3i(int a, int b, int c) {   // one v_max3_i32 on gfx950
+    const int ab = a > b ? a : b;
+    return ab > c ? ab : c;
+}
 constexpr int PAD_CODE = 5;                     // never equal to a read code (0..4)
 
 template <int RPL, bool AFFINE>
@@ -370,21 +384,30 @@ struct LaneDP {
     template <typename AdpFn, bool LAST>
     PCABI_HD void column(const int r, const int j, const AdpFn &adp, const int L, const int off,
                          const Scoring &sc) {
-        int sup = 0, vup = NEG, sdg = 0;
-        uint32_t saup = attr_start(j), vaup = 0, sadg = attr_start(j - 1);
+        int sup = 0, vup = NEG;
+        uint32_t saup = attr_start(j), vaup = 0;
         int slt_up = LT_NONE, vt_up = 0, vp_up = 0;
         int lv = 0, lh = 0, ls = 0, lslt = LT_D;
         bool lhext = false;
         uint32_t lva = 0, lha = 0, lsa = 0;
+        // diagonal candidate of row 1 (from the boundary cell (0, j-1)); every row computes the
+        // next row's candidate from its OLD S/SA before overwriting them (no rotation copies)
+        bool match = (r == adp(1));
+        int diag = 0 + (match ? sc.ma : mis[1]);
+        uint32_t da = attr_start(j - 1) + ids[1] + (uint32_t)match;
 #pragma unroll
         for (int s = 1; s <= RPL; ++s) {
-            const bool match = (r == adp(s));
-            const int mi_s = (s <= 3) ? mis[s] : sc.mi;
-            const uint32_t id_s = (s <= 3) ? ids[s] : INC_D;
-            const int diag = sdg + (match ? sc.ma : mi_s);
-            const uint32_t da = sadg + (match ? INC_M : id_s);
-            int hn, vn, g;
-            uint32_t han, van, ga;
+            int diag_nx = 0;
+            uint32_t da_nx = 0;
+            if (s < RPL) {
+                const bool mt = (r == adp(s + 1));
+                const int mi_n = (s + 1 <= 3) ? mis[s + 1] : sc.mi;
+                const uint32_t id_n = (s + 1 <= 3) ? ids[s + 1] : INC_D;
+                diag_nx = S[s] + (mt ? sc.ma : mi_n);
+                da_nx = SA[s] + id_n + (uint32_t)mt;
+            }
+            int hn, vn, sn;
+            uint32_t han, van;
             bool hext, vext, fromv;
             if (AFFINE) {
                 const int hx = H[s] + sc.ge, ho = S[s] + sc.go;
@@ -395,21 +418,18 @@ struct LaneDP {
                 vext = !(vx < vo);
                 vn = vext ? vx : vo;
                 van = vext ? vaup : saup;
-                fromv = !(vn < hn);
-                g = fromv ? vn : hn;
-                ga = fromv ? van : han;
             } else {
                 hext = vext = false;
-                const int vv = sup + sc.ge, hh = S[s] + sc.ge;
-                fromv = !(vv < hh);
-                g = fromv ? vv : hh;
-                ga = fromv ? saup : SA[s];
-                hn = vn = NEG;
-                han = van = 0;
+                vn = sup + sc.ge;
+                hn = S[s] + sc.ge;
+                van = saup;
+                han = SA[s];
             }
-            const bool isd = !(diag < g);
-            const int sn = isd ? diag : g;
-            const uint32_t san = isd ? da : ga;
+            // S = max(diag, V, H); ties: diagonal, then V (S/align/dp_formula.h:153-163)
+            sn = max3i(diag, vn, hn);
+            const bool isd = (diag == sn);
+            fromv = (vn == sn);
+            const uint32_t san = isd ? da : (fromv ? van : han);
             if (LAST && s < RPL) {
                 const int slt = isd ? LT_D : (fromv ? LT_V : LT_H);
                 // trailing V run of the V-state (affine) or of the S-state from V (linear)
@@ -448,16 +468,23 @@ struct LaneDP {
                     vp_up = vp;
                 }
             }
-            sdg = S[s];
-            sadg = SA[s];
             S[s] = sn;
-            H[s] = hn;
             SA[s] = san;
-            HA[s] = han;
+            if (AFFINE) {
+                H[s] = hn;
+                HA[s] = han;
+            }
             sup = sn;
             vup = vn;
             saup = san;
             vaup = van;
+            diag = diag_nx;
+            da = da_nx;
+#if defined(__HIP_DEVICE_COMPILE__)
+            // keep the scheduler from hoisting every row's diagonal work to the column top
+            // (it raises VGPR/SGPR pressure and costs occupancy)
+            if (PCABI_ROW_FENCE > 0 && (s % (PCABI_ROW_FENCE > 0 ? PCABI_ROW_FENCE : 1)) == 0) __builtin_amdgcn_sched_barrier(0);
+#endif
         }
         // ---- row L: H-state trailing run at (L, j) and the last-row scout ----
         const bool hcont = AFFINE ? (lhext || slt_last == LT_H) : (slt_last == LT_H);
@@ -517,8 +544,16 @@ PCABI_HD Result align_lane_fast(ReadFn &rd, int n, const AdpFn &adp, int L, cons
     st.slt_last = LT_NONE;
     st.ht_last = 0;
     st.hp_last = 0;
-    for (int j = 1; j < n; ++j) st.template column<AdpFn, false>(rd(j), j, adp, L, off, sc);
-    st.template column<AdpFn, true>(rd(n), n, adp, L, off, sc);
+    // The code of column j+1 is requested at the top of column j and only consumed after the
+    // column body, so the load has a whole column (RPL rows of VALU work) to land.
+    int r = rd(1);
+#pragma unroll 1
+    for (int j = 1; j < n; ++j) {
+        const int rn = rd(j + 1);      // buffers are padded: reading column n+... is safe
+        st.template column<AdpFn, false>(r, j, adp, L, off, sc);
+        r = rn;
+    }
+    st.template column<AdpFn, true>(r, n, adp, L, off, sc);
     Best b;
     b.score = st.bscore; b.bi = st.bi; b.bj = st.bj; b.attr = st.battr;
     b.ltype = st.blt; b.trail = st.btrail; b.precd = st.bprec;
@@ -531,6 +566,228 @@ PCABI_HD bool fast_ok(int L, int rpl, const Scoring &sc) {
     if (off < 0 || off > 3) return false;
     if (off == 0) return true;
     return (sc.go != sc.ge) ? (sc.go < 0 && sc.ge < 0) : (sc.ge < 0);
+}
+
+}  // namespace pcabi
+
+namespace pcabi {
+
+// ==========================================================================================
+// align_lane_packed<RPL, AFFINE>: the end-window core (RPL <= 32, windows <= 223 columns).
+//
+// Every DP value is ONE 32-bit signed key
+//      [ score : 10 (signed) ][ tb : 2 ][ c + 32 : 8 ][ nD : 6 ][ m : 6 ]      (MSB .. LSB)
+// so a plain signed max compares scores first, then the tie-break field tb, and carries the
+// traceback attributes of the winner along for free: the reference's tie rules become tb
+// values (S/align/dp_formula.h:153-163, dp_formula_affine.h:66-125):
+//      stored S keys tb = 0, stored H keys tb = 1, V keys tb = 2, diagonal candidates tb = 3
+//   H = max(H + ge [tb 1], S + go [tb 0])      -> extend wins ties
+//   V = max(V + ge [tb 2], S + go [tb 0])      -> extend wins ties
+//   S = max3(diag [tb 3], V|tb2 [tb 2], H [tb <= 1])  -> diagonal, then V, then H
+// The substitution score and the attribute increment of a diagonal step are ONE add of a
+// key-shaped constant (match / mismatch / padding). Per cell: 13 VALU ops (affine), 7 (linear),
+// and 2 (affine) / 1 (linear) registers per adapter row -- versus 21 ops and 4 registers when
+// scores and attributes live in separate registers (align_lane_fast).
+//
+// Range conditions (checked by the host, packed_ok): every reachable score and the NEG
+// sentinel fit the 10-bit field, c + 32 fits 8 bits (window <= 223), m, nD <= 32 fit 6 bits.
+// ==========================================================================================
+namespace pk {
+constexpr int M_SH = 0, D_SH = 6, C_SH = 12, TB_SH = 20, SC_SH = 22;
+constexpr int CB = 32;                          // c bias: c >= -L >= -32
+constexpr int32_t TB1 = 1 << TB_SH, TB2 = 2 << TB_SH, TB3 = 3 << TB_SH, TBM = 3 << TB_SH;
+constexpr int32_t INC_D = 1 << D_SH, INC_M = (1 << D_SH) + 1, INC_PAD = 1 << C_SH;
+constexpr int MAX_WINDOW = 255 - CB;            // 223
+constexpr int MAX_RPL = 32;
+PCABI_HD int32_t sc(int v) { return (int32_t)((uint32_t)v << SC_SH); }   // score -> key units
+PCABI_HD int32_t start(int c) { return (int32_t)((uint32_t)(c + CB) << C_SH); }
+PCABI_HD int score(int32_t k) { return k >> SC_SH; }
+PCABI_HD int tb(int32_t k) { return (k >> TB_SH) & 3; }
+PCABI_HD uint32_t attr(int32_t k) { return (uint32_t)k & ((1u << TB_SH) - 1u); }
+// packed attribute -> standard attribute word (finish())
+PCABI_HD uint32_t to_std(uint32_t a) {
+    const uint32_t m = a & 63u, nd = (a >> D_SH) & 63u;
+    const int c = (int)((a >> C_SH) & 255u) - CB;
+    return attr_start(c) | (nd << ATTR_B) | m;
+}
+PCABI_HD int neg_score(int L, const Scoring &s) {
+    const int g = (s.go < s.ge ? s.go : s.ge);
+    const int lo = (L * s.mi < 0 ? L * s.mi : 0) + 2 * (g < 0 ? g : 0);
+    const int gm = (-s.go > -s.ge ? -s.go : -s.ge);
+    return lo - 2 * (gm > 0 ? gm : 0) - 8;
+}
+}  // namespace pk
+
+PCABI_HD bool packed_ok(int L, int rpl, int max_window, const Scoring &s) {
+    if (rpl > pk::MAX_RPL || max_window > pk::MAX_WINDOW) return false;
+    if (!fast_ok(L, rpl, s)) return false;
+    const int hi = (rpl * s.ma > 0 ? rpl * s.ma : 0);
+    const int gm = (-s.go > -s.ge ? -s.go : -s.ge);
+    const int neg = pk::neg_score(rpl, s) - (gm > 0 ? gm : 0);
+    return hi <= 500 && neg >= -510 && s.ma <= 500 && s.mi >= -500;
+}
+
+template <int RPL, bool AFFINE>
+struct LanePacked {
+    int32_t SK[RPL + 1];   // S keys, tb = 0
+    int32_t HK[RPL + 1];   // H keys, tb = 1 (affine only)
+    int bscore, bi, bj, blt, btrail, bprec;
+    uint32_t battr;        // packed attribute
+    int slt_last, ht_last, hp_last;
+    int32_t k_match, k_mis[4], k_ge, k_go, k_gev, k_geh, neg2;
+
+    template <typename AdpFn, bool LAST>
+    PCABI_HD void column(const int r, const int j, const AdpFn &adp, const int L, const int off) {
+        int32_t sup = pk::start(j);                // S(0, j): score 0, tb 0
+        int32_t vup = neg2;                        // V(0, j) = NEG, tb 2
+        int slt_up = LT_NONE, vt_up = 0, vp_up = 0;
+        int32_t lv = 0, lh = 0, ls = 0;
+        int lslt = LT_D;
+        bool lhext = false;
+        int32_t diag = pk::start(j - 1) + ((r == adp(1)) ? k_match : k_mis[1]);
+#pragma unroll
+        for (int s = 1; s <= RPL; ++s) {
+            int32_t diag_nx = 0;
+            if (s < RPL) {
+                const int32_t kmis = (s + 1 <= 3) ? k_mis[s + 1] : k_mis[0];
+                diag_nx = SK[s] + ((r == adp(s + 1)) ? k_match : kmis);
+            }
+            int32_t hn, vn2, sn;
+            bool hext = false, vext = false;
+            if (AFFINE) {
+                const int32_t hx = HK[s] + k_ge, ho = SK[s] + k_go;
+                hn = hx > ho ? hx : ho;                  // tb 1 iff extend
+                const int32_t vx = vup + k_ge, vo = sup + k_go;
+                const int32_t vn = vx > vo ? vx : vo;    // tb 2 iff extend
+                vn2 = vn | pk::TB2;
+                if (LAST || s == RPL) { hext = pk::tb(hn) == 1; vext = pk::tb(vn) == 2; }
+            } else {
+                vn2 = sup + k_gev;                       // tb 2
+                hn = SK[s] + k_geh;                      // tb 1
+            }
+            sn = max3i(diag, vn2, hn);
+            const int t = pk::tb(sn);
+            const int slt = t == 3 ? LT_D : (t == 2 ? LT_V : LT_H);
+            if (LAST && s < RPL) {
+                const bool cont = AFFINE ? (vext || slt_up == LT_V) : (slt_up == LT_V);
+                const int vt = cont ? vt_up + 1 : 1;
+                const int vp = cont ? vp_up : (slt_up == LT_D ? 1 : 0);
+                const int sc_s = pk::score(sn);
+                if (sc_s > bscore) {
+                    bscore = sc_s;
+                    bi = s - off;
+                    bj = j;
+                    if (AFFINE) {
+                        const bool isv = pk::score(vn2) == sc_s, ish = !isv && pk::score(hn) == sc_s;
+                        battr = pk::attr(isv ? vn2 : (ish ? hn : sn));
+                        blt = isv ? LT_V : (ish ? LT_H : LT_D);
+                        btrail = isv ? vt : 0;
+                        bprec = isv ? vp : 0;
+                    } else {
+                        battr = pk::attr(sn);
+                        blt = slt;
+                        btrail = (slt == LT_V) ? vt : 0;
+                        bprec = (slt == LT_V) ? vp : 0;
+                    }
+                }
+                if (AFFINE) { vt_up = vt; vp_up = vp; }
+                else { vt_up = (slt == LT_V) ? vt : 0; vp_up = (slt == LT_V) ? vp : 0; }
+                slt_up = slt;
+            }
+            if (s == RPL) {
+                lv = vn2; lh = hn; ls = sn; lslt = slt; lhext = hext;
+                if (LAST) {
+                    const bool cont = AFFINE ? (vext || slt_up == LT_V) : (slt_up == LT_V);
+                    const int vt = cont ? vt_up + 1 : 1;
+                    const int vp = cont ? vp_up : (slt_up == LT_D ? 1 : 0);
+                    vt_up = vt;
+                    vp_up = vp;
+                }
+            }
+            SK[s] = sn & ~pk::TBM;
+            if (AFFINE) HK[s] = hn | pk::TB1;
+            sup = SK[s];
+            vup = vn2;
+            diag = diag_nx;
+#if defined(__HIP_DEVICE_COMPILE__)
+            if (PCABI_ROW_FENCE > 0 && (s % (PCABI_ROW_FENCE > 0 ? PCABI_ROW_FENCE : 1)) == 0) __builtin_amdgcn_sched_barrier(0);
+#endif
+        }
+        // ---- row L ----
+        const bool hcont = AFFINE ? (lhext || slt_last == LT_H) : (slt_last == LT_H);
+        const int ht = hcont ? ht_last + 1 : 1;
+        const int hp = hcont ? hp_last : (slt_last == LT_D ? 1 : 0);
+        const int lsc = pk::score(ls);
+        const bool upd = lsc > bscore;
+        int clt, ctrail, cprec;
+        uint32_t cattr;
+        if (AFFINE) {
+            const bool isv = pk::score(lv) == lsc, ish = !isv && pk::score(lh) == lsc;
+            cattr = pk::attr(isv ? lv : (ish ? lh : ls));
+            clt = isv ? LT_V : (ish ? LT_H : LT_D);
+            ctrail = isv ? (LAST ? vt_up : 0) : (ish ? ht : 0);
+            cprec = isv ? (LAST ? vp_up : 0) : (ish ? hp : 0);
+        } else {
+            cattr = pk::attr(ls);
+            clt = lslt;
+            ctrail = (lslt == LT_V) ? (LAST ? vt_up : 0) : (lslt == LT_H ? ht : 0);
+            cprec = (lslt == LT_V) ? (LAST ? vp_up : 0) : (lslt == LT_H ? hp : 0);
+        }
+        bscore = upd ? lsc : bscore;
+        bi = upd ? L : bi;
+        bj = upd ? j : bj;
+        battr = upd ? cattr : battr;
+        blt = upd ? clt : blt;
+        btrail = upd ? ctrail : btrail;
+        bprec = upd ? cprec : bprec;
+        if (AFFINE) { ht_last = ht; hp_last = hp; }
+        else { ht_last = (lslt == LT_H) ? ht : 0; hp_last = (lslt == LT_H) ? hp : 0; }
+        slt_last = lslt;
+    }
+};
+
+template <int RPL, bool AFFINE, typename ReadFn, typename AdpFn>
+PCABI_HD Result align_lane_packed(ReadFn &rd, int n, const AdpFn &adp, int L, const Scoring sc) {
+    LanePacked<RPL, AFFINE> st;
+    const int off = RPL - L;
+    const int32_t neg = pk::sc(pk::neg_score(RPL, sc));
+#pragma unroll
+    for (int s = 1; s <= RPL; ++s) {
+        st.SK[s] = pk::start(-(s > off ? s - off : 0));
+        st.HK[s] = neg | pk::TB1;
+    }
+    st.k_match = pk::sc(sc.ma) + pk::TB3 + pk::INC_M;
+    st.k_mis[0] = pk::sc(sc.mi) + pk::TB3 + pk::INC_D;
+#pragma unroll
+    for (int s = 1; s <= 3; ++s)
+        st.k_mis[s] = (s <= off) ? (pk::TB3 + pk::INC_PAD) : st.k_mis[0];
+    st.k_ge = pk::sc(sc.ge);
+    st.k_go = pk::sc(sc.go);
+    st.k_gev = pk::sc(sc.ge) + pk::TB2;
+    st.k_geh = pk::sc(sc.ge) + pk::TB1;
+    st.neg2 = neg | pk::TB2;
+    st.bscore = 0;
+    st.bi = L;
+    st.bj = 0;
+    st.battr = (uint32_t)pk::start(-L);
+    st.blt = LT_NONE;
+    st.btrail = 0;
+    st.bprec = 0;
+    st.slt_last = LT_NONE;
+    st.ht_last = 0;
+    st.hp_last = 0;
+    int r = rd(1);
+#pragma unroll 1
+    for (int j = 1; j < n; ++j) {
+        const int rn = rd(j + 1);
+        st.template column<AdpFn, false>(r, j, adp, L, off);
+        r = rn;
+    }
+    st.template column<AdpFn, true>(r, n, adp, L, off);
+    Best b;
+    b.score = st.bscore; b.bi = st.bi; b.bj = st.bj; b.attr = pk::to_std(st.battr);
+    b.ltype = st.blt; b.trail = st.btrail; b.precd = st.bprec;
+    return finish(b, L, n);
 }
 
 }  // namespace pcabi

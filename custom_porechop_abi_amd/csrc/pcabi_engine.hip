@@ -22,6 +22,10 @@
 #include "../../include/pcabi.h"
 #include "pcabi_dp.h"
 
+#ifndef PCABI_WAVES
+#define PCABI_WAVES 1
+#endif
+
 namespace {
 
 thread_local std::string g_err;
@@ -41,7 +45,7 @@ int fail(int code, const std::string &msg) {
 // Register buckets. FAST (branch-free core, pcabi_dp.h align_lane_fast): every multiple of 4 up
 // to 64, used whenever pcabi::fast_ok holds. GENERIC (guarded core, any scoring): a few sizes,
 // also the only path for 64 < L <= 128 for now.
-enum Kind { FAST = 0, GENERIC = 1 };
+enum Kind { FAST = 0, GENERIC = 1, PACKED = 2 };
 struct BucketDef {
     int rpl;
     Kind kind;
@@ -83,23 +87,12 @@ struct KParams {
     pcabi::Scoring sc;
 };
 
-// Streams one window's Dna5 codes 4 bytes at a time (window offsets are 4-byte aligned).
+// Window codes, one byte per column (buffers carry >= 16 bytes of padding past every window,
+// so the one-column-ahead read of the last column stays in bounds).
 struct WindowReader {
-    const uint32_t *p;
-    uint32_t cur, nxt;
-    __device__ __forceinline__ explicit WindowReader(const uint8_t *base) {
-        p = reinterpret_cast<const uint32_t *>(base);
-        cur = 0;
-        nxt = p[0];
-    }
-    __device__ __forceinline__ int operator()(int j) {
-        const int k = j - 1;
-        if ((k & 3) == 0) {
-            cur = nxt;
-            nxt = p[(k >> 2) + 1];   // prefetch; buffers carry >= 16 bytes of padding
-        }
-        return (int)((cur >> (8 * (k & 3))) & 0xFFu);
-    }
+    const uint8_t *p;
+    __device__ __forceinline__ explicit WindowReader(const uint8_t *base) : p(base) {}
+    __device__ __forceinline__ int operator()(int j) const { return (int)p[j - 1]; }
 };
 
 template <int RPL>
@@ -145,7 +138,8 @@ __device__ __forceinline__ void run_lane(const KParams &p, int a_local, int64_t 
         r = empty_result();
     } else {
         WindowReader rd(p.codes + p.win_off[w]);
-        if (KIND == FAST) r = pcabi::align_lane_fast<RPL, AFFINE>(rd, n, adp, L, p.sc);
+        if constexpr (KIND == PACKED) r = pcabi::align_lane_packed<(RPL <= 32 ? RPL : 32), AFFINE>(rd, n, adp, L, p.sc);
+        else if constexpr (KIND == FAST) r = pcabi::align_lane_fast<RPL, AFFINE>(rd, n, adp, L, p.sc);
         else r = pcabi::align_lane_generic<RPL, AFFINE>(rd, n, adp, L, p.sc);
     }
     store_result(p.out, p.out_stride, out_idx, r);
@@ -155,7 +149,7 @@ __device__ __forceinline__ void run_lane(const KParams &p, int a_local, int64_t 
 //  cross: grid (ceil(n_win/256), n_adp); lane = window, blockIdx.y = bucket-local adapter
 //  pairs: grid (ceil(n_waves/4)); wave = one adapter, lanes = host-grouped tasks
 template <int RPL, bool AFFINE, int KIND>
-__global__ __launch_bounds__(256) void k_align(KParams p) {
+__global__ __launch_bounds__(256, PCABI_WAVES) void k_align(KParams p) {
     if (p.task_win == nullptr) {
         const int a_local = blockIdx.y;
         const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -249,11 +243,17 @@ void launch(const KParams &p, bool affine, dim3 grid, hipStream_t st) {
     else hipLaunchKernelGGL((k_align<RPL, false, KIND>), grid, dim3(256), 0, st, p);
 }
 
-void dispatch(int b, const KParams &p, bool affine, hipStream_t st) {
+void dispatch(int b, const KParams &p, bool affine, hipStream_t st, bool packed) {
     dim3 grid = p.task_win ? dim3((unsigned)((p.n_waves + 3) / 4))
                            : dim3((unsigned)((p.n_win + 255) / 256), (unsigned)p.n_adp);
     const BucketDef d = kBuckets[b];
-    if (d.kind == FAST) {
+    if (d.kind == FAST && packed && d.rpl <= 32) {
+        switch (d.rpl) {
+#define C(R) case R: launch<R, PACKED>(p, affine, grid, st); break;
+        C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32)
+#undef C
+        }
+    } else if (d.kind == FAST) {
         switch (d.rpl) {
 #define C(R) case R: launch<R, FAST>(p, affine, grid, st); break;
         C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32) C(36) C(40) C(44) C(48) C(52) C(56) C(60) C(64)
@@ -268,6 +268,15 @@ void dispatch(int b, const KParams &p, bool affine, hipStream_t st) {
         case 128: launch<128, GENERIC>(p, affine, grid, st); break;
         }
     }
+}
+
+// Packed-key kernels serve a fast bucket when every adapter in it satisfies the range
+// conditions (pcabi_dp.h packed_ok) for the longest window of the launch.
+bool bucket_packed_ok(int b, const std::vector<int32_t> &lens, const pcabi::Scoring &sc, int64_t max_win) {
+    if (kBuckets[b].kind != FAST || kBuckets[b].rpl > 32 || max_win > pcabi::pk::MAX_WINDOW) return false;
+    for (int32_t L : lens)
+        if (!pcabi::packed_ok(L, kBuckets[b].rpl, (int)max_win, sc)) return false;
+    return true;
 }
 
 // Host-side layout of a bucket's adapter table.
@@ -298,6 +307,7 @@ void build_buckets(const uint8_t *adp_codes, const int32_t *adp_off, const int32
 struct pcabi_adapters {
     int32_t n_adp = 0;
     bool padded[kNumBuckets] = {};
+    std::vector<int32_t> lens[kNumBuckets];
     int32_t count[kNumBuckets] = {};
     uint32_t *pad[kNumBuckets] = {};
     int32_t *len[kNumBuckets] = {};
@@ -422,12 +432,14 @@ int pcabi_align_host(int device, const uint8_t *codes, int64_t codes_len, const 
     HIP_TRY(hipSetDevice(device));
 
     const pcabi::Scoring sc{match, mismatch, gap_open, gap_extend};
+    int64_t max_win = 0, max_win_tasks = 0;
     {
         int max_L = 0;
-        int64_t max_w = 0;
         for (int a = 0; a < n_adp; ++a) max_L = std::max(max_L, (int)adp_len[a]);
-        for (int64_t w = 0; w < n_win; ++w) max_w = std::max<int64_t>(max_w, win_len[w]);
-        if (int rc = check_span(sc, max_L, max_w)) return rc;
+        for (int64_t w = 0; w < n_win; ++w) max_win = std::max<int64_t>(max_win, win_len[w]);
+        if (int rc = check_span(sc, max_L, max_win)) return rc;
+        if (task_win)
+            for (int64_t t = 0; t < n_task; ++t) max_win_tasks = std::max<int64_t>(max_win_tasks, win_len[task_win[t]]);
     }
     BucketHost bk[kNumBuckets];
     build_buckets(adp_codes, adp_off, adp_len, n_adp, sc, bk);
@@ -478,7 +490,7 @@ int pcabi_align_host(int device, const uint8_t *codes, int64_t codes_len, const 
         p.n_adp = nb;
         if (!task_win) {
             p.task_win = nullptr;
-            if (n_win > 0) dispatch(b, p, affine, e.stream);
+            if (n_win > 0) dispatch(b, p, affine, e.stream, bucket_packed_ok(b, h.len, sc, max_win));
         } else {
             tw.clear(); to.clear(); wa.clear();
             for (int k = 0; k < nb; ++k) {
@@ -503,7 +515,7 @@ int pcabi_align_host(int device, const uint8_t *codes, int64_t codes_len, const 
             p.task_out = (const int32_t *)e.tasks_out.p;
             p.wave_adp = (const int32_t *)e.wave_adp.p;
             p.n_waves = (int64_t)wa.size();
-            dispatch(b, p, affine, e.stream);
+            dispatch(b, p, affine, e.stream, bucket_packed_ok(b, h.len, sc, max_win_tasks));
             // host vectors are reused by the next bucket: drain before overwriting
             HIP_TRY(hipStreamSynchronize(e.stream));
         }
@@ -608,6 +620,7 @@ int pcabi_adapters_create(const uint8_t *adp_codes, const int32_t *adp_off, cons
         const int nb = (int)bk[b].len.size();
         a->count[b] = nb;
         if (!nb) continue;
+        a->lens[b] = bk[b].len;
         for (int k = 0; k < nb; ++k)
             if (bk[b].len[k] != kBuckets[b].rpl) a->padded[b] = true;
         if (hipMalloc((void **)&a->pad[b], bk[b].pad.size()) != hipSuccess ||
@@ -635,8 +648,9 @@ void pcabi_adapters_destroy(pcabi_adapters *a) {
 }
 
 int pcabi_align_cross_dev(const uint8_t *codes, const int64_t *win_off, const int32_t *win_len,
-                          int64_t n_win, const pcabi_adapters *adps, int match, int mismatch,
-                          int gap_open, int gap_extend, int32_t *out, int64_t out_stride, void *stream) {
+                          int64_t n_win, int32_t max_win_len, const pcabi_adapters *adps, int match,
+                          int mismatch, int gap_open, int gap_extend, int32_t *out, int64_t out_stride,
+                          void *stream) {
     if (!adps || n_win < 0) return fail(PCABI_E_ARG, "bad arguments");
     if (n_win == 0) return 0;
     KParams p{};
@@ -658,7 +672,7 @@ int pcabi_align_cross_dev(const uint8_t *codes, const int64_t *win_off, const in
         p.adp_len = adps->len[b];
         p.adp_id = adps->id[b];
         p.n_adp = adps->count[b];
-        dispatch(b, p, affine, (hipStream_t)stream);
+        dispatch(b, p, affine, (hipStream_t)stream, bucket_packed_ok(b, adps->lens[b], p.sc, max_win_len));
     }
     HIP_TRY(hipGetLastError());
     return 0;

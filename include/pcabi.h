@@ -125,10 +125,12 @@ void pcabi_adapters_destroy(pcabi_adapters *a);
 
 /*
  * Cross-product alignment, every pointer a DEVICE pointer, asynchronous on `stream`:
- * result (a, w) -> out[f * out_stride + a * n_win + w].
+ * result (a, w) -> out[f * out_stride + a * n_win + w]. max_win_len (host value) bounds every
+ * win_len[w]: it selects the packed-key kernels (windows <= 223) and must be honest. Windows
+ * longer than 32k need negative gap costs.
  */
 int pcabi_align_cross_dev(const uint8_t *codes, const int64_t *win_off, const int32_t *win_len,
-                          int64_t n_win, const pcabi_adapters *adps,
+                          int64_t n_win, int32_t max_win_len, const pcabi_adapters *adps,
                           int match, int mismatch, int gap_open, int gap_extend,
                           int32_t *out, int64_t out_stride, void *stream);
 

@@ -35,10 +35,24 @@ extern "C" int pcabi_model_align(const char *read, int n, const char *adp, int L
 
 extern "C" double pcabi_model_pid6(int m, int l) { return pcabi::pid6(m, l); }
 
+struct HostReader {
+    const char *read;
+    int n;
+    uint32_t word(int k) const {
+        uint32_t w = 0;
+        for (int b = 0; b < 4; ++b) {
+            const int i = 4 * k + b;
+            const uint32_t c = i < n ? (uint32_t)dna5((unsigned char)read[i]) : 4u;
+            w |= c << (8 * b);
+        }
+        return w;
+    }
+};
+
 template <int RPL>
 static void run_fast(const char *read, int n, const char *adp, int L, pcabi::Scoring sc, int *out) {
     const int off = RPL - L;
-    auto rd = [&](int j) { return dna5((unsigned char)read[j - 1]); };
+    auto rd = [&](int j) { return j <= n ? dna5((unsigned char)read[j - 1]) : 4; };
     auto ad = [&](int s) { return s <= off ? pcabi::PAD_CODE : dna5((unsigned char)adp[s - off - 1]); };
     pcabi::Result r = (sc.go != sc.ge) ? pcabi::align_lane_fast<RPL, true>(rd, n, ad, L, sc)
                                        : pcabi::align_lane_fast<RPL, false>(rd, n, ad, L, sc);
@@ -57,6 +71,33 @@ extern "C" int pcabi_model_align_fast(const char *read, int n, const char *adp, 
 #define C(R) case R: run_fast<R>(read, n, adp, L, sc, out); break;
     C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32) C(36) C(40) C(44) C(48) C(52) C(56) C(60) C(64)
     C(68) C(72) C(76) C(80) C(84) C(88) C(92) C(96) C(100) C(104) C(108) C(112) C(116) C(120) C(124) C(128)
+#undef C
+    default: return -2;
+    }
+    return 0;
+}
+
+template <int RPL>
+static void run_packed(const char *read, int n, const char *adp, int L, pcabi::Scoring sc, int *out) {
+    const int off = RPL - L;
+    auto rd = [&](int j) { return j <= n ? dna5((unsigned char)read[j - 1]) : 4; };
+    auto ad = [&](int s) { return s <= off ? pcabi::PAD_CODE : dna5((unsigned char)adp[s - off - 1]); };
+    pcabi::Result r = (sc.go != sc.ge) ? pcabi::align_lane_packed<RPL, true>(rd, n, ad, L, sc)
+                                       : pcabi::align_lane_packed<RPL, false>(rd, n, ad, L, sc);
+    out[0] = r.rs; out[1] = r.re; out[2] = r.as; out[3] = r.ae;
+    out[4] = r.score; out[5] = r.m; out[6] = r.l1; out[7] = r.l2;
+}
+
+// packed-key core (end windows); -3 if the range preconditions fail
+extern "C" int pcabi_model_align_packed(const char *read, int n, const char *adp, int L,
+                                        int ma, int mi, int go, int ge, int *out) {
+    pcabi::Scoring sc{ma, mi, go, ge};
+    if (L <= 0 || n <= 0) return -1;
+    const int rpl = (L + 3) & ~3;
+    if (!pcabi::packed_ok(L, rpl, n, sc)) return -3;
+    switch (rpl) {
+#define C(R) case R: run_packed<R>(read, n, adp, L, sc, out); break;
+    C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32)
 #undef C
     default: return -2;
     }
