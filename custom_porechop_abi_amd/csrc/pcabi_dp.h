@@ -32,6 +32,10 @@
 #ifndef PCABI_ROW_FENCE
 #define PCABI_ROW_FENCE 1
 #endif
+// Packed core: substitution-key quads fetched this many quads ahead (0 = one read per slot).
+#ifndef PCABI_TAB_PD
+#define PCABI_TAB_PD 1
+#endif
 
 
 
@@ -629,41 +633,52 @@ PCABI_HD bool packed_ok(int L, int rpl, int max_window, const Scoring &s) {
 
 template <int RPL, bool AFFINE>
 struct LanePacked {
-    int32_t SK[RPL + 1];   // S keys, tb = 0
+    int32_t G[RPL + 1];    // S keys with tb cleared, plus the gap-open key: G = S + go
     int32_t HK[RPL + 1];   // H keys, tb = 1 (affine only)
     int bscore, bi, bj, blt, btrail, bprec;
     uint32_t battr;        // packed attribute
     int slt_last, ht_last, hp_last;
-    int32_t k_match, k_mis[4], k_ge, k_go, k_gev, k_geh, neg2;
+    int32_t k_ge, k_go, k_gev, k_geh, neg2;
 
-    template <typename AdpFn, bool LAST>
-    PCABI_HD void column(const int r, const int j, const AdpFn &adp, const int L, const int off) {
-        int32_t sup = pk::start(j);                // S(0, j): score 0, tb 0
+    // tab: substitution-key table of this lane's read code, tab(s) = key increment of the
+    // diagonal step into slot s (match / mismatch / padding), see pk::fill_sub_table.
+    template <typename TabRow, bool LAST>
+    PCABI_HD void column(const TabRow &tab, const int j, const int L, const int off) {
+        int32_t gup = pk::start(j) + k_go;         // G(0, j): S(0, j) = score 0, tb 0
         int32_t vup = neg2;                        // V(0, j) = NEG, tb 2
         int slt_up = LT_NONE, vt_up = 0, vp_up = 0;
         int32_t lv = 0, lh = 0, ls = 0;
         int lslt = LT_D;
         bool lhext = false;
-        int32_t diag = pk::start(j - 1) + ((r == adp(1)) ? k_match : k_mis[1]);
+        // Substitution keys of this column, fetched a quad (4 slots) at a time, PCABI_TAB_PD
+        // quads ahead of use so the LDS latency hides behind the rows in flight.
+        constexpr int NQ = RPL / 4;
+        int32_t t[RPL + 2];
+        if (PCABI_TAB_PD > 0) {
+#pragma unroll
+            for (int q = 0; q <= PCABI_TAB_PD && q < NQ; ++q) tab.quad(q, t + 4 * q + 1);
+        }
+        int32_t diag = (pk::start(j - 1) + k_go) + (PCABI_TAB_PD > 0 ? t[1] : tab(1));
 #pragma unroll
         for (int s = 1; s <= RPL; ++s) {
-            int32_t diag_nx = 0;
-            if (s < RPL) {
-                const int32_t kmis = (s + 1 <= 3) ? k_mis[s + 1] : k_mis[0];
-                diag_nx = SK[s] + ((r == adp(s + 1)) ? k_match : kmis);
+            if (PCABI_TAB_PD > 0 && (s & 3) == 1) {
+                const int q = (s - 1) / 4 + PCABI_TAB_PD + 1;
+                if (q < NQ) tab.quad(q, t + 4 * q + 1);
             }
+            int32_t diag_nx = 0;
+            if (s < RPL) diag_nx = G[s] + (PCABI_TAB_PD > 0 ? t[s + 1] : tab(s + 1));
             int32_t hn, vn2, sn;
             bool hext = false, vext = false;
             if (AFFINE) {
-                const int32_t hx = HK[s] + k_ge, ho = SK[s] + k_go;
+                const int32_t hx = HK[s] + k_ge, ho = G[s];
                 hn = hx > ho ? hx : ho;                  // tb 1 iff extend
-                const int32_t vx = vup + k_ge, vo = sup + k_go;
+                const int32_t vx = vup + k_ge, vo = gup;
                 const int32_t vn = vx > vo ? vx : vo;    // tb 2 iff extend
                 vn2 = vn | pk::TB2;
                 if (LAST || s == RPL) { hext = pk::tb(hn) == 1; vext = pk::tb(vn) == 2; }
             } else {
-                vn2 = sup + k_gev;                       // tb 2
-                hn = SK[s] + k_geh;                      // tb 1
+                vn2 = gup + k_gev;                       // tb 2
+                hn = G[s] + k_geh;                       // tb 1
             }
             sn = max3i(diag, vn2, hn);
             const int t = pk::tb(sn);
@@ -704,9 +719,9 @@ struct LanePacked {
                     vp_up = vp;
                 }
             }
-            SK[s] = sn & ~pk::TBM;
+            G[s] = (sn & ~pk::TBM) + k_go;
             if (AFFINE) HK[s] = hn | pk::TB1;
-            sup = SK[s];
+            gup = G[s];
             vup = vn2;
             diag = diag_nx;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -746,25 +761,39 @@ struct LanePacked {
     }
 };
 
-template <int RPL, bool AFFINE, typename ReadFn, typename AdpFn>
-PCABI_HD Result align_lane_packed(ReadFn &rd, int n, const AdpFn &adp, int L, const Scoring sc) {
+// Substitution-key table: row c (read code 0..7) holds, for slots s = 1..RPL at index s - 1, the
+// key increment of a diagonal step into slot s: match / mismatch keys, or the pass-through
+// padding key for slots <= off. Rows are RPL int32 long (RPL % 4 == 0) so a quad of slots is one
+// 16-byte LDS read.
+// One table per adapter (wave-uniform); kernels keep it in LDS so the per-cell substitution is
+// one LDS read + one add instead of a compare + select.
+namespace pk {
+constexpr int TAB_W = 8;
+template <typename AdpFn>
+PCABI_HD int32_t sub_key(int s, int c, const AdpFn &adp, int off, const Scoring &sc) {
+    // the core adds these to G = S + go, so the gap-open key is taken back out here
+    if (s <= off) return TB3 + INC_PAD - pk::sc(sc.go);
+    return (c == adp(s)) ? (pk::sc(sc.ma) + TB3 + INC_M - pk::sc(sc.go))
+                         : (pk::sc(sc.mi) + TB3 + INC_D - pk::sc(sc.go));
+}
+}  // namespace pk
+
+template <int RPL, bool AFFINE, typename ReadFn, typename TabFn>
+PCABI_HD Result align_lane_packed(ReadFn &rd, int n, const TabFn &tabfn, int L, const Scoring sc) {
+    // tabfn(r) returns a callable row(s) -> substitution key for read code r
     LanePacked<RPL, AFFINE> st;
     const int off = RPL - L;
     const int32_t neg = pk::sc(pk::neg_score(RPL, sc));
-#pragma unroll
-    for (int s = 1; s <= RPL; ++s) {
-        st.SK[s] = pk::start(-(s > off ? s - off : 0));
-        st.HK[s] = neg | pk::TB1;
-    }
-    st.k_match = pk::sc(sc.ma) + pk::TB3 + pk::INC_M;
-    st.k_mis[0] = pk::sc(sc.mi) + pk::TB3 + pk::INC_D;
-#pragma unroll
-    for (int s = 1; s <= 3; ++s)
-        st.k_mis[s] = (s <= off) ? (pk::TB3 + pk::INC_PAD) : st.k_mis[0];
     st.k_ge = pk::sc(sc.ge);
     st.k_go = pk::sc(sc.go);
-    st.k_gev = pk::sc(sc.ge) + pk::TB2;
-    st.k_geh = pk::sc(sc.ge) + pk::TB1;
+    // linear gaps: V / H straight from G (= S + go), so the constants take go back out
+    st.k_gev = pk::sc(sc.ge) - pk::sc(sc.go) + pk::TB2;
+    st.k_geh = pk::sc(sc.ge) - pk::sc(sc.go) + pk::TB1;
+#pragma unroll
+    for (int s = 1; s <= RPL; ++s) {
+        st.G[s] = pk::start(-(s > off ? s - off : 0)) + st.k_go;
+        st.HK[s] = neg | pk::TB1;
+    }
     st.neg2 = neg | pk::TB2;
     st.bscore = 0;
     st.bi = L;
@@ -780,10 +809,10 @@ PCABI_HD Result align_lane_packed(ReadFn &rd, int n, const AdpFn &adp, int L, co
 #pragma unroll 1
     for (int j = 1; j < n; ++j) {
         const int rn = rd(j + 1);
-        st.template column<AdpFn, false>(r, j, adp, L, off);
+        st.template column<decltype(tabfn(r)), false>(tabfn(r), j, L, off);
         r = rn;
     }
-    st.template column<AdpFn, true>(r, n, adp, L, off);
+    st.template column<decltype(tabfn(r)), true>(tabfn(r), n, L, off);
     Best b;
     b.score = st.bscore; b.bi = st.bi; b.bj = st.bj; b.attr = pk::to_std(st.battr);
     b.ltype = st.blt; b.trail = st.btrail; b.precd = st.bprec;

@@ -89,11 +89,41 @@ struct KParams {
 
 // Window codes, one byte per column (buffers carry >= 16 bytes of padding past every window,
 // so the one-column-ahead read of the last column stays in bounds).
+#ifndef PCABI_RD_MODE
+#define PCABI_RD_MODE 1
+#endif
+#if PCABI_RD_MODE == 0
 struct WindowReader {
     const uint8_t *p;
-    __device__ __forceinline__ explicit WindowReader(const uint8_t *base) : p(base) {}
-    __device__ __forceinline__ int operator()(int j) const { return (int)p[j - 1]; }
+    __device__ __forceinline__ explicit WindowReader(const uint8_t *base, int) : p(base) {}
+    __device__ __forceinline__ int operator()(int j) { return (int)p[j - 1]; }
 };
+#elif PCABI_RD_MODE == 1
+// Aligned-dword stream: one dword load per lane every 4 columns (a wave-uniform branch, j is the
+// same in every lane), fetched one chunk ahead; reads at most 12 bytes past the window end.
+struct WindowReader {
+    const uint32_t *q;   // aligned dword holding byte 0
+    int a8;              // 8 * misalignment
+    uint32_t lo, hi, nx;
+    __device__ __forceinline__ explicit WindowReader(const uint8_t *base, int) {
+        const int a0 = (int)((uintptr_t)base & 3);
+        a8 = 8 * a0;
+        q = reinterpret_cast<const uint32_t *>(base - a0);   // keeps the global address space
+        lo = q[0]; hi = q[1]; nx = q[2];
+    }
+    __device__ __forceinline__ int operator()(int j) {   // called with j = 1, 2, 3, ... in order
+        const int k = j - 1;
+        if (k > 0 && (k & 3) == 0) { lo = hi; hi = nx; nx = q[k / 4 + 2]; }
+        return (int)(((((uint64_t)hi << 32) | lo) >> (8 * (k & 3) + a8)) & 0xFFu);
+    }
+};
+#else
+struct WindowReader {   // timing experiment only: no window loads (results are wrong)
+    uint32_t v;
+    __device__ __forceinline__ explicit WindowReader(const uint8_t *base, int) : v((uint32_t)(uintptr_t)base) {}
+    __device__ __forceinline__ int operator()(int j) { return (int)((v >> (j & 15)) & 3); }
+};
+#endif
 
 template <int RPL>
 struct AdapterRegs {
@@ -126,21 +156,51 @@ __device__ __forceinline__ pcabi::Result empty_result() {
     return r;
 }
 
+// Packed-core substitution table in LDS: one (RPL+2) x 8 int32 table per wave (its adapter).
+constexpr int kTabW = pcabi::pk::TAB_W;
+
+struct LdsRow {
+    const int32_t *p;   // &tab[wave][c][0]: slot s at p[s - 1], 16-byte aligned
+    __device__ __forceinline__ int32_t operator()(int s) const { return p[s - 1]; }
+    __device__ __forceinline__ void quad(int q, int32_t *dst) const {
+        const int4 v = *reinterpret_cast<const int4 *>(p + 4 * q);
+        dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
+    }
+};
+
 template <int RPL, bool AFFINE, int KIND>
-__device__ __forceinline__ void run_lane(const KParams &p, int a_local, int64_t w, int64_t out_idx) {
+__device__ __forceinline__ void run_lane(const KParams &p, int a_local, int64_t w, int64_t out_idx,
+                                         int32_t *wave_tab) {
     AdapterRegs<RPL> adp;
     adp.load(p.adp_pad + (int64_t)a_local * (RPL / 4));
     const int L = __builtin_amdgcn_readfirstlane(p.adp_len[a_local]);
+    if constexpr (KIND == PACKED) {
+        // fill this wave's table (every lane of the block reaches the barrier)
+        const int off = RPL - L;
+        const int lane = threadIdx.x & 63;
+        for (int e = lane; e < kTabW * RPL; e += 64) {
+            const int c = e / RPL, srow = e % RPL + 1;
+            const uint32_t *ap = p.adp_pad + (int64_t)a_local * (RPL / 4);
+            auto code = [&](int sl) { return (int)((ap[(sl - 1) / 4] >> (8 * ((sl - 1) & 3))) & 0xFFu); };
+            wave_tab[e] = pcabi::pk::sub_key(srow, c, code, off, p.sc);
+        }
+        __syncthreads();
+    }
     if (w < 0) return;
     const int n = p.win_len[w];
     pcabi::Result r;
     if (n <= 0) {
         r = empty_result();
     } else {
-        WindowReader rd(p.codes + p.win_off[w]);
-        if constexpr (KIND == PACKED) r = pcabi::align_lane_packed<(RPL <= 32 ? RPL : 32), AFFINE>(rd, n, adp, L, p.sc);
-        else if constexpr (KIND == FAST) r = pcabi::align_lane_fast<RPL, AFFINE>(rd, n, adp, L, p.sc);
-        else r = pcabi::align_lane_generic<RPL, AFFINE>(rd, n, adp, L, p.sc);
+        WindowReader rd(p.codes + p.win_off[w], n);
+        if constexpr (KIND == PACKED) {
+            auto tabfn = [&](int rc) { return LdsRow{wave_tab + rc * RPL}; };
+            r = pcabi::align_lane_packed<(RPL <= 32 ? RPL : 32), AFFINE>(rd, n, tabfn, L, p.sc);
+        } else if constexpr (KIND == FAST) {
+            r = pcabi::align_lane_fast<RPL, AFFINE>(rd, n, adp, L, p.sc);
+        } else {
+            r = pcabi::align_lane_generic<RPL, AFFINE>(rd, n, adp, L, p.sc);
+        }
     }
     store_result(p.out, p.out_stride, out_idx, r);
 }
@@ -150,18 +210,21 @@ __device__ __forceinline__ void run_lane(const KParams &p, int a_local, int64_t 
 //  pairs: grid (ceil(n_waves/4)); wave = one adapter, lanes = host-grouped tasks
 template <int RPL, bool AFFINE, int KIND>
 __global__ __launch_bounds__(256, PCABI_WAVES) void k_align(KParams p) {
+    __shared__ __attribute__((aligned(16))) int32_t tab[KIND == PACKED ? 4 * kTabW * RPL : 4];
+    int32_t *wave_tab = tab + (KIND == PACKED ? (threadIdx.x >> 6) * kTabW * RPL : 0);
     if (p.task_win == nullptr) {
         const int a_local = blockIdx.y;
         const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
         const int a_glob = p.adp_id[a_local];
-        run_lane<RPL, AFFINE, KIND>(p, a_local, w < p.n_win ? w : -1, (int64_t)a_glob * p.n_win + w);
+        run_lane<RPL, AFFINE, KIND>(p, a_local, w < p.n_win ? w : -1, (int64_t)a_glob * p.n_win + w, wave_tab);
     } else {
-        const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-        if (wave >= p.n_waves) return;
+        int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+        const bool live = wave < p.n_waves;            // dead waves still join the table barrier
+        if (!live) wave = p.n_waves - 1;
         const int64_t slot = wave * 64 + (threadIdx.x & 63);
         const int a_local = __builtin_amdgcn_readfirstlane(p.wave_adp[wave]);
-        const int32_t tw = p.task_win[slot];
-        run_lane<RPL, AFFINE, KIND>(p, a_local, tw, tw >= 0 ? p.task_out[slot] : 0);
+        const int32_t tw = live ? p.task_win[slot] : -1;
+        run_lane<RPL, AFFINE, KIND>(p, a_local, tw, tw >= 0 ? p.task_out[slot] : 0, wave_tab);
     }
 }
 

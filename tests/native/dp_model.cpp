@@ -82,8 +82,18 @@ static void run_packed(const char *read, int n, const char *adp, int L, pcabi::S
     const int off = RPL - L;
     auto rd = [&](int j) { return j <= n ? dna5((unsigned char)read[j - 1]) : 4; };
     auto ad = [&](int s) { return s <= off ? pcabi::PAD_CODE : dna5((unsigned char)adp[s - off - 1]); };
-    pcabi::Result r = (sc.go != sc.ge) ? pcabi::align_lane_packed<RPL, true>(rd, n, ad, L, sc)
-                                       : pcabi::align_lane_packed<RPL, false>(rd, n, ad, L, sc);
+    // c-major table, the layout the kernels keep in LDS: tab[c * RPL + s - 1]
+    int32_t tab[pcabi::pk::TAB_W * RPL];
+    for (int c = 0; c < pcabi::pk::TAB_W; ++c)
+        for (int s = 1; s <= RPL; ++s) tab[c * RPL + s - 1] = pcabi::pk::sub_key(s, c, ad, off, sc);
+    struct Row {
+        const int32_t *p;
+        int32_t operator()(int s) const { return p[s - 1]; }
+        void quad(int q, int32_t *dst) const { for (int k = 0; k < 4; ++k) dst[k] = p[4 * q + k]; }
+    };
+    auto tabfn = [&](int rc) { return Row{tab + rc * RPL}; };
+    pcabi::Result r = (sc.go != sc.ge) ? pcabi::align_lane_packed<RPL, true>(rd, n, tabfn, L, sc)
+                                       : pcabi::align_lane_packed<RPL, false>(rd, n, tabfn, L, sc);
     out[0] = r.rs; out[1] = r.re; out[2] = r.as; out[3] = r.ae;
     out[4] = r.score; out[5] = r.m; out[6] = r.l1; out[7] = r.l2;
 }
