@@ -593,25 +593,30 @@ namespace pcabi {
 // and 2 (affine) / 1 (linear) registers per adapter row -- versus 21 ops and 4 registers when
 // scores and attributes live in separate registers (align_lane_fast).
 //
+// The start diagonal c is kept mod 256: nothing but the start keys ever writes the c field
+// (padding rows add 0 to it -- the row-0 keys already carry the c of the real cell the padded
+// path reaches), so it never carries into tb, and finish() recovers c from the end column
+// because the best path spans < 256 columns (packed_ok). Windows of any length are accepted.
+//
 // Range conditions (checked by the host, packed_ok): every reachable score and the NEG
-// sentinel fit the 10-bit field, c + 32 fits 8 bits (window <= 223), m, nD <= 32 fit 6 bits.
+// sentinel fit the 10-bit field, m, nD <= L <= 63 fit 6 bits, span bound <= 255.
 // ==========================================================================================
 namespace pk {
 constexpr int M_SH = 0, D_SH = 6, C_SH = 12, TB_SH = 20, SC_SH = 22;
-constexpr int CB = 32;                          // c bias: c >= -L >= -32
 constexpr int32_t TB1 = 1 << TB_SH, TB2 = 2 << TB_SH, TB3 = 3 << TB_SH, TBM = 3 << TB_SH;
-constexpr int32_t INC_D = 1 << D_SH, INC_M = (1 << D_SH) + 1, INC_PAD = 1 << C_SH;
-constexpr int MAX_WINDOW = 255 - CB;            // 223
-constexpr int MAX_RPL = 32;
+constexpr int32_t INC_D = 1 << D_SH, INC_M = (1 << D_SH) + 1;
+constexpr int MAX_RPL = 64;
+constexpr int MAX_L = 63;                       // m, nD fit 6 bits
 PCABI_HD int32_t sc(int v) { return (int32_t)((uint32_t)v << SC_SH); }   // score -> key units
-PCABI_HD int32_t start(int c) { return (int32_t)((uint32_t)(c + CB) << C_SH); }
+PCABI_HD int32_t start(int c) { return (int32_t)(((uint32_t)c & 255u) << C_SH); }   // c mod 256
 PCABI_HD int score(int32_t k) { return k >> SC_SH; }
 PCABI_HD int tb(int32_t k) { return (k >> TB_SH) & 3; }
 PCABI_HD uint32_t attr(int32_t k) { return (uint32_t)k & ((1u << TB_SH) - 1u); }
-// packed attribute -> standard attribute word (finish())
-PCABI_HD uint32_t to_std(uint32_t a) {
+// packed attribute of a path ending in column bj -> standard attribute word (finish()):
+// c in [bj - 255, bj] is recovered from its residue mod 256
+PCABI_HD uint32_t to_std(uint32_t a, int bj) {
     const uint32_t m = a & 63u, nd = (a >> D_SH) & 63u;
-    const int c = (int)((a >> C_SH) & 255u) - CB;
+    const int c = bj - (int)(((uint32_t)bj - (a >> C_SH)) & 255u);
     return attr_start(c) | (nd << ATTR_B) | m;
 }
 PCABI_HD int neg_score(int L, const Scoring &s) {
@@ -622,9 +627,17 @@ PCABI_HD int neg_score(int L, const Scoring &s) {
 }
 }  // namespace pk
 
-PCABI_HD bool packed_ok(int L, int rpl, int max_window, const Scoring &s) {
-    if (rpl > pk::MAX_RPL || max_window > pk::MAX_WINDOW) return false;
+// Columns spanned by the reported path: it scores >= 0 (the scout is seeded with 0), so its
+// horizontal moves (each costing >= g) are paid for by at most L diagonal matches.
+PCABI_HD int packed_span_bound(int L, const Scoring &s) {
+    const int g = (-s.go < -s.ge) ? -s.go : -s.ge;
+    return L + (s.ma > 0 ? (s.ma * L) / g : 0);
+}
+
+PCABI_HD bool packed_ok(int L, int rpl, const Scoring &s) {
+    if (rpl > pk::MAX_RPL || L > pk::MAX_L) return false;
     if (!fast_ok(L, rpl, s)) return false;
+    if (packed_span_bound(L, s) > 255) return false;
     const int hi = (rpl * s.ma > 0 ? rpl * s.ma : 0);
     const int gm = (-s.go > -s.ge ? -s.go : -s.ge);
     const int neg = pk::neg_score(rpl, s) - (gm > 0 ? gm : 0);
@@ -644,7 +657,7 @@ struct LanePacked {
     // diagonal step into slot s (match / mismatch / padding), see pk::fill_sub_table.
     template <typename TabRow, bool LAST>
     PCABI_HD void column(const TabRow &tab, const int j, const int L, const int off) {
-        int32_t gup = pk::start(j) + k_go;         // G(0, j): S(0, j) = score 0, tb 0
+        int32_t gup = pk::start(j + off) + k_go;   // G(0, j): S(0, j) = score 0, tb 0
         int32_t vup = neg2;                        // V(0, j) = NEG, tb 2
         int slt_up = LT_NONE, vt_up = 0, vp_up = 0;
         int32_t lv = 0, lh = 0, ls = 0;
@@ -658,7 +671,7 @@ struct LanePacked {
 #pragma unroll
             for (int q = 0; q <= PCABI_TAB_PD && q < NQ; ++q) tab.quad(q, t + 4 * q + 1);
         }
-        int32_t diag = (pk::start(j - 1) + k_go) + (PCABI_TAB_PD > 0 ? t[1] : tab(1));
+        int32_t diag = (pk::start(j - 1 + off) + k_go) + (PCABI_TAB_PD > 0 ? t[1] : tab(1));
 #pragma unroll
         for (int s = 1; s <= RPL; ++s) {
             if (PCABI_TAB_PD > 0 && (s & 3) == 1) {
@@ -772,7 +785,7 @@ constexpr int TAB_W = 8;
 template <typename AdpFn>
 PCABI_HD int32_t sub_key(int s, int c, const AdpFn &adp, int off, const Scoring &sc) {
     // the core adds these to G = S + go, so the gap-open key is taken back out here
-    if (s <= off) return TB3 + INC_PAD - pk::sc(sc.go);
+    if (s <= off) return TB3 - pk::sc(sc.go);
     return (c == adp(s)) ? (pk::sc(sc.ma) + TB3 + INC_M - pk::sc(sc.go))
                          : (pk::sc(sc.mi) + TB3 + INC_D - pk::sc(sc.go));
 }
@@ -791,7 +804,7 @@ PCABI_HD Result align_lane_packed(ReadFn &rd, int n, const TabFn &tabfn, int L, 
     st.k_geh = pk::sc(sc.ge) - pk::sc(sc.go) + pk::TB1;
 #pragma unroll
     for (int s = 1; s <= RPL; ++s) {
-        st.G[s] = pk::start(-(s > off ? s - off : 0)) + st.k_go;
+        st.G[s] = pk::start(off - s) + st.k_go;    // padded (s, 0) reaches real (0, off - s)
         st.HK[s] = neg | pk::TB1;
     }
     st.neg2 = neg | pk::TB2;
@@ -814,7 +827,7 @@ PCABI_HD Result align_lane_packed(ReadFn &rd, int n, const TabFn &tabfn, int L, 
     }
     st.template column<decltype(tabfn(r)), true>(tabfn(r), n, L, off);
     Best b;
-    b.score = st.bscore; b.bi = st.bi; b.bj = st.bj; b.attr = pk::to_std(st.battr);
+    b.score = st.bscore; b.bi = st.bi; b.bj = st.bj; b.attr = pk::to_std(st.battr, st.bj);
     b.ltype = st.blt; b.trail = st.btrail; b.precd = st.bprec;
     return finish(b, L, n);
 }

@@ -195,7 +195,7 @@ __device__ __forceinline__ void run_lane(const KParams &p, int a_local, int64_t 
         WindowReader rd(p.codes + p.win_off[w], n);
         if constexpr (KIND == PACKED) {
             auto tabfn = [&](int rc) { return LdsRow{wave_tab + rc * RPL}; };
-            r = pcabi::align_lane_packed<(RPL <= 32 ? RPL : 32), AFFINE>(rd, n, tabfn, L, p.sc);
+            r = pcabi::align_lane_packed<(RPL <= 64 ? RPL : 64), AFFINE>(rd, n, tabfn, L, p.sc);
         } else if constexpr (KIND == FAST) {
             r = pcabi::align_lane_fast<RPL, AFFINE>(rd, n, adp, L, p.sc);
         } else {
@@ -310,10 +310,10 @@ void dispatch(int b, const KParams &p, bool affine, hipStream_t st, bool packed)
     dim3 grid = p.task_win ? dim3((unsigned)((p.n_waves + 3) / 4))
                            : dim3((unsigned)((p.n_win + 255) / 256), (unsigned)p.n_adp);
     const BucketDef d = kBuckets[b];
-    if (d.kind == FAST && packed && d.rpl <= 32) {
+    if (d.kind == FAST && packed) {
         switch (d.rpl) {
 #define C(R) case R: launch<R, PACKED>(p, affine, grid, st); break;
-        C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32)
+        C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32) C(36) C(40) C(44) C(48) C(52) C(56) C(60) C(64)
 #undef C
         }
     } else if (d.kind == FAST) {
@@ -334,11 +334,11 @@ void dispatch(int b, const KParams &p, bool affine, hipStream_t st, bool packed)
 }
 
 // Packed-key kernels serve a fast bucket when every adapter in it satisfies the range
-// conditions (pcabi_dp.h packed_ok) for the longest window of the launch.
-bool bucket_packed_ok(int b, const std::vector<int32_t> &lens, const pcabi::Scoring &sc, int64_t max_win) {
-    if (kBuckets[b].kind != FAST || kBuckets[b].rpl > 32 || max_win > pcabi::pk::MAX_WINDOW) return false;
+// conditions of pcabi_dp.h packed_ok (any window length).
+bool bucket_packed_ok(int b, const std::vector<int32_t> &lens, const pcabi::Scoring &sc) {
+    if (kBuckets[b].kind != FAST || kBuckets[b].rpl > pcabi::pk::MAX_RPL) return false;
     for (int32_t L : lens)
-        if (!pcabi::packed_ok(L, kBuckets[b].rpl, (int)max_win, sc)) return false;
+        if (!pcabi::packed_ok(L, kBuckets[b].rpl, sc)) return false;
     return true;
 }
 
@@ -495,14 +495,12 @@ int pcabi_align_host(int device, const uint8_t *codes, int64_t codes_len, const 
     HIP_TRY(hipSetDevice(device));
 
     const pcabi::Scoring sc{match, mismatch, gap_open, gap_extend};
-    int64_t max_win = 0, max_win_tasks = 0;
+    int64_t max_win = 0;
     {
         int max_L = 0;
         for (int a = 0; a < n_adp; ++a) max_L = std::max(max_L, (int)adp_len[a]);
         for (int64_t w = 0; w < n_win; ++w) max_win = std::max<int64_t>(max_win, win_len[w]);
         if (int rc = check_span(sc, max_L, max_win)) return rc;
-        if (task_win)
-            for (int64_t t = 0; t < n_task; ++t) max_win_tasks = std::max<int64_t>(max_win_tasks, win_len[task_win[t]]);
     }
     BucketHost bk[kNumBuckets];
     build_buckets(adp_codes, adp_off, adp_len, n_adp, sc, bk);
@@ -553,7 +551,7 @@ int pcabi_align_host(int device, const uint8_t *codes, int64_t codes_len, const 
         p.n_adp = nb;
         if (!task_win) {
             p.task_win = nullptr;
-            if (n_win > 0) dispatch(b, p, affine, e.stream, bucket_packed_ok(b, h.len, sc, max_win));
+            if (n_win > 0) dispatch(b, p, affine, e.stream, bucket_packed_ok(b, h.len, sc));
         } else {
             tw.clear(); to.clear(); wa.clear();
             for (int k = 0; k < nb; ++k) {
@@ -578,7 +576,7 @@ int pcabi_align_host(int device, const uint8_t *codes, int64_t codes_len, const 
             p.task_out = (const int32_t *)e.tasks_out.p;
             p.wave_adp = (const int32_t *)e.wave_adp.p;
             p.n_waves = (int64_t)wa.size();
-            dispatch(b, p, affine, e.stream, bucket_packed_ok(b, h.len, sc, max_win_tasks));
+            dispatch(b, p, affine, e.stream, bucket_packed_ok(b, h.len, sc));
             // host vectors are reused by the next bucket: drain before overwriting
             HIP_TRY(hipStreamSynchronize(e.stream));
         }
@@ -735,7 +733,7 @@ int pcabi_align_cross_dev(const uint8_t *codes, const int64_t *win_off, const in
         p.adp_len = adps->len[b];
         p.adp_id = adps->id[b];
         p.n_adp = adps->count[b];
-        dispatch(b, p, affine, (hipStream_t)stream, bucket_packed_ok(b, adps->lens[b], p.sc, max_win_len));
+        dispatch(b, p, affine, (hipStream_t)stream, bucket_packed_ok(b, adps->lens[b], p.sc));
     }
     HIP_TRY(hipGetLastError());
     return 0;

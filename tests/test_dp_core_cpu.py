@@ -86,8 +86,48 @@ def test_core_long_reads_wrapped_start_column(model):
         r[p:p + 24] = list(a)
         r = ''.join(r)
         for sc in [(3, -6, -5, -2), (2, -1, -1, -1)]:
-            rc, res = _run(model, 'pcabi_model_align_fast', r, a, sc)
-            assert rc == 0 and res == oracle_lib.align(r, a, sc)
+            exp = oracle_lib.align(r, a, sc)
+            for fn in ('pcabi_model_align_fast', 'pcabi_model_align_packed'):
+                rc, res = _run(model, fn, r, a, sc)
+                assert rc == 0 and res == exp, fn
+
+
+def _mutate(rng, s, rate):
+    o = []
+    for c in s:
+        x = rng.random()
+        if x < rate / 3:
+            o.append(rng.choice('ACGT'))
+        elif x < 2 * rate / 3:
+            pass
+        elif x < rate:
+            o.append(c + rng.choice('ACGT'))
+        else:
+            o.append(c)
+    return ''.join(o)
+
+
+def test_packed_core_whole_reads(model):
+    """Packed core on whole reads (the middle-adapter scan shape): the start diagonal is kept
+    mod 256, so hits far into the read, gapped hits and adapters of 33..63 bp are the cases."""
+    rng = random.Random(5)
+    schemes = [(3, -6, -5, -2), (2, -1, -1, -1), (1, -1, -3, -1), (3, -6, -2, -5)]
+    n_checked = 0
+    for k in range(160):
+        sc = schemes[k % len(schemes)]
+        L = rng.choice([8, 22, 24, 31, 40, 52, 63])
+        a = ''.join(rng.choice('ACGT') for _ in range(L))
+        n = rng.randint(300, 2500)
+        r = ''.join(rng.choice('ACGT') for _ in range(n))
+        for _ in range(rng.randint(0, 3)):
+            p = rng.randint(0, len(r))
+            r = r[:p] + _mutate(rng, a, rng.choice([0.0, 0.05, 0.2])) + r[p:]
+        rc, res = _run(model, 'pcabi_model_align_packed', r, a, sc)
+        if rc == -3:
+            continue
+        assert rc == 0 and res == oracle_lib.align(r, a, sc), (sc, L, len(r))
+        n_checked += 1
+    assert n_checked > 100
 
 
 def test_pid6_matches_text_round_trip(model):
