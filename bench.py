@@ -2,8 +2,10 @@
 """Headline benchmark: reads/s trimmed, 100k synthetic ONT reads x 50 adapter sets (BASELINE.json).
 
 One *step* = the end-trim hot path for one batch of reads, inputs resident in HBM:
-    start windows (seq[:150]) x start adapters  -> k_align_cross   (nanopore_read.py:175-195)
-    end windows   (seq[-150:]) x end adapters   -> k_align_cross   (nanopore_read.py:197-217)
+    start windows (seq[:150]) -> tile layout    -> k_tile_windows
+    start windows x start adapters              -> k_align (cross)  (nanopore_read.py:175-195)
+    end windows (seq[-150:]) -> tile layout     -> k_tile_windows
+    end windows x end adapters                  -> k_align (cross)  (nanopore_read.py:197-217)
     per-read trim decisions                     -> k_end_trim
 for the first 50 non-"full sequence" adapter sets of the reference database
 (porechop_abi/adapters.py:77-), scoring 3,-6,-5,-2, end_size 150, end_threshold 75,
@@ -13,9 +15,11 @@ Multi-GPU: one process per GPU (torch.distributed.run); each rank trims its own 
 (weak scaling, no data-path collective); the step time is the max over ranks (RCCL all-reduce
 MAX of the rank times). value = reads all ranks trimmed / that time.
 
-Also reported: roofline of the dominant kernel (k_align_cross, VALU-bound: integer cell updates,
-DESIGN.md §5), an HBM figure, and the reference SeqAn CPU path (oracle/_ref, compiled from the
-reference sources) timed on a bounded sample on this host's cores.
+Also reported: roofline of the dominant kernel (k_align<24, true, PACKED>: the 21-24 bp adapters,
+~80% of the step; VALU-bound integer cell updates) from HIP events around its
+launches, its HBM traffic from the committed rocprofv3 PMC pass (profiles/traffic.json), and the
+reference SeqAn CPU path (oracle/_ref, compiled from the reference sources) timed on a bounded
+sample on this host's cores.
 """
 import argparse
 import ctypes
@@ -32,6 +36,7 @@ sys.path.insert(0, ROOT)
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # int32 lane-ops/s: 256 CU x 4 SIMD32 x 2.4 GHz
 HBM_PEAK_GBS = 8000.0
 OPS_PER_CELL = 10                               # algorithmic int ops per cell
+DOM_KERNEL = 'k_align<24, true, 2> (packed core, 21-24 bp adapters, affine)'
 
 
 def parse():
@@ -43,7 +48,7 @@ def parse():
     ap.add_argument('--sets', type=int, default=50)
     ap.add_argument('--end-size', type=int, default=150)
     ap.add_argument('--mean-len', type=int, default=8000)
-    ap.add_argument('--cpu-sample', type=int, default=3000, help='reads in the CPU-baseline sample (0 = skip)')
+    ap.add_argument('--cpu-sample', type=int, default=12000, help='reads in the CPU-baseline sample (0 = skip)')
     ap.add_argument('--cpu-threads', type=int, default=0, help='0 = min(16, cpus available)')
     ap.add_argument('--check', type=int, default=256, help='reads checked against the oracle after timing')
     return ap.parse_args()
@@ -67,8 +72,14 @@ def main():
 
     # ---- workload (host) ----
     sets = [a for a in A.fresh_adapters() if '(full sequence)' not in a.name][:args.sets]
+    # adapters of the dominant register bucket (21..24 bp -> k_align<24, *, PACKED>) first, so
+    # their launch can be timed on its own (roofline); the trim decision is a max over adapters
+    # and does not depend on their order
+    dom = lambda x: 20 < len(x) <= 24
     start_adps = [a.start_sequence[1] for a in sets if a.start_sequence]
     end_adps = [a.end_sequence[1] for a in sets if a.end_sequence]
+    start_adps = [x for x in start_adps if dom(x)] + [x for x in start_adps if not dom(x)]
+    end_adps = [x for x in end_adps if dom(x)] + [x for x in end_adps if not dom(x)]
     t0 = time.time()
     reads = synth.make_reads(args.reads, args.mean_len, seed=12345 + rank, keep=args.end_size)
     buf, s_off, s_len, e_off, e_len = synth.pack_end_windows(reads, args.end_size)
@@ -89,15 +100,16 @@ def main():
         _lib.check(L.pcabi_dev_h2d(p, arr.ctypes.data_as(vp), arr.nbytes), 'h2d')
         return p
 
+    def table(lst):
+        t = vp()
+        if lst:
+            c, o, l = encode_adapters(lst)
+            _lib.check(L.pcabi_adapters_create(c.ctypes.data_as(vp), o.ctypes.data_as(vp), l.ctypes.data_as(vp),
+                                               len(lst), ctypes.byref(t)), 'adapters_create')
+        return t, len(lst)
+
     d_codes = h2d(buf)
     d_soff, d_slen, d_eoff, d_elen = h2d(s_off), h2d(s_len), h2d(e_off), h2d(e_len)
-    tabs = []
-    for lst in (start_adps, end_adps):
-        c, o, l = encode_adapters(lst)
-        t = vp()
-        _lib.check(L.pcabi_adapters_create(c.ctypes.data_as(vp), o.ctypes.data_as(vp), l.ctypes.data_as(vp),
-                                           len(lst), ctypes.byref(t)), 'adapters_create')
-        tabs.append(t)
     n_sa, n_ea = len(start_adps), len(end_adps)
     s_stride, e_stride = n_sa * n, n_ea * n
     d_sres = dalloc(4 * 8 * s_stride)
@@ -107,29 +119,52 @@ def main():
     _lib.check(L.pcabi_stream_create(ctypes.byref(stream)), 'stream')
     sc = (3, -6, -5, -2)
 
-    def align_start():
-        _lib.check(L.pcabi_align_cross_dev(d_codes, d_soff, d_slen, n, int(s_len.max()), tabs[0], *sc, d_sres, s_stride, stream), 'align')
+    # tile layout: computed once from the host window lengths; the device
+    # re-tiles the windows inside every step
+    sides = []
+    for lens, d_off, d_len, adps, d_res, stride in ((s_len, d_soff, d_slen, start_adps, d_sres, s_stride),
+                                                    (e_len, d_eoff, d_elen, end_adps, d_eres, e_stride)):
+        toff = np.zeros((n + 255) // 256 + 1, np.int64)
+        nd = L.pcabi_tile_layout(lens.ctypes.data_as(vp), n, toff.ctypes.data_as(vp))
+        if nd < 0:
+            raise _lib.PcabiError('tile layout failed')
+        n_dom = sum(1 for x in adps if dom(x))
+        sides.append(dict(lens=lens, d_off=d_off, d_len=d_len, d_toff=h2d(toff), d_tiles=dalloc(4 * nd),
+                          mq=int(np.diff(toff).max() // 256), dom=table(adps[:n_dom]), rest=table(adps[n_dom:]),
+                          d_res=d_res, d_res_rest=vp(d_res.value + 4 * n_dom * n), stride=stride))
 
-    def align_end():
-        _lib.check(L.pcabi_align_cross_dev(d_codes, d_eoff, d_elen, n, int(e_len.max()), tabs[1], *sc, d_eres, e_stride, stream), 'align')
+    ev = []
+    for _ in range(4 * args.steps + 4):
+        e = vp()
+        _lib.check(L.pcabi_event_create(ctypes.byref(e)), 'event')
+        ev.append(e)
+
+    def align_side(sd, e0=None, e1=None):
+        _lib.check(L.pcabi_tile_windows_dev(d_codes, sd['d_off'], sd['d_len'], n, sd['d_toff'], sd['mq'],
+                                            sd['d_tiles'], stream), 'tile')
+        mx = int(sd['lens'].max())
+        for key, d_res in (('dom', sd['d_res']), ('rest', sd['d_res_rest'])):
+            tab, cnt = sd[key]
+            if not cnt:
+                continue
+            if key == 'dom' and e0 is not None:
+                L.pcabi_event_record(e0, stream)
+            _lib.check(L.pcabi_align_cross_dev(sd['d_tiles'], sd['d_toff'], sd['d_len'], n, mx, tab, *sc, d_res,
+                                               sd['stride'], stream), 'align')
+            if key == 'dom' and e1 is not None:
+                L.pcabi_event_record(e1, stream)
 
     def epilogue():
         _lib.check(L.pcabi_end_trim_dev(d_sres, s_stride, n_sa, d_eres, e_stride, n_ea, n, args.end_size,
                                         2, 75.0, 4, d_st, d_et, None, None, stream), 'end_trim')
 
-    ev = []
-    for _ in range(2 * args.steps + 2):
-        e = vp()
-        _lib.check(L.pcabi_event_create(ctypes.byref(e)), 'event')
-        ev.append(e)
-
     def step(k=None):
-        if k is not None:
-            L.pcabi_event_record(ev[2 * k], stream)
-        align_start()
-        align_end()
-        if k is not None:
-            L.pcabi_event_record(ev[2 * k + 1], stream)
+        if k is None:
+            align_side(sides[0])
+            align_side(sides[1])
+        else:
+            align_side(sides[0], ev[4 * k], ev[4 * k + 1])
+            align_side(sides[1], ev[4 * k + 2], ev[4 * k + 3])
         epilogue()
 
     for _ in range(args.warmup):
@@ -154,22 +189,32 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    align_ms = []
+    # dominant kernel: average launch duration, start and end launches separately
+    dom_ms = [[], []]
     for k in range(args.steps):
-        ms = ctypes.c_float()
-        _lib.check(L.pcabi_event_elapsed_ms(ctypes.byref(ms), ev[2 * k], ev[2 * k + 1]), 'elapsed')
-        align_ms.append(ms.value)
-    align_ms = float(np.mean(align_ms))
+        for side in (0, 1):
+            ms = ctypes.c_float()
+            _lib.check(L.pcabi_event_elapsed_ms(ctypes.byref(ms), ev[4 * k + 2 * side], ev[4 * k + 2 * side + 1]),
+                       'elapsed')
+            dom_ms[side].append(ms.value)
+    dom_ms = [float(np.mean(x)) for x in dom_ms]
 
-    # ---- algorithmic work per step (per GPU) ----
+    # ---- algorithmic work (per GPU) ----
     s_len64, e_len64 = s_len.astype(np.int64), e_len.astype(np.int64)
     La = np.array([len(x) for x in start_adps], np.int64)
     Le = np.array([len(x) for x in end_adps], np.int64)
     cells = int(s_len64.sum() * La.sum() + e_len64.sum() * Le.sum())
-    alignments = n * (n_sa + n_ea)
-    alg_bytes = int(s_len64.sum() * 1 + e_len64.sum() * 1 + La.sum() + Le.sum() + alignments * 32)
-    tops = cells * OPS_PER_CELL / (align_ms * 1e-3) / 1e12
-    gbs = alg_bytes / (align_ms * 1e-3) / 1e9
+    # dominant kernel, per launch (start launch and end launch averaged)
+    dom_cells = [int(s_len64.sum() * La[[dom(x) for x in start_adps]].sum()),
+                 int(e_len64.sum() * Le[[dom(x) for x in end_adps]].sum())]
+    dom_bytes = [int(s_len64.sum() + La[[dom(x) for x in start_adps]].sum() + 32 * n * sum(map(dom, start_adps))),
+                 int(e_len64.sum() + Le[[dom(x) for x in end_adps]].sum() + 32 * n * sum(map(dom, end_adps)))]
+    launch_ms = float(np.mean(dom_ms))
+    launch_cells = float(np.mean(dom_cells))
+    launch_bytes = float(np.mean(dom_bytes))
+    tops = launch_cells * OPS_PER_CELL / (launch_ms * 1e-3) / 1e12
+    gbs = launch_bytes / (launch_ms * 1e-3) / 1e9
+    step_ms = 1e3 * elapsed / args.steps
 
     # ---- correctness spot-check (outside the timed region) ----
     checked = None
@@ -191,7 +236,7 @@ def main():
             'n_gpus': world,
             'steps': args.steps,
             'warmup': args.warmup,
-            'ms_per_step': round(1e3 * elapsed / args.steps, 4),
+            'ms_per_step': round(step_ms, 4),
             'higher_is_better': True,
             'scaling': 'weak',
             'vs_baseline': None,
@@ -204,13 +249,16 @@ def main():
                        'scoring': list(sc), 'parallelism': 'dp%d (read shards)' % world},
             'roofline': {'bound': 'valu', 'achieved': round(tops, 3), 'peak': round(VALU_PEAK_TOPS, 1),
                          'unit': 'Tops/s (int32 lane-ops)', 'frac': round(tops / VALU_PEAK_TOPS, 4),
-                         'traffic': prof.get('traffic_bytes_per_step') if prof else None,
-                         'kernel': 'k_align_cross (start+end launches)',
-                         'ops_per_cell': OPS_PER_CELL, 'cells_per_step': cells,
-                         'kernel_ms_per_step': round(align_ms, 4)},
+                         'traffic': prof.get('traffic_bytes_per_launch') if prof else None,
+                         'kernel': DOM_KERNEL,
+                         'launch_ms': round(launch_ms, 4), 'cells_per_launch': int(launch_cells),
+                         'ops_per_cell': OPS_PER_CELL,
+                         'traffic_source': prof.get('source') if prof else None},
             'hbm': {'achieved': round(gbs, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                    'frac': round(gbs / HBM_PEAK_GBS, 5), 'algorithmic_bytes_per_step': alg_bytes},
-            'gcups': round(cells / (align_ms * 1e-3) / 1e9, 1),
+                    'frac': round(gbs / HBM_PEAK_GBS, 5), 'algorithmic_bytes_per_launch': int(launch_bytes),
+                    'kernel': DOM_KERNEL},
+            'gcups_step': round(cells / (step_ms * 1e-3) / 1e9, 1),
+            'cells_per_step': cells,
             'cpu_baseline': cpu,
             'gpu_vs_cpu': round(value / cpu['value'], 1) if cpu else None,
             'parity_spot_check': checked,

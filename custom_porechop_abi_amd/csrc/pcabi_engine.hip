@@ -1,11 +1,15 @@
 // pcabi_engine.hip -- gfx950 kernels + C ABI of the adapter-alignment engine (include/pcabi.h).
 //
 // Kernel map:
-//   k_align_cross<RPL, AFFINE>  one wave64 = 64 windows x ONE adapter (wave-uniform, SGPRs);
-//                               one lane = one (window, adapter) DP, rows in VGPRs
-//                               (pcabi_dp.h). VALU-bound integer work, no LDS, no shuffles.
-//   k_align_pairs<RPL, AFFINE>  same, work given as explicit (window, adapter) pairs grouped
-//                               by adapter into waves on the host.
+//   k_align<RPL, AFFINE, KIND>  one lane = one (window, adapter) DP with the adapter's RPL rows
+//                               in VGPRs, one column (read base) per step (pcabi_dp.h). The
+//                               wave's adapter is uniform. KIND picks the DP core: PACKED
+//                               (score|tie-break|attributes in one int32 key, substitution keys
+//                               from an LDS table), FAST (separate score/attribute registers,
+//                               adapters <= 64) or GENERIC (any scoring, adapters <= 128).
+//                               Two work shapes: cross (every window x every adapter of a
+//                               bucket; XCD-aware tile order) and pairs (explicit tasks grouped
+//                               into per-adapter waves on the host).
 //   k_end_trim                  per-read decision epilogue (nanopore_read.py:175-217).
 //   k_best_full_id              per-adapter max of the full-adapter identity
 //                               (nanopore_read.py:158-173), deterministic (max is exact).
@@ -68,10 +72,12 @@ int bucket_of(int L, const pcabi::Scoring &sc) {
 }
 
 struct KParams {
-    const uint8_t *codes;
+    const uint8_t *codes;      // pairs mode: windows read in place
     const int64_t *win_off;
     const int32_t *win_len;
     int64_t n_win;
+    const uint32_t *tiles;     // cross mode: windows in tile layout (pcabi_tile_windows_dev)
+    const int64_t *tile_off;   // [n_tiles + 1] dword offsets
     // bucket-local adapter table: RPL bytes per adapter, top padded (slot s-1 <-> byte s-1)
     const uint32_t *adp_pad;
     const int32_t *adp_len;
@@ -87,43 +93,27 @@ struct KParams {
     pcabi::Scoring sc;
 };
 
-// Window codes, one byte per column (buffers carry >= 16 bytes of padding past every window,
-// so the one-column-ahead read of the last column stays in bounds).
-#ifndef PCABI_RD_MODE
-#define PCABI_RD_MODE 1
-#endif
-#if PCABI_RD_MODE == 0
+// Window reader: one dword per lane every 4 columns (a wave-uniform branch -- j is the same in
+// every lane), fetched one chunk ahead. Two layouts share it:
+//   tiles (cross mode): chunk q of the lane's window at base[q * 256], so a wave's load is 256
+//                       contiguous bytes (pcabi_tile_windows_dev builds the layout);
+//   codes (pairs mode): the window's own bytes, base = its aligned dword, stride 1, a8 = 8 x
+//                       misalignment; reads at most 12 bytes past the window end.
 struct WindowReader {
-    const uint8_t *p;
-    __device__ __forceinline__ explicit WindowReader(const uint8_t *base, int) : p(base) {}
-    __device__ __forceinline__ int operator()(int j) { return (int)p[j - 1]; }
-};
-#elif PCABI_RD_MODE == 1
-// Aligned-dword stream: one dword load per lane every 4 columns (a wave-uniform branch, j is the
-// same in every lane), fetched one chunk ahead; reads at most 12 bytes past the window end.
-struct WindowReader {
-    const uint32_t *q;   // aligned dword holding byte 0
-    int a8;              // 8 * misalignment
+    const uint32_t *q;
+    int64_t stride;      // dwords between consecutive chunks
+    int a8;
     uint32_t lo, hi, nx;
-    __device__ __forceinline__ explicit WindowReader(const uint8_t *base, int) {
-        const int a0 = (int)((uintptr_t)base & 3);
-        a8 = 8 * a0;
-        q = reinterpret_cast<const uint32_t *>(base - a0);   // keeps the global address space
-        lo = q[0]; hi = q[1]; nx = q[2];
+    __device__ __forceinline__ WindowReader(const uint32_t *base, int64_t stride_, int a8_)
+        : q(base), stride(stride_), a8(a8_) {
+        lo = q[0]; hi = q[stride]; nx = q[2 * stride];
     }
     __device__ __forceinline__ int operator()(int j) {   // called with j = 1, 2, 3, ... in order
         const int k = j - 1;
-        if (k > 0 && (k & 3) == 0) { lo = hi; hi = nx; nx = q[k / 4 + 2]; }
+        if (k > 0 && (k & 3) == 0) { lo = hi; hi = nx; nx = q[(int64_t)(k / 4 + 2) * stride]; }
         return (int)(((((uint64_t)hi << 32) | lo) >> (8 * (k & 3) + a8)) & 0xFFu);
     }
 };
-#else
-struct WindowReader {   // timing experiment only: no window loads (results are wrong)
-    uint32_t v;
-    __device__ __forceinline__ explicit WindowReader(const uint8_t *base, int) : v((uint32_t)(uintptr_t)base) {}
-    __device__ __forceinline__ int operator()(int j) { return (int)((v >> (j & 15)) & 3); }
-};
-#endif
 
 template <int RPL>
 struct AdapterRegs {
@@ -170,7 +160,7 @@ struct LdsRow {
 
 template <int RPL, bool AFFINE, int KIND>
 __device__ __forceinline__ void run_lane(const KParams &p, int a_local, int64_t w, int64_t out_idx,
-                                         int32_t *wave_tab) {
+                                         int32_t *wave_tab, int64_t tile_off) {
     AdapterRegs<RPL> adp;
     adp.load(p.adp_pad + (int64_t)a_local * (RPL / 4));
     const int L = __builtin_amdgcn_readfirstlane(p.adp_len[a_local]);
@@ -192,7 +182,13 @@ __device__ __forceinline__ void run_lane(const KParams &p, int a_local, int64_t 
     if (n <= 0) {
         r = empty_result();
     } else {
-        WindowReader rd(p.codes + p.win_off[w], n);
+        WindowReader rd = tile_off >= 0
+            ? WindowReader(p.tiles + tile_off + (threadIdx.x & 255), 256, 0)
+            : [&] {
+                  const uint8_t *b = p.codes + p.win_off[w];
+                  const int a0 = (int)((uintptr_t)b & 3);
+                  return WindowReader(reinterpret_cast<const uint32_t *>(b - a0), 1, 8 * a0);
+              }();
         if constexpr (KIND == PACKED) {
             auto tabfn = [&](int rc) { return LdsRow{wave_tab + rc * RPL}; };
             r = pcabi::align_lane_packed<(RPL <= 64 ? RPL : 64), AFFINE>(rd, n, tabfn, L, p.sc);
@@ -206,17 +202,25 @@ __device__ __forceinline__ void run_lane(const KParams &p, int a_local, int64_t 
 }
 
 // One kernel for both work shapes (uniform branch on p.task_win):
-//  cross: grid (ceil(n_win/256), n_adp); lane = window, blockIdx.y = bucket-local adapter
+//  cross: 1-D grid of (window tile of 256, adapter) blocks in XCD-aware order; lane = window
 //  pairs: grid (ceil(n_waves/4)); wave = one adapter, lanes = host-grouped tasks
 template <int RPL, bool AFFINE, int KIND>
 __global__ __launch_bounds__(256, PCABI_WAVES) void k_align(KParams p) {
     __shared__ __attribute__((aligned(16))) int32_t tab[KIND == PACKED ? 4 * kTabW * RPL : 4];
     int32_t *wave_tab = tab + (KIND == PACKED ? (threadIdx.x >> 6) * kTabW * RPL : 0);
     if (p.task_win == nullptr) {
-        const int a_local = blockIdx.y;
-        const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
+        // XCD-aware order: workgroups are dealt to the 8 XCDs round-robin, so block b runs on
+        // XCD b % 8. Each XCD takes every 8th tile of 256 windows and runs ALL adapters of a
+        // tile back to back, so a tile is fetched into one L2 once instead of once per adapter.
+        const int64_t b = blockIdx.x;
+        const int64_t k = b >> 3;
+        const int a_local = (int)(k % p.n_adp);
+        const int64_t tile = (k / p.n_adp) * 8 + (b & 7);
+        const int64_t w = tile * 256 + threadIdx.x;
         const int a_glob = p.adp_id[a_local];
-        run_lane<RPL, AFFINE, KIND>(p, a_local, w < p.n_win ? w : -1, (int64_t)a_glob * p.n_win + w, wave_tab);
+        const int64_t toff = w < p.n_win ? p.tile_off[tile] : 0;
+        run_lane<RPL, AFFINE, KIND>(p, a_local, w < p.n_win ? w : -1, (int64_t)a_glob * p.n_win + w, wave_tab,
+                                    toff);
     } else {
         int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
         const bool live = wave < p.n_waves;            // dead waves still join the table barrier
@@ -224,7 +228,7 @@ __global__ __launch_bounds__(256, PCABI_WAVES) void k_align(KParams p) {
         const int64_t slot = wave * 64 + (threadIdx.x & 63);
         const int a_local = __builtin_amdgcn_readfirstlane(p.wave_adp[wave]);
         const int32_t tw = live ? p.task_win[slot] : -1;
-        run_lane<RPL, AFFINE, KIND>(p, a_local, tw, tw >= 0 ? p.task_out[slot] : 0, wave_tab);
+        run_lane<RPL, AFFINE, KIND>(p, a_local, tw, tw >= 0 ? p.task_out[slot] : 0, wave_tab, -1);
     }
 }
 
@@ -300,6 +304,64 @@ __global__ __launch_bounds__(256) void k_best_full_id(const int32_t *res, int64_
 
 // ---- launch plumbing -------------------------------------------------------------------------
 
+// Tile layout of a window list (cross mode): windows [256t, 256t + 256) form tile t; dword
+// (t, q, lane) = codes 4q..4q+3 of window 256t + lane, at tiles[tile_off[t] + 256q + lane].
+// Zero past each window's end. One block transposes 256 windows x 16 chunks through LDS: reads
+// are 64-byte runs of each window (offsets are 4-aligned), writes are 1 KB rows.
+// grid (n_tiles, <= 1024): blockIdx.y strides over 16-chunk slabs.
+__global__ __launch_bounds__(256) void k_tile_windows(const uint8_t *codes, const int64_t *win_off,
+                                                      const int32_t *win_len, int64_t n_win,
+                                                      const int64_t *tile_off, uint32_t *tiles) {
+    __shared__ uint32_t sh[256][17];
+    const int64_t t = blockIdx.x;
+    const int64_t base = tile_off[t];
+    const int64_t nq = (tile_off[t + 1] - base) / 256;
+    for (int64_t q0 = (int64_t)blockIdx.y * 16; q0 < nq; q0 += (int64_t)gridDim.y * 16) {
+        for (int k = threadIdx.x; k < 256 * 16; k += 256) {
+            const int wl = k >> 4, qq = k & 15;
+            const int64_t w = t * 256 + wl;
+            const int64_t c0 = 4 * (q0 + qq);
+            uint32_t v = 0;
+            if (w < n_win) {
+                const int n = win_len[w];
+                if (c0 < n) {
+                    v = *reinterpret_cast<const uint32_t *>(codes + win_off[w] + c0);
+                    if (n - c0 < 4) v &= (1u << (8 * (n - c0))) - 1u;
+                }
+            }
+            sh[wl][qq] = v;
+        }
+        __syncthreads();
+        const int nqq = (int)std::min<int64_t>(16, nq - q0);
+        for (int qq = 0; qq < nqq; ++qq) tiles[base + (q0 + qq) * 256 + threadIdx.x] = sh[threadIdx.x][qq];
+        __syncthreads();
+    }
+}
+
+int64_t tile_layout(const int32_t *win_len, int64_t n_win, int64_t *tile_off, int64_t *max_nq) {
+    const int64_t n_tiles = (n_win + 255) / 256;
+    int64_t off = 0, mq = 0;
+    for (int64_t t = 0; t < n_tiles; ++t) {
+        int32_t mx = 0;
+        for (int64_t w = t * 256; w < std::min<int64_t>(n_win, t * 256 + 256); ++w) mx = std::max(mx, win_len[w]);
+        const int64_t nq = (mx + 3) / 4 + 2;   // + the reader's one-chunk-ahead fetch
+        tile_off[t] = off;
+        off += nq * 256;
+        mq = std::max(mq, nq);
+    }
+    tile_off[n_tiles] = off;
+    if (max_nq) *max_nq = mq;
+    return off;
+}
+
+void launch_tiles(const uint8_t *codes, const int64_t *win_off, const int32_t *win_len, int64_t n_win,
+                  const int64_t *tile_off, int64_t max_nq, uint32_t *tiles, hipStream_t st) {
+    const int64_t n_tiles = (n_win + 255) / 256;
+    if (n_tiles == 0) return;
+    const dim3 grid((unsigned)n_tiles, (unsigned)std::min<int64_t>(std::max<int64_t>((max_nq + 15) / 16, 1), 1024));
+    hipLaunchKernelGGL(k_tile_windows, grid, dim3(256), 0, st, codes, win_off, win_len, n_win, tile_off, tiles);
+}
+
 template <int RPL, int KIND>
 void launch(const KParams &p, bool affine, dim3 grid, hipStream_t st) {
     if (affine) hipLaunchKernelGGL((k_align<RPL, true, KIND>), grid, dim3(256), 0, st, p);
@@ -307,8 +369,9 @@ void launch(const KParams &p, bool affine, dim3 grid, hipStream_t st) {
 }
 
 void dispatch(int b, const KParams &p, bool affine, hipStream_t st, bool packed) {
+    const int64_t tiles8 = (p.n_win + 8 * 256 - 1) / (8 * 256) * 8;   // window tiles, padded to 8
     dim3 grid = p.task_win ? dim3((unsigned)((p.n_waves + 3) / 4))
-                           : dim3((unsigned)((p.n_win + 255) / 256), (unsigned)p.n_adp);
+                           : dim3((unsigned)(tiles8 * p.n_adp));
     const BucketDef d = kBuckets[b];
     if (d.kind == FAST && packed) {
         switch (d.rpl) {
@@ -400,7 +463,7 @@ struct Engine {
     std::mutex mu;
     bool init = false;
     hipStream_t stream = nullptr;
-    DeviceBuf codes, woff, wlen, out, tasks_win, tasks_out, wave_adp;
+    DeviceBuf codes, woff, wlen, out, tasks_win, tasks_out, wave_adp, tiles, toff;
     DeviceBuf pad[kNumBuckets], len[kNumBuckets], id[kNumBuckets];
 };
 
@@ -551,6 +614,20 @@ int pcabi_align_host(int device, const uint8_t *codes, int64_t codes_len, const 
         p.n_adp = nb;
         if (!task_win) {
             p.task_win = nullptr;
+            if (n_win > 0 && !p.tiles) {
+                std::vector<int64_t> toff((size_t)((n_win + 255) / 256 + 1));
+                int64_t max_nq = 0;
+                const int64_t nd = tile_layout(win_len, n_win, toff.data(), &max_nq);
+                if (int rc = e.toff.ensure(sizeof(int64_t) * toff.size())) return rc;
+                if (int rc = e.tiles.ensure(sizeof(uint32_t) * (size_t)nd)) return rc;
+                HIP_TRY(hipMemcpyAsync(e.toff.p, toff.data(), sizeof(int64_t) * toff.size(), hipMemcpyHostToDevice, e.stream));
+                launch_tiles(p.codes, p.win_off, p.win_len, n_win, (const int64_t *)e.toff.p, max_nq,
+                             (uint32_t *)e.tiles.p, e.stream);
+                // toff (host) must outlive the async copy
+                HIP_TRY(hipStreamSynchronize(e.stream));
+                p.tiles = (const uint32_t *)e.tiles.p;
+                p.tile_off = (const int64_t *)e.toff.p;
+            }
             if (n_win > 0) dispatch(b, p, affine, e.stream, bucket_packed_ok(b, h.len, sc));
         } else {
             tw.clear(); to.clear(); wa.clear();
@@ -708,15 +785,36 @@ void pcabi_adapters_destroy(pcabi_adapters *a) {
     delete a;
 }
 
-int pcabi_align_cross_dev(const uint8_t *codes, const int64_t *win_off, const int32_t *win_len,
+int64_t pcabi_tile_layout(const int32_t *win_len, int64_t n_win, int64_t *tile_off) {
+    if (n_win < 0 || !win_len || !tile_off) return fail(PCABI_E_ARG, "bad arguments");
+    return tile_layout(win_len, n_win, tile_off, nullptr);
+}
+
+int pcabi_tile_windows_dev(const uint8_t *codes, const int64_t *win_off, const int32_t *win_len,
+                           int64_t n_win, const int64_t *tile_off, int64_t max_chunks, uint32_t *tiles,
+                           void *stream) {
+    if (n_win < 0) return fail(PCABI_E_ARG, "bad arguments");
+    launch_tiles(codes, win_off, win_len, n_win, tile_off, max_chunks, tiles, (hipStream_t)stream);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int pcabi_align_cross_dev(const uint32_t *tiles, const int64_t *tile_off, const int32_t *win_len,
                           int64_t n_win, int32_t max_win_len, const pcabi_adapters *adps, int match,
                           int mismatch, int gap_open, int gap_extend, int32_t *out, int64_t out_stride,
                           void *stream) {
-    if (!adps || n_win < 0) return fail(PCABI_E_ARG, "bad arguments");
+    if (!adps || n_win < 0 || (n_win > 0 && (!tiles || !tile_off))) return fail(PCABI_E_ARG, "bad arguments");
     if (n_win == 0) return 0;
+    {
+        int max_L = 0;
+        for (int b = 0; b < kNumBuckets; ++b)
+            for (int32_t L : adps->lens[b]) max_L = std::max<int>(max_L, L);
+        if (int rc = check_span(pcabi::Scoring{match, mismatch, gap_open, gap_extend}, max_L, max_win_len))
+            return rc;
+    }
     KParams p{};
-    p.codes = codes;
-    p.win_off = win_off;
+    p.tiles = tiles;
+    p.tile_off = tile_off;
     p.win_len = win_len;
     p.n_win = n_win;
     p.out = out;

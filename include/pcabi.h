@@ -124,12 +124,31 @@ int pcabi_adapters_create(const uint8_t *adp_codes, const int32_t *adp_off, cons
 void pcabi_adapters_destroy(pcabi_adapters *a);
 
 /*
- * Cross-product alignment, every pointer a DEVICE pointer, asynchronous on `stream`:
- * result (a, w) -> out[f * out_stride + a * n_win + w]. max_win_len (host value) bounds every
- * win_len[w]: it selects the packed-key kernels (windows <= 223) and must be honest. Windows
- * longer than 32k need negative gap costs.
+ * Tile layout of a window list, the form the cross-product kernels read:
+ * windows [256t, 256t + 256) form tile t; dword (t, q, lane) holds codes 4q..4q+3 of window
+ * 256t + lane at tiles[tile_off[t] + 256 q + lane], so a wavefront's load of one 4-column chunk
+ * is 256 contiguous bytes. A tile holds ceil(longest window in it / 4) + 2 chunks; sort the
+ * windows by length first when they vary (whole reads) to keep tiles dense.
+ *   pcabi_tile_layout      : host; fills tile_off[ceil(n_win/256) + 1] (dword offsets) from the
+ *                            host copy of win_len and returns the total dword count (< 0 on
+ *                            error).
+ *   pcabi_tile_windows_dev : device pointers, async on `stream`: writes `tiles` from windows
+ *                            laid out as for pcabi_align_host (codes/win_off/win_len);
+ *                            max_chunks = largest per-tile chunk count (a launch-shape hint).
  */
-int pcabi_align_cross_dev(const uint8_t *codes, const int64_t *win_off, const int32_t *win_len,
+int64_t pcabi_tile_layout(const int32_t *win_len, int64_t n_win, int64_t *tile_off);
+int pcabi_tile_windows_dev(const uint8_t *codes, const int64_t *win_off, const int32_t *win_len,
+                           int64_t n_win, const int64_t *tile_off, int64_t max_chunks,
+                           uint32_t *tiles, void *stream);
+
+/*
+ * Cross-product alignment, every pointer a DEVICE pointer, asynchronous on `stream`:
+ * result (a, w) -> out[f * out_stride + a * n_win + w]. Windows come in tile layout (above);
+ * win_len[n_win] is still passed per window. max_win_len (host value) bounds every win_len[w]
+ * and must be honest: windows longer than 32k need negative gap costs (the start-column field
+ * of the non-packed cores is kept mod 2^16).
+ */
+int pcabi_align_cross_dev(const uint32_t *tiles, const int64_t *tile_off, const int32_t *win_len,
                           int64_t n_win, int32_t max_win_len, const pcabi_adapters *adps,
                           int match, int mismatch, int gap_open, int gap_extend,
                           int32_t *out, int64_t out_stride, void *stream);

@@ -140,3 +140,58 @@ def test_long_reads_middle_shape(gpu_lib):
     n = len(reads)
     exp = oracle_lib.align_many(reads, adps, (np.tile(np.arange(n), 3), np.repeat(np.arange(3), n)), sc)
     assert np.array_equal(got, exp)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('scheme', [(3, -6, -5, -2), (2, -1, -1, -1)])
+def test_device_abi_tiled_cross(gpu_lib, scheme):
+    """Device-pointer ABI: pcabi_tile_layout -> pcabi_tile_windows_dev -> pcabi_align_cross_dev,
+    with ragged windows (empty, 1 bp, several kb) and more than one tile."""
+    from custom_porechop_abi_amd import _lib, engine
+    L, vp = gpu_lib, ctypes.c_void_p
+    reads, adps = _case_set(31, 700, 7, 3000, 64)
+    pack = engine.SeqPack(reads)
+    n = len(reads)
+    lens = pack.lengths.astype(np.int32)
+    toff = np.zeros((n + 255) // 256 + 1, np.int64)
+    nd = L.pcabi_tile_layout(lens.ctypes.data_as(vp), n, toff.ctypes.data_as(vp))
+    assert nd == toff[-1] > 0
+    bufs = []
+
+    def h2d(a):
+        a = np.ascontiguousarray(a)
+        p = vp()
+        _lib.check(L.pcabi_dev_malloc(ctypes.byref(p), max(a.nbytes, 16)), 'malloc')
+        _lib.check(L.pcabi_dev_h2d(p, a.ctypes.data_as(vp), a.nbytes), 'h2d')
+        bufs.append(p)
+        return p
+
+    d_codes, d_off, d_len, d_toff = h2d(pack.codes), h2d(pack.offsets), h2d(lens), h2d(toff)
+    d_tiles = vp()
+    _lib.check(L.pcabi_dev_malloc(ctypes.byref(d_tiles), 4 * int(nd)), 'malloc')
+    bufs.append(d_tiles)
+    c, o, l = engine.encode_adapters(adps)
+    tab = vp()
+    _lib.check(L.pcabi_adapters_create(c.ctypes.data_as(vp), o.ctypes.data_as(vp), l.ctypes.data_as(vp),
+                                       len(adps), ctypes.byref(tab)), 'adapters_create')
+    stride = n * len(adps)
+    d_out = vp()
+    _lib.check(L.pcabi_dev_malloc(ctypes.byref(d_out), 4 * 8 * stride), 'malloc')
+    bufs.append(d_out)
+    try:
+        mq = int(np.diff(toff).max() // 256)
+        _lib.check(L.pcabi_tile_windows_dev(d_codes, d_off, d_len, n, d_toff, mq, d_tiles, None), 'tile')
+        _lib.check(L.pcabi_align_cross_dev(d_tiles, d_toff, d_len, n, int(lens.max()), tab, *scheme, d_out,
+                                           stride, None), 'align')
+        _lib.check(L.pcabi_dev_sync(), 'sync')
+        got = np.zeros((8, stride), np.int32)
+        _lib.check(L.pcabi_dev_d2h(got.ctypes.data_as(vp), d_out, got.nbytes), 'd2h')
+    finally:
+        L.pcabi_adapters_destroy(tab)
+        for p in bufs:
+            L.pcabi_dev_free(p)
+    exp = oracle_lib.align_many(reads, adps, (np.tile(np.arange(n), len(adps)), np.repeat(np.arange(len(adps)), n)),
+                                scheme)
+    ok = exp[0] != -1
+    assert np.array_equal(got[0], exp[0])
+    assert np.array_equal(got[:, ok], exp[:, ok]), _first_diff(got, exp, reads, adps, n)
