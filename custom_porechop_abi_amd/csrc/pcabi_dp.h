@@ -37,10 +37,6 @@
 #define PCABI_TAB_PD 1
 #endif
 
-
-
-
-
 #include <stdint.h>
 
 #ifdef __HIPCC__

@@ -1,0 +1,143 @@
+"""Multi-GPU drivers: one process per GPU, each owning a contiguous shard of the reads
+(SURVEY.md §8(e)).
+
+Every (read, adapter) alignment is independent, so the trimming phases need no exchange at all:
+a rank runs the batched drivers of porechop_abi.py on its own reads. The one real exchange is
+the adapter-set search (porechop_abi/porechop_abi.py:200-245): a set is kept when its best
+full-adapter identity over ALL check reads reaches the threshold, so the per-set maxima are
+all-reduced with MAX (2 x n_sets float64, exact and order-free) before the same filter runs on
+every rank. With backend "nccl" (RCCL over xGMI on MI355X) the buffer lives on the rank's GPU;
+with "gloo" it stays on the host (the CPU tests).
+
+Shards are contiguous read ranges, balanced by read count (end windows: equal work per read) or
+by total bases (middle scan: work grows with read length). gather_trims() brings the per-read
+trim amounts back to every rank in the original read order; share_trims() writes them into the
+reads so the middle scan (which works on the end-trimmed sequence) can use its own shards.
+"""
+import numpy as np
+
+from . import porechop_abi as P
+from . import adapters as _adapters
+
+
+def _dist():
+    import torch.distributed as dist
+    return dist
+
+
+def shard_bounds(n, rank, world):
+    """[lo, hi) of an equal-count contiguous split of n items."""
+    lo = n * rank // world
+    hi = n * (rank + 1) // world
+    return lo, hi
+
+
+def shard_bounds_by_length(lengths, rank, world):
+    """[lo, hi) of a contiguous split balanced by the running sum of lengths (middle scan)."""
+    lengths = np.asarray(lengths, dtype=np.int64)
+    n = len(lengths)
+    if n == 0:
+        return 0, 0
+    cum = np.concatenate([[0], np.cumsum(lengths)])
+    total = cum[-1]
+    cut = lambda r: int(np.searchsorted(cum, total * r / world, side='left')) if 0 < r < world else (0 if r == 0 else n)
+    return min(cut(rank), n), min(cut(rank + 1), n)
+
+
+def _device_tensor(values, group):
+    import torch
+    dist = _dist()
+    t = torch.tensor(values, dtype=torch.float64)
+    if dist.get_backend(group) == 'nccl':
+        t = t.cuda()
+    return t
+
+
+def allreduce_set_scores(search_sets, group=None):
+    """All-reduce MAX of every set's best_start_score / best_end_score, written back in place."""
+    dist = _dist()
+    if not dist.is_initialized() or dist.get_world_size(group) == 1 or not search_sets:
+        return
+    t = _device_tensor([[a.best_start_score, a.best_end_score] for a in search_sets], group)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    vals = t.cpu().numpy()
+    for a, (s, e) in zip(search_sets, vals):
+        a.best_start_score, a.best_end_score = float(s), float(e)
+
+
+def find_matching_adapter_sets(check_reads, verbosity, end_size, scoring_scheme_vals, print_dest,
+                               adapter_threshold, threads, adapter_sets=None, group=None):
+    """Sharded porechop_abi.find_matching_adapter_sets: check_reads is the FULL check list (same
+    on every rank); each rank aligns its shard, then the per-set maxima are all-reduced."""
+    dist = _dist()
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if adapter_sets is None:
+        adapter_sets = _adapters.ADAPTERS
+    lo, hi = shard_bounds(len(check_reads), rank, world)
+    P.find_matching_adapter_sets(check_reads[lo:hi], verbosity if rank == 0 else 0, end_size,
+                                 scoring_scheme_vals, print_dest, adapter_threshold, threads,
+                                 adapter_sets=adapter_sets)
+    search = [a for a in adapter_sets if '(full sequence)' not in a.name]
+    allreduce_set_scores(search, group)
+    return [a for a in search if a.best_start_or_end_score() >= adapter_threshold]
+
+
+def local_reads(reads, group=None, by_length=False):
+    """This rank's contiguous shard of `reads` and its [lo, hi) bounds."""
+    dist = _dist()
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if by_length:
+        lo, hi = shard_bounds_by_length([len(r.seq) for r in reads], rank, world)
+    else:
+        lo, hi = shard_bounds(len(reads), rank, world)
+    return reads[lo:hi], (lo, hi)
+
+
+def find_adapters_at_read_ends(reads, matching_sets, *args, group=None, **kwargs):
+    """Sharded end trimming: each rank trims its own shard of `reads` (no collective).
+    Returns (lo, hi) of the shard this rank processed."""
+    mine, bounds = local_reads(reads, group)
+    P.find_adapters_at_read_ends(mine, matching_sets, *args, **kwargs)
+    return bounds
+
+
+def find_adapters_in_read_middles(reads, matching_sets, *args, group=None, **kwargs):
+    """Sharded middle-adapter scan, shards balanced by bases (no collective). The scan reads each
+    read's end-trim amounts (NanoporeRead.get_seq_with_start_end_adapters_trimmed), so they must
+    be set on every read first: share_trims() after the sharded end trimming.
+    Returns (lo, hi) of the shard this rank processed."""
+    mine, bounds = local_reads(reads, group, by_length=True)
+    P.find_adapters_in_read_middles(mine, matching_sets, *args, **kwargs)
+    return bounds
+
+
+def share_trims(reads, bounds, group=None):
+    """Write every rank's end-trim amounts into all of `reads` (one all-gather, 16 B per read)."""
+    st, et = gather_trims(reads, bounds, group)
+    for r, s, e in zip(reads, st.tolist(), et.tolist()):
+        r.start_trim_amount, r.end_trim_amount = s, e
+
+
+def gather_trims(reads, bounds, group=None):
+    """All-gather the (start_trim, end_trim) amounts of every rank's shard into arrays over the
+    full read list (original order). `bounds` = the (lo, hi) this rank processed."""
+    dist = _dist()
+    lo, hi = bounds
+    mine = np.array([[r.start_trim_amount, r.end_trim_amount] for r in reads[lo:hi]], np.float64).reshape(-1, 2)
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return mine[:, 0].astype(np.int64), mine[:, 1].astype(np.int64)
+    world = dist.get_world_size(group)
+    sizes = _device_tensor([float(hi - lo)], group)
+    all_sizes = [sizes.clone() for _ in range(world)]
+    dist.all_gather(all_sizes, sizes, group=group)
+    counts = [int(s.item()) for s in all_sizes]
+    width = max(counts) if counts else 0
+    buf = np.zeros((width, 2), np.float64)
+    buf[:len(mine)] = mine
+    t = _device_tensor(buf.tolist() if width else [[0.0, 0.0]], group)
+    parts = [t.clone() for _ in range(world)]
+    dist.all_gather(parts, t, group=group)
+    rows = np.concatenate([p.cpu().numpy()[:c] for p, c in zip(parts, counts)], axis=0)
+    return rows[:, 0].astype(np.int64), rows[:, 1].astype(np.int64)

@@ -1,0 +1,131 @@
+"""Multi-process (world size 2, gloo, CPU) runs of the sharded drivers (custom_porechop_abi_amd/
+shards.py) against the reference's own decisions (tests/golden/g2_decisions.json.gz).
+
+Each rank aligns only its shard; the adapter-set search all-reduces the per-set maxima. The
+alignment backend is the CPU oracle here (engine.align swapped in every rank, as in
+test_drivers.py's 'oracle' backend), so this checks the sharding and the collective, not the
+kernels; the GPU runs use the same module with backend "nccl".
+"""
+import io
+import json
+import os
+import socket
+import tempfile
+
+import pytest
+
+from tests import golden_lib
+
+G2 = golden_lib.g2()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _records(case):
+    if case['input'] == 'synthetic_reads':
+        return [tuple(x) for x in G2['synthetic_reads']]
+    return golden_lib.load_records(case['input'])
+
+
+def _ranges(positions):
+    out = []
+    for p in sorted(positions):
+        if out and out[-1][1] == p:
+            out[-1][1] = p + 1
+        else:
+            out.append([p, p + 1])
+    return out
+
+
+def _worker(rank, world, port, case_name, out_dir):
+    import torch.distributed as dist
+    from custom_porechop_abi_amd import adapters as A, engine, porechop_abi as P, shards
+    from custom_porechop_abi_amd.nanopore_read import NanoporeRead
+    from tests import oracle_lib
+    engine.align = oracle_lib.align_windows            # CPU stand-in for the HIP kernels
+    dist.init_process_group('gloo', init_method='tcp://127.0.0.1:%d' % port, rank=rank, world_size=world)
+    try:
+        case = next(c for c in G2['cases'] if c['case'] == case_name)
+        opts = case['opts']
+        sink = io.StringIO()
+        sets = A.fresh_adapters()
+        reads = [NanoporeRead(n, s, q) for n, s, q in _records(case)]
+        sc = opts['scoring']
+        check = reads[:opts.get('check_reads', 10000)]
+        matching = shards.find_matching_adapter_sets(check, 0, opts['end_size'], sc, sink, opts['adapter_threshold'],
+                                                     1, adapter_sets=sets)
+        matching = P.fix_up_1d2_sets(matching)
+        set_scores = [[a.name, a.best_start_score, a.best_end_score] for a in sets
+                      if '(full sequence)' not in a.name]
+        matching = P.add_full_barcode_adapter_sets(matching)
+        ends = mids = (0, 0)
+        if matching:
+            ends = shards.find_adapters_at_read_ends(reads, matching, 0, opts['end_size'], opts['extra_end_trim'],
+                                                     opts['end_threshold'], sc, sink, opts['min_trim_size'], 1,
+                                                     False, 75.0, 5.0, False, None)
+            shards.share_trims(reads, ends)
+            mids = shards.find_adapters_in_read_middles(reads, matching, 0, opts['middle_threshold'], 10, 100, sc,
+                                                        sink, 1, False)
+        st, et = shards.gather_trims(reads, ends)
+        out = {'rank': rank, 'matching': [a.name for a in matching], 'set_scores': set_scores,
+               'ends': list(ends), 'mids': list(mids),
+               'trims': {r.name: [r.start_trim_amount, r.end_trim_amount] for r in reads[ends[0]:ends[1]]},
+               'middle': {r.name: _ranges(r.middle_adapter_positions) for r in reads[mids[0]:mids[1]]},
+               'gathered': [st.tolist(), et.tolist()]}
+        with open(os.path.join(out_dir, 'rank%d.json' % rank), 'w') as f:
+            json.dump(out, f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('case_name', ['two_adapter_sets', 'synthetic_default'])
+def test_sharded_drivers_match_reference(case_name):
+    import torch.multiprocessing as mp
+    world = 2
+    out_dir = tempfile.mkdtemp(prefix='pcabi_shards_')
+    mp.spawn(_worker, args=(world, _free_port(), case_name, out_dir), nprocs=world, join=True)
+    res = [json.load(open(os.path.join(out_dir, 'rank%d.json' % r))) for r in range(world)]
+    case = next(c for c in G2['cases'] if c['case'] == case_name)
+    exp_reads = {r['name']: r for r in case['reads']}
+    for r in res:
+        # the collective: every rank ends with the all-check-reads set maxima and the same sets
+        assert r['matching'] == case['matching']
+        assert r['set_scores'] == case['set_scores']
+    # the shards tile the read list and each read's decisions match the reference
+    assert res[0]['ends'][0] == 0 and res[0]['ends'][1] == res[1]['ends'][0]
+    assert res[1]['ends'][1] == len(case['reads'])
+    seen = {}
+    for r in res:
+        seen.update(r['trims'])
+    assert len(seen) == len(case['reads'])
+    for name, (s, e) in seen.items():
+        assert [s, e] == [exp_reads[name]['start_trim'], exp_reads[name]['end_trim']], name
+    mids = {}
+    for r in res:
+        mids.update(r['middle'])
+    assert len(mids) == len(case['reads'])
+    for name, pos in mids.items():
+        assert pos == exp_reads[name]['middle_pos'], name
+    # all-gathered trim amounts, original read order, identical on both ranks
+    exp_st = [r['start_trim'] for r in case['reads']]
+    exp_et = [r['end_trim'] for r in case['reads']]
+    for r in res:
+        assert r['gathered'] == [exp_st, exp_et]
+
+
+def test_shard_bounds():
+    from custom_porechop_abi_amd.shards import shard_bounds, shard_bounds_by_length
+    for n in (0, 1, 7, 100):
+        for w in (1, 2, 3, 8):
+            b = [shard_bounds(n, r, w) for r in range(w)]
+            assert b[0][0] == 0 and b[-1][1] == n and all(b[k][1] == b[k + 1][0] for k in range(w - 1))
+    lens = [100, 5000, 20, 20, 20, 8000, 300]
+    for w in (1, 2, 3, 4):
+        b = [shard_bounds_by_length(lens, r, w) for r in range(w)]
+        assert b[0][0] == 0 and b[-1][1] == len(lens) and all(b[k][1] == b[k + 1][0] for k in range(w - 1))
