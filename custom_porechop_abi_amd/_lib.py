@@ -70,6 +70,9 @@ def lib():
         'pcabi_end_trim_dev': ([c_p, c_i64, ctypes.c_int32, c_p, c_i64, ctypes.c_int32, c_i64, c_int,
                                 c_int, c_d, c_int, c_p, c_p, c_p, c_p, c_p], c_int),
         'pcabi_best_full_identity_dev': ([c_p, c_i64, c_i64, ctypes.c_int32, c_p, c_p], c_int),
+        'pcabi_first_hits_host': ([c_int, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_p, ctypes.c_int32, c_int, c_int,
+                                   c_int, c_int, c_d, c_p], c_int),
+        'pcabi_first_hit_dev': ([c_p, c_i64, c_i64, ctypes.c_int32, c_d, c_p, c_i64, c_p], c_int),
     }
     for name, (argtypes, restype) in sig.items():
         fn = getattr(L, name)
@@ -90,7 +93,7 @@ def exported_symbols():
             'pcabi_stream_sync', 'pcabi_event_create', 'pcabi_event_destroy', 'pcabi_event_record',
             'pcabi_event_elapsed_ms', 'pcabi_adapters_create', 'pcabi_adapters_destroy',
             'pcabi_tile_layout', 'pcabi_tile_windows_dev', 'pcabi_align_cross_dev', 'pcabi_end_trim_dev',
-            'pcabi_best_full_identity_dev']
+            'pcabi_best_full_identity_dev', 'pcabi_first_hits_host', 'pcabi_first_hit_dev']
 
 
 def check(rc, what):

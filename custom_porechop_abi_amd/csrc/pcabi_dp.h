@@ -648,6 +648,11 @@ struct LanePacked {
     uint32_t battr;        // packed attribute
     int slt_last, ht_last, hp_last;
     int32_t k_ge, k_go, k_gev, k_geh, neg2;
+    // Last-row scout of the inner columns (column_tail): the best so far as ONE corrected key
+    // (score | tag | attributes), its column, and the H-run descriptor at that column; the
+    // fields above are materialised from them before the last column (materialize()).
+    int32_t bkey, ls_prev;
+    int bhph, hph_last;    // 2 * (H-run length) + (a diagonal precedes the run)
 
     // tab: substitution-key table of this lane's read code, tab(s) = key increment of the
     // diagonal step into slot s (match / mismatch / padding), see pk::fill_sub_table.
@@ -737,7 +742,11 @@ struct LanePacked {
             if (PCABI_ROW_FENCE > 0 && (s % (PCABI_ROW_FENCE > 0 ? PCABI_ROW_FENCE : 1)) == 0) __builtin_amdgcn_sched_barrier(0);
 #endif
         }
-        // ---- row L ----
+        if (!LAST) {
+            column_tail(lv, lh, ls, j);
+            return;
+        }
+        // ---- row L (last column) ----
         const bool hcont = AFFINE ? (lhext || slt_last == LT_H) : (slt_last == LT_H);
         const int ht = hcont ? ht_last + 1 : 1;
         const int hp = hcont ? hp_last : (slt_last == LT_D ? 1 : 0);
@@ -767,6 +776,47 @@ struct LanePacked {
         if (AFFINE) { ht_last = ht; hp_last = hp; }
         else { ht_last = (lslt == LT_H) ? ht : 0; hp_last = (lslt == LT_H) ? hp : 0; }
         slt_last = lslt;
+    }
+
+    // Row-L scout of an inner column, with the reference's rules (S/align/dp_scout.h:175, strict
+    // '>' so the first maximum wins; start-state correction V, then H, then S). Affine: the
+    // corrected state is ONE max3 over re-tagged keys -- V (tag 3) beats H (tag 2) beats S
+    // (tag 0) on equal scores, and a higher score always wins -- so the correction costs no
+    // compares. Linear gaps: no correction, the S key's own tb (3 D, 2 V, 1 H) is the type.
+    PCABI_HD void column_tail(int32_t lv, int32_t lh, int32_t ls, int j) {
+        int32_t corr;
+        if (AFFINE) corr = max3i(lv | pk::TB3, (lh & ~pk::TBM) | pk::TB2, ls & ~pk::TBM);
+        else corr = ls;
+        // H-run at (L, j): continues when H extends (affine: lh tb 1) or when it opens from an
+        // S that itself ended in H (tb 1); a new run is preceded by a diagonal iff S was one.
+        const int32_t tsp = ls_prev & pk::TBM;
+        const bool hcont = (AFFINE && (lh & pk::TB1) != 0) || tsp == pk::TB1;
+        const int hph = hcont ? hph_last + 2 : 2 + (tsp == pk::TB3 ? 1 : 0);
+        const bool upd = corr > (bkey | ((1 << pk::SC_SH) - 1));   // score(corr) > score(bkey)
+        bkey = upd ? corr : bkey;
+        bj = upd ? j : bj;
+        bhph = upd ? hph : bhph;
+        hph_last = hph;
+        ls_prev = ls;
+    }
+
+    // Inner-column scout state -> the fields the last column and finish() use.
+    PCABI_HD void materialize(int L) {
+        const int t = pk::tb(bkey);
+        int lt;
+        if (bj == 0) lt = LT_NONE;                          // still the (L, 0) seed
+        else if (AFFINE) lt = t == 3 ? LT_V : (t == 2 ? LT_H : LT_D);
+        else lt = t == 3 ? LT_D : (t == 2 ? LT_V : LT_H);
+        bscore = pk::score(bkey);
+        bi = L;
+        battr = pk::attr(bkey);
+        blt = lt;
+        btrail = lt == LT_H ? (bhph >> 1) : 0;             // a V run in row L before the last
+        bprec = lt == LT_H ? (bhph & 1) : 0;               // column is a 1-column trail: 0 here
+        const int tp = pk::tb(ls_prev);
+        slt_last = tp == 0 ? LT_NONE : (tp == 3 ? LT_D : (tp == 2 ? LT_V : LT_H));
+        ht_last = hph_last >> 1;
+        hp_last = hph_last & 1;
     }
 };
 
@@ -804,16 +854,11 @@ PCABI_HD Result align_lane_packed(ReadFn &rd, int n, const TabFn &tabfn, int L, 
         st.HK[s] = neg | pk::TB1;
     }
     st.neg2 = neg | pk::TB2;
-    st.bscore = 0;
-    st.bi = L;
+    st.bkey = pk::start(-L);                       // the (L, 0) seed: score 0, c = -L
     st.bj = 0;
-    st.battr = (uint32_t)pk::start(-L);
-    st.blt = LT_NONE;
-    st.btrail = 0;
-    st.bprec = 0;
-    st.slt_last = LT_NONE;
-    st.ht_last = 0;
-    st.hp_last = 0;
+    st.bhph = 0;
+    st.hph_last = 0;
+    st.ls_prev = 0;                                // tb 0: no S before column 1
     int r = rd(1);
 #pragma unroll 1
     for (int j = 1; j < n; ++j) {
@@ -821,6 +866,7 @@ PCABI_HD Result align_lane_packed(ReadFn &rd, int n, const TabFn &tabfn, int L, 
         st.template column<decltype(tabfn(r)), false>(tabfn(r), j, L, off);
         r = rn;
     }
+    st.materialize(L);
     st.template column<decltype(tabfn(r)), true>(tabfn(r), n, L, off);
     Best b;
     b.score = st.bscore; b.bi = st.bi; b.bj = st.bj; b.attr = pk::to_std(st.battr, st.bj);

@@ -13,6 +13,9 @@
 //   k_end_trim                  per-read decision epilogue (nanopore_read.py:175-217).
 //   k_best_full_id              per-adapter max of the full-adapter identity
 //                               (nanopore_read.py:158-173), deterministic (max is exact).
+//   k_first_hit                 middle-scan round 1: first adapter over the threshold per read
+//                               (nanopore_read.py:219-252).
+//   k_tile_windows              window list -> tile layout (coalesced cross-mode reads).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -302,6 +305,34 @@ __global__ __launch_bounds__(256) void k_best_full_id(const int32_t *res, int64_
     }
 }
 
+// Middle-scan round 1 (porechop_abi/nanopore_read.py:219-252): per read, the FIRST adapter in
+// list order whose full-adapter identity is not below the threshold on the unmasked read. The
+// reference's loop hits exactly that adapter first (the ones before it fail on this same
+// sequence and are never revisited), so only this hit leaves the device: hits[f * hit_stride +
+// w] for f = adapter (-1 = none), rs, re (inclusive), m, l2.
+__global__ __launch_bounds__(256) void k_first_hit(const int32_t *res, int64_t stride, int64_t n_win,
+                                                   int32_t n_adp, double thr, int32_t *hits,
+                                                   int64_t hit_stride) {
+    const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (w >= n_win) return;
+    int32_t fa = -1, frs = -1, fre = 0, fm = 0, fl = 0;
+    for (int a = 0; a < n_adp; ++a) {
+        const int64_t i = (int64_t)a * n_win + w;
+        const int rs = res[0 * stride + i];
+        const int m = res[5 * stride + i], l2 = res[7 * stride + i];
+        const double full = (rs == -1) ? 0.0 : pcabi::pid6(m, l2);
+        if (!(full < thr)) {   // Python: `if full < middle_threshold: break` (NaN does not break)
+            fa = a; frs = rs; fre = res[1 * stride + i]; fm = m; fl = l2;
+            break;
+        }
+    }
+    hits[0 * hit_stride + w] = fa;
+    hits[1 * hit_stride + w] = frs;
+    hits[2 * hit_stride + w] = fre;
+    hits[3 * hit_stride + w] = fm;
+    hits[4 * hit_stride + w] = fl;
+}
+
 // ---- launch plumbing -------------------------------------------------------------------------
 
 // Tile layout of a window list (cross mode): windows [256t, 256t + 256) form tile t; dword
@@ -463,7 +494,7 @@ struct Engine {
     std::mutex mu;
     bool init = false;
     hipStream_t stream = nullptr;
-    DeviceBuf codes, woff, wlen, out, tasks_win, tasks_out, wave_adp, tiles, toff;
+    DeviceBuf codes, woff, wlen, out, tasks_win, tasks_out, wave_adp, tiles, toff, hits;
     DeviceBuf pad[kNumBuckets], len[kNumBuckets], id[kNumBuckets];
 };
 
@@ -531,11 +562,17 @@ void pcabi_pid6_host(const int32_t *m, const int32_t *l, int64_t n, double *out)
     for (int64_t k = 0; k < n; ++k) out[k] = pcabi::pid6(m[k], l[k]);
 }
 
-int pcabi_align_host(int device, const uint8_t *codes, int64_t codes_len, const int64_t *win_off,
-                     const int32_t *win_len, int64_t n_win, const uint8_t *adp_codes,
-                     const int32_t *adp_off, const int32_t *adp_len, int32_t n_adp,
-                     const int32_t *task_win, const int32_t *task_adp, int64_t n_task, int match,
-                     int mismatch, int gap_open, int gap_extend, int32_t *out) {
+}  // extern "C"
+
+namespace {
+
+// Shared body of pcabi_align_host / pcabi_first_hits_host. first_thr != nullptr (cross mode
+// only): out receives the k_first_hit fields (5 x n_win) instead of the raw results.
+int align_host_impl(int device, const uint8_t *codes, int64_t codes_len, const int64_t *win_off,
+                    const int32_t *win_len, int64_t n_win, const uint8_t *adp_codes,
+                    const int32_t *adp_off, const int32_t *adp_len, int32_t n_adp,
+                    const int32_t *task_win, const int32_t *task_adp, int64_t n_task, int match,
+                    int mismatch, int gap_open, int gap_extend, const double *first_thr, int32_t *out) {
     if (device < 0 || device >= 16) return fail(PCABI_E_ARG, "bad device index");
     if (n_win < 0 || n_adp < 0 || n_task < 0) return fail(PCABI_E_ARG, "negative count");
     if (int rc = check_common(adp_len, n_adp)) return rc;
@@ -660,9 +697,57 @@ int pcabi_align_host(int device, const uint8_t *codes, int64_t codes_len, const 
         HIP_TRY(hipGetLastError());
         // bucket buffers are reused across calls only; keep them distinct per bucket
     }
-    HIP_TRY(hipMemcpyAsync(out, e.out.p, sizeof(int32_t) * PCABI_NFIELDS * (size_t)n_res,
-                           hipMemcpyDeviceToHost, e.stream));
+    if (first_thr) {
+        if (int rc = e.hits.ensure(sizeof(int32_t) * 5 * (size_t)n_win)) return rc;
+        hipLaunchKernelGGL(k_first_hit, dim3((unsigned)((n_win + 255) / 256)), dim3(256), 0, e.stream,
+                           (const int32_t *)e.out.p, n_res, n_win, n_adp, *first_thr, (int32_t *)e.hits.p,
+                           n_win);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(out, e.hits.p, sizeof(int32_t) * 5 * (size_t)n_win, hipMemcpyDeviceToHost,
+                               e.stream));
+    } else {
+        HIP_TRY(hipMemcpyAsync(out, e.out.p, sizeof(int32_t) * PCABI_NFIELDS * (size_t)n_res,
+                               hipMemcpyDeviceToHost, e.stream));
+    }
     HIP_TRY(hipStreamSynchronize(e.stream));
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pcabi_align_host(int device, const uint8_t *codes, int64_t codes_len, const int64_t *win_off,
+                     const int32_t *win_len, int64_t n_win, const uint8_t *adp_codes,
+                     const int32_t *adp_off, const int32_t *adp_len, int32_t n_adp,
+                     const int32_t *task_win, const int32_t *task_adp, int64_t n_task, int match,
+                     int mismatch, int gap_open, int gap_extend, int32_t *out) {
+    return align_host_impl(device, codes, codes_len, win_off, win_len, n_win, adp_codes, adp_off, adp_len,
+                           n_adp, task_win, task_adp, n_task, match, mismatch, gap_open, gap_extend, nullptr,
+                           out);
+}
+
+int pcabi_first_hits_host(int device, const uint8_t *codes, int64_t codes_len, const int64_t *win_off,
+                          const int32_t *win_len, int64_t n_win, const uint8_t *adp_codes,
+                          const int32_t *adp_off, const int32_t *adp_len, int32_t n_adp, int match,
+                          int mismatch, int gap_open, int gap_extend, double threshold, int32_t *hits) {
+    if (n_win > 0 && n_adp == 0) {
+        for (int64_t w = 0; w < n_win; ++w) {
+            hits[w] = -1; hits[n_win + w] = -1; hits[2 * n_win + w] = 0; hits[3 * n_win + w] = 0;
+            hits[4 * n_win + w] = 0;
+        }
+        return 0;
+    }
+    return align_host_impl(device, codes, codes_len, win_off, win_len, n_win, adp_codes, adp_off, adp_len,
+                           n_adp, nullptr, nullptr, 0, match, mismatch, gap_open, gap_extend, &threshold, hits);
+}
+
+int pcabi_first_hit_dev(const int32_t *res, int64_t stride, int64_t n_win, int32_t n_adp, double threshold,
+                        int32_t *hits, int64_t hit_stride, void *stream) {
+    if (n_win <= 0) return 0;
+    hipLaunchKernelGGL(k_first_hit, dim3((unsigned)((n_win + 255) / 256)), dim3(256), 0, (hipStream_t)stream, res,
+                       stride, n_win, n_adp, threshold, hits, hit_stride);
+    HIP_TRY(hipGetLastError());
     return 0;
 }
 

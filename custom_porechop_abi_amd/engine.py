@@ -144,6 +144,27 @@ def align(windows, adapter_seqs, scoring_scheme_vals, pairs=None, device=0):
     return out
 
 
+def first_hits(windows, adapter_seqs, scoring_scheme_vals, threshold, device=0):
+    """Middle-scan round 1 on the GPU (pcabi_first_hits_host): for every window, the first adapter
+    in list order whose full-adapter identity is not below `threshold`.
+    Returns int32 (5, n_win): adapter index (-1 = none), rs, re (inclusive), m, l2."""
+    codes, offs, lens = windows
+    codes = np.ascontiguousarray(codes, dtype=np.uint8)
+    offs = np.ascontiguousarray(offs, dtype=np.int64)
+    lens = np.ascontiguousarray(lens, dtype=np.int32)
+    acodes, aoffs, alens = encode_adapters(adapter_seqs)
+    n_win = len(lens)
+    out = np.zeros((5, n_win), dtype=np.int32)
+    if n_win == 0:
+        return out
+    m, mm, go, ge = (int(x) for x in scoring_scheme_vals[:4])
+    rc = lib().pcabi_first_hits_host(device, _ptr(codes), codes.size, _ptr(offs), _ptr(lens), n_win,
+                                     _ptr(acodes), _ptr(aoffs), _ptr(alens), len(alens), m, mm, go, ge,
+                                     float(threshold), _ptr(out))
+    check(rc, 'pcabi_first_hits_host')
+    return out
+
+
 def pid6(m, l):
     """float('%f' % (100*m/l)) elementwise (NaN where l == 0), the reference's identity text
     round trip (porechop_abi/src/alignment.cpp:118-119, porechop_abi/nanopore_read.py:497-498)."""

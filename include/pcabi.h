@@ -172,6 +172,26 @@ int pcabi_end_trim_dev(const int32_t *start_res, int64_t start_stride, int32_t n
                        uint8_t *start_hit, uint8_t *end_hit, void *stream);
 
 /*
+ * Middle-adapter scan, round 1 (porechop_abi/nanopore_read.py:219-252): for every window
+ * (whole end-trimmed read) the FIRST adapter in list order whose full-adapter identity
+ * (pid2, compared after the "%f" round trip like the reference) is not below `threshold`.
+ * The reference's masked re-alignment loop hits exactly that adapter first; later rounds
+ * re-align the masked read against that adapter and the ones after it (pcabi_align_host pairs).
+ * hits: int32 SoA, 5 rows x n_win: adapter index (-1 = none), rs, re (inclusive), m, l2.
+ *   pcabi_first_hits_host : host buffers as pcabi_align_host (cross product, tiled on device);
+ *                           only the 20 B/read of hits come back over PCIe.
+ *   pcabi_first_hit_dev   : epilogue over a device cross-product result block (layout of
+ *                           pcabi_align_cross_dev), async on `stream`.
+ */
+int pcabi_first_hits_host(int device, const uint8_t *codes, int64_t codes_len, const int64_t *win_off,
+                          const int32_t *win_len, int64_t n_win, const uint8_t *adp_codes,
+                          const int32_t *adp_off, const int32_t *adp_len, int32_t n_adp,
+                          int match, int mismatch, int gap_open, int gap_extend, double threshold,
+                          int32_t *hits);
+int pcabi_first_hit_dev(const int32_t *res, int64_t stride, int64_t n_win, int32_t n_adp,
+                        double threshold, int32_t *hits, int64_t hit_stride, void *stream);
+
+/*
  * Adapter-set discovery reduction (porechop_abi/nanopore_read.py:158-173): for each adapter a
  * of a cross-product result block, best[a] = max(best[a], max_w pid2(a, w)).
  */

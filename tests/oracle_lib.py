@@ -95,3 +95,25 @@ def align_windows(windows, adapter_seqs, scoring, pairs=None, device=0):
     if len(pr) == 0:
         return np.zeros((8, 0), np.int32)
     return align_many(reads, list(adapter_seqs), (pr, pa), scoring)
+
+
+def first_hits_windows(windows, adapter_seqs, scoring, threshold, device=0):
+    """Drop-in for custom_porechop_abi_amd.engine.first_hits computed by the oracle (CPU): the
+    first adapter (list order) whose full identity is not below threshold, per window."""
+    from custom_porechop_abi_amd.engine import pid6
+    n_win = len(windows[2])
+    out = np.zeros((5, n_win), np.int32)
+    out[0] = -1
+    out[1] = -1
+    if n_win == 0 or not adapter_seqs:
+        return out
+    res = align_windows(windows, adapter_seqs, scoring)
+    n_adp = len(adapter_seqs)
+    full = np.where(res[0] == -1, 0.0, pid6(res[5], res[7])).reshape(n_adp, n_win)
+    strong = ~(full < threshold)
+    for w in range(n_win):
+        hit = np.nonzero(strong[:, w])[0]
+        if len(hit):
+            i = int(hit[0]) * n_win + w
+            out[:, w] = [int(hit[0]), res[0, i], res[1, i], res[5, i], res[7, i]]
+    return out

@@ -195,3 +195,31 @@ def test_device_abi_tiled_cross(gpu_lib, scheme):
     ok = exp[0] != -1
     assert np.array_equal(got[0], exp[0])
     assert np.array_equal(got[:, ok], exp[:, ok]), _first_diff(got, exp, reads, adps, n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('threshold', [90.0, 70.0])
+def test_first_hits_middle_round1(gpu_lib, threshold):
+    """Middle-scan round 1 (k_first_hit over a tiled cross product): first adapter over the
+    threshold per whole read, vs the oracle."""
+    from custom_porechop_abi_amd import engine
+    rng = random.Random(int(threshold))
+    adps = ['AATGTACTTCGTTCAGTTACGTATTGCT', 'GCAATACGTAACTGAACGAAGT', 'ACGTTTAGGCATTGCA',
+            'TTGGCCAAGGTT' * 3]
+    reads = []
+    for k in range(300):
+        n = rng.choice([0, 5, rng.randint(100, 4000)])
+        r = _rand_seq(rng, n, 'ACGT')
+        for _ in range(rng.randint(0, 2)):
+            if n > 60:
+                a = _mutate(rng, rng.choice(adps), rng.choice([0.0, 0.05, 0.15]))
+                p = rng.randint(0, n - len(a))
+                r = r[:p] + a + r[p + len(a):]
+        reads.append(r)
+    pack = engine.SeqPack(reads)
+    views = pack.views(np.zeros(len(reads), np.int64), pack.lengths)
+    sc = (3, -6, -5, -2)
+    got = engine.first_hits(views, adps, sc, threshold)
+    exp = oracle_lib.first_hits_windows(views, adps, sc, threshold)
+    assert (exp[0] >= 0).sum() > 20
+    assert np.array_equal(got, exp)
