@@ -73,6 +73,12 @@ def lib():
         'pcabi_first_hits_host': ([c_int, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_p, ctypes.c_int32, c_int, c_int,
                                    c_int, c_int, c_d, c_p], c_int),
         'pcabi_first_hit_dev': ([c_p, c_i64, c_i64, ctypes.c_int32, c_d, c_p, c_i64, c_p], c_int),
+        'pcabi_scan_create': ([c_p, ctypes.POINTER(c_p)], c_int),
+        'pcabi_scan_destroy': ([c_p], None),
+        'pcabi_middle_scan_dev': ([c_p, c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_int, c_int, c_d, c_p, c_i64, c_p],
+                                  c_i64),
+        'pcabi_middle_scan_host': ([c_int, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_p, ctypes.c_int32, c_int, c_int,
+                                    c_int, c_int, c_d, c_p, c_i64], c_i64),
     }
     for name, (argtypes, restype) in sig.items():
         fn = getattr(L, name)
@@ -93,7 +99,8 @@ def exported_symbols():
             'pcabi_stream_sync', 'pcabi_event_create', 'pcabi_event_destroy', 'pcabi_event_record',
             'pcabi_event_elapsed_ms', 'pcabi_adapters_create', 'pcabi_adapters_destroy',
             'pcabi_tile_layout', 'pcabi_tile_windows_dev', 'pcabi_align_cross_dev', 'pcabi_end_trim_dev',
-            'pcabi_best_full_identity_dev', 'pcabi_first_hits_host', 'pcabi_first_hit_dev']
+            'pcabi_best_full_identity_dev', 'pcabi_first_hits_host', 'pcabi_first_hit_dev', 'pcabi_scan_create',
+            'pcabi_scan_destroy', 'pcabi_middle_scan_dev', 'pcabi_middle_scan_host']
 
 
 def check(rc, what):

@@ -311,12 +311,12 @@ __global__ __launch_bounds__(256) void k_best_full_id(const int32_t *res, int64_
 // sequence and are never revisited), so only this hit leaves the device: hits[f * hit_stride +
 // w] for f = adapter (-1 = none), rs, re (inclusive), m, l2.
 __global__ __launch_bounds__(256) void k_first_hit(const int32_t *res, int64_t stride, int64_t n_win,
-                                                   int32_t n_adp, double thr, int32_t *hits,
-                                                   int64_t hit_stride) {
+                                                   int32_t n_adp, double thr, const int32_t *start_adp,
+                                                   int32_t *hits, int64_t hit_stride) {
     const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (w >= n_win) return;
     int32_t fa = -1, frs = -1, fre = 0, fm = 0, fl = 0;
-    for (int a = 0; a < n_adp; ++a) {
+    for (int a = start_adp ? start_adp[w] : 0; a < n_adp; ++a) {
         const int64_t i = (int64_t)a * n_win + w;
         const int rs = res[0 * stride + i];
         const int m = res[5 * stride + i], l2 = res[7 * stride + i];
@@ -333,12 +333,31 @@ __global__ __launch_bounds__(256) void k_first_hit(const int32_t *res, int64_t s
     hits[4 * hit_stride + w] = fl;
 }
 
+// Views of a subset of windows: sub[k] = window idx[k].
+__global__ __launch_bounds__(256) void k_gather_views(const int64_t *win_off, const int32_t *win_len,
+                                                      const int32_t *idx, int64_t n, int64_t *sub_off,
+                                                      int32_t *sub_len) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= n) return;
+    sub_off[k] = win_off[idx[k]];
+    sub_len[k] = win_len[idx[k]];
+}
+
+// Masking of a middle hit (nanopore_read.py:245: the hit's read span becomes '-', Dna5 N):
+// one block per hit, codes[win_off[w] + s .. win_off[w] + e) = 4.
+__global__ __launch_bounds__(256) void k_mask(uint8_t *codes, const int64_t *win_off, const int32_t *mwin,
+                                              const int32_t *ms, const int32_t *me) {
+    const int64_t h = blockIdx.x;
+    const int64_t base = win_off[mwin[h]];
+    for (int64_t i = ms[h] + threadIdx.x; i < me[h]; i += 256) codes[base + i] = 4;
+}
+
 // ---- launch plumbing -------------------------------------------------------------------------
 
 // Tile layout of a window list (cross mode): windows [256t, 256t + 256) form tile t; dword
 // (t, q, lane) = codes 4q..4q+3 of window 256t + lane, at tiles[tile_off[t] + 256q + lane].
 // Zero past each window's end. One block transposes 256 windows x 16 chunks through LDS: reads
-// are 64-byte runs of each window (offsets are 4-aligned), writes are 1 KB rows.
+// are 64-byte runs of each window (any offset), writes are 1 KB rows.
 // grid (n_tiles, <= 1024): blockIdx.y strides over 16-chunk slabs.
 __global__ __launch_bounds__(256) void k_tile_windows(const uint8_t *codes, const int64_t *win_off,
                                                       const int32_t *win_len, int64_t n_win,
@@ -356,7 +375,11 @@ __global__ __launch_bounds__(256) void k_tile_windows(const uint8_t *codes, cons
             if (w < n_win) {
                 const int n = win_len[w];
                 if (c0 < n) {
-                    v = *reinterpret_cast<const uint32_t *>(codes + win_off[w] + c0);
+                    // any window offset: two aligned dwords and a byte funnel shift
+                    const uint8_t *b = codes + win_off[w] + c0;
+                    const int sh = (int)((uintptr_t)b & 3);
+                    const uint32_t *q = reinterpret_cast<const uint32_t *>(b - sh);
+                    v = sh ? __builtin_amdgcn_alignbyte(q[1], q[0], sh) : q[0];
                     if (n - c0 < 4) v &= (1u << (8 * (n - c0))) - 1u;
                 }
             }
@@ -488,6 +511,16 @@ struct DeviceBuf {
     }
 };
 
+}  // namespace
+
+// Scratch of the device-resident middle scan (pcabi_middle_scan_dev), grown on demand.
+struct pcabi_scan {
+    const pcabi_adapters *adps = nullptr;
+    DeviceBuf tiles, toff, res, hits, idx, start, soff, slen, mwin, ms, me;
+};
+
+namespace {
+
 // Per-device state for the host-buffer API (serialised by a mutex: the legacy ABI is called
 // concurrently from the reference's ThreadPool workers, porechop_abi.py:228,418,504).
 struct Engine {
@@ -495,6 +528,7 @@ struct Engine {
     bool init = false;
     hipStream_t stream = nullptr;
     DeviceBuf codes, woff, wlen, out, tasks_win, tasks_out, wave_adp, tiles, toff, hits;
+    pcabi_scan *scan = nullptr;   // scratch of the middle scan (pcabi_middle_scan_host)
     DeviceBuf pad[kNumBuckets], len[kNumBuckets], id[kNumBuckets];
 };
 
@@ -579,8 +613,8 @@ int align_host_impl(int device, const uint8_t *codes, int64_t codes_len, const i
     for (int64_t w = 0; w < n_win; ++w) {
         if (win_len[w] < 0 || win_len[w] > pcabi::MAX_WINDOW_LEN)
             return fail(PCABI_E_ARG, "window length out of range");
-        if (win_len[w] > 0 && ((win_off[w] & 3) != 0 || win_off[w] < 0 || win_off[w] + win_len[w] + 16 > codes_len))
-            return fail(PCABI_E_ARG, "window offset misaligned or buffer not padded by 16 bytes");
+        if (win_len[w] > 0 && (win_off[w] < 0 || win_off[w] + win_len[w] + 16 > codes_len))
+            return fail(PCABI_E_ARG, "window outside the buffer or buffer not padded by 16 bytes");
     }
     const int64_t n_res = task_win ? n_task : (int64_t)n_adp * n_win;
     if (task_win)
@@ -700,8 +734,8 @@ int align_host_impl(int device, const uint8_t *codes, int64_t codes_len, const i
     if (first_thr) {
         if (int rc = e.hits.ensure(sizeof(int32_t) * 5 * (size_t)n_win)) return rc;
         hipLaunchKernelGGL(k_first_hit, dim3((unsigned)((n_win + 255) / 256)), dim3(256), 0, e.stream,
-                           (const int32_t *)e.out.p, n_res, n_win, n_adp, *first_thr, (int32_t *)e.hits.p,
-                           n_win);
+                           (const int32_t *)e.out.p, n_res, n_win, n_adp, *first_thr, nullptr,
+                           (int32_t *)e.hits.p, n_win);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(out, e.hits.p, sizeof(int32_t) * 5 * (size_t)n_win, hipMemcpyDeviceToHost,
                                e.stream));
@@ -742,11 +776,49 @@ int pcabi_first_hits_host(int device, const uint8_t *codes, int64_t codes_len, c
                            n_adp, nullptr, nullptr, 0, match, mismatch, gap_open, gap_extend, &threshold, hits);
 }
 
+int64_t pcabi_middle_scan_host(int device, const uint8_t *codes, int64_t codes_len, const int64_t *win_off,
+                               const int32_t *win_len, int64_t n_win, const uint8_t *adp_codes,
+                               const int32_t *adp_off, const int32_t *adp_len, int32_t n_adp, int match,
+                               int mismatch, int gap_open, int gap_extend, double threshold, int32_t *hits,
+                               int64_t cap) {
+    if (device < 0 || device >= 16) return fail(PCABI_E_ARG, "bad device index");
+    if (n_win < 0 || n_adp < 0 || cap < 0) return fail(PCABI_E_ARG, "negative count");
+    if (int rc = check_common(adp_len, n_adp)) return rc;
+    for (int64_t w = 0; w < n_win; ++w) {
+        if (win_len[w] < 0 || win_len[w] > pcabi::MAX_WINDOW_LEN)
+            return fail(PCABI_E_ARG, "window length out of range");
+        if (win_len[w] > 0 && (win_off[w] < 0 || win_off[w] + win_len[w] + 16 > codes_len))
+            return fail(PCABI_E_ARG, "window outside the buffer or buffer not padded by 16 bytes");
+    }
+    if (n_win == 0 || n_adp == 0) return 0;
+    Engine &e = g_engines[device];
+    std::lock_guard<std::mutex> lock(e.mu);
+    if (int rc = engine_init(e, device)) return rc;
+    HIP_TRY(hipSetDevice(device));
+    if (int rc = e.codes.ensure((size_t)codes_len)) return rc;
+    if (int rc = e.woff.ensure(sizeof(int64_t) * (size_t)n_win)) return rc;
+    if (int rc = e.wlen.ensure(sizeof(int32_t) * (size_t)n_win)) return rc;
+    HIP_TRY(hipMemcpyAsync(e.codes.p, codes, (size_t)codes_len, hipMemcpyHostToDevice, e.stream));
+    HIP_TRY(hipMemcpyAsync(e.woff.p, win_off, sizeof(int64_t) * (size_t)n_win, hipMemcpyHostToDevice, e.stream));
+    HIP_TRY(hipMemcpyAsync(e.wlen.p, win_len, sizeof(int32_t) * (size_t)n_win, hipMemcpyHostToDevice, e.stream));
+    pcabi_adapters *tab = nullptr;
+    if (int rc = pcabi_adapters_create(adp_codes, adp_off, adp_len, n_adp, &tab)) return rc;
+    if (!e.scan) e.scan = new pcabi_scan();
+    e.scan->adps = tab;
+    const int64_t r = pcabi_middle_scan_dev(e.scan, (uint8_t *)e.codes.p, (const int64_t *)e.woff.p,
+                                            (const int32_t *)e.wlen.p, win_len, n_win, match, mismatch, gap_open,
+                                            gap_extend, threshold, hits, cap, e.stream);
+    (void)hipStreamSynchronize(e.stream);
+    e.scan->adps = nullptr;
+    pcabi_adapters_destroy(tab);
+    return r;
+}
+
 int pcabi_first_hit_dev(const int32_t *res, int64_t stride, int64_t n_win, int32_t n_adp, double threshold,
                         int32_t *hits, int64_t hit_stride, void *stream) {
     if (n_win <= 0) return 0;
     hipLaunchKernelGGL(k_first_hit, dim3((unsigned)((n_win + 255) / 256)), dim3(256), 0, (hipStream_t)stream, res,
-                       stride, n_win, n_adp, threshold, hits, hit_stride);
+                       stride, n_win, n_adp, threshold, nullptr, hits, hit_stride);
     HIP_TRY(hipGetLastError());
     return 0;
 }
@@ -920,6 +992,123 @@ int pcabi_align_cross_dev(const uint32_t *tiles, const int64_t *tile_off, const 
     }
     HIP_TRY(hipGetLastError());
     return 0;
+}
+
+}  // extern "C"
+
+
+extern "C" {
+
+int pcabi_scan_create(const pcabi_adapters *adps, pcabi_scan **out) {
+    if (!adps || !out) return fail(PCABI_E_ARG, "bad arguments");
+    pcabi_scan *s = new pcabi_scan();
+    s->adps = adps;
+    *out = s;
+    return 0;
+}
+
+void pcabi_scan_destroy(pcabi_scan *s) {
+    if (!s) return;
+    for (DeviceBuf *b : {&s->tiles, &s->toff, &s->res, &s->hits, &s->idx, &s->start, &s->soff, &s->slen,
+                         &s->mwin, &s->ms, &s->me})
+        if (b->p) (void)hipFree(b->p);
+    delete s;
+}
+
+int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win_off, const int32_t *win_len,
+                              const int32_t *h_win_len, int64_t n_win, int match, int mismatch, int gap_open,
+                              int gap_extend, double threshold, int32_t *hits, int64_t cap, void *stream) {
+    if (!sc || n_win < 0 || cap < 0) return fail(PCABI_E_ARG, "bad arguments");
+    if (!(threshold > 0.0))
+        return fail(PCABI_E_ARG, "middle threshold must be > 0 (the reference's loop never ends otherwise)");
+    const hipStream_t st = (hipStream_t)stream;
+    const int32_t n_adp = sc->adps->n_adp;
+    if (n_win == 0 || n_adp == 0) return 0;
+    int64_t n_hits = 0;
+    std::vector<int32_t> cur, nxt, nxt_start, hm_w, hm_s, hm_e, lens;
+    std::vector<int32_t> hb;
+    std::vector<int64_t> toff;
+    for (int round = 0;; ++round) {
+        const int64_t n = round == 0 ? n_win : (int64_t)cur.size();
+        const int64_t *v_off = win_off;
+        const int32_t *v_len = win_len;
+        lens.resize((size_t)n);
+        if (round == 0) {
+            std::copy(h_win_len, h_win_len + n, lens.begin());
+        } else {
+            for (int64_t k = 0; k < n; ++k) lens[k] = h_win_len[cur[k]];
+            if (int rc = sc->idx.ensure(sizeof(int32_t) * n)) return rc;
+            if (int rc = sc->start.ensure(sizeof(int32_t) * n)) return rc;
+            if (int rc = sc->soff.ensure(sizeof(int64_t) * n)) return rc;
+            if (int rc = sc->slen.ensure(sizeof(int32_t) * n)) return rc;
+            HIP_TRY(hipMemcpyAsync(sc->idx.p, cur.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
+            HIP_TRY(hipMemcpyAsync(sc->start.p, nxt_start.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
+            hipLaunchKernelGGL(k_gather_views, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, win_off, win_len,
+                               (const int32_t *)sc->idx.p, n, (int64_t *)sc->soff.p, (int32_t *)sc->slen.p);
+            v_off = (const int64_t *)sc->soff.p;
+            v_len = (const int32_t *)sc->slen.p;
+        }
+        // tiles of this round's windows
+        toff.assign((size_t)((n + 255) / 256 + 1), 0);
+        int64_t max_nq = 0;
+        const int64_t nd = tile_layout(lens.data(), n, toff.data(), &max_nq);
+        int32_t max_len = 0;
+        for (int32_t l : lens) max_len = std::max(max_len, l);
+        if (int rc = sc->toff.ensure(sizeof(int64_t) * toff.size())) return rc;
+        if (int rc = sc->tiles.ensure(sizeof(uint32_t) * (size_t)nd)) return rc;
+        if (int rc = sc->res.ensure(sizeof(int32_t) * PCABI_NFIELDS * (size_t)n * n_adp)) return rc;
+        if (int rc = sc->hits.ensure(sizeof(int32_t) * 5 * (size_t)n)) return rc;
+        HIP_TRY(hipMemcpyAsync(sc->toff.p, toff.data(), sizeof(int64_t) * toff.size(), hipMemcpyHostToDevice, st));
+        launch_tiles(codes, v_off, v_len, n, (const int64_t *)sc->toff.p, max_nq, (uint32_t *)sc->tiles.p, st);
+        if (int rc = pcabi_align_cross_dev((const uint32_t *)sc->tiles.p, (const int64_t *)sc->toff.p, v_len, n,
+                                           max_len, sc->adps, match, mismatch, gap_open, gap_extend,
+                                           (int32_t *)sc->res.p, n * n_adp, stream))
+            return rc;
+        hipLaunchKernelGGL(k_first_hit, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                           (const int32_t *)sc->res.p, n * n_adp, n, n_adp, threshold,
+                           round == 0 ? nullptr : (const int32_t *)sc->start.p, (int32_t *)sc->hits.p, n);
+        HIP_TRY(hipGetLastError());
+        hb.resize((size_t)(5 * n));
+        HIP_TRY(hipMemcpyAsync(hb.data(), sc->hits.p, sizeof(int32_t) * 5 * n, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        nxt.clear(); nxt_start.clear(); hm_w.clear(); hm_s.clear(); hm_e.clear();
+        for (int64_t k = 0; k < n; ++k) {
+            const int32_t a = hb[k];
+            if (a < 0) continue;
+            const int32_t r = round == 0 ? (int32_t)k : cur[k];
+            const int32_t rs = hb[n + k], re = hb[2 * n + k];
+            const int32_t rend = rs == -1 ? 0 : re + 1;
+            if (n_hits < cap) {
+                hits[0 * cap + n_hits] = r;
+                hits[1 * cap + n_hits] = a;
+                hits[2 * cap + n_hits] = rs;
+                hits[3 * cap + n_hits] = rend;
+                hits[4 * cap + n_hits] = hb[3 * n + k];
+                hits[5 * cap + n_hits] = hb[4 * n + k];
+            }
+            ++n_hits;
+            nxt.push_back(r);
+            nxt_start.push_back(a);
+            if (rend > rs) { hm_w.push_back(r); hm_s.push_back(rs); hm_e.push_back(rend); }
+        }
+        if (nxt.empty()) break;
+        if (!hm_w.empty()) {
+            const size_t m = hm_w.size();
+            if (int rc = sc->mwin.ensure(sizeof(int32_t) * m)) return rc;
+            if (int rc = sc->ms.ensure(sizeof(int32_t) * m)) return rc;
+            if (int rc = sc->me.ensure(sizeof(int32_t) * m)) return rc;
+            HIP_TRY(hipMemcpyAsync(sc->mwin.p, hm_w.data(), sizeof(int32_t) * m, hipMemcpyHostToDevice, st));
+            HIP_TRY(hipMemcpyAsync(sc->ms.p, hm_s.data(), sizeof(int32_t) * m, hipMemcpyHostToDevice, st));
+            HIP_TRY(hipMemcpyAsync(sc->me.p, hm_e.data(), sizeof(int32_t) * m, hipMemcpyHostToDevice, st));
+            hipLaunchKernelGGL(k_mask, dim3((unsigned)m), dim3(256), 0, st, codes, win_off,
+                               (const int32_t *)sc->mwin.p, (const int32_t *)sc->ms.p, (const int32_t *)sc->me.p);
+            HIP_TRY(hipGetLastError());
+        }
+        cur.swap(nxt);
+        // host vectors uploaded above must stay intact until the copies ran
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    return n_hits;
 }
 
 int pcabi_end_trim_dev(const int32_t *start_res, int64_t start_stride, int32_t n_sa,

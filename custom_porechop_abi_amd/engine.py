@@ -2,8 +2,8 @@
 
 Sequences travel as Dna5 codes (A=0 C=1 G=2 T/U=3 other=4; the table of
 S/basic/alphabet_residue_tabs.h:113-140 in the reference's vendored SeqAn) packed in one
-byte buffer. A *window* is an (offset, length) view into that buffer; offsets are 4-byte
-aligned and the buffer carries 16 bytes of padding, as libpcabi requires (include/pcabi.h).
+byte buffer. A *window* is an (offset, length) view into that buffer (any offset); the buffer
+carries 16 bytes of padding past its last sequence, as libpcabi requires (include/pcabi.h).
 
 The reference encodes each Python str with UTF-8 before handing it to SeqAn
 (porechop_abi/cpp_function_wrappers.py:52), so a non-ASCII character becomes several N codes;
@@ -60,26 +60,12 @@ class SeqPack(object):
         return len(self.lengths)
 
     def views(self, starts, lengths, index=None):
-        """Window views [start, start+len) of packed sequences (start relative to each sequence).
-        Starts that are not 4-aligned are re-packed (copied) so the kernel's dword reads stay
-        aligned; returns (codes, offsets, lengths)."""
+        """Window views [start, start+len) of packed sequences (start relative to each sequence):
+        (codes, offsets, lengths). No copy -- the kernels accept any offset."""
         idx = np.arange(len(self.lengths)) if index is None else np.asarray(index)
         starts = np.asarray(starts, dtype=np.int64)
         lengths = np.asarray(lengths, dtype=np.int32)
-        abs_off = self.offsets[idx] + starts
-        if np.all((abs_off & 3) == 0):
-            return self.codes, abs_off, lengths
-        # re-pack: one copy of every window at an aligned slot
-        stride_off = np.zeros(len(idx), dtype=np.int64)
-        padded = (lengths.astype(np.int64) + 3) & ~3
-        stride_off[1:] = np.cumsum(padded)[:-1]
-        total = int(padded.sum()) + PAD
-        out = np.full(total, 4, dtype=np.uint8)
-        for k in range(len(idx)):
-            n = int(lengths[k])
-            if n:
-                out[stride_off[k]:stride_off[k] + n] = self.codes[abs_off[k]:abs_off[k] + n]
-        return out, stride_off, lengths
+        return self.codes, self.offsets[idx] + starts, lengths
 
 
 def start_end_windows(pack, end_size):
@@ -163,6 +149,32 @@ def first_hits(windows, adapter_seqs, scoring_scheme_vals, threshold, device=0):
                                      float(threshold), _ptr(out))
     check(rc, 'pcabi_first_hits_host')
     return out
+
+
+def middle_scan(windows, adapter_seqs, scoring_scheme_vals, threshold, device=0):
+    """The reference's masked re-alignment loop (nanopore_read.py:219-252) for a batch of reads,
+    in rounds on the GPU (pcabi_middle_scan_host). Returns int32 (6, n_hits): read, adapter,
+    read_start, read_end (exclusive), m, l2, in discovery order (per read: the reference's order)."""
+    codes, offs, lens = windows
+    codes = np.ascontiguousarray(codes, dtype=np.uint8)
+    offs = np.ascontiguousarray(offs, dtype=np.int64)
+    lens = np.ascontiguousarray(lens, dtype=np.int32)
+    acodes, aoffs, alens = encode_adapters(adapter_seqs)
+    n_win = len(lens)
+    if n_win == 0 or not len(alens):
+        return np.zeros((6, 0), np.int32)
+    m, mm, go, ge = (int(x) for x in scoring_scheme_vals[:4])
+    cap = max(1024, n_win // 4)
+    while True:
+        out = np.zeros((6, cap), dtype=np.int32)
+        n = lib().pcabi_middle_scan_host(device, _ptr(codes), codes.size, _ptr(offs), _ptr(lens), n_win,
+                                         _ptr(acodes), _ptr(aoffs), _ptr(alens), len(alens), m, mm, go, ge,
+                                         float(threshold), _ptr(out), cap)
+        if n < 0:
+            check(int(n), 'pcabi_middle_scan_host')
+        if n <= cap:
+            return out[:, :n]
+        cap = int(n)
 
 
 def pid6(m, l):

@@ -242,13 +242,10 @@ def middle_adapter_list(matching_sets):
 
 def scan_middles(seqs, adapter_seqs, middle_threshold, scoring_scheme_vals, device=0):
     """Exact batched equivalent of the reference's masked re-alignment loop
-    (porechop_abi/nanopore_read.py:219-252).
-
-    Round 1 aligns every read against every adapter on the GPU and brings back only each read's
-    FIRST adapter over the threshold (engine.first_hits: the reference's loop hits exactly that
-    adapter first, the adapters before it fail on the same unmasked sequence and are never
-    revisited). Each later round re-aligns the reads that just got a hit, now masked with '-'
-    (Dna5 N), against that adapter and the ones after it (explicit pairs), until no read hits.
+    (porechop_abi/nanopore_read.py:219-252), run on the GPU in rounds (engine.middle_scan,
+    pcabi_middle_scan_host): round 1 keeps each read's first adapter over the threshold, later
+    rounds re-align only the reads that just hit -- masked with '-' (Dna5 N) -- from that adapter
+    onwards.
 
     Returns, per read, the ordered list of hits (adapter_index, full_identity, read_start,
     read_end) that nanopore_read.find_middle_adapters would record."""
@@ -258,44 +255,11 @@ def scan_middles(seqs, adapter_seqs, middle_threshold, scoring_scheme_vals, devi
         return hits
     pack = SeqPack(seqs)
     views = pack.views(np.zeros(n, np.int64), pack.lengths)
-    n_adp = len(adapter_seqs)
-    next_adp = np.zeros(n, dtype=np.int64)
-
-    def record(r, a, full, s0, e0):
-        hits[r].append((a, full, s0, e0))
-        pack.codes[pack.offsets[r] + s0:pack.offsets[r] + e0] = 4   # '-' -> Dna5 N
-        next_adp[r] = a
-
-    # round 1: first hit per read, on the device
-    fh = engine.first_hits(views, adapter_seqs, scoring_scheme_vals, middle_threshold, device=device)
-    rows = np.nonzero(fh[0] >= 0)[0]
-    full1 = engine.pid6(fh[3, rows], fh[4, rows])
-    for k, r in enumerate(rows.tolist()):
-        failed = fh[1, r] == -1
-        record(r, int(fh[0, r]), 0.0 if failed else float(full1[k]), int(fh[1, r]),
-               0 if failed else int(fh[2, r]) + 1)
-    active = rows.astype(np.int64)
-    while len(active):
-        # pairs: every active read against adapters next_adp[read]..end, adapter-major
-        reps = (n_adp - next_adp[active]).astype(np.int64)
-        pr = np.repeat(active, reps)
-        first = np.repeat(next_adp[active], reps)
-        offs = np.arange(len(pr)) - np.repeat(np.cumsum(reps) - reps, reps)
-        pa = first + offs
-        res = engine.align(views, adapter_seqs, scoring_scheme_vals, pairs=(pr, pa), device=device)
-        full, _, rs, re_ = identities(res)
-        strong = full >= middle_threshold
-        nxt = []
-        start = 0
-        for k, r in enumerate(active.tolist()):
-            cnt = int(reps[k])
-            seg = strong[start:start + cnt]
-            if seg.any():
-                q = start + int(np.argmax(seg))
-                record(r, int(pa[q]), float(full[q]), int(rs[q]), int(re_[q]))
-                nxt.append(r)
-            start += cnt
-        active = np.array(nxt, dtype=np.int64)
+    h = engine.middle_scan(views, adapter_seqs, scoring_scheme_vals, middle_threshold, device=device)
+    full = engine.pid6(h[4], h[5])
+    full[h[2] == -1] = 0.0
+    for r, a, s0, e0, f in zip(h[0].tolist(), h[1].tolist(), h[2].tolist(), h[3].tolist(), full.tolist()):
+        hits[r].append((a, f, s0, e0))
     return hits
 
 

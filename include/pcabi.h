@@ -18,7 +18,7 @@
  *  2. Batch ABI used by the batched phase drivers (replacing the per-read ThreadPool loops of
  *     porechop_abi/porechop_abi.py:200-245, 359-438, 457-522). Sequences are Dna5 codes
  *     (A=0 C=1 G=2 T/U=3 anything else=4, S/basic/alphabet_residue_tabs.h:113-140) packed in
- *     one byte buffer; a "window" is an (offset, length) view into it, offsets multiple of 4,
+ *     one byte buffer; a "window" is an (offset, length) view into it (any offset), the
  *     buffer padded with >= 16 readable bytes past the last window. Results are SoA int32,
  *     8 fields x n_results, field order PCABI_F_*.
  *
@@ -190,6 +190,35 @@ int pcabi_first_hits_host(int device, const uint8_t *codes, int64_t codes_len, c
                           int32_t *hits);
 int pcabi_first_hit_dev(const int32_t *res, int64_t stride, int64_t n_win, int32_t n_adp,
                         double threshold, int32_t *hits, int64_t hit_stride, void *stream);
+
+/*
+ * The whole middle-adapter scan (porechop_abi/nanopore_read.py:219-252, the masked re-alignment
+ * loop of find_middle_adapters) for a batch of end-trimmed reads, in rounds on the device:
+ * round 1 aligns every read against every adapter and keeps each read's first hit
+ * (k_first_hit); every later round masks the new hits in place (codes -> N, the reference's
+ * '-') and re-aligns only the reads that just hit, from the adapter that hit onwards, until no
+ * read hits. Hits are written to `hits` (HOST int32, 6 rows x cap: read, adapter, read_start,
+ * read_end (exclusive), m, l2 -- full identity = pid6(m, l2)) in discovery order, which per read
+ * is the reference's order. Returns the number of hits (may exceed cap: only the first cap are
+ * written) or a negative error. threshold must be > 0 (the reference never terminates otherwise).
+ *   pcabi_scan_create / destroy : scratch for one adapter table (current device).
+ *   pcabi_middle_scan_dev       : codes/win_off/win_len are DEVICE pointers (codes are masked in
+ *                                 place), h_win_len the host copy of the lengths.
+ *   pcabi_middle_scan_host      : host buffers (as pcabi_align_host), copies in, scans.
+ */
+typedef struct pcabi_scan pcabi_scan;
+int pcabi_scan_create(const pcabi_adapters *adps, pcabi_scan **out);
+void pcabi_scan_destroy(pcabi_scan *s);
+int64_t pcabi_middle_scan_dev(pcabi_scan *s, uint8_t *codes, const int64_t *win_off,
+                              const int32_t *win_len, const int32_t *h_win_len, int64_t n_win,
+                              int match, int mismatch, int gap_open, int gap_extend,
+                              double threshold, int32_t *hits, int64_t cap, void *stream);
+int64_t pcabi_middle_scan_host(int device, const uint8_t *codes, int64_t codes_len,
+                               const int64_t *win_off, const int32_t *win_len, int64_t n_win,
+                               const uint8_t *adp_codes, const int32_t *adp_off,
+                               const int32_t *adp_len, int32_t n_adp, int match, int mismatch,
+                               int gap_open, int gap_extend, double threshold, int32_t *hits,
+                               int64_t cap);
 
 /*
  * Adapter-set discovery reduction (porechop_abi/nanopore_read.py:158-173): for each adapter a

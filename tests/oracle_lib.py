@@ -117,3 +117,24 @@ def first_hits_windows(windows, adapter_seqs, scoring, threshold, device=0):
             i = int(hit[0]) * n_win + w
             out[:, w] = [int(hit[0]), res[0, i], res[1, i], res[5, i], res[7, i]]
     return out
+
+
+def middle_scan_windows(windows, adapter_seqs, scoring, threshold, device=0):
+    """Drop-in for custom_porechop_abi_amd.engine.middle_scan computed by the oracle (CPU): the
+    reference's loop (porechop_abi/nanopore_read.py:236-246) restated per read -- for each adapter
+    in order, re-align while the full identity is not below the threshold, masking each hit."""
+    from custom_porechop_abi_amd.engine import pid6
+    codes, offs, lens = windows
+    out = []
+    for w, (o, l) in enumerate(zip(offs.tolist(), lens.tolist())):
+        masked = _LETTERS[codes[o:o + l]].tobytes().decode()
+        for a, adp in enumerate(adapter_seqs):
+            while True:
+                r = align(masked, adp, scoring)
+                full = 0.0 if r[0] == -1 else float(pid6(np.array([r[5]]), np.array([r[7]]))[0])
+                if full < threshold:
+                    break
+                rs, rend = (r[0], r[1] + 1) if r[0] != -1 else (-1, 0)
+                masked = masked[:rs] + '-' * (rend - rs) + masked[rend:]
+                out.append([w, a, rs, rend, r[5], r[7]])
+    return np.array(out, np.int32).reshape(-1, 6).T.copy()

@@ -80,5 +80,5 @@ def test_window_views_match_python_slices():
         for k, s in enumerate(seqs):
             for (codes, off, ln), sl in ((sw, s[:E]), (ew, s[-E:])):
                 got = codes[off[k]:off[k] + ln[k]]
-                assert off[k] % 4 == 0
+                assert off[k] + ln[k] + 16 <= len(codes)      # the ABI's tail padding
                 assert np.array_equal(got, engine.encode_seq(sl))

@@ -152,7 +152,12 @@ def test_device_abi_tiled_cross(gpu_lib, scheme):
     reads, adps = _case_set(31, 700, 7, 3000, 64)
     pack = engine.SeqPack(reads)
     n = len(reads)
-    lens = pack.lengths.astype(np.int32)
+    # windows seq[k:] with random (unaligned) starts k
+    rng = random.Random(5)
+    starts = np.array([rng.randint(0, min(7, len(r))) for r in reads], np.int64)
+    _, offs, lens = pack.views(starts, (pack.lengths - starts).astype(np.int32))
+    reads = [r[k:] for r, k in zip(reads, starts.tolist())]
+    lens = lens.astype(np.int32)
     toff = np.zeros((n + 255) // 256 + 1, np.int64)
     nd = L.pcabi_tile_layout(lens.ctypes.data_as(vp), n, toff.ctypes.data_as(vp))
     assert nd == toff[-1] > 0
@@ -166,7 +171,7 @@ def test_device_abi_tiled_cross(gpu_lib, scheme):
         bufs.append(p)
         return p
 
-    d_codes, d_off, d_len, d_toff = h2d(pack.codes), h2d(pack.offsets), h2d(lens), h2d(toff)
+    d_codes, d_off, d_len, d_toff = h2d(pack.codes), h2d(offs), h2d(lens), h2d(toff)
     d_tiles = vp()
     _lib.check(L.pcabi_dev_malloc(ctypes.byref(d_tiles), 4 * int(nd)), 'malloc')
     bufs.append(d_tiles)
@@ -223,3 +228,33 @@ def test_first_hits_middle_round1(gpu_lib, threshold):
     exp = oracle_lib.first_hits_windows(views, adps, sc, threshold)
     assert (exp[0] >= 0).sum() > 20
     assert np.array_equal(got, exp)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('scheme', [(3, -6, -5, -2), (2, -1, -1, -1)])
+def test_middle_scan_rounds(gpu_lib, scheme):
+    """The whole masked re-alignment loop on the device (pcabi_middle_scan_host) vs the
+    reference's loop restated on the oracle: reads carrying 0-4 adapters, repeats of the same
+    adapter (several rounds), adjacent hits, empty and tiny reads."""
+    from custom_porechop_abi_amd import engine
+    rng = random.Random(sum(scheme) + 100)
+    adps = ['AATGTACTTCGTTCAGTTACGTATTGCT', 'GCAATACGTAACTGAACGAAGT', 'ACGTTTAGGCATTGCA']
+    reads = []
+    for k in range(160):
+        n = rng.choice([0, 3, rng.randint(200, 3000)])
+        r = _rand_seq(rng, n, 'ACGT')
+        for _ in range(rng.choice([0, 0, 1, 2, 4])):
+            if len(r) > 80:
+                a = _mutate(rng, rng.choice(adps), rng.choice([0.0, 0.03, 0.1]))
+                p = rng.randint(0, len(r))
+                r = r[:p] + a + (a if rng.random() < 0.2 else '') + r[p:]
+        reads.append(r)
+    pack = engine.SeqPack(reads)
+    views = pack.views(np.zeros(len(reads), np.int64), pack.lengths)
+    got = engine.middle_scan(views, adps, scheme, 85.0)
+    exp = oracle_lib.middle_scan_windows(views, adps, scheme, 85.0)
+    assert exp.shape[1] > 40 and np.bincount(exp[0]).max() >= 3
+    # per read, the hits in discovery order
+    order_g = np.lexsort((np.arange(got.shape[1]), got[0]))
+    order_e = np.lexsort((np.arange(exp.shape[1]), exp[0]))
+    assert np.array_equal(got[:, order_g], exp[:, order_e])
