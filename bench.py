@@ -51,6 +51,10 @@ def parse():
     ap.add_argument('--cpu-sample', type=int, default=12000, help='reads in the CPU-baseline sample (0 = skip)')
     ap.add_argument('--cpu-threads', type=int, default=0, help='0 = min(16, cpus available)')
     ap.add_argument('--check', type=int, default=256, help='reads checked against the oracle after timing')
+    ap.add_argument('--workload', choices=['endtrim', 'middle'], default='endtrim',
+                    help='endtrim: the headline metric (default); middle: end trim + middle-adapter scan '
+                         '(BASELINE.json configs[2])')
+    ap.add_argument('--middle-threshold', type=float, default=90.0)
     return ap.parse_args()
 
 
@@ -69,6 +73,8 @@ def main():
     from custom_porechop_abi_amd.engine import encode_adapters
     L = _lib.lib()
     _lib.check(L.pcabi_dev_set(local), 'pcabi_dev_set')
+    if args.workload == 'middle':
+        return run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapters)
 
     # ---- workload (host) ----
     sets = [a for a in A.fresh_adapters() if '(full sequence)' not in a.name][:args.sets]
@@ -267,6 +273,238 @@ def main():
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapters):
+    """BASELINE.json configs[2]: end trim + middle-adapter scan of whole synthetic reads (mean 8 kb)
+    against the first 50 adapter sets. One step, inputs resident in HBM:
+      pristine read pack -> working copy (the scan masks hits in place)
+      start/end windows -> tiles -> k_align -> k_end_trim                (as the headline step)
+      trim amounts -> host -> trimmed-read views                         (16 B/read each way)
+      pcabi_middle_scan_dev: round 1 every trimmed read x every middle adapter (tiled cross
+      product + k_first_hit), then rounds over the reads that just hit, masked, until none hits
+    value = reads / step time (all ranks, max over ranks)."""
+    from custom_porechop_abi_amd.porechop_abi import middle_adapter_list
+    vp = ctypes.c_void_p
+    sets = [a for a in A.fresh_adapters() if '(full sequence)' not in a.name][:args.sets]
+    start_adps = [a.start_sequence[1] for a in sets if a.start_sequence]
+    end_adps = [a.end_sequence[1] for a in sets if a.end_sequence]
+    mid_adps = [x[1] for x in middle_adapter_list(sets)[0]]
+    n, E = args.reads, args.end_size
+    t0 = time.time()
+    reads = synth.make_reads(n, args.mean_len, seed=12345 + rank)
+    lens = np.array([len(r) for r in reads], np.int64)
+    offs = np.zeros(n, np.int64)
+    offs[1:] = np.cumsum((lens + 3) & ~3)[:-1]
+    pack = np.full(int(offs[-1] + lens[-1]) + 64, 4, np.uint8)
+    for k, r in enumerate(reads):
+        pack[offs[k]:offs[k] + lens[k]] = r
+    s_len = np.minimum(lens, E).astype(np.int32)
+    e_len = s_len.copy()
+    s_off = offs.copy()
+    e_off = offs + lens - e_len
+    gen_s = time.time() - t0
+
+    def dalloc(nbytes):
+        p = vp()
+        _lib.check(L.pcabi_dev_malloc(ctypes.byref(p), max(int(nbytes), 16)), 'malloc')
+        return p
+
+    def h2d(arr):
+        arr = np.ascontiguousarray(arr)
+        p = dalloc(arr.nbytes)
+        _lib.check(L.pcabi_dev_h2d(p, arr.ctypes.data_as(vp), arr.nbytes), 'h2d')
+        return p
+
+    def table(lst):
+        c, o, l = encode_adapters(lst)
+        t = vp()
+        _lib.check(L.pcabi_adapters_create(c.ctypes.data_as(vp), o.ctypes.data_as(vp), l.ctypes.data_as(vp),
+                                           len(lst), ctypes.byref(t)), 'adapters_create')
+        return t
+
+    d_pristine = h2d(pack)
+    d_work = dalloc(pack.nbytes)
+    d_offs, d_lens = h2d(offs), h2d(lens.astype(np.int32))
+    n_sa, n_ea = len(start_adps), len(end_adps)
+    d_sres, d_eres = dalloc(4 * 8 * n_sa * n), dalloc(4 * 8 * n_ea * n)
+    d_st, d_et = dalloc(4 * n), dalloc(4 * n)
+    d_toff_mid, d_tlen_mid = dalloc(8 * n), dalloc(4 * n)
+    stream = vp()
+    _lib.check(L.pcabi_stream_create(ctypes.byref(stream)), 'stream')
+    sc = (3, -6, -5, -2)
+    sides = []
+    for w_off, w_len, adps, d_res in ((s_off, s_len, start_adps, d_sres), (e_off, e_len, end_adps, d_eres)):
+        toff = np.zeros((n + 255) // 256 + 1, np.int64)
+        nd = L.pcabi_tile_layout(w_len.ctypes.data_as(vp), n, toff.ctypes.data_as(vp))
+        sides.append(dict(d_off=h2d(w_off), d_len=h2d(w_len), d_toff=h2d(toff), d_tiles=dalloc(4 * nd),
+                          mq=int(np.diff(toff).max() // 256), mx=int(w_len.max()), tab=table(adps), d_res=d_res,
+                          stride=len(adps) * n))
+    mid_tab = table(mid_adps)
+    scan = vp()
+    _lib.check(L.pcabi_scan_create(mid_tab, ctypes.byref(scan)), 'scan_create')
+    cap = max(4096, n)
+    hits = np.zeros((6, cap), np.int32)
+    trims = np.zeros((2, n), np.int32)
+    t_off = np.zeros(n, np.int64)
+    t_len = np.zeros(n, np.int32)
+    stats = {}
+
+    def step():
+        _lib.check(L.pcabi_dev_copy_async(d_work, d_pristine, pack.nbytes, 2, stream), 'copy')
+        for sd in sides:
+            _lib.check(L.pcabi_tile_windows_dev(d_work, sd['d_off'], sd['d_len'], n, sd['d_toff'], sd['mq'],
+                                                sd['d_tiles'], stream), 'tile')
+            _lib.check(L.pcabi_align_cross_dev(sd['d_tiles'], sd['d_toff'], sd['d_len'], n, sd['mx'], sd['tab'], *sc,
+                                               sd['d_res'], sd['stride'], stream), 'align')
+        _lib.check(L.pcabi_end_trim_dev(d_sres, n_sa * n, n_sa, d_eres, n_ea * n, n_ea, n, E, 2, 75.0, 4, d_st, d_et,
+                                        None, None, stream), 'end_trim')
+        _lib.check(L.pcabi_dev_copy_async(trims[0].ctypes.data_as(vp), d_st, 4 * n, 1, stream), 'd2h')
+        _lib.check(L.pcabi_dev_copy_async(trims[1].ctypes.data_as(vp), d_et, 4 * n, 1, stream), 'd2h')
+        _lib.check(L.pcabi_stream_sync(stream), 'sync')
+        t1 = time.perf_counter()
+        # NanoporeRead.get_seq_with_start_end_adapters_trimmed (nanopore_read.py:44-49)
+        np.add(offs, trims[0], out=t_off)
+        np.maximum(lens - trims[0] - trims[1], 0, out=t_len, casting='unsafe')
+        _lib.check(L.pcabi_dev_copy_async(d_toff_mid, t_off.ctypes.data_as(vp), 8 * n, 0, stream), 'h2d')
+        _lib.check(L.pcabi_dev_copy_async(d_tlen_mid, t_len.ctypes.data_as(vp), 4 * n, 0, stream), 'h2d')
+        nh = L.pcabi_middle_scan_dev(scan, d_work, d_toff_mid, d_tlen_mid, t_len.ctypes.data_as(vp), n, *sc,
+                                     args.middle_threshold, hits.ctypes.data_as(vp), cap, stream)
+        if nh < 0:
+            _lib.check(int(nh), 'middle_scan')
+        stats['hits'] = int(nh)
+        stats['middle_s'] = stats.get('middle_s', 0.0) + time.perf_counter() - t1
+
+    for _ in range(args.warmup):
+        step()
+    _lib.check(L.pcabi_stream_sync(stream), 'sync')
+    stats['middle_s'] = 0.0
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize() if torch.cuda.is_available() else None
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    L.pcabi_stream_sync(stream)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device='cuda')
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    checked = None
+    if args.check and rank == 0:
+        checked = middle_spot_check(reads, trims, hits, stats['hits'], mid_adps, sc, args.middle_threshold,
+                                    min(args.check, 64))
+    Lm = np.array([len(x) for x in mid_adps], np.int64)
+    cells_mid = int(t_len.astype(np.int64).sum() * Lm.sum())
+    cells_end = int(s_len.astype(np.int64).sum() * sum(map(len, start_adps)) +
+                    e_len.astype(np.int64).sum() * sum(map(len, end_adps)))
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        cpu = cpu_baseline_middle(reads[:max(1, args.cpu_sample // 40)], trims, mid_adps, sc, args.middle_threshold,
+                                  args.cpu_threads)
+    if rank == 0:
+        step_ms = 1e3 * elapsed / args.steps
+        value = world * n * args.steps / elapsed
+        out = {
+            'metric': 'reads/sec trimmed + middle-adapter scan (ONT reads x 50 adapter sets)',
+            'value': round(value, 1), 'unit': 'reads/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(step_ms, 3), 'higher_is_better': True,
+            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'int32',
+            'data': 'synthetic (seeded ONT-like reads, SURVEY.md §8d recipe; mean %d bp)' % args.mean_len,
+            'config': {'workload': 'end trim + middle scan: %d whole reads/GPU (mean %d bp) x %d adapter sets '
+                                   '(%d start, %d end, %d middle adapters), threshold %.0f'
+                                   % (n, args.mean_len, len(sets), n_sa, n_ea, len(mid_adps), args.middle_threshold),
+                       'reads_per_gpu': n, 'adapter_sets': len(sets), 'scoring': list(sc),
+                       'parallelism': 'dp%d (read shards)' % world},
+            'middle_ms_per_step': round(1e3 * stats['middle_s'] / args.steps, 3),
+            'middle_hits_per_step': stats['hits'],
+            'cells_per_step': {'end_windows': cells_end, 'middle_round1': cells_mid},
+            'gcups_step': round((cells_end + cells_mid) / (step_ms * 1e-3) / 1e9, 1),
+            'cpu_baseline': cpu,
+            'gpu_vs_cpu': round(value / cpu['value'], 1) if cpu else None,
+            'parity_spot_check': checked,
+            'setup_s': round(gen_s, 2),
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def middle_spot_check(reads, trims, hits, n_hits, mid_adps, sc, thr, k):
+    """First k reads: trimmed sequence (from the device's trim amounts) through the reference's
+    middle loop restated on the oracle (tests/oracle_lib.middle_scan_windows) vs the device hits."""
+    from tests import oracle_lib
+    from custom_porechop_abi_amd import synth
+    from custom_porechop_abi_amd.engine import SeqPack
+    seqs = []
+    for i in range(k):
+        r = synth.codes_to_str(reads[i])
+        st, et = int(trims[0][i]), int(trims[1][i])
+        seqs.append(r[st:len(r) - et] if st or et else r)
+    pack = SeqPack(seqs)
+    exp = oracle_lib.middle_scan_windows(pack.views(np.zeros(k, np.int64), pack.lengths), mid_adps, sc, thr)
+    got = hits[:, :min(n_hits, hits.shape[1])]
+    got = got[:, got[0] < k]
+    og = np.lexsort((np.arange(got.shape[1]), got[0]))
+    oe = np.lexsort((np.arange(exp.shape[1]), exp[0]))
+    same = got.shape == exp.shape and bool(np.array_equal(got[:, og], exp[:, oe]))
+    return {'reads_checked': k, 'hits': int(exp.shape[1]), 'identical': same}
+
+
+def cpu_baseline_middle(reads, trims, mid_adps, sc, thr, threads):
+    """The reference CPU path for the middle scan on a bounded sample: each trimmed read's loop of
+    nanopore_read.find_middle_adapters (nanopore_read.py:236-246) through the reference's own
+    adapterAlignment (oracle/_ref/cpp_functions.so), reads fanned out over a ThreadPool."""
+    from multiprocessing.dummy import Pool as ThreadPool
+    from custom_porechop_abi_amd import synth
+    ref = os.path.join(ROOT, 'oracle', '_ref', 'cpp_functions.so')
+    kind = 'reference'
+    if os.path.isfile(ref):
+        lib = ctypes.CDLL(ref)
+        fn, fr = lib.adapterAlignment, lib.freeCString
+    else:
+        from tests import oracle_lib
+        lib = oracle_lib.load()
+        fn, fr = lib.pcabi_oracle_adapter_alignment, lib.pcabi_oracle_free
+        kind = 'port'
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_char_p] + [ctypes.c_int] * 4
+    fn.restype = ctypes.c_void_p
+    fr.argtypes = [ctypes.c_void_p]
+    seqs = []
+    for i, r in enumerate(reads):
+        s = synth.codes_to_str(r)
+        st, et = int(trims[0][i]), int(trims[1][i])
+        seqs.append(s[st:len(s) - et] if st or et else s)
+    adps = [a.encode() for a in mid_adps]
+
+    def one(seq):
+        masked = seq
+        n = 0
+        for a in adps:
+            while True:
+                p = fn(masked.encode(), a, *sc)
+                t = ctypes.cast(p, ctypes.c_char_p).value.decode()
+                fr(p)
+                f = t.split(',')
+                if int(f[0]) == -1 or float(f[6]) < thr:
+                    break
+                rs, re_ = int(f[0]), int(f[1]) + 1
+                masked = masked[:rs] + '-' * (re_ - rs) + masked[re_:]
+                n += 1
+        return n
+
+    threads = threads or min(16, len(os.sched_getaffinity(0)))
+    t0 = time.perf_counter()
+    with ThreadPool(threads) as pool:
+        pool.map(one, seqs)
+    wall = time.perf_counter() - t0
+    return {'value': round(len(seqs) / wall, 3), 'unit': 'reads/s', 'cores': threads, 'kind': kind,
+            'sample': '%d whole trimmed reads x %d middle adapters (find_middle_adapters loop), %.1f s wall, '
+                      'ThreadPool(%d) over ctypes adapterAlignment' % (len(seqs), len(adps), wall, threads)}
 
 
 def spot_check(L, _lib, d_sres, d_eres, d_st, d_et, s_stride, e_stride, n, n_sa, n_ea, reads, start_adps,

@@ -54,6 +54,7 @@ def lib():
         'pcabi_dev_d2h': ([c_p, c_p, c_i64], c_int),
         'pcabi_dev_memset': ([c_p, c_int, c_i64], c_int),
         'pcabi_dev_sync': ([], c_int),
+        'pcabi_dev_copy_async': ([c_p, c_p, c_i64, c_int, c_p], c_int),
         'pcabi_stream_create': ([ctypes.POINTER(c_p)], c_int),
         'pcabi_stream_destroy': ([c_p], c_int),
         'pcabi_stream_sync': ([c_p], c_int),
@@ -95,7 +96,7 @@ def exported_symbols():
             'pcabi_device_count', 'pcabi_max_adapter_len', 'pcabi_max_window_len',
             'pcabi_encode_dna5', 'pcabi_pid6_host', 'pcabi_align_host', 'pcabi_dev_set',
             'pcabi_dev_malloc', 'pcabi_dev_free', 'pcabi_dev_h2d', 'pcabi_dev_d2h',
-            'pcabi_dev_memset', 'pcabi_dev_sync', 'pcabi_stream_create', 'pcabi_stream_destroy',
+            'pcabi_dev_memset', 'pcabi_dev_sync', 'pcabi_dev_copy_async', 'pcabi_stream_create', 'pcabi_stream_destroy',
             'pcabi_stream_sync', 'pcabi_event_create', 'pcabi_event_destroy', 'pcabi_event_record',
             'pcabi_event_elapsed_ms', 'pcabi_adapters_create', 'pcabi_adapters_destroy',
             'pcabi_tile_layout', 'pcabi_tile_windows_dev', 'pcabi_align_cross_dev', 'pcabi_end_trim_dev',

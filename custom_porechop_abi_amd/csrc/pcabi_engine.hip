@@ -880,6 +880,12 @@ int pcabi_dev_d2h(void *dst, const void *src, int64_t bytes) {
 }
 int pcabi_dev_memset(void *dst, int value, int64_t bytes) { HIP_TRY(hipMemset(dst, value, (size_t)bytes)); return 0; }
 int pcabi_dev_sync(void) { HIP_TRY(hipDeviceSynchronize()); return 0; }
+int pcabi_dev_copy_async(void *dst, const void *src, int64_t bytes, int kind, void *stream) {
+    const hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : (kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice);
+    if (kind < 0 || kind > 2) return fail(PCABI_E_ARG, "copy kind must be 0 (h2d), 1 (d2h) or 2 (d2d)");
+    HIP_TRY(hipMemcpyAsync(dst, src, (size_t)bytes, k, (hipStream_t)stream));
+    return 0;
+}
 int pcabi_stream_create(void **stream) {
     hipStream_t s;
     HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
@@ -1028,21 +1034,25 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
     std::vector<int32_t> cur, nxt, nxt_start, hm_w, hm_s, hm_e, lens;
     std::vector<int32_t> hb;
     std::vector<int64_t> toff;
+    // Round 1 visits the reads longest first: lanes of a wave (and tiles) then run near-equal
+    // column counts (read lengths are log-normal; unsorted, a wave would idle ~2/3 of its lanes).
+    cur.resize((size_t)n_win);
+    for (int64_t k = 0; k < n_win; ++k) cur[k] = (int32_t)k;
+    std::stable_sort(cur.begin(), cur.end(), [&](int32_t x, int32_t y) { return h_win_len[x] > h_win_len[y]; });
     for (int round = 0;; ++round) {
-        const int64_t n = round == 0 ? n_win : (int64_t)cur.size();
+        const int64_t n = (int64_t)cur.size();
         const int64_t *v_off = win_off;
         const int32_t *v_len = win_len;
         lens.resize((size_t)n);
-        if (round == 0) {
-            std::copy(h_win_len, h_win_len + n, lens.begin());
-        } else {
+        {
             for (int64_t k = 0; k < n; ++k) lens[k] = h_win_len[cur[k]];
             if (int rc = sc->idx.ensure(sizeof(int32_t) * n)) return rc;
             if (int rc = sc->start.ensure(sizeof(int32_t) * n)) return rc;
             if (int rc = sc->soff.ensure(sizeof(int64_t) * n)) return rc;
             if (int rc = sc->slen.ensure(sizeof(int32_t) * n)) return rc;
             HIP_TRY(hipMemcpyAsync(sc->idx.p, cur.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
-            HIP_TRY(hipMemcpyAsync(sc->start.p, nxt_start.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
+            if (round > 0)
+                HIP_TRY(hipMemcpyAsync(sc->start.p, nxt_start.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
             hipLaunchKernelGGL(k_gather_views, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, win_off, win_len,
                                (const int32_t *)sc->idx.p, n, (int64_t *)sc->soff.p, (int32_t *)sc->slen.p);
             v_off = (const int64_t *)sc->soff.p;
@@ -1075,7 +1085,7 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
         for (int64_t k = 0; k < n; ++k) {
             const int32_t a = hb[k];
             if (a < 0) continue;
-            const int32_t r = round == 0 ? (int32_t)k : cur[k];
+            const int32_t r = cur[k];
             const int32_t rs = hb[n + k], re = hb[2 * n + k];
             const int32_t rend = rs == -1 ? 0 : re + 1;
             if (n_hits < cap) {
@@ -1104,9 +1114,17 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
                                (const int32_t *)sc->mwin.p, (const int32_t *)sc->ms.p, (const int32_t *)sc->me.p);
             HIP_TRY(hipGetLastError());
         }
-        cur.swap(nxt);
         // host vectors uploaded above must stay intact until the copies ran
         HIP_TRY(hipStreamSynchronize(st));
+        // next round: the reads that just hit, longest first, each from the adapter that hit
+        std::vector<int32_t> perm(nxt.size());
+        for (size_t k = 0; k < perm.size(); ++k) perm[k] = (int32_t)k;
+        std::stable_sort(perm.begin(), perm.end(),
+                         [&](int32_t x, int32_t y) { return h_win_len[nxt[x]] > h_win_len[nxt[y]]; });
+        cur.resize(perm.size());
+        std::vector<int32_t> st_sorted(perm.size());
+        for (size_t k = 0; k < perm.size(); ++k) { cur[k] = nxt[perm[k]]; st_sorted[k] = nxt_start[perm[k]]; }
+        nxt_start.swap(st_sorted);
     }
     return n_hits;
 }

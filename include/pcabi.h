@@ -106,6 +106,8 @@ int pcabi_dev_h2d(void *dst, const void *src, int64_t bytes);
 int pcabi_dev_d2h(void *dst, const void *src, int64_t bytes);
 int pcabi_dev_memset(void *dst, int value, int64_t bytes);
 int pcabi_dev_sync(void);
+/* ordered on `stream`; kind 0 = host->device, 1 = device->host, 2 = device->device */
+int pcabi_dev_copy_async(void *dst, const void *src, int64_t bytes, int kind, void *stream);
 int pcabi_stream_create(void **stream);
 int pcabi_stream_destroy(void *stream);
 int pcabi_stream_sync(void *stream);
