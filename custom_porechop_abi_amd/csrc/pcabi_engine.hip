@@ -521,6 +521,33 @@ struct pcabi_scan {
 
 namespace {
 
+// Side streams of a device for the fork / join of pcabi_align_cross_dev's bucket launches.
+struct SideStreams {
+    static constexpr int N = 3;
+    std::mutex mu;               // one fork / join region at a time per device
+    bool init = false;
+    hipStream_t s[N] = {};
+    hipEvent_t fork = nullptr, join[N] = {};
+};
+SideStreams g_side[16];
+std::mutex g_side_mu;
+
+int side_streams(int dev, SideStreams **out) {
+    if (dev < 0 || dev >= 16) return fail(PCABI_E_ARG, "bad device index");
+    std::lock_guard<std::mutex> g(g_side_mu);
+    SideStreams &ss = g_side[dev];
+    if (!ss.init) {
+        for (int i = 0; i < SideStreams::N; ++i) {
+            HIP_TRY(hipStreamCreateWithFlags(&ss.s[i], hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&ss.join[i], hipEventDisableTiming));
+        }
+        HIP_TRY(hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming));
+        ss.init = true;
+    }
+    *out = &ss;
+    return 0;
+}
+
 // Per-device state for the host-buffer API (serialised by a mutex: the legacy ABI is called
 // concurrently from the reference's ThreadPool workers, porechop_abi.py:228,418,504).
 struct Engine {
@@ -984,17 +1011,50 @@ int pcabi_align_cross_dev(const uint32_t *tiles, const int64_t *tile_off, const 
     p.out_stride = out_stride;
     p.sc = pcabi::Scoring{match, mismatch, gap_open, gap_extend};
     const bool affine = gap_open != gap_extend;
+    std::vector<int> order;
     for (int b = 0; b < kNumBuckets; ++b) {
         if (!adps->count[b]) continue;
         if (kBuckets[b].kind == FAST && adps->padded[b] &&
             !pcabi::fast_ok(kBuckets[b].rpl - 1, kBuckets[b].rpl, p.sc))
             return fail(PCABI_E_ARG, "scoring with non-negative gap costs: use pcabi_align_host "
                                      "(generic kernels) for this adapter table");
+        order.push_back(b);
+    }
+    // Largest bucket (adapters x rows) on the caller's stream, the others spread over the
+    // device's side streams (fork / join with events): a bucket holding one or two adapters is
+    // too small a grid to fill 256 CUs on its own, side by side they do.
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
+        return (int64_t)adps->count[x] * kBuckets[x].rpl > (int64_t)adps->count[y] * kBuckets[y].rpl;
+    });
+    const hipStream_t main = (hipStream_t)stream;
+    SideStreams *ss = nullptr;
+    std::unique_lock<std::mutex> lock;
+    if (order.size() > 1) {
+        int dev = 0;
+        HIP_TRY(hipGetDevice(&dev));
+        if (int rc = side_streams(dev, &ss)) return rc;
+        lock = std::unique_lock<std::mutex>(ss->mu);
+        HIP_TRY(hipEventRecord(ss->fork, main));
+    }
+    int used = 0;
+    for (size_t k = 0; k < order.size(); ++k) {
+        const int b = order[k];
+        hipStream_t st = main;
+        if (k > 0) {
+            const int i = (int)((k - 1) % SideStreams::N);
+            st = ss->s[i];
+            if (k - 1 < (size_t)SideStreams::N) HIP_TRY(hipStreamWaitEvent(st, ss->fork, 0));
+            used = std::max(used, i + 1);
+        }
         p.adp_pad = adps->pad[b];
         p.adp_len = adps->len[b];
         p.adp_id = adps->id[b];
         p.n_adp = adps->count[b];
-        dispatch(b, p, affine, (hipStream_t)stream, bucket_packed_ok(b, adps->lens[b], p.sc));
+        dispatch(b, p, affine, st, bucket_packed_ok(b, adps->lens[b], p.sc));
+    }
+    for (int i = 0; i < used; ++i) {
+        HIP_TRY(hipEventRecord(ss->join[i], ss->s[i]));
+        HIP_TRY(hipStreamWaitEvent(main, ss->join[i], 0));
     }
     HIP_TRY(hipGetLastError());
     return 0;
