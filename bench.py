@@ -36,6 +36,7 @@ sys.path.insert(0, ROOT)
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # int32 lane-ops/s: 256 CU x 4 SIMD32 x 2.4 GHz
 HBM_PEAK_GBS = 8000.0
 OPS_PER_CELL = 10                               # algorithmic int ops per cell
+SCORING = (3, -6, -5, -2)                       # reference default (arg_parser.py:178-180)
 DOM_KERNEL = 'k_align<24, true, 2> (packed core, 21-24 bp adapters, affine)'
 
 
@@ -110,8 +111,9 @@ def main():
         t = vp()
         if lst:
             c, o, l = encode_adapters(lst)
-            _lib.check(L.pcabi_adapters_create(c.ctypes.data_as(vp), o.ctypes.data_as(vp), l.ctypes.data_as(vp),
-                                               len(lst), ctypes.byref(t)), 'adapters_create')
+            _lib.check(L.pcabi_adapters_create_scored(c.ctypes.data_as(vp), o.ctypes.data_as(vp),
+                                                      l.ctypes.data_as(vp), len(lst), *SCORING, ctypes.byref(t)),
+                       'adapters_create')
         return t, len(lst)
 
     d_codes = h2d(buf)
@@ -123,7 +125,7 @@ def main():
     d_st, d_et = dalloc(4 * n), dalloc(4 * n)
     stream = vp()
     _lib.check(L.pcabi_stream_create(ctypes.byref(stream)), 'stream')
-    sc = (3, -6, -5, -2)
+    sc = SCORING
 
     # tile layout: computed once from the host window lengths; the device
     # re-tiles the windows inside every step
@@ -319,8 +321,8 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
     def table(lst):
         c, o, l = encode_adapters(lst)
         t = vp()
-        _lib.check(L.pcabi_adapters_create(c.ctypes.data_as(vp), o.ctypes.data_as(vp), l.ctypes.data_as(vp),
-                                           len(lst), ctypes.byref(t)), 'adapters_create')
+        _lib.check(L.pcabi_adapters_create_scored(c.ctypes.data_as(vp), o.ctypes.data_as(vp), l.ctypes.data_as(vp),
+                                                  len(lst), *SCORING, ctypes.byref(t)), 'adapters_create')
         return t
 
     d_pristine = h2d(pack)
@@ -332,7 +334,7 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
     d_toff_mid, d_tlen_mid = dalloc(8 * n), dalloc(4 * n)
     stream = vp()
     _lib.check(L.pcabi_stream_create(ctypes.byref(stream)), 'stream')
-    sc = (3, -6, -5, -2)
+    sc = SCORING
     sides = []
     for w_off, w_len, adps, d_res in ((s_off, s_len, start_adps, d_sres), (e_off, e_len, end_adps, d_eres)):
         toff = np.zeros((n + 255) // 256 + 1, np.int64)

@@ -631,8 +631,10 @@ PCABI_HD int packed_span_bound(int L, const Scoring &s) {
 }
 
 PCABI_HD bool packed_ok(int L, int rpl, const Scoring &s) {
-    if (rpl > pk::MAX_RPL || L > pk::MAX_L) return false;
-    if (!fast_ok(L, rpl, s)) return false;
+    if (rpl > pk::MAX_RPL || L > pk::MAX_L || L > rpl) return false;
+    // padding rows (any number: the substitution table passes scores through them) are exact
+    // only when opening or extending a gap always costs
+    if (L < rpl && !((s.go != s.ge) ? (s.go < 0 && s.ge < 0) : (s.ge < 0))) return false;
     if (packed_span_bound(L, s) > 255) return false;
     const int hi = (rpl * s.ma > 0 ? rpl * s.ma : 0);
     const int gm = (-s.go > -s.ge ? -s.go : -s.ge);

@@ -465,11 +465,58 @@ struct BucketHost {
     std::vector<int32_t> len, id;
 };
 
+// At most this many FAST buckets per adapter table: a cross product launches its buckets side by
+// side (the caller's stream + SideStreams::N), and a bucket of one or two adapters is too small
+// a grid to fill the GPU on its own.
+constexpr int kMaxFastBuckets = 4;
+
+// Bucket of every adapter: its own register bucket, then the cheapest merges of a FAST bucket
+// into the next larger non-empty one (cost = adapters x added padding rows) until at most
+// kMaxFastBuckets remain. Only merges the packed core can serve with the scoring `sc` (it
+// passes scores through any number of padding rows; the fast core allows at most 3).
+std::vector<int> assign_buckets(const int32_t *adp_len, int32_t n_adp, const pcabi::Scoring &sc, bool merge) {
+    std::vector<int> b_of(n_adp);
+    int count[kNumBuckets] = {};
+    for (int a = 0; a < n_adp; ++a) {
+        b_of[a] = bucket_of(adp_len[a], sc);
+        ++count[b_of[a]];
+    }
+    auto packed_all = [&](int b, int extra_from) {
+        for (int a = 0; a < n_adp; ++a)
+            if ((b_of[a] == b || b_of[a] == extra_from) && !pcabi::packed_ok(adp_len[a], kBuckets[b].rpl, sc))
+                return false;
+        return true;
+    };
+    while (merge) {
+        std::vector<int> fast;
+        for (int b = 0; b < kNumBuckets; ++b)
+            if (count[b] && kBuckets[b].kind == FAST) fast.push_back(b);
+        if ((int)fast.size() <= kMaxFastBuckets) break;
+        int best = -1;
+        int64_t best_cost = 0;
+        for (size_t k = 0; k + 1 < fast.size(); ++k) {
+            const int i = fast[k], j = fast[k + 1];
+            // more than 3 padding rows: only the packed core passes scores through them
+            if (!packed_all(j, i)) continue;
+            const int64_t cost = (int64_t)count[i] * (kBuckets[j].rpl - kBuckets[i].rpl);
+            if (best < 0 || cost < best_cost) { best = (int)k; best_cost = cost; }
+        }
+        if (best < 0) break;
+        const int i = fast[best], j = fast[best + 1];
+        for (int a = 0; a < n_adp; ++a)
+            if (b_of[a] == i) b_of[a] = j;
+        count[j] += count[i];
+        count[i] = 0;
+    }
+    return b_of;
+}
+
 void build_buckets(const uint8_t *adp_codes, const int32_t *adp_off, const int32_t *adp_len,
-                   int32_t n_adp, const pcabi::Scoring &sc, BucketHost (&bk)[kNumBuckets]) {
+                   int32_t n_adp, const pcabi::Scoring &sc, BucketHost (&bk)[kNumBuckets], bool merge = true) {
+    const std::vector<int> b_of = assign_buckets(adp_len, n_adp, sc, merge);
     for (int a = 0; a < n_adp; ++a) {
         const int L = adp_len[a];
-        const int b = bucket_of(L, sc);
+        const int b = b_of[a];
         const int R = kBuckets[b].rpl;
         BucketHost &h = bk[b];
         const size_t base = h.pad.size();
@@ -487,6 +534,7 @@ void build_buckets(const uint8_t *adp_codes, const int32_t *adp_off, const int32
 struct pcabi_adapters {
     int32_t n_adp = 0;
     bool padded[kNumBuckets] = {};
+    int max_off[kNumBuckets] = {};   // most padding rows above an adapter (> 3: packed core only)
     std::vector<int32_t> lens[kNumBuckets];
     int32_t count[kNumBuckets] = {};
     uint32_t *pad[kNumBuckets] = {};
@@ -829,7 +877,9 @@ int64_t pcabi_middle_scan_host(int device, const uint8_t *codes, int64_t codes_l
     HIP_TRY(hipMemcpyAsync(e.woff.p, win_off, sizeof(int64_t) * (size_t)n_win, hipMemcpyHostToDevice, e.stream));
     HIP_TRY(hipMemcpyAsync(e.wlen.p, win_len, sizeof(int32_t) * (size_t)n_win, hipMemcpyHostToDevice, e.stream));
     pcabi_adapters *tab = nullptr;
-    if (int rc = pcabi_adapters_create(adp_codes, adp_off, adp_len, n_adp, &tab)) return rc;
+    if (int rc = pcabi_adapters_create_scored(adp_codes, adp_off, adp_len, n_adp, match, mismatch, gap_open,
+                                              gap_extend, &tab))
+        return rc;
     if (!e.scan) e.scan = new pcabi_scan();
     e.scan->adps = tab;
     const int64_t r = pcabi_middle_scan_dev(e.scan, (uint8_t *)e.codes.p, (const int64_t *)e.woff.p,
@@ -935,13 +985,17 @@ int pcabi_event_elapsed_ms(float *ms, void *start, void *stop) {
     return 0;
 }
 
-int pcabi_adapters_create(const uint8_t *adp_codes, const int32_t *adp_off, const int32_t *adp_len,
-                          int32_t n_adp, pcabi_adapters **out) {
+}  // extern "C"
+
+namespace {
+// Device adapter table. sc == nullptr: laid out for the fast buckets (any scoring with negative
+// gap costs; pcabi_align_cross_dev rejects scorings the layout cannot serve); otherwise small
+// buckets are merged for that scoring (assign_buckets).
+int adapters_create_impl(const uint8_t *adp_codes, const int32_t *adp_off, const int32_t *adp_len,
+                         int32_t n_adp, const pcabi::Scoring *sc, pcabi_adapters **out) {
     if (int rc = check_common(adp_len, n_adp)) return rc;
-    // Tables are laid out for the fast buckets (any scoring with negative gap costs);
-    // pcabi_align_cross_dev rejects scorings the layout cannot serve.
     BucketHost bk[kNumBuckets];
-    build_buckets(adp_codes, adp_off, adp_len, n_adp, pcabi::Scoring{1, -1, -1, -1}, bk);
+    build_buckets(adp_codes, adp_off, adp_len, n_adp, sc ? *sc : pcabi::Scoring{1, -1, -1, -1}, bk, sc != nullptr);
     pcabi_adapters *a = new pcabi_adapters();
     a->n_adp = n_adp;
     for (int b = 0; b < kNumBuckets; ++b) {
@@ -949,8 +1003,10 @@ int pcabi_adapters_create(const uint8_t *adp_codes, const int32_t *adp_off, cons
         a->count[b] = nb;
         if (!nb) continue;
         a->lens[b] = bk[b].len;
-        for (int k = 0; k < nb; ++k)
+        for (int k = 0; k < nb; ++k) {
             if (bk[b].len[k] != kBuckets[b].rpl) a->padded[b] = true;
+            a->max_off[b] = std::max(a->max_off[b], kBuckets[b].rpl - bk[b].len[k]);
+        }
         if (hipMalloc((void **)&a->pad[b], bk[b].pad.size()) != hipSuccess ||
             hipMalloc((void **)&a->len[b], sizeof(int32_t) * nb) != hipSuccess ||
             hipMalloc((void **)&a->id[b], sizeof(int32_t) * nb) != hipSuccess) {
@@ -963,6 +1019,21 @@ int pcabi_adapters_create(const uint8_t *adp_codes, const int32_t *adp_off, cons
     }
     *out = a;
     return 0;
+}
+}  // namespace
+
+extern "C" {
+
+int pcabi_adapters_create(const uint8_t *adp_codes, const int32_t *adp_off, const int32_t *adp_len,
+                          int32_t n_adp, pcabi_adapters **out) {
+    return adapters_create_impl(adp_codes, adp_off, adp_len, n_adp, nullptr, out);
+}
+
+int pcabi_adapters_create_scored(const uint8_t *adp_codes, const int32_t *adp_off, const int32_t *adp_len,
+                                 int32_t n_adp, int match, int mismatch, int gap_open, int gap_extend,
+                                 pcabi_adapters **out) {
+    const pcabi::Scoring sc{match, mismatch, gap_open, gap_extend};
+    return adapters_create_impl(adp_codes, adp_off, adp_len, n_adp, &sc, out);
 }
 
 void pcabi_adapters_destroy(pcabi_adapters *a) {
@@ -1018,6 +1089,9 @@ int pcabi_align_cross_dev(const uint32_t *tiles, const int64_t *tile_off, const 
             !pcabi::fast_ok(kBuckets[b].rpl - 1, kBuckets[b].rpl, p.sc))
             return fail(PCABI_E_ARG, "scoring with non-negative gap costs: use pcabi_align_host "
                                      "(generic kernels) for this adapter table");
+        if (kBuckets[b].kind == FAST && adps->max_off[b] > 3 && !bucket_packed_ok(b, adps->lens[b], p.sc))
+            return fail(PCABI_E_ARG, "adapter table merged for another scoring (pcabi_adapters_create_scored): "
+                                     "rebuild it for this one");
         order.push_back(b);
     }
     // Largest bucket (adapters x rows) on the caller's stream, the others spread over the

@@ -123,6 +123,12 @@ int pcabi_event_elapsed_ms(float *ms, void *start, void *stop);
 typedef struct pcabi_adapters pcabi_adapters;
 int pcabi_adapters_create(const uint8_t *adp_codes, const int32_t *adp_off, const int32_t *adp_len,
                           int32_t n_adp, pcabi_adapters **out);   /* uploads to current device */
+/* Same, with small register buckets merged into larger ones for THIS scoring (fewer, fuller
+ * launches; the packed core passes scores through the extra padding rows). The table then
+ * serves that scoring only: pcabi_align_cross_dev rejects others. */
+int pcabi_adapters_create_scored(const uint8_t *adp_codes, const int32_t *adp_off,
+                                 const int32_t *adp_len, int32_t n_adp, int match, int mismatch,
+                                 int gap_open, int gap_extend, pcabi_adapters **out);
 void pcabi_adapters_destroy(pcabi_adapters *a);
 
 /*

@@ -98,6 +98,21 @@ static void run_packed(const char *read, int n, const char *adp, int L, pcabi::S
     out[4] = r.score; out[5] = r.m; out[6] = r.l1; out[7] = r.l2;
 }
 
+// packed-key core at an explicit register bucket (extra padding rows); -3 if out of range
+extern "C" int pcabi_model_align_packed_rpl(const char *read, int n, const char *adp, int L, int rpl,
+                                            int ma, int mi, int go, int ge, int *out) {
+    pcabi::Scoring sc{ma, mi, go, ge};
+    if (L <= 0 || n <= 0) return -1;
+    if (!pcabi::packed_ok(L, rpl, sc)) return -3;
+    switch (rpl) {
+#define C(R) case R: run_packed<R>(read, n, adp, L, sc, out); break;
+    C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32) C(36) C(40) C(44) C(48) C(52) C(56) C(60) C(64)
+#undef C
+    default: return -2;
+    }
+    return 0;
+}
+
 // packed-key core; -3 if the range preconditions fail
 extern "C" int pcabi_model_align_packed(const char *read, int n, const char *adp, int L,
                                         int ma, int mi, int go, int ge, int *out) {

@@ -25,6 +25,8 @@ def model():
     for fn in ('pcabi_model_align', 'pcabi_model_align_fast', 'pcabi_model_align_packed'):
         getattr(L, fn).argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int] + \
             [ctypes.c_int] * 4 + [ctypes.c_void_p]
+    L.pcabi_model_align_packed_rpl.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
+                                               ctypes.c_int] + [ctypes.c_int] * 4 + [ctypes.c_void_p]
     L.pcabi_model_pid6.restype = ctypes.c_double
     L.pcabi_model_pid6.argtypes = [ctypes.c_int, ctypes.c_int]
     return L
@@ -134,3 +136,25 @@ def test_pid6_matches_text_round_trip(model):
     for l in range(1, 700):
         for m in range(0, l + 1):
             assert model.pcabi_model_pid6(m, l) == float('%f' % (100.0 * m / l))
+
+
+def test_packed_core_extra_padding_rows(model):
+    """Adapters run in a larger register bucket than their own (merged buckets): any number of
+    pass-through padding rows above the adapter."""
+    rng = random.Random(17)
+    schemes = [(3, -6, -5, -2), (2, -1, -1, -1), (1, -1, -3, -1), (3, -6, -2, -5)]
+    n_checked = 0
+    for k in range(2500):
+        sc = schemes[k % len(schemes)]
+        al = rng.choice(['A', 'AT', 'ACGT', 'ACGTN'])
+        L = rng.randint(1, 60)
+        rpl = rng.choice([r for r in range(4, 68, 4) if r >= L])
+        a = ''.join(rng.choice(al) for _ in range(L))
+        r = ''.join(rng.choice(al) for _ in range(rng.randint(1, 260)))
+        out = (ctypes.c_int * 8)()
+        rc = model.pcabi_model_align_packed_rpl(r.encode(), len(r), a.encode(), L, rpl, *sc, out)
+        if rc == -3:
+            continue
+        assert rc == 0 and list(out) == oracle_lib.align(r, a, sc), (sc, r, a, rpl)
+        n_checked += 1
+    assert n_checked > 2000

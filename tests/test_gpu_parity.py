@@ -143,13 +143,16 @@ def test_long_reads_middle_shape(gpu_lib):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('scored', [False, True])
 @pytest.mark.parametrize('scheme', [(3, -6, -5, -2), (2, -1, -1, -1)])
-def test_device_abi_tiled_cross(gpu_lib, scheme):
+def test_device_abi_tiled_cross(gpu_lib, scheme, scored):
     """Device-pointer ABI: pcabi_tile_layout -> pcabi_tile_windows_dev -> pcabi_align_cross_dev,
-    with ragged windows (empty, 1 bp, several kb) and more than one tile."""
+    with ragged windows (empty, 1 bp, several kb) and more than one tile. scored: the table is
+    built for the scoring, so small register buckets are merged (extra padding rows)."""
     from custom_porechop_abi_amd import _lib, engine
     L, vp = gpu_lib, ctypes.c_void_p
     reads, adps = _case_set(31, 700, 7, 3000, 64)
+    adps = adps + ['ACGTTGCA' * k for k in (1, 2, 3, 4, 5, 6, 7)] + ['GATTACA' * 5 + 'G', 'TTAGGC' * 9]
     pack = engine.SeqPack(reads)
     n = len(reads)
     # windows seq[k:] with random (unaligned) starts k
@@ -177,8 +180,12 @@ def test_device_abi_tiled_cross(gpu_lib, scheme):
     bufs.append(d_tiles)
     c, o, l = engine.encode_adapters(adps)
     tab = vp()
-    _lib.check(L.pcabi_adapters_create(c.ctypes.data_as(vp), o.ctypes.data_as(vp), l.ctypes.data_as(vp),
-                                       len(adps), ctypes.byref(tab)), 'adapters_create')
+    if scored:
+        _lib.check(L.pcabi_adapters_create_scored(c.ctypes.data_as(vp), o.ctypes.data_as(vp), l.ctypes.data_as(vp),
+                                                  len(adps), *scheme, ctypes.byref(tab)), 'adapters_create')
+    else:
+        _lib.check(L.pcabi_adapters_create(c.ctypes.data_as(vp), o.ctypes.data_as(vp), l.ctypes.data_as(vp),
+                                           len(adps), ctypes.byref(tab)), 'adapters_create')
     stride = n * len(adps)
     d_out = vp()
     _lib.check(L.pcabi_dev_malloc(ctypes.byref(d_out), 4 * 8 * stride), 'malloc')
