@@ -876,4 +876,110 @@ PCABI_HD Result align_lane_packed(ReadFn &rd, int n, const TabFn &tabfn, int L, 
     return finish(b, L, n);
 }
 
+// ==========================================================================================
+// Score-only filter for the middle-adapter scan.
+//
+// The scan only needs the alignments whose full-adapter identity reaches the threshold, and
+// such an alignment must score high: pid2 = m / l2 >= theta with l2 >= L (the adapter span holds
+// all L adapter bases) and every non-matching column of the span costs at most
+// c = max(|mismatch|, |gap_open|, |gap_extend|), so the best score is at least
+// L * (theta * match - c * (1 - theta))  (filter_threshold; the reported path never ends in a
+// last-row H run, which would score below its own start). The filter computes the best score
+// S* alone -- no tie-break, no attributes -- in 16-bit lanes, TWO adapters per lane
+// (v_pk_add_u16 / v_pk_max_i16: 8 packed ops per row for two cells), and only the pairs at or
+// above the bound go through the attribute DP. S* is the same value the full DP returns.
+// ==========================================================================================
+namespace sf {
+typedef int16_t v2 __attribute__((vector_size(4)));
+PCABI_HD v2 vmax(v2 a, v2 b) {
+#if defined(__clang__)
+    return __builtin_elementwise_max(a, b);
+#else
+    return a > b ? a : b;
+#endif
+}
+PCABI_HD v2 splat(int x) { v2 r = {(int16_t)x, (int16_t)x}; return r; }
+constexpr int NEG16 = -8192;
+constexpr int MAX_RPL = 64;
+
+// Smallest best score an alignment with pid2 >= threshold_pct can have (-32768: no bound).
+// The threshold is lowered by 1e-5 % first: the reference compares the identity after its
+// 6-decimal text round trip (pid6), which can round a value up by < 5e-7 %.
+inline int filter_threshold(int L, double threshold_pct, const Scoring &sc) {
+    const double th = (threshold_pct - 1e-5) / 100.0;
+    if (th <= 0.0 || sc.ma <= 0) return -32768;
+    int c = -sc.mi;
+    c = c > -sc.go ? c : -sc.go;
+    c = c > -sc.ge ? c : -sc.ge;
+    if (c < 0) c = 0;
+    const double b = (double)L * (th * sc.ma - c * (1.0 - th));
+    if (b <= 0.0) return -32768;
+    return (int)b;   // floor: S* is an integer >= b
+}
+
+// Range: scores, the NEG sentinel and their sums stay inside int16 (and gaps cost something,
+// for the pass-through padding rows).
+PCABI_HD bool filter_ok(int rpl, const Scoring &s) {
+    if (rpl > MAX_RPL || !(s.go < 0 && s.ge < 0)) return false;
+    const int hi = rpl * (s.ma > 0 ? s.ma : 0);
+    const int lo = rpl * (s.mi < 0 ? s.mi : 0) + 4 * (s.go < s.ge ? s.go : s.ge);
+    return hi < 4000 && lo > -4000 && s.go > -2000 && s.ge > -2000;
+}
+}  // namespace sf
+
+// tabfn(r) -> row(s) / row.quad(q, v2 *dst): per slot the packed (adapter A, adapter B)
+// substitution score of read code r MINUS gap_open (it is added to G = S + gap_open); padding
+// slots hold -gap_open (score 0). Returns S* of both adapters (lo = A, hi = B).
+template <int RPL, bool AFFINE, typename ReadFn, typename TabFn>
+PCABI_HD sf::v2 filter_lane(ReadFn &rd, int n, const TabFn &tabfn, const Scoring sc) {
+    using sf::v2;
+    const v2 go2 = sf::splat(sc.go), ge2 = sf::splat(sc.ge), lin2 = sf::splat(sc.ge - sc.go);
+    v2 G[RPL + 1], H[RPL + 1];
+#pragma unroll
+    for (int s = 1; s <= RPL; ++s) { G[s] = go2; H[s] = sf::splat(sf::NEG16); }   // S(i, 0) = 0
+    v2 best = sf::splat(0);                         // the (L, 0) seed
+    constexpr int NQ = RPL / 4;
+    int r = rd(1);
+#pragma unroll 1
+    for (int j = 1; j <= n; ++j) {
+        const int rn = j < n ? rd(j + 1) : 0;
+        const auto tab = tabfn(r);
+        v2 t[RPL + 2];
+#pragma unroll
+        for (int q = 0; q <= 1 && q < NQ; ++q) tab.quad(q, t + 4 * q + 1);
+        v2 gup = go2;                               // S(0, j) = 0
+        v2 vup = sf::splat(sf::NEG16);
+        v2 diag = go2 + t[1];                       // S(0, j - 1) = 0
+#pragma unroll
+        for (int s = 1; s <= RPL; ++s) {
+            if ((s & 3) == 1) {
+                const int q = (s - 1) / 4 + 2;
+                if (q < NQ) tab.quad(q, t + 4 * q + 1);
+            }
+            v2 diag_nx = diag;
+            if (s < RPL) diag_nx = G[s] + t[s + 1];
+            v2 hn, vn;
+            if (AFFINE) {
+                hn = sf::vmax(H[s] + ge2, G[s]);
+                vn = sf::vmax(vup + ge2, gup);
+            } else {
+                hn = G[s] + lin2;
+                vn = gup + lin2;
+            }
+            const v2 sn = sf::vmax(sf::vmax(diag, vn), hn);
+            G[s] = sn + go2;
+            if (AFFINE) H[s] = hn;
+            gup = G[s];
+            vup = vn;
+            diag = diag_nx;
+        }
+        best = sf::vmax(best, G[RPL] - go2);        // last row
+        r = rn;
+    }
+    v2 cm = G[1];                                   // last column (padding rows hold 0)
+#pragma unroll
+    for (int s = 2; s <= RPL; ++s) cm = sf::vmax(cm, G[s]);
+    return sf::vmax(best, cm - go2);
+}
+
 }  // namespace pcabi

@@ -235,6 +235,92 @@ __global__ __launch_bounds__(256, PCABI_WAVES) void k_align(KParams p) {
     }
 }
 
+// ---- middle-scan score filter (pcabi_dp.h filter_lane) -------------------------------------------
+// PCABI_MIDDLE_FILTER=0 in the environment turns it off (A/B timing; results are identical).
+const bool g_middle_filter = [] {
+    const char *e = std::getenv("PCABI_MIDDLE_FILTER");
+    return !(e && e[0] == '0');
+}();
+
+// Cross mode over tiles, TWO adapters of a FAST bucket per wave (packed 16-bit lanes): block =
+// (tile of 256 windows, adapter pair) in the XCD-aware order of k_align. Writes the best score of
+// every (adapter, window) as int16: s16[a_glob * n_win + w].
+struct FParams {
+    const uint32_t *tiles;
+    const int64_t *tile_off;
+    const int32_t *win_len;
+    int64_t n_win;
+    const uint32_t *adp_pad;   // bucket table (RPL bytes per adapter)
+    const int32_t *adp_len;
+    const int32_t *adp_id;
+    int32_t n_adp;             // adapters in the bucket (pairs = ceil(n_adp / 2))
+    int16_t *s16;
+    pcabi::Scoring sc;
+};
+
+struct LdsRow16 {
+    const int32_t *p;
+    __device__ __forceinline__ void quad(int q, pcabi::sf::v2 *dst) const {
+        const int4 v = *reinterpret_cast<const int4 *>(p + 4 * q);
+        dst[0] = __builtin_bit_cast(pcabi::sf::v2, v.x);
+        dst[1] = __builtin_bit_cast(pcabi::sf::v2, v.y);
+        dst[2] = __builtin_bit_cast(pcabi::sf::v2, v.z);
+        dst[3] = __builtin_bit_cast(pcabi::sf::v2, v.w);
+    }
+};
+
+template <int RPL, bool AFFINE>
+__global__ __launch_bounds__(256) void k_score_filter(FParams p) {
+    __shared__ __attribute__((aligned(16))) int32_t tab[4 * kTabW * RPL];
+    int32_t *wave_tab = tab + (threadIdx.x >> 6) * kTabW * RPL;
+    const int n_pair = (p.n_adp + 1) / 2;
+    const int64_t b = blockIdx.x;
+    const int64_t k = b >> 3;
+    const int pr = (int)(k % n_pair);
+    const int64_t tile = (k / n_pair) * 8 + (b & 7);
+    const int64_t w = tile * 256 + threadIdx.x;
+    const int ia = 2 * pr, ib = (2 * pr + 1 < p.n_adp) ? 2 * pr + 1 : 2 * pr;
+    const int La = __builtin_amdgcn_readfirstlane(p.adp_len[ia]);
+    const int Lb = __builtin_amdgcn_readfirstlane(p.adp_len[ib]);
+    {
+        const int lane = threadIdx.x & 63;
+        const uint32_t *pa = p.adp_pad + (int64_t)ia * (RPL / 4), *pb = p.adp_pad + (int64_t)ib * (RPL / 4);
+        for (int e = lane; e < kTabW * RPL; e += 64) {
+            const int c = e / RPL, sl = e % RPL + 1;
+            const int ca = (int)((pa[(sl - 1) / 4] >> (8 * ((sl - 1) & 3))) & 0xFFu);
+            const int cb = (int)((pb[(sl - 1) / 4] >> (8 * ((sl - 1) & 3))) & 0xFFu);
+            const int va = sl <= RPL - La ? 0 : (c == ca ? p.sc.ma : p.sc.mi);
+            const int vb = sl <= RPL - Lb ? 0 : (c == cb ? p.sc.ma : p.sc.mi);
+            const uint32_t lo = (uint16_t)(int16_t)(va - p.sc.go), hi = (uint16_t)(int16_t)(vb - p.sc.go);
+            wave_tab[e] = (int32_t)(lo | (hi << 16));
+        }
+        __syncthreads();
+    }
+    if (w >= p.n_win) return;
+    const int n = p.win_len[w];
+    WindowReader rd(p.tiles + p.tile_off[tile] + threadIdx.x, 256, 0);
+    auto tabfn = [&](int rc) { return LdsRow16{wave_tab + rc * RPL}; };
+    const pcabi::sf::v2 r = pcabi::filter_lane<RPL, AFFINE>(rd, n, tabfn, p.sc);
+    p.s16[(int64_t)p.adp_id[ia] * p.n_win + w] = r[0];
+    if (ib != ia) p.s16[(int64_t)p.adp_id[ib] * p.n_win + w] = r[1];
+}
+
+template <int RPL>
+void launch_filter(const FParams &p, bool affine, hipStream_t st) {
+    const int64_t tiles8 = (p.n_win + 8 * 256 - 1) / (8 * 256) * 8;
+    const dim3 grid((unsigned)(tiles8 * ((p.n_adp + 1) / 2)));
+    if (affine) hipLaunchKernelGGL((k_score_filter<RPL, true>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((k_score_filter<RPL, false>), grid, dim3(256), 0, st, p);
+}
+
+void dispatch_filter(int rpl, const FParams &p, bool affine, hipStream_t st) {
+    switch (rpl) {
+#define C(R) case R: launch_filter<R>(p, affine, st); break;
+    C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32) C(36) C(40) C(44) C(48) C(52) C(56) C(60) C(64)
+#undef C
+    }
+}
+
 // ---- decision epilogues --------------------------------------------------------------------
 
 __global__ __launch_bounds__(256) void k_end_trim(const int32_t *sres, int64_t sstride, int32_t n_sa,
@@ -536,6 +622,8 @@ struct pcabi_adapters {
     bool padded[kNumBuckets] = {};
     int max_off[kNumBuckets] = {};   // most padding rows above an adapter (> 3: packed core only)
     std::vector<int32_t> lens[kNumBuckets];
+    std::vector<int32_t> ids[kNumBuckets];   // global adapter index of each bucket entry (host)
+    bool has_n = false;                      // some adapter holds an N (code 4) base
     int32_t count[kNumBuckets] = {};
     uint32_t *pad[kNumBuckets] = {};
     int32_t *len[kNumBuckets] = {};
@@ -565,6 +653,7 @@ struct DeviceBuf {
 struct pcabi_scan {
     const pcabi_adapters *adps = nullptr;
     DeviceBuf tiles, toff, res, hits, idx, start, soff, slen, mwin, ms, me;
+    DeviceBuf s16, tw, to, wa, pres;   // score filter + candidate pairs (round 1)
 };
 
 namespace {
@@ -595,6 +684,42 @@ int side_streams(int dev, SideStreams **out) {
     *out = &ss;
     return 0;
 }
+
+// Fork / join of independent launches: launch k runs on the caller's stream (k == 0) or on side
+// stream (k - 1) % N, each side stream first waiting for the work already queued on the caller's
+// stream; end() makes the caller's stream wait for every side stream used.
+struct ForkJoin {
+    hipStream_t main = nullptr;
+    SideStreams *ss = nullptr;
+    std::unique_lock<std::mutex> lock;
+    int used = 0;
+    int begin(hipStream_t m, size_t n_launch) {
+        main = m;
+        if (n_launch <= 1) return 0;
+        int dev = 0;
+        HIP_TRY(hipGetDevice(&dev));
+        if (int rc = side_streams(dev, &ss)) return rc;
+        lock = std::unique_lock<std::mutex>(ss->mu);
+        HIP_TRY(hipEventRecord(ss->fork, main));
+        return 0;
+    }
+    hipStream_t at(size_t k) {
+        if (k == 0 || !ss) return main;
+        const int i = (int)((k - 1) % SideStreams::N);
+        if (k - 1 < (size_t)SideStreams::N) (void)hipStreamWaitEvent(ss->s[i], ss->fork, 0);
+        used = std::max(used, i + 1);
+        return ss->s[i];
+    }
+    int end() {
+        for (int i = 0; i < used; ++i) {
+            HIP_TRY(hipEventRecord(ss->join[i], ss->s[i]));
+            HIP_TRY(hipStreamWaitEvent(main, ss->join[i], 0));
+        }
+        used = 0;
+        if (lock.owns_lock()) lock.unlock();
+        return 0;
+    }
+};
 
 // Per-device state for the host-buffer API (serialised by a mutex: the legacy ABI is called
 // concurrently from the reference's ThreadPool workers, porechop_abi.py:228,418,504).
@@ -998,11 +1123,15 @@ int adapters_create_impl(const uint8_t *adp_codes, const int32_t *adp_off, const
     build_buckets(adp_codes, adp_off, adp_len, n_adp, sc ? *sc : pcabi::Scoring{1, -1, -1, -1}, bk, sc != nullptr);
     pcabi_adapters *a = new pcabi_adapters();
     a->n_adp = n_adp;
+    for (int k = 0; k < n_adp; ++k)
+        for (int i = 0; i < adp_len[k]; ++i)
+            if (adp_codes[adp_off[k] + i] > 3) a->has_n = true;
     for (int b = 0; b < kNumBuckets; ++b) {
         const int nb = (int)bk[b].len.size();
         a->count[b] = nb;
         if (!nb) continue;
         a->lens[b] = bk[b].len;
+        a->ids[b] = bk[b].id;
         for (int k = 0; k < nb; ++k) {
             if (bk[b].len[k] != kBuckets[b].rpl) a->padded[b] = true;
             a->max_off[b] = std::max(a->max_off[b], kBuckets[b].rpl - bk[b].len[k]);
@@ -1100,36 +1229,17 @@ int pcabi_align_cross_dev(const uint32_t *tiles, const int64_t *tile_off, const 
     std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
         return (int64_t)adps->count[x] * kBuckets[x].rpl > (int64_t)adps->count[y] * kBuckets[y].rpl;
     });
-    const hipStream_t main = (hipStream_t)stream;
-    SideStreams *ss = nullptr;
-    std::unique_lock<std::mutex> lock;
-    if (order.size() > 1) {
-        int dev = 0;
-        HIP_TRY(hipGetDevice(&dev));
-        if (int rc = side_streams(dev, &ss)) return rc;
-        lock = std::unique_lock<std::mutex>(ss->mu);
-        HIP_TRY(hipEventRecord(ss->fork, main));
-    }
-    int used = 0;
+    ForkJoin fj;
+    if (int rc = fj.begin((hipStream_t)stream, order.size())) return rc;
     for (size_t k = 0; k < order.size(); ++k) {
         const int b = order[k];
-        hipStream_t st = main;
-        if (k > 0) {
-            const int i = (int)((k - 1) % SideStreams::N);
-            st = ss->s[i];
-            if (k - 1 < (size_t)SideStreams::N) HIP_TRY(hipStreamWaitEvent(st, ss->fork, 0));
-            used = std::max(used, i + 1);
-        }
         p.adp_pad = adps->pad[b];
         p.adp_len = adps->len[b];
         p.adp_id = adps->id[b];
         p.n_adp = adps->count[b];
-        dispatch(b, p, affine, st, bucket_packed_ok(b, adps->lens[b], p.sc));
+        dispatch(b, p, affine, fj.at(k), bucket_packed_ok(b, adps->lens[b], p.sc));
     }
-    for (int i = 0; i < used; ++i) {
-        HIP_TRY(hipEventRecord(ss->join[i], ss->s[i]));
-        HIP_TRY(hipStreamWaitEvent(main, ss->join[i], 0));
-    }
+    if (int rc = fj.end()) return rc;
     HIP_TRY(hipGetLastError());
     return 0;
 }
@@ -1155,6 +1265,165 @@ void pcabi_scan_destroy(pcabi_scan *s) {
     delete s;
 }
 
+}  // extern "C"
+
+namespace {
+
+// Round 1 of the middle scan through the score filter: best scores of every (read, adapter) in
+// packed 16-bit lanes (k_score_filter), then the attribute DP only for the pairs that can reach
+// the threshold (pairs mode), and per read the first of those (adapter order) that does.
+// Fills hb (5 x n, the k_first_hit layout). Returns 1 if it ran, 0 if the filter does not apply
+// to this scoring (caller falls back to the full cross product), < 0 on error.
+// Later rounds (h_start != nullptr) reuse round 1's scores as bounds: masking turns read bases
+// into N, which never matches an adapter base, so no alignment of the masked read scores above
+// the same alignment of the unmasked one -- a pair below the threshold in round 1 stays below.
+// h16 / pos1: round 1's scores (adapter-major, round-1 positions) and each read's position.
+int filtered_first_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_off, const int32_t *v_len,
+                        const int32_t *h_len, int64_t n, const int32_t *h_start, const int32_t *reads,
+                        std::vector<int16_t> &h16, int64_t n1, const std::vector<int32_t> &pos1,
+                        const pcabi::Scoring &scr, double threshold, std::vector<int32_t> &hb, hipStream_t st) {
+    const pcabi_adapters *adps = sc->adps;
+    const int32_t n_adp = adps->n_adp;
+    std::vector<int> fb;   // filterable buckets, largest first
+    for (int b = 0; b < kNumBuckets; ++b)
+        if (adps->count[b] && kBuckets[b].kind == FAST && pcabi::sf::filter_ok(kBuckets[b].rpl, scr)) fb.push_back(b);
+    if (fb.empty()) return 0;
+    std::stable_sort(fb.begin(), fb.end(), [&](int x, int y) {
+        return (int64_t)adps->count[x] * kBuckets[x].rpl > (int64_t)adps->count[y] * kBuckets[y].rpl;
+    });
+    std::vector<char> filtered((size_t)n_adp, 0);
+    std::vector<int32_t> lenof((size_t)n_adp, 0);
+    for (int b = 0; b < kNumBuckets; ++b)
+        for (size_t k = 0; k < adps->ids[b].size(); ++k) lenof[adps->ids[b][k]] = adps->lens[b][k];
+    for (int b : fb)
+        for (int32_t id : adps->ids[b]) filtered[id] = 1;
+    // 1. filter (round 1 only): best scores of every (adapter, read), buckets side by side
+    if (!h_start) {
+        if (int rc = sc->s16.ensure(sizeof(int16_t) * (size_t)n * n_adp)) return rc;
+        ForkJoin fj;
+        if (int rc = fj.begin(st, fb.size())) return rc;
+        for (size_t k = 0; k < fb.size(); ++k) {
+            const int b = fb[k];
+            FParams f{};
+            f.tiles = (const uint32_t *)sc->tiles.p;
+            f.tile_off = (const int64_t *)sc->toff.p;
+            f.win_len = v_len;
+            f.n_win = n;
+            f.adp_pad = adps->pad[b];
+            f.adp_len = adps->len[b];
+            f.adp_id = adps->id[b];
+            f.n_adp = adps->count[b];
+            f.s16 = (int16_t *)sc->s16.p;
+            f.sc = scr;
+            dispatch_filter(kBuckets[b].rpl, f, scr.go != scr.ge, fj.at(k));
+        }
+        if (int rc = fj.end()) return rc;
+        HIP_TRY(hipGetLastError());
+        h16.resize((size_t)n * n_adp);
+        HIP_TRY(hipMemcpyAsync(h16.data(), sc->s16.p, sizeof(int16_t) * h16.size(), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    // 2. candidates (adapter-major): pairs that can reach the threshold, from each read's start
+    //    adapter on
+    std::vector<int32_t> cand_w, cand_a;
+    for (int32_t a = 0; a < n_adp; ++a) {
+        const int T = pcabi::sf::filter_threshold(lenof[a], threshold, scr);
+        const int16_t *row = h16.data() + (size_t)a * n1;
+        for (int64_t k = 0; k < n; ++k) {
+            if (h_len[k] <= 0 || (h_start && a < h_start[k])) continue;
+            const int16_t bound = row[h_start ? pos1[reads[k]] : k];
+            if (!filtered[a] || bound >= T) { cand_w.push_back((int32_t)k); cand_a.push_back(a); }
+        }
+    }
+    const int64_t n_task = (int64_t)cand_w.size();
+    hb.assign((size_t)(5 * n), 0);
+    for (int64_t k = 0; k < n; ++k) { hb[k] = -1; hb[n + k] = -1; }
+    if (n_task == 0) return 1;
+    // attribute DP of the candidates: one task list per bucket (waves of 64 lanes, one adapter
+    // per wave), all buckets in one upload, launched side by side
+    std::vector<int64_t> first((size_t)n_adp + 1, 0);
+    for (int64_t t = 0; t < n_task; ++t) ++first[cand_a[t] + 1];
+    for (int32_t a = 0; a < n_adp; ++a) first[a + 1] += first[a];
+    std::vector<int32_t> tw, to, wa;
+    std::vector<int> nb_used;
+    std::vector<int64_t> lane0, wave0;
+    for (int b = 0; b < kNumBuckets; ++b) {
+        const int nb = adps->count[b];
+        if (!nb) continue;
+        const size_t w_before = wa.size();
+        for (int kk = 0; kk < nb; ++kk) {
+            const int32_t a = adps->ids[b][kk];
+            for (int64_t s0 = first[a]; s0 < first[a + 1]; s0 += 64) {
+                wa.push_back(kk);
+                for (int64_t q = 0; q < 64; ++q) {
+                    if (s0 + q < first[a + 1]) { tw.push_back(cand_w[s0 + q]); to.push_back((int32_t)(s0 + q)); }
+                    else { tw.push_back(-1); to.push_back(0); }
+                }
+            }
+        }
+        if (wa.size() == w_before) continue;
+        nb_used.push_back(b);
+        wave0.push_back((int64_t)w_before);
+    }
+    wave0.push_back((int64_t)wa.size());
+    if (int rc = sc->pres.ensure(sizeof(int32_t) * PCABI_NFIELDS * (size_t)n_task)) return rc;
+    if (int rc = sc->tw.ensure(sizeof(int32_t) * tw.size())) return rc;
+    if (int rc = sc->to.ensure(sizeof(int32_t) * to.size())) return rc;
+    if (int rc = sc->wa.ensure(sizeof(int32_t) * wa.size())) return rc;
+    HIP_TRY(hipMemcpyAsync(sc->tw.p, tw.data(), sizeof(int32_t) * tw.size(), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(sc->to.p, to.data(), sizeof(int32_t) * to.size(), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(sc->wa.p, wa.data(), sizeof(int32_t) * wa.size(), hipMemcpyHostToDevice, st));
+    KParams p{};
+    p.codes = codes;
+    p.win_off = v_off;
+    p.win_len = v_len;
+    p.n_win = n;
+    p.out = (int32_t *)sc->pres.p;
+    p.out_stride = n_task;
+    p.sc = scr;
+    {
+        ForkJoin fj;
+        if (int rc = fj.begin(st, nb_used.size())) return rc;
+        for (size_t k = 0; k < nb_used.size(); ++k) {
+            const int b = nb_used[k];
+            p.adp_pad = adps->pad[b];
+            p.adp_len = adps->len[b];
+            p.adp_id = adps->id[b];
+            p.n_adp = adps->count[b];
+            p.task_win = (const int32_t *)sc->tw.p + wave0[k] * 64;
+            p.task_out = (const int32_t *)sc->to.p + wave0[k] * 64;
+            p.wave_adp = (const int32_t *)sc->wa.p + wave0[k];
+            p.n_waves = wave0[k + 1] - wave0[k];
+            dispatch(b, p, scr.go != scr.ge, fj.at(k), bucket_packed_ok(b, adps->lens[b], scr));
+        }
+        if (int rc = fj.end()) return rc;
+    }
+    HIP_TRY(hipGetLastError());
+    std::vector<int32_t> res((size_t)PCABI_NFIELDS * n_task);
+    HIP_TRY(hipMemcpyAsync(res.data(), sc->pres.p, sizeof(int32_t) * res.size(), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    // 3. per read, the first candidate (adapter order) over the threshold
+    for (int64_t t = 0; t < n_task; ++t) {
+        const int64_t k = cand_w[t];
+        const int32_t a = cand_a[t];
+        if (hb[k] >= 0 && hb[k] <= a) continue;
+        const int rs = res[0 * n_task + t];
+        const int m = res[5 * n_task + t], l2 = res[7 * n_task + t];
+        const double full = rs == -1 ? 0.0 : pcabi::pid6(m, l2);
+        if (full < threshold) continue;
+        hb[k] = a;
+        hb[n + k] = rs;
+        hb[2 * n + k] = res[1 * n_task + t];
+        hb[3 * n + k] = m;
+        hb[4 * n + k] = l2;
+    }
+    return 1;
+}
+
+}  // namespace
+
+extern "C" {
+
 int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win_off, const int32_t *win_len,
                               const int32_t *h_win_len, int64_t n_win, int match, int mismatch, int gap_open,
                               int gap_extend, double threshold, int32_t *hits, int64_t cap, void *stream) {
@@ -1168,6 +1437,9 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
     std::vector<int32_t> cur, nxt, nxt_start, hm_w, hm_s, hm_e, lens;
     std::vector<int32_t> hb;
     std::vector<int64_t> toff;
+    std::vector<int16_t> h16;                       // round-1 filter scores (bounds for later rounds)
+    std::vector<int32_t> pos1((size_t)n_win, 0);    // read -> round-1 position
+    bool filt_round1 = false;
     // Round 1 visits the reads longest first: lanes of a wave (and tiles) then run near-equal
     // column counts (read lengths are log-normal; unsorted, a wave would idle ~2/3 of its lanes).
     cur.resize((size_t)n_win);
@@ -1200,21 +1472,35 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
         for (int32_t l : lens) max_len = std::max(max_len, l);
         if (int rc = sc->toff.ensure(sizeof(int64_t) * toff.size())) return rc;
         if (int rc = sc->tiles.ensure(sizeof(uint32_t) * (size_t)nd)) return rc;
-        if (int rc = sc->res.ensure(sizeof(int32_t) * PCABI_NFIELDS * (size_t)n * n_adp)) return rc;
         if (int rc = sc->hits.ensure(sizeof(int32_t) * 5 * (size_t)n)) return rc;
         HIP_TRY(hipMemcpyAsync(sc->toff.p, toff.data(), sizeof(int64_t) * toff.size(), hipMemcpyHostToDevice, st));
         launch_tiles(codes, v_off, v_len, n, (const int64_t *)sc->toff.p, max_nq, (uint32_t *)sc->tiles.p, st);
-        if (int rc = pcabi_align_cross_dev((const uint32_t *)sc->tiles.p, (const int64_t *)sc->toff.p, v_len, n,
-                                           max_len, sc->adps, match, mismatch, gap_open, gap_extend,
-                                           (int32_t *)sc->res.p, n * n_adp, stream))
-            return rc;
-        hipLaunchKernelGGL(k_first_hit, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
-                           (const int32_t *)sc->res.p, n * n_adp, n, n_adp, threshold,
-                           round == 0 ? nullptr : (const int32_t *)sc->start.p, (int32_t *)sc->hits.p, n);
-        HIP_TRY(hipGetLastError());
-        hb.resize((size_t)(5 * n));
-        HIP_TRY(hipMemcpyAsync(hb.data(), sc->hits.p, sizeof(int32_t) * 5 * n, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
+        int filt = 0;
+        if (g_middle_filter && (round == 0 || filt_round1)) {
+            filt = filtered_first_hits(sc, codes, v_off, v_len, lens.data(), n, round == 0 ? nullptr : nxt_start.data(),
+                                       cur.data(), h16, n_win, pos1,
+                                       pcabi::Scoring{match, mismatch, gap_open, gap_extend}, threshold, hb, st);
+            if (round == 0) {
+                // the bound needs masked bases (N) to never match an adapter base
+                filt_round1 = filt > 0 && !sc->adps->has_n;
+                for (int64_t k = 0; k < n; ++k) pos1[cur[k]] = (int32_t)k;
+            }
+            if (filt < 0) return filt;
+        }
+        if (!filt) {
+            if (int rc = sc->res.ensure(sizeof(int32_t) * PCABI_NFIELDS * (size_t)n * n_adp)) return rc;
+            if (int rc = pcabi_align_cross_dev((const uint32_t *)sc->tiles.p, (const int64_t *)sc->toff.p, v_len, n,
+                                               max_len, sc->adps, match, mismatch, gap_open, gap_extend,
+                                               (int32_t *)sc->res.p, n * n_adp, stream))
+                return rc;
+            hipLaunchKernelGGL(k_first_hit, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                               (const int32_t *)sc->res.p, n * n_adp, n, n_adp, threshold,
+                               round == 0 ? nullptr : (const int32_t *)sc->start.p, (int32_t *)sc->hits.p, n);
+            HIP_TRY(hipGetLastError());
+            hb.resize((size_t)(5 * n));
+            HIP_TRY(hipMemcpyAsync(hb.data(), sc->hits.p, sizeof(int32_t) * 5 * n, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+        }
         nxt.clear(); nxt_start.clear(); hm_w.clear(); hm_s.clear(); hm_e.clear();
         for (int64_t k = 0; k < n; ++k) {
             const int32_t a = hb[k];

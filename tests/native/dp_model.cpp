@@ -128,3 +128,45 @@ extern "C" int pcabi_model_align_packed(const char *read, int n, const char *adp
     }
     return 0;
 }
+
+// score-only filter, two adapters per lane (A in the low half, B in the high half)
+template <int RPL>
+static void run_filter(const char *read, int n, const char *a, int La, const char *b, int Lb, pcabi::Scoring sc,
+                       int *out) {
+    auto rd = [&](int j) { return j <= n ? dna5((unsigned char)read[j - 1]) : 4; };
+    const int offa = RPL - La, offb = RPL - Lb;
+    int32_t tab[pcabi::pk::TAB_W * RPL];
+    for (int c = 0; c < pcabi::pk::TAB_W; ++c)
+        for (int s = 1; s <= RPL; ++s) {
+            const int va = s <= offa ? 0 : (c == dna5((unsigned char)a[s - offa - 1]) ? sc.ma : sc.mi);
+            const int vb = s <= offb ? 0 : (c == dna5((unsigned char)b[s - offb - 1]) ? sc.ma : sc.mi);
+            const uint32_t lo = (uint16_t)(int16_t)(va - sc.go), hi = (uint16_t)(int16_t)(vb - sc.go);
+            tab[c * RPL + s - 1] = (int32_t)(lo | (hi << 16));
+        }
+    struct Row {
+        const int32_t *p;
+        void quad(int q, pcabi::sf::v2 *dst) const { std::memcpy(dst, p + 4 * q, 16); }
+    };
+    auto tabfn = [&](int rc) { return Row{tab + rc * RPL}; };
+    pcabi::sf::v2 r = (sc.go != sc.ge) ? pcabi::filter_lane<RPL, true>(rd, n, tabfn, sc)
+                                       : pcabi::filter_lane<RPL, false>(rd, n, tabfn, sc);
+    out[0] = r[0];
+    out[1] = r[1];
+}
+
+extern "C" int pcabi_model_filter(const char *read, int n, const char *a, int La, const char *b, int Lb, int rpl,
+                                  int ma, int mi, int go, int ge, int *out) {
+    pcabi::Scoring sc{ma, mi, go, ge};
+    if (La <= 0 || Lb <= 0 || La > rpl || Lb > rpl || !pcabi::sf::filter_ok(rpl, sc)) return -3;
+    switch (rpl) {
+#define C(R) case R: run_filter<R>(read, n, a, La, b, Lb, sc, out); break;
+    C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32) C(36) C(40) C(44) C(48) C(52) C(56) C(60) C(64)
+#undef C
+    default: return -2;
+    }
+    return 0;
+}
+
+extern "C" int pcabi_model_filter_threshold(int L, double thr, int ma, int mi, int go, int ge) {
+    return pcabi::sf::filter_threshold(L, thr, pcabi::Scoring{ma, mi, go, ge});
+}

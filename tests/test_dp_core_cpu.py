@@ -27,6 +27,9 @@ def model():
             [ctypes.c_int] * 4 + [ctypes.c_void_p]
     L.pcabi_model_align_packed_rpl.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
                                                ctypes.c_int] + [ctypes.c_int] * 4 + [ctypes.c_void_p]
+    L.pcabi_model_filter.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p,
+                                     ctypes.c_int, ctypes.c_int] + [ctypes.c_int] * 4 + [ctypes.c_void_p]
+    L.pcabi_model_filter_threshold.argtypes = [ctypes.c_int, ctypes.c_double] + [ctypes.c_int] * 4
     L.pcabi_model_pid6.restype = ctypes.c_double
     L.pcabi_model_pid6.argtypes = [ctypes.c_int, ctypes.c_int]
     return L
@@ -158,3 +161,65 @@ def test_packed_core_extra_padding_rows(model):
         assert rc == 0 and list(out) == oracle_lib.align(r, a, sc), (sc, r, a, rpl)
         n_checked += 1
     assert n_checked > 2000
+
+
+def test_score_filter_equals_best_score(model):
+    """The packed-16 score-only filter (two adapters per lane) returns exactly the best score the
+    reference reports, for both halves, across scorings, paddings and read lengths."""
+    rng = random.Random(23)
+    schemes = [(3, -6, -5, -2), (2, -1, -1, -1), (1, -1, -3, -1), (3, -6, -2, -5)]
+    n_checked = 0
+    for k in range(1500):
+        sc = schemes[k % len(schemes)]
+        al = rng.choice(['A', 'AT', 'ACGT', 'ACGTN'])
+        La, Lb = rng.randint(1, 60), rng.randint(1, 60)
+        rpl = rng.choice([x for x in range(4, 68, 4) if x >= max(La, Lb)])
+        a = ''.join(rng.choice(al) for _ in range(La))
+        b = ''.join(rng.choice(al) for _ in range(Lb))
+        r = ''.join(rng.choice(al) for _ in range(rng.randint(1, 400)))
+        if rng.random() < 0.3 and len(r) > 70:
+            p = rng.randint(0, len(r) - 60)
+            r = r[:p] + a + r[p:]
+        out = (ctypes.c_int * 2)()
+        rc = model.pcabi_model_filter(r.encode(), len(r), a.encode(), La, b.encode(), Lb, rpl, *sc, out)
+        if rc == -3:
+            continue
+        assert rc == 0
+        assert list(out) == [oracle_lib.align(r, a, sc)[4], oracle_lib.align(r, b, sc)[4]], (sc, r, a, b, rpl)
+        n_checked += 1
+    assert n_checked > 1000
+
+
+def test_score_filter_threshold_is_a_lower_bound(model):
+    """Every alignment whose full identity reaches the threshold scores at least the filter's
+    bound (checked on hits of mutated adapters, where the bound is tight)."""
+    from custom_porechop_abi_amd.engine import pid6
+    import numpy as np
+    rng = random.Random(29)
+    checked = 0
+    for k in range(3000):
+        sc = rng.choice([(3, -6, -5, -2), (2, -1, -1, -1), (1, -1, -3, -1), (3, -6, -2, -5)])
+        thr = rng.choice([90.0, 85.0, 80.0, 95.0])
+        L = rng.randint(8, 50)
+        a = ''.join(rng.choice('ACGT') for _ in range(L))
+        m = []
+        for c in a:
+            x = rng.random()
+            if x < 0.04:
+                m.append(rng.choice('ACGT'))
+            elif x < 0.06:
+                continue
+            elif x < 0.08:
+                m.append(c + rng.choice('ACGT'))
+            else:
+                m.append(c)
+        r = ''.join(rng.choice('ACGT') for _ in range(rng.randint(0, 40))) + ''.join(m) + \
+            ''.join(rng.choice('ACGT') for _ in range(rng.randint(0, 40)))
+        res = oracle_lib.align(r, a, sc)
+        if res[0] == -1:
+            continue
+        full = float(pid6(np.array([res[5]]), np.array([res[7]]))[0])
+        if full >= thr:
+            assert res[4] >= model.pcabi_model_filter_threshold(L, thr, *sc), (sc, thr, r, a, res)
+            checked += 1
+    assert checked > 500
