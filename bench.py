@@ -56,6 +56,8 @@ def parse():
                     help='endtrim: the headline metric (default); middle: end trim + middle-adapter scan '
                          '(BASELINE.json configs[2])')
     ap.add_argument('--middle-threshold', type=float, default=90.0)
+    ap.add_argument('--dist-backend', default='nccl', help='nccl (RCCL over xGMI, default) or gloo (rehearsal of '
+                                                           'several ranks sharing one GPU)')
     return ap.parse_args()
 
 
@@ -68,8 +70,11 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl')
+        if args.dist_backend == 'nccl':
+            torch.cuda.set_device(local)
+        dist.init_process_group(args.dist_backend)
+        if args.dist_backend != 'nccl':
+            local = local % max(1, torch.cuda.device_count())
     from custom_porechop_abi_amd import _lib, adapters as A, synth
     from custom_porechop_abi_amd.engine import encode_adapters
     L = _lib.lib()
@@ -193,7 +198,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device='cuda')
+        t = torch.tensor([elapsed], dtype=torch.float64, device='cuda' if args.dist_backend == 'nccl' else 'cpu')
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -392,7 +397,7 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device='cuda')
+        t = torch.tensor([elapsed], dtype=torch.float64, device='cuda' if args.dist_backend == 'nccl' else 'cpu')
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
