@@ -52,9 +52,11 @@ def parse():
     ap.add_argument('--cpu-sample', type=int, default=12000, help='reads in the CPU-baseline sample (0 = skip)')
     ap.add_argument('--cpu-threads', type=int, default=0, help='0 = min(16, cpus available)')
     ap.add_argument('--check', type=int, default=256, help='reads checked against the oracle after timing')
-    ap.add_argument('--workload', choices=['endtrim', 'middle'], default='endtrim',
+    ap.add_argument('--workload', choices=['endtrim', 'middle', 'barcodes'], default='endtrim',
                     help='endtrim: the headline metric (default); middle: end trim + middle-adapter scan '
-                         '(BASELINE.json configs[2])')
+                         '(BASELINE.json configs[2]); barcodes: end trim + barcode demultiplexing against '
+                         '96 barcode sets (configs[3])')
+    ap.add_argument('--barcodes', type=int, default=96, help='barcode sets of the barcodes workload')
     ap.add_argument('--middle-threshold', type=float, default=90.0)
     ap.add_argument('--dist-backend', default='nccl', help='nccl (RCCL over xGMI, default) or gloo (rehearsal of '
                                                            'several ranks sharing one GPU)')
@@ -83,17 +85,33 @@ def main():
         return run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapters)
 
     # ---- workload (host) ----
-    sets = [a for a in A.fresh_adapters() if '(full sequence)' not in a.name][:args.sets]
+    barcodes = args.workload == 'barcodes'
+    if barcodes:
+        # BASELINE.json configs[3]: demultiplexing against 96 barcode sets ('Barcode k (forward)',
+        # porechop_abi/adapters.py) plus the ligation kit adapters, forward orientation
+        allsets = A.fresh_adapters()
+        sets = [a for a in allsets if a.name == 'SQK-NSK007'] + \
+            [a for a in allsets if a.name.startswith('Barcode ') and a.name.endswith('(forward)')][:args.barcodes]
+    else:
+        sets = [a for a in A.fresh_adapters() if '(full sequence)' not in a.name][:args.sets]
     # adapters of the dominant register bucket (21..24 bp -> k_align<24, *, PACKED>) first, so
     # their launch can be timed on its own (roofline); the trim decision is a max over adapters
-    # and does not depend on their order
+    # and does not depend on their order (the barcode dict order is kept through bc slots)
     dom = lambda x: 20 < len(x) <= 24
-    start_adps = [a.start_sequence[1] for a in sets if a.start_sequence]
-    end_adps = [a.end_sequence[1] for a in sets if a.end_sequence]
-    start_adps = [x for x in start_adps if dom(x)] + [x for x in start_adps if not dom(x)]
-    end_adps = [x for x in end_adps if dom(x)] + [x for x in end_adps if not dom(x)]
+    start_sets = [a for a in sets if a.start_sequence]
+    end_sets = [a for a in sets if a.end_sequence]
+    order_s = sorted(range(len(start_sets)), key=lambda k: not dom(start_sets[k].start_sequence[1]))
+    order_e = sorted(range(len(end_sets)), key=lambda k: not dom(end_sets[k].end_sequence[1]))
+    start_adps = [start_sets[k].start_sequence[1] for k in order_s]
+    end_adps = [end_sets[k].end_sequence[1] for k in order_e]
+    pos_s, pos_e = np.argsort(order_s).astype(np.int32), np.argsort(order_e).astype(np.int32)
     t0 = time.time()
-    reads = synth.make_reads(args.reads, args.mean_len, seed=12345 + rank, keep=args.end_size)
+    truth = None
+    if barcodes:
+        reads, truth = synth.make_barcoded_reads(args.reads, [(a.start_sequence[1], a.end_sequence[1]) for a in sets[1:]],
+                                                 args.mean_len, seed=12345 + rank, keep=args.end_size)
+    else:
+        reads = synth.make_reads(args.reads, args.mean_len, seed=12345 + rank, keep=args.end_size)
     buf, s_off, s_len, e_off, e_len = synth.pack_end_windows(reads, args.end_size)
     gen_s = time.time() - t0
     n = args.reads
@@ -167,9 +185,23 @@ def main():
             if key == 'dom' and e1 is not None:
                 L.pcabi_event_record(e1, stream)
 
+    bc = None
+    if barcodes:
+        from custom_porechop_abi_amd.porechop_abi import barcode_slots
+        ids = {}
+        sa_, sn_ = barcode_slots(start_sets, 'forward', ids)
+        ea_, en_ = barcode_slots(end_sets, 'forward', ids)
+        bc = dict(s_adp=h2d(pos_s[sa_]), s_name=h2d(sn_), ns=len(sa_), e_adp=h2d(pos_e[ea_]), e_name=h2d(en_),
+                  ne=len(ea_), d_call=dalloc(4 * n), names={v: k for k, v in ids.items()})
+
     def epilogue():
         _lib.check(L.pcabi_end_trim_dev(d_sres, s_stride, n_sa, d_eres, e_stride, n_ea, n, args.end_size,
                                         2, 75.0, 4, d_st, d_et, None, None, stream), 'end_trim')
+        if bc is not None:
+            # determine_barcode, reference defaults: barcode_threshold 75, barcode_diff 5
+            _lib.check(L.pcabi_barcode_call_dev(d_sres, s_stride, bc['s_adp'], bc['s_name'], bc['ns'], d_eres,
+                                                e_stride, bc['e_adp'], bc['e_name'], bc['ne'], n, 75.0, 5.0, 0,
+                                                bc['d_call'], None, stream), 'barcode_call')
 
     def step(k=None):
         if k is None:
@@ -233,17 +265,29 @@ def main():
     checked = None
     if args.check and rank == 0:
         checked = spot_check(L, _lib, d_sres, d_eres, d_st, d_et, s_stride, e_stride, n, n_sa, n_ea, reads,
-                             start_adps, end_adps, args.end_size, min(args.check, n), sc)
+                             start_adps, end_adps, args.end_size, min(args.check, n), sc, bc=bc,
+                             bc_sets=(start_sets, end_sets, pos_s, pos_e))
+
+    if checked is not None and bc is not None:
+        # demultiplexing sanity: calls vs the barcode each synthetic read was built with
+        call = np.empty(n, np.int32)
+        _lib.check(L.pcabi_dev_d2h(call.ctypes.data_as(vp), bc['d_call'], call.nbytes), 'd2h')
+        ids = {v: k for k, v in bc['names'].items()}
+        want = np.array([ids.get(sets[1 + t].get_barcode_name(), -2) if t >= 0 else -1 for t in truth.tolist()])
+        checked['calls_equal_synthetic_truth'] = round(float(np.mean(call == want)), 4)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        cpu = cpu_baseline(reads[:args.cpu_sample], sets, args.end_size, sc, args.cpu_threads)
+        # bounded sample: ~1.2M reference alignments (~10 s on 16 host threads)
+        k_cpu = max(1, min(args.cpu_sample, args.cpu_sample * 98 // max(1, n_sa + n_ea)))
+        cpu = cpu_baseline(reads[:k_cpu], sets, args.end_size, sc, args.cpu_threads)
 
     if rank == 0:
         value = world * n * args.steps / elapsed
         prof = load_traffic()
         out = {
-            'metric': 'reads/sec trimmed (100k ONT reads x 50 adapter pairs)',
+            'metric': ('reads/sec trimmed + demultiplexed (ONT reads x %d barcode sets)' % (len(sets) - 1) if barcodes
+                       else 'reads/sec trimmed (100k ONT reads x 50 adapter pairs)'),
             'value': round(value, 1),
             'unit': 'reads/s',
             'n_gpus': world,
@@ -255,18 +299,22 @@ def main():
             'vs_baseline': None,
             'dtype': 'int32',
             'data': 'synthetic (seeded ONT-like reads, SURVEY.md §8d recipe; mean %d bp)' % args.mean_len,
-            'config': {'workload': 'end-trim: %d reads/GPU x %d adapter sets (%d start + %d end adapters), '
-                                   'start+end windows of %d bp, + per-read trim decisions'
-                                   % (n, len(sets), n_sa, n_ea, args.end_size),
+            'config': {'workload': ('barcode demux: %d reads/GPU x %d barcode sets + SQK-NSK007 (%d start + %d end '
+                                    'adapters), start+end windows of %d bp, + per-read trim decisions and barcode '
+                                    'calls (determine_barcode, threshold 75, diff 5)'
+                                    % (n, len(sets) - 1, n_sa, n_ea, args.end_size)) if barcodes else
+                                   ('end-trim: %d reads/GPU x %d adapter sets (%d start + %d end adapters), '
+                                    'start+end windows of %d bp, + per-read trim decisions'
+                                    % (n, len(sets), n_sa, n_ea, args.end_size)),
                        'reads_per_gpu': n, 'adapter_sets': len(sets), 'end_size': args.end_size,
                        'scoring': list(sc), 'parallelism': 'dp%d (read shards)' % world},
             'roofline': {'bound': 'valu', 'achieved': round(tops, 3), 'peak': round(VALU_PEAK_TOPS, 1),
                          'unit': 'Tops/s (int32 lane-ops)', 'frac': round(tops / VALU_PEAK_TOPS, 4),
-                         'traffic': prof.get('traffic_bytes_per_launch') if prof else None,
+                         'traffic': prof.get('traffic_bytes_per_launch') if prof and not barcodes else None,
                          'kernel': DOM_KERNEL,
                          'launch_ms': round(launch_ms, 4), 'cells_per_launch': int(launch_cells),
                          'ops_per_cell': OPS_PER_CELL,
-                         'traffic_source': prof.get('source') if prof else None},
+                         'traffic_source': prof.get('source') if prof and not barcodes else None},
             'hbm': {'achieved': round(gbs, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                     'frac': round(gbs / HBM_PEAK_GBS, 5), 'algorithmic_bytes_per_launch': int(launch_bytes),
                     'kernel': DOM_KERNEL},
@@ -515,8 +563,10 @@ def cpu_baseline_middle(reads, trims, mid_adps, sc, thr, threads):
 
 
 def spot_check(L, _lib, d_sres, d_eres, d_st, d_et, s_stride, e_stride, n, n_sa, n_ea, reads, start_adps,
-               end_adps, E, k, sc):
-    """Compare the first k reads' trim amounts and raw alignment fields with the oracle."""
+               end_adps, E, k, sc, bc=None, bc_sets=None):
+    """Compare the first k reads' raw alignment fields with the oracle (and, for the barcodes
+    workload, the device barcode calls with NanoporeRead.determine_barcode over the oracle's
+    identities, dicts filled in set order as find_start_trim / find_end_trim do)."""
     from tests import oracle_lib
     from custom_porechop_abi_amd import synth
     vp = ctypes.c_void_p
@@ -533,13 +583,34 @@ def spot_check(L, _lib, d_sres, d_eres, d_st, d_et, s_stride, e_stride, n, n_sa,
             heads.append(synth.codes_to_str(r[:E]))
             tails.append(synth.codes_to_str(r[-E:]))
     bad = 0
+    exps = []
     for wins, adps, res, nad in ((heads, start_adps, sres, n_sa), (tails, end_adps, eres, n_ea)):
         pr = np.tile(np.arange(k), nad)
         pa = np.repeat(np.arange(nad), k)
         exp = oracle_lib.align_many(wins, adps, (pr, pa), sc)
         got = res.reshape(8, nad, n)[:, :, :k].reshape(8, -1)
         bad += int(np.sum(np.any(got != exp, axis=0)))
-    return {'pairs_checked': int(k * (n_sa + n_ea)), 'mismatches': bad}
+        exps.append(exp)
+    out = {'pairs_checked': int(k * (n_sa + n_ea)), 'mismatches': bad}
+    if bc is not None:
+        from custom_porechop_abi_amd.nanopore_read import NanoporeRead
+        call = np.empty(n, np.int32)
+        _lib.check(L.pcabi_dev_d2h(call.ctypes.data_as(vp), bc['d_call'], call.nbytes), 'd2h')
+        start_sets, end_sets, pos_s, pos_e = bc_sets
+        bad_calls = 0
+        for r in range(k):
+            read = NanoporeRead('r', 'A', '')
+            for sets_, pos, exp, d in ((start_sets, pos_s, exps[0], read.start_barcode_scores),
+                                       (end_sets, pos_e, exps[1], read.end_barcode_scores)):
+                for j, a in enumerate(sets_):
+                    if a.is_barcode() and a.barcode_direction() == 'forward':
+                        i = int(pos[j]) * k + r
+                        d[a.get_barcode_name()] = 0.0 if exp[0, i] == -1 else float('%f' % (100.0 * exp[5, i] / exp[7, i]))
+            read.determine_barcode(75.0, 5.0, False)
+            bad_calls += int(read.barcode_call != bc['names'].get(int(call[r]), 'none'))
+        out.update({'barcode_calls_checked': k, 'barcode_call_mismatches': bad_calls,
+                    'barcoded_fraction': round(float(np.mean(call != -1)), 4)})
+    return out
 
 
 def cpu_baseline(reads, sets, E, sc, threads):

@@ -391,6 +391,84 @@ __global__ __launch_bounds__(256) void k_best_full_id(const int32_t *res, int64_
     }
 }
 
+// Barcode call (porechop_abi/nanopore_read.py:408-482) over the barcode dicts that
+// find_start_trim / find_end_trim fill (:193-195, :215-217). A side's dict is given as slots in
+// insertion order: slot k holds barcode id name[k] with the full-adapter identity of adapter
+// adp[k] (the LAST adapter of that name in set order -- a dict keeps a key's first position and
+// its last value). The reference's stable sorts reduce to strict '>' scans in slot order:
+//   per side  : best / second = first two of the descending stable sort
+//   merged    : entries ordered by (-score, start before end, slot); best = the first, second =
+//               the first entry whose name differs (the dedup keeps each name's first entry)
+// Missing entries are ('none', 0.0), the reference's defaults (nanopore_read.py:58-61).
+struct BcSide {
+    const int32_t *res;
+    int64_t stride;
+    const int32_t *adp, *name;
+    int32_t n;
+};
+
+__device__ __forceinline__ double bc_score(const BcSide &s, int k, int64_t n_read, int64_t r) {
+    const int64_t i = (int64_t)s.adp[k] * n_read + r;
+    return s.res[0 * s.stride + i] == -1 ? 0.0 : pcabi::pid6(s.res[5 * s.stride + i], s.res[7 * s.stride + i]);
+}
+
+__global__ __launch_bounds__(256) void k_barcode_call(BcSide st, BcSide en, int64_t n_read, double thr, double diff,
+                                                      int require_two, int32_t *call, double *scores) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_read) return;
+    int c = -1;
+    if (require_two) {
+        double b[2][2] = {{0.0, 0.0}, {0.0, 0.0}};   // [side][best, second]
+        int bn[2] = {-1, -1};
+        int cnt[2] = {0, 0};
+        for (int side = 0; side < 2; ++side) {
+            const BcSide &s = side ? en : st;
+            for (int k = 0; k < s.n; ++k) {
+                const double x = bc_score(s, k, n_read, r);
+                if (cnt[side] == 0 || x > b[side][0]) {
+                    if (cnt[side] > 0) b[side][1] = b[side][0];
+                    b[side][0] = x;
+                    bn[side] = s.name[k];
+                } else if (cnt[side] == 1 || x > b[side][1]) {
+                    b[side][1] = x;
+                }
+                ++cnt[side];
+            }
+        }
+        if (b[0][0] >= thr && b[1][0] >= thr && b[0][0] >= b[0][1] + diff && b[1][0] >= b[1][1] + diff &&
+            bn[0] == bn[1])
+            c = bn[0];
+        if (scores) {
+            scores[4 * r + 0] = b[0][0]; scores[4 * r + 1] = b[0][1];
+            scores[4 * r + 2] = b[1][0]; scores[4 * r + 3] = b[1][1];
+        }
+    } else {
+        double b1 = 0.0, b2 = 0.0;
+        int n1 = -1;
+        bool has1 = false, has2 = false;
+        for (int side = 0; side < 2; ++side) {
+            const BcSide &s = side ? en : st;
+            for (int k = 0; k < s.n; ++k) {
+                const double x = bc_score(s, k, n_read, r);
+                const int nm = s.name[k];
+                if (!has1 || x > b1) {
+                    // the previous best heads the entries of every other name
+                    if (has1 && n1 != nm) { b2 = b1; has2 = true; }
+                    b1 = x; n1 = nm; has1 = true;
+                } else if (nm != n1 && (!has2 || x > b2)) {
+                    b2 = x; has2 = true;
+                }
+            }
+        }
+        if (b1 >= thr && b1 >= b2 + diff) c = has1 ? n1 : -1;
+        if (scores) {
+            scores[4 * r + 0] = b1; scores[4 * r + 1] = b2;
+            scores[4 * r + 2] = 0.0; scores[4 * r + 3] = 0.0;
+        }
+    }
+    call[r] = c;
+}
+
 // Middle-scan round 1 (porechop_abi/nanopore_read.py:219-252): per read, the FIRST adapter in
 // list order whose full-adapter identity is not below the threshold on the unmasked read. The
 // reference's loop hits exactly that adapter first (the ones before it fail on this same
@@ -727,7 +805,7 @@ struct Engine {
     std::mutex mu;
     bool init = false;
     hipStream_t stream = nullptr;
-    DeviceBuf codes, woff, wlen, out, tasks_win, tasks_out, wave_adp, tiles, toff, hits;
+    DeviceBuf codes, woff, wlen, out, tasks_win, tasks_out, wave_adp, tiles, toff, hits, bc;
     pcabi_scan *scan = nullptr;   // scratch of the middle scan (pcabi_middle_scan_host)
     DeviceBuf pad[kNumBuckets], len[kNumBuckets], id[kNumBuckets];
 };
@@ -1569,6 +1647,71 @@ int pcabi_best_full_identity_dev(const int32_t *res, int64_t stride, int64_t n_w
     hipLaunchKernelGGL(k_best_full_id, dim3((unsigned)n_adp), dim3(256), 0, (hipStream_t)stream, res, stride,
                        n_win, best);
     HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int pcabi_barcode_call_dev(const int32_t *start_res, int64_t start_stride, const int32_t *start_slot_adp,
+                           const int32_t *start_slot_name, int32_t n_start_slots, const int32_t *end_res,
+                           int64_t end_stride, const int32_t *end_slot_adp, const int32_t *end_slot_name,
+                           int32_t n_end_slots, int64_t n_read, double barcode_threshold, double barcode_diff,
+                           int require_two, int32_t *call, double *scores, void *stream) {
+    if (n_read < 0 || n_start_slots < 0 || n_end_slots < 0) return fail(PCABI_E_ARG, "negative count");
+    if (n_read == 0) return 0;
+    const BcSide st{start_res, start_stride, start_slot_adp, start_slot_name, n_start_slots};
+    const BcSide en{end_res, end_stride, end_slot_adp, end_slot_name, n_end_slots};
+    hipLaunchKernelGGL(k_barcode_call, dim3((unsigned)((n_read + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       st, en, n_read, barcode_threshold, barcode_diff, require_two, call, scores);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int pcabi_barcode_call_host(int device, const int32_t *start_res, int32_t n_sa, const int32_t *start_slot_adp,
+                            const int32_t *start_slot_name, int32_t n_start_slots, const int32_t *end_res,
+                            int32_t n_ea, const int32_t *end_slot_adp, const int32_t *end_slot_name,
+                            int32_t n_end_slots, int64_t n_read, double barcode_threshold, double barcode_diff,
+                            int require_two, int32_t *call, double *scores) {
+    if (device < 0 || device >= 16) return fail(PCABI_E_ARG, "bad device index");
+    if (n_read < 0 || n_sa < 0 || n_ea < 0 || n_start_slots < 0 || n_end_slots < 0)
+        return fail(PCABI_E_ARG, "negative count");
+    for (int k = 0; k < n_start_slots; ++k)
+        if (start_slot_adp[k] < 0 || start_slot_adp[k] >= n_sa) return fail(PCABI_E_ARG, "start slot adapter out of range");
+    for (int k = 0; k < n_end_slots; ++k)
+        if (end_slot_adp[k] < 0 || end_slot_adp[k] >= n_ea) return fail(PCABI_E_ARG, "end slot adapter out of range");
+    if (n_read == 0) return 0;
+    Engine &e = g_engines[device];
+    std::lock_guard<std::mutex> lock(e.mu);
+    if (int rc = engine_init(e, device)) return rc;
+    HIP_TRY(hipSetDevice(device));
+    const size_t sres = sizeof(int32_t) * PCABI_NFIELDS * (size_t)n_sa * (size_t)n_read;
+    const size_t eres = sizeof(int32_t) * PCABI_NFIELDS * (size_t)n_ea * (size_t)n_read;
+    const size_t slots = sizeof(int32_t) * 2 * (size_t)(n_start_slots + n_end_slots);
+    if (int rc = e.bc.ensure(sres + eres + slots + sizeof(int32_t) * (size_t)n_read + 32 * (size_t)n_read + 64))
+        return rc;
+    char *p = (char *)e.bc.p;
+    int32_t *d_sres = (int32_t *)p; p += sres;
+    int32_t *d_eres = (int32_t *)p; p += eres;
+    int32_t *d_slots = (int32_t *)p; p += slots;
+    int32_t *d_call = (int32_t *)p; p += sizeof(int32_t) * (size_t)n_read;
+    p = (char *)(((uintptr_t)p + 7) & ~(uintptr_t)7);
+    double *d_scores = (double *)p;
+    std::vector<int32_t> h_slots;
+    h_slots.insert(h_slots.end(), start_slot_adp, start_slot_adp + n_start_slots);
+    h_slots.insert(h_slots.end(), start_slot_name, start_slot_name + n_start_slots);
+    h_slots.insert(h_slots.end(), end_slot_adp, end_slot_adp + n_end_slots);
+    h_slots.insert(h_slots.end(), end_slot_name, end_slot_name + n_end_slots);
+    if (sres) HIP_TRY(hipMemcpyAsync(d_sres, start_res, sres, hipMemcpyHostToDevice, e.stream));
+    if (eres) HIP_TRY(hipMemcpyAsync(d_eres, end_res, eres, hipMemcpyHostToDevice, e.stream));
+    if (slots) HIP_TRY(hipMemcpyAsync(d_slots, h_slots.data(), slots, hipMemcpyHostToDevice, e.stream));
+    const int32_t *ss = d_slots, *en_ = d_slots + 2 * n_start_slots;
+    if (int rc = pcabi_barcode_call_dev(d_sres, (int64_t)n_sa * n_read, ss, ss + n_start_slots, n_start_slots, d_eres,
+                                        (int64_t)n_ea * n_read, en_, en_ + n_end_slots, n_end_slots, n_read,
+                                        barcode_threshold, barcode_diff, require_two, d_call,
+                                        scores ? d_scores : nullptr, e.stream))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(call, d_call, sizeof(int32_t) * (size_t)n_read, hipMemcpyDeviceToHost, e.stream));
+    if (scores)
+        HIP_TRY(hipMemcpyAsync(scores, d_scores, 32 * (size_t)n_read, hipMemcpyDeviceToHost, e.stream));
+    HIP_TRY(hipStreamSynchronize(e.stream));
     return 0;
 }
 

@@ -198,3 +198,32 @@ def identities(res):
     part[failed] = 0.0
     read_end = np.where(failed, 0, res[1] + 1).astype(np.int64)
     return full, part, rs.astype(np.int64), read_end
+
+
+def barcode_call(start_res, end_res, start_slots, end_slots, n_read, barcode_threshold, barcode_diff,
+                 require_two, device=0, with_scores=False):
+    """determine_barcode for a batch of reads on the GPU (pcabi_barcode_call_host,
+    porechop_abi/nanopore_read.py:408-482).
+
+    start_res / end_res: int32 (8, n_adp * n_read) cross-product results (column a*n_read + r).
+    *_slots: (slot_adp, slot_name) int32 arrays, the side's barcode dict in insertion order
+    (porechop_abi.barcode_slots). Returns call int32[n_read] (barcode id, -1 = 'none') and, with
+    with_scores, float64 (n_read, 4)."""
+    def side(res, slots):
+        res = np.ascontiguousarray(res, dtype=np.int32).reshape(NFIELDS, -1)
+        adp = np.ascontiguousarray(slots[0], dtype=np.int32)
+        name = np.ascontiguousarray(slots[1], dtype=np.int32)
+        n_adp = res.shape[1] // n_read if n_read else 0
+        return res, adp, name, n_adp
+
+    sr, sa, sn, n_sa = side(start_res, start_slots)
+    er, ea, en, n_ea = side(end_res, end_slots)
+    call = np.full(n_read, -1, dtype=np.int32)
+    scores = np.zeros((n_read, 4), dtype=np.float64) if with_scores else None
+    if n_read:
+        rc = lib().pcabi_barcode_call_host(device, _ptr(sr), n_sa, _ptr(sa), _ptr(sn), len(sa), _ptr(er), n_ea,
+                                           _ptr(ea), _ptr(en), len(ea), n_read, float(barcode_threshold),
+                                           float(barcode_diff), int(bool(require_two)), _ptr(call),
+                                           _ptr(scores) if with_scores else None)
+        check(rc, 'pcabi_barcode_call_host')
+    return (call, scores) if with_scores else call

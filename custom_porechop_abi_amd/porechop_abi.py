@@ -225,6 +225,28 @@ def _apply_end_decisions(reads, starts, s_hits, ends, e_hits, end_size, extra, t
                     d[name] = v
 
 
+def barcode_slots(sets, forward_or_reverse, name_ids):
+    """The barcode dict find_start_trim / find_end_trim build for every read
+    (nanopore_read.py:193-195, 215-217) as slots for pcabi_barcode_call: in insertion order, the
+    table index (among `sets`, the side's adapter table) of the adapter whose identity is the
+    entry's final value -- a dict keeps a name's first position and its last value -- and the
+    name's id in `name_ids` (extended in place, shared by both sides)."""
+    pos, adp, name = {}, [], []
+    for k, a in enumerate(sets):
+        if not (a.is_barcode() and a.barcode_direction() == forward_or_reverse):
+            continue
+        nm = a.get_barcode_name()
+        if nm not in name_ids:
+            name_ids[nm] = len(name_ids)
+        if nm in pos:
+            adp[pos[nm]] = k
+        else:
+            pos[nm] = len(adp)
+            adp.append(k)
+            name.append(name_ids[nm])
+    return np.array(adp, np.int32), np.array(name, np.int32)
+
+
 # ---------------------------------------------------------------------------------------------
 def middle_adapter_list(matching_sets):
     """porechop_abi.py:465-479: start sequences, plus end sequences that differ from their

@@ -107,3 +107,50 @@ _LETTERS = np.frombuffer(b'ACGTN', dtype=np.uint8)
 
 def codes_to_str(c):
     return _LETTERS[np.asarray(c, dtype=np.intp)].tobytes().decode()
+
+
+def revcomp_codes(c):
+    return (3 - np.asarray(c, dtype=np.uint8)[::-1]).astype(np.uint8)
+
+
+def make_barcoded_reads(n_reads, barcodes, mean_len=8000, seed=12345, keep=None):
+    """Seeded barcoded reads for the demultiplexing workload (BASELINE.json configs[3]).
+
+    barcodes: list of (start_seq, end_seq) strings, e.g. the 'Barcode k (forward)' sets of
+    porechop_abi/adapters.py. Per read (lengths as make_reads):
+      * p=0.9 barcoded with a uniform barcode b, else no barcode;
+      * p=0.85: 0-20 random bases + Y_Top (10% mutated) + b's start sequence (10% mutated) prefix;
+      * p=0.75: b's end sequence (10% mutated) + Y_Bottom (10% mutated) + 0-20 random bases suffix.
+    Returns (reads, truth) with truth[k] = barcode index or -1; `keep` as in make_reads."""
+    rng = np.random.default_rng(seed)
+    top, bottom = _codes(Y_TOP), _codes(Y_BOTTOM)
+    bcs = [(_codes(s), _codes(e)) for s, e in barcodes]
+    lens = np.maximum(200, (rng.lognormal(0.0, 0.5, n_reads) * mean_len * 0.8825).astype(np.int64))
+    barcoded = rng.random(n_reads) < 0.9
+    which = rng.integers(0, len(bcs), n_reads)
+    has_start = rng.random(n_reads) < 0.85
+    has_end = rng.random(n_reads) < 0.75
+    out, truth = [], []
+    for k in range(n_reads):
+        n = int(lens[k])
+        b = int(which[k]) if barcoded[k] else -1
+        pre = np.empty(0, np.uint8)
+        suf = np.empty(0, np.uint8)
+        if has_start[k]:
+            parts = [rng.integers(0, 4, rng.integers(0, 21), dtype=np.uint8), mutate(rng, top, 0.10)]
+            if b >= 0:
+                parts.append(mutate(rng, bcs[b][0], 0.10))
+            pre = np.concatenate(parts)
+        if has_end[k]:
+            parts = [mutate(rng, bcs[b][1], 0.10)] if b >= 0 else []
+            parts += [mutate(rng, bottom, 0.10), rng.integers(0, 4, rng.integers(0, 21), dtype=np.uint8)]
+            suf = np.concatenate(parts)
+        body_len = max(0, n - len(pre) - len(suf))
+        truth.append(b)
+        if keep is not None and n > 2 * keep + 64:
+            head = np.concatenate([pre, rng.integers(0, 4, max(0, keep + 32 - len(pre)), dtype=np.uint8)])[:keep]
+            tail = np.concatenate([rng.integers(0, 4, max(0, keep + 32 - len(suf)), dtype=np.uint8), suf])[-keep:]
+            out.append((head, tail, len(pre) + body_len + len(suf)))
+            continue
+        out.append(np.concatenate([pre, rng.integers(0, 4, body_len, dtype=np.uint8), suf]))
+    return out, np.array(truth, np.int32)

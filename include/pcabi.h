@@ -235,6 +235,34 @@ int64_t pcabi_middle_scan_host(int device, const uint8_t *codes, int64_t codes_l
 int pcabi_best_full_identity_dev(const int32_t *res, int64_t stride, int64_t n_win, int32_t n_adp,
                                  double *best, void *stream);
 
+/*
+ * Barcode demultiplexing call (porechop_abi/nanopore_read.py:408-482, determine_barcode) from
+ * the barcode dicts find_start_trim / find_end_trim fill (nanopore_read.py:193-195, 215-217).
+ * Replaces the per-read Python loop of porechop_abi.py:359-438 when -b is given.
+ *   *_res            : cross-product result blocks (layout of pcabi_align_cross_dev), n_read
+ *                      windows x the side's adapters
+ *   *_slot_adp[k]    : slot k of the side's dict in insertion order = the adapter (index into the
+ *                      side's table) whose full identity is the entry's value (the last adapter of
+ *                      that barcode name in set order)
+ *   *_slot_name[k]   : the entry's barcode id (ids >= 0, shared by both sides)
+ * Identities are pid6(m, l2) (the reference's "%f" round trip), 0.0 for a failed alignment.
+ * Writes call[n_read] = barcode id or -1 ('none'); scores (optional, double[4 * n_read]):
+ * require_two -> best start, second start, best end, second end; else best, second overall.
+ * The albacore cross-check (nanopore_read.py:479-482) stays with the caller.
+ *   pcabi_barcode_call_dev  : device pointers, async on `stream`.
+ *   pcabi_barcode_call_host : host result arrays int32[PCABI_NFIELDS][n_adp * n_read] per side.
+ */
+int pcabi_barcode_call_dev(const int32_t *start_res, int64_t start_stride, const int32_t *start_slot_adp,
+                           const int32_t *start_slot_name, int32_t n_start_slots, const int32_t *end_res,
+                           int64_t end_stride, const int32_t *end_slot_adp, const int32_t *end_slot_name,
+                           int32_t n_end_slots, int64_t n_read, double barcode_threshold, double barcode_diff,
+                           int require_two, int32_t *call, double *scores, void *stream);
+int pcabi_barcode_call_host(int device, const int32_t *start_res, int32_t n_sa, const int32_t *start_slot_adp,
+                            const int32_t *start_slot_name, int32_t n_start_slots, const int32_t *end_res,
+                            int32_t n_ea, const int32_t *end_slot_adp, const int32_t *end_slot_name,
+                            int32_t n_end_slots, int64_t n_read, double barcode_threshold, double barcode_diff,
+                            int require_two, int32_t *call, double *scores);
+
 #ifdef __cplusplus
 }
 #endif
