@@ -57,6 +57,9 @@ def parse():
                          '(BASELINE.json configs[2]); barcodes: end trim + barcode demultiplexing against '
                          '96 barcode sets (configs[3])')
     ap.add_argument('--barcodes', type=int, default=96, help='barcode sets of the barcodes workload')
+    ap.add_argument('--kit', choices=['pcr96', 'native12'], default='pcr96',
+                    help='barcodes workload: pcr96 = Barcode 1..96 (forward) sets; native12 = native '
+                         'barcoding, Barcode 1..12 (reverse) + their 68/63 bp full-sequence adapters')
     ap.add_argument('--middle-threshold', type=float, default=90.0)
     ap.add_argument('--dist-backend', default='nccl', help='nccl (RCCL over xGMI, default) or gloo (rehearsal of '
                                                            'several ranks sharing one GPU)')
@@ -90,8 +93,17 @@ def main():
         # BASELINE.json configs[3]: demultiplexing against 96 barcode sets ('Barcode k (forward)',
         # porechop_abi/adapters.py) plus the ligation kit adapters, forward orientation
         allsets = A.fresh_adapters()
-        sets = [a for a in allsets if a.name == 'SQK-NSK007'] + \
-            [a for a in allsets if a.name.startswith('Barcode ') and a.name.endswith('(forward)')][:args.barcodes]
+        if args.kit == 'native12':
+            # porechop_abi.py:332-356 adds the full native sequences for every found barcode
+            nb = min(args.barcodes, 12)
+            sets = [a for a in allsets if a.name == 'SQK-NSK007'] + \
+                [a for a in allsets if a.name.startswith('Barcode ') and a.name.endswith('(reverse)')][:nb] + \
+                [A.make_full_native_barcode_adapter(i) for i in range(1, nb + 1)]
+            bc_dir = 'reverse'
+        else:
+            sets = [a for a in allsets if a.name == 'SQK-NSK007'] + \
+                [a for a in allsets if a.name.startswith('Barcode ') and a.name.endswith('(forward)')][:args.barcodes]
+            bc_dir = 'forward'
     else:
         sets = [a for a in A.fresh_adapters() if '(full sequence)' not in a.name][:args.sets]
     # adapters of the dominant register bucket (21..24 bp -> k_align<24, *, PACKED>) first, so
@@ -108,7 +120,8 @@ def main():
     t0 = time.time()
     truth = None
     if barcodes:
-        reads, truth = synth.make_barcoded_reads(args.reads, [(a.start_sequence[1], a.end_sequence[1]) for a in sets[1:]],
+        carried = [a for a in sets[1:] if '(full sequence)' in a.name] or sets[1:]
+        reads, truth = synth.make_barcoded_reads(args.reads, [(a.start_sequence[1], a.end_sequence[1]) for a in carried],
                                                  args.mean_len, seed=12345 + rank, keep=args.end_size)
     else:
         reads = synth.make_reads(args.reads, args.mean_len, seed=12345 + rank, keep=args.end_size)
@@ -189,10 +202,10 @@ def main():
     if barcodes:
         from custom_porechop_abi_amd.porechop_abi import barcode_slots
         ids = {}
-        sa_, sn_ = barcode_slots(start_sets, 'forward', ids)
-        ea_, en_ = barcode_slots(end_sets, 'forward', ids)
+        sa_, sn_ = barcode_slots(start_sets, bc_dir, ids)
+        ea_, en_ = barcode_slots(end_sets, bc_dir, ids)
         bc = dict(s_adp=h2d(pos_s[sa_]), s_name=h2d(sn_), ns=len(sa_), e_adp=h2d(pos_e[ea_]), e_name=h2d(en_),
-                  ne=len(ea_), d_call=dalloc(4 * n), names={v: k for k, v in ids.items()})
+                  ne=len(ea_), d_call=dalloc(4 * n), names={v: k for k, v in ids.items()}, dir=bc_dir)
 
     def epilogue():
         _lib.check(L.pcabi_end_trim_dev(d_sres, s_stride, n_sa, d_eres, e_stride, n_ea, n, args.end_size,
@@ -286,7 +299,10 @@ def main():
         value = world * n * args.steps / elapsed
         prof = load_traffic()
         out = {
-            'metric': ('reads/sec trimmed + demultiplexed (ONT reads x %d barcode sets)' % (len(sets) - 1) if barcodes
+            'metric': ('reads/sec trimmed + demultiplexed (ONT reads x %d barcode sets)' % (len(sets) - 1)
+                       if barcodes and args.kit == 'pcr96' else
+                       'reads/sec trimmed + demultiplexed (native barcoding, %d barcodes + full sequences)' % nb
+                       if barcodes
                        else 'reads/sec trimmed (100k ONT reads x 50 adapter pairs)'),
             'value': round(value, 1),
             'unit': 'reads/s',
@@ -299,10 +315,10 @@ def main():
             'vs_baseline': None,
             'dtype': 'int32',
             'data': 'synthetic (seeded ONT-like reads, SURVEY.md §8d recipe; mean %d bp)' % args.mean_len,
-            'config': {'workload': ('barcode demux: %d reads/GPU x %d barcode sets + SQK-NSK007 (%d start + %d end '
+            'config': {'workload': ('barcode demux (%s): %d reads/GPU x %d barcode sets + SQK-NSK007 (%d start + %d end '
                                     'adapters), start+end windows of %d bp, + per-read trim decisions and barcode '
                                     'calls (determine_barcode, threshold 75, diff 5)'
-                                    % (n, len(sets) - 1, n_sa, n_ea, args.end_size)) if barcodes else
+                                    % (args.kit, n, len(sets) - 1, n_sa, n_ea, args.end_size)) if barcodes else
                                    ('end-trim: %d reads/GPU x %d adapter sets (%d start + %d end adapters), '
                                     'start+end windows of %d bp, + per-read trim decisions'
                                     % (n, len(sets), n_sa, n_ea, args.end_size)),
@@ -603,7 +619,7 @@ def spot_check(L, _lib, d_sres, d_eres, d_st, d_et, s_stride, e_stride, n, n_sa,
             for sets_, pos, exp, d in ((start_sets, pos_s, exps[0], read.start_barcode_scores),
                                        (end_sets, pos_e, exps[1], read.end_barcode_scores)):
                 for j, a in enumerate(sets_):
-                    if a.is_barcode() and a.barcode_direction() == 'forward':
+                    if a.is_barcode() and a.barcode_direction() == bc['dir']:
                         i = int(pos[j]) * k + r
                         d[a.get_barcode_name()] = 0.0 if exp[0, i] == -1 else float('%f' % (100.0 * exp[5, i] / exp[7, i]))
             read.determine_barcode(75.0, 5.0, False)

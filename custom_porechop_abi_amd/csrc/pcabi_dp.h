@@ -598,29 +598,42 @@ namespace pcabi {
 // sentinel fit the 10-bit field, m, nD <= L <= 63 fit 6 bits, span bound <= 255.
 // ==========================================================================================
 namespace pk {
-constexpr int M_SH = 0, D_SH = 6, C_SH = 12, TB_SH = 20, SC_SH = 22;
-constexpr int32_t TB1 = 1 << TB_SH, TB2 = 2 << TB_SH, TB3 = 3 << TB_SH, TBM = 3 << TB_SH;
-constexpr int32_t INC_D = 1 << D_SH, INC_M = (1 << D_SH) + 1;
-constexpr int MAX_RPL = 64;
-constexpr int MAX_L = 63;                       // m, nD fit 6 bits
-PCABI_HD int32_t sc(int v) { return (int32_t)((uint32_t)v << SC_SH); }   // score -> key units
-PCABI_HD int32_t start(int c) { return (int32_t)(((uint32_t)c & 255u) << C_SH); }   // c mod 256
-PCABI_HD int score(int32_t k) { return k >> SC_SH; }
-PCABI_HD int tb(int32_t k) { return (k >> TB_SH) & 3; }
-PCABI_HD uint32_t attr(int32_t k) { return (uint32_t)k & ((1u << TB_SH) - 1u); }
-// packed attribute of a path ending in column bj -> standard attribute word (finish()):
-// c in [bj - 255, bj] is recovered from its residue mod 256
-PCABI_HD uint32_t to_std(uint32_t a, int bj) {
-    const uint32_t m = a & 63u, nd = (a >> D_SH) & 63u;
-    const int c = bj - (int)(((uint32_t)bj - (a >> C_SH)) & 255u);
-    return attr_start(c) | (nd << ATTR_B) | m;
-}
-PCABI_HD int neg_score(int L, const Scoring &s) {
-    const int g = (s.go < s.ge ? s.go : s.ge);
-    const int lo = (L * s.mi < 0 ? L * s.mi : 0) + 2 * (g < 0 ? g : 0);
-    const int gm = (-s.go > -s.ge ? -s.go : -s.ge);
-    return lo - 2 * (gm > 0 ? gm : 0) - 8;
-}
+// Key layout of a register bucket: RPL <= 64 keeps the layout above (score 10 bits, m / nD six
+// bits each = m + 64 nD); the wide buckets (64 < RPL <= 88: the 63-111 bp "full sequence" barcode
+// adapters) trade a score bit for a mixed-radix count field m + (RPL + 1) nD of 13 bits:
+//      [ score : 9 (signed) ][ tb : 2 ][ c mod 256 : 8 ][ m + (RPL+1) nD : 13 ]
+// Both counts grow only by adding the diagonal step's constant (INC_D / INC_M), so the field
+// never carries (m <= nD <= L <= RPL).
+template <int RPL>
+struct Lay {
+    static constexpr bool WIDE = RPL > 64;
+    static constexpr int SC_SH = WIDE ? 23 : 22;
+    static constexpr int TB_SH = SC_SH - 2;
+    static constexpr int C_SH = TB_SH - 8;
+    static constexpr int MB = WIDE ? RPL + 1 : 64;              // radix of the count field
+    static constexpr int32_t TB1 = 1 << TB_SH, TB2 = 2 << TB_SH, TB3 = 3 << TB_SH, TBM = 3 << TB_SH;
+    static constexpr int32_t INC_D = MB, INC_M = MB + 1;
+    static constexpr int SC_MIN = -(1 << (31 - SC_SH)), SC_MAX = (1 << (31 - SC_SH)) - 1;
+    static PCABI_HD int32_t sc(int v) { return (int32_t)((uint32_t)v << SC_SH); }   // score -> key units
+    static PCABI_HD int32_t start(int c) { return (int32_t)(((uint32_t)c & 255u) << C_SH); }   // c mod 256
+    static PCABI_HD int score(int32_t k) { return k >> SC_SH; }
+    static PCABI_HD int tb(int32_t k) { return (k >> TB_SH) & 3; }
+    static PCABI_HD uint32_t attr(int32_t k) { return (uint32_t)k & ((1u << TB_SH) - 1u); }
+    // packed attribute of a path ending in column bj -> standard attribute word (finish()):
+    // c in [bj - 255, bj] is recovered from its residue mod 256
+    static PCABI_HD uint32_t to_std(uint32_t a, int bj) {
+        const uint32_t cnt = a & ((1u << C_SH) - 1u);
+        const uint32_t m = cnt % (uint32_t)MB, nd = cnt / (uint32_t)MB;
+        const int c = bj - (int)(((uint32_t)bj - (a >> C_SH)) & 255u);
+        return attr_start(c) | (nd << ATTR_B) | m;
+    }
+};
+constexpr int MAX_RPL = 88;
+constexpr int MAX_L = 88;
+// The sentinel NEG (H(., 0), V(0, .)) only ever competes in column 1 (H-extend vs H-open from
+// S(i, 0) = 0) and row 1 (V-extend vs V-open from S(0, j) = 0): it must lose there, NEG + ge <
+// gap_open, and nothing else (after those maxes every value is a real DP value).
+PCABI_HD int neg_score(const Scoring &s) { return s.go - s.ge - 1; }
 }  // namespace pk
 
 // Columns spanned by the reported path: it scores >= 0 (the scout is seeded with 0), so its
@@ -630,20 +643,48 @@ PCABI_HD int packed_span_bound(int L, const Scoring &s) {
     return L + (s.ma > 0 ? (s.ma * L) / g : 0);
 }
 
-PCABI_HD bool packed_ok(int L, int rpl, const Scoring &s) {
-    if (rpl > pk::MAX_RPL || L > pk::MAX_L || L > rpl) return false;
-    // padding rows (any number: the substitution table passes scores through them) are exact
-    // only when opening or extending a gap always costs
-    if (L < rpl && !((s.go != s.ge) ? (s.go < 0 && s.ge < 0) : (s.ge < 0))) return false;
+// Range conditions of the packed core for an adapter of L bases in register bucket rpl:
+//   * gaps cost (go, ge < 0): padding rows pass scores through, and the span bound exists;
+//   * every key value fits the score field. All DP values of real rows are >= Smin = the
+//     vertical path from row 0 (go + (L-1) ge; L ge linear) and <= L ma; the candidates and
+//     stored keys add at most one gap pair or one substitution to a DP value: [Smin + min(go + ge,
+//     mi, ma), max(L ma, 0)]; the sentinel and its one extension NEG + ge must fit too;
+//   * m, nD <= L fit the count field, and the reported path spans < 256 columns (c mod 256).
+template <int RPL>
+PCABI_HD bool packed_ok_t(int L, const Scoring &s) {
+    using Y = pk::Lay<RPL>;
+    if (L < 1 || L > RPL || L > pk::MAX_L) return false;
+    if (!(s.go < 0 && s.ge < 0)) return false;
     if (packed_span_bound(L, s) > 255) return false;
-    const int hi = (rpl * s.ma > 0 ? rpl * s.ma : 0);
-    const int gm = (-s.go > -s.ge ? -s.go : -s.ge);
-    const int neg = pk::neg_score(rpl, s) - (gm > 0 ? gm : 0);
-    return hi <= 500 && neg >= -510 && s.ma <= 500 && s.mi >= -500;
+    const long long smin = (s.go != s.ge) ? (long long)s.go + (long long)(L - 1) * s.ge : (long long)L * s.ge;
+    const long long lo_sub = s.mi < s.ma ? s.mi : s.ma;
+    const long long lo_gap = (long long)s.go + s.ge;
+    long long lo = smin + (lo_gap < lo_sub ? lo_gap : lo_sub);
+    const long long neg = pk::neg_score(s);
+    if (neg + s.ge < lo) lo = neg + s.ge;
+    if (neg < lo) lo = neg;
+    if (s.go < lo) lo = s.go;
+    long long hi = (long long)L * s.ma;
+    if (hi < 0) hi = 0;
+    if (s.ma > hi) hi = s.ma;
+    if (!Y::WIDE && L > 63) return false;
+    return lo >= Y::SC_MIN && hi <= Y::SC_MAX;
+}
+
+PCABI_HD bool packed_ok(int L, int rpl, const Scoring &s) {
+    switch (rpl) {
+#define PCABI_PK(R) case R: return packed_ok_t<R>(L, s);
+    PCABI_PK(4) PCABI_PK(8) PCABI_PK(12) PCABI_PK(16) PCABI_PK(20) PCABI_PK(24) PCABI_PK(28) PCABI_PK(32)
+    PCABI_PK(36) PCABI_PK(40) PCABI_PK(44) PCABI_PK(48) PCABI_PK(52) PCABI_PK(56) PCABI_PK(60) PCABI_PK(64)
+    PCABI_PK(68) PCABI_PK(72) PCABI_PK(76) PCABI_PK(80) PCABI_PK(84) PCABI_PK(88)
+#undef PCABI_PK
+    default: return false;
+    }
 }
 
 template <int RPL, bool AFFINE>
 struct LanePacked {
+    using Y = pk::Lay<RPL>;
     int32_t G[RPL + 1];    // S keys with tb cleared, plus the gap-open key: G = S + go
     int32_t HK[RPL + 1];   // H keys, tb = 1 (affine only)
     int bscore, bi, bj, blt, btrail, bprec;
@@ -660,7 +701,7 @@ struct LanePacked {
     // diagonal step into slot s (match / mismatch / padding), see pk::fill_sub_table.
     template <typename TabRow, bool LAST>
     PCABI_HD void column(const TabRow &tab, const int j, const int L, const int off) {
-        int32_t gup = pk::start(j + off) + k_go;   // G(0, j): S(0, j) = score 0, tb 0
+        int32_t gup = Y::start(j + off) + k_go;   // G(0, j): S(0, j) = score 0, tb 0
         int32_t vup = neg2;                        // V(0, j) = NEG, tb 2
         int slt_up = LT_NONE, vt_up = 0, vp_up = 0;
         int32_t lv = 0, lh = 0, ls = 0;
@@ -674,7 +715,7 @@ struct LanePacked {
 #pragma unroll
             for (int q = 0; q <= PCABI_TAB_PD && q < NQ; ++q) tab.quad(q, t + 4 * q + 1);
         }
-        int32_t diag = (pk::start(j - 1 + off) + k_go) + (PCABI_TAB_PD > 0 ? t[1] : tab(1));
+        int32_t diag = (Y::start(j - 1 + off) + k_go) + (PCABI_TAB_PD > 0 ? t[1] : tab(1));
 #pragma unroll
         for (int s = 1; s <= RPL; ++s) {
             if (PCABI_TAB_PD > 0 && (s & 3) == 1) {
@@ -690,32 +731,32 @@ struct LanePacked {
                 hn = hx > ho ? hx : ho;                  // tb 1 iff extend
                 const int32_t vx = vup + k_ge, vo = gup;
                 const int32_t vn = vx > vo ? vx : vo;    // tb 2 iff extend
-                vn2 = vn | pk::TB2;
-                if (LAST || s == RPL) { hext = pk::tb(hn) == 1; vext = pk::tb(vn) == 2; }
+                vn2 = vn | Y::TB2;
+                if (LAST || s == RPL) { hext = Y::tb(hn) == 1; vext = Y::tb(vn) == 2; }
             } else {
                 vn2 = gup + k_gev;                       // tb 2
                 hn = G[s] + k_geh;                       // tb 1
             }
             sn = max3i(diag, vn2, hn);
-            const int t = pk::tb(sn);
+            const int t = Y::tb(sn);
             const int slt = t == 3 ? LT_D : (t == 2 ? LT_V : LT_H);
             if (LAST && s < RPL) {
                 const bool cont = AFFINE ? (vext || slt_up == LT_V) : (slt_up == LT_V);
                 const int vt = cont ? vt_up + 1 : 1;
                 const int vp = cont ? vp_up : (slt_up == LT_D ? 1 : 0);
-                const int sc_s = pk::score(sn);
+                const int sc_s = Y::score(sn);
                 if (sc_s > bscore) {
                     bscore = sc_s;
                     bi = s - off;
                     bj = j;
                     if (AFFINE) {
-                        const bool isv = pk::score(vn2) == sc_s, ish = !isv && pk::score(hn) == sc_s;
-                        battr = pk::attr(isv ? vn2 : (ish ? hn : sn));
+                        const bool isv = Y::score(vn2) == sc_s, ish = !isv && Y::score(hn) == sc_s;
+                        battr = Y::attr(isv ? vn2 : (ish ? hn : sn));
                         blt = isv ? LT_V : (ish ? LT_H : LT_D);
                         btrail = isv ? vt : 0;
                         bprec = isv ? vp : 0;
                     } else {
-                        battr = pk::attr(sn);
+                        battr = Y::attr(sn);
                         blt = slt;
                         btrail = (slt == LT_V) ? vt : 0;
                         bprec = (slt == LT_V) ? vp : 0;
@@ -735,8 +776,8 @@ struct LanePacked {
                     vp_up = vp;
                 }
             }
-            G[s] = (sn & ~pk::TBM) + k_go;
-            if (AFFINE) HK[s] = hn | pk::TB1;
+            G[s] = (sn & ~Y::TBM) + k_go;
+            if (AFFINE) HK[s] = hn | Y::TB1;
             gup = G[s];
             vup = vn2;
             diag = diag_nx;
@@ -752,18 +793,18 @@ struct LanePacked {
         const bool hcont = AFFINE ? (lhext || slt_last == LT_H) : (slt_last == LT_H);
         const int ht = hcont ? ht_last + 1 : 1;
         const int hp = hcont ? hp_last : (slt_last == LT_D ? 1 : 0);
-        const int lsc = pk::score(ls);
+        const int lsc = Y::score(ls);
         const bool upd = lsc > bscore;
         int clt, ctrail, cprec;
         uint32_t cattr;
         if (AFFINE) {
-            const bool isv = pk::score(lv) == lsc, ish = !isv && pk::score(lh) == lsc;
-            cattr = pk::attr(isv ? lv : (ish ? lh : ls));
+            const bool isv = Y::score(lv) == lsc, ish = !isv && Y::score(lh) == lsc;
+            cattr = Y::attr(isv ? lv : (ish ? lh : ls));
             clt = isv ? LT_V : (ish ? LT_H : LT_D);
             ctrail = isv ? (LAST ? vt_up : 0) : (ish ? ht : 0);
             cprec = isv ? (LAST ? vp_up : 0) : (ish ? hp : 0);
         } else {
-            cattr = pk::attr(ls);
+            cattr = Y::attr(ls);
             clt = lslt;
             ctrail = (lslt == LT_V) ? (LAST ? vt_up : 0) : (lslt == LT_H ? ht : 0);
             cprec = (lslt == LT_V) ? (LAST ? vp_up : 0) : (lslt == LT_H ? hp : 0);
@@ -787,14 +828,14 @@ struct LanePacked {
     // compares. Linear gaps: no correction, the S key's own tb (3 D, 2 V, 1 H) is the type.
     PCABI_HD void column_tail(int32_t lv, int32_t lh, int32_t ls, int j) {
         int32_t corr;
-        if (AFFINE) corr = max3i(lv | pk::TB3, (lh & ~pk::TBM) | pk::TB2, ls & ~pk::TBM);
+        if (AFFINE) corr = max3i(lv | Y::TB3, (lh & ~Y::TBM) | Y::TB2, ls & ~Y::TBM);
         else corr = ls;
         // H-run at (L, j): continues when H extends (affine: lh tb 1) or when it opens from an
         // S that itself ended in H (tb 1); a new run is preceded by a diagonal iff S was one.
-        const int32_t tsp = ls_prev & pk::TBM;
-        const bool hcont = (AFFINE && (lh & pk::TB1) != 0) || tsp == pk::TB1;
-        const int hph = hcont ? hph_last + 2 : 2 + (tsp == pk::TB3 ? 1 : 0);
-        const bool upd = corr > (bkey | ((1 << pk::SC_SH) - 1));   // score(corr) > score(bkey)
+        const int32_t tsp = ls_prev & Y::TBM;
+        const bool hcont = (AFFINE && (lh & Y::TB1) != 0) || tsp == Y::TB1;
+        const int hph = hcont ? hph_last + 2 : 2 + (tsp == Y::TB3 ? 1 : 0);
+        const bool upd = corr > (bkey | ((1 << Y::SC_SH) - 1));   // score(corr) > score(bkey)
         bkey = upd ? corr : bkey;
         bj = upd ? j : bj;
         bhph = upd ? hph : bhph;
@@ -804,18 +845,18 @@ struct LanePacked {
 
     // Inner-column scout state -> the fields the last column and finish() use.
     PCABI_HD void materialize(int L) {
-        const int t = pk::tb(bkey);
+        const int t = Y::tb(bkey);
         int lt;
         if (bj == 0) lt = LT_NONE;                          // still the (L, 0) seed
         else if (AFFINE) lt = t == 3 ? LT_V : (t == 2 ? LT_H : LT_D);
         else lt = t == 3 ? LT_D : (t == 2 ? LT_V : LT_H);
-        bscore = pk::score(bkey);
+        bscore = Y::score(bkey);
         bi = L;
-        battr = pk::attr(bkey);
+        battr = Y::attr(bkey);
         blt = lt;
         btrail = lt == LT_H ? (bhph >> 1) : 0;             // a V run in row L before the last
         bprec = lt == LT_H ? (bhph & 1) : 0;               // column is a 1-column trail: 0 here
-        const int tp = pk::tb(ls_prev);
+        const int tp = Y::tb(ls_prev);
         slt_last = tp == 0 ? LT_NONE : (tp == 3 ? LT_D : (tp == 2 ? LT_V : LT_H));
         ht_last = hph_last >> 1;
         hp_last = hph_last & 1;
@@ -830,33 +871,35 @@ struct LanePacked {
 // one LDS read + one add instead of a compare + select.
 namespace pk {
 constexpr int TAB_W = 8;
-template <typename AdpFn>
+template <int RPL, typename AdpFn>
 PCABI_HD int32_t sub_key(int s, int c, const AdpFn &adp, int off, const Scoring &sc) {
+    using Y = Lay<RPL>;
     // the core adds these to G = S + go, so the gap-open key is taken back out here
-    if (s <= off) return TB3 - pk::sc(sc.go);
-    return (c == adp(s)) ? (pk::sc(sc.ma) + TB3 + INC_M - pk::sc(sc.go))
-                         : (pk::sc(sc.mi) + TB3 + INC_D - pk::sc(sc.go));
+    if (s <= off) return Y::TB3 - Y::sc(sc.go);
+    return (c == adp(s)) ? (Y::sc(sc.ma) + Y::TB3 + Y::INC_M - Y::sc(sc.go))
+                         : (Y::sc(sc.mi) + Y::TB3 + Y::INC_D - Y::sc(sc.go));
 }
 }  // namespace pk
 
 template <int RPL, bool AFFINE, typename ReadFn, typename TabFn>
 PCABI_HD Result align_lane_packed(ReadFn &rd, int n, const TabFn &tabfn, int L, const Scoring sc) {
+    using Y = pk::Lay<RPL>;
     // tabfn(r) returns a callable row(s) -> substitution key for read code r
     LanePacked<RPL, AFFINE> st;
     const int off = RPL - L;
-    const int32_t neg = pk::sc(pk::neg_score(RPL, sc));
-    st.k_ge = pk::sc(sc.ge);
-    st.k_go = pk::sc(sc.go);
+    const int32_t neg = Y::sc(pk::neg_score(sc));
+    st.k_ge = Y::sc(sc.ge);
+    st.k_go = Y::sc(sc.go);
     // linear gaps: V / H straight from G (= S + go), so the constants take go back out
-    st.k_gev = pk::sc(sc.ge) - pk::sc(sc.go) + pk::TB2;
-    st.k_geh = pk::sc(sc.ge) - pk::sc(sc.go) + pk::TB1;
+    st.k_gev = Y::sc(sc.ge) - Y::sc(sc.go) + Y::TB2;
+    st.k_geh = Y::sc(sc.ge) - Y::sc(sc.go) + Y::TB1;
 #pragma unroll
     for (int s = 1; s <= RPL; ++s) {
-        st.G[s] = pk::start(off - s) + st.k_go;    // padded (s, 0) reaches real (0, off - s)
-        st.HK[s] = neg | pk::TB1;
+        st.G[s] = Y::start(off - s) + st.k_go;    // padded (s, 0) reaches real (0, off - s)
+        st.HK[s] = neg | Y::TB1;
     }
-    st.neg2 = neg | pk::TB2;
-    st.bkey = pk::start(-L);                       // the (L, 0) seed: score 0, c = -L
+    st.neg2 = neg | Y::TB2;
+    st.bkey = Y::start(-L);                       // the (L, 0) seed: score 0, c = -L
     st.bj = 0;
     st.bhph = 0;
     st.hph_last = 0;
@@ -871,7 +914,7 @@ PCABI_HD Result align_lane_packed(ReadFn &rd, int n, const TabFn &tabfn, int L, 
     st.materialize(L);
     st.template column<decltype(tabfn(r)), true>(tabfn(r), n, L, off);
     Best b;
-    b.score = st.bscore; b.bi = st.bi; b.bj = st.bj; b.attr = pk::to_std(st.battr, st.bj);
+    b.score = st.bscore; b.bi = st.bi; b.bj = st.bj; b.attr = Y::to_std(st.battr, st.bj);
     b.ltype = st.blt; b.trail = st.btrail; b.precd = st.bprec;
     return finish(b, L, n);
 }
@@ -900,7 +943,7 @@ PCABI_HD v2 vmax(v2 a, v2 b) {
 }
 PCABI_HD v2 splat(int x) { v2 r = {(int16_t)x, (int16_t)x}; return r; }
 constexpr int NEG16 = -8192;
-constexpr int MAX_RPL = 64;
+constexpr int MAX_RPL = 88;
 
 // Smallest best score an alignment with pid2 >= threshold_pct can have (-32768: no bound).
 // The threshold is lowered by 1e-5 % first: the reference compares the identity after its

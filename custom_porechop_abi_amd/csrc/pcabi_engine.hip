@@ -50,9 +50,12 @@ int fail(int code, const std::string &msg) {
     } while (0)
 
 // Register buckets. FAST (branch-free core, pcabi_dp.h align_lane_fast): every multiple of 4 up
-// to 64, used whenever pcabi::fast_ok holds. GENERIC (guarded core, any scoring): a few sizes,
-// also the only path for 64 < L <= 128 for now.
-enum Kind { FAST = 0, GENERIC = 1, PACKED = 2 };
+// to 64, used whenever pcabi::fast_ok holds (and served by the packed-key core when every
+// adapter of the bucket is pcabi::packed_ok). WIDE (packed-key core only, wide key layout
+// pk::Lay<RPL > 64>): every multiple of 4 from 68 to 88, for the 65-88 bp adapters (native
+// barcoding "full sequence" adapters) whenever packed_ok holds. GENERIC (guarded core, any
+// scoring): a few sizes, the path for everything else up to 128.
+enum Kind { FAST = 0, GENERIC = 1, PACKED = 2, WIDE = 3 };
 struct BucketDef {
     int rpl;
     Kind kind;
@@ -60,14 +63,18 @@ struct BucketDef {
 constexpr BucketDef kBuckets[] = {
     {4, FAST},  {8, FAST},  {12, FAST}, {16, FAST}, {20, FAST}, {24, FAST}, {28, FAST}, {32, FAST},
     {36, FAST}, {40, FAST}, {44, FAST}, {48, FAST}, {52, FAST}, {56, FAST}, {60, FAST}, {64, FAST},
+    {68, WIDE}, {72, WIDE}, {76, WIDE}, {80, WIDE}, {84, WIDE}, {88, WIDE},
     {16, GENERIC}, {32, GENERIC}, {64, GENERIC}, {96, GENERIC}, {128, GENERIC}};
 constexpr int kNumBuckets = sizeof(kBuckets) / sizeof(kBuckets[0]);
 constexpr int kMaxRPL = 128;
 
-int bucket_of(int L, const pcabi::Scoring &sc) {
+int bucket_of(int L, const pcabi::Scoring &sc, bool allow_wide = true) {
     if (L <= 64) {
         const int rpl = (L + 3) & ~3;
         if (pcabi::fast_ok(L, rpl, sc)) return rpl / 4 - 1;
+    } else if (allow_wide && L <= pcabi::pk::MAX_L) {
+        const int rpl = (L + 3) & ~3;
+        if (pcabi::packed_ok(L, rpl, sc)) return 16 + (rpl - 68) / 4;
     }
     for (int b = 0; b < kNumBuckets; ++b)
         if (kBuckets[b].kind == GENERIC && L <= kBuckets[b].rpl) return b;
@@ -175,7 +182,7 @@ __device__ __forceinline__ void run_lane(const KParams &p, int a_local, int64_t 
             const int c = e / RPL, srow = e % RPL + 1;
             const uint32_t *ap = p.adp_pad + (int64_t)a_local * (RPL / 4);
             auto code = [&](int sl) { return (int)((ap[(sl - 1) / 4] >> (8 * ((sl - 1) & 3))) & 0xFFu); };
-            wave_tab[e] = pcabi::pk::sub_key(srow, c, code, off, p.sc);
+            wave_tab[e] = pcabi::pk::sub_key<RPL>(srow, c, code, off, p.sc);
         }
         __syncthreads();
     }
@@ -194,7 +201,7 @@ __device__ __forceinline__ void run_lane(const KParams &p, int a_local, int64_t 
               }();
         if constexpr (KIND == PACKED) {
             auto tabfn = [&](int rc) { return LdsRow{wave_tab + rc * RPL}; };
-            r = pcabi::align_lane_packed<(RPL <= 64 ? RPL : 64), AFFINE>(rd, n, tabfn, L, p.sc);
+            r = pcabi::align_lane_packed<(RPL <= pcabi::pk::MAX_RPL ? RPL : 4), AFFINE>(rd, n, tabfn, L, p.sc);
         } else if constexpr (KIND == FAST) {
             r = pcabi::align_lane_fast<RPL, AFFINE>(rd, n, adp, L, p.sc);
         } else {
@@ -317,6 +324,7 @@ void dispatch_filter(int rpl, const FParams &p, bool affine, hipStream_t st) {
     switch (rpl) {
 #define C(R) case R: launch_filter<R>(p, affine, st); break;
     C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32) C(36) C(40) C(44) C(48) C(52) C(56) C(60) C(64)
+    C(68) C(72) C(76) C(80) C(84) C(88)
 #undef C
     }
 }
@@ -591,7 +599,13 @@ void dispatch(int b, const KParams &p, bool affine, hipStream_t st, bool packed)
     dim3 grid = p.task_win ? dim3((unsigned)((p.n_waves + 3) / 4))
                            : dim3((unsigned)(tiles8 * p.n_adp));
     const BucketDef d = kBuckets[b];
-    if (d.kind == FAST && packed) {
+    if (d.kind == WIDE) {
+        switch (d.rpl) {
+#define C(R) case R: launch<R, PACKED>(p, affine, grid, st); break;
+        C(68) C(72) C(76) C(80) C(84) C(88)
+#undef C
+        }
+    } else if (d.kind == FAST && packed) {
         switch (d.rpl) {
 #define C(R) case R: launch<R, PACKED>(p, affine, grid, st); break;
         C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32) C(36) C(40) C(44) C(48) C(52) C(56) C(60) C(64)
@@ -617,6 +631,7 @@ void dispatch(int b, const KParams &p, bool affine, hipStream_t st, bool packed)
 // Packed-key kernels serve a fast bucket when every adapter in it satisfies the range
 // conditions of pcabi_dp.h packed_ok (any window length).
 bool bucket_packed_ok(int b, const std::vector<int32_t> &lens, const pcabi::Scoring &sc) {
+    if (kBuckets[b].kind == WIDE) return true;   // assigned only when packed_ok holds
     if (kBuckets[b].kind != FAST || kBuckets[b].rpl > pcabi::pk::MAX_RPL) return false;
     for (int32_t L : lens)
         if (!pcabi::packed_ok(L, kBuckets[b].rpl, sc)) return false;
@@ -638,11 +653,12 @@ constexpr int kMaxFastBuckets = 4;
 // into the next larger non-empty one (cost = adapters x added padding rows) until at most
 // kMaxFastBuckets remain. Only merges the packed core can serve with the scoring `sc` (it
 // passes scores through any number of padding rows; the fast core allows at most 3).
-std::vector<int> assign_buckets(const int32_t *adp_len, int32_t n_adp, const pcabi::Scoring &sc, bool merge) {
+std::vector<int> assign_buckets(const int32_t *adp_len, int32_t n_adp, const pcabi::Scoring &sc, bool merge,
+                                bool allow_wide) {
     std::vector<int> b_of(n_adp);
     int count[kNumBuckets] = {};
     for (int a = 0; a < n_adp; ++a) {
-        b_of[a] = bucket_of(adp_len[a], sc);
+        b_of[a] = bucket_of(adp_len[a], sc, allow_wide);
         ++count[b_of[a]];
     }
     auto packed_all = [&](int b, int extra_from) {
@@ -676,8 +692,9 @@ std::vector<int> assign_buckets(const int32_t *adp_len, int32_t n_adp, const pca
 }
 
 void build_buckets(const uint8_t *adp_codes, const int32_t *adp_off, const int32_t *adp_len,
-                   int32_t n_adp, const pcabi::Scoring &sc, BucketHost (&bk)[kNumBuckets], bool merge = true) {
-    const std::vector<int> b_of = assign_buckets(adp_len, n_adp, sc, merge);
+                   int32_t n_adp, const pcabi::Scoring &sc, BucketHost (&bk)[kNumBuckets], bool merge = true,
+                   bool allow_wide = true) {
+    const std::vector<int> b_of = assign_buckets(adp_len, n_adp, sc, merge, allow_wide);
     for (int a = 0; a < n_adp; ++a) {
         const int L = adp_len[a];
         const int b = b_of[a];
@@ -1198,7 +1215,8 @@ int adapters_create_impl(const uint8_t *adp_codes, const int32_t *adp_off, const
                          int32_t n_adp, const pcabi::Scoring *sc, pcabi_adapters **out) {
     if (int rc = check_common(adp_len, n_adp)) return rc;
     BucketHost bk[kNumBuckets];
-    build_buckets(adp_codes, adp_off, adp_len, n_adp, sc ? *sc : pcabi::Scoring{1, -1, -1, -1}, bk, sc != nullptr);
+    build_buckets(adp_codes, adp_off, adp_len, n_adp, sc ? *sc : pcabi::Scoring{1, -1, -1, -1}, bk, sc != nullptr,
+                  sc != nullptr);
     pcabi_adapters *a = new pcabi_adapters();
     a->n_adp = n_adp;
     for (int k = 0; k < n_adp; ++k)
@@ -1228,6 +1246,16 @@ int adapters_create_impl(const uint8_t *adp_codes, const int32_t *adp_off, const
     return 0;
 }
 }  // namespace
+
+// A wide (packed-only) bucket serves only scorings its adapters are packed_ok for.
+int wide_ok(const pcabi_adapters *adps, int b, const pcabi::Scoring &sc) {
+    if (kBuckets[b].kind != WIDE) return 0;
+    for (int32_t L : adps->lens[b])
+        if (!pcabi::packed_ok(L, kBuckets[b].rpl, sc))
+            return fail(PCABI_E_ARG, "adapter table laid out for another scoring (pcabi_adapters_create_scored): "
+                                     "rebuild it for this one");
+    return 0;
+}
 
 extern "C" {
 
@@ -1299,6 +1327,7 @@ int pcabi_align_cross_dev(const uint32_t *tiles, const int64_t *tile_off, const 
         if (kBuckets[b].kind == FAST && adps->max_off[b] > 3 && !bucket_packed_ok(b, adps->lens[b], p.sc))
             return fail(PCABI_E_ARG, "adapter table merged for another scoring (pcabi_adapters_create_scored): "
                                      "rebuild it for this one");
+        if (int rc = wide_ok(adps, b, p.sc)) return rc;
         order.push_back(b);
     }
     // Largest bucket (adapters x rows) on the caller's stream, the others spread over the
@@ -1364,7 +1393,9 @@ int filtered_first_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_o
     const int32_t n_adp = adps->n_adp;
     std::vector<int> fb;   // filterable buckets, largest first
     for (int b = 0; b < kNumBuckets; ++b)
-        if (adps->count[b] && kBuckets[b].kind == FAST && pcabi::sf::filter_ok(kBuckets[b].rpl, scr)) fb.push_back(b);
+        if (adps->count[b] && (kBuckets[b].kind == FAST || kBuckets[b].kind == WIDE) &&
+            pcabi::sf::filter_ok(kBuckets[b].rpl, scr))
+            fb.push_back(b);
     if (fb.empty()) return 0;
     std::stable_sort(fb.begin(), fb.end(), [&](int x, int y) {
         return (int64_t)adps->count[x] * kBuckets[x].rpl > (int64_t)adps->count[y] * kBuckets[y].rpl;
@@ -1511,6 +1542,8 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
     const hipStream_t st = (hipStream_t)stream;
     const int32_t n_adp = sc->adps->n_adp;
     if (n_win == 0 || n_adp == 0) return 0;
+    for (int b = 0; b < kNumBuckets; ++b)
+        if (int rc = wide_ok(sc->adps, b, pcabi::Scoring{match, mismatch, gap_open, gap_extend})) return rc;
     int64_t n_hits = 0;
     std::vector<int32_t> cur, nxt, nxt_start, hm_w, hm_s, hm_e, lens;
     std::vector<int32_t> hb;

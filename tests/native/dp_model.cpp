@@ -85,7 +85,7 @@ static void run_packed(const char *read, int n, const char *adp, int L, pcabi::S
     // c-major table, the layout the kernels keep in LDS: tab[c * RPL + s - 1]
     int32_t tab[pcabi::pk::TAB_W * RPL];
     for (int c = 0; c < pcabi::pk::TAB_W; ++c)
-        for (int s = 1; s <= RPL; ++s) tab[c * RPL + s - 1] = pcabi::pk::sub_key(s, c, ad, off, sc);
+        for (int s = 1; s <= RPL; ++s) tab[c * RPL + s - 1] = pcabi::pk::sub_key<RPL>(s, c, ad, off, sc);
     struct Row {
         const int32_t *p;
         int32_t operator()(int s) const { return p[s - 1]; }
@@ -107,6 +107,7 @@ extern "C" int pcabi_model_align_packed_rpl(const char *read, int n, const char 
     switch (rpl) {
 #define C(R) case R: run_packed<R>(read, n, adp, L, sc, out); break;
     C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32) C(36) C(40) C(44) C(48) C(52) C(56) C(60) C(64)
+    C(68) C(72) C(76) C(80) C(84) C(88)
 #undef C
     default: return -2;
     }
@@ -123,6 +124,7 @@ extern "C" int pcabi_model_align_packed(const char *read, int n, const char *adp
     switch (rpl) {
 #define C(R) case R: run_packed<R>(read, n, adp, L, sc, out); break;
     C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32) C(36) C(40) C(44) C(48) C(52) C(56) C(60) C(64)
+    C(68) C(72) C(76) C(80) C(84) C(88)
 #undef C
     default: return -2;
     }
@@ -161,6 +163,7 @@ extern "C" int pcabi_model_filter(const char *read, int n, const char *a, int La
     switch (rpl) {
 #define C(R) case R: run_filter<R>(read, n, a, La, b, Lb, sc, out); break;
     C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32) C(36) C(40) C(44) C(48) C(52) C(56) C(60) C(64)
+    C(68) C(72) C(76) C(80) C(84) C(88)
 #undef C
     default: return -2;
     }

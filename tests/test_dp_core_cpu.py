@@ -163,6 +163,61 @@ def test_packed_core_extra_padding_rows(model):
     assert n_checked > 2000
 
 
+def test_packed_wide_core(model):
+    """Wide register buckets (68..88 rows, pk::Lay<RPL > 64>: 9-bit score, count field m +
+    (RPL + 1) nD): the 63-88 bp adapters -- the native barcoding "full sequence" adapters
+    (porechop_abi/adapters.py:466-477) among them -- on end windows and whole reads, embedded
+    mutated hits, extra padding rows, several scorings."""
+    from custom_porechop_abi_amd import adapters as A
+    full = []
+    for i in (1, 7, 12):
+        f = A.make_full_native_barcode_adapter(i)
+        full += [f.start_sequence[1], f.end_sequence[1]]
+    rng = random.Random(31)
+    schemes = [(3, -6, -5, -2), (2, -1, -1, -1), (1, -1, -3, -1), (3, -6, -2, -5)]
+    n_checked = 0
+    for k in range(700):
+        sc = schemes[k % len(schemes)]
+        if k % 3 == 0:
+            a = rng.choice(full)
+        else:
+            a = ''.join(rng.choice(rng.choice(['ACGT', 'AT', 'ACGTN'])) for _ in range(rng.randint(61, 88)))
+        L = len(a)
+        rpl = rng.choice([x for x in range(68, 92, 4) if x >= L])
+        n = rng.choice([rng.randint(1, 150), 150, rng.randint(200, 1500)])
+        r = ''.join(rng.choice('ACGT') for _ in range(n))
+        for _ in range(rng.randint(0, 2)):
+            p = rng.randint(0, len(r))
+            r = r[:p] + _mutate(rng, a, rng.choice([0.0, 0.05, 0.15])) + r[p:]
+        out = (ctypes.c_int * 8)()
+        rc = model.pcabi_model_align_packed_rpl(r.encode(), len(r), a.encode(), L, rpl, *sc, out)
+        if rc == -3:
+            continue
+        assert rc == 0 and list(out) == oracle_lib.align(r, a, sc), (sc, L, rpl, len(r))
+        n_checked += 1
+    assert n_checked > 500
+
+
+def test_score_filter_wide_buckets(model):
+    """The score filter at the wide register buckets (68..88 rows)."""
+    rng = random.Random(37)
+    schemes = [(3, -6, -5, -2), (2, -1, -1, -1), (3, -6, -2, -5)]
+    for k in range(300):
+        sc = schemes[k % len(schemes)]
+        La, Lb = rng.randint(40, 88), rng.randint(1, 88)
+        rpl = rng.choice([x for x in range(68, 92, 4) if x >= max(La, Lb)])
+        a = ''.join(rng.choice('ACGT') for _ in range(La))
+        b = ''.join(rng.choice('ACGT') for _ in range(Lb))
+        r = ''.join(rng.choice('ACGT') for _ in range(rng.randint(1, 600)))
+        if rng.random() < 0.5 and len(r) > 100:
+            p = rng.randint(0, len(r) - 90)
+            r = r[:p] + _mutate(rng, a, 0.05) + r[p:]
+        out = (ctypes.c_int * 2)()
+        rc = model.pcabi_model_filter(r.encode(), len(r), a.encode(), La, b.encode(), Lb, rpl, *sc, out)
+        assert rc == 0
+        assert list(out) == [oracle_lib.align(r, a, sc)[4], oracle_lib.align(r, b, sc)[4]], (sc, La, Lb, rpl)
+
+
 def test_score_filter_equals_best_score(model):
     """The packed-16 score-only filter (two adapters per lane) returns exactly the best score the
     reference reports, for both halves, across scorings, paddings and read lengths."""

@@ -38,6 +38,14 @@ def _mutate(rng, s, rate):
     return ''.join(out)
 
 
+def _native_full(i):
+    """The native barcoding "full sequence" adapters of barcode i (68 bp start, 63 bp end,
+    porechop_abi/adapters.py:466-477)."""
+    from custom_porechop_abi_amd import adapters as A
+    f = A.make_full_native_barcode_adapter(i)
+    return [f.start_sequence[1], f.end_sequence[1]]
+
+
 def _case_set(seed, n_reads, n_adp, max_read, max_adp):
     rng = random.Random(seed)
     alph = rng.choice(['ACGT', 'ACGTN', 'AT', 'A', 'ACGT-'])
@@ -153,6 +161,8 @@ def test_device_abi_tiled_cross(gpu_lib, scheme, scored):
     L, vp = gpu_lib, ctypes.c_void_p
     reads, adps = _case_set(31, 700, 7, 3000, 64)
     adps = adps + ['ACGTTGCA' * k for k in (1, 2, 3, 4, 5, 6, 7)] + ['GATTACA' * 5 + 'G', 'TTAGGC' * 9]
+    # wide register buckets (65..88 bp, packed-key core, pk::Lay<RPL > 64>) and past them (generic)
+    adps = adps + _native_full(3) + ['ACGTTGCA' * 9, 'GATTACA' * 12, 'TTAGGCA' * 13]
     pack = engine.SeqPack(reads)
     n = len(reads)
     # windows seq[k:] with random (unaligned) starts k
@@ -245,7 +255,7 @@ def test_middle_scan_rounds(gpu_lib, scheme):
     adapter (several rounds), adjacent hits, empty and tiny reads."""
     from custom_porechop_abi_amd import engine
     rng = random.Random(sum(scheme) + 100)
-    adps = ['AATGTACTTCGTTCAGTTACGTATTGCT', 'GCAATACGTAACTGAACGAAGT', 'ACGTTTAGGCATTGCA']
+    adps = ['AATGTACTTCGTTCAGTTACGTATTGCT', 'GCAATACGTAACTGAACGAAGT', 'ACGTTTAGGCATTGCA'] + _native_full(2)
     reads = []
     for k in range(160):
         n = rng.choice([0, 3, rng.randint(200, 3000)])

@@ -37,6 +37,11 @@ KERNEL(k_xor_b32, "v_xor_b32")
 KERNEL(k_and_b32, "v_and_b32")
 KERNEL(k_min_u32, "v_min_u32")
 KERNEL(k_lshr_b32, "v_lshrrev_b32")
+KERNEL(k_max_i16, "v_max_i16")
+KERNEL(k_max_u16, "v_max_u16")
+KERNEL(k_pk_max_u16, "v_pk_max_u16")
+KERNEL(k_max_f16, "v_max_f16")
+KERNEL(k_pk_max_f16, "v_pk_max_f16")
 
 #define KERNEL3(NAME, INS)                                                                      \
     __global__ __launch_bounds__(256) void NAME(int *out, int seed) {                           \
@@ -61,6 +66,9 @@ KERNEL3(k_med3_i32, "v_med3_i32")
 KERNEL3(k_and_or_b32, "v_and_or_b32")
 KERNEL3(k_mad_u24, "v_mad_u32_u24")
 KERNEL3(k_lshl_add, "v_lshl_add_u32")
+KERNEL3(k_max3_i16, "v_max3_i16")
+KERNEL3(k_max3_u32, "v_max3_u32")
+KERNEL3(k_or3_b32, "v_or3_b32")
 
 // compare + select pattern, mask rewritten every pair (realistic DP usage)
 __global__ __launch_bounds__(256) void k_cmp_cnd(int *out, int seed) {
@@ -176,7 +184,10 @@ int main() {
                                               {k_perm_b32, "v_perm_b32"}, {k_bfe_u32, "v_bfe_u32"},
                                               {k_med3_i32, "v_med3_i32"}, {k_and_or_b32, "v_and_or_b32"},
                                               {k_mad_u24, "v_mad_u32_u24"}, {k_lshl_add, "v_lshl_add_u32"},
-                                              {k_cmp_cnd, "cmp+cndmask32"}, {k_cmp_cnd64, "cmp+cndmask64"}};
+                                              {k_cmp_cnd, "cmp+cndmask32"}, {k_cmp_cnd64, "cmp+cndmask64"},
+                                              {k_max_i16, "v_max_i16"}, {k_max_u16, "v_max_u16"}, {k_pk_max_u16, "v_pk_max_u16"},
+                                              {k_max_f16, "v_max_f16"}, {k_pk_max_f16, "v_pk_max_f16"}, {k_max3_i16, "v_max3_i16"},
+                                              {k_max3_u32, "v_max3_u32"}, {k_or3_b32, "v_or3_b32"}};
     for (auto &k : ks)
         for (int b : {2, 4}) run(k.k, k.n, d, b);
     hipFree(d);
