@@ -108,7 +108,9 @@ def exported_symbols():
             'pcabi_tile_layout', 'pcabi_tile_windows_dev', 'pcabi_align_cross_dev', 'pcabi_end_trim_dev',
             'pcabi_best_full_identity_dev', 'pcabi_first_hits_host', 'pcabi_first_hit_dev', 'pcabi_scan_create',
             'pcabi_scan_destroy', 'pcabi_middle_scan_dev', 'pcabi_middle_scan_host', 'pcabi_barcode_call_dev',
-            'pcabi_barcode_call_host']
+            'pcabi_barcode_call_host', 'pcabi_fastx_open', 'pcabi_fastx_type', 'pcabi_fastx_next',
+            'pcabi_fastx_close', 'pcabi_fastx_load', 'pcabi_reads_count', 'pcabi_reads_type', 'pcabi_reads_views',
+            'pcabi_reads_free', 'pcabi_reads_write']
 
 
 def check(rc, what):

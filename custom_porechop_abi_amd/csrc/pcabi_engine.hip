@@ -711,6 +711,11 @@ void build_buckets(const uint8_t *adp_codes, const int32_t *adp_off, const int32
 
 }  // namespace
 
+// error channel shared with the host I/O unit (csrc/pcabi_io.cpp)
+namespace pcabi_internal {
+int fail(int code, const std::string &msg) { return ::fail(code, msg); }
+}  // namespace pcabi_internal
+
 // ---- prepared adapter tables (device) ---------------------------------------------------------
 struct pcabi_adapters {
     int32_t n_adp = 0;

@@ -1,0 +1,510 @@
+// pcabi_io.cpp -- native FASTA / FASTQ (plain or gzip) reader and trimmed-read writer for the
+// adapter-alignment engine (host code, part of libpcabi.so; declared in include/pcabi.h).
+//
+// The reader turns a sequence file straight into the engine's input layout -- Dna5 codes packed
+// back to back at 4-aligned offsets with 16 bytes of tail padding (engine.SeqPack) -- plus the
+// read names, upper-cased sequence text and qualities, in batches, with the reference's parsing
+// rules:
+//   * file type from the first decoded character: '>' FASTA, '@' FASTQ, else an error
+//     (porechop_abi/misc.py:84-105); gzip by its magic bytes, bzip2 / zip refused (:60-81);
+//   * FASTQ: 4 lines per record, each stripped; name = line[1:] (the full header), sequence,
+//     spacer, qualities (misc.py:148-165); a blank or truncated record is a parse error (the
+//     reference dies on it too);
+//   * FASTA: stripped lines, blank lines skipped, '>' starts a record whose sequence is the
+//     concatenation of the following lines; a record with an empty name is not emitted and its
+//     sequence carries over (misc.py:123-145, replicated exactly);
+//   * lines end at \n, \r\n or \r (Python's universal newlines), strip() removes the ASCII
+//     characters str.isspace() accepts;
+//   * NanoporeRead's normalisation (porechop_abi/nanopore_read.py:31-44): sequence upper-cased,
+//     U -> T when the read has more U than T (rna flag), qualities padded with '+' to the
+//     sequence length.
+// The writer reproduces NanoporeRead.get_fasta / get_fastq (nanopore_read.py:106-156) for a
+// batch: start / end trims with Python slice semantics, middle split parts (positions given as
+// [begin, end) ranges of the trimmed sequence, parts shorter than min_split_read_size dropped,
+// names numbered like add_number_to_read_name, :503-509), 70-column FASTA lines, T -> U for RNA
+// reads, optional gzip.
+#include <zlib.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/pcabi.h"
+
+namespace pcabi_internal {
+int fail(int code, const std::string &msg);   // pcabi_engine.hip: pcabi_last_error()
+}
+using pcabi_internal::fail;
+
+namespace {
+
+inline bool py_space(unsigned char c) {   // str.isspace() on ASCII
+    return (c >= 0x09 && c <= 0x0D) || (c >= 0x1C && c <= 0x20);
+}
+
+uint8_t g_dna5[256];
+const bool g_dna5_init = [] {
+    for (int i = 0; i < 256; ++i) g_dna5[i] = 4;
+    const char *s = "ACGTU", *l = "acgtu";
+    const uint8_t v[5] = {0, 1, 2, 3, 3};
+    for (int k = 0; k < 5; ++k) {
+        g_dna5[(unsigned char)s[k]] = v[k];
+        g_dna5[(unsigned char)l[k]] = v[k];
+    }
+    return true;
+}();
+
+}  // namespace
+
+struct pcabi_fastx {
+    gzFile f = nullptr;
+    int type = -1;                 // PCABI_FASTA / PCABI_FASTQ
+    std::vector<char> buf;
+    size_t pos = 0, end = 0;
+    bool eof = false;
+    int64_t line_no = 0;
+    bool raw = false;              // keep the file's text (misc.load_fasta_or_fastq tuples)
+    // FASTA state that crosses batch boundaries
+    bool fa_have_name = false;     // a header was seen (its name may be empty)
+    std::string fa_name, fa_seq;
+};
+
+struct pcabi_reads {
+    int type = -1;
+    int64_t n = 0;
+    std::vector<char> names;                 // full headers (after '@' / '>'), back to back
+    std::vector<int64_t> name_off{0};
+    std::vector<char> seq;                   // upper-cased, U->T for RNA reads
+    std::vector<int64_t> seq_off{0};
+    std::vector<char> qual;                  // padded with '+' to the sequence length
+    std::vector<int64_t> qual_off{0};
+    std::vector<uint8_t> rna;
+    std::vector<char> spacer;                // FASTQ '+' lines (stripped)
+    std::vector<int64_t> spacer_off{0};
+    std::vector<uint8_t> codes;              // Dna5, 4-aligned starts, 16 B tail padding (N)
+    std::vector<int64_t> code_off;
+    std::vector<int32_t> len;
+};
+
+namespace {
+
+// Next line (without its terminator) as [*p, *p + *n); false at end of file.
+bool next_line(pcabi_fastx *r, const char **p, size_t *n) {
+    for (;;) {
+        // look for a terminator in the buffered bytes
+        for (size_t i = r->pos; i < r->end; ++i) {
+            const char c = r->buf[i];
+            if (c == '\n' || c == '\r') {
+                if (c == '\r' && i + 1 == r->end && !r->eof) break;   // need to see if \n follows
+                *p = r->buf.data() + r->pos;
+                *n = i - r->pos;
+                size_t nx = i + 1;
+                if (c == '\r' && nx < r->end && r->buf[nx] == '\n') ++nx;
+                r->pos = nx;
+                ++r->line_no;
+                return true;
+            }
+        }
+        if (r->eof) {
+            if (r->pos < r->end) {   // last line without a terminator
+                *p = r->buf.data() + r->pos;
+                *n = r->end - r->pos;
+                r->pos = r->end;
+                ++r->line_no;
+                return true;
+            }
+            return false;
+        }
+        // refill: keep the partial line, grow if it fills the buffer
+        const size_t keep = r->end - r->pos;
+        if (r->pos > 0) {
+            std::memmove(r->buf.data(), r->buf.data() + r->pos, keep);
+            r->pos = 0;
+            r->end = keep;
+        }
+        if (r->buf.size() - r->end < (1u << 20)) r->buf.resize(std::max<size_t>(r->buf.size() * 2, 4u << 20));
+        const int got = gzread(r->f, r->buf.data() + r->end, (unsigned)std::min<size_t>(r->buf.size() - r->end, 1u << 30));
+        if (got < 0) {
+            int e = 0;
+            const char *m = gzerror(r->f, &e);
+            fail(PCABI_E_ARG, std::string("read error: ") + (m ? m : "?"));
+            r->eof = true;
+            r->end = r->pos;   // drop the partial data
+            return false;
+        }
+        if (got == 0) r->eof = true;
+        r->end += (size_t)got;
+    }
+}
+
+void strip(const char **p, size_t *n) {
+    const char *a = *p;
+    size_t m = *n;
+    while (m && py_space((unsigned char)a[0])) { ++a; --m; }
+    while (m && py_space((unsigned char)a[m - 1])) --m;
+    *p = a;
+    *n = m;
+}
+
+// One record appended to the batch, with NanoporeRead's normalisation unless raw.
+void add_record(pcabi_reads *b, const char *name, size_t nn, const char *seq, size_t ns, const char *q, size_t nq,
+                bool raw = false, const char *sp = nullptr, size_t nsp = 0) {
+    b->spacer.insert(b->spacer.end(), sp, sp + nsp);
+    b->spacer_off.push_back((int64_t)b->spacer.size());
+    b->names.insert(b->names.end(), name, name + nn);
+    b->name_off.push_back((int64_t)b->names.size());
+    const size_t s0 = b->seq.size();
+    b->seq.resize(s0 + ns);
+    char *d = b->seq.data() + s0;
+    int64_t nu = 0, nt = 0;
+    for (size_t i = 0; i < ns; ++i) {
+        char c = seq[i];
+        if (!raw && c >= 'a' && c <= 'z') c = (char)(c - 32);
+        nu += (c == 'U');
+        nt += (c == 'T');
+        d[i] = c;
+    }
+    const bool rna = !raw && nu > nt;
+    if (rna)
+        for (size_t i = 0; i < ns; ++i)
+            if (d[i] == 'U') d[i] = 'T';
+    b->rna.push_back(rna ? 1 : 0);
+    b->seq_off.push_back((int64_t)b->seq.size());
+    b->qual.insert(b->qual.end(), q, q + nq);
+    if (!raw && nq < ns) b->qual.insert(b->qual.end(), ns - nq, '+');
+    b->qual_off.push_back((int64_t)b->qual.size());
+    // engine layout
+    const int64_t off = (int64_t)b->codes.size();
+    b->code_off.push_back(off);
+    b->len.push_back((int32_t)ns);
+    const size_t padded = (ns + 3) & ~(size_t)3;
+    b->codes.resize((size_t)off + padded, 4);
+    uint8_t *c = b->codes.data() + off;
+    for (size_t i = 0; i < ns; ++i) c[i] = g_dna5[(unsigned char)d[i]];
+    ++b->n;
+}
+
+void finish_batch(pcabi_reads *b) { b->codes.resize(b->codes.size() + 16, 4); }
+
+}  // namespace
+
+extern "C" {
+
+int pcabi_fastx_open(const char *path, int raw, pcabi_fastx **out) {
+    if (!path || !out) return fail(PCABI_E_ARG, "bad arguments");
+    *out = nullptr;
+    FILE *fp = std::fopen(path, "rb");
+    if (!fp) return fail(PCABI_E_ARG, std::string("could not find ") + path);
+    unsigned char magic[4] = {0, 0, 0, 0};
+    const size_t nm = std::fread(magic, 1, 4, fp);
+    std::fclose(fp);
+    if (nm >= 3 && magic[0] == 0x42 && magic[1] == 0x5a && magic[2] == 0x68)
+        return fail(PCABI_E_ARG, "cannot use bzip2 format - use gzip instead");
+    if (nm >= 4 && magic[0] == 0x50 && magic[1] == 0x4b && magic[2] == 0x03 && magic[3] == 0x04)
+        return fail(PCABI_E_ARG, "cannot use zip format - use gzip instead");
+    gzFile f = gzopen(path, "rb");
+    if (!f) return fail(PCABI_E_ARG, std::string("could not open ") + path);
+    gzbuffer(f, 1u << 20);
+    pcabi_fastx *r = new pcabi_fastx();
+    r->f = f;
+    r->raw = raw != 0;
+    r->buf.resize(4u << 20);
+    // type from the first decoded character
+    while (r->end == 0 && !r->eof) {
+        const int got = gzread(f, r->buf.data(), (unsigned)r->buf.size());
+        if (got <= 0) r->eof = true;
+        else r->end = (size_t)got;
+    }
+    const char c0 = r->end ? r->buf[0] : 0;
+    if (c0 == '>') r->type = PCABI_FASTA;
+    else if (c0 == '@') r->type = PCABI_FASTQ;
+    else {
+        pcabi_fastx_close(r);
+        return fail(PCABI_E_PARSE, std::string("File is neither FASTA or FASTQ: ") + path);
+    }
+    *out = r;
+    return 0;
+}
+
+int pcabi_fastx_type(const pcabi_fastx *r) { return r ? r->type : -1; }
+
+void pcabi_fastx_close(pcabi_fastx *r) {
+    if (!r) return;
+    if (r->f) gzclose(r->f);
+    delete r;
+}
+
+int64_t pcabi_fastx_next(pcabi_fastx *r, int64_t max_reads, int64_t max_bases, pcabi_reads **out) {
+    if (!r || !out || max_reads <= 0) return fail(PCABI_E_ARG, "bad arguments");
+    pcabi_reads *b = new pcabi_reads();
+    b->type = r->type;
+    int64_t bases = 0;
+    const char *p;
+    size_t n;
+    if (r->type == PCABI_FASTQ) {
+        while (b->n < max_reads && bases < max_bases) {
+            if (!next_line(r, &p, &n)) break;
+            strip(&p, &n);
+            if (n == 0 || n == 1) {   // full_name.split()[0] fails in the reference (IndexError)
+                delete b;
+                return fail(PCABI_E_PARSE, "could not be parsed - is it formatted correctly? (empty FASTQ header at line " +
+                                               std::to_string(r->line_no) + ")");
+            }
+            // the name must hold a non-space character after the leading one
+            bool tok = false;
+            for (size_t i = 1; i < n && !tok; ++i) tok = !py_space((unsigned char)p[i]);
+            if (!tok) {
+                delete b;
+                return fail(PCABI_E_PARSE, "could not be parsed - empty FASTQ name at line " + std::to_string(r->line_no));
+            }
+            std::string name(p + 1, n - 1);
+            const char *sp, *qp, *xp;
+            size_t sn, qn, xn;
+            if (!next_line(r, &sp, &sn)) { delete b; return fail(PCABI_E_PARSE, "truncated FASTQ record"); }
+            strip(&sp, &sn);
+            std::string seq(sp, sn);
+            if (!next_line(r, &xp, &xn)) { delete b; return fail(PCABI_E_PARSE, "truncated FASTQ record"); }
+            if (!next_line(r, &qp, &qn)) { delete b; return fail(PCABI_E_PARSE, "truncated FASTQ record"); }
+            strip(&qp, &qn);
+            std::string spacer;
+            if (r->raw) {
+                strip(&xp, &xn);
+                spacer.assign(xp, xn);
+            }
+            add_record(b, name.data(), name.size(), seq.data(), seq.size(), qp, qn, r->raw, spacer.data(), spacer.size());
+            bases += (int64_t)seq.size();
+        }
+    } else {
+        while (b->n < max_reads && bases < max_bases) {
+            if (!next_line(r, &p, &n)) {
+                if (r->fa_have_name && !r->fa_name.empty()) {
+                    add_record(b, r->fa_name.data(), r->fa_name.size(), r->fa_seq.data(), r->fa_seq.size(), "", 0, r->raw);
+                    bases += (int64_t)r->fa_seq.size();
+                }
+                r->fa_have_name = false;
+                r->fa_name.clear();
+                r->fa_seq.clear();
+                break;
+            }
+            strip(&p, &n);
+            if (n == 0) continue;
+            if (p[0] == '>') {
+                if (!r->fa_name.empty()) {
+                    add_record(b, r->fa_name.data(), r->fa_name.size(), r->fa_seq.data(), r->fa_seq.size(), "", 0, r->raw);
+                    bases += (int64_t)r->fa_seq.size();
+                    r->fa_seq.clear();
+                }
+                r->fa_name.assign(p + 1, n - 1);
+                r->fa_have_name = true;
+            } else {
+                r->fa_seq.append(p, n);
+            }
+        }
+    }
+    if (r->eof && r->pos >= r->end && r->type == PCABI_FASTQ) {
+        // nothing more
+    }
+    finish_batch(b);
+    *out = b;
+    return b->n;
+}
+
+int pcabi_fastx_load(const char *path, int raw, pcabi_reads **out) {
+    if (!out) return fail(PCABI_E_ARG, "bad arguments");
+    *out = nullptr;
+    pcabi_fastx *r = nullptr;
+    if (int rc = pcabi_fastx_open(path, raw, &r)) return rc;
+    pcabi_reads *all = nullptr;
+    const int64_t got = pcabi_fastx_next(r, INT64_MAX, INT64_MAX, &all);
+    pcabi_fastx_close(r);
+    if (got < 0) return (int)got;
+    *out = all;
+    return 0;
+}
+
+void pcabi_reads_free(pcabi_reads *b) { delete b; }
+
+int64_t pcabi_reads_count(const pcabi_reads *b) { return b ? b->n : 0; }
+int pcabi_reads_type(const pcabi_reads *b) { return b ? b->type : -1; }
+
+int pcabi_reads_views(const pcabi_reads *b, pcabi_reads_view *v) {
+    if (!b || !v) return fail(PCABI_E_ARG, "bad arguments");
+    v->n = b->n;
+    v->type = b->type;
+    v->names = b->names.data();
+    v->name_off = b->name_off.data();
+    v->seq = b->seq.data();
+    v->seq_off = b->seq_off.data();
+    v->qual = b->qual.data();
+    v->qual_off = b->qual_off.data();
+    v->rna = b->rna.data();
+    v->spacer = b->spacer.data();
+    v->spacer_off = b->spacer_off.data();
+    v->codes = b->codes.data();
+    v->codes_len = (int64_t)b->codes.size();
+    v->code_off = b->code_off.data();
+    v->len = b->len.data();
+    return 0;
+}
+
+}  // extern "C"
+
+// ---- writer ----------------------------------------------------------------------------------
+namespace {
+
+struct Sink {
+    FILE *fp = nullptr;
+    gzFile gz = nullptr;
+    std::string buf;
+    bool ok = true;
+    void flush() {
+        if (buf.empty()) return;
+        if (gz) ok = ok && gzwrite(gz, buf.data(), (unsigned)buf.size()) == (int)buf.size();
+        else ok = ok && std::fwrite(buf.data(), 1, buf.size(), fp) == buf.size();
+        buf.clear();
+    }
+    void put(const char *p, size_t n) {
+        buf.append(p, n);
+        if (buf.size() > (8u << 20)) flush();
+    }
+    void put(const std::string &s) { put(s.data(), s.size()); }
+    void put(char c) { buf.push_back(c); }
+};
+
+// Python seq[start:end] with start >= 0 and end possibly negative (counts from the end).
+inline void py_slice(int64_t len, int64_t start, int64_t end, int64_t *a, int64_t *b) {
+    if (end < 0) end = std::max<int64_t>(0, len + end);
+    if (end > len) end = len;
+    if (start > len) start = len;
+    *a = start;
+    *b = std::max(start, end);
+}
+
+std::string numbered(const char *name, size_t nn, int k) {
+    std::string s(name, nn);
+    const std::string tag = "_" + std::to_string(k);
+    size_t p = s.find('\t');
+    if (p != std::string::npos) return s.substr(0, p) + tag + s.substr(p);
+    p = s.find(' ');
+    if (p != std::string::npos) return s.substr(0, p) + tag + s.substr(p);
+    return s + tag;
+}
+
+void put_seq(Sink &o, const char *s, size_t n, bool rna, bool fasta) {
+    std::string t(s, n);
+    if (rna)
+        for (char &c : t)
+            if (c == 'T') c = 'U';
+    if (!fasta) {
+        o.put(t);
+        return;
+    }
+    for (size_t p = 0; p < t.size(); p += 70) {   // add_line_breaks_to_sequence(seq, 70)
+        o.put(t.data() + p, std::min<size_t>(70, t.size() - p));
+        o.put('\n');
+    }
+}
+
+void put_record(Sink &o, bool fasta, const std::string &name, const char *s, size_t ns, const char *q, size_t nq,
+                bool rna) {
+    if (fasta) {
+        o.put('>');
+        o.put(name);
+        o.put('\n');
+        put_seq(o, s, ns, rna, true);
+    } else {
+        o.put('@');
+        o.put(name);
+        o.put('\n');
+        put_seq(o, s, ns, rna, false);
+        o.put("\n+\n", 3);
+        o.put(q, nq);
+        o.put('\n');
+    }
+}
+
+}  // namespace
+
+extern "C" int pcabi_reads_write(const pcabi_reads *b, const char *path, int append, int gz, int fasta,
+                                 const int32_t *start_trim, const int32_t *end_trim, const int64_t *cut_off,
+                                 const int64_t *cuts, int min_split_read_size, int discard_middle,
+                                 int untrimmed, const uint8_t *select) {
+    if (!b || !path) return fail(PCABI_E_ARG, "bad arguments");
+    Sink o;
+    if (gz) {
+        o.gz = gzopen(path, append ? "ab" : "wb");
+        if (!o.gz) return fail(PCABI_E_ARG, std::string("could not write ") + path);
+    } else {
+        o.fp = std::strcmp(path, "-") == 0 ? stdout : std::fopen(path, append ? "ab" : "wb");
+        if (!o.fp) return fail(PCABI_E_ARG, std::string("could not write ") + path);
+    }
+    std::vector<std::pair<int64_t, int64_t>> rg;
+    std::string ps, pq;
+    for (int64_t i = 0; i < b->n; ++i) {
+        if (select && !select[i]) continue;
+        const char *name = b->names.data() + b->name_off[i];
+        const size_t nn = (size_t)(b->name_off[i + 1] - b->name_off[i]);
+        const char *seq = b->seq.data() + b->seq_off[i];
+        const int64_t ns = b->seq_off[i + 1] - b->seq_off[i];
+        const char *qual = b->qual.data() + b->qual_off[i];
+        const int64_t nq = b->qual_off[i + 1] - b->qual_off[i];
+        const bool rna = b->rna[i] != 0;
+        const int64_t st = start_trim ? start_trim[i] : 0, et = end_trim ? end_trim[i] : 0;
+        // get_seq_with_start_end_adapters_trimmed / get_quals_... (nanopore_read.py:66-82)
+        int64_t sa = 0, sb = ns, qa = 0, qb = nq;
+        if (st || et) {
+            py_slice(ns, st, ns - et, &sa, &sb);
+            py_slice(nq, st, nq - et, &qa, &qb);
+        }
+        bool split = false;
+        if (cut_off)
+            for (int64_t k = cut_off[i]; k < cut_off[i + 1] && !split; ++k) split = cuts[2 * k + 1] > cuts[2 * k];
+        if (!split) {
+            if (untrimmed) { sa = 0; sb = ns; qa = 0; qb = nq; }
+            if (sb == sa) continue;   // no empty sequences
+            put_record(o, fasta != 0, std::string(name, nn), seq + sa, (size_t)(sb - sa), qual + qa, (size_t)(qb - qa), rna);
+            continue;
+        }
+        if (discard_middle) continue;
+        // split parts (get_split_read_parts, nanopore_read.py:84-104): positions of the trimmed
+        // sequence inside any cut range are dropped
+        rg.clear();
+        for (int64_t k = cut_off[i]; k < cut_off[i + 1]; ++k)
+            if (cuts[2 * k + 1] > cuts[2 * k]) rg.emplace_back(cuts[2 * k], cuts[2 * k + 1]);
+        std::sort(rg.begin(), rg.end());
+        const int64_t tl = sb - sa;
+        int part = 0;
+        size_t ri = 0;
+        int64_t run = 0;   // start of the current kept run
+        auto emit = [&](int64_t a, int64_t e) {
+            if (e - a <= 0 || e - a < min_split_read_size) return;
+            ++part;
+            put_record(o, fasta != 0, numbered(name, nn, part), seq + sa + a, (size_t)(e - a), qual + qa + a,
+                       (size_t)(e - a), rna);
+        };
+        int64_t pos = 0;
+        while (pos < tl) {
+            while (ri < rg.size() && rg[ri].second <= pos) ++ri;
+            if (ri < rg.size() && rg[ri].first <= pos) {   // pos is cut
+                emit(run, pos);
+                int64_t e = rg[ri].second;
+                for (size_t rj = ri; rj < rg.size() && rg[rj].first <= e; ++rj) e = std::max(e, rg[rj].second);
+                pos = std::min(e, tl);
+                run = pos;
+            } else {
+                const int64_t nxt = ri < rg.size() ? std::min(rg[ri].first, tl) : tl;
+                pos = nxt;
+            }
+        }
+        emit(run, tl);
+    }
+    o.flush();
+    const bool ok = o.ok;
+    if (o.gz) gzclose(o.gz);
+    else if (o.fp && o.fp != stdout) std::fclose(o.fp);
+    else if (o.fp) std::fflush(o.fp);
+    return ok ? 0 : fail(PCABI_E_ARG, std::string("write failed: ") + path);
+}

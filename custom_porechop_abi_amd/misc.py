@@ -1,0 +1,299 @@
+"""Sequence-file I/O on both sides of the alignment engine (mirror of porechop_abi/misc.py:60-168
+and the read loading / output of porechop_abi/porechop_abi.py:133-187, 535-668).
+
+The parsing and writing run in libpcabi's native host unit (csrc/pcabi_io.cpp: zlib, the
+reference's parse rules, NanoporeRead's normalisation); this module is the Python surface:
+  * load_fasta_or_fastq(filename) -> (records, 'FASTA' | 'FASTQ'), the reference's tuples
+    (FASTA: (short_name, seq, full_name); FASTQ: (short_name, seq, spacer, quals, full_name));
+    the sequence text is the file's own (the reference normalises it later, in NanoporeRead);
+  * load_reads(path, verbosity, print_dest, check_read_count) -> (reads, check_reads, read_type)
+    with NanoporeRead objects, for a file or an Albacore-style directory of FASTQs;
+  * ReadBatch / read_batches(path): the batched path -- names, normalised sequences, qualities
+    and the Dna5 codes already in the engine's packed layout (engine.SeqPack's), no per-read
+    Python objects;
+  * write_reads(batch, path, ...): the reference's trimmed FASTA / FASTQ output for a batch.
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+from ._lib import check, lib
+
+FASTA, FASTQ = 0, 1
+
+
+class _View(ctypes.Structure):
+    _fields_ = [('n', ctypes.c_int64), ('type', ctypes.c_int32), ('names', ctypes.c_void_p),
+                ('name_off', ctypes.c_void_p), ('seq', ctypes.c_void_p), ('seq_off', ctypes.c_void_p),
+                ('qual', ctypes.c_void_p), ('qual_off', ctypes.c_void_p), ('rna', ctypes.c_void_p),
+                ('spacer', ctypes.c_void_p), ('spacer_off', ctypes.c_void_p), ('codes', ctypes.c_void_p), ('codes_len', ctypes.c_int64), ('code_off', ctypes.c_void_p),
+                ('len', ctypes.c_void_p)]
+
+
+def _declare(L):
+    if getattr(L, '_io_declared', False):
+        return L
+    P, i64, c_int = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+    sig = {
+        'pcabi_fastx_open': ([ctypes.c_char_p, c_int, ctypes.POINTER(P)], c_int),
+        'pcabi_fastx_type': ([P], c_int),
+        'pcabi_fastx_next': ([P, i64, i64, ctypes.POINTER(P)], i64),
+        'pcabi_fastx_close': ([P], None),
+        'pcabi_fastx_load': ([ctypes.c_char_p, c_int, ctypes.POINTER(P)], c_int),
+        'pcabi_reads_count': ([P], i64),
+        'pcabi_reads_type': ([P], c_int),
+        'pcabi_reads_views': ([P, ctypes.POINTER(_View)], c_int),
+        'pcabi_reads_free': ([P], None),
+        'pcabi_reads_write': ([P, ctypes.c_char_p, c_int, c_int, c_int, P, P, P, P, c_int, c_int, c_int, P], c_int),
+    }
+    for name, (a, r) in sig.items():
+        f = getattr(L, name)
+        f.argtypes, f.restype = a, r
+    L._io_declared = True
+    return L
+
+
+def _arr(ptr, dtype, n):
+    if n == 0 or not ptr:
+        return np.zeros(0, dtype)
+    return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(np.ctypeslib.as_ctypes_type(dtype))),
+                                 shape=(n,)).copy()
+
+
+class ReadBatch(object):
+    """One batch of parsed reads (owned copies of the native buffers).
+
+    names / seq / qual: bytes buffers with int64 offsets [n + 1]; rna: uint8 [n];
+    codes: Dna5 uint8 buffer, code_off int64 [n] (4-aligned), lengths int32 [n] -- the layout
+    engine.SeqPack builds, so (codes, code_off + start, length) are engine windows directly.
+    The native batch stays alive (self._h) for write_reads."""
+
+    def __init__(self, handle):
+        L = _declare(lib())
+        v = _View()
+        check(L.pcabi_reads_views(handle, ctypes.byref(v)), 'pcabi_reads_views')
+        n = int(v.n)
+        self._h = handle
+        self.type = int(v.type)
+        self.n = n
+        self.name_off = _arr(v.name_off, np.int64, n + 1)
+        self.seq_off = _arr(v.seq_off, np.int64, n + 1)
+        self.qual_off = _arr(v.qual_off, np.int64, n + 1)
+        self.names = ctypes.string_at(v.names, int(self.name_off[-1])) if n else b''
+        self.seq = ctypes.string_at(v.seq, int(self.seq_off[-1])) if n else b''
+        self.qual = ctypes.string_at(v.qual, int(self.qual_off[-1])) if n else b''
+        self.rna = _arr(v.rna, np.uint8, n)
+        self.spacer_off = _arr(v.spacer_off, np.int64, n + 1)
+        self.spacer = ctypes.string_at(v.spacer, int(self.spacer_off[-1])) if n and self.spacer_off[-1] else b''
+        self.codes = _arr(v.codes, np.uint8, int(v.codes_len))
+        self.code_off = _arr(v.code_off, np.int64, n)
+        self.lengths = _arr(v.len, np.int32, n)
+
+    def __len__(self):
+        return self.n
+
+    def __del__(self):
+        h, self._h = getattr(self, '_h', None), None
+        if h:
+            try:
+                _declare(lib()).pcabi_reads_free(h)
+            except Exception:
+                pass
+
+    def name(self, i):
+        return self.names[self.name_off[i]:self.name_off[i + 1]].decode()
+
+    def sequence(self, i):
+        return self.seq[self.seq_off[i]:self.seq_off[i + 1]].decode()
+
+    def quals(self, i):
+        return self.qual[self.qual_off[i]:self.qual_off[i + 1]].decode()
+
+    def spacer_line(self, i):
+        return self.spacer[self.spacer_off[i]:self.spacer_off[i + 1]].decode()
+
+    def views(self, starts=None, lengths=None):
+        """Engine windows (codes, offsets, lengths) of [start, start + length) of every read."""
+        st = np.zeros(self.n, np.int64) if starts is None else np.asarray(starts, np.int64)
+        ln = self.lengths if lengths is None else np.asarray(lengths, np.int32)
+        return self.codes, self.code_off + st, ln
+
+    def nanopore_reads(self):
+        """The reference's NanoporeRead objects (name = full header; seq / quals already
+        normalised, so the constructor leaves them unchanged except for the rna flag)."""
+        from .nanopore_read import NanoporeRead
+        out = []
+        for i in range(self.n):
+            r = NanoporeRead(self.name(i), self.sequence(i), self.quals(i))
+            r.rna = bool(self.rna[i])
+            out.append(r)
+        return out
+
+
+def _open_error(path):
+    msg = lib().pcabi_last_error()
+    return msg.decode() if msg else path
+
+
+def read_batches(path, max_reads=100000, max_bases=1 << 30, raw=False):
+    """Stream a FASTA / FASTQ(.gz) file as ReadBatch objects (pcabi_fastx_next)."""
+    L = _declare(lib())
+    h = ctypes.c_void_p()
+    rc = L.pcabi_fastx_open(os.fsencode(path), int(raw), ctypes.byref(h))
+    if rc != 0:
+        raise ValueError(_open_error(path))
+    try:
+        while True:
+            b = ctypes.c_void_p()
+            n = L.pcabi_fastx_next(h, int(max_reads), int(max_bases), ctypes.byref(b))
+            if n < 0:
+                raise ValueError(_open_error(path))
+            if n == 0:
+                L.pcabi_reads_free(b)
+                return
+            yield ReadBatch(b)
+    finally:
+        L.pcabi_fastx_close(h)
+
+
+def load_batch(path, raw=False):
+    """The whole file as one ReadBatch (pcabi_fastx_load); raw keeps the file's own text."""
+    L = _declare(lib())
+    b = ctypes.c_void_p()
+    rc = L.pcabi_fastx_load(os.fsencode(path), int(raw), ctypes.byref(b))
+    if rc != 0:
+        raise ValueError(_open_error(path))
+    return ReadBatch(b)
+
+
+# ---- the reference's Python surface (porechop_abi/misc.py) -----------------------------------
+def get_compression_type(filename):
+    """misc.py:60-81: 'gz' / 'plain' by magic bytes; bzip2 / zip exit with the reference's text."""
+    with open(filename, 'rb') as f:
+        start = f.read(4)
+    if start.startswith(b'\x1f\x8b\x08'):
+        return 'gz'
+    if start.startswith(b'\x42\x5a\x68'):
+        sys.exit('Error: cannot use bzip2 format - use gzip instead')
+    if start.startswith(b'\x50\x4b\x03\x04'):
+        sys.exit('Error: cannot use zip format - use gzip instead')
+    return 'plain'
+
+
+def load_fasta_or_fastq(filename):
+    """misc.py:108-120 through the native reader in raw mode (the file's own text; the reference
+    normalises it later, in NanoporeRead)."""
+    if not os.path.isfile(filename):
+        sys.exit('Error: could not find ' + filename)
+    get_compression_type(filename)
+    try:
+        b = load_batch(filename, raw=True)
+    except ValueError:
+        sys.exit('\nError: ' + filename + ' could not be parsed - is it formatted correctly?')
+    if b.type == FASTA:
+        recs = []
+        for i in range(b.n):
+            full = b.name(i)
+            recs.append((full.split()[0], b.sequence(i), full))
+        return recs, 'FASTA'
+    recs = []
+    for i in range(b.n):
+        full = b.name(i)
+        recs.append((full.split()[0], b.sequence(i), b.spacer_line(i), b.quals(i), full))
+    return recs, 'FASTQ'
+
+
+def add_line_breaks_to_sequence(sequence, line_length):
+    """misc.py:327-338."""
+    if not sequence:
+        return '\n'
+    return ''.join(sequence[p:p + line_length] + '\n' for p in range(0, len(sequence), line_length))
+
+
+def load_reads(input_file_or_directory, verbosity, print_dest, check_read_count):
+    """porechop_abi.py:133-187: NanoporeRead objects from a file, or from every *.fastq(.gz)
+    under an Albacore-style directory (check reads spread over the files, barcode from the path)."""
+    if os.path.isfile(input_file_or_directory):
+        if verbosity > 0:
+            print('\nLoading reads', flush=True, file=print_dest)
+            print(input_file_or_directory, flush=True, file=print_dest)
+        get_compression_type(input_file_or_directory)
+        try:
+            b = load_batch(input_file_or_directory)
+        except ValueError:
+            sys.exit('\nError: ' + input_file_or_directory + ' could not be parsed - is it formatted correctly?')
+        reads = b.nanopore_reads()
+        read_type = 'FASTA' if b.type == FASTA else 'FASTQ'
+        check_reads = reads[:check_read_count]
+    elif os.path.isdir(input_file_or_directory):
+        fastqs = sorted([os.path.join(d, f) for d, _, fs in os.walk(input_file_or_directory) for f in fs
+                         if f.lower().endswith('.fastq') or f.lower().endswith('.fastq.gz')])
+        if not fastqs:
+            sys.exit('Error: could not find fastq files in ' + input_file_or_directory)
+        reads, check_reads, read_type = [], [], 'FASTQ'
+        per_file = int(round(check_read_count / len(fastqs)))
+        for fq in fastqs:
+            if verbosity > 0:
+                print(fq, flush=True, file=print_dest)
+            file_reads = load_batch(fq).nanopore_reads()
+            bc = get_albacore_barcode_from_path(fq)
+            for r in file_reads:
+                r.albacore_barcode_call = bc
+            reads += file_reads
+            check_reads += file_reads[:per_file]
+    else:
+        sys.exit('Error: could not find ' + input_file_or_directory)
+    if verbosity > 0:
+        print('{:,}'.format(len(reads)) + ' reads loaded\n\n', flush=True, file=print_dest)
+    return reads, check_reads, read_type
+
+
+def get_albacore_barcode_from_path(albacore_path):
+    """porechop_abi.py:190-197: the last /barcodeNN/ directory of the path."""
+    import re
+    if '/unclassified/' in albacore_path:
+        return 'none'
+    matches = re.findall('/barcode(\\d\\d)/', albacore_path)
+    return 'BC' + matches[-1] if matches else None
+
+
+def write_reads(batch, path, out_format='fastq', start_trim=None, end_trim=None, middle_cuts=None,
+                min_split_read_size=1000, discard_middle=False, untrimmed=False, select=None, append=False):
+    """NanoporeRead.get_fasta / get_fastq for every read of a ReadBatch, natively
+    (pcabi_reads_write). out_format: 'fasta' | 'fastq' | 'fasta.gz' | 'fastq.gz'.
+    middle_cuts: per read a list of (begin, end) ranges of the trimmed sequence (the reference's
+    middle_trim_positions as ranges), or None."""
+    L = _declare(lib())
+    gz = out_format.endswith('.gz')
+    fasta = out_format.startswith('fasta')
+    n = batch.n
+    st = None if start_trim is None else np.ascontiguousarray(start_trim, np.int32)
+    et = None if end_trim is None else np.ascontiguousarray(end_trim, np.int32)
+    co = cu = None
+    if middle_cuts is not None:
+        co = np.zeros(n + 1, np.int64)
+        flat = []
+        for i, rg in enumerate(middle_cuts):
+            rg = [(int(a), int(b)) for a, b in (rg or []) if b > a]
+            co[i + 1] = co[i] + len(rg)
+            for a, b in rg:
+                flat += [a, b]
+        cu = np.array(flat if flat else [0, 0], np.int64)
+    sel = None if select is None else np.ascontiguousarray(select, np.uint8)
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+    rc = L.pcabi_reads_write(batch._h, os.fsencode(path), int(append), int(gz), int(fasta), p(st), p(et), p(co), p(cu),
+                             int(min_split_read_size), int(discard_middle), int(untrimmed), p(sel))
+    check(rc, 'pcabi_reads_write')
+
+
+def positions_to_ranges(positions):
+    """A set of positions (NanoporeRead.middle_trim_positions) -> sorted disjoint [a, b) ranges."""
+    out = []
+    for x in sorted(positions):
+        if out and out[-1][1] == x:
+            out[-1][1] = x + 1
+        else:
+            out.append([x, x + 1])
+    return [tuple(r) for r in out]

@@ -13,8 +13,9 @@ call). The batched drivers in porechop_abi.py do the same work in bulk and then 
 decision rules through the _apply_* helpers below, so both paths share one implementation of
 the trimming logic.
 
-Output formatting (colourised windows, FASTA/FASTQ writers) is outside the hot path and is not
-mirrored here.
+Trimmed output (get_fasta / get_fastq / get_split_read_parts, :66-156) is mirrored for the
+per-read interface; the batched path writes through the native writer (misc.write_reads,
+pcabi_reads_write). Colourised verbose windows are not mirrored.
 """
 from .cpp_function_wrappers import adapter_alignment
 
@@ -58,6 +59,56 @@ class NanoporeRead(object):
 
     def seq_length_with_start_end_adapters_trimmed(self):
         return len(self.get_seq_with_start_end_adapters_trimmed())
+
+    def get_quals_with_start_end_adapters_trimmed(self):
+        if not self.start_trim_amount and not self.end_trim_amount:
+            return self.quals
+        return self.quals[self.start_trim_amount:len(self.quals) - self.end_trim_amount]
+
+    # --- trimmed output (porechop_abi/nanopore_read.py:84-156) ------------------------------
+    def get_split_read_parts(self, min_split_read_size):
+        """Maximal runs of the trimmed read outside middle_trim_positions, at least
+        min_split_read_size long, as (seq, quals)."""
+        seq = self.get_seq_with_start_end_adapters_trimmed()
+        quals = self.get_quals_with_start_end_adapters_trimmed()
+        parts, a = [], 0
+        cut = self.middle_trim_positions
+        for i in range(len(seq) + 1):
+            if i == len(seq) or i in cut:
+                if i > a:
+                    parts.append((seq[a:i], quals[a:i]))
+                a = i + 1
+        return [x for x in parts if len(x[0]) >= min_split_read_size]
+
+    def _output_parts(self, min_split_read_size, discard_middle, untrimmed):
+        """(name, seq, quals) records get_fasta / get_fastq write, or None for ''."""
+        if not self.middle_trim_positions:
+            if untrimmed:
+                seq, quals = self.seq, self.quals
+            else:
+                seq = self.get_seq_with_start_end_adapters_trimmed()
+                quals = self.get_quals_with_start_end_adapters_trimmed()
+            return [(self.name, seq, quals)] if seq else []
+        if discard_middle:
+            return []
+        return [(add_number_to_read_name(self.name, i + 1), s, q)
+                for i, (s, q) in enumerate(self.get_split_read_parts(min_split_read_size))]
+
+    def get_fasta(self, min_split_read_size, discard_middle, untrimmed=False):
+        out = []
+        for name, seq, _ in self._output_parts(min_split_read_size, discard_middle, untrimmed):
+            if self.rna:
+                seq = seq.replace('T', 'U')
+            out.append('>' + name + '\n' + ''.join(seq[p:p + 70] + '\n' for p in range(0, len(seq), 70)))
+        return ''.join(out)
+
+    def get_fastq(self, min_split_read_size, discard_middle, untrimmed=False):
+        out = []
+        for name, seq, quals in self._output_parts(min_split_read_size, discard_middle, untrimmed):
+            if self.rna:
+                seq = seq.replace('T', 'U')
+            out.append('@' + name + '\n' + seq + '\n+\n' + quals + '\n')
+        return ''.join(out)
 
     # --- hot path, one alignment per call --------------------------------------------------
     def align_adapter_set(self, adapter_set, end_size, scoring_scheme_vals):

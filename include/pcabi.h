@@ -54,7 +54,8 @@ enum {
     PCABI_OK = 0,
     PCABI_E_ARG = -1,      /* bad argument / unsupported size                   */
     PCABI_E_DEVICE = -2,   /* no usable gfx950 device / HIP runtime error       */
-    PCABI_E_NOMEM = -3
+    PCABI_E_NOMEM = -3,
+    PCABI_E_PARSE = -4     /* malformed FASTA / FASTQ input                     */
 };
 
 /* ---- legacy drop-in ------------------------------------------------------------------ */
@@ -262,6 +263,65 @@ int pcabi_barcode_call_host(int device, const int32_t *start_res, int32_t n_sa, 
                             int32_t n_ea, const int32_t *end_slot_adp, const int32_t *end_slot_name,
                             int32_t n_end_slots, int64_t n_read, double barcode_threshold, double barcode_diff,
                             int require_two, int32_t *call, double *scores);
+
+/*
+ * Sequence files (host code, csrc/pcabi_io.cpp; replaces porechop_abi/misc.py:60-168
+ * load_fasta_or_fastq and NanoporeRead's normalisation, nanopore_read.py:31-44, for the batched
+ * path, and NanoporeRead.get_fasta / get_fastq, nanopore_read.py:84-156, for output).
+ *   pcabi_fastx_open / next / close : streaming reader, plain or gzip, FASTA or FASTQ (by the
+ *       first character), the reference's parse rules; next() returns up to max_reads records
+ *       (stopping once max_bases sequence bytes are in the batch) as a new pcabi_reads, or a
+ *       negative PCABI_E_* (PCABI_E_PARSE for a malformed file); 0 records at end of file.
+ *   pcabi_fastx_load : the whole file as one batch.
+ *   raw != 0 : keep the file's text (no upper-casing, no U -> T, no quality padding; FASTQ '+'
+ *       lines kept in spacer) -- the tuples of misc.load_fasta_or_fastq.
+ *   pcabi_reads_views: borrowed pointers into a batch (valid until pcabi_reads_free):
+ *       names   : full headers (text after '@' / '>'), name_off[n + 1]
+ *       seq     : upper-cased sequences, U -> T for RNA reads (rna[i] = 1), seq_off[n + 1]
+ *       qual    : qualities padded with '+' to the sequence length (FASTA: all '+'), qual_off[n + 1]
+ *       codes   : Dna5 codes in the engine layout (4-aligned code_off[n], len[n], 16 bytes of
+ *                 N padding at the end) -- ready for pcabi_align_host / the device ABI.
+ *   pcabi_reads_write: the reference's trimmed output of every read (select[i] != 0 if given):
+ *       start_trim / end_trim (NULL = untrimmed), middle cut ranges [cuts[2k], cuts[2k+1]) of the
+ *       trimmed sequence for k in [cut_off[i], cut_off[i+1]) (NULL = none; a read with cuts is
+ *       written as its split parts, or dropped with discard_middle), FASTA (70-column lines) or
+ *       FASTQ, gzip when gz != 0, appended when append != 0, path "-" = stdout (plain only);
+ *       untrimmed != 0 writes reads without cuts whole (split parts still come from the trimmed
+ *       sequence, as in the reference).
+ */
+enum { PCABI_FASTA = 0, PCABI_FASTQ = 1 };
+typedef struct pcabi_fastx pcabi_fastx;
+typedef struct pcabi_reads pcabi_reads;
+typedef struct pcabi_reads_view {
+    int64_t n;
+    int32_t type;
+    const char *names;
+    const int64_t *name_off;
+    const char *seq;
+    const int64_t *seq_off;
+    const char *qual;
+    const int64_t *qual_off;
+    const uint8_t *rna;
+    const char *spacer;
+    const int64_t *spacer_off;
+    const uint8_t *codes;
+    int64_t codes_len;
+    const int64_t *code_off;
+    const int32_t *len;
+} pcabi_reads_view;
+int pcabi_fastx_open(const char *path, int raw, pcabi_fastx **out);
+int pcabi_fastx_type(const pcabi_fastx *r);
+int64_t pcabi_fastx_next(pcabi_fastx *r, int64_t max_reads, int64_t max_bases, pcabi_reads **out);
+void pcabi_fastx_close(pcabi_fastx *r);
+int pcabi_fastx_load(const char *path, int raw, pcabi_reads **out);
+int64_t pcabi_reads_count(const pcabi_reads *b);
+int pcabi_reads_type(const pcabi_reads *b);
+int pcabi_reads_views(const pcabi_reads *b, pcabi_reads_view *v);
+void pcabi_reads_free(pcabi_reads *b);
+int pcabi_reads_write(const pcabi_reads *b, const char *path, int append, int gz, int fasta,
+                      const int32_t *start_trim, const int32_t *end_trim, const int64_t *cut_off,
+                      const int64_t *cuts, int min_split_read_size, int discard_middle,
+                      int untrimmed, const uint8_t *select);
 
 #ifdef __cplusplus
 }
