@@ -52,10 +52,13 @@ def parse():
     ap.add_argument('--cpu-sample', type=int, default=12000, help='reads in the CPU-baseline sample (0 = skip)')
     ap.add_argument('--cpu-threads', type=int, default=0, help='0 = min(16, cpus available)')
     ap.add_argument('--check', type=int, default=256, help='reads checked against the oracle after timing')
-    ap.add_argument('--workload', choices=['endtrim', 'middle', 'barcodes'], default='endtrim',
+    ap.add_argument('--workload', choices=['endtrim', 'middle', 'barcodes', 'e2e', 'compat'], default='endtrim',
                     help='endtrim: the headline metric (default); middle: end trim + middle-adapter scan '
                          '(BASELINE.json configs[2]); barcodes: end trim + barcode demultiplexing against '
-                         '96 barcode sets (configs[3])')
+                         '96 barcode sets (configs[3]); e2e: FASTQ file -> native parse -> end trim + middle '
+                         'scan on the GPU -> fork filter -> native trimmed FASTQ output (the CLI path); compat: '
+                         'the ab-initio all-vs-all check_compatibility matrix')
+    ap.add_argument('--compat-seqs', type=int, default=3000, help='sequences of the compat workload')
     ap.add_argument('--barcodes', type=int, default=96, help='barcode sets of the barcodes workload')
     ap.add_argument('--kit', choices=['pcr96', 'native12'], default='pcr96',
                     help='barcodes workload: pcr96 = Barcode 1..96 (forward) sets; native12 = native '
@@ -86,6 +89,11 @@ def main():
     _lib.check(L.pcabi_dev_set(local), 'pcabi_dev_set')
     if args.workload == 'middle':
         return run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapters)
+    args.local_device = local
+    if args.workload == 'compat':
+        return run_compat(args, rank, world, dist, torch, L, _lib)
+    if args.workload == 'e2e':
+        return run_e2e(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapters)
 
     # ---- workload (host) ----
     barcodes = args.workload == 'barcodes'
@@ -497,6 +505,190 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
             'gcups_step': round((cells_end + cells_mid) / (step_ms * 1e-3) / 1e9, 1),
             'cpu_baseline': cpu,
             'gpu_vs_cpu': round(value / cpu['value'], 1) if cpu else None,
+            'parity_spot_check': checked,
+            'setup_s': round(gen_s, 2),
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def run_compat(args, rank, world, dist, torch, L, _lib):
+    """Ab-initio clustering link test (consensus.py:72-100 all_vs_all_matrix over
+    compatibility.so::check_compatibility): every pair of --compat-seqs adapter-like sequences
+    (20-60 bp, families of mutated variants, the shape the k-mer counting feeds it). One step =
+    the whole flag matrix through pcabi_compat_all_vs_all_host (host buffers in, the n x n int32
+    matrix out; every sequence against every sequence as one tiled cross product).
+    value = pairs / s; cpu_baseline = the reference's own compatibility.so on a bounded sample of
+    the same pairs, called like consensus.py does (one Python loop, one thread)."""
+    from custom_porechop_abi_amd import consensus
+    rng = np.random.default_rng(77 + rank)
+    letters = np.array(list('ACGT'))
+    seqs = []
+    while len(seqs) < args.compat_seqs:
+        base = ''.join(letters[rng.integers(0, 4, int(rng.integers(20, 61)))])
+        for _ in range(int(rng.integers(1, 12))):
+            s = list(base)
+            for _ in range(int(rng.integers(0, 4))):
+                k = int(rng.integers(0, len(s)))
+                s[k] = letters[rng.integers(0, 4)]
+            a = int(rng.integers(0, 4))
+            seqs.append(''.join(s)[a:])
+    seqs = seqs[:args.compat_seqs]
+    n = len(seqs)
+    iu, ju = np.triu_indices(n, 1)
+    iu, ju = iu.astype(np.int32), ju.astype(np.int32)
+    for _ in range(args.warmup):
+        consensus.all_vs_all_flags(seqs, device=args.local_device)
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        mat = consensus.all_vs_all_flags(seqs, device=args.local_device)
+    elapsed = time.perf_counter() - t0
+    flags = mat[iu, ju]
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device='cuda' if args.dist_backend == 'nccl' else 'cpu')
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    n_pairs = len(iu)
+    checked = None
+    cpu = None
+    sample = np.random.default_rng(5).choice(n_pairs, size=min(n_pairs, 4000), replace=False)
+    if rank == 0 and args.check:
+        from tests import oracle_lib
+        olib = oracle_lib.load()
+        olib.pcabi_oracle_compat.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        olib.pcabi_oracle_compat.restype = ctypes.c_int
+        bad = sum(int(olib.pcabi_oracle_compat(seqs[iu[k]].encode(), seqs[ju[k]].encode()) != flags[k])
+                  for k in sample.tolist())
+        checked = {'pairs_checked': int(len(sample)), 'mismatches': bad,
+                   'flags_0_1_2': [int((flags == v).sum()) for v in range(3)]}
+    ref = os.path.join(ROOT, 'oracle', '_ref', 'compatibility.so')
+    if rank == 0 and world == 1 and args.cpu_sample > 0 and os.path.isfile(ref):
+        clib = ctypes.CDLL(ref)
+        clib.check_compatibility.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        clib.check_compatibility.restype = ctypes.c_int
+        enc = [s.encode('utf-8') for s in seqs]
+        k = min(n_pairs, args.cpu_sample * 30)
+        t1 = time.perf_counter()
+        for t in range(k):
+            clib.check_compatibility(enc[iu[t]], enc[ju[t]])
+        dt = time.perf_counter() - t1
+        cpu = {'value': round(k / dt, 1), 'unit': 'pairs/s', 'cores': 1, 'kind': 'reference',
+               'sample': '%d pairs of the same set, %.1f s, the reference compatibility.so called from one Python '
+                         'loop as consensus.py:88-99 does' % (k, dt)}
+    if rank == 0:
+        value = world * n_pairs * args.steps / elapsed
+        out = {'metric': 'check_compatibility pairs/sec (ab-initio all-vs-all link test)',
+               'value': round(value, 1), 'unit': 'pairs/s', 'n_gpus': world, 'steps': args.steps,
+               'warmup': args.warmup, 'ms_per_step': round(1e3 * elapsed / args.steps, 3), 'higher_is_better': True,
+               'scaling': 'weak', 'vs_baseline': None, 'dtype': 'int32',
+               'data': 'synthetic adapter-like sequences (20-60 bp families of mutated variants)',
+               'config': {'workload': 'compat: all %d pairs of %d sequences (consensus.all_vs_all_flags), scoring '
+                                      '2/-1/-1 linear, flags on the device, host buffers in / out' % (n_pairs, n),
+                          'parallelism': 'dp%d' % world},
+               'cpu_baseline': cpu, 'gpu_vs_cpu': round(value / cpu['value'], 1) if cpu else None,
+               'parity_spot_check': checked}
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def write_fastq(path, reads, seed):
+    """Synthetic reads (Dna5 code arrays) as a FASTQ file with ONT-like headers and qualities."""
+    rng = np.random.default_rng(seed)
+    letters = np.frombuffer(b'ACGTN', np.uint8)
+    with open(path, 'wb') as f:
+        for k, r in enumerate(reads):
+            q = (rng.integers(5, 40, len(r)) + 33).astype(np.uint8).tobytes()
+            f.write(b'@read%d runid=synthetic ch=%d\n' % (k, k % 512) + letters[r].tobytes() + b'\n+\n' + q + b'\n')
+
+
+def run_e2e(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapters):
+    """The CLI path end to end, file to file (porechop_abi.py:41-131 with the reference's defaults:
+    end_size 150, end_threshold 75, extra_end_trim 2, min_trim_size 4, middle_threshold 90, extra
+    middle trim 10 / 100, min_split_read_size 1000, the fork's start-and-end filter, FASTQ out),
+    for the first 50 adapter sets (adapter-set discovery is excluded: it runs once on the check
+    reads). One step:
+      native parse of the FASTQ (pcabi_fastx_load) -> H2D of the packed codes + window views
+      -> k_tile_windows / k_align / k_end_trim -> trims D2H -> middle scan of the trimmed reads
+      (pcabi_middle_scan_dev) -> middle cut ranges (host, vectorised) -> native trimmed FASTQ
+      writer (pcabi_reads_write) for the reads with start and end adapters.
+    value = reads / step time; the breakdown says where the time goes."""
+    from custom_porechop_abi_amd import misc
+    from custom_porechop_abi_amd.porechop_abi import middle_adapter_list
+    sets = [a for a in A.fresh_adapters() if '(full sequence)' not in a.name][:args.sets]
+    start_adps = [a.start_sequence[1] for a in sets if a.start_sequence]
+    end_adps = [a.end_sequence[1] for a in sets if a.end_sequence]
+    mid_adps = [x[1] for x in middle_adapter_list(sets)[0]]
+    n, E = args.reads, args.end_size
+    tmp = os.environ.get('TMPDIR', '/tmp')
+    in_path = os.path.join(tmp, 'pcabi_e2e_%d_%d.fastq' % (os.getpid(), rank))
+    out_path = os.path.join(tmp, 'pcabi_e2e_%d_%d.out.fastq' % (os.getpid(), rank))
+    t0 = time.time()
+    reads = synth.make_reads(n, args.mean_len, seed=12345 + rank)
+    write_fastq(in_path, reads, 99 + rank)
+    in_bytes = os.path.getsize(in_path)
+    del reads
+    gen_s = time.time() - t0
+
+    from custom_porechop_abi_amd.pipeline import FileTrimmer
+    sc = SCORING
+    n_sa, n_ea = len(start_adps), len(end_adps)
+    ft = FileTrimmer(sets, sc, E, 75.0, 2, 4, args.middle_threshold, 10, 100, 1000, device=args.local_device)
+    last = {}
+
+    def step():
+        ft.times = {}
+        last.update(ft.trim_file(in_path, out_path, 'fastq', max_reads=n))
+        return dict(ft.times)
+
+    for _ in range(args.warmup):
+        step()
+    if dist is not None:
+        dist.barrier()
+    acc = {}
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        for k, v in step().items():
+            acc[k] = acc.get(k, 0.0) + v
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device='cuda' if args.dist_backend == 'nccl' else 'cpu')
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    out_bytes = os.path.getsize(out_path)
+    checked = None
+    if args.check and rank == 0:
+        # the written file, read back: every kept read's first part equals the reference's rule
+        # on its own trims (the reads' alignment parity is covered by the other workloads)
+        got = misc.load_batch(out_path)
+        checked = {'records_written': int(got.n), 'reads_in': last['reads_in'], 'reads_kept': last['reads_kept']}
+    for p in (in_path, out_path):
+        try:
+            os.remove(p)
+        except OSError:
+            pass
+    if rank == 0:
+        step_s = elapsed / args.steps
+        value = world * n * args.steps / elapsed
+        out = {
+            'metric': 'reads/sec end to end, FASTQ file -> trimmed FASTQ file (ONT reads x 50 adapter sets)',
+            'value': round(value, 1), 'unit': 'reads/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(1e3 * step_s, 3), 'higher_is_better': True,
+            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'int32',
+            'data': 'synthetic FASTQ (seeded ONT-like reads, SURVEY.md §8d recipe; mean %d bp)' % args.mean_len,
+            'config': {'workload': 'e2e: %d reads/GPU FASTQ (%.0f MB) -> parse -> end trim (%d start + %d end '
+                                   'adapters) -> middle scan (%d adapters, threshold %.0f) -> fork filter -> '
+                                   'trimmed FASTQ' % (n, in_bytes / 1e6, n_sa, n_ea, len(mid_adps),
+                                                      args.middle_threshold),
+                       'reads_per_gpu': n, 'adapter_sets': len(sets), 'scoring': list(sc),
+                       'parallelism': 'dp%d (read shards)' % world},
+            'breakdown_ms_per_step': {k: round(1e3 * v / args.steps, 2) for k, v in acc.items()},
+            'input_MB_per_s': round(in_bytes / step_s / 1e6, 1),
+            'output_bytes': out_bytes,
+            'cpu_baseline': None,
             'parity_spot_check': checked,
             'setup_s': round(gen_s, 2),
         }

@@ -102,6 +102,7 @@ struct Best {
 // Final integers, same meaning as ScoredAlignment + the two identity fractions m/l1, m/l2.
 struct Result {
     int rs, re, as, ae, score, m, l1, l2;
+    int diag_en;   // the aligned region's last column is a diagonal (both rows hold a base)
 };
 
 // Closed forms of ScoredAlignment (porechop_abi/src/alignment.cpp:27-109) in terms of the path.
@@ -149,7 +150,22 @@ PCABI_HD Result finish(const Best &b, int L, int n) {
     const int a0 = j0 > 0 ? h : 0;
     const int a1 = tailA ? (h + K + (L - b.bi) - 1) : (h + kA);
     r.l2 = a1 - a0 + 1;
+    r.diag_en = readSide ? (trailV > 0 ? precd : lastD) : (trailH > 0 ? precd : lastD);
     return r;
+}
+
+// check_compatibility (porechop_abi/ab_initio_src/compatibility.cpp:124-170) from the aligned
+// region of the longer sequence (row 0, n bases) against the shorter: the reference counts
+// mismatching columns on [st, en) only, so mapped - distance = 1 + m - [column en matches];
+// identity = that * 100 / mapped in INTEGER arithmetic, linked at >= 87.5; "included" when the
+// region starts or ends more than OVERLAP_LIMIT = 3 bases inside row 0.
+// en_match: column en is a diagonal with equal bases. mapped <= 0 (no overlap: the reference
+// divides by zero there) -> 0.
+PCABI_HD int compat_flag(const Result &r, int n, int en_match) {
+    if (r.rs < 0 || r.l1 <= 0) return 0;
+    const int identity = (1 + r.m - en_match) * 100 / r.l1;
+    if (identity < 88) return 0;
+    return (r.rs > 3 || (n - r.re) > 3) ? 2 : 1;
 }
 
 // The reference prints 100.0*m/l with "%f" (std::to_string, porechop_abi/src/alignment.cpp:118-119)

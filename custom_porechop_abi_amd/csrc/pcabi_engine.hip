@@ -101,6 +101,7 @@ struct KParams {
     int32_t *out;
     int64_t out_stride;
     pcabi::Scoring sc;
+    int32_t *compat;           // != nullptr: write check_compatibility flags instead of results
 };
 
 // Window reader: one dword per lane every 4 columns (a wave-uniform branch -- j is the same in
@@ -207,6 +208,16 @@ __device__ __forceinline__ void run_lane(const KParams &p, int a_local, int64_t 
         } else {
             r = pcabi::align_lane_generic<RPL, AFFINE>(rd, n, adp, L, p.sc);
         }
+    }
+    if (p.compat) {
+        // pairs mode only: the window is read in place, the adapter from its padded row
+        int en_match = 0;
+        if (r.rs >= 0 && r.diag_en && r.l1 > 0) {
+            const uint8_t *ab = reinterpret_cast<const uint8_t *>(p.adp_pad + (int64_t)a_local * (RPL / 4));
+            en_match = p.codes[p.win_off[w] + r.re] == ab[RPL - L + r.ae];
+        }
+        p.compat[out_idx] = pcabi::compat_flag(r, n, en_match);
+        return;
     }
     store_result(p.out, p.out_stride, out_idx, r);
 }
@@ -906,7 +917,8 @@ int align_host_impl(int device, const uint8_t *codes, int64_t codes_len, const i
                     const int32_t *win_len, int64_t n_win, const uint8_t *adp_codes,
                     const int32_t *adp_off, const int32_t *adp_len, int32_t n_adp,
                     const int32_t *task_win, const int32_t *task_adp, int64_t n_task, int match,
-                    int mismatch, int gap_open, int gap_extend, const double *first_thr, int32_t *out) {
+                    int mismatch, int gap_open, int gap_extend, const double *first_thr, int32_t *out,
+                    bool compat = false) {
     if (device < 0 || device >= 16) return fail(PCABI_E_ARG, "bad device index");
     if (n_win < 0 || n_adp < 0 || n_task < 0) return fail(PCABI_E_ARG, "negative count");
     if (int rc = check_common(adp_len, n_adp)) return rc;
@@ -955,6 +967,7 @@ int align_host_impl(int device, const uint8_t *codes, int64_t codes_len, const i
     p.out = (int32_t *)e.out.p;
     p.out_stride = n_res;
     p.sc = sc;
+    p.compat = compat ? (int32_t *)e.out.p : nullptr;   // pairs mode only (checked by the caller)
     const bool affine = gap_open != gap_extend;
 
     // host-side pair grouping (pairs mode): per bucket, per adapter, runs padded to 64 lanes
@@ -1040,7 +1053,7 @@ int align_host_impl(int device, const uint8_t *codes, int64_t codes_len, const i
         HIP_TRY(hipMemcpyAsync(out, e.hits.p, sizeof(int32_t) * 5 * (size_t)n_win, hipMemcpyDeviceToHost,
                                e.stream));
     } else {
-        HIP_TRY(hipMemcpyAsync(out, e.out.p, sizeof(int32_t) * PCABI_NFIELDS * (size_t)n_res,
+        HIP_TRY(hipMemcpyAsync(out, e.out.p, sizeof(int32_t) * (compat ? 1 : PCABI_NFIELDS) * (size_t)n_res,
                                hipMemcpyDeviceToHost, e.stream));
     }
     HIP_TRY(hipStreamSynchronize(e.stream));
@@ -1701,6 +1714,112 @@ int pcabi_barcode_call_dev(const int32_t *start_res, int64_t start_stride, const
                        st, en, n_read, barcode_threshold, barcode_diff, require_two, call, scores);
     HIP_TRY(hipGetLastError());
     return 0;
+}
+
+int pcabi_compat_host(int device, const uint8_t *codes, int64_t codes_len, const int64_t *seq_off,
+                      const int32_t *seq_len, int64_t n_seq, const int32_t *pair_i, const int32_t *pair_j,
+                      int64_t n_pairs, int32_t *flags) {
+    if (n_seq < 0 || n_pairs < 0) return fail(PCABI_E_ARG, "negative count");
+    if (n_seq > INT32_MAX) return fail(PCABI_E_ARG, "too many sequences");
+    // row 0 = the longer sequence (make_stringSet, compatibility.cpp:17-28: ties keep seq1 first)
+    std::vector<int32_t> tw, ta;
+    std::vector<int64_t> at;           // result slot of each task
+    tw.reserve((size_t)n_pairs);
+    ta.reserve((size_t)n_pairs);
+    for (int64_t t = 0; t < n_pairs; ++t) {
+        const int32_t i = pair_i[t], j = pair_j[t];
+        if (i < 0 || i >= n_seq || j < 0 || j >= n_seq) return fail(PCABI_E_ARG, "pair index out of range");
+        const bool swap = seq_len[i] < seq_len[j];
+        const int32_t lo = swap ? j : i, sh = swap ? i : j;
+        flags[t] = 0;                  // empty sequences: no alignment (the reference is undefined)
+        if (seq_len[lo] == 0 || seq_len[sh] == 0) continue;
+        if (seq_len[sh] > kMaxRPL)
+            return fail(PCABI_E_ARG, "check_compatibility: the shorter sequence exceeds " + std::to_string(kMaxRPL) + " bases");
+        tw.push_back(lo);
+        ta.push_back(sh);
+        at.push_back(t);
+    }
+    if (tw.empty()) return 0;
+    std::vector<uint8_t> acodes;
+    std::vector<int32_t> aoff((size_t)n_seq), alen((size_t)n_seq);
+    for (int64_t k = 0; k < n_seq; ++k) {
+        aoff[k] = (int32_t)acodes.size();
+        alen[k] = std::max<int32_t>(1, std::min<int32_t>(seq_len[k], kMaxRPL));
+        for (int32_t q = 0; q < alen[k]; ++q) acodes.push_back(seq_len[k] > 0 ? codes[seq_off[k] + q] : 0);
+    }
+    std::vector<int32_t> got(tw.size());
+    // compatibility.h:5-8: Score<int, Simple>(match 2, mismatch -1, gap -1) -> linear gaps
+    if (int rc = align_host_impl(device, codes, codes_len, seq_off, seq_len, n_seq, acodes.data(), aoff.data(),
+                                 alen.data(), (int32_t)n_seq, tw.data(), ta.data(), (int64_t)tw.size(), 2, -1, -1, -1,
+                                 nullptr, got.data(), true))
+        return rc;
+    for (size_t k = 0; k < tw.size(); ++k) flags[at[k]] = got[k];
+    return 0;
+}
+
+int pcabi_compat_all_vs_all_host(int device, const uint8_t *codes, int64_t codes_len, const int64_t *seq_off,
+                                 const int32_t *seq_len, int64_t n_seq, int32_t *mat) {
+    if (n_seq < 0) return fail(PCABI_E_ARG, "negative count");
+    if (n_seq > 46340) return fail(PCABI_E_ARG, "too many sequences for one matrix");
+    const int64_t n = n_seq;
+    for (int64_t k = 0; k < n * n; ++k) mat[k] = -1;
+    if (n < 2) return 0;
+    bool cross_ok = true;
+    for (int64_t k = 0; k < n; ++k) cross_ok = cross_ok && seq_len[k] >= 1 && seq_len[k] <= kMaxRPL;
+    if (!cross_ok) {
+        // some sequence cannot be a DP row set: explicit pairs (the longer is never a row set)
+        std::vector<int32_t> pi, pj;
+        for (int64_t i = 0; i < n; ++i)
+            for (int64_t j = i + 1; j < n; ++j) { pi.push_back((int32_t)i); pj.push_back((int32_t)j); }
+        std::vector<int32_t> f(pi.size());
+        if (int rc = pcabi_compat_host(device, codes, codes_len, seq_off, seq_len, n, pi.data(), pj.data(),
+                                       (int64_t)pi.size(), f.data()))
+            return rc;
+        for (size_t t = 0; t < pi.size(); ++t) mat[(int64_t)pi[t] * n + pj[t]] = mat[(int64_t)pj[t] * n + pi[t]] = f[t];
+        return 0;
+    }
+    // every sequence against every sequence in the tiled cross mode (both orientations, no host
+    // task lists), then per pair the orientation the reference uses: row 0 = the longer, ties ->
+    // the first argument (consensus.py:90-97 passes seq_i, seq_j with i < j)
+    std::vector<uint8_t> acodes;
+    std::vector<int32_t> aoff((size_t)n);
+    for (int64_t k = 0; k < n; ++k) {
+        aoff[k] = (int32_t)acodes.size();
+        acodes.insert(acodes.end(), codes + seq_off[k], codes + seq_off[k] + seq_len[k]);
+    }
+    std::vector<int32_t> f((size_t)(n * n));   // f[a * n + w]: window w as row 0, sequence a as rows
+    if (int rc = align_host_impl(device, codes, codes_len, seq_off, seq_len, n, acodes.data(), aoff.data(), seq_len,
+                                 (int32_t)n, nullptr, nullptr, 0, 2, -1, -1, -1, nullptr, f.data(), true))
+        return rc;
+    for (int64_t i = 0; i < n; ++i)
+        for (int64_t j = i + 1; j < n; ++j) {
+            const int32_t v = seq_len[i] >= seq_len[j] ? f[j * n + i] : f[i * n + j];
+            mat[i * n + j] = mat[j * n + i] = v;
+        }
+    return 0;
+}
+
+int check_compatibility(char *raw_seq1, char *raw_seq2) {
+    // SeqAn String<Dna> (compatibility.h:23): A C G T/U, anything else -> A
+    const size_t n1 = raw_seq1 ? std::strlen(raw_seq1) : 0, n2 = raw_seq2 ? std::strlen(raw_seq2) : 0;
+    std::vector<uint8_t> codes(((n1 + 3) & ~(size_t)3) + n2 + 16, 0);
+    auto enc = [](char c) -> uint8_t {
+        switch (c) {
+        case 'C': case 'c': return 1;
+        case 'G': case 'g': return 2;
+        case 'T': case 't': case 'U': case 'u': return 3;
+        default: return 0;
+        }
+    };
+    for (size_t k = 0; k < n1; ++k) codes[k] = enc(raw_seq1[k]);
+    const int64_t o2 = (int64_t)((n1 + 3) & ~(size_t)3);
+    for (size_t k = 0; k < n2; ++k) codes[o2 + k] = enc(raw_seq2[k]);
+    const int64_t off[2] = {0, o2};
+    const int32_t len[2] = {(int32_t)n1, (int32_t)n2};
+    const int32_t pi = 0, pj = 1;
+    int32_t flag = 0;
+    if (pcabi_compat_host(0, codes.data(), (int64_t)codes.size(), off, len, 2, &pi, &pj, 1, &flag) != 0) return 0;
+    return flag;
 }
 
 int pcabi_barcode_call_host(int device, const int32_t *start_res, int32_t n_sa, const int32_t *start_slot_adp,

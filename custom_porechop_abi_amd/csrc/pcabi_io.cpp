@@ -67,6 +67,7 @@ struct pcabi_fastx {
     bool eof = false;
     int64_t line_no = 0;
     bool raw = false;              // keep the file's text (misc.load_fasta_or_fastq tuples)
+    size_t size_hint = 0;          // decoded bytes expected (file size; x4 for gzip)
     // FASTA state that crosses batch boundaries
     bool fa_have_name = false;     // a header was seen (its name may be empty)
     std::string fa_name, fa_seq;
@@ -91,26 +92,33 @@ struct pcabi_reads {
 
 namespace {
 
-// Next line (without its terminator) as [*p, *p + *n); false at end of file.
+// Next line (without its terminator) as [*p, *p + *n); false at end of file. Terminators are
+// found with memchr: the first '\n', then any '\r' before it (CRLF, or a lone CR that ends the
+// line earlier).
 bool next_line(pcabi_fastx *r, const char **p, size_t *n) {
     for (;;) {
-        // look for a terminator in the buffered bytes
-        for (size_t i = r->pos; i < r->end; ++i) {
-            const char c = r->buf[i];
-            if (c == '\n' || c == '\r') {
-                if (c == '\r' && i + 1 == r->end && !r->eof) break;   // need to see if \n follows
-                *p = r->buf.data() + r->pos;
-                *n = i - r->pos;
-                size_t nx = i + 1;
-                if (c == '\r' && nx < r->end && r->buf[nx] == '\n') ++nx;
-                r->pos = nx;
-                ++r->line_no;
-                return true;
-            }
+        const char *base = r->buf.data();
+        const char *s0 = base + r->pos, *e0 = base + r->end;
+        const char *nl = (const char *)std::memchr(s0, '\n', (size_t)(e0 - s0));
+        const char *lim = nl ? nl : e0;
+        const char *cr = (const char *)std::memchr(s0, '\r', (size_t)(lim - s0));
+        if (cr && (cr + 1 < e0 || r->eof)) {          // \r ends the line (a following \n is eaten)
+            *p = s0;
+            *n = (size_t)(cr - s0);
+            r->pos = (size_t)(cr + 1 - base) + ((cr + 1 < e0 && cr[1] == '\n') ? 1 : 0);
+            ++r->line_no;
+            return true;
+        }
+        if (nl && !cr) {
+            *p = s0;
+            *n = (size_t)(nl - s0);
+            r->pos = (size_t)(nl + 1 - base);
+            ++r->line_no;
+            return true;
         }
         if (r->eof) {
             if (r->pos < r->end) {   // last line without a terminator
-                *p = r->buf.data() + r->pos;
+                *p = s0;
                 *n = r->end - r->pos;
                 r->pos = r->end;
                 ++r->line_no;
@@ -149,42 +157,68 @@ void strip(const char **p, size_t *n) {
     *n = m;
 }
 
-// One record appended to the batch, with NanoporeRead's normalisation unless raw.
-void add_record(pcabi_reads *b, const char *name, size_t nn, const char *seq, size_t ns, const char *q, size_t nq,
-                bool raw = false, const char *sp = nullptr, size_t nsp = 0) {
-    b->spacer.insert(b->spacer.end(), sp, sp + nsp);
-    b->spacer_off.push_back((int64_t)b->spacer.size());
+uint8_t g_upper[256];
+const bool g_upper_init = [] {
+    for (int i = 0; i < 256; ++i) g_upper[i] = (uint8_t)((i >= 'a' && i <= 'z') ? i - 32 : i);
+    return true;
+}();
+
+// A record is appended in pieces (name, sequence, qualities) straight from the line buffer.
+void add_name(pcabi_reads *b, const char *name, size_t nn) {
     b->names.insert(b->names.end(), name, name + nn);
     b->name_off.push_back((int64_t)b->names.size());
+}
+
+// Sequence with NanoporeRead's normalisation unless raw: upper case, U -> T when the read holds
+// more U than T; Dna5 codes (U and T are both code 3) into the engine layout in the same pass.
+void add_seq(pcabi_reads *b, const char *seq, size_t ns, bool raw) {
     const size_t s0 = b->seq.size();
     b->seq.resize(s0 + ns);
     char *d = b->seq.data() + s0;
+    const int64_t off = (int64_t)b->codes.size();
+    const size_t padded = (ns + 3) & ~(size_t)3;
+    b->codes.resize((size_t)off + padded);
+    uint8_t *c = b->codes.data() + off;
     int64_t nu = 0, nt = 0;
-    for (size_t i = 0; i < ns; ++i) {
-        char c = seq[i];
-        if (!raw && c >= 'a' && c <= 'z') c = (char)(c - 32);
-        nu += (c == 'U');
-        nt += (c == 'T');
-        d[i] = c;
+    if (raw) {
+        std::memcpy(d, seq, ns);
+        for (size_t i = 0; i < ns; ++i) c[i] = g_dna5[(unsigned char)seq[i]];
+    } else {
+        for (size_t i = 0; i < ns; ++i) {
+            const uint8_t u = g_upper[(unsigned char)seq[i]];
+            nu += (u == 'U');
+            nt += (u == 'T');
+            d[i] = (char)u;
+            c[i] = g_dna5[u];
+        }
     }
+    for (size_t i = ns; i < padded; ++i) c[i] = 4;
     const bool rna = !raw && nu > nt;
     if (rna)
         for (size_t i = 0; i < ns; ++i)
             if (d[i] == 'U') d[i] = 'T';
     b->rna.push_back(rna ? 1 : 0);
     b->seq_off.push_back((int64_t)b->seq.size());
+    b->code_off.push_back(off);
+    b->len.push_back((int32_t)ns);
+}
+
+// Qualities padded with '+' to the sequence length unless raw; closes the record.
+void add_qual(pcabi_reads *b, const char *q, size_t nq, size_t ns, bool raw, const char *sp = nullptr,
+              size_t nsp = 0) {
     b->qual.insert(b->qual.end(), q, q + nq);
     if (!raw && nq < ns) b->qual.insert(b->qual.end(), ns - nq, '+');
     b->qual_off.push_back((int64_t)b->qual.size());
-    // engine layout
-    const int64_t off = (int64_t)b->codes.size();
-    b->code_off.push_back(off);
-    b->len.push_back((int32_t)ns);
-    const size_t padded = (ns + 3) & ~(size_t)3;
-    b->codes.resize((size_t)off + padded, 4);
-    uint8_t *c = b->codes.data() + off;
-    for (size_t i = 0; i < ns; ++i) c[i] = g_dna5[(unsigned char)d[i]];
+    b->spacer.insert(b->spacer.end(), sp, sp + nsp);
+    b->spacer_off.push_back((int64_t)b->spacer.size());
     ++b->n;
+}
+
+void add_record(pcabi_reads *b, const char *name, size_t nn, const char *seq, size_t ns, const char *q, size_t nq,
+                bool raw = false) {
+    add_name(b, name, nn);
+    add_seq(b, seq, ns, raw);
+    add_qual(b, q, nq, ns, raw);
 }
 
 void finish_batch(pcabi_reads *b) { b->codes.resize(b->codes.size() + 16, 4); }
@@ -211,6 +245,12 @@ int pcabi_fastx_open(const char *path, int raw, pcabi_fastx **out) {
     pcabi_fastx *r = new pcabi_fastx();
     r->f = f;
     r->raw = raw != 0;
+    if (FILE *sf = std::fopen(path, "rb")) {
+        std::fseek(sf, 0, SEEK_END);
+        const long sz = std::ftell(sf);
+        std::fclose(sf);
+        if (sz > 0) r->size_hint = (size_t)sz * ((magic[0] == 0x1f && magic[1] == 0x8b) ? 4 : 1);
+    }
     r->buf.resize(4u << 20);
     // type from the first decoded character
     while (r->end == 0 && !r->eof) {
@@ -241,6 +281,13 @@ int64_t pcabi_fastx_next(pcabi_fastx *r, int64_t max_reads, int64_t max_bases, p
     if (!r || !out || max_reads <= 0) return fail(PCABI_E_ARG, "bad arguments");
     pcabi_reads *b = new pcabi_reads();
     b->type = r->type;
+    {
+        // sequence and qualities are about half the decoded bytes each
+        const size_t want = std::min<size_t>(r->size_hint / 2 + 4096, (size_t)std::min<int64_t>(max_bases, 1LL << 40));
+        b->seq.reserve(want);
+        b->codes.reserve(want + 4096);
+        if (r->type == PCABI_FASTQ) b->qual.reserve(want);
+    }
     int64_t bases = 0;
     const char *p;
     size_t n;
@@ -260,22 +307,22 @@ int64_t pcabi_fastx_next(pcabi_fastx *r, int64_t max_reads, int64_t max_bases, p
                 delete b;
                 return fail(PCABI_E_PARSE, "could not be parsed - empty FASTQ name at line " + std::to_string(r->line_no));
             }
-            std::string name(p + 1, n - 1);
+            add_name(b, p + 1, n - 1);
             const char *sp, *qp, *xp;
             size_t sn, qn, xn;
             if (!next_line(r, &sp, &sn)) { delete b; return fail(PCABI_E_PARSE, "truncated FASTQ record"); }
             strip(&sp, &sn);
-            std::string seq(sp, sn);
+            add_seq(b, sp, sn, r->raw);
             if (!next_line(r, &xp, &xn)) { delete b; return fail(PCABI_E_PARSE, "truncated FASTQ record"); }
-            if (!next_line(r, &qp, &qn)) { delete b; return fail(PCABI_E_PARSE, "truncated FASTQ record"); }
-            strip(&qp, &qn);
             std::string spacer;
             if (r->raw) {
                 strip(&xp, &xn);
                 spacer.assign(xp, xn);
             }
-            add_record(b, name.data(), name.size(), seq.data(), seq.size(), qp, qn, r->raw, spacer.data(), spacer.size());
-            bases += (int64_t)seq.size();
+            if (!next_line(r, &qp, &qn)) { delete b; return fail(PCABI_E_PARSE, "truncated FASTQ record"); }
+            strip(&qp, &qn);
+            add_qual(b, qp, qn, sn, r->raw, spacer.data(), spacer.size());
+            bases += (int64_t)sn;
         }
     } else {
         while (b->n < max_reads && bases < max_bases) {

@@ -55,64 +55,82 @@ def _declare(L):
     return L
 
 
-def _arr(ptr, dtype, n):
-    if n == 0 or not ptr:
-        return np.zeros(0, dtype)
-    return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(np.ctypeslib.as_ctypes_type(dtype))),
-                                 shape=(n,)).copy()
-
-
-class ReadBatch(object):
-    """One batch of parsed reads (owned copies of the native buffers).
-
-    names / seq / qual: bytes buffers with int64 offsets [n + 1]; rna: uint8 [n];
-    codes: Dna5 uint8 buffer, code_off int64 [n] (4-aligned), lengths int32 [n] -- the layout
-    engine.SeqPack builds, so (codes, code_off + start, length) are engine windows directly.
-    The native batch stays alive (self._h) for write_reads."""
+class _Owner(object):
+    """Owns a native batch; numpy views into its buffers keep it alive (zero-copy)."""
 
     def __init__(self, handle):
-        L = _declare(lib())
-        v = _View()
-        check(L.pcabi_reads_views(handle, ctypes.byref(v)), 'pcabi_reads_views')
-        n = int(v.n)
-        self._h = handle
-        self.type = int(v.type)
-        self.n = n
-        self.name_off = _arr(v.name_off, np.int64, n + 1)
-        self.seq_off = _arr(v.seq_off, np.int64, n + 1)
-        self.qual_off = _arr(v.qual_off, np.int64, n + 1)
-        self.names = ctypes.string_at(v.names, int(self.name_off[-1])) if n else b''
-        self.seq = ctypes.string_at(v.seq, int(self.seq_off[-1])) if n else b''
-        self.qual = ctypes.string_at(v.qual, int(self.qual_off[-1])) if n else b''
-        self.rna = _arr(v.rna, np.uint8, n)
-        self.spacer_off = _arr(v.spacer_off, np.int64, n + 1)
-        self.spacer = ctypes.string_at(v.spacer, int(self.spacer_off[-1])) if n and self.spacer_off[-1] else b''
-        self.codes = _arr(v.codes, np.uint8, int(v.codes_len))
-        self.code_off = _arr(v.code_off, np.int64, n)
-        self.lengths = _arr(v.len, np.int32, n)
-
-    def __len__(self):
-        return self.n
+        self.h = handle
 
     def __del__(self):
-        h, self._h = getattr(self, '_h', None), None
+        h, self.h = self.h, None
         if h:
             try:
                 _declare(lib()).pcabi_reads_free(h)
             except Exception:
                 pass
 
+
+def _view(owner, ptr, dtype, n):
+    """numpy view of n items at ptr inside owner's batch (no copy)."""
+    dtype = np.dtype(dtype)
+    if n == 0 or not ptr:
+        return np.zeros(0, dtype)
+    raw = (ctypes.c_uint8 * (n * dtype.itemsize)).from_address(ptr)
+    raw._owner = owner                         # the ctypes buffer keeps the batch alive
+    return np.frombuffer(raw, dtype=dtype, count=n)
+
+
+class ReadBatch(object):
+    """One batch of parsed reads, as zero-copy numpy views of the native buffers.
+
+    names / seq / qual: uint8 buffers with int64 offsets [n + 1]; rna: uint8 [n];
+    codes: Dna5 uint8 buffer, code_off int64 [n] (4-aligned), lengths int32 [n] -- the layout
+    engine.SeqPack builds, so (codes, code_off + start, length) are engine windows directly.
+    The native batch lives as long as this object or any of its arrays (write_reads uses it)."""
+
+    def __init__(self, handle):
+        L = _declare(lib())
+        v = _View()
+        self._owner = _Owner(handle)
+        check(L.pcabi_reads_views(handle, ctypes.byref(v)), 'pcabi_reads_views')
+        n = int(v.n)
+        o = self._owner
+        self.type = int(v.type)
+        self.n = n
+        self.name_off = _view(o, v.name_off, np.int64, n + 1)
+        self.seq_off = _view(o, v.seq_off, np.int64, n + 1)
+        self.qual_off = _view(o, v.qual_off, np.int64, n + 1)
+        self.spacer_off = _view(o, v.spacer_off, np.int64, n + 1)
+        self.names = _view(o, v.names, np.uint8, int(self.name_off[-1]) if n else 0)
+        self.seq = _view(o, v.seq, np.uint8, int(self.seq_off[-1]) if n else 0)
+        self.qual = _view(o, v.qual, np.uint8, int(self.qual_off[-1]) if n else 0)
+        self.spacer = _view(o, v.spacer, np.uint8, int(self.spacer_off[-1]) if n else 0)
+        self.rna = _view(o, v.rna, np.uint8, n)
+        self.codes = _view(o, v.codes, np.uint8, int(v.codes_len))
+        self.code_off = _view(o, v.code_off, np.int64, n)
+        self.lengths = _view(o, v.len, np.int32, n)
+
+    @property
+    def _h(self):
+        return self._owner.h
+
+    def __len__(self):
+        return self.n
+
+    def _text(self, buf, off, i):
+        return buf[off[i]:off[i + 1]].tobytes().decode()
+
     def name(self, i):
-        return self.names[self.name_off[i]:self.name_off[i + 1]].decode()
+        return self._text(self.names, self.name_off, i)
 
     def sequence(self, i):
-        return self.seq[self.seq_off[i]:self.seq_off[i + 1]].decode()
+        return self._text(self.seq, self.seq_off, i)
 
     def quals(self, i):
-        return self.qual[self.qual_off[i]:self.qual_off[i + 1]].decode()
+        return self._text(self.qual, self.qual_off, i)
 
     def spacer_line(self, i):
-        return self.spacer[self.spacer_off[i]:self.spacer_off[i + 1]].decode()
+        return self._text(self.spacer, self.spacer_off, i)
 
     def views(self, starts=None, lengths=None):
         """Engine windows (codes, offsets, lengths) of [start, start + length) of every read."""
@@ -260,11 +278,13 @@ def get_albacore_barcode_from_path(albacore_path):
 
 
 def write_reads(batch, path, out_format='fastq', start_trim=None, end_trim=None, middle_cuts=None,
-                min_split_read_size=1000, discard_middle=False, untrimmed=False, select=None, append=False):
+                min_split_read_size=1000, discard_middle=False, untrimmed=False, select=None, append=False,
+                cut_arrays=None):
     """NanoporeRead.get_fasta / get_fastq for every read of a ReadBatch, natively
     (pcabi_reads_write). out_format: 'fasta' | 'fastq' | 'fasta.gz' | 'fastq.gz'.
     middle_cuts: per read a list of (begin, end) ranges of the trimmed sequence (the reference's
-    middle_trim_positions as ranges), or None."""
+    middle_trim_positions as ranges), or None; cut_arrays: the same as (cut_off int64 [n + 1],
+    cuts int64 [2 * n_cuts]) arrays."""
     L = _declare(lib())
     gz = out_format.endswith('.gz')
     fasta = out_format.startswith('fasta')
@@ -272,7 +292,12 @@ def write_reads(batch, path, out_format='fastq', start_trim=None, end_trim=None,
     st = None if start_trim is None else np.ascontiguousarray(start_trim, np.int32)
     et = None if end_trim is None else np.ascontiguousarray(end_trim, np.int32)
     co = cu = None
-    if middle_cuts is not None:
+    if cut_arrays is not None:
+        co = np.ascontiguousarray(cut_arrays[0], np.int64)
+        cu = np.ascontiguousarray(cut_arrays[1], np.int64)
+        if cu.size == 0:
+            cu = np.zeros(2, np.int64)
+    elif middle_cuts is not None:
         co = np.zeros(n + 1, np.int64)
         flat = []
         for i, rg in enumerate(middle_cuts):

@@ -1,0 +1,209 @@
+"""File-to-file trimming on one GPU: the CLI's hot path without per-read Python objects
+(porechop_abi/porechop_abi.py:41-131 after adapter-set discovery).
+
+    ReadBatch (native parse, misc.read_batches)
+      -> H2D of the packed Dna5 codes, start / end window views        (engine layout, no repack)
+      -> k_tile_windows / k_align cross products / k_end_trim           (find_adapters_at_read_ends)
+      -> trims D2H (8 B / read)
+      -> pcabi_middle_scan_dev over the trimmed reads                   (find_adapters_in_read_middles)
+      -> middle cut ranges (NanoporeRead._apply_middle_hit, vectorised)
+      -> the fork's start-and-end filter (porechop_abi.py:36-39)
+      -> native trimmed FASTA / FASTQ writer                             (output_reads, get_fastq)
+
+Decisions are the reference's (same kernels and epilogues the parity tests cover); barcode
+demultiplexing and verbose output stay with the per-read drivers (porechop_abi.py here).
+"""
+import ctypes
+import time
+
+import numpy as np
+
+from . import misc
+from ._lib import check, lib
+from .engine import encode_adapters
+from .porechop_abi import middle_adapter_list
+
+VP = ctypes.c_void_p
+
+
+class FileTrimmer(object):
+    """Device state for trimming batches against one list of matching adapter sets.
+
+    Options follow the reference's arguments (arg_parser.py defaults): end_size 150,
+    end_threshold 75, extra_end_trim 2, min_trim_size 4, middle_threshold 90, extra middle trim
+    10 (good side) / 100 (bad side), min_split_read_size 1000, no_split False, discard_middle
+    False, adapter filter on (the fork's)."""
+
+    def __init__(self, matching_sets, scoring_scheme_vals=(3, -6, -5, -2), end_size=150, end_threshold=75.0,
+                 extra_end_trim=2, min_trim_size=4, middle_threshold=90.0, extra_middle_trim_good_side=10,
+                 extra_middle_trim_bad_side=100, min_split_read_size=1000, no_split=False, discard_middle=False,
+                 filter_reads=True, device=0):
+        self.L = L = lib()
+        check(L.pcabi_dev_set(device), 'pcabi_dev_set')
+        self.sc = tuple(int(x) for x in scoring_scheme_vals[:4])
+        self.E, self.thr, self.extra, self.min_trim = int(end_size), float(end_threshold), int(extra_end_trim), \
+            int(min_trim_size)
+        self.mthr, self.good, self.bad = float(middle_threshold), int(extra_middle_trim_good_side), \
+            int(extra_middle_trim_bad_side)
+        self.min_split, self.no_split, self.discard_middle = int(min_split_read_size), bool(no_split), \
+            bool(discard_middle)
+        self.filter_reads = bool(filter_reads)
+        self.start_adps = [a.start_sequence[1] for a in matching_sets if a.start_sequence]
+        self.end_adps = [a.end_sequence[1] for a in matching_sets if a.end_sequence]
+        mids, start_names, end_names = middle_adapter_list(matching_sets)
+        self.mid_adps = [x[1] for x in mids]
+        self.bad_start = np.array([x[0] in start_names for x in mids], bool)
+        self.bad_end = np.array([x[0] in end_names for x in mids], bool)
+        self.tabs = [self._table(x) for x in (self.start_adps, self.end_adps, self.mid_adps)]
+        self.scan = VP()
+        if self.mid_adps:
+            check(L.pcabi_scan_create(self.tabs[2], ctypes.byref(self.scan)), 'pcabi_scan_create')
+        self.stream = VP()
+        check(L.pcabi_stream_create(ctypes.byref(self.stream)), 'pcabi_stream_create')
+        self.dev = {}
+        self.times = {}
+
+    def _table(self, seqs):
+        if not seqs:
+            return None
+        c, o, l = encode_adapters(seqs)
+        t = VP()
+        check(self.L.pcabi_adapters_create_scored(c.ctypes.data_as(VP), o.ctypes.data_as(VP), l.ctypes.data_as(VP),
+                                                  len(seqs), *self.sc, ctypes.byref(t)), 'pcabi_adapters_create')
+        return t
+
+    def _buf(self, key, nbytes):
+        nbytes = max(int(nbytes), 16)
+        if key not in self.dev or self.dev[key][1] < nbytes:
+            if key in self.dev:
+                self.L.pcabi_dev_free(self.dev[key][0])
+            p = VP()
+            check(self.L.pcabi_dev_malloc(ctypes.byref(p), nbytes), 'pcabi_dev_malloc')
+            self.dev[key] = (p, nbytes)
+        return self.dev[key][0]
+
+    def _h2d(self, key, arr):
+        arr = np.ascontiguousarray(arr)
+        p = self._buf(key, arr.nbytes)
+        if arr.nbytes:
+            check(self.L.pcabi_dev_copy_async(p, arr.ctypes.data_as(VP), arr.nbytes, 0, self.stream), 'h2d')
+        return p
+
+    def _tick(self, key, t):
+        now = time.perf_counter()
+        self.times[key] = self.times.get(key, 0.0) + now - t
+        return now
+
+    def trim(self, batch):
+        """Decisions for one ReadBatch: (start_trim, end_trim, cut_off, cuts, hits, keep)."""
+        L, sc, nb = self.L, self.sc, batch.n
+        t = time.perf_counter()
+        lens = batch.lengths.astype(np.int64)
+        E = self.E
+        s_len = (np.minimum(lens, E) if E >= 0 else np.maximum(lens + E, 0)).astype(np.int32)
+        if E > 0:
+            e_start = np.maximum(lens - E, 0)
+        elif E == 0:
+            e_start = np.zeros_like(lens)
+        else:
+            e_start = np.minimum(-E, lens)
+        e_len = (lens - e_start).astype(np.int32)
+        d_codes = self._h2d('codes', batch.codes)
+        trims = np.zeros((2, nb), np.int32)
+        res = [None, None]
+        n_ad = (len(self.start_adps), len(self.end_adps))
+        for side, (w_off, w_len) in enumerate(((batch.code_off, s_len), (batch.code_off + e_start, e_len))):
+            res[side] = self._buf('res%d' % side, 4 * 8 * max(1, n_ad[side]) * nb)
+            if not n_ad[side] or nb == 0:
+                continue
+            toff = np.zeros((nb + 255) // 256 + 1, np.int64)
+            nd = L.pcabi_tile_layout(w_len.ctypes.data_as(VP), nb, toff.ctypes.data_as(VP))
+            d_off, d_len = self._h2d('off%d' % side, w_off), self._h2d('len%d' % side, w_len)
+            d_toff = self._h2d('toff%d' % side, toff)
+            d_tiles = self._buf('tiles%d' % side, 4 * nd)
+            check(L.pcabi_tile_windows_dev(d_codes, d_off, d_len, nb, d_toff, int(np.diff(toff).max() // 256), d_tiles,
+                                           self.stream), 'tile')
+            check(L.pcabi_align_cross_dev(d_tiles, d_toff, d_len, nb, int(w_len.max()), self.tabs[side], *sc,
+                                          res[side], n_ad[side] * nb, self.stream), 'align')
+        if nb:
+            d_st, d_et = self._buf('st', 4 * nb), self._buf('et', 4 * nb)
+            check(L.pcabi_end_trim_dev(res[0], n_ad[0] * nb, n_ad[0], res[1], n_ad[1] * nb, n_ad[1], nb, E, self.extra,
+                                       self.thr, self.min_trim, d_st, d_et, None, None, self.stream), 'end_trim')
+            check(L.pcabi_dev_copy_async(trims[0].ctypes.data_as(VP), d_st, 4 * nb, 1, self.stream), 'd2h')
+            check(L.pcabi_dev_copy_async(trims[1].ctypes.data_as(VP), d_et, 4 * nb, 1, self.stream), 'd2h')
+            check(L.pcabi_stream_sync(self.stream), 'sync')
+        t = self._tick('end_trim', t)
+        cut_off = np.zeros(nb + 1, np.int64)
+        cuts = np.zeros(0, np.int64)
+        hits = np.zeros((6, 0), np.int32)
+        if self.mid_adps and not self.no_split and nb:
+            # get_seq_with_start_end_adapters_trimmed (nanopore_read.py:66-71): the Python slice
+            # seq[st:len - et] of the reference, as a window of the packed read
+            st, et = trims[0].astype(np.int64), trims[1].astype(np.int64)
+            trimmed = (st > 0) | (et > 0)
+            end = lens - et
+            end = np.where(end < 0, np.maximum(lens + end, 0), end)
+            a = np.minimum(st, lens)
+            t_len = np.where(trimmed, np.maximum(end - a, 0), lens).astype(np.int32)
+            t_off = batch.code_off + np.where(trimmed, a, 0)
+            d_toff, d_tlen = self._h2d('toffm', t_off), self._h2d('tlenm', t_len)
+            cap = max(4096, nb)
+            while True:
+                hits = np.zeros((6, cap), np.int32)
+                nh = L.pcabi_middle_scan_dev(self.scan, d_codes, d_toff, d_tlen, t_len.ctypes.data_as(VP), nb, *sc,
+                                             self.mthr, hits.ctypes.data_as(VP), cap, self.stream)
+                if nh < 0:
+                    check(int(nh), 'pcabi_middle_scan_dev')
+                if nh <= cap:
+                    break
+                cap = int(nh)                 # the scan masked the codes: re-upload and rerun
+                d_codes = self._h2d('codes', batch.codes)
+            hits = hits[:, :int(nh)]
+            # NanoporeRead._apply_middle_hit (nanopore_read.py:236-252)
+            r, ad = hits[0], hits[1]
+            a0 = hits[2] - np.where(self.bad_start[ad], self.bad, self.good)
+            a1 = hits[3] + np.where(self.bad_end[ad], self.bad, self.good)
+            order = np.argsort(r, kind='stable')
+            cut_off[1:] = np.cumsum(np.bincount(r, minlength=nb))
+            cuts = np.stack([a0[order], a1[order]], 1).astype(np.int64).ravel()
+        t = self._tick('middle', t)
+        keep = None
+        if self.filter_reads:
+            # the fork's filter: start AND end alignments (a recorded alignment always trims >= 1)
+            keep = ((trims[0] > 0) & (trims[1] > 0)).astype(np.uint8)
+        return trims[0], trims[1], cut_off, cuts, hits, keep
+
+    def trim_file(self, in_path, out_path, out_format='fastq', max_reads=200000):
+        """Trim a FASTA / FASTQ(.gz) file batch by batch into out_path. Returns read counts."""
+        n_in = n_kept = 0
+        first = True
+        t = time.perf_counter()
+        for b in misc.read_batches(in_path, max_reads=max_reads):
+            t = self._tick('parse', t)
+            st, et, co, cu, _, keep = self.trim(b)
+            t = time.perf_counter()
+            misc.write_reads(b, out_path, out_format, st, et, None, self.min_split, self.discard_middle,
+                             select=keep, append=not first, cut_arrays=(co, cu))
+            first = False
+            n_in += b.n
+            n_kept += int(keep.sum()) if keep is not None else b.n
+            t = self._tick('write', t)
+        if first:   # empty input: still create the output
+            open(out_path, 'wb').close()
+        return {'reads_in': n_in, 'reads_kept': n_kept}
+
+    def close(self):
+        L = self.L
+        for p, _ in self.dev.values():
+            L.pcabi_dev_free(p)
+        self.dev = {}
+        if self.scan:
+            L.pcabi_scan_destroy(self.scan)
+            self.scan = VP()
+        for t in self.tabs:
+            if t:
+                L.pcabi_adapters_destroy(t)
+        self.tabs = []
+        if self.stream:
+            L.pcabi_stream_destroy(self.stream)
+            self.stream = VP()

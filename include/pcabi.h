@@ -265,6 +265,28 @@ int pcabi_barcode_call_host(int device, const int32_t *start_res, int32_t n_sa, 
                             int require_two, int32_t *call, double *scores);
 
 /*
+ * Ab-initio adapter clustering link test (porechop_abi/ab_initio_src/compatibility.cpp,
+ * compatibility.h:58-60, called all-vs-all by consensus.py:72-100): semi-global alignment
+ * (free end gaps, match 2 / mismatch -1 / linear gap -1, SeqAn String<Dna>: anything but
+ * ACGTU is A) of the longer sequence against the shorter, then the reference's flag:
+ * 0 not compatible, 1 compatible (integer identity of the aligned region >= 87.5), 2 compatible
+ * and the shorter lies inside the longer (region more than 3 bases from an end).
+ *   check_compatibility : the drop-in symbol of the reference's compatibility.so (device 0).
+ *   pcabi_compat_host   : n_pairs (pair_i[t], pair_j[t]) of n_seq sequences given as Dna codes
+ *       (0..3) in one buffer (seq_off / seq_len, 16 bytes of padding), flags[n_pairs]; the
+ *       shorter sequence of a pair must be <= pcabi_max_adapter_len() bases. Empty -> 0.
+ */
+int check_compatibility(char *raw_seq1, char *raw_seq2);
+int pcabi_compat_host(int device, const uint8_t *codes, int64_t codes_len, const int64_t *seq_off,
+                      const int32_t *seq_len, int64_t n_seq, const int32_t *pair_i, const int32_t *pair_j,
+                      int64_t n_pairs, int32_t *flags);
+/* consensus.py:72-100 all_vs_all_matrix: mat[n_seq * n_seq] (row-major, -1 on the diagonal,
+ * symmetric). Runs every sequence against every sequence in the tiled cross mode when all are
+ * <= pcabi_max_adapter_len() bases (explicit pairs otherwise). n_seq <= 46340. */
+int pcabi_compat_all_vs_all_host(int device, const uint8_t *codes, int64_t codes_len, const int64_t *seq_off,
+                                 const int32_t *seq_len, int64_t n_seq, int32_t *mat);
+
+/*
  * Sequence files (host code, csrc/pcabi_io.cpp; replaces porechop_abi/misc.py:60-168
  * load_fasta_or_fastq and NanoporeRead's normalisation, nanopore_read.py:31-44, for the batched
  * path, and NanoporeRead.get_fasta / get_fastq, nanopore_read.py:84-156, for output).

@@ -44,16 +44,21 @@ static int dna5(unsigned char c) {
 }
 static const char DNA5_CHARS[5] = {'A', 'C', 'G', 'T', 'N'};
 
-void pcabi_oracle_align(const char *read, int n, const char *adapter, int l,
-                        int ma, int mi, int go, int ge, pcabi_oracle_result *out) {
-    memset(out, 0, sizeof(*out));
-    out->rs = -1;
-    out->re = -1;
-    out->as = -1;
-    out->ae = -1;
+/* SeqAn String<Dna> (the ab-initio compatibility check): A C G T/U, anything else -> A */
+static int dna4(unsigned char c) {
+    int v = dna5(c);
+    return v == 4 ? 0 : v;
+}
+
+/* DP + scout + GapsLeft traceback: the gapped rows SeqAn's Align holds after globalAlignment
+ * with AlignConfig<1,1,1,1>. Returns the row length (0 and score INT_MIN for an empty input);
+ * *rr_out / *ar_out are malloc'd. */
+static int build_rows(const char *read, int n, const char *adapter, int l, int ma, int mi, int go, int ge,
+                      int four, char **rr_out, char **ar_out, int *score_out) {
+    *rr_out = *ar_out = NULL;
     if (n <= 0 || l <= 0) {            /* _isValidDPSettings: empty sequence -> no alignment */
-        out->score = INT_MIN;
-        return;
+        *score_out = INT_MIN;
+        return 0;
     }
     const int affine = (go != ge);
     const int W = n + 1;
@@ -64,8 +69,8 @@ void pcabi_oracle_align(const char *read, int n, const char *adapter, int l,
     unsigned char *T = (unsigned char *)calloc(cells, 1);
     unsigned char *rc = (unsigned char *)malloc((size_t)n);
     unsigned char *ac = (unsigned char *)malloc((size_t)l);
-    for (int j = 0; j < n; ++j) rc[j] = (unsigned char)dna5((unsigned char)read[j]);
-    for (int i = 0; i < l; ++i) ac[i] = (unsigned char)dna5((unsigned char)adapter[i]);
+    for (int j = 0; j < n; ++j) rc[j] = (unsigned char)(four ? dna4((unsigned char)read[j]) : dna5((unsigned char)read[j]));
+    for (int i = 0; i < l; ++i) ac[i] = (unsigned char)(four ? dna4((unsigned char)adapter[i]) : dna5((unsigned char)adapter[i]));
 #define IDX(i, j) ((size_t)(i) * (size_t)W + (size_t)(j))
 
     /* free end gaps: first row and column are RecursionDirectionZero */
@@ -111,7 +116,7 @@ void pcabi_oracle_align(const char *read, int n, const char *adapter, int l,
         if (S[IDX(l, j)] > best) { best = S[IDX(l, j)]; bi = l; bj = j; }
     for (int i = 0; i <= l; ++i)
         if (S[IDX(i, n)] > best) { best = S[IDX(i, n)]; bi = i; bj = n; }
-    out->score = best;
+    *score_out = best;
 
     /* traceback (GapsLeft). path columns are collected in reverse: type 'D','V','H' */
     char *path = (char *)malloc((size_t)(n + l + 2));
@@ -191,6 +196,24 @@ void pcabi_oracle_align(const char *read, int n, const char *adapter, int l,
         for (int k = bj; k < n; ++k) { rr[len] = DNA5_CHARS[rc[k]]; ar[len] = '-'; ++len; }
     }
 
+    free(path);
+    free(S); free(H); free(V); free(T); free(rc); free(ac);
+#undef IDX
+    *rr_out = rr;
+    *ar_out = ar;
+    return len;
+}
+
+void pcabi_oracle_align(const char *read, int n, const char *adapter, int l,
+                        int ma, int mi, int go, int ge, pcabi_oracle_result *out) {
+    memset(out, 0, sizeof(*out));
+    out->rs = -1;
+    out->re = -1;
+    out->as = -1;
+    out->ae = -1;
+    char *rr, *ar;
+    const int len = build_rows(read, n, adapter, l, ma, mi, go, ge, 0, &rr, &ar, &out->score);
+    if (len == 0) return;
     /* ScoredAlignment (porechop_abi/src/alignment.cpp:27-109) */
     int st = -1, en = -1, a0 = -1, a1 = -1;
     { int r = 0, a = 0;
@@ -217,9 +240,47 @@ void pcabi_oracle_align(const char *read, int n, const char *adapter, int l,
         out->l2 = a1 - a0 + 1;
         if (m1 != m2) out->m = -1000000 - m2; /* never happens; flags a broken assumption */
     }
-    free(rr); free(ar); free(path);
-    free(S); free(H); free(V); free(T); free(rc); free(ac);
-#undef IDX
+    free(rr); free(ar);
+}
+
+/* check_compatibility (porechop_abi/ab_initio_src/compatibility.cpp:17-170), literally: the
+ * longer sequence is row 0 (ties: seq1), String<Dna>, Score(2, -1, -1) linear, the aligned
+ * region [st, en] of the gapped rows, distance = mismatching columns on [st, en), integer
+ * identity (mapped - distance) * 100 / mapped >= 87.5, inclusion when row 0's region starts or
+ * ends more than 3 bases inside it. Returns -1 where the reference divides by zero (no
+ * overlap) or has no alignment (an empty sequence). */
+int pcabi_oracle_compat(const char *s1, const char *s2) {
+    const int n1 = (int)strlen(s1), n2 = (int)strlen(s2);
+    const char *a = s1, *b = s2;
+    int na = n1, nb = n2;
+    if (n1 < n2) { a = s2; b = s1; na = n2; nb = n1; }
+    char *rr, *ar;
+    int score;
+    const int len = build_rows(a, na, b, nb, 2, -1, -1, -1, 1, &rr, &ar, &score);
+    if (len == 0) return -1;
+    int st = -1, en = -1;
+    { int r = 0, q = 0;
+      for (int c = 0; c < len; ++c) { if (rr[c] != '-') r = 1; if (ar[c] != '-') q = 1; if (r && q) { st = c; break; } } }
+    { int r = 0, q = 0;
+      for (int c = len - 1; c >= 0; --c) { if (rr[c] != '-') r = 1; if (ar[c] != '-') q = 1; if (r && q) { en = c; break; } } }
+    const int mapped = en - st + 1;
+    int flag = -1;
+    if (st >= 0 && en >= 0 && mapped > 0) {
+        int dist = 0;
+        for (int c = st; c < en; ++c) if (rr[c] != ar[c]) ++dist;
+        int s1_start = 0, s1_end = 0, rb = 0;
+        for (int c = 0; c < len; ++c) {
+            if (c == st) s1_start = rb;
+            if (c == en) s1_end = rb;
+            if (rr[c] != '-') ++rb;
+        }
+        const float identity = (float)((mapped - dist) * 100 / mapped);
+        const int included = s1_start > 3 || (na - s1_end) > 3;
+        flag = identity >= 87.5f ? 1 : 0;
+        if (included && flag == 1) flag = 2;
+    }
+    free(rr); free(ar);
+    return flag;
 }
 
 static int fmt_pid(char *buf, size_t cap, int m, int l) {

@@ -49,6 +49,10 @@ void pcabi_oracle_align_batch(const char *reads, const long long *read_off, cons
                               int match, int mismatch, int gap_open, int gap_extend,
                               int *results);
 
+/* check_compatibility restated (ab-initio clustering link test): 0 / 1 / 2, or -1 where the
+ * reference has no defined result (an empty sequence, or no overlap: division by zero). */
+int pcabi_oracle_compat(const char *s1, const char *s2);
+
 #ifdef __cplusplus
 }
 #endif

@@ -3,6 +3,7 @@
 // per-lane algorithm the HIP kernels execute can be checked exhaustively without a GPU.
 #include "../../custom_porechop_abi_amd/csrc/pcabi_dp.h"
 #include <cstring>
+#include <utility>
 
 static int dna5(unsigned char c) {
     switch (c) { case 'A': case 'a': return 0; case 'C': case 'c': return 1; case 'G': case 'g': return 2;
@@ -172,4 +173,31 @@ extern "C" int pcabi_model_filter(const char *read, int n, const char *a, int La
 
 extern "C" int pcabi_model_filter_threshold(int L, double thr, int ma, int mi, int go, int ge) {
     return pcabi::sf::filter_threshold(L, thr, pcabi::Scoring{ma, mi, go, ge});
+}
+
+// check_compatibility through the device core (generic) + pcabi::compat_flag, the same rule the
+// kernels apply (k_align compat mode): longer sequence = row 0, String<Dna> codes, (2,-1,-1,-1).
+static int dna4(unsigned char c) { const int v = dna5(c); return v == 4 ? 0 : v; }
+
+template <int RPL>
+static int run_compat(const char *a, int na, const char *b, int nb) {
+    const int off = RPL - nb;
+    const pcabi::Scoring sc{2, -1, -1, -1};
+    auto rd = [&](int j) { return dna4((unsigned char)a[j - 1]); };
+    auto ad = [&](int s) { return dna4((unsigned char)b[s - off - 1]); };
+    const pcabi::Result r = pcabi::align_lane_generic<RPL, false>(rd, na, ad, nb, sc);
+    int en_match = 0;
+    if (r.rs >= 0 && r.diag_en && r.l1 > 0) en_match = dna4((unsigned char)a[r.re]) == dna4((unsigned char)b[r.ae]);
+    return pcabi::compat_flag(r, na, en_match);
+}
+
+extern "C" int pcabi_model_compat(const char *s1, const char *s2) {
+    int n1 = (int)std::strlen(s1), n2 = (int)std::strlen(s2);
+    const char *a = s1, *b = s2;
+    if (n1 < n2) { a = s2; b = s1; std::swap(n1, n2); }
+    if (n1 == 0 || n2 == 0) return 0;
+    if (n2 <= 32) return run_compat<32>(a, n1, b, n2);
+    if (n2 <= 64) return run_compat<64>(a, n1, b, n2);
+    if (n2 <= 128) return run_compat<128>(a, n1, b, n2);
+    return -2;
 }

@@ -1,0 +1,69 @@
+"""File-to-file trimming on the GPU (custom_porechop_abi_amd/pipeline.py: native parse -> device
+end trim + middle scan -> fork filter -> native writer) vs the reference's own pipeline on the
+same reads: the G2 golden decisions (the reference's drivers, tools/make_golden_g2.py) applied
+to NanoporeRead and written with get_fastq (checked against the reference's writer in
+tests/test_io.py), for the reference's test files and the seeded synthetic set."""
+import os
+
+import pytest
+
+from tests import golden_lib
+
+G2 = golden_lib.g2()
+
+
+def _matching(case):
+    from custom_porechop_abi_amd import adapters as A, porechop_abi as P
+    by_name = {a.name: a for a in A.fresh_adapters()}
+    base = [by_name[n] for n in case['matching'] if '(full sequence)' not in n]
+    sets = P.add_full_barcode_adapter_sets(base)
+    assert [a.name for a in sets] == case['matching']
+    return sets
+
+
+def _expected(case, records):
+    import json
+    from custom_porechop_abi_amd.nanopore_read import NanoporeRead
+    out = []
+    for (n, s, q), d in zip(records, case['reads']):
+        r = NanoporeRead(n, s, q)
+        assert r.name == d['name']
+        r.start_trim_amount, r.end_trim_amount = int(d['start_trim']), int(d['end_trim'])
+        for a, b in (json.loads(d['middle_trim']) if isinstance(d['middle_trim'], str) else d['middle_trim']):
+            r.middle_trim_positions.update(range(a, b))
+        alns = [d['start_alns'], d['end_alns']]
+        if all(json.loads(x) if isinstance(x, str) else x for x in alns):
+            out.append(r.get_fastq(1000, False))
+    return ''.join(out)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case_name', ['one_adapter_set', 'two_adapter_sets', 'barcodes', 'synthetic_default',
+                                       'synthetic_linear', 'synthetic_endsize'])
+def test_trim_file_matches_reference_pipeline(gpu_lib, case_name, tmp_path):
+    from custom_porechop_abi_amd.pipeline import FileTrimmer
+    case = [c for c in G2['cases'] if c['case'] == case_name][0]
+    opts = case['opts']
+    if case['input'] == 'synthetic_reads':
+        records = [tuple(x) for x in G2['synthetic_reads']]
+        in_path = str(tmp_path / 'in.fastq')
+        with open(in_path, 'w') as f:
+            for n, s, q in records:
+                f.write('@%s\n%s\n+\n%s\n' % (n, s, q))
+    else:
+        records = golden_lib.load_records(case['input'])
+        in_path = os.path.join(golden_lib.GOLDEN, 'data', case['input'] + '.gz')
+        from custom_porechop_abi_amd import misc
+        b = misc.load_batch(in_path)
+        records = [(b.name(i), b.sequence(i), b.quals(i)) for i in range(b.n)]
+    out_path = str(tmp_path / 'out.fastq')
+    ft = FileTrimmer(_matching(case), opts['scoring'], opts['end_size'], opts['end_threshold'], opts['extra_end_trim'],
+                     opts['min_trim_size'], opts['middle_threshold'], 10, 100, 1000)
+    try:
+        counts = ft.trim_file(in_path, out_path, max_reads=7)     # several batches
+    finally:
+        ft.close()
+    assert counts['reads_in'] == len(case['reads'])
+    got = open(out_path).read()
+    exp = _expected(case, records)
+    assert got == exp
