@@ -52,12 +52,14 @@ def parse():
     ap.add_argument('--cpu-sample', type=int, default=12000, help='reads in the CPU-baseline sample (0 = skip)')
     ap.add_argument('--cpu-threads', type=int, default=0, help='0 = min(16, cpus available)')
     ap.add_argument('--check', type=int, default=256, help='reads checked against the oracle after timing')
-    ap.add_argument('--workload', choices=['endtrim', 'middle', 'barcodes', 'e2e', 'compat'], default='endtrim',
+    ap.add_argument('--workload', choices=['endtrim', 'middle', 'barcodes', 'e2e', 'compat', 'kmer'],
+                    default='endtrim',
                     help='endtrim: the headline metric (default); middle: end trim + middle-adapter scan '
                          '(BASELINE.json configs[2]); barcodes: end trim + barcode demultiplexing against '
                          '96 barcode sets (configs[3]); e2e: FASTQ file -> native parse -> end trim + middle '
                          'scan on the GPU -> fork filter -> native trimmed FASTQ output (the CLI path); compat: '
-                         'the ab-initio all-vs-all check_compatibility matrix')
+                         'the ab-initio all-vs-all check_compatibility matrix; kmer: the ab-initio k-mer counter '
+                         '(approx_counter) on 40k sampled read ends')
     ap.add_argument('--compat-seqs', type=int, default=3000, help='sequences of the compat workload')
     ap.add_argument('--barcodes', type=int, default=96, help='barcode sets of the barcodes workload')
     ap.add_argument('--kit', choices=['pcr96', 'native12'], default='pcr96',
@@ -92,6 +94,8 @@ def main():
     args.local_device = local
     if args.workload == 'compat':
         return run_compat(args, rank, world, dist, torch, L, _lib)
+    if args.workload == 'kmer':
+        return run_kmer(args, rank, world, dist, torch, L, _lib, synth)
     if args.workload == 'e2e':
         return run_e2e(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapters)
 
@@ -587,6 +591,84 @@ def run_compat(args, rank, world, dist, torch, L, _lib):
                'data': 'synthetic adapter-like sequences (20-60 bp families of mutated variants)',
                'config': {'workload': 'compat: all %d pairs of %d sequences (consensus.all_vs_all_flags), scoring '
                                       '2/-1/-1 linear, flags on the device, host buffers in / out' % (n_pairs, n),
+                          'parallelism': 'dp%d' % world},
+               'cpu_baseline': cpu, 'gpu_vs_cpu': round(value / cpu['value'], 1) if cpu else None,
+               'parity_spot_check': checked}
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def run_kmer(args, rank, world, dist, torch, L, _lib, synth):
+    """The ab-initio k-mer counter (approx_counter.cpp, run by abinitio.py:392-440) with the
+    reference's config (ab_initio.config: k 16, sl 100, sn 40000, lim 500, lc 1.0) on a
+    synthetic FASTA of 40k reads: one step = one run of the program minus the file parse (the
+    reads are already loaded): both read ends sampled, exact counts on the GPU (k_kmer_keys,
+    radix sort, RLE), the 500 most frequent, approximate counts at <= 2 errors on the GPU
+    (k_kmer_approx: 500 k-mers x 40k sequences of ~100 bp), ordering and export.
+    cpu_baseline: the reference program itself (oracle/_ref/approx_counter, OpenMP on the host
+    cores) on the same file, its wall time minus nothing (it parses the file too)."""
+    import subprocess
+    import tempfile
+    from custom_porechop_abi_amd import approx_counter as AC, misc
+    n = 40000
+    tmp = tempfile.mkdtemp(prefix='pcabi_kmer_')
+    path = os.path.join(tmp, 'reads.fasta')
+    reads = synth.make_reads(n, 1500, seed=31 + rank)
+    letters = np.frombuffer(b'ACGTN', np.uint8)
+    with open(path, 'wb') as f:
+        for k, r in enumerate(reads):
+            f.write(b'>r%d\n' % k + letters[r].tobytes() + b'\n')
+    batch = misc.load_batch(path)
+    K, SL, LIM = 16, 100, 500
+    lct = AC.adjust_threshold(1.0, 16, K)
+
+    def step():
+        out = []
+        for bottom in (False, True):
+            smp = AC.sample_sequences(batch, n, SL, bottom, seed=0)
+            km, cn = AC.count_kmers(smp, K, lct, (), device=args.local_device)
+            tk, tc = AC.most_frequent(km, cn, LIM, K)
+            err = AC.error_count(smp, tk, K, device=args.local_device)
+            out.append(AC.most_frequent(tk, err, LIM, K))
+        return out
+
+    for _ in range(args.warmup):
+        step()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    elapsed = time.perf_counter() - t0
+    cpu = None
+    ref = os.path.join(ROOT, 'oracle', '_ref', 'approx_counter')
+    checked = None
+    if rank == 0 and args.cpu_sample > 0 and os.path.isfile(ref):
+        nthr = args.cpu_threads or max(1, min(16, len(os.sched_getaffinity(0))))
+        t1 = time.perf_counter()
+        subprocess.run([ref, path, '-o', os.path.join(tmp, 'ref'), '-k', str(K), '-sl', str(SL), '-sn', str(n),
+                        '-lim', str(LIM), '-nt', str(nthr), '-v', '0'], check=True, stdout=subprocess.DEVNULL,
+                       stderr=subprocess.DEVNULL)
+        dt = time.perf_counter() - t1
+        cpu = {'value': round(1.0 / dt, 4), 'unit': 'runs/s', 'cores': nthr, 'kind': 'reference',
+               'sample': 'one full run of the reference approx_counter (file parse included) on the same %d-read '
+                         'file, %.2f s' % (n, dt)}
+        # every read is sampled (sn = n), so the reference's output is deterministic: compare
+        got = {}
+        for which, (tk, tc) in zip(('start', 'end'), res):
+            got[which] = ''.join('%s\t%d\n' % (AC.kmer_to_str(v, K), c) for v, c in zip(tk.tolist(), tc.tolist()))
+        same = all(open(os.path.join(tmp, 'ref_0.' + w)).read() == got[w] for w in ('start', 'end'))
+        checked = {'identical_to_reference_outputs': same}
+    shutil_rm = __import__('shutil').rmtree
+    shutil_rm(tmp, ignore_errors=True)
+    if rank == 0:
+        value = world * args.steps / elapsed
+        out = {'metric': 'approx_counter runs/sec (ab-initio k-mer counts, 40k reads, k 16, both ends)',
+               'value': round(value, 3), 'unit': 'runs/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+               'ms_per_step': round(1e3 * elapsed / args.steps, 2), 'higher_is_better': True, 'scaling': 'weak',
+               'vs_baseline': None, 'dtype': 'int32 / uint64',
+               'data': 'synthetic reads (SURVEY.md §8d recipe, mean 1.5 kb)',
+               'config': {'workload': 'kmer: sample 40000 read starts and ends (100 bp), exact 16-mer counts, top 500, '
+                                      'approximate counts at <= 2 edits, ordering (reference ab_initio.config)',
                           'parallelism': 'dp%d' % world},
                'cpu_baseline': cpu, 'gpu_vs_cpu': round(value / cpu['value'], 1) if cpu else None,
                'parity_spot_check': checked}

@@ -287,6 +287,27 @@ int pcabi_compat_all_vs_all_host(int device, const uint8_t *codes, int64_t codes
                                  const int32_t *seq_len, int64_t n_seq, int32_t *mat);
 
 /*
+ * Ab-initio k-mer counts (porechop_abi/ab_initio_src/approx_counter.cpp, csrc/pcabi_kmer.hip).
+ * Sequences: Dna5 codes (0..4) in one buffer, seq_off / seq_len.
+ *   pcabi_kmer_count_host : count_kmers (:487-519): every k-mer (2 <= k <= 32, 2-bit value,
+ *       first base in the top bits) without N, not low-complexity (dimer score >= lc_threshold,
+ *       :214-234) and not in forbidden_sorted (ascending); writes (k-mer, count) ascending by
+ *       k-mer, returns the number of distinct k-mers (if > cap nothing is written: call again
+ *       with cap >= the return value) or a negative PCABI_E_*.
+ *   pcabi_kmer_approx_host : errorCount (:531-601): counts[q] = sum over sequences of
+ *       3 - d for the best substring edit distance d <= 2 of kmers[q] (SeqAn's search at <= 2
+ *       errors reports a sequence once at every level from d to 2). Sequences start at 4-aligned
+ *       offsets of a buffer whose length is a multiple of 4 (N padding); n_kmers <= 65535 * 64.
+ */
+int64_t pcabi_kmer_count_host(int device, const uint8_t *codes, int64_t codes_len, const int64_t *seq_off,
+                              const int32_t *seq_len, int64_t n_seq, int k, float lc_threshold,
+                              const uint64_t *forbidden_sorted, int64_t n_forbidden, uint64_t *kmers,
+                              uint32_t *counts, int64_t cap);
+int pcabi_kmer_approx_host(int device, const uint8_t *codes, int64_t codes_len, const int64_t *seq_off,
+                           const int32_t *seq_len, int64_t n_seq, int k, const uint64_t *kmers, int64_t n_kmers,
+                           uint64_t *counts);
+
+/*
  * Sequence files (host code, csrc/pcabi_io.cpp; replaces porechop_abi/misc.py:60-168
  * load_fasta_or_fastq and NanoporeRead's normalisation, nanopore_read.py:31-44, for the batched
  * path, and NanoporeRead.get_fasta / get_fastq, nanopore_read.py:84-156, for output).
