@@ -23,9 +23,15 @@
 // [begin, end) ranges of the trimmed sequence, parts shorter than min_split_read_size dropped,
 // names numbered like add_number_to_read_name, :503-509), 70-column FASTA lines, T -> U for RNA
 // reads, optional gzip.
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <zlib.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <thread>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -62,7 +68,11 @@ const bool g_dna5_init = [] {
 struct pcabi_fastx {
     gzFile f = nullptr;
     int type = -1;                 // PCABI_FASTA / PCABI_FASTQ
-    std::vector<char> buf;
+    std::vector<char> buf;         // gzip: decoded bytes [0, end)
+    const char *base = nullptr;    // buf.data(), or the mapping of a plain file
+    void *map = nullptr;           // plain files are memory-mapped whole
+    size_t map_len = 0;
+    size_t pin = (size_t)-1;       // refills keep the bytes from here on (a batch's records)
     size_t pos = 0, end = 0;
     bool eof = false;
     int64_t line_no = 0;
@@ -73,19 +83,36 @@ struct pcabi_fastx {
     std::string fa_name, fa_seq;
 };
 
+// vector whose resize() leaves new elements uninitialised (the batch buffers are written once,
+// in parallel; zero-filling gigabytes first would cost as much as the parse)
+template <typename T>
+struct NoInit : std::allocator<T> {
+    template <typename U>
+    struct rebind { using other = NoInit<U>; };
+    NoInit() = default;
+    template <typename U>
+    NoInit(const NoInit<U> &) {}
+    template <typename U>
+    void construct(U *p) noexcept { ::new ((void *)p) U; }
+    template <typename U, typename... A>
+    void construct(U *p, A &&...a) { ::new ((void *)p) U(std::forward<A>(a)...); }
+};
+template <typename T>
+using RawVec = std::vector<T, NoInit<T>>;
+
 struct pcabi_reads {
     int type = -1;
     int64_t n = 0;
-    std::vector<char> names;                 // full headers (after '@' / '>'), back to back
+    RawVec<char> names;                      // full headers (after '@' / '>'), back to back
     std::vector<int64_t> name_off{0};
-    std::vector<char> seq;                   // upper-cased, U->T for RNA reads
+    RawVec<char> seq;                        // upper-cased, U->T for RNA reads
     std::vector<int64_t> seq_off{0};
-    std::vector<char> qual;                  // padded with '+' to the sequence length
+    RawVec<char> qual;                       // padded with '+' to the sequence length
     std::vector<int64_t> qual_off{0};
     std::vector<uint8_t> rna;
-    std::vector<char> spacer;                // FASTQ '+' lines (stripped)
+    RawVec<char> spacer;                     // FASTQ '+' lines (stripped)
     std::vector<int64_t> spacer_off{0};
-    std::vector<uint8_t> codes;              // Dna5, 4-aligned starts, 16 B tail padding (N)
+    RawVec<uint8_t> codes;                   // Dna5, 4-aligned starts, 16 B tail padding (N)
     std::vector<int64_t> code_off;
     std::vector<int32_t> len;
 };
@@ -97,7 +124,7 @@ namespace {
 // line earlier).
 bool next_line(pcabi_fastx *r, const char **p, size_t *n) {
     for (;;) {
-        const char *base = r->buf.data();
+        const char *base = r->base;
         const char *s0 = base + r->pos, *e0 = base + r->end;
         const char *nl = (const char *)std::memchr(s0, '\n', (size_t)(e0 - s0));
         const char *lim = nl ? nl : e0;
@@ -126,14 +153,16 @@ bool next_line(pcabi_fastx *r, const char **p, size_t *n) {
             }
             return false;
         }
-        // refill: keep the partial line, grow if it fills the buffer
-        const size_t keep = r->end - r->pos;
-        if (r->pos > 0) {
-            std::memmove(r->buf.data(), r->buf.data() + r->pos, keep);
-            r->pos = 0;
-            r->end = keep;
+        // refill: keep the partial line (and a pinned batch), grow if it fills the buffer
+        const size_t from = std::min(r->pos, r->pin);
+        if (from > 0) {
+            std::memmove(r->buf.data(), r->buf.data() + from, r->end - from);
+            r->pos -= from;
+            r->end -= from;
+            if (r->pin != (size_t)-1) r->pin -= from;
         }
         if (r->buf.size() - r->end < (1u << 20)) r->buf.resize(std::max<size_t>(r->buf.size() * 2, 4u << 20));
+        r->base = r->buf.data();
         const int got = gzread(r->f, r->buf.data() + r->end, (unsigned)std::min<size_t>(r->buf.size() - r->end, 1u << 30));
         if (got < 0) {
             int e = 0;
@@ -223,6 +252,93 @@ void add_record(pcabi_reads *b, const char *name, size_t nn, const char *seq, si
 
 void finish_batch(pcabi_reads *b) { b->codes.resize(b->codes.size() + 16, 4); }
 
+// A FASTQ record as spans of the batch's text (offsets from the batch start).
+struct Span {
+    size_t no, nn, so, sn, xo, xn, qo, qn;
+};
+
+int io_threads() {
+    if (const char *e = std::getenv("PCABI_IO_THREADS")) {
+        const int t = std::atoi(e);
+        if (t > 0) return std::min(t, 256);
+    }
+    const unsigned hw = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(hw ? hw : 1u, 16u));
+}
+
+// The records of one FASTQ batch, normalised into b in parallel: offsets first (prefix sums),
+// then every thread fills a contiguous range of records (names, sequence + Dna5 codes + rna
+// flag, qualities + padding, spacer lines).
+void fill_fastq(pcabi_reads *b, const char *T, const std::vector<Span> &rec, bool raw) {
+    const size_t n = rec.size();
+    const size_t n0 = (size_t)b->n;
+    b->name_off.resize(n0 + n + 1);
+    b->seq_off.resize(n0 + n + 1);
+    b->qual_off.resize(n0 + n + 1);
+    b->spacer_off.resize(n0 + n + 1);
+    b->code_off.resize(n0 + n);
+    b->len.resize(n0 + n);
+    b->rna.resize(n0 + n);
+    int64_t code_end = (int64_t)b->codes.size();
+    for (size_t i = 0; i < n; ++i) {
+        const Span &r = rec[i];
+        b->name_off[n0 + i + 1] = b->name_off[n0 + i] + (int64_t)r.nn;
+        b->seq_off[n0 + i + 1] = b->seq_off[n0 + i] + (int64_t)r.sn;
+        b->qual_off[n0 + i + 1] = b->qual_off[n0 + i] + (int64_t)(raw ? r.qn : std::max(r.qn, r.sn));
+        b->spacer_off[n0 + i + 1] = b->spacer_off[n0 + i] + (int64_t)r.xn;
+        b->code_off[n0 + i] = code_end;
+        b->len[n0 + i] = (int32_t)r.sn;
+        code_end += (int64_t)((r.sn + 3) & ~(size_t)3);
+    }
+    b->names.resize((size_t)b->name_off[n0 + n]);
+    b->seq.resize((size_t)b->seq_off[n0 + n]);
+    b->qual.resize((size_t)b->qual_off[n0 + n]);
+    b->spacer.resize((size_t)b->spacer_off[n0 + n]);
+    b->codes.resize((size_t)code_end);
+    auto work = [&](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; ++i) {
+            const Span &r = rec[i];
+            const size_t k = n0 + i;
+            std::memcpy(b->names.data() + b->name_off[k], T + r.no, r.nn);
+            std::memcpy(b->spacer.data() + b->spacer_off[k], T + r.xo, r.xn);
+            char *d = b->seq.data() + b->seq_off[k];
+            uint8_t *c = b->codes.data() + b->code_off[k];
+            const unsigned char *sq = (const unsigned char *)T + r.so;
+            int64_t nu = 0, nt = 0;
+            if (raw) {
+                std::memcpy(d, sq, r.sn);
+                for (size_t j = 0; j < r.sn; ++j) c[j] = g_dna5[sq[j]];
+            } else {
+                for (size_t j = 0; j < r.sn; ++j) {
+                    const uint8_t u = g_upper[sq[j]];
+                    nu += (u == 'U');
+                    nt += (u == 'T');
+                    d[j] = (char)u;
+                    c[j] = g_dna5[u];
+                }
+            }
+            for (size_t j = r.sn; j < ((r.sn + 3) & ~(size_t)3); ++j) c[j] = 4;
+            const bool rna = !raw && nu > nt;
+            if (rna)
+                for (size_t j = 0; j < r.sn; ++j)
+                    if (d[j] == 'U') d[j] = 'T';
+            b->rna[k] = rna ? 1 : 0;
+            char *q = b->qual.data() + b->qual_off[k];
+            std::memcpy(q, T + r.qo, r.qn);
+            if (!raw && r.qn < r.sn) std::memset(q + r.qn, '+', r.sn - r.qn);
+        }
+    };
+    const int nt = (int)std::min<size_t>((size_t)io_threads(), std::max<size_t>(1, n / 256));
+    if (nt <= 1) {
+        work(0, n);
+    } else {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nt; ++t) th.emplace_back(work, n * t / nt, n * (t + 1) / nt);
+        for (auto &x : th) x.join();
+    }
+    b->n = (int64_t)(n0 + n);
+}
+
 }  // namespace
 
 extern "C" {
@@ -239,26 +355,52 @@ int pcabi_fastx_open(const char *path, int raw, pcabi_fastx **out) {
         return fail(PCABI_E_ARG, "cannot use bzip2 format - use gzip instead");
     if (nm >= 4 && magic[0] == 0x50 && magic[1] == 0x4b && magic[2] == 0x03 && magic[3] == 0x04)
         return fail(PCABI_E_ARG, "cannot use zip format - use gzip instead");
-    gzFile f = gzopen(path, "rb");
-    if (!f) return fail(PCABI_E_ARG, std::string("could not open ") + path);
-    gzbuffer(f, 1u << 20);
+    const bool gz = nm >= 2 && magic[0] == 0x1f && magic[1] == 0x8b;
     pcabi_fastx *r = new pcabi_fastx();
-    r->f = f;
     r->raw = raw != 0;
+    if (!gz) {
+        // plain text: map the file, lines are read in place (no copies, no refills)
+        const int fd = ::open(path, O_RDONLY);
+        struct stat st;
+        if (fd >= 0 && fstat(fd, &st) == 0 && st.st_size > 0) {
+            void *m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
+            if (m != MAP_FAILED) {
+                madvise(m, (size_t)st.st_size, MADV_SEQUENTIAL);
+                r->map = m;
+                r->map_len = (size_t)st.st_size;
+                r->base = (const char *)m;
+                r->end = r->map_len;
+                r->eof = true;
+            }
+        }
+        if (fd >= 0) ::close(fd);
+    }
+    if (!r->map) {
+        gzFile f = gzopen(path, "rb");
+        if (!f) {
+            delete r;
+            return fail(PCABI_E_ARG, std::string("could not open ") + path);
+        }
+        gzbuffer(f, 1u << 20);
+        r->f = f;
+    }
     if (FILE *sf = std::fopen(path, "rb")) {
         std::fseek(sf, 0, SEEK_END);
         const long sz = std::ftell(sf);
         std::fclose(sf);
         if (sz > 0) r->size_hint = (size_t)sz * ((magic[0] == 0x1f && magic[1] == 0x8b) ? 4 : 1);
     }
-    r->buf.resize(4u << 20);
-    // type from the first decoded character
-    while (r->end == 0 && !r->eof) {
-        const int got = gzread(f, r->buf.data(), (unsigned)r->buf.size());
-        if (got <= 0) r->eof = true;
-        else r->end = (size_t)got;
+    if (!r->map) {
+        r->buf.resize(4u << 20);
+        r->base = r->buf.data();
+        // type from the first decoded character
+        while (r->end == 0 && !r->eof) {
+            const int got = gzread(r->f, r->buf.data(), (unsigned)r->buf.size());
+            if (got <= 0) r->eof = true;
+            else r->end = (size_t)got;
+        }
     }
-    const char c0 = r->end ? r->buf[0] : 0;
+    const char c0 = r->end ? r->base[0] : 0;
     if (c0 == '>') r->type = PCABI_FASTA;
     else if (c0 == '@') r->type = PCABI_FASTQ;
     else {
@@ -274,6 +416,7 @@ int pcabi_fastx_type(const pcabi_fastx *r) { return r ? r->type : -1; }
 void pcabi_fastx_close(pcabi_fastx *r) {
     if (!r) return;
     if (r->f) gzclose(r->f);
+    if (r->map) munmap(r->map, r->map_len);
     delete r;
 }
 
@@ -292,38 +435,42 @@ int64_t pcabi_fastx_next(pcabi_fastx *r, int64_t max_reads, int64_t max_bases, p
     const char *p;
     size_t n;
     if (r->type == PCABI_FASTQ) {
-        while (b->n < max_reads && bases < max_bases) {
+        std::vector<Span> rec;
+        r->pin = r->pos;                 // the batch's bytes survive refills (shifted with the pin)
+        auto rel = [&](const char *q) { return (size_t)(q - r->base) - r->pin; };
+        while ((int64_t)rec.size() < max_reads && bases < max_bases) {
             if (!next_line(r, &p, &n)) break;
             strip(&p, &n);
             if (n == 0 || n == 1) {   // full_name.split()[0] fails in the reference (IndexError)
                 delete b;
+                r->pin = (size_t)-1;
                 return fail(PCABI_E_PARSE, "could not be parsed - is it formatted correctly? (empty FASTQ header at line " +
                                                std::to_string(r->line_no) + ")");
             }
-            // the name must hold a non-space character after the leading one
-            bool tok = false;
-            for (size_t i = 1; i < n && !tok; ++i) tok = !py_space((unsigned char)p[i]);
-            if (!tok) {
-                delete b;
-                return fail(PCABI_E_PARSE, "could not be parsed - empty FASTQ name at line " + std::to_string(r->line_no));
-            }
-            add_name(b, p + 1, n - 1);
-            const char *sp, *qp, *xp;
-            size_t sn, qn, xn;
-            if (!next_line(r, &sp, &sn)) { delete b; return fail(PCABI_E_PARSE, "truncated FASTQ record"); }
-            strip(&sp, &sn);
-            add_seq(b, sp, sn, r->raw);
-            if (!next_line(r, &xp, &xn)) { delete b; return fail(PCABI_E_PARSE, "truncated FASTQ record"); }
-            std::string spacer;
+            Span sp{};
+            sp.no = rel(p + 1);
+            sp.nn = n - 1;
+            const char *q;
+            size_t qn;
+            if (!next_line(r, &q, &qn)) { delete b; r->pin = (size_t)-1; return fail(PCABI_E_PARSE, "truncated FASTQ record"); }
+            strip(&q, &qn);
+            sp.so = rel(q);
+            sp.sn = qn;
+            if (!next_line(r, &q, &qn)) { delete b; r->pin = (size_t)-1; return fail(PCABI_E_PARSE, "truncated FASTQ record"); }
             if (r->raw) {
-                strip(&xp, &xn);
-                spacer.assign(xp, xn);
+                strip(&q, &qn);
+                sp.xo = rel(q);
+                sp.xn = qn;
             }
-            if (!next_line(r, &qp, &qn)) { delete b; return fail(PCABI_E_PARSE, "truncated FASTQ record"); }
-            strip(&qp, &qn);
-            add_qual(b, qp, qn, sn, r->raw, spacer.data(), spacer.size());
-            bases += (int64_t)sn;
+            if (!next_line(r, &q, &qn)) { delete b; r->pin = (size_t)-1; return fail(PCABI_E_PARSE, "truncated FASTQ record"); }
+            strip(&q, &qn);
+            sp.qo = rel(q);
+            sp.qn = qn;
+            rec.push_back(sp);
+            bases += (int64_t)sp.sn;
         }
+        fill_fastq(b, r->base + r->pin, rec, r->raw);
+        r->pin = (size_t)-1;
     } else {
         while (b->n < max_reads && bases < max_bases) {
             if (!next_line(r, &p, &n)) {
@@ -488,10 +635,8 @@ extern "C" int pcabi_reads_write(const pcabi_reads *b, const char *path, int app
         o.fp = std::strcmp(path, "-") == 0 ? stdout : std::fopen(path, append ? "ab" : "wb");
         if (!o.fp) return fail(PCABI_E_ARG, std::string("could not write ") + path);
     }
-    std::vector<std::pair<int64_t, int64_t>> rg;
-    std::string ps, pq;
-    for (int64_t i = 0; i < b->n; ++i) {
-        if (select && !select[i]) continue;
+    auto format = [&](int64_t i, Sink &o, std::vector<std::pair<int64_t, int64_t>> &rg) {
+        if (select && !select[i]) return;
         const char *name = b->names.data() + b->name_off[i];
         const size_t nn = (size_t)(b->name_off[i + 1] - b->name_off[i]);
         const char *seq = b->seq.data() + b->seq_off[i];
@@ -511,11 +656,11 @@ extern "C" int pcabi_reads_write(const pcabi_reads *b, const char *path, int app
             for (int64_t k = cut_off[i]; k < cut_off[i + 1] && !split; ++k) split = cuts[2 * k + 1] > cuts[2 * k];
         if (!split) {
             if (untrimmed) { sa = 0; sb = ns; qa = 0; qb = nq; }
-            if (sb == sa) continue;   // no empty sequences
+            if (sb == sa) return;   // no empty sequences
             put_record(o, fasta != 0, std::string(name, nn), seq + sa, (size_t)(sb - sa), qual + qa, (size_t)(qb - qa), rna);
-            continue;
+            return;
         }
-        if (discard_middle) continue;
+        if (discard_middle) return;
         // split parts (get_split_read_parts, nanopore_read.py:84-104): positions of the trimmed
         // sequence inside any cut range are dropped
         rg.clear();
@@ -547,7 +692,11 @@ extern "C" int pcabi_reads_write(const pcabi_reads *b, const char *path, int app
             }
         }
         emit(run, tl);
-    }
+    };
+    // formatting is cheap next to the write itself (measured: parallel formatting into chunk
+    // buffers was slower than this single pass), so records go straight to the sink
+    std::vector<std::pair<int64_t, int64_t>> rg;
+    for (int64_t i = 0; i < b->n; ++i) format(i, o, rg);
     o.flush();
     const bool ok = o.ok;
     if (o.gz) gzclose(o.gz);

@@ -112,3 +112,43 @@ def test_parse_errors(tmp_path):
     bz.write_bytes(b'BZh91AY&SY')
     with pytest.raises(SystemExit):
         misc.load_fasta_or_fastq(str(bz))
+
+
+def test_large_gzip_streaming_and_threads(tmp_path, monkeypatch):
+    """Batches that outgrow the 4 MB decode buffer (pinned refills), plain (memory-mapped) and
+    gzip input, one and several parse threads: all equal the reference's rules restated."""
+    import random
+    from custom_porechop_abi_amd import misc
+    rng = random.Random(3)
+    recs = []
+    for k in range(3000):
+        n = rng.randint(0, 6000)
+        s = ''.join(rng.choice('ACGTacgtNU') for _ in range(n))
+        q = ''.join(rng.choice('!#5?I') for _ in range(max(0, n - rng.randint(0, 3))))
+        recs.append(('r%d x=%d' % (k, k), s, q))
+    text = ''.join('@%s\n%s\n+\n%s\n' % r for r in recs)
+    plain = tmp_path / 'big.fastq'
+    plain.write_text(text.replace('\n', '\r\n') if False else text)
+    gz = tmp_path / 'big.fastq.gz'
+    with gzip.open(gz, 'wt') as f:
+        f.write(text)
+
+    def expect():
+        out = []
+        for name, s, q in recs:
+            u = s.upper()
+            rna = u.count('U') > u.count('T')
+            u = u.replace('U', 'T') if rna else u
+            out.append([name, u, q + '+' * (len(s) - len(q)), rna])
+        return out
+
+    exp = expect()
+    for threads in ('1', '7'):
+        monkeypatch.setenv('PCABI_IO_THREADS', threads)
+        for path in (str(plain), str(gz)):
+            got = []
+            for b in misc.read_batches(path, max_reads=700, max_bases=2_000_000):
+                got += [[b.name(i), b.sequence(i), b.quals(i), bool(b.rna[i])] for i in range(b.n)]
+            assert got == exp, (threads, path)
+            b = misc.load_batch(path)
+            assert b.n == len(exp) and b.sequence(len(exp) - 1) == exp[-1][1]
