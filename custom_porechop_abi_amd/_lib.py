@@ -82,6 +82,7 @@ def lib():
                                   c_i64),
         'pcabi_middle_scan_host': ([c_int, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_p, ctypes.c_int32, c_int, c_int,
                                     c_int, c_int, c_d, c_p, c_i64], c_i64),
+        'pcabi_middle_seed_runs': ([], c_i64),
         'pcabi_barcode_call_dev': ([c_p, c_i64, c_p, c_p, ctypes.c_int32, c_p, c_i64, c_p, c_p, ctypes.c_int32,
                                     c_i64, c_d, c_d, c_int, c_p, c_p, c_p], c_int),
         'pcabi_barcode_call_host': ([c_int, c_p, ctypes.c_int32, c_p, c_p, ctypes.c_int32, c_p, ctypes.c_int32, c_p,
@@ -107,7 +108,8 @@ def exported_symbols():
             'pcabi_event_elapsed_ms', 'pcabi_adapters_create', 'pcabi_adapters_create_scored', 'pcabi_adapters_destroy',
             'pcabi_tile_layout', 'pcabi_tile_windows_dev', 'pcabi_align_cross_dev', 'pcabi_end_trim_dev',
             'pcabi_best_full_identity_dev', 'pcabi_first_hits_host', 'pcabi_first_hit_dev', 'pcabi_scan_create',
-            'pcabi_scan_destroy', 'pcabi_middle_scan_dev', 'pcabi_middle_scan_host', 'pcabi_barcode_call_dev',
+            'pcabi_scan_destroy', 'pcabi_middle_scan_dev', 'pcabi_middle_scan_host', 'pcabi_middle_seed_runs',
+            'pcabi_barcode_call_dev',
             'pcabi_barcode_call_host', 'pcabi_fastx_open', 'pcabi_fastx_type', 'pcabi_fastx_next',
             'pcabi_fastx_close', 'pcabi_fastx_load', 'pcabi_reads_count', 'pcabi_reads_type', 'pcabi_reads_views',
             'pcabi_reads_free', 'pcabi_reads_write', 'check_compatibility', 'pcabi_compat_host',

@@ -38,6 +38,7 @@
 #endif
 
 #include <stdint.h>
+#include <algorithm>
 
 #ifdef __HIPCC__
 #define PCABI_HD __host__ __device__ __forceinline__
@@ -715,8 +716,9 @@ struct LanePacked {
 
     // tab: substitution-key table of this lane's read code, tab(s) = key increment of the
     // diagonal step into slot s (match / mismatch / padding), see pk::fill_sub_table.
-    template <typename TabRow, bool LAST>
-    PCABI_HD void column(const TabRow &tab, const int j, const int L, const int off) {
+    // GATE (chunked reads): only owned columns may become the row-L best (owned per column).
+    template <typename TabRow, bool LAST, bool GATE = false>
+    PCABI_HD void column(const TabRow &tab, const int j, const int L, const int off, const bool owned = true) {
         int32_t gup = Y::start(j + off) + k_go;   // G(0, j): S(0, j) = score 0, tb 0
         int32_t vup = neg2;                        // V(0, j) = NEG, tb 2
         int slt_up = LT_NONE, vt_up = 0, vp_up = 0;
@@ -802,7 +804,7 @@ struct LanePacked {
 #endif
         }
         if (!LAST) {
-            column_tail(lv, lh, ls, j);
+            column_tail<GATE>(lv, lh, ls, j, owned);
             return;
         }
         // ---- row L (last column) ----
@@ -842,7 +844,8 @@ struct LanePacked {
     // corrected state is ONE max3 over re-tagged keys -- V (tag 3) beats H (tag 2) beats S
     // (tag 0) on equal scores, and a higher score always wins -- so the correction costs no
     // compares. Linear gaps: no correction, the S key's own tb (3 D, 2 V, 1 H) is the type.
-    PCABI_HD void column_tail(int32_t lv, int32_t lh, int32_t ls, int j) {
+    template <bool GATE = false>
+    PCABI_HD void column_tail(int32_t lv, int32_t lh, int32_t ls, int j, bool owned = true) {
         int32_t corr;
         if (AFFINE) corr = max3i(lv | Y::TB3, (lh & ~Y::TBM) | Y::TB2, ls & ~Y::TBM);
         else corr = ls;
@@ -851,7 +854,8 @@ struct LanePacked {
         const int32_t tsp = ls_prev & Y::TBM;
         const bool hcont = (AFFINE && (lh & Y::TB1) != 0) || tsp == Y::TB1;
         const int hph = hcont ? hph_last + 2 : 2 + (tsp == Y::TB3 ? 1 : 0);
-        const bool upd = corr > (bkey | ((1 << Y::SC_SH) - 1));   // score(corr) > score(bkey)
+        bool upd = corr > (bkey | ((1 << Y::SC_SH) - 1));   // score(corr) > score(bkey)
+        if (GATE) upd = upd && owned;
         bkey = upd ? corr : bkey;
         bj = upd ? j : bj;
         bhph = upd ? hph : bhph;
@@ -897,8 +901,13 @@ PCABI_HD int32_t sub_key(int s, int c, const AdpFn &adp, int off, const Scoring 
 }
 }  // namespace pk
 
-template <int RPL, bool AFFINE, typename ReadFn, typename TabFn>
-PCABI_HD Result align_lane_packed(ReadFn &rd, int n, const TabFn &tabfn, int L, const Scoring sc) {
+// CHUNK: the window is one chunk of a longer read (middle-scan candidates): only
+// columns [own_lo, own_hi) may hold the reported end cell, and own_hi < 0 marks the read's last
+// chunk (its last column is the read end); an inner chunk ends on an inner read column, so no
+// last-column cell of it is an alignment end and its tail is reported as not at the read end.
+template <int RPL, bool AFFINE, bool CHUNK = false, typename ReadFn, typename TabFn>
+PCABI_HD Result align_lane_packed(ReadFn &rd, int n, const TabFn &tabfn, int L, const Scoring sc, int own_lo = 1,
+                                  int own_hi = -1) {
     using Y = pk::Lay<RPL>;
     // tabfn(r) returns a callable row(s) -> substitution key for read code r
     LanePacked<RPL, AFFINE> st;
@@ -921,18 +930,27 @@ PCABI_HD Result align_lane_packed(ReadFn &rd, int n, const TabFn &tabfn, int L, 
     st.hph_last = 0;
     st.ls_prev = 0;                                // tb 0: no S before column 1
     int r = rd(1);
+    const int hi = own_hi < 0 ? n + 1 : own_hi;
 #pragma unroll 1
     for (int j = 1; j < n; ++j) {
         const int rn = rd(j + 1);
-        st.template column<decltype(tabfn(r)), false>(tabfn(r), j, L, off);
+        if (CHUNK) st.template column<decltype(tabfn(r)), false, true>(tabfn(r), j, L, off, j >= own_lo && j < hi);
+        else st.template column<decltype(tabfn(r)), false>(tabfn(r), j, L, off);
         r = rn;
     }
-    st.materialize(L);
-    st.template column<decltype(tabfn(r)), true>(tabfn(r), n, L, off);
+    int n_fin = n;
+    if (CHUNK && own_hi >= 0) {
+        st.template column<decltype(tabfn(r)), false, true>(tabfn(r), n, L, off, n >= own_lo && n < hi);
+        st.materialize(L);
+        n_fin = n + 1;                            // the read goes on past the chunk
+    } else {
+        st.materialize(L);
+        st.template column<decltype(tabfn(r)), true>(tabfn(r), n, L, off);
+    }
     Best b;
     b.score = st.bscore; b.bi = st.bi; b.bj = st.bj; b.attr = Y::to_std(st.battr, st.bj);
     b.ltype = st.blt; b.trail = st.btrail; b.precd = st.bprec;
-    return finish(b, L, n);
+    return finish(b, L, n_fin);
 }
 
 // ==========================================================================================
@@ -983,6 +1001,44 @@ PCABI_HD bool filter_ok(int rpl, const Scoring &s) {
     const int hi = rpl * (s.ma > 0 ? s.ma : 0);
     const int lo = rpl * (s.mi < 0 ? s.mi : 0) + 4 * (s.go < s.ge ? s.go : s.ge);
     return hi < 4000 && lo > -4000 && s.go > -2000 && s.ge > -2000;
+}
+
+// Chunks of a long read for the middle scan's candidate DP (align_lane_packed<.., CHUNK>), so a
+// long read no longer serialises one lane over all its columns. Only alignments
+// scoring >= T matter (a hit's full identity >= theta forces it), and such an alignment holds
+// at most L diagonal columns and at most (L * match - T) / g inserted read bases (g = the
+// cheapest gap column), so its read span is at most D columns (chunk_span). A chunk owns C
+// consecutive end columns and starts D + 1 columns before the first of them:
+//   * an owned cell whose true best score is >= T has that alignment inside the chunk, and the
+//     chunk's own DP cannot do better there: its only extra alignments let the adapter head
+//     hang off for free at the chunk start, and those reach the owned columns only with a span
+//     > D, i.e. a score < T. Along the alignment's path every prefix is optimal in both DPs, so
+//     the tie-break bits agree too: the chunk reports the same cell, score and attributes;
+//   * an owned cell below T stays below T in the chunk.
+// Merging the chunks in read order, the first with the largest score, is then the full DP's
+// answer whenever that score is >= T (first maximum = the reference's strict '>' scan); below
+// T the pair cannot hit either way.
+struct Chunk {
+    int start, len, own_lo, own_hi;   // read offset, columns, owned end columns [lo, hi) (hi -1: last chunk)
+};
+
+inline int chunk_span(int L, int T, const Scoring &sc) {   // D, or -1 when chunking does not apply
+    const int g = std::min(-sc.go, -sc.ge);
+    if (g <= 0 || T <= 0 || sc.ma <= 0 || L <= 0) return -1;
+    return L + (L * sc.ma - T + g - 1) / g + 2;
+}
+
+template <typename F>
+inline void chunk_plan(int n, int D, int C, F &&emit) {
+    for (int lo = 1; lo <= n; lo += C) {
+        const int hi = lo + C;
+        const int start = std::max(0, lo - 1 - D);
+        if (hi > n) {
+            emit(Chunk{start, n - start, lo - start, -1});
+            break;
+        }
+        emit(Chunk{start, hi - 1 - start, lo - start, hi - start});
+    }
 }
 }  // namespace sf
 

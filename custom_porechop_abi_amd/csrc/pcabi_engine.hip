@@ -102,6 +102,7 @@ struct KParams {
     int64_t out_stride;
     pcabi::Scoring sc;
     int32_t *compat;           // != nullptr: write check_compatibility flags instead of results
+    const int4 *task_chunk;    // k_align_chunk: per task slot (read offset, columns, owned lo, hi)
 };
 
 // Window reader: one dword per lane every 4 columns (a wave-uniform branch -- j is the same in
@@ -169,24 +170,27 @@ struct LdsRow {
     }
 };
 
+// This wave's packed-core substitution table (every lane of the block reaches the barrier).
+template <int RPL>
+__device__ __forceinline__ void fill_wave_tab(const KParams &p, int a_local, int L, int32_t *wave_tab) {
+    const int off = RPL - L;
+    const int lane = threadIdx.x & 63;
+    for (int e = lane; e < kTabW * RPL; e += 64) {
+        const int c = e / RPL, srow = e % RPL + 1;
+        const uint32_t *ap = p.adp_pad + (int64_t)a_local * (RPL / 4);
+        auto code = [&](int sl) { return (int)((ap[(sl - 1) / 4] >> (8 * ((sl - 1) & 3))) & 0xFFu); };
+        wave_tab[e] = pcabi::pk::sub_key<RPL>(srow, c, code, off, p.sc);
+    }
+    __syncthreads();
+}
+
 template <int RPL, bool AFFINE, int KIND>
 __device__ __forceinline__ void run_lane(const KParams &p, int a_local, int64_t w, int64_t out_idx,
                                          int32_t *wave_tab, int64_t tile_off) {
     AdapterRegs<RPL> adp;
     adp.load(p.adp_pad + (int64_t)a_local * (RPL / 4));
     const int L = __builtin_amdgcn_readfirstlane(p.adp_len[a_local]);
-    if constexpr (KIND == PACKED) {
-        // fill this wave's table (every lane of the block reaches the barrier)
-        const int off = RPL - L;
-        const int lane = threadIdx.x & 63;
-        for (int e = lane; e < kTabW * RPL; e += 64) {
-            const int c = e / RPL, srow = e % RPL + 1;
-            const uint32_t *ap = p.adp_pad + (int64_t)a_local * (RPL / 4);
-            auto code = [&](int sl) { return (int)((ap[(sl - 1) / 4] >> (8 * ((sl - 1) & 3))) & 0xFFu); };
-            wave_tab[e] = pcabi::pk::sub_key<RPL>(srow, c, code, off, p.sc);
-        }
-        __syncthreads();
-    }
+    if constexpr (KIND == PACKED) fill_wave_tab<RPL>(p, a_local, L, wave_tab);
     if (w < 0) return;
     const int n = p.win_len[w];
     pcabi::Result r;
@@ -259,6 +263,25 @@ const bool g_middle_filter = [] {
     const char *e = std::getenv("PCABI_MIDDLE_FILTER");
     return !(e && e[0] == '0');
 }();
+
+// Owned end columns per chunk of the middle scan's candidate DP (pcabi_dp.h sf::chunk_plan):
+// short enough that the longest read's chunks finish with the rest, long enough that the D-column
+// lead-in of each chunk stays a few percent.
+constexpr int kChunkCols = 512;
+
+// PCABI_DEBUG=1: the middle scan prints its candidate counts per round to stderr.
+const bool g_debug = [] {
+    const char *e = std::getenv("PCABI_DEBUG");
+    return e && e[0] == '1';
+}();
+
+// Round 1 of the middle scan from exact seeds (pcabi_seed.hip) instead of the score filter:
+// PCABI_MIDDLE_SEEDS=0 off, 1 (default) when the cost model prefers them, 2 whenever they apply.
+int middle_seed_mode() {
+    const char *e = std::getenv("PCABI_MIDDLE_SEEDS");
+    if (!e || !e[0]) return 1;
+    return e[0] == '0' ? 0 : (e[0] == '2' ? 2 : 1);
+}
 
 // Cross mode over tiles, TWO adapters of a FAST bucket per wave (packed 16-bit lanes): block =
 // (tile of 256 windows, adapter pair) in the XCD-aware order of k_align. Writes the best score of
@@ -599,6 +622,48 @@ void launch_tiles(const uint8_t *codes, const int64_t *win_off, const int32_t *w
     hipLaunchKernelGGL(k_tile_windows, grid, dim3(256), 0, st, codes, win_off, win_len, n_win, tile_off, tiles);
 }
 
+// Pairs mode over CHUNKS of long reads (middle-scan candidates, pcabi_dp.h sf::chunk_plan): the
+// packed core on (read offset, columns) of the task's read with the end cell restricted to the
+// owned columns. Wave = one adapter, as k_align's pairs mode; results unmerged, one per task.
+template <int RPL, bool AFFINE>
+__global__ __launch_bounds__(256, PCABI_WAVES) void k_align_chunk(KParams p) {
+    __shared__ __attribute__((aligned(16))) int32_t tab[4 * kTabW * RPL];
+    int32_t *wave_tab = tab + (threadIdx.x >> 6) * kTabW * RPL;
+    int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const bool live = wave < p.n_waves;            // dead waves still join the table barrier
+    if (!live) wave = p.n_waves - 1;
+    const int64_t slot = wave * 64 + (threadIdx.x & 63);
+    const int a_local = __builtin_amdgcn_readfirstlane(p.wave_adp[wave]);
+    const int L = __builtin_amdgcn_readfirstlane(p.adp_len[a_local]);
+    fill_wave_tab<RPL>(p, a_local, L, wave_tab);
+    const int32_t tw = live ? p.task_win[slot] : -1;
+    if (tw < 0) return;
+    const int4 ck = p.task_chunk[slot];
+    const uint8_t *b = p.codes + p.win_off[tw] + ck.x;
+    const int a0 = (int)((uintptr_t)b & 3);
+    WindowReader rd(reinterpret_cast<const uint32_t *>(b - a0), 1, 8 * a0);
+    auto tabfn = [&](int rc) { return LdsRow{wave_tab + rc * RPL}; };
+    const pcabi::Result r = pcabi::align_lane_packed<RPL, AFFINE, true>(rd, ck.y, tabfn, L, p.sc, ck.z, ck.w);
+    store_result(p.out, p.out_stride, p.task_out[slot], r);
+}
+
+// Buckets the chunked candidate DP serves: the packed core's (FAST buckets laid out packed, WIDE).
+bool chunkable(int b, bool packed) { return kBuckets[b].kind == WIDE || (kBuckets[b].kind == FAST && packed); }
+
+void dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st) {
+    const dim3 grid((unsigned)((p.n_waves + 3) / 4));
+    switch (kBuckets[b].rpl) {
+#define C(R)                                                                                   \
+    case R:                                                                                    \
+        if (affine) hipLaunchKernelGGL((k_align_chunk<R, true>), grid, dim3(256), 0, st, p);   \
+        else hipLaunchKernelGGL((k_align_chunk<R, false>), grid, dim3(256), 0, st, p);         \
+        break;
+    C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32) C(36) C(40) C(44) C(48) C(52) C(56) C(60) C(64)
+    C(68) C(72) C(76) C(80) C(84) C(88)
+#undef C
+    }
+}
+
 template <int RPL, int KIND>
 void launch(const KParams &p, bool affine, dim3 grid, hipStream_t st) {
     if (affine) hipLaunchKernelGGL((k_align<RPL, true, KIND>), grid, dim3(256), 0, st, p);
@@ -735,6 +800,8 @@ struct pcabi_adapters {
     std::vector<int32_t> lens[kNumBuckets];
     std::vector<int32_t> ids[kNumBuckets];   // global adapter index of each bucket entry (host)
     bool has_n = false;                      // some adapter holds an N (code 4) base
+    std::vector<uint8_t> hcodes;             // host copy of the adapters (middle-scan seeds)
+    std::vector<int32_t> hoff, hlen;
     int32_t count[kNumBuckets] = {};
     uint32_t *pad[kNumBuckets] = {};
     int32_t *len[kNumBuckets] = {};
@@ -761,10 +828,21 @@ struct DeviceBuf {
 }  // namespace
 
 // Scratch of the device-resident middle scan (pcabi_middle_scan_dev), grown on demand.
+namespace pcabi_seed {   // pcabi_seed.hip
+struct State;
+State *create();
+void destroy(State *s);
+int bounds(State *s, const void *adps_key, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hlen,
+           int32_t n_adp, const std::vector<int> &fb_rows, const uint8_t *codes, const int64_t *v_off,
+           const int32_t *v_len, int64_t n, const pcabi::Scoring &sc, double threshold, int mode, int16_t *s16,
+           std::vector<int64_t> *cands, hipStream_t st);
+}  // namespace pcabi_seed
+
 struct pcabi_scan {
     const pcabi_adapters *adps = nullptr;
     DeviceBuf tiles, toff, res, hits, idx, start, soff, slen, mwin, ms, me;
-    DeviceBuf s16, tw, to, wa, pres;   // score filter + candidate pairs (round 1)
+    DeviceBuf s16, tw, to, wa, pres, tck;   // score filter + candidate pairs (chunks)
+    pcabi_seed::State *seed = nullptr; // seeded round-1 bounds (pcabi_seed.hip)
 };
 
 namespace {
@@ -1237,9 +1315,15 @@ int adapters_create_impl(const uint8_t *adp_codes, const int32_t *adp_off, const
                   sc != nullptr);
     pcabi_adapters *a = new pcabi_adapters();
     a->n_adp = n_adp;
-    for (int k = 0; k < n_adp; ++k)
-        for (int i = 0; i < adp_len[k]; ++i)
+    a->hoff.resize((size_t)n_adp);
+    a->hlen.assign(adp_len, adp_len + n_adp);
+    for (int k = 0; k < n_adp; ++k) {
+        a->hoff[k] = (int32_t)a->hcodes.size();
+        for (int i = 0; i < adp_len[k]; ++i) {
             if (adp_codes[adp_off[k] + i] > 3) a->has_n = true;
+            a->hcodes.push_back(adp_codes[adp_off[k] + i]);
+        }
+    }
     for (int b = 0; b < kNumBuckets; ++b) {
         const int nb = (int)bk[b].len.size();
         a->count[b] = nb;
@@ -1385,8 +1469,9 @@ int pcabi_scan_create(const pcabi_adapters *adps, pcabi_scan **out) {
 void pcabi_scan_destroy(pcabi_scan *s) {
     if (!s) return;
     for (DeviceBuf *b : {&s->tiles, &s->toff, &s->res, &s->hits, &s->idx, &s->start, &s->soff, &s->slen,
-                         &s->mwin, &s->ms, &s->me})
+                         &s->mwin, &s->ms, &s->me, &s->s16, &s->tw, &s->to, &s->wa, &s->pres, &s->tck})
         if (b->p) (void)hipFree(b->p);
+    if (s->seed) pcabi_seed::destroy(s->seed);
     delete s;
 }
 
@@ -1403,10 +1488,16 @@ namespace {
 // into N, which never matches an adapter base, so no alignment of the masked read scores above
 // the same alignment of the unmasked one -- a pair below the threshold in round 1 stays below.
 // h16 / pos1: round 1's scores (adapter-major, round-1 positions) and each read's position.
+// Seeds (pcabi_seed.hip) replace the filter when they apply; they are cheap enough to run again
+// in every later round on the masked reads (seeded: in, round 1 used them; out, this call did),
+// where the hits just masked no longer seed their adapter. make_tiles() lays out this round's
+// tiles, which only the filter reads.
+template <typename MakeTiles>
 int filtered_first_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_off, const int32_t *v_len,
                         const int32_t *h_len, int64_t n, const int32_t *h_start, const int32_t *reads,
                         std::vector<int16_t> &h16, int64_t n1, const std::vector<int32_t> &pos1,
-                        const pcabi::Scoring &scr, double threshold, std::vector<int32_t> &hb, hipStream_t st) {
+                        const pcabi::Scoring &scr, double threshold, std::vector<int32_t> &hb, bool &seeded,
+                        const MakeTiles &make_tiles, hipStream_t st) {
     const pcabi_adapters *adps = sc->adps;
     const int32_t n_adp = adps->n_adp;
     std::vector<int> fb;   // filterable buckets, largest first
@@ -1424,89 +1515,164 @@ int filtered_first_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_o
         for (size_t k = 0; k < adps->ids[b].size(); ++k) lenof[adps->ids[b][k]] = adps->lens[b][k];
     for (int b : fb)
         for (int32_t id : adps->ids[b]) filtered[id] = 1;
-    // 1. filter (round 1 only): best scores of every (adapter, read), buckets side by side
-    if (!h_start) {
+    // 1. bounds of every (adapter, read): seeds (any round, when round 1 used them) or the score
+    //    filter (round 1 only), buckets side by side
+    bool local = !h_start;   // h16 holds this round's bounds (a * n + k), not round 1's
+    std::vector<int64_t> seed_cands;   // seeded: the filtered candidates, sorted (a << 32 | k)
+    if (!h_start || seeded) {
         if (int rc = sc->s16.ensure(sizeof(int16_t) * (size_t)n * n_adp)) return rc;
-        ForkJoin fj;
-        if (int rc = fj.begin(st, fb.size())) return rc;
-        for (size_t k = 0; k < fb.size(); ++k) {
-            const int b = fb[k];
-            FParams f{};
-            f.tiles = (const uint32_t *)sc->tiles.p;
-            f.tile_off = (const int64_t *)sc->toff.p;
-            f.win_len = v_len;
-            f.n_win = n;
-            f.adp_pad = adps->pad[b];
-            f.adp_len = adps->len[b];
-            f.adp_id = adps->id[b];
-            f.n_adp = adps->count[b];
-            f.s16 = (int16_t *)sc->s16.p;
-            f.sc = scr;
-            dispatch_filter(kBuckets[b].rpl, f, scr.go != scr.ge, fj.at(k));
+        int got = 0;
+        const int mode = middle_seed_mode();
+        if (mode && (!h_start || seeded)) {
+            if (!sc->seed) sc->seed = pcabi_seed::create();
+            std::vector<int> rows((size_t)n_adp, 0);
+            for (int b : fb)
+                for (int32_t id : adps->ids[b]) rows[id] = kBuckets[b].rpl;
+            got = pcabi_seed::bounds(sc->seed, adps, adps->hcodes.data(), adps->hoff.data(), adps->hlen.data(),
+                                     n_adp, rows, codes, v_off, v_len, n, scr, threshold, h_start ? 2 : mode,
+                                     (int16_t *)sc->s16.p, &seed_cands, st);
+            if (got < 0) return got;
         }
-        if (int rc = fj.end()) return rc;
-        HIP_TRY(hipGetLastError());
-        h16.resize((size_t)n * n_adp);
-        HIP_TRY(hipMemcpyAsync(h16.data(), sc->s16.p, sizeof(int16_t) * h16.size(), hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
+        if (h_start && !got) return fail(PCABI_E_DEVICE, "middle scan: seeds stopped applying after round 1");
+        seeded = got > 0;
+        if (!seeded) {
+            if (int rc = make_tiles()) return rc;
+            ForkJoin fj;
+            if (int rc = fj.begin(st, fb.size())) return rc;
+            for (size_t k = 0; k < fb.size(); ++k) {
+                const int b = fb[k];
+                FParams f{};
+                f.tiles = (const uint32_t *)sc->tiles.p;
+                f.tile_off = (const int64_t *)sc->toff.p;
+                f.win_len = v_len;
+                f.n_win = n;
+                f.adp_pad = adps->pad[b];
+                f.adp_len = adps->len[b];
+                f.adp_id = adps->id[b];
+                f.n_adp = adps->count[b];
+                f.s16 = (int16_t *)sc->s16.p;
+                f.sc = scr;
+                dispatch_filter(kBuckets[b].rpl, f, scr.go != scr.ge, fj.at(k));
+            }
+            if (int rc = fj.end()) return rc;
+            HIP_TRY(hipGetLastError());
+            h16.resize((size_t)n * n_adp);
+            HIP_TRY(hipMemcpyAsync(h16.data(), sc->s16.p, sizeof(int16_t) * h16.size(), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+        }
+        local = true;
     }
     // 2. candidates (adapter-major): pairs that can reach the threshold, from each read's start
     //    adapter on
     std::vector<int32_t> cand_w, cand_a;
+    size_t sc_i = 0;
     for (int32_t a = 0; a < n_adp; ++a) {
+        if (seeded && filtered[a]) {                   // from the device's list
+            for (; sc_i < seed_cands.size() && (int32_t)(seed_cands[sc_i] >> 32) == a; ++sc_i) {
+                const int32_t k = (int32_t)(seed_cands[sc_i] & 0xFFFFFFFF);
+                if (h_len[k] <= 0 || (h_start && a < h_start[k])) continue;
+                cand_w.push_back(k);
+                cand_a.push_back(a);
+            }
+            continue;
+        }
         const int T = pcabi::sf::filter_threshold(lenof[a], threshold, scr);
-        const int16_t *row = h16.data() + (size_t)a * n1;
+        const int16_t *row = filtered[a] ? h16.data() + (size_t)a * (local ? n : n1) : nullptr;
         for (int64_t k = 0; k < n; ++k) {
             if (h_len[k] <= 0 || (h_start && a < h_start[k])) continue;
-            const int16_t bound = row[h_start ? pos1[reads[k]] : k];
-            if (!filtered[a] || bound >= T) { cand_w.push_back((int32_t)k); cand_a.push_back(a); }
+            if (!row || row[local ? k : pos1[reads[k]]] >= T) { cand_w.push_back((int32_t)k); cand_a.push_back(a); }
         }
     }
     const int64_t n_task = (int64_t)cand_w.size();
     hb.assign((size_t)(5 * n), 0);
     for (int64_t k = 0; k < n; ++k) { hb[k] = -1; hb[n + k] = -1; }
+    if (g_debug) {
+        std::vector<int64_t> per((size_t)n_adp, 0);
+        for (int32_t a : cand_a) ++per[a];
+        std::string s;
+        for (int32_t a = 0; a < n_adp; ++a) s += std::to_string(per[a]) + (a + 1 < n_adp ? "," : "");
+        std::fprintf(stderr, "[pcabi] middle round %s: %lld reads, %lld candidate pairs; per adapter: %s\n",
+                     h_start ? "2+" : "1", (long long)n, (long long)n_task, s.c_str());
+    }
     if (n_task == 0) return 1;
     // attribute DP of the candidates: one task list per bucket (waves of 64 lanes, one adapter
-    // per wave), all buckets in one upload, launched side by side
+    // per wave), all buckets in one upload, launched side by side. Packed-core buckets split
+    // long reads into chunks (sf::chunk_plan), so no lane walks a whole long read alone: a task
+    // is one chunk, and a candidate's chunks are merged below.
     std::vector<int64_t> first((size_t)n_adp + 1, 0);
     for (int64_t t = 0; t < n_task; ++t) ++first[cand_a[t] + 1];
     for (int32_t a = 0; a < n_adp; ++a) first[a + 1] += first[a];
     std::vector<int32_t> tw, to, wa;
+    std::vector<int4> tck;
+    std::vector<int64_t> task_cand;                 // task -> candidate
+    std::vector<int32_t> task_start;                // task -> read offset of its chunk
     std::vector<int> nb_used;
-    std::vector<int64_t> lane0, wave0;
+    std::vector<char> nb_chunked;
+    std::vector<int64_t> wave0;
     for (int b = 0; b < kNumBuckets; ++b) {
         const int nb = adps->count[b];
         if (!nb) continue;
         const size_t w_before = wa.size();
+        bool chunk = chunkable(b, bucket_packed_ok(b, adps->lens[b], scr));
+        std::vector<int> span((size_t)nb, -1);
+        for (int kk = 0; chunk && kk < nb; ++kk) {
+            const int L = adps->lens[b][kk];
+            span[kk] = pcabi::sf::chunk_span(L, pcabi::sf::filter_threshold(L, threshold, scr), scr);
+            if (span[kk] < 0) chunk = false;
+        }
         for (int kk = 0; kk < nb; ++kk) {
             const int32_t a = adps->ids[b][kk];
-            for (int64_t s0 = first[a]; s0 < first[a + 1]; s0 += 64) {
-                wa.push_back(kk);
-                for (int64_t q = 0; q < 64; ++q) {
-                    if (s0 + q < first[a + 1]) { tw.push_back(cand_w[s0 + q]); to.push_back((int32_t)(s0 + q)); }
-                    else { tw.push_back(-1); to.push_back(0); }
+            int lane = 64;
+            auto add = [&](int64_t t, int32_t w, int4 ck) {
+                if (lane == 64) {
+                    wa.push_back(kk);
+                    lane = 0;
                 }
+                tw.push_back(w);
+                to.push_back((int32_t)task_cand.size());
+                tck.push_back(ck);
+                task_cand.push_back(t);
+                task_start.push_back(ck.x);
+                ++lane;
+            };
+            for (int64_t t = first[a]; t < first[a + 1]; ++t) {
+                const int32_t k = cand_w[t];
+                if (chunk)
+                    pcabi::sf::chunk_plan(h_len[k], span[kk], kChunkCols, [&](const pcabi::sf::Chunk &c) {
+                        add(t, k, make_int4(c.start, c.len, c.own_lo, c.own_hi));
+                    });
+                else
+                    add(t, k, make_int4(0, 0, 0, 0));
+            }
+            for (; lane < 64; ++lane) {                // idle lanes of the adapter's last wave
+                tw.push_back(-1);
+                to.push_back(0);
+                tck.push_back(make_int4(0, 0, 0, 0));
             }
         }
         if (wa.size() == w_before) continue;
         nb_used.push_back(b);
+        nb_chunked.push_back(chunk ? 1 : 0);
         wave0.push_back((int64_t)w_before);
     }
     wave0.push_back((int64_t)wa.size());
-    if (int rc = sc->pres.ensure(sizeof(int32_t) * PCABI_NFIELDS * (size_t)n_task)) return rc;
+    const int64_t n_run = (int64_t)task_cand.size();
+    if (int rc = sc->pres.ensure(sizeof(int32_t) * PCABI_NFIELDS * (size_t)n_run)) return rc;
     if (int rc = sc->tw.ensure(sizeof(int32_t) * tw.size())) return rc;
     if (int rc = sc->to.ensure(sizeof(int32_t) * to.size())) return rc;
     if (int rc = sc->wa.ensure(sizeof(int32_t) * wa.size())) return rc;
+    if (int rc = sc->tck.ensure(sizeof(int4) * tck.size())) return rc;
     HIP_TRY(hipMemcpyAsync(sc->tw.p, tw.data(), sizeof(int32_t) * tw.size(), hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(sc->to.p, to.data(), sizeof(int32_t) * to.size(), hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(sc->wa.p, wa.data(), sizeof(int32_t) * wa.size(), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(sc->tck.p, tck.data(), sizeof(int4) * tck.size(), hipMemcpyHostToDevice, st));
     KParams p{};
     p.codes = codes;
     p.win_off = v_off;
     p.win_len = v_len;
     p.n_win = n;
     p.out = (int32_t *)sc->pres.p;
-    p.out_stride = n_task;
+    p.out_stride = n_run;
     p.sc = scr;
     {
         ForkJoin fj;
@@ -1520,27 +1686,37 @@ int filtered_first_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_o
             p.task_win = (const int32_t *)sc->tw.p + wave0[k] * 64;
             p.task_out = (const int32_t *)sc->to.p + wave0[k] * 64;
             p.wave_adp = (const int32_t *)sc->wa.p + wave0[k];
+            p.task_chunk = (const int4 *)sc->tck.p + wave0[k] * 64;
             p.n_waves = wave0[k + 1] - wave0[k];
-            dispatch(b, p, scr.go != scr.ge, fj.at(k), bucket_packed_ok(b, adps->lens[b], scr));
+            if (nb_chunked[k]) dispatch_chunk(b, p, scr.go != scr.ge, fj.at(k));
+            else dispatch(b, p, scr.go != scr.ge, fj.at(k), bucket_packed_ok(b, adps->lens[b], scr));
         }
         if (int rc = fj.end()) return rc;
     }
     HIP_TRY(hipGetLastError());
-    std::vector<int32_t> res((size_t)PCABI_NFIELDS * n_task);
+    std::vector<int32_t> res((size_t)PCABI_NFIELDS * n_run);
     HIP_TRY(hipMemcpyAsync(res.data(), sc->pres.p, sizeof(int32_t) * res.size(), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    // merge each candidate's chunks: the first (read order) with the largest score; read offsets
+    // back to the whole read
+    std::vector<int64_t> best((size_t)n_task, -1);
+    for (int64_t u = 0; u < n_run; ++u) {
+        const int64_t t = task_cand[u];
+        if (best[t] < 0 || res[4 * n_run + u] > res[4 * n_run + best[t]]) best[t] = u;
+    }
     // 3. per read, the first candidate (adapter order) over the threshold
     for (int64_t t = 0; t < n_task; ++t) {
         const int64_t k = cand_w[t];
         const int32_t a = cand_a[t];
         if (hb[k] >= 0 && hb[k] <= a) continue;
-        const int rs = res[0 * n_task + t];
-        const int m = res[5 * n_task + t], l2 = res[7 * n_task + t];
+        const int64_t u = best[t];
+        const int rs = res[0 * n_run + u];
+        const int m = res[5 * n_run + u], l2 = res[7 * n_run + u];
         const double full = rs == -1 ? 0.0 : pcabi::pid6(m, l2);
         if (full < threshold) continue;
         hb[k] = a;
-        hb[n + k] = rs;
-        hb[2 * n + k] = res[1 * n_task + t];
+        hb[n + k] = rs + task_start[u];
+        hb[2 * n + k] = res[1 * n_run + u] + task_start[u];
         hb[3 * n + k] = m;
         hb[4 * n + k] = l2;
     }
@@ -1569,11 +1745,19 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
     std::vector<int16_t> h16;                       // round-1 filter scores (bounds for later rounds)
     std::vector<int32_t> pos1((size_t)n_win, 0);    // read -> round-1 position
     bool filt_round1 = false;
+    bool seeded = false;                            // round 1 took its bounds from seeds
     // Round 1 visits the reads longest first: lanes of a wave (and tiles) then run near-equal
     // column counts (read lengths are log-normal; unsorted, a wave would idle ~2/3 of its lanes).
     cur.resize((size_t)n_win);
     for (int64_t k = 0; k < n_win; ++k) cur[k] = (int32_t)k;
-    std::stable_sort(cur.begin(), cur.end(), [&](int32_t x, int32_t y) { return h_win_len[x] > h_win_len[y]; });
+    {
+        // longest first, ties in read order (a stable sort by length, as unique 64-bit keys)
+        std::vector<uint64_t> key((size_t)n_win);
+        for (int64_t k = 0; k < n_win; ++k)
+            key[k] = ((uint64_t)(uint32_t)(INT32_MAX - std::max(h_win_len[k], 0)) << 32) | (uint32_t)k;
+        std::sort(key.begin(), key.end());
+        for (int64_t k = 0; k < n_win; ++k) cur[k] = (int32_t)(key[k] & 0xFFFFFFFFu);
+    }
     for (int round = 0;; ++round) {
         const int64_t n = (int64_t)cur.size();
         const int64_t *v_off = win_off;
@@ -1593,22 +1777,29 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
             v_off = (const int64_t *)sc->soff.p;
             v_len = (const int32_t *)sc->slen.p;
         }
-        // tiles of this round's windows
-        toff.assign((size_t)((n + 255) / 256 + 1), 0);
-        int64_t max_nq = 0;
-        const int64_t nd = tile_layout(lens.data(), n, toff.data(), &max_nq);
+        // tiles of this round's windows (the score filter and the full cross product read them)
         int32_t max_len = 0;
         for (int32_t l : lens) max_len = std::max(max_len, l);
-        if (int rc = sc->toff.ensure(sizeof(int64_t) * toff.size())) return rc;
-        if (int rc = sc->tiles.ensure(sizeof(uint32_t) * (size_t)nd)) return rc;
         if (int rc = sc->hits.ensure(sizeof(int32_t) * 5 * (size_t)n)) return rc;
-        HIP_TRY(hipMemcpyAsync(sc->toff.p, toff.data(), sizeof(int64_t) * toff.size(), hipMemcpyHostToDevice, st));
-        launch_tiles(codes, v_off, v_len, n, (const int64_t *)sc->toff.p, max_nq, (uint32_t *)sc->tiles.p, st);
+        bool tiled = false;
+        auto make_tiles = [&]() -> int {
+            if (tiled) return 0;
+            toff.assign((size_t)((n + 255) / 256 + 1), 0);
+            int64_t max_nq = 0;
+            const int64_t nd = tile_layout(lens.data(), n, toff.data(), &max_nq);
+            if (int rc = sc->toff.ensure(sizeof(int64_t) * toff.size())) return rc;
+            if (int rc = sc->tiles.ensure(sizeof(uint32_t) * (size_t)nd)) return rc;
+            HIP_TRY(hipMemcpyAsync(sc->toff.p, toff.data(), sizeof(int64_t) * toff.size(), hipMemcpyHostToDevice, st));
+            launch_tiles(codes, v_off, v_len, n, (const int64_t *)sc->toff.p, max_nq, (uint32_t *)sc->tiles.p, st);
+            tiled = true;
+            return 0;
+        };
         int filt = 0;
         if (g_middle_filter && (round == 0 || filt_round1)) {
             filt = filtered_first_hits(sc, codes, v_off, v_len, lens.data(), n, round == 0 ? nullptr : nxt_start.data(),
                                        cur.data(), h16, n_win, pos1,
-                                       pcabi::Scoring{match, mismatch, gap_open, gap_extend}, threshold, hb, st);
+                                       pcabi::Scoring{match, mismatch, gap_open, gap_extend}, threshold, hb, seeded,
+                                       make_tiles, st);
             if (round == 0) {
                 // the bound needs masked bases (N) to never match an adapter base
                 filt_round1 = filt > 0 && !sc->adps->has_n;
@@ -1617,6 +1808,7 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
             if (filt < 0) return filt;
         }
         if (!filt) {
+            if (int rc = make_tiles()) return rc;
             if (int rc = sc->res.ensure(sizeof(int32_t) * PCABI_NFIELDS * (size_t)n * n_adp)) return rc;
             if (int rc = pcabi_align_cross_dev((const uint32_t *)sc->tiles.p, (const int64_t *)sc->toff.p, v_len, n,
                                                max_len, sc->adps, match, mismatch, gap_open, gap_extend,

@@ -214,6 +214,10 @@ int pcabi_first_hit_dev(const int32_t *res, int64_t stride, int64_t n_win, int32
  *   pcabi_middle_scan_dev       : codes/win_off/win_len are DEVICE pointers (codes are masked in
  *                                 place), h_win_len the host copy of the lengths.
  *   pcabi_middle_scan_host      : host buffers (as pcabi_align_host), copies in, scans.
+ *   pcabi_middle_seed_runs      : how many round-1 scans took their bounds from exact k-mer seeds
+ *                                 (pcabi_seed.hip) instead of the score filter, process-wide.
+ *                                 PCABI_MIDDLE_SEEDS=0 / 1 (default, cost model) / 2 (always when
+ *                                 the seeds apply) selects; the hits are the same either way.
  */
 typedef struct pcabi_scan pcabi_scan;
 int pcabi_scan_create(const pcabi_adapters *adps, pcabi_scan **out);
@@ -228,6 +232,7 @@ int64_t pcabi_middle_scan_host(int device, const uint8_t *codes, int64_t codes_l
                                const int32_t *adp_len, int32_t n_adp, int match, int mismatch,
                                int gap_open, int gap_extend, double threshold, int32_t *hits,
                                int64_t cap);
+int64_t pcabi_middle_seed_runs(void);
 
 /*
  * Adapter-set discovery reduction (porechop_abi/nanopore_read.py:158-173): for each adapter a

@@ -201,3 +201,56 @@ extern "C" int pcabi_model_compat(const char *s1, const char *s2) {
     if (n2 <= 128) return run_compat<128>(a, n1, b, n2);
     return -2;
 }
+
+// Middle-scan chunking (pcabi::sf::chunk_plan + align_lane_packed<.., CHUNK>): the read split into
+// chunks of C owned columns for threshold score T, each aligned alone, merged in read order (first
+// largest score), read offsets added back. Returns the number of chunks, -3 if out of range, -4
+// if chunking does not apply (chunk_span < 0).
+template <int RPL>
+static void run_packed_chunk(const char *read, int n, const char *adp, int L, pcabi::Scoring sc, int own_lo,
+                             int own_hi, int *out) {
+    const int off = RPL - L;
+    auto rd = [&](int j) { return j <= n ? dna5((unsigned char)read[j - 1]) : 4; };
+    auto ad = [&](int s) { return s <= off ? pcabi::PAD_CODE : dna5((unsigned char)adp[s - off - 1]); };
+    int32_t tab[pcabi::pk::TAB_W * RPL];
+    for (int c = 0; c < pcabi::pk::TAB_W; ++c)
+        for (int s = 1; s <= RPL; ++s) tab[c * RPL + s - 1] = pcabi::pk::sub_key<RPL>(s, c, ad, off, sc);
+    struct Row {
+        const int32_t *p;
+        int32_t operator()(int s) const { return p[s - 1]; }
+        void quad(int q, int32_t *dst) const { for (int k = 0; k < 4; ++k) dst[k] = p[4 * q + k]; }
+    };
+    auto tabfn = [&](int rc) { return Row{tab + rc * RPL}; };
+    pcabi::Result r = (sc.go != sc.ge)
+        ? pcabi::align_lane_packed<RPL, true, true>(rd, n, tabfn, L, sc, own_lo, own_hi)
+        : pcabi::align_lane_packed<RPL, false, true>(rd, n, tabfn, L, sc, own_lo, own_hi);
+    out[0] = r.rs; out[1] = r.re; out[2] = r.as; out[3] = r.ae;
+    out[4] = r.score; out[5] = r.m; out[6] = r.l1; out[7] = r.l2;
+}
+
+extern "C" int pcabi_model_align_chunked(const char *read, int n, const char *adp, int L, int ma, int mi, int go,
+                                         int ge, int T, int C, int *out) {
+    pcabi::Scoring sc{ma, mi, go, ge};
+    if (L <= 0 || n <= 0 || C <= 0) return -1;
+    const int rpl = (L + 3) & ~3;
+    if (!pcabi::packed_ok(L, rpl, sc)) return -3;
+    const int D = pcabi::sf::chunk_span(L, T, sc);
+    if (D < 0) return -4;
+    int n_chunks = 0, best = 0;
+    int got[8];
+    pcabi::sf::chunk_plan(n, D, C, [&](const pcabi::sf::Chunk &ck) {
+        switch (rpl) {
+#define C_(R) case R: run_packed_chunk<R>(read + ck.start, ck.len, adp, L, sc, ck.own_lo, ck.own_hi, got); break;
+        C_(4) C_(8) C_(12) C_(16) C_(20) C_(24) C_(28) C_(32) C_(36) C_(40) C_(44) C_(48) C_(52) C_(56) C_(60)
+        C_(64) C_(68) C_(72) C_(76) C_(80) C_(84) C_(88)
+#undef C_
+        }
+        if (n_chunks == 0 || got[4] > best) {
+            best = got[4];
+            for (int k = 0; k < 8; ++k) out[k] = got[k];
+            if (out[0] >= 0) { out[0] += ck.start; out[1] += ck.start; }
+        }
+        ++n_chunks;
+    });
+    return n_chunks;
+}

@@ -30,6 +30,8 @@ def model():
     L.pcabi_model_filter.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p,
                                      ctypes.c_int, ctypes.c_int] + [ctypes.c_int] * 4 + [ctypes.c_void_p]
     L.pcabi_model_filter_threshold.argtypes = [ctypes.c_int, ctypes.c_double] + [ctypes.c_int] * 4
+    L.pcabi_model_align_chunked.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int] + \
+        [ctypes.c_int] * 6 + [ctypes.c_void_p]
     L.pcabi_model_pid6.restype = ctypes.c_double
     L.pcabi_model_pid6.argtypes = [ctypes.c_int, ctypes.c_int]
     return L
@@ -278,3 +280,68 @@ def test_score_filter_threshold_is_a_lower_bound(model):
             assert res[4] >= model.pcabi_model_filter_threshold(L, thr, *sc), (sc, thr, r, a, res)
             checked += 1
     assert checked > 500
+
+
+@pytest.mark.parametrize('sc', [(3, -6, -5, -2), (2, -1, -1, -1), (1, -1, -3, -1), (5, -4, -8, -6)])
+def test_chunked_candidate_dp(model, sc):
+    """The middle scan's chunked candidate DP (pcabi_dp.h sf::chunk_plan + align_lane_packed with
+    CHUNK): reads split into chunks of C owned columns, each aligned alone, merged in read order.
+    Whenever the whole-read best score reaches T (the bound every hit must reach) the merged
+    result equals the whole-read result field for field; below T it stays below T. Chunk sizes
+    down to a few columns put chunk boundaries inside adapter copies, at read ends and between
+    equal-score copies (the first must win)."""
+    rng = random.Random(sum(sc) * 31 + 7)
+    n_hi = n_lo = n_multi = 0
+    adps = ['AATGTACTTCGTTCAGTTACGTATTGCT', 'GCAATACGTAACTGAACGAAGT', 'ACGTTTAGGCATTGCA',
+            ''.join(rng.choice('ACGT') for _ in range(40)), ''.join(rng.choice('ACGT') for _ in range(64))]
+    for it in range(1500):
+        a = rng.choice(adps)
+        n = rng.choice([rng.randint(1, 60), rng.randint(60, 600), rng.randint(600, 2500)])
+        r = ''.join(rng.choice('ACGT') for _ in range(n))
+        for _ in range(rng.choice([0, 1, 1, 2, 3])):
+            copy = _mutate_cpu(rng, a, rng.choice([0.0, 0.05, 0.1, 0.2]))
+            where = rng.random()
+            if where < 0.2:
+                r = copy[rng.randint(0, 5):] + r
+            elif where < 0.4:
+                r = r + copy[:max(1, len(copy) - rng.randint(0, 5))]
+            else:
+                p = rng.randint(0, len(r))
+                r = r[:p] + copy + (copy if rng.random() < 0.3 else '') + r[p:]
+        for thr in (90.0, 75.0):
+            T = model.pcabi_model_filter_threshold(len(a), thr, *sc)
+            if T <= 0:
+                continue
+            rc, whole = _run(model, 'pcabi_model_align_packed', r, a, sc)
+            if rc == -3:
+                continue
+            C = rng.choice([1, 3, 17, 64, 200, 1000])
+            out = (ctypes.c_int * 8)()
+            rb, ab = r.encode(), a.encode()
+            nc = model.pcabi_model_align_chunked(rb, len(rb), ab, len(ab), *sc, T, C, out)
+            assert nc > 0, (nc, sc, T, C)
+            got = list(out)
+            if whole[4] >= T:
+                assert got == whole, (sc, thr, T, C, r, a, got, whole)
+                n_hi += 1
+                n_multi += nc > 1
+            else:
+                assert got[4] < T, (sc, thr, T, C, r, a, got, whole)
+                n_lo += 1
+    assert n_hi > 300 and n_lo > 300 and n_multi > 200, (n_hi, n_lo, n_multi)
+
+
+def _mutate_cpu(rng, s, rate):
+    out = []
+    for c in s:
+        x = rng.random()
+        if x < rate / 3:
+            out.append(rng.choice('ACGT'))
+        elif x < 2 * rate / 3:
+            continue
+        elif x < rate:
+            out.append(c)
+            out.append(rng.choice('ACGT'))
+        else:
+            out.append(c)
+    return ''.join(out)

@@ -275,3 +275,70 @@ def test_middle_scan_rounds(gpu_lib, scheme):
     order_g = np.lexsort((np.arange(got.shape[1]), got[0]))
     order_e = np.lexsort((np.arange(exp.shape[1]), exp[0]))
     assert np.array_equal(got[:, order_g], exp[:, order_e])
+
+
+def _edit_exactly(rng, s, k):
+    """s with exactly k random edits (substitution to another base, deletion, insertion)."""
+    s = list(s)
+    for _ in range(k):
+        op = rng.randrange(3)
+        p = rng.randrange(len(s))
+        if op == 0:
+            s[p] = rng.choice([c for c in 'ACGT' if c != s[p]])
+        elif op == 1 and len(s) > 1:
+            del s[p]
+        else:
+            s.insert(p, rng.choice('ACGT'))
+    return ''.join(s)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('threshold,scheme', [(90.0, (3, -6, -5, -2)), (88.0, (3, -6, -5, -2)),
+                                              (85.0, (2, -1, -1, -1)), (90.0, (1, -1, -3, -1))])
+def test_middle_scan_seeds(gpu_lib, monkeypatch, threshold, scheme):
+    """Round 1 from exact k-mer seeds (pcabi_seed.hip, PCABI_MIDDLE_SEEDS=2) vs the oracle's
+    masked loop: adapter copies with exactly 0 .. e_max + 2 edits (e_max = the most non-matching
+    columns an alignment at the threshold can hold), copies cut at either read end (the adapter
+    hangs off), repeats, N runs, and adapters of 16..64 bp (both window row classes)."""
+    from custom_porechop_abi_amd import engine
+    L = gpu_lib
+    rng = random.Random(int(threshold) * 7 + scheme[0])
+    adps = ['AATGTACTTCGTTCAGTTACGTATTGCT', 'GCAATACGTAACTGAACGAAGT', 'ACGTTTAGGCATTGCA',
+            _rand_seq(rng, 50, 'ACGT'), _rand_seq(rng, 64, 'ACGT'), _rand_seq(rng, 33, 'ACGT'),
+            'TTTTTTTTTTAAAAAAAAAACCCCCGGGGG']
+    th = threshold / 100.0
+    reads = []
+    for k in range(240):
+        n = rng.choice([0, 7, rng.randint(100, 2500)])
+        r = _rand_seq(rng, n, 'ACGT' if rng.random() < 0.8 else 'ACGTN')
+        for _ in range(rng.choice([0, 1, 1, 2, 3])):
+            a = rng.choice(adps)
+            e = int(len(a) * (1 - th) / th)
+            a = _edit_exactly(rng, a, rng.randint(0, e + 2))
+            where = rng.random()
+            if where < 0.15:
+                a = a[rng.randint(0, 4):]
+                r = a + r
+            elif where < 0.3:
+                a = a[:len(a) - rng.randint(0, 4)]
+                r = r + a
+            else:
+                p = rng.randint(0, len(r))
+                r = r[:p] + a + (a if rng.random() < 0.15 else '') + r[p:]
+        reads.append(r)
+    pack = engine.SeqPack(reads)
+    views = pack.views(np.zeros(len(reads), np.int64), pack.lengths)
+    exp = oracle_lib.middle_scan_windows(views, adps, scheme, threshold)
+    assert exp.shape[1] > 60
+    order_e = np.lexsort((np.arange(exp.shape[1]), exp[0]))
+    runs0 = L.pcabi_middle_seed_runs()
+    monkeypatch.setenv('PCABI_MIDDLE_SEEDS', '2')
+    got = engine.middle_scan(views, adps, scheme, threshold)
+    assert L.pcabi_middle_seed_runs() > runs0, 'the seeded round 1 did not run'
+    order_g = np.lexsort((np.arange(got.shape[1]), got[0]))
+    assert np.array_equal(got[:, order_g], exp[:, order_e])
+    monkeypatch.setenv('PCABI_MIDDLE_SEEDS', '0')
+    runs1 = L.pcabi_middle_seed_runs()
+    got0 = engine.middle_scan(views, adps, scheme, threshold)
+    assert L.pcabi_middle_seed_runs() == runs1
+    assert np.array_equal(got0, got)
