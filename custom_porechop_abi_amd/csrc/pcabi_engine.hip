@@ -1751,12 +1751,19 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
     cur.resize((size_t)n_win);
     for (int64_t k = 0; k < n_win; ++k) cur[k] = (int32_t)k;
     {
-        // longest first, ties in read order (a stable sort by length, as unique 64-bit keys)
-        std::vector<uint64_t> key((size_t)n_win);
-        for (int64_t k = 0; k < n_win; ++k)
-            key[k] = ((uint64_t)(uint32_t)(INT32_MAX - std::max(h_win_len[k], 0)) << 32) | (uint32_t)k;
-        std::sort(key.begin(), key.end());
-        for (int64_t k = 0; k < n_win; ++k) cur[k] = (int32_t)(key[k] & 0xFFFFFFFFu);
+        // longest first, ties in read order: a stable LSD radix sort on ~length, two 16-bit digits
+        std::vector<int32_t> tmp((size_t)n_win);
+        std::vector<int64_t> cnt(1 << 16);
+        auto key = [&](int32_t k) { return ~(uint32_t)std::max(h_win_len[k], 0); };
+        for (int pass = 0; pass < 2; ++pass) {
+            const int sh = 16 * pass;
+            std::fill(cnt.begin(), cnt.end(), 0);
+            for (int64_t k = 0; k < n_win; ++k) ++cnt[(key(cur[k]) >> sh) & 0xFFFF];
+            int64_t run = 0;
+            for (int64_t &c : cnt) { const int64_t x = c; c = run; run += x; }
+            for (int64_t k = 0; k < n_win; ++k) tmp[cnt[(key(cur[k]) >> sh) & 0xFFFF]++] = cur[k];
+            cur.swap(tmp);
+        }
     }
     for (int round = 0;; ++round) {
         const int64_t n = (int64_t)cur.size();

@@ -1,10 +1,10 @@
-// pcabi_seed.hip -- exact seeding of the middle-adapter scan (round 1) on the GPU (gfx950).
+// pcabi_seed.hip -- exact seeding of the middle-adapter scan on the GPU (gfx950).
 //
 // Reference: porechop_abi/nanopore_read.py:219-252 (find_middle_adapters): every read against
 // every middle adapter, a hit when the best alignment's full identity (pid2 = m / l2) reaches
 // the threshold. The engine's score filter computes every pair's best score S* to find the
-// pairs that can hit. This unit finds them from exact k-mer seeds instead, and
-// hands the engine the same kind of per-pair bound (int16 s16[a * n + k]).
+// pairs that can hit. This unit finds them from exact k-mer seeds instead and
+// hands the engine the pairs whose bound reaches the filter threshold T.
 //
 // Why it is exact ("Seeds"):
 //   * l2 counts the columns of the adapter span: every adapter base once (matched, mismatched,
@@ -13,22 +13,23 @@
 //   * Cut the adapter into e + 1 pieces. An error column touches at most one piece, so one
 //     piece aligns as an unbroken run of matches: the read holds that piece exactly. Each piece
 //     contributes its first K bases (K = min(8, piece length)) as a probe.
-//   * A probe found at read position q with adapter offset o puts the whole alignment inside
-//     read columns [q - o - e, q - o + L + e) (at most e insertions on either side), clipped
-//     to the read. The score-only DP over that window (free end gaps, as the full DP) scores
-//     every alignment inside it, in particular that one, so the window's best S_w >= its score
-//     >= the filter bound T (sf::filter_threshold). A window starting inside the read lets the
-//     adapter head hang off for free there, which only raises S_w: still a bound.
-//   * Pairs with no probe hit get NEG16 (no alignment can reach theta); the others the largest
-//     S_w. Pairs with a bound >= T go to the full attribute DP exactly as after the filter, and
-//     masking in later rounds never creates a new theta-alignment, so the bounds carry over.
+//   * A probe found at read position q for adapter offset o fixes the diagonal d0 = q - o of
+//     that run, and the alignment never leaves the band d0 +- e (at most e gap columns shift
+//     it). The score-only DP restricted to that band (free end gaps as the full DP: row 0,
+//     column 0 and the read's last column) scores that alignment among others, so the band's
+//     best S_b >= its score >= T (sf::filter_threshold). A wider band only raises S_b.
+//   * Pairs with no probe hit get no bound (no alignment can reach theta); the others the
+//     largest S_b. Pairs with a bound >= T go to the full attribute DP exactly as after the
+//     filter. The engine re-seeds every later round on the masked reads (N never matches).
 // Kernels (integer work, no MFMA):
-//   k_seed_scan    one block per read (grid-stride), 4 positions per lane: the 8-mer codes of the
-//                  positions, probe bitmaps (K = 4..8, 4^K bits each) in LDS, hits expanded into
-//                  (read, adapter, window) tasks per row class, staged per block in LDS;
-//   k_seed_window  one lane per task: Gotoh score DP over the window, rows in registers (32 or
-//                  64 with pass-through padding rows), atomicMax into the pair's bound;
-//   k_bound16      bound -> int16 s16.
+//   k_seed_scan   reads grid-stride over blocks, 4 positions per lane: the 8-mer codes of the
+//                 positions, and per probe length K (4..8) a bitmap test and a rank into the probe
+//                 entries, all in LDS; hits become (read, adapter, diagonal) tasks per band class,
+//                 staged per block in LDS and appended with one global atomic per chunk;
+//   k_seed_band   one lane per task: the banded Gotoh score DP (2E+1 cells per adapter row in
+//                 registers), atomicMax into the pair's bound;
+//   k_cands       the pairs whose bound reaches T, compacted for the host (k_bound16: or all
+//                 bounds as int16).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -58,10 +59,12 @@ namespace pcabi_seed {
 std::atomic<int64_t> g_runs{0};
 
 constexpr int kMinK = 4, kMaxK = 8, kNK = kMaxK - kMinK + 1;
-constexpr int kCls = 2;                        // row classes of k_seed_window
-constexpr int kClsRows[kCls] = {32, 64};
-constexpr int kMaxL = 64;
-constexpr int kBitsDw = (1 << 16) / 32 + (1 << 14) / 32 + (1 << 12) / 32 + (1 << 10) / 32 + (1 << 8) / 32;
+constexpr int kCls = 2;            // band classes: e <= E0, e <= E1
+constexpr int kMaxE = 15;          // band half-width the kernels are built for
+constexpr int kMaxL = 255;
+constexpr int kMaxEnt = 8192;      // probe entries / distinct probes kept in LDS
+constexpr int kBuf = 512;          // staged tasks per block and class
+constexpr int kLdsMax = 64 * 1024; // per block: probe tables + stage
 constexpr int kNeg = -(1 << 20);
 
 struct ScanArgs {
@@ -69,22 +72,17 @@ struct ScanArgs {
     const int64_t *v_off;
     const int32_t *v_len;
     int64_t n;
-    const uint32_t *bits;       // bitmaps of the probe k-mers, K = 4..8 (absent: no dwords)
-    int32_t bits_off[kNK];      // dword offset of K's bitmap, -1 when no probe has length K
-    int32_t n_bits;             // dwords in all bitmaps
-    const int32_t *head;        // CSR over the probe codes, 4^K + 1 entries per present K
-    int64_t head_off[kNK];
-    const int32_t *ent;         // (adapter << 8) | piece offset o
-    const int32_t *info;        // per adapter: L | e << 8 | cls << 16
-    int4 *task;                 // kCls regions of cap tasks: (read, adapter, window start, columns)
+    const uint32_t *tabs;       // LDS image: bits | rank16 | estart16 | ent (dwords, copied as is)
+    int32_t tab_dw;             // its dwords
+    int32_t bits_off[kNK];      // dword offset of K's bitmap in the image, -1 when no probe has length K;
+                                // K = 8 is the merged table: every 8-mer extending a probe of any K
+    int32_t min_k;              // shortest probe
+    int32_t rank_off, estart_off, ent_off;   // dword offsets of the other sections
+                                             // (entries: adapter << 9 | band class << 8 | offset)
+    int4 *task;                 // kCls regions of cap tasks: (read, adapter, diagonal, 0)
     int64_t cap;
     int32_t *cnt;               // tasks per class (may exceed cap: the caller grows and reruns)
 };
-
-// Tasks are staged per block in LDS (LDS atomics) and appended to the global regions in
-// chunks, one global atomic per chunk: a global atomic per task on the two class counters
-// serialised the scan (76 ms for ~10 M tasks).
-constexpr int kBuf = 512;
 
 struct Stage {
     int4 buf[kCls][kBuf];
@@ -130,107 +128,179 @@ __device__ __forceinline__ void flush(Stage &sg, int at_least, const ScanArgs &a
 }
 
 __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
-    __shared__ uint32_t bits[kBitsDw];
+    extern __shared__ uint32_t lds[];
     __shared__ Stage sg;
-    for (int i = threadIdx.x; i < a.n_bits; i += 256) bits[i] = a.bits[i];
+    for (int i = threadIdx.x; i < a.tab_dw; i += 256) lds[i] = a.tabs[i];
     if (threadIdx.x < kCls) sg.cnt[threadIdx.x] = 0;
     __syncthreads();
-    for (int64_t k = blockIdx.x; k < a.n; k += gridDim.x) {
-        const int len = a.v_len[k];
-        const uint8_t *base = a.codes + a.v_off[k];
-        for (int p0b = 0; p0b < len; p0b += 1024) {      // block-uniform: every lane takes part
-            const int p0 = p0b + 4 * (int)threadIdx.x;
-            uint32_t valid = 0;
-            uint32_t c2[11];
-#pragma unroll
-            for (int t = 0; t < 11; ++t) {
-                const uint32_t b = (p0 + t < len) ? base[p0 + t] : 4u;
-                valid |= (b < 4u ? 1u : 0u) << t;
-                c2[t] = b & 3u;
+    const uint16_t *rank = reinterpret_cast<const uint16_t *>(lds + a.rank_off);
+    const uint16_t *estart = reinterpret_cast<const uint16_t *>(lds + a.estart_off);
+    const int32_t *ent = reinterpret_cast<const int32_t *>(lds + a.ent_off);
+    // The block walks its reads (blockIdx.x, + gridDim.x, ...) 1024 positions at a time; the
+    // bytes of the next step (and the next read's length / offset) are loaded before the current
+    // step is processed, so the global latency hides behind the lookups.
+    int64_t k = blockIdx.x, nk = k;
+    int len = 0, nlen = 0;
+    const uint8_t *base = a.codes, *nbase = a.codes;
+    auto next_read = [&](int64_t from, int &ln, const uint8_t *&bs) -> int64_t {
+        for (; from < a.n; from += gridDim.x) {
+            ln = a.v_len[from];
+            if (ln > 0) {
+                bs = a.codes + a.v_off[from];
+                return from;
             }
+        }
+        return from;
+    };
+    auto fetch = [&](const uint8_t *bs, int ln, int p0b, uint32_t (&w)[3]) {
+        const int p0 = p0b + 4 * (int)threadIdx.x;
+        w[0] = w[1] = w[2] = 0x04040404u;
+        if (p0 < ln) {   // bytes p0 .. p0 + 11 from four aligned dwords (>= 16 B tail padding)
+            const uint8_t *ad = bs + p0;
+            const int a0 = (int)((uintptr_t)ad & 3);
+            const uint32_t *q = reinterpret_cast<const uint32_t *>(ad - a0);
+            const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3];
+            w[0] = __builtin_amdgcn_alignbyte(d1, d0, a0);
+            w[1] = __builtin_amdgcn_alignbyte(d2, d1, a0);
+            w[2] = __builtin_amdgcn_alignbyte(d3, d2, a0);
+        }
+    };
+    k = next_read(k, len, base);
+    if (k < a.n) nk = next_read(k + gridDim.x, nlen, nbase);
+    int p0b = 0;
+    uint32_t wn[3];
+    if (k < a.n) fetch(base, len, 0, wn);
+    int iter = 0;
+    while (k < a.n) {                                  // block-uniform: every lane takes part
+        const int64_t ck = k;
+        const int clen = len, cp0 = p0b + 4 * (int)threadIdx.x;
+        const uint32_t w[3] = {wn[0], wn[1], wn[2]};
+        p0b += 1024;
+        if (p0b >= len) {                              // on to the next read
+            k = nk;
+            len = nlen;
+            base = nbase;
+            p0b = 0;
+            if (k < a.n) nk = next_read(k + gridDim.x, nlen, nbase);
+        }
+        if (k < a.n) fetch(base, len, p0b, wn);
+        // 12 bases in two words (SWAR): c24 = their 2-bit codes, first base in the top bits;
+        // vmask bit t = base t is A/C/G/T inside the read (Dna5 codes are 0..4: N has bit 2)
+        uint32_t c24 = 0, vmask = 0;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                uint32_t c8 = 0;
+        for (int d = 0; d < 3; ++d) {
+            const uint32_t c4 = ((w[d] & 0x03030303u) * 0x40100401u) >> 24;
+            const uint32_t nb = (((~w[d]) >> 2) & 0x01010101u) * 0x10204080u >> 28;
+            c24 = (c24 << 8) | c4;
+            vmask |= nb << (4 * d);
+        }
+        const int rem = clen - cp0;
+        vmask &= rem >= 12 ? 0xFFFu : (rem > 0 ? (1u << rem) - 1u : 0u);
+        // fast path: every probe is a prefix of the 8-mer at its position, and the K = 8 table
+        // holds every 8-mer that extends a probe -- one LDS word per position
+        uint32_t hits = 0, slow = 0;
 #pragma unroll
-                for (int t = 0; t < 8; ++t) c8 = (c8 << 2) | c2[i + t];
-                const int q = p0 + i;
-#pragma unroll
-                for (int kk = 0; kk < kNK; ++kk) {
-                    if (a.bits_off[kk] < 0) continue;      // uniform
-                    const int K = kMinK + kk;
-                    const uint32_t need = (1u << K) - 1;
-                    const uint32_t code = c8 >> (2 * (kMaxK - K));
-                    if (((valid >> i) & need) != need) continue;
-                    if (!((bits[a.bits_off[kk] + (code >> 5)] >> (code & 31)) & 1u)) continue;
-                    const int e = a.head[a.head_off[kk] + code + 1];
-                    for (int b = a.head[a.head_off[kk] + code]; b < e; ++b) {
-                        const int en = a.ent[b];
-                        const int ad = en >> 8, o = en & 255;
-                        const int inf = a.info[ad];
-                        const int L = inf & 255, er = (inf >> 8) & 255;
-                        const int ws = max(q - o - er, 0);
-                        const int we = min(q - o + L + er, len);
-                        stage_task(sg, inf >> 16, make_int4((int)k, ad, ws, we - ws), a);
-                    }
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t c8 = (c24 >> (8 - 2 * i)) & 0xFFFFu;
+            const uint32_t word = lds[a.bits_off[kNK - 1] + (int)(c8 >> 5)];
+            const bool full = ((vmask >> i) & 0xFFu) == 0xFFu;
+            hits |= (full && ((word >> (c8 & 31)) & 1u)) ? 1u << i : 0u;
+            // a valid run shorter than 8 bases (an N or the read end ahead): the short tables
+            slow |= (!full && ((vmask >> i) & ((1u << a.min_k) - 1u)) == (1u << a.min_k) - 1u) ? 1u << i : 0u;
+        }
+        while (hits | slow) {
+            const bool fast = hits != 0;
+            const int i = __builtin_ctz(fast ? hits : slow);
+            if (fast) hits &= hits - 1;
+            else slow &= slow - 1;
+            const uint32_t c8 = (c24 >> (8 - 2 * i)) & 0xFFFFu;
+            const int q = cp0 + i;
+            const int run = __builtin_ctz(~(vmask >> i));
+            for (int kk = fast ? kNK - 1 : 0; kk < (fast ? kNK : kNK - 1); ++kk) {
+                const int K = kMinK + kk;
+                if (a.bits_off[kk] < 0 || (!fast && K > run)) continue;
+                const uint32_t code = c8 >> (2 * (kMaxK - K));
+                const int dw = a.bits_off[kk] + (int)(code >> 5);
+                const uint32_t word = lds[dw], bit = 1u << (code & 31);
+                if (!(word & bit)) continue;
+                const int r = rank[dw] + __popc(word & (bit - 1));
+                const int e = estart[r + 1];
+                for (int b = estart[r]; b < e; ++b) {
+                    const int en = ent[b];                 // adapter << 9 | class << 8 | offset
+                    stage_task(sg, (en >> 8) & 1, make_int4((int)ck, en >> 9, q - (en & 255), 0), a);
                 }
             }
-            flush(sg, kBuf / 2, a);
         }
+        if ((++iter & 7) == 0) flush(sg, kBuf / 2, a);
     }
     flush(sg, 1, a);
 }
 
-// One lane per task: the best score of the adapter against the window (free end gaps on all
-// four sides, as pcabi_dp.h / the oracle's build_rows), RPL rows with the adapter in the
-// bottom L rows; the rows above it score 0 against anything, so they pass S = 0 through (row 0).
-// Substitution scores come from one 6-bit signed field per read code (0..4) per row.
-template <int RPL>
-__global__ __launch_bounds__(256) void k_seed_window(const int4 *task, int32_t n_task, const uint8_t *codes,
-                                                     const int64_t *v_off, const uint8_t *adp, const int32_t *adp_off,
-                                                     const int32_t *info, pcabi::Scoring sc, int32_t *bound,
-                                                     int64_t n) {
+// Banded score DP of one task: rows i = 1..L of the adapter, per row the 2E+1 cells of the
+// diagonals d0 - E .. d0 + E (cell x <-> read column j = i + d0 + x - E), free end gaps as the
+// full DP: S(0, j) = 0, S(i, 0) = 0, ends in row L (j < len) or in the last column (j = len).
+// CHECK: the band touches column 0 or the last column, or leaves the read.
+template <int E, bool CHECK>
+__device__ __forceinline__ int band_best(const uint8_t *rd, int len, const uint8_t *ac, int L, int d0,
+                                         const pcabi::Scoring &sc) {
+    constexpr int W = 2 * E + 1;
+    int S[W], V[W], R[W];
+#pragma unroll
+    for (int x = 0; x < W; ++x) {
+        const int j0 = d0 + x - E;                           // row 0
+        S[x] = (!CHECK || (j0 >= 0 && j0 <= len)) ? 0 : kNeg;
+        V[x] = kNeg;
+        const int j1 = j0 + 1;                               // row 1's read column
+        R[x] = (!CHECK || (j1 >= 1 && j1 <= len)) ? rd[j1 - 1] : 7;
+    }
+    int best = 0;                                            // S(L, 0) = 0 is always scouted
+    for (int i = 1; i <= L; ++i) {
+        const int ab = ac[i - 1];
+        int h = kNeg, sl = kNeg;                             // H, S of the cell to the left
+#pragma unroll
+        for (int x = 0; x < W; ++x) {
+            const int dg = S[x] + ((R[x] == ab) ? sc.ma : sc.mi);
+            const int vu = (x + 1 < W) ? max(V[x + 1] + sc.ge, S[x + 1] + sc.go) : kNeg;
+            h = max(h + sc.ge, sl + sc.go);
+            int s = max(dg, max(vu, h)), v = vu;
+            if (CHECK) {
+                const int j = i + d0 + x - E;
+                if (j == 0) { s = 0; v = kNeg; h = kNeg; }              // the adapter head hangs off
+                else if (j < 0 || j > len) { s = kNeg; v = kNeg; h = kNeg; }
+                if (j == len) best = max(best, s);                      // last column
+            }
+            S[x] = s;
+            V[x] = v;
+            sl = s;
+        }
+#pragma unroll
+        for (int x = 0; x + 1 < W; ++x) R[x] = R[x + 1];
+        const int jn = i + 1 + d0 + E;
+        R[W - 1] = (!CHECK || (jn >= 1 && jn <= len)) ? rd[jn - 1] : 7;
+    }
+#pragma unroll
+    for (int x = 0; x < W; ++x) {                            // last row, j < len
+        const int j = L + d0 + x - E;
+        if (!CHECK || (j >= 0 && j < len)) best = max(best, S[x]);
+    }
+    return best;
+}
+
+template <int E>
+__global__ __launch_bounds__(256) void k_seed_band(const int4 *task, int32_t n_task, const uint8_t *codes,
+                                                   const int64_t *v_off, const int32_t *v_len, const uint8_t *adp,
+                                                   const int32_t *adp_off, const int32_t *adp_len, pcabi::Scoring sc,
+                                                   int32_t *bound, int64_t n) {
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (t >= n_task) return;
     const int4 tk = task[t];
-    const int L = info[tk.y] & 255;
-    const int pad = RPL - L;
-    const uint8_t *ac = adp + adp_off[tk.y] - pad;
-    uint32_t tab[RPL];
-#pragma unroll
-    for (int i = 0; i < RPL; ++i) {
-        uint32_t f = 0;
-        if (i >= pad) {
-            const int b = ac[i];
-#pragma unroll
-            for (int c = 0; c < 5; ++c) f |= ((uint32_t)((c == b) ? sc.ma : sc.mi) & 63u) << (6 * c);
-        }
-        tab[i] = f;
-    }
-    int S[RPL], H[RPL];
-#pragma unroll
-    for (int i = 0; i < RPL; ++i) { S[i] = 0; H[i] = kNeg; }
-    int best = 0;                                        // S(L, 0)
-    const uint8_t *w = codes + v_off[tk.x] + tk.z;
-    const int nw = tk.w;
-    for (int j = 0; j < nw; ++j) {
-        const int sh = 6 * min((int)w[j], 4);
-        int diag = 0, up = 0, V = kNeg;                  // row 0: S = 0
-#pragma unroll
-        for (int i = 0; i < RPL; ++i) {
-            const int sub = __builtin_amdgcn_sbfe((int)tab[i], sh, 6);
-            const int d = diag + sub;
-            const int h = max(H[i] + sc.ge, S[i] + sc.go);
-            V = max(V + sc.ge, up + sc.go);
-            const int s = max(d, max(h, V));
-            diag = S[i];
-            S[i] = s;
-            H[i] = h;
-            up = s;
-        }
-        best = max(best, S[RPL - 1]);                    // last row
-    }
-#pragma unroll
-    for (int i = 0; i < RPL; ++i) best = max(best, S[i]);   // last column
+    const int L = adp_len[tk.y];
+    const int len = v_len[tk.x];
+    const int d0 = tk.z;
+    const uint8_t *rd = codes + v_off[tk.x];
+    const uint8_t *ac = adp + adp_off[tk.y];
+    const bool inside = d0 - E >= 1 && d0 + E + L + 1 < len;
+    const int best = inside ? band_best<E, false>(rd, len, ac, L, d0, sc) : band_best<E, true>(rd, len, ac, L, d0, sc);
     atomicMax(&bound[(int64_t)tk.y * n + tk.x], best);
 }
 
@@ -284,8 +354,10 @@ struct State {
     pcabi::Scoring sc{0, 0, 0, 0};
     bool planned = false, ok = false;
     double cost_seed = 0.0, cost_filter = 0.0;    // per read position (model units)
+    int band[kCls] = {0, 0};                      // E of each class
+    size_t lds_bytes = 0;
     ScanArgs a{};
-    Buf bits, head, ent, info, adp, adp_off, task, cnt, bound, thr, cands, ccnt;
+    Buf tabs, adp, adp_off, adp_len, task, cnt, bound, thr, cands, ccnt;
     int64_t cap = 0, ccap = 0;
 };
 
@@ -294,22 +366,22 @@ void destroy(State *s) { delete s; }
 
 namespace {
 // Cost model per read position (VALU slots / issue rate, tools/valu_microbench.hip): the packed
-// filter spends 4 packed ops per cell (rate 0.23), a window cell ~8 ops (~0.3), the scan ~60
+// filter spends 4 packed ops per cell (rate 0.23), a band cell ~11 ops (~0.3), the scan ~60
 // (~0.4) per position, and a random position hits a K-probe with probability 1 / 4^K.
-constexpr double kFilterCell = 4.0 / 0.23, kWindowCell = 8.0 / 0.3, kScanPos = 60.0 / 0.4;
+constexpr double kFilterCell = 4.0 / 0.23, kBandCell = 11.0 / 0.3, kScanPos = 60.0 / 0.4;
 
 int plan(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hlen, int32_t n_adp,
          const std::vector<int> &fb_rows, const pcabi::Scoring &sc, double threshold) {
     s->planned = true;
     s->ok = false;
-    if (!(threshold > 0.0) || sc.ma > 31 || sc.ma < -32 || sc.mi > 31 || sc.mi < -32 || sc.go >= 0 || sc.ge >= 0)
-        return 0;
+    if (!(threshold > 0.0) || sc.go >= 0 || sc.ge >= 0 || n_adp >= (1 << 22)) return 0;
     const double th = (threshold - 1e-5) / 100.0;
     if (th <= 0.0 || th > 1.0) return 0;
     std::vector<std::vector<std::vector<int32_t>>> lists(kNK);
-    std::vector<int32_t> info((size_t)n_adp, 0);
+    std::vector<int32_t> es((size_t)n_adp, -1);
     std::vector<int32_t> thr((size_t)n_adp, INT32_MAX);   // not under the filter: the caller adds them
     double filt = 0.0, seed = kScanPos;
+    int e_lo = kMaxE + 1, e_hi = -1;
     for (int32_t a = 0; a < n_adp; ++a) {
         if (fb_rows[a] <= 0) continue;                 // not under the filter: always a candidate
         const int L = hlen[a];
@@ -319,13 +391,14 @@ int plan(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hl
         const int T = pcabi::sf::filter_threshold(L, threshold, sc);
         if (T <= pcabi::sf::NEG16) return 0;
         const int e = (int)std::floor((double)L * (1.0 - th) / th + 1e-9);
-        if (e > 200) return 0;
+        if (e > kMaxE) return 0;
         const int plen = L / (e + 1);
         const int K = std::min(kMaxK, plen);
         if (K < kMinK) return 0;
-        const int cls = L <= kClsRows[0] ? 0 : 1;
-        info[a] = L | (e << 8) | (cls << 16);
+        es[a] = e;
         thr[a] = T;
+        e_lo = std::min(e_lo, e);
+        e_hi = std::max(e_hi, e);
         filt += kFilterCell * fb_rows[a];
         auto &lk = lists[K - kMinK];
         if (lk.empty()) lk.resize((size_t)1 << (2 * K));
@@ -333,72 +406,121 @@ int plan(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hl
             const int o = p * plen;
             uint32_t code = 0;
             for (int t = 0; t < K; ++t) code = (code << 2) | hcodes[hoff[a] + o + t];
-            lk[code].push_back((a << 8) | o);
-            seed += kWindowCell * (double)(L + 2 * e) * kClsRows[cls] / (double)((size_t)1 << (2 * K));
+            lk[code].push_back((a << 9) | o);   // the class bit (8) is set below
         }
     }
-    s->cost_seed = seed;
-    s->cost_filter = filt;
-    // device tables
+    if (e_hi < 0) return 0;
+    // the merged K = 8 table: an 8-mer lists the entries of every probe it extends
+    {
+        std::vector<std::vector<int32_t>> merged((size_t)1 << 16);
+        for (int kk = 0; kk < kNK; ++kk) {
+            if (lists[kk].empty()) continue;
+            const int sh = 2 * (kMaxK - (kMinK + kk));
+            for (uint32_t c = 0; c < (1u << 16); ++c)
+                for (int32_t x : lists[kk][c >> sh]) merged[c].push_back(x);
+        }
+        s->a.min_k = kMaxK;
+        for (int kk = 0; kk < kNK - 1; ++kk)
+            if (!lists[kk].empty()) s->a.min_k = std::min(s->a.min_k, kMinK + kk);
+        lists[kNK - 1].swap(merged);
+    }
+    s->band[0] = std::max(1, e_lo);
+    s->band[1] = std::max(s->band[0], e_hi);
+    std::vector<int32_t> cls((size_t)n_adp, 0);
+    for (int32_t a = 0; a < n_adp; ++a) cls[a] = es[a] > s->band[0] ? 1 : 0;
+    // LDS image: bitmaps of the present K, per-dword rank (probes before the dword), the probe
+    // entry ranges, the entries
     std::vector<uint32_t> bits;
-    std::vector<int32_t> head, ent;
+    std::vector<uint16_t> estart;
+    std::vector<int32_t> ent;
     ScanArgs &A = s->a;
     for (int kk = 0; kk < kNK; ++kk) {
         A.bits_off[kk] = -1;
-        A.head_off[kk] = 0;
         if (lists[kk].empty()) continue;
         const size_t nc = lists[kk].size();
+        const int K = kMinK + kk;
         A.bits_off[kk] = (int32_t)bits.size();
-        A.head_off[kk] = (int64_t)head.size();
         bits.resize(bits.size() + std::max<size_t>(nc / 32, 1), 0u);
         for (size_t c = 0; c < nc; ++c) {
-            head.push_back((int32_t)ent.size());
-            if (!lists[kk][c].empty()) bits[A.bits_off[kk] + c / 32] |= 1u << (c % 32);
-            for (int32_t x : lists[kk][c]) ent.push_back(x);
+            if (lists[kk][c].empty()) continue;
+            bits[A.bits_off[kk] + c / 32] |= 1u << (c % 32);
+            estart.push_back((uint16_t)ent.size());
+            for (int32_t x : lists[kk][c]) {
+                const int a = x >> 9;
+                ent.push_back(x | (cls[a] << 8));
+                if (kk == kNK - 1)                     // the merged table: each random hit costs a band
+                    seed += kBandCell * (double)hlen[a] * (2.0 * s->band[cls[a]] + 1.0) / (double)((size_t)1 << (2 * K));
+            }
+            if (ent.size() >= (size_t)kMaxEnt) return 0;
         }
-        head.push_back((int32_t)ent.size());
     }
     if (ent.empty()) return 0;
-    A.n_bits = (int32_t)bits.size();
-    std::vector<int32_t> aoff((size_t)n_adp);
+    estart.push_back((uint16_t)ent.size());
+    std::vector<uint16_t> rank(bits.size());
+    uint32_t run = 0;
+    for (size_t d = 0; d < bits.size(); ++d) {
+        rank[d] = (uint16_t)run;
+        run += (uint32_t)__builtin_popcount(bits[d]);
+    }
+    std::vector<uint32_t> img(bits);
+    auto append16 = [&](const std::vector<uint16_t> &v) {
+        const int32_t off = (int32_t)img.size();
+        img.resize(img.size() + (v.size() + 1) / 2, 0u);
+        std::copy(v.begin(), v.end(), reinterpret_cast<uint16_t *>(img.data() + off));
+        return off;
+    };
+    A.rank_off = append16(rank);
+    A.estart_off = append16(estart);
+    A.ent_off = (int32_t)img.size();
+    for (int32_t x : ent) img.push_back((uint32_t)x);
+    A.tab_dw = (int32_t)img.size();
+    s->lds_bytes = 4 * img.size();
+    if (s->lds_bytes + sizeof(Stage) > (size_t)kLdsMax) return 0;
+    s->cost_seed = seed;
+    s->cost_filter = filt;
+    std::vector<int32_t> aoff((size_t)n_adp), alen((size_t)n_adp);
     int32_t tot = 0;
-    for (int32_t a = 0; a < n_adp; ++a) { aoff[a] = tot; tot += std::max(hlen[a], 0); }
-    if (int rc = s->bits.ensure(4 * bits.size())) return rc;
-    if (int rc = s->head.ensure(4 * head.size())) return rc;
-    if (int rc = s->ent.ensure(4 * ent.size())) return rc;
-    if (int rc = s->info.ensure(4 * info.size())) return rc;
-    if (int rc = s->adp.ensure((size_t)tot + 2 * kMaxL)) return rc;
+    for (int32_t a = 0; a < n_adp; ++a) {
+        aoff[a] = tot;
+        alen[a] = std::max(hlen[a], 0);
+        tot += alen[a];
+    }
+    std::vector<uint8_t> flat((size_t)tot + 16, 0);
+    for (int32_t a = 0; a < n_adp; ++a) std::copy(hcodes + hoff[a], hcodes + hoff[a] + alen[a], flat.begin() + aoff[a]);
+    if (int rc = s->tabs.ensure(4 * img.size())) return rc;
+    if (int rc = s->adp.ensure(flat.size())) return rc;
     if (int rc = s->adp_off.ensure(4 * aoff.size())) return rc;
+    if (int rc = s->adp_len.ensure(4 * alen.size())) return rc;
     if (int rc = s->cnt.ensure(4 * kCls)) return rc;
     if (int rc = s->thr.ensure(4 * thr.size())) return rc;
     if (int rc = s->ccnt.ensure(8)) return rc;
-    SD_TRY(hipMemcpy(s->thr.p, thr.data(), 4 * thr.size(), hipMemcpyHostToDevice));
-    // kMaxL bytes before the first adapter: the window kernel forms addresses of up to RPL - L
-    // bytes before an adapter (padding rows it never reads)
-    std::vector<uint8_t> flat((size_t)tot + 2 * kMaxL, 0);
-    for (int32_t a = 0; a < n_adp; ++a)
-        std::copy(hcodes + hoff[a], hcodes + hoff[a] + std::max(hlen[a], 0), flat.begin() + kMaxL + aoff[a]);
-    SD_TRY(hipMemcpy(s->bits.p, bits.data(), 4 * bits.size(), hipMemcpyHostToDevice));
-    SD_TRY(hipMemcpy(s->head.p, head.data(), 4 * head.size(), hipMemcpyHostToDevice));
-    SD_TRY(hipMemcpy(s->ent.p, ent.data(), 4 * ent.size(), hipMemcpyHostToDevice));
-    SD_TRY(hipMemcpy(s->info.p, info.data(), 4 * info.size(), hipMemcpyHostToDevice));
-    SD_TRY(hipMemcpy((uint8_t *)s->adp.p, flat.data(), flat.size(), hipMemcpyHostToDevice));
+    SD_TRY(hipMemcpy(s->tabs.p, img.data(), 4 * img.size(), hipMemcpyHostToDevice));
+    SD_TRY(hipMemcpy(s->adp.p, flat.data(), flat.size(), hipMemcpyHostToDevice));
     SD_TRY(hipMemcpy(s->adp_off.p, aoff.data(), 4 * aoff.size(), hipMemcpyHostToDevice));
-    A.bits = (const uint32_t *)s->bits.p;
-    A.head = (const int32_t *)s->head.p;
-    A.ent = (const int32_t *)s->ent.p;
-    A.info = (const int32_t *)s->info.p;
+    SD_TRY(hipMemcpy(s->adp_len.p, alen.data(), 4 * alen.size(), hipMemcpyHostToDevice));
+    SD_TRY(hipMemcpy(s->thr.p, thr.data(), 4 * thr.size(), hipMemcpyHostToDevice));
+    A.tabs = (const uint32_t *)s->tabs.p;
     A.cnt = (int32_t *)s->cnt.p;
     s->ok = true;
     return 0;
 }
 
-template <int RPL>
-void launch_window(const State *s, int32_t cnt, int c, const uint8_t *codes, const int64_t *v_off,
-                   const pcabi::Scoring &sc, int64_t n, hipStream_t st) {
-    hipLaunchKernelGGL(k_seed_window<RPL>, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st,
-                       (const int4 *)s->task.p + c * s->cap, cnt, codes, v_off, (const uint8_t *)s->adp.p + kMaxL,
-                       (const int32_t *)s->adp_off.p, (const int32_t *)s->info.p, sc, (int32_t *)s->bound.p, n);
+void launch_band(const State *s, int E, int32_t cnt, int c, const uint8_t *codes, const int64_t *v_off,
+                 const int32_t *v_len, const pcabi::Scoring &sc, int64_t n, hipStream_t st) {
+    const dim3 grid((unsigned)((cnt + 255) / 256));
+    const int4 *task = (const int4 *)s->task.p + c * s->cap;
+    const uint8_t *adp = (const uint8_t *)s->adp.p;
+    const int32_t *aoff = (const int32_t *)s->adp_off.p, *alen = (const int32_t *)s->adp_len.p;
+    int32_t *bound = (int32_t *)s->bound.p;
+    switch (E) {
+#define C(X)                                                                                                   \
+    case X:                                                                                                    \
+        hipLaunchKernelGGL(k_seed_band<X>, grid, dim3(256), 0, st, task, cnt, codes, v_off, v_len, adp, aoff, \
+                           alen, sc, bound, n);                                                               \
+        break;
+        C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8) C(9) C(10) C(11) C(12) C(13) C(14) C(15)
+#undef C
+    }
 }
 }  // namespace
 
@@ -407,7 +529,7 @@ void launch_window(const State *s, int32_t cnt, int c, const uint8_t *codes, con
 // apply. Returns 1 when done, 0 when seeds do not apply (the caller runs the score filter), < 0
 // on error. Done: cands != nullptr receives the filtered pairs whose bound reaches their
 // threshold, as sorted (a << 32 | read) keys (no bound array leaves the device); otherwise s16
-// (int16, a * n + read) holds every bound.
+// (int16, a * n + read) holds every bound (-8192: no seed).
 int bounds(State *s, const void *adps_key, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hlen,
            int32_t n_adp, const std::vector<int> &fb_rows, const uint8_t *codes, const int64_t *v_off,
            const int32_t *v_len, int64_t n, const pcabi::Scoring &sc, double threshold, int mode, int16_t *s16,
@@ -439,8 +561,8 @@ int bounds(State *s, const void *adps_key, const uint8_t *hcodes, const int32_t 
         A.task = (int4 *)s->task.p;
         A.cap = s->cap;
         SD_TRY(hipMemsetAsync(A.cnt, 0, 4 * kCls, st));
-        const unsigned grid = (unsigned)std::min<int64_t>(n, 8192);
-        hipLaunchKernelGGL(k_seed_scan, dim3(grid), dim3(256), 0, st, A);
+        const unsigned grid = (unsigned)std::min<int64_t>(n, 2048);
+        hipLaunchKernelGGL(k_seed_scan, dim3(grid), dim3(256), s->lds_bytes, st, A);
         SD_TRY(hipGetLastError());
         int32_t cnt[kCls];
         SD_TRY(hipMemcpyAsync(cnt, A.cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
@@ -456,8 +578,9 @@ int bounds(State *s, const void *adps_key, const uint8_t *hcodes, const int32_t 
             continue;
         }
         SD_TRY(hipMemsetD32Async((hipDeviceptr_t)s->bound.p, pcabi::sf::NEG16, (size_t)n * n_adp, st));
-        if (cnt[0]) launch_window<32>(s, cnt[0], 0, codes, v_off, sc, n, st);
-        if (cnt[1]) launch_window<64>(s, cnt[1], 1, codes, v_off, sc, n, st);
+        for (int c = 0; c < kCls; ++c)
+            if (cnt[c]) launch_band(s, s->band[c], cnt[c], c, codes, v_off, v_len, sc, n, st);
+        SD_TRY(hipGetLastError());
         const int64_t tot = n * (int64_t)n_adp;
         const unsigned grid_all = (unsigned)((tot + 255) / 256);
         if (!cands) {
