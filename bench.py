@@ -767,7 +767,8 @@ def run_e2e(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapters):
                                                       args.middle_threshold),
                        'reads_per_gpu': n, 'adapter_sets': len(sets), 'scoring': list(sc),
                        'parallelism': 'dp%d (read shards)' % world},
-            'breakdown_ms_per_step': {k: round(1e3 * v / args.steps, 2) for k, v in acc.items()},
+            'breakdown_ms_per_step': dict({k: round(1e3 * v / args.steps, 2) for k, v in acc.items()},
+                                          other=round(1e3 * (step_s - sum(acc.values()) / args.steps), 2)),
             'input_MB_per_s': round(in_bytes / step_s / 1e6, 1),
             'output_bytes': out_bytes,
             'cpu_baseline': None,

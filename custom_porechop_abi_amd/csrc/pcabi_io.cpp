@@ -25,13 +25,19 @@
 // reads, optional gzip.
 #include <fcntl.h>
 #include <sys/mman.h>
+#include <sys/uio.h>
 #include <sys/stat.h>
 #include <unistd.h>
 #include <zlib.h>
 
 #include <algorithm>
+#include <cerrno>
 #include <cstdlib>
+#include <memory>
+#include <mutex>
+#include <new>
 #include <thread>
+#include <unordered_map>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -83,6 +89,63 @@ struct pcabi_fastx {
     std::string fa_name, fa_seq;
 };
 
+// Large batch buffers (>= 64 MB) come from anonymous mappings with transparent huge pages and
+// go back to a small process-wide cache when a batch is freed, so the next batch reuses pages
+// that are already faulted in: first-touch faults and the unmapping of gigabyte buffers cost
+// about as much as the parse itself (4 KB pages: ~400 k faults per 1.6 GB batch).
+namespace {
+namespace bigmem {
+constexpr size_t kBig = 64ull << 20;
+constexpr size_t kCacheMax = 24ull << 30;
+std::mutex mu;
+std::unordered_map<void *, size_t> mapped;          // live and cached blocks -> mapped bytes
+std::vector<std::pair<void *, size_t>> cache;       // free blocks
+size_t cached = 0;
+
+inline size_t round2m(size_t b) { return (b + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1); }
+
+void *get(size_t bytes) {
+    if (bytes < kBig) return ::operator new(bytes);
+    std::lock_guard<std::mutex> g(mu);
+    size_t best = SIZE_MAX, bi = 0;
+    for (size_t i = 0; i < cache.size(); ++i)
+        if (cache[i].second >= bytes && cache[i].second < best) { best = cache[i].second; bi = i; }
+    if (best != SIZE_MAX && best <= 2 * bytes + (256ull << 20)) {
+        void *p = cache[bi].first;
+        cached -= best;
+        cache.erase(cache.begin() + (long)bi);
+        return p;
+    }
+    const size_t m = round2m(bytes);
+    void *p = mmap(nullptr, m, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (p == MAP_FAILED) throw std::bad_alloc();
+#ifdef MADV_HUGEPAGE
+    madvise(p, m, MADV_HUGEPAGE);
+#endif
+    mapped[p] = m;
+    return p;
+}
+
+void put(void *p, size_t bytes) {
+    if (!p) return;
+    if (bytes < kBig) {
+        ::operator delete(p);
+        return;
+    }
+    std::lock_guard<std::mutex> g(mu);
+    const size_t m = mapped.at(p);
+    cache.emplace_back(p, m);
+    cached += m;
+    while (cached > kCacheMax && !cache.empty()) {   // drop the oldest
+        munmap(cache.front().first, cache.front().second);
+        mapped.erase(cache.front().first);
+        cached -= cache.front().second;
+        cache.erase(cache.begin());
+    }
+}
+}  // namespace bigmem
+}  // namespace
+
 // vector whose resize() leaves new elements uninitialised (the batch buffers are written once,
 // in parallel; zero-filling gigabytes first would cost as much as the parse)
 template <typename T>
@@ -92,11 +155,17 @@ struct NoInit : std::allocator<T> {
     NoInit() = default;
     template <typename U>
     NoInit(const NoInit<U> &) {}
+    T *allocate(size_t n) { return static_cast<T *>(bigmem::get(n * sizeof(T))); }
+    void deallocate(T *p, size_t n) noexcept { bigmem::put(p, n * sizeof(T)); }
     template <typename U>
     void construct(U *p) noexcept { ::new ((void *)p) U; }
     template <typename U, typename... A>
     void construct(U *p, A &&...a) { ::new ((void *)p) U(std::forward<A>(a)...); }
 };
+template <typename T, typename U>
+bool operator==(const NoInit<T> &, const NoInit<U> &) { return true; }
+template <typename T, typename U>
+bool operator!=(const NoInit<T> &, const NoInit<U> &) { return false; }
 template <typename T>
 using RawVec = std::vector<T, NoInit<T>>;
 
@@ -363,7 +432,8 @@ int pcabi_fastx_open(const char *path, int raw, pcabi_fastx **out) {
         const int fd = ::open(path, O_RDONLY);
         struct stat st;
         if (fd >= 0 && fstat(fd, &st) == 0 && st.st_size > 0) {
-            void *m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
+            // MAP_POPULATE: the pages of a cached file are mapped in one pass, not fault by fault
+            void *m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
             if (m != MAP_FAILED) {
                 madvise(m, (size_t)st.st_size, MADV_SEQUENTIAL);
                 r->map = m;
@@ -416,7 +486,12 @@ int pcabi_fastx_type(const pcabi_fastx *r) { return r ? r->type : -1; }
 void pcabi_fastx_close(pcabi_fastx *r) {
     if (!r) return;
     if (r->f) gzclose(r->f);
-    if (r->map) munmap(r->map, r->map_len);
+    if (r->map) {
+        // tearing down a gigabyte mapping takes ~0.1 s: off the caller's path
+        void *m = r->map;
+        const size_t n = r->map_len;
+        std::thread([m, n] { munmap(m, n); }).detach();
+    }
     delete r;
 }
 
@@ -549,23 +624,84 @@ int pcabi_reads_views(const pcabi_reads *b, pcabi_reads_view *v) {
 // ---- writer ----------------------------------------------------------------------------------
 namespace {
 
+// Output sink. Plain files are written with writev straight from the batch's buffers (one
+// copy, into the page cache); only text the writer makes itself (numbered names, U for T, FASTA
+// line breaks) is staged in an arena first. gzip / stdout go through a buffer.
 struct Sink {
     FILE *fp = nullptr;
     gzFile gz = nullptr;
+    int fd = -1;
     std::string buf;
+    std::vector<iovec> iov;
+    std::vector<std::unique_ptr<char[]>> arena;
+    size_t arena_left = 0;
+    char *arena_p = nullptr;
     bool ok = true;
     void flush() {
+        if (fd >= 0) {
+            size_t k = 0;
+            while (ok && k < iov.size()) {
+                const int cnt = (int)std::min<size_t>(iov.size() - k, 1024);
+                const ssize_t w = ::writev(fd, iov.data() + k, cnt);
+                if (w < 0) {
+                    if (errno == EINTR) continue;
+                    ok = false;
+                    break;
+                }
+                size_t left = (size_t)w;   // advance past what was written (partial writes)
+                while (left > 0 && k < iov.size()) {
+                    if (left >= iov[k].iov_len) {
+                        left -= iov[k].iov_len;
+                        ++k;
+                    } else {
+                        iov[k].iov_base = (char *)iov[k].iov_base + left;
+                        iov[k].iov_len -= left;
+                        left = 0;
+                    }
+                }
+            }
+            iov.clear();
+            arena.clear();
+            arena_left = 0;
+            return;
+        }
         if (buf.empty()) return;
         if (gz) ok = ok && gzwrite(gz, buf.data(), (unsigned)buf.size()) == (int)buf.size();
         else ok = ok && std::fwrite(buf.data(), 1, buf.size(), fp) == buf.size();
         buf.clear();
     }
+    // bytes that stay valid until the next flush (the batch, string literals)
+    void ref(const char *p, size_t n) {
+        if (n == 0) return;
+        if (fd < 0) {
+            put(p, n);
+            return;
+        }
+        iov.push_back(iovec{const_cast<char *>(p), n});
+        if (iov.size() >= 8192) flush();
+    }
+    // bytes the caller may reuse: copied
     void put(const char *p, size_t n) {
+        if (n == 0) return;
+        if (fd >= 0) {
+            if (n > arena_left) {
+                const size_t sz = std::max<size_t>(n, 1 << 20);
+                arena.emplace_back(new char[sz]);
+                arena_p = arena.back().get();
+                arena_left = sz;
+            }
+            std::memcpy(arena_p, p, n);
+            iov.push_back(iovec{arena_p, n});
+            arena_p += n;
+            arena_left -= n;
+            if (iov.size() >= 8192) flush();
+            return;
+        }
         buf.append(p, n);
         if (buf.size() > (8u << 20)) flush();
     }
     void put(const std::string &s) { put(s.data(), s.size()); }
-    void put(char c) { buf.push_back(c); }
+    void put(char c) { put(&c, 1); }
 };
 
 // Python seq[start:end] with start >= 0 and end possibly negative (counts from the end).
@@ -588,35 +724,39 @@ std::string numbered(const char *name, size_t nn, int k) {
 }
 
 void put_seq(Sink &o, const char *s, size_t n, bool rna, bool fasta) {
-    std::string t(s, n);
-    if (rna)
+    std::string t;
+    if (rna) {   // T -> U (a copy); otherwise the batch's bytes go out as they are
+        t.assign(s, n);
         for (char &c : t)
             if (c == 'T') c = 'U';
+        s = t.data();
+    }
     if (!fasta) {
-        o.put(t);
+        if (rna) o.put(s, n);
+        else o.ref(s, n);
         return;
     }
-    for (size_t p = 0; p < t.size(); p += 70) {   // add_line_breaks_to_sequence(seq, 70)
-        o.put(t.data() + p, std::min<size_t>(70, t.size() - p));
-        o.put('\n');
+    for (size_t p = 0; p < n; p += 70) {   // add_line_breaks_to_sequence(seq, 70)
+        if (rna) o.put(s + p, std::min<size_t>(70, n - p));
+        else o.ref(s + p, std::min<size_t>(70, n - p));
+        o.ref("\n", 1);
     }
 }
 
-void put_record(Sink &o, bool fasta, const std::string &name, const char *s, size_t ns, const char *q, size_t nq,
-                bool rna) {
+// name: the batch's own header bytes (stable) or a numbered copy (own = true)
+void put_record(Sink &o, bool fasta, const char *name, size_t nn, bool own, const char *s, size_t ns,
+                const char *q, size_t nq, bool rna) {
+    o.ref(fasta ? ">" : "@", 1);
+    if (own) o.put(name, nn);
+    else o.ref(name, nn);
+    o.ref("\n", 1);
     if (fasta) {
-        o.put('>');
-        o.put(name);
-        o.put('\n');
         put_seq(o, s, ns, rna, true);
     } else {
-        o.put('@');
-        o.put(name);
-        o.put('\n');
         put_seq(o, s, ns, rna, false);
-        o.put("\n+\n", 3);
-        o.put(q, nq);
-        o.put('\n');
+        o.ref("\n+\n", 3);
+        o.ref(q, nq);
+        o.ref("\n", 1);
     }
 }
 
@@ -631,9 +771,11 @@ extern "C" int pcabi_reads_write(const pcabi_reads *b, const char *path, int app
     if (gz) {
         o.gz = gzopen(path, append ? "ab" : "wb");
         if (!o.gz) return fail(PCABI_E_ARG, std::string("could not write ") + path);
+    } else if (std::strcmp(path, "-") == 0) {
+        o.fp = stdout;
     } else {
-        o.fp = std::strcmp(path, "-") == 0 ? stdout : std::fopen(path, append ? "ab" : "wb");
-        if (!o.fp) return fail(PCABI_E_ARG, std::string("could not write ") + path);
+        o.fd = ::open(path, O_WRONLY | O_CREAT | (append ? O_APPEND : O_TRUNC), 0666);
+        if (o.fd < 0) return fail(PCABI_E_ARG, std::string("could not write ") + path);
     }
     auto format = [&](int64_t i, Sink &o, std::vector<std::pair<int64_t, int64_t>> &rg) {
         if (select && !select[i]) return;
@@ -657,7 +799,7 @@ extern "C" int pcabi_reads_write(const pcabi_reads *b, const char *path, int app
         if (!split) {
             if (untrimmed) { sa = 0; sb = ns; qa = 0; qb = nq; }
             if (sb == sa) return;   // no empty sequences
-            put_record(o, fasta != 0, std::string(name, nn), seq + sa, (size_t)(sb - sa), qual + qa, (size_t)(qb - qa), rna);
+            put_record(o, fasta != 0, name, nn, false, seq + sa, (size_t)(sb - sa), qual + qa, (size_t)(qb - qa), rna);
             return;
         }
         if (discard_middle) return;
@@ -674,7 +816,8 @@ extern "C" int pcabi_reads_write(const pcabi_reads *b, const char *path, int app
         auto emit = [&](int64_t a, int64_t e) {
             if (e - a <= 0 || e - a < min_split_read_size) return;
             ++part;
-            put_record(o, fasta != 0, numbered(name, nn, part), seq + sa + a, (size_t)(e - a), qual + qa + a,
+            const std::string nm = numbered(name, nn, part);
+            put_record(o, fasta != 0, nm.data(), nm.size(), true, seq + sa + a, (size_t)(e - a), qual + qa + a,
                        (size_t)(e - a), rna);
         };
         int64_t pos = 0;
@@ -693,14 +836,14 @@ extern "C" int pcabi_reads_write(const pcabi_reads *b, const char *path, int app
         }
         emit(run, tl);
     };
-    // formatting is cheap next to the write itself (measured: parallel formatting into chunk
-    // buffers was slower than this single pass), so records go straight to the sink
+    // One stream: the page-cache copy is the cost, and writers of one file serialise on its
+    // inode (measured: threads writing disjoint ranges with pwritev were no faster).
     std::vector<std::pair<int64_t, int64_t>> rg;
     for (int64_t i = 0; i < b->n; ++i) format(i, o, rg);
     o.flush();
     const bool ok = o.ok;
     if (o.gz) gzclose(o.gz);
-    else if (o.fp && o.fp != stdout) std::fclose(o.fp);
+    else if (o.fd >= 0) ::close(o.fd);
     else if (o.fp) std::fflush(o.fp);
     return ok ? 0 : fail(PCABI_E_ARG, std::string("write failed: ") + path);
 }

@@ -188,6 +188,7 @@ class FileTrimmer(object):
             n_in += b.n
             n_kept += int(keep.sum()) if keep is not None else b.n
             t = self._tick('write', t)
+        self._tick('parse', t)   # the end-of-file step and the reader's close
         if first:   # empty input: still create the output
             open(out_path, 'wb').close()
         return {'reads_in': n_in, 'reads_kept': n_kept}
