@@ -62,9 +62,10 @@ def parse():
                          '(approx_counter) on 40k sampled read ends')
     ap.add_argument('--compat-seqs', type=int, default=3000, help='sequences of the compat workload')
     ap.add_argument('--barcodes', type=int, default=96, help='barcode sets of the barcodes workload')
-    ap.add_argument('--kit', choices=['pcr96', 'native12'], default='pcr96',
+    ap.add_argument('--kit', choices=['pcr96', 'native12', 'rapid12'], default='pcr96',
                     help='barcodes workload: pcr96 = Barcode 1..96 (forward) sets; native12 = native '
-                         'barcoding, Barcode 1..12 (reverse) + their 68/63 bp full-sequence adapters')
+                         'barcoding, Barcode 1..12 (reverse) + their 68/63 bp full-sequence adapters; rapid12 = '
+                         'Rapid + RBK004, Barcode 1..12 (forward) + their 111 bp full rapid sequences')
     ap.add_argument('--middle-threshold', type=float, default=90.0)
     ap.add_argument('--dist-backend', default='nccl', help='nccl (RCCL over xGMI, default) or gloo (rehearsal of '
                                                            'several ranks sharing one GPU)')
@@ -101,6 +102,7 @@ def main():
 
     # ---- workload (host) ----
     barcodes = args.workload == 'barcodes'
+    kit_n = 2 if args.kit == 'rapid12' else 1      # kit adapter sets ahead of the barcode sets
     if barcodes:
         # BASELINE.json configs[3]: demultiplexing against 96 barcode sets ('Barcode k (forward)',
         # porechop_abi/adapters.py) plus the ligation kit adapters, forward orientation
@@ -112,6 +114,13 @@ def main():
                 [a for a in allsets if a.name.startswith('Barcode ') and a.name.endswith('(reverse)')][:nb] + \
                 [A.make_full_native_barcode_adapter(i) for i in range(1, nb + 1)]
             bc_dir = 'reverse'
+        elif args.kit == 'rapid12':
+            # porechop_abi.py:348-354: Rapid + RBK004 found -> the new full rapid sequences (111 bp)
+            nb = min(args.barcodes, 12)
+            sets = [a for a in allsets if a.name in ('Rapid', 'RBK004_upstream')] + \
+                [a for a in allsets if a.name.startswith('Barcode ') and a.name.endswith('(forward)')][:nb] + \
+                [A.make_new_full_rapid_barcode_adapter(i) for i in range(1, nb + 1)]
+            bc_dir = 'forward'
         else:
             sets = [a for a in allsets if a.name == 'SQK-NSK007'] + \
                 [a for a in allsets if a.name.startswith('Barcode ') and a.name.endswith('(forward)')][:args.barcodes]
@@ -132,8 +141,9 @@ def main():
     t0 = time.time()
     truth = None
     if barcodes:
-        carried = [a for a in sets[1:] if '(full sequence)' in a.name] or sets[1:]
-        reads, truth = synth.make_barcoded_reads(args.reads, [(a.start_sequence[1], a.end_sequence[1]) for a in carried],
+        carried = [a for a in sets[kit_n:] if '(full sequence)' in a.name] or sets[kit_n:]
+        reads, truth = synth.make_barcoded_reads(args.reads, [(a.start_sequence[1], a.end_sequence[1] if a.end_sequence
+                                                               else '') for a in carried],
                                                  args.mean_len, seed=12345 + rank, keep=args.end_size)
     else:
         reads = synth.make_reads(args.reads, args.mean_len, seed=12345 + rank, keep=args.end_size)
@@ -298,7 +308,7 @@ def main():
         call = np.empty(n, np.int32)
         _lib.check(L.pcabi_dev_d2h(call.ctypes.data_as(vp), bc['d_call'], call.nbytes), 'd2h')
         ids = {v: k for k, v in bc['names'].items()}
-        want = np.array([ids.get(sets[1 + t].get_barcode_name(), -2) if t >= 0 else -1 for t in truth.tolist()])
+        want = np.array([ids.get(sets[kit_n + t].get_barcode_name(), -2) if t >= 0 else -1 for t in truth.tolist()])
         checked['calls_equal_synthetic_truth'] = round(float(np.mean(call == want)), 4)
 
     cpu = None
@@ -311,9 +321,10 @@ def main():
         value = world * n * args.steps / elapsed
         prof = load_traffic()
         out = {
-            'metric': ('reads/sec trimmed + demultiplexed (ONT reads x %d barcode sets)' % (len(sets) - 1)
+            'metric': ('reads/sec trimmed + demultiplexed (ONT reads x %d barcode sets)' % (len(sets) - kit_n)
                        if barcodes and args.kit == 'pcr96' else
-                       'reads/sec trimmed + demultiplexed (native barcoding, %d barcodes + full sequences)' % nb
+                       'reads/sec trimmed + demultiplexed (%s barcoding, %d barcodes + full sequences)'
+                       % ('native' if args.kit == 'native12' else 'rapid', nb)
                        if barcodes
                        else 'reads/sec trimmed (100k ONT reads x 50 adapter pairs)'),
             'value': round(value, 1),
@@ -330,7 +341,7 @@ def main():
             'config': {'workload': ('barcode demux (%s): %d reads/GPU x %d barcode sets + SQK-NSK007 (%d start + %d end '
                                     'adapters), start+end windows of %d bp, + per-read trim decisions and barcode '
                                     'calls (determine_barcode, threshold 75, diff 5)'
-                                    % (args.kit, n, len(sets) - 1, n_sa, n_ea, args.end_size)) if barcodes else
+                                    % (args.kit, n, len(sets) - kit_n, n_sa, n_ea, args.end_size)) if barcodes else
                                    ('end-trim: %d reads/GPU x %d adapter sets (%d start + %d end adapters), '
                                     'start+end windows of %d bp, + per-read trim decisions'
                                     % (n, len(sets), n_sa, n_ea, args.end_size)),

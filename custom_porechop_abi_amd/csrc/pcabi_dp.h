@@ -202,9 +202,14 @@ PCABI_HD void open_run(int slt, int same_kind, int t_prev, int p_prev, int &t, i
 //   rd(j)  : read code at column j (1-based), 0..4
 //   adp[s] : adapter code of slot s (1-based; slots off+1..RPL), 0..4
 // ------------------------------------------------------------------------------------------
-template <int RPL, bool AFFINE, typename ReadFn, typename AdpFn>
-PCABI_HD Result align_lane_generic(ReadFn rd, int n, AdpFn adp, int L, const Scoring sc) {
+// CHUNK: as align_lane_packed's (sf::chunk_plan): the end cell only in owned columns
+// [own_lo, own_hi), own_hi < 0 = the read's last chunk.
+template <int RPL, bool AFFINE, bool CHUNK = false, typename ReadFn, typename AdpFn>
+PCABI_HD Result align_lane_generic(ReadFn rd, int n, AdpFn adp, int L, const Scoring sc, int own_lo = 1,
+                                   int own_hi = -1) {
     const int off = RPL - L;
+    const bool fin = !CHUNK || own_hi < 0;
+    const int hi = own_hi < 0 ? n + 1 : own_hi;
     int S[RPL + 1], H[RPL + 1];
     uint32_t SA[RPL + 1], HA[RPL + 1];
 #pragma unroll
@@ -229,7 +234,7 @@ PCABI_HD Result align_lane_generic(ReadFn rd, int n, AdpFn adp, int L, const Sco
 
     for (int j = 1; j <= n; ++j) {
         const int r = rd(j);
-        const bool lastcol = (j == n);
+        const bool lastcol = (j == n) && fin;   // an inner chunk's last column is an inner read column
         int sup = 0, vup = NEG, sdg = 0;
         uint32_t saup = attr_start(j), vaup = 0, sadg = attr_start(j - 1);
         // last-column running state: S-state last type of (i-1, n), V-state run (t, p)
@@ -332,7 +337,7 @@ PCABI_HD Result align_lane_generic(ReadFn rd, int n, AdpFn adp, int L, const Sco
         } else {
             open_run(slt_last, LT_H, ht_last, hp_last, ht, hp);
         }
-        if (ls > best.score) {   // last row, columns 1..n-1 in order; (L, n) ends the last column
+        if (ls > best.score && (!CHUNK || (j >= own_lo && j < hi))) {   // last row, columns 1..n-1 in order; (L, n) ends the last column
             best.score = ls; best.bi = L; best.bj = j;
             int vt = 0, vp = 0;
             if (lastcol) { vt = vt_up; vp = vp_up; }
@@ -354,7 +359,7 @@ PCABI_HD Result align_lane_generic(ReadFn rd, int n, AdpFn adp, int L, const Sco
         }
         slt_last = lt_type;
     }
-    return finish(best, L, n);
+    return finish(best, L, fin ? n : n + 1);
 }
 
 }  // namespace pcabi

@@ -625,38 +625,60 @@ void launch_tiles(const uint8_t *codes, const int64_t *win_off, const int32_t *w
 // Pairs mode over CHUNKS of long reads (middle-scan candidates, pcabi_dp.h sf::chunk_plan): the
 // packed core on (read offset, columns) of the task's read with the end cell restricted to the
 // owned columns. Wave = one adapter, as k_align's pairs mode; results unmerged, one per task.
-template <int RPL, bool AFFINE>
+template <int RPL, bool AFFINE, int KIND>
 __global__ __launch_bounds__(256, PCABI_WAVES) void k_align_chunk(KParams p) {
-    __shared__ __attribute__((aligned(16))) int32_t tab[4 * kTabW * RPL];
-    int32_t *wave_tab = tab + (threadIdx.x >> 6) * kTabW * RPL;
+    __shared__ __attribute__((aligned(16))) int32_t tab[KIND == PACKED ? 4 * kTabW * RPL : 4];
+    int32_t *wave_tab = tab + (KIND == PACKED ? (threadIdx.x >> 6) * kTabW * RPL : 0);
     int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const bool live = wave < p.n_waves;            // dead waves still join the table barrier
     if (!live) wave = p.n_waves - 1;
     const int64_t slot = wave * 64 + (threadIdx.x & 63);
     const int a_local = __builtin_amdgcn_readfirstlane(p.wave_adp[wave]);
     const int L = __builtin_amdgcn_readfirstlane(p.adp_len[a_local]);
-    fill_wave_tab<RPL>(p, a_local, L, wave_tab);
+    if constexpr (KIND == PACKED) fill_wave_tab<RPL>(p, a_local, L, wave_tab);
     const int32_t tw = live ? p.task_win[slot] : -1;
     if (tw < 0) return;
     const int4 ck = p.task_chunk[slot];
     const uint8_t *b = p.codes + p.win_off[tw] + ck.x;
     const int a0 = (int)((uintptr_t)b & 3);
     WindowReader rd(reinterpret_cast<const uint32_t *>(b - a0), 1, 8 * a0);
-    auto tabfn = [&](int rc) { return LdsRow{wave_tab + rc * RPL}; };
-    const pcabi::Result r = pcabi::align_lane_packed<RPL, AFFINE, true>(rd, ck.y, tabfn, L, p.sc, ck.z, ck.w);
+    pcabi::Result r;
+    if constexpr (KIND == PACKED) {
+        auto tabfn = [&](int rc) { return LdsRow{wave_tab + rc * RPL}; };
+        r = pcabi::align_lane_packed<RPL, AFFINE, true>(rd, ck.y, tabfn, L, p.sc, ck.z, ck.w);
+    } else {
+        AdapterRegs<RPL> adp;
+        adp.load(p.adp_pad + (int64_t)a_local * (RPL / 4));
+        r = pcabi::align_lane_generic<RPL, AFFINE, true>(rd, ck.y, adp, L, p.sc, ck.z, ck.w);
+    }
     store_result(p.out, p.out_stride, p.task_out[slot], r);
 }
 
-// Buckets the chunked candidate DP serves: the packed core's (FAST buckets laid out packed, WIDE).
-bool chunkable(int b, bool packed) { return kBuckets[b].kind == WIDE || (kBuckets[b].kind == FAST && packed); }
+// Buckets the chunked candidate DP serves: the packed core's (FAST buckets laid out packed, WIDE)
+// and the generic core's (long adapters).
+bool chunkable(int b, bool packed) {
+    return kBuckets[b].kind == WIDE || kBuckets[b].kind == GENERIC || (kBuckets[b].kind == FAST && packed);
+}
 
 void dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st) {
     const dim3 grid((unsigned)((p.n_waves + 3) / 4));
+    if (kBuckets[b].kind == GENERIC) {
+        switch (kBuckets[b].rpl) {
+#define C(R)                                                                                            \
+    case R:                                                                                             \
+        if (affine) hipLaunchKernelGGL((k_align_chunk<R, true, GENERIC>), grid, dim3(256), 0, st, p);   \
+        else hipLaunchKernelGGL((k_align_chunk<R, false, GENERIC>), grid, dim3(256), 0, st, p);         \
+        break;
+        C(16) C(32) C(64) C(96) C(128)
+#undef C
+        }
+        return;
+    }
     switch (kBuckets[b].rpl) {
-#define C(R)                                                                                   \
-    case R:                                                                                    \
-        if (affine) hipLaunchKernelGGL((k_align_chunk<R, true>), grid, dim3(256), 0, st, p);   \
-        else hipLaunchKernelGGL((k_align_chunk<R, false>), grid, dim3(256), 0, st, p);         \
+#define C(R)                                                                                           \
+    case R:                                                                                            \
+        if (affine) hipLaunchKernelGGL((k_align_chunk<R, true, PACKED>), grid, dim3(256), 0, st, p);   \
+        else hipLaunchKernelGGL((k_align_chunk<R, false, PACKED>), grid, dim3(256), 0, st, p);         \
         break;
     C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32) C(36) C(40) C(44) C(48) C(52) C(56) C(60) C(64)
     C(68) C(72) C(76) C(80) C(84) C(88)
@@ -1500,12 +1522,13 @@ int filtered_first_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_o
                         const MakeTiles &make_tiles, hipStream_t st) {
     const pcabi_adapters *adps = sc->adps;
     const int32_t n_adp = adps->n_adp;
-    std::vector<int> fb;   // filterable buckets, largest first
+    std::vector<int> fb;   // buckets the score filter serves, largest first
     for (int b = 0; b < kNumBuckets; ++b)
         if (adps->count[b] && (kBuckets[b].kind == FAST || kBuckets[b].kind == WIDE) &&
             pcabi::sf::filter_ok(kBuckets[b].rpl, scr))
             fb.push_back(b);
-    if (fb.empty()) return 0;
+    const int seed_mode = middle_seed_mode();
+    if (fb.empty() && !seed_mode) return 0;
     std::stable_sort(fb.begin(), fb.end(), [&](int x, int y) {
         return (int64_t)adps->count[x] * kBuckets[x].rpl > (int64_t)adps->count[y] * kBuckets[y].rpl;
     });
@@ -1522,11 +1545,12 @@ int filtered_first_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_o
     if (!h_start || seeded) {
         if (int rc = sc->s16.ensure(sizeof(int16_t) * (size_t)n * n_adp)) return rc;
         int got = 0;
-        const int mode = middle_seed_mode();
+        const int mode = seed_mode;
         if (mode && (!h_start || seeded)) {
             if (!sc->seed) sc->seed = pcabi_seed::create();
+            // seeds cover every adapter the plan accepts, long (generic-core) ones included
             std::vector<int> rows((size_t)n_adp, 0);
-            for (int b : fb)
+            for (int b = 0; b < kNumBuckets; ++b)
                 for (int32_t id : adps->ids[b]) rows[id] = kBuckets[b].rpl;
             got = pcabi_seed::bounds(sc->seed, adps, adps->hcodes.data(), adps->hoff.data(), adps->hlen.data(),
                                      n_adp, rows, codes, v_off, v_len, n, scr, threshold, h_start ? 2 : mode,
@@ -1535,7 +1559,12 @@ int filtered_first_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_o
         }
         if (h_start && !got) return fail(PCABI_E_DEVICE, "middle scan: seeds stopped applying after round 1");
         seeded = got > 0;
-        if (!seeded) {
+        if (seeded) {
+            for (int b = 0; b < kNumBuckets; ++b)
+                for (int32_t id : adps->ids[b]) filtered[id] = 1;
+        } else if (fb.empty()) {
+            return 0;
+        } else {
             if (int rc = make_tiles()) return rc;
             ForkJoin fj;
             if (int rc = fj.begin(st, fb.size())) return rc;

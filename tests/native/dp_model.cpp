@@ -228,18 +228,36 @@ static void run_packed_chunk(const char *read, int n, const char *adp, int L, pc
     out[4] = r.score; out[5] = r.m; out[6] = r.l1; out[7] = r.l2;
 }
 
+template <int RPL>
+static void run_generic_chunk(const char *read, int n, const char *adp, int L, pcabi::Scoring sc, int own_lo,
+                              int own_hi, int *out) {
+    const int off = RPL - L;
+    auto rd = [&](int j) { return dna5((unsigned char)read[j - 1]); };
+    auto ad = [&](int s) { return dna5((unsigned char)adp[s - off - 1]); };
+    pcabi::Result r = (sc.go != sc.ge)
+        ? pcabi::align_lane_generic<RPL, true, true>(rd, n, ad, L, sc, own_lo, own_hi)
+        : pcabi::align_lane_generic<RPL, false, true>(rd, n, ad, L, sc, own_lo, own_hi);
+    out[0] = r.rs; out[1] = r.re; out[2] = r.as; out[3] = r.ae;
+    out[4] = r.score; out[5] = r.m; out[6] = r.l1; out[7] = r.l2;
+}
+
+// generic != 0: the generic core (long adapters) instead of the packed one
 extern "C" int pcabi_model_align_chunked(const char *read, int n, const char *adp, int L, int ma, int mi, int go,
-                                         int ge, int T, int C, int *out) {
+                                         int ge, int T, int C, int generic, int *out) {
     pcabi::Scoring sc{ma, mi, go, ge};
     if (L <= 0 || n <= 0 || C <= 0) return -1;
     const int rpl = (L + 3) & ~3;
-    if (!pcabi::packed_ok(L, rpl, sc)) return -3;
+    if (!generic && !pcabi::packed_ok(L, rpl, sc)) return -3;
+    if (generic && L > 128) return -3;
     const int D = pcabi::sf::chunk_span(L, T, sc);
     if (D < 0) return -4;
     int n_chunks = 0, best = 0;
     int got[8];
     pcabi::sf::chunk_plan(n, D, C, [&](const pcabi::sf::Chunk &ck) {
-        switch (rpl) {
+        if (generic) {
+            if (L <= 64) run_generic_chunk<64>(read + ck.start, ck.len, adp, L, sc, ck.own_lo, ck.own_hi, got);
+            else run_generic_chunk<128>(read + ck.start, ck.len, adp, L, sc, ck.own_lo, ck.own_hi, got);
+        } else switch (rpl) {
 #define C_(R) case R: run_packed_chunk<R>(read + ck.start, ck.len, adp, L, sc, ck.own_lo, ck.own_hi, got); break;
         C_(4) C_(8) C_(12) C_(16) C_(20) C_(24) C_(28) C_(32) C_(36) C_(40) C_(44) C_(48) C_(52) C_(56) C_(60)
         C_(64) C_(68) C_(72) C_(76) C_(80) C_(84) C_(88)

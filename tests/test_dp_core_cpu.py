@@ -31,7 +31,7 @@ def model():
                                      ctypes.c_int, ctypes.c_int] + [ctypes.c_int] * 4 + [ctypes.c_void_p]
     L.pcabi_model_filter_threshold.argtypes = [ctypes.c_int, ctypes.c_double] + [ctypes.c_int] * 4
     L.pcabi_model_align_chunked.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int] + \
-        [ctypes.c_int] * 6 + [ctypes.c_void_p]
+        [ctypes.c_int] * 7 + [ctypes.c_void_p]
     L.pcabi_model_pid6.restype = ctypes.c_double
     L.pcabi_model_pid6.argtypes = [ctypes.c_int, ctypes.c_int]
     return L
@@ -282,8 +282,9 @@ def test_score_filter_threshold_is_a_lower_bound(model):
     assert checked > 500
 
 
+@pytest.mark.parametrize('core', ['packed', 'generic'])
 @pytest.mark.parametrize('sc', [(3, -6, -5, -2), (2, -1, -1, -1), (1, -1, -3, -1), (5, -4, -8, -6)])
-def test_chunked_candidate_dp(model, sc):
+def test_chunked_candidate_dp(model, sc, core):
     """The middle scan's chunked candidate DP (pcabi_dp.h sf::chunk_plan + align_lane_packed with
     CHUNK): reads split into chunks of C owned columns, each aligned alone, merged in read order.
     Whenever the whole-read best score reaches T (the bound every hit must reach) the merged
@@ -294,7 +295,9 @@ def test_chunked_candidate_dp(model, sc):
     n_hi = n_lo = n_multi = 0
     adps = ['AATGTACTTCGTTCAGTTACGTATTGCT', 'GCAATACGTAACTGAACGAAGT', 'ACGTTTAGGCATTGCA',
             ''.join(rng.choice('ACGT') for _ in range(40)), ''.join(rng.choice('ACGT') for _ in range(64))]
-    for it in range(1500):
+    if core == 'generic':   # long adapters (the 102 / 111 bp full rapid sequences) too
+        adps += [''.join(rng.choice('ACGT') for _ in range(L)) for L in (102, 111)]
+    for it in range(1500 if core == 'packed' else 300):
         a = rng.choice(adps)
         n = rng.choice([rng.randint(1, 60), rng.randint(60, 600), rng.randint(600, 2500)])
         r = ''.join(rng.choice('ACGT') for _ in range(n))
@@ -312,13 +315,13 @@ def test_chunked_candidate_dp(model, sc):
             T = model.pcabi_model_filter_threshold(len(a), thr, *sc)
             if T <= 0:
                 continue
-            rc, whole = _run(model, 'pcabi_model_align_packed', r, a, sc)
+            rc, whole = _run(model, 'pcabi_model_align_packed' if core == 'packed' else 'pcabi_model_align', r, a, sc)
             if rc == -3:
                 continue
             C = rng.choice([1, 3, 17, 64, 200, 1000])
             out = (ctypes.c_int * 8)()
             rb, ab = r.encode(), a.encode()
-            nc = model.pcabi_model_align_chunked(rb, len(rb), ab, len(ab), *sc, T, C, out)
+            nc = model.pcabi_model_align_chunked(rb, len(rb), ab, len(ab), *sc, T, C, int(core == 'generic'), out)
             assert nc > 0, (nc, sc, T, C)
             got = list(out)
             if whole[4] >= T:
@@ -328,7 +331,7 @@ def test_chunked_candidate_dp(model, sc):
             else:
                 assert got[4] < T, (sc, thr, T, C, r, a, got, whole)
                 n_lo += 1
-    assert n_hi > 300 and n_lo > 300 and n_multi > 200, (n_hi, n_lo, n_multi)
+    assert n_hi > 40 and n_lo > 40 and n_multi > 40, (n_hi, n_lo, n_multi)
 
 
 def _mutate_cpu(rng, s, rate):

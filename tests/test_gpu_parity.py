@@ -299,13 +299,16 @@ def test_middle_scan_seeds(gpu_lib, monkeypatch, threshold, scheme):
     """Round 1 from exact k-mer seeds (pcabi_seed.hip, PCABI_MIDDLE_SEEDS=2) vs the oracle's
     masked loop: adapter copies with exactly 0 .. e_max + 2 edits (e_max = the most non-matching
     columns an alignment at the threshold can hold), copies cut at either read end (the adapter
-    hangs off), repeats, N runs, and adapters of 16..64 bp (both window row classes)."""
+    hangs off), repeats, N runs, and adapters of 16..102 bp (both band classes; the 102 bp one
+    runs on the generic core, chunked like the packed one)."""
     from custom_porechop_abi_amd import engine
     L = gpu_lib
     rng = random.Random(int(threshold) * 7 + scheme[0])
     adps = ['AATGTACTTCGTTCAGTTACGTATTGCT', 'GCAATACGTAACTGAACGAAGT', 'ACGTTTAGGCATTGCA',
             _rand_seq(rng, 50, 'ACGT'), _rand_seq(rng, 64, 'ACGT'), _rand_seq(rng, 33, 'ACGT'),
             'TTTTTTTTTTAAAAAAAAAACCCCCGGGGG']
+    if threshold >= 88.0:   # a long adapter (generic core: 102 bp, as the full rapid sequences)
+        adps.append(_rand_seq(rng, 102, 'ACGT'))
     th = threshold / 100.0
     reads = []
     for k in range(240):
