@@ -650,8 +650,37 @@ struct Lay {
         return attr_start(c) | (nd << ATTR_B) | m;
     }
 };
+// Long buckets (88 < RPL <= 128: the 102 / 111 bp full rapid-barcode sequences): the counts no
+// longer fit next to the score, so the DP runs twice with the same scores and tie-break bits --
+// which select the same path in both runs -- and a different payload each time:
+//      pass 0: [ score : 12 (signed) ][ tb : 2 ][ c mod 1024 : 10 ][ nD : 8 ]
+//      pass 1: [ score : 12 (signed) ][ tb : 2 ][ 0 : 10 ][ m : 8 ]
+// A max never decides on the payload (candidates of one max differ in tb), so both passes keep
+// the same winners everywhere, and their attributes merge into one path (align_lane_packed_long).
+template <int RPL, int PASS>
+struct LayL {
+    static constexpr bool WIDE = true;
+    static constexpr int SC_SH = 20;
+    static constexpr int TB_SH = 18;
+    static constexpr int C_SH = 8;
+    static constexpr int32_t TB1 = 1 << TB_SH, TB2 = 2 << TB_SH, TB3 = 3 << TB_SH, TBM = 3 << TB_SH;
+    static constexpr int32_t INC_D = PASS == 0 ? 1 : 0, INC_M = 1;
+    static constexpr int SC_MIN = -(1 << (31 - SC_SH)), SC_MAX = (1 << (31 - SC_SH)) - 1;
+    static PCABI_HD int32_t sc(int v) { return (int32_t)((uint32_t)v << SC_SH); }
+    static PCABI_HD int32_t start(int c) { return PASS == 0 ? (int32_t)(((uint32_t)c & 1023u) << C_SH) : 0; }
+    static PCABI_HD int score(int32_t k) { return k >> SC_SH; }
+    static PCABI_HD int tb(int32_t k) { return (k >> TB_SH) & 3; }
+    static PCABI_HD uint32_t attr(int32_t k) { return (uint32_t)k & ((1u << TB_SH) - 1u); }
+    static PCABI_HD uint32_t to_std(uint32_t a, int bj) {
+        if (PASS == 1) return a & 255u;                         // m
+        const uint32_t nd = a & 255u;
+        const int c = bj - (int)(((uint32_t)bj - (a >> C_SH)) & 1023u);
+        return attr_start(c) | (nd << ATTR_B);
+    }
+};
 constexpr int MAX_RPL = 88;
 constexpr int MAX_L = 88;
+constexpr int MAX_L_LONG = 128;
 // The sentinel NEG (H(., 0), V(0, .)) only ever competes in column 1 (H-extend vs H-open from
 // S(i, 0) = 0) and row 1 (V-extend vs V-open from S(0, j) = 0): it must lose there, NEG + ge <
 // gap_open, and nothing else (after those maxes every value is a real DP value).
@@ -693,6 +722,27 @@ PCABI_HD bool packed_ok_t(int L, const Scoring &s) {
     return lo >= Y::SC_MIN && hi <= Y::SC_MAX;
 }
 
+// Range conditions of the long (two-pass) layout: as packed_ok_t with the 12-bit score field,
+// counts <= 255 and a reported path spanning < 1024 columns.
+PCABI_HD bool long_ok(int L, int rpl, const Scoring &s) {
+    using Y = pk::LayL<128, 0>;
+    if (L < 1 || L > rpl || L > pk::MAX_L_LONG) return false;
+    if (!(s.go < 0 && s.ge < 0)) return false;
+    if (packed_span_bound(L, s) > 1023) return false;
+    const long long smin = (s.go != s.ge) ? (long long)s.go + (long long)(L - 1) * s.ge : (long long)L * s.ge;
+    const long long lo_sub = s.mi < s.ma ? s.mi : s.ma;
+    const long long lo_gap = (long long)s.go + s.ge;
+    long long lo = smin + (lo_gap < lo_sub ? lo_gap : lo_sub);
+    const long long neg = pk::neg_score(s);
+    if (neg + s.ge < lo) lo = neg + s.ge;
+    if (neg < lo) lo = neg;
+    if (s.go < lo) lo = s.go;
+    long long hi = (long long)L * s.ma;
+    if (hi < 0) hi = 0;
+    if (s.ma > hi) hi = s.ma;
+    return lo >= Y::SC_MIN && hi <= Y::SC_MAX;
+}
+
 PCABI_HD bool packed_ok(int L, int rpl, const Scoring &s) {
     switch (rpl) {
 #define PCABI_PK(R) case R: return packed_ok_t<R>(L, s);
@@ -704,9 +754,9 @@ PCABI_HD bool packed_ok(int L, int rpl, const Scoring &s) {
     }
 }
 
-template <int RPL, bool AFFINE>
+template <int RPL, bool AFFINE, typename LAY = pk::Lay<RPL>>
 struct LanePacked {
-    using Y = pk::Lay<RPL>;
+    using Y = LAY;
     int32_t G[RPL + 1];    // S keys with tb cleared, plus the gap-open key: G = S + go
     int32_t HK[RPL + 1];   // H keys, tb = 1 (affine only)
     int bscore, bi, bj, blt, btrail, bprec;
@@ -896,9 +946,8 @@ struct LanePacked {
 // one LDS read + one add instead of a compare + select.
 namespace pk {
 constexpr int TAB_W = 8;
-template <int RPL, typename AdpFn>
+template <int RPL, typename AdpFn, typename Y = Lay<RPL>>
 PCABI_HD int32_t sub_key(int s, int c, const AdpFn &adp, int off, const Scoring &sc) {
-    using Y = Lay<RPL>;
     // the core adds these to G = S + go, so the gap-open key is taken back out here
     if (s <= off) return Y::TB3 - Y::sc(sc.go);
     return (c == adp(s)) ? (Y::sc(sc.ma) + Y::TB3 + Y::INC_M - Y::sc(sc.go))
@@ -910,12 +959,11 @@ PCABI_HD int32_t sub_key(int s, int c, const AdpFn &adp, int off, const Scoring 
 // columns [own_lo, own_hi) may hold the reported end cell, and own_hi < 0 marks the read's last
 // chunk (its last column is the read end); an inner chunk ends on an inner read column, so no
 // last-column cell of it is an alignment end and its tail is reported as not at the read end.
-template <int RPL, bool AFFINE, bool CHUNK = false, typename ReadFn, typename TabFn>
-PCABI_HD Result align_lane_packed(ReadFn &rd, int n, const TabFn &tabfn, int L, const Scoring sc, int own_lo = 1,
-                                  int own_hi = -1) {
-    using Y = pk::Lay<RPL>;
+template <int RPL, bool AFFINE, bool CHUNK = false, typename Y = pk::Lay<RPL>, typename ReadFn, typename TabFn>
+PCABI_HD Best packed_best(ReadFn &rd, int n, const TabFn &tabfn, int L, const Scoring sc, int own_lo, int own_hi,
+                          int &n_fin) {
     // tabfn(r) returns a callable row(s) -> substitution key for read code r
-    LanePacked<RPL, AFFINE> st;
+    LanePacked<RPL, AFFINE, Y> st;
     const int off = RPL - L;
     const int32_t neg = Y::sc(pk::neg_score(sc));
     st.k_ge = Y::sc(sc.ge);
@@ -943,7 +991,7 @@ PCABI_HD Result align_lane_packed(ReadFn &rd, int n, const TabFn &tabfn, int L, 
         else st.template column<decltype(tabfn(r)), false>(tabfn(r), j, L, off);
         r = rn;
     }
-    int n_fin = n;
+    n_fin = n;
     if (CHUNK && own_hi >= 0) {
         st.template column<decltype(tabfn(r)), false, true>(tabfn(r), n, L, off, n >= own_lo && n < hi);
         st.materialize(L);
@@ -955,6 +1003,26 @@ PCABI_HD Result align_lane_packed(ReadFn &rd, int n, const TabFn &tabfn, int L, 
     Best b;
     b.score = st.bscore; b.bi = st.bi; b.bj = st.bj; b.attr = Y::to_std(st.battr, st.bj);
     b.ltype = st.blt; b.trail = st.btrail; b.precd = st.bprec;
+    return b;
+}
+
+template <int RPL, bool AFFINE, bool CHUNK = false, typename ReadFn, typename TabFn>
+PCABI_HD Result align_lane_packed(ReadFn &rd, int n, const TabFn &tabfn, int L, const Scoring sc, int own_lo = 1,
+                                  int own_hi = -1) {
+    int n_fin;
+    const Best b = packed_best<RPL, AFFINE, CHUNK>(rd, n, tabfn, L, sc, own_lo, own_hi, n_fin);
+    return finish(b, L, n_fin);
+}
+
+// Long buckets: pass 0 (c, nD) and pass 1 (m) over the same window (two readers, two tables);
+// the passes end in the same cell with the same trailing run, so one Best carries all three.
+template <int RPL, bool AFFINE, bool CHUNK = false, typename ReadFn, typename TabFn0, typename TabFn1>
+PCABI_HD Result align_lane_packed_long(ReadFn &rd0, ReadFn &rd1, int n, const TabFn0 &tab0, const TabFn1 &tab1,
+                                       int L, const Scoring sc, int own_lo = 1, int own_hi = -1) {
+    int n_fin;
+    Best b = packed_best<RPL, AFFINE, CHUNK, pk::LayL<RPL, 0>>(rd0, n, tab0, L, sc, own_lo, own_hi, n_fin);
+    const Best bm = packed_best<RPL, AFFINE, CHUNK, pk::LayL<RPL, 1>>(rd1, n, tab1, L, sc, own_lo, own_hi, n_fin);
+    b.attr |= bm.attr;
     return finish(b, L, n_fin);
 }
 

@@ -55,7 +55,9 @@ int fail(int code, const std::string &msg) {
 // pk::Lay<RPL > 64>): every multiple of 4 from 68 to 88, for the 65-88 bp adapters (native
 // barcoding "full sequence" adapters) whenever packed_ok holds. GENERIC (guarded core, any
 // scoring): a few sizes, the path for everything else up to 128.
-enum Kind { FAST = 0, GENERIC = 1, PACKED = 2, WIDE = 3 };
+// LONG (two-pass packed core, pk::LayL): 96 / 112 / 128 rows for the 89-128 bp adapters (the
+// 102 / 111 bp full rapid-barcode sequences) whenever pcabi::long_ok holds.
+enum Kind { FAST = 0, GENERIC = 1, PACKED = 2, WIDE = 3, LONG = 4 };
 struct BucketDef {
     int rpl;
     Kind kind;
@@ -64,6 +66,7 @@ constexpr BucketDef kBuckets[] = {
     {4, FAST},  {8, FAST},  {12, FAST}, {16, FAST}, {20, FAST}, {24, FAST}, {28, FAST}, {32, FAST},
     {36, FAST}, {40, FAST}, {44, FAST}, {48, FAST}, {52, FAST}, {56, FAST}, {60, FAST}, {64, FAST},
     {68, WIDE}, {72, WIDE}, {76, WIDE}, {80, WIDE}, {84, WIDE}, {88, WIDE},
+    {96, LONG}, {112, LONG}, {128, LONG},
     {16, GENERIC}, {32, GENERIC}, {64, GENERIC}, {96, GENERIC}, {128, GENERIC}};
 constexpr int kNumBuckets = sizeof(kBuckets) / sizeof(kBuckets[0]);
 constexpr int kMaxRPL = 128;
@@ -75,6 +78,9 @@ int bucket_of(int L, const pcabi::Scoring &sc, bool allow_wide = true) {
     } else if (allow_wide && L <= pcabi::pk::MAX_L) {
         const int rpl = (L + 3) & ~3;
         if (pcabi::packed_ok(L, rpl, sc)) return 16 + (rpl - 68) / 4;
+    } else if (allow_wide && L <= pcabi::pk::MAX_L_LONG) {
+        const int b = L <= 96 ? 22 : (L <= 112 ? 23 : 24);
+        if (pcabi::long_ok(L, kBuckets[b].rpl, sc)) return b;
     }
     for (int b = 0; b < kNumBuckets; ++b)
         if (kBuckets[b].kind == GENERIC && L <= kBuckets[b].rpl) return b;
@@ -184,13 +190,30 @@ __device__ __forceinline__ void fill_wave_tab(const KParams &p, int a_local, int
     __syncthreads();
 }
 
+// The two tables of a long bucket's wave: pass 0 (c, nD) then pass 1 (m), kTabW x RPL each.
+template <int RPL>
+__device__ __forceinline__ void fill_wave_tab_long(const KParams &p, int a_local, int L, int32_t *wave_tab) {
+    const int off = RPL - L;
+    const int lane = threadIdx.x & 63;
+    const uint32_t *ap = p.adp_pad + (int64_t)a_local * (RPL / 4);
+    auto code = [&](int sl) { return (int)((ap[(sl - 1) / 4] >> (8 * ((sl - 1) & 3))) & 0xFFu); };
+    for (int e = lane; e < kTabW * RPL; e += 64) {
+        const int c = e / RPL, srow = e % RPL + 1;
+        wave_tab[e] = pcabi::pk::sub_key<RPL, decltype(code), pcabi::pk::LayL<RPL, 0>>(srow, c, code, off, p.sc);
+        wave_tab[kTabW * RPL + e] =
+            pcabi::pk::sub_key<RPL, decltype(code), pcabi::pk::LayL<RPL, 1>>(srow, c, code, off, p.sc);
+    }
+    __syncthreads();
+}
+
 template <int RPL, bool AFFINE, int KIND>
 __device__ __forceinline__ void run_lane(const KParams &p, int a_local, int64_t w, int64_t out_idx,
                                          int32_t *wave_tab, int64_t tile_off) {
     AdapterRegs<RPL> adp;
-    adp.load(p.adp_pad + (int64_t)a_local * (RPL / 4));
+    if constexpr (KIND != LONG) adp.load(p.adp_pad + (int64_t)a_local * (RPL / 4));
     const int L = __builtin_amdgcn_readfirstlane(p.adp_len[a_local]);
     if constexpr (KIND == PACKED) fill_wave_tab<RPL>(p, a_local, L, wave_tab);
+    if constexpr (KIND == LONG) fill_wave_tab_long<RPL>(p, a_local, L, wave_tab);
     if (w < 0) return;
     const int n = p.win_len[w];
     pcabi::Result r;
@@ -207,6 +230,11 @@ __device__ __forceinline__ void run_lane(const KParams &p, int a_local, int64_t 
         if constexpr (KIND == PACKED) {
             auto tabfn = [&](int rc) { return LdsRow{wave_tab + rc * RPL}; };
             r = pcabi::align_lane_packed<(RPL <= pcabi::pk::MAX_RPL ? RPL : 4), AFFINE>(rd, n, tabfn, L, p.sc);
+        } else if constexpr (KIND == LONG) {
+            WindowReader rd1 = rd;   // the second pass reads the window again from its start
+            auto tab0 = [&](int rc) { return LdsRow{wave_tab + rc * RPL}; };
+            auto tab1 = [&](int rc) { return LdsRow{wave_tab + kTabW * RPL + rc * RPL}; };
+            r = pcabi::align_lane_packed_long<RPL, AFFINE>(rd, rd1, n, tab0, tab1, L, p.sc);
         } else if constexpr (KIND == FAST) {
             r = pcabi::align_lane_fast<RPL, AFFINE>(rd, n, adp, L, p.sc);
         } else {
@@ -229,10 +257,13 @@ __device__ __forceinline__ void run_lane(const KParams &p, int a_local, int64_t 
 // One kernel for both work shapes (uniform branch on p.task_win):
 //  cross: 1-D grid of (window tile of 256, adapter) blocks in XCD-aware order; lane = window
 //  pairs: grid (ceil(n_waves/4)); wave = one adapter, lanes = host-grouped tasks
+template <int KIND, int RPL>
+constexpr int wave_tab_ints() { return KIND == PACKED ? kTabW * RPL : (KIND == LONG ? 2 * kTabW * RPL : 1); }
+
 template <int RPL, bool AFFINE, int KIND>
 __global__ __launch_bounds__(256, PCABI_WAVES) void k_align(KParams p) {
-    __shared__ __attribute__((aligned(16))) int32_t tab[KIND == PACKED ? 4 * kTabW * RPL : 4];
-    int32_t *wave_tab = tab + (KIND == PACKED ? (threadIdx.x >> 6) * kTabW * RPL : 0);
+    __shared__ __attribute__((aligned(16))) int32_t tab[4 * wave_tab_ints<KIND, RPL>()];
+    int32_t *wave_tab = tab + (threadIdx.x >> 6) * wave_tab_ints<KIND, RPL>();
     if (p.task_win == nullptr) {
         // XCD-aware order: workgroups are dealt to the 8 XCDs round-robin, so block b runs on
         // XCD b % 8. Each XCD takes every 8th tile of 256 windows and runs ALL adapters of a
@@ -627,8 +658,8 @@ void launch_tiles(const uint8_t *codes, const int64_t *win_off, const int32_t *w
 // owned columns. Wave = one adapter, as k_align's pairs mode; results unmerged, one per task.
 template <int RPL, bool AFFINE, int KIND>
 __global__ __launch_bounds__(256, PCABI_WAVES) void k_align_chunk(KParams p) {
-    __shared__ __attribute__((aligned(16))) int32_t tab[KIND == PACKED ? 4 * kTabW * RPL : 4];
-    int32_t *wave_tab = tab + (KIND == PACKED ? (threadIdx.x >> 6) * kTabW * RPL : 0);
+    __shared__ __attribute__((aligned(16))) int32_t tab[4 * wave_tab_ints<KIND, RPL>()];
+    int32_t *wave_tab = tab + (threadIdx.x >> 6) * wave_tab_ints<KIND, RPL>();
     int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const bool live = wave < p.n_waves;            // dead waves still join the table barrier
     if (!live) wave = p.n_waves - 1;
@@ -636,6 +667,7 @@ __global__ __launch_bounds__(256, PCABI_WAVES) void k_align_chunk(KParams p) {
     const int a_local = __builtin_amdgcn_readfirstlane(p.wave_adp[wave]);
     const int L = __builtin_amdgcn_readfirstlane(p.adp_len[a_local]);
     if constexpr (KIND == PACKED) fill_wave_tab<RPL>(p, a_local, L, wave_tab);
+    if constexpr (KIND == LONG) fill_wave_tab_long<RPL>(p, a_local, L, wave_tab);
     const int32_t tw = live ? p.task_win[slot] : -1;
     if (tw < 0) return;
     const int4 ck = p.task_chunk[slot];
@@ -646,6 +678,11 @@ __global__ __launch_bounds__(256, PCABI_WAVES) void k_align_chunk(KParams p) {
     if constexpr (KIND == PACKED) {
         auto tabfn = [&](int rc) { return LdsRow{wave_tab + rc * RPL}; };
         r = pcabi::align_lane_packed<RPL, AFFINE, true>(rd, ck.y, tabfn, L, p.sc, ck.z, ck.w);
+    } else if constexpr (KIND == LONG) {
+        WindowReader rd1 = rd;
+        auto tab0 = [&](int rc) { return LdsRow{wave_tab + rc * RPL}; };
+        auto tab1 = [&](int rc) { return LdsRow{wave_tab + kTabW * RPL + rc * RPL}; };
+        r = pcabi::align_lane_packed_long<RPL, AFFINE, true>(rd, rd1, ck.y, tab0, tab1, L, p.sc, ck.z, ck.w);
     } else {
         AdapterRegs<RPL> adp;
         adp.load(p.adp_pad + (int64_t)a_local * (RPL / 4));
@@ -657,7 +694,8 @@ __global__ __launch_bounds__(256, PCABI_WAVES) void k_align_chunk(KParams p) {
 // Buckets the chunked candidate DP serves: the packed core's (FAST buckets laid out packed, WIDE)
 // and the generic core's (long adapters).
 bool chunkable(int b, bool packed) {
-    return kBuckets[b].kind == WIDE || kBuckets[b].kind == GENERIC || (kBuckets[b].kind == FAST && packed);
+    return kBuckets[b].kind == WIDE || kBuckets[b].kind == LONG || kBuckets[b].kind == GENERIC ||
+           (kBuckets[b].kind == FAST && packed);
 }
 
 void dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st) {
@@ -670,6 +708,18 @@ void dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st) {
         else hipLaunchKernelGGL((k_align_chunk<R, false, GENERIC>), grid, dim3(256), 0, st, p);         \
         break;
         C(16) C(32) C(64) C(96) C(128)
+#undef C
+        }
+        return;
+    }
+    if (kBuckets[b].kind == LONG) {
+        switch (kBuckets[b].rpl) {
+#define C(R)                                                                                         \
+    case R:                                                                                          \
+        if (affine) hipLaunchKernelGGL((k_align_chunk<R, true, LONG>), grid, dim3(256), 0, st, p);   \
+        else hipLaunchKernelGGL((k_align_chunk<R, false, LONG>), grid, dim3(256), 0, st, p);         \
+        break;
+        C(96) C(112) C(128)
 #undef C
         }
         return;
@@ -697,7 +747,13 @@ void dispatch(int b, const KParams &p, bool affine, hipStream_t st, bool packed)
     dim3 grid = p.task_win ? dim3((unsigned)((p.n_waves + 3) / 4))
                            : dim3((unsigned)(tiles8 * p.n_adp));
     const BucketDef d = kBuckets[b];
-    if (d.kind == WIDE) {
+    if (d.kind == LONG) {
+        switch (d.rpl) {
+        case 96: launch<96, LONG>(p, affine, grid, st); break;
+        case 112: launch<112, LONG>(p, affine, grid, st); break;
+        case 128: launch<128, LONG>(p, affine, grid, st); break;
+        }
+    } else if (d.kind == WIDE) {
         switch (d.rpl) {
 #define C(R) case R: launch<R, PACKED>(p, affine, grid, st); break;
         C(68) C(72) C(76) C(80) C(84) C(88)
@@ -729,7 +785,7 @@ void dispatch(int b, const KParams &p, bool affine, hipStream_t st, bool packed)
 // Packed-key kernels serve a fast bucket when every adapter in it satisfies the range
 // conditions of pcabi_dp.h packed_ok (any window length).
 bool bucket_packed_ok(int b, const std::vector<int32_t> &lens, const pcabi::Scoring &sc) {
-    if (kBuckets[b].kind == WIDE) return true;   // assigned only when packed_ok holds
+    if (kBuckets[b].kind == WIDE || kBuckets[b].kind == LONG) return true;   // assigned only when packed_ok / long_ok holds
     if (kBuckets[b].kind != FAST || kBuckets[b].rpl > pcabi::pk::MAX_RPL) return false;
     for (int32_t L : lens)
         if (!pcabi::packed_ok(L, kBuckets[b].rpl, sc)) return false;
@@ -1373,9 +1429,9 @@ int adapters_create_impl(const uint8_t *adp_codes, const int32_t *adp_off, const
 
 // A wide (packed-only) bucket serves only scorings its adapters are packed_ok for.
 int wide_ok(const pcabi_adapters *adps, int b, const pcabi::Scoring &sc) {
-    if (kBuckets[b].kind != WIDE) return 0;
+    if (kBuckets[b].kind != WIDE && kBuckets[b].kind != LONG) return 0;
     for (int32_t L : adps->lens[b])
-        if (!pcabi::packed_ok(L, kBuckets[b].rpl, sc))
+        if (kBuckets[b].kind == WIDE ? !pcabi::packed_ok(L, kBuckets[b].rpl, sc) : !pcabi::long_ok(L, kBuckets[b].rpl, sc))
             return fail(PCABI_E_ARG, "adapter table laid out for another scoring (pcabi_adapters_create_scored): "
                                      "rebuild it for this one");
     return 0;

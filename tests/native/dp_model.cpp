@@ -272,3 +272,41 @@ extern "C" int pcabi_model_align_chunked(const char *read, int n, const char *ad
     });
     return n_chunks;
 }
+
+// Long (two-pass) packed core, buckets of 96 / 112 / 128 rows; -3 if long_ok fails
+template <int RPL>
+static void run_long(const char *read, int n, const char *adp, int L, pcabi::Scoring sc, int *out) {
+    const int off = RPL - L;
+    auto rd0 = [&](int j) { return j <= n ? dna5((unsigned char)read[j - 1]) : 4; };
+    auto rd1 = rd0;
+    auto ad = [&](int s) { return s <= off ? pcabi::PAD_CODE : dna5((unsigned char)adp[s - off - 1]); };
+    static thread_local int32_t tab[2][pcabi::pk::TAB_W * 128];
+    for (int c = 0; c < pcabi::pk::TAB_W; ++c)
+        for (int s = 1; s <= RPL; ++s) {
+            tab[0][c * RPL + s - 1] = pcabi::pk::sub_key<RPL, decltype(ad), pcabi::pk::LayL<RPL, 0>>(s, c, ad, off, sc);
+            tab[1][c * RPL + s - 1] = pcabi::pk::sub_key<RPL, decltype(ad), pcabi::pk::LayL<RPL, 1>>(s, c, ad, off, sc);
+        }
+    struct Row {
+        const int32_t *p;
+        int32_t operator()(int s) const { return p[s - 1]; }
+        void quad(int q, int32_t *dst) const { for (int k = 0; k < 4; ++k) dst[k] = p[4 * q + k]; }
+    };
+    auto t0 = [&](int rc) { return Row{tab[0] + rc * RPL}; };
+    auto t1 = [&](int rc) { return Row{tab[1] + rc * RPL}; };
+    pcabi::Result r = (sc.go != sc.ge) ? pcabi::align_lane_packed_long<RPL, true>(rd0, rd1, n, t0, t1, L, sc)
+                                       : pcabi::align_lane_packed_long<RPL, false>(rd0, rd1, n, t0, t1, L, sc);
+    out[0] = r.rs; out[1] = r.re; out[2] = r.as; out[3] = r.ae;
+    out[4] = r.score; out[5] = r.m; out[6] = r.l1; out[7] = r.l2;
+}
+
+extern "C" int pcabi_model_align_long(const char *read, int n, const char *adp, int L, int ma, int mi, int go,
+                                      int ge, int *out) {
+    pcabi::Scoring sc{ma, mi, go, ge};
+    if (L <= 0 || n <= 0) return -1;
+    const int rpl = L <= 96 ? 96 : (L <= 112 ? 112 : 128);
+    if (L > 128 || !pcabi::long_ok(L, rpl, sc)) return -3;
+    if (rpl == 96) run_long<96>(read, n, adp, L, sc, out);
+    else if (rpl == 112) run_long<112>(read, n, adp, L, sc, out);
+    else run_long<128>(read, n, adp, L, sc, out);
+    return 0;
+}

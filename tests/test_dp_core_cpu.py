@@ -22,7 +22,7 @@ def model():
     subprocess.check_call(['g++', '-std=c++17', '-O2', '-shared', '-fPIC', '-o', out,
                            os.path.join(ROOT, 'tests', 'native', 'dp_model.cpp')])
     L = ctypes.CDLL(out)
-    for fn in ('pcabi_model_align', 'pcabi_model_align_fast', 'pcabi_model_align_packed'):
+    for fn in ('pcabi_model_align', 'pcabi_model_align_fast', 'pcabi_model_align_packed', 'pcabi_model_align_long'):
         getattr(L, fn).argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int] + \
             [ctypes.c_int] * 4 + [ctypes.c_void_p]
     L.pcabi_model_align_packed_rpl.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
@@ -348,3 +348,37 @@ def _mutate_cpu(rng, s, rate):
         else:
             out.append(c)
     return ''.join(out)
+
+
+def test_long_two_pass_core(model):
+    """The long buckets' two-pass packed core (pk::LayL, align_lane_packed_long: c / nD in one
+    pass, m in the other, same scores and tie bits) vs the oracle: the reference's 89-111 bp
+    golden rows, then random and tie-heavy reads against 89-128 bp adapters with embedded
+    mutated copies, every scoring scheme that fits."""
+    n_checked = 0
+    for sc, r, a, exp in golden_lib.g1_rows():
+        if not r or not a or not (88 < len(a) <= 128):
+            continue
+        rc, res = _run(model, 'pcabi_model_align_long', r, a, sc)
+        if rc == -3:
+            continue
+        assert rc == 0 and _fmt(res) == exp, (sc, r, a, _fmt(res), exp)
+        n_checked += 1
+    rng = random.Random(77)
+    for it in range(600):
+        sc = rng.choice([(3, -6, -5, -2), (2, -1, -1, -1), (1, -1, -3, -1), (3, -6, -2, -5), (5, -4, -8, -6)])
+        L = rng.choice([89, 96, 97, 102, 111, 112, 113, 128])
+        alph = rng.choice(['ACGT', 'AT', 'ACGTN'])
+        a = ''.join(rng.choice('ACGT') for _ in range(L))
+        n = rng.choice([1, 5, 40, 150, rng.randint(1, 400)])
+        r = ''.join(rng.choice(alph) for _ in range(n))
+        if n > 30 and rng.random() < 0.7:
+            cp = _mutate_cpu(rng, a, rng.choice([0.0, 0.05, 0.15]))
+            p = rng.randint(-20, n)
+            r = (r[:max(p, 0)] + cp[max(-p, 0):] + r[max(p, 0):])[:max(n, 1) + L]
+        rc, res = _run(model, 'pcabi_model_align_long', r, a, sc)
+        if rc == -3:
+            continue
+        assert rc == 0 and list(res) == oracle_lib.align(r, a, sc), (sc, r, a)
+        n_checked += 1
+    assert n_checked > 400

@@ -345,3 +345,41 @@ def test_middle_scan_seeds(gpu_lib, monkeypatch, threshold, scheme):
     got0 = engine.middle_scan(views, adps, scheme, threshold)
     assert L.pcabi_middle_seed_runs() == runs1
     assert np.array_equal(got0, got)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('scheme', SCHEMES)
+def test_long_adapters_two_pass(gpu_lib, scheme):
+    """89-128 bp adapters (the 102 / 111 bp full rapid-barcode sequences among them) on the
+    two-pass long buckets (pk::LayL) in cross mode, vs the oracle: end windows and whole reads
+    carrying mutated copies, cut copies at the read ends, N runs."""
+    from custom_porechop_abi_amd import adapters as A
+    from custom_porechop_abi_amd import engine
+    rng = random.Random(sum(scheme) * 13 + 5)
+    adps = [A.make_new_full_rapid_barcode_adapter(3).start_sequence[1],
+            A.make_old_full_rapid_barcode_adapter(7).start_sequence[1]] + \
+        [_rand_seq(rng, L, 'ACGT') for L in (89, 96, 97, 112, 113, 128)]
+    reads = []
+    for k in range(180):
+        n = rng.choice([1, 30, 150, rng.randint(100, 700)])
+        r = _rand_seq(rng, n, 'ACGT' if rng.random() < 0.8 else 'ACGTN')
+        if rng.random() < 0.7:
+            cp = _mutate(rng, rng.choice(adps), rng.choice([0.0, 0.05, 0.15]))
+            where = rng.random()
+            if where < 0.25:
+                r = cp[rng.randint(0, 30):] + r
+            elif where < 0.5:
+                r = r + cp[:len(cp) - rng.randint(0, 30)]
+            else:
+                p = rng.randint(0, len(r))
+                r = r[:p] + cp + r[p:]
+        reads.append(r)
+    pack = engine.SeqPack(reads)
+    views = pack.views(np.zeros(len(reads), np.int64), pack.lengths)
+    got = engine.align(views, adps, scheme)
+    n = len(reads)
+    exp = oracle_lib.align_many(reads, adps, (np.tile(np.arange(n), len(adps)), np.repeat(np.arange(len(adps)), n)),
+                                scheme)
+    ok = exp[0] != -1
+    assert np.array_equal(got[0], exp[0])
+    assert np.array_equal(got[:, ok], exp[:, ok]), _first_diff(got, exp, reads, adps, n)
