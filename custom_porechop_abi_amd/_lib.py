@@ -113,7 +113,8 @@ def exported_symbols():
             'pcabi_barcode_call_host', 'pcabi_fastx_open', 'pcabi_fastx_type', 'pcabi_fastx_next',
             'pcabi_fastx_close', 'pcabi_fastx_load', 'pcabi_reads_count', 'pcabi_reads_type', 'pcabi_reads_views',
             'pcabi_reads_free', 'pcabi_reads_write', 'check_compatibility', 'pcabi_compat_host',
-            'pcabi_compat_all_vs_all_host', 'pcabi_kmer_count_host', 'pcabi_kmer_approx_host']
+            'pcabi_compat_all_vs_all_host', 'pcabi_kmer_count_host', 'pcabi_kmer_top_host', 'pcabi_gather_host',
+            'pcabi_kmer_approx_host']
 
 
 def check(rc, what):

@@ -39,6 +39,11 @@ def _declare(L):
         L.pcabi_kmer_count_host.restype = i64
         L.pcabi_kmer_approx_host.argtypes = [ctypes.c_int, P, i64, P, P, i64, ctypes.c_int, P, i64, P]
         L.pcabi_kmer_approx_host.restype = ctypes.c_int
+        L.pcabi_kmer_top_host.argtypes = [ctypes.c_int, P, i64, P, P, i64, ctypes.c_int, ctypes.c_float, P, i64, i64,
+                                          i64, P, P, i64]
+        L.pcabi_kmer_top_host.restype = i64
+        L.pcabi_gather_host.argtypes = [P, P, P, i64, P, P]
+        L.pcabi_gather_host.restype = None
         L._kmer_declared = True
     return L
 
@@ -136,9 +141,10 @@ def sample_sequences(batch, nb_sample, cut_size, bottom, seed=0):
         offs[1:] = np.cumsum((ln + 3) & ~3)[:-1]
     total = int(offs[-1] + ln[-1]) if len(take) else 0
     codes = np.full(((total + 3) & ~3) + 16, 4, np.uint8)
-    within = np.arange(int(ln.sum())) - np.repeat(np.cumsum(ln) - ln, ln)     # position inside a sample
-    codes[np.repeat(offs, ln) + within] = batch.codes[np.repeat(batch.code_off[take] + start, ln) + within]
-    return Samples(codes, offs, ln.astype(np.int32))
+    src = np.ascontiguousarray(batch.code_off[take] + start, np.int64)
+    ln32 = ln.astype(np.int32)
+    _declare(lib()).pcabi_gather_host(_p(batch.codes), _p(src), _p(ln32), len(take), _p(codes), _p(offs))
+    return Samples(codes, offs, ln32)
 
 
 def count_kmers(samples, k, threshold, forbidden=(), device=0):
@@ -154,6 +160,26 @@ def count_kmers(samples, k, threshold, forbidden=(), device=0):
     if n < 0:
         check(int(n), 'pcabi_kmer_count_host')
     return km[:n].copy(), cn[:n].astype(np.int64)
+
+
+def count_kmers_top(samples, k, threshold, forbidden=(), top=0, min_count=0, device=0):
+    """count_kmers followed by the cut get_most_frequent (top) or get_solid_kmers (min_count)
+    applies, on the GPU: every k-mer with count >= max(min_count, the top-th largest count),
+    count descending (ties k-mer ascending) -- all the ranking below can keep."""
+    L = _declare(lib())
+    forb = np.array(sorted(set(int(x) for x in forbidden)), np.uint64)
+    cap = max(4096, 4 * int(top))
+    while True:
+        km = np.empty(cap, np.uint64)
+        cn = np.empty(cap, np.uint32)
+        n = L.pcabi_kmer_top_host(device, _p(samples.codes), samples.codes.size, _p(samples.offs), _p(samples.lens),
+                                  len(samples), int(k), float(threshold), _p(forb) if len(forb) else None, len(forb),
+                                  int(top), int(min_count), _p(km), _p(cn), cap)
+        if n < 0:
+            check(int(n), 'pcabi_kmer_top_host')
+        if n <= cap:
+            return km[:n].copy(), cn[:n].astype(np.int64)
+        cap = int(n)
 
 
 def error_count(samples, kmers, k, device=0):
@@ -233,7 +259,11 @@ def run(input_file, output='out.txt', exact_out='', k=16, sl=100, sn=40000, limi
         bottom = False
         for which in ('start', 'end'):
             sample = sample_sequences(batch, sn, sl, bottom, seed=seed + 2 * run_i + (1 if bottom else 0))
-            kmers, counts = count_kmers(sample, k, lct, kmer_set, device)
+            # only the k-mers the cut can keep leave the device (pcabi_kmer_top_host)
+            if solid_km:
+                kmers, counts = count_kmers_top(sample, k, lct, kmer_set, top=0, min_count=solid_km, device=device)
+            else:
+                kmers, counts = count_kmers_top(sample, k, lct, kmer_set, top=limit, device=device)
             if solid_km:
                 top_k, top_c = solid_kmers(kmers, counts, solid_km)
             else:

@@ -596,6 +596,12 @@ int pcabi_fastx_load(const char *path, int raw, pcabi_reads **out) {
 
 void pcabi_reads_free(pcabi_reads *b) { delete b; }
 
+void pcabi_gather_host(const uint8_t *src, const int64_t *src_off, const int32_t *len, int64_t n, uint8_t *dst,
+                       const int64_t *dst_off) {
+    for (int64_t i = 0; i < n; ++i)
+        if (len[i] > 0) std::memcpy(dst + dst_off[i], src + src_off[i], (size_t)len[i]);
+}
+
 int64_t pcabi_reads_count(const pcabi_reads *b) { return b ? b->n : 0; }
 int pcabi_reads_type(const pcabi_reads *b) { return b ? b->type : -1; }
 

@@ -168,6 +168,14 @@ int64_t pcabi_kmer_count_host(int device, const uint8_t *codes, int64_t codes_le
                               const int32_t *seq_len, int64_t n_seq, int k, float lc_threshold,
                               const uint64_t *forbidden_sorted, int64_t n_forbidden, uint64_t *kmers,
                               uint32_t *counts, int64_t cap) {
+    return pcabi_kmer_top_host(device, codes, codes_len, seq_off, seq_len, n_seq, k, lc_threshold, forbidden_sorted,
+                               n_forbidden, -1, 0, kmers, counts, cap);
+}
+
+int64_t pcabi_kmer_top_host(int device, const uint8_t *codes, int64_t codes_len, const int64_t *seq_off,
+                            const int32_t *seq_len, int64_t n_seq, int k, float lc_threshold,
+                            const uint64_t *forbidden_sorted, int64_t n_forbidden, int64_t top, int64_t min_count,
+                            uint64_t *kmers, uint32_t *counts, int64_t cap) {
     if (int rc = check_seqs(codes_len, seq_off, seq_len, n_seq, k)) return rc;
     if (n_forbidden < 0 || cap < 0) return fail(PCABI_E_ARG, "negative count");
     KM_TRY(hipSetDevice(device));
@@ -216,12 +224,50 @@ int64_t pcabi_kmer_count_host(int device, const uint8_t *codes, int64_t codes_le
     if (nruns > 0) KM_TRY(hipMemcpy(&last, d_unique + nruns - 1, sizeof(uint64_t), hipMemcpyDeviceToHost));
     int64_t n_unique = nruns;
     if (nruns > 0 && (last == kSkip || (2 * k < 64 && (last >> (2 * k)) != 0))) --n_unique;   // the skipped positions
-    if (n_unique > cap) return n_unique;
-    if (n_unique) {
-        KM_TRY(hipMemcpy(kmers, d_unique, sizeof(uint64_t) * n_unique, hipMemcpyDeviceToHost));
-        KM_TRY(hipMemcpy(counts, d_counts, sizeof(uint32_t) * n_unique, hipMemcpyDeviceToHost));
+    if (top < 0) {                                     // every k-mer, ascending
+        if (n_unique > cap) return n_unique;
+        if (n_unique) {
+            KM_TRY(hipMemcpy(kmers, d_unique, sizeof(uint64_t) * n_unique, hipMemcpyDeviceToHost));
+            KM_TRY(hipMemcpy(counts, d_counts, sizeof(uint32_t) * n_unique, hipMemcpyDeviceToHost));
+        }
+        return n_unique;
     }
-    return n_unique;
+    if (n_unique == 0) return 0;
+    // count descending (a stable radix sort: equal counts stay k-mer ascending), then only the
+    // prefix that can matter leaves the device
+    uint32_t *d_cnt2;
+    uint64_t *d_km2;
+    if (int rc = m.alloc(&d_cnt2, (size_t)n_unique)) return rc;
+    if (int rc = m.alloc(&d_km2, (size_t)n_unique)) return rc;
+    size_t tmp_pairs = 0;
+    KM_TRY(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp_pairs, d_counts, d_cnt2, d_unique, d_km2,
+                                                        (int)n_unique, 0, 32));
+    void *d_tmp2 = nullptr;
+    if (int rc = m.alloc((char **)&d_tmp2, tmp_pairs)) return rc;
+    KM_TRY(hipcub::DeviceRadixSort::SortPairsDescending(d_tmp2, tmp_pairs, d_counts, d_cnt2, d_unique, d_km2,
+                                                        (int)n_unique, 0, 32));
+    uint32_t thr = (uint32_t)std::max<int64_t>(min_count, 0);
+    if (top > 0 && top <= n_unique) {
+        uint32_t cut = 0;
+        KM_TRY(hipMemcpy(&cut, d_cnt2 + top - 1, sizeof(uint32_t), hipMemcpyDeviceToHost));
+        thr = std::max(thr, cut);
+    }
+    // entries with count >= thr: a binary search over the descending counts
+    int64_t lo = 0, hi = n_unique;   // first index with count < thr lies in [lo, hi]
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) / 2;
+        uint32_t c = 0;
+        KM_TRY(hipMemcpy(&c, d_cnt2 + mid, sizeof(uint32_t), hipMemcpyDeviceToHost));
+        if (c >= thr) lo = mid + 1;
+        else hi = mid;
+    }
+    const int64_t n_out = lo;
+    if (n_out > cap) return n_out;
+    if (n_out) {
+        KM_TRY(hipMemcpy(kmers, d_km2, sizeof(uint64_t) * n_out, hipMemcpyDeviceToHost));
+        KM_TRY(hipMemcpy(counts, d_cnt2, sizeof(uint32_t) * n_out, hipMemcpyDeviceToHost));
+    }
+    return n_out;
 }
 
 int pcabi_kmer_approx_host(int device, const uint8_t *codes, int64_t codes_len, const int64_t *seq_off,

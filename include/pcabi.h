@@ -308,6 +308,17 @@ int64_t pcabi_kmer_count_host(int device, const uint8_t *codes, int64_t codes_le
                               const int32_t *seq_len, int64_t n_seq, int k, float lc_threshold,
                               const uint64_t *forbidden_sorted, int64_t n_forbidden, uint64_t *kmers,
                               uint32_t *counts, int64_t cap);
+/*   pcabi_kmer_top_host : the same counts, sorted by count descending (equal counts k-mer
+ *       ascending), only the entries with count >= max(min_count, the top-th largest count)
+ *       (top <= 0: no rank cut) -- every k-mer get_most_frequent / get_solid_kmers can keep
+ *       (:372-405). Returns the entries written, or the capacity needed when > cap. */
+int64_t pcabi_kmer_top_host(int device, const uint8_t *codes, int64_t codes_len, const int64_t *seq_off,
+                            const int32_t *seq_len, int64_t n_seq, int k, float lc_threshold,
+                            const uint64_t *forbidden_sorted, int64_t n_forbidden, int64_t top, int64_t min_count,
+                            uint64_t *kmers, uint32_t *counts, int64_t cap);
+/* Host gather of byte segments: dst[dst_off[i] .. + len[i]) = src[src_off[i] .. + len[i]). */
+void pcabi_gather_host(const uint8_t *src, const int64_t *src_off, const int32_t *len, int64_t n, uint8_t *dst,
+                       const int64_t *dst_off);
 int pcabi_kmer_approx_host(int device, const uint8_t *codes, int64_t codes_len, const int64_t *seq_off,
                            const int32_t *seq_len, int64_t n_seq, int k, const uint64_t *kmers, int64_t n_kmers,
                            uint64_t *counts);

@@ -57,3 +57,19 @@ def error_count(samples, kmers, k, device=0):
             prev = np.where(live[:, None], cur, prev)
         out.append(int(np.where(best <= 2, 3 - best, 0).sum()))
     return np.array(out, np.int64)
+
+
+def count_kmers_top(samples, k, threshold, forbidden=(), top=0, min_count=0, device=0):
+    """pcabi_kmer_top_host restated: count_kmers, then count descending (ties k-mer ascending),
+    only the entries with count >= max(min_count, the top-th largest count)."""
+    import numpy as np
+    km, cn = count_kmers(samples, k, threshold, forbidden, device)
+    km = np.asarray(km, np.uint64)
+    cn = np.asarray(cn, np.int64)
+    order = np.lexsort((km, -cn))
+    km, cn = km[order], cn[order]
+    thr = max(int(min_count), 0)
+    if 0 < top <= len(cn):
+        thr = max(thr, int(cn[top - 1]))
+    keep = cn >= thr
+    return km[keep], cn[keep]

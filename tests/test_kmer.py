@@ -47,6 +47,7 @@ def test_counter_driver_with_cpu_restatement(idx, tmp_path, monkeypatch):
     from custom_porechop_abi_amd import approx_counter as AC
     from tests import kmer_oracle
     monkeypatch.setattr(AC, 'count_kmers', kmer_oracle.count_kmers)
+    monkeypatch.setattr(AC, 'count_kmers_top', kmer_oracle.count_kmers_top)
     monkeypatch.setattr(AC, 'error_count', kmer_oracle.error_count)
     case = G5[idx]
     if idx not in (0, 4, 5, 7):
