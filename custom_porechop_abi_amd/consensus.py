@@ -69,7 +69,7 @@ def all_vs_all_flags(sequences, device=0):
     L = _declare(lib())
     codes, offs, lens = _pack(sequences)
     n = len(lens)
-    mat = np.full((n, n), -1, np.int32)
+    mat = np.empty((n, n), np.int32) if n >= 2 else np.full((n, n), -1, np.int32)   # the library writes every entry
     if n >= 2:
         p = lambda a: a.ctypes.data_as(ctypes.c_void_p)
         check(L.pcabi_compat_all_vs_all_host(device, p(codes), codes.size, p(offs), p(lens), n, p(mat)),

@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <memory>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -1069,12 +1070,42 @@ namespace {
 
 // Shared body of pcabi_align_host / pcabi_first_hits_host. first_thr != nullptr (cross mode
 // only): out receives the k_first_hit fields (5 x n_win) instead of the raw results.
+// All-vs-all link matrix from the cross product f[a * n + w] (window w as row 0, sequence a as
+// rows): per pair the reference's orientation (row 0 = the longer, ties -> the first argument of
+// consensus.py:90-97, i < j), mirrored; -1 on the diagonal. 32 x 32 tiles through LDS so both
+// the direct and the transposed reads are coalesced.
+__global__ __launch_bounds__(256) void k_orient(const int32_t *f, const int32_t *len, int64_t n, int32_t *mat) {
+    __shared__ int32_t direct[32][33], trans[32][33];
+    const int64_t r0 = (int64_t)blockIdx.y * 32, c0 = (int64_t)blockIdx.x * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8 threads
+    for (int y = ty; y < 32; y += 8) {
+        const int64_t r = r0 + y, c = c0 + tx;
+        direct[y][tx] = (r < n && c < n) ? f[r * n + c] : 0;
+        const int64_t rt = c0 + y, ct = r0 + tx;                 // f[c][r] for the tile, row-wise
+        trans[tx][y] = (rt < n && ct < n) ? f[rt * n + ct] : 0;
+    }
+    __syncthreads();
+    for (int y = ty; y < 32; y += 8) {
+        const int64_t r = r0 + y, c = c0 + tx;
+        if (r >= n || c >= n) continue;
+        int32_t v = -1;
+        if (r != c) {
+            const int64_t i = r < c ? r : c, j = r < c ? c : r;
+            // want f[j * n + i] when len[i] >= len[j], else f[i * n + j]
+            const bool from_j = len[i] >= len[j];
+            const bool j_is_r = (j == r);
+            v = (from_j == j_is_r) ? direct[y][tx] : trans[y][tx];
+        }
+        mat[r * n + c] = v;
+    }
+}
+
 int align_host_impl(int device, const uint8_t *codes, int64_t codes_len, const int64_t *win_off,
                     const int32_t *win_len, int64_t n_win, const uint8_t *adp_codes,
                     const int32_t *adp_off, const int32_t *adp_len, int32_t n_adp,
                     const int32_t *task_win, const int32_t *task_adp, int64_t n_task, int match,
                     int mismatch, int gap_open, int gap_extend, const double *first_thr, int32_t *out,
-                    bool compat = false) {
+                    bool compat = false, bool orient = false) {
     if (device < 0 || device >= 16) return fail(PCABI_E_ARG, "bad device index");
     if (n_win < 0 || n_adp < 0 || n_task < 0) return fail(PCABI_E_ARG, "negative count");
     if (int rc = check_common(adp_len, n_adp)) return rc;
@@ -1208,6 +1239,13 @@ int align_host_impl(int device, const uint8_t *codes, int64_t codes_len, const i
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(out, e.hits.p, sizeof(int32_t) * 5 * (size_t)n_win, hipMemcpyDeviceToHost,
                                e.stream));
+    } else if (orient) {   // compat all-vs-all: n_win == n_adp == n, the matrix comes back
+        if (int rc = e.hits.ensure(sizeof(int32_t) * (size_t)n_res)) return rc;
+        const unsigned tb = (unsigned)((n_win + 31) / 32);
+        hipLaunchKernelGGL(k_orient, dim3(tb, tb), dim3(256), 0, e.stream, (const int32_t *)e.out.p,
+                           (const int32_t *)e.wlen.p, n_win, (int32_t *)e.hits.p);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(out, e.hits.p, sizeof(int32_t) * (size_t)n_res, hipMemcpyDeviceToHost, e.stream));
     } else {
         HIP_TRY(hipMemcpyAsync(out, e.out.p, sizeof(int32_t) * (compat ? 1 : PCABI_NFIELDS) * (size_t)n_res,
                                hipMemcpyDeviceToHost, e.stream));
@@ -2046,7 +2084,7 @@ int pcabi_compat_all_vs_all_host(int device, const uint8_t *codes, int64_t codes
     if (n_seq < 0) return fail(PCABI_E_ARG, "negative count");
     if (n_seq > 46340) return fail(PCABI_E_ARG, "too many sequences for one matrix");
     const int64_t n = n_seq;
-    for (int64_t k = 0; k < n * n; ++k) mat[k] = -1;
+    for (int64_t k = 0; k < n; ++k) mat[k * n + k] = -1;   // every other entry is written below
     if (n < 2) return 0;
     bool cross_ok = true;
     for (int64_t k = 0; k < n; ++k) cross_ok = cross_ok && seq_len[k] >= 1 && seq_len[k] <= kMaxRPL;
@@ -2071,16 +2109,9 @@ int pcabi_compat_all_vs_all_host(int device, const uint8_t *codes, int64_t codes
         aoff[k] = (int32_t)acodes.size();
         acodes.insert(acodes.end(), codes + seq_off[k], codes + seq_off[k] + seq_len[k]);
     }
-    std::vector<int32_t> f((size_t)(n * n));   // f[a * n + w]: window w as row 0, sequence a as rows
-    if (int rc = align_host_impl(device, codes, codes_len, seq_off, seq_len, n, acodes.data(), aoff.data(), seq_len,
-                                 (int32_t)n, nullptr, nullptr, 0, 2, -1, -1, -1, nullptr, f.data(), true))
-        return rc;
-    for (int64_t i = 0; i < n; ++i)
-        for (int64_t j = i + 1; j < n; ++j) {
-            const int32_t v = seq_len[i] >= seq_len[j] ? f[j * n + i] : f[i * n + j];
-            mat[i * n + j] = mat[j * n + i] = v;
-        }
-    return 0;
+    // the cross product f[a * n + w] stays on the device; k_orient writes the matrix
+    return align_host_impl(device, codes, codes_len, seq_off, seq_len, n, acodes.data(), aoff.data(), seq_len,
+                           (int32_t)n, nullptr, nullptr, 0, 2, -1, -1, -1, nullptr, mat, true, true);
 }
 
 int check_compatibility(char *raw_seq1, char *raw_seq2) {
