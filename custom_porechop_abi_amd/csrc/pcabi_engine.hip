@@ -1169,6 +1169,12 @@ int align_host_impl(int device, const uint8_t *codes, int64_t codes_len, const i
             });
     }
     std::vector<int32_t> tw, to, wa;
+    struct CrossLaunch {
+        int b;
+        KParams p;
+        bool packed;
+    };
+    std::vector<CrossLaunch> cross;
     for (int b = 0; b < kNumBuckets; ++b) {
         BucketHost &h = bk[b];
         if (h.len.empty()) continue;
@@ -1199,7 +1205,8 @@ int align_host_impl(int device, const uint8_t *codes, int64_t codes_len, const i
                 p.tiles = (const uint32_t *)e.tiles.p;
                 p.tile_off = (const int64_t *)e.toff.p;
             }
-            if (n_win > 0) dispatch(b, p, affine, e.stream, bucket_packed_ok(b, h.len, sc));
+            // launched below, side by side once every bucket's table is on its way
+            if (n_win > 0) cross.push_back({b, p, bucket_packed_ok(b, h.len, sc)});
         } else {
             tw.clear(); to.clear(); wa.clear();
             for (int k = 0; k < nb; ++k) {
@@ -1230,6 +1237,18 @@ int align_host_impl(int device, const uint8_t *codes, int64_t codes_len, const i
         }
         HIP_TRY(hipGetLastError());
         // bucket buffers are reused across calls only; keep them distinct per bucket
+    }
+    if (!cross.empty()) {
+        // the host bucket tables (bk) outlive these launches: they are read by the copies queued
+        // on e.stream before the fork
+        std::stable_sort(cross.begin(), cross.end(), [&](const CrossLaunch &x, const CrossLaunch &y) {
+            return (int64_t)x.p.n_adp * kBuckets[x.b].rpl > (int64_t)y.p.n_adp * kBuckets[y.b].rpl;
+        });
+        ForkJoin fj;
+        if (int rc = fj.begin(e.stream, cross.size())) return rc;
+        for (size_t k = 0; k < cross.size(); ++k) dispatch(cross[k].b, cross[k].p, affine, fj.at(k), cross[k].packed);
+        if (int rc = fj.end()) return rc;
+        HIP_TRY(hipGetLastError());
     }
     if (first_thr) {
         if (int rc = e.hits.ensure(sizeof(int32_t) * 5 * (size_t)n_win)) return rc;
