@@ -14,6 +14,8 @@ Decisions are the reference's (same kernels and epilogues the parity tests cover
 demultiplexing and verbose output stay with the per-read drivers (porechop_abi.py here).
 """
 import ctypes
+import queue
+import threading
 import time
 
 import numpy as np
@@ -174,24 +176,72 @@ class FileTrimmer(object):
         return trims[0], trims[1], cut_off, cuts, hits, keep
 
     def trim_file(self, in_path, out_path, out_format='fastq', max_reads=200000):
-        """Trim a FASTA / FASTQ(.gz) file batch by batch into out_path. Returns read counts."""
-        n_in = n_kept = 0
-        first = True
+        """Trim a FASTA / FASTQ(.gz) file batch by batch into out_path. Returns read counts.
+
+        Three stages overlap across batches: a reader thread parses the next batch, this thread
+        runs the device work, a writer thread writes the previous batch (in file order). The
+        library's parse, alignment and write calls release the GIL. times: 'parse' / 'write_wait'
+        are this thread's waits, 'write' the writer's own busy time (overlapped)."""
+        counts = {'reads_in': 0, 'reads_kept': 0}
+        pq = queue.Queue(maxsize=2)
+        wq = queue.Queue(maxsize=2)
+        errors = []
+
+        def produce():
+            try:
+                for b in misc.read_batches(in_path, max_reads=max_reads):
+                    pq.put(b)
+                pq.put(None)
+            except BaseException as ex:   # handed to the consumer
+                pq.put(ex)
+
+        def consume_writes():
+            first = True
+            while True:
+                item = wq.get()
+                if item is None:
+                    break
+                if errors:
+                    continue                 # drain after a failure
+                b, st, et, co, cu, keep = item
+                t0 = time.perf_counter()
+                try:
+                    misc.write_reads(b, out_path, out_format, st, et, None, self.min_split, self.discard_middle,
+                                     select=keep, append=not first, cut_arrays=(co, cu))
+                except BaseException as ex:
+                    errors.append(ex)
+                first = False
+                counts['reads_in'] += b.n
+                counts['reads_kept'] += int(keep.sum()) if keep is not None else b.n
+                self.times['write'] = self.times.get('write', 0.0) + time.perf_counter() - t0
+            if first and not errors:     # empty input: still create the output
+                open(out_path, 'wb').close()
+
+        reader = threading.Thread(target=produce, daemon=True)
+        writer = threading.Thread(target=consume_writes, daemon=True)
+        reader.start()
+        writer.start()
         t = time.perf_counter()
-        for b in misc.read_batches(in_path, max_reads=max_reads):
-            t = self._tick('parse', t)
-            st, et, co, cu, _, keep = self.trim(b)
-            t = time.perf_counter()
-            misc.write_reads(b, out_path, out_format, st, et, None, self.min_split, self.discard_middle,
-                             select=keep, append=not first, cut_arrays=(co, cu))
-            first = False
-            n_in += b.n
-            n_kept += int(keep.sum()) if keep is not None else b.n
-            t = self._tick('write', t)
-        self._tick('parse', t)   # the end-of-file step and the reader's close
-        if first:   # empty input: still create the output
-            open(out_path, 'wb').close()
-        return {'reads_in': n_in, 'reads_kept': n_kept}
+        try:
+            while True:
+                b = pq.get()
+                t = self._tick('parse', t)   # waiting for a parsed batch
+                if b is None:
+                    break
+                if isinstance(b, BaseException):
+                    raise b
+                st, et, co, cu, _, keep = self.trim(b)
+                wq.put((b, st, et, co, cu, keep))
+                del b
+                t = time.perf_counter()
+        finally:
+            wq.put(None)
+            writer.join()
+            reader.join()
+        self._tick('write_wait', t)
+        if errors:
+            raise errors[0]
+        return counts
 
     def close(self):
         L = self.L
