@@ -348,8 +348,9 @@ struct Buf {
 };
 
 struct State {
-    // plan cache key
-    const void *adps = nullptr;
+    // plan cache key: the adapters themselves (a table at a reused address may hold others)
+    std::vector<uint8_t> key_codes;
+    std::vector<int32_t> key_len, key_rows;
     double threshold = -1.0;
     pcabi::Scoring sc{0, 0, 0, 0};
     bool planned = false, ok = false;
@@ -535,11 +536,23 @@ int bounds(State *s, const void *adps_key, const uint8_t *hcodes, const int32_t 
            const int32_t *v_len, int64_t n, const pcabi::Scoring &sc, double threshold, int mode, int16_t *s16,
            std::vector<int64_t> *cands, hipStream_t st) {
     if (mode <= 0 || n <= 0) return 0;
-    if (!s->planned || s->adps != adps_key || s->threshold != threshold || s->sc.ma != sc.ma || s->sc.mi != sc.mi ||
-        s->sc.go != sc.go || s->sc.ge != sc.ge) {
+    (void)adps_key;
+    bool same = s->planned && s->threshold == threshold && s->sc.ma == sc.ma && s->sc.mi == sc.mi &&
+                s->sc.go == sc.go && s->sc.ge == sc.ge && (int32_t)s->key_len.size() == n_adp && s->key_rows == fb_rows;
+    for (int32_t a = 0; same && a < n_adp; ++a) same = s->key_len[a] == hlen[a];
+    if (same) {
+        size_t q = 0;
+        for (int32_t a = 0; same && a < n_adp; ++a)
+            for (int32_t i = 0; same && i < hlen[a]; ++i) same = s->key_codes[q++] == hcodes[hoff[a] + i];
+    }
+    if (!same) {
         // a new plan: the old tables may still be read by work queued on `st`
         SD_TRY(hipStreamSynchronize(st));
-        s->adps = adps_key;
+        s->key_len.assign(hlen, hlen + n_adp);
+        s->key_rows = fb_rows;
+        s->key_codes.clear();
+        for (int32_t a = 0; a < n_adp; ++a)
+            s->key_codes.insert(s->key_codes.end(), hcodes + hoff[a], hcodes + hoff[a] + std::max(hlen[a], 0));
         s->threshold = threshold;
         s->sc = sc;
         if (int rc = plan(s, hcodes, hoff, hlen, n_adp, fb_rows, sc, threshold)) {

@@ -383,3 +383,32 @@ def test_long_adapters_two_pass(gpu_lib, scheme):
     ok = exp[0] != -1
     assert np.array_equal(got[0], exp[0])
     assert np.array_equal(got[:, ok], exp[:, ok]), _first_diff(got, exp, reads, adps, n)
+
+
+@pytest.mark.gpu
+def test_middle_scan_seed_plan_follows_adapters(gpu_lib, monkeypatch):
+    """The seed plan is cached per scan; consecutive host-API scans with different adapters of
+    the same lengths (their tables may land at the same address) must each use their own
+    probes: every scan equals the oracle."""
+    from custom_porechop_abi_amd import engine
+    monkeypatch.setenv('PCABI_MIDDLE_SEEDS', '2')
+    rng = random.Random(4242)
+    sc = (3, -6, -5, -2)
+    for trial in range(4):
+        adps = [_rand_seq(rng, L, 'ACGT') for L in (24, 24, 22, 28)]
+        reads = []
+        for k in range(60):
+            r = _rand_seq(rng, rng.randint(300, 3000), 'ACGT')
+            for _ in range(rng.choice([1, 2, 3])):
+                a = _mutate(rng, rng.choice(adps), rng.choice([0.0, 0.04]))
+                p = rng.randint(0, len(r))
+                r = r[:p] + a + r[p:]
+            reads.append(r)
+        pack = engine.SeqPack(reads)
+        views = pack.views(np.zeros(len(reads), np.int64), pack.lengths)
+        got = engine.middle_scan(views, adps, sc, 90.0)
+        exp = oracle_lib.middle_scan_windows(views, adps, sc, 90.0)
+        assert exp.shape[1] > 40
+        order_g = np.lexsort((np.arange(got.shape[1]), got[0]))
+        order_e = np.lexsort((np.arange(exp.shape[1]), exp[0]))
+        assert np.array_equal(got[:, order_g], exp[:, order_e]), trial
