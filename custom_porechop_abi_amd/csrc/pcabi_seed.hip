@@ -22,7 +22,7 @@
 //     largest S_b. Pairs with a bound >= T go to the full attribute DP exactly as after the
 //     filter. The engine re-seeds every later round on the masked reads (N never matches).
 // Kernels (integer work, no MFMA):
-//   k_seed_scan   reads grid-stride over blocks, 4 positions per lane: the 8-mer codes of the
+//   k_seed_scan   reads grid-stride over blocks, 8 positions per lane: the 8-mer codes of the
 //                 positions, and per probe length K (4..8) a bitmap test and a rank into the probe
 //                 entries, all in LDS; hits become (read, adapter, diagonal) tasks per band class,
 //                 staged per block in LDS and appended with one global atomic per chunk;
@@ -66,6 +66,8 @@ constexpr int kMaxEnt = 8192;      // probe entries / distinct probes kept in LD
 constexpr int kBuf = 512;          // staged tasks per block and class
 constexpr int kLdsMax = 64 * 1024; // per block: probe tables + stage
 constexpr int kNeg = -(1 << 20);
+constexpr int kPos = 8;            // read positions per lane and scan step (16 bases loaded)
+constexpr int kNW = 4;             // dwords of bases per lane and step
 
 struct ScanArgs {
     const uint8_t *codes;
@@ -136,7 +138,7 @@ __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
     const uint16_t *rank = reinterpret_cast<const uint16_t *>(lds + a.rank_off);
     const uint16_t *estart = reinterpret_cast<const uint16_t *>(lds + a.estart_off);
     const int32_t *ent = reinterpret_cast<const int32_t *>(lds + a.ent_off);
-    // The block walks its reads (blockIdx.x, + gridDim.x, ...) 1024 positions at a time; the
+    // The block walks its reads (blockIdx.x, + gridDim.x, ...) 2048 positions at a time; the
     // bytes of the next step (and the next read's length / offset) are loaded before the current
     // step is processed, so the global latency hides behind the lookups.
     int64_t k = blockIdx.x, nk = k;
@@ -152,30 +154,35 @@ __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
         }
         return from;
     };
-    auto fetch = [&](const uint8_t *bs, int ln, int p0b, uint32_t (&w)[3]) {
-        const int p0 = p0b + 4 * (int)threadIdx.x;
-        w[0] = w[1] = w[2] = 0x04040404u;
-        if (p0 < ln) {   // bytes p0 .. p0 + 11 from four aligned dwords (>= 16 B tail padding)
+    auto fetch = [&](const uint8_t *bs, int ln, int p0b, uint32_t (&w)[kNW]) {
+        const int p0 = p0b + kPos * (int)threadIdx.x;
+#pragma unroll
+        for (int d = 0; d < kNW; ++d) w[d] = 0x04040404u;
+        if (p0 < ln) {   // bytes p0 .. p0 + 15 from five aligned dwords; past the read they stay
+                         // inside the caller's >= 16 B tail padding (dword-aligned loads)
             const uint8_t *ad = bs + p0;
             const int a0 = (int)((uintptr_t)ad & 3);
             const uint32_t *q = reinterpret_cast<const uint32_t *>(ad - a0);
-            const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3];
-            w[0] = __builtin_amdgcn_alignbyte(d1, d0, a0);
-            w[1] = __builtin_amdgcn_alignbyte(d2, d1, a0);
-            w[2] = __builtin_amdgcn_alignbyte(d3, d2, a0);
+            uint32_t d[kNW + 1];
+#pragma unroll
+            for (int t = 0; t <= kNW; ++t) d[t] = q[t];
+#pragma unroll
+            for (int t = 0; t < kNW; ++t) w[t] = __builtin_amdgcn_alignbyte(d[t + 1], d[t], a0);
         }
     };
     k = next_read(k, len, base);
     if (k < a.n) nk = next_read(k + gridDim.x, nlen, nbase);
     int p0b = 0;
-    uint32_t wn[3];
+    uint32_t wn[kNW];
     if (k < a.n) fetch(base, len, 0, wn);
     int iter = 0;
     while (k < a.n) {                                  // block-uniform: every lane takes part
         const int64_t ck = k;
-        const int clen = len, cp0 = p0b + 4 * (int)threadIdx.x;
-        const uint32_t w[3] = {wn[0], wn[1], wn[2]};
-        p0b += 1024;
+        const int clen = len, cp0 = p0b + kPos * (int)threadIdx.x;
+        uint32_t w[kNW];
+#pragma unroll
+        for (int d = 0; d < kNW; ++d) w[d] = wn[d];
+        p0b += 256 * kPos;
         if (p0b >= len) {                              // on to the next read
             k = nk;
             len = nlen;
@@ -184,24 +191,24 @@ __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
             if (k < a.n) nk = next_read(k + gridDim.x, nlen, nbase);
         }
         if (k < a.n) fetch(base, len, p0b, wn);
-        // 12 bases in two words (SWAR): c24 = their 2-bit codes, first base in the top bits;
-        // vmask bit t = base t is A/C/G/T inside the read (Dna5 codes are 0..4: N has bit 2)
-        uint32_t c24 = 0, vmask = 0;
+        // 16 bases (SWAR): c32 = their 2-bit codes, first base in the top bits; vmask bit t =
+        // base t is A/C/G/T inside the read (Dna5 codes are 0..4: N has bit 2)
+        uint32_t c32 = 0, vmask = 0;
 #pragma unroll
-        for (int d = 0; d < 3; ++d) {
+        for (int d = 0; d < kNW; ++d) {
             const uint32_t c4 = ((w[d] & 0x03030303u) * 0x40100401u) >> 24;
             const uint32_t nb = (((~w[d]) >> 2) & 0x01010101u) * 0x10204080u >> 28;
-            c24 = (c24 << 8) | c4;
+            c32 = (c32 << 8) | c4;
             vmask |= nb << (4 * d);
         }
         const int rem = clen - cp0;
-        vmask &= rem >= 12 ? 0xFFFu : (rem > 0 ? (1u << rem) - 1u : 0u);
+        vmask &= rem >= 16 ? 0xFFFFu : (rem > 0 ? (1u << rem) - 1u : 0u);
         // fast path: every probe is a prefix of the 8-mer at its position, and the K = 8 table
         // holds every 8-mer that extends a probe -- one LDS word per position
         uint32_t hits = 0, slow = 0;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t c8 = (c24 >> (8 - 2 * i)) & 0xFFFFu;
+        for (int i = 0; i < kPos; ++i) {
+            const uint32_t c8 = (c32 >> (16 - 2 * i)) & 0xFFFFu;
             const uint32_t word = lds[a.bits_off[kNK - 1] + (int)(c8 >> 5)];
             const bool full = ((vmask >> i) & 0xFFu) == 0xFFu;
             hits |= (full && ((word >> (c8 & 31)) & 1u)) ? 1u << i : 0u;
@@ -213,7 +220,7 @@ __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
             const int i = __builtin_ctz(fast ? hits : slow);
             if (fast) hits &= hits - 1;
             else slow &= slow - 1;
-            const uint32_t c8 = (c24 >> (8 - 2 * i)) & 0xFFFFu;
+            const uint32_t c8 = (c32 >> (16 - 2 * i)) & 0xFFFFu;
             const int q = cp0 + i;
             const int run = __builtin_ctz(~(vmask >> i));
             for (int kk = fast ? kNK - 1 : 0; kk < (fast ? kNK : kNK - 1); ++kk) {
