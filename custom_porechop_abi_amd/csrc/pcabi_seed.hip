@@ -355,6 +355,14 @@ struct Buf {
 };
 
 struct State {
+    // the second band class runs beside the first on a side stream (fork / join by events)
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+    ~State() {
+        if (side) (void)hipStreamDestroy(side);
+        if (fork) (void)hipEventDestroy(fork);
+        if (join) (void)hipEventDestroy(join);
+    }
     // plan cache key: the adapters themselves (a table at a reused address may hold others)
     std::vector<uint8_t> key_codes;
     std::vector<int32_t> key_len, key_rows;
@@ -598,8 +606,22 @@ int bounds(State *s, const void *adps_key, const uint8_t *hcodes, const int32_t 
             continue;
         }
         SD_TRY(hipMemsetD32Async((hipDeviceptr_t)s->bound.p, pcabi::sf::NEG16, (size_t)n * n_adp, st));
-        for (int c = 0; c < kCls; ++c)
-            if (cnt[c]) launch_band(s, s->band[c], cnt[c], c, codes, v_off, v_len, sc, n, st);
+        if (cnt[0] && cnt[1]) {   // both classes: side by side (atomicMax into one bound array)
+            if (!s->side) {
+                SD_TRY(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
+                SD_TRY(hipEventCreateWithFlags(&s->fork, hipEventDisableTiming));
+                SD_TRY(hipEventCreateWithFlags(&s->join, hipEventDisableTiming));
+            }
+            SD_TRY(hipEventRecord(s->fork, st));
+            SD_TRY(hipStreamWaitEvent(s->side, s->fork, 0));
+            launch_band(s, s->band[1], cnt[1], 1, codes, v_off, v_len, sc, n, s->side);
+            launch_band(s, s->band[0], cnt[0], 0, codes, v_off, v_len, sc, n, st);
+            SD_TRY(hipEventRecord(s->join, s->side));
+            SD_TRY(hipStreamWaitEvent(st, s->join, 0));
+        } else {
+            for (int c = 0; c < kCls; ++c)
+                if (cnt[c]) launch_band(s, s->band[c], cnt[c], c, codes, v_off, v_len, sc, n, st);
+        }
         SD_TRY(hipGetLastError());
         const int64_t tot = n * (int64_t)n_adp;
         const unsigned grid_all = (unsigned)((tot + 255) / 256);
