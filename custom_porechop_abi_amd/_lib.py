@@ -6,7 +6,7 @@ entry points raise PcabiError. The CPU restatement under oracle/ is test infrast
 HIP runtime sharing: PyTorch-ROCm wheels bundle their own libamdhip64.so.7. If torch is already
 imported (the multi-GPU path uses torch.distributed/RCCL), loading libpcabi.so after it binds
 to the SAME runtime (identical SONAME), so one process never holds two HIP runtimes. Import
-torch before this module whenever both are used (bench.py and parallel.py do).
+torch before this module whenever both are used (bench.py and shards.py do).
 """
 import ctypes
 import os
@@ -83,6 +83,7 @@ def lib():
         'pcabi_middle_scan_host': ([c_int, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_p, ctypes.c_int32, c_int, c_int,
                                     c_int, c_int, c_d, c_p, c_i64], c_i64),
         'pcabi_middle_seed_runs': ([], c_i64),
+        'pcabi_io_release_cache': ([], None),
         'pcabi_barcode_call_dev': ([c_p, c_i64, c_p, c_p, ctypes.c_int32, c_p, c_i64, c_p, c_p, ctypes.c_int32,
                                     c_i64, c_d, c_d, c_int, c_p, c_p, c_p], c_int),
         'pcabi_barcode_call_host': ([c_int, c_p, ctypes.c_int32, c_p, c_p, ctypes.c_int32, c_p, ctypes.c_int32, c_p,
@@ -114,7 +115,7 @@ def exported_symbols():
             'pcabi_fastx_close', 'pcabi_fastx_load', 'pcabi_reads_count', 'pcabi_reads_type', 'pcabi_reads_views',
             'pcabi_reads_free', 'pcabi_reads_write', 'check_compatibility', 'pcabi_compat_host',
             'pcabi_compat_all_vs_all_host', 'pcabi_kmer_count_host', 'pcabi_kmer_top_host', 'pcabi_gather_host',
-            'pcabi_kmer_approx_host']
+            'pcabi_kmer_approx_host', 'pcabi_io_release_cache']
 
 
 def check(rc, what):

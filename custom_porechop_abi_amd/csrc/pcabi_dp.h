@@ -108,13 +108,10 @@ struct Result {
 
 // Closed forms of ScoredAlignment (porechop_abi/src/alignment.cpp:27-109) in terms of the path.
 // Derivation in DESIGN.md §3. bi/bj: end cell, L/n: sequence lengths.
-PCABI_HD Result finish(const Best &b, int L, int n) {
+// finish_path: the same from the path's start diagonal c, match count m and diagonal count nd
+// (b.attr unused); finish: from the packed attribute word.
+PCABI_HD Result finish_path(const Best &b, int c, int m, int nd, int L, int n) {
     Result r;
-    // c lies in [bj - span, bj] with span < 2^15: undo the mod-2^16 wrap
-    const int u = (int)(b.attr >> ATTR_CSH) - ATTR_CBIAS;
-    const int c = b.bj - ((b.bj - u) & 0xFFFF);
-    const int m = (int)(b.attr & ATTR_MASK);
-    const int nd = (int)((b.attr >> ATTR_B) & ATTR_MASK);
     const int i0 = c < 0 ? -c : 0;
     const int j0 = c > 0 ? c : 0;
     const int h = i0 + j0;                             // head length == first path column
@@ -153,6 +150,15 @@ PCABI_HD Result finish(const Best &b, int L, int n) {
     r.l2 = a1 - a0 + 1;
     r.diag_en = readSide ? (trailV > 0 ? precd : lastD) : (trailH > 0 ? precd : lastD);
     return r;
+}
+
+PCABI_HD Result finish(const Best &b, int L, int n) {
+    // c lies in [bj - span, bj] with span < 2^15: undo the mod-2^16 wrap
+    const int u = (int)(b.attr >> ATTR_CSH) - ATTR_CBIAS;
+    const int c = b.bj - ((b.bj - u) & 0xFFFF);
+    const int m = (int)(b.attr & ATTR_MASK);
+    const int nd = (int)((b.attr >> ATTR_B) & ATTR_MASK);
+    return finish_path(b, c, m, nd, L, n);
 }
 
 // check_compatibility (porechop_abi/ab_initio_src/compatibility.cpp:124-170) from the aligned
@@ -360,6 +366,263 @@ PCABI_HD Result align_lane_generic(ReadFn rd, int n, AdpFn adp, int L, const Sco
         slt_last = lt_type;
     }
     return finish(best, L, fin ? n : n + 1);
+}
+
+// ------------------------------------------------------------------------------------------
+// align_lane_striped<R, AFFINE>: adapters of any length up to MAX_STRIPED_LEN and any scoring --
+// the core for everything the register-resident cores cannot hold (L > 128; the reference puts
+// no bound on the adapter, porechop_abi/src/adapter_align.cpp:11-31).
+//
+// The adapter's rows are cut into stripes of R rows (the table is top-padded to rt rows, a
+// multiple of R; the first stripe skips its padding slots by a wave-uniform branch, as the
+// generic core does). One lane sweeps the window once per stripe with the stripe's rows in
+// registers, running exactly align_lane_generic's recurrences; between stripes the stripe's
+// bottom row (S- and V-state values with their attributes, per column) goes through a per-lane
+// boundary buffer `bnd`, which the next stripe reads as its row 0. Two more things cross
+// stripes, in registers: the last column's running V-run state (its rows flow top-down), and
+// `bc`, the first maximum of the last column over the rows above the final stripe. The final
+// stripe merges bc into its last-row scout at column n before its own last-column rows: the
+// reference's visit order (S/align/dp_scout.h:175: the last row left to right, then the last
+// column top-down, strict '>').
+// Attributes are two words and never wrap: c = j0 - i0, and nD << 16 | m.
+//
+//   bnd.load(j, BndCell &) / bnd.store(j, const BndCell &), j = 1..n: the boundary row
+//   adp.load(k) loads stripe k (table slots kR+1 .. kR+R), adp(s) = code of slot s of it
+// CHUNK semantics as align_lane_generic's (own_lo / own_hi).
+// ------------------------------------------------------------------------------------------
+constexpr int MAX_STRIPED_LEN = 65535;           // nD, m <= L fit 16 bits each
+constexpr uint32_t INC2_D = 1u << 16;            // mismatching diagonal: nD + 1
+constexpr uint32_t INC2_M = INC2_D + 1u;         // matching diagonal: nD + 1, m + 1
+constexpr int SCORE_FLOOR = -(1 << 30);          // below every reachable score
+
+// One column of the row above a stripe: S- and V-state values with their attributes.
+struct BndCell {
+    int s, v;
+    int32_t sc, vc;     // start diagonals
+    uint32_t sn, vn;    // nD << 16 | m
+};
+
+// Scout state: the end cell (Best's geometry; attr unused) and the path's two attribute words.
+struct BestS {
+    Best b;
+    int32_t c;
+    uint32_t n;
+};
+
+template <int R, bool AFFINE>
+struct StripeDP {
+    int S[R + 1], H[R + 1];
+    int32_t SC[R + 1], HC[R + 1];
+    uint32_t SN[R + 1], HN[R + 1];
+    BestS best;                          // last row (final stripe) and, from column n on, everything
+    BestS bc;                            // last column, rows above the final stripe
+    int cslt, cvt, cvp;                  // last column: S type and V run (t, p) at the row above
+    int slt_last, ht_last, hp_last;      // row L running state (final stripe)
+    int sdg;                             // S(row above the stripe, j - 1) and its attributes
+    int32_t sdc;
+    uint32_t sdn;
+
+    PCABI_HD void init_stripe(int ib, int off) {
+#pragma unroll
+        for (int s = 1; s <= R; ++s) {
+            S[s] = 0;
+            H[s] = NEG;
+            SC[s] = -(ib + s);           // S(i, 0) = 0, the path starts at (i, 0)
+            SN[s] = 0;
+            HC[s] = 0;
+            HN[s] = 0;
+        }
+        sdg = 0;
+        sdc = -(ib + off);
+        sdn = 0;
+        slt_last = LT_NONE;
+        ht_last = 0;
+        hp_last = 0;
+    }
+
+    // One column of the stripe. ib: absolute row of slot s is ib + s; off: padding slots to skip;
+    // fin: the stripe holds row L; owned: this column may hold the last-row end cell.
+    // Writes the stripe's bottom row at this column to `bot`.
+    template <bool LAST, typename AdpFn>
+    PCABI_HD void column(const int r, const int j, const BndCell &up, const AdpFn &adp, const int off, const int ib,
+                         const int L, const bool fin, const bool owned, const Scoring &sc, BndCell &bot) {
+        int sup = up.s, vup = up.v;
+        int32_t scup = up.sc, vcup = up.vc;
+        uint32_t snup = up.sn, vnup = up.vn;
+        int dg = sdg;
+        int32_t dgc = sdc;
+        uint32_t dgn = sdn;
+        int slt_up = cslt, vt_up = cvt, vp_up = cvp;
+        if (LAST && fin && bc.b.score > best.b.score) best = bc;
+        int lv = NEG, lh = NEG, ls = 0, lt_type = LT_NONE;
+        bool l_hext = false;
+        int32_t lvc = 0, lhc = 0, lsc = 0;
+        uint32_t lvn = 0, lhn = 0, lsn = 0;
+#pragma unroll
+        for (int s = 1; s <= R; ++s) {
+            if (s > off) {
+                const bool match = (r == adp(s));
+                const int diag = dg + (match ? sc.ma : sc.mi);
+                const uint32_t dn = dgn + (match ? INC2_M : INC2_D);
+                int hn, vn, g;
+                int32_t hc, vc, gc;
+                uint32_t hnn, vnn, gn;
+                bool hext, vext, fromv;
+                if (AFFINE) {
+                    const int hx = H[s] + sc.ge, ho = S[s] + sc.go;
+                    hext = !(hx < ho);
+                    hn = hext ? hx : ho;
+                    hc = hext ? HC[s] : SC[s];
+                    hnn = hext ? HN[s] : SN[s];
+                    const int vx = vup + sc.ge, vo = sup + sc.go;
+                    vext = !(vx < vo);
+                    vn = vext ? vx : vo;
+                    vc = vext ? vcup : scup;
+                    vnn = vext ? vnup : snup;
+                    fromv = !(vn < hn);
+                    g = fromv ? vn : hn;
+                    gc = fromv ? vc : hc;
+                    gn = fromv ? vnn : hnn;
+                } else {
+                    hext = vext = false;
+                    const int vv = sup + sc.ge, hh = S[s] + sc.ge;
+                    fromv = !(vv < hh);
+                    g = fromv ? vv : hh;
+                    gc = fromv ? scup : SC[s];
+                    gn = fromv ? snup : SN[s];
+                    hn = NEG; vn = NEG; hc = vc = 0; hnn = vnn = 0;
+                }
+                const bool isd = !(diag < g);
+                const int sn = isd ? diag : g;
+                const int32_t snc = isd ? dgc : gc;
+                const uint32_t snn = isd ? dn : gn;
+                const int slt = isd ? LT_D : (fromv ? LT_V : LT_H);
+                const bool lastrow = fin && s == R;
+                if (LAST) {
+                    int vt, vp;
+                    if (AFFINE && vext) { vt = vt_up + 1; vp = vp_up; }
+                    else open_run(slt_up, LT_V, vt_up, vp_up, vt, vp);
+                    if (!lastrow) {                 // last column, rows 1..L-1 in order
+                        BestS &t = fin ? best : bc;
+                        if (sn > t.b.score) {
+                            t.b.score = sn;
+                            t.b.bi = ib + s;
+                            t.b.bj = j;
+                            if (AFFINE) {
+                                if (vn == sn)      { t.c = vc; t.n = vnn; t.b.ltype = LT_V; t.b.trail = vt; t.b.precd = vp; }
+                                else if (hn == sn) { t.c = hc; t.n = hnn; t.b.ltype = LT_H; t.b.trail = 0; t.b.precd = 0; }
+                                else               { t.c = snc; t.n = snn; t.b.ltype = LT_D; t.b.trail = 0; t.b.precd = 0; }
+                            } else {
+                                t.c = snc; t.n = snn; t.b.ltype = slt;
+                                t.b.trail = (slt == LT_V) ? vt : 0;
+                                t.b.precd = (slt == LT_V) ? vp : 0;
+                            }
+                        }
+                    }
+                    if (AFFINE || slt == LT_V) { vt_up = vt; vp_up = vp; }
+                    else { vt_up = 0; vp_up = 0; }
+                    slt_up = slt;
+                }
+                if (lastrow) {
+                    lv = vn; lh = hn; ls = sn; lvc = vc; lhc = hc; lsc = snc; lvn = vnn; lhn = hnn; lsn = snn;
+                    lt_type = slt; l_hext = hext;
+                }
+                dg = S[s];
+                dgc = SC[s];
+                dgn = SN[s];
+                S[s] = sn;
+                SC[s] = snc;
+                SN[s] = snn;
+                if (AFFINE) {
+                    H[s] = hn;
+                    HC[s] = hc;
+                    HN[s] = hnn;
+                }
+                sup = sn; scup = snc; snup = snn;
+                vup = vn; vcup = vc; vnup = vnn;
+            }
+        }
+        if (LAST) { cslt = slt_up; cvt = vt_up; cvp = vp_up; }
+        sdg = up.s;
+        sdc = up.sc;
+        sdn = up.sn;
+        bot.s = sup; bot.v = vup; bot.sc = scup; bot.vc = vcup; bot.sn = snup; bot.vn = vnup;
+        if (!fin) return;
+        // ---- row L: H-state run and the last-row scout ----
+        int ht, hp;
+        if (AFFINE && l_hext) { ht = ht_last + 1; hp = hp_last; }
+        else open_run(slt_last, LT_H, ht_last, hp_last, ht, hp);
+        if (ls > best.b.score && owned) {
+            best.b.score = ls;
+            best.b.bi = L;
+            best.b.bj = j;
+            const int vt = LAST ? vt_up : 0, vp = LAST ? vp_up : 0;
+            if (AFFINE) {
+                if (lv == ls)      { best.c = lvc; best.n = lvn; best.b.ltype = LT_V; best.b.trail = vt; best.b.precd = vp; }
+                else if (lh == ls) { best.c = lhc; best.n = lhn; best.b.ltype = LT_H; best.b.trail = ht; best.b.precd = hp; }
+                else               { best.c = lsc; best.n = lsn; best.b.ltype = LT_D; best.b.trail = 0; best.b.precd = 0; }
+            } else {
+                best.c = lsc; best.n = lsn; best.b.ltype = lt_type;
+                best.b.trail = (lt_type == LT_V) ? vt : (lt_type == LT_H ? ht : 0);
+                best.b.precd = (lt_type == LT_V) ? vp : (lt_type == LT_H ? hp : 0);
+            }
+        }
+        if (AFFINE || lt_type == LT_H) { ht_last = ht; hp_last = hp; }
+        else { ht_last = 0; hp_last = 0; }
+        slt_last = lt_type;
+    }
+};
+
+template <int R, bool AFFINE, typename ReadFn, typename AdpFn, typename BndFn>
+PCABI_HD Result align_lane_striped(const ReadFn &rd0, int n, AdpFn &adp, int L, int rt, const Scoring sc, BndFn &bnd,
+                                   int own_lo = 1, int own_hi = -1) {
+    const bool fin_read = own_hi < 0;      // the window's last column is the read's last column
+    const int hi = fin_read ? n + 1 : own_hi;
+    const int pad = rt - L, k0 = pad / R, nst = rt / R;
+    StripeDP<R, AFFINE> st;
+    st.best.b.score = 0;                   // first scouted cell: (L, 0), S = 0
+    st.best.b.bi = L;
+    st.best.b.bj = 0;
+    st.best.b.attr = 0;
+    st.best.b.ltype = LT_NONE;
+    st.best.b.trail = 0;
+    st.best.b.precd = 0;
+    st.best.c = -L;
+    st.best.n = 0;
+    st.bc = st.best;
+    st.bc.b.score = SCORE_FLOOR;
+    st.cslt = LT_NONE;
+    st.cvt = 0;
+    st.cvp = 0;
+#pragma unroll 1
+    for (int k = k0; k < nst; ++k) {
+        adp.load(k);
+        const bool first = k == k0, fin = k == nst - 1;
+        const int off = first ? pad - k0 * R : 0;
+        const int ib = k * R - pad;
+        st.init_stripe(ib, off);
+        ReadFn rd = rd0;
+        BndCell up, nx, bot;
+        auto row0 = [](int j, BndCell &u) { u.s = 0; u.v = NEG; u.sc = j; u.vc = 0; u.sn = 0; u.vn = 0; };
+        if (first) row0(1, up);
+        else bnd.load(1, up);
+        int r = rd(1);
+#pragma unroll 1
+        for (int j = 1; j < n; ++j) {
+            const int rn = rd(j + 1);
+            if (first) row0(j + 1, nx);
+            else bnd.load(j + 1, nx);
+            st.template column<false>(r, j, up, adp, off, ib, L, fin, j >= own_lo && j < hi, sc, bot);
+            if (!fin) bnd.store(j, bot);
+            up = nx;
+            r = rn;
+        }
+        if (fin_read) st.template column<true>(r, n, up, adp, off, ib, L, fin, n >= own_lo && n < hi, sc, bot);
+        else st.template column<false>(r, n, up, adp, off, ib, L, fin, n >= own_lo && n < hi, sc, bot);
+        if (!fin) bnd.store(n, bot);
+    }
+    return finish_path(st.best.b, st.best.c, (int)(st.best.n & 0xFFFFu), (int)(st.best.n >> 16), L,
+                       fin_read ? n : n + 1);
 }
 
 }  // namespace pcabi

@@ -58,7 +58,10 @@ int fail(int code, const std::string &msg) {
 // scoring): a few sizes, the path for everything else up to 128.
 // LONG (two-pass packed core, pk::LayL): 96 / 112 / 128 rows for the 89-128 bp adapters (the
 // 102 / 111 bp full rapid-barcode sequences) whenever pcabi::long_ok holds.
-enum Kind { FAST = 0, GENERIC = 1, PACKED = 2, WIDE = 3, LONG = 4 };
+// STRIPED (pcabi_dp.h align_lane_striped, k_align_striped): every adapter longer than kMaxRPL, any
+// scoring, rows in stripes of kStripeRows with the boundary row in global scratch; its table pads
+// every adapter to the bucket's longest, rounded up to kStripeTab rows (pcabi_adapters::rt).
+enum Kind { FAST = 0, GENERIC = 1, PACKED = 2, WIDE = 3, LONG = 4, STRIPED = 5 };
 struct BucketDef {
     int rpl;
     Kind kind;
@@ -68,11 +71,16 @@ constexpr BucketDef kBuckets[] = {
     {36, FAST}, {40, FAST}, {44, FAST}, {48, FAST}, {52, FAST}, {56, FAST}, {60, FAST}, {64, FAST},
     {68, WIDE}, {72, WIDE}, {76, WIDE}, {80, WIDE}, {84, WIDE}, {88, WIDE},
     {96, LONG}, {112, LONG}, {128, LONG},
-    {16, GENERIC}, {32, GENERIC}, {64, GENERIC}, {96, GENERIC}, {128, GENERIC}};
+    {16, GENERIC}, {32, GENERIC}, {64, GENERIC}, {96, GENERIC}, {128, GENERIC},
+    {256, STRIPED}};
 constexpr int kNumBuckets = sizeof(kBuckets) / sizeof(kBuckets[0]);
-constexpr int kMaxRPL = 128;
+constexpr int kStripedBucket = kNumBuckets - 1;
+constexpr int kMaxRPL = 128;                          // longest adapter a register-resident core holds
+constexpr int kStripeRows = 32;
+constexpr int kStripeTab = 64;
 
 int bucket_of(int L, const pcabi::Scoring &sc, bool allow_wide = true) {
+    if (L > kMaxRPL) return kStripedBucket;
     if (L <= 64) {
         const int rpl = (L + 3) & ~3;
         if (pcabi::fast_ok(L, rpl, sc)) return rpl / 4 - 1;
@@ -110,6 +118,11 @@ struct KParams {
     pcabi::Scoring sc;
     int32_t *compat;           // != nullptr: write check_compatibility flags instead of results
     const int4 *task_chunk;    // k_align_chunk: per task slot (read offset, columns, owned lo, hi)
+    // striped bucket (k_align_striped)
+    int32_t rt;                // table rows per adapter (multiple of kStripeTab)
+    int32_t max_cols;          // host value: no window / chunk of the launch is longer
+    int32_t *scratch;          // boundary rows: per wave slot max_cols x fields x 64 lanes
+    int64_t n_items;           // waves of work (cross: 64-window groups x adapters)
 };
 
 // Window reader: one dword per lane every 4 columns (a wave-uniform branch -- j is the same in
@@ -291,10 +304,10 @@ __global__ __launch_bounds__(256, PCABI_WAVES) void k_align(KParams p) {
 
 // ---- middle-scan score filter (pcabi_dp.h filter_lane) -------------------------------------------
 // PCABI_MIDDLE_FILTER=0 in the environment turns it off (A/B timing; results are identical).
-const bool g_middle_filter = [] {
+bool middle_filter_on() {
     const char *e = std::getenv("PCABI_MIDDLE_FILTER");
     return !(e && e[0] == '0');
-}();
+}
 
 // Owned end columns per chunk of the middle scan's candidate DP (pcabi_dp.h sf::chunk_plan):
 // short enough that the longest read's chunks finish with the rest, long enough that the D-column
@@ -692,15 +705,152 @@ __global__ __launch_bounds__(256, PCABI_WAVES) void k_align_chunk(KParams p) {
     store_result(p.out, p.out_stride, p.task_out[slot], r);
 }
 
-// Buckets the chunked candidate DP serves: the packed core's (FAST buckets laid out packed, WIDE)
-// and the generic core's (long adapters).
-bool chunkable(int b, bool packed) {
-    return kBuckets[b].kind == WIDE || kBuckets[b].kind == LONG || kBuckets[b].kind == GENERIC ||
-           (kBuckets[b].kind == FAST && packed);
+// ---- striped bucket: adapters longer than kMaxRPL (pcabi_dp.h align_lane_striped) ----------------
+// The boundary row between stripes lives in global scratch, [column][field][lane] per wave slot,
+// so a wave's access to one field of one column is 256 contiguous bytes.
+template <bool AFFINE>
+struct StripeBnd {
+    static constexpr int NF = AFFINE ? 6 : 3;   // linear gaps carry no V state
+    int32_t *p;                                 // this lane's column-1 field-0 entry
+    __device__ __forceinline__ void load(int j, pcabi::BndCell &c) const {
+        const int32_t *q = p + (int64_t)(j - 1) * (NF * 64);
+        c.s = q[0];
+        c.sc = q[64];
+        c.sn = (uint32_t)q[128];
+        if (AFFINE) {
+            c.v = q[192];
+            c.vc = q[256];
+            c.vn = (uint32_t)q[320];
+        } else {
+            c.v = pcabi::NEG;
+            c.vc = 0;
+            c.vn = 0;
+        }
+    }
+    __device__ __forceinline__ void store(int j, const pcabi::BndCell &c) const {
+        int32_t *q = p + (int64_t)(j - 1) * (NF * 64);
+        q[0] = c.s;
+        q[64] = c.sc;
+        q[128] = (int32_t)c.sn;
+        if (AFFINE) {
+            q[192] = c.v;
+            q[256] = c.vc;
+            q[320] = (int32_t)c.vn;
+        }
+    }
+};
+
+// The current stripe's R adapter codes in SGPRs (the adapter is wave-uniform).
+template <int R>
+struct StripeAdp {
+    const uint32_t *base;   // the adapter's rt-byte table row (top-padded)
+    uint32_t w[R / 4];
+    __device__ __forceinline__ void load(int k) {
+#pragma unroll
+        for (int q = 0; q < R / 4; ++q) w[q] = __builtin_amdgcn_readfirstlane(base[k * (R / 4) + q]);
+    }
+    __device__ __forceinline__ int operator()(int s) const { return (int)((w[(s - 1) >> 2] >> (8 * ((s - 1) & 3))) & 0xFFu); }
+};
+
+// Persistent grid: wave slot = blockIdx * 4 + wave owns one scratch region and walks the work
+// items (cross: 64 windows of a tile x one adapter; pairs: one host-built wave of tasks, chunks
+// included) with a stride of the slot count. Every lane reaches the loop's end: no barriers.
+template <int R, bool AFFINE>
+__global__ __launch_bounds__(256) void k_align_striped(KParams p) {
+    const int64_t slot = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int64_t n_slots = (int64_t)gridDim.x * 4;
+    StripeBnd<AFFINE> bnd{p.scratch + slot * (int64_t)p.max_cols * (StripeBnd<AFFINE>::NF * 64) + lane};
+    for (int64_t item = slot; item < p.n_items; item += n_slots) {
+        const bool cross = p.task_win == nullptr;
+        int a_local;
+        int64_t w, out_idx, q = 0;
+        int4 ck = make_int4(0, 0, 1, -1);
+        if (cross) {
+            a_local = (int)(item % p.n_adp);
+            q = item / p.n_adp;
+            w = q * 64 + lane;
+            if (w >= p.n_win) continue;
+            out_idx = (int64_t)p.adp_id[a_local] * p.n_win + w;
+        } else {
+            a_local = p.wave_adp[item];
+            const int64_t sl = item * 64 + lane;
+            w = p.task_win[sl];
+            if (w < 0) continue;
+            out_idx = p.task_out[sl];
+            if (p.task_chunk) ck = p.task_chunk[sl];
+        }
+        a_local = __builtin_amdgcn_readfirstlane(a_local);
+        const int L = __builtin_amdgcn_readfirstlane(p.adp_len[a_local]);
+        const int n = p.task_chunk ? ck.y : p.win_len[w];
+        pcabi::Result r;
+        if (n <= 0) {
+            r = empty_result();
+        } else {
+            WindowReader rd = cross
+                ? WindowReader(p.tiles + p.tile_off[q >> 2] + (q & 3) * 64 + lane, 256, 0)
+                : [&] {
+                      const uint8_t *b = p.codes + p.win_off[w] + ck.x;
+                      const int a0 = (int)((uintptr_t)b & 3);
+                      return WindowReader(reinterpret_cast<const uint32_t *>(b - a0), 1, 8 * a0);
+                  }();
+            StripeAdp<R> adp{p.adp_pad + (int64_t)a_local * (p.rt / 4)};
+            r = pcabi::align_lane_striped<R, AFFINE>(rd, n, adp, L, p.rt, p.sc, bnd, ck.z, ck.w);
+        }
+        if (p.compat) {
+            int en_match = 0;
+            if (r.rs >= 0 && r.diag_en && r.l1 > 0) {
+                const uint8_t *ab = reinterpret_cast<const uint8_t *>(p.adp_pad + (int64_t)a_local * (p.rt / 4));
+                en_match = p.codes[p.win_off[w] + r.re] == ab[p.rt - L + r.ae];
+            }
+            p.compat[out_idx] = pcabi::compat_flag(r, n, en_match);
+            continue;
+        }
+        store_result(p.out, p.out_stride, out_idx, r);
+    }
 }
 
-void dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st) {
+// Scratch budget of one striped launch (PCABI_STRIPE_SCRATCH_MB, default 4096): it bounds the wave
+// slots when windows are long (each slot holds a boundary row as long as the longest window).
+const int64_t g_stripe_budget = [] {
+    const char *e = std::getenv("PCABI_STRIPE_SCRATCH_MB");
+    const int64_t mb = (e && e[0]) ? std::max<int64_t>(16, std::atoll(e)) : 4096;
+    return mb << 20;
+}();
+
+// Launch the striped kernel for one bucket: p.rt, p.max_cols set by the caller; scratch is
+// stream-ordered (hipMallocAsync / hipFreeAsync on `st`), so concurrent launches never share it.
+int launch_striped(KParams p, bool affine, hipStream_t st) {
+    p.n_items = p.task_win ? p.n_waves : (p.n_win + 63) / 64 * p.n_adp;
+    if (p.n_items <= 0) return 0;
+    const int64_t nf = affine ? 6 : 3;
+    const int64_t per_slot = std::max<int64_t>(1, p.max_cols) * nf * 64 * 4;
+    int64_t slots = std::min<int64_t>({(p.n_items + 3) / 4 * 4, (int64_t)2048, g_stripe_budget / per_slot / 4 * 4});
+    slots = std::max<int64_t>(slots, 4);
+    void *scr = nullptr;
+    // slots past the last item never touch their scratch
+    HIP_TRY(hipMallocAsync(&scr, (size_t)(std::min(slots, p.n_items) * per_slot), st));
+    p.scratch = (int32_t *)scr;
+    p.max_cols = std::max<int32_t>(1, p.max_cols);
+    const dim3 grid((unsigned)(slots / 4));
+    if (affine) hipLaunchKernelGGL((k_align_striped<kStripeRows, true>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((k_align_striped<kStripeRows, false>), grid, dim3(256), 0, st, p);
+    const hipError_t le = hipGetLastError();
+    HIP_TRY(hipFreeAsync(scr, st));
+    if (le != hipSuccess) return fail(PCABI_E_DEVICE, std::string("k_align_striped: ") + hipGetErrorString(le));
+    return 0;
+}
+
+// Buckets the chunked candidate DP serves: the packed core's (FAST buckets laid out packed, WIDE)
+// and the generic and striped cores' (long adapters).
+bool chunkable(int b, bool packed) {
+    return kBuckets[b].kind == WIDE || kBuckets[b].kind == LONG || kBuckets[b].kind == GENERIC ||
+           kBuckets[b].kind == STRIPED || (kBuckets[b].kind == FAST && packed);
+}
+
+int dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st) {
     const dim3 grid((unsigned)((p.n_waves + 3) / 4));
+    if (kBuckets[b].kind == STRIPED) return launch_striped(p, affine, st);
     if (kBuckets[b].kind == GENERIC) {
         switch (kBuckets[b].rpl) {
 #define C(R)                                                                                            \
@@ -711,7 +861,7 @@ void dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st) {
         C(16) C(32) C(64) C(96) C(128)
 #undef C
         }
-        return;
+        return 0;
     }
     if (kBuckets[b].kind == LONG) {
         switch (kBuckets[b].rpl) {
@@ -723,7 +873,7 @@ void dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st) {
         C(96) C(112) C(128)
 #undef C
         }
-        return;
+        return 0;
     }
     switch (kBuckets[b].rpl) {
 #define C(R)                                                                                           \
@@ -735,6 +885,7 @@ void dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st) {
     C(68) C(72) C(76) C(80) C(84) C(88)
 #undef C
     }
+    return 0;
 }
 
 template <int RPL, int KIND>
@@ -743,7 +894,8 @@ void launch(const KParams &p, bool affine, dim3 grid, hipStream_t st) {
     else hipLaunchKernelGGL((k_align<RPL, false, KIND>), grid, dim3(256), 0, st, p);
 }
 
-void dispatch(int b, const KParams &p, bool affine, hipStream_t st, bool packed) {
+int dispatch(int b, const KParams &p, bool affine, hipStream_t st, bool packed) {
+    if (kBuckets[b].kind == STRIPED) return launch_striped(p, affine, st);
     const int64_t tiles8 = (p.n_win + 8 * 256 - 1) / (8 * 256) * 8;   // window tiles, padded to 8
     dim3 grid = p.task_win ? dim3((unsigned)((p.n_waves + 3) / 4))
                            : dim3((unsigned)(tiles8 * p.n_adp));
@@ -781,6 +933,7 @@ void dispatch(int b, const KParams &p, bool affine, hipStream_t st, bool packed)
         case 128: launch<128, GENERIC>(p, affine, grid, st); break;
         }
     }
+    return 0;
 }
 
 // Packed-key kernels serve a fast bucket when every adapter in it satisfies the range
@@ -795,8 +948,9 @@ bool bucket_packed_ok(int b, const std::vector<int32_t> &lens, const pcabi::Scor
 
 // Host-side layout of a bucket's adapter table.
 struct BucketHost {
-    std::vector<uint8_t> pad;   // n * RPL bytes
+    std::vector<uint8_t> pad;   // n * RPL bytes (striped: n * rt)
     std::vector<int32_t> len, id;
+    int rt = 0;                 // striped: table rows per adapter
 };
 
 // At most this many FAST buckets per adapter table: a cross product launches its buckets side by
@@ -850,10 +1004,13 @@ void build_buckets(const uint8_t *adp_codes, const int32_t *adp_off, const int32
                    int32_t n_adp, const pcabi::Scoring &sc, BucketHost (&bk)[kNumBuckets], bool merge = true,
                    bool allow_wide = true) {
     const std::vector<int> b_of = assign_buckets(adp_len, n_adp, sc, merge, allow_wide);
+    for (int a = 0; a < n_adp; ++a)
+        if (b_of[a] == kStripedBucket)
+            bk[kStripedBucket].rt = std::max(bk[kStripedBucket].rt, (adp_len[a] + kStripeTab - 1) / kStripeTab * kStripeTab);
     for (int a = 0; a < n_adp; ++a) {
         const int L = adp_len[a];
         const int b = b_of[a];
-        const int R = kBuckets[b].rpl;
+        const int R = b == kStripedBucket ? bk[b].rt : kBuckets[b].rpl;
         BucketHost &h = bk[b];
         const size_t base = h.pad.size();
         h.pad.resize(base + R, (uint8_t)pcabi::PAD_CODE);
@@ -874,6 +1031,7 @@ int fail(int code, const std::string &msg) { return ::fail(code, msg); }
 // ---- prepared adapter tables (device) ---------------------------------------------------------
 struct pcabi_adapters {
     int32_t n_adp = 0;
+    int rt[kNumBuckets] = {};        // striped bucket: table rows per adapter
     bool padded[kNumBuckets] = {};
     int max_off[kNumBuckets] = {};   // most padding rows above an adapter (> 3: packed core only)
     std::vector<int32_t> lens[kNumBuckets];
@@ -1016,9 +1174,9 @@ int engine_init(Engine &e, int device) {
 
 int check_common(const int32_t *adp_len, int32_t n_adp) {
     for (int a = 0; a < n_adp; ++a)
-        if (adp_len[a] < 1 || adp_len[a] > kMaxRPL)
+        if (adp_len[a] < 1 || adp_len[a] > pcabi::MAX_STRIPED_LEN)
             return fail(PCABI_E_ARG, "adapter length " + std::to_string(adp_len[a]) + " outside 1.." +
-                                         std::to_string(kMaxRPL));
+                                         std::to_string(pcabi::MAX_STRIPED_LEN));
     return 0;
 }
 
@@ -1037,7 +1195,7 @@ extern "C" {
 
 const char *pcabi_last_error(void) { return g_err.c_str(); }
 int pcabi_version(void) { return 1; }
-int pcabi_max_adapter_len(void) { return kMaxRPL; }
+int pcabi_max_adapter_len(void) { return pcabi::MAX_STRIPED_LEN; }
 int pcabi_max_window_len(void) { return pcabi::MAX_WINDOW_LEN; }
 
 int pcabi_device_count(void) {
@@ -1131,7 +1289,8 @@ int align_host_impl(int device, const uint8_t *codes, int64_t codes_len, const i
     int64_t max_win = 0;
     {
         int max_L = 0;
-        for (int a = 0; a < n_adp; ++a) max_L = std::max(max_L, (int)adp_len[a]);
+        for (int a = 0; a < n_adp; ++a)
+            if (adp_len[a] <= kMaxRPL) max_L = std::max(max_L, (int)adp_len[a]);   // striped: c never wraps
         for (int64_t w = 0; w < n_win; ++w) max_win = std::max<int64_t>(max_win, win_len[w]);
         if (int rc = check_span(sc, max_L, max_win)) return rc;
     }
@@ -1189,6 +1348,8 @@ int align_host_impl(int device, const uint8_t *codes, int64_t codes_len, const i
         p.adp_len = (const int32_t *)e.len[b].p;
         p.adp_id = (const int32_t *)e.id[b].p;
         p.n_adp = nb;
+        p.rt = h.rt;
+        p.max_cols = (int32_t)std::min<int64_t>(max_win, INT32_MAX);
         if (!task_win) {
             p.task_win = nullptr;
             if (n_win > 0 && !p.tiles) {
@@ -1231,7 +1392,7 @@ int align_host_impl(int device, const uint8_t *codes, int64_t codes_len, const i
             p.task_out = (const int32_t *)e.tasks_out.p;
             p.wave_adp = (const int32_t *)e.wave_adp.p;
             p.n_waves = (int64_t)wa.size();
-            dispatch(b, p, affine, e.stream, bucket_packed_ok(b, h.len, sc));
+            if (int rc = dispatch(b, p, affine, e.stream, bucket_packed_ok(b, h.len, sc))) return rc;
             // host vectors are reused by the next bucket: drain before overwriting
             HIP_TRY(hipStreamSynchronize(e.stream));
         }
@@ -1246,7 +1407,11 @@ int align_host_impl(int device, const uint8_t *codes, int64_t codes_len, const i
         });
         ForkJoin fj;
         if (int rc = fj.begin(e.stream, cross.size())) return rc;
-        for (size_t k = 0; k < cross.size(); ++k) dispatch(cross[k].b, cross[k].p, affine, fj.at(k), cross[k].packed);
+        for (size_t k = 0; k < cross.size(); ++k)
+            if (int rc = dispatch(cross[k].b, cross[k].p, affine, fj.at(k), cross[k].packed)) {
+                (void)fj.end();
+                return rc;
+            }
         if (int rc = fj.end()) return rc;
         HIP_TRY(hipGetLastError());
     }
@@ -1382,9 +1547,11 @@ char *adapterAlignment(char *readSeq, char *adapterSeq, int matchScore, int mism
                               &L, 1, nullptr, nullptr, 0, matchScore, mismatchScore, gapOpenScore,
                               gapExtensionScore, out);
     if (rc != 0) {
+        // The reference has no error channel and answers every non-empty input: a "-1" sentinel
+        // here would read as "no alignment" and silently change trimming decisions, so stop.
         std::fprintf(stderr, "libpcabi: adapterAlignment failed: %s\n", pcabi_last_error());
-        std::snprintf(s, 256, "-1,0,-1,0,%d,0.000000,0.000000", (int)0x80000000);
-        return s;
+        std::free(s);
+        std::abort();
     }
     char p1[64], p2[64];
     fmt_pid(p1, sizeof p1, out[PCABI_F_M], out[PCABI_F_L1]);
@@ -1465,6 +1632,7 @@ int adapters_create_impl(const uint8_t *adp_codes, const int32_t *adp_off, const
         if (!nb) continue;
         a->lens[b] = bk[b].len;
         a->ids[b] = bk[b].id;
+        a->rt[b] = bk[b].rt;
         for (int k = 0; k < nb; ++k) {
             if (bk[b].len[k] != kBuckets[b].rpl) a->padded[b] = true;
             a->max_off[b] = std::max(a->max_off[b], kBuckets[b].rpl - bk[b].len[k]);
@@ -1541,7 +1709,8 @@ int pcabi_align_cross_dev(const uint32_t *tiles, const int64_t *tile_off, const 
     {
         int max_L = 0;
         for (int b = 0; b < kNumBuckets; ++b)
-            for (int32_t L : adps->lens[b]) max_L = std::max<int>(max_L, L);
+            if (kBuckets[b].kind != STRIPED)   // the striped core's start column never wraps
+                for (int32_t L : adps->lens[b]) max_L = std::max<int>(max_L, L);
         if (int rc = check_span(pcabi::Scoring{match, mismatch, gap_open, gap_extend}, max_L, max_win_len))
             return rc;
     }
@@ -1553,6 +1722,7 @@ int pcabi_align_cross_dev(const uint32_t *tiles, const int64_t *tile_off, const 
     p.out = out;
     p.out_stride = out_stride;
     p.sc = pcabi::Scoring{match, mismatch, gap_open, gap_extend};
+    p.max_cols = max_win_len;
     const bool affine = gap_open != gap_extend;
     std::vector<int> order;
     for (int b = 0; b < kNumBuckets; ++b) {
@@ -1581,7 +1751,11 @@ int pcabi_align_cross_dev(const uint32_t *tiles, const int64_t *tile_off, const 
         p.adp_len = adps->len[b];
         p.adp_id = adps->id[b];
         p.n_adp = adps->count[b];
-        dispatch(b, p, affine, fj.at(k), bucket_packed_ok(b, adps->lens[b], p.sc));
+        p.rt = adps->rt[b];
+        if (int rc = dispatch(b, p, affine, fj.at(k), bucket_packed_ok(b, adps->lens[b], p.sc))) {
+            (void)fj.end();
+            return rc;
+        }
     }
     if (int rc = fj.end()) return rc;
     HIP_TRY(hipGetLastError());
@@ -1662,9 +1836,11 @@ int filtered_first_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_o
         if (mode && (!h_start || seeded)) {
             if (!sc->seed) sc->seed = pcabi_seed::create();
             // seeds cover every adapter the plan accepts, long (generic-core) ones included
+            // (striped adapters stay outside: every read is their candidate)
             std::vector<int> rows((size_t)n_adp, 0);
             for (int b = 0; b < kNumBuckets; ++b)
-                for (int32_t id : adps->ids[b]) rows[id] = kBuckets[b].rpl;
+                if (kBuckets[b].kind != STRIPED)
+                    for (int32_t id : adps->ids[b]) rows[id] = kBuckets[b].rpl;
             got = pcabi_seed::bounds(sc->seed, adps, adps->hcodes.data(), adps->hoff.data(), adps->hlen.data(),
                                      n_adp, rows, codes, v_off, v_len, n, scr, threshold, h_start ? 2 : mode,
                                      (int16_t *)sc->s16.p, &seed_cands, st);
@@ -1674,7 +1850,8 @@ int filtered_first_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_o
         seeded = got > 0;
         if (seeded) {
             for (int b = 0; b < kNumBuckets; ++b)
-                for (int32_t id : adps->ids[b]) filtered[id] = 1;
+                if (kBuckets[b].kind != STRIPED)
+                    for (int32_t id : adps->ids[b]) filtered[id] = 1;
         } else if (fb.empty()) {
             return 0;
         } else {
@@ -1750,6 +1927,7 @@ int filtered_first_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_o
     std::vector<int32_t> task_start;                // task -> read offset of its chunk
     std::vector<int> nb_used;
     std::vector<char> nb_chunked;
+    std::vector<int32_t> nb_maxcols;                // longest window / chunk per bucket (striped scratch)
     std::vector<int64_t> wave0;
     for (int b = 0; b < kNumBuckets; ++b) {
         const int nb = adps->count[b];
@@ -1762,10 +1940,12 @@ int filtered_first_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_o
             span[kk] = pcabi::sf::chunk_span(L, pcabi::sf::filter_threshold(L, threshold, scr), scr);
             if (span[kk] < 0) chunk = false;
         }
+        int32_t maxcols = 0;
         for (int kk = 0; kk < nb; ++kk) {
             const int32_t a = adps->ids[b][kk];
             int lane = 64;
             auto add = [&](int64_t t, int32_t w, int4 ck) {
+                maxcols = std::max(maxcols, chunk ? ck.y : h_len[w]);
                 if (lane == 64) {
                     wa.push_back(kk);
                     lane = 0;
@@ -1795,6 +1975,7 @@ int filtered_first_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_o
         if (wa.size() == w_before) continue;
         nb_used.push_back(b);
         nb_chunked.push_back(chunk ? 1 : 0);
+        nb_maxcols.push_back(maxcols);
         wave0.push_back((int64_t)w_before);
     }
     wave0.push_back((int64_t)wa.size());
@@ -1830,8 +2011,19 @@ int filtered_first_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_o
             p.wave_adp = (const int32_t *)sc->wa.p + wave0[k];
             p.task_chunk = (const int4 *)sc->tck.p + wave0[k] * 64;
             p.n_waves = wave0[k + 1] - wave0[k];
-            if (nb_chunked[k]) dispatch_chunk(b, p, scr.go != scr.ge, fj.at(k));
-            else dispatch(b, p, scr.go != scr.ge, fj.at(k), bucket_packed_ok(b, adps->lens[b], scr));
+            p.rt = adps->rt[b];
+            p.max_cols = nb_maxcols[k];
+            int rc;
+            if (nb_chunked[k]) {
+                rc = dispatch_chunk(b, p, scr.go != scr.ge, fj.at(k));
+            } else {
+                p.task_chunk = nullptr;   // whole windows
+                rc = dispatch(b, p, scr.go != scr.ge, fj.at(k), bucket_packed_ok(b, adps->lens[b], scr));
+            }
+            if (rc) {
+                (void)fj.end();
+                return rc;
+            }
         }
         if (int rc = fj.end()) return rc;
     }
@@ -1944,7 +2136,7 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
             return 0;
         };
         int filt = 0;
-        if (g_middle_filter && (round == 0 || filt_round1)) {
+        if (middle_filter_on() && (round == 0 || filt_round1)) {
             filt = filtered_first_hits(sc, codes, v_off, v_len, lens.data(), n, round == 0 ? nullptr : nxt_start.data(),
                                        cur.data(), h16, n_win, pos1,
                                        pcabi::Scoring{match, mismatch, gap_open, gap_extend}, threshold, hb, seeded,
@@ -2074,8 +2266,9 @@ int pcabi_compat_host(int device, const uint8_t *codes, int64_t codes_len, const
         const int32_t lo = swap ? j : i, sh = swap ? i : j;
         flags[t] = 0;                  // empty sequences: no alignment (the reference is undefined)
         if (seq_len[lo] == 0 || seq_len[sh] == 0) continue;
-        if (seq_len[sh] > kMaxRPL)
-            return fail(PCABI_E_ARG, "check_compatibility: the shorter sequence exceeds " + std::to_string(kMaxRPL) + " bases");
+        if (seq_len[sh] > pcabi::MAX_STRIPED_LEN)
+            return fail(PCABI_E_ARG, "check_compatibility: the shorter sequence exceeds " +
+                                         std::to_string(pcabi::MAX_STRIPED_LEN) + " bases");
         tw.push_back(lo);
         ta.push_back(sh);
         at.push_back(t);
@@ -2085,7 +2278,7 @@ int pcabi_compat_host(int device, const uint8_t *codes, int64_t codes_len, const
     std::vector<int32_t> aoff((size_t)n_seq), alen((size_t)n_seq);
     for (int64_t k = 0; k < n_seq; ++k) {
         aoff[k] = (int32_t)acodes.size();
-        alen[k] = std::max<int32_t>(1, std::min<int32_t>(seq_len[k], kMaxRPL));
+        alen[k] = std::max<int32_t>(1, std::min<int32_t>(seq_len[k], pcabi::MAX_STRIPED_LEN));
         for (int32_t q = 0; q < alen[k]; ++q) acodes.push_back(seq_len[k] > 0 ? codes[seq_off[k] + q] : 0);
     }
     std::vector<int32_t> got(tw.size());
@@ -2106,7 +2299,7 @@ int pcabi_compat_all_vs_all_host(int device, const uint8_t *codes, int64_t codes
     for (int64_t k = 0; k < n; ++k) mat[k * n + k] = -1;   // every other entry is written below
     if (n < 2) return 0;
     bool cross_ok = true;
-    for (int64_t k = 0; k < n; ++k) cross_ok = cross_ok && seq_len[k] >= 1 && seq_len[k] <= kMaxRPL;
+    for (int64_t k = 0; k < n; ++k) cross_ok = cross_ok && seq_len[k] >= 1 && seq_len[k] <= pcabi::MAX_STRIPED_LEN;
     if (!cross_ok) {
         // some sequence cannot be a DP row set: explicit pairs (the longer is never a row set)
         std::vector<int32_t> pi, pj;
@@ -2152,7 +2345,13 @@ int check_compatibility(char *raw_seq1, char *raw_seq2) {
     const int32_t len[2] = {(int32_t)n1, (int32_t)n2};
     const int32_t pi = 0, pj = 1;
     int32_t flag = 0;
-    if (pcabi_compat_host(0, codes.data(), (int64_t)codes.size(), off, len, 2, &pi, &pj, 1, &flag) != 0) return 0;
+    int device = 0;
+    (void)hipGetDevice(&device);
+    if (pcabi_compat_host(device, codes.data(), (int64_t)codes.size(), off, len, 2, &pi, &pj, 1, &flag) != 0) {
+        // the reference has no error channel and never fails here: stop rather than answer wrongly
+        std::fprintf(stderr, "libpcabi: check_compatibility failed: %s\n", pcabi_last_error());
+        std::abort();
+    }
     return flag;
 }
 

@@ -96,7 +96,18 @@ struct pcabi_fastx {
 namespace {
 namespace bigmem {
 constexpr size_t kBig = 64ull << 20;
-constexpr size_t kCacheMax = 24ull << 30;
+// Free blocks kept for reuse: PCABI_IO_CACHE_MB, default min(4 GB, physical memory / 8) -- enough
+// for the batches a pipeline keeps in flight; pcabi_io_release_cache() returns them all.
+size_t cache_max() {
+    static const size_t v = [] {
+        const char *e = std::getenv("PCABI_IO_CACHE_MB");
+        if (e && e[0]) return (size_t)std::max(0LL, std::atoll(e)) << 20;
+        const long pages = sysconf(_SC_PHYS_PAGES), psz = sysconf(_SC_PAGE_SIZE);
+        const size_t ram = (pages > 0 && psz > 0) ? (size_t)pages * (size_t)psz : (8ull << 30);
+        return std::min<size_t>(4ull << 30, ram / 8);
+    }();
+    return v;
+}
 std::mutex mu;
 std::unordered_map<void *, size_t> mapped;          // live and cached blocks -> mapped bytes
 std::vector<std::pair<void *, size_t>> cache;       // free blocks
@@ -136,15 +147,26 @@ void put(void *p, size_t bytes) {
     const size_t m = mapped.at(p);
     cache.emplace_back(p, m);
     cached += m;
-    while (cached > kCacheMax && !cache.empty()) {   // drop the oldest
+    while (cached > cache_max() && !cache.empty()) {   // drop the oldest
         munmap(cache.front().first, cache.front().second);
         mapped.erase(cache.front().first);
         cached -= cache.front().second;
         cache.erase(cache.begin());
     }
 }
+void release() {
+    std::lock_guard<std::mutex> g(mu);
+    for (auto &c : cache) {
+        munmap(c.first, c.second);
+        mapped.erase(c.first);
+    }
+    cache.clear();
+    cached = 0;
+}
 }  // namespace bigmem
 }  // namespace
+
+extern "C" void pcabi_io_release_cache(void) { bigmem::release(); }
 
 // vector whose resize() leaves new elements uninitialised (the batch buffers are written once,
 // in parallel; zero-filling gigabytes first would cost as much as the parse)

@@ -49,7 +49,9 @@ class FileTrimmer(object):
             int(extra_middle_trim_bad_side)
         self.min_split, self.no_split, self.discard_middle = int(min_split_read_size), bool(no_split), \
             bool(discard_middle)
-        self.filter_reads = bool(filter_reads)
+        # the reference filters only when some adapter set matched (porechop_abi.py:93-122); with
+        # none, every read is written unchanged
+        self.filter_reads = bool(filter_reads) and bool(matching_sets)
         self.start_adps = [a.start_sequence[1] for a in matching_sets if a.start_sequence]
         self.end_adps = [a.end_sequence[1] for a in matching_sets if a.end_sequence]
         mids, start_names, end_names = middle_adapter_list(matching_sets)
@@ -186,14 +188,25 @@ class FileTrimmer(object):
         pq = queue.Queue(maxsize=2)
         wq = queue.Queue(maxsize=2)
         errors = []
+        stop = threading.Event()          # set when this thread leaves: the reader stops putting
+
+        def put_parsed(item):
+            while not stop.is_set():
+                try:
+                    pq.put(item, timeout=0.05)
+                    return True
+                except queue.Full:
+                    pass
+            return False
 
         def produce():
             try:
                 for b in misc.read_batches(in_path, max_reads=max_reads):
-                    pq.put(b)
-                pq.put(None)
+                    if not put_parsed(b):
+                        return
+                put_parsed(None)
             except BaseException as ex:   # handed to the consumer
-                pq.put(ex)
+                put_parsed(ex)
 
         def consume_writes():
             first = True
@@ -223,7 +236,7 @@ class FileTrimmer(object):
         writer.start()
         t = time.perf_counter()
         try:
-            while True:
+            while not errors:                # a failed write stops the run at the next batch
                 b = pq.get()
                 t = self._tick('parse', t)   # waiting for a parsed batch
                 if b is None:
@@ -231,10 +244,13 @@ class FileTrimmer(object):
                 if isinstance(b, BaseException):
                     raise b
                 st, et, co, cu, _, keep = self.trim(b)
-                wq.put((b, st, et, co, cu, keep))
+                wq.put((b, st, et, co, cu, keep))   # the writer drains even after a failure
                 del b
                 t = time.perf_counter()
         finally:
+            # on every exit (errors included) the reader's pending put times out on `stop`, so
+            # joining it cannot block on a full queue
+            stop.set()
             wq.put(None)
             writer.join()
             reader.join()

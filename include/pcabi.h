@@ -24,9 +24,17 @@
  *
  * Errors: functions return 0 on success, a negative PCABI_E_* code otherwise;
  * pcabi_last_error() returns a thread-local message. No exceptions cross the ABI.
- * There is no CPU fallback: without a usable gfx950 device every compute entry point fails
- * (the legacy adapterAlignment then returns a string whose first field is -1 and sets
- * pcabi_last_error()).
+ * There is no CPU fallback: without a usable gfx950 device every compute entry point fails.
+ * The two drop-in symbols have no error channel (the reference's never fail on valid input):
+ * when the engine fails under them they print pcabi_last_error() to stderr and abort() rather
+ * than return an answer the reference would not give (adapterAlignment's "-1" sentinel would read
+ * as "no alignment" and silently change trimming decisions). Empty inputs keep the reference's
+ * "-1" result.
+ *
+ * Lengths: windows / reads of any length up to pcabi_max_window_len(); adapters (and the
+ * shorter sequence of a check_compatibility pair) up to pcabi_max_adapter_len() = 65535 bases.
+ * Adapters up to 128 bases run register-resident cores; longer ones the striped core
+ * (row stripes of 32, the boundary row in stream-ordered device scratch).
  */
 #ifndef PCABI_H
 #define PCABI_H
@@ -67,7 +75,7 @@ void freeCString(char *p);
 const char *pcabi_last_error(void);
 int pcabi_version(void);                 /* ABI version, currently 1                     */
 int pcabi_device_count(void);            /* visible HIP devices (0 if none)              */
-int pcabi_max_adapter_len(void);         /* longest adapter the kernels accept           */
+int pcabi_max_adapter_len(void);         /* longest adapter the kernels accept (65535)   */
 int pcabi_max_window_len(void);          /* longest window / read the kernels accept     */
 
 /* ASCII -> Dna5 codes (host, table lookup). n bytes. */
@@ -276,7 +284,8 @@ int pcabi_barcode_call_host(int device, const int32_t *start_res, int32_t n_sa, 
  * ACGTU is A) of the longer sequence against the shorter, then the reference's flag:
  * 0 not compatible, 1 compatible (integer identity of the aligned region >= 87.5), 2 compatible
  * and the shorter lies inside the longer (region more than 3 bases from an end).
- *   check_compatibility : the drop-in symbol of the reference's compatibility.so (device 0).
+ *   check_compatibility : the drop-in symbol of the reference's compatibility.so (current device;
+ *       aborts with a message if the engine fails, see Errors above).
  *   pcabi_compat_host   : n_pairs (pair_i[t], pair_j[t]) of n_seq sequences given as Dna codes
  *       (0..3) in one buffer (seq_off / seq_len, 16 bytes of padding), flags[n_pairs]; the
  *       shorter sequence of a pair must be <= pcabi_max_adapter_len() bases. Empty -> 0.
@@ -286,8 +295,9 @@ int pcabi_compat_host(int device, const uint8_t *codes, int64_t codes_len, const
                       const int32_t *seq_len, int64_t n_seq, const int32_t *pair_i, const int32_t *pair_j,
                       int64_t n_pairs, int32_t *flags);
 /* consensus.py:72-100 all_vs_all_matrix: mat[n_seq * n_seq] (row-major, -1 on the diagonal,
- * symmetric). Runs every sequence against every sequence in the tiled cross mode when all are
- * <= pcabi_max_adapter_len() bases (explicit pairs otherwise). n_seq <= 46340. */
+ * symmetric). Runs every sequence against every sequence in the tiled cross mode (sequences over
+ * 128 bases as rows on the striped core) when all are 1..pcabi_max_adapter_len() bases, explicit
+ * pairs otherwise. n_seq <= 46340. */
 int pcabi_compat_all_vs_all_host(int device, const uint8_t *codes, int64_t codes_len, const int64_t *seq_off,
                                  const int32_t *seq_len, int64_t n_seq, int32_t *mat);
 
@@ -381,6 +391,10 @@ int pcabi_reads_write(const pcabi_reads *b, const char *path, int append, int gz
                       const int32_t *start_trim, const int32_t *end_trim, const int64_t *cut_off,
                       const int64_t *cuts, int min_split_read_size, int discard_middle,
                       int untrimmed, const uint8_t *select);
+/* Batches of 64 MB and more live in huge-page mappings that freed batches hand to a process-wide
+ * cache (PCABI_IO_CACHE_MB, default min(4 GB, RAM / 8)) for the next batch to reuse; this
+ * returns every cached mapping to the system. */
+void pcabi_io_release_cache(void);
 
 #ifdef __cplusplus
 }

@@ -61,52 +61,72 @@ static int build_rows(const char *read, int n, const char *adapter, int l, int m
         return 0;
     }
     const int affine = (go != ge);
-    const int W = n + 1;
-    const size_t cells = (size_t)(l + 1) * (size_t)W;
-    int *S = (int *)malloc(cells * sizeof(int));
-    int *H = (int *)malloc(cells * sizeof(int));
-    int *V = (int *)malloc(cells * sizeof(int));
-    unsigned char *T = (unsigned char *)calloc(cells, 1);
+    const size_t cells = (size_t)(l + 1) * (size_t)(n + 1);
+    /* per-thread matrices, grown on demand and kept (fresh pages on every call cost more than
+     * the DP); every cell read below is written first (row 0 / column 0 by the init loops) */
+    static _Thread_local int *S, *H, *V;
+    static _Thread_local unsigned char *T;
+    static _Thread_local size_t cap_cells;
+    if (cells > cap_cells) {
+        free(S); free(H); free(V); free(T);
+        S = (int *)malloc(cells * sizeof(int));
+        H = (int *)malloc(cells * sizeof(int));
+        V = (int *)malloc(cells * sizeof(int));
+        T = (unsigned char *)malloc(cells);
+        cap_cells = cells;
+    }
     unsigned char *rc = (unsigned char *)malloc((size_t)n);
     unsigned char *ac = (unsigned char *)malloc((size_t)l);
     for (int j = 0; j < n; ++j) rc[j] = (unsigned char)(four ? dna4((unsigned char)read[j]) : dna5((unsigned char)read[j]));
     for (int i = 0; i < l; ++i) ac[i] = (unsigned char)(four ? dna4((unsigned char)adapter[i]) : dna5((unsigned char)adapter[i]));
-#define IDX(i, j) ((size_t)(i) * (size_t)W + (size_t)(j))
+/* column-major (the DP walks columns j, rows i inside): contiguous inner loop */
+#define IDX(i, j) ((size_t)(j) * (size_t)(l + 1) + (size_t)(i))
 
     /* free end gaps: first row and column are RecursionDirectionZero */
-    for (int j = 0; j <= n; ++j) { S[IDX(0, j)] = 0; H[IDX(0, j)] = NEG; V[IDX(0, j)] = NEG; }
-    for (int i = 0; i <= l; ++i) { S[IDX(i, 0)] = 0; H[IDX(i, 0)] = NEG; V[IDX(i, 0)] = NEG; }
+    for (int j = 0; j <= n; ++j) { S[IDX(0, j)] = 0; H[IDX(0, j)] = NEG; V[IDX(0, j)] = NEG; T[IDX(0, j)] = T_NONE; }
+    for (int i = 0; i <= l; ++i) { S[IDX(i, 0)] = 0; H[IDX(i, 0)] = NEG; V[IDX(i, 0)] = NEG; T[IDX(i, 0)] = T_NONE; }
 
+    /* (selects written as masks: the same values, without data-dependent branches) */
     for (int j = 1; j <= n; ++j) {
+        const int *Sp = S + IDX(0, j - 1), *Hp = H + IDX(0, j - 1);
+        int *Sc = S + IDX(0, j), *Hc = H + IDX(0, j), *Vc = V + IDX(0, j);
+        unsigned char *Tc = T + IDX(0, j);
+        const unsigned char r = rc[j - 1];
         for (int i = 1; i <= l; ++i) {
-            int sub = (rc[j - 1] == ac[i - 1]) ? ma : mi;
-            int diag = S[IDX(i - 1, j - 1)] + sub;
+            int sub = (r == ac[i - 1]) ? ma : mi;
+            int diag = Sp[i - 1] + sub;
             unsigned char tv;
             int s;
             if (affine) {
-                int hx = H[IDX(i, j - 1)] + ge, ho = S[IDX(i, j - 1)] + go;
-                int h = (hx < ho) ? ho : hx;
-                unsigned char hb = (hx < ho) ? T_HO : T_H;
-                int vx = V[IDX(i - 1, j)] + ge, vo = S[IDX(i - 1, j)] + go;
-                int v = (vx < vo) ? vo : vx;
-                unsigned char vb = (vx < vo) ? T_VO : T_V;
-                int g = (v < h) ? h : v;
-                unsigned char gb = (v < h) ? T_MAXH : T_MAXV;
-                if (diag < g) { s = g; tv = (unsigned char)(gb | hb | vb); }
-                else          { s = diag; tv = (unsigned char)(T_D | hb | vb); }
-                H[IDX(i, j)] = h;
-                V[IDX(i, j)] = v;
+                int hx = Hp[i] + ge, ho = Sp[i] + go;
+                int hopen = hx < ho;
+                int h = hopen ? ho : hx;
+                unsigned char hb = (unsigned char)(hopen ? T_HO : T_H);
+                int vx = Vc[i - 1] + ge, vo = Sc[i - 1] + go;
+                int vopen = vx < vo;
+                int v = vopen ? vo : vx;
+                unsigned char vb = (unsigned char)(vopen ? T_VO : T_V);
+                int fromh = v < h;
+                int g = fromh ? h : v;
+                unsigned char gb = (unsigned char)(fromh ? T_MAXH : T_MAXV);
+                int notd = diag < g;
+                s = notd ? g : diag;
+                tv = (unsigned char)((notd ? gb : T_D) | hb | vb);
+                Hc[i] = h;
+                Vc[i] = v;
             } else {
-                int v = S[IDX(i - 1, j)] + ge, h = S[IDX(i, j - 1)] + ge;
-                int g = (v < h) ? h : v;
-                unsigned char gb = (v < h) ? (T_H | T_MAXH) : (T_V | T_MAXV);
-                if (diag < g) { s = g; tv = gb; }
-                else          { s = diag; tv = T_D; }
-                H[IDX(i, j)] = NEG;
-                V[IDX(i, j)] = NEG;
+                int v = Sc[i - 1] + ge, h = Sp[i] + ge;
+                int fromh = v < h;
+                int g = fromh ? h : v;
+                unsigned char gb = (unsigned char)(fromh ? (T_H | T_MAXH) : (T_V | T_MAXV));
+                int notd = diag < g;
+                s = notd ? g : diag;
+                tv = notd ? gb : (unsigned char)T_D;
+                Hc[i] = NEG;
+                Vc[i] = NEG;
             }
-            S[IDX(i, j)] = s;
-            T[IDX(i, j)] = tv;
+            Sc[i] = s;
+            Tc[i] = tv;
         }
     }
 
@@ -197,7 +217,7 @@ static int build_rows(const char *read, int n, const char *adapter, int l, int m
     }
 
     free(path);
-    free(S); free(H); free(V); free(T); free(rc); free(ac);
+    free(rc); free(ac);
 #undef IDX
     *rr_out = rr;
     *ar_out = ar;
@@ -321,4 +341,96 @@ void pcabi_oracle_align_batch(const char *reads, const long long *read_off, cons
         o[0] = r.rs; o[1] = r.re; o[2] = r.as; o[3] = r.ae;
         o[4] = r.score; o[5] = r.m; o[6] = r.l1; o[7] = r.l2;
     }
+}
+
+/* find_middle_adapters' masked re-alignment loop (porechop_abi/nanopore_read.py:236-246), per
+ * read: for each adapter in order, align the (masked) read; while the full-adapter identity
+ * (the reference's "%f" text parsed back, nanopore_read.py:497-498) is not below the threshold,
+ * record the hit and mask its aligned read bases with '-' (which SeqAn's Dna5 reads as N).
+ * Reads are spread over n_threads threads. Hits come out per read in discovery order, reads in
+ * order: rows (read, adapter, read_start, read_end_exclusive, m, l2), row-major out[6][cap].
+ * Returns the number of hits (only the first cap are written). */
+#include <pthread.h>
+#include <stdlib.h>
+
+typedef struct {
+    int *v;
+    long long n, cap;
+} ivec;
+
+static void ivec_push6(ivec *x, const int *six) {
+    if (x->n + 6 > x->cap) {
+        x->cap = x->cap ? 2 * x->cap : 64;
+        x->v = (int *)realloc(x->v, sizeof(int) * (size_t)x->cap);
+    }
+    memcpy(x->v + x->n, six, 6 * sizeof(int));
+    x->n += 6;
+}
+
+typedef struct {
+    const char *reads, *adapters;
+    const long long *read_off;
+    const int *read_len, *adp_off, *adp_len;
+    long long n_reads;
+    int n_adp, ma, mi, go, ge, stride, first;
+    double threshold;
+    ivec *per_read;
+} middle_job;
+
+static double text_identity(int m, int l) {
+    char buf[64];
+    if (l == 0) return 0.0 / 0.0;
+    snprintf(buf, sizeof buf, "%f", 100.0 * m / l);
+    return strtod(buf, NULL);
+}
+
+static void *middle_worker(void *arg) {
+    const middle_job *J = (const middle_job *)arg;
+    for (long long w = J->first; w < J->n_reads; w += J->stride) {
+        const int n = J->read_len[w];
+        char *masked = (char *)malloc((size_t)n + 1);
+        memcpy(masked, J->reads + J->read_off[w], (size_t)n);
+        masked[n] = 0;
+        for (int a = 0; a < J->n_adp; ++a) {
+            for (;;) {
+                pcabi_oracle_result r;
+                pcabi_oracle_align(masked, n, J->adapters + J->adp_off[a], J->adp_len[a], J->ma, J->mi, J->go,
+                                   J->ge, &r);
+                const double full = r.rs == -1 ? 0.0 : text_identity(r.m, r.l2);
+                if (!(full >= J->threshold)) break;   /* NaN never hits (l2 > 0 whenever rs >= 0) */
+                const int rs = r.rs, rend = r.rs == -1 ? 0 : r.re + 1;
+                for (int k = rs; k < rend; ++k) masked[k] = '-';
+                const int six[6] = {(int)w, a, rs, rend, r.m, r.l2};
+                ivec_push6(&J->per_read[w], six);
+            }
+        }
+        free(masked);
+    }
+    return NULL;
+}
+
+long long pcabi_oracle_middle_scan(const char *reads, const long long *read_off, const int *read_len,
+                                   long long n_reads, const char *adapters, const int *adp_off, const int *adp_len,
+                                   int n_adp, int ma, int mi, int go, int ge, double threshold, int n_threads,
+                                   int *out, long long cap) {
+    if (n_threads < 1) n_threads = 1;
+    if (n_threads > 64) n_threads = 64;
+    ivec *per_read = (ivec *)calloc((size_t)(n_reads > 0 ? n_reads : 1), sizeof(ivec));
+    middle_job jobs[64];
+    pthread_t th[64];
+    for (int t = 0; t < n_threads; ++t) {
+        jobs[t] = (middle_job){reads, adapters, read_off, read_len, adp_off, adp_len, n_reads, n_adp, ma, mi, go, ge,
+                               n_threads, t, threshold, per_read};
+        pthread_create(&th[t], NULL, middle_worker, &jobs[t]);
+    }
+    for (int t = 0; t < n_threads; ++t) pthread_join(th[t], NULL);
+    long long h = 0;
+    for (long long w = 0; w < n_reads; ++w) {
+        for (long long k = 0; k < per_read[w].n; k += 6, ++h)
+            if (h < cap)
+                for (int f = 0; f < 6; ++f) out[f * cap + h] = per_read[w].v[k + f];
+        free(per_read[w].v);
+    }
+    free(per_read);
+    return h;
 }

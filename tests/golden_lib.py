@@ -6,10 +6,10 @@ import os
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 
 
-def g1_rows():
+def g1_rows(name='g1_alignments.tsv.gz'):
     """[(scheme tuple, read, adapter, reference result string)] -- tools/make_golden_g1.py."""
     rows = []
-    with gzip.open(os.path.join(GOLDEN, 'g1_alignments.tsv.gz'), 'rt') as f:
+    with gzip.open(os.path.join(GOLDEN, name), 'rt') as f:
         for line in f:
             line = line.rstrip('\n')
             if not line:
@@ -17,6 +17,11 @@ def g1_rows():
             sc, r, a, res = line.split('\t')
             rows.append((tuple(int(x) for x in sc.split(',')), r, a, res))
     return rows
+
+
+def g1_long_rows():
+    """The same for adapters longer than 128 bp -- tools/make_golden_g1_long.py."""
+    return g1_rows('g1_long.tsv.gz')
 
 
 def g2():

@@ -4,6 +4,7 @@
 #include "../../custom_porechop_abi_amd/csrc/pcabi_dp.h"
 #include <cstring>
 #include <utility>
+#include <vector>
 
 static int dna5(unsigned char c) {
     switch (c) { case 'A': case 'a': return 0; case 'C': case 'c': return 1; case 'G': case 'g': return 2;
@@ -191,6 +192,34 @@ static int run_compat(const char *a, int na, const char *b, int nb) {
     return pcabi::compat_flag(r, na, en_match);
 }
 
+// longer than 128: the striped core (what k_align_striped runs), boundary row in a host buffer
+struct HostBnd2 {
+    std::vector<pcabi::BndCell> v;
+    void load(int j, pcabi::BndCell &c) const { c = v[j]; }
+    void store(int j, const pcabi::BndCell &c) { v[j] = c; }
+};
+static int run_compat_striped(const char *a, int na, const char *b, int nb) {
+    constexpr int R = 32;
+    const int rt = (nb + 63) / 64 * 64;
+    struct Adp {
+        const char *b;
+        int pad, k;
+        void load(int kk) { k = kk; }
+        int operator()(int s) const {
+            const int i = k * R + s - 1 - pad;
+            return i < 0 ? pcabi::PAD_CODE : dna4((unsigned char)b[i]);
+        }
+    } ad{b, rt - nb, 0};
+    const pcabi::Scoring sc{2, -1, -1, -1};
+    auto rd = [&](int j) { return j <= na ? dna4((unsigned char)a[j - 1]) : 0; };
+    HostBnd2 bnd;
+    bnd.v.resize((size_t)na + 2);
+    const pcabi::Result r = pcabi::align_lane_striped<R, false>(rd, na, ad, nb, rt, sc, bnd);
+    int en_match = 0;
+    if (r.rs >= 0 && r.diag_en && r.l1 > 0) en_match = dna4((unsigned char)a[r.re]) == dna4((unsigned char)b[r.ae]);
+    return pcabi::compat_flag(r, na, en_match);
+}
+
 extern "C" int pcabi_model_compat(const char *s1, const char *s2) {
     int n1 = (int)std::strlen(s1), n2 = (int)std::strlen(s2);
     const char *a = s1, *b = s2;
@@ -199,7 +228,7 @@ extern "C" int pcabi_model_compat(const char *s1, const char *s2) {
     if (n2 <= 32) return run_compat<32>(a, n1, b, n2);
     if (n2 <= 64) return run_compat<64>(a, n1, b, n2);
     if (n2 <= 128) return run_compat<128>(a, n1, b, n2);
-    return -2;
+    return run_compat_striped(a, n1, b, n2);
 }
 
 // Middle-scan chunking (pcabi::sf::chunk_plan + align_lane_packed<.., CHUNK>): the read split into
@@ -271,6 +300,55 @@ extern "C" int pcabi_model_align_chunked(const char *read, int n, const char *ad
         ++n_chunks;
     });
     return n_chunks;
+}
+
+// Striped core (any adapter length): stripes of R rows, the boundary row in a host buffer, the
+// adapter top-padded to rt rows (a multiple of R, >= L; rt > the next multiple of R exercises whole
+// padding stripes). CHUNK semantics as the others (own_hi < 0: the read's last chunk).
+struct HostBnd {
+    std::vector<pcabi::BndCell> v;
+    void load(int j, pcabi::BndCell &c) const { c = v[j]; }
+    void store(int j, const pcabi::BndCell &c) { v[j] = c; }
+};
+
+template <int R>
+struct HostStripeAdp {
+    const char *adp;
+    int pad;
+    int k = 0;
+    void load(int kk) { k = kk; }
+    int operator()(int s) const {
+        const int i = k * R + s - 1 - pad;   // adapter index of table slot kR + s
+        return i < 0 ? pcabi::PAD_CODE : dna5((unsigned char)adp[i]);
+    }
+};
+
+template <int R>
+static void run_striped(const char *read, int n, const char *adp, int L, int rt, pcabi::Scoring sc, int own_lo,
+                        int own_hi, int *out) {
+    auto rd = [&](int j) { return j <= n ? dna5((unsigned char)read[j - 1]) : 4; };
+    HostStripeAdp<R> ad{adp, rt - L};
+    HostBnd bnd;
+    bnd.v.resize((size_t)n + 2);
+    pcabi::Result r = (sc.go != sc.ge)
+        ? pcabi::align_lane_striped<R, true>(rd, n, ad, L, rt, sc, bnd, own_lo, own_hi)
+        : pcabi::align_lane_striped<R, false>(rd, n, ad, L, rt, sc, bnd, own_lo, own_hi);
+    out[0] = r.rs; out[1] = r.re; out[2] = r.as; out[3] = r.ae;
+    out[4] = r.score; out[5] = r.m; out[6] = r.l1; out[7] = r.l2;
+}
+
+extern "C" int pcabi_model_align_striped(const char *read, int n, const char *adp, int L, int R, int extra_pad,
+                                         int ma, int mi, int go, int ge, int own_lo, int own_hi, int *out) {
+    pcabi::Scoring sc{ma, mi, go, ge};
+    if (L <= 0 || n <= 0 || L > pcabi::MAX_STRIPED_LEN) return -1;
+    const int rt = (L + R - 1) / R * R + extra_pad * R;
+    switch (R) {
+    case 8: run_striped<8>(read, n, adp, L, rt, sc, own_lo, own_hi, out); break;
+    case 16: run_striped<16>(read, n, adp, L, rt, sc, own_lo, own_hi, out); break;
+    case 32: run_striped<32>(read, n, adp, L, rt, sc, own_lo, own_hi, out); break;
+    default: return -2;
+    }
+    return 0;
 }
 
 // Long (two-pass) packed core, buckets of 96 / 112 / 128 rows; -3 if long_ok fails

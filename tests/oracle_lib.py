@@ -138,3 +138,33 @@ def middle_scan_windows(windows, adapter_seqs, scoring, threshold, device=0):
                 masked = masked[:rs] + '-' * (rend - rs) + masked[rend:]
                 out.append([w, a, rs, rend, r[5], r[7]])
     return np.array(out, np.int32).reshape(-1, 6).T.copy()
+
+
+def middle_scan_threaded(windows, adapter_seqs, scoring, threshold, threads=None):
+    """middle_scan_windows in C (pcabi_oracle_middle_scan), the reads spread over threads: the
+    checker for bench-sized middle scans (thousands of reads x the 98-adapter list)."""
+    L = load()
+    L.pcabi_oracle_middle_scan.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int] + \
+        [ctypes.c_int] * 4 + [ctypes.c_double, ctypes.c_int, ctypes.c_void_p, ctypes.c_longlong]
+    L.pcabi_oracle_middle_scan.restype = ctypes.c_longlong
+    codes, offs, lens = windows
+    text = _LETTERS[np.asarray(codes)]                     # '-'-free: masked bases are N, as '-' is
+    roff = np.ascontiguousarray(offs, np.int64)
+    rlen = np.ascontiguousarray(lens, np.int32)
+    ab = [a.encode() for a in adapter_seqs]
+    abuf = np.frombuffer(b''.join(ab) + b'\0', np.uint8)
+    alen = np.array([len(x) for x in ab], np.int32)
+    aoff = np.zeros(len(ab), np.int32)
+    if len(ab) > 1:
+        aoff[1:] = np.cumsum(alen)[:-1]
+    threads = threads or min(16, os.cpu_count() or 1)
+    vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    cap = 1 << 16
+    while True:
+        out = np.zeros((6, cap), np.int32)
+        nh = L.pcabi_oracle_middle_scan(vp(text), vp(roff), vp(rlen), len(rlen), vp(abuf), vp(aoff), vp(alen), len(ab),
+                                        *scoring[:4], float(threshold), threads, vp(out), cap)
+        if nh <= cap:
+            return out[:, :nh].copy()
+        cap = int(nh)

@@ -33,7 +33,8 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(so, name), name
     assert set(_lib.exported_symbols()) == set(declared_functions())
     assert L.pcabi_version() == 1
-    assert L.pcabi_max_adapter_len() >= 111       # full rapid barcode adapters
+    assert L.pcabi_max_adapter_len() == 65535     # striped core: adapters of any practical length
+    L.pcabi_io_release_cache()                    # host only: returns the cached batch mappings
 
 
 def test_encode_dna5_matches_seqan_table():
@@ -64,11 +65,23 @@ def test_compute_fails_loudly_without_device():
     L = _lib.lib()
     if L.pcabi_device_count() > 0:
         pytest.skip('a GPU is visible')
-    # no CPU fallback: batch API raises, legacy ABI returns the no-alignment sentinel
+    # no CPU fallback: the batch API raises ...
     pack = engine.SeqPack(['ACGTACGTAC'])
     with pytest.raises(_lib.PcabiError):
         engine.align(pack.views([0], pack.lengths), ['GTAC'], [3, -6, -5, -2])
-    assert w.adapter_alignment('ACGTACGTAC', 'GTAC', [3, -6, -5, -2]).split(',')[0] == '-1'
+    # ... and the legacy symbols, which have no error channel, stop the process with the reason
+    # instead of answering "no alignment" (VERDICT r1); empty inputs keep the reference's "-1"
+    assert w.adapter_alignment('', 'GTAC', [3, -6, -5, -2]).split(',')[0] == '-1'
+    import subprocess
+    import sys
+    code = ('import sys; sys.path.insert(0, %r); from custom_porechop_abi_amd import cpp_function_wrappers as w; '
+            'print(w.adapter_alignment("ACGTACGTAC", "GTAC", [3, -6, -5, -2]))' % ROOT)
+    p = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0 and 'adapterAlignment failed' in p.stderr, (p.returncode, p.stdout, p.stderr[-400:])
+    code = ('import sys; sys.path.insert(0, %r); from custom_porechop_abi_amd import _lib; '
+            'print(_lib.lib().check_compatibility(b"ACGTACGTAC", b"ACGTAC"))' % ROOT)
+    p = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0 and 'check_compatibility failed' in p.stderr, (p.returncode, p.stdout, p.stderr[-400:])
 
 
 def test_window_views_match_python_slices():

@@ -382,3 +382,106 @@ def test_long_two_pass_core(model):
         assert rc == 0 and list(res) == oracle_lib.align(r, a, sc), (sc, r, a)
         n_checked += 1
     assert n_checked > 400
+
+
+def _striped(model, r, a, sc, R, extra_pad=0, own_lo=1, own_hi=-1):
+    model.pcabi_model_align_striped.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int] + \
+        [ctypes.c_int] * 8 + [ctypes.c_void_p]
+    out = (ctypes.c_int * 8)()
+    rb, ab = r.encode(), a.encode()
+    rc = model.pcabi_model_align_striped(rb, len(rb), ab, len(ab), R, extra_pad, *sc, own_lo, own_hi, out)
+    assert rc == 0
+    return list(out)
+
+
+def test_striped_core_many_stripes(model):
+    """The striped core (align_lane_striped: adapters of any length, row stripes of R rows, the
+    boundary row through a per-lane buffer) with narrow stripes, so short adapters already cross
+    many stripe boundaries: random and tie-heavy alphabets, every scheme (linear and affine,
+    open cheaper than extend), whole padding stripes above the adapter."""
+    rng = random.Random(101)
+    schemes = [(3, -6, -5, -2), (2, -1, -1, -1), (1, -1, -3, -1), (3, -6, -2, -5), (5, -4, -8, -6)]
+    for it in range(2500):
+        sc = schemes[it % len(schemes)]
+        al = rng.choice(['A', 'AT', 'ACGT', 'ACGTN'])
+        L = rng.randint(1, 80)
+        a = ''.join(rng.choice(al) for _ in range(L))
+        r = ''.join(rng.choice(al) for _ in range(rng.randint(1, 220)))
+        if rng.random() < 0.4 and len(r) > 20:
+            p = rng.randint(0, len(r))
+            r = r[:p] + _mutate_cpu(rng, a, rng.choice([0.0, 0.1])) + r[p:]
+        R = rng.choice([8, 16, 32])
+        got = _striped(model, r, a, sc, R, extra_pad=rng.choice([0, 0, 1, 2]))
+        assert got == oracle_lib.align(r, a, sc), (sc, R, r, a)
+
+
+def test_striped_core_long_adapters(model):
+    """Adapters of 129-1200 bp (custom adapter files, ab-initio adapters with a large -sl) on end
+    windows and longer reads, mutated copies (whole, cut at the read ends), the reference's
+    golden rows above 128 bp."""
+    n_gold = 0
+    for sc, r, a, exp in golden_lib.g1_rows() + golden_lib.g1_long_rows():
+        if not r or not a or len(a) <= 128:
+            continue
+        assert _fmt(_striped(model, r, a, sc, 32)) == exp, (sc, len(r), len(a))
+        n_gold += 1
+    assert n_gold >= 500
+    rng = random.Random(103)
+    schemes = [(3, -6, -5, -2), (2, -1, -1, -1), (1, -1, -3, -1), (3, -6, -2, -5), (5, -4, -8, -6)]
+    for it in range(150):
+        sc = schemes[it % len(schemes)]
+        L = rng.choice([129, 200, 255, 256, 300, 512, 700])
+        a = ''.join(rng.choice('ACGT') for _ in range(L))
+        n = rng.choice([1, 40, 150, rng.randint(150, 1500)])
+        r = ''.join(rng.choice('ACGT' if rng.random() < 0.8 else 'ACGTN') for _ in range(n))
+        if rng.random() < 0.7:
+            cp = _mutate_cpu(rng, a, rng.choice([0.0, 0.05, 0.15]))
+            w = rng.random()
+            if w < 0.25:
+                r = cp[rng.randint(0, L // 2):] + r
+            elif w < 0.5:
+                r = r + cp[:rng.randint(1, len(cp))]
+            else:
+                p = rng.randint(0, len(r))
+                r = r[:p] + cp + r[p:]
+        got = _striped(model, r, a, sc, 32)
+        assert got == oracle_lib.align(r, a, sc), (sc, L, len(r))
+
+
+@pytest.mark.parametrize('sc', [(3, -6, -5, -2), (2, -1, -1, -1), (5, -4, -8, -6)])
+def test_striped_core_chunks(model, sc):
+    """The striped core in chunk mode (the middle scan's candidate DP on long adapters): chunks
+    of C owned columns merged in read order equal the whole read whenever its score reaches T."""
+    rng = random.Random(sum(sc) + 211)
+    adps = [''.join(rng.choice('ACGT') for _ in range(L)) for L in (40, 150, 260)]
+    n_hi = 0
+    for it in range(60):
+        a = rng.choice(adps)
+        r = ''.join(rng.choice('ACGT') for _ in range(rng.randint(200, 2500)))
+        for _ in range(rng.choice([1, 1, 2])):
+            p = rng.randint(0, len(r))
+            r = r[:p] + _mutate_cpu(rng, a, rng.choice([0.0, 0.05])) + r[p:]
+        T = model.pcabi_model_filter_threshold(len(a), 85.0, *sc)
+        D = len(a) + (len(a) * sc[0] - T + min(-sc[2], -sc[3]) - 1) // min(-sc[2], -sc[3]) + 2
+        whole = oracle_lib.align(r, a, sc)
+        C = rng.choice([7, 100, 512])
+        best = None
+        for lo in range(1, len(r) + 1, C):
+            hi = lo + C
+            start = max(0, lo - 1 - D)
+            last = hi > len(r)
+            seg = r[start:] if last else r[start:hi - 1]
+            got = _striped(model, seg, a, sc, 32, own_lo=lo - start, own_hi=-1 if last else hi - start)
+            if best is None or got[4] > best[4]:
+                best = got[:]
+                if best[0] >= 0:
+                    best[0] += start
+                    best[1] += start
+            if last:
+                break
+        if whole[4] >= T:
+            assert best == whole, (sc, len(a), C)
+            n_hi += 1
+        else:
+            assert best[4] < T
+    assert n_hi > 20

@@ -1,12 +1,15 @@
 """The CPU oracle (oracle/pcabi_oracle.c) reproduces the reference's adapterAlignment text on
 every golden vector produced by the reference itself (tests/golden/g1_alignments.tsv.gz,
 tools/make_golden_g1.py) and on the reference's known answers."""
+import pytest
+
 from tests import golden_lib, oracle_lib
 
 
-def test_oracle_matches_reference_vectors():
-    rows = golden_lib.g1_rows()
-    assert len(rows) >= 20000
+@pytest.mark.parametrize('which', ['g1', 'g1_long'])
+def test_oracle_matches_reference_vectors(which):
+    rows = golden_lib.g1_rows() if which == 'g1' else golden_lib.g1_long_rows()
+    assert len(rows) >= (20000 if which == 'g1' else 1500)
     bad = []
     for sc, r, a, exp in rows:
         got = oracle_lib.result_string(r, a, sc)
@@ -30,3 +33,29 @@ def test_known_answers():
     for r, a, exp in cases:
         assert oracle_lib.result_string(r, a, sc) == exp
     assert oracle_lib.result_string('', 'ACGT', sc).split(',')[0] == '-1'
+
+
+def test_threaded_middle_loop_equals_python_loop():
+    """The oracle's C middle loop (pcabi_oracle_middle_scan, threads over reads: the checker of
+    the bench-sized middle-scan tests) == the reference's loop restated in Python on the oracle."""
+    import random
+
+    import numpy as np
+
+    from custom_porechop_abi_amd import engine
+    rng = random.Random(5)
+    adps = ['AATGTACTTCGTTCAGTTACGTATTGCT', 'GCAATACGTAACTGAACGAAGT', ''.join(rng.choice('ACGT') for _ in range(150))]
+    reads = []
+    for k in range(60):
+        r = ''.join(rng.choice('ACGT') for _ in range(rng.randint(0, 1500)))
+        for _ in range(rng.choice([0, 1, 2, 3])):
+            p = rng.randint(0, len(r))
+            a = rng.choice(adps)
+            r = r[:p] + a + (a if rng.random() < 0.2 else '') + r[p:]
+        reads.append(r)
+    pack = engine.SeqPack(reads)
+    views = pack.views(np.zeros(len(reads), np.int64), pack.lengths)
+    for sc in [(3, -6, -5, -2), (2, -1, -1, -1)]:
+        a = oracle_lib.middle_scan_windows(views, adps, sc, 85.0)
+        b = oracle_lib.middle_scan_threaded(views, adps, sc, 85.0, 4)
+        assert a.shape[1] > 50 and np.array_equal(a, b)

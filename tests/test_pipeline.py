@@ -67,3 +67,81 @@ def test_trim_file_matches_reference_pipeline(gpu_lib, case_name, tmp_path):
     got = open(out_path).read()
     exp = _expected(case, records)
     assert got == exp
+
+
+def _fastq(path, n, seed=3):
+    import random
+    rng = random.Random(seed)
+    with open(path, 'w') as f:
+        for k in range(n):
+            s = ''.join(rng.choice('ACGT') for _ in range(rng.randint(50, 300)))
+            f.write('@r%d\n%s\n+\n%s\n' % (k, s, 'I' * len(s)))
+
+
+def _bare_trimmer(filter_reads=True, matching=True):
+    """A FileTrimmer without device state (trim() is replaced by the test): trim_file's threads
+    and the native reader / writer only."""
+    from custom_porechop_abi_amd.pipeline import FileTrimmer
+    ft = object.__new__(FileTrimmer)
+    ft.min_split, ft.discard_middle, ft.times = 1000, False, {}
+    ft.filter_reads = filter_reads and matching
+    return ft
+
+
+@pytest.mark.parametrize('fail_at', ['trim', 'write'])
+def test_trim_file_stops_on_failure_without_hanging(tmp_path, fail_at):
+    """A failing trim() (device error) or write must end trim_file with that error, not a hang:
+    tiny batches keep the parsed-batch queue full when the failure hits."""
+    import threading
+    import numpy as np
+    from custom_porechop_abi_amd import misc
+    in_path, out_path = str(tmp_path / 'in.fastq'), str(tmp_path / 'out.fastq')
+    _fastq(in_path, 400)
+    ft = _bare_trimmer()
+    calls = []
+
+    def trim(b):
+        calls.append(b.n)
+        if fail_at == 'trim' and len(calls) == 3:
+            raise RuntimeError('injected device failure')
+        z = np.zeros(b.n, np.int32)
+        return z, z, np.zeros(b.n + 1, np.int64), np.zeros(0, np.int64), None, np.ones(b.n, np.uint8)
+    ft.trim = trim
+    if fail_at == 'write':
+        real = misc.write_reads
+
+        def bad_write(*a, **k):
+            raise OSError('injected write failure')
+        misc.write_reads = bad_write
+    res = {}
+
+    def run():
+        try:
+            ft.trim_file(in_path, out_path, max_reads=5)
+        except BaseException as ex:
+            res['ex'] = ex
+    th = threading.Thread(target=run, daemon=True)
+    th.start()
+    th.join(30)
+    if fail_at == 'write':
+        misc.write_reads = real
+    assert not th.is_alive(), 'trim_file hung after a failure'
+    assert 'injected' in str(res.get('ex')), res
+    if fail_at == 'write':
+        assert len(calls) < 80, 'the run did not stop early after the write failure'
+
+
+@pytest.mark.gpu
+def test_trim_file_without_matching_sets_writes_reads_unchanged(gpu_lib, tmp_path):
+    """No adapter set matched: the reference writes every read unchanged (porechop_abi.py:93-125
+    applies filter_reads_by_adapter only inside `if matching_sets:`)."""
+    from custom_porechop_abi_amd.pipeline import FileTrimmer
+    in_path, out_path = str(tmp_path / 'in.fastq'), str(tmp_path / 'out.fastq')
+    _fastq(in_path, 30)
+    ft = FileTrimmer([])
+    try:
+        counts = ft.trim_file(in_path, out_path, max_reads=7)
+    finally:
+        ft.close()
+    assert counts == {'reads_in': 30, 'reads_kept': 30}
+    assert open(out_path).read() == open(in_path).read()

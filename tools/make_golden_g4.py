@@ -3,7 +3,9 @@
 porechop_abi/ab_initio_src/compatibility.cpp and the vendored SeqAn), for the ab-initio
 clustering's all-vs-all link test (porechop_abi/consensus.py:72-100).
 
-Container-only generator. Pairs: adapter-like sequences of 4-120 bp and their mutated copies
+Container-only generator. `--long` writes tests/golden/g4_compat_long.json.gz instead: the same
+pair kinds over 129-600 bp sequences (both longer than the register-resident cores' 128 rows,
+so the shorter one runs on the striped core). Pairs: adapter-like sequences of 4-120 bp and their mutated copies
 (substitutions / insertions / deletions at 0-25%), contained substrings, prefix / suffix
 overlaps, unrelated pairs, equal lengths (row-order ties), lower case, U, N and IUPAC letters
 (SeqAn String<Dna> maps them to A). Pairs whose Dna letters share nothing are skipped: with no
@@ -40,17 +42,21 @@ def dna(c):
     return c if c in 'CGT' else ('T' if c == 'U' else 'A')
 
 
-def main():
+def main(long=False):
     ref = ctypes.CDLL(os.path.join(ROOT, 'oracle', '_ref', 'compatibility.so'))
     ref.check_compatibility.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
     ref.check_compatibility.restype = ctypes.c_int
     orc = ctypes.CDLL(os.path.join(ROOT, 'oracle', 'liboracle.so'))
     orc.pcabi_oracle_compat.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
     orc.pcabi_oracle_compat.restype = ctypes.c_int
-    rng = random.Random(4242)
+    rng = random.Random(4243 if long else 4242)
+    out = OUT.replace('g4_compat', 'g4_compat_long') if long else OUT
     pairs = []
-    while len(pairs) < 20000:
-        L = rng.choice([4, 8, 12, 16, 20, 22, 24, 28, 32, 40, 50, 64, 80, 100, 120, rng.randint(4, 120)])
+    while len(pairs) < (2000 if long else 20000):
+        if long:
+            L = rng.choice([129, 150, 200, 255, 300, 400, 600, rng.randint(129, 600)])
+        else:
+            L = rng.choice([4, 8, 12, 16, 20, 22, 24, 28, 32, 40, 50, 64, 80, 100, 120, rng.randint(4, 120)])
         alph = rng.choice(['ACGT'] * 6 + ['acgt', 'ACGTN', 'ACGU', 'AT', 'ACGTRYKM'])
         a = ''.join(rng.choice(alph) for _ in range(L))
         kind = rng.random()
@@ -68,7 +74,9 @@ def main():
             b = mutate(rng, a, 0.05)
             b = b[:L] if len(b) >= L else b + a[len(b):]          # equal lengths
         else:
-            b = ''.join(rng.choice(alph) for _ in range(rng.randint(4, 120)))
+            b = ''.join(rng.choice(alph) for _ in range(rng.randint(129, 600) if long else rng.randint(4, 120)))
+        if long and min(len(a), len(b)) <= 128:
+            continue
         if not b:
             continue
         if not (set(map(dna, a)) & set(map(dna, b))):
@@ -80,11 +88,12 @@ def main():
         if o != f:
             raise SystemExit('oracle restatement differs: %r %r ref=%d oracle=%d' % (a, b, f, o))
         pairs.append([a, b, f])
-    with gzip.open(OUT, 'wt') as fh:
-        json.dump({'generator': 'tools/make_golden_g4.py', 'pairs': pairs}, fh)
+    with gzip.open(out, 'wt') as fh:
+        json.dump({'generator': 'tools/make_golden_g4.py' + (' --long' if long else ''), 'pairs': pairs}, fh)
     counts = [sum(1 for p in pairs if p[2] == k) for k in range(3)]
-    print('wrote', OUT, len(pairs), 'pairs; flags 0/1/2:', counts)
+    print('wrote', out, len(pairs), 'pairs; flags 0/1/2:', counts)
 
 
 if __name__ == '__main__':
-    main()
+    import sys
+    main(long='--long' in sys.argv[1:])
