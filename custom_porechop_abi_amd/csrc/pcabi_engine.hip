@@ -29,55 +29,23 @@
 
 #include "../../include/pcabi.h"
 #include "pcabi_dp.h"
-
-#ifndef PCABI_WAVES
-#define PCABI_WAVES 1
-#endif
+#include "pcabi_kern.h"
 
 namespace {
-
 thread_local std::string g_err;
+}  // namespace
 
+namespace pcabi_eng {
 int fail(int code, const std::string &msg) {
     g_err = msg;
     return code;
 }
+}  // namespace pcabi_eng
 
-#define HIP_TRY(expr)                                                                   \
-    do {                                                                                \
-        hipError_t e_ = (expr);                                                         \
-        if (e_ != hipSuccess)                                                           \
-            return fail(PCABI_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
-    } while (0)
+using namespace pcabi_eng;
 
-// Register buckets. FAST (branch-free core, pcabi_dp.h align_lane_fast): every multiple of 4 up
-// to 64, used whenever pcabi::fast_ok holds (and served by the packed-key core when every
-// adapter of the bucket is pcabi::packed_ok). WIDE (packed-key core only, wide key layout
-// pk::Lay<RPL > 64>): every multiple of 4 from 68 to 88, for the 65-88 bp adapters (native
-// barcoding "full sequence" adapters) whenever packed_ok holds. GENERIC (guarded core, any
-// scoring): a few sizes, the path for everything else up to 128.
-// LONG (two-pass packed core, pk::LayL): 96 / 112 / 128 rows for the 89-128 bp adapters (the
-// 102 / 111 bp full rapid-barcode sequences) whenever pcabi::long_ok holds.
-// STRIPED (pcabi_dp.h align_lane_striped, k_align_striped): every adapter longer than kMaxRPL, any
-// scoring, rows in stripes of kStripeRows with the boundary row in global scratch; its table pads
-// every adapter to the bucket's longest, rounded up to kStripeTab rows (pcabi_adapters::rt).
-enum Kind { FAST = 0, GENERIC = 1, PACKED = 2, WIDE = 3, LONG = 4, STRIPED = 5 };
-struct BucketDef {
-    int rpl;
-    Kind kind;
-};
-constexpr BucketDef kBuckets[] = {
-    {4, FAST},  {8, FAST},  {12, FAST}, {16, FAST}, {20, FAST}, {24, FAST}, {28, FAST}, {32, FAST},
-    {36, FAST}, {40, FAST}, {44, FAST}, {48, FAST}, {52, FAST}, {56, FAST}, {60, FAST}, {64, FAST},
-    {68, WIDE}, {72, WIDE}, {76, WIDE}, {80, WIDE}, {84, WIDE}, {88, WIDE},
-    {96, LONG}, {112, LONG}, {128, LONG},
-    {16, GENERIC}, {32, GENERIC}, {64, GENERIC}, {96, GENERIC}, {128, GENERIC},
-    {256, STRIPED}};
-constexpr int kNumBuckets = sizeof(kBuckets) / sizeof(kBuckets[0]);
-constexpr int kStripedBucket = kNumBuckets - 1;
-constexpr int kMaxRPL = 128;                          // longest adapter a register-resident core holds
-constexpr int kStripeRows = 32;
-constexpr int kStripeTab = 64;
+namespace {
+
 
 int bucket_of(int L, const pcabi::Scoring &sc, bool allow_wide = true) {
     if (L > kMaxRPL) return kStripedBucket;
@@ -94,212 +62,6 @@ int bucket_of(int L, const pcabi::Scoring &sc, bool allow_wide = true) {
     for (int b = 0; b < kNumBuckets; ++b)
         if (kBuckets[b].kind == GENERIC && L <= kBuckets[b].rpl) return b;
     return -1;
-}
-
-struct KParams {
-    const uint8_t *codes;      // pairs mode: windows read in place
-    const int64_t *win_off;
-    const int32_t *win_len;
-    int64_t n_win;
-    const uint32_t *tiles;     // cross mode: windows in tile layout (pcabi_tile_windows_dev)
-    const int64_t *tile_off;   // [n_tiles + 1] dword offsets
-    // bucket-local adapter table: RPL bytes per adapter, top padded (slot s-1 <-> byte s-1)
-    const uint32_t *adp_pad;
-    const int32_t *adp_len;
-    const int32_t *adp_id;     // global adapter index (result row in cross mode)
-    int32_t n_adp;
-    // pairs mode
-    const int32_t *task_win;   // [n_waves*64], -1 = idle lane
-    const int32_t *task_out;   // [n_waves*64] result index
-    const int32_t *wave_adp;   // [n_waves] bucket-local adapter
-    int64_t n_waves;
-    int32_t *out;
-    int64_t out_stride;
-    pcabi::Scoring sc;
-    int32_t *compat;           // != nullptr: write check_compatibility flags instead of results
-    const int4 *task_chunk;    // k_align_chunk: per task slot (read offset, columns, owned lo, hi)
-    // striped bucket (k_align_striped)
-    int32_t rt;                // table rows per adapter (multiple of kStripeTab)
-    int32_t max_cols;          // host value: no window / chunk of the launch is longer
-    int32_t *scratch;          // boundary rows: per wave slot max_cols x fields x 64 lanes
-    int64_t n_items;           // waves of work (cross: 64-window groups x adapters)
-};
-
-// Window reader: one dword per lane every 4 columns (a wave-uniform branch -- j is the same in
-// every lane), fetched one chunk ahead. Two layouts share it:
-//   tiles (cross mode): chunk q of the lane's window at base[q * 256], so a wave's load is 256
-//                       contiguous bytes (pcabi_tile_windows_dev builds the layout);
-//   codes (pairs mode): the window's own bytes, base = its aligned dword, stride 1, a8 = 8 x
-//                       misalignment; reads at most 12 bytes past the window end.
-struct WindowReader {
-    const uint32_t *q;
-    int64_t stride;      // dwords between consecutive chunks
-    int a8;
-    uint32_t lo, hi, nx;
-    __device__ __forceinline__ WindowReader(const uint32_t *base, int64_t stride_, int a8_)
-        : q(base), stride(stride_), a8(a8_) {
-        lo = q[0]; hi = q[stride]; nx = q[2 * stride];
-    }
-    __device__ __forceinline__ int operator()(int j) {   // called with j = 1, 2, 3, ... in order
-        const int k = j - 1;
-        if (k > 0 && (k & 3) == 0) { lo = hi; hi = nx; nx = q[(int64_t)(k / 4 + 2) * stride]; }
-        return (int)(((((uint64_t)hi << 32) | lo) >> (8 * (k & 3) + a8)) & 0xFFu);
-    }
-};
-
-template <int RPL>
-struct AdapterRegs {
-    uint32_t w[RPL / 4];
-    __device__ __forceinline__ void load(const uint32_t *src) {
-#pragma unroll
-        for (int k = 0; k < RPL / 4; ++k) w[k] = __builtin_amdgcn_readfirstlane(src[k]);
-    }
-    __device__ __forceinline__ int operator()(int s) const {   // s: 1-based slot, compile-time
-        return (int)((w[(s - 1) >> 2] >> (8 * ((s - 1) & 3))) & 0xFFu);
-    }
-};
-
-__device__ __forceinline__ void store_result(int32_t *out, int64_t stride, int64_t idx,
-                                             const pcabi::Result &r) {
-    out[0 * stride + idx] = r.rs;
-    out[1 * stride + idx] = r.re;
-    out[2 * stride + idx] = r.as;
-    out[3 * stride + idx] = r.ae;
-    out[4 * stride + idx] = r.score;
-    out[5 * stride + idx] = r.m;
-    out[6 * stride + idx] = r.l1;
-    out[7 * stride + idx] = r.l2;
-}
-
-__device__ __forceinline__ pcabi::Result empty_result() {
-    pcabi::Result r;
-    r.rs = -1; r.re = 0; r.as = -1; r.ae = 0;
-    r.score = (int)0x80000000; r.m = 0; r.l1 = 0; r.l2 = 0;
-    return r;
-}
-
-// Packed-core substitution table in LDS: one (RPL+2) x 8 int32 table per wave (its adapter).
-constexpr int kTabW = pcabi::pk::TAB_W;
-
-struct LdsRow {
-    const int32_t *p;   // &tab[wave][c][0]: slot s at p[s - 1], 16-byte aligned
-    __device__ __forceinline__ int32_t operator()(int s) const { return p[s - 1]; }
-    __device__ __forceinline__ void quad(int q, int32_t *dst) const {
-        const int4 v = *reinterpret_cast<const int4 *>(p + 4 * q);
-        dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
-    }
-};
-
-// This wave's packed-core substitution table (every lane of the block reaches the barrier).
-template <int RPL>
-__device__ __forceinline__ void fill_wave_tab(const KParams &p, int a_local, int L, int32_t *wave_tab) {
-    const int off = RPL - L;
-    const int lane = threadIdx.x & 63;
-    for (int e = lane; e < kTabW * RPL; e += 64) {
-        const int c = e / RPL, srow = e % RPL + 1;
-        const uint32_t *ap = p.adp_pad + (int64_t)a_local * (RPL / 4);
-        auto code = [&](int sl) { return (int)((ap[(sl - 1) / 4] >> (8 * ((sl - 1) & 3))) & 0xFFu); };
-        wave_tab[e] = pcabi::pk::sub_key<RPL>(srow, c, code, off, p.sc);
-    }
-    __syncthreads();
-}
-
-// The two tables of a long bucket's wave: pass 0 (c, nD) then pass 1 (m), kTabW x RPL each.
-template <int RPL>
-__device__ __forceinline__ void fill_wave_tab_long(const KParams &p, int a_local, int L, int32_t *wave_tab) {
-    const int off = RPL - L;
-    const int lane = threadIdx.x & 63;
-    const uint32_t *ap = p.adp_pad + (int64_t)a_local * (RPL / 4);
-    auto code = [&](int sl) { return (int)((ap[(sl - 1) / 4] >> (8 * ((sl - 1) & 3))) & 0xFFu); };
-    for (int e = lane; e < kTabW * RPL; e += 64) {
-        const int c = e / RPL, srow = e % RPL + 1;
-        wave_tab[e] = pcabi::pk::sub_key<RPL, decltype(code), pcabi::pk::LayL<RPL, 0>>(srow, c, code, off, p.sc);
-        wave_tab[kTabW * RPL + e] =
-            pcabi::pk::sub_key<RPL, decltype(code), pcabi::pk::LayL<RPL, 1>>(srow, c, code, off, p.sc);
-    }
-    __syncthreads();
-}
-
-template <int RPL, bool AFFINE, int KIND>
-__device__ __forceinline__ void run_lane(const KParams &p, int a_local, int64_t w, int64_t out_idx,
-                                         int32_t *wave_tab, int64_t tile_off) {
-    AdapterRegs<RPL> adp;
-    if constexpr (KIND != LONG) adp.load(p.adp_pad + (int64_t)a_local * (RPL / 4));
-    const int L = __builtin_amdgcn_readfirstlane(p.adp_len[a_local]);
-    if constexpr (KIND == PACKED) fill_wave_tab<RPL>(p, a_local, L, wave_tab);
-    if constexpr (KIND == LONG) fill_wave_tab_long<RPL>(p, a_local, L, wave_tab);
-    if (w < 0) return;
-    const int n = p.win_len[w];
-    pcabi::Result r;
-    if (n <= 0) {
-        r = empty_result();
-    } else {
-        WindowReader rd = tile_off >= 0
-            ? WindowReader(p.tiles + tile_off + (threadIdx.x & 255), 256, 0)
-            : [&] {
-                  const uint8_t *b = p.codes + p.win_off[w];
-                  const int a0 = (int)((uintptr_t)b & 3);
-                  return WindowReader(reinterpret_cast<const uint32_t *>(b - a0), 1, 8 * a0);
-              }();
-        if constexpr (KIND == PACKED) {
-            auto tabfn = [&](int rc) { return LdsRow{wave_tab + rc * RPL}; };
-            r = pcabi::align_lane_packed<(RPL <= pcabi::pk::MAX_RPL ? RPL : 4), AFFINE>(rd, n, tabfn, L, p.sc);
-        } else if constexpr (KIND == LONG) {
-            WindowReader rd1 = rd;   // the second pass reads the window again from its start
-            auto tab0 = [&](int rc) { return LdsRow{wave_tab + rc * RPL}; };
-            auto tab1 = [&](int rc) { return LdsRow{wave_tab + kTabW * RPL + rc * RPL}; };
-            r = pcabi::align_lane_packed_long<RPL, AFFINE>(rd, rd1, n, tab0, tab1, L, p.sc);
-        } else if constexpr (KIND == FAST) {
-            r = pcabi::align_lane_fast<RPL, AFFINE>(rd, n, adp, L, p.sc);
-        } else {
-            r = pcabi::align_lane_generic<RPL, AFFINE>(rd, n, adp, L, p.sc);
-        }
-    }
-    if (p.compat) {
-        // pairs mode only: the window is read in place, the adapter from its padded row
-        int en_match = 0;
-        if (r.rs >= 0 && r.diag_en && r.l1 > 0) {
-            const uint8_t *ab = reinterpret_cast<const uint8_t *>(p.adp_pad + (int64_t)a_local * (RPL / 4));
-            en_match = p.codes[p.win_off[w] + r.re] == ab[RPL - L + r.ae];
-        }
-        p.compat[out_idx] = pcabi::compat_flag(r, n, en_match);
-        return;
-    }
-    store_result(p.out, p.out_stride, out_idx, r);
-}
-
-// One kernel for both work shapes (uniform branch on p.task_win):
-//  cross: 1-D grid of (window tile of 256, adapter) blocks in XCD-aware order; lane = window
-//  pairs: grid (ceil(n_waves/4)); wave = one adapter, lanes = host-grouped tasks
-template <int KIND, int RPL>
-constexpr int wave_tab_ints() { return KIND == PACKED ? kTabW * RPL : (KIND == LONG ? 2 * kTabW * RPL : 1); }
-
-template <int RPL, bool AFFINE, int KIND>
-__global__ __launch_bounds__(256, PCABI_WAVES) void k_align(KParams p) {
-    __shared__ __attribute__((aligned(16))) int32_t tab[4 * wave_tab_ints<KIND, RPL>()];
-    int32_t *wave_tab = tab + (threadIdx.x >> 6) * wave_tab_ints<KIND, RPL>();
-    if (p.task_win == nullptr) {
-        // XCD-aware order: workgroups are dealt to the 8 XCDs round-robin, so block b runs on
-        // XCD b % 8. Each XCD takes every 8th tile of 256 windows and runs ALL adapters of a
-        // tile back to back, so a tile is fetched into one L2 once instead of once per adapter.
-        const int64_t b = blockIdx.x;
-        const int64_t k = b >> 3;
-        const int a_local = (int)(k % p.n_adp);
-        const int64_t tile = (k / p.n_adp) * 8 + (b & 7);
-        const int64_t w = tile * 256 + threadIdx.x;
-        const int a_glob = p.adp_id[a_local];
-        const int64_t toff = w < p.n_win ? p.tile_off[tile] : 0;
-        run_lane<RPL, AFFINE, KIND>(p, a_local, w < p.n_win ? w : -1, (int64_t)a_glob * p.n_win + w, wave_tab,
-                                    toff);
-    } else {
-        int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-        const bool live = wave < p.n_waves;            // dead waves still join the table barrier
-        if (!live) wave = p.n_waves - 1;
-        const int64_t slot = wave * 64 + (threadIdx.x & 63);
-        const int a_local = __builtin_amdgcn_readfirstlane(p.wave_adp[wave]);
-        const int32_t tw = live ? p.task_win[slot] : -1;
-        run_lane<RPL, AFFINE, KIND>(p, a_local, tw, tw >= 0 ? p.task_out[slot] : 0, wave_tab, -1);
-    }
 }
 
 // ---- middle-scan score filter (pcabi_dp.h filter_lane) -------------------------------------------
@@ -326,86 +88,6 @@ int middle_seed_mode() {
     const char *e = std::getenv("PCABI_MIDDLE_SEEDS");
     if (!e || !e[0]) return 1;
     return e[0] == '0' ? 0 : (e[0] == '2' ? 2 : 1);
-}
-
-// Cross mode over tiles, TWO adapters of a FAST bucket per wave (packed 16-bit lanes): block =
-// (tile of 256 windows, adapter pair) in the XCD-aware order of k_align. Writes the best score of
-// every (adapter, window) as int16: s16[a_glob * n_win + w].
-struct FParams {
-    const uint32_t *tiles;
-    const int64_t *tile_off;
-    const int32_t *win_len;
-    int64_t n_win;
-    const uint32_t *adp_pad;   // bucket table (RPL bytes per adapter)
-    const int32_t *adp_len;
-    const int32_t *adp_id;
-    int32_t n_adp;             // adapters in the bucket (pairs = ceil(n_adp / 2))
-    int16_t *s16;
-    pcabi::Scoring sc;
-};
-
-struct LdsRow16 {
-    const int32_t *p;
-    __device__ __forceinline__ void quad(int q, pcabi::sf::v2 *dst) const {
-        const int4 v = *reinterpret_cast<const int4 *>(p + 4 * q);
-        dst[0] = __builtin_bit_cast(pcabi::sf::v2, v.x);
-        dst[1] = __builtin_bit_cast(pcabi::sf::v2, v.y);
-        dst[2] = __builtin_bit_cast(pcabi::sf::v2, v.z);
-        dst[3] = __builtin_bit_cast(pcabi::sf::v2, v.w);
-    }
-};
-
-template <int RPL, bool AFFINE>
-__global__ __launch_bounds__(256) void k_score_filter(FParams p) {
-    __shared__ __attribute__((aligned(16))) int32_t tab[4 * kTabW * RPL];
-    int32_t *wave_tab = tab + (threadIdx.x >> 6) * kTabW * RPL;
-    const int n_pair = (p.n_adp + 1) / 2;
-    const int64_t b = blockIdx.x;
-    const int64_t k = b >> 3;
-    const int pr = (int)(k % n_pair);
-    const int64_t tile = (k / n_pair) * 8 + (b & 7);
-    const int64_t w = tile * 256 + threadIdx.x;
-    const int ia = 2 * pr, ib = (2 * pr + 1 < p.n_adp) ? 2 * pr + 1 : 2 * pr;
-    const int La = __builtin_amdgcn_readfirstlane(p.adp_len[ia]);
-    const int Lb = __builtin_amdgcn_readfirstlane(p.adp_len[ib]);
-    {
-        const int lane = threadIdx.x & 63;
-        const uint32_t *pa = p.adp_pad + (int64_t)ia * (RPL / 4), *pb = p.adp_pad + (int64_t)ib * (RPL / 4);
-        for (int e = lane; e < kTabW * RPL; e += 64) {
-            const int c = e / RPL, sl = e % RPL + 1;
-            const int ca = (int)((pa[(sl - 1) / 4] >> (8 * ((sl - 1) & 3))) & 0xFFu);
-            const int cb = (int)((pb[(sl - 1) / 4] >> (8 * ((sl - 1) & 3))) & 0xFFu);
-            const int va = sl <= RPL - La ? 0 : (c == ca ? p.sc.ma : p.sc.mi);
-            const int vb = sl <= RPL - Lb ? 0 : (c == cb ? p.sc.ma : p.sc.mi);
-            const uint32_t lo = (uint16_t)(int16_t)(va - p.sc.go), hi = (uint16_t)(int16_t)(vb - p.sc.go);
-            wave_tab[e] = (int32_t)(lo | (hi << 16));
-        }
-        __syncthreads();
-    }
-    if (w >= p.n_win) return;
-    const int n = p.win_len[w];
-    WindowReader rd(p.tiles + p.tile_off[tile] + threadIdx.x, 256, 0);
-    auto tabfn = [&](int rc) { return LdsRow16{wave_tab + rc * RPL}; };
-    const pcabi::sf::v2 r = pcabi::filter_lane<RPL, AFFINE>(rd, n, tabfn, p.sc);
-    p.s16[(int64_t)p.adp_id[ia] * p.n_win + w] = r[0];
-    if (ib != ia) p.s16[(int64_t)p.adp_id[ib] * p.n_win + w] = r[1];
-}
-
-template <int RPL>
-void launch_filter(const FParams &p, bool affine, hipStream_t st) {
-    const int64_t tiles8 = (p.n_win + 8 * 256 - 1) / (8 * 256) * 8;
-    const dim3 grid((unsigned)(tiles8 * ((p.n_adp + 1) / 2)));
-    if (affine) hipLaunchKernelGGL((k_score_filter<RPL, true>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((k_score_filter<RPL, false>), grid, dim3(256), 0, st, p);
-}
-
-void dispatch_filter(int rpl, const FParams &p, bool affine, hipStream_t st) {
-    switch (rpl) {
-#define C(R) case R: launch_filter<R>(p, affine, st); break;
-    C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32) C(36) C(40) C(44) C(48) C(52) C(56) C(60) C(64)
-    C(68) C(72) C(76) C(80) C(84) C(88)
-#undef C
-    }
 }
 
 // ---- decision epilogues --------------------------------------------------------------------
@@ -667,231 +349,11 @@ void launch_tiles(const uint8_t *codes, const int64_t *win_off, const int32_t *w
     hipLaunchKernelGGL(k_tile_windows, grid, dim3(256), 0, st, codes, win_off, win_len, n_win, tile_off, tiles);
 }
 
-// Pairs mode over CHUNKS of long reads (middle-scan candidates, pcabi_dp.h sf::chunk_plan): the
-// packed core on (read offset, columns) of the task's read with the end cell restricted to the
-// owned columns. Wave = one adapter, as k_align's pairs mode; results unmerged, one per task.
-template <int RPL, bool AFFINE, int KIND>
-__global__ __launch_bounds__(256, PCABI_WAVES) void k_align_chunk(KParams p) {
-    __shared__ __attribute__((aligned(16))) int32_t tab[4 * wave_tab_ints<KIND, RPL>()];
-    int32_t *wave_tab = tab + (threadIdx.x >> 6) * wave_tab_ints<KIND, RPL>();
-    int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const bool live = wave < p.n_waves;            // dead waves still join the table barrier
-    if (!live) wave = p.n_waves - 1;
-    const int64_t slot = wave * 64 + (threadIdx.x & 63);
-    const int a_local = __builtin_amdgcn_readfirstlane(p.wave_adp[wave]);
-    const int L = __builtin_amdgcn_readfirstlane(p.adp_len[a_local]);
-    if constexpr (KIND == PACKED) fill_wave_tab<RPL>(p, a_local, L, wave_tab);
-    if constexpr (KIND == LONG) fill_wave_tab_long<RPL>(p, a_local, L, wave_tab);
-    const int32_t tw = live ? p.task_win[slot] : -1;
-    if (tw < 0) return;
-    const int4 ck = p.task_chunk[slot];
-    const uint8_t *b = p.codes + p.win_off[tw] + ck.x;
-    const int a0 = (int)((uintptr_t)b & 3);
-    WindowReader rd(reinterpret_cast<const uint32_t *>(b - a0), 1, 8 * a0);
-    pcabi::Result r;
-    if constexpr (KIND == PACKED) {
-        auto tabfn = [&](int rc) { return LdsRow{wave_tab + rc * RPL}; };
-        r = pcabi::align_lane_packed<RPL, AFFINE, true>(rd, ck.y, tabfn, L, p.sc, ck.z, ck.w);
-    } else if constexpr (KIND == LONG) {
-        WindowReader rd1 = rd;
-        auto tab0 = [&](int rc) { return LdsRow{wave_tab + rc * RPL}; };
-        auto tab1 = [&](int rc) { return LdsRow{wave_tab + kTabW * RPL + rc * RPL}; };
-        r = pcabi::align_lane_packed_long<RPL, AFFINE, true>(rd, rd1, ck.y, tab0, tab1, L, p.sc, ck.z, ck.w);
-    } else {
-        AdapterRegs<RPL> adp;
-        adp.load(p.adp_pad + (int64_t)a_local * (RPL / 4));
-        r = pcabi::align_lane_generic<RPL, AFFINE, true>(rd, ck.y, adp, L, p.sc, ck.z, ck.w);
-    }
-    store_result(p.out, p.out_stride, p.task_out[slot], r);
-}
-
-// ---- striped bucket: adapters longer than kMaxRPL (pcabi_dp.h align_lane_striped) ----------------
-// The boundary row between stripes lives in global scratch, [column][field][lane] per wave slot,
-// so a wave's access to one field of one column is 256 contiguous bytes.
-template <bool AFFINE>
-struct StripeBnd {
-    static constexpr int NF = AFFINE ? 6 : 3;   // linear gaps carry no V state
-    int32_t *p;                                 // this lane's column-1 field-0 entry
-    __device__ __forceinline__ void load(int j, pcabi::BndCell &c) const {
-        const int32_t *q = p + (int64_t)(j - 1) * (NF * 64);
-        c.s = q[0];
-        c.sc = q[64];
-        c.sn = (uint32_t)q[128];
-        if (AFFINE) {
-            c.v = q[192];
-            c.vc = q[256];
-            c.vn = (uint32_t)q[320];
-        } else {
-            c.v = pcabi::NEG;
-            c.vc = 0;
-            c.vn = 0;
-        }
-    }
-    __device__ __forceinline__ void store(int j, const pcabi::BndCell &c) const {
-        int32_t *q = p + (int64_t)(j - 1) * (NF * 64);
-        q[0] = c.s;
-        q[64] = c.sc;
-        q[128] = (int32_t)c.sn;
-        if (AFFINE) {
-            q[192] = c.v;
-            q[256] = c.vc;
-            q[320] = (int32_t)c.vn;
-        }
-    }
-};
-
-// The current stripe's R adapter codes in SGPRs (the adapter is wave-uniform).
-template <int R>
-struct StripeAdp {
-    const uint32_t *base;   // the adapter's rt-byte table row (top-padded)
-    uint32_t w[R / 4];
-    __device__ __forceinline__ void load(int k) {
-#pragma unroll
-        for (int q = 0; q < R / 4; ++q) w[q] = __builtin_amdgcn_readfirstlane(base[k * (R / 4) + q]);
-    }
-    __device__ __forceinline__ int operator()(int s) const { return (int)((w[(s - 1) >> 2] >> (8 * ((s - 1) & 3))) & 0xFFu); }
-};
-
-// Persistent grid: wave slot = blockIdx * 4 + wave owns one scratch region and walks the work
-// items (cross: 64 windows of a tile x one adapter; pairs: one host-built wave of tasks, chunks
-// included) with a stride of the slot count. Every lane reaches the loop's end: no barriers.
-template <int R, bool AFFINE>
-__global__ __launch_bounds__(256) void k_align_striped(KParams p) {
-    const int64_t slot = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const int64_t n_slots = (int64_t)gridDim.x * 4;
-    StripeBnd<AFFINE> bnd{p.scratch + slot * (int64_t)p.max_cols * (StripeBnd<AFFINE>::NF * 64) + lane};
-    for (int64_t item = slot; item < p.n_items; item += n_slots) {
-        const bool cross = p.task_win == nullptr;
-        int a_local;
-        int64_t w, out_idx, q = 0;
-        int4 ck = make_int4(0, 0, 1, -1);
-        if (cross) {
-            a_local = (int)(item % p.n_adp);
-            q = item / p.n_adp;
-            w = q * 64 + lane;
-            if (w >= p.n_win) continue;
-            out_idx = (int64_t)p.adp_id[a_local] * p.n_win + w;
-        } else {
-            a_local = p.wave_adp[item];
-            const int64_t sl = item * 64 + lane;
-            w = p.task_win[sl];
-            if (w < 0) continue;
-            out_idx = p.task_out[sl];
-            if (p.task_chunk) ck = p.task_chunk[sl];
-        }
-        a_local = __builtin_amdgcn_readfirstlane(a_local);
-        const int L = __builtin_amdgcn_readfirstlane(p.adp_len[a_local]);
-        const int n = p.task_chunk ? ck.y : p.win_len[w];
-        pcabi::Result r;
-        if (n <= 0) {
-            r = empty_result();
-        } else {
-            WindowReader rd = cross
-                ? WindowReader(p.tiles + p.tile_off[q >> 2] + (q & 3) * 64 + lane, 256, 0)
-                : [&] {
-                      const uint8_t *b = p.codes + p.win_off[w] + ck.x;
-                      const int a0 = (int)((uintptr_t)b & 3);
-                      return WindowReader(reinterpret_cast<const uint32_t *>(b - a0), 1, 8 * a0);
-                  }();
-            StripeAdp<R> adp{p.adp_pad + (int64_t)a_local * (p.rt / 4)};
-            r = pcabi::align_lane_striped<R, AFFINE>(rd, n, adp, L, p.rt, p.sc, bnd, ck.z, ck.w);
-        }
-        if (p.compat) {
-            int en_match = 0;
-            if (r.rs >= 0 && r.diag_en && r.l1 > 0) {
-                const uint8_t *ab = reinterpret_cast<const uint8_t *>(p.adp_pad + (int64_t)a_local * (p.rt / 4));
-                en_match = p.codes[p.win_off[w] + r.re] == ab[p.rt - L + r.ae];
-            }
-            p.compat[out_idx] = pcabi::compat_flag(r, n, en_match);
-            continue;
-        }
-        store_result(p.out, p.out_stride, out_idx, r);
-    }
-}
-
-// Scratch budget of one striped launch (PCABI_STRIPE_SCRATCH_MB, default 4096): it bounds the wave
-// slots when windows are long (each slot holds a boundary row as long as the longest window).
-const int64_t g_stripe_budget = [] {
-    const char *e = std::getenv("PCABI_STRIPE_SCRATCH_MB");
-    const int64_t mb = (e && e[0]) ? std::max<int64_t>(16, std::atoll(e)) : 4096;
-    return mb << 20;
-}();
-
-// Launch the striped kernel for one bucket: p.rt, p.max_cols set by the caller; scratch is
-// stream-ordered (hipMallocAsync / hipFreeAsync on `st`), so concurrent launches never share it.
-int launch_striped(KParams p, bool affine, hipStream_t st) {
-    p.n_items = p.task_win ? p.n_waves : (p.n_win + 63) / 64 * p.n_adp;
-    if (p.n_items <= 0) return 0;
-    const int64_t nf = affine ? 6 : 3;
-    const int64_t per_slot = std::max<int64_t>(1, p.max_cols) * nf * 64 * 4;
-    int64_t slots = std::min<int64_t>({(p.n_items + 3) / 4 * 4, (int64_t)2048, g_stripe_budget / per_slot / 4 * 4});
-    slots = std::max<int64_t>(slots, 4);
-    void *scr = nullptr;
-    // slots past the last item never touch their scratch
-    HIP_TRY(hipMallocAsync(&scr, (size_t)(std::min(slots, p.n_items) * per_slot), st));
-    p.scratch = (int32_t *)scr;
-    p.max_cols = std::max<int32_t>(1, p.max_cols);
-    const dim3 grid((unsigned)(slots / 4));
-    if (affine) hipLaunchKernelGGL((k_align_striped<kStripeRows, true>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((k_align_striped<kStripeRows, false>), grid, dim3(256), 0, st, p);
-    const hipError_t le = hipGetLastError();
-    HIP_TRY(hipFreeAsync(scr, st));
-    if (le != hipSuccess) return fail(PCABI_E_DEVICE, std::string("k_align_striped: ") + hipGetErrorString(le));
-    return 0;
-}
-
 // Buckets the chunked candidate DP serves: the packed core's (FAST buckets laid out packed, WIDE)
 // and the generic and striped cores' (long adapters).
 bool chunkable(int b, bool packed) {
     return kBuckets[b].kind == WIDE || kBuckets[b].kind == LONG || kBuckets[b].kind == GENERIC ||
            kBuckets[b].kind == STRIPED || (kBuckets[b].kind == FAST && packed);
-}
-
-int dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st) {
-    const dim3 grid((unsigned)((p.n_waves + 3) / 4));
-    if (kBuckets[b].kind == STRIPED) return launch_striped(p, affine, st);
-    if (kBuckets[b].kind == GENERIC) {
-        switch (kBuckets[b].rpl) {
-#define C(R)                                                                                            \
-    case R:                                                                                             \
-        if (affine) hipLaunchKernelGGL((k_align_chunk<R, true, GENERIC>), grid, dim3(256), 0, st, p);   \
-        else hipLaunchKernelGGL((k_align_chunk<R, false, GENERIC>), grid, dim3(256), 0, st, p);         \
-        break;
-        C(16) C(32) C(64) C(96) C(128)
-#undef C
-        }
-        return 0;
-    }
-    if (kBuckets[b].kind == LONG) {
-        switch (kBuckets[b].rpl) {
-#define C(R)                                                                                         \
-    case R:                                                                                          \
-        if (affine) hipLaunchKernelGGL((k_align_chunk<R, true, LONG>), grid, dim3(256), 0, st, p);   \
-        else hipLaunchKernelGGL((k_align_chunk<R, false, LONG>), grid, dim3(256), 0, st, p);         \
-        break;
-        C(96) C(112) C(128)
-#undef C
-        }
-        return 0;
-    }
-    switch (kBuckets[b].rpl) {
-#define C(R)                                                                                           \
-    case R:                                                                                            \
-        if (affine) hipLaunchKernelGGL((k_align_chunk<R, true, PACKED>), grid, dim3(256), 0, st, p);   \
-        else hipLaunchKernelGGL((k_align_chunk<R, false, PACKED>), grid, dim3(256), 0, st, p);         \
-        break;
-    C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32) C(36) C(40) C(44) C(48) C(52) C(56) C(60) C(64)
-    C(68) C(72) C(76) C(80) C(84) C(88)
-#undef C
-    }
-    return 0;
-}
-
-template <int RPL, int KIND>
-void launch(const KParams &p, bool affine, dim3 grid, hipStream_t st) {
-    if (affine) hipLaunchKernelGGL((k_align<RPL, true, KIND>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((k_align<RPL, false, KIND>), grid, dim3(256), 0, st, p);
 }
 
 int dispatch(int b, const KParams &p, bool affine, hipStream_t st, bool packed) {
@@ -900,39 +362,12 @@ int dispatch(int b, const KParams &p, bool affine, hipStream_t st, bool packed) 
     dim3 grid = p.task_win ? dim3((unsigned)((p.n_waves + 3) / 4))
                            : dim3((unsigned)(tiles8 * p.n_adp));
     const BucketDef d = kBuckets[b];
-    if (d.kind == LONG) {
-        switch (d.rpl) {
-        case 96: launch<96, LONG>(p, affine, grid, st); break;
-        case 112: launch<112, LONG>(p, affine, grid, st); break;
-        case 128: launch<128, LONG>(p, affine, grid, st); break;
-        }
-    } else if (d.kind == WIDE) {
-        switch (d.rpl) {
-#define C(R) case R: launch<R, PACKED>(p, affine, grid, st); break;
-        C(68) C(72) C(76) C(80) C(84) C(88)
-#undef C
-        }
-    } else if (d.kind == FAST && packed) {
-        switch (d.rpl) {
-#define C(R) case R: launch<R, PACKED>(p, affine, grid, st); break;
-        C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32) C(36) C(40) C(44) C(48) C(52) C(56) C(60) C(64)
-#undef C
-        }
-    } else if (d.kind == FAST) {
-        switch (d.rpl) {
-#define C(R) case R: launch<R, FAST>(p, affine, grid, st); break;
-        C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32) C(36) C(40) C(44) C(48) C(52) C(56) C(60) C(64)
-#undef C
-        }
-    } else {
-        switch (d.rpl) {
-        case 16: launch<16, GENERIC>(p, affine, grid, st); break;
-        case 32: launch<32, GENERIC>(p, affine, grid, st); break;
-        case 64: launch<64, GENERIC>(p, affine, grid, st); break;
-        case 96: launch<96, GENERIC>(p, affine, grid, st); break;
-        case 128: launch<128, GENERIC>(p, affine, grid, st); break;
-        }
-    }
+    if (d.kind == LONG || d.kind == WIDE || (d.kind == FAST && packed && d.rpl > 32))
+        dispatch_packed_large(d.rpl, d.kind == LONG, p, affine, grid, st);
+    else if (d.kind == FAST && packed)
+        dispatch_packed_small(d.rpl, p, affine, grid, st);
+    else
+        dispatch_fast(d.rpl, d.kind == GENERIC, p, affine, grid, st);
     return 0;
 }
 
@@ -1025,7 +460,7 @@ void build_buckets(const uint8_t *adp_codes, const int32_t *adp_off, const int32
 
 // error channel shared with the host I/O unit (csrc/pcabi_io.cpp)
 namespace pcabi_internal {
-int fail(int code, const std::string &msg) { return ::fail(code, msg); }
+int fail(int code, const std::string &msg) { return pcabi_eng::fail(code, msg); }
 }  // namespace pcabi_internal
 
 // ---- prepared adapter tables (device) ---------------------------------------------------------

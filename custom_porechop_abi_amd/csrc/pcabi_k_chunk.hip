@@ -1,0 +1,48 @@
+// pcabi_k_chunk.hip -- k_align_chunk instantiations: the middle scan's candidate DP over
+// owned-column chunks of long reads (pcabi_dp.h sf::chunk_plan), every core.
+#include "pcabi_kern.h"
+
+namespace pcabi_eng {
+
+int dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st) {
+    const dim3 grid((unsigned)((p.n_waves + 3) / 4));
+    if (kBuckets[b].kind == STRIPED) return launch_striped(p, affine, st);
+    if (kBuckets[b].kind == GENERIC) {
+        switch (kBuckets[b].rpl) {
+#define C(R)                                                                                            \
+    case R:                                                                                             \
+        if (affine) hipLaunchKernelGGL((k_align_chunk<R, true, GENERIC>), grid, dim3(256), 0, st, p);   \
+        else hipLaunchKernelGGL((k_align_chunk<R, false, GENERIC>), grid, dim3(256), 0, st, p);         \
+        break;
+        C(16) C(32) C(64) C(96) C(128)
+#undef C
+        }
+        return 0;
+    }
+    if (kBuckets[b].kind == LONG) {
+        switch (kBuckets[b].rpl) {
+#define C(R)                                                                                         \
+    case R:                                                                                          \
+        if (affine) hipLaunchKernelGGL((k_align_chunk<R, true, LONG>), grid, dim3(256), 0, st, p);   \
+        else hipLaunchKernelGGL((k_align_chunk<R, false, LONG>), grid, dim3(256), 0, st, p);         \
+        break;
+        C(96) C(112) C(128)
+#undef C
+        }
+        return 0;
+    }
+    switch (kBuckets[b].rpl) {
+#define C(R)                                                                                           \
+    case R:                                                                                            \
+        if (affine) hipLaunchKernelGGL((k_align_chunk<R, true, PACKED>), grid, dim3(256), 0, st, p);   \
+        else hipLaunchKernelGGL((k_align_chunk<R, false, PACKED>), grid, dim3(256), 0, st, p);         \
+        break;
+    C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32) C(36) C(40) C(44) C(48) C(52) C(56) C(60) C(64)
+    C(68) C(72) C(76) C(80) C(84) C(88)
+#undef C
+    }
+    return 0;
+}
+
+
+}  // namespace pcabi_eng
