@@ -84,6 +84,11 @@ def lib():
                                     c_int, c_int, c_d, c_p, c_i64], c_i64),
         'pcabi_middle_seed_runs': ([], c_i64),
         'pcabi_io_release_cache': ([], None),
+        'pcabi_best_full_identity_host': ([c_int, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_p, ctypes.c_int32, c_int,
+                                           c_int, c_int, c_int, c_p, c_int], c_int),
+        'pcabi_middle_cuts_dev': ([c_p, c_i64, c_i64, c_i64, c_p, c_p, c_int, c_int, c_p, c_p, c_p], c_int),
+        'pcabi_middle_cuts_host': ([c_int, c_p, c_i64, c_i64, c_i64, c_p, c_p, ctypes.c_int32, c_int, c_int, c_p, c_p],
+                                   c_int),
         'pcabi_barcode_call_dev': ([c_p, c_i64, c_p, c_p, ctypes.c_int32, c_p, c_i64, c_p, c_p, ctypes.c_int32,
                                     c_i64, c_d, c_d, c_int, c_p, c_p, c_p], c_int),
         'pcabi_barcode_call_host': ([c_int, c_p, ctypes.c_int32, c_p, c_p, ctypes.c_int32, c_p, ctypes.c_int32, c_p,
@@ -115,7 +120,8 @@ def exported_symbols():
             'pcabi_fastx_close', 'pcabi_fastx_load', 'pcabi_reads_count', 'pcabi_reads_type', 'pcabi_reads_views',
             'pcabi_reads_free', 'pcabi_reads_write', 'check_compatibility', 'pcabi_compat_host',
             'pcabi_compat_all_vs_all_host', 'pcabi_kmer_count_host', 'pcabi_kmer_top_host', 'pcabi_gather_host',
-            'pcabi_kmer_approx_host', 'pcabi_io_release_cache']
+            'pcabi_kmer_approx_host', 'pcabi_io_release_cache', 'pcabi_best_full_identity_host',
+            'pcabi_middle_cuts_dev', 'pcabi_middle_cuts_host']
 
 
 def check(rc, what):

@@ -698,7 +698,7 @@ int align_host_impl(int device, const uint8_t *codes, int64_t codes_len, const i
                     const int32_t *adp_off, const int32_t *adp_len, int32_t n_adp,
                     const int32_t *task_win, const int32_t *task_adp, int64_t n_task, int match,
                     int mismatch, int gap_open, int gap_extend, const double *first_thr, int32_t *out,
-                    bool compat = false, bool orient = false) {
+                    bool compat = false, bool orient = false, double *best = nullptr, bool best_dev = false) {
     if (device < 0 || device >= 16) return fail(PCABI_E_ARG, "bad device index");
     if (n_win < 0 || n_adp < 0 || n_task < 0) return fail(PCABI_E_ARG, "negative count");
     if (int rc = check_common(adp_len, n_adp)) return rc;
@@ -858,6 +858,18 @@ int align_host_impl(int device, const uint8_t *codes, int64_t codes_len, const i
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(out, e.hits.p, sizeof(int32_t) * 5 * (size_t)n_win, hipMemcpyDeviceToHost,
                                e.stream));
+    } else if (best) {     // adapter-set search: per-adapter max of the full identity, on the device
+        double *d_best = best;
+        if (!best_dev) {
+            if (int rc = e.hits.ensure(sizeof(double) * (size_t)n_adp)) return rc;
+            d_best = (double *)e.hits.p;
+            HIP_TRY(hipMemcpyAsync(d_best, best, sizeof(double) * (size_t)n_adp, hipMemcpyHostToDevice, e.stream));
+        }
+        hipLaunchKernelGGL(k_best_full_id, dim3((unsigned)n_adp), dim3(256), 0, e.stream, (const int32_t *)e.out.p,
+                           n_res, n_win, d_best);
+        HIP_TRY(hipGetLastError());
+        if (!best_dev)
+            HIP_TRY(hipMemcpyAsync(best, d_best, sizeof(double) * (size_t)n_adp, hipMemcpyDeviceToHost, e.stream));
     } else if (orient) {   // compat all-vs-all: n_win == n_adp == n, the matrix comes back
         if (int rc = e.hits.ensure(sizeof(int32_t) * (size_t)n_res)) return rc;
         const unsigned tb = (unsigned)((n_win + 31) / 32);
@@ -885,6 +897,17 @@ int pcabi_align_host(int device, const uint8_t *codes, int64_t codes_len, const 
     return align_host_impl(device, codes, codes_len, win_off, win_len, n_win, adp_codes, adp_off, adp_len,
                            n_adp, task_win, task_adp, n_task, match, mismatch, gap_open, gap_extend, nullptr,
                            out);
+}
+
+int pcabi_best_full_identity_host(int device, const uint8_t *codes, int64_t codes_len, const int64_t *win_off,
+                                  const int32_t *win_len, int64_t n_win, const uint8_t *adp_codes,
+                                  const int32_t *adp_off, const int32_t *adp_len, int32_t n_adp, int match,
+                                  int mismatch, int gap_open, int gap_extend, double *best, int best_on_device) {
+    if (!best && n_adp > 0) return fail(PCABI_E_ARG, "best is NULL");
+    if (n_win == 0 || n_adp == 0) return 0;     // no window: every maximum stays as given
+    return align_host_impl(device, codes, codes_len, win_off, win_len, n_win, adp_codes, adp_off, adp_len, n_adp,
+                           nullptr, nullptr, 0, match, mismatch, gap_open, gap_extend, nullptr, nullptr, false, false,
+                           best, best_on_device != 0);
 }
 
 int pcabi_first_hits_host(int device, const uint8_t *codes, int64_t codes_len, const int64_t *win_off,
@@ -1644,6 +1667,45 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
         nxt_start.swap(st_sorted);
     }
     return n_hits;
+}
+
+int pcabi_middle_cuts_host(int device, const int32_t *hits, int64_t hit_stride, int64_t n_hits, int64_t n_reads,
+                           const uint8_t *bad_start, const uint8_t *bad_end, int32_t n_adp, int good_side,
+                           int bad_side, int64_t *cut_off, int64_t *cuts) {
+    if (device < 0 || device >= 16) return fail(PCABI_E_ARG, "bad device index");
+    if (n_hits < 0 || n_reads < 0 || n_adp < 0 || hit_stride < n_hits) return fail(PCABI_E_ARG, "bad counts");
+    for (int64_t k = 0; k < n_hits; ++k)
+        if (hits[k] < 0 || hits[k] >= n_reads || hits[hit_stride + k] < 0 || hits[hit_stride + k] >= n_adp)
+            return fail(PCABI_E_ARG, "hit read / adapter index out of range");
+    Engine &e = g_engines[device];
+    std::lock_guard<std::mutex> lock(e.mu);
+    if (int rc = engine_init(e, device)) return rc;
+    HIP_TRY(hipSetDevice(device));
+    const size_t hb = sizeof(int32_t) * 4 * (size_t)std::max<int64_t>(n_hits, 1);
+    const size_t fb = 2 * (size_t)std::max<int32_t>(n_adp, 1);
+    const size_t ob = sizeof(int64_t) * ((size_t)n_reads + 1), cb = sizeof(int64_t) * 2 * (size_t)std::max<int64_t>(n_hits, 1);
+    if (int rc = e.bc.ensure(hb + fb + ob + cb + 64)) return rc;
+    char *p = (char *)e.bc.p;
+    int32_t *d_hits = (int32_t *)p;
+    uint8_t *d_flags = (uint8_t *)(p + hb);
+    int64_t *d_off = (int64_t *)(((uintptr_t)(p + hb + fb) + 7) & ~(uintptr_t)7);
+    int64_t *d_cuts = d_off + n_reads + 1;
+    // the four used rows (read, adapter, read_start, read_end), packed with stride n_hits
+    for (int f = 0; f < 4 && n_hits; ++f)
+        HIP_TRY(hipMemcpyAsync(d_hits + f * n_hits, hits + f * hit_stride, sizeof(int32_t) * (size_t)n_hits,
+                               hipMemcpyHostToDevice, e.stream));
+    if (n_adp) {
+        HIP_TRY(hipMemcpyAsync(d_flags, bad_start, (size_t)n_adp, hipMemcpyHostToDevice, e.stream));
+        HIP_TRY(hipMemcpyAsync(d_flags + n_adp, bad_end, (size_t)n_adp, hipMemcpyHostToDevice, e.stream));
+    }
+    if (int rc = pcabi_middle_cuts_dev(d_hits, n_hits, n_hits, n_reads, d_flags, d_flags + n_adp, good_side, bad_side,
+                                       d_off, d_cuts, e.stream))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(cut_off, d_off, sizeof(int64_t) * ((size_t)n_reads + 1), hipMemcpyDeviceToHost, e.stream));
+    if (n_hits)
+        HIP_TRY(hipMemcpyAsync(cuts, d_cuts, sizeof(int64_t) * 2 * (size_t)n_hits, hipMemcpyDeviceToHost, e.stream));
+    HIP_TRY(hipStreamSynchronize(e.stream));
+    return 0;
 }
 
 int pcabi_end_trim_dev(const int32_t *start_res, int64_t start_stride, int32_t n_sa,

@@ -177,6 +177,51 @@ def middle_scan(windows, adapter_seqs, scoring_scheme_vals, threshold, device=0)
         cap = int(n)
 
 
+def best_full_identity(windows, adapter_seqs, scoring_scheme_vals, best=None, device=0, best_device_ptr=None):
+    """Adapter-set search reduction on the GPU (pcabi_best_full_identity_host,
+    porechop_abi/nanopore_read.py:158-173): best[a] = max(best[a], max over windows of the full
+    identity of (window, adapter a)), the (adapter, window) results never leaving the device.
+    best: float64[n_adp] start values (zeros if None), returned updated. best_device_ptr: an int
+    device address of float64[n_adp] on `device` to update in place instead (e.g. the tensor an
+    RCCL all-reduce reduces next); then None is returned."""
+    codes, offs, lens = windows
+    codes = np.ascontiguousarray(codes, dtype=np.uint8)
+    offs = np.ascontiguousarray(offs, dtype=np.int64)
+    lens = np.ascontiguousarray(lens, dtype=np.int32)
+    acodes, aoffs, alens = encode_adapters(adapter_seqs)
+    m, mm, go, ge = (int(x) for x in scoring_scheme_vals[:4])
+    if best_device_ptr is not None:
+        rc = lib().pcabi_best_full_identity_host(device, _ptr(codes), codes.size, _ptr(offs), _ptr(lens), len(lens),
+                                                 _ptr(acodes), _ptr(aoffs), _ptr(alens), len(alens), m, mm, go, ge,
+                                                 ctypes.c_void_p(int(best_device_ptr)), 1)
+        check(rc, 'pcabi_best_full_identity_host')
+        return None
+    out = np.zeros(len(alens), np.float64) if best is None else np.array(best, dtype=np.float64)
+    rc = lib().pcabi_best_full_identity_host(device, _ptr(codes), codes.size, _ptr(offs), _ptr(lens), len(lens),
+                                             _ptr(acodes), _ptr(aoffs), _ptr(alens), len(alens), m, mm, go, ge,
+                                             _ptr(out), 0)
+    check(rc, 'pcabi_best_full_identity_host')
+    return out
+
+
+def middle_cuts(hits, n_reads, bad_start, bad_end, good_side, bad_side, device=0):
+    """Middle trim ranges of a scan's hits on the GPU (pcabi_middle_cuts_host,
+    porechop_abi/nanopore_read.py:233-250): hits int32 (>= 4, n_hits) rows read, adapter,
+    read_start, read_end (exclusive); bad_start / bad_end: per adapter, its name is a start / end
+    sequence name. Returns (cut_off int64[n_reads + 1], cuts int64[2 * n_hits]) grouped per read
+    in discovery order -- pcabi_reads_write's cut layout."""
+    hits = np.ascontiguousarray(hits, dtype=np.int32)
+    n_hits = hits.shape[1] if hits.ndim == 2 else 0
+    bs = np.ascontiguousarray(bad_start, dtype=np.uint8)
+    be = np.ascontiguousarray(bad_end, dtype=np.uint8)
+    cut_off = np.zeros(n_reads + 1, np.int64)
+    cuts = np.zeros(2 * n_hits, np.int64)
+    rc = lib().pcabi_middle_cuts_host(device, _ptr(hits), n_hits, n_hits, n_reads, _ptr(bs), _ptr(be), len(bs),
+                                      int(good_side), int(bad_side), _ptr(cut_off), _ptr(cuts))
+    check(rc, 'pcabi_middle_cuts_host')
+    return cut_off, cuts
+
+
 def pid6(m, l):
     """float('%f' % (100*m/l)) elementwise (NaN where l == 0), the reference's identity text
     round trip (porechop_abi/src/alignment.cpp:118-119, porechop_abi/nanopore_read.py:497-498)."""

@@ -6,7 +6,7 @@
       -> k_tile_windows / k_align cross products / k_end_trim           (find_adapters_at_read_ends)
       -> trims D2H (8 B / read)
       -> pcabi_middle_scan_dev over the trimmed reads                   (find_adapters_in_read_middles)
-      -> middle cut ranges (NanoporeRead._apply_middle_hit, vectorised)
+      -> middle cut ranges (NanoporeRead._apply_middle_hit: pcabi_middle_cuts on the device)
       -> the fork's start-and-end filter (porechop_abi.py:36-39)
       -> native trimmed FASTA / FASTQ writer                             (output_reads, get_fastq)
 
@@ -22,7 +22,7 @@ import numpy as np
 
 from . import misc
 from ._lib import check, lib
-from .engine import encode_adapters
+from .engine import encode_adapters, middle_cuts
 from .porechop_abi import middle_adapter_list
 
 VP = ctypes.c_void_p
@@ -41,6 +41,7 @@ class FileTrimmer(object):
                  extra_middle_trim_bad_side=100, min_split_read_size=1000, no_split=False, discard_middle=False,
                  filter_reads=True, device=0):
         self.L = L = lib()
+        self.device = int(device)
         check(L.pcabi_dev_set(device), 'pcabi_dev_set')
         self.sc = tuple(int(x) for x in scoring_scheme_vals[:4])
         self.E, self.thr, self.extra, self.min_trim = int(end_size), float(end_threshold), int(extra_end_trim), \
@@ -163,13 +164,9 @@ class FileTrimmer(object):
                 cap = int(nh)                 # the scan masked the codes: re-upload and rerun
                 d_codes = self._h2d('codes', batch.codes)
             hits = hits[:, :int(nh)]
-            # NanoporeRead._apply_middle_hit (nanopore_read.py:236-252)
-            r, ad = hits[0], hits[1]
-            a0 = hits[2] - np.where(self.bad_start[ad], self.bad, self.good)
-            a1 = hits[3] + np.where(self.bad_end[ad], self.bad, self.good)
-            order = np.argsort(r, kind='stable')
-            cut_off[1:] = np.cumsum(np.bincount(r, minlength=nb))
-            cuts = np.stack([a0[order], a1[order]], 1).astype(np.int64).ravel()
+            # NanoporeRead._apply_middle_hit's trim ranges (nanopore_read.py:242-250) on the device,
+            # grouped per read in the writer's cut layout
+            cut_off, cuts = middle_cuts(hits, nb, self.bad_start, self.bad_end, self.good, self.bad, self.device)
         t = self._tick('middle', t)
         keep = None
         if self.filter_reads:

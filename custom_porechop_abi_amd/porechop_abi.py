@@ -83,19 +83,50 @@ def find_matching_adapter_sets(check_reads, verbosity, end_size, scoring_scheme_
         output_progress_line(0, read_count, print_dest)
     search = [a for a in adapter_sets if '(full sequence)' not in a.name]
     if check_reads:
-        pack = SeqPack([r.seq for r in check_reads])
-        sw, ew = start_end_windows(pack, end_size)
-        starts = [a for a in search if a.start_sequence]
-        ends = [a for a in search if a.end_sequence]
-        sfull = _window_hits(sw, [a.start_sequence[1] for a in starts], scoring_scheme_vals)[0]
-        efull = _window_hits(ew, [a.end_sequence[1] for a in ends], scoring_scheme_vals)[0]
-        for a, row in zip(starts, sfull):
-            a.best_start_score = max(a.best_start_score, float(row.max()))
-        for a, row in zip(ends, efull):
-            a.best_end_score = max(a.best_end_score, float(row.max()))
+        maxima = set_search_maxima(check_reads, end_size, scoring_scheme_vals, search)
+        apply_set_maxima(search, maxima)
     if verbosity > 0:
         output_progress_line(read_count, read_count, print_dest, end_newline=True)
     return [a for a in search if a.best_start_or_end_score() >= adapter_threshold]
+
+
+def set_search_maxima(check_reads, end_size, scoring_scheme_vals, search, out_device_ptr=None):
+    """The check phase's reduction (nanopore_read.py:158-173 over every check read): per distinct
+    start sequence, then per distinct end sequence of the searched sets, the best full-adapter
+    identity over the reads' windows -- reduced on the GPU (engine.best_full_identity), the
+    (adapter, window) results never leaving the device. Returns the float64 maxima (start
+    sequences first), or, with out_device_ptr (an int device address of as many float64), writes
+    them there and returns None (the buffer the sharded drivers all-reduce)."""
+    starts_u, _ = _unique([a.start_sequence[1] for a in search if a.start_sequence])
+    ends_u, _ = _unique([a.end_sequence[1] for a in search if a.end_sequence])
+    pack = SeqPack([r.seq for r in check_reads])
+    sw, ew = start_end_windows(pack, end_size)
+    if out_device_ptr is not None:
+        if starts_u and len(check_reads):
+            engine.best_full_identity(sw, starts_u, scoring_scheme_vals, best_device_ptr=out_device_ptr)
+        if ends_u and len(check_reads):
+            engine.best_full_identity(ew, ends_u, scoring_scheme_vals, best_device_ptr=out_device_ptr + 8 * len(starts_u))
+        return None
+    out = np.zeros(len(starts_u) + len(ends_u), np.float64)
+    if len(check_reads):
+        if starts_u:
+            out[:len(starts_u)] = engine.best_full_identity(sw, starts_u, scoring_scheme_vals)
+        if ends_u:
+            out[len(starts_u):] = engine.best_full_identity(ew, ends_u, scoring_scheme_vals)
+    return out
+
+
+def apply_set_maxima(search, maxima):
+    """best_start_score / best_end_score of every searched set = max(itself, its sequence's maximum)."""
+    starts = [a for a in search if a.start_sequence]
+    ends = [a for a in search if a.end_sequence]
+    starts_u, s_idx = _unique([a.start_sequence[1] for a in starts])
+    _, e_idx = _unique([a.end_sequence[1] for a in ends])
+    maxima = np.asarray(maxima, dtype=np.float64)
+    for a, k in zip(starts, s_idx.tolist()):
+        a.best_start_score = max(a.best_start_score, float(maxima[k]))
+    for a, k in zip(ends, e_idx.tolist()):
+        a.best_end_score = max(a.best_end_score, float(maxima[len(starts_u) + k]))
 
 
 def fix_up_1d2_sets(matching_sets):

@@ -4,10 +4,11 @@
 Every (read, adapter) alignment is independent, so the trimming phases need no exchange at all:
 a rank runs the batched drivers of porechop_abi.py on its own reads. The one real exchange is
 the adapter-set search (porechop_abi/porechop_abi.py:200-245): a set is kept when its best
-full-adapter identity over ALL check reads reaches the threshold, so the per-set maxima are
-all-reduced with MAX (2 x n_sets float64, exact and order-free) before the same filter runs on
-every rank. With backend "nccl" (RCCL over xGMI on MI355X) the buffer lives on the rank's GPU;
-with "gloo" it stays on the host (the CPU tests).
+full-adapter identity over ALL check reads reaches the threshold, so the per-sequence maxima
+(one float64 per distinct start / end sequence, exact and order-free) are all-reduced with MAX
+before the same filter runs on every rank. With backend "nccl" (RCCL over xGMI on MI355X) the
+GPU reduction writes them straight into the device buffer the collective reduces; with "gloo"
+they go through the host (the CPU tests).
 
 Shards are contiguous read ranges, balanced by read count (end windows: equal work per read) or
 by total bases (middle scan: work grows with read length). gather_trims() brings the per-read
@@ -53,33 +54,35 @@ def _device_tensor(values, group):
     return t
 
 
-def allreduce_set_scores(search_sets, group=None):
-    """All-reduce MAX of every set's best_start_score / best_end_score, written back in place."""
-    dist = _dist()
-    if not dist.is_initialized() or dist.get_world_size(group) == 1 or not search_sets:
-        return
-    t = _device_tensor([[a.best_start_score, a.best_end_score] for a in search_sets], group)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
-    vals = t.cpu().numpy()
-    for a, (s, e) in zip(search_sets, vals):
-        a.best_start_score, a.best_end_score = float(s), float(e)
-
-
 def find_matching_adapter_sets(check_reads, verbosity, end_size, scoring_scheme_vals, print_dest,
                                adapter_threshold, threads, adapter_sets=None, group=None):
     """Sharded porechop_abi.find_matching_adapter_sets: check_reads is the FULL check list (same
-    on every rank); each rank aligns its shard, then the per-set maxima are all-reduced."""
+    on every rank); each rank reduces its shard's windows on its GPU into the per-sequence maxima
+    (porechop_abi.set_search_maxima: the (adapter, window) results never leave the device), and
+    those maxima are all-reduced with MAX. With "nccl" (RCCL) the kernel writes them straight into
+    the device buffer the collective reduces; with "gloo" they go through the host."""
     dist = _dist()
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     if adapter_sets is None:
         adapter_sets = _adapters.ADAPTERS
+    if not dist.is_initialized():
+        return P.find_matching_adapter_sets(check_reads, verbosity, end_size, scoring_scheme_vals, print_dest,
+                                            adapter_threshold, threads, adapter_sets=adapter_sets)
     lo, hi = shard_bounds(len(check_reads), rank, world)
-    P.find_matching_adapter_sets(check_reads[lo:hi], verbosity if rank == 0 else 0, end_size,
-                                 scoring_scheme_vals, print_dest, adapter_threshold, threads,
-                                 adapter_sets=adapter_sets)
     search = [a for a in adapter_sets if '(full sequence)' not in a.name]
-    allreduce_set_scores(search, group)
+    n_u = len(set(a.start_sequence[1] for a in search if a.start_sequence)) + \
+        len(set(a.end_sequence[1] for a in search if a.end_sequence))
+    import torch
+    if dist.get_backend(group) == 'nccl':
+        t = torch.zeros(max(n_u, 1), dtype=torch.float64, device='cuda')
+        torch.cuda.synchronize()
+        P.set_search_maxima(check_reads[lo:hi], end_size, scoring_scheme_vals, search, out_device_ptr=t.data_ptr())
+    else:
+        t = torch.zeros(max(n_u, 1), dtype=torch.float64)
+        t[:n_u] = torch.from_numpy(P.set_search_maxima(check_reads[lo:hi], end_size, scoring_scheme_vals, search))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    P.apply_set_maxima(search, t.cpu().numpy()[:n_u])
     return [a for a in search if a.best_start_or_end_score() >= adapter_threshold]
 
 

@@ -248,6 +248,33 @@ int64_t pcabi_middle_seed_runs(void);
  */
 int pcabi_best_full_identity_dev(const int32_t *res, int64_t stride, int64_t n_win, int32_t n_adp,
                                  double *best, void *stream);
+/* The same over windows in host buffers (layout of pcabi_align_host, cross product): the
+ * (adapter, window) results stay on the device, only n_adp doubles move. best_on_device != 0:
+ * `best` is a device pointer on `device` (e.g. the buffer a collective reduces next; it must be
+ * ready when called and is updated when the call returns); else a host array. */
+int pcabi_best_full_identity_host(int device, const uint8_t *codes, int64_t codes_len, const int64_t *win_off,
+                                  const int32_t *win_len, int64_t n_win, const uint8_t *adp_codes,
+                                  const int32_t *adp_off, const int32_t *adp_len, int32_t n_adp, int match,
+                                  int mismatch, int gap_open, int gap_extend, double *best, int best_on_device);
+
+/*
+ * Middle-adapter trim ranges (porechop_abi/nanopore_read.py:233-250) of a scan's hits: hit k =
+ * (read hits[k], adapter hits[stride + k], read_start hits[2 stride + k], read_end (exclusive)
+ * hits[3 stride + k]) -- the layout pcabi_middle_scan_* return -- becomes the range
+ * [read_start - (bad_start[a] ? bad_side : good_side), read_end + (bad_end[a] ? bad_side : good_side))
+ * of NanoporeRead.middle_trim_positions; bad_start / bad_end flag the adapters whose name is a
+ * start / end sequence name. Output grouped per read, each read's hits in discovery order:
+ * ranges of read r at cuts[2 k], cuts[2 k + 1] for k in [cut_off[r], cut_off[r + 1]) (cut_off has
+ * n_reads + 1 entries) -- the cut layout of pcabi_reads_write.
+ *   pcabi_middle_cuts_dev  : device pointers, asynchronous on `stream`.
+ *   pcabi_middle_cuts_host : host arrays (n_adp flags each).
+ */
+int pcabi_middle_cuts_dev(const int32_t *hits, int64_t hit_stride, int64_t n_hits, int64_t n_reads,
+                          const uint8_t *bad_start, const uint8_t *bad_end, int good_side, int bad_side,
+                          int64_t *cut_off, int64_t *cuts, void *stream);
+int pcabi_middle_cuts_host(int device, const int32_t *hits, int64_t hit_stride, int64_t n_hits, int64_t n_reads,
+                           const uint8_t *bad_start, const uint8_t *bad_end, int32_t n_adp, int good_side,
+                           int bad_side, int64_t *cut_off, int64_t *cuts);
 
 /*
  * Barcode demultiplexing call (porechop_abi/nanopore_read.py:408-482, determine_barcode) from

@@ -168,3 +168,16 @@ def middle_scan_threaded(windows, adapter_seqs, scoring, threshold, threads=None
         if nh <= cap:
             return out[:, :nh].copy()
         cap = int(nh)
+
+
+def best_full_identity_windows(windows, adapter_seqs, scoring, best=None, device=0, best_device_ptr=None):
+    """Drop-in for custom_porechop_abi_amd.engine.best_full_identity computed by the oracle (CPU)."""
+    from custom_porechop_abi_amd.engine import pid6
+    assert best_device_ptr is None, 'the CPU stand-in has no device buffer'
+    n_win, n_adp = len(windows[2]), len(adapter_seqs)
+    out = np.zeros(n_adp, np.float64) if best is None else np.array(best, dtype=np.float64)
+    if n_win == 0 or n_adp == 0:
+        return out
+    res = align_windows(windows, adapter_seqs, scoring)
+    full = np.where(res[0] == -1, 0.0, pid6(res[5], res[7])).reshape(n_adp, n_win)
+    return np.maximum(out, full.max(axis=1))

@@ -83,6 +83,7 @@ def check_case(case):
 def test_drivers_match_reference_with_oracle_backend(case_name, monkeypatch):
     from custom_porechop_abi_amd import engine
     monkeypatch.setattr(engine, 'align', oracle_lib.align_windows)
+    monkeypatch.setattr(engine, 'best_full_identity', oracle_lib.best_full_identity_windows)
     monkeypatch.setattr(engine, 'first_hits', oracle_lib.first_hits_windows)
     monkeypatch.setattr(engine, 'middle_scan', oracle_lib.middle_scan_windows)
     check_case([c for c in G2['cases'] if c['case'] == case_name][0])
@@ -99,6 +100,7 @@ def test_reference_test_expectations_one_adapter_set(monkeypatch):
     3 of 9 end-trimmed -- on the G2 decisions and through our drivers."""
     from custom_porechop_abi_amd import engine
     monkeypatch.setattr(engine, 'align', oracle_lib.align_windows)
+    monkeypatch.setattr(engine, 'best_full_identity', oracle_lib.best_full_identity_windows)
     monkeypatch.setattr(engine, 'first_hits', oracle_lib.first_hits_windows)
     monkeypatch.setattr(engine, 'middle_scan', oracle_lib.middle_scan_windows)
     case = [c for c in G2['cases'] if c['case'] == 'one_adapter_set'][0]
@@ -143,3 +145,83 @@ def test_per_read_methods_on_gpu(gpu_lib, case_name):
             (exp['start_trim'], exp['end_trim'], exp['barcode_call'])
         assert _ranges(r.middle_trim_positions) == exp['middle_trim']
         assert r.middle_hit_str == exp['middle_hit_str']
+
+
+@pytest.mark.gpu
+def test_middle_cut_ranges_on_device(gpu_lib):
+    """pcabi_middle_cuts (the device epilogue of the middle scan) == NanoporeRead._apply_middle_hit's
+    middle_trim_positions (nanopore_read.py:242-250) for random hits in discovery order: per read,
+    the same ranges in the same order (CSR, the writer's cut layout)."""
+    import random
+    import numpy as np
+    from custom_porechop_abi_amd import engine
+    from custom_porechop_abi_amd.nanopore_read import NanoporeRead
+    rng = random.Random(12)
+    n_reads, n_adp = 300, 9
+    names = ['a%d' % k for k in range(n_adp)]
+    start_names = set(names[:4]) | {names[7]}
+    end_names = set(names[3:6]) | {names[7]}
+    hits = []
+    for _ in range(1500):
+        r = rng.randrange(n_reads)
+        a = rng.randrange(n_adp)
+        s0 = rng.randrange(0, 5000)
+        hits.append([r, a, s0, s0 + rng.randrange(0, 60), 20, 24])
+    h = np.array(hits, np.int32).T.copy()
+    bs = np.array([x in start_names for x in names], np.uint8)
+    be = np.array([x in end_names for x in names], np.uint8)
+    cut_off, cuts = engine.middle_cuts(h, n_reads, bs, be, 10, 100)
+    assert cut_off[0] == 0 and cut_off[-1] == len(hits)
+    for r in range(n_reads):
+        read = NanoporeRead('r', 'A', '')
+        exp = []
+        for k, (rr, a, s0, e0, _, _) in enumerate(hits):
+            if rr == r:
+                read._apply_middle_hit(names[a], 90.0, s0, e0, 10, 100, start_names, end_names)
+                exp.append((s0 - (100 if names[a] in start_names else 10), e0 + (100 if names[a] in end_names else 10)))
+        got = [tuple(cuts[2 * k:2 * k + 2].tolist()) for k in range(cut_off[r], cut_off[r + 1])]
+        assert got == exp, r
+        pos = set()
+        for a0, a1 in got:
+            pos.update(range(a0, a1))
+        assert pos == read.middle_trim_positions
+    # no hits: every read gets an empty range list
+    cut_off, cuts = engine.middle_cuts(np.zeros((6, 0), np.int32), 5, bs, be, 10, 100)
+    assert cut_off.tolist() == [0] * 6 and len(cuts) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case_name', ['two_adapter_sets', 'synthetic_default'])
+def test_set_search_reduced_on_device_through_rccl(gpu_lib, case_name):
+    """The check phase as the sharded drivers run it on a GPU: the per-sequence maxima reduced by
+    k_best_full_id straight into a device tensor, all-reduced by RCCL (a world of one rank on
+    this box's GPU), then the reference's set filter: set scores and matching sets == the
+    reference's (G2)."""
+    import io
+    import socket
+    import torch
+    import torch.distributed as dist
+    from custom_porechop_abi_amd import adapters as A, shards
+    from custom_porechop_abi_amd.nanopore_read import NanoporeRead
+    case = next(c for c in G2['cases'] if c['case'] == case_name)
+    opts = case['opts']
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group('nccl', init_method='tcp://127.0.0.1:%d' % port, rank=0, world_size=1)
+    try:
+        sets = A.fresh_adapters()
+        if case['input'] == 'synthetic_reads':
+            recs = [tuple(x) for x in G2['synthetic_reads']]
+        else:
+            recs = golden_lib.load_records(case['input'])
+        reads = [NanoporeRead(n, sq, q) for n, sq, q in recs]
+        check = reads[:opts.get('check_reads', 10000)]
+        matching = shards.find_matching_adapter_sets(check, 0, opts['end_size'], opts['scoring'], io.StringIO(),
+                                                     opts['adapter_threshold'], 1, adapter_sets=sets)
+        got = [[a.name, a.best_start_score, a.best_end_score] for a in sets if '(full sequence)' not in a.name]
+        assert got == case['set_scores']
+        assert [a.name for a in matching] == [n for n in case['matching'] if '(full sequence)' not in n]
+    finally:
+        dist.destroy_process_group()

@@ -49,6 +49,7 @@ def _worker(rank, world, port, case_name, out_dir):
     from custom_porechop_abi_amd.nanopore_read import NanoporeRead
     from tests import oracle_lib
     engine.align = oracle_lib.align_windows            # CPU stand-ins for the HIP kernels
+    engine.best_full_identity = oracle_lib.best_full_identity_windows
     engine.first_hits = oracle_lib.first_hits_windows
     engine.middle_scan = oracle_lib.middle_scan_windows
     dist.init_process_group('gloo', init_method='tcp://127.0.0.1:%d' % port, rank=rank, world_size=world)
