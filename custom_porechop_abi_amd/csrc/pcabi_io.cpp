@@ -31,6 +31,7 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <cctype>
 #include <cerrno>
 #include <cstdlib>
 #include <memory>
@@ -455,7 +456,9 @@ int pcabi_fastx_open(const char *path, int raw, pcabi_fastx **out) {
         struct stat st;
         if (fd >= 0 && fstat(fd, &st) == 0 && st.st_size > 0) {
             // MAP_POPULATE: the pages of a cached file are mapped in one pass, not fault by fault
-            void *m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+            // (files past 8 GB are mapped lazily: a range reader touches only its own part)
+            const int pop = st.st_size <= (8ll << 30) ? MAP_POPULATE : 0;
+            void *m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE | pop, fd, 0);
             if (m != MAP_FAILED) {
                 madvise(m, (size_t)st.st_size, MADV_SEQUENTIAL);
                 r->map = m;
@@ -504,6 +507,79 @@ int pcabi_fastx_open(const char *path, int raw, pcabi_fastx **out) {
 }
 
 int pcabi_fastx_type(const pcabi_fastx *r) { return r ? r->type : -1; }
+
+}  // extern "C"
+
+namespace {
+// Universal-newline line starts inside a memory-mapped file (the reader's line rules).
+size_t line_after(const char *b, size_t n, size_t p) {
+    while (p < n && b[p] != '\n' && b[p] != '\r') ++p;
+    if (p < n && b[p] == '\r') {
+        ++p;
+        if (p < n && b[p] == '\n') ++p;
+    } else if (p < n) {
+        ++p;
+    }
+    return p;
+}
+size_t line_at_or_after(const char *b, size_t n, size_t p) {
+    if (p == 0 || p >= n) return std::min(p, n);
+    if (b[p - 1] == '\n' || (b[p - 1] == '\r' && b[p] != '\n')) return p;
+    return line_after(b, n, p);
+}
+bool blank_after(const char *b, size_t n, size_t p) {   // only whitespace up to the line end
+    for (; p < n && b[p] != '\n' && b[p] != '\r'; ++p)
+        if (!std::isspace((unsigned char)b[p])) return false;
+    return true;
+}
+// the nearest header ('>' at a line start) before position p, or n if none
+size_t header_before(const char *b, size_t n, size_t p) {
+    while (p > 0) {
+        --p;
+        if (b[p] == '>' && (p == 0 || b[p - 1] == '\n' || b[p - 1] == '\r')) return p;
+    }
+    return n;
+}
+}  // namespace
+
+extern "C" {
+
+int64_t pcabi_fastx_record_start(const pcabi_fastx *r, int64_t byte) {
+    if (!r || !r->map) return fail(PCABI_E_ARG, "record starts need a plain (memory-mapped) file");
+    const char *b = r->base;
+    const size_t n = r->map_len;
+    size_t p = line_at_or_after(b, n, byte < 0 ? 0 : (size_t)byte);
+    for (; p < n; p = line_after(b, n, p)) {
+        if (r->type == PCABI_FASTQ) {
+            // a header line ('@') whose third line is the '+' line: a quality line may start
+            // with '@', but two lines after it comes the next record's sequence, never '+'
+            if (b[p] != '@') continue;
+            const size_t q = line_after(b, n, line_after(b, n, p));
+            if (q < n && b[q] == '+') return (int64_t)p;
+        } else {
+            // a header with a name, after a header with a name: an empty header's sequence runs
+            // on into the next record (the reader's rule), so no record starts there
+            if (b[p] != '>' || blank_after(b, n, p + 1)) continue;
+            const size_t h = header_before(b, n, p);
+            if (h == n || !blank_after(b, n, h + 1)) return (int64_t)p;
+        }
+    }
+    return (int64_t)n;
+}
+
+int pcabi_fastx_set_range(pcabi_fastx *r, int64_t begin, int64_t end) {
+    if (!r || !r->map) return fail(PCABI_E_ARG, "byte ranges need a plain (memory-mapped) file");
+    if (begin < 0 || end < begin || (size_t)end > r->map_len) return fail(PCABI_E_ARG, "byte range outside the file");
+    r->pos = (size_t)begin;
+    r->end = (size_t)end;
+    const size_t pg = (size_t)begin & ~(size_t)4095;
+    if (end > begin) madvise((char *)r->map + pg, (size_t)end - pg, MADV_WILLNEED);
+    r->eof = true;
+    r->fa_have_name = false;
+    r->fa_name.clear();
+    r->fa_seq.clear();
+    return 0;
+}
 
 void pcabi_fastx_close(pcabi_fastx *r) {
     if (!r) return;

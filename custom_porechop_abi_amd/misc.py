@@ -47,6 +47,8 @@ def _declare(L):
         'pcabi_reads_views': ([P, ctypes.POINTER(_View)], c_int),
         'pcabi_reads_free': ([P], None),
         'pcabi_reads_write': ([P, ctypes.c_char_p, c_int, c_int, c_int, P, P, P, P, c_int, c_int, c_int, P], c_int),
+        'pcabi_fastx_record_start': ([P, i64], i64),
+        'pcabi_fastx_set_range': ([P, i64, i64], c_int),
     }
     for name, (a, r) in sig.items():
         f = getattr(L, name)
@@ -155,12 +157,41 @@ def _open_error(path):
     return msg.decode() if msg else path
 
 
-def read_batches(path, max_reads=100000, max_bases=1 << 30, raw=False):
-    """Stream a FASTA / FASTQ(.gz) file as ReadBatch objects (pcabi_fastx_next)."""
+def record_boundaries(path, parts):
+    """Byte offsets [parts + 1] splitting a plain FASTA / FASTQ file into `parts` contiguous record
+    ranges of about equal size (so about equal bases): each cut is moved forward to the next record
+    start (pcabi_fastx_record_start). None for a gzip file (it cannot be entered mid-stream)."""
+    L = _declare(lib())
+    h = ctypes.c_void_p()
+    rc = L.pcabi_fastx_open(os.fsencode(path), 0, ctypes.byref(h))
+    if rc != 0:
+        raise ValueError(_open_error(path))
+    try:
+        if get_compression_type(path) != 'plain':
+            return None
+        size = os.path.getsize(path)
+        cuts = [0]
+        for k in range(1, parts):
+            b = L.pcabi_fastx_record_start(h, size * k // parts)
+            if b < 0:
+                return None
+            cuts.append(max(int(b), cuts[-1]))
+        cuts.append(size)
+        return cuts
+    finally:
+        L.pcabi_fastx_close(h)
+
+
+def read_batches(path, max_reads=100000, max_bases=1 << 30, raw=False, byte_range=None):
+    """Stream a FASTA / FASTQ(.gz) file as ReadBatch objects (pcabi_fastx_next); byte_range =
+    (begin, end) record starts of a plain file (record_boundaries) reads only that range."""
     L = _declare(lib())
     h = ctypes.c_void_p()
     rc = L.pcabi_fastx_open(os.fsencode(path), int(raw), ctypes.byref(h))
     if rc != 0:
+        raise ValueError(_open_error(path))
+    if byte_range is not None and L.pcabi_fastx_set_range(h, int(byte_range[0]), int(byte_range[1])) != 0:
+        L.pcabi_fastx_close(h)
         raise ValueError(_open_error(path))
     try:
         while True:

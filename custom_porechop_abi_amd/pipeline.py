@@ -14,6 +14,7 @@ Decisions are the reference's (same kernels and epilogues the parity tests cover
 demultiplexing and verbose output stay with the per-read drivers (porechop_abi.py here).
 """
 import ctypes
+import os
 import queue
 import threading
 import time
@@ -174,8 +175,13 @@ class FileTrimmer(object):
             keep = ((trims[0] > 0) & (trims[1] > 0)).astype(np.uint8)
         return trims[0], trims[1], cut_off, cuts, hits, keep
 
-    def trim_file(self, in_path, out_path, out_format='fastq', max_reads=200000):
+    def trim_file(self, in_path, out_path, out_format='fastq', max_reads=200000, byte_range=None, batch_filter=None,
+                  segments=None):
         """Trim a FASTA / FASTQ(.gz) file batch by batch into out_path. Returns read counts.
+
+        Shards (shards.trim_file_sharded): byte_range = (begin, end) record starts of a plain file
+        reads only that range; batch_filter(k) False skips batch k (parsed, not trimmed or
+        written); segments, a list, receives (k, begin, end) byte spans of out_path per written batch.
 
         Three stages overlap across batches: a reader thread parses the next batch, this thread
         runs the device work, a writer thread writes the previous batch (in file order). The
@@ -198,8 +204,10 @@ class FileTrimmer(object):
 
         def produce():
             try:
-                for b in misc.read_batches(in_path, max_reads=max_reads):
-                    if not put_parsed(b):
+                for k, b in enumerate(misc.read_batches(in_path, max_reads=max_reads, byte_range=byte_range)):
+                    if batch_filter is not None and not batch_filter(k):
+                        continue
+                    if not put_parsed((k, b)):
                         return
                 put_parsed(None)
             except BaseException as ex:   # handed to the consumer
@@ -213,11 +221,14 @@ class FileTrimmer(object):
                     break
                 if errors:
                     continue                 # drain after a failure
-                b, st, et, co, cu, keep = item
+                k, b, st, et, co, cu, keep = item
                 t0 = time.perf_counter()
                 try:
+                    at = os.path.getsize(out_path) if (segments is not None and not first) else 0
                     misc.write_reads(b, out_path, out_format, st, et, None, self.min_split, self.discard_middle,
                                      select=keep, append=not first, cut_arrays=(co, cu))
+                    if segments is not None:
+                        segments.append((k, at, os.path.getsize(out_path)))
                 except BaseException as ex:
                     errors.append(ex)
                 first = False
@@ -240,8 +251,9 @@ class FileTrimmer(object):
                     break
                 if isinstance(b, BaseException):
                     raise b
+                k, b = b
                 st, et, co, cu, _, keep = self.trim(b)
-                wq.put((b, st, et, co, cu, keep))   # the writer drains even after a failure
+                wq.put((k, b, st, et, co, cu, keep))   # the writer drains even after a failure
                 del b
                 t = time.perf_counter()
         finally:

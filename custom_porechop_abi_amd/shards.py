@@ -144,3 +144,91 @@ def gather_trims(reads, bounds, group=None):
     dist.all_gather(parts, t, group=group)
     rows = np.concatenate([p.cpu().numpy()[:c] for p, c in zip(parts, counts)], axis=0)
     return rows[:, 0].astype(np.int64), rows[:, 1].astype(np.int64)
+
+
+def trim_file_sharded(in_path, out_path, out_format='fastq', scoring_scheme_vals=(3, -6, -5, -2), end_size=150,
+                      end_threshold=75.0, extra_end_trim=2, min_trim_size=4, middle_threshold=90.0,
+                      extra_middle_trim_good_side=10, extra_middle_trim_bad_side=100, min_split_read_size=1000,
+                      check_reads=10000, adapter_threshold=90.0, max_reads=100000, group=None, device=None,
+                      trimmer_factory=None):
+    """The CLI's file-to-file path (porechop_abi.py:41-131: adapter-set search on the first
+    check_reads records, end trim, middle scan, the fork's filter, trimmed output) on every rank of
+    `group`, one GPU each:
+
+      * adapter-set search: every rank reads the check records, aligns its shard of them and the
+        per-sequence maxima are all-reduced once (find_matching_adapter_sets: the device buffer
+        under RCCL);
+      * trimming: a plain file is split into contiguous record ranges of about equal bytes (so
+        bases), cut at record starts (misc.record_boundaries); each rank trims its range with a
+        pipeline.FileTrimmer into its own part file, in order; a gzip file cannot be entered
+        mid-stream, so every rank streams it and trims every world-th batch, recording the byte
+        span of each batch it writes;
+      * output: rank 0 concatenates the parts in record order (the reference's output order) --
+        the only other exchange is the span lists (gzip input) and the read counts.
+
+    Returns the job's read counts (every rank). trimmer_factory(matching_sets, **options) builds
+    the per-rank trimmer (FileTrimmer by default; the CPU tests pass an oracle-backed one)."""
+    import io
+    import os
+    import shutil
+    from . import misc
+    dist = _dist()
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    check = []
+    if check_reads > 0:
+        for b in misc.read_batches(in_path, max_reads=check_reads):
+            check = b.nanopore_reads()
+            break
+    matching = find_matching_adapter_sets(check, 0, end_size, scoring_scheme_vals, io.StringIO(), adapter_threshold, 1,
+                                          group=group)
+    matching = P.add_full_barcode_adapter_sets(P.fix_up_1d2_sets(matching))
+    opts = dict(scoring_scheme_vals=scoring_scheme_vals, end_size=end_size, end_threshold=end_threshold,
+                extra_end_trim=extra_end_trim, min_trim_size=min_trim_size, middle_threshold=middle_threshold,
+                extra_middle_trim_good_side=extra_middle_trim_good_side,
+                extra_middle_trim_bad_side=extra_middle_trim_bad_side, min_split_read_size=min_split_read_size)
+    if trimmer_factory is None:
+        from .pipeline import FileTrimmer
+        trimmer_factory = FileTrimmer
+        opts['device'] = int(os.environ.get('LOCAL_RANK', rank)) if device is None else device
+    ft = trimmer_factory(matching, **opts)
+    d, base = os.path.split(os.path.abspath(out_path))
+    part = lambda r: os.path.join(d, '.pcabi_part%d_%s' % (r, base))
+    bounds = misc.record_boundaries(in_path, world)
+    segments = None if bounds is not None else []
+    try:
+        if bounds is not None:
+            counts = ft.trim_file(in_path, part(rank), out_format, max_reads, byte_range=(bounds[rank], bounds[rank + 1]))
+        else:
+            counts = ft.trim_file(in_path, part(rank), out_format, max_reads,
+                                  batch_filter=lambda k: k % world == rank, segments=segments)
+    finally:
+        if hasattr(ft, 'close'):
+            ft.close()
+    if world > 1:
+        spans = [None] * world
+        dist.all_gather_object(spans, (segments, counts), group=group)
+    else:
+        spans = [(segments, counts)]
+    if rank == 0:
+        with open(out_path, 'wb') as out:
+            if bounds is not None:
+                for r in range(world):
+                    with open(part(r), 'rb') as f:
+                        shutil.copyfileobj(f, out, 1 << 24)
+            else:
+                order = sorted((k, r, a, e) for r, (segs, _) in enumerate(spans) for k, a, e in segs)
+                files = [open(part(r), 'rb') for r in range(world)]
+                try:
+                    for k, r, a, e in order:
+                        files[r].seek(a)
+                        out.write(files[r].read(e - a))
+                finally:
+                    for f in files:
+                        f.close()
+        for r in range(world):
+            if os.path.exists(part(r)):
+                os.remove(part(r))
+    if world > 1:
+        dist.barrier(group=group)
+    return {k: sum(c[k] for _, c in spans) for k in ('reads_in', 'reads_kept')}

@@ -407,6 +407,15 @@ typedef struct pcabi_reads_view {
 } pcabi_reads_view;
 int pcabi_fastx_open(const char *path, int raw, pcabi_fastx **out);
 int pcabi_fastx_type(const pcabi_fastx *r);
+/* Byte-range reading of a plain (not gzip) file, for read shards split by position:
+ *   pcabi_fastx_record_start : the first record start at or after `byte` (the file size if
+ *       none): a FASTQ header line whose third line is the '+' line; a FASTA header with a name
+ *       whose previous header has one too (an empty header's sequence runs on into the next
+ *       record). Splitting at record starts gives every record to exactly one range.
+ *   pcabi_fastx_set_range    : read only [begin, end) from now on (both record starts, or 0 / the
+ *       file size); a fresh reader (no record read yet). */
+int64_t pcabi_fastx_record_start(const pcabi_fastx *r, int64_t byte);
+int pcabi_fastx_set_range(pcabi_fastx *r, int64_t begin, int64_t end);
 int64_t pcabi_fastx_next(pcabi_fastx *r, int64_t max_reads, int64_t max_bases, pcabi_reads **out);
 void pcabi_fastx_close(pcabi_fastx *r);
 int pcabi_fastx_load(const char *path, int raw, pcabi_reads **out);

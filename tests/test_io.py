@@ -20,6 +20,7 @@ import pytest
 from tests import golden_lib
 
 G3 = json.load(gzip.open(os.path.join(golden_lib.GOLDEN, 'g3_io.json.gz'), 'rt'))
+GOLDEN_IO = os.path.join(golden_lib.GOLDEN, "io")
 CASES = G3['cases']
 
 
@@ -152,3 +153,56 @@ def test_large_gzip_streaming_and_threads(tmp_path, monkeypatch):
             assert got == exp, (threads, path)
             b = misc.load_batch(path)
             assert b.n == len(exp) and b.sequence(len(exp) - 1) == exp[-1][1]
+
+
+def _batches_text(path, byte_range=None, max_reads=3):
+    from custom_porechop_abi_amd import misc
+    out = []
+    for b in misc.read_batches(path, max_reads=max_reads, byte_range=byte_range):
+        out += [(b.name(i), b.sequence(i), b.quals(i), int(b.rna[i])) for i in range(b.n)]
+    return out
+
+
+def test_byte_range_shards_cover_every_record_once(tmp_path):
+    """Reads split into byte ranges at record starts (misc.record_boundaries /
+    pcabi_fastx_record_start, the sharded file pipeline's split): for every cut position of the
+    plain fixtures (CRLF / lone-CR endings, blank and whitespace lines, empty FASTA headers whose
+    sequence runs on, qualities starting with '@'), the ranges' records concatenated == the
+    whole file's records."""
+    import random
+    from custom_porechop_abi_amd import _lib, misc
+    L = misc._declare(_lib.lib())
+    import ctypes
+    files = [os.path.join(GOLDEN_IO, f) for f in sorted(os.listdir(GOLDEN_IO)) if not f.endswith('.gz')]
+    # FASTQ whose qualities start with '@' and FASTA with empty headers in the middle
+    rng = random.Random(8)
+    q = str(tmp_path / 'at_quals.fastq')
+    with open(q, 'w') as f:
+        for k in range(40):
+            s = ''.join(rng.choice('ACGT') for _ in range(rng.randint(0, 30)))
+            f.write('@r%d x\n%s\n+\n%s\n' % (k, s, '@' * len(s) if k % 2 else ''.join(rng.choice('@+!#I') for _ in s)))
+    a = str(tmp_path / 'empty_headers.fasta')
+    with open(a, 'w') as f:
+        for k in range(30):
+            f.write('>%s\n%s\n\n%s\n' % ('' if k % 4 == 1 else 'r%d' % k, 'ACGT' * (k % 5), 'GG' * (k % 3)))
+    files += [q, a]
+    for path in files:
+        whole = _batches_text(path, max_reads=1 << 20)
+        size = os.path.getsize(path)
+        h = ctypes.c_void_p()
+        assert L.pcabi_fastx_open(os.fsencode(path), 0, ctypes.byref(h)) == 0
+        try:
+            starts = sorted({int(L.pcabi_fastx_record_start(h, b)) for b in range(size + 1)})
+        finally:
+            L.pcabi_fastx_close(h)
+        assert starts[-1] == size
+        for cut in starts:
+            got = _batches_text(path, (0, cut)) + _batches_text(path, (cut, size))
+            assert got == whole, (path, cut)
+        for parts in (2, 3, 5):
+            b = misc.record_boundaries(path, parts)
+            got = []
+            for k in range(parts):
+                got += _batches_text(path, (b[k], b[k + 1]))
+            assert got == whole, (path, parts)
+    assert misc.record_boundaries(os.path.join(GOLDEN_IO, 'plain_mixed.fastq.gz'), 2) is None

@@ -145,3 +145,36 @@ def test_trim_file_without_matching_sets_writes_reads_unchanged(gpu_lib, tmp_pat
         ft.close()
     assert counts == {'reads_in': 30, 'reads_kept': 30}
     assert open(out_path).read() == open(in_path).read()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('gz', [False, True])
+def test_sharded_file_pipeline_on_gpu(gpu_lib, tmp_path, gz):
+    """shards.trim_file_sharded with the real FileTrimmer on this box's GPU, the set search
+    all-reduced by RCCL (a world of one rank): the written file == the reference's output (G2)."""
+    import gzip
+    import socket
+    import torch.distributed as dist
+    from custom_porechop_abi_amd import shards
+    case = [c for c in G2['cases'] if c['case'] == 'synthetic_default'][0]
+    o = case['opts']
+    records = [tuple(x) for x in G2['synthetic_reads']]
+    text = ''.join('@%s\n%s\n+\n%s\n' % r for r in records)
+    in_path = str(tmp_path / ('in.fastq.gz' if gz else 'in.fastq'))
+    with (gzip.open(in_path, 'wt') if gz else open(in_path, 'w')) as f:
+        f.write(text)
+    out_path = str(tmp_path / 'out.fastq')
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group('nccl', init_method='tcp://127.0.0.1:%d' % port, rank=0, world_size=1)
+    try:
+        counts = shards.trim_file_sharded(in_path, out_path, 'fastq', o['scoring'], o['end_size'], o['end_threshold'],
+                                          o['extra_end_trim'], o['min_trim_size'], o['middle_threshold'], 10, 100, 1000,
+                                          check_reads=o.get('check_reads', 10000),
+                                          adapter_threshold=o['adapter_threshold'], max_reads=7, device=0)
+    finally:
+        dist.destroy_process_group()
+    assert counts['reads_in'] == len(records)
+    assert open(out_path).read() == _expected(case, records)

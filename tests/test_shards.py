@@ -132,3 +132,97 @@ def test_shard_bounds():
     for w in (1, 2, 3, 4):
         b = [shard_bounds_by_length(lens, r, w) for r in range(w)]
         assert b[0][0] == 0 and b[-1][1] == len(lens) and all(b[k][1] == b[k + 1][0] for k in range(w - 1))
+
+
+class _OracleTrimmer(object):
+    """pipeline.FileTrimmer's file loop with the batch decisions made by the batched drivers on the
+    CPU oracle (TEST INFRASTRUCTURE: the GPU tests run the real FileTrimmer)."""
+
+    def __init__(self, matching_sets, scoring_scheme_vals, end_size, end_threshold, extra_end_trim, min_trim_size,
+                 middle_threshold, extra_middle_trim_good_side, extra_middle_trim_bad_side, min_split_read_size):
+        from custom_porechop_abi_amd.pipeline import FileTrimmer
+        self.m, self.sc, self.E, self.thr = matching_sets, scoring_scheme_vals, end_size, end_threshold
+        self.extra, self.min_trim, self.mthr = extra_end_trim, min_trim_size, middle_threshold
+        self.good, self.bad = extra_middle_trim_good_side, extra_middle_trim_bad_side
+        self.min_split, self.discard_middle, self.times = min_split_read_size, False, {}
+        self.filter_reads = bool(matching_sets)
+        self.trim_file = FileTrimmer.trim_file.__get__(self)
+        self._tick = FileTrimmer._tick.__get__(self)
+
+    def trim(self, batch):
+        import numpy as np
+        from custom_porechop_abi_amd import misc, porechop_abi as P
+        reads = batch.nanopore_reads()
+        sink = io.StringIO()
+        if self.m:
+            P.find_adapters_at_read_ends(reads, self.m, 0, self.E, self.extra, self.thr, self.sc, sink, self.min_trim, 1,
+                                         False, 75.0, 5.0, False, None)
+            P.find_adapters_in_read_middles(reads, self.m, 0, self.mthr, self.good, self.bad, self.sc, sink, 1, False)
+        st = np.array([r.start_trim_amount for r in reads], np.int32)
+        et = np.array([r.end_trim_amount for r in reads], np.int32)
+        cut_off = np.zeros(len(reads) + 1, np.int64)
+        flat = []
+        for i, r in enumerate(reads):
+            rg = misc.positions_to_ranges(sorted(r.middle_trim_positions))
+            cut_off[i + 1] = cut_off[i] + len(rg)
+            for a, b in rg:
+                flat += [a, b]
+        keep = None
+        if self.filter_reads:
+            keep = np.array([bool(r.start_adapter_alignments and r.end_adapter_alignments) for r in reads], np.uint8)
+        return st, et, cut_off, np.array(flat, np.int64), None, keep
+
+
+def _file_worker(rank, world, port, case_name, in_path, out_path, res_path):
+    import torch.distributed as dist
+    from custom_porechop_abi_amd import engine, shards
+    from tests import oracle_lib
+    engine.align = oracle_lib.align_windows
+    engine.best_full_identity = oracle_lib.best_full_identity_windows
+    engine.first_hits = oracle_lib.first_hits_windows
+    engine.middle_scan = oracle_lib.middle_scan_windows
+    dist.init_process_group('gloo', init_method='tcp://127.0.0.1:%d' % port, rank=rank, world_size=world)
+    try:
+        case = next(c for c in G2['cases'] if c['case'] == case_name)
+        o = case['opts']
+        counts = shards.trim_file_sharded(in_path, out_path, 'fastq', o['scoring'], o['end_size'], o['end_threshold'],
+                                          o['extra_end_trim'], o['min_trim_size'], o['middle_threshold'], 10, 100, 1000,
+                                          check_reads=o.get('check_reads', 10000),
+                                          adapter_threshold=o['adapter_threshold'], max_reads=7,
+                                          trimmer_factory=_OracleTrimmer)
+        with open(res_path % rank, 'w') as f:
+            json.dump(counts, f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('gz', [False, True])
+@pytest.mark.parametrize('case_name', ['two_adapter_sets', 'synthetic_default'])
+def test_sharded_file_pipeline_matches_reference(case_name, gz, tmp_path):
+    """shards.trim_file_sharded at world size 2 (gloo): the check-read set search with one MAX
+    all-reduce, record ranges split at record starts (plain input) or every other batch (gzip
+    input), per-rank part files stitched in record order -- the written file == the reference's
+    output for the same reads (G2 decisions through get_fastq, as tests/test_pipeline.py)."""
+    import gzip
+    import torch.multiprocessing as mp
+    from tests.test_pipeline import _expected
+    case = next(c for c in G2['cases'] if c['case'] == case_name)
+    if case['input'] == 'synthetic_reads':
+        records = [tuple(x) for x in G2['synthetic_reads']]
+    else:
+        records = _records(case)
+    text = ''.join('@%s\n%s\n+\n%s\n' % r for r in records)
+    in_path = str(tmp_path / ('in.fastq.gz' if gz else 'in.fastq'))
+    if gz:
+        with gzip.open(in_path, 'wt') as f:
+            f.write(text)
+    else:
+        with open(in_path, 'w') as f:
+            f.write(text)
+    out_path = str(tmp_path / 'out.fastq')
+    res_path = str(tmp_path / 'counts%d.json')
+    mp.spawn(_file_worker, args=(2, _free_port(), case_name, in_path, out_path, res_path), nprocs=2, join=True)
+    counts = [json.load(open(res_path % r)) for r in range(2)]
+    assert counts[0] == counts[1] and counts[0]['reads_in'] == len(records)
+    assert open(out_path).read() == _expected(case, records)
+    assert not [f for f in os.listdir(str(tmp_path)) if f.startswith('.pcabi_part')]
