@@ -33,8 +33,16 @@
 #define PCABI_ROW_FENCE 1
 #endif
 // Packed core: substitution-key quads fetched this many quads ahead (0 = one read per slot).
+// Packed-core substitution keys (LanePacked<.., PD>): PD = 0, one LDS read per row, issued a row
+// ahead -- the end-window buckets (k_align<24>: 3.58 vs 4.07 ms per launch against quads, 74
+// instead of 88 VGPRs, the waves interleave at every row's wait); PD > 0, quads
+// (4 slots) fetched at the column top, PD quads ahead -- the long two-pass buckets, where the
+// per-row reads measured 1.5x slower. PCABI_TAB_PD overrides the end-window default.
 #ifndef PCABI_TAB_PD
-#define PCABI_TAB_PD 1
+#define PCABI_TAB_PD 0
+#endif
+#ifndef PCABI_TAB_PD_LONG
+#define PCABI_TAB_PD_LONG 1
 #endif
 
 #include <stdint.h>
@@ -1017,7 +1025,7 @@ PCABI_HD bool packed_ok(int L, int rpl, const Scoring &s) {
     }
 }
 
-template <int RPL, bool AFFINE, typename LAY = pk::Lay<RPL>>
+template <int RPL, bool AFFINE, typename LAY = pk::Lay<RPL>, int PD = PCABI_TAB_PD>
 struct LanePacked {
     using Y = LAY;
     int32_t G[RPL + 1];    // S keys with tb cleared, plus the gap-open key: G = S + go
@@ -1029,8 +1037,7 @@ struct LanePacked {
     // Last-row scout of the inner columns (column_tail): the best so far as ONE corrected key
     // (score | tag | attributes), its column, and the H-run descriptor at that column; the
     // fields above are materialised from them before the last column (materialize()).
-    int32_t bkey, ls_prev;
-    int bhph, hph_last;    // 2 * (H-run length) + (a diagonal precedes the run)
+    int32_t bkey;
 
     // tab: substitution-key table of this lane's read code, tab(s) = key increment of the
     // diagonal step into slot s (match / mismatch / padding), see pk::fill_sub_table.
@@ -1043,23 +1050,23 @@ struct LanePacked {
         int32_t lv = 0, lh = 0, ls = 0;
         int lslt = LT_D;
         bool lhext = false;
-        // Substitution keys of this column, fetched a quad (4 slots) at a time, PCABI_TAB_PD
+        // Substitution keys of this column, fetched a quad (4 slots) at a time, PD
         // quads ahead of use so the LDS latency hides behind the rows in flight.
         constexpr int NQ = RPL / 4;
         int32_t t[RPL + 2];
-        if (PCABI_TAB_PD > 0) {
+        if (PD > 0) {
 #pragma unroll
-            for (int q = 0; q <= PCABI_TAB_PD && q < NQ; ++q) tab.quad(q, t + 4 * q + 1);
+            for (int q = 0; q <= PD && q < NQ; ++q) tab.quad(q, t + 4 * q + 1);
         }
-        int32_t diag = (Y::start(j - 1 + off) + k_go) + (PCABI_TAB_PD > 0 ? t[1] : tab(1));
+        int32_t diag = (Y::start(j - 1 + off) + k_go) + (PD > 0 ? t[1] : tab(1));
 #pragma unroll
         for (int s = 1; s <= RPL; ++s) {
-            if (PCABI_TAB_PD > 0 && (s & 3) == 1) {
-                const int q = (s - 1) / 4 + PCABI_TAB_PD + 1;
+            if (PD > 0 && (s & 3) == 1) {
+                const int q = (s - 1) / 4 + PD + 1;
                 if (q < NQ) tab.quad(q, t + 4 * q + 1);
             }
             int32_t diag_nx = 0;
-            if (s < RPL) diag_nx = G[s] + (PCABI_TAB_PD > 0 ? t[s + 1] : tab(s + 1));
+            if (s < RPL) diag_nx = G[s] + (PD > 0 ? t[s + 1] : tab(s + 1));
             int32_t hn, vn2, sn;
             bool hext = false, vext = false;
             if (AFFINE) {
@@ -1159,45 +1166,45 @@ struct LanePacked {
 
     // Row-L scout of an inner column, with the reference's rules (S/align/dp_scout.h:175, strict
     // '>' so the first maximum wins; start-state correction V, then H, then S). Affine: the
-    // corrected state is ONE max3 over re-tagged keys -- V (tag 3) beats H (tag 2) beats S
-    // (tag 0) on equal scores, and a higher score always wins -- so the correction costs no
-    // compares. Linear gaps: no correction, the S key's own tb (3 D, 2 V, 1 H) is the type.
+    // corrected state is ONE max over re-tagged keys -- V (tag 3) beats S (tag 0) on equal
+    // scores, a higher score always wins. Linear gaps: no correction, the S key's own tb (3 D,
+    // 2 V, 1 H) is the type.
+    // The H state never wins a scout update here, so neither H nor its trailing run is tracked:
+    // the packed cores need gap costs < 0, and an update at (L, j) means S(L, j) > S(L, j') for
+    // every earlier column j' (the (L, 0) seed's 0 included), while H(L, j) <= max(H(L, j-1),
+    // S(L, j-1)) + max(go, ge) < S(L, j-1) -- so H(L, j) == S(L, j) (the H correction, or an S
+    // that came from H) is impossible there. In a chunk (GATE) the first owned column can
+    // update after an unowned higher one, but then the previous chunk holds a strictly higher
+    // score and wins the merge (sf::chunk_plan); the same holds for the last column's (L, n).
     template <bool GATE = false>
     PCABI_HD void column_tail(int32_t lv, int32_t lh, int32_t ls, int j, bool owned = true) {
+        (void)lh;
         int32_t corr;
-        if (AFFINE) corr = max3i(lv | Y::TB3, (lh & ~Y::TBM) | Y::TB2, ls & ~Y::TBM);
+        if (AFFINE) corr = std::max(lv | Y::TB3, ls & ~Y::TBM);
         else corr = ls;
-        // H-run at (L, j): continues when H extends (affine: lh tb 1) or when it opens from an
-        // S that itself ended in H (tb 1); a new run is preceded by a diagonal iff S was one.
-        const int32_t tsp = ls_prev & Y::TBM;
-        const bool hcont = (AFFINE && (lh & Y::TB1) != 0) || tsp == Y::TB1;
-        const int hph = hcont ? hph_last + 2 : 2 + (tsp == Y::TB3 ? 1 : 0);
         bool upd = corr > (bkey | ((1 << Y::SC_SH) - 1));   // score(corr) > score(bkey)
         if (GATE) upd = upd && owned;
         bkey = upd ? corr : bkey;
         bj = upd ? j : bj;
-        bhph = upd ? hph : bhph;
-        hph_last = hph;
-        ls_prev = ls;
     }
 
-    // Inner-column scout state -> the fields the last column and finish() use.
+    // Inner-column scout state -> the fields the last column and finish() use (no H-state
+    // best, see column_tail: the trailing-H bookkeeping of the last column starts empty).
     PCABI_HD void materialize(int L) {
         const int t = Y::tb(bkey);
         int lt;
         if (bj == 0) lt = LT_NONE;                          // still the (L, 0) seed
-        else if (AFFINE) lt = t == 3 ? LT_V : (t == 2 ? LT_H : LT_D);
+        else if (AFFINE) lt = t == 3 ? LT_V : LT_D;
         else lt = t == 3 ? LT_D : (t == 2 ? LT_V : LT_H);
         bscore = Y::score(bkey);
         bi = L;
         battr = Y::attr(bkey);
         blt = lt;
-        btrail = lt == LT_H ? (bhph >> 1) : 0;             // a V run in row L before the last
-        bprec = lt == LT_H ? (bhph & 1) : 0;               // column is a 1-column trail: 0 here
-        const int tp = Y::tb(ls_prev);
-        slt_last = tp == 0 ? LT_NONE : (tp == 3 ? LT_D : (tp == 2 ? LT_V : LT_H));
-        ht_last = hph_last >> 1;
-        hp_last = hph_last & 1;
+        btrail = 0;                                        // a V run in row L before the last
+        bprec = 0;                                         // column is a 1-column trail: 0 here
+        slt_last = LT_NONE;
+        ht_last = 0;
+        hp_last = 0;
     }
 };
 
@@ -1222,11 +1229,12 @@ PCABI_HD int32_t sub_key(int s, int c, const AdpFn &adp, int off, const Scoring 
 // columns [own_lo, own_hi) may hold the reported end cell, and own_hi < 0 marks the read's last
 // chunk (its last column is the read end); an inner chunk ends on an inner read column, so no
 // last-column cell of it is an alignment end and its tail is reported as not at the read end.
-template <int RPL, bool AFFINE, bool CHUNK = false, typename Y = pk::Lay<RPL>, typename ReadFn, typename TabFn>
+template <int RPL, bool AFFINE, bool CHUNK = false, typename Y = pk::Lay<RPL>, int PD = PCABI_TAB_PD,
+          typename ReadFn, typename TabFn>
 PCABI_HD Best packed_best(ReadFn &rd, int n, const TabFn &tabfn, int L, const Scoring sc, int own_lo, int own_hi,
                           int &n_fin) {
     // tabfn(r) returns a callable row(s) -> substitution key for read code r
-    LanePacked<RPL, AFFINE, Y> st;
+    LanePacked<RPL, AFFINE, Y, PD> st;
     const int off = RPL - L;
     const int32_t neg = Y::sc(pk::neg_score(sc));
     st.k_ge = Y::sc(sc.ge);
@@ -1242,9 +1250,6 @@ PCABI_HD Best packed_best(ReadFn &rd, int n, const TabFn &tabfn, int L, const Sc
     st.neg2 = neg | Y::TB2;
     st.bkey = Y::start(-L);                       // the (L, 0) seed: score 0, c = -L
     st.bj = 0;
-    st.bhph = 0;
-    st.hph_last = 0;
-    st.ls_prev = 0;                                // tb 0: no S before column 1
     int r = rd(1);
     const int hi = own_hi < 0 ? n + 1 : own_hi;
 #pragma unroll 1
@@ -1283,8 +1288,10 @@ template <int RPL, bool AFFINE, bool CHUNK = false, typename ReadFn, typename Ta
 PCABI_HD Result align_lane_packed_long(ReadFn &rd0, ReadFn &rd1, int n, const TabFn0 &tab0, const TabFn1 &tab1,
                                        int L, const Scoring sc, int own_lo = 1, int own_hi = -1) {
     int n_fin;
-    Best b = packed_best<RPL, AFFINE, CHUNK, pk::LayL<RPL, 0>>(rd0, n, tab0, L, sc, own_lo, own_hi, n_fin);
-    const Best bm = packed_best<RPL, AFFINE, CHUNK, pk::LayL<RPL, 1>>(rd1, n, tab1, L, sc, own_lo, own_hi, n_fin);
+    Best b = packed_best<RPL, AFFINE, CHUNK, pk::LayL<RPL, 0>, PCABI_TAB_PD_LONG>(rd0, n, tab0, L, sc, own_lo, own_hi,
+                                                                                 n_fin);
+    const Best bm = packed_best<RPL, AFFINE, CHUNK, pk::LayL<RPL, 1>, PCABI_TAB_PD_LONG>(rd1, n, tab1, L, sc, own_lo,
+                                                                                        own_hi, n_fin);
     b.attr |= bm.attr;
     return finish(b, L, n_fin);
 }

@@ -1,4 +1,12 @@
 #!/bin/bash
-# build/variants/<name>.so = libpcabi built with extra -D flags (perf experiments only)
+# perf_variants/<name>.so = libpcabi with one kernel translation unit (TU, default the packed-core
+# kernels for <= 32 rows: the headline's k_align<24>) rebuilt with extra -D flags; every other
+# object as built by __graft_entry__. Perf experiments only:
+#   [TU=pcabi_k_chunk] tools/build_variant.sh <name> [-DFLAG=...]
+set -e
 name=$1; shift
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared "$@" -o build/variants/$name.so custom_porechop_abi_amd/csrc/pcabi_engine.hip
+mkdir -p perf_variants build/vobj
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -c "$@" -o build/vobj/$name.o custom_porechop_abi_amd/csrc/${TU:-pcabi_k_packed_small}.hip
+objs=$(ls build/*.o | grep -v ${TU:-pcabi_k_packed_small}.o)
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o perf_variants/$name.so build/vobj/$name.o $objs -lz
+echo built perf_variants/$name.so
