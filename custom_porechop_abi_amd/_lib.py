@@ -70,6 +70,8 @@ def lib():
         'pcabi_tile_windows_dev': ([c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p], c_int),
         'pcabi_align_cross_dev': ([c_p, c_p, c_p, c_i64, ctypes.c_int32, c_p, c_int, c_int, c_int, c_int,
                                    c_p, c_i64, c_p], c_int),
+        'pcabi_align_cross_dev_marked': ([c_p, c_p, c_p, c_i64, ctypes.c_int32, c_p, c_int, c_int, c_int, c_int,
+                                          c_p, c_i64, c_p, c_p, c_p], c_int),
         'pcabi_end_trim_dev': ([c_p, c_i64, ctypes.c_int32, c_p, c_i64, ctypes.c_int32, c_i64, c_int,
                                 c_int, c_d, c_int, c_p, c_p, c_p, c_p, c_p], c_int),
         'pcabi_best_full_identity_dev': ([c_p, c_i64, c_i64, ctypes.c_int32, c_p, c_p], c_int),
@@ -112,7 +114,8 @@ def exported_symbols():
             'pcabi_dev_memset', 'pcabi_dev_sync', 'pcabi_dev_copy_async', 'pcabi_stream_create', 'pcabi_stream_destroy',
             'pcabi_stream_sync', 'pcabi_event_create', 'pcabi_event_destroy', 'pcabi_event_record',
             'pcabi_event_elapsed_ms', 'pcabi_adapters_create', 'pcabi_adapters_create_scored', 'pcabi_adapters_destroy',
-            'pcabi_tile_layout', 'pcabi_tile_windows_dev', 'pcabi_align_cross_dev', 'pcabi_end_trim_dev',
+            'pcabi_tile_layout', 'pcabi_tile_windows_dev', 'pcabi_align_cross_dev', 'pcabi_align_cross_dev_marked',
+            'pcabi_end_trim_dev',
             'pcabi_best_full_identity_dev', 'pcabi_first_hits_host', 'pcabi_first_hit_dev', 'pcabi_scan_create',
             'pcabi_scan_destroy', 'pcabi_middle_scan_dev', 'pcabi_middle_scan_host', 'pcabi_middle_seed_runs',
             'pcabi_barcode_call_dev',

@@ -1162,6 +1162,14 @@ int pcabi_align_cross_dev(const uint32_t *tiles, const int64_t *tile_off, const 
                           int64_t n_win, int32_t max_win_len, const pcabi_adapters *adps, int match,
                           int mismatch, int gap_open, int gap_extend, int32_t *out, int64_t out_stride,
                           void *stream) {
+    return pcabi_align_cross_dev_marked(tiles, tile_off, win_len, n_win, max_win_len, adps, match, mismatch,
+                                        gap_open, gap_extend, out, out_stride, stream, nullptr, nullptr);
+}
+
+int pcabi_align_cross_dev_marked(const uint32_t *tiles, const int64_t *tile_off, const int32_t *win_len,
+                                 int64_t n_win, int32_t max_win_len, const pcabi_adapters *adps, int match,
+                                 int mismatch, int gap_open, int gap_extend, int32_t *out, int64_t out_stride,
+                                 void *stream, void *ev_begin, void *ev_end) {
     if (!adps || n_win < 0 || (n_win > 0 && (!tiles || !tile_off))) return fail(PCABI_E_ARG, "bad arguments");
     if (n_win == 0) return 0;
     {
@@ -1210,10 +1218,14 @@ int pcabi_align_cross_dev(const uint32_t *tiles, const int64_t *tile_off, const 
         p.adp_id = adps->id[b];
         p.n_adp = adps->count[b];
         p.rt = adps->rt[b];
-        if (int rc = dispatch(b, p, affine, fj.at(k), bucket_packed_ok(b, adps->lens[b], p.sc))) {
+        const hipStream_t st = fj.at(k);
+        // the largest bucket runs on the caller's stream (k == 0): the optional events bracket it
+        if (k == 0 && ev_begin) HIP_TRY(hipEventRecord((hipEvent_t)ev_begin, st));
+        if (int rc = dispatch(b, p, affine, st, bucket_packed_ok(b, adps->lens[b], p.sc))) {
             (void)fj.end();
             return rc;
         }
+        if (k == 0 && ev_end) HIP_TRY(hipEventRecord((hipEvent_t)ev_end, st));
     }
     if (int rc = fj.end()) return rc;
     HIP_TRY(hipGetLastError());

@@ -169,6 +169,15 @@ int pcabi_align_cross_dev(const uint32_t *tiles, const int64_t *tile_off, const 
                           int64_t n_win, int32_t max_win_len, const pcabi_adapters *adps,
                           int match, int mismatch, int gap_open, int gap_extend,
                           int32_t *out, int64_t out_stride, void *stream);
+/* Same, and records ev_begin / ev_end (pcabi_event_create; either may be NULL) on `stream`
+ * around the launch of the table's largest bucket (adapters x rows), which runs on `stream`
+ * while the other buckets run beside it on the device's side streams: the events time that
+ * kernel inside a full cross product (bench.py's roofline). */
+int pcabi_align_cross_dev_marked(const uint32_t *tiles, const int64_t *tile_off, const int32_t *win_len,
+                                 int64_t n_win, int32_t max_win_len, const pcabi_adapters *adps,
+                                 int match, int mismatch, int gap_open, int gap_extend,
+                                 int32_t *out, int64_t out_stride, void *stream, void *ev_begin,
+                                 void *ev_end);
 
 /*
  * End-trim decision epilogue (porechop_abi/nanopore_read.py:175-217), device pointers:

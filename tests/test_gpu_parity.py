@@ -156,7 +156,9 @@ def test_long_reads_middle_shape(gpu_lib):
 def test_device_abi_tiled_cross(gpu_lib, scheme, scored):
     """Device-pointer ABI: pcabi_tile_layout -> pcabi_tile_windows_dev -> pcabi_align_cross_dev,
     with ragged windows (empty, 1 bp, several kb) and more than one tile. scored: the table is
-    built for the scoring, so small register buckets are merged (extra padding rows)."""
+    built for the scoring, so small register buckets are merged (extra padding rows), and the
+    call goes through pcabi_align_cross_dev_marked on a stream of its own (events around the
+    largest bucket)."""
     from custom_porechop_abi_amd import _lib, engine
     L, vp = gpu_lib, ctypes.c_void_p
     reads, adps = _case_set(31, 700, 7, 3000, 64)
@@ -203,8 +205,24 @@ def test_device_abi_tiled_cross(gpu_lib, scheme, scored):
     try:
         mq = int(np.diff(toff).max() // 256)
         _lib.check(L.pcabi_tile_windows_dev(d_codes, d_off, d_len, n, d_toff, mq, d_tiles, None), 'tile')
-        _lib.check(L.pcabi_align_cross_dev(d_tiles, d_toff, d_len, n, int(lens.max()), tab, *scheme, d_out,
-                                           stride, None), 'align')
+        if scored:
+            # the marked entry point: events around the largest bucket's launch, on the stream
+            st, e0, e1 = vp(), vp(), vp()
+            _lib.check(L.pcabi_stream_create(ctypes.byref(st)), 'stream')
+            _lib.check(L.pcabi_event_create(ctypes.byref(e0)), 'event')
+            _lib.check(L.pcabi_event_create(ctypes.byref(e1)), 'event')
+            _lib.check(L.pcabi_align_cross_dev_marked(d_tiles, d_toff, d_len, n, int(lens.max()), tab, *scheme,
+                                                      d_out, stride, st, e0, e1), 'align')
+            _lib.check(L.pcabi_stream_sync(st), 'sync')
+            ms = ctypes.c_float()
+            _lib.check(L.pcabi_event_elapsed_ms(ctypes.byref(ms), e0, e1), 'elapsed')
+            assert ms.value > 0.0
+            for e in (e0, e1):
+                L.pcabi_event_destroy(e)
+            L.pcabi_stream_destroy(st)
+        else:
+            _lib.check(L.pcabi_align_cross_dev(d_tiles, d_toff, d_len, n, int(lens.max()), tab, *scheme, d_out,
+                                               stride, None), 'align')
         _lib.check(L.pcabi_dev_sync(), 'sync')
         got = np.zeros((8, stride), np.int32)
         _lib.check(L.pcabi_dev_d2h(got.ctypes.data_as(vp), d_out, got.nbytes), 'd2h')
