@@ -73,8 +73,13 @@ bool middle_filter_on() {
 
 // Owned end columns per chunk of the middle scan's candidate DP (pcabi_dp.h sf::chunk_plan):
 // short enough that the longest read's chunks finish with the rest, long enough that the D-column
-// lead-in of each chunk stays a few percent.
+// lead-in of each chunk stays a few percent. A round with few candidates (later rounds: the
+// reads that just hit) takes shorter chunks, down to kChunkColsMin, while the task list stays
+// within kChunkTasks: a launch of a few waves runs as long as its longest chunk, one lane per
+// column, so the chunk length is its latency.
 constexpr int kChunkCols = 512;
+constexpr int kChunkColsMin = 64;
+constexpr int64_t kChunkTasks = 65536;
 
 // PCABI_DEBUG=1: the middle scan prints its candidate counts per round to stderr.
 const bool g_debug = [] {
@@ -88,6 +93,19 @@ int middle_seed_mode() {
     const char *e = std::getenv("PCABI_MIDDLE_SEEDS");
     if (!e || !e[0]) return 1;
     return e[0] == '0' ? 0 : (e[0] == '2' ? 2 : 1);
+}
+
+// Seeded rounds plan their candidate DP on the device (PCABI_MIDDLE_DEVPLAN=0: on the host).
+bool middle_devplan_on() {
+    const char *e = std::getenv("PCABI_MIDDLE_DEVPLAN");
+    return !(e && e[0] == '0');
+}
+
+// Device planning aims at this many waves per candidate-DP round (4 per SIMD): the chunk length
+// is the longest of 512, 256, 128, 64 owned columns that still reaches it.
+int64_t middle_plan_waves() {
+    const char *e = std::getenv("PCABI_MIDDLE_PLAN_WAVES");
+    return (e && e[0]) ? std::max<int64_t>(1, std::atoll(e)) : 4096;
 }
 
 // ---- decision epilogues --------------------------------------------------------------------
@@ -283,6 +301,176 @@ __global__ __launch_bounds__(256) void k_mask(uint8_t *codes, const int64_t *win
     const int64_t h = blockIdx.x;
     const int64_t base = win_off[mwin[h]];
     for (int64_t i = ms[h] + threadIdx.x; i < me[h]; i += 256) codes[base + i] = 4;
+}
+
+// ---- device-planned candidate DP (middle scan, seeded rounds) --------------------------------
+// The seeds leave the candidate pairs on the device as unordered keys (adapter << 32 | window).
+// k_plan_count counts each adapter's tasks for the four chunk lengths, the host lays the waves
+// out (one adapter per wave, adapters in bucket order: n_adp numbers, not tasks), k_plan_place
+// writes the task slots, the DP runs per bucket, and k_merge_* pick per candidate the first chunk
+// (read order) with the largest score, then per window the first adapter (list order) whose
+// full identity is not below the threshold -- the host path's rules (filtered_first_hits).
+constexpr int kPlanC = 4;   // chunk lengths 64 << c, c = 0..3
+
+__device__ __forceinline__ int plan_tasks(int len, int span, int c) {
+    if (span < 0) return 1;                          // whole windows
+    const int C = 64 << c;
+    return (len + C - 1) / C;                        // sf::chunk_plan's chunk count
+}
+
+__device__ __forceinline__ bool plan_valid(int64_t key, const int32_t *v_len, const int32_t *start) {
+    const int32_t a = (int32_t)(key >> 32), k = (int32_t)(key & 0xFFFFFFFF);
+    return v_len[k] > 0 && (!start || a >= start[k]);
+}
+
+// Wave helpers (every lane of the wave takes part): sum, inclusive scan.
+__device__ __forceinline__ int wave_sum(int x) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d);
+    return x;
+}
+__device__ __forceinline__ int wave_incl_scan(int x) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+    }
+    return x;
+}
+
+// Candidates of one adapter are typically many (the reads' own adapter), so the per-adapter
+// counters are updated once per (wave, adapter): the lanes of one adapter are reduced first.
+__global__ __launch_bounds__(256) void k_plan_count(const int64_t *cand, int64_t nc, const int32_t *v_len,
+                                                    const int32_t *start, const int32_t *span, int32_t *adp_tasks) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int64_t key = i < nc ? cand[i] : 0;
+    const bool active = i < nc && plan_valid(key, v_len, start);
+    const int32_t a = active ? (int32_t)(key >> 32) : -1;
+    int nt[kPlanC] = {0, 0, 0, 0};
+    if (active) {
+        const int32_t k = (int32_t)(key & 0xFFFFFFFF);
+#pragma unroll
+        for (int c = 0; c < kPlanC; ++c) nt[c] = plan_tasks(v_len[k], span[a], c);
+    }
+    uint64_t pending = __ballot(active);
+    while (pending) {                                // wave-uniform
+        const int leader = __ffsll((unsigned long long)pending) - 1;
+        const int32_t a0 = __shfl(a, leader);
+        const bool mine = active && a == a0;
+#pragma unroll
+        for (int c = 0; c < kPlanC; ++c) {
+            const int sum = wave_sum(mine ? nt[c] : 0);
+            if (lane == leader) atomicAdd(&adp_tasks[a0 * kPlanC + c], sum);
+        }
+        pending &= ~__ballot(mine);
+    }
+}
+
+// Task slots: adapter a's tasks fill slots [wave_off[a] * 64, ...) in any order (a slot's result
+// depends only on its own task); idle slots keep task_win = -1. cidx[a]: the chunk length of a's
+// bucket (64 << cidx).
+__global__ __launch_bounds__(256) void k_plan_place(const int64_t *cand, int64_t nc, const int32_t *v_len,
+                                                    const int32_t *start, const int32_t *span, const int32_t *cidx,
+                                                    const int64_t *wave_off, int32_t *fill, int32_t *tw, int32_t *to,
+                                                    int4 *tck, int32_t *tcand) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int64_t key = i < nc ? cand[i] : 0;
+    const bool active = i < nc && plan_valid(key, v_len, start);
+    const int32_t a = active ? (int32_t)(key >> 32) : -1, k = (int32_t)(key & 0xFFFFFFFF);
+    int n = 0, D = -1, c = 0, nt = 0;
+    if (active) {
+        n = v_len[k];
+        D = span[a];
+        c = cidx[a];
+        nt = plan_tasks(n, D, c);
+    }
+    int64_t base = 0;
+    uint64_t pending = __ballot(active);
+    while (pending) {                                // wave-uniform: one atomic per (wave, adapter)
+        const int leader = __ffsll((unsigned long long)pending) - 1;
+        const int32_t a0 = __shfl(a, leader);
+        const bool mine = active && a == a0;
+        const int x = mine ? nt : 0;
+        const int incl = wave_incl_scan(x);
+        const int total = __shfl(incl, 63);
+        int b0 = 0;
+        if (lane == leader) b0 = atomicAdd(&fill[a0], total);
+        b0 = __shfl(b0, leader);
+        if (mine) base = wave_off[a0] * 64 + b0 + (incl - x);
+        pending &= ~__ballot(mine);
+    }
+    if (!active) return;
+    const int C = 64 << c;
+    for (int t = 0; t < nt; ++t) {
+        const int64_t q = base + t;
+        int4 ck = make_int4(0, 0, 0, 0);
+        if (D >= 0) {                                // sf::chunk_plan, chunk t
+            const int lo = 1 + t * C, hi = lo + C;
+            const int st = max(0, lo - 1 - D);
+            ck = hi > n ? make_int4(st, n - st, lo - st, -1) : make_int4(st, hi - 1 - st, lo - st, hi - st);
+        }
+        tw[q] = k;
+        to[q] = (int32_t)q;
+        tck[q] = ck;
+        tcand[q] = (int32_t)i;
+    }
+}
+
+// Merge key of a task: larger score first, then the earlier chunk. Chunks are told apart by their
+// first owned column (start + own_lo, unique per chunk), not by their start: near the read
+// start several chunks begin at offset 0.
+__device__ __forceinline__ uint64_t merge_key(int32_t score, int4 ck) {
+    return ((uint64_t)((uint32_t)score ^ 0x80000000u) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)(ck.x + ck.z));
+}
+
+__global__ __launch_bounds__(256) void k_merge_best(const int32_t *tw, const int4 *tck, const int32_t *tcand,
+                                                    const int32_t *res, int64_t slots, unsigned long long *best) {
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (q >= slots || tw[q] < 0) return;
+    atomicMax(&best[tcand[q]], (unsigned long long)merge_key(res[4 * slots + q], tck[q]));
+}
+
+// pass 0: per window the smallest adapter whose winning chunk reaches the threshold (atomicMin);
+// pass 1: that candidate writes the window's hit (rs / re back to whole-window offsets).
+__global__ __launch_bounds__(256) void k_merge_hit(const int64_t *cand, const int32_t *tw, const int4 *tck,
+                                                   const int32_t *tcand, const int32_t *res, int64_t slots,
+                                                   const unsigned long long *best, double thr, int pass,
+                                                   int32_t *hit_a, int32_t *hb, int64_t n) {
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (q >= slots || tw[q] < 0) return;
+    const int32_t ci = tcand[q];
+    const int4 ck = tck[q];
+    const int32_t st = ck.x;
+    if ((unsigned long long)merge_key(res[4 * slots + q], ck) != best[ci]) return;
+    const int rs = res[0 * slots + q];
+    const int m = res[5 * slots + q], l2 = res[7 * slots + q];
+    const double full = rs == -1 ? 0.0 : pcabi::pid6(m, l2);
+    if (full < thr) return;                          // NaN goes on, as the reference's loop
+    const int32_t k = tw[q], a = (int32_t)(cand[ci] >> 32);
+    if (pass == 0) {
+        atomicMin(&hit_a[k], a);
+    } else if (hit_a[k] == a) {
+        hb[0 * n + k] = a;
+        hb[1 * n + k] = rs + st;
+        hb[2 * n + k] = res[1 * slots + q] + st;
+        hb[3 * n + k] = m;
+        hb[4 * n + k] = l2;
+    }
+}
+
+// The windows that hit, compacted (window, adapter, rs, re, m, l2), in any order.
+__global__ __launch_bounds__(256) void k_hits_compact(const int32_t *hb, int64_t n, int32_t *out,
+                                                      unsigned int *cnt) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= n || hb[k] < 0) return;
+    const unsigned int j = atomicAdd(cnt, 1u);
+    int32_t *o = out + 6 * (int64_t)j;
+    o[0] = (int32_t)k;
+#pragma unroll
+    for (int f = 0; f < 5; ++f) o[1 + f] = hb[f * n + k];
 }
 
 // ---- launch plumbing -------------------------------------------------------------------------
@@ -507,13 +695,14 @@ void destroy(State *s);
 int bounds(State *s, const void *adps_key, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hlen,
            int32_t n_adp, const std::vector<int> &fb_rows, const uint8_t *codes, const int64_t *v_off,
            const int32_t *v_len, int64_t n, const pcabi::Scoring &sc, double threshold, int mode, int16_t *s16,
-           std::vector<int64_t> *cands, hipStream_t st);
+           std::vector<int64_t> *cands, const int64_t **dcands, int64_t *n_dcands, hipStream_t st);
 }  // namespace pcabi_seed
 
 struct pcabi_scan {
     const pcabi_adapters *adps = nullptr;
     DeviceBuf tiles, toff, res, hits, idx, start, soff, slen, mwin, ms, me;
     DeviceBuf s16, tw, to, wa, pres, tck;   // score filter + candidate pairs (chunks)
+    DeviceBuf pspan, ptasks, pfill, pwoff, pcidx, pcand, pbest, phit, phb, plist, pcnt;   // device planning
     pcabi_seed::State *seed = nullptr; // seeded round-1 bounds (pcabi_seed.hip)
 };
 
@@ -1248,7 +1437,9 @@ int pcabi_scan_create(const pcabi_adapters *adps, pcabi_scan **out) {
 void pcabi_scan_destroy(pcabi_scan *s) {
     if (!s) return;
     for (DeviceBuf *b : {&s->tiles, &s->toff, &s->res, &s->hits, &s->idx, &s->start, &s->soff, &s->slen,
-                         &s->mwin, &s->ms, &s->me, &s->s16, &s->tw, &s->to, &s->wa, &s->pres, &s->tck})
+                         &s->mwin, &s->ms, &s->me, &s->s16, &s->tw, &s->to, &s->wa, &s->pres, &s->tck,
+                         &s->pspan, &s->ptasks, &s->pfill, &s->pwoff, &s->pcidx, &s->pcand, &s->pbest, &s->phit, &s->phb,
+                         &s->plist, &s->pcnt})
         if (b->p) (void)hipFree(b->p);
     if (s->seed) pcabi_seed::destroy(s->seed);
     delete s;
@@ -1271,9 +1462,200 @@ namespace {
 // in every later round on the masked reads (seeded: in, round 1 used them; out, this call did),
 // where the hits just masked no longer seed their adapter. make_tiles() lays out this round's
 // tiles, which only the filter reads.
+// Seeded round with the candidates on the device (dcand: nc unordered keys a << 32 | window):
+// plans, runs and merges the candidate DP on the device (kernels above) and fills hb (5 x n, the
+// k_first_hit layout) from the windows that hit, the only data that comes back. d_start: this
+// round's first adapter per window (device), nullptr in round 1. max_len: longest window.
+int device_plan_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_off, const int32_t *v_len, int64_t n,
+                     int32_t max_len, const int32_t *d_start, const int64_t *dcand, int64_t nc,
+                     const pcabi::Scoring &scr, double threshold, std::vector<int32_t> &hb, hipStream_t st) {
+    const pcabi_adapters *adps = sc->adps;
+    const int32_t n_adp = adps->n_adp;
+    hb.assign((size_t)(5 * n), 0);
+    for (int64_t k = 0; k < n; ++k) hb[k] = -1;
+    if (nc == 0) return 1;
+    // per adapter: the chunk lead-in D of its bucket's plan (-1: whole windows), as the host plan
+    std::vector<int32_t> span((size_t)n_adp, -1);
+    std::vector<char> bchunk(kNumBuckets, 0);
+    std::vector<int32_t> bspan(kNumBuckets, 0);       // largest D of a chunked bucket
+    for (int b = 0; b < kNumBuckets; ++b) {
+        const int nb = adps->count[b];
+        if (!nb) continue;
+        bool chunk = chunkable(b, bucket_packed_ok(b, adps->lens[b], scr));
+        std::vector<int> sp((size_t)nb, -1);
+        for (int kk = 0; chunk && kk < nb; ++kk) {
+            const int L = adps->lens[b][kk];
+            sp[kk] = pcabi::sf::chunk_span(L, pcabi::sf::filter_threshold(L, threshold, scr), scr);
+            if (sp[kk] < 0) chunk = false;
+        }
+        bchunk[b] = chunk;
+        if (chunk)
+            for (int kk = 0; kk < nb; ++kk) {
+                span[adps->ids[b][kk]] = sp[kk];
+                bspan[b] = std::max(bspan[b], sp[kk]);
+            }
+    }
+    if (int rc = sc->pspan.ensure(sizeof(int32_t) * n_adp)) return rc;
+    if (int rc = sc->ptasks.ensure(sizeof(int32_t) * n_adp * kPlanC)) return rc;
+    if (int rc = sc->pfill.ensure(sizeof(int32_t) * n_adp)) return rc;
+    if (int rc = sc->pwoff.ensure(sizeof(int64_t) * n_adp)) return rc;
+    if (int rc = sc->pcidx.ensure(sizeof(int32_t) * n_adp)) return rc;
+    HIP_TRY(hipMemcpyAsync(sc->pspan.p, span.data(), sizeof(int32_t) * n_adp, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(sc->ptasks.p, 0, sizeof(int32_t) * n_adp * kPlanC, st));
+    const unsigned gc = (unsigned)((nc + 255) / 256);
+    hipLaunchKernelGGL(k_plan_count, dim3(gc), dim3(256), 0, st, dcand, nc, v_len, d_start,
+                       (const int32_t *)sc->pspan.p, (int32_t *)sc->ptasks.p);
+    HIP_TRY(hipGetLastError());
+    std::vector<int32_t> tasks((size_t)n_adp * kPlanC);
+    HIP_TRY(hipMemcpyAsync(tasks.data(), sc->ptasks.p, sizeof(int32_t) * tasks.size(), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    // chunk length per bucket (the buckets run side by side): the longest whose waves reach the
+    // target -- a launch of few waves runs as long as its longest chunk -- else the shortest
+    const int64_t target = middle_plan_waves();
+    std::vector<int32_t> cidx((size_t)n_adp, 0);
+    std::vector<int> bc(kNumBuckets, 0);
+    for (int b = 0; b < kNumBuckets; ++b) {
+        if (!adps->count[b] || !bchunk[b]) continue;
+        for (int cc = kPlanC - 1; cc > 0; --cc) {
+            int64_t w = 0;
+            for (int32_t a : adps->ids[b]) w += (tasks[(size_t)a * kPlanC + cc] + 63) / 64;
+            if (w >= target) {
+                bc[b] = cc;
+                break;
+            }
+        }
+        for (int32_t a : adps->ids[b]) cidx[a] = bc[b];
+    }
+    // wave layout: buckets in order, a bucket's adapters in order, one adapter per wave
+    std::vector<int64_t> woff((size_t)n_adp, 0);
+    std::vector<int32_t> wa;
+    std::vector<int> nb_used;
+    std::vector<int32_t> nb_maxcols;
+    std::vector<int64_t> wave0;
+    for (int b = 0; b < kNumBuckets; ++b) {
+        const int nb = adps->count[b];
+        if (!nb) continue;
+        const size_t w_before = wa.size();
+        for (int kk = 0; kk < nb; ++kk) {
+            const int32_t a = adps->ids[b][kk];
+            woff[a] = (int64_t)wa.size();
+            const int64_t nw = (tasks[(size_t)a * kPlanC + bc[b]] + 63) / 64;
+            for (int64_t w = 0; w < nw; ++w) wa.push_back(kk);
+        }
+        if (wa.size() == w_before) continue;
+        nb_used.push_back(b);
+        nb_maxcols.push_back(bchunk[b] ? std::min<int32_t>(max_len, (64 << bc[b]) + bspan[b] + 1) : max_len);
+        wave0.push_back((int64_t)w_before);
+    }
+    wave0.push_back((int64_t)wa.size());
+    const int64_t slots = (int64_t)wa.size() * 64;
+    if (g_debug) {
+        std::string d;
+        for (size_t k = 0; k < nb_used.size(); ++k)
+            d += " rpl" + std::to_string(kBuckets[nb_used[k]].rpl) + ":" + std::to_string(wave0[k + 1] - wave0[k]) +
+                 "w/c" + std::to_string(64 << bc[nb_used[k]]);
+        std::fprintf(stderr, "[pcabi] middle device plan: %lld candidates, waves per bucket:%s\n", (long long)nc,
+                     d.c_str());
+    }
+    if (slots == 0) return 1;
+    if (int rc = sc->tw.ensure(sizeof(int32_t) * slots)) return rc;
+    if (int rc = sc->to.ensure(sizeof(int32_t) * slots)) return rc;
+    if (int rc = sc->tck.ensure(sizeof(int4) * slots)) return rc;
+    if (int rc = sc->pcand.ensure(sizeof(int32_t) * slots)) return rc;
+    if (int rc = sc->wa.ensure(sizeof(int32_t) * wa.size())) return rc;
+    if (int rc = sc->pres.ensure(sizeof(int32_t) * PCABI_NFIELDS * (size_t)slots)) return rc;
+    if (int rc = sc->pbest.ensure(sizeof(unsigned long long) * nc)) return rc;
+    if (int rc = sc->phit.ensure(sizeof(int32_t) * n)) return rc;
+    if (int rc = sc->phb.ensure(sizeof(int32_t) * 5 * n)) return rc;
+    if (int rc = sc->plist.ensure(sizeof(int32_t) * 6 * n)) return rc;
+    if (int rc = sc->pcnt.ensure(sizeof(unsigned int))) return rc;
+    HIP_TRY(hipMemcpyAsync(sc->pwoff.p, woff.data(), sizeof(int64_t) * n_adp, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(sc->pcidx.p, cidx.data(), sizeof(int32_t) * n_adp, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(sc->wa.p, wa.data(), sizeof(int32_t) * wa.size(), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)sc->tw.p, -1, (size_t)slots, st));
+    HIP_TRY(hipMemsetAsync(sc->pfill.p, 0, sizeof(int32_t) * n_adp, st));
+    hipLaunchKernelGGL(k_plan_place, dim3(gc), dim3(256), 0, st, dcand, nc, v_len, d_start,
+                       (const int32_t *)sc->pspan.p, (const int32_t *)sc->pcidx.p, (const int64_t *)sc->pwoff.p,
+                       (int32_t *)sc->pfill.p,
+                       (int32_t *)sc->tw.p, (int32_t *)sc->to.p, (int4 *)sc->tck.p, (int32_t *)sc->pcand.p);
+    HIP_TRY(hipGetLastError());
+    KParams p{};
+    p.codes = codes;
+    p.win_off = v_off;
+    p.win_len = v_len;
+    p.n_win = n;
+    p.out = (int32_t *)sc->pres.p;
+    p.out_stride = slots;
+    p.sc = scr;
+    {
+        ForkJoin fj;
+        if (int rc = fj.begin(st, nb_used.size())) return rc;
+        for (size_t k = 0; k < nb_used.size(); ++k) {
+            const int b = nb_used[k];
+            p.adp_pad = adps->pad[b];
+            p.adp_len = adps->len[b];
+            p.adp_id = adps->id[b];
+            p.n_adp = adps->count[b];
+            p.task_win = (const int32_t *)sc->tw.p + wave0[k] * 64;
+            p.task_out = (const int32_t *)sc->to.p + wave0[k] * 64;
+            p.wave_adp = (const int32_t *)sc->wa.p + wave0[k];
+            p.task_chunk = (const int4 *)sc->tck.p + wave0[k] * 64;
+            p.n_waves = wave0[k + 1] - wave0[k];
+            p.rt = adps->rt[b];
+            p.max_cols = nb_maxcols[k];
+            int rc;
+            if (bchunk[b]) {
+                rc = dispatch_chunk(b, p, scr.go != scr.ge, fj.at(k));
+            } else {
+                p.task_chunk = nullptr;   // whole windows
+                rc = dispatch(b, p, scr.go != scr.ge, fj.at(k), bucket_packed_ok(b, adps->lens[b], scr));
+            }
+            if (rc) {
+                (void)fj.end();
+                return rc;
+            }
+        }
+        if (int rc = fj.end()) return rc;
+    }
+    HIP_TRY(hipGetLastError());
+    const unsigned gs = (unsigned)((slots + 255) / 256), gn = (unsigned)((n + 255) / 256);
+    HIP_TRY(hipMemsetAsync(sc->pbest.p, 0, sizeof(unsigned long long) * nc, st));
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)sc->phit.p, INT32_MAX, (size_t)n, st));
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)sc->phb.p, -1, (size_t)n, st));
+    HIP_TRY(hipMemsetAsync(sc->pcnt.p, 0, sizeof(unsigned int), st));
+    const int32_t *tw = (const int32_t *)sc->tw.p, *tcand = (const int32_t *)sc->pcand.p;
+    const int4 *tck = (const int4 *)sc->tck.p;
+    const int32_t *res = (const int32_t *)sc->pres.p;
+    hipLaunchKernelGGL(k_merge_best, dim3(gs), dim3(256), 0, st, tw, tck, tcand, res, slots,
+                       (unsigned long long *)sc->pbest.p);
+    for (int pass = 0; pass < 2; ++pass)
+        hipLaunchKernelGGL(k_merge_hit, dim3(gs), dim3(256), 0, st, dcand, tw, tck, tcand, res, slots,
+                           (const unsigned long long *)sc->pbest.p, threshold, pass, (int32_t *)sc->phit.p,
+                           (int32_t *)sc->phb.p, n);
+    hipLaunchKernelGGL(k_hits_compact, dim3(gn), dim3(256), 0, st, (const int32_t *)sc->phb.p, n,
+                       (int32_t *)sc->plist.p, (unsigned int *)sc->pcnt.p);
+    HIP_TRY(hipGetLastError());
+    unsigned int nh = 0;
+    HIP_TRY(hipMemcpyAsync(&nh, sc->pcnt.p, sizeof(nh), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if ((int64_t)nh > n) return fail(PCABI_E_DEVICE, "middle scan: hit count overflow");
+    std::vector<int32_t> list((size_t)6 * nh);
+    if (nh) {
+        HIP_TRY(hipMemcpyAsync(list.data(), sc->plist.p, sizeof(int32_t) * list.size(), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    for (unsigned int j = 0; j < nh; ++j) {
+        const int32_t *o = list.data() + 6 * (size_t)j;
+        const int64_t k = o[0];
+        for (int f = 0; f < 5; ++f) hb[(size_t)f * n + k] = o[1 + f];
+    }
+    return 1;
+}
+
 template <typename MakeTiles>
 int filtered_first_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_off, const int32_t *v_len,
-                        const int32_t *h_len, int64_t n, const int32_t *h_start, const int32_t *reads,
+                        const int32_t *h_len, int64_t n, const int32_t *h_start, const int32_t *d_start,
+                        int32_t max_len, const int32_t *reads,
                         std::vector<int16_t> &h16, int64_t n1, const std::vector<int32_t> &pos1,
                         const pcabi::Scoring &scr, double threshold, std::vector<int32_t> &hb, bool &seeded,
                         const MakeTiles &make_tiles, hipStream_t st) {
@@ -1311,10 +1693,20 @@ int filtered_first_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_o
             for (int b = 0; b < kNumBuckets; ++b)
                 if (kBuckets[b].kind != STRIPED)
                     for (int32_t id : adps->ids[b]) rows[id] = kBuckets[b].rpl;
+            // every adapter seeded (no striped one): the candidates stay on the device
+            const bool devplan = middle_devplan_on() && adps->count[kStripedBucket] == 0;
+            const int64_t *dcand = nullptr;
+            int64_t ndc = 0;
             got = pcabi_seed::bounds(sc->seed, adps, adps->hcodes.data(), adps->hoff.data(), adps->hlen.data(),
                                      n_adp, rows, codes, v_off, v_len, n, scr, threshold, h_start ? 2 : mode,
-                                     (int16_t *)sc->s16.p, &seed_cands, st);
+                                     (int16_t *)sc->s16.p, devplan ? nullptr : &seed_cands,
+                                     devplan ? &dcand : nullptr, &ndc, st);
             if (got < 0) return got;
+            if (got > 0 && devplan) {
+                seeded = true;
+                return device_plan_hits(sc, codes, v_off, v_len, n, max_len, h_start ? d_start : nullptr, dcand, ndc,
+                                        scr, threshold, hb, st);
+            }
         }
         if (h_start && !got) return fail(PCABI_E_DEVICE, "middle scan: seeds stopped applying after round 1");
         seeded = got > 0;
@@ -1399,6 +1791,17 @@ int filtered_first_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_o
     std::vector<char> nb_chunked;
     std::vector<int32_t> nb_maxcols;                // longest window / chunk per bucket (striped scratch)
     std::vector<int64_t> wave0;
+    // chunk length: the shortest (power of two >= kChunkColsMin) whose task count stays within
+    // kChunkTasks (the count over all candidates, chunked or not -- a bound)
+    int chunk_cols = kChunkCols;
+    for (int c = kChunkColsMin; c < kChunkCols; c *= 2) {
+        int64_t tasks = 0;
+        for (int64_t t = 0; t < n_task && tasks <= kChunkTasks; ++t) tasks += (h_len[cand_w[t]] + c - 1) / c;
+        if (tasks <= kChunkTasks) {
+            chunk_cols = c;
+            break;
+        }
+    }
     for (int b = 0; b < kNumBuckets; ++b) {
         const int nb = adps->count[b];
         if (!nb) continue;
@@ -1430,7 +1833,7 @@ int filtered_first_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_o
             for (int64_t t = first[a]; t < first[a + 1]; ++t) {
                 const int32_t k = cand_w[t];
                 if (chunk)
-                    pcabi::sf::chunk_plan(h_len[k], span[kk], kChunkCols, [&](const pcabi::sf::Chunk &c) {
+                    pcabi::sf::chunk_plan(h_len[k], span[kk], chunk_cols, [&](const pcabi::sf::Chunk &c) {
                         add(t, k, make_int4(c.start, c.len, c.own_lo, c.own_hi));
                     });
                 else
@@ -1450,6 +1853,14 @@ int filtered_first_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_o
     }
     wave0.push_back((int64_t)wa.size());
     const int64_t n_run = (int64_t)task_cand.size();
+    if (g_debug) {
+        std::string s;
+        for (size_t k = 0; k < nb_used.size(); ++k)
+            s += " rpl" + std::to_string(kBuckets[nb_used[k]].rpl) + ":" + std::to_string(wave0[k + 1] - wave0[k]) +
+                 "w/" + std::to_string(nb_maxcols[k]) + "c";
+        std::fprintf(stderr, "[pcabi] middle tasks %lld (chunks of %d), waves per bucket:%s\n", (long long)n_run,
+                     chunk_cols, s.c_str());
+    }
     if (int rc = sc->pres.ensure(sizeof(int32_t) * PCABI_NFIELDS * (size_t)n_run)) return rc;
     if (int rc = sc->tw.ensure(sizeof(int32_t) * tw.size())) return rc;
     if (int rc = sc->to.ensure(sizeof(int32_t) * to.size())) return rc;
@@ -1608,6 +2019,7 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
         int filt = 0;
         if (middle_filter_on() && (round == 0 || filt_round1)) {
             filt = filtered_first_hits(sc, codes, v_off, v_len, lens.data(), n, round == 0 ? nullptr : nxt_start.data(),
+                                       round == 0 ? nullptr : (const int32_t *)sc->start.p, max_len,
                                        cur.data(), h16, n_win, pos1,
                                        pcabi::Scoring{match, mismatch, gap_open, gap_extend}, threshold, hb, seeded,
                                        make_tiles, st);

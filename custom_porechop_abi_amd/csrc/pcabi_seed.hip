@@ -544,12 +544,13 @@ void launch_band(const State *s, int E, int32_t cnt, int c, const uint8_t *codes
 // adapter is not filtered). mode: 1 use seeds when the cost model prefers them, 2 whenever they
 // apply. Returns 1 when done, 0 when seeds do not apply (the caller runs the score filter), < 0
 // on error. Done: cands != nullptr receives the filtered pairs whose bound reaches their
-// threshold, as sorted (a << 32 | read) keys (no bound array leaves the device); otherwise s16
-// (int16, a * n + read) holds every bound (-8192: no seed).
+// threshold, as sorted (a << 32 | read) keys (no bound array leaves the device); dcands !=
+// nullptr receives the same keys unordered in device memory (valid until the next call) and
+// n_dcands their count; otherwise s16 (int16, a * n + read) holds every bound (-8192: no seed).
 int bounds(State *s, const void *adps_key, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hlen,
            int32_t n_adp, const std::vector<int> &fb_rows, const uint8_t *codes, const int64_t *v_off,
            const int32_t *v_len, int64_t n, const pcabi::Scoring &sc, double threshold, int mode, int16_t *s16,
-           std::vector<int64_t> *cands, hipStream_t st) {
+           std::vector<int64_t> *cands, const int64_t **dcands, int64_t *n_dcands, hipStream_t st) {
     if (mode <= 0 || n <= 0) return 0;
     (void)adps_key;
     bool same = s->planned && s->threshold == threshold && s->sc.ma == sc.ma && s->sc.mi == sc.mi &&
@@ -625,7 +626,7 @@ int bounds(State *s, const void *adps_key, const uint8_t *hcodes, const int32_t 
         SD_TRY(hipGetLastError());
         const int64_t tot = n * (int64_t)n_adp;
         const unsigned grid_all = (unsigned)((tot + 255) / 256);
-        if (!cands) {
+        if (!cands && !dcands) {
             hipLaunchKernelGGL(k_bound16, dim3(grid_all), dim3(256), 0, st, (const int32_t *)s->bound.p, tot, s16);
             SD_TRY(hipGetLastError());
             g_runs.fetch_add(1);
@@ -645,6 +646,12 @@ int bounds(State *s, const void *adps_key, const uint8_t *hcodes, const int32_t 
             if ((int64_t)nc > s->ccap) {
                 s->ccap = (int64_t)nc + (int64_t)nc / 4;
                 continue;
+            }
+            if (dcands) {                              // the keys stay on the device, unordered
+                *dcands = (const int64_t *)s->cands.p;
+                *n_dcands = (int64_t)nc;
+                g_runs.fetch_add(1);
+                return 1;
             }
             cands->resize((size_t)nc);
             if (nc) {

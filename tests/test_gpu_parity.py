@@ -358,11 +358,46 @@ def test_middle_scan_seeds(gpu_lib, monkeypatch, threshold, scheme):
     assert L.pcabi_middle_seed_runs() > runs0, 'the seeded round 1 did not run'
     order_g = np.lexsort((np.arange(got.shape[1]), got[0]))
     assert np.array_equal(got[:, order_g], exp[:, order_e])
+    # the seeded rounds plan the candidate DP on the device (default) with the chunk length set
+    # by the wave target: the longest (512) and the shortest (64) chunks, and the host plan
+    for env in (('PCABI_MIDDLE_PLAN_WAVES', '1'), ('PCABI_MIDDLE_PLAN_WAVES', '100000000'),
+                ('PCABI_MIDDLE_DEVPLAN', '0')):
+        monkeypatch.setenv(*env)
+        assert np.array_equal(engine.middle_scan(views, adps, scheme, threshold), got), env
+        monkeypatch.delenv(env[0])
     monkeypatch.setenv('PCABI_MIDDLE_SEEDS', '0')
     runs1 = L.pcabi_middle_seed_runs()
     got0 = engine.middle_scan(views, adps, scheme, threshold)
     assert L.pcabi_middle_seed_runs() == runs1
     assert np.array_equal(got0, got)
+
+
+@pytest.mark.gpu
+def test_middle_scan_equal_scores_in_chunks_from_the_read_start(gpu_lib, monkeypatch):
+    """Device-planned candidate DP with the shortest chunks (64 owned columns): in a short read
+    every chunk starts at offset 0 (the lead-in D covers the read start), and two exact copies of
+    the adapter score the same in chunks 0 and 1 -- the merge must take chunk 0 (the full DP's
+    first maximum) every time, the later copy is the second round's hit."""
+    from custom_porechop_abi_amd import engine
+    rng = random.Random(41)
+    adp = _rand_seq(rng, 50, 'ACGT')
+    reads = []
+    for k in range(300):
+        pre = _rand_seq(rng, rng.randint(0, 14), 'ACGT')
+        mid = _rand_seq(rng, rng.randint(0, 6), 'ACGT')
+        reads.append(pre + adp + mid + adp + _rand_seq(rng, rng.randint(0, 20), 'ACGT'))
+    pack = engine.SeqPack(reads)
+    views = pack.views(np.zeros(len(reads), np.int64), pack.lengths)
+    sc = (3, -6, -5, -2)
+    exp = oracle_lib.middle_scan_windows(views, [adp], sc, 88.0)
+    monkeypatch.setenv('PCABI_MIDDLE_SEEDS', '2')
+    monkeypatch.setenv('PCABI_MIDDLE_PLAN_WAVES', '100000000')
+    assert exp.shape[1] == 2 * len(reads)
+    order_e = np.lexsort((np.arange(exp.shape[1]), exp[0]))
+    for _ in range(3):
+        got = engine.middle_scan(views, [adp], sc, 88.0)
+        order_g = np.lexsort((np.arange(got.shape[1]), got[0]))
+        assert np.array_equal(got[:, order_g], exp[:, order_e])
 
 
 @pytest.mark.gpu
