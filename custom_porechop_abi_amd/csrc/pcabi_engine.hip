@@ -1966,18 +1966,29 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
     cur.resize((size_t)n_win);
     for (int64_t k = 0; k < n_win; ++k) cur[k] = (int32_t)k;
     {
-        // longest first, ties in read order: a stable LSD radix sort on ~length, two 16-bit digits
+        // longest first, ties in read order: a stable LSD radix sort on (longest - length), 11-bit
+        // digits over the bits the longest length needs (two passes up to 4 M bases)
+        int32_t longest = 0;
+        for (int64_t k = 0; k < n_win; ++k) longest = std::max(longest, h_win_len[k]);
+        int bits = 1;
+        while (bits < 31 && (1u << bits) <= (uint32_t)longest) ++bits;
         std::vector<int32_t> tmp((size_t)n_win);
-        std::vector<int64_t> cnt(1 << 16);
-        auto key = [&](int32_t k) { return ~(uint32_t)std::max(h_win_len[k], 0); };
-        for (int pass = 0; pass < 2; ++pass) {
-            const int sh = 16 * pass;
+        std::vector<uint32_t> key((size_t)n_win), ktmp((size_t)n_win);
+        for (int64_t k = 0; k < n_win; ++k) key[k] = (uint32_t)(longest - std::max(h_win_len[k], 0));
+        constexpr int kDig = 11;
+        std::vector<int64_t> cnt((size_t)1 << kDig);
+        for (int sh = 0; sh < bits; sh += kDig) {
             std::fill(cnt.begin(), cnt.end(), 0);
-            for (int64_t k = 0; k < n_win; ++k) ++cnt[(key(cur[k]) >> sh) & 0xFFFF];
+            for (int64_t k = 0; k < n_win; ++k) ++cnt[(key[k] >> sh) & ((1u << kDig) - 1)];
             int64_t run = 0;
             for (int64_t &c : cnt) { const int64_t x = c; c = run; run += x; }
-            for (int64_t k = 0; k < n_win; ++k) tmp[cnt[(key(cur[k]) >> sh) & 0xFFFF]++] = cur[k];
+            for (int64_t k = 0; k < n_win; ++k) {
+                const int64_t d = cnt[(key[k] >> sh) & ((1u << kDig) - 1)]++;
+                tmp[d] = cur[k];
+                ktmp[d] = key[k];
+            }
             cur.swap(tmp);
+            key.swap(ktmp);
         }
     }
     for (int round = 0;; ++round) {

@@ -36,6 +36,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <string>
 #include <vector>
@@ -63,11 +64,22 @@ constexpr int kCls = 2;            // band classes: e <= E0, e <= E1
 constexpr int kMaxE = 15;          // band half-width the kernels are built for
 constexpr int kMaxL = 255;
 constexpr int kMaxEnt = 8192;      // probe entries / distinct probes kept in LDS
-constexpr int kBuf = 512;          // staged tasks per block and class
+#ifndef PCABI_SEED_BUF
+#define PCABI_SEED_BUF 256
+#endif
+
+constexpr int kBuf = PCABI_SEED_BUF;   // staged tasks per block and class
 constexpr int kLdsMax = 64 * 1024; // per block: probe tables + stage
 constexpr int kNeg = -(1 << 20);
 constexpr int kPos = 8;            // read positions per lane and scan step (16 bases loaded)
 constexpr int kNW = 4;             // dwords of bases per lane and step
+#ifndef PCABI_SEED_SUB
+#define PCABI_SEED_SUB 2
+#endif
+constexpr int kSub = PCABI_SEED_SUB;   // sub-steps per scan iteration
+#ifndef PCABI_SEED_FLUSH
+#define PCABI_SEED_FLUSH (8 / PCABI_SEED_SUB - 1)   // stage flush every 8 sub-steps
+#endif
 
 struct ScanArgs {
     const uint8_t *codes;
@@ -173,16 +185,22 @@ __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
     k = next_read(k, len, base);
     if (k < a.n) nk = next_read(k + gridDim.x, nlen, nbase);
     int p0b = 0;
-    uint32_t wn[kNW];
-    if (k < a.n) fetch(base, len, 0, wn);
+    // kSub sub-steps of 2048 positions per iteration, fetched together one iteration ahead:
+    // more bytes in flight per latency
+    uint32_t wn[kSub][kNW];
+#pragma unroll
+    for (int h = 0; h < kSub; ++h)
+        if (k < a.n) fetch(base, len, h * 256 * kPos, wn[h]);
     int iter = 0;
     while (k < a.n) {                                  // block-uniform: every lane takes part
         const int64_t ck = k;
-        const int clen = len, cp0 = p0b + kPos * (int)threadIdx.x;
-        uint32_t w[kNW];
+        const int clen = len, cp0b = p0b;
+        uint32_t wc[kSub][kNW];
 #pragma unroll
-        for (int d = 0; d < kNW; ++d) w[d] = wn[d];
-        p0b += 256 * kPos;
+        for (int h = 0; h < kSub; ++h)
+#pragma unroll
+            for (int d = 0; d < kNW; ++d) wc[h][d] = wn[h][d];
+        p0b += kSub * 256 * kPos;
         if (p0b >= len) {                              // on to the next read
             k = nk;
             len = nlen;
@@ -190,7 +208,13 @@ __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
             p0b = 0;
             if (k < a.n) nk = next_read(k + gridDim.x, nlen, nbase);
         }
-        if (k < a.n) fetch(base, len, p0b, wn);
+#pragma unroll
+        for (int h = 0; h < kSub; ++h)
+            if (k < a.n) fetch(base, len, p0b + h * 256 * kPos, wn[h]);
+#pragma unroll
+        for (int h = 0; h < kSub; ++h) {
+        const int cp0 = cp0b + h * 256 * kPos + kPos * (int)threadIdx.x;
+        const uint32_t *w = wc[h];
         // 16 bases (SWAR): c32 = their 2-bit codes, first base in the top bits; vmask bit t =
         // base t is A/C/G/T inside the read (Dna5 codes are 0..4: N has bit 2)
         uint32_t c32 = 0, vmask = 0;
@@ -206,6 +230,17 @@ __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
         // fast path: every probe is a prefix of the 8-mer at its position, and the K = 8 table
         // holds every 8-mer that extends a probe -- one LDS word per position
         uint32_t hits = 0, slow = 0;
+        if (__all((vmask & 0x7FFFu) == 0x7FFFu)) {
+            // every lane's 8 positions see 8 valid bases: one bitmap word each, the K = 8 bitmap
+            // at LDS byte 0 (plan()), byte address (c8 >> 5) << 2 straight from c32
+#pragma unroll
+            for (int i = 0; i < kPos; ++i) {
+                const int sh = 16 - 2 * i;
+                const uint32_t word = *reinterpret_cast<const uint32_t *>(
+                    reinterpret_cast<const char *>(lds) + ((c32 >> (sh + 3)) & 0x1FFCu));
+                hits |= ((word >> ((c32 >> sh) & 31u)) & 1u) << i;
+            }
+        } else {
 #pragma unroll
         for (int i = 0; i < kPos; ++i) {
             const uint32_t c8 = (c32 >> (16 - 2 * i)) & 0xFFFFu;
@@ -214,6 +249,7 @@ __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
             hits |= (full && ((word >> (c8 & 31)) & 1u)) ? 1u << i : 0u;
             // a valid run shorter than 8 bases (an N or the read end ahead): the short tables
             slow |= (!full && ((vmask >> i) & ((1u << a.min_k) - 1u)) == (1u << a.min_k) - 1u) ? 1u << i : 0u;
+        }
         }
         while (hits | slow) {
             const bool fast = hits != 0;
@@ -238,7 +274,8 @@ __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
                 }
             }
         }
-        if ((++iter & 7) == 0) flush(sg, kBuf / 2, a);
+        }
+        if ((++iter & PCABI_SEED_FLUSH) == 0) flush(sg, kBuf / 2, a);
     }
     flush(sg, 1, a);
 }
@@ -247,9 +284,13 @@ __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
 // diagonals d0 - E .. d0 + E (cell x <-> read column j = i + d0 + x - E), free end gaps as the
 // full DP: S(0, j) = 0, S(i, 0) = 0, ends in row L (j < len) or in the last column (j = len).
 // CHECK: the band touches column 0 or the last column, or leaves the read.
+// Early exit (inside bands, T > 0): no path gains more than `match` per remaining row (gaps cost),
+// and an inside band holds no column-0 restart and no last-column end, so once every cell of row
+// i satisfies S + match (L - i) < T the pair cannot reach T: the DP stops and returns that bound
+// (below T, which is all the caller compares). Random probe hits -- most tasks -- stop early.
 template <int E, bool CHECK>
 __device__ __forceinline__ int band_best(const uint8_t *rd, int len, const uint8_t *ac, int L, int d0,
-                                         const pcabi::Scoring &sc) {
+                                         const pcabi::Scoring &sc, int T) {
     constexpr int W = 2 * E + 1;
     int S[W], V[W], R[W];
 #pragma unroll
@@ -284,6 +325,13 @@ __device__ __forceinline__ int band_best(const uint8_t *rd, int len, const uint8
         for (int x = 0; x + 1 < W; ++x) R[x] = R[x + 1];
         const int jn = i + 1 + d0 + E;
         R[W - 1] = (!CHECK || (jn >= 1 && jn <= len)) ? rd[jn - 1] : 7;
+        if (!CHECK && (i & 3) == 0) {
+            int mx = S[0];
+#pragma unroll
+            for (int x = 1; x < W; ++x) mx = max(mx, S[x]);
+            const int ub = mx + sc.ma * (L - i);
+            if (ub < T) return ub;
+        }
     }
 #pragma unroll
     for (int x = 0; x < W; ++x) {                            // last row, j < len
@@ -297,7 +345,7 @@ template <int E>
 __global__ __launch_bounds__(256) void k_seed_band(const int4 *task, int32_t n_task, const uint8_t *codes,
                                                    const int64_t *v_off, const int32_t *v_len, const uint8_t *adp,
                                                    const int32_t *adp_off, const int32_t *adp_len, pcabi::Scoring sc,
-                                                   int32_t *bound, int64_t n) {
+                                                   const int32_t *thr, int32_t *bound, int64_t n) {
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (t >= n_task) return;
     const int4 tk = task[t];
@@ -307,7 +355,9 @@ __global__ __launch_bounds__(256) void k_seed_band(const int4 *task, int32_t n_t
     const uint8_t *rd = codes + v_off[tk.x];
     const uint8_t *ac = adp + adp_off[tk.y];
     const bool inside = d0 - E >= 1 && d0 + E + L + 1 < len;
-    const int best = inside ? band_best<E, false>(rd, len, ac, L, d0, sc) : band_best<E, true>(rd, len, ac, L, d0, sc);
+    const int T = thr[tk.y];
+    const int best = inside ? band_best<E, false>(rd, len, ac, L, d0, sc, T)
+                            : band_best<E, true>(rd, len, ac, L, d0, sc, T);
     atomicMax(&bound[(int64_t)tk.y * n + tk.x], best);
 }
 
@@ -375,6 +425,7 @@ struct State {
     ScanArgs a{};
     Buf tabs, adp, adp_off, adp_len, task, cnt, bound, thr, cands, ccnt;
     int64_t cap = 0, ccap = 0;
+    int scan_blocks = 0;                          // resident k_seed_scan blocks (per plan)
 };
 
 State *create() { return new State(); }
@@ -450,8 +501,10 @@ int plan(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hl
     std::vector<uint16_t> estart;
     std::vector<int32_t> ent;
     ScanArgs &A = s->a;
-    for (int kk = 0; kk < kNK; ++kk) {
-        A.bits_off[kk] = -1;
+    for (int kk = 0; kk < kNK; ++kk) A.bits_off[kk] = -1;
+    // the merged K = 8 bitmap first: the scan's fast path addresses it from LDS byte 0
+    for (int pass = 0; pass < kNK; ++pass) {
+        const int kk = pass == 0 ? kNK - 1 : pass - 1;
         if (lists[kk].empty()) continue;
         const size_t nc = lists[kk].size();
         const int K = kMinK + kk;
@@ -532,7 +585,7 @@ void launch_band(const State *s, int E, int32_t cnt, int c, const uint8_t *codes
 #define C(X)                                                                                                   \
     case X:                                                                                                    \
         hipLaunchKernelGGL(k_seed_band<X>, grid, dim3(256), 0, st, task, cnt, codes, v_off, v_len, adp, aoff, \
-                           alen, sc, bound, n);                                                               \
+                           alen, sc, (const int32_t *)s->thr.p, bound, n);                                    \
         break;
         C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8) C(9) C(10) C(11) C(12) C(13) C(14) C(15)
 #undef C
@@ -571,6 +624,7 @@ int bounds(State *s, const void *adps_key, const uint8_t *hcodes, const int32_t 
             s->key_codes.insert(s->key_codes.end(), hcodes + hoff[a], hcodes + hoff[a] + std::max(hlen[a], 0));
         s->threshold = threshold;
         s->sc = sc;
+        s->scan_blocks = 0;
         if (int rc = plan(s, hcodes, hoff, hlen, n_adp, fb_rows, sc, threshold)) {
             s->planned = false;
             return rc;
@@ -590,7 +644,16 @@ int bounds(State *s, const void *adps_key, const uint8_t *hcodes, const int32_t 
         A.task = (int4 *)s->task.p;
         A.cap = s->cap;
         SD_TRY(hipMemsetAsync(A.cnt, 0, 4 * kCls, st));
-        const unsigned grid = (unsigned)std::min<int64_t>(n, 2048);
+        // every block resident at once (the blocks stride over the reads evenly: a second wave
+        // of blocks would run on a partly idle chip)
+        if (s->scan_blocks == 0) {
+            int dev = 0, cus = 0, per_cu = 0;
+            SD_TRY(hipGetDevice(&dev));
+            SD_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+            SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_scan, 256, s->lds_bytes));
+            s->scan_blocks = std::max(1, cus * std::max(1, per_cu));
+        }
+        const unsigned grid = (unsigned)std::min<int64_t>(n, s->scan_blocks);
         hipLaunchKernelGGL(k_seed_scan, dim3(grid), dim3(256), s->lds_bytes, st, A);
         SD_TRY(hipGetLastError());
         int32_t cnt[kCls];
@@ -606,6 +669,10 @@ int bounds(State *s, const void *adps_key, const uint8_t *hcodes, const int32_t 
             s->cap = most + most / 4;
             continue;
         }
+        if (const char *dbg = std::getenv("PCABI_DEBUG"))
+            if (dbg[0] == '1')
+                std::fprintf(stderr, "[pcabi] seeds: %lld windows, band tasks %d (E=%d) + %d (E=%d), scan grid %u\n",
+                             (long long)n, cnt[0], s->band[0], cnt[1], s->band[1], grid);
         SD_TRY(hipMemsetD32Async((hipDeviceptr_t)s->bound.p, pcabi::sf::NEG16, (size_t)n * n_adp, st));
         if (cnt[0] && cnt[1]) {   // both classes: side by side (atomicMax into one bound array)
             if (!s->side) {
