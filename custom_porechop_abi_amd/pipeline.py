@@ -37,10 +37,14 @@ class FileTrimmer(object):
     10 (good side) / 100 (bad side), min_split_read_size 1000, no_split False, discard_middle
     False, adapter filter on (the fork's)."""
 
+    barcode_dir = None                    # -b off (set by __init__)
+
     def __init__(self, matching_sets, scoring_scheme_vals=(3, -6, -5, -2), end_size=150, end_threshold=75.0,
                  extra_end_trim=2, min_trim_size=4, middle_threshold=90.0, extra_middle_trim_good_side=10,
                  extra_middle_trim_bad_side=100, min_split_read_size=1000, no_split=False, discard_middle=False,
-                 filter_reads=True, device=0):
+                 filter_reads=True, device=0, barcode_dir=None, forward_or_reverse_barcodes='forward',
+                 barcode_threshold=75.0, barcode_diff=5.0, require_two_barcodes=False, untrimmed=False,
+                 discard_unassigned=False):
         self.L = L = lib()
         self.device = int(device)
         check(L.pcabi_dev_set(device), 'pcabi_dev_set')
@@ -68,6 +72,23 @@ class FileTrimmer(object):
         check(L.pcabi_stream_create(ctypes.byref(self.stream)), 'pcabi_stream_create')
         self.dev = {}
         self.times = {}
+        # -b: barcode bins (porechop_abi.py:80-104, 581-638). The dicts find_start_trim /
+        # find_end_trim fill become slot tables (porechop_abi.barcode_slots), the call runs on the
+        # device after the end trim (pcabi_barcode_call_dev), and the writer sends every read to
+        # <barcode_dir>/<call>.<format>; --untrimmed and --discard_unassigned as the reference
+        # (the former only applies to bins there too).
+        self.barcode_dir = barcode_dir
+        if barcode_dir is not None:
+            from .porechop_abi import barcode_slots
+            ids = {}
+            start_sets = [a for a in matching_sets if a.start_sequence]
+            end_sets = [a for a in matching_sets if a.end_sequence]
+            self.bc_slots = (barcode_slots(start_sets, forward_or_reverse_barcodes, ids),
+                             barcode_slots(end_sets, forward_or_reverse_barcodes, ids))
+            self.bc_names = {v: k for k, v in ids.items()}
+            self.bc_thr, self.bc_diff, self.bc_two = float(barcode_threshold), float(barcode_diff), \
+                bool(require_two_barcodes)
+            self.untrimmed, self.discard_unassigned = bool(untrimmed), bool(discard_unassigned)
 
     def _table(self, seqs):
         if not seqs:
@@ -137,7 +158,20 @@ class FileTrimmer(object):
                                        self.thr, self.min_trim, d_st, d_et, None, None, self.stream), 'end_trim')
             check(L.pcabi_dev_copy_async(trims[0].ctypes.data_as(VP), d_st, 4 * nb, 1, self.stream), 'd2h')
             check(L.pcabi_dev_copy_async(trims[1].ctypes.data_as(VP), d_et, 4 * nb, 1, self.stream), 'd2h')
+            if self.barcode_dir is not None:
+                calls = np.full(nb, -1, np.int32)
+                (sa, sn), (ea, en) = self.bc_slots
+                d_call = self._buf('bcall', 4 * nb)
+                slots = [self._h2d('bc%d' % i, x) for i, x in enumerate((sa, sn, ea, en))]
+                check(L.pcabi_barcode_call_dev(res[0], n_ad[0] * nb, slots[0], slots[1], len(sa), res[1],
+                                               n_ad[1] * nb, slots[2], slots[3], len(ea), nb, self.bc_thr,
+                                               self.bc_diff, int(self.bc_two), d_call, None, self.stream),
+                      'barcode_call')
+                check(L.pcabi_dev_copy_async(calls.ctypes.data_as(VP), d_call, 4 * nb, 1, self.stream), 'd2h')
+                self.last_calls = calls
             check(L.pcabi_stream_sync(self.stream), 'sync')
+        elif self.barcode_dir is not None:
+            self.last_calls = np.full(nb, -1, np.int32)
         t = self._tick('end_trim', t)
         cut_off = np.zeros(nb + 1, np.int64)
         cuts = np.zeros(0, np.int64)
@@ -188,6 +222,10 @@ class FileTrimmer(object):
         library's parse, alignment and write calls release the GIL. times: 'parse' / 'write_wait'
         are this thread's waits, 'write' the writer's own busy time (overlapped)."""
         counts = {'reads_in': 0, 'reads_kept': 0}
+        bins = {}                             # barcode name -> (path, reads selected for it)
+        if self.barcode_dir is not None:
+            os.makedirs(self.barcode_dir, exist_ok=True)
+            counts['bins'] = bins
         pq = queue.Queue(maxsize=2)
         wq = queue.Queue(maxsize=2)
         errors = []
@@ -221,21 +259,24 @@ class FileTrimmer(object):
                     break
                 if errors:
                     continue                 # drain after a failure
-                k, b, st, et, co, cu, keep = item
+                k, b, st, et, co, cu, keep, calls = item
                 t0 = time.perf_counter()
                 try:
-                    at = os.path.getsize(out_path) if (segments is not None and not first) else 0
-                    misc.write_reads(b, out_path, out_format, st, et, None, self.min_split, self.discard_middle,
-                                     select=keep, append=not first, cut_arrays=(co, cu))
-                    if segments is not None:
-                        segments.append((k, at, os.path.getsize(out_path)))
+                    if calls is not None:
+                        self._write_bins(b, out_format, st, et, co, cu, keep, calls, bins, k, segments)
+                    else:
+                        at = os.path.getsize(out_path) if (segments is not None and not first) else 0
+                        misc.write_reads(b, out_path, out_format, st, et, None, self.min_split, self.discard_middle,
+                                         select=keep, append=not first, cut_arrays=(co, cu))
+                        if segments is not None:
+                            segments.append((k, at, os.path.getsize(out_path)))
                 except BaseException as ex:
                     errors.append(ex)
                 first = False
                 counts['reads_in'] += b.n
                 counts['reads_kept'] += int(keep.sum()) if keep is not None else b.n
                 self.times['write'] = self.times.get('write', 0.0) + time.perf_counter() - t0
-            if first and not errors:     # empty input: still create the output
+            if first and not errors and self.barcode_dir is None:   # empty input: still create the output
                 open(out_path, 'wb').close()
 
         reader = threading.Thread(target=produce, daemon=True)
@@ -253,7 +294,8 @@ class FileTrimmer(object):
                     raise b
                 k, b = b
                 st, et, co, cu, _, keep = self.trim(b)
-                wq.put((k, b, st, et, co, cu, keep))   # the writer drains even after a failure
+                calls = self.last_calls if self.barcode_dir is not None else None
+                wq.put((k, b, st, et, co, cu, keep, calls))   # the writer drains even after a failure
                 del b
                 t = time.perf_counter()
         finally:
@@ -267,6 +309,26 @@ class FileTrimmer(object):
         if errors:
             raise errors[0]
         return counts
+
+    def _write_bins(self, b, out_format, st, et, co, cu, keep, calls, bins, k=0, segments=None):
+        """One batch into the barcode bins (porechop_abi.py:581-610): the reads of each call, in
+        read order, appended to <barcode_dir>/<name>.<format> (created, not appended, the first
+        time the run writes it, as the reference opens each bin with 'wt'). segments (sharded
+        runs) receives (k, name, begin, end) byte spans per bin write."""
+        sel = np.ones(b.n, bool) if keep is None else keep.astype(bool)
+        if self.discard_unassigned:
+            sel &= calls >= 0
+        for cid in np.unique(calls[sel]).tolist():
+            name = self.bc_names.get(cid, 'none') if cid >= 0 else 'none'
+            mask = (sel & (calls == cid)).astype(np.uint8)
+            path = os.path.join(self.barcode_dir, name + '.' + out_format)
+            fresh = name not in bins
+            at = 0 if fresh else os.path.getsize(path)
+            misc.write_reads(b, path, out_format, st, et, None, self.min_split, self.discard_middle,
+                             untrimmed=self.untrimmed, select=mask, append=not fresh, cut_arrays=(co, cu))
+            bins[name] = (path, (0 if fresh else bins[name][1]) + int(mask.sum()))
+            if segments is not None:
+                segments.append((k, name, at, os.path.getsize(path)))
 
     def close(self):
         L = self.L

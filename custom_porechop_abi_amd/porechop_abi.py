@@ -345,3 +345,112 @@ def filter_reads_by_adapter(reads, print_dest=sys.stdout):
     kept = [r for r in reads if r.adapters_found()]
     print('Filtered reads: %d' % len(kept), file=print_dest)
     return kept
+
+
+# ---------------------------------------------------------------------------------------------
+def _print_table(table, print_dest, alignments='', col_separation=2, indent=2):
+    """Plain-text table (the reference's misc.print_table without colours or wrapping): display
+    only."""
+    n = len(table[0])
+    alignments = (alignments + 'L' * n)[:n]
+    widths = [max(len(str(r[c])) for r in table) for c in range(n)]
+    for r in table:
+        cells = [str(x).ljust(w) if a == 'L' else str(x).rjust(w) for x, w, a in zip(r, widths, alignments)]
+        print(' ' * indent + (' ' * col_separation).join(cells).rstrip(), file=print_dest)
+
+
+def output_reads(reads, out_format, output, read_type, verbosity, discard_middle, min_split_size, print_dest,
+                 barcode_dir, input_filename, untrimmed, threads, discard_unassigned):
+    """porechop_abi.py:535-668 for a list of NanoporeRead: barcode bins (-b), stdout, or a file;
+    the output format from `out_format` / the output name / the input read type as the reference
+    ('auto'). Gzipped outputs are compressed here (gzip module) rather than by a gzip / pigz
+    subprocess: the decompressed contents are the reference's byte for byte. As in the
+    reference, `untrimmed` only applies to barcode bins. For files of millions of reads the
+    native path is pipeline.FileTrimmer (barcode_dir included)."""
+    import gzip
+    import os
+    from collections import defaultdict
+    if verbosity > 0:
+        trimmed_or_untrimmed = 'untrimmed' if untrimmed else 'trimmed'
+        if barcode_dir is not None:
+            verb, destination = 'Saving ', 'barcode-specific files'
+        elif output is None:
+            verb, destination = 'Outputting ', 'stdout'
+        else:
+            verb, destination = 'Saving ', 'file'
+        print(bold_underline(verb + trimmed_or_untrimmed + ' reads to ' + destination), flush=True, file=print_dest)
+    if out_format == 'auto':
+        if output is None:
+            out_format = read_type.lower()
+            if barcode_dir is not None and input_filename.lower().endswith('.gz'):
+                out_format += '.gz'
+        elif '.fasta.gz' in output.lower():
+            out_format = 'fasta.gz'
+        elif '.fastq.gz' in output.lower():
+            out_format = 'fastq.gz'
+        elif '.fasta' in output.lower():
+            out_format = 'fasta'
+        elif '.fastq' in output.lower():
+            out_format = 'fastq'
+        else:
+            out_format = read_type.lower()
+    gzipped_out = False
+    if out_format.endswith('.gz') and (barcode_dir is not None or output is not None):
+        gzipped_out = True
+        out_format = out_format[:-3]
+
+    def read_string(read, with_untrimmed):
+        if out_format == 'fasta':
+            return read.get_fasta(min_split_size, discard_middle, untrimmed) if with_untrimmed \
+                else read.get_fasta(min_split_size, discard_middle)
+        return read.get_fastq(min_split_size, discard_middle, untrimmed) if with_untrimmed \
+            else read.get_fastq(min_split_size, discard_middle)
+
+    if barcode_dir is not None:
+        os.makedirs(barcode_dir, exist_ok=True)
+        parts = defaultdict(list)
+        read_counts, base_counts = defaultdict(int), defaultdict(int)
+        for read in reads:
+            name = read.barcode_call
+            if discard_unassigned and name == 'none':
+                continue
+            s = read_string(read, True)
+            if not s:
+                continue
+            parts[name].append(s)
+            read_counts[name] += 1
+            base_counts[name] += len(read.seq) if untrimmed else read.seq_length_with_start_end_adapters_trimmed()
+        table = [['Barcode', 'Reads', 'Bases', 'File']]
+        for name in sorted(parts):
+            path = os.path.join(barcode_dir, name + '.' + out_format)
+            data = ''.join(parts[name]).encode()
+            if gzipped_out:
+                if os.path.isfile(path):
+                    os.remove(path)
+                path += '.gz'
+                with gzip.open(path, 'wb') as f:
+                    f.write(data)
+            else:
+                with open(path, 'wb') as f:
+                    f.write(data)
+            table.append([name, int_to_str(read_counts[name]), int_to_str(base_counts[name]), path])
+        if verbosity > 0:
+            print('', file=print_dest)
+            _print_table(table, print_dest, alignments='LRRL')
+    elif output is None:
+        for read in reads:
+            print(read_string(read, False), end='')
+        if verbosity > 0:
+            print('Done', flush=True, file=print_dest)
+    else:
+        data = ''.join(read_string(read, False) for read in reads).encode()
+        if gzipped_out:
+            with gzip.open(output, 'wb') as f:
+                f.write(data)
+        else:
+            with open(output, 'wb') as f:
+                f.write(data)
+        if verbosity > 0:
+            print('\nSaved result to ' + os.path.abspath(output), file=print_dest)
+    if verbosity > 0:
+        print('', flush=True, file=print_dest)

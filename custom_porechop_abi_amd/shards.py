@@ -150,7 +150,8 @@ def trim_file_sharded(in_path, out_path, out_format='fastq', scoring_scheme_vals
                       end_threshold=75.0, extra_end_trim=2, min_trim_size=4, middle_threshold=90.0,
                       extra_middle_trim_good_side=10, extra_middle_trim_bad_side=100, min_split_read_size=1000,
                       check_reads=10000, adapter_threshold=90.0, max_reads=100000, group=None, device=None,
-                      trimmer_factory=None):
+                      trimmer_factory=None, barcode_dir=None, barcode_threshold=75.0, barcode_diff=5.0,
+                      require_two_barcodes=False, untrimmed=False, discard_unassigned=False):
     """The CLI's file-to-file path (porechop_abi.py:41-131: adapter-set search on the first
     check_reads records, end trim, middle scan, the fork's filter, trimmed output) on every rank of
     `group`, one GPU each:
@@ -165,6 +166,10 @@ def trim_file_sharded(in_path, out_path, out_format='fastq', scoring_scheme_vals
         span of each batch it writes;
       * output: rank 0 concatenates the parts in record order (the reference's output order) --
         the only other exchange is the span lists (gzip input) and the read counts.
+
+    With barcode_dir (-b) every rank writes its bins into a private directory, recording the
+    byte span of each bin write, and rank 0 stitches every bin in record order; the barcoding
+    kit direction comes from choose_barcoding_kit on the all-reduced set scores, as in the CLI.
 
     Returns the job's read counts (every rank). trimmer_factory(matching_sets, **options) builds
     the per-rank trimmer (FileTrimmer by default; the CPU tests pass an oracle-backed one)."""
@@ -182,11 +187,18 @@ def trim_file_sharded(in_path, out_path, out_format='fastq', scoring_scheme_vals
             break
     matching = find_matching_adapter_sets(check, 0, end_size, scoring_scheme_vals, io.StringIO(), adapter_threshold, 1,
                                           group=group)
-    matching = P.add_full_barcode_adapter_sets(P.fix_up_1d2_sets(matching))
+    matching = P.fix_up_1d2_sets(matching)
+    fwd_rev = P.choose_barcoding_kit(matching, 0, io.StringIO()) if barcode_dir is not None else None
+    matching = P.add_full_barcode_adapter_sets(matching)
     opts = dict(scoring_scheme_vals=scoring_scheme_vals, end_size=end_size, end_threshold=end_threshold,
                 extra_end_trim=extra_end_trim, min_trim_size=min_trim_size, middle_threshold=middle_threshold,
                 extra_middle_trim_good_side=extra_middle_trim_good_side,
                 extra_middle_trim_bad_side=extra_middle_trim_bad_side, min_split_read_size=min_split_read_size)
+    bdir = lambda r: os.path.join(barcode_dir, '.pcabi_rank%d' % r)
+    if barcode_dir is not None:
+        opts.update(barcode_dir=bdir(rank), forward_or_reverse_barcodes=fwd_rev, barcode_threshold=barcode_threshold,
+                    barcode_diff=barcode_diff, require_two_barcodes=require_two_barcodes, untrimmed=untrimmed,
+                    discard_unassigned=discard_unassigned)
     if trimmer_factory is None:
         from .pipeline import FileTrimmer
         trimmer_factory = FileTrimmer
@@ -195,10 +207,11 @@ def trim_file_sharded(in_path, out_path, out_format='fastq', scoring_scheme_vals
     d, base = os.path.split(os.path.abspath(out_path))
     part = lambda r: os.path.join(d, '.pcabi_part%d_%s' % (r, base))
     bounds = misc.record_boundaries(in_path, world)
-    segments = None if bounds is not None else []
+    segments = None if (bounds is not None and barcode_dir is None) else []
     try:
         if bounds is not None:
-            counts = ft.trim_file(in_path, part(rank), out_format, max_reads, byte_range=(bounds[rank], bounds[rank + 1]))
+            counts = ft.trim_file(in_path, part(rank), out_format, max_reads, byte_range=(bounds[rank], bounds[rank + 1]),
+                                  segments=segments)
         else:
             counts = ft.trim_file(in_path, part(rank), out_format, max_reads,
                                   batch_filter=lambda k: k % world == rank, segments=segments)
@@ -207,10 +220,28 @@ def trim_file_sharded(in_path, out_path, out_format='fastq', scoring_scheme_vals
             ft.close()
     if world > 1:
         spans = [None] * world
-        dist.all_gather_object(spans, (segments, counts), group=group)
+        dist.all_gather_object(spans, (segments, {k: v for k, v in counts.items() if k != 'bins'}), group=group)
     else:
         spans = [(segments, counts)]
-    if rank == 0:
+    if rank == 0 and barcode_dir is not None:
+        # every bin in record order: plain inputs by (rank, batch), gzip inputs by global batch
+        order = sorted(((k, r) if bounds is None else (r, k), r, nm, a, e)
+                       for r, (segs, _) in enumerate(spans) for k, nm, a, e in segs)
+        outs = {}
+        try:
+            for _, r, nm, a, e in order:
+                fmt_name = nm + '.' + out_format
+                if fmt_name not in outs:
+                    outs[fmt_name] = open(os.path.join(barcode_dir, fmt_name), 'wb')
+                with open(os.path.join(bdir(r), fmt_name), 'rb') as f:
+                    f.seek(a)
+                    outs[fmt_name].write(f.read(e - a))
+        finally:
+            for f in outs.values():
+                f.close()
+        for r in range(world):
+            shutil.rmtree(bdir(r), ignore_errors=True)
+    elif rank == 0:
         with open(out_path, 'wb') as out:
             if bounds is not None:
                 for r in range(world):
@@ -231,4 +262,7 @@ def trim_file_sharded(in_path, out_path, out_format='fastq', scoring_scheme_vals
                 os.remove(part(r))
     if world > 1:
         dist.barrier(group=group)
-    return {k: sum(c[k] for _, c in spans) for k in ('reads_in', 'reads_kept')}
+    out = {k: sum(c[k] for _, c in spans) for k in ('reads_in', 'reads_kept')}
+    if barcode_dir is not None:
+        out['bins'] = sorted(set(nm for segs, _ in spans for _, nm, _, _ in segs))
+    return out

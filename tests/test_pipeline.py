@@ -178,3 +178,106 @@ def test_sharded_file_pipeline_on_gpu(gpu_lib, tmp_path, gz):
         dist.destroy_process_group()
     assert counts['reads_in'] == len(records)
     assert open(out_path).read() == _expected(case, records)
+
+
+def _expected_bins(case, records, discard_unassigned=False, untrimmed=False, fasta=False):
+    """The reference's barcode bins (porechop_abi.py:581-610) from its own decisions (G2): the
+    reads with start and end alignments (the fork's filter), each into <barcode_call>.<fmt>."""
+    import json
+    from custom_porechop_abi_amd.nanopore_read import NanoporeRead
+    bins = {}
+    for (n, s, q), d in zip(records, case['reads']):
+        r = NanoporeRead(n, s, q)
+        r.start_trim_amount, r.end_trim_amount = int(d['start_trim']), int(d['end_trim'])
+        for a, b in (json.loads(d['middle_trim']) if isinstance(d['middle_trim'], str) else d['middle_trim']):
+            r.middle_trim_positions.update(range(a, b))
+        alns = [d['start_alns'], d['end_alns']]
+        if not all(json.loads(x) if isinstance(x, str) else x for x in alns):
+            continue
+        call = d['barcode_call']
+        if discard_unassigned and call == 'none':
+            continue
+        txt = r.get_fasta(1000, False, untrimmed) if fasta else r.get_fastq(1000, False, untrimmed)
+        if txt:
+            bins[call] = bins.get(call, '') + txt
+    return bins
+
+
+def _records(case, tmp_path):
+    from custom_porechop_abi_amd import misc
+    in_path = os.path.join(golden_lib.GOLDEN, 'data', case['input'] + '.gz')
+    b = misc.load_batch(in_path)
+    return in_path, [(b.name(i), b.sequence(i), b.quals(i)) for i in range(b.n)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case_name,flags', [('barcodes', {}), ('barcodes_two', {}),
+                                             ('barcodes', {'discard_unassigned': True, 'untrimmed': True}),
+                                             ('barcodes', {'gz': True})])
+def test_trim_file_barcode_bins_match_reference(gpu_lib, case_name, flags, tmp_path):
+    """-b: FileTrimmer's barcode bins (device barcode call + per-bin native writes) == the
+    reference's output_reads bins built from its own decisions and calls (G2)."""
+    import gzip
+    from custom_porechop_abi_amd.pipeline import FileTrimmer
+    case = [c for c in G2['cases'] if c['case'] == case_name][0]
+    opts = case['opts']
+    in_path, records = _records(case, tmp_path)
+    bdir = str(tmp_path / 'bins')
+    fmt = 'fastq.gz' if flags.get('gz') else 'fastq'
+    ft = FileTrimmer(_matching(case), opts['scoring'], opts['end_size'], opts['end_threshold'], opts['extra_end_trim'],
+                     opts['min_trim_size'], opts['middle_threshold'], 10, 100, 1000, barcode_dir=bdir,
+                     forward_or_reverse_barcodes=case['forward_or_reverse'],
+                     require_two_barcodes=bool(opts.get('require_two')),
+                     discard_unassigned=flags.get('discard_unassigned', False), untrimmed=flags.get('untrimmed', False))
+    try:
+        counts = ft.trim_file(in_path, str(tmp_path / 'unused.fastq'), fmt, max_reads=3)   # several batches
+    finally:
+        ft.close()
+    exp = _expected_bins(case, records, flags.get('discard_unassigned', False), flags.get('untrimmed', False))
+    assert exp and sorted(counts['bins']) == sorted(exp)
+    assert sorted(os.listdir(bdir)) == sorted(k + '.' + fmt for k in exp)
+    for name, txt in exp.items():
+        path = os.path.join(bdir, name + '.' + fmt)
+        got = gzip.open(path, 'rt').read() if fmt.endswith('.gz') else open(path).read()
+        assert got == txt, name
+
+
+@pytest.mark.parametrize('flags', [{}, {'discard_unassigned': True, 'untrimmed': True}, {'gz': True}])
+def test_output_reads_barcode_bins_and_file(flags, tmp_path):
+    """porechop_abi.output_reads (porechop_abi.py:535-668) on NanoporeRead objects carrying the
+    reference's decisions (G2): the bins, and the single-file output (where --untrimmed does
+    not apply, as in the reference)."""
+    import gzip
+    import io
+    import json
+    from custom_porechop_abi_amd import porechop_abi as P
+    from custom_porechop_abi_amd.nanopore_read import NanoporeRead
+    case = [c for c in G2['cases'] if c['case'] == 'barcodes'][0]
+    _, records = _records(case, tmp_path)
+    reads = []
+    for (n, s, q), d in zip(records, case['reads']):
+        r = NanoporeRead(n, s, q)
+        r.start_trim_amount, r.end_trim_amount = int(d['start_trim']), int(d['end_trim'])
+        for a, b in (json.loads(d['middle_trim']) if isinstance(d['middle_trim'], str) else d['middle_trim']):
+            r.middle_trim_positions.update(range(a, b))
+        alns = [d['start_alns'], d['end_alns']]
+        if all(json.loads(x) if isinstance(x, str) else x for x in alns):
+            r.barcode_call = d['barcode_call']
+            reads.append(r)
+    gz = flags.get('gz', False)
+    fmt = 'fastq.gz' if gz else 'fastq'
+    bdir = str(tmp_path / 'bins')
+    log = io.StringIO()
+    P.output_reads(reads, fmt, None, 'FASTQ', 1, False, 1000, log, bdir, 'in.fastq',
+                   flags.get('untrimmed', False), 1, flags.get('discard_unassigned', False))
+    exp = _expected_bins(case, records, flags.get('discard_unassigned', False), flags.get('untrimmed', False))
+    assert sorted(os.listdir(bdir)) == sorted(k + '.' + fmt for k in exp)
+    for name, txt in exp.items():
+        path = os.path.join(bdir, name + '.' + fmt)
+        assert (gzip.open(path, 'rt').read() if gz else open(path).read()) == txt
+    assert 'Barcode' in log.getvalue() and 'barcode-specific files' in log.getvalue()
+    out = str(tmp_path / ('all.' + fmt))
+    P.output_reads(reads, 'auto', out, 'FASTQ', 0, False, 1000, io.StringIO(), None, 'in.fastq',
+                   flags.get('untrimmed', False), 1, False)
+    got = gzip.open(out, 'rt').read() if gz else open(out).read()
+    assert got == ''.join(r.get_fastq(1000, False) for r in reads)

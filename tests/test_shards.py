@@ -139,15 +139,22 @@ class _OracleTrimmer(object):
     CPU oracle (TEST INFRASTRUCTURE: the GPU tests run the real FileTrimmer)."""
 
     def __init__(self, matching_sets, scoring_scheme_vals, end_size, end_threshold, extra_end_trim, min_trim_size,
-                 middle_threshold, extra_middle_trim_good_side, extra_middle_trim_bad_side, min_split_read_size):
+                 middle_threshold, extra_middle_trim_good_side, extra_middle_trim_bad_side, min_split_read_size,
+                 barcode_dir=None, forward_or_reverse_barcodes='forward', barcode_threshold=75.0, barcode_diff=5.0,
+                 require_two_barcodes=False, untrimmed=False, discard_unassigned=False):
         from custom_porechop_abi_amd.pipeline import FileTrimmer
         self.m, self.sc, self.E, self.thr = matching_sets, scoring_scheme_vals, end_size, end_threshold
         self.extra, self.min_trim, self.mthr = extra_end_trim, min_trim_size, middle_threshold
         self.good, self.bad = extra_middle_trim_good_side, extra_middle_trim_bad_side
         self.min_split, self.discard_middle, self.times = min_split_read_size, False, {}
         self.filter_reads = bool(matching_sets)
+        self.barcode_dir, self.fwd_rev = barcode_dir, forward_or_reverse_barcodes
+        self.bc = (barcode_threshold, barcode_diff, require_two_barcodes)
+        self.untrimmed, self.discard_unassigned = untrimmed, discard_unassigned
+        self.bc_names, self.bc_ids = {}, {}
         self.trim_file = FileTrimmer.trim_file.__get__(self)
         self._tick = FileTrimmer._tick.__get__(self)
+        self._write_bins = FileTrimmer._write_bins.__get__(self)
 
     def trim(self, batch):
         import numpy as np
@@ -156,8 +163,14 @@ class _OracleTrimmer(object):
         sink = io.StringIO()
         if self.m:
             P.find_adapters_at_read_ends(reads, self.m, 0, self.E, self.extra, self.thr, self.sc, sink, self.min_trim, 1,
-                                         False, 75.0, 5.0, False, None)
+                                         self.barcode_dir is not None, self.bc[0], self.bc[1], self.bc[2], self.fwd_rev)
             P.find_adapters_in_read_middles(reads, self.m, 0, self.mthr, self.good, self.bad, self.sc, sink, 1, False)
+        if self.barcode_dir is not None:
+            for r in reads:
+                if r.barcode_call != 'none' and r.barcode_call not in self.bc_ids:
+                    self.bc_ids[r.barcode_call] = len(self.bc_ids)
+                    self.bc_names[self.bc_ids[r.barcode_call]] = r.barcode_call
+            self.last_calls = np.array([self.bc_ids.get(r.barcode_call, -1) for r in reads], np.int32)
         st = np.array([r.start_trim_amount for r in reads], np.int32)
         et = np.array([r.end_trim_amount for r in reads], np.int32)
         cut_off = np.zeros(len(reads) + 1, np.int64)
@@ -173,7 +186,7 @@ class _OracleTrimmer(object):
         return st, et, cut_off, np.array(flat, np.int64), None, keep
 
 
-def _file_worker(rank, world, port, case_name, in_path, out_path, res_path):
+def _file_worker(rank, world, port, case_name, in_path, out_path, res_path, bins=None):
     import torch.distributed as dist
     from custom_porechop_abi_amd import engine, shards
     from tests import oracle_lib
@@ -188,8 +201,9 @@ def _file_worker(rank, world, port, case_name, in_path, out_path, res_path):
         counts = shards.trim_file_sharded(in_path, out_path, 'fastq', o['scoring'], o['end_size'], o['end_threshold'],
                                           o['extra_end_trim'], o['min_trim_size'], o['middle_threshold'], 10, 100, 1000,
                                           check_reads=o.get('check_reads', 10000),
-                                          adapter_threshold=o['adapter_threshold'], max_reads=7,
-                                          trimmer_factory=_OracleTrimmer)
+                                          adapter_threshold=o['adapter_threshold'], max_reads=3 if bins else 7,
+                                          trimmer_factory=_OracleTrimmer, barcode_dir=bins,
+                                          require_two_barcodes=bool(o.get('require_two')))
         with open(res_path % rank, 'w') as f:
             json.dump(counts, f)
     finally:
@@ -226,3 +240,30 @@ def test_sharded_file_pipeline_matches_reference(case_name, gz, tmp_path):
     assert counts[0] == counts[1] and counts[0]['reads_in'] == len(records)
     assert open(out_path).read() == _expected(case, records)
     assert not [f for f in os.listdir(str(tmp_path)) if f.startswith('.pcabi_part')]
+
+
+@pytest.mark.parametrize('gz', [False, True])
+@pytest.mark.parametrize('case_name', ['barcodes', 'barcodes_two'])
+def test_sharded_barcode_bins_match_reference(case_name, gz, tmp_path):
+    """-b through shards.trim_file_sharded at world size 2 (gloo): the kit direction from the
+    all-reduced set search (choose_barcoding_kit), per-rank bins with recorded byte spans,
+    stitched per bin by rank 0 in record order -- every bin == the reference's (G2)."""
+    import gzip
+    import torch.multiprocessing as mp
+    from tests.test_pipeline import _expected_bins
+    case = next(c for c in G2['cases'] if c['case'] == case_name)
+    records = _records(case)
+    text = ''.join('@%s\n%s\n+\n%s\n' % r for r in records)
+    in_path = str(tmp_path / ('in.fastq.gz' if gz else 'in.fastq'))
+    with (gzip.open(in_path, 'wt') if gz else open(in_path, 'w')) as f:
+        f.write(text)
+    bdir = str(tmp_path / 'bins')
+    res_path = str(tmp_path / 'counts%d.json')
+    mp.spawn(_file_worker, args=(2, _free_port(), case_name, in_path, str(tmp_path / 'out.fastq'), res_path, bdir),
+             nprocs=2, join=True)
+    counts = [json.load(open(res_path % r)) for r in range(2)]
+    exp = _expected_bins(case, records)
+    assert counts[0]['reads_in'] == len(records) and counts[0]['bins'] == sorted(exp)
+    assert sorted(os.listdir(bdir)) == sorted(k + '.fastq' for k in exp)
+    for name, txt in exp.items():
+        assert open(os.path.join(bdir, name + '.fastq')).read() == txt, name
