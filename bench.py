@@ -20,6 +20,11 @@ Also reported: roofline of the dominant kernel (k_align<24, true, PACKED>: the 2
 launches, its HBM traffic from the committed rocprofv3 PMC pass (profiles/traffic.json), and the
 reference SeqAn CPU path (oracle/_ref, compiled from the reference sources) timed on a bounded
 sample on this host's cores.
+
+At N = 1 the same line carries BASELINE.json's other configurations per GPU as sub-records
+(run_other_configs): the production schedule, the host-buffer path, middle scan at 8 kb and 20 kb,
+barcode demux, the configs[1] shape, file-to-file e2e, check_compatibility and approx_counter,
+each with its own oracle spot check and CPU baseline (--sub 0 skips them, --only-subs picks).
 """
 import argparse
 import ctypes
@@ -70,6 +75,7 @@ def parse():
                          'Rapid + RBK004, Barcode 1..12 (forward) + their 111 bp full rapid sequences')
     ap.add_argument('--middle-threshold', type=float, default=90.0)
     ap.add_argument('--middle-check', type=int, default=1000, help='middle: reads checked against the oracle loop')
+    ap.add_argument('--only-subs', default='', help='comma-separated sub-record names to run (default: all)')
     ap.add_argument('--sub', type=int, default=1,
                     help='endtrim at N=1: also time the middle workload (configs[2]) and the host-buffer path '
                          '(H2D + kernels + D2H) as sub-records of the same JSON line')
@@ -96,21 +102,30 @@ def main():
     from custom_porechop_abi_amd.engine import encode_adapters
     L = _lib.lib()
     _lib.check(L.pcabi_dev_set(local), 'pcabi_dev_set')
-    if args.workload == 'middle':
-        out = run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapters)
-        if rank == 0:
-            print(json.dumps(out), flush=True)
-        if dist is not None:
-            dist.destroy_process_group()
-        return
     args.local_device = local
-    if args.workload == 'compat':
-        return run_compat(args, rank, world, dist, torch, L, _lib)
-    if args.workload == 'kmer':
-        return run_kmer(args, rank, world, dist, torch, L, _lib, synth)
-    if args.workload == 'e2e':
-        return run_e2e(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapters)
+    ctx = (rank, world, dist, torch, L, _lib, A, synth, encode_adapters)
+    if args.workload == 'middle':
+        out = run_middle(args, *ctx)
+    elif args.workload == 'compat':
+        out = run_compat(args, rank, world, dist, torch, L, _lib)
+    elif args.workload == 'kmer':
+        out = run_kmer(args, rank, world, dist, torch, L, _lib, synth)
+    elif args.workload == 'e2e':
+        out = run_e2e(args, *ctx)
+    else:
+        out = run_endtrim(args, *ctx)
+        if out is not None and world == 1 and args.sub and args.workload == 'endtrim':
+            out.update(run_other_configs(args, ctx))
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
 
+
+def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapters):
+    """The headline (BASELINE.json metric): end trim of 100k reads/GPU x 50 adapter sets, or the
+    barcode demux workload (configs[3] shape per GPU) with --workload barcodes."""
+    local = args.local_device
     # ---- workload (host) ----
     barcodes = args.workload == 'barcodes'
     kit_n = 2 if args.kit == 'rapid12' else 1      # kit adapter sets ahead of the barcode sets
@@ -357,21 +372,20 @@ def main():
                                   '(pcabi_align_cross_dev_marked): register buckets side by side with the dominant one'}
         subs['host_path'] = run_host_path(args, L, _lib, buf, s_off, s_len, e_off, e_len, sides, d_sres, d_eres, d_st,
                                           d_et, n, n_sa, n_ea, stream, start_adps, end_adps)
-    if rank == 0 and world == 1 and args.sub and not barcodes:
-        margs = argparse.Namespace(**vars(args))
-        margs.steps, margs.warmup = max(5, args.steps // 2), 2
-        subs['middle'] = run_middle(margs, rank, world, None, torch, L, _lib, A, synth, encode_adapters)
 
     if rank == 0:
         value = world * n * args.steps / elapsed
         prof = load_traffic()
+        # the PMC traffic record belongs to the headline configuration's dominant launch only
+        headline = not barcodes and n == 100000 and len(sets) == 50 and args.end_size == 150
         out = {
             'metric': ('reads/sec trimmed + demultiplexed (ONT reads x %d barcode sets)' % (len(sets) - kit_n)
                        if barcodes and args.kit == 'pcr96' else
                        'reads/sec trimmed + demultiplexed (%s barcoding, %d barcodes + full sequences)'
                        % ('native' if args.kit == 'native12' else 'rapid', nb)
                        if barcodes
-                       else 'reads/sec trimmed (100k ONT reads x 50 adapter pairs)'),
+                       else 'reads/sec trimmed (100k ONT reads x 50 adapter pairs)' if n == 100000 and len(sets) == 50
+                       else 'reads/sec trimmed (%d ONT reads x %d adapter sets)' % (n, len(sets))),
             'value': round(value, 1),
             'unit': 'reads/s',
             'n_gpus': world,
@@ -394,11 +408,11 @@ def main():
                        'scoring': list(sc), 'parallelism': 'dp%d (read shards)' % world},
             'roofline': {'bound': 'valu', 'achieved': round(tops, 3), 'peak': round(VALU_PEAK_TOPS, 1),
                          'unit': 'Tops/s (int32 lane-ops)', 'frac': round(tops / VALU_PEAK_TOPS, 4),
-                         'traffic': prof.get('traffic_bytes_per_launch') if prof and not barcodes else None,
+                         'traffic': prof.get('traffic_bytes_per_launch') if prof and headline else None,
                          'kernel': DOM_KERNEL,
                          'launch_ms': round(launch_ms, 4), 'cells_per_launch': int(launch_cells),
                          'ops_per_cell': OPS_PER_CELL,
-                         'traffic_source': prof.get('source') if prof and not barcodes else None},
+                         'traffic_source': prof.get('source') if prof and headline else None},
             'hbm': {'achieved': round(gbs, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                     'frac': round(gbs / HBM_PEAK_GBS, 5), 'algorithmic_bytes_per_launch': int(launch_bytes),
                     'kernel': DOM_KERNEL},
@@ -410,9 +424,61 @@ def main():
             'setup_s': round(gen_s, 2),
         }
         out.update(subs)
-        print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+        return out
+    return None
+
+
+def run_other_configs(args, ctx):
+    """The default run's sub-records (N = 1): BASELINE.json's other configs, per GPU, each with its
+    own oracle spot check and CPU baseline, so one driver-timed line carries every workload.
+    A sub-record that fails reports its error instead of taking the headline down."""
+    rank, world, dist, torch, L, _lib, A, synth, encode_adapters = ctx
+
+    def sub(**kw):
+        s = argparse.Namespace(**vars(args))
+        s.steps, s.warmup = max(5, args.steps // 2), 2
+        for k, v in kw.items():
+            setattr(s, k, v)
+        return s
+
+    runs = [
+        # configs[2]: end trim + middle scan, 100k x 8 kb per GPU
+        ('middle', lambda: run_middle(sub(workload='middle'), rank, 1, None, torch, L, _lib, A, synth,
+                                      encode_adapters)),
+        # configs[4] per GPU: 100k x 20 kb, middle scan on (CPU sample scaled to the read length)
+        ('middle_20kb', lambda: run_middle(sub(workload='middle', mean_len=20000, steps=5,
+                                               cpu_sample=args.cpu_sample * 2 // 5, middle_check=300),
+                                           rank, 1, None, torch, L, _lib, A, synth, encode_adapters)),
+        # configs[3] per GPU: 100k reads x 96 forward barcode sets + SQK-NSK007, demux calls
+        ('barcodes', lambda: run_endtrim(sub(workload='barcodes', sub=0, cpu_sample=args.cpu_sample // 4), rank, 1,
+                                         None, torch, L, _lib, A, synth, encode_adapters)),
+        # configs[1] shape: a 10k-read batch against all 119 adapter sets
+        ('config2_10k_119sets', lambda: run_endtrim(sub(workload='endtrim', sub=0, reads=10000, sets=119,
+                                                        cpu_sample=args.cpu_sample // 4),
+                                                    rank, 1, None, torch, L, _lib, A, synth, encode_adapters)),
+        # the CLI path file to file (parse + trim + middle + write), 25k reads
+        ('e2e', lambda: run_e2e(sub(workload='e2e', reads=25000, steps=3, warmup=1), rank, 1, None, torch, L, _lib, A,
+                                synth, encode_adapters)),
+        # SURVEY §8(f) 3 and 4
+        ('compat', lambda: run_compat(sub(workload='compat', cpu_sample=args.cpu_sample // 4), rank, 1, None, torch,
+                                      L, _lib)),
+        ('kmer', lambda: run_kmer(sub(workload='kmer', steps=5, warmup=1), rank, 1, None, torch, L, _lib, synth)),
+    ]
+    subs = {}
+    for name, fn in runs:
+        if args.only_subs and name not in args.only_subs.split(','):
+            continue
+        t0 = time.perf_counter()
+        try:
+            rec = fn()
+            for k in ('n_gpus', 'higher_is_better', 'scaling', 'vs_baseline'):
+                rec.pop(k, None)
+        except Exception as ex:   # reported, never fatal for the headline line
+            rec = {'error': '%s: %s' % (type(ex).__name__, ex)}
+        rec['sub_wall_s'] = round(time.perf_counter() - t0, 2)
+        subs[name] = rec
+        print('sub-record %s: %.1f s' % (name, rec['sub_wall_s']), file=sys.stderr, flush=True)
+    return subs
 
 
 def run_host_path(args, L, _lib, buf, s_off, s_len, e_off, e_len, sides, d_sres, d_eres, d_st, d_et, n, n_sa, n_ea,
@@ -730,9 +796,8 @@ def run_compat(args, rank, world, dist, torch, L, _lib):
                           'parallelism': 'dp%d' % world},
                'cpu_baseline': cpu, 'gpu_vs_cpu': round(value / cpu['value'], 1) if cpu else None,
                'parity_spot_check': checked}
-        print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+        return out
+    return None
 
 
 def run_kmer(args, rank, world, dist, torch, L, _lib, synth):
@@ -809,9 +874,8 @@ def run_kmer(args, rank, world, dist, torch, L, _lib, synth):
                           'parallelism': 'dp%d' % world},
                'cpu_baseline': cpu, 'gpu_vs_cpu': round(value / cpu['value'], 1) if cpu else None,
                'parity_spot_check': checked}
-        print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+        return out
+    return None
 
 
 def write_fastq(path, reads, seed):
@@ -849,6 +913,8 @@ def run_e2e(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapters):
     reads = synth.make_reads(n, args.mean_len, seed=12345 + rank)
     write_fastq(in_path, reads, 99 + rank)
     in_bytes = os.path.getsize(in_path)
+    k_cpu = max(1, args.cpu_sample // 80) if rank == 0 and world == 1 and args.cpu_sample > 0 else 0
+    sample = reads[:k_cpu]
     del reads
     gen_s = time.time() - t0
 
@@ -889,6 +955,17 @@ def run_e2e(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapters):
             os.remove(p)
         except OSError:
             pass
+    cpu = None
+    if k_cpu:
+        # the reference's alignment work for the same reads (every end window x every adapter,
+        # then the whole-read middle loop), on a bounded sample; its FASTQ parse and write are not
+        # timed, so this is a lower bound on the reference CLI's time per read
+        ce = cpu_baseline(sample, sets, E, sc, args.cpu_threads)
+        cm = cpu_baseline_middle(sample, np.zeros((2, len(sample)), np.int32), mid_adps, sc, args.middle_threshold,
+                                 args.cpu_threads)
+        v = 1.0 / (1.0 / ce['value'] + 1.0 / cm['value'])
+        cpu = {'value': round(v, 3), 'unit': 'reads/s', 'cores': ce['cores'], 'kind': ce['kind'],
+               'sample': 'alignment work only (parse / write not timed): %s; then %s' % (ce['sample'], cm['sample'])}
     if rank == 0:
         step_s = elapsed / args.steps
         value = world * n * args.steps / elapsed
@@ -910,13 +987,13 @@ def run_e2e(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapters):
                                                              / args.steps), 2)),
             'input_MB_per_s': round(in_bytes / step_s / 1e6, 1),
             'output_bytes': out_bytes,
-            'cpu_baseline': None,
+            'cpu_baseline': cpu,
+            'gpu_vs_cpu': round(value / cpu['value'], 1) if cpu else None,
             'parity_spot_check': checked,
             'setup_s': round(gen_s, 2),
         }
-        print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+        return out
+    return None
 
 
 def middle_spot_check(reads, trims, hits, n_hits, mid_adps, sc, thr, k):
