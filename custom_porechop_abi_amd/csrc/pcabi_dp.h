@@ -900,6 +900,7 @@ namespace pk {
 template <int RPL>
 struct Lay {
     static constexpr bool WIDE = RPL > 64;
+    static constexpr bool TAGGED = false;
     static constexpr int SC_SH = WIDE ? 23 : 22;
     static constexpr int TB_SH = SC_SH - 2;
     static constexpr int C_SH = TB_SH - 8;
@@ -931,6 +932,7 @@ struct Lay {
 template <int RPL, int PASS>
 struct LayL {
     static constexpr bool WIDE = true;
+    static constexpr bool TAGGED = false;
     static constexpr int SC_SH = 20;
     static constexpr int TB_SH = 18;
     static constexpr int C_SH = 8;
@@ -947,6 +949,40 @@ struct LayL {
         const uint32_t nd = a & 255u;
         const int c = bj - (int)(((uint32_t)bj - (a >> C_SH)) & 1023u);
         return attr_start(c) | (nd << ATTR_B);
+    }
+};
+// Run-tagged buckets (affine gaps, adapters <= 31 bp: the end-window adapters): the tie-break
+// field widens to an 8-bit tag that COUNTS the extends of the current gap run, so the H key
+// needs no re-tagging before it is stored (one VALU op per cell less than Lay):
+//      [ score : 8 (signed) ][ tag : 8 ][ c mod 64 : 6 ][ nD : 5 ][ m : 5 ]
+//   H:  open = tag 0 (G = S + go as stored), extend = previous H tag + 1   -> extend wins ties
+//   V:  open = tag 128 (G + TVB), extend = previous V tag + 1              -> extend wins ties
+//   diagonal candidates tag 255                                            -> D > V > H on ties
+// H runs are bounded by the score range ((L ma - Smin) / |ge| extends, layt_ok checks < 128),
+// V runs by the rows (< 32), so H tags stay below every V tag and V tags below 255.
+template <int RPL>
+struct LayT {
+    static constexpr bool WIDE = false;
+    static constexpr bool TAGGED = true;
+    static constexpr int SC_SH = 24;
+    static constexpr int TB_SH = 16;
+    static constexpr int C_SH = 10;
+    static constexpr int MB = 32;
+    static constexpr int32_t TAG1 = 1 << TB_SH, TVB = 128 << TB_SH;
+    static constexpr int32_t TB1 = TAG1, TB2 = TVB;   // the untagged core's names (unused here)
+    static constexpr int32_t TB3 = 255 << TB_SH, TBM = 255 << TB_SH;
+    static constexpr int32_t INC_D = MB, INC_M = MB + 1;
+    static constexpr int SC_MIN = -128, SC_MAX = 127;
+    static PCABI_HD int32_t sc(int v) { return (int32_t)((uint32_t)v << SC_SH); }
+    static PCABI_HD int32_t start(int c) { return (int32_t)(((uint32_t)c & 63u) << C_SH); }
+    static PCABI_HD int score(int32_t k) { return k >> SC_SH; }
+    static PCABI_HD int tb(int32_t k) { return (k >> TB_SH) & 255; }
+    static PCABI_HD uint32_t attr(int32_t k) { return (uint32_t)k & ((1u << TB_SH) - 1u); }
+    static PCABI_HD uint32_t to_std(uint32_t a, int bj) {
+        const uint32_t cnt = a & ((1u << C_SH) - 1u);
+        const uint32_t m = cnt % (uint32_t)MB, nd = cnt / (uint32_t)MB;
+        const int c = bj - (int)(((uint32_t)bj - (a >> C_SH)) & 63u);
+        return attr_start(c) | (nd << ATTR_B) | m;
     }
 };
 constexpr int MAX_RPL = 88;
@@ -1014,6 +1050,33 @@ PCABI_HD bool long_ok(int L, int rpl, const Scoring &s) {
     return lo >= Y::SC_MIN && hi <= Y::SC_MAX;
 }
 
+// Range conditions of the run-tagged layout (pk::LayT): affine gaps, the packed ranges with an
+// 8-bit score field, counts <= 31, a reported path spanning < 64 columns (c mod 64), and every H
+// run shorter than 128 extends: an extend at (i, j) needs H(i, j-1) + ge >= S(i, j-1) + go >=
+// Smin + go, and a run that opened at <= Smax + go loses |ge| per extend, so a run holds at most
+// (Smax - Smin) / |ge| extends (Smax = max(L ma, 0), Smin = go + (L-1) ge; padding rows stay at
+// S = 0 and never extend).
+PCABI_HD bool layt_ok(int L, int rpl, const Scoring &s) {
+    using Y = pk::LayT<32>;
+    if (L < 1 || L > rpl || rpl > 32 || L > 31) return false;
+    if (!(s.go < 0 && s.ge < 0) || s.go == s.ge) return false;
+    if (packed_span_bound(L, s) > 63) return false;
+    const long long smin = (long long)s.go + (long long)(L - 1) * s.ge;
+    const long long lo_sub = s.mi < s.ma ? s.mi : s.ma;
+    const long long lo_gap = (long long)s.go + s.ge;
+    long long lo = smin + (lo_gap < lo_sub ? lo_gap : lo_sub);
+    const long long neg = pk::neg_score(s);
+    if (neg + s.ge < lo) lo = neg + s.ge;
+    if (neg < lo) lo = neg;
+    if (s.go < lo) lo = s.go;
+    long long hi = (long long)L * s.ma;
+    if (hi < 0) hi = 0;
+    if (s.ma > hi) hi = s.ma;
+    if (lo < Y::SC_MIN || hi > Y::SC_MAX) return false;
+    const long long smax = (long long)L * s.ma > 0 ? (long long)L * s.ma : 0;
+    return (smax - smin) / (-(long long)s.ge) + 1 < 128;
+}
+
 PCABI_HD bool packed_ok(int L, int rpl, const Scoring &s) {
     switch (rpl) {
 #define PCABI_PK(R) case R: return packed_ok_t<R>(L, s);
@@ -1034,6 +1097,7 @@ struct LanePacked {
     uint32_t battr;        // packed attribute
     int slt_last, ht_last, hp_last;
     int32_t k_ge, k_go, k_gev, k_geh, neg2;
+    int32_t k_gex, k_vo;   // run-tagged layout: gap extend + one tag, V-open tag
     // Last-row scout of the inner columns (column_tail): the best so far as ONE corrected key
     // (score | tag | attributes), its column, and the H-run descriptor at that column; the
     // fields above are materialised from them before the last column (materialize()).
@@ -1069,7 +1133,13 @@ struct LanePacked {
             if (s < RPL) diag_nx = G[s] + (PD > 0 ? t[s + 1] : tab(s + 1));
             int32_t hn, vn2, sn;
             bool hext = false, vext = false;
-            if (AFFINE) {
+            if (AFFINE && Y::TAGGED) {
+                const int32_t hx = HK[s] + k_gex, ho = G[s];
+                hn = hx > ho ? hx : ho;                  // tag > 0 iff extend
+                const int32_t vx = vup + k_gex, vo = gup + k_vo;
+                vn2 = vx > vo ? vx : vo;                 // tag > 128 iff extend
+                if (LAST || s == RPL) { hext = Y::tb(hn) != 0; vext = Y::tb(vn2) > 128; }
+            } else if (AFFINE) {
                 const int32_t hx = HK[s] + k_ge, ho = G[s];
                 hn = hx > ho ? hx : ho;                  // tb 1 iff extend
                 const int32_t vx = vup + k_ge, vo = gup;
@@ -1082,7 +1152,8 @@ struct LanePacked {
             }
             sn = max3i(diag, vn2, hn);
             const int t = Y::tb(sn);
-            const int slt = t == 3 ? LT_D : (t == 2 ? LT_V : LT_H);
+            const int slt = Y::TAGGED ? (t == 255 ? LT_D : (t >= 128 ? LT_V : LT_H))
+                                      : (t == 3 ? LT_D : (t == 2 ? LT_V : LT_H));
             if (LAST && s < RPL) {
                 const bool cont = AFFINE ? (vext || slt_up == LT_V) : (slt_up == LT_V);
                 const int vt = cont ? vt_up + 1 : 1;
@@ -1120,7 +1191,7 @@ struct LanePacked {
                 }
             }
             G[s] = (sn & ~Y::TBM) + k_go;
-            if (AFFINE) HK[s] = hn | Y::TB1;
+            if (AFFINE) HK[s] = Y::TAGGED ? hn : (hn | Y::TB1);
             gup = G[s];
             vup = vn2;
             diag = diag_nx;
@@ -1180,7 +1251,8 @@ struct LanePacked {
     PCABI_HD void column_tail(int32_t lv, int32_t lh, int32_t ls, int j, bool owned = true) {
         (void)lh;
         int32_t corr;
-        if (AFFINE) corr = std::max(lv | Y::TB3, ls & ~Y::TBM);
+        if (AFFINE && Y::TAGGED) corr = std::max(lv, ls & ~Y::TBM);   // V tags >= 128 > 0
+        else if (AFFINE) corr = std::max(lv | Y::TB3, ls & ~Y::TBM);
         else corr = ls;
         bool upd = corr > (bkey | ((1 << Y::SC_SH) - 1));   // score(corr) > score(bkey)
         if (GATE) upd = upd && owned;
@@ -1194,7 +1266,7 @@ struct LanePacked {
         const int t = Y::tb(bkey);
         int lt;
         if (bj == 0) lt = LT_NONE;                          // still the (L, 0) seed
-        else if (AFFINE) lt = t == 3 ? LT_V : LT_D;
+        else if (AFFINE) lt = (Y::TAGGED ? t != 0 : t == 3) ? LT_V : LT_D;
         else lt = t == 3 ? LT_D : (t == 2 ? LT_V : LT_H);
         bscore = Y::score(bkey);
         bi = L;
@@ -1242,10 +1314,12 @@ PCABI_HD Best packed_best(ReadFn &rd, int n, const TabFn &tabfn, int L, const Sc
     // linear gaps: V / H straight from G (= S + go), so the constants take go back out
     st.k_gev = Y::sc(sc.ge) - Y::sc(sc.go) + Y::TB2;
     st.k_geh = Y::sc(sc.ge) - Y::sc(sc.go) + Y::TB1;
+    st.k_gex = Y::sc(sc.ge) + (Y::TAGGED ? Y::TB1 : 0);
+    st.k_vo = Y::TAGGED ? Y::TB2 : 0;
 #pragma unroll
     for (int s = 1; s <= RPL; ++s) {
         st.G[s] = Y::start(off - s) + st.k_go;    // padded (s, 0) reaches real (0, off - s)
-        st.HK[s] = neg | Y::TB1;
+        st.HK[s] = Y::TAGGED ? neg : (neg | Y::TB1);
     }
     st.neg2 = neg | Y::TB2;
     st.bkey = Y::start(-L);                       // the (L, 0) seed: score 0, c = -L
@@ -1274,11 +1348,11 @@ PCABI_HD Best packed_best(ReadFn &rd, int n, const TabFn &tabfn, int L, const Sc
     return b;
 }
 
-template <int RPL, bool AFFINE, bool CHUNK = false, typename ReadFn, typename TabFn>
+template <int RPL, bool AFFINE, bool CHUNK = false, typename Y = pk::Lay<RPL>, typename ReadFn, typename TabFn>
 PCABI_HD Result align_lane_packed(ReadFn &rd, int n, const TabFn &tabfn, int L, const Scoring sc, int own_lo = 1,
                                   int own_hi = -1) {
     int n_fin;
-    const Best b = packed_best<RPL, AFFINE, CHUNK>(rd, n, tabfn, L, sc, own_lo, own_hi, n_fin);
+    const Best b = packed_best<RPL, AFFINE, CHUNK, Y>(rd, n, tabfn, L, sc, own_lo, own_hi, n_fin);
     return finish(b, L, n_fin);
 }
 

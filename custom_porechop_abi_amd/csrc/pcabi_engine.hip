@@ -544,7 +544,8 @@ bool chunkable(int b, bool packed) {
            kBuckets[b].kind == STRIPED || (kBuckets[b].kind == FAST && packed);
 }
 
-int dispatch(int b, const KParams &p, bool affine, hipStream_t st, bool packed) {
+// packed: bucket_pack_mode (0 untagged cores off, 1 packed key layout, 2 run-tagged layout)
+int dispatch(int b, const KParams &p, bool affine, hipStream_t st, int packed) {
     if (kBuckets[b].kind == STRIPED) return launch_striped(p, affine, st);
     const int64_t tiles8 = (p.n_win + 8 * 256 - 1) / (8 * 256) * 8;   // window tiles, padded to 8
     dim3 grid = p.task_win ? dim3((unsigned)((p.n_waves + 3) / 4))
@@ -553,7 +554,7 @@ int dispatch(int b, const KParams &p, bool affine, hipStream_t st, bool packed) 
     if (d.kind == LONG || d.kind == WIDE || (d.kind == FAST && packed && d.rpl > 32))
         dispatch_packed_large(d.rpl, d.kind == LONG, p, affine, grid, st);
     else if (d.kind == FAST && packed)
-        dispatch_packed_small(d.rpl, p, affine, grid, st);
+        dispatch_packed_small(d.rpl, p, affine, grid, st, packed == 2);
     else
         dispatch_fast(d.rpl, d.kind == GENERIC, p, affine, grid, st);
     return 0;
@@ -567,6 +568,21 @@ bool bucket_packed_ok(int b, const std::vector<int32_t> &lens, const pcabi::Scor
     for (int32_t L : lens)
         if (!pcabi::packed_ok(L, kBuckets[b].rpl, sc)) return false;
     return true;
+}
+
+// How k_align serves a bucket: 0 = not packed (fast / generic cores), 1 = packed key layout,
+// 2 = the run-tagged layout (pcabi_dp.h pk::LayT: affine buckets of <= 32 rows whose adapters all
+// pass layt_ok; one VALU op per cell less). PCABI_TAGGED=0 keeps the untagged layout (A/B runs).
+int bucket_pack_mode(int b, const std::vector<int32_t> &lens, const pcabi::Scoring &sc) {
+    if (!bucket_packed_ok(b, lens, sc)) return 0;
+    static const bool tagged_on = [] {
+        const char *e = std::getenv("PCABI_TAGGED");
+        return !(e && e[0] == '0');
+    }();
+    if (!tagged_on || kBuckets[b].kind != FAST || kBuckets[b].rpl > 32) return 1;
+    for (int32_t L : lens)
+        if (!pcabi::layt_ok(L, kBuckets[b].rpl, sc)) return 1;
+    return 2;
 }
 
 // Host-side layout of a bucket's adapter table.
@@ -955,7 +971,7 @@ int align_host_impl(int device, const uint8_t *codes, int64_t codes_len, const i
     struct CrossLaunch {
         int b;
         KParams p;
-        bool packed;
+        int packed;   // bucket_pack_mode
     };
     std::vector<CrossLaunch> cross;
     for (int b = 0; b < kNumBuckets; ++b) {
@@ -991,7 +1007,7 @@ int align_host_impl(int device, const uint8_t *codes, int64_t codes_len, const i
                 p.tile_off = (const int64_t *)e.toff.p;
             }
             // launched below, side by side once every bucket's table is on its way
-            if (n_win > 0) cross.push_back({b, p, bucket_packed_ok(b, h.len, sc)});
+            if (n_win > 0) cross.push_back({b, p, bucket_pack_mode(b, h.len, sc)});
         } else {
             tw.clear(); to.clear(); wa.clear();
             for (int k = 0; k < nb; ++k) {
@@ -1016,7 +1032,7 @@ int align_host_impl(int device, const uint8_t *codes, int64_t codes_len, const i
             p.task_out = (const int32_t *)e.tasks_out.p;
             p.wave_adp = (const int32_t *)e.wave_adp.p;
             p.n_waves = (int64_t)wa.size();
-            if (int rc = dispatch(b, p, affine, e.stream, bucket_packed_ok(b, h.len, sc))) return rc;
+            if (int rc = dispatch(b, p, affine, e.stream, bucket_pack_mode(b, h.len, sc))) return rc;
             // host vectors are reused by the next bucket: drain before overwriting
             HIP_TRY(hipStreamSynchronize(e.stream));
         }
@@ -1410,7 +1426,7 @@ int pcabi_align_cross_dev_marked(const uint32_t *tiles, const int64_t *tile_off,
         const hipStream_t st = fj.at(k);
         // the largest bucket runs on the caller's stream (k == 0): the optional events bracket it
         if (k == 0 && ev_begin) HIP_TRY(hipEventRecord((hipEvent_t)ev_begin, st));
-        if (int rc = dispatch(b, p, affine, st, bucket_packed_ok(b, adps->lens[b], p.sc))) {
+        if (int rc = dispatch(b, p, affine, st, bucket_pack_mode(b, adps->lens[b], p.sc))) {
             (void)fj.end();
             return rc;
         }
@@ -1608,7 +1624,7 @@ int device_plan_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_off,
                 rc = dispatch_chunk(b, p, scr.go != scr.ge, fj.at(k));
             } else {
                 p.task_chunk = nullptr;   // whole windows
-                rc = dispatch(b, p, scr.go != scr.ge, fj.at(k), bucket_packed_ok(b, adps->lens[b], scr));
+                rc = dispatch(b, p, scr.go != scr.ge, fj.at(k), bucket_pack_mode(b, adps->lens[b], scr));
             }
             if (rc) {
                 (void)fj.end();
@@ -1899,7 +1915,7 @@ int filtered_first_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_o
                 rc = dispatch_chunk(b, p, scr.go != scr.ge, fj.at(k));
             } else {
                 p.task_chunk = nullptr;   // whole windows
-                rc = dispatch(b, p, scr.go != scr.ge, fj.at(k), bucket_packed_ok(b, adps->lens[b], scr));
+                rc = dispatch(b, p, scr.go != scr.ge, fj.at(k), bucket_pack_mode(b, adps->lens[b], scr));
             }
             if (rc) {
                 (void)fj.end();

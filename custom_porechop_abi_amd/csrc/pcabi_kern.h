@@ -40,7 +40,8 @@ int fail(int code, const std::string &msg);
 // STRIPED (pcabi_dp.h align_lane_striped, k_align_striped): every adapter longer than kMaxRPL, any
 // scoring, rows in stripes of kStripeRows with the boundary row in global scratch; its table pads
 // every adapter to the bucket's longest, rounded up to kStripeTab rows (pcabi_adapters::rt).
-enum Kind { FAST = 0, GENERIC = 1, PACKED = 2, WIDE = 3, LONG = 4, STRIPED = 5 };
+enum Kind { FAST = 0, GENERIC = 1, PACKED = 2, WIDE = 3, LONG = 4, STRIPED = 5,
+            TAGGED = 6 };   // TAGGED: PACKED with the run-tagged key layout (pcabi_dp.h pk::LayT), a launch-time choice
 struct BucketDef {
     int rpl;
     Kind kind;
@@ -153,7 +154,7 @@ struct LdsRow {
 };
 
 // This wave's packed-core substitution table (every lane of the block reaches the barrier).
-template <int RPL>
+template <int RPL, typename Y = pcabi::pk::Lay<RPL>>
 __device__ __forceinline__ void fill_wave_tab(const KParams &p, int a_local, int L, int32_t *wave_tab) {
     const int off = RPL - L;
     const int lane = threadIdx.x & 63;
@@ -161,7 +162,7 @@ __device__ __forceinline__ void fill_wave_tab(const KParams &p, int a_local, int
         const int c = e / RPL, srow = e % RPL + 1;
         const uint32_t *ap = p.adp_pad + (int64_t)a_local * (RPL / 4);
         auto code = [&](int sl) { return (int)((ap[(sl - 1) / 4] >> (8 * ((sl - 1) & 3))) & 0xFFu); };
-        wave_tab[e] = pcabi::pk::sub_key<RPL>(srow, c, code, off, p.sc);
+        wave_tab[e] = pcabi::pk::sub_key<RPL, decltype(code), Y>(srow, c, code, off, p.sc);
     }
     __syncthreads();
 }
@@ -189,6 +190,7 @@ __device__ __forceinline__ void run_lane(const KParams &p, int a_local, int64_t 
     if constexpr (KIND != LONG) adp.load(p.adp_pad + (int64_t)a_local * (RPL / 4));
     const int L = __builtin_amdgcn_readfirstlane(p.adp_len[a_local]);
     if constexpr (KIND == PACKED) fill_wave_tab<RPL>(p, a_local, L, wave_tab);
+    if constexpr (KIND == TAGGED) fill_wave_tab<RPL, pcabi::pk::LayT<RPL>>(p, a_local, L, wave_tab);
     if constexpr (KIND == LONG) fill_wave_tab_long<RPL>(p, a_local, L, wave_tab);
     if (w < 0) return;
     const int n = p.win_len[w];
@@ -206,6 +208,10 @@ __device__ __forceinline__ void run_lane(const KParams &p, int a_local, int64_t 
         if constexpr (KIND == PACKED) {
             auto tabfn = [&](int rc) { return LdsRow{wave_tab + rc * RPL}; };
             r = pcabi::align_lane_packed<(RPL <= pcabi::pk::MAX_RPL ? RPL : 4), AFFINE>(rd, n, tabfn, L, p.sc);
+        } else if constexpr (KIND == TAGGED) {
+            static_assert(RPL <= 32 && AFFINE, "run-tagged layout: affine buckets of <= 32 rows");
+            auto tabfn = [&](int rc) { return LdsRow{wave_tab + rc * RPL}; };
+            r = pcabi::align_lane_packed<RPL, true, false, pcabi::pk::LayT<RPL>>(rd, n, tabfn, L, p.sc);
         } else if constexpr (KIND == LONG) {
             WindowReader rd1 = rd;   // the second pass reads the window again from its start
             auto tab0 = [&](int rc) { return LdsRow{wave_tab + rc * RPL}; };
@@ -234,7 +240,9 @@ __device__ __forceinline__ void run_lane(const KParams &p, int a_local, int64_t 
 //  cross: 1-D grid of (window tile of 256, adapter) blocks in XCD-aware order; lane = window
 //  pairs: grid (ceil(n_waves/4)); wave = one adapter, lanes = host-grouped tasks
 template <int KIND, int RPL>
-constexpr int wave_tab_ints() { return KIND == PACKED ? kTabW * RPL : (KIND == LONG ? 2 * kTabW * RPL : 1); }
+constexpr int wave_tab_ints() {
+    return (KIND == PACKED || KIND == TAGGED) ? kTabW * RPL : (KIND == LONG ? 2 * kTabW * RPL : 1);
+}
 
 template <int RPL, bool AFFINE, int KIND>
 __global__ __launch_bounds__(256, PCABI_WAVES) void k_align(KParams p) {
@@ -479,7 +487,8 @@ void launch(const KParams &p, bool affine, dim3 grid, hipStream_t st) {
 // ---- kernel translation units (pcabi_k_*.hip) ----------------------------------------------
 // k_align launches by core, grid as k_align expects (cross: XCD-ordered tiles x adapters;
 // pairs: ceil(waves / 4) blocks).
-void dispatch_packed_small(int rpl, const KParams &p, bool affine, dim3 grid, hipStream_t st);  // PACKED <= 32 rows
+// PACKED <= 32 rows; tagged (affine only): the run-tagged layout, every adapter passing layt_ok
+void dispatch_packed_small(int rpl, const KParams &p, bool affine, dim3 grid, hipStream_t st, bool tagged);
 void dispatch_packed_large(int rpl, bool long_kind, const KParams &p, bool affine, dim3 grid,
                            hipStream_t st);                                                   // PACKED 36..88, LONG
 void dispatch_fast(int rpl, bool generic, const KParams &p, bool affine, dim3 grid, hipStream_t st);

@@ -100,6 +100,41 @@ static void run_packed(const char *read, int n, const char *adp, int L, pcabi::S
     out[4] = r.score; out[5] = r.m; out[6] = r.l1; out[7] = r.l2;
 }
 
+// run-tagged packed core (pk::LayT, affine buckets <= 32 rows); -3 if layt_ok fails
+template <int RPL>
+static void run_tagged(const char *read, int n, const char *adp, int L, pcabi::Scoring sc, int *out) {
+    using Y = pcabi::pk::LayT<RPL>;
+    const int off = RPL - L;
+    auto rd = [&](int j) { return j <= n ? dna5((unsigned char)read[j - 1]) : 4; };
+    auto ad = [&](int s) { return s <= off ? pcabi::PAD_CODE : dna5((unsigned char)adp[s - off - 1]); };
+    int32_t tab[pcabi::pk::TAB_W * RPL];
+    for (int c = 0; c < pcabi::pk::TAB_W; ++c)
+        for (int s = 1; s <= RPL; ++s) tab[c * RPL + s - 1] = pcabi::pk::sub_key<RPL, decltype(ad), Y>(s, c, ad, off, sc);
+    struct Row {
+        const int32_t *p;
+        int32_t operator()(int s) const { return p[s - 1]; }
+        void quad(int q, int32_t *dst) const { for (int k = 0; k < 4; ++k) dst[k] = p[4 * q + k]; }
+    };
+    auto tabfn = [&](int rc) { return Row{tab + rc * RPL}; };
+    pcabi::Result r = pcabi::align_lane_packed<RPL, true, false, Y>(rd, n, tabfn, L, sc);
+    out[0] = r.rs; out[1] = r.re; out[2] = r.as; out[3] = r.ae;
+    out[4] = r.score; out[5] = r.m; out[6] = r.l1; out[7] = r.l2;
+}
+
+extern "C" int pcabi_model_align_tagged(const char *read, int n, const char *adp, int L, int rpl,
+                                        int ma, int mi, int go, int ge, int *out) {
+    pcabi::Scoring sc{ma, mi, go, ge};
+    if (L <= 0 || n <= 0) return -1;
+    if (!pcabi::layt_ok(L, rpl, sc)) return -3;
+    switch (rpl) {
+#define C(R) case R: run_tagged<R>(read, n, adp, L, sc, out); break;
+    C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32)
+#undef C
+    default: return -2;
+    }
+    return 0;
+}
+
 // packed-key core at an explicit register bucket (extra padding rows); -3 if out of range
 extern "C" int pcabi_model_align_packed_rpl(const char *read, int n, const char *adp, int L, int rpl,
                                             int ma, int mi, int go, int ge, int *out) {

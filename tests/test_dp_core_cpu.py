@@ -27,6 +27,7 @@ def model():
             [ctypes.c_int] * 4 + [ctypes.c_void_p]
     L.pcabi_model_align_packed_rpl.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
                                                ctypes.c_int] + [ctypes.c_int] * 4 + [ctypes.c_void_p]
+    L.pcabi_model_align_tagged.argtypes = L.pcabi_model_align_packed_rpl.argtypes
     L.pcabi_model_filter.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p,
                                      ctypes.c_int, ctypes.c_int] + [ctypes.c_int] * 4 + [ctypes.c_void_p]
     L.pcabi_model_filter_threshold.argtypes = [ctypes.c_int, ctypes.c_double] + [ctypes.c_int] * 4
@@ -163,6 +164,61 @@ def test_packed_core_extra_padding_rows(model):
         assert rc == 0 and list(out) == oracle_lib.align(r, a, sc), (sc, r, a, rpl)
         n_checked += 1
     assert n_checked > 2000
+
+
+def _tagged(model, r, a, rpl, sc):
+    out = (ctypes.c_int * 8)()
+    rc = model.pcabi_model_align_tagged(r.encode(), len(r), a.encode(), len(a), rpl, *sc, out)
+    return rc, list(out)
+
+
+def test_tagged_core(model):
+    """The run-tagged packed layout (pk::LayT: 8-bit run-counting tie tags, so the H key is
+    stored without re-tagging) against the oracle: tie-heavy alphabets, every small bucket with
+    extra padding rows, long gap runs (adapters embedded with long insertions / deletions), and
+    the reference's golden rows; layt_ok must accept the default scheme up to 25 bp (the span
+    bound L + 3L/2 reaches 64 at 26)."""
+    rng = random.Random(23)
+    schemes = [(3, -6, -5, -2), (1, -1, -3, -1), (3, -6, -2, -5), (5, -4, -8, -6), (2, -3, -5, -1)]
+    for L in range(1, 26):
+        assert model.pcabi_model_align_tagged(b'A', 1, b'A' * L, L, (L + 3) & ~3, 3, -6, -5, -2,
+                                              (ctypes.c_int * 8)()) == 0
+    n_checked = 0
+    for k in range(6000):
+        sc = schemes[k % len(schemes)]
+        al = rng.choice(['A', 'AT', 'ACGT', 'ACGTN'])
+        L = rng.randint(1, 31)
+        rpl = rng.choice([r for r in range(4, 33, 4) if r >= L])
+        a = ''.join(rng.choice(al) for _ in range(L))
+        if k % 3 == 0:
+            r = ''.join(rng.choice(al) for _ in range(rng.randint(0, 60)))
+            b = list(a)
+            for _ in range(rng.randint(0, 3)):
+                p = rng.randint(0, len(b))
+                if rng.random() < 0.5:
+                    b[p:p] = [rng.choice(al) for _ in range(rng.randint(1, 30))]
+                else:
+                    del b[p:p + rng.randint(1, 8)]
+            r += ''.join(b) + ''.join(rng.choice(al) for _ in range(rng.randint(0, 60)))
+            r = r or 'A'
+        else:
+            r = ''.join(rng.choice(al) for _ in range(rng.randint(1, 260)))
+        rc, res = _tagged(model, r, a, rpl, sc)
+        if rc == -3:
+            continue
+        assert rc == 0 and res == oracle_lib.align(r, a, sc), (sc, r, a, rpl)
+        n_checked += 1
+    assert n_checked > 4000
+    n_gold = 0
+    for sc, r, a, exp in golden_lib.g1_rows():
+        if not r or not a or len(a) > 31:
+            continue
+        rc, res = _tagged(model, r, a, (len(a) + 3) & ~3, sc)
+        if rc == -3:
+            continue
+        assert rc == 0 and _fmt(res) == exp, (sc, r, a, exp, res)
+        n_gold += 1
+    assert n_gold > 1000
 
 
 def test_packed_wide_core(model):
