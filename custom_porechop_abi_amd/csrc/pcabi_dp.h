@@ -85,7 +85,7 @@ PCABI_HD uint32_t attr_start(int c) { return (uint32_t)(c + ATTR_CBIAS) << ATTR_
 PCABI_HD int span_bound(int L, int ma, int mi, int go, int ge) {
     if (go >= 0 || ge >= 0) return -1;
     const int g = (-go < -ge) ? -go : -ge;
-    const int d = (ma > mi ? ma - mi : 0) + 1;
+    const int d = (ma > mi ? ma - mi : mi - ma) + 1;   // mismatch may outscore match
     const long long t = ((long long)L * d + g - 1) / g + 2;
     const long long b = (long long)L + 2 * t + 4;
     return b > (1 << 30) ? (1 << 30) : (int)b;
@@ -97,6 +97,10 @@ enum : int { LT_NONE = 0, LT_D = 1, LT_V = 2, LT_H = 3 };
 struct Scoring {
     int ma, mi, go, ge;  // match, mismatch, gap open, gap extend (Python order)
 };
+
+// The most a diagonal column can add: match, or mismatch when a scheme scores it higher (the
+// reference accepts any --scoring_scheme; every range and span bound below uses this).
+PCABI_HD int best_sub(const Scoring &s) { return s.ma > s.mi ? s.ma : s.mi; }
 
 // What the scout keeps for the current best end cell.
 struct Best {
@@ -998,7 +1002,8 @@ PCABI_HD int neg_score(const Scoring &s) { return s.go - s.ge - 1; }
 // horizontal moves (each costing >= g) are paid for by at most L diagonal matches.
 PCABI_HD int packed_span_bound(int L, const Scoring &s) {
     const int g = (-s.go < -s.ge) ? -s.go : -s.ge;
-    return L + (s.ma > 0 ? (s.ma * L) / g : 0);
+    const int p = best_sub(s);
+    return L + (p > 0 ? (p * L) / g : 0);
 }
 
 // Range conditions of the packed core for an adapter of L bases in register bucket rpl:
@@ -1022,9 +1027,9 @@ PCABI_HD bool packed_ok_t(int L, const Scoring &s) {
     if (neg + s.ge < lo) lo = neg + s.ge;
     if (neg < lo) lo = neg;
     if (s.go < lo) lo = s.go;
-    long long hi = (long long)L * s.ma;
+    long long hi = (long long)L * best_sub(s);
     if (hi < 0) hi = 0;
-    if (s.ma > hi) hi = s.ma;
+    if (best_sub(s) > hi) hi = best_sub(s);
     if (!Y::WIDE && L > 63) return false;
     return lo >= Y::SC_MIN && hi <= Y::SC_MAX;
 }
@@ -1044,9 +1049,9 @@ PCABI_HD bool long_ok(int L, int rpl, const Scoring &s) {
     if (neg + s.ge < lo) lo = neg + s.ge;
     if (neg < lo) lo = neg;
     if (s.go < lo) lo = s.go;
-    long long hi = (long long)L * s.ma;
+    long long hi = (long long)L * best_sub(s);
     if (hi < 0) hi = 0;
-    if (s.ma > hi) hi = s.ma;
+    if (best_sub(s) > hi) hi = best_sub(s);
     return lo >= Y::SC_MIN && hi <= Y::SC_MAX;
 }
 
@@ -1069,11 +1074,11 @@ PCABI_HD bool layt_ok(int L, int rpl, const Scoring &s) {
     if (neg + s.ge < lo) lo = neg + s.ge;
     if (neg < lo) lo = neg;
     if (s.go < lo) lo = s.go;
-    long long hi = (long long)L * s.ma;
+    long long hi = (long long)L * best_sub(s);
     if (hi < 0) hi = 0;
-    if (s.ma > hi) hi = s.ma;
+    if (best_sub(s) > hi) hi = best_sub(s);
     if (lo < Y::SC_MIN || hi > Y::SC_MAX) return false;
-    const long long smax = (long long)L * s.ma > 0 ? (long long)L * s.ma : 0;
+    const long long smax = hi;
     return (smax - smin) / (-(long long)s.ge) + 1 < 128;
 }
 
@@ -1415,7 +1420,7 @@ inline int filter_threshold(int L, double threshold_pct, const Scoring &sc) {
 // for the pass-through padding rows).
 PCABI_HD bool filter_ok(int rpl, const Scoring &s) {
     if (rpl > MAX_RPL || !(s.go < 0 && s.ge < 0)) return false;
-    const int hi = rpl * (s.ma > 0 ? s.ma : 0);
+    const int hi = rpl * (best_sub(s) > 0 ? best_sub(s) : 0);
     const int lo = rpl * (s.mi < 0 ? s.mi : 0) + 4 * (s.go < s.ge ? s.go : s.ge);
     return hi < 4000 && lo > -4000 && s.go > -2000 && s.ge > -2000;
 }
@@ -1442,7 +1447,7 @@ struct Chunk {
 inline int chunk_span(int L, int T, const Scoring &sc) {   // D, or -1 when chunking does not apply
     const int g = std::min(-sc.go, -sc.ge);
     if (g <= 0 || T <= 0 || sc.ma <= 0 || L <= 0) return -1;
-    return L + (L * sc.ma - T + g - 1) / g + 2;
+    return L + (L * best_sub(sc) - T + g - 1) / g + 2;
 }
 
 template <typename F>

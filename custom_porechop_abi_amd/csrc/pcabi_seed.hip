@@ -329,7 +329,7 @@ __device__ __forceinline__ int band_best(const uint8_t *rd, int len, const uint8
             int mx = S[0];
 #pragma unroll
             for (int x = 1; x < W; ++x) mx = max(mx, S[x]);
-            const int ub = mx + sc.ma * (L - i);
+            const int ub = mx + pcabi::best_sub(sc) * (L - i);
             if (ub < T) return ub;
         }
     }
