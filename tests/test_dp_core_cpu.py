@@ -209,6 +209,14 @@ def test_tagged_core(model):
         assert rc == 0 and res == oracle_lib.align(r, a, sc), (sc, r, a, rpl)
         n_checked += 1
     assert n_checked > 4000
+    # the longest gap runs: nothing matches, so H / V extend as far as the scores allow
+    for sc in schemes:
+        for L in (1, 8, 17, 24, 25, 31):
+            for n in (1, 60, 150, 400):
+                a, r = 'C' * L, 'A' * n
+                rc, res = _tagged(model, r, a, (L + 3) & ~3, sc)
+                if rc == 0:
+                    assert res == oracle_lib.align(r, a, sc), (sc, L, n)
     n_gold = 0
     for sc, r, a, exp in golden_lib.g1_rows():
         if not r or not a or len(a) > 31:
