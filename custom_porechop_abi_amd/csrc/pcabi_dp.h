@@ -962,7 +962,7 @@ struct LayL {
 //   H:  open = tag 0 (G = S + go as stored), extend = previous H tag + 1   -> extend wins ties
 //   V:  open = tag 128 (G + TVB), extend = previous V tag + 1              -> extend wins ties
 //   diagonal candidates tag 255                                            -> D > V > H on ties
-// H runs are bounded by the score range ((L ma - Smin) / |ge| extends, layt_ok checks < 128),
+// H runs are bounded by the score range ((Smax - Smin) / |ge| extends, layt_ok checks < 128),
 // V runs by the rows (< 32), so H tags stay below every V tag and V tags below 255.
 template <int RPL>
 struct LayT {
@@ -1059,7 +1059,7 @@ PCABI_HD bool long_ok(int L, int rpl, const Scoring &s) {
 // 8-bit score field, counts <= 31, a reported path spanning < 64 columns (c mod 64), and every H
 // run shorter than 128 extends: an extend at (i, j) needs H(i, j-1) + ge >= S(i, j-1) + go >=
 // Smin + go, and a run that opened at <= Smax + go loses |ge| per extend, so a run holds at most
-// (Smax - Smin) / |ge| extends (Smax = max(L ma, 0), Smin = go + (L-1) ge; padding rows stay at
+// (Smax - Smin) / |ge| extends (Smax = max(L best_sub, 0), Smin = go + (L-1) ge; padding rows stay at
 // S = 0 and never extend).
 PCABI_HD bool layt_ok(int L, int rpl, const Scoring &s) {
     using Y = pk::LayT<32>;
