@@ -68,6 +68,9 @@ constexpr int kMaxEnt = 8192;      // probe entries / distinct probes kept in LD
 #define PCABI_SEED_BUF 256
 #endif
 
+#ifndef PCABI_BAND_EXIT
+#define PCABI_BAND_EXIT 4   // rows between the banded DP's early-exit checks
+#endif
 constexpr int kBuf = PCABI_SEED_BUF;   // staged tasks per block and class
 constexpr int kLdsMax = 64 * 1024; // per block: probe tables + stage
 constexpr int kNeg = -(1 << 20);
@@ -325,7 +328,7 @@ __device__ __forceinline__ int band_best(const uint8_t *rd, int len, const uint8
         for (int x = 0; x + 1 < W; ++x) R[x] = R[x + 1];
         const int jn = i + 1 + d0 + E;
         R[W - 1] = (!CHECK || (jn >= 1 && jn <= len)) ? rd[jn - 1] : 7;
-        if (!CHECK && (i & 3) == 0) {
+        if (!CHECK && (i % PCABI_BAND_EXIT) == 0) {
             int mx = S[0];
 #pragma unroll
             for (int x = 1; x < W; ++x) mx = max(mx, S[x]);
