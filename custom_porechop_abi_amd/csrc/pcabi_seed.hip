@@ -69,7 +69,7 @@ constexpr int kMaxEnt = 8192;      // probe entries / distinct probes kept in LD
 #endif
 
 #ifndef PCABI_BAND_EXIT
-#define PCABI_BAND_EXIT 4   // rows between the banded DP's early-exit checks
+#define PCABI_BAND_EXIT 1   // rows between the banded DP's early-exit checks (1: every row, r02 A/B)
 #endif
 constexpr int kBuf = PCABI_SEED_BUF;   // staged tasks per block and class
 constexpr int kLdsMax = 64 * 1024; // per block: probe tables + stage
