@@ -78,6 +78,8 @@ def parse():
                          'Rapid + RBK004, Barcode 1..12 (forward) + their 111 bp full rapid sequences')
     ap.add_argument('--middle-threshold', type=float, default=90.0)
     ap.add_argument('--middle-check', type=int, default=1000, help='middle: reads checked against the oracle loop')
+    ap.add_argument('--check-phase-check', type=int, default=400,
+                    help='check_phase: check reads whose device reduction is compared with the oracle')
     ap.add_argument('--only-subs', default='', help='comma-separated sub-record names to run (default: all)')
     ap.add_argument('--sub', type=int, default=1,
                     help='endtrim at N=1: also time the middle workload (configs[2]) and the host-buffer path '
@@ -117,6 +119,14 @@ def main():
         out = run_e2e(args, *ctx)
     else:
         out = run_endtrim(args, *ctx)
+        if world > 1 and args.workload == 'endtrim' and args.sub:
+            # the path's one collective (the adapter-set search's MAX all-reduce), timed at every N
+            # with every rank taking part; at N = 1 it is one of run_other_configs' sub-records
+            cp = run_check_phase(args, *ctx)
+            if out is not None:
+                for k in ('n_gpus', 'higher_is_better', 'scaling', 'vs_baseline'):
+                    cp.pop(k, None)
+                out['check_phase'] = cp
         if out is not None and world == 1 and args.sub and args.workload == 'endtrim':
             out.update(run_other_configs(args, ctx))
     if rank == 0:
@@ -453,6 +463,9 @@ def run_other_configs(args, ctx):
         return s
 
     runs = [
+        # the adapter-set search (configs[1]'s check phase: 10k reads x 119 sets) and its MAX
+        # all-reduce (here over one rank)
+        ('check_phase', lambda: run_check_phase(sub(), rank, 1, None, torch, L, _lib, A, synth, encode_adapters)),
         # configs[2]: end trim + middle scan, 100k x 8 kb per GPU
         ('middle', lambda: run_middle(sub(workload='middle'), rank, 1, None, torch, L, _lib, A, synth,
                                       encode_adapters)),
@@ -490,6 +503,170 @@ def run_other_configs(args, ctx):
         subs[name] = rec
         print('sub-record %s: %.1f s' % (name, rec['sub_wall_s']), file=sys.stderr, flush=True)
     return subs
+
+
+def run_check_phase(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapters, n_check=10000):
+    """The adapter-set search (porechop_abi.py:200-245, nanopore_read.py:158-173), the path's one
+    collective: the job's first n_check reads (every rank generates the same
+    seeded set) against every non-"full sequence" set of the database (119 sets: their distinct
+    start and end sequences), start / end windows of 150 bp. Rank r takes its contiguous shard
+    of the check reads. One step, inputs resident in HBM:
+        windows -> tiles -> k_align cross product -> k_best_full_id        (per sequence, on the device,
+                                                                         into a torch tensor on the rank's GPU)
+        dist.all_reduce(MAX) of the tensor (RCCL over xGMI; gloo: the host copy)
+    value = check reads / step time (max over ranks). Parity: the maxima after the all-reduce are
+    compared with the oracle's reduction over the same reads (the first --check-phase-check reads
+    separately on the device, so the oracle's share stays bounded) and every rank must hold the
+    same maxima."""
+    from custom_porechop_abi_amd import porechop_abi as P
+    vp = ctypes.c_void_p
+    search = [a for a in A.fresh_adapters() if '(full sequence)' not in a.name]
+    starts_u, _ = P._unique([a.start_sequence[1] for a in search if a.start_sequence])
+    ends_u, _ = P._unique([a.end_sequence[1] for a in search if a.end_sequence])
+    n_u = len(starts_u) + len(ends_u)
+    E = args.end_size
+    reads = synth.make_reads(n_check, args.mean_len, seed=4242, keep=E)
+    lo, hi = n_check * rank // world, n_check * (rank + 1) // world
+    mine = reads[lo:hi]
+    n = len(mine)
+    buf, s_off, s_len, e_off, e_len = synth.pack_end_windows(mine, E)
+
+    def dalloc(nbytes):
+        p = vp()
+        _lib.check(L.pcabi_dev_malloc(ctypes.byref(p), max(int(nbytes), 16)), 'malloc')
+        return p
+
+    def h2d(arr):
+        arr = np.ascontiguousarray(arr)
+        p = dalloc(arr.nbytes)
+        _lib.check(L.pcabi_dev_h2d(p, arr.ctypes.data_as(vp), arr.nbytes), 'h2d')
+        return p
+
+    def table(lst):
+        t = vp()
+        c, o, l = encode_adapters(lst)
+        _lib.check(L.pcabi_adapters_create_scored(c.ctypes.data_as(vp), o.ctypes.data_as(vp), l.ctypes.data_as(vp),
+                                                  len(lst), *SCORING, ctypes.byref(t)), 'adapters_create')
+        return t
+
+    stream = vp()
+    _lib.check(L.pcabi_stream_create(ctypes.byref(stream)), 'stream')
+    d_codes = h2d(buf)
+    nccl = dist is not None and args.dist_backend == 'nccl'
+    dev = torch.device('cuda', args.local_device) if nccl else None
+    # the buffer the collective reduces: on the rank's GPU (RCCL), or a device buffer copied to
+    # a host tensor (gloo)
+    t_best = torch.zeros(n_u, dtype=torch.float64, device=dev) if nccl else torch.zeros(n_u, dtype=torch.float64)
+    d_best = vp(t_best.data_ptr()) if nccl else dalloc(8 * n_u)
+    sides = []
+    for off, ln, adps, b0 in ((s_off, s_len, starts_u, 0), (e_off, e_len, ends_u, len(starts_u))):
+        toff = np.zeros((n + 255) // 256 + 1, np.int64)
+        nd = L.pcabi_tile_layout(ln.ctypes.data_as(vp), n, toff.ctypes.data_as(vp))
+        sides.append(dict(d_off=h2d(off), d_len=h2d(ln), d_toff=h2d(toff), d_tiles=dalloc(4 * max(nd, 1)),
+                          mq=int(np.diff(toff).max() // 256) if n else 0, mx=int(ln.max()) if n else 0,
+                          tab=table(adps), n_adp=len(adps), d_res=dalloc(4 * 8 * len(adps) * max(n, 1)),
+                          d_best=vp(d_best.value + 8 * b0)))
+
+    def reduce_local(n_win):
+        if nccl:
+            t_best.zero_()
+            torch.cuda.synchronize(dev)   # zeroed before the library's stream writes the tensor
+        else:
+            _lib.check(L.pcabi_dev_memset(d_best, 0, 8 * n_u), 'memset')
+        for sd in sides:
+            if n_win == 0:
+                continue
+            _lib.check(L.pcabi_tile_windows_dev(d_codes, sd['d_off'], sd['d_len'], n_win, sd['d_toff'], sd['mq'],
+                                                sd['d_tiles'], stream), 'tile')
+            _lib.check(L.pcabi_align_cross_dev(sd['d_tiles'], sd['d_toff'], sd['d_len'], n_win, sd['mx'], sd['tab'],
+                                               *SCORING, sd['d_res'], sd['n_adp'] * n_win, stream), 'align')
+            _lib.check(L.pcabi_best_full_identity_dev(sd['d_res'], sd['n_adp'] * n_win, n_win, sd['n_adp'],
+                                                      sd['d_best'], stream), 'best')
+        _lib.check(L.pcabi_stream_sync(stream), 'sync')
+
+    def step():
+        reduce_local(n)
+        if not nccl:   # one process or gloo: the maxima through the host
+            _lib.check(L.pcabi_dev_d2h(ctypes.c_void_p(t_best.data_ptr()), d_best, 8 * n_u), 'd2h')
+        if dist is not None:
+            dist.all_reduce(t_best, op=dist.ReduceOp.MAX)
+        if nccl:
+            torch.cuda.synchronize(dev)
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    if dist is not None:
+        dist.barrier()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if nccl else 'cpu')
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    maxima = t_best.cpu().numpy().copy()
+    agree = None
+    if dist is not None:
+        # every rank must hold the same reduced maxima
+        g = torch.tensor(maxima, dtype=torch.float64, device=dev if nccl else 'cpu')
+        g_min = g.clone()
+        dist.all_reduce(g_min, op=dist.ReduceOp.MIN)
+        agree = bool(torch.equal(g, g_min))
+    checked = None
+    k = min(getattr(args, 'check_phase_check', 400), n)
+    if args.check and rank == 0 and k > 0:
+        # the device reduction over the first k check reads of this rank vs the oracle's
+        from tests import oracle_lib
+        from custom_porechop_abi_amd.engine import pid6
+        from multiprocessing.dummy import Pool as ThreadPool
+        reduce_local(k)
+        got = np.empty(n_u, np.float64)
+        _lib.check(L.pcabi_dev_d2h(got.ctypes.data_as(vp), d_best if not nccl else vp(t_best.data_ptr()), 8 * n_u),
+                   'd2h')
+        heads = [synth.codes_to_str(r[0] if isinstance(r, tuple) else r[:E]) for r in mine[:k]]
+        tails = [synth.codes_to_str(r[1] if isinstance(r, tuple) else r[-E:]) for r in mine[:k]]
+
+        def one(job):
+            wins, adps, a0 = job
+            exp = oracle_lib.align_many(wins, adps, (np.zeros(len(adps), np.int64), np.arange(len(adps))), SCORING)
+            return exp
+
+        jobs = [([heads[i]], starts_u, i) for i in range(k)] + [([tails[i]], ends_u, i) for i in range(k)]
+        with ThreadPool(min(16, len(os.sched_getaffinity(0)))) as pool:
+            res = pool.map(one, jobs)
+        exp = np.zeros(n_u, np.float64)
+        for (wins, adps, _), r in zip(jobs, res):
+            full = np.where(r[0] == -1, 0.0, pid6(r[5], r[7]))
+            b0 = 0 if adps is starts_u else len(starts_u)
+            exp[b0:b0 + len(adps)] = np.maximum(exp[b0:b0 + len(adps)], full)
+        checked = {'reads_checked': k, 'sequences': n_u, 'maxima_identical': bool(np.array_equal(got, exp)),
+                   'matching_sets_at_90': int(sum(1 for a in search
+                                                  if max(maxima[starts_u.index(a.start_sequence[1])]
+                                                         if a.start_sequence else 0.0,
+                                                         maxima[len(starts_u) + ends_u.index(a.end_sequence[1])]
+                                                         if a.end_sequence else 0.0) >= 90.0))}
+    if rank == 0:
+        step_ms = 1e3 * elapsed / args.steps
+        cells = int(s_len.astype(np.int64).sum() * sum(map(len, starts_u)) +
+                    e_len.astype(np.int64).sum() * sum(map(len, ends_u)))
+        return {'metric': 'check reads/sec through the adapter-set search (%d reads x %d sets, MAX all-reduce)'
+                          % (n_check, len(search)),
+                'value': round(n_check * args.steps / elapsed, 1), 'unit': 'reads/s', 'n_gpus': world,
+                'steps': args.steps, 'warmup': max(1, args.warmup), 'ms_per_step': round(step_ms, 4),
+                'dtype': 'int32', 'data': 'synthetic (seeded ONT-like reads, mean %d bp)' % args.mean_len,
+                'config': {'workload': 'adapter-set search: %d check reads sharded over %d rank(s) x %d sets (%d start + '
+                                       '%d end sequences), windows of %d bp, per-sequence maxima on the device, '
+                                       'all-reduce MAX (%s)' % (n_check, world, len(search), len(starts_u),
+                                                                len(ends_u), E, args.dist_backend if dist else 'none'),
+                           'reads_per_rank': n, 'collective_bytes': 8 * n_u},
+                'gcups_rank0': round(cells / (step_ms * 1e-3) / 1e9, 1),
+                'ranks_agree': agree, 'parity_spot_check': checked}
+    return None
 
 
 def run_host_path(args, L, _lib, buf, s_off, s_len, e_off, e_len, sides, d_sres, d_eres, d_st, d_et, n, n_sa, n_ea,

@@ -601,14 +601,17 @@ constexpr int kMaxFastBuckets = 4;
 // into the next larger non-empty one (cost = adapters x added padding rows) until at most
 // kMaxFastBuckets remain. Only merges the packed core can serve with the scoring `sc` (it
 // passes scores through any number of padding rows; the fast core allows at most 3).
+// all_striped: every adapter on the striped core (needs_striped: long windows under a scoring
+// with no path-span bound).
 std::vector<int> assign_buckets(const int32_t *adp_len, int32_t n_adp, const pcabi::Scoring &sc, bool merge,
-                                bool allow_wide) {
+                                bool allow_wide, bool all_striped = false) {
     std::vector<int> b_of(n_adp);
     int count[kNumBuckets] = {};
     for (int a = 0; a < n_adp; ++a) {
-        b_of[a] = bucket_of(adp_len[a], sc, allow_wide);
+        b_of[a] = all_striped ? kStripedBucket : bucket_of(adp_len[a], sc, allow_wide);
         ++count[b_of[a]];
     }
+    if (all_striped) return b_of;
     auto packed_all = [&](int b, int extra_from) {
         for (int a = 0; a < n_adp; ++a)
             if ((b_of[a] == b || b_of[a] == extra_from) && !pcabi::packed_ok(adp_len[a], kBuckets[b].rpl, sc))
@@ -641,8 +644,8 @@ std::vector<int> assign_buckets(const int32_t *adp_len, int32_t n_adp, const pca
 
 void build_buckets(const uint8_t *adp_codes, const int32_t *adp_off, const int32_t *adp_len,
                    int32_t n_adp, const pcabi::Scoring &sc, BucketHost (&bk)[kNumBuckets], bool merge = true,
-                   bool allow_wide = true) {
-    const std::vector<int> b_of = assign_buckets(adp_len, n_adp, sc, merge, allow_wide);
+                   bool allow_wide = true, bool all_striped = false) {
+    const std::vector<int> b_of = assign_buckets(adp_len, n_adp, sc, merge, allow_wide, all_striped);
     for (int a = 0; a < n_adp; ++a)
         if (b_of[a] == kStripedBucket)
             bk[kStripedBucket].rt = std::max(bk[kStripedBucket].rt, (adp_len[a] + kStripeTab - 1) / kStripeTab * kStripeTab);
@@ -682,6 +685,13 @@ struct pcabi_adapters {
     uint32_t *pad[kNumBuckets] = {};
     int32_t *len[kNumBuckets] = {};
     int32_t *id[kNumBuckets] = {};
+    // Other layouts of the same adapters, built on first use by adapters_for() for a scoring this
+    // layout cannot serve (gap costs >= 0 under padded register buckets, a merge made for another
+    // scoring) or for long windows that need the striped core; kept until the table is destroyed
+    // (launches queued on a stream may still read them).
+    std::mutex alt_mu;
+    std::vector<std::pair<pcabi::Scoring, pcabi_adapters *>> alt_scored;
+    pcabi_adapters *alt_striped = nullptr;
 };
 
 namespace {
@@ -796,6 +806,15 @@ struct Engine {
     DeviceBuf codes, woff, wlen, out, tasks_win, tasks_out, wave_adp, tiles, toff, hits, bc;
     pcabi_scan *scan = nullptr;   // scratch of the middle scan (pcabi_middle_scan_host)
     DeviceBuf pad[kNumBuckets], len[kNumBuckets], id[kNumBuckets];
+    // pcabi_end_decisions_host: both sides' windows, results, trims, flags and lists; the two
+    // sides' prepared adapter tables, kept while the adapters and the scoring stay the same
+    DeviceBuf dec[16];
+    struct DTab {
+        std::vector<uint8_t> codes;
+        std::vector<int32_t> lens;
+        pcabi::Scoring sc{0, 0, 0, 0};
+        pcabi_adapters *t = nullptr;
+    } dtab[2];
 };
 
 Engine g_engines[16];
@@ -820,13 +839,15 @@ int check_common(const int32_t *adp_len, int32_t n_adp) {
     return 0;
 }
 
-// The wrapped start-column field needs a bounded path span unless every window is short.
-int check_span(const pcabi::Scoring &sc, int max_L, int64_t max_win) {
-    if (max_win < 32768 - 256) return 0;
+// The register cores keep the path's start column mod 2^16 (pcabi_dp.h attribute word), which
+// is exact only when every window is short or the path span is bounded (gap costs < 0). Any
+// other scoring the reference accepts (arg_parser.py:229-236: any four integers, e.g. gap costs
+// >= 0) on windows of 32 k and more runs on the striped core instead, whose two-word attributes
+// never wrap (align_lane_striped): true when that routing is needed.
+bool needs_striped(const pcabi::Scoring &sc, int max_L, int64_t max_win) {
+    if (max_win < 32768 - 256) return false;
     const int b = pcabi::span_bound(max_L, sc.ma, sc.mi, sc.go, sc.ge);
-    if (b < 0 || b + max_L >= 32768)
-        return fail(PCABI_E_ARG, "windows longer than 32k need negative gap costs with a bounded path span");
-    return 0;
+    return b < 0 || b + max_L >= 32768;
 }
 
 }  // namespace
@@ -927,15 +948,16 @@ int align_host_impl(int device, const uint8_t *codes, int64_t codes_len, const i
 
     const pcabi::Scoring sc{match, mismatch, gap_open, gap_extend};
     int64_t max_win = 0;
+    bool striped_only = false;
     {
         int max_L = 0;
         for (int a = 0; a < n_adp; ++a)
             if (adp_len[a] <= kMaxRPL) max_L = std::max(max_L, (int)adp_len[a]);   // striped: c never wraps
         for (int64_t w = 0; w < n_win; ++w) max_win = std::max<int64_t>(max_win, win_len[w]);
-        if (int rc = check_span(sc, max_L, max_win)) return rc;
+        striped_only = needs_striped(sc, max_L, max_win);
     }
     BucketHost bk[kNumBuckets];
-    build_buckets(adp_codes, adp_off, adp_len, n_adp, sc, bk);
+    build_buckets(adp_codes, adp_off, adp_len, n_adp, sc, bk, true, true, striped_only);
 
     if (int rc = e.codes.ensure((size_t)codes_len)) return rc;
     if (int rc = e.woff.ensure(sizeof(int64_t) * (size_t)std::max<int64_t>(n_win, 1))) return rc;
@@ -1273,11 +1295,11 @@ namespace {
 // gap costs; pcabi_align_cross_dev rejects scorings the layout cannot serve); otherwise small
 // buckets are merged for that scoring (assign_buckets).
 int adapters_create_impl(const uint8_t *adp_codes, const int32_t *adp_off, const int32_t *adp_len,
-                         int32_t n_adp, const pcabi::Scoring *sc, pcabi_adapters **out) {
+                         int32_t n_adp, const pcabi::Scoring *sc, pcabi_adapters **out, bool all_striped = false) {
     if (int rc = check_common(adp_len, n_adp)) return rc;
     BucketHost bk[kNumBuckets];
     build_buckets(adp_codes, adp_off, adp_len, n_adp, sc ? *sc : pcabi::Scoring{1, -1, -1, -1}, bk, sc != nullptr,
-                  sc != nullptr);
+                  sc != nullptr, all_striped);
     pcabi_adapters *a = new pcabi_adapters();
     a->n_adp = n_adp;
     a->hoff.resize((size_t)n_adp);
@@ -1315,13 +1337,62 @@ int adapters_create_impl(const uint8_t *adp_codes, const int32_t *adp_off, const
 }
 }  // namespace
 
-// A wide (packed-only) bucket serves only scorings its adapters are packed_ok for.
-int wide_ok(const pcabi_adapters *adps, int b, const pcabi::Scoring &sc) {
-    if (kBuckets[b].kind != WIDE && kBuckets[b].kind != LONG) return 0;
-    for (int32_t L : adps->lens[b])
-        if (kBuckets[b].kind == WIDE ? !pcabi::packed_ok(L, kBuckets[b].rpl, sc) : !pcabi::long_ok(L, kBuckets[b].rpl, sc))
-            return fail(PCABI_E_ARG, "adapter table laid out for another scoring (pcabi_adapters_create_scored): "
-                                     "rebuild it for this one");
+// Whether a table's register layout serves a scoring on windows up to max_win long: padded FAST
+// buckets need gap costs < 0 (the fast core's pass-through padding rows), merged buckets (more
+// than 3 padding rows) and the wide / long buckets the packed core's range conditions, and long
+// windows a bounded path span (needs_striped).
+bool layout_serves(const pcabi_adapters *adps, const pcabi::Scoring &sc, int64_t max_win) {
+    int max_L = 0;
+    bool regs = false;
+    for (int b = 0; b < kNumBuckets; ++b) {
+        if (!adps->count[b] || kBuckets[b].kind == STRIPED) continue;
+        regs = true;
+        for (int32_t L : adps->lens[b]) max_L = std::max<int>(max_L, L);
+        if (kBuckets[b].kind == FAST && adps->padded[b] && !pcabi::fast_ok(kBuckets[b].rpl - 1, kBuckets[b].rpl, sc))
+            return false;
+        if (kBuckets[b].kind == FAST && adps->max_off[b] > 3 && !bucket_packed_ok(b, adps->lens[b], sc)) return false;
+        if (kBuckets[b].kind == WIDE || kBuckets[b].kind == LONG)
+            for (int32_t L : adps->lens[b])
+                if (kBuckets[b].kind == WIDE ? !pcabi::packed_ok(L, kBuckets[b].rpl, sc)
+                                             : !pcabi::long_ok(L, kBuckets[b].rpl, sc))
+                    return false;
+    }
+    return !regs || !needs_striped(sc, max_L, max_win);
+}
+
+// The layout of `adps` to run a scoring on windows up to max_win long: the table itself when it
+// serves them, else a layout of the same adapters built for them on first use and cached in the
+// table -- every adapter on the striped core when the windows need it, else register buckets for
+// this scoring. The reference accepts any scoring for any read (arg_parser.py:229-236,
+// adapter_align.cpp:11-31), so the device ABI does too.
+int adapters_for(const pcabi_adapters *adps, const pcabi::Scoring &sc, int64_t max_win, const pcabi_adapters **use) {
+    if (layout_serves(adps, sc, max_win)) {
+        *use = adps;
+        return 0;
+    }
+    pcabi_adapters *a = const_cast<pcabi_adapters *>(adps);   // the cache is the only mutable part
+    std::lock_guard<std::mutex> g(a->alt_mu);
+    std::vector<int32_t> off((size_t)a->n_adp);
+    for (int32_t k = 0; k < a->n_adp; ++k) off[k] = a->hoff[k];
+    // register buckets laid out (and merged) for this scoring, if they serve these windows
+    pcabi_adapters *t = nullptr;
+    for (auto &e : a->alt_scored)
+        if (e.first.ma == sc.ma && e.first.mi == sc.mi && e.first.go == sc.go && e.first.ge == sc.ge) t = e.second;
+    if (!t) {
+        if (int rc = adapters_create_impl(a->hcodes.data(), off.data(), a->hlen.data(), a->n_adp, &sc, &t)) return rc;
+        a->alt_scored.emplace_back(sc, t);
+    }
+    if (layout_serves(t, sc, max_win)) {
+        *use = t;
+        return 0;
+    }
+    if (!a->alt_striped) {
+        t = nullptr;
+        if (int rc = adapters_create_impl(a->hcodes.data(), off.data(), a->hlen.data(), a->n_adp, &sc, &t, true))
+            return rc;
+        a->alt_striped = t;
+    }
+    *use = a->alt_striped;
     return 0;
 }
 
@@ -1341,6 +1412,8 @@ int pcabi_adapters_create_scored(const uint8_t *adp_codes, const int32_t *adp_of
 
 void pcabi_adapters_destroy(pcabi_adapters *a) {
     if (!a) return;
+    for (auto &e : a->alt_scored) pcabi_adapters_destroy(e.second);
+    pcabi_adapters_destroy(a->alt_striped);
     for (int b = 0; b < kNumBuckets; ++b) {
         if (a->pad[b]) (void)hipFree(a->pad[b]);
         if (a->len[b]) (void)hipFree(a->len[b]);
@@ -1377,14 +1450,9 @@ int pcabi_align_cross_dev_marked(const uint32_t *tiles, const int64_t *tile_off,
                                  void *stream, void *ev_begin, void *ev_end) {
     if (!adps || n_win < 0 || (n_win > 0 && (!tiles || !tile_off))) return fail(PCABI_E_ARG, "bad arguments");
     if (n_win == 0) return 0;
-    {
-        int max_L = 0;
-        for (int b = 0; b < kNumBuckets; ++b)
-            if (kBuckets[b].kind != STRIPED)   // the striped core's start column never wraps
-                for (int32_t L : adps->lens[b]) max_L = std::max<int>(max_L, L);
-        if (int rc = check_span(pcabi::Scoring{match, mismatch, gap_open, gap_extend}, max_L, max_win_len))
-            return rc;
-    }
+    // a layout of the table that serves this scoring on these windows (the table's own when it can)
+    if (int rc = adapters_for(adps, pcabi::Scoring{match, mismatch, gap_open, gap_extend}, max_win_len, &adps))
+        return rc;
     KParams p{};
     p.tiles = tiles;
     p.tile_off = tile_off;
@@ -1396,18 +1464,8 @@ int pcabi_align_cross_dev_marked(const uint32_t *tiles, const int64_t *tile_off,
     p.max_cols = max_win_len;
     const bool affine = gap_open != gap_extend;
     std::vector<int> order;
-    for (int b = 0; b < kNumBuckets; ++b) {
-        if (!adps->count[b]) continue;
-        if (kBuckets[b].kind == FAST && adps->padded[b] &&
-            !pcabi::fast_ok(kBuckets[b].rpl - 1, kBuckets[b].rpl, p.sc))
-            return fail(PCABI_E_ARG, "scoring with non-negative gap costs: use pcabi_align_host "
-                                     "(generic kernels) for this adapter table");
-        if (kBuckets[b].kind == FAST && adps->max_off[b] > 3 && !bucket_packed_ok(b, adps->lens[b], p.sc))
-            return fail(PCABI_E_ARG, "adapter table merged for another scoring (pcabi_adapters_create_scored): "
-                                     "rebuild it for this one");
-        if (int rc = wide_ok(adps, b, p.sc)) return rc;
-        order.push_back(b);
-    }
+    for (int b = 0; b < kNumBuckets; ++b)
+        if (adps->count[b]) order.push_back(b);
     // Largest bucket (adapters x rows) on the caller's stream, the others spread over the
     // device's side streams (fork / join with events): a bucket holding one or two adapters is
     // too small a grid to fill 256 CUs on its own, side by side they do.
@@ -1967,8 +2025,21 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
     const hipStream_t st = (hipStream_t)stream;
     const int32_t n_adp = sc->adps->n_adp;
     if (n_win == 0 || n_adp == 0) return 0;
-    for (int b = 0; b < kNumBuckets; ++b)
-        if (int rc = wide_ok(sc->adps, b, pcabi::Scoring{match, mismatch, gap_open, gap_extend})) return rc;
+    // the layout of the scan's table that serves this scoring on these reads (adapters_for: any
+    // scoring the reference accepts, any read length), for the duration of the call
+    struct TableSwap {
+        pcabi_scan *s;
+        const pcabi_adapters *own;
+        ~TableSwap() { s->adps = own; }
+    } swap_back{sc, sc->adps};
+    {
+        int32_t longest = 0;
+        for (int64_t k = 0; k < n_win; ++k) longest = std::max(longest, h_win_len[k]);
+        const pcabi_adapters *use = nullptr;
+        if (int rc = adapters_for(sc->adps, pcabi::Scoring{match, mismatch, gap_open, gap_extend}, longest, &use))
+            return rc;
+        sc->adps = use;
+    }
     int64_t n_hits = 0;
     std::vector<int32_t> cur, nxt, nxt_start, hm_w, hm_s, hm_e, lens;
     std::vector<int32_t> hb;
@@ -2354,3 +2425,172 @@ int pcabi_barcode_call_host(int device, const int32_t *start_res, int32_t n_sa, 
 }
 
 }  // extern "C"
+
+// ---- end-trim decisions of the reference-API driver (find_adapters_at_read_ends) -----------------
+extern "C" int pcabi_flag_list_dev(const uint8_t *flag, int32_t n_adp, int64_t n_read, const int32_t *res,
+                                   int64_t stride, int32_t *out, int64_t cap, unsigned long long *n_out,
+                                   void *stream);
+
+namespace {
+
+// out[j * n_read + r] = the full-adapter identity (pid6(m, l2), 0.0 for no alignment) of adapter
+// sel[j] on read r: the barcode dicts of find_start_trim / find_end_trim (nanopore_read.py:193-195).
+__global__ __launch_bounds__(256) void k_full_ids(const int32_t *res, int64_t stride, int64_t n_read,
+                                                  const int32_t *sel, int32_t n_sel, double *out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)n_sel * n_read) return;
+    const int32_t j = (int32_t)(i / n_read);
+    const int64_t q = (int64_t)sel[j] * n_read + (i - (int64_t)j * n_read);
+    out[i] = res[q] == -1 ? 0.0 : pcabi::pid6(res[5 * stride + q], res[7 * stride + q]);
+}
+
+int side_table(Engine::DTab &c, const uint8_t *codes, const int32_t *off, const int32_t *len, int32_t n,
+               const pcabi::Scoring &sc, pcabi_adapters **out) {
+    std::vector<uint8_t> key;
+    for (int32_t a = 0; a < n; ++a) key.insert(key.end(), codes + off[a], codes + off[a] + len[a]);
+    if (c.t && c.sc.ma == sc.ma && c.sc.mi == sc.mi && c.sc.go == sc.go && c.sc.ge == sc.ge && c.codes == key &&
+        c.lens == std::vector<int32_t>(len, len + n)) {
+        *out = c.t;
+        return 0;
+    }
+    if (c.t) pcabi_adapters_destroy(c.t);   // the previous call synchronised its stream
+    c.t = nullptr;
+    if (int rc = adapters_create_impl(codes, off, len, n, &sc, &c.t)) return rc;
+    c.codes.swap(key);
+    c.lens.assign(len, len + n);
+    c.sc = sc;
+    *out = c.t;
+    return 0;
+}
+
+}  // namespace
+
+extern "C" int pcabi_end_decisions_host(
+    int device, const uint8_t *codes, int64_t codes_len, const int64_t *s_off, const int32_t *s_len,
+    const int64_t *e_off, const int32_t *e_len, int64_t n_read, const uint8_t *sa_codes, const int32_t *sa_off,
+    const int32_t *sa_len, int32_t n_sa, const uint8_t *ea_codes, const int32_t *ea_off, const int32_t *ea_len,
+    int32_t n_ea, int match, int mismatch, int gap_open, int gap_extend, int end_size, int extra_trim,
+    double end_threshold, int min_trim_size, int32_t *start_trim, int32_t *end_trim, int32_t *start_hits,
+    int32_t *end_hits, int64_t cap, int64_t *n_hits, const int32_t *bc_s, int32_t n_bc_s, const int32_t *bc_e,
+    int32_t n_bc_e, double *bc_full) {
+    if (device < 0 || device >= 16) return fail(PCABI_E_ARG, "bad device index");
+    if (n_read < 0 || n_sa < 0 || n_ea < 0 || cap < 0 || n_bc_s < 0 || n_bc_e < 0) return fail(PCABI_E_ARG, "negative count");
+    if (int rc = check_common(sa_len, n_sa)) return rc;
+    if (int rc = check_common(ea_len, n_ea)) return rc;
+    for (int side = 0; side < 2; ++side) {
+        const int64_t *off = side ? e_off : s_off;
+        const int32_t *len = side ? e_len : s_len;
+        for (int64_t w = 0; w < n_read; ++w) {
+            if (len[w] < 0 || len[w] > pcabi::MAX_WINDOW_LEN) return fail(PCABI_E_ARG, "window length out of range");
+            if (len[w] > 0 && (off[w] < 0 || off[w] + len[w] + 16 > codes_len))
+                return fail(PCABI_E_ARG, "window outside the buffer or buffer not padded by 16 bytes");
+        }
+    }
+    for (int32_t j = 0; j < n_bc_s; ++j)
+        if (bc_s[j] < 0 || bc_s[j] >= n_sa) return fail(PCABI_E_ARG, "start barcode adapter out of range");
+    for (int32_t j = 0; j < n_bc_e; ++j)
+        if (bc_e[j] < 0 || bc_e[j] >= n_ea) return fail(PCABI_E_ARG, "end barcode adapter out of range");
+    n_hits[0] = n_hits[1] = 0;
+    if (n_read == 0) return 0;
+    Engine &e = g_engines[device];
+    std::lock_guard<std::mutex> lock(e.mu);
+    if (int rc = engine_init(e, device)) return rc;
+    HIP_TRY(hipSetDevice(device));
+    const pcabi::Scoring sc{match, mismatch, gap_open, gap_extend};
+    const hipStream_t st = e.stream;
+    const size_t n = (size_t)n_read;
+    const int32_t n_adp[2] = {n_sa, n_ea};
+    // buffers: 0 codes; per side (base 1 + 6 side): offsets, lengths, tile offsets, tiles, results, flags;
+    // 13 trims (2 x n); 14 lists (2 sides x 7 x n_read x n_adp bound); 15 counts + barcode identities
+    if (int rc = e.dec[0].ensure((size_t)codes_len)) return rc;
+    HIP_TRY(hipMemcpyAsync(e.dec[0].p, codes, (size_t)codes_len, hipMemcpyHostToDevice, st));
+    if (int rc = e.dec[13].ensure(8 * n)) return rc;
+    int32_t *d_st = (int32_t *)e.dec[13].p, *d_et = d_st + n;
+    std::vector<int64_t> toff[2];
+    const int32_t *res[2] = {nullptr, nullptr};
+    uint8_t *flag[2] = {nullptr, nullptr};
+    for (int side = 0; side < 2; ++side) {
+        const int64_t *off = side ? e_off : s_off;
+        const int32_t *len = side ? e_len : s_len;
+        DeviceBuf *b = e.dec + 1 + 6 * side;
+        if (int rc = b[0].ensure(8 * n)) return rc;
+        if (int rc = b[1].ensure(4 * n)) return rc;
+        toff[side].assign((n + 255) / 256 + 1, 0);
+        int64_t max_nq = 0;
+        const int64_t nd = tile_layout(len, n_read, toff[side].data(), &max_nq);
+        if (int rc = b[2].ensure(8 * toff[side].size())) return rc;
+        if (int rc = b[3].ensure(4 * (size_t)std::max<int64_t>(nd, 1))) return rc;
+        if (int rc = b[4].ensure(4 * PCABI_NFIELDS * n * (size_t)std::max(n_adp[side], 1))) return rc;
+        if (int rc = b[5].ensure(n * (size_t)std::max(n_adp[side], 1))) return rc;
+        HIP_TRY(hipMemcpyAsync(b[0].p, off, 8 * n, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(b[1].p, len, 4 * n, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(b[2].p, toff[side].data(), 8 * toff[side].size(), hipMemcpyHostToDevice, st));
+        res[side] = (const int32_t *)b[4].p;
+        flag[side] = (uint8_t *)b[5].p;
+        if (!n_adp[side]) continue;
+        int32_t max_len = 0;
+        for (size_t w = 0; w < n; ++w) max_len = std::max(max_len, len[w]);
+        pcabi_adapters *tab = nullptr;
+        if (int rc = side_table(e.dtab[side], side ? ea_codes : sa_codes, side ? ea_off : sa_off, side ? ea_len : sa_len,
+                                n_adp[side], sc, &tab))
+            return rc;
+        launch_tiles((const uint8_t *)e.dec[0].p, (const int64_t *)b[0].p, (const int32_t *)b[1].p, n_read,
+                     (const int64_t *)b[2].p, max_nq, (uint32_t *)b[3].p, st);
+        if (int rc = pcabi_align_cross_dev((const uint32_t *)b[3].p, (const int64_t *)b[2].p, (const int32_t *)b[1].p,
+                                           n_read, max_len, tab, match, mismatch, gap_open, gap_extend, (int32_t *)b[4].p,
+                                           (int64_t)n_adp[side] * n_read, st))
+            return rc;
+    }
+    if (int rc = pcabi_end_trim_dev(res[0], (int64_t)n_sa * n_read, n_sa, res[1], (int64_t)n_ea * n_read, n_ea, n_read,
+                                    end_size, extra_trim, end_threshold, min_trim_size, d_st, d_et, flag[0], flag[1], st))
+        return rc;
+    // the alignment lists (device capacity: every pair of the side -- they never overflow there)
+    const size_t dcap[2] = {n * (size_t)n_sa, n * (size_t)n_ea};
+    if (int rc = e.dec[14].ensure(4 * 7 * (dcap[0] + dcap[1]) + 16)) return rc;
+    int32_t *d_list[2] = {(int32_t *)e.dec[14].p, (int32_t *)e.dec[14].p + 7 * dcap[0]};
+    const size_t nbc = (size_t)n_bc_s + (size_t)n_bc_e;
+    if (int rc = e.dec[15].ensure(64 + 4 * nbc + 8 * nbc * n)) return rc;
+    unsigned long long *d_cnt = (unsigned long long *)e.dec[15].p;
+    int32_t *d_sel = (int32_t *)((char *)e.dec[15].p + 16);
+    double *d_full = (double *)((char *)e.dec[15].p + 64 + ((4 * nbc + 7) & ~(size_t)7));
+    for (int side = 0; side < 2; ++side) {
+        if (!n_adp[side]) {
+            HIP_TRY(hipMemsetAsync(d_cnt + side, 0, 8, st));
+            continue;
+        }
+        if (int rc = pcabi_flag_list_dev(flag[side], n_adp[side], n_read, res[side], (int64_t)n_adp[side] * n_read,
+                                         d_list[side], (int64_t)dcap[side], d_cnt + side, st))
+            return rc;
+    }
+    if (nbc && bc_full) {
+        std::vector<int32_t> sel(bc_s, bc_s + n_bc_s);
+        sel.insert(sel.end(), bc_e, bc_e + n_bc_e);
+        HIP_TRY(hipMemcpyAsync(d_sel, sel.data(), 4 * nbc, hipMemcpyHostToDevice, st));
+        for (int side = 0; side < 2; ++side) {
+            const int32_t ns = side ? n_bc_e : n_bc_s;
+            if (!ns) continue;
+            const int64_t tot = (int64_t)ns * n_read;
+            hipLaunchKernelGGL(k_full_ids, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, res[side],
+                               (int64_t)n_adp[side] * n_read, n_read, d_sel + (side ? n_bc_s : 0), ns,
+                               d_full + (side ? (size_t)n_bc_s * n : 0));
+        }
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(bc_full, d_full, 8 * nbc * n, hipMemcpyDeviceToHost, st));
+    }
+    unsigned long long cnt[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(start_trim, d_st, 4 * n, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(end_trim, d_et, 4 * n, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(cnt, d_cnt, 16, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    n_hits[0] = (int64_t)cnt[0];
+    n_hits[1] = (int64_t)cnt[1];
+    for (int side = 0; side < 2; ++side) {
+        int32_t *dst = side ? end_hits : start_hits;
+        const int64_t k = (int64_t)cnt[side];
+        if (k > cap || !k) continue;                // too many: the caller grows cap and calls again
+        for (int f = 0; f < 7; ++f)                 // rows of the device list (stride dcap) -> stride cap
+            HIP_TRY(hipMemcpyAsync(dst + f * cap, d_list[side] + f * dcap[side], 4 * (size_t)k, hipMemcpyDeviceToHost, st));
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+}

@@ -881,8 +881,10 @@ extern "C" int pcabi_reads_write(const pcabi_reads *b, const char *path, int app
         o.fd = ::open(path, O_WRONLY | O_CREAT | (append ? O_APPEND : O_TRUNC), 0666);
         if (o.fd < 0) return fail(PCABI_E_ARG, std::string("could not write ") + path);
     }
-    auto format = [&](int64_t i, Sink &o, std::vector<std::pair<int64_t, int64_t>> &rg) {
-        if (select && !select[i]) return;
+    // returns whether the read produced any output (the reference counts a read into its bin only
+    // then, porechop_abi.py:598-604)
+    auto format = [&](int64_t i, Sink &o, std::vector<std::pair<int64_t, int64_t>> &rg) -> bool {
+        if (select && !select[i]) return false;
         const char *name = b->names.data() + b->name_off[i];
         const size_t nn = (size_t)(b->name_off[i + 1] - b->name_off[i]);
         const char *seq = b->seq.data() + b->seq_off[i];
@@ -902,11 +904,11 @@ extern "C" int pcabi_reads_write(const pcabi_reads *b, const char *path, int app
             for (int64_t k = cut_off[i]; k < cut_off[i + 1] && !split; ++k) split = cuts[2 * k + 1] > cuts[2 * k];
         if (!split) {
             if (untrimmed) { sa = 0; sb = ns; qa = 0; qb = nq; }
-            if (sb == sa) return;   // no empty sequences
+            if (sb == sa) return false;   // no empty sequences
             put_record(o, fasta != 0, name, nn, false, seq + sa, (size_t)(sb - sa), qual + qa, (size_t)(qb - qa), rna);
-            return;
+            return true;
         }
-        if (discard_middle) return;
+        if (discard_middle) return false;
         // split parts (get_split_read_parts, nanopore_read.py:84-104): positions of the trimmed
         // sequence inside any cut range are dropped
         rg.clear();
@@ -939,15 +941,18 @@ extern "C" int pcabi_reads_write(const pcabi_reads *b, const char *path, int app
             }
         }
         emit(run, tl);
+        return part > 0;
     };
     // One stream: the page-cache copy is the cost, and writers of one file serialise on its
     // inode (measured: threads writing disjoint ranges with pwritev were no faster).
     std::vector<std::pair<int64_t, int64_t>> rg;
-    for (int64_t i = 0; i < b->n; ++i) format(i, o, rg);
+    int64_t emitted = 0;
+    for (int64_t i = 0; i < b->n; ++i) emitted += format(i, o, rg) ? 1 : 0;
     o.flush();
     const bool ok = o.ok;
     if (o.gz) gzclose(o.gz);
     else if (o.fd >= 0) ::close(o.fd);
     else if (o.fp) std::fflush(o.fp);
-    return ok ? 0 : fail(PCABI_E_ARG, std::string("write failed: ") + path);
+    if (!ok) return fail(PCABI_E_ARG, std::string("write failed: ") + path);
+    return (int)std::min<int64_t>(emitted, INT32_MAX);
 }

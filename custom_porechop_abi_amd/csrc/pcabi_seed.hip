@@ -445,6 +445,9 @@ int plan(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hl
     s->planned = true;
     s->ok = false;
     if (!(threshold > 0.0) || sc.go >= 0 || sc.ge >= 0 || n_adp >= (1 << 22)) return 0;
+    // band_best's early exit bounds the rows still to come by best_sub per row: sound only when no
+    // row step can gain more (every gap step costs, checked above, and best_sub > 0 > go, ge)
+    if (pcabi::best_sub(sc) <= 0) return 0;
     const double th = (threshold - 1e-5) / 100.0;
     if (th <= 0.0 || th > 1.0) return 0;
     std::vector<std::vector<std::vector<int32_t>>> lists(kNK);
@@ -459,7 +462,7 @@ int plan(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hl
         for (int i = 0; i < L; ++i)
             if (hcodes[hoff[a] + i] > 3) return 0;
         const int T = pcabi::sf::filter_threshold(L, threshold, sc);
-        if (T <= pcabi::sf::NEG16) return 0;
+        if (T <= pcabi::sf::NEG16 || T <= 0) return 0;   // no usable bound: the filter / cross product
         const int e = (int)std::floor((double)L * (1.0 - th) / th + 1e-9);
         if (e > kMaxE) return 0;
         const int plen = L / (e + 1);

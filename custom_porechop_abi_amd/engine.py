@@ -204,6 +204,48 @@ def best_full_identity(windows, adapter_seqs, scoring_scheme_vals, best=None, de
     return out
 
 
+def end_decisions(codes, start_windows, end_windows, start_seqs, end_seqs, scoring_scheme_vals, end_size, extra_trim,
+                  end_threshold, min_trim_size, bc_start=None, bc_end=None, device=0):
+    """find_start_trim / find_end_trim for a batch of reads on the GPU (pcabi_end_decisions_host,
+    porechop_abi/nanopore_read.py:175-217): only the decisions come back, never the result matrix.
+
+    codes: one Dna5 buffer holding both window sets; start_windows / end_windows: (offsets int64,
+    lengths int32). Returns (start_trim int32[n], end_trim int32[n], start_list, end_list,
+    bc_full): each list is int32 (7, k) -- read, adapter, rs, re (inclusive), m, l1, l2 -- of the
+    alignments the reference records, read-major in adapter order; bc_full is float64
+    (len(bc_start) + len(bc_end), n) full identities of the listed adapters (None without them)."""
+    codes = np.ascontiguousarray(codes, dtype=np.uint8)
+    s_off = np.ascontiguousarray(start_windows[0], dtype=np.int64)
+    s_len = np.ascontiguousarray(start_windows[1], dtype=np.int32)
+    e_off = np.ascontiguousarray(end_windows[0], dtype=np.int64)
+    e_len = np.ascontiguousarray(end_windows[1], dtype=np.int32)
+    n = len(s_len)
+    sa, so, sl = encode_adapters(start_seqs)
+    ea, eo, el = encode_adapters(end_seqs)
+    bs = np.ascontiguousarray(bc_start if bc_start is not None else [], dtype=np.int32)
+    be = np.ascontiguousarray(bc_end if bc_end is not None else [], dtype=np.int32)
+    st = np.zeros(n, np.int32)
+    et = np.zeros(n, np.int32)
+    nb = len(bs) + len(be)
+    bc_full = np.zeros((nb, n), np.float64) if nb else None
+    cap = 2 * n + 1024
+    m, mm, go, ge = (int(x) for x in scoring_scheme_vals[:4])
+    while True:
+        sh = np.zeros((7, cap), np.int32)
+        eh = np.zeros((7, cap), np.int32)
+        cnt = np.zeros(2, np.int64)
+        rc = lib().pcabi_end_decisions_host(device, _ptr(codes), codes.size, _ptr(s_off), _ptr(s_len), _ptr(e_off),
+                                            _ptr(e_len), n, _ptr(sa), _ptr(so), _ptr(sl), len(sl), _ptr(ea), _ptr(eo),
+                                            _ptr(el), len(el), m, mm, go, ge, int(end_size), int(extra_trim),
+                                            float(end_threshold), int(min_trim_size), _ptr(st), _ptr(et), _ptr(sh),
+                                            _ptr(eh), cap, _ptr(cnt), _ptr(bs), len(bs), _ptr(be), len(be),
+                                            _ptr(bc_full))
+        check(rc, 'pcabi_end_decisions_host')
+        if cnt.max() <= cap:
+            return st, et, sh[:, :cnt[0]], eh[:, :cnt[1]], bc_full
+        cap = int(cnt.max())
+
+
 def middle_cuts(hits, n_reads, bad_start, bad_end, good_side, bad_side, device=0):
     """Middle trim ranges of a scan's hits on the GPU (pcabi_middle_cuts_host,
     porechop_abi/nanopore_read.py:233-250): hits int32 (>= 4, n_hits) rows read, adapter,

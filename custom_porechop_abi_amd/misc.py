@@ -157,10 +157,45 @@ def _open_error(path):
     return msg.decode() if msg else path
 
 
+def input_files(path):
+    """The sequence files of an input, as load_reads sees it (porechop_abi.py:133-187): a file is
+    itself (albacore barcode None); a directory is an Albacore output directory -- every *.fastq /
+    *.fastq.gz under it, sorted by path, each with the barcode its path names
+    (get_albacore_barcode_from_path). Exits like the reference when nothing is found."""
+    if os.path.isfile(path):
+        return [(path, None)]
+    if os.path.isdir(path):
+        fastqs = sorted([os.path.join(d, f) for d, _, fs in os.walk(path) for f in fs
+                         if f.lower().endswith('.fastq') or f.lower().endswith('.fastq.gz')])
+        if not fastqs:
+            sys.exit('Error: could not find fastq files in ' + path)
+        return [(f, get_albacore_barcode_from_path(f)) for f in fastqs]
+    sys.exit('Error: could not find ' + path)
+
+
+def load_check_reads(path, check_read_count):
+    """The check reads of load_reads (porechop_abi.py:133-187) as NanoporeRead objects: a file's
+    first check_read_count records; for an Albacore directory the first
+    round(check_read_count / files) records of every file, in file order."""
+    files = input_files(path)
+    per_file = check_read_count if os.path.isfile(path) else int(round(check_read_count / len(files)))
+    out = []
+    for f, _ in files:
+        if per_file <= 0:
+            break
+        for b in read_batches(f, max_reads=per_file, max_bases=1 << 62):
+            out += b.nanopore_reads()
+            break
+    return out
+
+
 def record_boundaries(path, parts):
     """Byte offsets [parts + 1] splitting a plain FASTA / FASTQ file into `parts` contiguous record
     ranges of about equal size (so about equal bases): each cut is moved forward to the next record
-    start (pcabi_fastx_record_start). None for a gzip file (it cannot be entered mid-stream)."""
+    start (pcabi_fastx_record_start). None for a gzip file (it cannot be entered mid-stream) and for
+    a directory (its files are streamed in order)."""
+    if os.path.isdir(path):
+        return None
     L = _declare(lib())
     h = ctypes.c_void_p()
     rc = L.pcabi_fastx_open(os.fsencode(path), 0, ctypes.byref(h))
@@ -312,7 +347,7 @@ def write_reads(batch, path, out_format='fastq', start_trim=None, end_trim=None,
                 min_split_read_size=1000, discard_middle=False, untrimmed=False, select=None, append=False,
                 cut_arrays=None):
     """NanoporeRead.get_fasta / get_fastq for every read of a ReadBatch, natively
-    (pcabi_reads_write). out_format: 'fasta' | 'fastq' | 'fasta.gz' | 'fastq.gz'.
+    (pcabi_reads_write). Returns how many reads produced output (a non-empty read string). out_format: 'fasta' | 'fastq' | 'fasta.gz' | 'fastq.gz'.
     middle_cuts: per read a list of (begin, end) ranges of the trimmed sequence (the reference's
     middle_trim_positions as ranges), or None; cut_arrays: the same as (cut_off int64 [n + 1],
     cuts int64 [2 * n_cuts]) arrays."""
@@ -341,7 +376,9 @@ def write_reads(batch, path, out_format='fastq', start_trim=None, end_trim=None,
     p = lambda a: a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
     rc = L.pcabi_reads_write(batch._h, os.fsencode(path), int(append), int(gz), int(fasta), p(st), p(et), p(co), p(cu),
                              int(min_split_read_size), int(discard_middle), int(untrimmed), p(sel))
-    check(rc, 'pcabi_reads_write')
+    if rc < 0:
+        check(rc, 'pcabi_reads_write')
+    return int(rc)
 
 
 def positions_to_ranges(positions):

@@ -121,8 +121,10 @@ class FileTrimmer(object):
         self.times[key] = self.times.get(key, 0.0) + now - t
         return now
 
-    def trim(self, batch):
-        """Decisions for one ReadBatch: (start_trim, end_trim, cut_off, cuts, hits, keep)."""
+    def trim(self, batch, albacore=None):
+        """Decisions for one ReadBatch: (start_trim, end_trim, cut_off, cuts, hits, keep).
+        albacore: the barcode of the Albacore directory the batch came from (misc.input_files), or
+        None; with -b a device call that disagrees with it becomes 'none' (nanopore_read.py:479-482)."""
         L, sc, nb = self.L, self.sc, batch.n
         t = time.perf_counter()
         lens = batch.lengths.astype(np.int64)
@@ -170,6 +172,8 @@ class FileTrimmer(object):
                 check(L.pcabi_dev_copy_async(calls.ctypes.data_as(VP), d_call, 4 * nb, 1, self.stream), 'd2h')
                 self.last_calls = calls
             check(L.pcabi_stream_sync(self.stream), 'sync')
+            if self.barcode_dir is not None and albacore is not None:
+                self.last_calls = self.albacore_filter(self.last_calls, albacore)
         elif self.barcode_dir is not None:
             self.last_calls = np.full(nb, -1, np.int32)
         t = self._tick('end_trim', t)
@@ -209,9 +213,20 @@ class FileTrimmer(object):
             keep = ((trims[0] > 0) & (trims[1] > 0)).astype(np.uint8)
         return trims[0], trims[1], cut_off, cuts, hits, keep
 
+    def albacore_filter(self, calls, albacore):
+        """determine_barcode's Albacore cross-check (nanopore_read.py:479-482): a read binned by
+        Albacore keeps Porechop's call only when both agree, else it is 'none' (-1); reads of the
+        'unclassified' directory (albacore 'none') all become 'none'."""
+        ids = {v: k for k, v in self.bc_names.items()}
+        want = ids.get(albacore, -2)
+        return np.where(calls == want, calls, -1).astype(np.int32)
+
     def trim_file(self, in_path, out_path, out_format='fastq', max_reads=200000, byte_range=None, batch_filter=None,
                   segments=None):
-        """Trim a FASTA / FASTQ(.gz) file batch by batch into out_path. Returns read counts.
+        """Trim a FASTA / FASTQ(.gz) file -- or an Albacore output directory, its *.fastq(.gz) files
+        in sorted order as load_reads reads them (porechop_abi.py:133-187), each batch carrying
+        its file's barcode for the -b cross-check -- batch by batch into out_path. Returns read
+        counts.
 
         Shards (shards.trim_file_sharded): byte_range = (begin, end) record starts of a plain file
         reads only that range; batch_filter(k) False skips batch k (parsed, not trimmed or
@@ -240,12 +255,21 @@ class FileTrimmer(object):
                     pass
             return False
 
+        def batches():
+            files = misc.input_files(in_path)
+            if len(files) > 1 or files[0][1] is not None:
+                if byte_range is not None:
+                    raise ValueError('byte ranges apply to a single plain file, not to a directory')
+            for f, alb in files:
+                for b in misc.read_batches(f, max_reads=max_reads, byte_range=byte_range):
+                    yield b, alb
+
         def produce():
             try:
-                for k, b in enumerate(misc.read_batches(in_path, max_reads=max_reads, byte_range=byte_range)):
+                for k, (b, alb) in enumerate(batches()):
                     if batch_filter is not None and not batch_filter(k):
                         continue
-                    if not put_parsed((k, b)):
+                    if not put_parsed((k, b, alb)):
                         return
                 put_parsed(None)
             except BaseException as ex:   # handed to the consumer
@@ -292,8 +316,8 @@ class FileTrimmer(object):
                     break
                 if isinstance(b, BaseException):
                     raise b
-                k, b = b
-                st, et, co, cu, _, keep = self.trim(b)
+                k, b, alb = b
+                st, et, co, cu, _, keep = self.trim(b) if alb is None else self.trim(b, albacore=alb)
                 calls = self.last_calls if self.barcode_dir is not None else None
                 wq.put((k, b, st, et, co, cu, keep, calls))   # the writer drains even after a failure
                 del b
@@ -314,7 +338,9 @@ class FileTrimmer(object):
         """One batch into the barcode bins (porechop_abi.py:581-610): the reads of each call, in
         read order, appended to <barcode_dir>/<name>.<format> (created, not appended, the first
         time the run writes it, as the reference opens each bin with 'wt'). segments (sharded
-        runs) receives (k, name, begin, end) byte spans per bin write."""
+        runs) receives (k, name, begin, end) byte spans per bin write. As in the reference
+        (porechop_abi.py:598-604) a bin exists only once some read of it produced output, and it
+        counts only those reads: a write that emitted nothing leaves no file and no span."""
         sel = np.ones(b.n, bool) if keep is None else keep.astype(bool)
         if self.discard_unassigned:
             sel &= calls >= 0
@@ -324,9 +350,13 @@ class FileTrimmer(object):
             path = os.path.join(self.barcode_dir, name + '.' + out_format)
             fresh = name not in bins
             at = 0 if fresh else os.path.getsize(path)
-            misc.write_reads(b, path, out_format, st, et, None, self.min_split, self.discard_middle,
-                             untrimmed=self.untrimmed, select=mask, append=not fresh, cut_arrays=(co, cu))
-            bins[name] = (path, (0 if fresh else bins[name][1]) + int(mask.sum()))
+            emitted = misc.write_reads(b, path, out_format, st, et, None, self.min_split, self.discard_middle,
+                                       untrimmed=self.untrimmed, select=mask, append=not fresh, cut_arrays=(co, cu))
+            if emitted == 0:
+                if fresh and os.path.exists(path):
+                    os.remove(path)             # the reference never opens an empty bin
+                continue
+            bins[name] = (path, (0 if fresh else bins[name][1]) + emitted)
             if segments is not None:
                 segments.append((k, name, at, os.path.getsize(path)))
 

@@ -22,7 +22,7 @@ from . import adapters as _adapters
 from .adapters import make_full_native_barcode_adapter, make_new_full_rapid_barcode_adapter, \
     make_old_full_rapid_barcode_adapter
 from . import engine
-from .engine import SeqPack, identities, start_end_windows
+from .engine import SeqPack
 
 END_FORMATTING = '\033[0m'
 BOLD = '\033[1m'
@@ -57,18 +57,6 @@ def _unique(seqs):
     return uniq, np.array(idx, dtype=np.int64)
 
 
-def _window_hits(windows, seqs, scoring_scheme_vals):
-    """Cross product windows x seqs on the GPU -> (full, partial, rs, re_excl), each (n_seq, n_win)."""
-    n_win = len(windows[2])
-    uniq, idx = _unique(seqs)
-    if not uniq or n_win == 0:
-        z = np.zeros((len(seqs), n_win))
-        return z, z.copy(), z.astype(np.int64), z.astype(np.int64)
-    res = engine.align(windows, uniq, scoring_scheme_vals)
-    full, part, rs, re_ = (x.reshape(len(uniq), n_win)[idx] for x in identities(res))
-    return full, part, rs, re_
-
-
 # ---------------------------------------------------------------------------------------------
 def find_matching_adapter_sets(check_reads, verbosity, end_size, scoring_scheme_vals, print_dest,
                                adapter_threshold, threads, adapter_sets=None):
@@ -90,29 +78,30 @@ def find_matching_adapter_sets(check_reads, verbosity, end_size, scoring_scheme_
     return [a for a in search if a.best_start_or_end_score() >= adapter_threshold]
 
 
-def set_search_maxima(check_reads, end_size, scoring_scheme_vals, search, out_device_ptr=None):
+def set_search_maxima(check_reads, end_size, scoring_scheme_vals, search, out_device_ptr=None, device=0):
     """The check phase's reduction (nanopore_read.py:158-173 over every check read): per distinct
     start sequence, then per distinct end sequence of the searched sets, the best full-adapter
-    identity over the reads' windows -- reduced on the GPU (engine.best_full_identity), the
-    (adapter, window) results never leaving the device. Returns the float64 maxima (start
-    sequences first), or, with out_device_ptr (an int device address of as many float64), writes
-    them there and returns None (the buffer the sharded drivers all-reduce)."""
+    identity over the reads' windows -- reduced on GPU `device` (engine.best_full_identity), the
+    (adapter, window) results never leaving it. Returns the float64 maxima (start sequences
+    first), or, with out_device_ptr (an int device address of as many float64 ON `device`),
+    writes them there and returns None (the buffer the sharded drivers all-reduce)."""
     starts_u, _ = _unique([a.start_sequence[1] for a in search if a.start_sequence])
     ends_u, _ = _unique([a.end_sequence[1] for a in search if a.end_sequence])
-    pack = SeqPack([r.seq for r in check_reads])
-    sw, ew = start_end_windows(pack, end_size)
+    codes, (s_off, s_len), (e_off, e_len) = end_windows_pack(check_reads, end_size)
+    sw, ew = (codes, s_off, s_len), (codes, e_off, e_len)
     if out_device_ptr is not None:
         if starts_u and len(check_reads):
-            engine.best_full_identity(sw, starts_u, scoring_scheme_vals, best_device_ptr=out_device_ptr)
+            engine.best_full_identity(sw, starts_u, scoring_scheme_vals, device=device, best_device_ptr=out_device_ptr)
         if ends_u and len(check_reads):
-            engine.best_full_identity(ew, ends_u, scoring_scheme_vals, best_device_ptr=out_device_ptr + 8 * len(starts_u))
+            engine.best_full_identity(ew, ends_u, scoring_scheme_vals, device=device,
+                                      best_device_ptr=out_device_ptr + 8 * len(starts_u))
         return None
     out = np.zeros(len(starts_u) + len(ends_u), np.float64)
     if len(check_reads):
         if starts_u:
-            out[:len(starts_u)] = engine.best_full_identity(sw, starts_u, scoring_scheme_vals)
+            out[:len(starts_u)] = engine.best_full_identity(sw, starts_u, scoring_scheme_vals, device=device)
         if ends_u:
-            out[len(starts_u):] = engine.best_full_identity(ew, ends_u, scoring_scheme_vals)
+            out[len(starts_u):] = engine.best_full_identity(ew, ends_u, scoring_scheme_vals, device=device)
     return out
 
 
@@ -204,14 +193,10 @@ def find_adapters_at_read_ends(reads, matching_sets, verbosity, end_size, extra_
     if verbosity == 1:
         output_progress_line(0, read_count, print_dest)
     if reads:
-        pack = SeqPack([r.seq for r in reads])
-        sw, ew = start_end_windows(pack, end_size)
         starts = [a for a in matching_sets if a.start_sequence]
         ends = [a for a in matching_sets if a.end_sequence]
-        s_hits = _window_hits(sw, [a.start_sequence[1] for a in starts], scoring_scheme_vals)
-        e_hits = _window_hits(ew, [a.end_sequence[1] for a in ends], scoring_scheme_vals)
-        _apply_end_decisions(reads, starts, s_hits, ends, e_hits, end_size, extra_trim_size, end_threshold,
-                             min_trim_size, check_barcodes, forward_or_reverse_barcodes)
+        _end_decisions(reads, starts, ends, end_size, extra_trim_size, end_threshold, scoring_scheme_vals,
+                       min_trim_size, check_barcodes, forward_or_reverse_barcodes)
         if check_barcodes:
             for r in reads:
                 r.determine_barcode(barcode_threshold, barcode_diff, require_two_barcodes)
@@ -221,38 +206,67 @@ def find_adapters_at_read_ends(reads, matching_sets, verbosity, end_size, extra_
         print('', file=print_dest)
 
 
-def _apply_end_decisions(reads, starts, s_hits, ends, e_hits, end_size, extra, thr, min_trim,
-                         check_barcodes, fwd_rev):
-    """Vectorised trim amounts + the reference's per-read alignment lists, in adapter order."""
-    for side, sets, hits in (('start', starts, s_hits), ('end', ends, e_hits)):
-        full, part, rs, re_ = hits
-        if not sets:
+def end_windows_pack(reads, end_size):
+    """The reads' start and end windows, seq[:end_size] and seq[-end_size:] as the reference slices
+    them (nanopore_read.py:181, 203), packed into one Dna5 buffer: (codes, start views, end views)
+    -- only the 2 x end_size bases per read travel, not the whole reads."""
+    n = len(reads)
+    pack = SeqPack([r.seq[:end_size] for r in reads] + [r.seq[-end_size:] for r in reads])
+    return pack.codes, (pack.offsets[:n], pack.lengths[:n]), (pack.offsets[n:], pack.lengths[n:])
+
+
+def _end_decisions(reads, starts, ends, end_size, extra, thr, scoring_scheme_vals, min_trim, check_barcodes,
+                   fwd_rev):
+    """The decisions of find_start_trim / find_end_trim (nanopore_read.py:175-217) for every read at
+    once, on the device (engine.end_decisions: k_end_trim, then only the recorded alignments and --
+    with -b -- the barcode identities come back): trim amounts, the start / end alignment lists in
+    the reference's order (read, then set order) and the barcode dicts. Distinct sequences are
+    aligned once; a list entry is made for every set holding the sequence."""
+    codes, sw, ew = end_windows_pack(reads, end_size)
+    s_u, s_idx = _unique([a.start_sequence[1] for a in starts])
+    e_u, e_idx = _unique([a.end_sequence[1] for a in ends])
+    bc = [[k for k, a in enumerate(sets) if check_barcodes and a.is_barcode() and a.barcode_direction() == fwd_rev]
+          for sets in (starts, ends)]
+    st, et, s_list, e_list, bc_full = engine.end_decisions(
+        codes, sw, ew, s_u, e_u, scoring_scheme_vals, end_size, extra, thr, min_trim,
+        bc_start=s_idx[bc[0]] if bc[0] else None, bc_end=e_idx[bc[1]] if bc[1] else None)
+    for r, a, b in zip(reads, st.tolist(), et.tolist()):
+        if a > r.start_trim_amount:
+            r.start_trim_amount = a
+        if b > r.end_trim_amount:
+            r.end_trim_amount = b
+    for sets, idx, lst, attr in ((starts, s_idx, s_list, 'start_adapter_alignments'),
+                                 (ends, e_idx, e_list, 'end_adapter_alignments')):
+        if not sets or not lst.shape[1]:
             continue
-        if side == 'start':
-            ok = (part > thr) & (re_ != end_size) & (re_ - rs >= min_trim)
-            amount = np.where(ok, re_ + extra, 0)
-        else:
-            ok = (part > thr) & (rs != 0) & (re_ - rs >= min_trim)
-            amount = np.where(ok, (end_size - rs) + extra, 0)
-        best = amount.max(axis=0)
-        hit_reads, hit_adps = np.nonzero(ok.T)          # read-major, adapter order within a read
-        bc = [k for k, a in enumerate(sets)
-              if check_barcodes and a.is_barcode() and a.barcode_direction() == fwd_rev]
-        bc_names = [sets[k].get_barcode_name() for k in bc]
-        for i, r in enumerate(reads):
-            if side == 'start':
-                r.start_trim_amount = max(r.start_trim_amount, int(best[i]))
-            else:
-                r.end_trim_amount = max(r.end_trim_amount, int(best[i]))
-        lst_attr = 'start_adapter_alignments' if side == 'start' else 'end_adapter_alignments'
-        for i, k in zip(hit_reads.tolist(), hit_adps.tolist()):
-            getattr(reads[i], lst_attr).append((sets[k], float(full[k, i]), float(part[k, i]),
-                                                int(rs[k, i]), int(re_[k, i])))
-        if bc:
-            fb = full[bc]
+        # distinct sequence -> the sets holding it (set order)
+        members = {}
+        for k, u in enumerate(idx.tolist()):
+            members.setdefault(u, []).append(k)
+        read, u, rs, re_, m, l1, l2 = lst
+        rep = np.array([len(members[x]) for x in u.tolist()], np.int64)
+        set_k = np.concatenate([np.array(members[x], np.int64) for x in u.tolist()])
+        read = np.repeat(read, rep)
+        order = np.lexsort((set_k, read))           # read-major, set order within a read
+        failed = rs == -1
+        full = np.where(failed, 0.0, engine.pid6(m, l2))
+        part = np.where(failed, 0.0, engine.pid6(m, l1))
+        re_x = np.where(failed, 0, re_ + 1)
+        full, part, rs, re_x = (np.repeat(x, rep)[order] for x in (full, part, rs, re_x))
+        for i, k, f, p, a, b in zip(read[order].tolist(), set_k[order].tolist(), full.tolist(), part.tolist(),
+                                    rs.tolist(), re_x.tolist()):
+            getattr(reads[i], attr).append((sets[k], f, p, a, b))
+    if bc_full is not None:
+        j0 = 0
+        for side, sets in ((0, starts), (1, ends)):
+            names = [sets[k].get_barcode_name() for k in bc[side]]
+            block = bc_full[j0:j0 + len(names)]
+            j0 += len(names)
+            if not names:
+                continue
             for i, r in enumerate(reads):
-                d = r.start_barcode_scores if side == 'start' else r.end_barcode_scores
-                for name, v in zip(bc_names, fb[:, i].tolist()):
+                d = r.start_barcode_scores if side == 0 else r.end_barcode_scores
+                for name, v in zip(names, block[:, i].tolist()):
                     d[name] = v
 
 

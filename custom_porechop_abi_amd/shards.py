@@ -54,16 +54,31 @@ def _device_tensor(values, group):
     return t
 
 
+def rank_device(device=None):
+    """The GPU of this rank: `device` if given, else LOCAL_RANK (torch.distributed.run sets it),
+    else 0 -- one process per GPU, each rank on its own card."""
+    import os
+    if device is not None:
+        return int(device)
+    dev = int(os.environ.get('LOCAL_RANK', '0'))
+    import torch
+    n = torch.cuda.device_count()   # counting does not initialise the GPU
+    return dev % n if n > 0 else dev
+
+
 def find_matching_adapter_sets(check_reads, verbosity, end_size, scoring_scheme_vals, print_dest,
-                               adapter_threshold, threads, adapter_sets=None, group=None):
+                               adapter_threshold, threads, adapter_sets=None, group=None, device=None):
     """Sharded porechop_abi.find_matching_adapter_sets: check_reads is the FULL check list (same
-    on every rank); each rank reduces its shard's windows on its GPU into the per-sequence maxima
-    (porechop_abi.set_search_maxima: the (adapter, window) results never leave the device), and
-    those maxima are all-reduced with MAX. With "nccl" (RCCL) the kernel writes them straight into
-    the device buffer the collective reduces; with "gloo" they go through the host."""
+    on every rank); each rank reduces its shard's windows on its GPU (rank_device(device)) into
+    the per-sequence maxima (porechop_abi.set_search_maxima: the (adapter, window) results never
+    leave the device), and those maxima are all-reduced with MAX. With "nccl" (RCCL) the kernel
+    writes them straight into the device buffer the collective reduces -- allocated on the same
+    GPU the kernel runs on (include/pcabi.h: `best` lives on `device`); with "gloo" they go
+    through the host."""
     dist = _dist()
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     world = dist.get_world_size(group) if dist.is_initialized() else 1
+    dev = rank_device(device)
     if adapter_sets is None:
         adapter_sets = _adapters.ADAPTERS
     if not dist.is_initialized():
@@ -75,12 +90,18 @@ def find_matching_adapter_sets(check_reads, verbosity, end_size, scoring_scheme_
         len(set(a.end_sequence[1] for a in search if a.end_sequence))
     import torch
     if dist.get_backend(group) == 'nccl':
-        t = torch.zeros(max(n_u, 1), dtype=torch.float64, device='cuda')
-        torch.cuda.synchronize()
-        P.set_search_maxima(check_reads[lo:hi], end_size, scoring_scheme_vals, search, out_device_ptr=t.data_ptr())
+        # RCCL reduces on the current device: make it the rank's, and put the buffer there
+        torch.cuda.set_device(dev)
+        t = torch.zeros(max(n_u, 1), dtype=torch.float64, device=torch.device('cuda', dev))
+        if t.device.index != dev:
+            raise RuntimeError('set-search buffer on cuda:%s, kernels on device %d' % (t.device.index, dev))
+        torch.cuda.synchronize(dev)
+        P.set_search_maxima(check_reads[lo:hi], end_size, scoring_scheme_vals, search, out_device_ptr=t.data_ptr(),
+                            device=dev)
     else:
         t = torch.zeros(max(n_u, 1), dtype=torch.float64)
-        t[:n_u] = torch.from_numpy(P.set_search_maxima(check_reads[lo:hi], end_size, scoring_scheme_vals, search))
+        t[:n_u] = torch.from_numpy(P.set_search_maxima(check_reads[lo:hi], end_size, scoring_scheme_vals, search,
+                                                       device=dev))
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     P.apply_set_maxima(search, t.cpu().numpy()[:n_u])
     return [a for a in search if a.best_start_or_end_score() >= adapter_threshold]
@@ -151,7 +172,7 @@ def trim_file_sharded(in_path, out_path, out_format='fastq', scoring_scheme_vals
                       extra_middle_trim_good_side=10, extra_middle_trim_bad_side=100, min_split_read_size=1000,
                       check_reads=10000, adapter_threshold=90.0, max_reads=100000, group=None, device=None,
                       trimmer_factory=None, barcode_dir=None, barcode_threshold=75.0, barcode_diff=5.0,
-                      require_two_barcodes=False, untrimmed=False, discard_unassigned=False):
+                      require_two_barcodes=False, untrimmed=False, discard_unassigned=False, inflate_dir=None):
     """The CLI's file-to-file path (porechop_abi.py:41-131: adapter-set search on the first
     check_reads records, end trim, middle scan, the fork's filter, trimmed output) on every rank of
     `group`, one GPU each:
@@ -161,9 +182,11 @@ def trim_file_sharded(in_path, out_path, out_format='fastq', scoring_scheme_vals
         under RCCL);
       * trimming: a plain file is split into contiguous record ranges of about equal bytes (so
         bases), cut at record starts (misc.record_boundaries); each rank trims its range with a
-        pipeline.FileTrimmer into its own part file, in order; a gzip file cannot be entered
-        mid-stream, so every rank streams it and trims every world-th batch, recording the byte
-        span of each batch it writes;
+        pipeline.FileTrimmer into its own part file, in order. A gzip file cannot be entered
+        mid-stream: rank 0 alone inflates it (one zlib stream per job, not one per rank) into a
+        plain file next to the output (inflate_dir overrides, e.g. /dev/shm), and every rank then
+        takes its record range of that file as above. An Albacore directory is streamed by every
+        rank, which trims every world-th batch and records the byte span of each batch it writes;
       * output: rank 0 concatenates the parts in record order (the reference's output order) --
         the only other exchange is the span lists (gzip input) and the read counts.
 
@@ -180,13 +203,12 @@ def trim_file_sharded(in_path, out_path, out_format='fastq', scoring_scheme_vals
     dist = _dist()
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     world = dist.get_world_size(group) if dist.is_initialized() else 1
-    check = []
-    if check_reads > 0:
-        for b in misc.read_batches(in_path, max_reads=check_reads):
-            check = b.nanopore_reads()
-            break
+    # load_reads' check reads (porechop_abi.py:133-187): the first check_reads records of a file,
+    # however many bases they hold; spread over the files of an Albacore directory
+    check = misc.load_check_reads(in_path, check_reads) if check_reads > 0 else []
+    dev = rank_device(device)
     matching = find_matching_adapter_sets(check, 0, end_size, scoring_scheme_vals, io.StringIO(), adapter_threshold, 1,
-                                          group=group)
+                                          group=group, device=dev)
     matching = P.fix_up_1d2_sets(matching)
     fwd_rev = P.choose_barcoding_kit(matching, 0, io.StringIO()) if barcode_dir is not None else None
     matching = P.add_full_barcode_adapter_sets(matching)
@@ -202,18 +224,30 @@ def trim_file_sharded(in_path, out_path, out_format='fastq', scoring_scheme_vals
     if trimmer_factory is None:
         from .pipeline import FileTrimmer
         trimmer_factory = FileTrimmer
-        opts['device'] = int(os.environ.get('LOCAL_RANK', rank)) if device is None else device
+        opts['device'] = dev
     ft = trimmer_factory(matching, **opts)
     d, base = os.path.split(os.path.abspath(out_path))
     part = lambda r: os.path.join(d, '.pcabi_part%d_%s' % (r, base))
-    bounds = misc.record_boundaries(in_path, world)
+    src = in_path
+    inflated = None
+    if world > 1 and os.path.isfile(in_path) and misc.get_compression_type(in_path) == 'gz':
+        # one inflater per job: rank 0 writes the plain text once, every rank maps its range of it
+        inflated = os.path.join(inflate_dir or d, '.pcabi_inflated_%s' % base)
+        if rank == 0:
+            import gzip
+            with gzip.open(in_path, 'rb') as fi, open(inflated + '.tmp', 'wb') as fo:
+                shutil.copyfileobj(fi, fo, 1 << 24)
+            os.replace(inflated + '.tmp', inflated)
+        dist.barrier(group=group)
+        src = inflated
+    bounds = misc.record_boundaries(src, world)
     segments = None if (bounds is not None and barcode_dir is None) else []
     try:
         if bounds is not None:
-            counts = ft.trim_file(in_path, part(rank), out_format, max_reads, byte_range=(bounds[rank], bounds[rank + 1]),
+            counts = ft.trim_file(src, part(rank), out_format, max_reads, byte_range=(bounds[rank], bounds[rank + 1]),
                                   segments=segments)
         else:
-            counts = ft.trim_file(in_path, part(rank), out_format, max_reads,
+            counts = ft.trim_file(src, part(rank), out_format, max_reads,
                                   batch_filter=lambda k: k % world == rank, segments=segments)
     finally:
         if hasattr(ft, 'close'):
@@ -262,6 +296,8 @@ def trim_file_sharded(in_path, out_path, out_format='fastq', scoring_scheme_vals
                 os.remove(part(r))
     if world > 1:
         dist.barrier(group=group)
+    if inflated is not None and rank == 0 and os.path.exists(inflated):
+        os.remove(inflated)
     out = {k: sum(c[k] for _, c in spans) for k in ('reads_in', 'reads_kept')}
     if barcode_dir is not None:
         out['bins'] = sorted(set(nm for segs, _ in spans for _, nm, _, _ in segs))

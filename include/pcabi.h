@@ -198,6 +198,39 @@ int pcabi_end_trim_dev(const int32_t *start_res, int64_t start_stride, int32_t n
                        uint8_t *start_hit, uint8_t *end_hit, void *stream);
 
 /*
+ * End-trim decisions with their alignment lists (porechop_abi/nanopore_read.py:175-217, the loop of
+ * find_adapters_at_read_ends, porechop_abi.py:359-438) from HOST buffers, with only the decisions
+ * coming back -- never the (read, adapter) result matrix:
+ *   codes / s_off, s_len / e_off, e_len : start and end windows of n_read reads (layout of
+ *                         pcabi_align_host: one buffer, any offsets, 16 bytes of padding)
+ *   sa_* / ea_*         : start and end adapters (Dna5 codes)
+ *   start_trim / end_trim[n_read] : NanoporeRead.start_trim_amount / end_trim_amount
+ *   start_hits / end_hits : 7 rows x cap int32 -- every alignment find_start_trim / find_end_trim
+ *                         record, read-major and in adapter order within a read (the order they
+ *                         are appended): read, adapter, rs, re (inclusive), m, l1, l2 (full identity
+ *                         = pid6(m, l2), partial = pid6(m, l1)); n_hits[2] receives the two counts,
+ *                         and a side whose count exceeds cap is not written (call again, larger cap)
+ *   bc_s[n_bc_s], bc_e[n_bc_e] : adapters whose full identity of every read the barcode dicts keep
+ *                         (nanopore_read.py:193-195, 215-217); bc_full (double, (n_bc_s + n_bc_e) x
+ *                         n_read, start adapters first) receives them when non-NULL
+ * The prepared adapter tables are kept per device between calls with the same adapters and scoring.
+ *   pcabi_flag_list_dev : the list of one side from device pointers (async on `stream`): flagged
+ *                         pairs (k_end_trim's flags, layout of pcabi_end_trim_dev) of a result
+ *                         block -> out (7 rows x cap, as above), *n_out (device uint64) = the count.
+ */
+int pcabi_end_decisions_host(int device, const uint8_t *codes, int64_t codes_len, const int64_t *s_off,
+                             const int32_t *s_len, const int64_t *e_off, const int32_t *e_len, int64_t n_read,
+                             const uint8_t *sa_codes, const int32_t *sa_off, const int32_t *sa_len, int32_t n_sa,
+                             const uint8_t *ea_codes, const int32_t *ea_off, const int32_t *ea_len, int32_t n_ea,
+                             int match, int mismatch, int gap_open, int gap_extend, int end_size, int extra_trim,
+                             double end_threshold, int min_trim_size, int32_t *start_trim, int32_t *end_trim,
+                             int32_t *start_hits, int32_t *end_hits, int64_t cap, int64_t *n_hits,
+                             const int32_t *bc_s, int32_t n_bc_s, const int32_t *bc_e, int32_t n_bc_e,
+                             double *bc_full);
+int pcabi_flag_list_dev(const uint8_t *flag, int32_t n_adp, int64_t n_read, const int32_t *res, int64_t stride,
+                        int32_t *out, int64_t cap, unsigned long long *n_out, void *stream);
+
+/*
  * Middle-adapter scan, round 1 (porechop_abi/nanopore_read.py:219-252): for every window
  * (whole end-trimmed read) the FIRST adapter in list order whose full-adapter identity
  * (pid2, compared after the "%f" round trip like the reference) is not below `threshold`.
@@ -392,7 +425,8 @@ int pcabi_kmer_approx_host(int device, const uint8_t *codes, int64_t codes_len, 
  *       written as its split parts, or dropped with discard_middle), FASTA (70-column lines) or
  *       FASTQ, gzip when gz != 0, appended when append != 0, path "-" = stdout (plain only);
  *       untrimmed != 0 writes reads without cuts whole (split parts still come from the trimmed
- *       sequence, as in the reference).
+ *       sequence, as in the reference). Returns the number of reads that produced output (the
+ *       reference's non-empty read strings, porechop_abi.py:598-604), or a negative PCABI_E_*.
  */
 enum { PCABI_FASTA = 0, PCABI_FASTQ = 1 };
 typedef struct pcabi_fastx pcabi_fastx;

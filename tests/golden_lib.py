@@ -24,6 +24,12 @@ def g1_long_rows():
     return g1_rows('g1_long.tsv.gz')
 
 
+def g1_freegap_rows():
+    """The same under gap costs >= 0, match <= 0 and all-zero scorings, reads up to 70 kb --
+    tools/make_golden_g1_freegap.py."""
+    return g1_rows('g1_freegap.tsv.gz')
+
+
 def g2():
     """Reference driver decisions -- tools/make_golden_g2.py."""
     with gzip.open(os.path.join(GOLDEN, 'g2_decisions.json.gz'), 'rt') as f:

@@ -181,3 +181,36 @@ def best_full_identity_windows(windows, adapter_seqs, scoring, best=None, device
     res = align_windows(windows, adapter_seqs, scoring)
     full = np.where(res[0] == -1, 0.0, pid6(res[5], res[7])).reshape(n_adp, n_win)
     return np.maximum(out, full.max(axis=1))
+
+
+def end_decisions_windows(codes, start_windows, end_windows, start_seqs, end_seqs, scoring, end_size, extra_trim,
+                          end_threshold, min_trim_size, bc_start=None, bc_end=None, device=0):
+    """Drop-in for custom_porechop_abi_amd.engine.end_decisions computed by the oracle (CPU): the
+    alignments of both sides, find_start_trim / find_end_trim's rules (nanopore_read.py:175-217)
+    restated over them, the recorded alignments as (read, adapter, rs, re, m, l1, l2) lists in the
+    reference's order, and the listed adapters' full identities."""
+    from custom_porechop_abi_amd.engine import pid6
+    n = len(start_windows[1])
+    trims, lists, fulls = [], [], []
+    for side, (win, seqs, sel) in enumerate(((start_windows, start_seqs, bc_start), (end_windows, end_seqs, bc_end))):
+        na = len(seqs)
+        if na == 0 or n == 0:
+            trims.append(np.zeros(n, np.int32))
+            lists.append(np.zeros((7, 0), np.int32))
+            continue
+        res = align_windows((codes, win[0], win[1]), list(seqs), scoring).reshape(8, na, n)
+        rs = res[0]
+        failed = rs == -1
+        re1 = np.where(failed, 0, res[1] + 1)
+        part = np.where(failed, 0.0, pid6(res[5].ravel(), res[6].ravel()).reshape(na, n))
+        full = np.where(failed, 0.0, pid6(res[5].ravel(), res[7].ravel()).reshape(na, n))
+        edge = (re1 != end_size) if side == 0 else (rs != 0)
+        ok = (part > end_threshold) & edge & (re1 - rs >= min_trim_size)
+        amount = np.where(ok, (re1 + extra_trim) if side == 0 else (end_size - rs) + extra_trim, 0)
+        trims.append(np.maximum(amount.max(axis=0), 0).astype(np.int32))
+        r, a = np.nonzero(ok.T)                    # read-major, adapter order within a read
+        lists.append(np.stack([r, a, rs[a, r], res[1][a, r], res[5][a, r], res[6][a, r], res[7][a, r]]).astype(np.int32))
+        if sel is not None and len(sel):
+            fulls.append(full[np.asarray(sel)])
+    bc_full = np.concatenate(fulls, axis=0) if fulls else None
+    return trims[0], trims[1], lists[0], lists[1], bc_full

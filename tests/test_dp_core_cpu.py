@@ -579,3 +579,23 @@ def test_striped_core_chunks(model, sc):
         else:
             assert best[4] < T
     assert n_hi > 20
+
+
+def test_cores_free_gap_schemes_golden(model):
+    """Scorings with gap costs >= 0, match <= 0 or all zero (the reference accepts any four
+    integers, porechop_abi/arg_parser.py:229-236), on the reference's own rows
+    (tests/golden/g1_freegap.tsv.gz): the generic core (the register buckets such schemes get) on
+    windows below 32 k, and the striped core -- where the engine routes windows of 32 k and more
+    under a scoring with no path-span bound -- on every row, the 33-70 kb reads included."""
+    n_gen = n_str = n_long = 0
+    for sc, r, a, exp in golden_lib.g1_freegap_rows():
+        if not r or not a:
+            continue
+        if len(a) <= 128 and len(r) < 32768 - 256:
+            rc, res = _run(model, 'pcabi_model_align', r, a, sc)
+            assert rc == 0 and _fmt(res) == exp, (sc, len(r), len(a), exp, res)
+            n_gen += 1
+        assert _fmt(_striped(model, r, a, sc, 32)) == exp, (sc, len(r), len(a))
+        n_str += 1
+        n_long += len(r) >= 32768
+    assert n_gen >= 1500 and n_str >= 1800 and n_long >= 30

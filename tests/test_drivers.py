@@ -83,6 +83,7 @@ def check_case(case):
 def test_drivers_match_reference_with_oracle_backend(case_name, monkeypatch):
     from custom_porechop_abi_amd import engine
     monkeypatch.setattr(engine, 'align', oracle_lib.align_windows)
+    monkeypatch.setattr(engine, 'end_decisions', oracle_lib.end_decisions_windows)
     monkeypatch.setattr(engine, 'best_full_identity', oracle_lib.best_full_identity_windows)
     monkeypatch.setattr(engine, 'first_hits', oracle_lib.first_hits_windows)
     monkeypatch.setattr(engine, 'middle_scan', oracle_lib.middle_scan_windows)
@@ -100,6 +101,7 @@ def test_reference_test_expectations_one_adapter_set(monkeypatch):
     3 of 9 end-trimmed -- on the G2 decisions and through our drivers."""
     from custom_porechop_abi_amd import engine
     monkeypatch.setattr(engine, 'align', oracle_lib.align_windows)
+    monkeypatch.setattr(engine, 'end_decisions', oracle_lib.end_decisions_windows)
     monkeypatch.setattr(engine, 'best_full_identity', oracle_lib.best_full_identity_windows)
     monkeypatch.setattr(engine, 'first_hits', oracle_lib.first_hits_windows)
     monkeypatch.setattr(engine, 'middle_scan', oracle_lib.middle_scan_windows)

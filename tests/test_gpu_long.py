@@ -19,7 +19,8 @@ import pytest
 
 from tests import golden_lib, oracle_lib
 
-SCHEMES = [(3, -6, -5, -2), (2, -1, -1, -1), (1, -1, -3, -1), (3, -6, -2, -5), (5, -4, -8, -6)]
+SCHEMES = [(3, -6, -5, -2), (2, -1, -1, -1), (1, -1, -3, -1), (3, -6, -2, -5), (5, -4, -8, -6),
+           (2, -1, 0, 0), (5, -4, -1, 0)]   # the last two: gap costs >= 0 (no path-span bound)
 LONG_L = (129, 200, 255, 512, 1000)
 
 

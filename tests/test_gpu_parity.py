@@ -16,7 +16,10 @@ SCHEMES = [(3, -6, -5, -2),   # reference default (arg_parser.py:178-180)
            (1, -1, -3, -1),
            (3, -6, -2, -5),   # open cheaper than extend
            (5, -4, -8, -6),
-           (1, 3, -5, -2)]    # mismatch outscoring match (any --scoring_scheme is accepted)
+           (1, 3, -5, -2),    # mismatch outscoring match (any --scoring_scheme is accepted)
+           # gap costs >= 0, match <= 0, all zero: no path-span bound (tests/test_gpu_freegap.py
+           # covers them on 32 k+ reads and the device table ABI)
+           (2, -1, 0, 0), (3, -6, 0, -2), (1, -1, 1, 1), (0, 0, 0, 0), (-1, -1, -1, -1), (3, -6, 2, -1)]
 
 
 def _rand_seq(rng, n, alph):

@@ -6,10 +6,10 @@ import pytest
 from tests import golden_lib, oracle_lib
 
 
-@pytest.mark.parametrize('which', ['g1', 'g1_long'])
+@pytest.mark.parametrize('which', ['g1', 'g1_long', 'g1_freegap'])
 def test_oracle_matches_reference_vectors(which):
-    rows = golden_lib.g1_rows() if which == 'g1' else golden_lib.g1_long_rows()
-    assert len(rows) >= (20000 if which == 'g1' else 1500)
+    rows = {'g1': golden_lib.g1_rows, 'g1_long': golden_lib.g1_long_rows, 'g1_freegap': golden_lib.g1_freegap_rows}[which]()
+    assert len(rows) >= {'g1': 20000, 'g1_long': 1500, 'g1_freegap': 2000}[which]
     bad = []
     for sc, r, a, exp in rows:
         got = oracle_lib.result_string(r, a, sc)

@@ -281,3 +281,40 @@ def test_output_reads_barcode_bins_and_file(flags, tmp_path):
                    flags.get('untrimmed', False), 1, False)
     got = gzip.open(out, 'rt').read() if gz else open(out).read()
     assert got == ''.join(r.get_fastq(1000, False) for r in reads)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('run', [0, 1, 2])
+def test_albacore_directory_on_gpu(gpu_lib, tmp_path, run):
+    """An Albacore output directory (the reference's own test/test_albacore_directory: barcode01..03
+    and unclassified) through shards.trim_file_sharded with the real FileTrimmer on this GPU and
+    the set search through RCCL: the check reads spread over the files, -b calls nulled where the
+    directory's barcode disagrees (nanopore_read.py:479-482) -- bins / output == the reference's own
+    CLI flow on the same directory (tests/golden/g2_albacore.json.gz)."""
+    import gzip
+    import json
+    import socket
+    import torch.distributed as dist
+    from custom_porechop_abi_amd import shards
+    with gzip.open(os.path.join(golden_lib.GOLDEN, 'g2_albacore.json.gz'), 'rt') as f:
+        exp = json.load(f)['runs'][run]
+    in_dir = os.path.join(golden_lib.GOLDEN, 'data', 'albacore')
+    bdir = str(tmp_path / 'bins') if exp['barcodes'] else None
+    out_path = str(tmp_path / 'out.fastq')
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group('nccl', init_method='tcp://127.0.0.1:%d' % port, rank=0, world_size=1)
+    try:
+        counts = shards.trim_file_sharded(in_dir, out_path, 'fastq', check_reads=exp['check_reads_arg'], max_reads=5,
+                                          device=0, barcode_dir=bdir)
+    finally:
+        dist.destroy_process_group()
+    assert counts['reads_in'] == 32
+    if bdir:
+        assert sorted(os.listdir(bdir)) == sorted(exp['bins'])
+        for name, txt in exp['bins'].items():
+            assert open(os.path.join(bdir, name)).read() == txt, name
+    else:
+        assert open(out_path).read() == exp['output']

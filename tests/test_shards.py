@@ -49,6 +49,7 @@ def _worker(rank, world, port, case_name, out_dir):
     from custom_porechop_abi_amd.nanopore_read import NanoporeRead
     from tests import oracle_lib
     engine.align = oracle_lib.align_windows            # CPU stand-ins for the HIP kernels
+    engine.end_decisions = oracle_lib.end_decisions_windows
     engine.best_full_identity = oracle_lib.best_full_identity_windows
     engine.first_hits = oracle_lib.first_hits_windows
     engine.middle_scan = oracle_lib.middle_scan_windows
@@ -156,10 +157,12 @@ class _OracleTrimmer(object):
         self._tick = FileTrimmer._tick.__get__(self)
         self._write_bins = FileTrimmer._write_bins.__get__(self)
 
-    def trim(self, batch):
+    def trim(self, batch, albacore=None):
         import numpy as np
         from custom_porechop_abi_amd import misc, porechop_abi as P
         reads = batch.nanopore_reads()
+        for r in reads:                       # load_reads' Albacore barcode (porechop_abi.py:172-177)
+            r.albacore_barcode_call = albacore
         sink = io.StringIO()
         if self.m:
             P.find_adapters_at_read_ends(reads, self.m, 0, self.E, self.extra, self.thr, self.sc, sink, self.min_trim, 1,
@@ -191,6 +194,7 @@ def _file_worker(rank, world, port, case_name, in_path, out_path, res_path, bins
     from custom_porechop_abi_amd import engine, shards
     from tests import oracle_lib
     engine.align = oracle_lib.align_windows
+    engine.end_decisions = oracle_lib.end_decisions_windows
     engine.best_full_identity = oracle_lib.best_full_identity_windows
     engine.first_hits = oracle_lib.first_hits_windows
     engine.middle_scan = oracle_lib.middle_scan_windows
@@ -214,8 +218,8 @@ def _file_worker(rank, world, port, case_name, in_path, out_path, res_path, bins
 @pytest.mark.parametrize('case_name', ['two_adapter_sets', 'synthetic_default'])
 def test_sharded_file_pipeline_matches_reference(case_name, gz, tmp_path):
     """shards.trim_file_sharded at world size 2 (gloo): the check-read set search with one MAX
-    all-reduce, record ranges split at record starts (plain input) or every other batch (gzip
-    input), per-rank part files stitched in record order -- the written file == the reference's
+    all-reduce, record ranges split at record starts (plain input; gzip input: of the plain text
+    rank 0 alone inflated), per-rank part files stitched in record order -- the written file == the reference's
     output for the same reads (G2 decisions through get_fastq, as tests/test_pipeline.py)."""
     import gzip
     import torch.multiprocessing as mp
@@ -239,7 +243,8 @@ def test_sharded_file_pipeline_matches_reference(case_name, gz, tmp_path):
     counts = [json.load(open(res_path % r)) for r in range(2)]
     assert counts[0] == counts[1] and counts[0]['reads_in'] == len(records)
     assert open(out_path).read() == _expected(case, records)
-    assert not [f for f in os.listdir(str(tmp_path)) if f.startswith('.pcabi_part')]
+    # gzip input: rank 0 inflated it once into a plain file both ranks took record ranges of
+    assert not [f for f in os.listdir(str(tmp_path)) if f.startswith('.pcabi_part') or f.startswith('.pcabi_inflated')]
 
 
 @pytest.mark.parametrize('gz', [False, True])
@@ -267,3 +272,53 @@ def test_sharded_barcode_bins_match_reference(case_name, gz, tmp_path):
     assert sorted(os.listdir(bdir)) == sorted(k + '.fastq' for k in exp)
     for name, txt in exp.items():
         assert open(os.path.join(bdir, name + '.fastq')).read() == txt, name
+
+
+ALBACORE = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden', 'data', 'albacore')
+
+
+def _albacore_worker(rank, world, port, bins, check, out_path, res_path):
+    import torch.distributed as dist
+    from custom_porechop_abi_amd import engine, shards
+    from tests import oracle_lib
+    engine.align = oracle_lib.align_windows
+    engine.end_decisions = oracle_lib.end_decisions_windows
+    engine.best_full_identity = oracle_lib.best_full_identity_windows
+    engine.first_hits = oracle_lib.first_hits_windows
+    engine.middle_scan = oracle_lib.middle_scan_windows
+    dist.init_process_group('gloo', init_method='tcp://127.0.0.1:%d' % port, rank=rank, world_size=world)
+    try:
+        counts = shards.trim_file_sharded(ALBACORE, out_path, 'fastq', check_reads=check, max_reads=3,
+                                          trimmer_factory=_OracleTrimmer, barcode_dir=bins)
+        with open(res_path % rank, 'w') as f:
+            json.dump(counts, f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('run', [0, 1, 2])
+def test_sharded_albacore_directory_matches_reference(run, tmp_path):
+    """An Albacore output directory as the input (porechop_abi.py:133-187: every *.fastq(.gz) under
+    it in sorted order, the check reads spread over the files, each read tagged with its
+    directory's barcode) through shards.trim_file_sharded at world size 2 (gloo), with -b (the
+    device call nulled where Albacore disagrees, nanopore_read.py:479-482) and without: the bins /
+    the output == what the reference's own CLI flow wrote on the reference's own test directory
+    (tests/golden/g2_albacore.json.gz, tools/make_golden_albacore.py)."""
+    import gzip
+    import torch.multiprocessing as mp
+    with gzip.open(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden', 'g2_albacore.json.gz'),
+                   'rt') as f:
+        exp = json.load(f)['runs'][run]
+    bdir = str(tmp_path / 'bins') if exp['barcodes'] else None
+    out_path = str(tmp_path / 'out.fastq')
+    res_path = str(tmp_path / 'counts%d.json')
+    mp.spawn(_albacore_worker, args=(2, _free_port(), bdir, exp['check_reads_arg'], out_path, res_path), nprocs=2,
+             join=True)
+    counts = [json.load(open(res_path % r)) for r in range(2)]
+    assert counts[0]['reads_in'] == 32
+    if bdir:
+        assert sorted(os.listdir(bdir)) == sorted(exp['bins'])
+        for name, txt in exp['bins'].items():
+            assert open(os.path.join(bdir, name)).read() == txt, name
+    else:
+        assert open(out_path).read() == exp['output']

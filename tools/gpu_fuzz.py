@@ -3,7 +3,8 @@
 
     python tools/gpu_fuzz.py [seconds] [seed]
 
-Each iteration draws a scoring scheme, adapters (1..40 bp mostly, some up to 140, a few past
+Each iteration draws a scoring scheme (tests/test_gpu_parity.SCHEMES: gap costs >= 0, match <= 0
+and all-zero schemes among them), adapters (1..40 bp mostly, some up to 140, a few past
 128 -- the striped core) and windows (empty to 3 kb, ACGT / ACGTN / low-complexity alphabets,
 planted mutated adapter copies), then checks
   * the cross product (engine.align) and a random pairs subset, all 8 fields;
@@ -88,7 +89,7 @@ def main():
             print('PAIRS MISMATCH seed %d scheme %s' % (seed, sc), flush=True)
             fails += 1
         # middle scan (the reference's masked loop), a random threshold and mode
-        if sc[0] > 0 and rng.random() < 0.5:
+        if rng.random() < 0.5:
             th = rng.choice([80.0, 85.0, 88.0, 90.0, 95.0])
             mode = rng.choice([('PCABI_MIDDLE_SEEDS', '2'), ('PCABI_MIDDLE_SEEDS', '1'),
                                ('PCABI_MIDDLE_DEVPLAN', '0'), ('PCABI_MIDDLE_PLAN_WAVES', '1'),
