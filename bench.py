@@ -78,6 +78,8 @@ def parse():
                          'Rapid + RBK004, Barcode 1..12 (forward) + their 111 bp full rapid sequences')
     ap.add_argument('--middle-threshold', type=float, default=90.0)
     ap.add_argument('--middle-check', type=int, default=1000, help='middle: reads checked against the oracle loop')
+    ap.add_argument('--drivers-check', type=int, default=200,
+                    help='drivers: reads whose decisions are compared with the same drivers over the oracle')
     ap.add_argument('--check-phase-check', type=int, default=400,
                     help='check_phase: check reads whose device reduction is compared with the oracle')
     ap.add_argument('--only-subs', default='', help='comma-separated sub-record names to run (default: all)')
@@ -466,6 +468,8 @@ def run_other_configs(args, ctx):
         # the adapter-set search (configs[1]'s check phase: 10k reads x 119 sets) and its MAX
         # all-reduce (here over one rank)
         ('check_phase', lambda: run_check_phase(sub(), rank, 1, None, torch, L, _lib, A, synth, encode_adapters)),
+        # the reference-API path (porechop_abi.py's three drivers on 100k NanoporeRead objects)
+        ('drivers', lambda: run_drivers(sub(steps=2), rank, 1, None, torch, L, _lib, A, synth, encode_adapters)),
         # configs[2]: end trim + middle scan, 100k x 8 kb per GPU
         ('middle', lambda: run_middle(sub(workload='middle'), rank, 1, None, torch, L, _lib, A, synth,
                                       encode_adapters)),
@@ -667,6 +671,98 @@ def run_check_phase(args, rank, world, dist, torch, L, _lib, A, synth, encode_ad
                 'gcups_rank0': round(cells / (step_ms * 1e-3) / 1e9, 1),
                 'ranks_agree': agree, 'parity_spot_check': checked}
     return None
+
+
+def run_drivers(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapters):
+    """The reference-API path INTEGRATION.md §2 hands maintainers: the three phase drivers of
+    porechop_abi.py (find_matching_adapter_sets :200-245, find_adapters_at_read_ends :359-438,
+    find_adapters_in_read_middles :457-522) with their own signatures, on NanoporeRead objects of
+    100k synthetic reads (mean 8 kb) against the first 50 adapter sets. A step builds fresh
+    NanoporeRead objects (untimed) and times the three drivers: the check phase on the first 10k
+    reads against all sets, end trimming (device decisions: only trims and the recorded alignments
+    come back, engine.end_decisions) and the middle scan (only hits come back). Decisions of the
+    first --drivers-check reads are compared with the same drivers over the CPU oracle."""
+    import io
+    from custom_porechop_abi_amd import engine, porechop_abi as P
+    from custom_porechop_abi_amd.nanopore_read import NanoporeRead
+    n, E, sc = args.reads, args.end_size, SCORING
+    t0 = time.time()
+    seqs = [synth.codes_to_str(r) for r in synth.make_reads(n, args.mean_len, seed=12345 + rank)]
+    sets = [a for a in A.fresh_adapters() if '(full sequence)' not in a.name][:args.sets]
+    gen_s = time.time() - t0
+    sink = io.StringIO()
+    d2h = {}
+    real = engine.end_decisions
+
+    def counted(*a, **kw):                  # the end-trim driver's device -> host bytes
+        st, et, sl, el, bcf = real(*a, **kw)
+        d2h['bytes'] = st.nbytes + et.nbytes + sl.nbytes + el.nbytes + (bcf.nbytes if bcf is not None else 0) + 16
+        return st, et, sl, el, bcf
+
+    def drivers(reads, times):
+        ta = time.perf_counter()
+        P.find_matching_adapter_sets(reads[:10000], 0, E, sc, sink, 90.0, 1, adapter_sets=A.fresh_adapters())
+        tb = time.perf_counter()
+        P.find_adapters_at_read_ends(reads, sets, 0, E, 2, 75.0, sc, sink, 4, 1, False, 75.0, 5.0, False, None)
+        tc = time.perf_counter()
+        P.find_adapters_in_read_middles(reads, sets, 0, 90.0, 10, 100, sc, sink, 1, False)
+        td = time.perf_counter()
+        for k, v in (('check', tb - ta), ('ends', tc - tb), ('middles', td - tc)):
+            times[k] = times.get(k, 0.0) + v
+
+    engine.end_decisions = counted
+    try:
+        drivers([NanoporeRead('r%d' % i, s, '') for i, s in enumerate(seqs[:2000])], {})   # warm-up
+        times = {}
+        build = 0.0
+        for _ in range(args.steps):
+            tb = time.perf_counter()
+            reads = [NanoporeRead('r%d' % i, s, '') for i, s in enumerate(seqs)]
+            build += time.perf_counter() - tb
+            drivers(reads, times)
+    finally:
+        engine.end_decisions = real
+    total = sum(times.values()) / args.steps
+    checked = None
+    k = min(args.drivers_check, n)
+    if args.check and k:
+        # the same drivers over the CPU oracle (TEST INFRASTRUCTURE: the checker) on the first k
+        # reads, decisions compared read by read
+        from tests import oracle_lib
+        got = reads[:k]
+        sub = [NanoporeRead('r%d' % i, s, '') for i, s in enumerate(seqs[:k])]
+        saved = {f: getattr(engine, f) for f in ('align', 'end_decisions', 'best_full_identity', 'middle_scan')}
+        engine.align, engine.end_decisions = oracle_lib.align_windows, oracle_lib.end_decisions_windows
+        engine.best_full_identity = oracle_lib.best_full_identity_windows
+        engine.middle_scan = lambda v, a, s_, t, device=0: oracle_lib.middle_scan_threaded(v, a, s_, t)
+        try:
+            P.find_adapters_at_read_ends(sub, sets, 0, E, 2, 75.0, sc, sink, 4, 1, False, 75.0, 5.0, False, None)
+            P.find_adapters_in_read_middles(sub, sets, 0, 90.0, 10, 100, sc, sink, 1, False)
+        finally:
+            for f, v in saved.items():
+                setattr(engine, f, v)
+
+        def dec(r):
+            return (r.start_trim_amount, r.end_trim_amount,
+                    [(a[0].name,) + tuple(a[1:]) for a in r.start_adapter_alignments],
+                    [(a[0].name,) + tuple(a[1:]) for a in r.end_adapter_alignments],
+                    sorted(r.middle_adapter_positions), sorted(r.middle_trim_positions), r.middle_hit_str)
+        bad = sum(1 for a, b in zip(got, sub) if dec(a) != dec(b))
+        checked = {'reads_checked': k, 'mismatches': bad,
+                   'recorded_alignments': sum(len(r.start_adapter_alignments) + len(r.end_adapter_alignments)
+                                              for r in sub)}
+    return {'metric': 'reads/sec through the reference-API phase drivers (NanoporeRead objects)',
+            'value': round(n / total, 1), 'unit': 'reads/s', 'steps': args.steps, 'ms_per_step': round(1e3 * total, 2),
+            'ms_per_driver': {k: round(1e3 * v / args.steps, 2) for k, v in times.items()},
+            'nanopore_read_objects_ms': round(1e3 * build / args.steps, 1),
+            'end_trim_d2h_bytes_per_100k_reads': int(d2h.get('bytes', 0) * 100000 / max(n, 1)),
+            'dtype': 'int32', 'data': 'synthetic (seeded ONT-like reads, mean %d bp)' % args.mean_len,
+            'config': {'workload': 'porechop_abi.find_matching_adapter_sets (first 10k reads x %d sets) + '
+                                   'find_adapters_at_read_ends + find_adapters_in_read_middles on %d NanoporeRead '
+                                   'objects x %d adapter sets' % (len([a for a in A.fresh_adapters()
+                                                                       if '(full sequence)' not in a.name]), n,
+                                                                  len(sets))},
+            'parity_spot_check': checked, 'setup_s': round(gen_s, 2)}
 
 
 def run_host_path(args, L, _lib, buf, s_off, s_len, e_off, e_len, sides, d_sres, d_eres, d_st, d_et, n, n_sa, n_ea,

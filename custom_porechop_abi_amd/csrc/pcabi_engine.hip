@@ -25,6 +25,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/pcabi.h"
@@ -341,81 +342,93 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
 
 // Candidates of one adapter are typically many (the reads' own adapter), so the per-adapter
 // counters are updated once per (wave, adapter): the lanes of one adapter are reduced first.
-__global__ __launch_bounds__(256) void k_plan_count(const int64_t *cand, int64_t nc, const int32_t *v_len,
-                                                    const int32_t *start, const int32_t *span, int32_t *adp_tasks) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+// nc_dev != nullptr: the candidate count is on the device (at most nc); the blocks stride.
+__global__ __launch_bounds__(256) void k_plan_count(const int64_t *cand, int64_t nc, const unsigned long long *nc_dev,
+                                                    const int32_t *v_len, const int32_t *start, const int32_t *span,
+                                                    int32_t *adp_tasks) {
+    const int64_t ncl = nc_dev ? min((int64_t)*nc_dev, nc) : nc;
     const int lane = threadIdx.x & 63;
-    const int64_t key = i < nc ? cand[i] : 0;
-    const bool active = i < nc && plan_valid(key, v_len, start);
-    const int32_t a = active ? (int32_t)(key >> 32) : -1;
-    int nt[kPlanC] = {0, 0, 0, 0};
-    if (active) {
-        const int32_t k = (int32_t)(key & 0xFFFFFFFF);
+    for (int64_t b0 = (int64_t)blockIdx.x * 256; b0 < ncl; b0 += (int64_t)gridDim.x * 256) {   // uniform
+        const int64_t i = b0 + threadIdx.x;
+        const int64_t key = i < ncl ? cand[i] : 0;
+        const bool active = i < ncl && plan_valid(key, v_len, start);
+        const int32_t a = active ? (int32_t)(key >> 32) : -1;
+        int nt[kPlanC] = {0, 0, 0, 0};
+        if (active) {
+            const int32_t k = (int32_t)(key & 0xFFFFFFFF);
 #pragma unroll
-        for (int c = 0; c < kPlanC; ++c) nt[c] = plan_tasks(v_len[k], span[a], c);
-    }
-    uint64_t pending = __ballot(active);
-    while (pending) {                                // wave-uniform
-        const int leader = __ffsll((unsigned long long)pending) - 1;
-        const int32_t a0 = __shfl(a, leader);
-        const bool mine = active && a == a0;
-#pragma unroll
-        for (int c = 0; c < kPlanC; ++c) {
-            const int sum = wave_sum(mine ? nt[c] : 0);
-            if (lane == leader) atomicAdd(&adp_tasks[a0 * kPlanC + c], sum);
+            for (int c = 0; c < kPlanC; ++c) nt[c] = plan_tasks(v_len[k], span[a], c);
         }
-        pending &= ~__ballot(mine);
+        uint64_t pending = __ballot(active);
+        while (pending) {                            // wave-uniform
+            const int leader = __ffsll((unsigned long long)pending) - 1;
+            const int32_t a0 = __shfl(a, leader);
+            const bool mine = active && a == a0;
+#pragma unroll
+            for (int c = 0; c < kPlanC; ++c) {
+                const int sum = wave_sum(mine ? nt[c] : 0);
+                if (lane == leader) atomicAdd(&adp_tasks[a0 * kPlanC + c], sum);
+            }
+            pending &= ~__ballot(mine);
+        }
     }
 }
 
 // Task slots: adapter a's tasks fill slots [wave_off[a] * 64, ...) in any order (a slot's result
 // depends only on its own task); idle slots keep task_win = -1. cidx[a]: the chunk length of a's
-// bucket (64 << cidx).
-__global__ __launch_bounds__(256) void k_plan_place(const int64_t *cand, int64_t nc, const int32_t *v_len,
-                                                    const int32_t *start, const int32_t *span, const int32_t *cidx,
-                                                    const int64_t *wave_off, int32_t *fill, int32_t *tw, int32_t *to,
-                                                    int4 *tck, int32_t *tcand) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+// bucket (64 << cidx). nc_dev / slots_dev (device counts, nullptr: host values): the candidate
+// count, and the slots the layout holds (a task past them is not written: the layout overflowed).
+__global__ __launch_bounds__(256) void k_plan_place(const int64_t *cand, int64_t nc, const unsigned long long *nc_dev,
+                                                    const int32_t *v_len, const int32_t *start, const int32_t *span,
+                                                    const int32_t *cidx, const int64_t *wave_off, int32_t *fill,
+                                                    int32_t *tw, int32_t *to, int4 *tck, int32_t *tcand,
+                                                    const int64_t *slots_dev) {
+    const int64_t ncl = nc_dev ? min((int64_t)*nc_dev, nc) : nc;
+    const int64_t slots = slots_dev ? *slots_dev : INT64_MAX;
     const int lane = threadIdx.x & 63;
-    const int64_t key = i < nc ? cand[i] : 0;
-    const bool active = i < nc && plan_valid(key, v_len, start);
-    const int32_t a = active ? (int32_t)(key >> 32) : -1, k = (int32_t)(key & 0xFFFFFFFF);
-    int n = 0, D = -1, c = 0, nt = 0;
-    if (active) {
-        n = v_len[k];
-        D = span[a];
-        c = cidx[a];
-        nt = plan_tasks(n, D, c);
-    }
-    int64_t base = 0;
-    uint64_t pending = __ballot(active);
-    while (pending) {                                // wave-uniform: one atomic per (wave, adapter)
-        const int leader = __ffsll((unsigned long long)pending) - 1;
-        const int32_t a0 = __shfl(a, leader);
-        const bool mine = active && a == a0;
-        const int x = mine ? nt : 0;
-        const int incl = wave_incl_scan(x);
-        const int total = __shfl(incl, 63);
-        int b0 = 0;
-        if (lane == leader) b0 = atomicAdd(&fill[a0], total);
-        b0 = __shfl(b0, leader);
-        if (mine) base = wave_off[a0] * 64 + b0 + (incl - x);
-        pending &= ~__ballot(mine);
-    }
-    if (!active) return;
-    const int C = 64 << c;
-    for (int t = 0; t < nt; ++t) {
-        const int64_t q = base + t;
-        int4 ck = make_int4(0, 0, 0, 0);
-        if (D >= 0) {                                // sf::chunk_plan, chunk t
-            const int lo = 1 + t * C, hi = lo + C;
-            const int st = max(0, lo - 1 - D);
-            ck = hi > n ? make_int4(st, n - st, lo - st, -1) : make_int4(st, hi - 1 - st, lo - st, hi - st);
+    for (int64_t b0 = (int64_t)blockIdx.x * 256; b0 < ncl; b0 += (int64_t)gridDim.x * 256) {   // uniform
+        const int64_t i = b0 + threadIdx.x;
+        const int64_t key = i < ncl ? cand[i] : 0;
+        const bool active = i < ncl && plan_valid(key, v_len, start);
+        const int32_t a = active ? (int32_t)(key >> 32) : -1, k = (int32_t)(key & 0xFFFFFFFF);
+        int n = 0, D = -1, c = 0, nt = 0;
+        if (active) {
+            n = v_len[k];
+            D = span[a];
+            c = cidx[a];
+            nt = plan_tasks(n, D, c);
         }
-        tw[q] = k;
-        to[q] = (int32_t)q;
-        tck[q] = ck;
-        tcand[q] = (int32_t)i;
+        int64_t base = 0;
+        uint64_t pending = __ballot(active);
+        while (pending) {                            // wave-uniform: one atomic per (wave, adapter)
+            const int leader = __ffsll((unsigned long long)pending) - 1;
+            const int32_t a0 = __shfl(a, leader);
+            const bool mine = active && a == a0;
+            const int x = mine ? nt : 0;
+            const int incl = wave_incl_scan(x);
+            const int total = __shfl(incl, 63);
+            int b1 = 0;
+            if (lane == leader) b1 = atomicAdd(&fill[a0], total);
+            b1 = __shfl(b1, leader);
+            if (mine) base = wave_off[a0] * 64 + b1 + (incl - x);
+            pending &= ~__ballot(mine);
+        }
+        if (!active) continue;
+        const int C = 64 << c;
+        for (int t = 0; t < nt; ++t) {
+            const int64_t q = base + t;
+            if (q >= slots) break;
+            int4 ck = make_int4(0, 0, 0, 0);
+            if (D >= 0) {                            // sf::chunk_plan, chunk t
+                const int lo = 1 + t * C, hi = lo + C;
+                const int st = max(0, lo - 1 - D);
+                ck = hi > n ? make_int4(st, n - st, lo - st, -1) : make_int4(st, hi - 1 - st, lo - st, hi - st);
+            }
+            tw[q] = k;
+            to[q] = (int32_t)q;
+            tck[q] = ck;
+            tcand[q] = (int32_t)i;
+        }
     }
 }
 
@@ -427,37 +440,43 @@ __device__ __forceinline__ uint64_t merge_key(int32_t score, int4 ck) {
 }
 
 __global__ __launch_bounds__(256) void k_merge_best(const int32_t *tw, const int4 *tck, const int32_t *tcand,
-                                                    const int32_t *res, int64_t slots, unsigned long long *best) {
-    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (q >= slots || tw[q] < 0) return;
-    atomicMax(&best[tcand[q]], (unsigned long long)merge_key(res[4 * slots + q], tck[q]));
+                                                    const int32_t *res, int64_t slots, const int64_t *slots_dev,
+                                                    unsigned long long *best) {
+    const int64_t ns = slots_dev ? *slots_dev : slots;
+    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < ns; q += (int64_t)gridDim.x * 256) {
+        if (tw[q] < 0) continue;
+        atomicMax(&best[tcand[q]], (unsigned long long)merge_key(res[4 * slots + q], tck[q]));
+    }
 }
 
 // pass 0: per window the smallest adapter whose winning chunk reaches the threshold (atomicMin);
 // pass 1: that candidate writes the window's hit (rs / re back to whole-window offsets).
+// slots: the result rows' stride; slots_dev: the live slots (nullptr: all).
 __global__ __launch_bounds__(256) void k_merge_hit(const int64_t *cand, const int32_t *tw, const int4 *tck,
                                                    const int32_t *tcand, const int32_t *res, int64_t slots,
-                                                   const unsigned long long *best, double thr, int pass,
-                                                   int32_t *hit_a, int32_t *hb, int64_t n) {
-    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (q >= slots || tw[q] < 0) return;
-    const int32_t ci = tcand[q];
-    const int4 ck = tck[q];
-    const int32_t st = ck.x;
-    if ((unsigned long long)merge_key(res[4 * slots + q], ck) != best[ci]) return;
-    const int rs = res[0 * slots + q];
-    const int m = res[5 * slots + q], l2 = res[7 * slots + q];
-    const double full = rs == -1 ? 0.0 : pcabi::pid6(m, l2);
-    if (full < thr) return;                          // NaN goes on, as the reference's loop
-    const int32_t k = tw[q], a = (int32_t)(cand[ci] >> 32);
-    if (pass == 0) {
-        atomicMin(&hit_a[k], a);
-    } else if (hit_a[k] == a) {
-        hb[0 * n + k] = a;
-        hb[1 * n + k] = rs + st;
-        hb[2 * n + k] = res[1 * slots + q] + st;
-        hb[3 * n + k] = m;
-        hb[4 * n + k] = l2;
+                                                   const int64_t *slots_dev, const unsigned long long *best, double thr,
+                                                   int pass, int32_t *hit_a, int32_t *hb, int64_t n) {
+    const int64_t ns = slots_dev ? *slots_dev : slots;
+    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < ns; q += (int64_t)gridDim.x * 256) {
+        if (tw[q] < 0) continue;
+        const int32_t ci = tcand[q];
+        const int4 ck = tck[q];
+        const int32_t st = ck.x;
+        if ((unsigned long long)merge_key(res[4 * slots + q], ck) != best[ci]) continue;
+        const int rs = res[0 * slots + q];
+        const int m = res[5 * slots + q], l2 = res[7 * slots + q];
+        const double full = rs == -1 ? 0.0 : pcabi::pid6(m, l2);
+        if (full < thr) continue;                    // NaN goes on, as the reference's loop
+        const int32_t k = tw[q], a = (int32_t)(cand[ci] >> 32);
+        if (pass == 0) {
+            atomicMin(&hit_a[k], a);
+        } else if (hit_a[k] == a) {
+            hb[0 * n + k] = a;
+            hb[1 * n + k] = rs + st;
+            hb[2 * n + k] = res[1 * slots + q] + st;
+            hb[3 * n + k] = m;
+            hb[4 * n + k] = l2;
+        }
     }
 }
 
@@ -471,6 +490,134 @@ __global__ __launch_bounds__(256) void k_hits_compact(const int32_t *hb, int64_t
     o[0] = (int32_t)k;
 #pragma unroll
     for (int f = 0; f < 5; ++f) o[1 + f] = hb[f * n + k];
+}
+
+
+// ---- queued middle-scan rounds (middle_device_rounds): the kernels between the seeded plan's ------
+// steps, every count read on the device
+
+// views of this round's windows: sub[k] = window cur[k], k < n_dev
+__global__ __launch_bounds__(256) void k_round_views(const int64_t *win_off, const int32_t *win_len, const int32_t *cur,
+                                                     const int32_t *n_dev, int64_t *sub_off, int32_t *sub_len) {
+    const int64_t n = *n_dev;
+    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256) {
+        sub_off[k] = win_off[cur[k]];
+        sub_len[k] = win_len[cur[k]];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_zero_u64(unsigned long long *p, const unsigned long long *n_dev, int64_t cap) {
+    const int64_t n = min((int64_t)*n_dev, cap);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = 0ull;
+}
+
+// The device plan's layout (device_plan_hits' host part, on the device, one block): per bucket
+// the longest chunk length whose waves reach `target` (else the shortest), every adapter's wave
+// offset (buckets in order, a bucket's adapters in order, one adapter per wave), the wave ->
+// bucket-local adapter table, the idle lanes of every adapter's last wave (task -1), and per
+// bucket (first wave, waves). More slots than slots_cap: flag, need = the slots, no waves.
+//   bk_first[n_bk + 1]: the buckets' ranges of bk_adp (global adapter ids) / bk_local (their
+//   index in the bucket's table); tasks[a * kPlanC + c]: k_plan_count's counts.
+__global__ __launch_bounds__(256) void k_plan_layout(const int32_t *tasks, int32_t n_bk, const int32_t *bk_first,
+                                                     const int32_t *bk_adp, const int32_t *bk_local, int64_t target,
+                                                     int64_t slots_cap, int32_t *cidx, int64_t *woff, int32_t *wa,
+                                                     int32_t *tw, int32_t *bk_waves, int64_t *slots_total,
+                                                     int32_t *flag, int64_t *need) {
+    __shared__ unsigned long long s_w[kPlanC];
+    __shared__ int64_t s_base;
+    if (threadIdx.x == 0) s_base = 0;
+    for (int32_t b = 0; b < n_bk; ++b) {
+        if (threadIdx.x < kPlanC) s_w[threadIdx.x] = 0;
+        __syncthreads();
+        for (int32_t j = bk_first[b] + threadIdx.x; j < bk_first[b + 1]; j += 256) {
+            const int32_t a = bk_adp[j];
+#pragma unroll
+            for (int c = 1; c < kPlanC; ++c) atomicAdd(&s_w[c], (unsigned long long)((tasks[a * kPlanC + c] + 63) / 64));
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int bc = 0;
+            for (int c = kPlanC - 1; c > 0; --c)
+                if ((int64_t)s_w[c] >= target) {
+                    bc = c;
+                    break;
+                }
+            int64_t w = s_base;
+            const int64_t w0 = w;
+            for (int32_t j = bk_first[b]; j < bk_first[b + 1]; ++j) {
+                const int32_t a = bk_adp[j];
+                woff[a] = w;
+                cidx[a] = bc;
+                w += (tasks[a * kPlanC + bc] + 63) / 64;
+            }
+            bk_waves[2 * b] = (int32_t)w0;
+            bk_waves[2 * b + 1] = (int32_t)(w - w0);
+            s_base = w;
+        }
+        __syncthreads();
+    }
+    const int64_t slots = s_base * 64;
+    if (slots > slots_cap) {                         // too small: no waves, the round reruns larger
+        if (threadIdx.x == 0) {
+            *flag = 1;
+            *need = slots;
+            *slots_total = 0;
+        }
+        for (int32_t b = threadIdx.x; b < n_bk; b += 256) bk_waves[2 * b + 1] = 0;
+        return;
+    }
+    if (threadIdx.x == 0) *slots_total = slots;
+    for (int32_t j = 0; j < bk_first[n_bk]; ++j) {  // uniform
+        const int32_t a = bk_adp[j];
+        const int32_t nt = tasks[a * kPlanC + cidx[a]];
+        const int64_t nw = (nt + 63) / 64, w0 = woff[a];
+        for (int64_t w = threadIdx.x; w < nw; w += 256) wa[w0 + w] = bk_local[j];
+        for (int64_t t = nt + threadIdx.x; t < nw * 64; t += 256) tw[w0 * 64 + t] = -1;
+    }
+}
+
+// A round's hits (k_merge_hit's per-window table hb, row stride n) -> the round's list (8 int32
+// each: read, adapter, rs, re, m, l2, position, 0), the next round's reads (those that hit, from
+// the adapter that hit) and their count. A round whose seed / plan buffers overflowed keeps nothing
+// (no hits, no next round, no masking): the host sees rflag and reruns it with larger buffers.
+__global__ __launch_bounds__(256) void k_round_hits(const int32_t *hb, int64_t n, const int32_t *n_dev, const int32_t *cur,
+                                                    int32_t *list, int32_t *n_next, int32_t *cur_next,
+                                                    int32_t *start_next, const int32_t *seed_flags,
+                                                    const int32_t *plan_flag, int32_t *rflag) {
+    const int32_t f = (seed_flags[0] ? 1 : 0) | (seed_flags[1] ? 2 : 0) | (*plan_flag ? 4 : 0);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *rflag = f;
+    if (f) return;
+    const int64_t nr = *n_dev;
+    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < nr; k += (int64_t)gridDim.x * 256) {
+        const int32_t a = hb[k];
+        if (a < 0) continue;
+        const int32_t j = atomicAdd(n_next, 1);
+        const int32_t r = cur[k];
+        int32_t *o = list + 8 * (int64_t)j;
+        o[0] = r;
+        o[1] = a;
+        o[2] = hb[1 * n + k];
+        o[3] = hb[2 * n + k];
+        o[4] = hb[3 * n + k];
+        o[5] = hb[4 * n + k];
+        o[6] = (int32_t)k;
+        o[7] = 0;
+        cur_next[j] = r;
+        start_next[j] = a;
+    }
+}
+
+// Masking of a round's hits (nanopore_read.py:245, the span becomes '-', Dna5 N): the blocks stride
+// over the list, a block's threads over the span.
+__global__ __launch_bounds__(256) void k_mask_list(uint8_t *codes, const int64_t *win_off, const int32_t *list,
+                                                   const int32_t *n_dev) {
+    const int64_t nh = *n_dev;
+    for (int64_t j = blockIdx.x; j < nh; j += gridDim.x) {
+        const int32_t *o = list + 8 * j;
+        const int32_t rs = o[2], rend = rs == -1 ? 0 : o[3] + 1;
+        const int64_t base = win_off[o[0]];
+        for (int64_t i = rs + threadIdx.x; i < rend; i += 256) codes[base + i] = 4;
+    }
 }
 
 // ---- launch plumbing -------------------------------------------------------------------------
@@ -722,6 +869,12 @@ int bounds(State *s, const void *adps_key, const uint8_t *hcodes, const int32_t 
            int32_t n_adp, const std::vector<int> &fb_rows, const uint8_t *codes, const int64_t *v_off,
            const int32_t *v_len, int64_t n, const pcabi::Scoring &sc, double threshold, int mode, int16_t *s16,
            std::vector<int64_t> *cands, const int64_t **dcands, int64_t *n_dcands, hipStream_t st);
+int plan_ready(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hlen, int32_t n_adp,
+               const std::vector<int> &fb_rows, const pcabi::Scoring &sc, double threshold, int mode, hipStream_t st);
+int bounds_dev(State *s, const uint8_t *codes, const int64_t *v_off, const int32_t *v_len, int64_t n,
+               const int32_t *n_dev, int32_t n_adp, const pcabi::Scoring &sc, const int64_t **dcands,
+               const unsigned long long **dcount, const int32_t **flags, hipStream_t st);
+bool grow_after_overflow(State *s, int raw_overflow, int task_overflow);
 }  // namespace pcabi_seed
 
 struct pcabi_scan {
@@ -730,6 +883,10 @@ struct pcabi_scan {
     DeviceBuf s16, tw, to, wa, pres, tck;   // score filter + candidate pairs (chunks)
     DeviceBuf pspan, ptasks, pfill, pwoff, pcidx, pcand, pbest, phit, phb, plist, pcnt;   // device planning
     pcabi_seed::State *seed = nullptr; // seeded round-1 bounds (pcabi_seed.hip)
+    // queued rounds (middle_device_rounds): per round slot the reads, their start adapters and the
+    // hit list; round counts and flags; the plan's bucket tables and scratch
+    DeviceBuf q_cur, q_start, q_list, q_n, q_flags, q_sort, q_bk, q_wave, q_misc;
+    int64_t q_slots_cap = 0;
 };
 
 namespace {
@@ -866,17 +1023,29 @@ int pcabi_device_count(void) {
 }
 
 void pcabi_encode_dna5(const char *ascii, uint8_t *codes, int64_t n) {
-    static uint8_t tab[256];
-    static bool built = false;
-    if (!built) {
-        for (int c = 0; c < 256; ++c) tab[c] = 4;
-        tab['A'] = tab['a'] = 0;
-        tab['C'] = tab['c'] = 1;
-        tab['G'] = tab['g'] = 2;
-        tab['T'] = tab['t'] = tab['U'] = tab['u'] = 3;
-        built = true;
+    static const struct Tab {
+        uint8_t t[256];
+        Tab() {
+            for (int c = 0; c < 256; ++c) t[c] = 4;
+            t['A'] = t['a'] = 0;
+            t['C'] = t['c'] = 1;
+            t['G'] = t['g'] = 2;
+            t['T'] = t['t'] = t['U'] = t['u'] = 3;
+        }
+    } tab;
+    auto run = [&](int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; ++i) codes[i] = tab.t[(unsigned char)ascii[i]];
+    };
+    // whole batches of reads (hundreds of MB from the Python drivers) on up to 16 host threads
+    const int64_t per = 8 << 20;
+    const int nt = (int)std::min<int64_t>(16, std::max<int64_t>(1, n / per));
+    if (nt <= 1) {
+        run(0, n);
+        return;
     }
-    for (int64_t i = 0; i < n; ++i) codes[i] = tab[(unsigned char)ascii[i]];
+    std::vector<std::thread> th;
+    for (int k = 0; k < nt; ++k) th.emplace_back(run, n * k / nt, n * (k + 1) / nt);
+    for (auto &t : th) t.join();
 }
 
 void pcabi_pid6_host(const int32_t *m, const int32_t *l, int64_t n, double *out) {
@@ -1513,7 +1682,8 @@ void pcabi_scan_destroy(pcabi_scan *s) {
     for (DeviceBuf *b : {&s->tiles, &s->toff, &s->res, &s->hits, &s->idx, &s->start, &s->soff, &s->slen,
                          &s->mwin, &s->ms, &s->me, &s->s16, &s->tw, &s->to, &s->wa, &s->pres, &s->tck,
                          &s->pspan, &s->ptasks, &s->pfill, &s->pwoff, &s->pcidx, &s->pcand, &s->pbest, &s->phit, &s->phb,
-                         &s->plist, &s->pcnt})
+                         &s->plist, &s->pcnt, &s->q_cur, &s->q_start, &s->q_list, &s->q_n, &s->q_flags, &s->q_sort,
+                         &s->q_bk, &s->q_wave, &s->q_misc})
         if (b->p) (void)hipFree(b->p);
     if (s->seed) pcabi_seed::destroy(s->seed);
     delete s;
@@ -1577,7 +1747,7 @@ int device_plan_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_off,
     HIP_TRY(hipMemcpyAsync(sc->pspan.p, span.data(), sizeof(int32_t) * n_adp, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemsetAsync(sc->ptasks.p, 0, sizeof(int32_t) * n_adp * kPlanC, st));
     const unsigned gc = (unsigned)((nc + 255) / 256);
-    hipLaunchKernelGGL(k_plan_count, dim3(gc), dim3(256), 0, st, dcand, nc, v_len, d_start,
+    hipLaunchKernelGGL(k_plan_count, dim3(gc), dim3(256), 0, st, dcand, nc, nullptr, v_len, d_start,
                        (const int32_t *)sc->pspan.p, (int32_t *)sc->ptasks.p);
     HIP_TRY(hipGetLastError());
     std::vector<int32_t> tasks((size_t)n_adp * kPlanC);
@@ -1648,10 +1818,10 @@ int device_plan_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_off,
     HIP_TRY(hipMemcpyAsync(sc->wa.p, wa.data(), sizeof(int32_t) * wa.size(), hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)sc->tw.p, -1, (size_t)slots, st));
     HIP_TRY(hipMemsetAsync(sc->pfill.p, 0, sizeof(int32_t) * n_adp, st));
-    hipLaunchKernelGGL(k_plan_place, dim3(gc), dim3(256), 0, st, dcand, nc, v_len, d_start,
+    hipLaunchKernelGGL(k_plan_place, dim3(gc), dim3(256), 0, st, dcand, nc, nullptr, v_len, d_start,
                        (const int32_t *)sc->pspan.p, (const int32_t *)sc->pcidx.p, (const int64_t *)sc->pwoff.p,
                        (int32_t *)sc->pfill.p,
-                       (int32_t *)sc->tw.p, (int32_t *)sc->to.p, (int4 *)sc->tck.p, (int32_t *)sc->pcand.p);
+                       (int32_t *)sc->tw.p, (int32_t *)sc->to.p, (int4 *)sc->tck.p, (int32_t *)sc->pcand.p, nullptr);
     HIP_TRY(hipGetLastError());
     KParams p{};
     p.codes = codes;
@@ -1700,10 +1870,10 @@ int device_plan_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_off,
     const int32_t *tw = (const int32_t *)sc->tw.p, *tcand = (const int32_t *)sc->pcand.p;
     const int4 *tck = (const int4 *)sc->tck.p;
     const int32_t *res = (const int32_t *)sc->pres.p;
-    hipLaunchKernelGGL(k_merge_best, dim3(gs), dim3(256), 0, st, tw, tck, tcand, res, slots,
+    hipLaunchKernelGGL(k_merge_best, dim3(gs), dim3(256), 0, st, tw, tck, tcand, res, slots, nullptr,
                        (unsigned long long *)sc->pbest.p);
     for (int pass = 0; pass < 2; ++pass)
-        hipLaunchKernelGGL(k_merge_hit, dim3(gs), dim3(256), 0, st, dcand, tw, tck, tcand, res, slots,
+        hipLaunchKernelGGL(k_merge_hit, dim3(gs), dim3(256), 0, st, dcand, tw, tck, tcand, res, slots, nullptr,
                            (const unsigned long long *)sc->pbest.p, threshold, pass, (int32_t *)sc->phit.p,
                            (int32_t *)sc->phb.p, n);
     hipLaunchKernelGGL(k_hits_compact, dim3(gn), dim3(256), 0, st, (const int32_t *)sc->phb.p, n,
@@ -2012,6 +2182,269 @@ int filtered_first_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_o
     return 1;
 }
 
+
+// PCABI_MIDDLE_DEVROUNDS=0: the seeded scan keeps the host-driven round loop (A/B runs).
+bool middle_devrounds_on() {
+    const char *e = std::getenv("PCABI_MIDDLE_DEVROUNDS");
+    return !(e && e[0] == '0');
+}
+
+// The whole seeded middle scan as QUEUED rounds: no host synchronisation between the end trim and
+// the scan's result. Every round runs the seeded plan's steps with its counts on the device -- the
+// reads of the round (round 1: all windows, longest first by a device radix sort; later: those
+// that just hit, from the adapter that hit), the seeds (pcabi_seed::bounds_dev), the plan's counts,
+// layout and task slots (k_plan_count, k_plan_layout, k_plan_place), the chunked candidate DP (the
+// launches stride over the device's wave counts), the merges, the round's hit list and the
+// masking. The host queues kBatch rounds, reads the round counts once, and queues more while
+// reads still hit. A buffer that overflowed in a round flags it before anything of it is kept or
+// masked; the host grows the buffers and queues that round again. The hits come back once, sorted
+// by (round, read): per read the reference's discovery order.
+// Returns the hit count (> 0, <= 0 on error as pcabi_middle_scan_dev); applied = false when the
+// seeded plan does not cover this table and scoring (the caller runs the host-driven loop).
+int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_off, const int32_t *win_len,
+                             int64_t n_win, const pcabi::Scoring &scr, double threshold, int32_t *hits, int64_t cap,
+                             hipStream_t st, bool &applied) {
+    applied = false;
+    const pcabi_adapters *adps = sc->adps;
+    const int32_t n_adp = adps->n_adp;
+    if (!middle_devrounds_on() || !middle_devplan_on() || adps->count[kStripedBucket] || n_win >= (1ll << 31) ||
+        (int64_t)n_win * n_adp >= (1ll << 40))
+        return 0;
+    // every bucket chunked (the device plan's launches are k_align_chunk), with its span
+    std::vector<int32_t> span((size_t)n_adp, -1);
+    std::vector<int> used;
+    std::vector<int32_t> bk_first(1, 0), bk_adp, bk_local;
+    for (int b = 0; b < kNumBuckets; ++b) {
+        const int nb = adps->count[b];
+        if (!nb) continue;
+        if (!chunkable(b, bucket_packed_ok(b, adps->lens[b], scr))) return 0;
+        for (int kk = 0; kk < nb; ++kk) {
+            const int L = adps->lens[b][kk];
+            const int D = pcabi::sf::chunk_span(L, pcabi::sf::filter_threshold(L, threshold, scr), scr);
+            if (D < 0) return 0;
+            span[adps->ids[b][kk]] = D;
+            bk_adp.push_back(adps->ids[b][kk]);
+            bk_local.push_back(kk);
+        }
+        used.push_back(b);
+        bk_first.push_back((int32_t)bk_adp.size());
+    }
+    std::vector<int> rows((size_t)n_adp, 0);
+    for (int b = 0; b < kNumBuckets; ++b)
+        for (int32_t id : adps->ids[b]) rows[id] = kBuckets[b].rpl;
+    if (!sc->seed) sc->seed = pcabi_seed::create();
+    {
+        const int rc = pcabi_seed::plan_ready(sc->seed, adps->hcodes.data(), adps->hoff.data(), adps->hlen.data(), n_adp,
+                                              rows, scr, threshold, middle_seed_mode(), st);
+        if (rc < 0) return rc;
+        if (rc == 0) return 0;
+    }
+    applied = true;
+    const int n_bk = (int)used.size();
+    const int64_t n = n_win;
+    constexpr int kSlots = 16;                      // round slots held on the device (wrapped past)
+    constexpr int kBatch = 3;                       // rounds queued per host check
+    constexpr unsigned kGrid = 2048;                // blocks of the device-counted launches
+    // ---- device buffers ----
+    if (int rc = sc->q_cur.ensure(4 * (size_t)n * (kSlots + 1))) return rc;
+    if (int rc = sc->q_start.ensure(4 * (size_t)n * (kSlots + 1))) return rc;
+    if (int rc = sc->q_list.ensure(4 * 8 * (size_t)n * kSlots)) return rc;
+    if (int rc = sc->q_n.ensure(4 * (kSlots + 2))) return rc;
+    if (int rc = sc->q_flags.ensure(4 * (kSlots + 2))) return rc;
+    if (int rc = sc->q_sort.ensure(sort_by_length_bytes(n))) return rc;
+    if (int rc = sc->soff.ensure(sizeof(int64_t) * n)) return rc;
+    if (int rc = sc->slen.ensure(sizeof(int32_t) * n)) return rc;
+    if (int rc = sc->pspan.ensure(sizeof(int32_t) * n_adp)) return rc;
+    if (int rc = sc->ptasks.ensure(sizeof(int32_t) * n_adp * kPlanC)) return rc;
+    if (int rc = sc->pfill.ensure(sizeof(int32_t) * n_adp)) return rc;
+    if (int rc = sc->pwoff.ensure(sizeof(int64_t) * n_adp)) return rc;
+    if (int rc = sc->pcidx.ensure(sizeof(int32_t) * n_adp)) return rc;
+    if (int rc = sc->phit.ensure(sizeof(int32_t) * n)) return rc;
+    if (int rc = sc->phb.ensure(sizeof(int32_t) * 5 * n)) return rc;
+    if (int rc = sc->pbest.ensure(sizeof(unsigned long long) * n * n_adp)) return rc;
+    if (int rc = sc->q_bk.ensure(4 * (bk_first.size() + 2 * bk_adp.size() + 2 * (size_t)n_bk + 16))) return rc;
+    if (int rc = sc->q_misc.ensure(64)) return rc;   // [0] slots (int64), [8] need (int64), [16] plan flag
+    int32_t *d_bk_first = (int32_t *)sc->q_bk.p, *d_bk_adp = d_bk_first + bk_first.size();
+    int32_t *d_bk_local = d_bk_adp + bk_adp.size(), *d_bk_waves = d_bk_local + bk_adp.size();
+    std::vector<int32_t> bk_host(bk_first);
+    bk_host.insert(bk_host.end(), bk_adp.begin(), bk_adp.end());
+    bk_host.insert(bk_host.end(), bk_local.begin(), bk_local.end());
+    HIP_TRY(hipMemcpyAsync(sc->q_bk.p, bk_host.data(), 4 * bk_host.size(), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(sc->pspan.p, span.data(), 4 * (size_t)n_adp, hipMemcpyHostToDevice, st));
+    int64_t *d_slots = (int64_t *)sc->q_misc.p, *d_need = d_slots + 1;
+    int32_t *d_pflag = (int32_t *)(d_slots + 2);
+    int32_t *d_n = (int32_t *)sc->q_n.p, *d_rflag = (int32_t *)sc->q_flags.p;
+    auto cur_of = [&](int slot) { return (int32_t *)sc->q_cur.p + (int64_t)slot * n; };
+    auto start_of = [&](int slot) { return (int32_t *)sc->q_start.p + (int64_t)slot * n; };
+    auto list_of = [&](int slot) { return (int32_t *)sc->q_list.p + (int64_t)slot * 8 * n; };
+    // round 1: every window, longest first
+    if (int rc = sort_by_length(win_len, n, cur_of(0), sc->q_sort.p, st)) return rc;
+    {
+        const int32_t n32 = (int32_t)n;
+        HIP_TRY(hipMemcpyAsync(d_n, &n32, 4, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipStreamSynchronize(st));           // n32 leaves scope
+    }
+    if (sc->q_slots_cap == 0) sc->q_slots_cap = std::max<int64_t>(1 << 20, 4 * n);
+    const int64_t target = middle_plan_waves();
+    const unsigned gn = (unsigned)std::min<int64_t>((n + 255) / 256, kGrid);
+    std::vector<int32_t> out;                       // (round, 8 ints) of finished slots
+    std::vector<int64_t> out_round;
+    int64_t round_base = 0;                         // global round number of slot 0
+    int slot = 0;                                   // next round to queue (slot index)
+    int queued_to = 0;                              // rounds [0, queued_to) are queued
+    auto queue_round = [&](int r) -> int {
+        const int64_t slots_cap = sc->q_slots_cap;
+        if (int rc = sc->tw.ensure(sizeof(int32_t) * slots_cap)) return rc;
+        if (int rc = sc->to.ensure(sizeof(int32_t) * slots_cap)) return rc;
+        if (int rc = sc->tck.ensure(sizeof(int4) * slots_cap)) return rc;
+        if (int rc = sc->pcand.ensure(sizeof(int32_t) * slots_cap)) return rc;
+        if (int rc = sc->wa.ensure(sizeof(int32_t) * (slots_cap / 64 + 1))) return rc;
+        if (int rc = sc->pres.ensure(sizeof(int32_t) * PCABI_NFIELDS * (size_t)slots_cap)) return rc;
+        const int32_t *nr = d_n + r;
+        const int32_t *start = r == 0 && round_base == 0 ? nullptr : start_of(r);
+        HIP_TRY(hipMemsetAsync(d_n + r + 1, 0, 4, st));
+        HIP_TRY(hipMemsetAsync(d_pflag, 0, 4, st));
+        hipLaunchKernelGGL(k_round_views, dim3(gn), dim3(256), 0, st, win_off, win_len, cur_of(r), nr,
+                           (int64_t *)sc->soff.p, (int32_t *)sc->slen.p);
+        const int64_t *dcand = nullptr;
+        const unsigned long long *dcount = nullptr;
+        const int32_t *sflags = nullptr;
+        const int64_t *v_off = (const int64_t *)sc->soff.p;
+        const int32_t *v_len = (const int32_t *)sc->slen.p;
+        if (int rc = pcabi_seed::bounds_dev(sc->seed, codes, v_off, v_len, n, nr, n_adp, scr, &dcand, &dcount, &sflags, st))
+            return rc;
+        const int64_t ncap = n * (int64_t)n_adp;
+        HIP_TRY(hipMemsetAsync(sc->ptasks.p, 0, sizeof(int32_t) * n_adp * kPlanC, st));
+        HIP_TRY(hipMemsetAsync(sc->pfill.p, 0, sizeof(int32_t) * n_adp, st));
+        hipLaunchKernelGGL(k_plan_count, dim3(kGrid), dim3(256), 0, st, dcand, ncap, dcount, v_len, start,
+                           (const int32_t *)sc->pspan.p, (int32_t *)sc->ptasks.p);
+        hipLaunchKernelGGL(k_plan_layout, dim3(1), dim3(256), 0, st, (const int32_t *)sc->ptasks.p, n_bk, d_bk_first,
+                           d_bk_adp, d_bk_local, target, slots_cap, (int32_t *)sc->pcidx.p, (int64_t *)sc->pwoff.p,
+                           (int32_t *)sc->wa.p, (int32_t *)sc->tw.p, d_bk_waves, d_slots, d_pflag, d_need);
+        hipLaunchKernelGGL(k_plan_place, dim3(kGrid), dim3(256), 0, st, dcand, ncap, dcount, v_len, start,
+                           (const int32_t *)sc->pspan.p, (const int32_t *)sc->pcidx.p, (const int64_t *)sc->pwoff.p,
+                           (int32_t *)sc->pfill.p, (int32_t *)sc->tw.p, (int32_t *)sc->to.p, (int4 *)sc->tck.p,
+                           (int32_t *)sc->pcand.p, (const int64_t *)d_slots);
+        HIP_TRY(hipGetLastError());
+        KParams p{};
+        p.codes = codes;
+        p.win_off = v_off;
+        p.win_len = v_len;
+        p.n_win = n;
+        p.out = (int32_t *)sc->pres.p;
+        p.out_stride = slots_cap;
+        p.sc = scr;
+        p.task_win = (const int32_t *)sc->tw.p;
+        p.task_out = (const int32_t *)sc->to.p;
+        p.wave_adp = (const int32_t *)sc->wa.p;
+        p.task_chunk = (const int4 *)sc->tck.p;
+        p.n_waves = kGrid;
+        {
+            ForkJoin fj;
+            if (int rc = fj.begin(st, used.size())) return rc;
+            for (int k = 0; k < n_bk; ++k) {
+                const int b = used[k];
+                p.adp_pad = adps->pad[b];
+                p.adp_len = adps->len[b];
+                p.adp_id = adps->id[b];
+                p.n_adp = adps->count[b];
+                p.rt = adps->rt[b];
+                p.dev_waves = d_bk_waves + 2 * k;
+                if (int rc = dispatch_chunk(b, p, scr.go != scr.ge, fj.at(k))) {
+                    (void)fj.end();
+                    return rc;
+                }
+            }
+            if (int rc = fj.end()) return rc;
+        }
+        HIP_TRY(hipGetLastError());
+        const int32_t *tw = (const int32_t *)sc->tw.p, *tcand = (const int32_t *)sc->pcand.p;
+        const int4 *tck = (const int4 *)sc->tck.p;
+        const int32_t *res = (const int32_t *)sc->pres.p;
+        hipLaunchKernelGGL(k_zero_u64, dim3(kGrid), dim3(256), 0, st, (unsigned long long *)sc->pbest.p, dcount, ncap);
+        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)sc->phit.p, INT32_MAX, (size_t)n, st));
+        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)sc->phb.p, -1, (size_t)n, st));
+        hipLaunchKernelGGL(k_merge_best, dim3(kGrid), dim3(256), 0, st, tw, tck, tcand, res, slots_cap,
+                           (const int64_t *)d_slots, (unsigned long long *)sc->pbest.p);
+        for (int pass = 0; pass < 2; ++pass)
+            hipLaunchKernelGGL(k_merge_hit, dim3(kGrid), dim3(256), 0, st, dcand, tw, tck, tcand, res, slots_cap,
+                               (const int64_t *)d_slots, (const unsigned long long *)sc->pbest.p, threshold, pass,
+                               (int32_t *)sc->phit.p, (int32_t *)sc->phb.p, n);
+        hipLaunchKernelGGL(k_round_hits, dim3(gn), dim3(256), 0, st, (const int32_t *)sc->phb.p, n, nr, cur_of(r),
+                           list_of(r), d_n + r + 1, cur_of(r + 1), start_of(r + 1), sflags, d_pflag, d_rflag + r);
+        hipLaunchKernelGGL(k_mask_list, dim3(1024), dim3(256), 0, st, codes, win_off, list_of(r), d_n + r + 1);
+        HIP_TRY(hipGetLastError());
+        return 0;
+    };
+    std::vector<int32_t> h_n(kSlots + 2), h_flag(kSlots + 2);
+    int64_t need = 0;
+    for (int guard = 0;; ++guard) {
+        if (guard > 10000) return fail(PCABI_E_DEVICE, "middle scan: rounds did not settle");
+        // queue up to kBatch rounds from `slot`
+        const int upto = std::min(slot + kBatch, kSlots);
+        for (int r = slot; r < upto; ++r)
+            if (int rc = queue_round(r)) return rc;
+        queued_to = upto;
+        HIP_TRY(hipMemcpyAsync(h_n.data(), d_n, 4 * (size_t)(queued_to + 1), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(h_flag.data(), d_rflag, 4 * (size_t)queued_to, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(&need, d_need, 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        // the first flagged round (nothing of it or after it was kept): grow, queue it again
+        int bad = -1;
+        for (int r = slot; r < queued_to && bad < 0; ++r)
+            if (h_flag[r]) bad = r;
+        int done_to = bad >= 0 ? bad : queued_to;    // rounds [slot, done_to) are final
+        for (int r = slot; r < done_to; ++r) {
+            const int32_t nh = h_n[r + 1];
+            if (!nh) continue;
+            const size_t at = out.size();
+            out.resize(at + 8 * (size_t)nh);
+            HIP_TRY(hipMemcpyAsync(out.data() + at, list_of(r), 32 * (size_t)nh, hipMemcpyDeviceToHost, st));
+            out_round.insert(out_round.end(), (size_t)nh, round_base + r);
+        }
+        if (g_debug)
+            for (int r = slot; r < queued_to; ++r)
+                std::fprintf(stderr, "[pcabi] middle queued round %lld: %d reads, %d hits, flag %d\n",
+                             (long long)(round_base + r), h_n[r], h_n[r + 1], h_flag[r]);
+        if (bad >= 0) {
+            if ((h_flag[bad] & 3) && !pcabi_seed::grow_after_overflow(sc->seed, h_flag[bad] & 1, (h_flag[bad] >> 1) & 1))
+                return fail(PCABI_E_DEVICE, "middle scan: seed buffers past their limits");
+            if (h_flag[bad] & 4) sc->q_slots_cap = std::max<int64_t>(2 * sc->q_slots_cap, need + need / 4);
+            HIP_TRY(hipStreamSynchronize(st));
+            slot = bad;
+            continue;
+        }
+        if (h_n[queued_to] == 0) break;              // the last queued round found no hit
+        slot = queued_to;
+        if (slot == kSlots) {                        // wrap: the next round's reads to slot 0
+            HIP_TRY(hipMemcpyAsync(cur_of(0), cur_of(kSlots), 4 * (size_t)h_n[kSlots], hipMemcpyDeviceToDevice, st));
+            HIP_TRY(hipMemcpyAsync(start_of(0), start_of(kSlots), 4 * (size_t)h_n[kSlots], hipMemcpyDeviceToDevice, st));
+            HIP_TRY(hipMemcpyAsync(d_n, d_n + kSlots, 4, hipMemcpyDeviceToDevice, st));
+            round_base += kSlots;
+            slot = 0;
+        }
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    // (round, read) order: per read the reference's discovery order
+    const int64_t total = (int64_t)out_round.size();
+    std::vector<int64_t> ord((size_t)total);
+    for (int64_t j = 0; j < total; ++j) ord[j] = j;
+    std::sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) {
+        if (out_round[x] != out_round[y]) return out_round[x] < out_round[y];
+        return out[8 * x] < out[8 * y];
+    });
+    for (int64_t q = 0; q < total && q < cap; ++q) {
+        const int32_t *o = out.data() + 8 * ord[q];
+        hits[0 * cap + q] = o[0];
+        hits[1 * cap + q] = o[1];
+        hits[2 * cap + q] = o[2];
+        hits[3 * cap + q] = o[2] == -1 ? 0 : o[3] + 1;
+        hits[4 * cap + q] = o[4];
+        hits[5 * cap + q] = o[5];
+    }
+    return total;
+}
+
 }  // namespace
 
 extern "C" {
@@ -2032,13 +2465,25 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
         const pcabi_adapters *own;
         ~TableSwap() { s->adps = own; }
     } swap_back{sc, sc->adps};
+    std::vector<int32_t> h_len_copy;
+    if (!h_win_len) {                               // lengths only on the device: one small copy
+        h_len_copy.resize((size_t)n_win);
+        HIP_TRY(hipMemcpyAsync(h_len_copy.data(), win_len, 4 * (size_t)n_win, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        h_win_len = h_len_copy.data();
+    }
+    const pcabi::Scoring scoring{match, mismatch, gap_open, gap_extend};
     {
         int32_t longest = 0;
         for (int64_t k = 0; k < n_win; ++k) longest = std::max(longest, h_win_len[k]);
         const pcabi_adapters *use = nullptr;
-        if (int rc = adapters_for(sc->adps, pcabi::Scoring{match, mismatch, gap_open, gap_extend}, longest, &use))
-            return rc;
+        if (int rc = adapters_for(sc->adps, scoring, longest, &use)) return rc;
         sc->adps = use;
+    }
+    {
+        bool applied = false;
+        const int64_t r = middle_device_rounds(sc, codes, win_off, win_len, n_win, scoring, threshold, hits, cap, st, applied);
+        if (applied || r < 0) return r;
     }
     int64_t n_hits = 0;
     std::vector<int32_t> cur, nxt, nxt_start, hm_w, hm_s, hm_e, lens;

@@ -5,7 +5,8 @@
 namespace pcabi_eng {
 
 int dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st) {
-    const dim3 grid((unsigned)((p.n_waves + 3) / 4));
+    // planned on the device: n_waves is the grid (blocks striding over the device wave count)
+    const dim3 grid((unsigned)(p.dev_waves ? p.n_waves : (p.n_waves + 3) / 4));
     if (kBuckets[b].kind == STRIPED) return launch_striped(p, affine, st);
     if (kBuckets[b].kind == GENERIC) {
         switch (kBuckets[b].rpl) {

@@ -86,6 +86,10 @@ struct KParams {
     int32_t max_cols;          // host value: no window / chunk of the launch is longer
     int32_t *scratch;          // boundary rows: per wave slot max_cols x fields x 64 lanes
     int64_t n_items;           // waves of work (cross: 64-window groups x adapters)
+    // k_align_chunk planned on the device (the middle scan's queued rounds): dev_waves[0] = the
+    // launch's first wave in the task arrays, dev_waves[1] = its wave count; the grid is n_waves
+    // blocks that stride over the waves
+    const int32_t *dev_waves;
 };
 
 // Window reader: one dword per lane every 4 columns (a wave-uniform branch -- j is the same in
@@ -339,12 +343,7 @@ __global__ __launch_bounds__(256) void k_score_filter(FParams p) {
 // packed core on (read offset, columns) of the task's read with the end cell restricted to the
 // owned columns. Wave = one adapter, as k_align's pairs mode; results unmerged, one per task.
 template <int RPL, bool AFFINE, int KIND>
-__global__ __launch_bounds__(256, PCABI_WAVES) void k_align_chunk(KParams p) {
-    __shared__ __attribute__((aligned(16))) int32_t tab[4 * wave_tab_ints<KIND, RPL>()];
-    int32_t *wave_tab = tab + (threadIdx.x >> 6) * wave_tab_ints<KIND, RPL>();
-    int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const bool live = wave < p.n_waves;            // dead waves still join the table barrier
-    if (!live) wave = p.n_waves - 1;
+__device__ __forceinline__ void chunk_wave(const KParams &p, int64_t wave, bool live, int32_t *wave_tab) {
     const int64_t slot = wave * 64 + (threadIdx.x & 63);
     const int a_local = __builtin_amdgcn_readfirstlane(p.wave_adp[wave]);
     const int L = __builtin_amdgcn_readfirstlane(p.adp_len[a_local]);
@@ -371,6 +370,29 @@ __global__ __launch_bounds__(256, PCABI_WAVES) void k_align_chunk(KParams p) {
         r = pcabi::align_lane_generic<RPL, AFFINE, true>(rd, ck.y, adp, L, p.sc, ck.z, ck.w);
     }
     store_result(p.out, p.out_stride, p.task_out[slot], r);
+}
+
+template <int RPL, bool AFFINE, int KIND>
+__global__ __launch_bounds__(256, PCABI_WAVES) void k_align_chunk(KParams p) {
+    __shared__ __attribute__((aligned(16))) int32_t tab[4 * wave_tab_ints<KIND, RPL>()];
+    int32_t *wave_tab = tab + (threadIdx.x >> 6) * wave_tab_ints<KIND, RPL>();
+    if (!p.dev_waves) {
+        int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+        const bool live = wave < p.n_waves;        // dead waves still join the table barrier
+        if (!live) wave = p.n_waves - 1;
+        chunk_wave<RPL, AFFINE, KIND>(p, wave, live, wave_tab);
+        return;
+    }
+    // planned on the device: the launch's waves from dev_waves, the blocks striding over them
+    // (block-uniform trip count: every wave joins every table barrier); a wave rewrites only its
+    // own table, after its own reads of the previous one
+    const int64_t w0 = p.dev_waves[0], nw = p.dev_waves[1];
+    for (int64_t wb = blockIdx.x; wb * 4 < nw; wb += gridDim.x) {
+        int64_t wave = wb * 4 + (threadIdx.x >> 6);
+        const bool live = wave < nw;
+        if (!live) wave = nw - 1;
+        chunk_wave<RPL, AFFINE, KIND>(p, w0 + wave, live, wave_tab);
+    }
 }
 
 // ---- striped bucket: adapters longer than kMaxRPL (pcabi_dp.h align_lane_striped) ----------------
@@ -498,5 +520,8 @@ int dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st);
 void dispatch_filter(int rpl, const FParams &p, bool affine, hipStream_t st);
 // the striped bucket (k_align_striped): p.rt, p.max_cols set by the caller
 int launch_striped(KParams p, bool affine, hipStream_t st);
+// pcabi_decide.hip: window order longest first (stable), scratch size and the async sort
+size_t sort_by_length_bytes(int64_t n);
+int sort_by_length(const int32_t *len, int64_t n, int32_t *order, void *tmp, hipStream_t st);
 
 }  // namespace pcabi_eng

@@ -21,16 +21,25 @@
 //   * Pairs with no probe hit get no bound (no alignment can reach theta); the others the
 //     largest S_b. Pairs with a bound >= T go to the full attribute DP exactly as after the
 //     filter. The engine re-seeds every later round on the masked reads (N never matches).
-// Kernels (integer work, no MFMA):
-//   k_seed_scan   reads grid-stride over blocks, 8 positions per lane: the 8-mer codes of the
-//                 positions, and per probe length K (4..8) a bitmap test and a rank into the probe
-//                 entries, all in LDS; hits become (read, adapter, diagonal) tasks per band class,
-//                 staged per block in LDS and appended with one global atomic per chunk;
-//   k_seed_band   one lane per task: the banded Gotoh score DP (2E+1 cells per adapter row in
-//                 registers), atomicMax into the pair's bound;
-//   k_cands       the pairs whose bound reaches T, compacted for the host (k_bound16: or all
-//                 bounds as int16).
+// Kernels (integer work, no MFMA), r03 layout: the streaming part and the irregular part apart.
+//   k_seed_scan   the read bytes stream through (grid-stride over reads, 8 positions per lane and
+//                 sub-step): 2-bit codes by SWAR, one LDS bitmap word per position (the merged
+//                 8-mer table; positions whose valid run is shorter than 8 flagged for the short
+//                 tables). Only the bitmaps sit in LDS. A position that hits is appended as a raw
+//                 hit (read, position) to the block's own slab in global memory (an LDS counter,
+//                 no global atomics, no barriers inside the loop);
+//   k_seed_expand one block per slab: the probe entries of every raw hit (rank / entry tables in
+//                 LDS) become (read, adapter, diagonal) tasks per band class -- a block scan of the
+//                 per-hit counts, one global atomic per class and 256 hits;
+//   k_seed_band   grid-stride over a class's tasks: the banded Gotoh score DP (2E+1 cells per
+//                 adapter row in registers; the read bytes of the band streamed in dwords, the
+//                 adapters in LDS), atomicMax into the pair's bound;
+//   k_cands       the pairs whose bound reaches T, compacted (k_bound16: or all bounds as int16).
+// Every count the launches need may live on the device (the read count of a round included), so
+// the engine can queue whole rounds without a host round trip; capacities that a launch could
+// exceed raise a flag the host checks once, and the scan is then rerun with larger buffers.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <atomic>
@@ -64,15 +73,12 @@ constexpr int kCls = 2;            // band classes: e <= E0, e <= E1
 constexpr int kMaxE = 15;          // band half-width the kernels are built for
 constexpr int kMaxL = 255;
 constexpr int kMaxEnt = 8192;      // probe entries / distinct probes kept in LDS
-#ifndef PCABI_SEED_BUF
-#define PCABI_SEED_BUF 256
-#endif
 
 #ifndef PCABI_BAND_EXIT
 #define PCABI_BAND_EXIT 1   // rows between the banded DP's early-exit checks (1: every row, r02 A/B)
 #endif
-constexpr int kBuf = PCABI_SEED_BUF;   // staged tasks per block and class
-constexpr int kLdsMax = 64 * 1024; // per block: probe tables + stage
+constexpr int kLdsMax = 64 * 1024; // per block: probe tables
+constexpr int kAdpLds = 16 * 1024; // adapters copied to LDS by the band kernels up to this size
 constexpr int kNeg = -(1 << 20);
 constexpr int kPos = 8;            // read positions per lane and scan step (16 bases loaded)
 constexpr int kNW = 4;             // dwords of bases per lane and step
@@ -80,87 +86,52 @@ constexpr int kNW = 4;             // dwords of bases per lane and step
 #define PCABI_SEED_SUB 2
 #endif
 constexpr int kSub = PCABI_SEED_SUB;   // sub-steps per scan iteration
-#ifndef PCABI_SEED_FLUSH
-#define PCABI_SEED_FLUSH (8 / PCABI_SEED_SUB - 1)   // stage flush every 8 sub-steps
-#endif
+constexpr unsigned kSlowBit = 0x80000000u;   // raw hit: the position's valid run is shorter than 8
+constexpr int kBandGrid = 4096;    // band / cands launches whose count is on the device: grid-stride
 
 struct ScanArgs {
     const uint8_t *codes;
     const int64_t *v_off;
     const int32_t *v_len;
-    int64_t n;
+    int64_t n;                  // reads (host upper bound)
+    const int32_t *n_dev;       // != nullptr: the read count on the device (<= n)
     const uint32_t *tabs;       // LDS image: bits | rank16 | estart16 | ent (dwords, copied as is)
     int32_t tab_dw;             // its dwords
+    int32_t bits_dw;            // the bitmaps' dwords at its head (all the scan needs)
     int32_t bits_off[kNK];      // dword offset of K's bitmap in the image, -1 when no probe has length K;
                                 // K = 8 is the merged table: every 8-mer extending a probe of any K
     int32_t min_k;              // shortest probe
     int32_t rank_off, estart_off, ent_off;   // dword offsets of the other sections
                                              // (entries: adapter << 9 | band class << 8 | offset)
+    uint2 *raw;                 // per scan block a slab of raw hits (read, position | kSlowBit)
+    int32_t slab;
+    int32_t *raw_cnt;           // raw hits per slab
+    int32_t *flags;             // [0] a slab overflowed, [1] a task region overflowed
     int4 *task;                 // kCls regions of cap tasks: (read, adapter, diagonal, 0)
     int64_t cap;
-    int32_t *cnt;               // tasks per class (may exceed cap: the caller grows and reruns)
+    int32_t *cnt;               // tasks per class (may exceed cap: flags[1])
 };
 
-struct Stage {
-    int4 buf[kCls][kBuf];
-    int cnt[kCls];
-    int base[kCls];
-};
-
-__device__ __forceinline__ void stage_task(Stage &sg, int cls, int4 t, const ScanArgs &a) {
-    const int slot = atomicAdd(&sg.cnt[cls], 1);
-    if (slot < kBuf) {
-        sg.buf[cls][slot] = t;
-    } else {                                           // burst past the stage: straight out
-        const int g = atomicAdd(&a.cnt[cls], 1);
-        if (g < a.cap) a.task[cls * a.cap + g] = t;
-    }
-}
-
-// Block-uniform: writes out the classes whose stage holds at least `at_least` tasks.
-__device__ __forceinline__ void flush(Stage &sg, int at_least, const ScanArgs &a) {
-    __syncthreads();
-    bool any = false;
-#pragma unroll
-    for (int c = 0; c < kCls; ++c) any |= sg.cnt[c] >= at_least && sg.cnt[c] > 0;
-    if (!any) return;                                  // uniform: every thread read the same counts
-    if (threadIdx.x < kCls) {
-        const int c = threadIdx.x;
-        const int m = min(sg.cnt[c], kBuf);
-        sg.base[c] = (sg.cnt[c] >= at_least && m > 0) ? atomicAdd(&a.cnt[c], m) : -1;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < kCls; ++c) {
-        if (sg.base[c] < 0) continue;
-        const int m = min(sg.cnt[c], kBuf);
-        for (int i = threadIdx.x; i < m; i += 256) {
-            const int64_t g = (int64_t)sg.base[c] + i;
-            if (g < a.cap) a.task[c * a.cap + g] = sg.buf[c][i];
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < kCls && sg.base[threadIdx.x] >= 0) sg.cnt[threadIdx.x] = 0;
-    __syncthreads();
+__device__ __forceinline__ int64_t dev_count(const int32_t *n_dev, int64_t n) {
+    return n_dev ? min((int64_t)*n_dev, n) : n;
 }
 
 __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
     extern __shared__ uint32_t lds[];
-    __shared__ Stage sg;
-    for (int i = threadIdx.x; i < a.tab_dw; i += 256) lds[i] = a.tabs[i];
-    if (threadIdx.x < kCls) sg.cnt[threadIdx.x] = 0;
+    __shared__ int s_cnt;
+    for (int i = threadIdx.x; i < a.bits_dw; i += 256) lds[i] = a.tabs[i];
+    if (threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
-    const uint16_t *rank = reinterpret_cast<const uint16_t *>(lds + a.rank_off);
-    const uint16_t *estart = reinterpret_cast<const uint16_t *>(lds + a.estart_off);
-    const int32_t *ent = reinterpret_cast<const int32_t *>(lds + a.ent_off);
-    // The block walks its reads (blockIdx.x, + gridDim.x, ...) 2048 positions at a time; the
+    const int64_t nr = dev_count(a.n_dev, a.n);
+    uint2 *slab = a.raw + (int64_t)blockIdx.x * a.slab;
+    // The block walks its reads (blockIdx.x, + gridDim.x, ...) 4096 positions at a time; the
     // bytes of the next step (and the next read's length / offset) are loaded before the current
     // step is processed, so the global latency hides behind the lookups.
     int64_t k = blockIdx.x, nk = k;
     int len = 0, nlen = 0;
     const uint8_t *base = a.codes, *nbase = a.codes;
     auto next_read = [&](int64_t from, int &ln, const uint8_t *&bs) -> int64_t {
-        for (; from < a.n; from += gridDim.x) {
+        for (; from < nr; from += gridDim.x) {
             ln = a.v_len[from];
             if (ln > 0) {
                 bs = a.codes + a.v_off[from];
@@ -186,16 +157,13 @@ __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
         }
     };
     k = next_read(k, len, base);
-    if (k < a.n) nk = next_read(k + gridDim.x, nlen, nbase);
+    if (k < nr) nk = next_read(k + gridDim.x, nlen, nbase);
     int p0b = 0;
-    // kSub sub-steps of 2048 positions per iteration, fetched together one iteration ahead:
-    // more bytes in flight per latency
     uint32_t wn[kSub][kNW];
 #pragma unroll
     for (int h = 0; h < kSub; ++h)
-        if (k < a.n) fetch(base, len, h * 256 * kPos, wn[h]);
-    int iter = 0;
-    while (k < a.n) {                                  // block-uniform: every lane takes part
+        if (k < nr) fetch(base, len, h * 256 * kPos, wn[h]);
+    while (k < nr) {                                   // block-uniform
         const int64_t ck = k;
         const int clen = len, cp0b = p0b;
         uint32_t wc[kSub][kNW];
@@ -209,100 +177,206 @@ __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
             len = nlen;
             base = nbase;
             p0b = 0;
-            if (k < a.n) nk = next_read(k + gridDim.x, nlen, nbase);
+            if (k < nr) nk = next_read(k + gridDim.x, nlen, nbase);
         }
 #pragma unroll
         for (int h = 0; h < kSub; ++h)
-            if (k < a.n) fetch(base, len, p0b + h * 256 * kPos, wn[h]);
+            if (k < nr) fetch(base, len, p0b + h * 256 * kPos, wn[h]);
 #pragma unroll
         for (int h = 0; h < kSub; ++h) {
-        const int cp0 = cp0b + h * 256 * kPos + kPos * (int)threadIdx.x;
-        const uint32_t *w = wc[h];
-        // 16 bases (SWAR): c32 = their 2-bit codes, first base in the top bits; vmask bit t =
-        // base t is A/C/G/T inside the read (Dna5 codes are 0..4: N has bit 2)
-        uint32_t c32 = 0, vmask = 0;
+            const int cp0 = cp0b + h * 256 * kPos + kPos * (int)threadIdx.x;
+            const uint32_t *w = wc[h];
+            // 16 bases (SWAR): c32 = their 2-bit codes, first base in the top bits; vmask bit t =
+            // base t is A/C/G/T inside the read (Dna5 codes are 0..4: N has bit 2)
+            uint32_t c32 = 0, vmask = 0;
 #pragma unroll
-        for (int d = 0; d < kNW; ++d) {
-            const uint32_t c4 = ((w[d] & 0x03030303u) * 0x40100401u) >> 24;
-            const uint32_t nb = (((~w[d]) >> 2) & 0x01010101u) * 0x10204080u >> 28;
-            c32 = (c32 << 8) | c4;
-            vmask |= nb << (4 * d);
-        }
-        const int rem = clen - cp0;
-        vmask &= rem >= 16 ? 0xFFFFu : (rem > 0 ? (1u << rem) - 1u : 0u);
-        // fast path: every probe is a prefix of the 8-mer at its position, and the K = 8 table
-        // holds every 8-mer that extends a probe -- one LDS word per position
-        uint32_t hits = 0, slow = 0;
-        if (__all((vmask & 0x7FFFu) == 0x7FFFu)) {
-            // every lane's 8 positions see 8 valid bases: one bitmap word each, the K = 8 bitmap
-            // at LDS byte 0 (plan()), byte address (c8 >> 5) << 2 straight from c32
-#pragma unroll
-            for (int i = 0; i < kPos; ++i) {
-                const int sh = 16 - 2 * i;
-                const uint32_t word = *reinterpret_cast<const uint32_t *>(
-                    reinterpret_cast<const char *>(lds) + ((c32 >> (sh + 3)) & 0x1FFCu));
-                hits |= ((word >> ((c32 >> sh) & 31u)) & 1u) << i;
+            for (int d = 0; d < kNW; ++d) {
+                const uint32_t c4 = ((w[d] & 0x03030303u) * 0x40100401u) >> 24;
+                const uint32_t nb = (((~w[d]) >> 2) & 0x01010101u) * 0x10204080u >> 28;
+                c32 = (c32 << 8) | c4;
+                vmask |= nb << (4 * d);
             }
-        } else {
+            const int rem = clen - cp0;
+            vmask &= rem >= 16 ? 0xFFFFu : (rem > 0 ? (1u << rem) - 1u : 0u);
+            uint32_t hits = 0, slow = 0;
+            if (__all((vmask & 0x7FFFu) == 0x7FFFu)) {
+                // every lane's 8 positions see 8 valid bases: one bitmap word each, the K = 8 bitmap
+                // at LDS byte 0 (plan()), byte address (c8 >> 5) << 2 straight from c32
 #pragma unroll
-        for (int i = 0; i < kPos; ++i) {
-            const uint32_t c8 = (c32 >> (16 - 2 * i)) & 0xFFFFu;
-            const uint32_t word = lds[a.bits_off[kNK - 1] + (int)(c8 >> 5)];
-            const bool full = ((vmask >> i) & 0xFFu) == 0xFFu;
-            hits |= (full && ((word >> (c8 & 31)) & 1u)) ? 1u << i : 0u;
-            // a valid run shorter than 8 bases (an N or the read end ahead): the short tables
-            slow |= (!full && ((vmask >> i) & ((1u << a.min_k) - 1u)) == (1u << a.min_k) - 1u) ? 1u << i : 0u;
-        }
-        }
-        while (hits | slow) {
-            const bool fast = hits != 0;
-            const int i = __builtin_ctz(fast ? hits : slow);
-            if (fast) hits &= hits - 1;
-            else slow &= slow - 1;
-            const uint32_t c8 = (c32 >> (16 - 2 * i)) & 0xFFFFu;
-            const int q = cp0 + i;
-            const int run = __builtin_ctz(~(vmask >> i));
-            for (int kk = fast ? kNK - 1 : 0; kk < (fast ? kNK : kNK - 1); ++kk) {
-                const int K = kMinK + kk;
-                if (a.bits_off[kk] < 0 || (!fast && K > run)) continue;
-                const uint32_t code = c8 >> (2 * (kMaxK - K));
-                const int dw = a.bits_off[kk] + (int)(code >> 5);
-                const uint32_t word = lds[dw], bit = 1u << (code & 31);
-                if (!(word & bit)) continue;
-                const int r = rank[dw] + __popc(word & (bit - 1));
-                const int e = estart[r + 1];
-                for (int b = estart[r]; b < e; ++b) {
-                    const int en = ent[b];                 // adapter << 9 | class << 8 | offset
-                    stage_task(sg, (en >> 8) & 1, make_int4((int)ck, en >> 9, q - (en & 255), 0), a);
+                for (int i = 0; i < kPos; ++i) {
+                    const int sh = 16 - 2 * i;
+                    const uint32_t word = *reinterpret_cast<const uint32_t *>(
+                        reinterpret_cast<const char *>(lds) + ((c32 >> (sh + 3)) & 0x1FFCu));
+                    hits |= ((word >> ((c32 >> sh) & 31u)) & 1u) << i;
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < kPos; ++i) {
+                    const uint32_t c8 = (c32 >> (16 - 2 * i)) & 0xFFFFu;
+                    const uint32_t word = lds[(int)(c8 >> 5)];
+                    const bool full = ((vmask >> i) & 0xFFu) == 0xFFu;
+                    hits |= (full && ((word >> (c8 & 31)) & 1u)) ? 1u << i : 0u;
+                    // a valid run shorter than 8 bases (an N or the read end ahead): the short tables
+                    slow |= (!full && ((vmask >> i) & ((1u << a.min_k) - 1u)) == (1u << a.min_k) - 1u) ? 1u << i : 0u;
+                }
+            }
+            const uint32_t any = hits | slow;
+            if (any) {                                 // ~4 % of the lanes: append to the block's slab
+                int slot = atomicAdd(&s_cnt, __popc(any));
+                uint32_t left = any;
+                while (left) {
+                    const int i = __builtin_ctz(left);
+                    left &= left - 1;
+                    if (slot < a.slab) slab[slot] = make_uint2((uint32_t)ck, (uint32_t)(cp0 + i) | ((slow >> i) & 1u ? kSlowBit : 0u));
+                    ++slot;
                 }
             }
         }
-        }
-        if ((++iter & PCABI_SEED_FLUSH) == 0) flush(sg, kBuf / 2, a);
     }
-    flush(sg, 1, a);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        a.raw_cnt[blockIdx.x] = min(s_cnt, a.slab);
+        if (s_cnt > a.slab) atomicOr(&a.flags[0], 1);
+    }
 }
+
+// One block per slab: the probe entries of its raw hits become tasks. Each pass of 256 hits counts
+// the tasks per class, takes its place with one atomic per class, then writes them (the same
+// lookups again from LDS).
+__global__ __launch_bounds__(256) void k_seed_expand(ScanArgs a) {
+    extern __shared__ uint32_t lds[];
+    typedef hipcub::BlockScan<long long, 256> Scan;
+    __shared__ typename Scan::TempStorage scan_tmp;
+    __shared__ long long s_base[kCls];
+    for (int i = threadIdx.x; i < a.tab_dw; i += 256) lds[i] = a.tabs[i];
+    __syncthreads();
+    const uint16_t *rank = reinterpret_cast<const uint16_t *>(lds + a.rank_off);
+    const uint16_t *estart = reinterpret_cast<const uint16_t *>(lds + a.estart_off);
+    const int32_t *ent = reinterpret_cast<const int32_t *>(lds + a.ent_off);
+    const int cnt = a.raw_cnt[blockIdx.x];
+    const uint2 *slab = a.raw + (int64_t)blockIdx.x * a.slab;
+    for (int base = 0; base < cnt; base += 256) {      // block-uniform
+        const int i = base + (int)threadIdx.x;
+        int64_t rd = -1;
+        int q = 0, run = 0;
+        bool fast = false;
+        uint32_t c8 = 0;
+        if (i < cnt) {
+            const uint2 r = slab[i];
+            rd = r.x;
+            q = (int)(r.y & ~kSlowBit);
+            fast = !(r.y & kSlowBit);
+            const int len = a.v_len[rd];
+            const uint8_t *p = a.codes + a.v_off[rd] + q;
+            const int a0 = (int)((uintptr_t)p & 3);
+            const uint32_t *dq = reinterpret_cast<const uint32_t *>(p - a0);
+            const uint32_t w0 = __builtin_amdgcn_alignbyte(dq[1], dq[0], a0);
+            const uint32_t w1 = __builtin_amdgcn_alignbyte(dq[2], dq[1], a0);
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const uint32_t b = ((t < 4 ? w0 : w1) >> (8 * (t & 3))) & 0xFFu;
+                const bool valid = b < 4 && q + t < len;
+                if (valid && run == t) ++run;
+                c8 = (c8 << 2) | (b & 3u);
+            }
+        }
+        // two passes over this hit's entries: count (pass 0), then write (pass 1)
+        long long mine = 0;
+        for (int pass = 0; pass < 2; ++pass) {
+            long long at[kCls] = {0, 0};
+            if (pass == 1) {
+                at[0] = s_base[0] + (mine & 0xFFFFFFFFll);
+                at[1] = s_base[1] + (mine >> 32);
+            }
+            long long c = 0;
+            if (rd >= 0) {
+                for (int kk = fast ? kNK - 1 : 0; kk < (fast ? kNK : kNK - 1); ++kk) {
+                    const int K = kMinK + kk;
+                    if (a.bits_off[kk] < 0 || (!fast && K > run)) continue;
+                    const uint32_t code = c8 >> (2 * (kMaxK - K));
+                    const int dw = a.bits_off[kk] + (int)(code >> 5);
+                    const uint32_t word = lds[dw], bit = 1u << (code & 31);
+                    if (!(word & bit)) continue;
+                    const int r = rank[dw] + __popc(word & (bit - 1));
+                    const int e = estart[r + 1];
+                    for (int b = estart[r]; b < e; ++b) {
+                        const int en = ent[b];                 // adapter << 9 | class << 8 | offset
+                        const int cls = (en >> 8) & 1;
+                        if (pass == 0) {
+                            c += cls ? (1ll << 32) : 1ll;
+                        } else {
+                            const long long g = at[cls]++;
+                            if (g < a.cap) a.task[cls * a.cap + g] = make_int4((int)rd, en >> 9, q - (en & 255), 0);
+                        }
+                    }
+                }
+            }
+            if (pass == 0) {
+                long long total;
+                Scan(scan_tmp).ExclusiveSum(c, mine, total);
+                if (threadIdx.x == 0) {
+                    const long long t0 = total & 0xFFFFFFFFll, t1 = total >> 32;
+                    s_base[0] = t0 ? atomicAdd(&a.cnt[0], (int)t0) : 0;
+                    s_base[1] = t1 ? atomicAdd(&a.cnt[1], (int)t1) : 0;
+                    if (s_base[0] + t0 > a.cap || s_base[1] + t1 > a.cap) atomicOr(&a.flags[1], 1);
+                }
+                __syncthreads();
+            }
+        }
+        __syncthreads();                               // s_base / scan_tmp reused by the next pass
+    }
+}
+
+// The band's read bytes as a stream: rd[p], rd[p + 1], ... one dword load per 4 bytes, issued one
+// dword ahead (the band DP of a random probe hit usually stops within a dozen rows, so the first
+// loads cover most tasks). Reads at most 11 bytes past the last byte taken.
+struct ByteStream {
+    const uint32_t *q;
+    uint64_t buf;
+    uint32_t nx;
+    int o;
+    __device__ __forceinline__ explicit ByteStream(const uint8_t *p) {
+        const int a0 = (int)((uintptr_t)p & 3);
+        q = reinterpret_cast<const uint32_t *>(p - a0);
+        buf = ((uint64_t)q[1] << 32) | q[0];
+        nx = q[2];
+        q += 3;
+        o = 8 * a0;
+    }
+    __device__ __forceinline__ int next() {
+        const int v = (int)((buf >> o) & 0xFFu);
+        o += 8;
+        if (o == 32) {
+            buf = (buf >> 32) | ((uint64_t)nx << 32);
+            nx = *q++;
+            o = 0;
+        }
+        return v;
+    }
+};
 
 // Banded score DP of one task: rows i = 1..L of the adapter, per row the 2E+1 cells of the
 // diagonals d0 - E .. d0 + E (cell x <-> read column j = i + d0 + x - E), free end gaps as the
 // full DP: S(0, j) = 0, S(i, 0) = 0, ends in row L (j < len) or in the last column (j = len).
 // CHECK: the band touches column 0 or the last column, or leaves the read.
-// Early exit (inside bands, T > 0): no path gains more than `match` per remaining row (gaps cost),
-// and an inside band holds no column-0 restart and no last-column end, so once every cell of row
-// i satisfies S + match (L - i) < T the pair cannot reach T: the DP stops and returns that bound
-// (below T, which is all the caller compares). Random probe hits -- most tasks -- stop early.
+// Early exit (inside bands, T > 0, best_sub > 0 -- plan() requires both): no path gains more
+// than best_sub per remaining row (gaps cost), and an inside band holds no column-0 restart and
+// no last-column end, so once every cell of row i satisfies S + best_sub (L - i) < T the pair
+// cannot reach T: the DP stops and returns that bound (below T, which is all the caller
+// compares). Random probe hits -- most tasks -- stop early.
 template <int E, bool CHECK>
 __device__ __forceinline__ int band_best(const uint8_t *rd, int len, const uint8_t *ac, int L, int d0,
                                          const pcabi::Scoring &sc, int T) {
     constexpr int W = 2 * E + 1;
     int S[W], V[W], R[W];
+    ByteStream bs(rd + (CHECK ? 0 : d0 - E));          // inside bands: rd[d0 - E] onwards
 #pragma unroll
     for (int x = 0; x < W; ++x) {
         const int j0 = d0 + x - E;                           // row 0
         S[x] = (!CHECK || (j0 >= 0 && j0 <= len)) ? 0 : kNeg;
         V[x] = kNeg;
         const int j1 = j0 + 1;                               // row 1's read column
-        R[x] = (!CHECK || (j1 >= 1 && j1 <= len)) ? rd[j1 - 1] : 7;
+        R[x] = CHECK ? ((j1 >= 1 && j1 <= len) ? rd[j1 - 1] : 7) : bs.next();
     }
     int best = 0;                                            // S(L, 0) = 0 is always scouted
     for (int i = 1; i <= L; ++i) {
@@ -327,7 +401,8 @@ __device__ __forceinline__ int band_best(const uint8_t *rd, int len, const uint8
 #pragma unroll
         for (int x = 0; x + 1 < W; ++x) R[x] = R[x + 1];
         const int jn = i + 1 + d0 + E;
-        R[W - 1] = (!CHECK || (jn >= 1 && jn <= len)) ? rd[jn - 1] : 7;
+        if (CHECK) R[W - 1] = (jn >= 1 && jn <= len) ? rd[jn - 1] : 7;
+        else if (i < L) R[W - 1] = bs.next();
         if (!CHECK && (i % PCABI_BAND_EXIT) == 0) {
             int mx = S[0];
 #pragma unroll
@@ -344,49 +419,74 @@ __device__ __forceinline__ int band_best(const uint8_t *rd, int len, const uint8
     return best;
 }
 
+// Grid-stride over the class's tasks (their count from the device, clamped to the capacity).
+// adp_lds > 0: the flat adapter table (that many bytes) is copied to LDS first.
 template <int E>
-__global__ __launch_bounds__(256) void k_seed_band(const int4 *task, int32_t n_task, const uint8_t *codes,
-                                                   const int64_t *v_off, const int32_t *v_len, const uint8_t *adp,
-                                                   const int32_t *adp_off, const int32_t *adp_len, pcabi::Scoring sc,
-                                                   const int32_t *thr, int32_t *bound, int64_t n) {
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (t >= n_task) return;
-    const int4 tk = task[t];
-    const int L = adp_len[tk.y];
-    const int len = v_len[tk.x];
-    const int d0 = tk.z;
-    const uint8_t *rd = codes + v_off[tk.x];
-    const uint8_t *ac = adp + adp_off[tk.y];
-    const bool inside = d0 - E >= 1 && d0 + E + L + 1 < len;
-    const int T = thr[tk.y];
-    const int best = inside ? band_best<E, false>(rd, len, ac, L, d0, sc, T)
-                            : band_best<E, true>(rd, len, ac, L, d0, sc, T);
-    atomicMax(&bound[(int64_t)tk.y * n + tk.x], best);
+__global__ __launch_bounds__(256) void k_seed_band(const int4 *task, const int32_t *n_task, int64_t cap,
+                                                   const uint8_t *codes, const int64_t *v_off, const int32_t *v_len,
+                                                   const uint8_t *adp, int32_t adp_lds, const int32_t *adp_off,
+                                                   const int32_t *adp_len, pcabi::Scoring sc, const int32_t *thr,
+                                                   int32_t *bound, int64_t n) {
+    extern __shared__ uint32_t lds_adp[];
+    const uint8_t *ad = adp;
+    if (adp_lds > 0) {
+        for (int i = threadIdx.x; i < adp_lds / 4; i += 256) lds_adp[i] = reinterpret_cast<const uint32_t *>(adp)[i];
+        __syncthreads();
+        ad = reinterpret_cast<const uint8_t *>(lds_adp);
+    }
+    const int64_t nt = min((int64_t)*n_task, cap);
+    for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < nt; t += (int64_t)gridDim.x * 256) {
+        const int4 tk = task[t];
+        const int L = adp_len[tk.y];
+        const int len = v_len[tk.x];
+        const int d0 = tk.z;
+        const uint8_t *rd = codes + v_off[tk.x];
+        const uint8_t *ac = ad + adp_off[tk.y];
+        const bool inside = d0 - E >= 1 && d0 + E + L + 1 < len;
+        const int T = thr[tk.y];
+        const int best = inside ? band_best<E, false>(rd, len, ac, L, d0, sc, T)
+                                : band_best<E, true>(rd, len, ac, L, d0, sc, T);
+        atomicMax(&bound[(int64_t)tk.y * n + tk.x], best);
+    }
 }
 
 // The pairs whose bound reaches their adapter's threshold T[a], as (a << 32 | read) keys
-// (unordered; one atomic per wave).
-__global__ __launch_bounds__(256) void k_cands(const int32_t *bound, int64_t n, int64_t total, const int32_t *T,
-                                               int64_t *out, int64_t cap, unsigned long long *cnt) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t a = i / (n > 0 ? n : 1);
-    const bool want = i < total && bound[i] >= T[a];
-    const uint64_t m = __ballot(want);
-    if (!m) return;
+// (unordered; one atomic per wave), grid-stride over the n_dev x n_adp bounds (row stride n).
+__global__ __launch_bounds__(256) void k_cands(const int32_t *bound, int64_t n, const int32_t *n_dev, int32_t n_adp,
+                                               const int32_t *T, int64_t *out, int64_t cap, unsigned long long *cnt) {
+    const int64_t nr = dev_count(n_dev, n);
+    const int64_t total = nr * n_adp;
     const int lane = threadIdx.x & 63;
-    const int leader = __ffsll((unsigned long long)m) - 1;
-    unsigned long long base = 0;
-    if (lane == leader) base = atomicAdd(cnt, (unsigned long long)__popcll(m));
-    base = __shfl(base, leader);
-    if (want) {
-        const unsigned long long slot = base + __popcll(m & ((1ull << lane) - 1));
-        if ((int64_t)slot < cap) out[slot] = (a << 32) | (i - a * n);
+    for (int64_t base = (int64_t)blockIdx.x * 256; base < total; base += (int64_t)gridDim.x * 256) {   // uniform
+        const int64_t i = base + threadIdx.x;
+        const int64_t a = nr > 0 ? i / nr : 0, r = i - a * nr;
+        const bool want = i < total && bound[a * n + r] >= T[a];
+        const uint64_t m = __ballot(want);
+        if (!m) continue;
+        const int leader = __ffsll((unsigned long long)m) - 1;
+        unsigned long long b0 = 0;
+        if (lane == leader) b0 = atomicAdd(cnt, (unsigned long long)__popcll(m));
+        b0 = __shfl(b0, leader);
+        if (want) {
+            const unsigned long long slot = b0 + __popcll(m & ((1ull << lane) - 1));
+            if ((int64_t)slot < cap) out[slot] = (a << 32) | r;
+        }
     }
 }
 
 __global__ __launch_bounds__(256) void k_bound16(const int32_t *bound, int64_t cnt, int16_t *s16) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i < cnt) s16[i] = (int16_t)max(min(bound[i], 32767), -32768);
+}
+
+// bound[a * n + r] = NEG16 for the n_dev x n_adp live entries (row stride n).
+__global__ __launch_bounds__(256) void k_bound_reset(int32_t *bound, int64_t n, const int32_t *n_dev, int32_t n_adp) {
+    const int64_t nr = dev_count(n_dev, n);
+    const int64_t total = nr * n_adp;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        const int64_t a = i / nr;
+        bound[a * n + (i - a * nr)] = pcabi::sf::NEG16;
+    }
 }
 
 struct Buf {
@@ -424,11 +524,12 @@ struct State {
     bool planned = false, ok = false;
     double cost_seed = 0.0, cost_filter = 0.0;    // per read position (model units)
     int band[kCls] = {0, 0};                      // E of each class
-    size_t lds_bytes = 0;
+    size_t lds_bytes = 0;                         // the whole probe image (k_seed_expand)
+    int32_t adp_bytes = 0;                        // flat adapter table, dword-rounded
     ScanArgs a{};
-    Buf tabs, adp, adp_off, adp_len, task, cnt, bound, thr, cands, ccnt;
-    int64_t cap = 0, ccap = 0;
-    int scan_blocks = 0;                          // resident k_seed_scan blocks (per plan)
+    Buf tabs, adp, adp_off, adp_len, task, cnt, bound, thr, cands, ccnt, raw, rawcnt;
+    int64_t cap = 0, ccap = 0, raw_cap = 0;
+    int scan_blocks = 0;                          // resident k_seed_scan blocks
 };
 
 State *create() { return new State(); }
@@ -544,13 +645,14 @@ int plan(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hl
         std::copy(v.begin(), v.end(), reinterpret_cast<uint16_t *>(img.data() + off));
         return off;
     };
+    A.bits_dw = (int32_t)img.size();                // the scan copies only the bitmaps
     A.rank_off = append16(rank);
     A.estart_off = append16(estart);
     A.ent_off = (int32_t)img.size();
     for (int32_t x : ent) img.push_back((uint32_t)x);
     A.tab_dw = (int32_t)img.size();
     s->lds_bytes = 4 * img.size();
-    if (s->lds_bytes + sizeof(Stage) > (size_t)kLdsMax) return 0;
+    if (s->lds_bytes + 4096 > (size_t)kLdsMax) return 0;
     s->cost_seed = seed;
     s->cost_filter = filt;
     std::vector<int32_t> aoff((size_t)n_adp), alen((size_t)n_adp);
@@ -560,6 +662,7 @@ int plan(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hl
         alen[a] = std::max(hlen[a], 0);
         tot += alen[a];
     }
+    s->adp_bytes = (tot + 3) & ~3;
     std::vector<uint8_t> flat((size_t)tot + 16, 0);
     for (int32_t a = 0; a < n_adp; ++a) std::copy(hcodes + hoff[a], hcodes + hoff[a] + alen[a], flat.begin() + aoff[a]);
     if (int rc = s->tabs.ensure(4 * img.size())) return rc;
@@ -580,38 +683,109 @@ int plan(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hl
     return 0;
 }
 
-void launch_band(const State *s, int E, int32_t cnt, int c, const uint8_t *codes, const int64_t *v_off,
-                 const int32_t *v_len, const pcabi::Scoring &sc, int64_t n, hipStream_t st) {
-    const dim3 grid((unsigned)((cnt + 255) / 256));
+void launch_band(const State *s, int E, int c, const uint8_t *codes, const int64_t *v_off, const int32_t *v_len,
+                 const pcabi::Scoring &sc, int64_t n, unsigned grid, hipStream_t st) {
     const int4 *task = (const int4 *)s->task.p + c * s->cap;
+    const int32_t *n_task = (const int32_t *)s->cnt.p + c;
     const uint8_t *adp = (const uint8_t *)s->adp.p;
     const int32_t *aoff = (const int32_t *)s->adp_off.p, *alen = (const int32_t *)s->adp_len.p;
     int32_t *bound = (int32_t *)s->bound.p;
+    const int32_t lds = s->adp_bytes <= kAdpLds ? s->adp_bytes : 0;
     switch (E) {
-#define C(X)                                                                                                   \
-    case X:                                                                                                    \
-        hipLaunchKernelGGL(k_seed_band<X>, grid, dim3(256), 0, st, task, cnt, codes, v_off, v_len, adp, aoff, \
-                           alen, sc, (const int32_t *)s->thr.p, bound, n);                                    \
+#define C(X)                                                                                                  \
+    case X:                                                                                                   \
+        hipLaunchKernelGGL(k_seed_band<X>, dim3(grid), dim3(256), (size_t)lds, st, task, n_task, s->cap, codes, \
+                           v_off, v_len, adp, lds, aoff, alen, sc, (const int32_t *)s->thr.p, bound, n);      \
         break;
         C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8) C(9) C(10) C(11) C(12) C(13) C(14) C(15)
 #undef C
     }
 }
-}  // namespace
 
-// Middle-scan bounds from seeds. fb_rows[a]: register rows of adapter a's filter bucket (0: the
-// adapter is not filtered). mode: 1 use seeds when the cost model prefers them, 2 whenever they
-// apply. Returns 1 when done, 0 when seeds do not apply (the caller runs the score filter), < 0
-// on error. Done: cands != nullptr receives the filtered pairs whose bound reaches their
-// threshold, as sorted (a << 32 | read) keys (no bound array leaves the device); dcands !=
-// nullptr receives the same keys unordered in device memory (valid until the next call) and
-// n_dcands their count; otherwise s16 (int16, a * n + read) holds every bound (-8192: no seed).
-int bounds(State *s, const void *adps_key, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hlen,
-           int32_t n_adp, const std::vector<int> &fb_rows, const uint8_t *codes, const int64_t *v_off,
-           const int32_t *v_len, int64_t n, const pcabi::Scoring &sc, double threshold, int mode, int16_t *s16,
-           std::vector<int64_t> *cands, const int64_t **dcands, int64_t *n_dcands, hipStream_t st) {
-    if (mode <= 0 || n <= 0) return 0;
-    (void)adps_key;
+// Queue the seeds of one round on `st`: bounds reset, scan, expand, the band classes side by side.
+// n: reads (host upper bound); n_dev: their count on the device (nullptr: n). band_grid: the band
+// launches' grid (0: sized from the host task counts in `tasks`).
+int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const int32_t *v_len, int64_t n,
+                  const int32_t *n_dev, int32_t n_adp, const pcabi::Scoring &sc, const int32_t *tasks, hipStream_t st) {
+    if (s->scan_blocks == 0) {
+        int dev = 0, cus = 0, per_cu = 0;
+        SD_TRY(hipGetDevice(&dev));
+        SD_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_scan, 256, 4 * (size_t)s->a.bits_dw));
+        s->scan_blocks = std::max(1, cus * std::max(1, per_cu));
+    }
+    const int grid = s->scan_blocks;
+    if (s->raw_cap == 0) s->raw_cap = (int64_t)grid * 4096;
+    if (s->cap == 0) s->cap = 1 << 22;
+    if (int rc = s->raw.ensure(sizeof(uint2) * (size_t)s->raw_cap)) return rc;
+    if (int rc = s->rawcnt.ensure(4 * (size_t)grid)) return rc;
+    if (int rc = s->task.ensure(sizeof(int4) * kCls * (size_t)s->cap)) return rc;
+    if (int rc = s->cnt.ensure(4 * (kCls + 2))) return rc;
+    if (int rc = s->bound.ensure(sizeof(int32_t) * (size_t)n * n_adp)) return rc;
+    ScanArgs A = s->a;
+    A.codes = codes;
+    A.v_off = v_off;
+    A.v_len = v_len;
+    A.n = n;
+    A.n_dev = n_dev;
+    A.raw = (uint2 *)s->raw.p;
+    A.slab = (int32_t)std::min<int64_t>(s->raw_cap / grid, INT32_MAX);
+    A.raw_cnt = (int32_t *)s->rawcnt.p;
+    A.cnt = (int32_t *)s->cnt.p;
+    A.flags = A.cnt + kCls;
+    A.task = (int4 *)s->task.p;
+    A.cap = s->cap;
+    SD_TRY(hipMemsetAsync(A.cnt, 0, 4 * (kCls + 2), st));
+    hipLaunchKernelGGL(k_bound_reset, dim3(1024), dim3(256), 0, st, (int32_t *)s->bound.p, n, n_dev, n_adp);
+    hipLaunchKernelGGL(k_seed_scan, dim3(grid), dim3(256), 4 * (size_t)A.bits_dw, st, A);
+    hipLaunchKernelGGL(k_seed_expand, dim3(grid), dim3(256), s->lds_bytes, st, A);
+    SD_TRY(hipGetLastError());
+    unsigned g[kCls];
+    for (int c = 0; c < kCls; ++c)
+        g[c] = tasks ? (unsigned)std::max<int64_t>(1, (std::min<int64_t>(tasks[c], s->cap) + 255) / 256) : kBandGrid;
+    if (!tasks || (tasks[0] && tasks[1])) {   // both classes: side by side (atomicMax into one bound array)
+        if (!s->side) {
+            SD_TRY(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
+            SD_TRY(hipEventCreateWithFlags(&s->fork, hipEventDisableTiming));
+            SD_TRY(hipEventCreateWithFlags(&s->join, hipEventDisableTiming));
+        }
+        SD_TRY(hipEventRecord(s->fork, st));
+        SD_TRY(hipStreamWaitEvent(s->side, s->fork, 0));
+        launch_band(s, s->band[1], 1, codes, v_off, v_len, sc, n, g[1], s->side);
+        launch_band(s, s->band[0], 0, codes, v_off, v_len, sc, n, g[0], st);
+        SD_TRY(hipEventRecord(s->join, s->side));
+        SD_TRY(hipStreamWaitEvent(st, s->join, 0));
+    } else {
+        for (int c = 0; c < kCls; ++c)
+            if (tasks[c]) launch_band(s, s->band[c], c, codes, v_off, v_len, sc, n, g[c], st);
+    }
+    SD_TRY(hipGetLastError());
+    return 0;
+}
+
+// Device -> host: the task counts and the overflow flags (synchronises `st`).
+int read_counts(State *s, int32_t (&out)[kCls + 2], hipStream_t st) {
+    SD_TRY(hipMemcpyAsync(out, s->cnt.p, sizeof(out), hipMemcpyDeviceToHost, st));
+    SD_TRY(hipStreamSynchronize(st));
+    return 0;
+}
+
+// Larger buffers after an overflow; false when they would pass sane limits.
+bool grow(State *s, const int32_t (&c)[kCls + 2]) {
+    if (c[2]) {
+        if (s->raw_cap > (1ll << 31)) return false;
+        s->raw_cap *= 2;
+    }
+    if (c[3]) {
+        int64_t most = std::max<int64_t>(c[0], c[1]);
+        if (most > (1ll << 30)) return false;
+        s->cap = std::max<int64_t>(2 * s->cap, most + most / 4);
+    }
+    return true;
+}
+
+int check_plan(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hlen, int32_t n_adp,
+               const std::vector<int> &fb_rows, const pcabi::Scoring &sc, double threshold, hipStream_t st) {
     bool same = s->planned && s->threshold == threshold && s->sc.ma == sc.ma && s->sc.mi == sc.mi &&
                 s->sc.go == sc.go && s->sc.ge == sc.ge && (int32_t)s->key_len.size() == n_adp && s->key_rows == fb_rows;
     for (int32_t a = 0; same && a < n_adp; ++a) same = s->key_len[a] == hlen[a];
@@ -636,51 +810,47 @@ int bounds(State *s, const void *adps_key, const uint8_t *hcodes, const int32_t 
             return rc;
         }
     }
+    return 0;
+}
+}  // namespace
+
+// Middle-scan bounds from seeds. fb_rows[a]: register rows of adapter a's filter bucket (0: the
+// adapter is not filtered). mode: 1 use seeds when the cost model prefers them, 2 whenever they
+// apply. Returns 1 when done, 0 when seeds do not apply (the caller runs the score filter), < 0
+// on error. Done: cands != nullptr receives the filtered pairs whose bound reaches their
+// threshold, as sorted (a << 32 | read) keys (no bound array leaves the device); dcands !=
+// nullptr receives the same keys unordered in device memory (valid until the next call) and
+// n_dcands their count; otherwise s16 (int16, a * n + read) holds every bound (-8192: no seed).
+int bounds(State *s, const void *adps_key, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hlen,
+           int32_t n_adp, const std::vector<int> &fb_rows, const uint8_t *codes, const int64_t *v_off,
+           const int32_t *v_len, int64_t n, const pcabi::Scoring &sc, double threshold, int mode, int16_t *s16,
+           std::vector<int64_t> *cands, const int64_t **dcands, int64_t *n_dcands, hipStream_t st) {
+    if (mode <= 0 || n <= 0) return 0;
+    (void)adps_key;
+    if (int rc = check_plan(s, hcodes, hoff, hlen, n_adp, fb_rows, sc, threshold, st)) return rc;
     if (!s->ok) return 0;
     if (mode == 1 && !(s->cost_seed < 0.5 * s->cost_filter)) return 0;
-    if (int rc = s->bound.ensure(sizeof(int32_t) * (size_t)n * n_adp)) return rc;
-    ScanArgs A = s->a;
-    A.codes = codes;
-    A.v_off = v_off;
-    A.v_len = v_len;
-    A.n = n;
-    for (int pass = 0; pass < 2; ++pass) {
-        if (s->cap == 0) s->cap = 1 << 20;
-        if (int rc = s->task.ensure(sizeof(int4) * kCls * (size_t)s->cap)) return rc;
-        A.task = (int4 *)s->task.p;
-        A.cap = s->cap;
-        SD_TRY(hipMemsetAsync(A.cnt, 0, 4 * kCls, st));
-        // every block resident at once (the blocks stride over the reads evenly: a second wave
-        // of blocks would run on a partly idle chip)
-        if (s->scan_blocks == 0) {
-            int dev = 0, cus = 0, per_cu = 0;
-            SD_TRY(hipGetDevice(&dev));
-            SD_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-            SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_scan, 256, s->lds_bytes));
-            s->scan_blocks = std::max(1, cus * std::max(1, per_cu));
-        }
-        const unsigned grid = (unsigned)std::min<int64_t>(n, s->scan_blocks);
-        hipLaunchKernelGGL(k_seed_scan, dim3(grid), dim3(256), s->lds_bytes, st, A);
-        SD_TRY(hipGetLastError());
-        int32_t cnt[kCls];
-        SD_TRY(hipMemcpyAsync(cnt, A.cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
-        SD_TRY(hipStreamSynchronize(st));
-        int64_t most = 0;
-        for (int c = 0; c < kCls; ++c) {
-            if (cnt[c] < 0) return fail(PCABI_E_DEVICE, "seed task counter overflow");
-            most = std::max<int64_t>(most, cnt[c]);
-        }
-        if (most > s->cap) {
-            if (pass == 1) return fail(PCABI_E_DEVICE, "seed tasks grew between passes");
-            s->cap = most + most / 4;
-            continue;
-        }
-        if (const char *dbg = std::getenv("PCABI_DEBUG"))
-            if (dbg[0] == '1')
-                std::fprintf(stderr, "[pcabi] seeds: %lld windows, band tasks %d (E=%d) + %d (E=%d), scan grid %u\n",
-                             (long long)n, cnt[0], s->band[0], cnt[1], s->band[1], grid);
-        SD_TRY(hipMemsetD32Async((hipDeviceptr_t)s->bound.p, pcabi::sf::NEG16, (size_t)n * n_adp, st));
-        if (cnt[0] && cnt[1]) {   // both classes: side by side (atomicMax into one bound array)
+    // the scan and the expansion, again with larger buffers after an overflow; then the band
+    // launches sized from the task counts
+    int32_t c[kCls + 2];
+    for (int tries = 0;; ++tries) {
+        int32_t none[kCls] = {0, 0};
+        // scan + expand only: with both counts zero the band kernels are not queued
+        if (int rc = enqueue_seeds(s, codes, v_off, v_len, n, nullptr, n_adp, sc, none, st)) return rc;
+        if (int rc = read_counts(s, c, st)) return rc;
+        if (!c[2] && !c[3]) break;
+        if (tries > 8 || !grow(s, c)) return fail(PCABI_E_DEVICE, "seed scan did not settle");
+    }
+    if (const char *dbg = std::getenv("PCABI_DEBUG"))
+        if (dbg[0] == '1')
+            std::fprintf(stderr, "[pcabi] seeds: %lld windows, band tasks %d (E=%d) + %d (E=%d), scan grid %d\n",
+                         (long long)n, c[0], s->band[0], c[1], s->band[1], s->scan_blocks);
+    {
+        // the band classes from the counted tasks (the tasks are still in place)
+        int32_t tasks[kCls] = {c[0], c[1]};
+        unsigned g[kCls];
+        for (int k = 0; k < kCls; ++k) g[k] = (unsigned)std::max<int64_t>(1, (tasks[k] + 255) / 256);
+        if (tasks[0] && tasks[1]) {
             if (!s->side) {
                 SD_TRY(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
                 SD_TRY(hipEventCreateWithFlags(&s->fork, hipEventDisableTiming));
@@ -688,56 +858,94 @@ int bounds(State *s, const void *adps_key, const uint8_t *hcodes, const int32_t 
             }
             SD_TRY(hipEventRecord(s->fork, st));
             SD_TRY(hipStreamWaitEvent(s->side, s->fork, 0));
-            launch_band(s, s->band[1], cnt[1], 1, codes, v_off, v_len, sc, n, s->side);
-            launch_band(s, s->band[0], cnt[0], 0, codes, v_off, v_len, sc, n, st);
+            launch_band(s, s->band[1], 1, codes, v_off, v_len, sc, n, g[1], s->side);
+            launch_band(s, s->band[0], 0, codes, v_off, v_len, sc, n, g[0], st);
             SD_TRY(hipEventRecord(s->join, s->side));
             SD_TRY(hipStreamWaitEvent(st, s->join, 0));
         } else {
-            for (int c = 0; c < kCls; ++c)
-                if (cnt[c]) launch_band(s, s->band[c], cnt[c], c, codes, v_off, v_len, sc, n, st);
+            for (int k = 0; k < kCls; ++k)
+                if (tasks[k]) launch_band(s, s->band[k], k, codes, v_off, v_len, sc, n, g[k], st);
         }
         SD_TRY(hipGetLastError());
-        const int64_t tot = n * (int64_t)n_adp;
-        const unsigned grid_all = (unsigned)((tot + 255) / 256);
-        if (!cands && !dcands) {
-            hipLaunchKernelGGL(k_bound16, dim3(grid_all), dim3(256), 0, st, (const int32_t *)s->bound.p, tot, s16);
-            SD_TRY(hipGetLastError());
-            g_runs.fetch_add(1);
-            return 1;
-        }
-        for (int cpass = 0; cpass < 2; ++cpass) {
-            if (s->ccap == 0) s->ccap = 1 << 16;
-            if (int rc = s->cands.ensure(sizeof(int64_t) * (size_t)s->ccap)) return rc;
-            SD_TRY(hipMemsetAsync(s->ccnt.p, 0, 8, st));
-            hipLaunchKernelGGL(k_cands, dim3(grid_all), dim3(256), 0, st, (const int32_t *)s->bound.p, n, tot,
-                               (const int32_t *)s->thr.p, (int64_t *)s->cands.p, s->ccap,
-                               (unsigned long long *)s->ccnt.p);
-            SD_TRY(hipGetLastError());
-            unsigned long long nc = 0;
-            SD_TRY(hipMemcpyAsync(&nc, s->ccnt.p, 8, hipMemcpyDeviceToHost, st));
-            SD_TRY(hipStreamSynchronize(st));
-            if ((int64_t)nc > s->ccap) {
-                s->ccap = (int64_t)nc + (int64_t)nc / 4;
-                continue;
-            }
-            if (dcands) {                              // the keys stay on the device, unordered
-                *dcands = (const int64_t *)s->cands.p;
-                *n_dcands = (int64_t)nc;
-                g_runs.fetch_add(1);
-                return 1;
-            }
-            cands->resize((size_t)nc);
-            if (nc) {
-                SD_TRY(hipMemcpyAsync(cands->data(), s->cands.p, sizeof(int64_t) * nc, hipMemcpyDeviceToHost, st));
-                SD_TRY(hipStreamSynchronize(st));
-            }
-            std::sort(cands->begin(), cands->end());
-            g_runs.fetch_add(1);
-            return 1;
-        }
-        return fail(PCABI_E_DEVICE, "seed candidates did not settle");
     }
-    return fail(PCABI_E_DEVICE, "seed scan did not settle");
+    const int64_t tot = n * (int64_t)n_adp;
+    if (!cands && !dcands) {
+        hipLaunchKernelGGL(k_bound16, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, (const int32_t *)s->bound.p,
+                           tot, s16);
+        SD_TRY(hipGetLastError());
+        g_runs.fetch_add(1);
+        return 1;
+    }
+    if (s->ccap < tot) s->ccap = tot;                 // every pair fits: no overflow pass
+    if (int rc = s->cands.ensure(sizeof(int64_t) * (size_t)s->ccap)) return rc;
+    if (int rc = s->ccnt.ensure(8)) return rc;
+    SD_TRY(hipMemsetAsync(s->ccnt.p, 0, 8, st));
+    hipLaunchKernelGGL(k_cands, dim3((unsigned)std::min<int64_t>((tot + 255) / 256, kBandGrid)), dim3(256), 0, st,
+                       (const int32_t *)s->bound.p, n, nullptr, n_adp, (const int32_t *)s->thr.p, (int64_t *)s->cands.p,
+                       s->ccap, (unsigned long long *)s->ccnt.p);
+    SD_TRY(hipGetLastError());
+    unsigned long long nc = 0;
+    SD_TRY(hipMemcpyAsync(&nc, s->ccnt.p, 8, hipMemcpyDeviceToHost, st));
+    SD_TRY(hipStreamSynchronize(st));
+    if (dcands) {                                     // the keys stay on the device, unordered
+        *dcands = (const int64_t *)s->cands.p;
+        *n_dcands = (int64_t)nc;
+        g_runs.fetch_add(1);
+        return 1;
+    }
+    cands->resize((size_t)nc);
+    if (nc) {
+        SD_TRY(hipMemcpyAsync(cands->data(), s->cands.p, sizeof(int64_t) * nc, hipMemcpyDeviceToHost, st));
+        SD_TRY(hipStreamSynchronize(st));
+    }
+    std::sort(cands->begin(), cands->end());
+    g_runs.fetch_add(1);
+    return 1;
+}
+
+// The device-resident form for the engine's queued rounds (no host synchronisation): the plan must
+// be ready (bounds() ran it this call or earlier: s->ok); n_dev is the round's read count on the
+// device, n its host upper bound (the bound array's row stride). Queues bounds reset, scan,
+// expansion, both band classes (grid-stride over the device task counts) and k_cands; the keys
+// (a << 32 | read, unordered) land in *dcands, their count in *dcount (device uint64), and
+// *flags (device int32[2]) is set when a buffer overflowed (the caller reruns the round after
+// grow_after_overflow()).
+int bounds_dev(State *s, const uint8_t *codes, const int64_t *v_off, const int32_t *v_len, int64_t n,
+               const int32_t *n_dev, int32_t n_adp, const pcabi::Scoring &sc, const int64_t **dcands,
+               const unsigned long long **dcount, const int32_t **flags, hipStream_t st) {
+    if (!s->ok) return fail(PCABI_E_ARG, "seed plan not ready");
+    if (int rc = enqueue_seeds(s, codes, v_off, v_len, n, n_dev, n_adp, sc, nullptr, st)) return rc;
+    const int64_t tot = n * (int64_t)n_adp;
+    if (s->ccap < tot) s->ccap = tot;
+    if (int rc = s->cands.ensure(sizeof(int64_t) * (size_t)s->ccap)) return rc;
+    if (int rc = s->ccnt.ensure(8)) return rc;
+    SD_TRY(hipMemsetAsync(s->ccnt.p, 0, 8, st));
+    hipLaunchKernelGGL(k_cands, dim3((unsigned)std::min<int64_t>((tot + 255) / 256, kBandGrid)), dim3(256), 0, st,
+                       (const int32_t *)s->bound.p, n, n_dev, n_adp, (const int32_t *)s->thr.p, (int64_t *)s->cands.p,
+                       s->ccap, (unsigned long long *)s->ccnt.p);
+    SD_TRY(hipGetLastError());
+    *dcands = (const int64_t *)s->cands.p;
+    *dcount = (const unsigned long long *)s->ccnt.p;
+    *flags = (const int32_t *)s->cnt.p + kCls;
+    g_runs.fetch_add(1);
+    return 0;
+}
+
+// After a device-resident run reported an overflow (flags from bounds_dev, read by the caller):
+// larger buffers for the rerun. Returns false past the limits.
+bool grow_after_overflow(State *s, int raw_overflow, int task_overflow) {
+    int32_t c[kCls + 2] = {(int32_t)std::min<int64_t>(4 * s->cap, INT32_MAX), 0, raw_overflow, task_overflow};
+    return grow(s, c);
+}
+
+// the plan for these adapters, without running anything: true when seeds apply (mode as bounds()).
+int plan_ready(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hlen, int32_t n_adp,
+               const std::vector<int> &fb_rows, const pcabi::Scoring &sc, double threshold, int mode, hipStream_t st) {
+    if (mode <= 0) return 0;
+    if (int rc = check_plan(s, hcodes, hoff, hlen, n_adp, fb_rows, sc, threshold, st)) return rc;
+    if (!s->ok) return 0;
+    if (mode == 1 && !(s->cost_seed < 0.5 * s->cost_filter)) return 0;
+    return 1;
 }
 
 }  // namespace pcabi_seed

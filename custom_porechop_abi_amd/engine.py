@@ -51,8 +51,10 @@ class SeqPack(object):
                 parts.append(b'N' * pad)
             pos += n + pad
         parts.append(b'N' * PAD)
-        raw = np.frombuffer(b''.join(parts), dtype=np.uint8)
-        self.codes = np.ascontiguousarray(DNA5[raw])
+        raw = b''.join(parts)
+        self.codes = np.empty(len(raw), dtype=np.uint8)
+        # the S/basic/alphabet_residue_tabs.h table, in C (threads for large batches)
+        lib().pcabi_encode_dna5(raw, self.codes.ctypes.data_as(ctypes.c_void_p), len(raw))
         self.offsets = offs
         self.lengths = lens
 

@@ -207,8 +207,10 @@ def trim_file_sharded(in_path, out_path, out_format='fastq', scoring_scheme_vals
     # however many bases they hold; spread over the files of an Albacore directory
     check = misc.load_check_reads(in_path, check_reads) if check_reads > 0 else []
     dev = rank_device(device)
+    # a fresh copy of the database: the search raises every set's best scores in place (the
+    # reference's main() does that once per process; this function may run many times in one)
     matching = find_matching_adapter_sets(check, 0, end_size, scoring_scheme_vals, io.StringIO(), adapter_threshold, 1,
-                                          group=group, device=dev)
+                                          adapter_sets=_adapters.fresh_adapters(), group=group, device=dev)
     matching = P.fix_up_1d2_sets(matching)
     fwd_rev = P.choose_barcoding_kit(matching, 0, io.StringIO()) if barcode_dir is not None else None
     matching = P.add_full_barcode_adapter_sets(matching)

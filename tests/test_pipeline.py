@@ -312,9 +312,18 @@ def test_albacore_directory_on_gpu(gpu_lib, tmp_path, run):
     finally:
         dist.destroy_process_group()
     assert counts['reads_in'] == 32
+
+    def same(got, want, what):
+        if got == want:
+            return
+        g, w = got.split('\n'), want.split('\n')
+        k = next((i for i, (x, y) in enumerate(zip(g, w)) if x != y), min(len(g), len(w)))
+        ctx = lambda lines: [x[:80] + ('...%d' % len(x) if len(x) > 80 else '') for x in lines[max(0, k - 2):k + 2]]
+        raise AssertionError('%s: %d vs %d lines, first difference at line %d: got %s want %s'
+                             % (what, len(g), len(w), k, ctx(g), ctx(w)))
     if bdir:
         assert sorted(os.listdir(bdir)) == sorted(exp['bins'])
         for name, txt in exp['bins'].items():
-            assert open(os.path.join(bdir, name)).read() == txt, name
+            same(open(os.path.join(bdir, name)).read(), txt, name)
     else:
-        assert open(out_path).read() == exp['output']
+        same(open(out_path).read(), exp['output'], 'output')
