@@ -846,10 +846,11 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
     against the first 50 adapter sets. One step, inputs resident in HBM:
       pristine read pack -> working copy (the scan masks hits in place)
       start/end windows -> tiles -> k_align -> k_end_trim                (as the headline step)
-      trim amounts -> host -> trimmed-read views                         (16 B/read each way)
-      pcabi_middle_scan_dev: round 1 from exact k-mer seeds (k_seed_scan -> banded k_seed_band ->
-      k_cands -> chunked candidate DP), then rounds over the reads that just hit, masked, until
-      none hits
+      pcabi_trim_views_dev: trimmed-read views on the device (no host round trip)
+      pcabi_middle_scan_dev: queued rounds on the device -- round 1 from exact k-mer
+      seeds (k_seed_scan -> k_seed_expand -> banded k_seed_band -> k_cands -> device plan ->
+      chunked candidate DP -> merges), then rounds over the reads that just hit, masked, until
+      none hits; the host reads the round counts once per three rounds
     value = reads / step time (all ranks, max over ranks). Also the default bench's 'middle'
     sub-record (N = 1), with the oracle loop over the first --middle-check reads."""
     from custom_porechop_abi_amd.porechop_abi import middle_adapter_list
@@ -900,6 +901,9 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
     d_toff_mid, d_tlen_mid = dalloc(8 * n), dalloc(4 * n)
     stream = vp()
     _lib.check(L.pcabi_stream_create(ctypes.byref(stream)), 'stream')
+    ev = [vp(), vp()]
+    for e in ev:
+        _lib.check(L.pcabi_event_create(ctypes.byref(e)), 'event')
     sc = SCORING
     sides = []
     for w_off, w_len, adps, d_res in ((s_off, s_len, start_adps, d_sres), (e_off, e_len, end_adps, d_eres)):
@@ -914,7 +918,6 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
     cap = max(4096, n)
     hits = np.zeros((6, cap), np.int32)
     trims = np.zeros((2, n), np.int32)
-    t_off = np.zeros(n, np.int64)
     t_len = np.zeros(n, np.int32)
     stats = {}
 
@@ -927,21 +930,19 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
                                                sd['d_res'], sd['stride'], stream), 'align')
         _lib.check(L.pcabi_end_trim_dev(d_sres, n_sa * n, n_sa, d_eres, n_ea * n, n_ea, n, E, 2, 75.0, 4, d_st, d_et,
                                         None, None, stream), 'end_trim')
-        _lib.check(L.pcabi_dev_copy_async(trims[0].ctypes.data_as(vp), d_st, 4 * n, 1, stream), 'd2h')
-        _lib.check(L.pcabi_dev_copy_async(trims[1].ctypes.data_as(vp), d_et, 4 * n, 1, stream), 'd2h')
-        _lib.check(L.pcabi_stream_sync(stream), 'sync')
-        t1 = time.perf_counter()
-        # NanoporeRead.get_seq_with_start_end_adapters_trimmed (nanopore_read.py:44-49)
-        np.add(offs, trims[0], out=t_off)
-        np.maximum(lens - trims[0] - trims[1], 0, out=t_len, casting='unsafe')
-        _lib.check(L.pcabi_dev_copy_async(d_toff_mid, t_off.ctypes.data_as(vp), 8 * n, 0, stream), 'h2d')
-        _lib.check(L.pcabi_dev_copy_async(d_tlen_mid, t_len.ctypes.data_as(vp), 4 * n, 0, stream), 'h2d')
-        nh = L.pcabi_middle_scan_dev(scan, d_work, d_toff_mid, d_tlen_mid, t_len.ctypes.data_as(vp), n, *sc,
+        _lib.check(L.pcabi_event_record(ev[0], stream), 'event')
+        # NanoporeRead.get_seq_with_start_end_adapters_trimmed (nanopore_read.py:44-49), on the device
+        _lib.check(L.pcabi_trim_views_dev(d_offs, d_lens, d_st, d_et, n, d_toff_mid, d_tlen_mid, stream), 'views')
+        nh = L.pcabi_middle_scan_dev(scan, d_work, d_toff_mid, d_tlen_mid, None, n, *sc,
                                      args.middle_threshold, hits.ctypes.data_as(vp), cap, stream)
         if nh < 0:
             _lib.check(int(nh), 'middle_scan')
+        _lib.check(L.pcabi_event_record(ev[1], stream), 'event')
+        _lib.check(L.pcabi_stream_sync(stream), 'sync')
+        ms = ctypes.c_float()
+        _lib.check(L.pcabi_event_elapsed_ms(ctypes.byref(ms), ev[0], ev[1]), 'elapsed')
         stats['hits'] = int(nh)
-        stats['middle_s'] = stats.get('middle_s', 0.0) + time.perf_counter() - t1
+        stats['middle_s'] = stats.get('middle_s', 0.0) + 1e-3 * ms.value
 
     for _ in range(args.warmup):
         step()
@@ -961,6 +962,11 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
         t = torch.tensor([elapsed], dtype=torch.float64, device='cuda' if args.dist_backend == 'nccl' else 'cpu')
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # the last step's trims and views, for the checks and the cell counts (after the timed region)
+    _lib.check(L.pcabi_dev_copy_async(trims[0].ctypes.data_as(vp), d_st, 4 * n, 1, stream), 'd2h')
+    _lib.check(L.pcabi_dev_copy_async(trims[1].ctypes.data_as(vp), d_et, 4 * n, 1, stream), 'd2h')
+    _lib.check(L.pcabi_dev_copy_async(t_len.ctypes.data_as(vp), d_tlen_mid, 4 * n, 1, stream), 'd2h')
+    _lib.check(L.pcabi_stream_sync(stream), 'sync')
 
     checked = None
     if args.check and rank == 0:

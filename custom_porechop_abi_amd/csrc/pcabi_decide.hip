@@ -89,42 +89,3 @@ extern "C" int pcabi_flag_list_dev(const uint8_t *flag, int32_t n_adp, int64_t n
     HIP_TRY(hipFreeAsync(buf, st));
     return rc;
 }
-
-// ---- the middle scan's round-1 order on the device -------------------------------------------------
-namespace pcabi_eng {
-namespace {
-__global__ __launch_bounds__(256) void k_iota_keys(const int32_t *len, int64_t n, uint32_t *key, int32_t *idx) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    key[i] = (uint32_t)max(len[i], 0);
-    idx[i] = (int32_t)i;
-}
-}  // namespace
-
-// order[0 .. n) = the windows longest first, ties in window order (a stable radix sort of the
-// lengths, descending): round 1 of the middle scan visits the reads so, and a wave's lanes then run
-// near-equal column counts. tmp: scratch of at least sort_by_length_bytes(n) bytes. Async.
-size_t sort_by_length_bytes(int64_t n) {
-    size_t t = 0;
-    (void)hipcub::DeviceRadixSort::SortPairsDescending(nullptr, t, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                                       (int32_t *)nullptr, (int32_t *)nullptr, (int)std::max<int64_t>(n, 1),
-                                                       0, 32);
-    const size_t a = (4 * (size_t)std::max<int64_t>(n, 1) + 255) & ~(size_t)255;
-    return 3 * a + t + 256;
-}
-
-int sort_by_length(const int32_t *len, int64_t n, int32_t *order, void *tmp, hipStream_t st) {
-    if (n <= 0) return 0;
-    if (n >= (1ll << 31)) return fail(PCABI_E_ARG, "too many windows");
-    const size_t a = (4 * (size_t)n + 255) & ~(size_t)255;
-    char *b = (char *)tmp;
-    uint32_t *key = (uint32_t *)b, *key2 = (uint32_t *)(b + a);
-    int32_t *idx = (int32_t *)(b + 2 * a);
-    size_t t = 0;
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, t, key, key2, idx, order, (int)n, 0, 32, st));
-    hipLaunchKernelGGL(k_iota_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, len, n, key, idx);
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(b + 3 * a, t, key, key2, idx, order, (int)n, 0, 32, st));
-    HIP_TRY(hipGetLastError());
-    return 0;
-}
-}  // namespace pcabi_eng

@@ -17,6 +17,7 @@
 //                               (nanopore_read.py:219-252).
 //   k_tile_windows              window list -> tile layout (coalesced cross-mode reads).
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstdio>
@@ -496,9 +497,22 @@ __global__ __launch_bounds__(256) void k_hits_compact(const int32_t *hb, int64_t
 // ---- queued middle-scan rounds (middle_device_rounds): the kernels between the seeded plan's ------
 // steps, every count read on the device
 
-// views of this round's windows: sub[k] = window cur[k], k < n_dev
+// Start of a round: views of its windows (sub[k] = window cur[k], k < n_dev; cur == nullptr: none,
+// round 1 reads the windows themselves) and the round's counters zeroed -- the next round's read
+// count, the plan flag, the plan's per-adapter task counts (n_adp x kPlanC) and fill counters.
 __global__ __launch_bounds__(256) void k_round_views(const int64_t *win_off, const int32_t *win_len, const int32_t *cur,
-                                                     const int32_t *n_dev, int64_t *sub_off, int32_t *sub_len) {
+                                                     const int32_t *n_dev, int64_t *sub_off, int32_t *sub_len,
+                                                     int32_t *n_next, int32_t *plan_flag, int32_t *ptasks,
+                                                     int32_t *pfill, int32_t n_adp) {
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) {
+            *n_next = 0;
+            *plan_flag = 0;
+        }
+        for (int i = threadIdx.x; i < n_adp * kPlanC; i += 256) ptasks[i] = 0;
+        for (int i = threadIdx.x; i < n_adp; i += 256) pfill[i] = 0;
+    }
+    if (!cur) return;
     const int64_t n = *n_dev;
     for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256) {
         sub_off[k] = win_off[cur[k]];
@@ -506,9 +520,16 @@ __global__ __launch_bounds__(256) void k_round_views(const int64_t *win_off, con
     }
 }
 
-__global__ __launch_bounds__(256) void k_zero_u64(unsigned long long *p, const unsigned long long *n_dev, int64_t cap) {
-    const int64_t n = min((int64_t)*n_dev, cap);
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = 0ull;
+// Before the merges: the candidates' best keys zeroed (k < *n_cand), the round's per-window hit
+// adapter (INT32_MAX) and hit table row 0 (-1) reset (k < *n_dev).
+__global__ __launch_bounds__(256) void k_merge_reset(unsigned long long *best, const unsigned long long *n_cand, int64_t cap,
+                                                     int32_t *hit_a, int32_t *hb, const int32_t *n_dev) {
+    const int64_t nc = min((int64_t)*n_cand, cap), nr = *n_dev;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nc; i += (int64_t)gridDim.x * 256) best[i] = 0ull;
+    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < nr; k += (int64_t)gridDim.x * 256) {
+        hit_a[k] = INT32_MAX;
+        hb[k] = -1;
+    }
 }
 
 // The device plan's layout (device_plan_hits' host part, on the device, one block): per bucket
@@ -523,56 +544,82 @@ __global__ __launch_bounds__(256) void k_plan_layout(const int32_t *tasks, int32
                                                      int64_t slots_cap, int32_t *cidx, int64_t *woff, int32_t *wa,
                                                      int32_t *tw, int32_t *bk_waves, int64_t *slots_total,
                                                      int32_t *flag, int64_t *need) {
-    __shared__ unsigned long long s_w[kPlanC];
-    __shared__ int64_t s_base;
-    if (threadIdx.x == 0) s_base = 0;
-    for (int32_t b = 0; b < n_bk; ++b) {
-        if (threadIdx.x < kPlanC) s_w[threadIdx.x] = 0;
-        __syncthreads();
-        for (int32_t j = bk_first[b] + threadIdx.x; j < bk_first[b + 1]; j += 256) {
-            const int32_t a = bk_adp[j];
+    typedef hipcub::BlockScan<long long, 256> Scan;
+    __shared__ typename Scan::TempStorage scan_tmp;
+    __shared__ unsigned long long s_w[kNumBuckets][kPlanC];
+    __shared__ int s_bc[kNumBuckets];
+    __shared__ long long s_carry;
+    const int32_t n_all = bk_first[n_bk];
+    for (int i = threadIdx.x; i < kNumBuckets * kPlanC; i += 256) s_w[i / kPlanC][i % kPlanC] = 0;
+    if (threadIdx.x == 0) s_carry = 0;
+    __syncthreads();
+    auto bucket_of = [&](int32_t j) {
+        int32_t b = 0;
+        while (b + 1 < n_bk && bk_first[b + 1] <= j) ++b;
+        return b;
+    };
+    // per bucket the waves of each chunk length; the longest length whose waves reach the target
+    for (int32_t j = threadIdx.x; j < n_all; j += 256) {
+        const int32_t a = bk_adp[j], b = bucket_of(j);
 #pragma unroll
-            for (int c = 1; c < kPlanC; ++c) atomicAdd(&s_w[c], (unsigned long long)((tasks[a * kPlanC + c] + 63) / 64));
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int bc = 0;
-            for (int c = kPlanC - 1; c > 0; --c)
-                if ((int64_t)s_w[c] >= target) {
-                    bc = c;
-                    break;
-                }
-            int64_t w = s_base;
-            const int64_t w0 = w;
-            for (int32_t j = bk_first[b]; j < bk_first[b + 1]; ++j) {
-                const int32_t a = bk_adp[j];
-                woff[a] = w;
-                cidx[a] = bc;
-                w += (tasks[a * kPlanC + bc] + 63) / 64;
+        for (int c = 1; c < kPlanC; ++c) atomicAdd(&s_w[b][c], (unsigned long long)((tasks[a * kPlanC + c] + 63) / 64));
+    }
+    __syncthreads();
+    for (int32_t b = threadIdx.x; b < n_bk; b += 256) {
+        int bc = 0;
+        for (int c = kPlanC - 1; c > 0; --c)
+            if ((int64_t)s_w[b][c] >= target) {
+                bc = c;
+                break;
             }
-            bk_waves[2 * b] = (int32_t)w0;
-            bk_waves[2 * b + 1] = (int32_t)(w - w0);
-            s_base = w;
+        s_bc[b] = bc;
+    }
+    __syncthreads();
+    // wave offsets: an exclusive scan over the adapters (buckets in order, a bucket's in order)
+    for (int32_t j0 = 0; j0 < n_all; j0 += 256) {      // block-uniform
+        const int32_t j = j0 + threadIdx.x;
+        long long w = 0;
+        int32_t a = -1, b = 0;
+        if (j < n_all) {
+            a = bk_adp[j];
+            b = bucket_of(j);
+            cidx[a] = s_bc[b];
+            w = (tasks[a * kPlanC + s_bc[b]] + 63) / 64;
         }
+        long long ex, tot;
+        Scan(scan_tmp).ExclusiveSum(w, ex, tot);
+        ex += s_carry;
+        if (a >= 0) woff[a] = ex;
+        __syncthreads();
+        if (threadIdx.x == 0) s_carry += tot;
         __syncthreads();
     }
-    const int64_t slots = s_base * 64;
+    const int64_t slots = s_carry * 64;
+    for (int32_t b = threadIdx.x; b < n_bk; b += 256) {
+        const int64_t lo = bk_first[b] < n_all ? woff[bk_adp[bk_first[b]]] : s_carry;
+        const int64_t hi = bk_first[b + 1] < n_all ? woff[bk_adp[bk_first[b + 1]]] : s_carry;
+        bk_waves[2 * b] = (int32_t)lo;
+        bk_waves[2 * b + 1] = slots > slots_cap ? 0 : (int32_t)(hi - lo);
+    }
     if (slots > slots_cap) {                         // too small: no waves, the round reruns larger
         if (threadIdx.x == 0) {
             *flag = 1;
             *need = slots;
             *slots_total = 0;
         }
-        for (int32_t b = threadIdx.x; b < n_bk; b += 256) bk_waves[2 * b + 1] = 0;
         return;
     }
     if (threadIdx.x == 0) *slots_total = slots;
-    for (int32_t j = 0; j < bk_first[n_bk]; ++j) {  // uniform
+    // the wave -> bucket-local adapter table and the idle lanes of every adapter's last wave: one
+    // wave per adapter
+    const int lane = threadIdx.x & 63;
+    for (int32_t j = threadIdx.x >> 6; j < n_all; j += 4) {
         const int32_t a = bk_adp[j];
         const int32_t nt = tasks[a * kPlanC + cidx[a]];
         const int64_t nw = (nt + 63) / 64, w0 = woff[a];
-        for (int64_t w = threadIdx.x; w < nw; w += 256) wa[w0 + w] = bk_local[j];
-        for (int64_t t = nt + threadIdx.x; t < nw * 64; t += 256) tw[w0 * 64 + t] = -1;
+        for (int64_t w = lane; w < nw; w += 64) wa[w0 + w] = bk_local[j];
+        const int64_t t = nt + lane;
+        if (t < nw * 64) tw[w0 * 64 + t] = -1;
     }
 }
 
@@ -592,7 +639,7 @@ __global__ __launch_bounds__(256) void k_round_hits(const int32_t *hb, int64_t n
         const int32_t a = hb[k];
         if (a < 0) continue;
         const int32_t j = atomicAdd(n_next, 1);
-        const int32_t r = cur[k];
+        const int32_t r = cur ? cur[k] : (int32_t)k;
         int32_t *o = list + 8 * (int64_t)j;
         o[0] = r;
         o[1] = a;
@@ -617,6 +664,19 @@ __global__ __launch_bounds__(256) void k_mask_list(uint8_t *codes, const int64_t
         const int32_t rs = o[2], rend = rs == -1 ? 0 : o[3] + 1;
         const int64_t base = win_off[o[0]];
         for (int64_t i = rs + threadIdx.x; i < rend; i += 256) codes[base + i] = 4;
+    }
+}
+
+// The reads with their end adapters trimmed (nanopore_read.py:44-49,
+// get_seq_with_start_end_adapters_trimmed): view = [start_trim, len - end_trim), empty when the
+// trims meet.
+__global__ __launch_bounds__(256) void k_trim_views(const int64_t *read_off, const int32_t *read_len,
+                                                    const int32_t *start_trim, const int32_t *end_trim, int64_t n,
+                                                    int64_t *view_off, int32_t *view_len) {
+    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256) {
+        const int32_t st = start_trim[k];
+        view_off[k] = read_off[k] + st;
+        view_len[k] = max(read_len[k] - st - end_trim[k], 0);
     }
 }
 
@@ -875,6 +935,7 @@ int bounds_dev(State *s, const uint8_t *codes, const int64_t *v_off, const int32
                const int32_t *n_dev, int32_t n_adp, const pcabi::Scoring &sc, const int64_t **dcands,
                const unsigned long long **dcount, const int32_t **flags, hipStream_t st);
 bool grow_after_overflow(State *s, int raw_overflow, int task_overflow);
+int debug_counts(State *s, int64_t (&out)[3], hipStream_t st);
 }  // namespace pcabi_seed
 
 struct pcabi_scan {
@@ -885,7 +946,7 @@ struct pcabi_scan {
     pcabi_seed::State *seed = nullptr; // seeded round-1 bounds (pcabi_seed.hip)
     // queued rounds (middle_device_rounds): per round slot the reads, their start adapters and the
     // hit list; round counts and flags; the plan's bucket tables and scratch
-    DeviceBuf q_cur, q_start, q_list, q_n, q_flags, q_sort, q_bk, q_wave, q_misc;
+    DeviceBuf q_cur, q_start, q_list, q_n, q_flags, q_bk, q_wave, q_misc;
     int64_t q_slots_cap = 0;
 };
 
@@ -1682,7 +1743,7 @@ void pcabi_scan_destroy(pcabi_scan *s) {
     for (DeviceBuf *b : {&s->tiles, &s->toff, &s->res, &s->hits, &s->idx, &s->start, &s->soff, &s->slen,
                          &s->mwin, &s->ms, &s->me, &s->s16, &s->tw, &s->to, &s->wa, &s->pres, &s->tck,
                          &s->pspan, &s->ptasks, &s->pfill, &s->pwoff, &s->pcidx, &s->pcand, &s->pbest, &s->phit, &s->phb,
-                         &s->plist, &s->pcnt, &s->q_cur, &s->q_start, &s->q_list, &s->q_n, &s->q_flags, &s->q_sort,
+                         &s->plist, &s->pcnt, &s->q_cur, &s->q_start, &s->q_list, &s->q_n, &s->q_flags,
                          &s->q_bk, &s->q_wave, &s->q_misc})
         if (b->p) (void)hipFree(b->p);
     if (s->seed) pcabi_seed::destroy(s->seed);
@@ -2251,7 +2312,6 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
     if (int rc = sc->q_list.ensure(4 * 8 * (size_t)n * kSlots)) return rc;
     if (int rc = sc->q_n.ensure(4 * (kSlots + 2))) return rc;
     if (int rc = sc->q_flags.ensure(4 * (kSlots + 2))) return rc;
-    if (int rc = sc->q_sort.ensure(sort_by_length_bytes(n))) return rc;
     if (int rc = sc->soff.ensure(sizeof(int64_t) * n)) return rc;
     if (int rc = sc->slen.ensure(sizeof(int32_t) * n)) return rc;
     if (int rc = sc->pspan.ensure(sizeof(int32_t) * n_adp)) return rc;
@@ -2277,8 +2337,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
     auto cur_of = [&](int slot) { return (int32_t *)sc->q_cur.p + (int64_t)slot * n; };
     auto start_of = [&](int slot) { return (int32_t *)sc->q_start.p + (int64_t)slot * n; };
     auto list_of = [&](int slot) { return (int32_t *)sc->q_list.p + (int64_t)slot * 8 * n; };
-    // round 1: every window, longest first
-    if (int rc = sort_by_length(win_len, n, cur_of(0), sc->q_sort.p, st)) return rc;
+    // round 1: every window (in window order: a round's results do not depend on its order)
     {
         const int32_t n32 = (int32_t)n;
         HIP_TRY(hipMemcpyAsync(d_n, &n32, 4, hipMemcpyHostToDevice, st));
@@ -2301,21 +2360,20 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
         if (int rc = sc->wa.ensure(sizeof(int32_t) * (slots_cap / 64 + 1))) return rc;
         if (int rc = sc->pres.ensure(sizeof(int32_t) * PCABI_NFIELDS * (size_t)slots_cap)) return rc;
         const int32_t *nr = d_n + r;
-        const int32_t *start = r == 0 && round_base == 0 ? nullptr : start_of(r);
-        HIP_TRY(hipMemsetAsync(d_n + r + 1, 0, 4, st));
-        HIP_TRY(hipMemsetAsync(d_pflag, 0, 4, st));
-        hipLaunchKernelGGL(k_round_views, dim3(gn), dim3(256), 0, st, win_off, win_len, cur_of(r), nr,
-                           (int64_t *)sc->soff.p, (int32_t *)sc->slen.p);
+        const bool first = r == 0 && round_base == 0;  // round 1: the windows themselves
+        const int32_t *start = first ? nullptr : start_of(r);
+        const int32_t *cur = first ? nullptr : cur_of(r);
+        hipLaunchKernelGGL(k_round_views, dim3(first ? 1 : gn), dim3(256), 0, st, win_off, win_len, cur, nr,
+                           (int64_t *)sc->soff.p, (int32_t *)sc->slen.p, d_n + r + 1, d_pflag, (int32_t *)sc->ptasks.p,
+                           (int32_t *)sc->pfill.p, n_adp);
         const int64_t *dcand = nullptr;
         const unsigned long long *dcount = nullptr;
         const int32_t *sflags = nullptr;
-        const int64_t *v_off = (const int64_t *)sc->soff.p;
-        const int32_t *v_len = (const int32_t *)sc->slen.p;
+        const int64_t *v_off = first ? win_off : (const int64_t *)sc->soff.p;
+        const int32_t *v_len = first ? win_len : (const int32_t *)sc->slen.p;
         if (int rc = pcabi_seed::bounds_dev(sc->seed, codes, v_off, v_len, n, nr, n_adp, scr, &dcand, &dcount, &sflags, st))
             return rc;
         const int64_t ncap = n * (int64_t)n_adp;
-        HIP_TRY(hipMemsetAsync(sc->ptasks.p, 0, sizeof(int32_t) * n_adp * kPlanC, st));
-        HIP_TRY(hipMemsetAsync(sc->pfill.p, 0, sizeof(int32_t) * n_adp, st));
         hipLaunchKernelGGL(k_plan_count, dim3(kGrid), dim3(256), 0, st, dcand, ncap, dcount, v_len, start,
                            (const int32_t *)sc->pspan.p, (int32_t *)sc->ptasks.p);
         hipLaunchKernelGGL(k_plan_layout, dim3(1), dim3(256), 0, st, (const int32_t *)sc->ptasks.p, n_bk, d_bk_first,
@@ -2361,19 +2419,29 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
         const int32_t *tw = (const int32_t *)sc->tw.p, *tcand = (const int32_t *)sc->pcand.p;
         const int4 *tck = (const int4 *)sc->tck.p;
         const int32_t *res = (const int32_t *)sc->pres.p;
-        hipLaunchKernelGGL(k_zero_u64, dim3(kGrid), dim3(256), 0, st, (unsigned long long *)sc->pbest.p, dcount, ncap);
-        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)sc->phit.p, INT32_MAX, (size_t)n, st));
-        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)sc->phb.p, -1, (size_t)n, st));
+        hipLaunchKernelGGL(k_merge_reset, dim3(kGrid), dim3(256), 0, st, (unsigned long long *)sc->pbest.p, dcount, ncap,
+                           (int32_t *)sc->phit.p, (int32_t *)sc->phb.p, nr);
         hipLaunchKernelGGL(k_merge_best, dim3(kGrid), dim3(256), 0, st, tw, tck, tcand, res, slots_cap,
                            (const int64_t *)d_slots, (unsigned long long *)sc->pbest.p);
         for (int pass = 0; pass < 2; ++pass)
             hipLaunchKernelGGL(k_merge_hit, dim3(kGrid), dim3(256), 0, st, dcand, tw, tck, tcand, res, slots_cap,
                                (const int64_t *)d_slots, (const unsigned long long *)sc->pbest.p, threshold, pass,
                                (int32_t *)sc->phit.p, (int32_t *)sc->phb.p, n);
-        hipLaunchKernelGGL(k_round_hits, dim3(gn), dim3(256), 0, st, (const int32_t *)sc->phb.p, n, nr, cur_of(r),
+        hipLaunchKernelGGL(k_round_hits, dim3(gn), dim3(256), 0, st, (const int32_t *)sc->phb.p, n, nr, cur,
                            list_of(r), d_n + r + 1, cur_of(r + 1), start_of(r + 1), sflags, d_pflag, d_rflag + r);
         hipLaunchKernelGGL(k_mask_list, dim3(1024), dim3(256), 0, st, codes, win_off, list_of(r), d_n + r + 1);
         HIP_TRY(hipGetLastError());
+        if (g_debug) {                               // debugging only: a synchronisation per round
+            int64_t c[3];
+            if (int rc = pcabi_seed::debug_counts(sc->seed, c, st)) return rc;
+            int32_t rn[2];
+            int64_t sl = 0;
+            HIP_TRY(hipMemcpy(rn, d_n + r, 8, hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(&sl, d_slots, 8, hipMemcpyDeviceToHost));
+            std::fprintf(stderr, "[pcabi] middle round %lld: %d reads, band tasks %lld + %lld, %lld candidates, "
+                         "%lld task slots, %d hits\n", (long long)(round_base + r), rn[0], (long long)c[0],
+                         (long long)c[1], (long long)c[2], (long long)sl, rn[1]);
+        }
         return 0;
     };
     std::vector<int32_t> h_n(kSlots + 2), h_flag(kSlots + 2);
@@ -2685,6 +2753,16 @@ int pcabi_end_trim_dev(const int32_t *start_res, int64_t start_stride, int32_t n
     hipLaunchKernelGGL(k_end_trim, dim3(blocks), dim3(256), 0, (hipStream_t)stream, start_res, start_stride,
                        n_sa, end_res, end_stride, n_ea, n_read, end_size, extra_trim, end_threshold,
                        min_trim_size, start_trim, end_trim, start_hit, end_hit);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int pcabi_trim_views_dev(const int64_t *read_off, const int32_t *read_len, const int32_t *start_trim,
+                         const int32_t *end_trim, int64_t n_read, int64_t *view_off, int32_t *view_len, void *stream) {
+    if (n_read < 0) return fail(PCABI_E_ARG, "bad read count");
+    if (n_read == 0) return 0;
+    hipLaunchKernelGGL(k_trim_views, dim3((unsigned)std::min<int64_t>((n_read + 255) / 256, 4096)), dim3(256), 0,
+                       (hipStream_t)stream, read_off, read_len, start_trim, end_trim, n_read, view_off, view_len);
     HIP_TRY(hipGetLastError());
     return 0;
 }

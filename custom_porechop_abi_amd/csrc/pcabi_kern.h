@@ -520,8 +520,5 @@ int dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st);
 void dispatch_filter(int rpl, const FParams &p, bool affine, hipStream_t st);
 // the striped bucket (k_align_striped): p.rt, p.max_cols set by the caller
 int launch_striped(KParams p, bool affine, hipStream_t st);
-// pcabi_decide.hip: window order longest first (stable), scratch size and the async sort
-size_t sort_by_length_bytes(int64_t n);
-int sort_by_length(const int32_t *len, int64_t n, int32_t *order, void *tmp, hipStream_t st);
 
 }  // namespace pcabi_eng

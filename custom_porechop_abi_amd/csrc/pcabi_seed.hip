@@ -103,8 +103,10 @@ struct ScanArgs {
     int32_t min_k;              // shortest probe
     int32_t rank_off, estart_off, ent_off;   // dword offsets of the other sections
                                              // (entries: adapter << 9 | band class << 8 | offset)
-    uint2 *raw;                 // per scan block a slab of raw hits (read, position | kSlowBit)
+    uint4 *raw;                 // per scan block a slab of raw hits (read, position | kSlowBit,
+                                // 8-mer code | valid run << 16, 0): the expansion reads no read bytes
     int32_t slab;
+    int32_t n_slab;             // slabs (scan blocks); the expansion's blocks stride over them
     int32_t *raw_cnt;           // raw hits per slab
     int32_t *flags;             // [0] a slab overflowed, [1] a task region overflowed
     int4 *task;                 // kCls regions of cap tasks: (read, adapter, diagonal, 0)
@@ -123,69 +125,79 @@ __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
     if (threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
     const int64_t nr = dev_count(a.n_dev, a.n);
-    uint2 *slab = a.raw + (int64_t)blockIdx.x * a.slab;
-    // The block walks its reads (blockIdx.x, + gridDim.x, ...) 4096 positions at a time; the
-    // bytes of the next step (and the next read's length / offset) are loaded before the current
-    // step is processed, so the global latency hides behind the lookups.
+    uint4 *slab = a.raw + (int64_t)blockIdx.x * a.slab;
+    // The block walks its reads (blockIdx.x, + gridDim.x, ...) kSub x 2048 positions at a time;
+    // the bytes of the next step and the next read's length / offset are loaded before the current
+    // step is processed, so the global latency hides behind the lookups. No branch waits on a
+    // length: an empty read is one step of N (no hits), not a loop that stalls every read switch.
+    // (the next read's offset stays a raw loaded value until the switch: using it earlier would
+    // wait for the load)
     int64_t k = blockIdx.x, nk = k;
     int len = 0, nlen = 0;
-    const uint8_t *base = a.codes, *nbase = a.codes;
-    auto next_read = [&](int64_t from, int &ln, const uint8_t *&bs) -> int64_t {
-        for (; from < nr; from += gridDim.x) {
+    int64_t noff = 0;
+    const uint8_t *base = a.codes;
+    auto next_read = [&](int64_t from, int &ln, int64_t &off) -> int64_t {
+        ln = 0;
+        off = 0;
+        if (from < nr) {
             ln = a.v_len[from];
-            if (ln > 0) {
-                bs = a.codes + a.v_off[from];
-                return from;
-            }
+            off = a.v_off[from];
         }
         return from;
     };
-    auto fetch = [&](const uint8_t *bs, int ln, int p0b, uint32_t (&w)[kNW]) {
+    // A lane's 16 bases p0 .. p0 + 15 come from five aligned dwords (past the read they stay inside
+    // the caller's >= 16 B tail padding); the loads land in d[] and are only aligned (alignbyte by
+    // al) when the step is processed, so they stay in flight behind the current step's lookups.
+    auto fetch = [&](const uint8_t *bs, int ln, int p0b, uint32_t (&d)[kNW + 1], int &al) {
         const int p0 = p0b + kPos * (int)threadIdx.x;
+        al = 0;
 #pragma unroll
-        for (int d = 0; d < kNW; ++d) w[d] = 0x04040404u;
-        if (p0 < ln) {   // bytes p0 .. p0 + 15 from five aligned dwords; past the read they stay
-                         // inside the caller's >= 16 B tail padding (dword-aligned loads)
+        for (int t = 0; t <= kNW; ++t) d[t] = 0x04040404u;
+        if (p0 < ln) {
             const uint8_t *ad = bs + p0;
-            const int a0 = (int)((uintptr_t)ad & 3);
-            const uint32_t *q = reinterpret_cast<const uint32_t *>(ad - a0);
-            uint32_t d[kNW + 1];
+            al = (int)((uintptr_t)ad & 3);
+            const uint32_t *q = reinterpret_cast<const uint32_t *>(ad - al);
 #pragma unroll
             for (int t = 0; t <= kNW; ++t) d[t] = q[t];
-#pragma unroll
-            for (int t = 0; t < kNW; ++t) w[t] = __builtin_amdgcn_alignbyte(d[t + 1], d[t], a0);
         }
     };
-    k = next_read(k, len, base);
-    if (k < nr) nk = next_read(k + gridDim.x, nlen, nbase);
+    k = next_read(k, len, noff);
+    base = a.codes + noff;
+    if (k < nr) nk = next_read(k + gridDim.x, nlen, noff);
     int p0b = 0;
-    uint32_t wn[kSub][kNW];
+    uint32_t wn[kSub][kNW + 1];
+    int an[kSub];
 #pragma unroll
     for (int h = 0; h < kSub; ++h)
-        if (k < nr) fetch(base, len, h * 256 * kPos, wn[h]);
+        if (k < nr) fetch(base, len, h * 256 * kPos, wn[h], an[h]);
     while (k < nr) {                                   // block-uniform
         const int64_t ck = k;
         const int clen = len, cp0b = p0b;
-        uint32_t wc[kSub][kNW];
+        uint32_t wc[kSub][kNW + 1];
+        int ac[kSub];
 #pragma unroll
-        for (int h = 0; h < kSub; ++h)
+        for (int h = 0; h < kSub; ++h) {
+            ac[h] = an[h];
 #pragma unroll
-            for (int d = 0; d < kNW; ++d) wc[h][d] = wn[h][d];
+            for (int d = 0; d <= kNW; ++d) wc[h][d] = wn[h][d];
+        }
         p0b += kSub * 256 * kPos;
         if (p0b >= len) {                              // on to the next read
             k = nk;
             len = nlen;
-            base = nbase;
+            base = a.codes + noff;
             p0b = 0;
-            if (k < nr) nk = next_read(k + gridDim.x, nlen, nbase);
+            if (k < nr) nk = next_read(k + gridDim.x, nlen, noff);
         }
 #pragma unroll
         for (int h = 0; h < kSub; ++h)
-            if (k < nr) fetch(base, len, p0b + h * 256 * kPos, wn[h]);
+            if (k < nr) fetch(base, len, p0b + h * 256 * kPos, wn[h], an[h]);
 #pragma unroll
         for (int h = 0; h < kSub; ++h) {
             const int cp0 = cp0b + h * 256 * kPos + kPos * (int)threadIdx.x;
-            const uint32_t *w = wc[h];
+            uint32_t w[kNW];
+#pragma unroll
+            for (int t = 0; t < kNW; ++t) w[t] = __builtin_amdgcn_alignbyte(wc[h][t + 1], wc[h][t], ac[h]);
             // 16 bases (SWAR): c32 = their 2-bit codes, first base in the top bits; vmask bit t =
             // base t is A/C/G/T inside the read (Dna5 codes are 0..4: N has bit 2)
             uint32_t c32 = 0, vmask = 0;
@@ -227,7 +239,12 @@ __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
                 while (left) {
                     const int i = __builtin_ctz(left);
                     left &= left - 1;
-                    if (slot < a.slab) slab[slot] = make_uint2((uint32_t)ck, (uint32_t)(cp0 + i) | ((slow >> i) & 1u ? kSlowBit : 0u));
+                    // the 8-mer at position i (its first base in the top bits) and its valid run
+                    const uint32_t c8 = (c32 >> (16 - 2 * i)) & 0xFFFFu;
+                    const uint32_t run = min(8u, (uint32_t)__builtin_ctz(~(vmask >> i)));
+                    if (slot < a.slab)
+                        slab[slot] = make_uint4((uint32_t)ck, (uint32_t)(cp0 + i) | ((slow >> i) & 1u ? kSlowBit : 0u),
+                                                c8 | (run << 16), 0u);
                     ++slot;
                 }
             }
@@ -240,9 +257,45 @@ __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
     }
 }
 
-// One block per slab: the probe entries of its raw hits become tasks. Each pass of 256 hits counts
-// the tasks per class, takes its place with one atomic per class, then writes them (the same
-// lookups again from LDS).
+// Resident blocks striding over the slabs: the probe entries of the slabs' raw hits become tasks.
+// The raw hits carry their 8-mer and valid run, so nothing here touches the reads: the slabs, the
+// LDS image and the task stores. A block first counts its tasks per class (all its slabs) and
+// takes its place with one atomic per class -- one per block, not per 256 hits: a few thousand
+// same-address atomics serialise at the L2 -- then writes them, 256 hits at a time at the offsets
+// of a block scan of their counts (the LDS lookups are repeated; they are cheap).
+template <bool WRITE>
+__device__ __forceinline__ long long expand_hit(const ScanArgs &a, const uint32_t *lds, const uint16_t *rank,
+                                                const uint16_t *estart, const int32_t *ent, const uint4 &r, long long at0,
+                                                long long at1) {
+    const int64_t rd = r.x;
+    const int q = (int)(r.y & ~kSlowBit);
+    const bool fast = !(r.y & kSlowBit);
+    const uint32_t c8 = r.z & 0xFFFFu;
+    const int run = (int)(r.z >> 16);
+    long long c = 0;
+    for (int kk = fast ? kNK - 1 : 0; kk < (fast ? kNK : kNK - 1); ++kk) {
+        const int K = kMinK + kk;
+        if (a.bits_off[kk] < 0 || (!fast && K > run)) continue;
+        const uint32_t code = c8 >> (2 * (kMaxK - K));
+        const int dw = a.bits_off[kk] + (int)(code >> 5);
+        const uint32_t word = lds[dw], bit = 1u << (code & 31);
+        if (!(word & bit)) continue;
+        const int rr = rank[dw] + __popc(word & (bit - 1));
+        const int e = estart[rr + 1];
+        for (int b = estart[rr]; b < e; ++b) {
+            const int en = ent[b];                       // adapter << 9 | class << 8 | offset
+            const int cls = (en >> 8) & 1;
+            if (WRITE) {
+                const long long g = cls ? at1++ : at0++;
+                if (g < a.cap) a.task[cls * a.cap + g] = make_int4((int)rd, en >> 9, q - (en & 255), en & 255);
+            } else {
+                c += cls ? (1ll << 32) : 1ll;
+            }
+        }
+    }
+    return c;
+}
+
 __global__ __launch_bounds__(256) void k_seed_expand(ScanArgs a) {
     extern __shared__ uint32_t lds[];
     typedef hipcub::BlockScan<long long, 256> Scan;
@@ -253,77 +306,43 @@ __global__ __launch_bounds__(256) void k_seed_expand(ScanArgs a) {
     const uint16_t *rank = reinterpret_cast<const uint16_t *>(lds + a.rank_off);
     const uint16_t *estart = reinterpret_cast<const uint16_t *>(lds + a.estart_off);
     const int32_t *ent = reinterpret_cast<const int32_t *>(lds + a.ent_off);
-    const int cnt = a.raw_cnt[blockIdx.x];
-    const uint2 *slab = a.raw + (int64_t)blockIdx.x * a.slab;
-    for (int base = 0; base < cnt; base += 256) {      // block-uniform
-        const int i = base + (int)threadIdx.x;
-        int64_t rd = -1;
-        int q = 0, run = 0;
-        bool fast = false;
-        uint32_t c8 = 0;
-        if (i < cnt) {
-            const uint2 r = slab[i];
-            rd = r.x;
-            q = (int)(r.y & ~kSlowBit);
-            fast = !(r.y & kSlowBit);
-            const int len = a.v_len[rd];
-            const uint8_t *p = a.codes + a.v_off[rd] + q;
-            const int a0 = (int)((uintptr_t)p & 3);
-            const uint32_t *dq = reinterpret_cast<const uint32_t *>(p - a0);
-            const uint32_t w0 = __builtin_amdgcn_alignbyte(dq[1], dq[0], a0);
-            const uint32_t w1 = __builtin_amdgcn_alignbyte(dq[2], dq[1], a0);
-#pragma unroll
-            for (int t = 0; t < 8; ++t) {
-                const uint32_t b = ((t < 4 ? w0 : w1) >> (8 * (t & 3))) & 0xFFu;
-                const bool valid = b < 4 && q + t < len;
-                if (valid && run == t) ++run;
-                c8 = (c8 << 2) | (b & 3u);
-            }
+    // 1. the block's task counts (classes packed 32 | 32) and its place
+    long long mine = 0;
+    for (int sl = blockIdx.x; sl < a.n_slab; sl += gridDim.x) {
+        const uint4 *slab = a.raw + (int64_t)sl * a.slab;
+        const int cnt = a.raw_cnt[sl];
+        for (int i = threadIdx.x; i < cnt; i += 256) mine += expand_hit<false>(a, lds, rank, estart, ent, slab[i], 0, 0);
+    }
+    {
+        long long ex, total;
+        Scan(scan_tmp).ExclusiveSum(mine, ex, total);
+        if (threadIdx.x == 0) {
+            const long long t0 = total & 0xFFFFFFFFll, t1 = total >> 32;
+            s_base[0] = t0 ? atomicAdd(&a.cnt[0], (int)t0) : 0;
+            s_base[1] = t1 ? atomicAdd(&a.cnt[1], (int)t1) : 0;
+            if (s_base[0] + t0 > a.cap || s_base[1] + t1 > a.cap) atomicOr(&a.flags[1], 1);
         }
-        // two passes over this hit's entries: count (pass 0), then write (pass 1)
-        long long mine = 0;
-        for (int pass = 0; pass < 2; ++pass) {
-            long long at[kCls] = {0, 0};
-            if (pass == 1) {
-                at[0] = s_base[0] + (mine & 0xFFFFFFFFll);
-                at[1] = s_base[1] + (mine >> 32);
+        __syncthreads();
+    }
+    // 2. the tasks, 256 hits at a time
+    for (int sl = blockIdx.x; sl < a.n_slab; sl += gridDim.x) {      // block-uniform
+        const uint4 *slab = a.raw + (int64_t)sl * a.slab;
+        const int cnt = a.raw_cnt[sl];
+        for (int base = 0; base < cnt; base += 256) {
+            const int i = base + (int)threadIdx.x;
+            const uint4 r = i < cnt ? slab[i] : make_uint4(0u, 0u, 0u, 0u);
+            const long long c = i < cnt ? expand_hit<false>(a, lds, rank, estart, ent, r, 0, 0) : 0ll;
+            long long ex, total;
+            Scan(scan_tmp).ExclusiveSum(c, ex, total);
+            if (i < cnt)
+                expand_hit<true>(a, lds, rank, estart, ent, r, s_base[0] + (ex & 0xFFFFFFFFll), s_base[1] + (ex >> 32));
+            __syncthreads();                           // scan_tmp reused; s_base advanced
+            if (threadIdx.x == 0) {
+                s_base[0] += total & 0xFFFFFFFFll;
+                s_base[1] += total >> 32;
             }
-            long long c = 0;
-            if (rd >= 0) {
-                for (int kk = fast ? kNK - 1 : 0; kk < (fast ? kNK : kNK - 1); ++kk) {
-                    const int K = kMinK + kk;
-                    if (a.bits_off[kk] < 0 || (!fast && K > run)) continue;
-                    const uint32_t code = c8 >> (2 * (kMaxK - K));
-                    const int dw = a.bits_off[kk] + (int)(code >> 5);
-                    const uint32_t word = lds[dw], bit = 1u << (code & 31);
-                    if (!(word & bit)) continue;
-                    const int r = rank[dw] + __popc(word & (bit - 1));
-                    const int e = estart[r + 1];
-                    for (int b = estart[r]; b < e; ++b) {
-                        const int en = ent[b];                 // adapter << 9 | class << 8 | offset
-                        const int cls = (en >> 8) & 1;
-                        if (pass == 0) {
-                            c += cls ? (1ll << 32) : 1ll;
-                        } else {
-                            const long long g = at[cls]++;
-                            if (g < a.cap) a.task[cls * a.cap + g] = make_int4((int)rd, en >> 9, q - (en & 255), 0);
-                        }
-                    }
-                }
-            }
-            if (pass == 0) {
-                long long total;
-                Scan(scan_tmp).ExclusiveSum(c, mine, total);
-                if (threadIdx.x == 0) {
-                    const long long t0 = total & 0xFFFFFFFFll, t1 = total >> 32;
-                    s_base[0] = t0 ? atomicAdd(&a.cnt[0], (int)t0) : 0;
-                    s_base[1] = t1 ? atomicAdd(&a.cnt[1], (int)t1) : 0;
-                    if (s_base[0] + t0 > a.cap || s_base[1] + t1 > a.cap) atomicOr(&a.flags[1], 1);
-                }
-                __syncthreads();
-            }
+            __syncthreads();
         }
-        __syncthreads();                               // s_base / scan_tmp reused by the next pass
     }
 }
 
@@ -479,8 +498,14 @@ __global__ __launch_bounds__(256) void k_bound16(const int32_t *bound, int64_t c
     if (i < cnt) s16[i] = (int16_t)max(min(bound[i], 32767), -32768);
 }
 
-// bound[a * n + r] = NEG16 for the n_dev x n_adp live entries (row stride n).
-__global__ __launch_bounds__(256) void k_bound_reset(int32_t *bound, int64_t n, const int32_t *n_dev, int32_t n_adp) {
+// bound[a * n + r] = NEG16 for the n_dev x n_adp live entries (row stride n); block 0 also zeroes
+// the counters of the launches that follow (z32[0 .. nz32), *z64 when given).
+__global__ __launch_bounds__(256) void k_bound_reset(int32_t *bound, int64_t n, const int32_t *n_dev, int32_t n_adp,
+                                                     int32_t *z32, int nz32, unsigned long long *z64) {
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < nz32) z32[threadIdx.x] = 0;
+        if (z64 && threadIdx.x == 0) *z64 = 0ull;
+    }
     const int64_t nr = dev_count(n_dev, n);
     const int64_t total = nr * n_adp;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
@@ -530,6 +555,7 @@ struct State {
     Buf tabs, adp, adp_off, adp_len, task, cnt, bound, thr, cands, ccnt, raw, rawcnt;
     int64_t cap = 0, ccap = 0, raw_cap = 0;
     int scan_blocks = 0;                          // resident k_seed_scan blocks
+    int expand_blocks = 0;                        // resident k_seed_expand blocks
 };
 
 State *create() { return new State(); }
@@ -713,11 +739,14 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
         SD_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
         SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_scan, 256, 4 * (size_t)s->a.bits_dw));
         s->scan_blocks = std::max(1, cus * std::max(1, per_cu));
+        per_cu = 0;
+        SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_expand, 256, s->lds_bytes));
+        s->expand_blocks = std::min(s->scan_blocks, std::max(1, cus * std::max(1, per_cu)));
     }
     const int grid = s->scan_blocks;
     if (s->raw_cap == 0) s->raw_cap = (int64_t)grid * 4096;
     if (s->cap == 0) s->cap = 1 << 22;
-    if (int rc = s->raw.ensure(sizeof(uint2) * (size_t)s->raw_cap)) return rc;
+    if (int rc = s->raw.ensure(sizeof(uint4) * (size_t)s->raw_cap)) return rc;
     if (int rc = s->rawcnt.ensure(4 * (size_t)grid)) return rc;
     if (int rc = s->task.ensure(sizeof(int4) * kCls * (size_t)s->cap)) return rc;
     if (int rc = s->cnt.ensure(4 * (kCls + 2))) return rc;
@@ -728,17 +757,19 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
     A.v_len = v_len;
     A.n = n;
     A.n_dev = n_dev;
-    A.raw = (uint2 *)s->raw.p;
+    A.raw = (uint4 *)s->raw.p;
+    A.n_slab = grid;
     A.slab = (int32_t)std::min<int64_t>(s->raw_cap / grid, INT32_MAX);
     A.raw_cnt = (int32_t *)s->rawcnt.p;
     A.cnt = (int32_t *)s->cnt.p;
     A.flags = A.cnt + kCls;
     A.task = (int4 *)s->task.p;
     A.cap = s->cap;
-    SD_TRY(hipMemsetAsync(A.cnt, 0, 4 * (kCls + 2), st));
-    hipLaunchKernelGGL(k_bound_reset, dim3(1024), dim3(256), 0, st, (int32_t *)s->bound.p, n, n_dev, n_adp);
+    if (int rc = s->ccnt.ensure(8)) return rc;
+    hipLaunchKernelGGL(k_bound_reset, dim3(1024), dim3(256), 0, st, (int32_t *)s->bound.p, n, n_dev, n_adp, A.cnt,
+                       kCls + 2, (unsigned long long *)s->ccnt.p);
     hipLaunchKernelGGL(k_seed_scan, dim3(grid), dim3(256), 4 * (size_t)A.bits_dw, st, A);
-    hipLaunchKernelGGL(k_seed_expand, dim3(grid), dim3(256), s->lds_bytes, st, A);
+    hipLaunchKernelGGL(k_seed_expand, dim3(s->expand_blocks), dim3(256), s->lds_bytes, st, A);
     SD_TRY(hipGetLastError());
     unsigned g[kCls];
     for (int c = 0; c < kCls; ++c)
@@ -918,8 +949,7 @@ int bounds_dev(State *s, const uint8_t *codes, const int64_t *v_off, const int32
     const int64_t tot = n * (int64_t)n_adp;
     if (s->ccap < tot) s->ccap = tot;
     if (int rc = s->cands.ensure(sizeof(int64_t) * (size_t)s->ccap)) return rc;
-    if (int rc = s->ccnt.ensure(8)) return rc;
-    SD_TRY(hipMemsetAsync(s->ccnt.p, 0, 8, st));
+    // (ccnt zeroed by k_bound_reset)
     hipLaunchKernelGGL(k_cands, dim3((unsigned)std::min<int64_t>((tot + 255) / 256, kBandGrid)), dim3(256), 0, st,
                        (const int32_t *)s->bound.p, n, n_dev, n_adp, (const int32_t *)s->thr.p, (int64_t *)s->cands.p,
                        s->ccap, (unsigned long long *)s->ccnt.p);
@@ -936,6 +966,20 @@ int bounds_dev(State *s, const uint8_t *codes, const int64_t *v_off, const int32
 bool grow_after_overflow(State *s, int raw_overflow, int task_overflow) {
     int32_t c[kCls + 2] = {(int32_t)std::min<int64_t>(4 * s->cap, INT32_MAX), 0, raw_overflow, task_overflow};
     return grow(s, c);
+}
+
+// Debugging (PCABI_DEBUG=1): the last queued seeding's band task counts per class and candidate
+// count (synchronises `st`).
+int debug_counts(State *s, int64_t (&out)[3], hipStream_t st) {
+    int32_t c[kCls + 2] = {0, 0, 0, 0};
+    unsigned long long nc = 0;
+    SD_TRY(hipMemcpyAsync(c, s->cnt.p, sizeof(c), hipMemcpyDeviceToHost, st));
+    SD_TRY(hipMemcpyAsync(&nc, s->ccnt.p, 8, hipMemcpyDeviceToHost, st));
+    SD_TRY(hipStreamSynchronize(st));
+    out[0] = c[0];
+    out[1] = c[1];
+    out[2] = (int64_t)nc;
+    return 0;
 }
 
 // the plan for these adapters, without running anything: true when seeds apply (mode as bounds()).

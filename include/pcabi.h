@@ -198,6 +198,15 @@ int pcabi_end_trim_dev(const int32_t *start_res, int64_t start_stride, int32_t n
                        uint8_t *start_hit, uint8_t *end_hit, void *stream);
 
 /*
+ * The reads with their end adapters trimmed, on the device (nanopore_read.py:44-49,
+ * get_seq_with_start_end_adapters_trimmed): view_off = read_off + start_trim, view_len =
+ * max(read_len - start_trim - end_trim, 0) -- the middle scan's windows straight from
+ * pcabi_end_trim_dev's amounts, with no host round trip. Async on `stream`.
+ */
+int pcabi_trim_views_dev(const int64_t *read_off, const int32_t *read_len, const int32_t *start_trim,
+                         const int32_t *end_trim, int64_t n_read, int64_t *view_off, int32_t *view_len, void *stream);
+
+/*
  * End-trim decisions with their alignment lists (porechop_abi/nanopore_read.py:175-217, the loop of
  * find_adapters_at_read_ends, porechop_abi.py:359-438) from HOST buffers, with only the decisions
  * coming back -- never the (read, adapter) result matrix:
@@ -262,7 +271,11 @@ int pcabi_first_hit_dev(const int32_t *res, int64_t stride, int64_t n_win, int32
  * written) or a negative error. threshold must be > 0 (the reference never terminates otherwise).
  *   pcabi_scan_create / destroy : scratch for one adapter table (current device).
  *   pcabi_middle_scan_dev       : codes/win_off/win_len are DEVICE pointers (codes are masked in
- *                                 place), h_win_len the host copy of the lengths.
+ *                                 place), h_win_len the host copy of the lengths or NULL (the call
+ *                                 then copies them: e.g. views from pcabi_trim_views_dev). When the
+ *                                 seeded plan covers the table and scoring, the rounds are queued on
+ *                                 the device with their counts there (no host round trip between
+ *                                 rounds; PCABI_MIDDLE_DEVROUNDS=0 keeps the host-driven loop).
  *   pcabi_middle_scan_host      : host buffers (as pcabi_align_host), copies in, scans.
  *   pcabi_middle_seed_runs      : how many round-1 scans took their bounds from exact k-mer seeds
  *                                 (pcabi_seed.hip) instead of the score filter, process-wide.
