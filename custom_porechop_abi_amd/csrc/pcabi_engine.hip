@@ -20,6 +20,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <memory>
 #include <cstdlib>
@@ -935,7 +936,7 @@ int bounds_dev(State *s, const uint8_t *codes, const int64_t *v_off, const int32
                const int32_t *n_dev, int32_t n_adp, const pcabi::Scoring &sc, const int64_t **dcands,
                const unsigned long long **dcount, const int32_t **flags, hipStream_t st);
 bool grow_after_overflow(State *s, int raw_overflow, int task_overflow);
-int debug_counts(State *s, int64_t (&out)[3], hipStream_t st);
+int debug_counts(State *s, int64_t (&out)[5], hipStream_t st);
 }  // namespace pcabi_seed
 
 struct pcabi_scan {
@@ -2432,15 +2433,16 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
         hipLaunchKernelGGL(k_mask_list, dim3(1024), dim3(256), 0, st, codes, win_off, list_of(r), d_n + r + 1);
         HIP_TRY(hipGetLastError());
         if (g_debug) {                               // debugging only: a synchronisation per round
-            int64_t c[3];
+            int64_t c[5];
             if (int rc = pcabi_seed::debug_counts(sc->seed, c, st)) return rc;
             int32_t rn[2];
             int64_t sl = 0;
             HIP_TRY(hipMemcpy(rn, d_n + r, 8, hipMemcpyDeviceToHost));
             HIP_TRY(hipMemcpy(&sl, d_slots, 8, hipMemcpyDeviceToHost));
-            std::fprintf(stderr, "[pcabi] middle round %lld: %d reads, band tasks %lld + %lld, %lld candidates, "
-                         "%lld task slots, %d hits\n", (long long)(round_base + r), rn[0], (long long)c[0],
-                         (long long)c[1], (long long)c[2], (long long)sl, rn[1]);
+            std::fprintf(stderr, "[pcabi] middle round %lld: %d reads, band tasks %lld + %lld edge, %lld + %lld edge, "
+                         "%lld candidates, %lld task slots, %d hits\n", (long long)(round_base + r), rn[0],
+                         (long long)c[0], (long long)c[1], (long long)c[2], (long long)c[3], (long long)c[4],
+                         (long long)sl, rn[1]);
         }
         return 0;
     };
@@ -2642,12 +2644,22 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
             if (filt < 0) return filt;
         }
         if (!filt) {
+            const auto t0 = std::chrono::steady_clock::now();
             if (int rc = make_tiles()) return rc;
+            if (g_debug) HIP_TRY(hipStreamSynchronize(st));
+            const auto t1 = std::chrono::steady_clock::now();
             if (int rc = sc->res.ensure(sizeof(int32_t) * PCABI_NFIELDS * (size_t)n * n_adp)) return rc;
             if (int rc = pcabi_align_cross_dev((const uint32_t *)sc->tiles.p, (const int64_t *)sc->toff.p, v_len, n,
                                                max_len, sc->adps, match, mismatch, gap_open, gap_extend,
                                                (int32_t *)sc->res.p, n * n_adp, stream))
                 return rc;
+            if (g_debug) {
+                HIP_TRY(hipStreamSynchronize(st));
+                const auto t2 = std::chrono::steady_clock::now();
+                std::fprintf(stderr, "[pcabi] middle host round %d: tiles %.3f ms, cross product %.3f ms (%lld x %d, longest %d)\n",
+                             round, std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                             std::chrono::duration<double, std::milli>(t2 - t1).count(), (long long)n, n_adp, max_len);
+            }
             hipLaunchKernelGGL(k_first_hit, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
                                (const int32_t *)sc->res.p, n * n_adp, n, n_adp, threshold,
                                round == 0 ? nullptr : (const int32_t *)sc->start.p, (int32_t *)sc->hits.p, n);
@@ -2676,6 +2688,9 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
             nxt_start.push_back(a);
             if (rend > rs) { hm_w.push_back(r); hm_s.push_back(rs); hm_e.push_back(rend); }
         }
+        if (g_debug)
+            std::fprintf(stderr, "[pcabi] middle host round %d: %lld reads, %zu hits (%s)\n", round, (long long)n,
+                         nxt.size(), filt ? "filtered" : "cross product");
         if (nxt.empty()) break;
         if (!hm_w.empty()) {
             const size_t m = hm_w.size();

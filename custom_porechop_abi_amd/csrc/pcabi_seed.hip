@@ -88,6 +88,11 @@ constexpr int kNW = 4;             // dwords of bases per lane and step
 constexpr int kSub = PCABI_SEED_SUB;   // sub-steps per scan iteration
 constexpr unsigned kSlowBit = 0x80000000u;   // raw hit: the position's valid run is shorter than 8
 constexpr int kBandGrid = 4096;    // band / cands launches whose count is on the device: grid-stride
+// task counters: [c] inside-band tasks of class c (from the region's start), [kCls + c] edge tasks
+// (bands touching a read end, from the region's end), then the two overflow flags
+constexpr int kCnt = 2 * kCls + 2;
+constexpr int kFlag = 2 * kCls;
+constexpr int kPinMaxE = 8;        // the pinned band is built for E <= kPinMaxE
 
 struct ScanArgs {
     const uint8_t *codes;
@@ -109,9 +114,14 @@ struct ScanArgs {
     int32_t n_slab;             // slabs (scan blocks); the expansion's blocks stride over them
     int32_t *raw_cnt;           // raw hits per slab
     int32_t *flags;             // [0] a slab overflowed, [1] a task region overflowed
-    int4 *task;                 // kCls regions of cap tasks: (read, adapter, diagonal, 0)
-    int64_t cap;
-    int32_t *cnt;               // tasks per class (may exceed cap: flags[1])
+    int4 *task;                 // per class cap inside-band tasks, then ecap edge tasks (bands that touch
+                                // a read end): (read, adapter, diagonal, probe offset)
+    int64_t cap, ecap;
+    int32_t *cnt;               // kCnt counters (inside / edge tasks per class, flags)
+    int32_t ent2_off;           // dword offset of the entries' inside limits (lo | hi << 16): a task
+                                // is inside when q >= lo and (read length - q) > hi
+    int32_t pin_cls[kCls];      // class c's inside tasks run the pinned band: records (read,
+                                // adapter << 8 | o, the probe's byte offset in codes: lo, hi)
 };
 
 __device__ __forceinline__ int64_t dev_count(const int32_t *n_dev, int64_t n) {
@@ -165,6 +175,9 @@ __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
     base = a.codes + noff;
     if (k < nr) nk = next_read(k + gridDim.x, nlen, noff);
     int p0b = 0;
+#if defined(PCABI_SCAN_EXP)
+    uint32_t sink = 0;                                 // perf experiments only (tools/build_variant.sh)
+#endif
     uint32_t wn[kSub][kNW + 1];
     int an[kSub];
 #pragma unroll
@@ -232,6 +245,15 @@ __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
                     slow |= (!full && ((vmask >> i) & ((1u << a.min_k) - 1u)) == (1u << a.min_k) - 1u) ? 1u << i : 0u;
                 }
             }
+#if defined(PCABI_SCAN_EXP) && PCABI_SCAN_EXP == 1
+            hits = 0;
+            slow = 0;
+            sink ^= c32 ^ vmask;
+#elif defined(PCABI_SCAN_EXP) && PCABI_SCAN_EXP == 2
+            sink ^= hits ^ slow;
+            hits = 0;
+            slow = 0;
+#endif
             const uint32_t any = hits | slow;
             if (any) {                                 // ~4 % of the lanes: append to the block's slab
                 int slot = atomicAdd(&s_cnt, __popc(any));
@@ -244,12 +266,15 @@ __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
                     const uint32_t run = min(8u, (uint32_t)__builtin_ctz(~(vmask >> i)));
                     if (slot < a.slab)
                         slab[slot] = make_uint4((uint32_t)ck, (uint32_t)(cp0 + i) | ((slow >> i) & 1u ? kSlowBit : 0u),
-                                                c8 | (run << 16), 0u);
+                                                c8 | (run << 16), (uint32_t)(clen - (cp0 + i)));
                     ++slot;
                 }
             }
         }
     }
+#if defined(PCABI_SCAN_EXP)
+    if (sink == 0x12345678u) a.flags[0] = 2;       // keeps the experiment's work alive
+#endif
     __syncthreads();
     if (threadIdx.x == 0) {
         a.raw_cnt[blockIdx.x] = min(s_cnt, a.slab);
@@ -263,16 +288,23 @@ __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
 // takes its place with one atomic per class -- one per block, not per 256 hits: a few thousand
 // same-address atomics serialise at the L2 -- then writes them, 256 hits at a time at the offsets
 // of a block scan of their counts (the LDS lookups are repeated; they are cheap).
+// Counts are packed per class pair: inside tasks (classes 0 | 1 << 32) and edge tasks likewise.
+struct TaskCount {
+    long long in, edge;
+};
+
 template <bool WRITE>
-__device__ __forceinline__ long long expand_hit(const ScanArgs &a, const uint32_t *lds, const uint16_t *rank,
-                                                const uint16_t *estart, const int32_t *ent, const uint4 &r, long long at0,
-                                                long long at1) {
+__device__ __forceinline__ TaskCount expand_hit(const ScanArgs &a, const uint32_t *lds, const uint16_t *rank,
+                                                const uint16_t *estart, const int32_t *ent, const uint32_t *ent2,
+                                                const uint4 &r, TaskCount at) {
     const int64_t rd = r.x;
     const int q = (int)(r.y & ~kSlowBit);
     const bool fast = !(r.y & kSlowBit);
     const uint32_t c8 = r.z & 0xFFFFu;
     const int run = (int)(r.z >> 16);
-    long long c = 0;
+    const int dist = (int)r.w;                           // read length - q
+    const int64_t probe0 = WRITE && (a.pin_cls[0] | a.pin_cls[1]) ? a.v_off[rd] + q : 0;
+    TaskCount c{0, 0};
     for (int kk = fast ? kNK - 1 : 0; kk < (fast ? kNK : kNK - 1); ++kk) {
         const int K = kMinK + kk;
         if (a.bits_off[kk] < 0 || (!fast && K > run)) continue;
@@ -284,12 +316,31 @@ __device__ __forceinline__ long long expand_hit(const ScanArgs &a, const uint32_
         const int e = estart[rr + 1];
         for (int b = estart[rr]; b < e; ++b) {
             const int en = ent[b];                       // adapter << 9 | class << 8 | offset
+            const uint32_t lim = ent2[b];
+            const bool inside = q >= (int)(lim & 0xFFFFu) && dist > (int)(lim >> 16);
             const int cls = (en >> 8) & 1;
+            const long long one = cls ? (1ll << 32) : 1ll;
             if (WRITE) {
-                const long long g = cls ? at1++ : at0++;
-                if (g < a.cap) a.task[cls * a.cap + g] = make_int4((int)rd, en >> 9, q - (en & 255), en & 255);
+                const long long sh = cls ? 32 : 0;
+                int4 *region = a.task + cls * (a.cap + a.ecap);
+                if (inside) {
+                    const long long g = (at.in >> sh) & 0xFFFFFFFFll;
+                    at.in += one;
+                    if (g < a.cap) {
+                        if (a.pin_cls[cls])
+                            region[g] = make_int4((int)rd, ((en >> 9) << 8) | (en & 255), (int)(uint32_t)probe0,
+                                                  (int)(uint32_t)((uint64_t)probe0 >> 32));
+                        else
+                            region[g] = make_int4((int)rd, en >> 9, q - (en & 255), en & 255);
+                    }
+                } else {
+                    const long long g = (at.edge >> sh) & 0xFFFFFFFFll;
+                    at.edge += one;
+                    if (g < a.ecap) region[a.cap + g] = make_int4((int)rd, en >> 9, q - (en & 255), en & 255);
+                }
             } else {
-                c += cls ? (1ll << 32) : 1ll;
+                if (inside) c.in += one;
+                else c.edge += one;
             }
         }
     }
@@ -300,27 +351,43 @@ __global__ __launch_bounds__(256) void k_seed_expand(ScanArgs a) {
     extern __shared__ uint32_t lds[];
     typedef hipcub::BlockScan<long long, 256> Scan;
     __shared__ typename Scan::TempStorage scan_tmp;
-    __shared__ long long s_base[kCls];
+    __shared__ long long s_base[2];                      // inside / edge bases, classes packed 32 | 32
     for (int i = threadIdx.x; i < a.tab_dw; i += 256) lds[i] = a.tabs[i];
     __syncthreads();
     const uint16_t *rank = reinterpret_cast<const uint16_t *>(lds + a.rank_off);
     const uint16_t *estart = reinterpret_cast<const uint16_t *>(lds + a.estart_off);
     const int32_t *ent = reinterpret_cast<const int32_t *>(lds + a.ent_off);
-    // 1. the block's task counts (classes packed 32 | 32) and its place
-    long long mine = 0;
+    const uint32_t *ent2 = lds + a.ent2_off;
+    // 1. the block's task counts and its places (one atomic per counter and block)
+    TaskCount mine{0, 0};
     for (int sl = blockIdx.x; sl < a.n_slab; sl += gridDim.x) {
         const uint4 *slab = a.raw + (int64_t)sl * a.slab;
         const int cnt = a.raw_cnt[sl];
-        for (int i = threadIdx.x; i < cnt; i += 256) mine += expand_hit<false>(a, lds, rank, estart, ent, slab[i], 0, 0);
+        for (int i = threadIdx.x; i < cnt; i += 256) {
+            const TaskCount c = expand_hit<false>(a, lds, rank, estart, ent, ent2, slab[i], TaskCount{0, 0});
+            mine.in += c.in;
+            mine.edge += c.edge;
+        }
     }
     {
-        long long ex, total;
-        Scan(scan_tmp).ExclusiveSum(mine, ex, total);
+        long long ex, tin, tedge;
+        Scan(scan_tmp).ExclusiveSum(mine.in, ex, tin);
+        __syncthreads();
+        Scan(scan_tmp).ExclusiveSum(mine.edge, ex, tedge);
         if (threadIdx.x == 0) {
-            const long long t0 = total & 0xFFFFFFFFll, t1 = total >> 32;
-            s_base[0] = t0 ? atomicAdd(&a.cnt[0], (int)t0) : 0;
-            s_base[1] = t1 ? atomicAdd(&a.cnt[1], (int)t1) : 0;
-            if (s_base[0] + t0 > a.cap || s_base[1] + t1 > a.cap) atomicOr(&a.flags[1], 1);
+            long long b[2] = {0, 0};
+            bool over = false;
+            for (int c = 0; c < kCls; ++c) {
+                const long long ti = (tin >> (32 * c)) & 0xFFFFFFFFll, te = (tedge >> (32 * c)) & 0xFFFFFFFFll;
+                const long long bi = ti ? atomicAdd(&a.cnt[c], (int)ti) : 0;
+                const long long be = te ? atomicAdd(&a.cnt[kCls + c], (int)te) : 0;
+                b[0] |= bi << (32 * c);
+                b[1] |= be << (32 * c);
+                over |= bi + ti > a.cap || be + te > a.ecap;
+            }
+            s_base[0] = b[0];
+            s_base[1] = b[1];
+            if (over) atomicOr(&a.flags[1], 1);
         }
         __syncthreads();
     }
@@ -331,15 +398,17 @@ __global__ __launch_bounds__(256) void k_seed_expand(ScanArgs a) {
         for (int base = 0; base < cnt; base += 256) {
             const int i = base + (int)threadIdx.x;
             const uint4 r = i < cnt ? slab[i] : make_uint4(0u, 0u, 0u, 0u);
-            const long long c = i < cnt ? expand_hit<false>(a, lds, rank, estart, ent, r, 0, 0) : 0ll;
-            long long ex, total;
-            Scan(scan_tmp).ExclusiveSum(c, ex, total);
-            if (i < cnt)
-                expand_hit<true>(a, lds, rank, estart, ent, r, s_base[0] + (ex & 0xFFFFFFFFll), s_base[1] + (ex >> 32));
+            const TaskCount c = i < cnt ? expand_hit<false>(a, lds, rank, estart, ent, ent2, r, TaskCount{0, 0})
+                                        : TaskCount{0, 0};
+            long long exi, exe, ti, te;
+            Scan(scan_tmp).ExclusiveSum(c.in, exi, ti);
+            __syncthreads();
+            Scan(scan_tmp).ExclusiveSum(c.edge, exe, te);
+            if (i < cnt) expand_hit<true>(a, lds, rank, estart, ent, ent2, r, TaskCount{s_base[0] + exi, s_base[1] + exe});
             __syncthreads();                           // scan_tmp reused; s_base advanced
             if (threadIdx.x == 0) {
-                s_base[0] += total & 0xFFFFFFFFll;
-                s_base[1] += total >> 32;
+                s_base[0] += ti;
+                s_base[1] += te;
             }
             __syncthreads();
         }
@@ -469,6 +538,184 @@ __global__ __launch_bounds__(256) void k_seed_band(const int4 *task, const int32
     }
 }
 
+// ---- the pinned band (inside tasks) ----------------------------------------------------------
+// A task comes from probe p of adapter a found at read position q: the piece's first K bases sit on
+// diagonal d0 = q - o as K matches (o = p * plen). The seed argument needs only the alignment whose
+// piece p is exact -- it passes through those K diagonal matches -- so the bound is the best score
+// of band alignments that do: B = P + K * match + Q, with
+//   Q: the best suffix from the pinned run's end cell (row o + K, diagonal d0) to the adapter's last
+//      row (inside bands end anywhere in it): the band DP of rows o + K + 1 .. L started from that
+//      cell -- and from the read bases an alignment may insert right after the run in that same row
+//      (a horizontal gap: go, ge, ... to the cell's right);
+//   P: the best prefix from row 0 (free start, any band column) to the run's first cell (row o): the
+//      same DP run backwards -- the adapter prefix and the read reversed, the band mirrored
+//      (x' = 2E - x), which turns the reverse recurrence into the forward one -- started likewise,
+//      its best over the last row (row 0).
+// B <= the band best (a subset of its alignments) and B >= the score of any alignment whose piece p
+// is exact, so a pair whose hit has exact piece p still reaches T through this task: the bound stays
+// exact (tests/test_seed_pin_cpu.py checks B against the band DP constrained to the run). Both halves
+// start from one cell, so random probe hits fall below T within a few rows, and rows o + 1 .. o + K
+// are never computed. Early exit as band_best: the running maximum plus best_sub per remaining row
+// plus the other half's bound (best_sub per row before it is known).
+//
+// Inside tasks (expand, pinned classes) carry (read, adapter << 8 | o, the probe's byte offset in
+// codes): the read bytes of the whole band, [probe - o - E, probe - o + L + E), are one range. Per
+// lane the range of the NEXT task is loaded (uint4 loads) while the current task computes, then
+// copied to the lane's LDS slot (NC4 x 16 bytes), where the rows read their one new byte each: the
+// row loop touches no global memory, so no wait of the loop is a memory latency.
+template <int E, int NC4>
+__global__ __launch_bounds__(256) void k_seed_band_pin(const int4 *task, const int32_t *n_task, int64_t cap,
+                                                       const uint8_t *codes, const uint8_t *adp, int32_t adp_dw,
+                                                       const int32_t *adp_off, const int32_t *adp_meta, int32_t n_adp,
+                                                       pcabi::Scoring sc, int32_t *bound, int64_t n) {
+    constexpr int W = 2 * E + 1;
+    extern __shared__ uint4 lds4[];
+    uint32_t *lds = reinterpret_cast<uint32_t *>(lds4);
+    // LDS: the flat adapters (adp_dw dwords), their offsets, their meta (L | K << 8 | T << 12), then
+    // per lane NC4 uint4 of read bytes
+    for (int i = threadIdx.x; i < adp_dw; i += 256) lds[i] = reinterpret_cast<const uint32_t *>(adp)[i];
+    for (int i = threadIdx.x; i < n_adp; i += 256) {
+        lds[adp_dw + i] = (uint32_t)adp_off[i];
+        lds[adp_dw + n_adp + i] = (uint32_t)adp_meta[i];
+    }
+    __syncthreads();
+    const uint8_t *ad = reinterpret_cast<const uint8_t *>(lds);
+    const int32_t *aoffs = reinterpret_cast<const int32_t *>(lds + adp_dw);
+    const int32_t *ameta = aoffs + n_adp;
+    uint4 *slot4 = lds4 + ((adp_dw + 2 * n_adp + 3) >> 2) + (int)threadIdx.x * NC4;
+    const uint8_t *slot = reinterpret_cast<const uint8_t *>(slot4);
+    const int64_t nt = min((int64_t)*n_task, cap);
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int bs = pcabi::best_sub(sc), ma = sc.ma, mi = sc.mi, go = sc.go, ge = sc.ge;
+    const uintptr_t lo_addr = (uintptr_t)codes & ~(uintptr_t)15;
+    // the range of a task: [cb, cb + 16 * nld) with cb = (probe - o - E) & ~15
+    auto range_of = [&](const int4 &rc, uintptr_t &cb, int &nld) {
+        const int a = rc.y >> 8, o = rc.y & 255;
+        const int L = (int)((uint32_t)ameta[a] & 255u);
+        const uintptr_t pa = (uintptr_t)codes + (uintptr_t)(((uint64_t)(uint32_t)rc.w << 32) | (uint32_t)rc.z);
+        const uintptr_t lo = pa - (uintptr_t)(o + E), hi = pa - (uintptr_t)o + (uintptr_t)(L + E);
+        cb = lo & ~(uintptr_t)15;
+        if (cb < lo_addr) cb = lo_addr;
+        nld = (int)((hi - cb + 15) >> 4);
+    };
+    // ---- pipeline: recA / chA = the task to copy into the slot next, recB = the one after
+    int4 recA = make_int4(0, 0, 0, 0), recB = recA;
+    bool vA = false, vB = false;
+    uint4 chA[NC4];
+    uintptr_t cbA = lo_addr;
+    auto load_range = [&]() {                         // chA := recA's range (recA has arrived)
+        int nld = 0;
+        range_of(recA, cbA, nld);
+#pragma unroll
+        for (int k = 0; k < NC4; ++k)
+            chA[k] = k < nld ? *reinterpret_cast<const uint4 *>(cbA + 16 * (uintptr_t)k) : make_uint4(0u, 0u, 0u, 0u);
+    };
+    if (t < nt) { recA = task[t]; vA = true; t += stride; }
+    if (vA) load_range();
+    if (t < nt) { recB = task[t]; vB = true; t += stride; }
+    auto pin_start = [&](int x) -> int { return x == E ? 0 : (x > E ? go + (x - E - 1) * ge : kNeg); };
+    while (__any(vA)) {                               // one task per lane and pass
+        bool active = vA;
+        int4 rc = recA;
+        uintptr_t cb = cbA;
+        if (vA) {
+#pragma unroll
+            for (int k = 0; k < NC4; ++k) slot4[k] = chA[k];
+        }
+        // the pipeline moves on: B's range loads while this task computes
+        vA = vB;
+        recA = recB;
+        if (vA) load_range();
+        vB = t < nt;
+        if (vB) {
+            recB = task[t];
+            t += stride;
+        }
+        // ---- this task
+        const int a = rc.y >> 8, o = rc.y & 255;
+        const uint32_t meta = (uint32_t)ameta[a];
+        const int L = (int)(meta & 255u), K = (int)((meta >> 8) & 15u), T = (int)(meta >> 12);
+        const int aoff = aoffs[a];
+        const int64_t bidx = (int64_t)a * n + rc.x;
+        const uintptr_t pa = (uintptr_t)codes + (uintptr_t)(((uint64_t)(uint32_t)rc.w << 32) | (uint32_t)rc.z);
+        const int base = (int)(pa - cb);              // the probe's byte in the slot
+        const int pin = ma * K;
+        int S[W], V[W], R[W];
+        int phase = 0, rows = L - o - K, other = pin + bs * o, mx = 0;
+        int apos = aoff + o + K, adir = 1;
+        int bpos = base + K + E + 1, bdir = 1;          // the slot byte entering the next row
+#pragma unroll
+        for (int x = 0; x < W; ++x) {
+            S[x] = pin_start(x);
+            V[x] = kNeg;
+            R[x] = active ? slot[base + K + x - E] : 0;   // row o + K + 1: read q + K + x - E
+        }
+        auto begin_prefix = [&]() {                   // rows o .. 1 backwards, mirrored band
+            phase = 1;
+            rows = o;
+            other = pin + mx;                         // K * match + Q
+            mx = 0;
+#pragma unroll
+            for (int x = 0; x < W; ++x) {
+                S[x] = pin_start(x);
+                V[x] = kNeg;
+                R[x] = slot[base - 1 + E - x];        // read q - 1 + E - x
+            }
+            bpos = base - 2 - E;
+            bdir = -1;
+            apos = aoff + o - 1;
+            adir = -1;
+        };
+        if (active && rows == 0) {                    // the run ends the adapter: Q = 0
+            if (o == 0) {
+                atomicMax(&bound[bidx], pin);
+                active = false;
+            } else {
+                begin_prefix();
+            }
+        }
+        while (__any(active)) {
+            if (active) {
+                const int ab = ad[apos];
+                apos += adir;
+                const int nb = slot[bpos];
+                bpos += bdir;
+                int h = kNeg, sl = kNeg;
+#pragma unroll
+                for (int x = 0; x < W; ++x) {
+                    const int dg = S[x] + (R[x] == ab ? ma : mi);
+                    const int vu = (x + 1 < W) ? max(V[x + 1] + ge, S[x + 1] + go) : kNeg;
+                    h = max(h + ge, sl + go);
+                    const int sv = max(dg, max(vu, h));
+                    S[x] = sv;
+                    V[x] = vu;
+                    sl = sv;
+                }
+#pragma unroll
+                for (int x = 0; x + 1 < W; ++x) R[x] = R[x + 1];
+                R[W - 1] = nb;
+                --rows;
+                mx = S[0];
+#pragma unroll
+                for (int x = 1; x < W; ++x) mx = max(mx, S[x]);
+                const int ub = mx + bs * rows + other;
+                if (ub < T) {
+                    atomicMax(&bound[bidx], ub);
+                    active = false;
+                } else if (rows == 0) {
+                    if (phase == 0 && o > 0) {
+                        begin_prefix();
+                    } else {
+                        atomicMax(&bound[bidx], mx + other);
+                        active = false;
+                    }
+                }
+            }
+        }
+    }
+}
+
 // The pairs whose bound reaches their adapter's threshold T[a], as (a << 32 | read) keys
 // (unordered; one atomic per wave), grid-stride over the n_dev x n_adp bounds (row stride n).
 __global__ __launch_bounds__(256) void k_cands(const int32_t *bound, int64_t n, const int32_t *n_dev, int32_t n_adp,
@@ -552,10 +799,13 @@ struct State {
     size_t lds_bytes = 0;                         // the whole probe image (k_seed_expand)
     int32_t adp_bytes = 0;                        // flat adapter table, dword-rounded
     ScanArgs a{};
-    Buf tabs, adp, adp_off, adp_len, task, cnt, bound, thr, cands, ccnt, raw, rawcnt;
-    int64_t cap = 0, ccap = 0, raw_cap = 0;
+    Buf tabs, adp, adp_off, adp_len, adp_meta, task, cnt, bound, thr, cands, ccnt, raw, rawcnt;
+    int pin_nc4[kCls] = {0, 0};                   // class c's pinned band slot (uint4 per lane), 0: band_best
+    int32_t n_adp = 0;
+    int64_t cap = 0, ecap = 0, ccap = 0, raw_cap = 0;
     int scan_blocks = 0;                          // resident k_seed_scan blocks
     int expand_blocks = 0;                        // resident k_seed_expand blocks
+    int pin_blocks[kCls] = {0, 0};                // resident k_seed_band_pin blocks per class
 };
 
 State *create() { return new State(); }
@@ -578,7 +828,7 @@ int plan(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hl
     const double th = (threshold - 1e-5) / 100.0;
     if (th <= 0.0 || th > 1.0) return 0;
     std::vector<std::vector<std::vector<int32_t>>> lists(kNK);
-    std::vector<int32_t> es((size_t)n_adp, -1);
+    std::vector<int32_t> es((size_t)n_adp, -1), pk((size_t)n_adp, 0);
     std::vector<int32_t> thr((size_t)n_adp, INT32_MAX);   // not under the filter: the caller adds them
     double filt = 0.0, seed = kScanPos;
     int e_lo = kMaxE + 1, e_hi = -1;
@@ -596,6 +846,7 @@ int plan(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hl
         const int K = std::min(kMaxK, plen);
         if (K < kMinK) return 0;
         es[a] = e;
+        pk[a] = K;
         thr[a] = T;
         e_lo = std::min(e_lo, e);
         e_hi = std::max(e_hi, e);
@@ -676,6 +927,12 @@ int plan(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hl
     A.estart_off = append16(estart);
     A.ent_off = (int32_t)img.size();
     for (int32_t x : ent) img.push_back((uint32_t)x);
+    // per entry the inside-band limits of its tasks (k_seed_band: d0 - E >= 1, d0 + E + L + 1 < len)
+    A.ent2_off = (int32_t)img.size();
+    for (int32_t x : ent) {
+        const int a = x >> 9, o = x & 255, E = s->band[(x >> 8) & 1];
+        img.push_back((uint32_t)(o + E + 1) | ((uint32_t)(hlen[a] - o + E + 1) << 16));
+    }
     A.tab_dw = (int32_t)img.size();
     s->lds_bytes = 4 * img.size();
     if (s->lds_bytes + 4096 > (size_t)kLdsMax) return 0;
@@ -695,8 +952,39 @@ int plan(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hl
     if (int rc = s->adp.ensure(flat.size())) return rc;
     if (int rc = s->adp_off.ensure(4 * aoff.size())) return rc;
     if (int rc = s->adp_len.ensure(4 * alen.size())) return rc;
-    if (int rc = s->cnt.ensure(4 * kCls)) return rc;
+    if (int rc = s->cnt.ensure(4 * kCnt)) return rc;
     if (int rc = s->thr.ensure(4 * thr.size())) return rc;
+    // the pinned band: adapters and their (offset, meta) in LDS, meta = L | K << 8 | T << 12
+    {
+        std::vector<int32_t> meta((size_t)n_adp, 0);
+        bool fits = s->adp_bytes <= kAdpLds && (size_t)n_adp * 8 <= (size_t)kAdpLds;
+        for (int32_t a = 0; a < n_adp && fits; ++a)
+            if (es[a] >= 0) {
+                if (thr[a] >= (1 << 19)) fits = false;
+                meta[a] = alen[a] | (pk[a] << 8) | (thr[a] << 12);
+            }
+        const char *e = std::getenv("PCABI_SEED_PIN");
+        const bool on = fits && !(e && e[0] == '0');
+        s->n_adp = n_adp;
+        for (int c = 0; c < kCls; ++c) {
+            // the slot holds the band's read range: L + 2E bytes from a 16-byte boundary, one more
+            int lmax = 0;
+            for (int32_t a = 0; a < n_adp; ++a)
+                if (es[a] >= 0 && cls[a] == c) lmax = std::max(lmax, alen[a]);
+            const int need = lmax + 2 * s->band[c] + 17;
+            s->pin_nc4[c] = 0;
+            if (on && s->band[c] <= kPinMaxE)
+                for (int nc4 : {4, 6, 8})
+                    if (16 * nc4 >= need) {
+                        s->pin_nc4[c] = nc4;
+                        break;
+                    }
+            A.pin_cls[c] = s->pin_nc4[c] ? 1 : 0;
+            s->pin_blocks[c] = 0;
+        }
+        if (int rc = s->adp_meta.ensure(4 * meta.size())) return rc;
+        SD_TRY(hipMemcpy(s->adp_meta.p, meta.data(), 4 * meta.size(), hipMemcpyHostToDevice));
+    }
     if (int rc = s->ccnt.ensure(8)) return rc;
     SD_TRY(hipMemcpy(s->tabs.p, img.data(), 4 * img.size(), hipMemcpyHostToDevice));
     SD_TRY(hipMemcpy(s->adp.p, flat.data(), flat.size(), hipMemcpyHostToDevice));
@@ -709,23 +997,111 @@ int plan(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hl
     return 0;
 }
 
-void launch_band(const State *s, int E, int c, const uint8_t *codes, const int64_t *v_off, const int32_t *v_len,
-                 const pcabi::Scoring &sc, int64_t n, unsigned grid, hipStream_t st) {
-    const int4 *task = (const int4 *)s->task.p + c * s->cap;
-    const int32_t *n_task = (const int32_t *)s->cnt.p + c;
+// One band class: its inside tasks (the pinned band when the plan allows, else band_best) and its
+// edge tasks (band_best with the read-end checks). n_in / n_edge: the host's task counts, or -1
+// when they live only on the device (the launches then stride over the device counts).
+template <int E, int NC4>
+int launch_pin(State *s, int c, const int4 *task, const uint8_t *codes, const pcabi::Scoring &sc, int64_t n,
+               int64_t n_in, hipStream_t st) {
+    const size_t lds = 16 * (((size_t)s->adp_bytes / 4 + 2 * (size_t)s->n_adp + 3) / 4) + 16 * 256 * (size_t)NC4;
+    if (!s->pin_blocks[c]) {
+        int dev = 0, cus = 0, per_cu = 0;
+        SD_TRY(hipGetDevice(&dev));
+        SD_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_band_pin<E, NC4>, 256, lds));
+        s->pin_blocks[c] = std::max(1, cus * std::max(1, per_cu));
+    }
+    const int64_t blocks = n_in >= 0 ? std::max<int64_t>(1, std::min<int64_t>((n_in + 255) / 256, s->pin_blocks[c]))
+                                     : s->pin_blocks[c];
+    hipLaunchKernelGGL((k_seed_band_pin<E, NC4>), dim3((unsigned)blocks), dim3(256), lds, st, task,
+                       (const int32_t *)s->cnt.p + c, s->cap, codes, (const uint8_t *)s->adp.p, s->adp_bytes / 4,
+                       (const int32_t *)s->adp_off.p, (const int32_t *)s->adp_meta.p, s->n_adp, sc,
+                       (int32_t *)s->bound.p, n);
+    return 0;
+}
+
+template <int E>
+int launch_pin_e(State *s, int c, const int4 *task, const uint8_t *codes, const pcabi::Scoring &sc, int64_t n,
+                 int64_t n_in, hipStream_t st) {
+    switch (s->pin_nc4[c]) {
+    case 4: return launch_pin<E, 4>(s, c, task, codes, sc, n, n_in, st);
+    case 6: return launch_pin<E, 6>(s, c, task, codes, sc, n, n_in, st);
+    default: return launch_pin<E, 8>(s, c, task, codes, sc, n, n_in, st);
+    }
+}
+
+// One band class: its inside tasks (the pinned band when the plan chose it, else band_best) and
+// its edge tasks (band_best with the read-end checks). n_in / n_edge: the host's task counts, or -1
+// when they live only on the device (the launches then stride over the device counts).
+int launch_band(State *s, int E, int c, const uint8_t *codes, const int64_t *v_off, const int32_t *v_len,
+                const pcabi::Scoring &sc, int64_t n, int64_t n_in, int64_t n_edge, hipStream_t st) {
+    const int4 *task = (const int4 *)s->task.p + c * (s->cap + s->ecap);
+    const int32_t *cnt = (const int32_t *)s->cnt.p;
     const uint8_t *adp = (const uint8_t *)s->adp.p;
     const int32_t *aoff = (const int32_t *)s->adp_off.p, *alen = (const int32_t *)s->adp_len.p;
     int32_t *bound = (int32_t *)s->bound.p;
     const int32_t lds = s->adp_bytes <= kAdpLds ? s->adp_bytes : 0;
+    auto grid_of = [](int64_t cnt_host, int64_t dflt) {
+        return (unsigned)(cnt_host >= 0 ? std::max<int64_t>(1, std::min<int64_t>((cnt_host + 255) / 256, dflt)) : dflt);
+    };
+    if (n_in != 0 && s->pin_nc4[c]) {
+        int rc = 0;
+        switch (E) {
+        case 1: rc = launch_pin_e<1>(s, c, task, codes, sc, n, n_in, st); break;
+        case 2: rc = launch_pin_e<2>(s, c, task, codes, sc, n, n_in, st); break;
+        case 3: rc = launch_pin_e<3>(s, c, task, codes, sc, n, n_in, st); break;
+        case 4: rc = launch_pin_e<4>(s, c, task, codes, sc, n, n_in, st); break;
+        case 5: rc = launch_pin_e<5>(s, c, task, codes, sc, n, n_in, st); break;
+        case 6: rc = launch_pin_e<6>(s, c, task, codes, sc, n, n_in, st); break;
+        case 7: rc = launch_pin_e<7>(s, c, task, codes, sc, n, n_in, st); break;
+        default: rc = launch_pin_e<kPinMaxE>(s, c, task, codes, sc, n, n_in, st); break;
+        }
+        if (rc) return rc;
+        n_in = 0;
+    }
     switch (E) {
-#define C(X)                                                                                                  \
-    case X:                                                                                                   \
-        hipLaunchKernelGGL(k_seed_band<X>, dim3(grid), dim3(256), (size_t)lds, st, task, n_task, s->cap, codes, \
-                           v_off, v_len, adp, lds, aoff, alen, sc, (const int32_t *)s->thr.p, bound, n);      \
+#define C(X)                                                                                                    \
+    case X:                                                                                                     \
+        if (n_in != 0)                                                                                          \
+            hipLaunchKernelGGL(k_seed_band<X>, dim3(grid_of(n_in, kBandGrid)), dim3(256), (size_t)lds, st, task,  \
+                               cnt + c, s->cap, codes, v_off, v_len, adp, lds, aoff, alen, sc,                  \
+                               (const int32_t *)s->thr.p, bound, n);                                            \
+        if (n_edge != 0)                                                                                        \
+            hipLaunchKernelGGL(k_seed_band<X>, dim3(grid_of(n_edge, 512)), dim3(256), (size_t)lds, st,           \
+                               task + s->cap, cnt + kCls + c, s->ecap, codes, v_off, v_len, adp, lds, aoff,     \
+                               alen, sc, (const int32_t *)s->thr.p, bound, n);                                  \
         break;
         C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8) C(9) C(10) C(11) C(12) C(13) C(14) C(15)
 #undef C
     }
+    SD_TRY(hipGetLastError());
+    return 0;
+}
+
+// Both band classes side by side (atomicMax into one bound array). c: host task counts (kCnt, as
+// the counters) or nullptr (device counts only).
+int launch_bands(State *s, const uint8_t *codes, const int64_t *v_off, const int32_t *v_len, const pcabi::Scoring &sc,
+                 int64_t n, const int32_t *c, hipStream_t st) {
+    auto in_of = [&](int k) { return c ? (int64_t)std::min<int64_t>(c[k], s->cap) : (int64_t)-1; };
+    auto edge_of = [&](int k) { return c ? (int64_t)std::min<int64_t>(c[kCls + k], s->ecap) : (int64_t)-1; };
+    const bool both = !c || ((c[0] || c[kCls]) && (c[1] || c[kCls + 1]));
+    if (both) {
+        if (!s->side) {
+            SD_TRY(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
+            SD_TRY(hipEventCreateWithFlags(&s->fork, hipEventDisableTiming));
+            SD_TRY(hipEventCreateWithFlags(&s->join, hipEventDisableTiming));
+        }
+        SD_TRY(hipEventRecord(s->fork, st));
+        SD_TRY(hipStreamWaitEvent(s->side, s->fork, 0));
+        if (int rc = launch_band(s, s->band[1], 1, codes, v_off, v_len, sc, n, in_of(1), edge_of(1), s->side)) return rc;
+        if (int rc = launch_band(s, s->band[0], 0, codes, v_off, v_len, sc, n, in_of(0), edge_of(0), st)) return rc;
+        SD_TRY(hipEventRecord(s->join, s->side));
+        SD_TRY(hipStreamWaitEvent(st, s->join, 0));
+    } else {
+        for (int k = 0; k < kCls; ++k)
+            if (int rc = launch_band(s, s->band[k], k, codes, v_off, v_len, sc, n, in_of(k), edge_of(k), st)) return rc;
+    }
+    return 0;
 }
 
 // Queue the seeds of one round on `st`: bounds reset, scan, expand, the band classes side by side.
@@ -746,10 +1122,11 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
     const int grid = s->scan_blocks;
     if (s->raw_cap == 0) s->raw_cap = (int64_t)grid * 4096;
     if (s->cap == 0) s->cap = 1 << 22;
+    s->ecap = std::max<int64_t>(s->cap / 4, 1 << 16);
     if (int rc = s->raw.ensure(sizeof(uint4) * (size_t)s->raw_cap)) return rc;
     if (int rc = s->rawcnt.ensure(4 * (size_t)grid)) return rc;
-    if (int rc = s->task.ensure(sizeof(int4) * kCls * (size_t)s->cap)) return rc;
-    if (int rc = s->cnt.ensure(4 * (kCls + 2))) return rc;
+    if (int rc = s->task.ensure(sizeof(int4) * kCls * (size_t)(s->cap + s->ecap))) return rc;
+    if (int rc = s->cnt.ensure(4 * kCnt)) return rc;
     if (int rc = s->bound.ensure(sizeof(int32_t) * (size_t)n * n_adp)) return rc;
     ScanArgs A = s->a;
     A.codes = codes;
@@ -762,55 +1139,38 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
     A.slab = (int32_t)std::min<int64_t>(s->raw_cap / grid, INT32_MAX);
     A.raw_cnt = (int32_t *)s->rawcnt.p;
     A.cnt = (int32_t *)s->cnt.p;
-    A.flags = A.cnt + kCls;
+    A.flags = A.cnt + kFlag;
     A.task = (int4 *)s->task.p;
     A.cap = s->cap;
+    A.ecap = s->ecap;
     if (int rc = s->ccnt.ensure(8)) return rc;
     hipLaunchKernelGGL(k_bound_reset, dim3(1024), dim3(256), 0, st, (int32_t *)s->bound.p, n, n_dev, n_adp, A.cnt,
-                       kCls + 2, (unsigned long long *)s->ccnt.p);
+                       kCnt, (unsigned long long *)s->ccnt.p);
     hipLaunchKernelGGL(k_seed_scan, dim3(grid), dim3(256), 4 * (size_t)A.bits_dw, st, A);
     hipLaunchKernelGGL(k_seed_expand, dim3(s->expand_blocks), dim3(256), s->lds_bytes, st, A);
     SD_TRY(hipGetLastError());
-    unsigned g[kCls];
-    for (int c = 0; c < kCls; ++c)
-        g[c] = tasks ? (unsigned)std::max<int64_t>(1, (std::min<int64_t>(tasks[c], s->cap) + 255) / 256) : kBandGrid;
-    if (!tasks || (tasks[0] && tasks[1])) {   // both classes: side by side (atomicMax into one bound array)
-        if (!s->side) {
-            SD_TRY(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
-            SD_TRY(hipEventCreateWithFlags(&s->fork, hipEventDisableTiming));
-            SD_TRY(hipEventCreateWithFlags(&s->join, hipEventDisableTiming));
-        }
-        SD_TRY(hipEventRecord(s->fork, st));
-        SD_TRY(hipStreamWaitEvent(s->side, s->fork, 0));
-        launch_band(s, s->band[1], 1, codes, v_off, v_len, sc, n, g[1], s->side);
-        launch_band(s, s->band[0], 0, codes, v_off, v_len, sc, n, g[0], st);
-        SD_TRY(hipEventRecord(s->join, s->side));
-        SD_TRY(hipStreamWaitEvent(st, s->join, 0));
-    } else {
-        for (int c = 0; c < kCls; ++c)
-            if (tasks[c]) launch_band(s, s->band[c], c, codes, v_off, v_len, sc, n, g[c], st);
-    }
-    SD_TRY(hipGetLastError());
-    return 0;
+    if (tasks) return 0;                                // the caller launches the bands (host counts)
+    return launch_bands(s, codes, v_off, v_len, sc, n, nullptr, st);
 }
 
 // Device -> host: the task counts and the overflow flags (synchronises `st`).
-int read_counts(State *s, int32_t (&out)[kCls + 2], hipStream_t st) {
+int read_counts(State *s, int32_t (&out)[kCnt], hipStream_t st) {
     SD_TRY(hipMemcpyAsync(out, s->cnt.p, sizeof(out), hipMemcpyDeviceToHost, st));
     SD_TRY(hipStreamSynchronize(st));
     return 0;
 }
 
 // Larger buffers after an overflow; false when they would pass sane limits.
-bool grow(State *s, const int32_t (&c)[kCls + 2]) {
-    if (c[2]) {
+bool grow(State *s, const int32_t (&c)[kCnt]) {
+    if (c[kFlag]) {
         if (s->raw_cap > (1ll << 31)) return false;
         s->raw_cap *= 2;
     }
-    if (c[3]) {
-        int64_t most = std::max<int64_t>(c[0], c[1]);
+    if (c[kFlag + 1]) {
+        int64_t most = 0;
+        for (int k = 0; k < kCls; ++k) most = std::max<int64_t>(most, std::max<int64_t>(c[k], 4 * (int64_t)c[kCls + k]));
         if (most > (1ll << 30)) return false;
-        s->cap = std::max<int64_t>(2 * s->cap, most + most / 4);
+        s->cap = std::max<int64_t>(2 * s->cap, most + most / 4);   // ecap follows (cap / 4)
     }
     return true;
 }
@@ -863,42 +1223,22 @@ int bounds(State *s, const void *adps_key, const uint8_t *hcodes, const int32_t 
     if (mode == 1 && !(s->cost_seed < 0.5 * s->cost_filter)) return 0;
     // the scan and the expansion, again with larger buffers after an overflow; then the band
     // launches sized from the task counts
-    int32_t c[kCls + 2];
+    int32_t c[kCnt];
     for (int tries = 0;; ++tries) {
         int32_t none[kCls] = {0, 0};
-        // scan + expand only: with both counts zero the band kernels are not queued
+        // scan + expand only (tasks given: the band kernels are not queued)
         if (int rc = enqueue_seeds(s, codes, v_off, v_len, n, nullptr, n_adp, sc, none, st)) return rc;
         if (int rc = read_counts(s, c, st)) return rc;
-        if (!c[2] && !c[3]) break;
+        if (!c[kFlag] && !c[kFlag + 1]) break;
         if (tries > 8 || !grow(s, c)) return fail(PCABI_E_DEVICE, "seed scan did not settle");
     }
     if (const char *dbg = std::getenv("PCABI_DEBUG"))
         if (dbg[0] == '1')
-            std::fprintf(stderr, "[pcabi] seeds: %lld windows, band tasks %d (E=%d) + %d (E=%d), scan grid %d\n",
-                         (long long)n, c[0], s->band[0], c[1], s->band[1], s->scan_blocks);
-    {
-        // the band classes from the counted tasks (the tasks are still in place)
-        int32_t tasks[kCls] = {c[0], c[1]};
-        unsigned g[kCls];
-        for (int k = 0; k < kCls; ++k) g[k] = (unsigned)std::max<int64_t>(1, (tasks[k] + 255) / 256);
-        if (tasks[0] && tasks[1]) {
-            if (!s->side) {
-                SD_TRY(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
-                SD_TRY(hipEventCreateWithFlags(&s->fork, hipEventDisableTiming));
-                SD_TRY(hipEventCreateWithFlags(&s->join, hipEventDisableTiming));
-            }
-            SD_TRY(hipEventRecord(s->fork, st));
-            SD_TRY(hipStreamWaitEvent(s->side, s->fork, 0));
-            launch_band(s, s->band[1], 1, codes, v_off, v_len, sc, n, g[1], s->side);
-            launch_band(s, s->band[0], 0, codes, v_off, v_len, sc, n, g[0], st);
-            SD_TRY(hipEventRecord(s->join, s->side));
-            SD_TRY(hipStreamWaitEvent(st, s->join, 0));
-        } else {
-            for (int k = 0; k < kCls; ++k)
-                if (tasks[k]) launch_band(s, s->band[k], k, codes, v_off, v_len, sc, n, g[k], st);
-        }
-        SD_TRY(hipGetLastError());
-    }
+            std::fprintf(stderr, "[pcabi] seeds: %lld windows, band tasks %d + %d edge (E=%d), %d + %d edge (E=%d), "
+                         "scan grid %d, pinned slots %d\n", (long long)n, c[0], c[kCls], s->band[0], c[1], c[kCls + 1],
+                         s->band[1], s->scan_blocks, s->pin_nc4[0] * 10 + s->pin_nc4[1]);
+    // the band classes from the counted tasks (the tasks are still in place)
+    if (int rc = launch_bands(s, codes, v_off, v_len, sc, n, c, st)) return rc;
     const int64_t tot = n * (int64_t)n_adp;
     if (!cands && !dcands) {
         hipLaunchKernelGGL(k_bound16, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, (const int32_t *)s->bound.p,
@@ -956,7 +1296,7 @@ int bounds_dev(State *s, const uint8_t *codes, const int64_t *v_off, const int32
     SD_TRY(hipGetLastError());
     *dcands = (const int64_t *)s->cands.p;
     *dcount = (const unsigned long long *)s->ccnt.p;
-    *flags = (const int32_t *)s->cnt.p + kCls;
+    *flags = (const int32_t *)s->cnt.p + kFlag;
     g_runs.fetch_add(1);
     return 0;
 }
@@ -964,21 +1304,26 @@ int bounds_dev(State *s, const uint8_t *codes, const int64_t *v_off, const int32
 // After a device-resident run reported an overflow (flags from bounds_dev, read by the caller):
 // larger buffers for the rerun. Returns false past the limits.
 bool grow_after_overflow(State *s, int raw_overflow, int task_overflow) {
-    int32_t c[kCls + 2] = {(int32_t)std::min<int64_t>(4 * s->cap, INT32_MAX), 0, raw_overflow, task_overflow};
+    int32_t c[kCnt] = {};
+    c[0] = (int32_t)std::min<int64_t>(4 * s->cap, INT32_MAX);
+    c[kFlag] = raw_overflow;
+    c[kFlag + 1] = task_overflow;
     return grow(s, c);
 }
 
-// Debugging (PCABI_DEBUG=1): the last queued seeding's band task counts per class and candidate
-// count (synchronises `st`).
-int debug_counts(State *s, int64_t (&out)[3], hipStream_t st) {
-    int32_t c[kCls + 2] = {0, 0, 0, 0};
+// Debugging (PCABI_DEBUG=1): the last queued seeding's band task counts per class (inside, edge)
+// and candidate count (synchronises `st`).
+int debug_counts(State *s, int64_t (&out)[5], hipStream_t st) {
+    int32_t c[kCnt] = {};
     unsigned long long nc = 0;
     SD_TRY(hipMemcpyAsync(c, s->cnt.p, sizeof(c), hipMemcpyDeviceToHost, st));
     SD_TRY(hipMemcpyAsync(&nc, s->ccnt.p, 8, hipMemcpyDeviceToHost, st));
     SD_TRY(hipStreamSynchronize(st));
     out[0] = c[0];
-    out[1] = c[1];
-    out[2] = (int64_t)nc;
+    out[1] = c[kCls];
+    out[2] = c[1];
+    out[3] = c[kCls + 1];
+    out[4] = (int64_t)nc;
     return 0;
 }
 

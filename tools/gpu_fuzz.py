@@ -95,6 +95,9 @@ def main():
                                ('PCABI_MIDDLE_DEVPLAN', '0'), ('PCABI_MIDDLE_PLAN_WAVES', '1'),
                                ('PCABI_MIDDLE_PLAN_WAVES', '100000000'), ('PCABI_MIDDLE_FILTER', '0')])
             os.environ[mode[0]] = mode[1]
+            if os.environ.get('FUZZ_VERBOSE'):
+                print('case %d: scheme %s threshold %s mode %s, %d reads (longest %d), adapters %s' %
+                      (seed, sc, th, mode, len(reads), max(map(len, reads)), [len(a) for a in adps]), flush=True)
             try:
                 got = engine.middle_scan(views, adps, sc, th)
             finally:
