@@ -62,6 +62,10 @@ int bucket_of(int L, const pcabi::Scoring &sc, bool allow_wide = true) {
         const int b = L <= 96 ? 22 : (L <= 112 ? 23 : 24);
         if (pcabi::long_ok(L, kBuckets[b].rpl, sc)) return b;
     }
+    // The generic core keeps every row's state in registers: past 64 rows under affine gaps it
+    // spills (k_align<96 / 128, true, 1>: hundreds of VGPRs to scratch) and runs slower than the
+    // striped core, which holds 32 rows at a time.
+    if (L > 64 && sc.go != sc.ge) return kStripedBucket;
     for (int b = 0; b < kNumBuckets; ++b)
         if (kBuckets[b].kind == GENERIC && L <= kBuckets[b].rpl) return b;
     return -1;
@@ -384,7 +388,7 @@ __global__ __launch_bounds__(256) void k_plan_place(const int64_t *cand, int64_t
                                                     const int32_t *v_len, const int32_t *start, const int32_t *span,
                                                     const int32_t *cidx, const int64_t *wave_off, int32_t *fill,
                                                     int32_t *tw, int32_t *to, int4 *tck, int32_t *tcand,
-                                                    const int64_t *slots_dev) {
+                                                    const int64_t *slots_dev, int32_t *cbase_out) {
     const int64_t ncl = nc_dev ? min((int64_t)*nc_dev, nc) : nc;
     const int64_t slots = slots_dev ? *slots_dev : INT64_MAX;
     const int lane = threadIdx.x & 63;
@@ -415,10 +419,48 @@ __global__ __launch_bounds__(256) void k_plan_place(const int64_t *cand, int64_t
             if (mine) base = wave_off[a0] * 64 + b1 + (incl - x);
             pending &= ~__ballot(mine);
         }
+        if (cbase_out) {                             // the tasks are written by k_plan_fill
+            if (i < ncl) cbase_out[i] = active ? (int32_t)base : -1;
+            continue;
+        }
         if (!active) continue;
         const int C = 64 << c;
         for (int t = 0; t < nt; ++t) {
             const int64_t q = base + t;
+            if (q >= slots) break;
+            int4 ck = make_int4(0, 0, 0, 0);
+            if (D >= 0) {                            // sf::chunk_plan, chunk t
+                const int lo = 1 + t * C, hi = lo + C;
+                const int st = max(0, lo - 1 - D);
+                ck = hi > n ? make_int4(st, n - st, lo - st, -1) : make_int4(st, hi - 1 - st, lo - st, hi - st);
+            }
+            tw[q] = k;
+            to[q] = (int32_t)q;
+            tck[q] = ck;
+            tcand[q] = (int32_t)i;
+        }
+    }
+}
+
+// The task slots of k_plan_place's candidates, one wave per candidate (its lanes over the chunks):
+// a read of 8 kb has 63 chunks of 128 columns, which one lane wrote one after another.
+__global__ __launch_bounds__(256) void k_plan_fill(const int64_t *cand, int64_t nc, const unsigned long long *nc_dev,
+                                                   const int32_t *v_len, const int32_t *span, const int32_t *cidx,
+                                                   const int32_t *cbase, int32_t *tw, int32_t *to, int4 *tck,
+                                                   int32_t *tcand, const int64_t *slots_dev) {
+    const int64_t ncl = nc_dev ? min((int64_t)*nc_dev, nc) : nc;
+    const int64_t slots = *slots_dev;
+    const int lane = threadIdx.x & 63;
+    const int64_t waves = (int64_t)gridDim.x * 4;
+    for (int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < ncl; i += waves) {
+        const int32_t base = cbase[i];
+        if (base < 0) continue;                      // wave-uniform
+        const int64_t key = cand[i];
+        const int32_t a = (int32_t)(key >> 32), k = (int32_t)(key & 0xFFFFFFFF);
+        const int n = v_len[k], D = span[a], c = cidx[a];
+        const int nt = plan_tasks(n, D, c), C = 64 << c;
+        for (int t = lane; t < nt; t += 64) {
+            const int64_t q = (int64_t)base + t;
             if (q >= slots) break;
             int4 ck = make_int4(0, 0, 0, 0);
             if (D >= 0) {                            // sf::chunk_plan, chunk t
@@ -947,7 +989,9 @@ struct pcabi_scan {
     pcabi_seed::State *seed = nullptr; // seeded round-1 bounds (pcabi_seed.hip)
     // queued rounds (middle_device_rounds): per round slot the reads, their start adapters and the
     // hit list; round counts and flags; the plan's bucket tables and scratch
-    DeviceBuf q_cur, q_start, q_list, q_n, q_flags, q_bk, q_wave, q_misc;
+    DeviceBuf q_cur, q_start, q_list, q_n, q_flags, q_bk, q_wave, q_misc, pcbase;
+    int32_t *h_stage = nullptr;                     // pinned host staging of the queued rounds' hit lists
+    size_t h_stage_cap = 0;                         // (int32 elements)
     int64_t q_slots_cap = 0;
 };
 
@@ -1745,8 +1789,9 @@ void pcabi_scan_destroy(pcabi_scan *s) {
                          &s->mwin, &s->ms, &s->me, &s->s16, &s->tw, &s->to, &s->wa, &s->pres, &s->tck,
                          &s->pspan, &s->ptasks, &s->pfill, &s->pwoff, &s->pcidx, &s->pcand, &s->pbest, &s->phit, &s->phb,
                          &s->plist, &s->pcnt, &s->q_cur, &s->q_start, &s->q_list, &s->q_n, &s->q_flags,
-                         &s->q_bk, &s->q_wave, &s->q_misc})
+                         &s->q_bk, &s->q_wave, &s->q_misc, &s->pcbase})
         if (b->p) (void)hipFree(b->p);
+    if (s->h_stage) (void)hipHostFree(s->h_stage);
     if (s->seed) pcabi_seed::destroy(s->seed);
     delete s;
 }
@@ -1883,7 +1928,8 @@ int device_plan_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_off,
     hipLaunchKernelGGL(k_plan_place, dim3(gc), dim3(256), 0, st, dcand, nc, nullptr, v_len, d_start,
                        (const int32_t *)sc->pspan.p, (const int32_t *)sc->pcidx.p, (const int64_t *)sc->pwoff.p,
                        (int32_t *)sc->pfill.p,
-                       (int32_t *)sc->tw.p, (int32_t *)sc->to.p, (int4 *)sc->tck.p, (int32_t *)sc->pcand.p, nullptr);
+                       (int32_t *)sc->tw.p, (int32_t *)sc->to.p, (int4 *)sc->tck.p, (int32_t *)sc->pcand.p, nullptr,
+                       nullptr);
     HIP_TRY(hipGetLastError());
     KParams p{};
     p.codes = codes;
@@ -2323,6 +2369,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
     if (int rc = sc->phit.ensure(sizeof(int32_t) * n)) return rc;
     if (int rc = sc->phb.ensure(sizeof(int32_t) * 5 * n)) return rc;
     if (int rc = sc->pbest.ensure(sizeof(unsigned long long) * n * n_adp)) return rc;
+    if (int rc = sc->pcbase.ensure(sizeof(int32_t) * n * n_adp)) return rc;
     if (int rc = sc->q_bk.ensure(4 * (bk_first.size() + 2 * bk_adp.size() + 2 * (size_t)n_bk + 16))) return rc;
     if (int rc = sc->q_misc.ensure(64)) return rc;   // [0] slots (int64), [8] need (int64), [16] plan flag
     int32_t *d_bk_first = (int32_t *)sc->q_bk.p, *d_bk_adp = d_bk_first + bk_first.size();
@@ -2383,7 +2430,11 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
         hipLaunchKernelGGL(k_plan_place, dim3(kGrid), dim3(256), 0, st, dcand, ncap, dcount, v_len, start,
                            (const int32_t *)sc->pspan.p, (const int32_t *)sc->pcidx.p, (const int64_t *)sc->pwoff.p,
                            (int32_t *)sc->pfill.p, (int32_t *)sc->tw.p, (int32_t *)sc->to.p, (int4 *)sc->tck.p,
-                           (int32_t *)sc->pcand.p, (const int64_t *)d_slots);
+                           (int32_t *)sc->pcand.p, (const int64_t *)d_slots, (int32_t *)sc->pcbase.p);
+        hipLaunchKernelGGL(k_plan_fill, dim3(kGrid), dim3(256), 0, st, dcand, ncap, dcount, v_len,
+                           (const int32_t *)sc->pspan.p, (const int32_t *)sc->pcidx.p, (const int32_t *)sc->pcbase.p,
+                           (int32_t *)sc->tw.p, (int32_t *)sc->to.p, (int4 *)sc->tck.p, (int32_t *)sc->pcand.p,
+                           (const int64_t *)d_slots);
         HIP_TRY(hipGetLastError());
         KParams p{};
         p.codes = codes;
@@ -2464,13 +2515,30 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
         for (int r = slot; r < queued_to && bad < 0; ++r)
             if (h_flag[r]) bad = r;
         int done_to = bad >= 0 ? bad : queued_to;    // rounds [slot, done_to) are final
-        for (int r = slot; r < done_to; ++r) {
-            const int32_t nh = h_n[r + 1];
-            if (!nh) continue;
-            const size_t at = out.size();
-            out.resize(at + 8 * (size_t)nh);
-            HIP_TRY(hipMemcpyAsync(out.data() + at, list_of(r), 32 * (size_t)nh, hipMemcpyDeviceToHost, st));
-            out_round.insert(out_round.end(), (size_t)nh, round_base + r);
+        {
+            // the finished rounds' lists, through pinned staging (one synchronisation)
+            size_t want = 0;
+            for (int r = slot; r < done_to; ++r) want += 8 * (size_t)h_n[r + 1];
+            if (want > sc->h_stage_cap) {
+                if (sc->h_stage) HIP_TRY(hipHostFree(sc->h_stage));
+                sc->h_stage = nullptr;
+                sc->h_stage_cap = 0;
+                const size_t cap2 = std::max<size_t>(want, 1 << 16);
+                HIP_TRY(hipHostMalloc((void **)&sc->h_stage, 4 * cap2, hipHostMallocDefault));
+                sc->h_stage_cap = cap2;
+            }
+            size_t at = 0;
+            for (int r = slot; r < done_to; ++r) {
+                const int32_t nh = h_n[r + 1];
+                if (!nh) continue;
+                HIP_TRY(hipMemcpyAsync(sc->h_stage + at, list_of(r), 32 * (size_t)nh, hipMemcpyDeviceToHost, st));
+                at += 8 * (size_t)nh;
+                out_round.insert(out_round.end(), (size_t)nh, round_base + r);
+            }
+            if (at) {
+                HIP_TRY(hipStreamSynchronize(st));
+                out.insert(out.end(), sc->h_stage, sc->h_stage + at);
+            }
         }
         if (g_debug)
             for (int r = slot; r < queued_to; ++r)
@@ -2536,16 +2604,24 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
         ~TableSwap() { s->adps = own; }
     } swap_back{sc, sc->adps};
     std::vector<int32_t> h_len_copy;
-    if (!h_win_len) {                               // lengths only on the device: one small copy
+    auto host_lengths = [&]() -> int {              // lengths only on the device: one small copy
+        if (h_win_len) return 0;
         h_len_copy.resize((size_t)n_win);
         HIP_TRY(hipMemcpyAsync(h_len_copy.data(), win_len, 4 * (size_t)n_win, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         h_win_len = h_len_copy.data();
-    }
+        return 0;
+    };
     const pcabi::Scoring scoring{match, mismatch, gap_open, gap_extend};
     {
-        int32_t longest = 0;
-        for (int64_t k = 0; k < n_win; ++k) longest = std::max(longest, h_win_len[k]);
+        // the longest window decides the layout only when the table may not serve every length
+        // (a scoring without a span bound): otherwise no length needs to come to the host
+        int32_t longest = INT32_MAX / 2;
+        if (!layout_serves(sc->adps, scoring, longest)) {
+            if (int rc = host_lengths()) return rc;
+            longest = 0;
+            for (int64_t k = 0; k < n_win; ++k) longest = std::max(longest, h_win_len[k]);
+        }
         const pcabi_adapters *use = nullptr;
         if (int rc = adapters_for(sc->adps, scoring, longest, &use)) return rc;
         sc->adps = use;
@@ -2555,6 +2631,7 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
         const int64_t r = middle_device_rounds(sc, codes, win_off, win_len, n_win, scoring, threshold, hits, cap, st, applied);
         if (applied || r < 0) return r;
     }
+    if (int rc = host_lengths()) return rc;
     int64_t n_hits = 0;
     std::vector<int32_t> cur, nxt, nxt_start, hm_w, hm_s, hm_e, lens;
     std::vector<int32_t> hb;

@@ -781,10 +781,12 @@ struct Buf {
 
 struct State {
     // the second band class runs beside the first on a side stream (fork / join by events)
-    hipStream_t side = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
+    hipStream_t side = nullptr, side2 = nullptr;   // class 1's inside tasks; both classes' edge tasks
+    hipEvent_t fork = nullptr, join = nullptr, join2 = nullptr;
     ~State() {
         if (side) (void)hipStreamDestroy(side);
+        if (side2) (void)hipStreamDestroy(side2);
+        if (join2) (void)hipEventDestroy(join2);
         if (fork) (void)hipEventDestroy(fork);
         if (join) (void)hipEventDestroy(join);
     }
@@ -1034,7 +1036,7 @@ int launch_pin_e(State *s, int c, const int4 *task, const uint8_t *codes, const 
 // its edge tasks (band_best with the read-end checks). n_in / n_edge: the host's task counts, or -1
 // when they live only on the device (the launches then stride over the device counts).
 int launch_band(State *s, int E, int c, const uint8_t *codes, const int64_t *v_off, const int32_t *v_len,
-                const pcabi::Scoring &sc, int64_t n, int64_t n_in, int64_t n_edge, hipStream_t st) {
+                const pcabi::Scoring &sc, int64_t n, int64_t n_in, int64_t n_edge, hipStream_t st, hipStream_t st_edge) {
     const int4 *task = (const int4 *)s->task.p + c * (s->cap + s->ecap);
     const int32_t *cnt = (const int32_t *)s->cnt.p;
     const uint8_t *adp = (const uint8_t *)s->adp.p;
@@ -1067,7 +1069,7 @@ int launch_band(State *s, int E, int c, const uint8_t *codes, const int64_t *v_o
                                cnt + c, s->cap, codes, v_off, v_len, adp, lds, aoff, alen, sc,                  \
                                (const int32_t *)s->thr.p, bound, n);                                            \
         if (n_edge != 0)                                                                                        \
-            hipLaunchKernelGGL(k_seed_band<X>, dim3(grid_of(n_edge, 512)), dim3(256), (size_t)lds, st,           \
+            hipLaunchKernelGGL(k_seed_band<X>, dim3(grid_of(n_edge, 512)), dim3(256), (size_t)lds, st_edge,      \
                                task + s->cap, cnt + kCls + c, s->ecap, codes, v_off, v_len, adp, lds, aoff,     \
                                alen, sc, (const int32_t *)s->thr.p, bound, n);                                  \
         break;
@@ -1084,23 +1086,26 @@ int launch_bands(State *s, const uint8_t *codes, const int64_t *v_off, const int
                  int64_t n, const int32_t *c, hipStream_t st) {
     auto in_of = [&](int k) { return c ? (int64_t)std::min<int64_t>(c[k], s->cap) : (int64_t)-1; };
     auto edge_of = [&](int k) { return c ? (int64_t)std::min<int64_t>(c[kCls + k], s->ecap) : (int64_t)-1; };
-    const bool both = !c || ((c[0] || c[kCls]) && (c[1] || c[kCls + 1]));
-    if (both) {
-        if (!s->side) {
-            SD_TRY(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
-            SD_TRY(hipEventCreateWithFlags(&s->fork, hipEventDisableTiming));
-            SD_TRY(hipEventCreateWithFlags(&s->join, hipEventDisableTiming));
-        }
-        SD_TRY(hipEventRecord(s->fork, st));
-        SD_TRY(hipStreamWaitEvent(s->side, s->fork, 0));
-        if (int rc = launch_band(s, s->band[1], 1, codes, v_off, v_len, sc, n, in_of(1), edge_of(1), s->side)) return rc;
-        if (int rc = launch_band(s, s->band[0], 0, codes, v_off, v_len, sc, n, in_of(0), edge_of(0), st)) return rc;
-        SD_TRY(hipEventRecord(s->join, s->side));
-        SD_TRY(hipStreamWaitEvent(st, s->join, 0));
-    } else {
-        for (int k = 0; k < kCls; ++k)
-            if (int rc = launch_band(s, s->band[k], k, codes, v_off, v_len, sc, n, in_of(k), edge_of(k), st)) return rc;
+    if (!s->side) {
+        SD_TRY(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
+        SD_TRY(hipStreamCreateWithFlags(&s->side2, hipStreamNonBlocking));
+        SD_TRY(hipEventCreateWithFlags(&s->fork, hipEventDisableTiming));
+        SD_TRY(hipEventCreateWithFlags(&s->join, hipEventDisableTiming));
+        SD_TRY(hipEventCreateWithFlags(&s->join2, hipEventDisableTiming));
     }
+    // class 0's inside tasks on `st`, class 1's on a side stream, the (few, latency-bound) edge tasks
+    // of both on a second side stream: the three run side by side (atomicMax into one bound array)
+    SD_TRY(hipEventRecord(s->fork, st));
+    SD_TRY(hipStreamWaitEvent(s->side, s->fork, 0));
+    SD_TRY(hipStreamWaitEvent(s->side2, s->fork, 0));
+    if (int rc = launch_band(s, s->band[1], 1, codes, v_off, v_len, sc, n, in_of(1), edge_of(1), s->side, s->side2))
+        return rc;
+    if (int rc = launch_band(s, s->band[0], 0, codes, v_off, v_len, sc, n, in_of(0), edge_of(0), st, s->side2))
+        return rc;
+    SD_TRY(hipEventRecord(s->join, s->side));
+    SD_TRY(hipEventRecord(s->join2, s->side2));
+    SD_TRY(hipStreamWaitEvent(st, s->join, 0));
+    SD_TRY(hipStreamWaitEvent(st, s->join2, 0));
     return 0;
 }
 
