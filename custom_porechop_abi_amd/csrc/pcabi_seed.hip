@@ -418,16 +418,26 @@ __global__ __launch_bounds__(256) void k_seed_expand(ScanArgs a) {
 // The band's read bytes as a stream: rd[p], rd[p + 1], ... one dword load per 4 bytes, issued one
 // dword ahead (the band DP of a random probe hit usually stops within a dozen rows, so the first
 // loads cover most tasks). Reads at most 11 bytes past the last byte taken.
+// CLAMP (edge bands, which run off the read): every dword address is clamped into [lo, hi] --
+// the bytes outside the read are masked by the caller, so their values do not matter, but no load
+// leaves the codes buffer.
+template <bool CLAMP>
 struct ByteStream {
     const uint32_t *q;
     uint64_t buf;
     uint32_t nx;
     int o;
-    __device__ __forceinline__ explicit ByteStream(const uint8_t *p) {
+    uintptr_t lo, hi;
+    __device__ __forceinline__ uint32_t ld(const uint32_t *a) const {
+        if (!CLAMP) return *a;
+        const uintptr_t x = (uintptr_t)a;
+        return *reinterpret_cast<const uint32_t *>(x < lo ? lo : (x > hi ? hi : x));
+    }
+    __device__ __forceinline__ ByteStream(const uint8_t *p, uintptr_t lo_ = 0, uintptr_t hi_ = 0) : lo(lo_), hi(hi_) {
         const int a0 = (int)((uintptr_t)p & 3);
         q = reinterpret_cast<const uint32_t *>(p - a0);
-        buf = ((uint64_t)q[1] << 32) | q[0];
-        nx = q[2];
+        buf = ((uint64_t)ld(q + 1) << 32) | ld(q);
+        nx = ld(q + 2);
         q += 3;
         o = 8 * a0;
     }
@@ -436,7 +446,7 @@ struct ByteStream {
         o += 8;
         if (o == 32) {
             buf = (buf >> 32) | ((uint64_t)nx << 32);
-            nx = *q++;
+            nx = ld(q++);
             o = 0;
         }
         return v;
@@ -454,17 +464,20 @@ struct ByteStream {
 // compares). Random probe hits -- most tasks -- stop early.
 template <int E, bool CHECK>
 __device__ __forceinline__ int band_best(const uint8_t *rd, int len, const uint8_t *ac, int L, int d0,
-                                         const pcabi::Scoring &sc, int T) {
+                                         const pcabi::Scoring &sc, int T, const uint8_t *codes) {
     constexpr int W = 2 * E + 1;
     int S[W], V[W], R[W];
-    ByteStream bs(rd + (CHECK ? 0 : d0 - E));          // inside bands: rd[d0 - E] onwards
+    // rd[d0 - E] onwards; an edge band's columns outside 1 .. len are masked (7 never matches) and
+    // its loads stay inside [codes, rd + len] (the buffer's start; the read's end)
+    ByteStream<CHECK> bs(rd + (d0 - E), (uintptr_t)codes & ~(uintptr_t)3, ((uintptr_t)(rd + len)) & ~(uintptr_t)3);
 #pragma unroll
     for (int x = 0; x < W; ++x) {
         const int j0 = d0 + x - E;                           // row 0
         S[x] = (!CHECK || (j0 >= 0 && j0 <= len)) ? 0 : kNeg;
         V[x] = kNeg;
         const int j1 = j0 + 1;                               // row 1's read column
-        R[x] = CHECK ? ((j1 >= 1 && j1 <= len) ? rd[j1 - 1] : 7) : bs.next();
+        const int v = bs.next();
+        R[x] = CHECK ? ((j1 >= 1 && j1 <= len) ? v : 7) : v;
     }
     int best = 0;                                            // S(L, 0) = 0 is always scouted
     for (int i = 1; i <= L; ++i) {
@@ -489,8 +502,10 @@ __device__ __forceinline__ int band_best(const uint8_t *rd, int len, const uint8
 #pragma unroll
         for (int x = 0; x + 1 < W; ++x) R[x] = R[x + 1];
         const int jn = i + 1 + d0 + E;
-        if (CHECK) R[W - 1] = (jn >= 1 && jn <= len) ? rd[jn - 1] : 7;
-        else if (i < L) R[W - 1] = bs.next();
+        if (i < L) {
+            const int v = bs.next();
+            R[W - 1] = CHECK ? ((jn >= 1 && jn <= len) ? v : 7) : v;
+        }
         if (!CHECK && (i % PCABI_BAND_EXIT) == 0) {
             int mx = S[0];
 #pragma unroll
@@ -532,8 +547,8 @@ __global__ __launch_bounds__(256) void k_seed_band(const int4 *task, const int32
         const uint8_t *ac = ad + adp_off[tk.y];
         const bool inside = d0 - E >= 1 && d0 + E + L + 1 < len;
         const int T = thr[tk.y];
-        const int best = inside ? band_best<E, false>(rd, len, ac, L, d0, sc, T)
-                                : band_best<E, true>(rd, len, ac, L, d0, sc, T);
+        const int best = inside ? band_best<E, false>(rd, len, ac, L, d0, sc, T, codes)
+                                : band_best<E, true>(rd, len, ac, L, d0, sc, T, codes);
         atomicMax(&bound[(int64_t)tk.y * n + tk.x], best);
     }
 }
@@ -1098,10 +1113,13 @@ int launch_bands(State *s, const uint8_t *codes, const int64_t *v_off, const int
     SD_TRY(hipEventRecord(s->fork, st));
     SD_TRY(hipStreamWaitEvent(s->side, s->fork, 0));
     SD_TRY(hipStreamWaitEvent(s->side2, s->fork, 0));
-    if (int rc = launch_band(s, s->band[1], 1, codes, v_off, v_len, sc, n, in_of(1), edge_of(1), s->side, s->side2))
-        return rc;
-    if (int rc = launch_band(s, s->band[0], 0, codes, v_off, v_len, sc, n, in_of(0), edge_of(0), st, s->side2))
-        return rc;
+    // (submission order: the inside launches first -- streams may share a hardware queue, and the
+    // edge launches are the ones that can wait)
+    if (int rc = launch_band(s, s->band[0], 0, codes, v_off, v_len, sc, n, in_of(0), 0, st, s->side2)) return rc;
+    if (int rc = launch_band(s, s->band[1], 1, codes, v_off, v_len, sc, n, in_of(1), 0, s->side, s->side2)) return rc;
+    for (int k = 0; k < kCls; ++k)
+        if (int rc = launch_band(s, s->band[k], k, codes, v_off, v_len, sc, n, 0, edge_of(k), s->side2, s->side2))
+            return rc;
     SD_TRY(hipEventRecord(s->join, s->side));
     SD_TRY(hipEventRecord(s->join2, s->side2));
     SD_TRY(hipStreamWaitEvent(st, s->join, 0));
