@@ -696,7 +696,12 @@ def run_drivers(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
 
     def counted(*a, **kw):                  # the end-trim driver's device -> host bytes
         st, et, sl, el, bcf = real(*a, **kw)
-        d2h['bytes'] = st.nbytes + et.nbytes + sl.nbytes + el.nbytes + (bcf.nbytes if bcf is not None else 0) + 16
+        # pcabi_end_decisions_host's transfer (windows < 32 k, < 32 k adapters): the trims, the two
+        # alignment counts, per side 12 B per alignment (six int16 fields) + 2 B per read (counts),
+        # the barcode identities
+        n = len(st)
+        d2h['bytes'] = (st.nbytes + et.nbytes + 16 + 12 * (sl.shape[1] + el.shape[1]) + 2 * 4 * ((n + 1) // 2)
+                        + (bcf.nbytes if bcf is not None else 0))
         return st, et, sl, el, bcf
 
     def drivers(reads, times):

@@ -1071,7 +1071,7 @@ struct Engine {
     DeviceBuf pad[kNumBuckets], len[kNumBuckets], id[kNumBuckets];
     // pcabi_end_decisions_host: both sides' windows, results, trims, flags and lists; the two
     // sides' prepared adapter tables, kept while the adapters and the scoring stay the same
-    DeviceBuf dec[16];
+    DeviceBuf dec[17];
     struct DTab {
         std::vector<uint8_t> codes;
         std::vector<int32_t> lens;
@@ -3059,6 +3059,20 @@ __global__ __launch_bounds__(256) void k_full_ids(const int32_t *res, int64_t st
     out[i] = res[q] == -1 ? 0.0 : pcabi::pid6(res[5 * stride + q], res[7 * stride + q]);
 }
 
+// The compact form of a side's alignment list for the D2H (pcabi_end_decisions_host): per
+// alignment six int16 (adapter, rs, re, m, l1, l2), per read its alignment count (uint16, two per
+// dword); the read row is rebuilt on the host from the counts (the list is read-major). 12 B per
+// alignment + 2 B per read instead of 28 B per alignment.
+__global__ __launch_bounds__(256) void k_list_pack(const int32_t *list, int64_t dcap, int64_t cnt, int16_t *out,
+                                                   uint32_t *counts) {
+    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < cnt; k += (int64_t)gridDim.x * 256) {
+        const int32_t r = list[k];
+#pragma unroll
+        for (int f = 0; f < 6; ++f) out[f * cnt + k] = (int16_t)list[(f + 1) * dcap + k];
+        atomicAdd(&counts[r >> 1], 1u << (16 * (r & 1)));
+    }
+}
+
 int side_table(Engine::DTab &c, const uint8_t *codes, const int32_t *off, const int32_t *len, int32_t n,
                const pcabi::Scoring &sc, pcabi_adapters **out) {
     std::vector<uint8_t> key;
@@ -3199,6 +3213,46 @@ extern "C" int pcabi_end_decisions_host(
     HIP_TRY(hipStreamSynchronize(st));
     n_hits[0] = (int64_t)cnt[0];
     n_hits[1] = (int64_t)cnt[1];
+    // the lists: compact (int16 fields, per-read counts) when every field fits 16 bits
+    int32_t max_win = 0;
+    for (size_t w = 0; w < n; ++w) max_win = std::max(max_win, std::max(s_len[w], e_len[w]));
+    const bool compact = max_win < 32768 && n_sa < 32768 && n_ea < 32768;
+    const size_t half = (n + 1) / 2;                // count dwords per side
+    if (compact) {
+        size_t words = 0;
+        for (int side = 0; side < 2; ++side)
+            if ((int64_t)cnt[side] <= cap) words += 3 * (size_t)cnt[side] + half;   // 6 int16 = 3 dwords
+        if (int rc = e.dec[16].ensure(4 * words + 64)) return rc;
+        std::vector<uint32_t> h((size_t)words);
+        size_t at = 0, at_side[2] = {0, 0};
+        for (int side = 0; side < 2; ++side) {
+            const int64_t k = (int64_t)cnt[side];
+            if (k > cap) continue;
+            at_side[side] = at;
+            uint32_t *dc = (uint32_t *)e.dec[16].p + at + 3 * (size_t)k;
+            HIP_TRY(hipMemsetAsync(dc, 0, 4 * half, st));
+            if (k)
+                hipLaunchKernelGGL(k_list_pack, dim3((unsigned)std::min<int64_t>((k + 255) / 256, 4096)), dim3(256), 0, st,
+                                   d_list[side], (int64_t)dcap[side], k, (int16_t *)((uint32_t *)e.dec[16].p + at), dc);
+            at += 3 * (size_t)k + half;
+        }
+        HIP_TRY(hipGetLastError());
+        if (words) HIP_TRY(hipMemcpyAsync(h.data(), e.dec[16].p, 4 * words, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        for (int side = 0; side < 2; ++side) {
+            int32_t *dst = side ? end_hits : start_hits;
+            const int64_t k = (int64_t)cnt[side];
+            if (k > cap || !k) continue;            // too many: the caller grows cap and calls again
+            const int16_t *f16 = (const int16_t *)(h.data() + at_side[side]);
+            const uint16_t *c16 = (const uint16_t *)(h.data() + at_side[side] + 3 * (size_t)k);
+            int64_t j = 0;
+            for (size_t r = 0; r < n && j < k; ++r)
+                for (uint16_t c = c16[r]; c > 0; --c) dst[j++] = (int32_t)r;
+            for (int f = 0; f < 6; ++f)
+                for (int64_t q = 0; q < k; ++q) dst[(f + 1) * cap + q] = f16[f * k + q];
+        }
+        return 0;
+    }
     for (int side = 0; side < 2; ++side) {
         int32_t *dst = side ? end_hits : start_hits;
         const int64_t k = (int64_t)cnt[side];
