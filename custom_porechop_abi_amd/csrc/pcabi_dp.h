@@ -956,36 +956,42 @@ struct LayL {
     }
 };
 // Run-tagged buckets (affine gaps, adapters <= 31 bp: the end-window adapters): the tie-break
-// field widens to an 8-bit tag that COUNTS the extends of the current gap run, so the H key
-// needs no re-tagging before it is stored (one VALU op per cell less than Lay):
-//      [ score : 8 (signed) ][ tag : 8 ][ c mod 64 : 6 ][ nD : 5 ][ m : 5 ]
+// field widens to a 7-bit tag that COUNTS the extends of the current gap run, so the H key needs
+// no re-tagging before it is stored (one VALU op per cell less than Lay):
+//      [ score : 8 (signed) ][ tag : 7 ][ c mod 128 : 7 ][ nD : 5 ][ m : 5 ]
 //   H:  open = tag 0 (G = S + go as stored), extend = previous H tag + 1   -> extend wins ties
-//   V:  open = tag 128 (G + TVB), extend = previous V tag + 1              -> extend wins ties
-//   diagonal candidates tag 255                                            -> D > V > H on ties
-// H runs are bounded by the score range ((Smax - Smin) / |ge| extends, layt_ok checks < 128),
-// V runs by the rows (< 32), so H tags stay below every V tag and V tags below 255.
+//   V:  open = tag VB = 127 - RPL (G + TVB), extend = previous V tag + 1   -> extend wins ties
+//   diagonal candidates tag 127                                            -> D > V > H on ties
+// H runs are bounded by the score range ((Smax - Smin) / |ge| extends, layt_ok checks < VB), V
+// runs by the rows (a V run holds at most RPL - 1 extends: tags VB .. 126), so H tags stay below
+// every V tag and V tags below 127. r02 used an 8-bit tag with c mod 64 (span < 64: adapters of
+// <= 25 bp under the default scheme); the 7-bit tag frees a c bit and the 26-31 bp adapters (the
+// 28 / 32-row buckets) fit too (span <= 76 at the default scheme).
 template <int RPL>
 struct LayT {
     static constexpr bool WIDE = false;
     static constexpr bool TAGGED = true;
     static constexpr int SC_SH = 24;
-    static constexpr int TB_SH = 16;
+    static constexpr int TB_SH = 17;
     static constexpr int C_SH = 10;
+    static constexpr int CB = 7;                        // c mod 128
     static constexpr int MB = 32;
-    static constexpr int32_t TAG1 = 1 << TB_SH, TVB = 128 << TB_SH;
+    static constexpr int TD = 127;                      // diagonal tag (the tag field's maximum)
+    static constexpr int VB = TD - RPL;                 // V-open tag
+    static constexpr int32_t TAG1 = 1 << TB_SH, TVB = VB << TB_SH;
     static constexpr int32_t TB1 = TAG1, TB2 = TVB;   // the untagged core's names (unused here)
-    static constexpr int32_t TB3 = 255 << TB_SH, TBM = 255 << TB_SH;
+    static constexpr int32_t TB3 = TD << TB_SH, TBM = TD << TB_SH;
     static constexpr int32_t INC_D = MB, INC_M = MB + 1;
     static constexpr int SC_MIN = -128, SC_MAX = 127;
     static PCABI_HD int32_t sc(int v) { return (int32_t)((uint32_t)v << SC_SH); }
-    static PCABI_HD int32_t start(int c) { return (int32_t)(((uint32_t)c & 63u) << C_SH); }
+    static PCABI_HD int32_t start(int c) { return (int32_t)(((uint32_t)c & ((1u << CB) - 1u)) << C_SH); }
     static PCABI_HD int score(int32_t k) { return k >> SC_SH; }
-    static PCABI_HD int tb(int32_t k) { return (k >> TB_SH) & 255; }
+    static PCABI_HD int tb(int32_t k) { return (k >> TB_SH) & TD; }
     static PCABI_HD uint32_t attr(int32_t k) { return (uint32_t)k & ((1u << TB_SH) - 1u); }
     static PCABI_HD uint32_t to_std(uint32_t a, int bj) {
         const uint32_t cnt = a & ((1u << C_SH) - 1u);
         const uint32_t m = cnt % (uint32_t)MB, nd = cnt / (uint32_t)MB;
-        const int c = bj - (int)(((uint32_t)bj - (a >> C_SH)) & 63u);
+        const int c = bj - (int)(((uint32_t)bj - (a >> C_SH)) & ((1u << CB) - 1u));
         return attr_start(c) | (nd << ATTR_B) | m;
     }
 };
@@ -1056,16 +1062,16 @@ PCABI_HD bool long_ok(int L, int rpl, const Scoring &s) {
 }
 
 // Range conditions of the run-tagged layout (pk::LayT): affine gaps, the packed ranges with an
-// 8-bit score field, counts <= 31, a reported path spanning < 64 columns (c mod 64), and every H
-// run shorter than 128 extends: an extend at (i, j) needs H(i, j-1) + ge >= S(i, j-1) + go >=
-// Smin + go, and a run that opened at <= Smax + go loses |ge| per extend, so a run holds at most
-// (Smax - Smin) / |ge| extends (Smax = max(L best_sub, 0), Smin = go + (L-1) ge; padding rows stay at
-// S = 0 and never extend).
+// 8-bit score field, counts <= 31, a reported path spanning < 128 columns (c mod 128), and every H
+// run shorter than VB = 127 - rpl extends: an extend at (i, j) needs H(i, j-1) + ge >= S(i, j-1) +
+// go >= Smin + go, and a run that opened at <= Smax + go loses |ge| per extend, so a run holds at
+// most (Smax - Smin) / |ge| extends (Smax = max(L best_sub, 0), Smin = go + (L-1) ge; padding rows
+// stay at S = 0 and never extend).
 PCABI_HD bool layt_ok(int L, int rpl, const Scoring &s) {
     using Y = pk::LayT<32>;
     if (L < 1 || L > rpl || rpl > 32 || L > 31) return false;
     if (!(s.go < 0 && s.ge < 0) || s.go == s.ge) return false;
-    if (packed_span_bound(L, s) > 63) return false;
+    if (packed_span_bound(L, s) >= (1 << Y::CB)) return false;
     const long long smin = (long long)s.go + (long long)(L - 1) * s.ge;
     const long long lo_sub = s.mi < s.ma ? s.mi : s.ma;
     const long long lo_gap = (long long)s.go + s.ge;
@@ -1079,7 +1085,7 @@ PCABI_HD bool layt_ok(int L, int rpl, const Scoring &s) {
     if (best_sub(s) > hi) hi = best_sub(s);
     if (lo < Y::SC_MIN || hi > Y::SC_MAX) return false;
     const long long smax = hi;
-    return (smax - smin) / (-(long long)s.ge) + 1 < 128;
+    return (smax - smin) / (-(long long)s.ge) + 1 < Y::TD - rpl;
 }
 
 PCABI_HD bool packed_ok(int L, int rpl, const Scoring &s) {
@@ -1142,8 +1148,8 @@ struct LanePacked {
                 const int32_t hx = HK[s] + k_gex, ho = G[s];
                 hn = hx > ho ? hx : ho;                  // tag > 0 iff extend
                 const int32_t vx = vup + k_gex, vo = gup + k_vo;
-                vn2 = vx > vo ? vx : vo;                 // tag > 128 iff extend
-                if (LAST || s == RPL) { hext = Y::tb(hn) != 0; vext = Y::tb(vn2) > 128; }
+                vn2 = vx > vo ? vx : vo;                 // tag > VB iff extend
+                if (LAST || s == RPL) { hext = Y::tb(hn) != 0; vext = Y::tb(vn2) > Y::TB2 >> Y::TB_SH; }
             } else if (AFFINE) {
                 const int32_t hx = HK[s] + k_ge, ho = G[s];
                 hn = hx > ho ? hx : ho;                  // tb 1 iff extend
@@ -1157,7 +1163,7 @@ struct LanePacked {
             }
             sn = max3i(diag, vn2, hn);
             const int t = Y::tb(sn);
-            const int slt = Y::TAGGED ? (t == 255 ? LT_D : (t >= 128 ? LT_V : LT_H))
+            const int slt = Y::TAGGED ? (t == (Y::TBM >> Y::TB_SH) ? LT_D : (t >= (Y::TB2 >> Y::TB_SH) ? LT_V : LT_H))
                                       : (t == 3 ? LT_D : (t == 2 ? LT_V : LT_H));
             if (LAST && s < RPL) {
                 const bool cont = AFFINE ? (vext || slt_up == LT_V) : (slt_up == LT_V);
@@ -1256,7 +1262,7 @@ struct LanePacked {
     PCABI_HD void column_tail(int32_t lv, int32_t lh, int32_t ls, int j, bool owned = true) {
         (void)lh;
         int32_t corr;
-        if (AFFINE && Y::TAGGED) corr = std::max(lv, ls & ~Y::TBM);   // V tags >= 128 > 0
+        if (AFFINE && Y::TAGGED) corr = std::max(lv, ls & ~Y::TBM);   // V tags >= VB > 0
         else if (AFFINE) corr = std::max(lv | Y::TB3, ls & ~Y::TBM);
         else corr = ls;
         bool upd = corr > (bkey | ((1 << Y::SC_SH) - 1));   // score(corr) > score(bkey)

@@ -173,16 +173,18 @@ def _tagged(model, r, a, rpl, sc):
 
 
 def test_tagged_core(model):
-    """The run-tagged packed layout (pk::LayT: 8-bit run-counting tie tags, so the H key is
-    stored without re-tagging) against the oracle: tie-heavy alphabets, every small bucket with
-    extra padding rows, long gap runs (adapters embedded with long insertions / deletions), and
-    the reference's golden rows; layt_ok must accept the default scheme up to 25 bp (the span
-    bound L + 3L/2 reaches 64 at 26)."""
+    """The run-tagged packed layout (pk::LayT: 7-bit run-counting tie tags, so the H key is
+    stored without re-tagging, and c mod 128) against the oracle: tie-heavy alphabets, every small
+    bucket with extra padding rows, long gap runs (adapters embedded with long insertions /
+    deletions), and the reference's golden rows; layt_ok must accept the default scheme up to 31 bp
+    in every bucket that holds the adapter (span bound L + 3L/2 <= 77 < 128, H runs <= 80 < the
+    V-open tag 127 - rpl)."""
     rng = random.Random(23)
-    schemes = [(3, -6, -5, -2), (1, -1, -3, -1), (3, -6, -2, -5), (5, -4, -8, -6), (2, -3, -5, -1)]
-    for L in range(1, 26):
-        assert model.pcabi_model_align_tagged(b'A', 1, b'A' * L, L, (L + 3) & ~3, 3, -6, -5, -2,
-                                              (ctypes.c_int * 8)()) == 0
+    schemes = [(3, -6, -5, -2), (1, -1, -3, -1), (3, -6, -2, -5), (5, -4, -8, -6), (2, -3, -5, -1), (2, -3, -2, -1)]
+    for L in range(1, 32):
+        for rpl in range((L + 3) & ~3, 33, 4):
+            assert model.pcabi_model_align_tagged(b'A', 1, b'A' * L, L, rpl, 3, -6, -5, -2,
+                                                  (ctypes.c_int * 8)()) == 0
     n_checked = 0
     for k in range(6000):
         sc = schemes[k % len(schemes)]
@@ -211,7 +213,7 @@ def test_tagged_core(model):
     assert n_checked > 4000
     # the longest gap runs: nothing matches, so H / V extend as far as the scores allow
     for sc in schemes:
-        for L in (1, 8, 17, 24, 25, 31):
+        for L in (1, 8, 17, 24, 25, 26, 28, 30, 31):
             for n in (1, 60, 150, 400):
                 a, r = 'C' * L, 'A' * n
                 rc, res = _tagged(model, r, a, (L + 3) & ~3, sc)
