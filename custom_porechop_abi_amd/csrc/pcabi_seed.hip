@@ -80,12 +80,7 @@ constexpr int kMaxEnt = 8192;      // probe entries / distinct probes kept in LD
 constexpr int kLdsMax = 64 * 1024; // per block: probe tables
 constexpr int kAdpLds = 16 * 1024; // adapters copied to LDS by the band kernels up to this size
 constexpr int kNeg = -(1 << 20);
-constexpr int kPos = 8;            // read positions per lane and scan step (16 bases loaded)
-constexpr int kNW = 4;             // dwords of bases per lane and step
-#ifndef PCABI_SEED_SUB
-#define PCABI_SEED_SUB 2
-#endif
-constexpr int kSub = PCABI_SEED_SUB;   // sub-steps per scan iteration
+constexpr int kSeg = 32;           // read positions per lane and scan step (a segment; 40 bytes loaded)
 constexpr unsigned kSlowBit = 0x80000000u;   // raw hit: the position's valid run is shorter than 8
 constexpr int kBandGrid = 4096;    // band / cands launches whose count is on the device: grid-stride
 // task counters: [c] inside-band tasks of class c (from the region's start), [kCls + c] edge tasks
@@ -122,159 +117,217 @@ struct ScanArgs {
                                 // is inside when q >= lo and (read length - q) > hi
     int32_t pin_cls[kCls];      // class c's inside tasks run the pinned band: records (read,
                                 // adapter << 8 | o, the probe's byte offset in codes: lo, hi)
+    const int64_t *seg_cum;     // n + 1 entries: segments (kSeg positions) before each read, the total last
 };
 
 __device__ __forceinline__ int64_t dev_count(const int32_t *n_dev, int64_t n) {
     return n_dev ? min((int64_t)*n_dev, n) : n;
 }
 
+// Segments (kSeg positions) of read r of a round: 0 past the round's read count.
+struct SegCount {
+    const int32_t *len;
+    const int32_t *n_dev;
+    int64_t n;
+    __host__ __device__ int64_t operator()(int64_t r) const {
+        const int64_t nr = n_dev ? (*n_dev < n ? (int64_t)*n_dev : n) : n;
+        return r < nr ? ((int64_t)max(len[r], 0) + kSeg - 1) / kSeg : 0;
+    }
+};
+
+// A dword of k_seed_scan's LDS by byte address: the kernel declares no static LDS, so its dynamic
+// area starts at LDS address 0 and the code's mask is the whole address computation.
+__device__ __forceinline__ uint32_t lds_at(uint32_t byte_addr) {
+    return *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>((size_t)byte_addr);
+}
+
+// 64-bit wave-uniform value (readfirstlane per half)
+__device__ __forceinline__ int64_t rfl64(int64_t v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// A read's segment end, code offset and length (reads past the round's count: an empty read at
+// the end of the segment space).
+struct ReadMeta {
+    int64_t s1, off;
+    int32_t len;
+};
+__device__ __forceinline__ ReadMeta read_meta(const ScanArgs &a, int64_t r, int64_t nr, int64_t S) {
+    ReadMeta m{S, 0, 0};
+    if (r < nr) {
+        m.s1 = rfl64(a.seg_cum[r + 1]);
+        m.off = rfl64(a.v_off[r]);
+        m.len = __builtin_amdgcn_readfirstlane(a.v_len[r]);
+    }
+    return m;
+}
+
+// k_seed_scan (r03 rewrite): the reads' positions are cut into segments of kSeg = 32 (seg_cum, an
+// exclusive scan of ceil(len / 32) over the round's reads), and every WAVE takes an equal,
+// contiguous range of segments -- no read-length imbalance between waves, and no idle lanes at
+// a read's end beyond its last segment (r02 / early r03: blocks took whole reads in steps of
+// 4096 positions, so a 5 kb read cost as much as an 8 kb one and the slowest block set the time).
+// Lane l of a step holds segment b + l: 40 bytes (its 32 positions and the 7-base lookahead), in
+// three loads issued one step ahead. The wave keeps the metadata of its current read and the next
+// one (scalar loads when the wave crosses a read end); a lane past both (reads < 2 kb) looks its
+// read up itself.
+// Per position: the rolling 8-mer (first base in the top bits), its bitmap word (LDS byte address
+// (code >> 3) & 0x1FFC: the merged K = 8 bitmap sits at LDS byte 0) and the bit shifted into the
+// step's hit mask (alignbit) -- no validity work. A lane whose 40 bytes hold an N or pass its
+// read's end masks the hits afterwards: bit i survives when bytes i .. i + 7 are valid bases of
+// the read (doubling ORs of the invalid-byte mask), and the positions whose valid run is shorter
+// than 8 but at least the shortest probe are flagged for the short tables. (An N byte = 4 only
+// disturbs the codes of windows that contain it, and those are masked.)
+// Hits are appended to the block's slab as before: (read, position | kSlowBit, its clean 8-mer |
+// valid run << 16, read length - position).
 __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
+    // dynamic LDS: the bitmaps from byte 0 (so a word's address is one mask away from the code),
+    // then the slab counter
     extern __shared__ uint32_t lds[];
-    __shared__ int s_cnt;
+    int &s_cnt = *reinterpret_cast<int *>(lds + a.bits_dw);
     for (int i = threadIdx.x; i < a.bits_dw; i += 256) lds[i] = a.tabs[i];
     if (threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
     const int64_t nr = dev_count(a.n_dev, a.n);
+    const int64_t S = rfl64(a.seg_cum[nr]);
+    const int lane = (int)(threadIdx.x & 63);
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t lo = S * gw / nw, hi = S * (gw + 1) / nw;
     uint4 *slab = a.raw + (int64_t)blockIdx.x * a.slab;
-    // The block walks its reads (blockIdx.x, + gridDim.x, ...) kSub x 2048 positions at a time;
-    // the bytes of the next step and the next read's length / offset are loaded before the current
-    // step is processed, so the global latency hides behind the lookups. No branch waits on a
-    // length: an empty read is one step of N (no hits), not a loop that stalls every read switch.
-    // (the next read's offset stays a raw loaded value until the switch: using it earlier would
-    // wait for the load)
-    int64_t k = blockIdx.x, nk = k;
-    int len = 0, nlen = 0;
-    int64_t noff = 0;
-    const uint8_t *base = a.codes;
-    auto next_read = [&](int64_t from, int &ln, int64_t &off) -> int64_t {
-        ln = 0;
-        off = 0;
-        if (from < nr) {
-            ln = a.v_len[from];
-            off = a.v_off[from];
+    if (lo < hi) {
+        // the read holding segment lo: a 64-ary search over seg_cum (seg_cum[ra] <= lo < seg_cum[rb])
+        int64_t ra = 0, rb = nr;
+        while (rb - ra > 1) {
+            const int64_t step = (rb - ra + 63) / 64;
+            const int64_t idx = ra + (int64_t)lane * step;
+            const bool le = idx < rb && a.seg_cum[idx] <= lo;
+            const int c = __popcll(__ballot(le));
+            ra = rfl64(ra + (int64_t)(c - 1) * step);
+            rb = rfl64(min(rb, ra + step));
         }
-        return from;
-    };
-    // A lane's 16 bases p0 .. p0 + 15 come from five aligned dwords (past the read they stay inside
-    // the caller's >= 16 B tail padding); the loads land in d[] and are only aligned (alignbyte by
-    // al) when the step is processed, so they stay in flight behind the current step's lookups.
-    auto fetch = [&](const uint8_t *bs, int ln, int p0b, uint32_t (&d)[kNW + 1], int &al) {
-        const int p0 = p0b + kPos * (int)threadIdx.x;
-        al = 0;
-#pragma unroll
-        for (int t = 0; t <= kNW; ++t) d[t] = 0x04040404u;
-        if (p0 < ln) {
-            const uint8_t *ad = bs + p0;
-            al = (int)((uintptr_t)ad & 3);
-            const uint32_t *q = reinterpret_cast<const uint32_t *>(ad - al);
-#pragma unroll
-            for (int t = 0; t <= kNW; ++t) d[t] = q[t];
-        }
-    };
-    k = next_read(k, len, noff);
-    base = a.codes + noff;
-    if (k < nr) nk = next_read(k + gridDim.x, nlen, noff);
-    int p0b = 0;
-#if defined(PCABI_SCAN_EXP)
-    uint32_t sink = 0;                                 // perf experiments only (tools/build_variant.sh)
-#endif
-    uint32_t wn[kSub][kNW + 1];
-    int an[kSub];
-#pragma unroll
-    for (int h = 0; h < kSub; ++h)
-        if (k < nr) fetch(base, len, h * 256 * kPos, wn[h], an[h]);
-    while (k < nr) {                                   // block-uniform
-        const int64_t ck = k;
-        const int clen = len, cp0b = p0b;
-        uint32_t wc[kSub][kNW + 1];
-        int ac[kSub];
-#pragma unroll
-        for (int h = 0; h < kSub; ++h) {
-            ac[h] = an[h];
-#pragma unroll
-            for (int d = 0; d <= kNW; ++d) wc[h][d] = wn[h][d];
-        }
-        p0b += kSub * 256 * kPos;
-        if (p0b >= len) {                              // on to the next read
-            k = nk;
-            len = nlen;
-            base = a.codes + noff;
-            p0b = 0;
-            if (k < nr) nk = next_read(k + gridDim.x, nlen, noff);
-        }
-#pragma unroll
-        for (int h = 0; h < kSub; ++h)
-            if (k < nr) fetch(base, len, p0b + h * 256 * kPos, wn[h], an[h]);
-#pragma unroll
-        for (int h = 0; h < kSub; ++h) {
-            const int cp0 = cp0b + h * 256 * kPos + kPos * (int)threadIdx.x;
-            uint32_t w[kNW];
-#pragma unroll
-            for (int t = 0; t < kNW; ++t) w[t] = __builtin_amdgcn_alignbyte(wc[h][t + 1], wc[h][t], ac[h]);
-            // 16 bases (SWAR): c32 = their 2-bit codes, first base in the top bits; vmask bit t =
-            // base t is A/C/G/T inside the read (Dna5 codes are 0..4: N has bit 2)
-            uint32_t c32 = 0, vmask = 0;
-#pragma unroll
-            for (int d = 0; d < kNW; ++d) {
-                const uint32_t c4 = ((w[d] & 0x03030303u) * 0x40100401u) >> 24;
-                const uint32_t nb = (((~w[d]) >> 2) & 0x01010101u) * 0x10204080u >> 28;
-                c32 = (c32 << 8) | c4;
-                vmask |= nb << (4 * d);
+        int64_t rc = ra, s0c = rfl64(a.seg_cum[ra]);
+        ReadMeta mc = read_meta(a, rc, nr, S), mn = read_meta(a, rc + 1, nr, S);
+        // the wave's window moves to the read holding segment b (b < hi <= S: terminates)
+        auto advance = [&](int64_t b) {
+            while (b >= mc.s1) {
+                ++rc;
+                s0c = mc.s1;
+                mc = mn;
+                mn = read_meta(a, rc + 1, nr, S);
             }
-            const int rem = clen - cp0;
-            vmask &= rem >= 16 ? 0xFFFFu : (rem > 0 ? (1u << rem) - 1u : 0u);
-            uint32_t hits = 0, slow = 0;
-            if (__all((vmask & 0x7FFFu) == 0x7FFFu)) {
-                // every lane's 8 positions see 8 valid bases: one bitmap word each, the K = 8 bitmap
-                // at LDS byte 0 (plan()), byte address (c8 >> 5) << 2 straight from c32
-#pragma unroll
-                for (int i = 0; i < kPos; ++i) {
-                    const int sh = 16 - 2 * i;
-                    const uint32_t word = *reinterpret_cast<const uint32_t *>(
-                        reinterpret_cast<const char *>(lds) + ((c32 >> (sh + 3)) & 0x1FFCu));
-                    hits |= ((word >> ((c32 >> sh) & 31u)) & 1u) << i;
-                }
-            } else {
-#pragma unroll
-                for (int i = 0; i < kPos; ++i) {
-                    const uint32_t c8 = (c32 >> (16 - 2 * i)) & 0xFFFFu;
-                    const uint32_t word = lds[(int)(c8 >> 5)];
-                    const bool full = ((vmask >> i) & 0xFFu) == 0xFFu;
-                    hits |= (full && ((word >> (c8 & 31)) & 1u)) ? 1u << i : 0u;
-                    // a valid run shorter than 8 bases (an N or the read end ahead): the short tables
-                    slow |= (!full && ((vmask >> i) & ((1u << a.min_k) - 1u)) == (1u << a.min_k) - 1u) ? 1u << i : 0u;
-                }
+        };
+        // lane's segment b + lane -> read, position, code offset, length; false past the range
+        auto map = [&](int64_t b, int64_t &r, int &p, int64_t &off, int &len) -> bool {
+            const int64_t sg = b + lane;
+            if (sg >= hi) return false;
+            if (sg < mc.s1) {
+                r = rc; p = (int)(sg - s0c) * kSeg; off = mc.off; len = mc.len;
+            } else if (sg < mn.s1) {
+                r = rc + 1; p = (int)(sg - mc.s1) * kSeg; off = mn.off; len = mn.len;
+            } else {                                   // a read past the next one (short reads)
+                r = rc + 2;
+                int64_t e = a.seg_cum[r + 1];
+                while (e <= sg) e = a.seg_cum[++r + 1];
+                p = (int)(sg - a.seg_cum[r]) * kSeg;
+                off = a.v_off[r];
+                len = a.v_len[r];
             }
-#if defined(PCABI_SCAN_EXP) && PCABI_SCAN_EXP == 1
-            hits = 0;
-            slow = 0;
-            sink ^= c32 ^ vmask;
-#elif defined(PCABI_SCAN_EXP) && PCABI_SCAN_EXP == 2
-            sink ^= hits ^ slow;
-            hits = 0;
-            slow = 0;
-#endif
+            return true;
+        };
+        // a lane's 40 bytes: dwords 0-3 always inside the buffer (p < len, >= 16 B of padding past
+        // every view), 4-7 and 8-9 only when they start inside that reach -- otherwise re-read from
+        // the segment start (those bytes lie past the read and are masked)
+        auto fetch = [&](int64_t off, int p, int len, uint32_t (&d)[10]) {
+            const uint32_t *q = reinterpret_cast<const uint32_t *>(a.codes + off + p);
+            const uint32_t *q1 = p + 16 <= len ? q + 4 : q;
+            const uint32_t *q2 = p + 24 <= len ? q + 8 : q;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) d[t] = q[t];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) d[4 + t] = q1[t];
+            d[8] = q2[0];
+            d[9] = q2[1];
+        };
+        int64_t b = lo;
+        advance(b);
+        int64_t nrd = 0, noff = 0;
+        int np = 0, nlen = 0;
+        uint32_t nd[10];
+#pragma unroll
+        for (int t = 0; t < 10; ++t) nd[t] = 0x04040404u;
+        bool nact = map(b, nrd, np, noff, nlen);
+        if (nact) fetch(noff, np, nlen, nd);
+        while (b < hi) {                               // wave-uniform
+            const int64_t crd = nrd, coff = noff;
+            const int cp = np, clen = nlen;
+            const bool cact = nact;
+            uint32_t d[10];
+#pragma unroll
+            for (int t = 0; t < 10; ++t) d[t] = nd[t];
+            const int64_t bn = b + 64;
+            nact = false;
+            if (bn < hi) {
+                advance(bn);
+                nact = map(bn, nrd, np, noff, nlen);
+                if (nact) fetch(noff, np, nlen, nd);
+            }
+            b = bn;
+            if (!cact) continue;
+            // ---- the segment's 32 positions ----
+            auto byte = [&](int j) -> uint32_t {
+                return (j & 3) == 3 ? d[j >> 2] >> 24 : (d[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            };
+            uint32_t c = 0;
+#pragma unroll
+            for (int j = 0; j < 7; ++j) c = (c << 2) | byte(j);
+            uint32_t hits = 0;
+#pragma unroll
+            for (int i = 0; i < kSeg; ++i) {
+                c = (c << 2) | byte(i + 7);
+                const uint32_t word = lds_at((c >> 3) & 0x1FFCu);
+                hits = __builtin_amdgcn_alignbit(word >> (c & 31u), hits, 1);
+            }
+            // ---- validity: N bytes and the read end ----
+            const int rem = clen - cp;                 // >= 1
+            uint32_t nor = 0;
+#pragma unroll
+            for (int t = 0; t < 10; ++t) nor |= d[t];
+            uint64_t inv = 0;
+            uint32_t slow = 0;
+            if ((nor & 0x04040404u) || rem < 40) {
+#pragma unroll
+                for (int t = 0; t < 10; ++t)
+                    inv |= (uint64_t)((((d[t] >> 2) & 0x01010101u) * 0x10204080u) >> 28) << (4 * t);
+                if (rem < 64) inv |= ~0ull << rem;
+                const uint64_t t1 = inv | (inv >> 1), t2 = t1 | (t1 >> 2), t3 = t2 | (t2 >> 4);
+                const uint32_t full8 = ~(uint32_t)t3;
+                hits &= full8;
+                if (a.min_k < kMaxK) slow = ~(uint32_t)(t2 | (t2 >> (a.min_k - kMinK))) & ~full8;
+            }
             const uint32_t any = hits | slow;
-            if (any) {                                 // ~4 % of the lanes: append to the block's slab
+            if (any) {                                 // ~15 % of the lanes: append to the block's slab
                 int slot = atomicAdd(&s_cnt, __popc(any));
                 uint32_t left = any;
+                const uint8_t *seg = a.codes + coff + cp;
                 while (left) {
                     const int i = __builtin_ctz(left);
                     left &= left - 1;
-                    // the 8-mer at position i (its first base in the top bits) and its valid run
-                    const uint32_t c8 = (c32 >> (16 - 2 * i)) & 0xFFFFu;
-                    const uint32_t run = min(8u, (uint32_t)__builtin_ctz(~(vmask >> i)));
+                    // the position's 8-mer from the (cached) read bytes, its valid run
+                    uint32_t c8 = 0;
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) c8 = (c8 << 2) | (seg[i + t] & 3u);
+                    const uint32_t run = (slow >> i) & 1u ? (uint32_t)min(8, __builtin_ctzll(inv >> i)) : 8u;
                     if (slot < a.slab)
-                        slab[slot] = make_uint4((uint32_t)ck, (uint32_t)(cp0 + i) | ((slow >> i) & 1u ? kSlowBit : 0u),
-                                                c8 | (run << 16), (uint32_t)(clen - (cp0 + i)));
+                        slab[slot] = make_uint4((uint32_t)crd, (uint32_t)(cp + i) | ((slow >> i) & 1u ? kSlowBit : 0u),
+                                                c8 | (run << 16), (uint32_t)(clen - (cp + i)));
                     ++slot;
                 }
             }
         }
     }
-#if defined(PCABI_SCAN_EXP)
-    if (sink == 0x12345678u) a.flags[0] = 2;       // keeps the experiment's work alive
-#endif
     __syncthreads();
     if (threadIdx.x == 0) {
         a.raw_cnt[blockIdx.x] = min(s_cnt, a.slab);
@@ -816,7 +869,7 @@ struct State {
     size_t lds_bytes = 0;                         // the whole probe image (k_seed_expand)
     int32_t adp_bytes = 0;                        // flat adapter table, dword-rounded
     ScanArgs a{};
-    Buf tabs, adp, adp_off, adp_len, adp_meta, task, cnt, bound, thr, cands, ccnt, raw, rawcnt;
+    Buf tabs, adp, adp_off, adp_len, adp_meta, task, cnt, bound, thr, cands, ccnt, raw, rawcnt, segcum, scantmp;
     int pin_nc4[kCls] = {0, 0};                   // class c's pinned band slot (uint4 per lane), 0: band_best
     int32_t n_adp = 0;
     int64_t cap = 0, ecap = 0, ccap = 0, raw_cap = 0;
@@ -1136,7 +1189,7 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
         int dev = 0, cus = 0, per_cu = 0;
         SD_TRY(hipGetDevice(&dev));
         SD_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_scan, 256, 4 * (size_t)s->a.bits_dw));
+        SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_scan, 256, 4 * (size_t)s->a.bits_dw + 4));
         s->scan_blocks = std::max(1, cus * std::max(1, per_cu));
         per_cu = 0;
         SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_expand, 256, s->lds_bytes));
@@ -1167,9 +1220,21 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
     A.cap = s->cap;
     A.ecap = s->ecap;
     if (int rc = s->ccnt.ensure(8)) return rc;
+    // the scan's segment space: seg_cum[r] = segments before read r, seg_cum[n_dev] = all
+    {
+        hipcub::CountingInputIterator<int64_t> idx(0);
+        hipcub::TransformInputIterator<int64_t, SegCount, hipcub::CountingInputIterator<int64_t>> segs(
+            idx, SegCount{v_len, n_dev, n});
+        size_t tmp = 0;
+        SD_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, segs, (int64_t *)nullptr, n + 1, st));
+        if (int rc = s->scantmp.ensure(tmp)) return rc;
+        if (int rc = s->segcum.ensure(sizeof(int64_t) * (size_t)(n + 1))) return rc;
+        SD_TRY(hipcub::DeviceScan::ExclusiveSum(s->scantmp.p, tmp, segs, (int64_t *)s->segcum.p, n + 1, st));
+        A.seg_cum = (const int64_t *)s->segcum.p;
+    }
     hipLaunchKernelGGL(k_bound_reset, dim3(1024), dim3(256), 0, st, (int32_t *)s->bound.p, n, n_dev, n_adp, A.cnt,
                        kCnt, (unsigned long long *)s->ccnt.p);
-    hipLaunchKernelGGL(k_seed_scan, dim3(grid), dim3(256), 4 * (size_t)A.bits_dw, st, A);
+    hipLaunchKernelGGL(k_seed_scan, dim3(grid), dim3(256), 4 * (size_t)A.bits_dw + 4, st, A);
     hipLaunchKernelGGL(k_seed_expand, dim3(s->expand_blocks), dim3(256), s->lds_bytes, st, A);
     SD_TRY(hipGetLastError());
     if (tasks) return 0;                                // the caller launches the bands (host counts)
