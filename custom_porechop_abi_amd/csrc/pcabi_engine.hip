@@ -108,6 +108,14 @@ bool middle_devplan_on() {
     return !(e && e[0] == '0');
 }
 
+// Queued rounds run the candidate DP over the verified seeds' windows instead of whole reads
+// (PCABI_MIDDLE_WINDOWS=1; off by default: a window's best is the whole read's only when no
+// alignment without an exact piece can outscore it -- work in progress).
+bool middle_windows_on() {
+    const char *e = std::getenv("PCABI_MIDDLE_WINDOWS");
+    return e && e[0] == '1';
+}
+
 // Device planning aims at this many waves per candidate-DP round (4 per SIMD): the chunk length
 // is the longest of 512, 256, 128, 64 owned columns that still reaches it.
 int64_t middle_plan_waves() {
@@ -473,6 +481,100 @@ __global__ __launch_bounds__(256) void k_plan_fill(const int64_t *cand, int64_t 
             tck[q] = ck;
             tcand[q] = (int32_t)i;
         }
+    }
+}
+
+// ---- candidate windows (device rounds, PCABI_MIDDLE_WINDOWS): one chunk per verified seed ------
+// A verified seed (pcabi_seed.hip put_verified: read, adapter | E << 24, the diagonal's codes offset)
+// is a band task of a candidate pair whose bound reached T. Every alignment of the pair scoring >= T
+// holds an exact piece, whose task is verified, and stays within E diagonals of it: it ends in row L
+// at a column of d0 + L - E .. d0 + L + E, or in the read's last column when the band reaches it. One
+// chunk per verified seed that owns those columns (started D + 1 columns earlier: sf::chunk_plan's
+// rule, so an owned cell >= T gets the whole read's score and attributes) replaces the pair's
+// whole-read chunks -- 8 kb x L cells become ~(D + 2E) x L. The merge's rules are unchanged and
+// still give the whole-read answer whenever it reaches T: the largest score, then the smallest first
+// owned column (overlapping windows of one pair report the same first maximum of a shared cell).
+__device__ __forceinline__ bool wseed_valid(const int4 &v, const int32_t *v_len, const int32_t *start) {
+    const int32_t a = v.y & 0xFFFFFF, k = v.x;
+    return v_len[k] > 0 && (!start || a >= start[k]);
+}
+
+__device__ __forceinline__ int4 wseed_chunk(const int4 &v, const int64_t *v_off, const int32_t *v_len,
+                                            const int32_t *alen, const int32_t *span) {
+    const int32_t a = v.y & 0xFFFFFF, E = (int32_t)((uint32_t)v.y >> 24), k = v.x;
+    const int64_t dabs = (int64_t)(((uint64_t)(uint32_t)v.w << 32) | (uint32_t)v.z);
+    const int d0 = (int)(dabs - v_off[k]);
+    const int n = v_len[k], L = alen[a], D = span[a];
+    int lo = max(1, d0 + L - E);
+    const int hi = d0 + L + E + 1;
+    if (hi > n) {                                    // the band reaches the read end: the last chunk
+        lo = min(lo, n);
+        const int st = max(0, lo - 1 - D);
+        return make_int4(st, n - st, lo - st, -1);
+    }
+    const int st = max(0, lo - 1 - D);
+    return make_int4(st, hi - 1 - st, lo - st, hi - st);
+}
+
+// Per adapter its windows (the same count under every chunk length, so k_plan_layout's choice does
+// not matter): one atomic per (wave, adapter).
+__global__ __launch_bounds__(256) void k_wplan_count(const int4 *vl, const int32_t *vcount, int64_t vcap,
+                                                     const int32_t *v_len, const int32_t *start, int32_t *adp_tasks) {
+    const int64_t nv = min((int64_t)*vcount, vcap);
+    const int lane = threadIdx.x & 63;
+    for (int64_t b0 = (int64_t)blockIdx.x * 256; b0 < nv; b0 += (int64_t)gridDim.x * 256) {   // uniform
+        const int64_t i = b0 + threadIdx.x;
+        const int4 v = i < nv ? vl[i] : make_int4(0, 0, 0, 0);
+        const bool active = i < nv && wseed_valid(v, v_len, start);
+        const int32_t a = active ? (v.y & 0xFFFFFF) : -1;
+        uint64_t pending = __ballot(active);
+        while (pending) {                            // wave-uniform
+            const int leader = __ffsll((unsigned long long)pending) - 1;
+            const int32_t a0 = __shfl(a, leader);
+            const bool mine = active && a == a0;
+            const int sum = wave_sum(mine ? 1 : 0);
+            if (lane == leader)
+                for (int c = 0; c < kPlanC; ++c) atomicAdd(&adp_tasks[a0 * kPlanC + c], sum);
+            pending &= ~__ballot(mine);
+        }
+    }
+}
+
+// The window task slots (k_plan_place's layout: adapter a's tasks from wave_off[a] * 64), the
+// candidate of each from the pair map k_cands wrote (pmap, row stride n).
+__global__ __launch_bounds__(256) void k_wplan_place(const int4 *vl, const int32_t *vcount, int64_t vcap,
+                                                     const int64_t *v_off, const int32_t *v_len, const int32_t *start,
+                                                     const int32_t *alen, const int32_t *span, const int32_t *pmap,
+                                                     int64_t n, const int64_t *wave_off, int32_t *fill, int32_t *tw,
+                                                     int32_t *to, int4 *tck, int32_t *tcand, const int64_t *slots_dev) {
+    const int64_t nv = min((int64_t)*vcount, vcap);
+    const int64_t slots = *slots_dev;
+    const int lane = threadIdx.x & 63;
+    for (int64_t b0 = (int64_t)blockIdx.x * 256; b0 < nv; b0 += (int64_t)gridDim.x * 256) {   // uniform
+        const int64_t i = b0 + threadIdx.x;
+        const int4 v = i < nv ? vl[i] : make_int4(0, 0, 0, 0);
+        const bool active = i < nv && wseed_valid(v, v_len, start);
+        const int32_t a = active ? (v.y & 0xFFFFFF) : -1;
+        int64_t q = 0;
+        uint64_t pending = __ballot(active);
+        while (pending) {                            // wave-uniform: one atomic per (wave, adapter)
+            const int leader = __ffsll((unsigned long long)pending) - 1;
+            const int32_t a0 = __shfl(a, leader);
+            const bool mine = active && a == a0;
+            const int x = mine ? 1 : 0;
+            const int incl = wave_incl_scan(x);
+            const int total = __shfl(incl, 63);
+            int b1 = 0;
+            if (lane == leader) b1 = atomicAdd(&fill[a0], total);
+            b1 = __shfl(b1, leader);
+            if (mine) q = wave_off[a0] * 64 + b1 + (incl - x);
+            pending &= ~__ballot(mine);
+        }
+        if (!active || q >= slots) continue;
+        tw[q] = v.x;
+        to[q] = (int32_t)q;
+        tck[q] = wseed_chunk(v, v_off, v_len, alen, span);
+        tcand[q] = pmap[(int64_t)a * n + v.x];
     }
 }
 
@@ -976,7 +1078,8 @@ int plan_ready(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32
                const std::vector<int> &fb_rows, const pcabi::Scoring &sc, double threshold, int mode, hipStream_t st);
 int bounds_dev(State *s, const uint8_t *codes, const int64_t *v_off, const int32_t *v_len, int64_t n,
                const int32_t *n_dev, int32_t n_adp, const pcabi::Scoring &sc, const int64_t **dcands,
-               const unsigned long long **dcount, const int32_t **flags, hipStream_t st);
+               const unsigned long long **dcount, const int32_t **flags, const int4 **vlist, const int32_t **vcount,
+               const int32_t **pmap, int64_t *vcap, hipStream_t st);
 bool grow_after_overflow(State *s, int raw_overflow, int task_overflow);
 int debug_counts(State *s, int64_t (&out)[5], hipStream_t st);
 }  // namespace pcabi_seed
@@ -985,7 +1088,7 @@ struct pcabi_scan {
     const pcabi_adapters *adps = nullptr;
     DeviceBuf tiles, toff, res, hits, idx, start, soff, slen, mwin, ms, me;
     DeviceBuf s16, tw, to, wa, pres, tck;   // score filter + candidate pairs (chunks)
-    DeviceBuf pspan, ptasks, pfill, pwoff, pcidx, pcand, pbest, phit, phb, plist, pcnt;   // device planning
+    DeviceBuf pspan, ptasks, pfill, pwoff, pcidx, pcand, pbest, phit, phb, plist, pcnt, plen;   // device planning
     pcabi_seed::State *seed = nullptr; // seeded round-1 bounds (pcabi_seed.hip)
     // queued rounds (middle_device_rounds): per round slot the reads, their start adapters and the
     // hit list; round counts and flags; the plan's bucket tables and scratch
@@ -2362,6 +2465,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
     if (int rc = sc->soff.ensure(sizeof(int64_t) * n)) return rc;
     if (int rc = sc->slen.ensure(sizeof(int32_t) * n)) return rc;
     if (int rc = sc->pspan.ensure(sizeof(int32_t) * n_adp)) return rc;
+    if (int rc = sc->plen.ensure(sizeof(int32_t) * n_adp)) return rc;
     if (int rc = sc->ptasks.ensure(sizeof(int32_t) * n_adp * kPlanC)) return rc;
     if (int rc = sc->pfill.ensure(sizeof(int32_t) * n_adp)) return rc;
     if (int rc = sc->pwoff.ensure(sizeof(int64_t) * n_adp)) return rc;
@@ -2379,6 +2483,8 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
     bk_host.insert(bk_host.end(), bk_local.begin(), bk_local.end());
     HIP_TRY(hipMemcpyAsync(sc->q_bk.p, bk_host.data(), 4 * bk_host.size(), hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(sc->pspan.p, span.data(), 4 * (size_t)n_adp, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(sc->plen.p, adps->hlen.data(), 4 * (size_t)n_adp, hipMemcpyHostToDevice, st));
+    const bool windows = middle_windows_on();
     int64_t *d_slots = (int64_t *)sc->q_misc.p, *d_need = d_slots + 1;
     int32_t *d_pflag = (int32_t *)(d_slots + 2);
     int32_t *d_n = (int32_t *)sc->q_n.p, *d_rflag = (int32_t *)sc->q_flags.p;
@@ -2419,22 +2525,37 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
         const int32_t *sflags = nullptr;
         const int64_t *v_off = first ? win_off : (const int64_t *)sc->soff.p;
         const int32_t *v_len = first ? win_len : (const int32_t *)sc->slen.p;
-        if (int rc = pcabi_seed::bounds_dev(sc->seed, codes, v_off, v_len, n, nr, n_adp, scr, &dcand, &dcount, &sflags, st))
+        const int4 *vlist = nullptr;
+        const int32_t *vcount = nullptr, *pmap = nullptr;
+        int64_t vcap = 0;
+        if (int rc = pcabi_seed::bounds_dev(sc->seed, codes, v_off, v_len, n, nr, n_adp, scr, &dcand, &dcount, &sflags,
+                                            windows ? &vlist : nullptr, &vcount, &pmap, &vcap, st))
             return rc;
         const int64_t ncap = n * (int64_t)n_adp;
-        hipLaunchKernelGGL(k_plan_count, dim3(kGrid), dim3(256), 0, st, dcand, ncap, dcount, v_len, start,
-                           (const int32_t *)sc->pspan.p, (int32_t *)sc->ptasks.p);
+        if (windows)
+            hipLaunchKernelGGL(k_wplan_count, dim3(kGrid), dim3(256), 0, st, vlist, vcount, vcap, v_len, start,
+                               (int32_t *)sc->ptasks.p);
+        else
+            hipLaunchKernelGGL(k_plan_count, dim3(kGrid), dim3(256), 0, st, dcand, ncap, dcount, v_len, start,
+                               (const int32_t *)sc->pspan.p, (int32_t *)sc->ptasks.p);
         hipLaunchKernelGGL(k_plan_layout, dim3(1), dim3(256), 0, st, (const int32_t *)sc->ptasks.p, n_bk, d_bk_first,
                            d_bk_adp, d_bk_local, target, slots_cap, (int32_t *)sc->pcidx.p, (int64_t *)sc->pwoff.p,
                            (int32_t *)sc->wa.p, (int32_t *)sc->tw.p, d_bk_waves, d_slots, d_pflag, d_need);
-        hipLaunchKernelGGL(k_plan_place, dim3(kGrid), dim3(256), 0, st, dcand, ncap, dcount, v_len, start,
-                           (const int32_t *)sc->pspan.p, (const int32_t *)sc->pcidx.p, (const int64_t *)sc->pwoff.p,
-                           (int32_t *)sc->pfill.p, (int32_t *)sc->tw.p, (int32_t *)sc->to.p, (int4 *)sc->tck.p,
-                           (int32_t *)sc->pcand.p, (const int64_t *)d_slots, (int32_t *)sc->pcbase.p);
-        hipLaunchKernelGGL(k_plan_fill, dim3(kGrid), dim3(256), 0, st, dcand, ncap, dcount, v_len,
-                           (const int32_t *)sc->pspan.p, (const int32_t *)sc->pcidx.p, (const int32_t *)sc->pcbase.p,
-                           (int32_t *)sc->tw.p, (int32_t *)sc->to.p, (int4 *)sc->tck.p, (int32_t *)sc->pcand.p,
-                           (const int64_t *)d_slots);
+        if (windows) {
+            hipLaunchKernelGGL(k_wplan_place, dim3(kGrid), dim3(256), 0, st, vlist, vcount, vcap, v_off, v_len, start,
+                               (const int32_t *)sc->plen.p, (const int32_t *)sc->pspan.p, pmap, n,
+                               (const int64_t *)sc->pwoff.p, (int32_t *)sc->pfill.p, (int32_t *)sc->tw.p,
+                               (int32_t *)sc->to.p, (int4 *)sc->tck.p, (int32_t *)sc->pcand.p, (const int64_t *)d_slots);
+        } else {
+            hipLaunchKernelGGL(k_plan_place, dim3(kGrid), dim3(256), 0, st, dcand, ncap, dcount, v_len, start,
+                               (const int32_t *)sc->pspan.p, (const int32_t *)sc->pcidx.p, (const int64_t *)sc->pwoff.p,
+                               (int32_t *)sc->pfill.p, (int32_t *)sc->tw.p, (int32_t *)sc->to.p, (int4 *)sc->tck.p,
+                               (int32_t *)sc->pcand.p, (const int64_t *)d_slots, (int32_t *)sc->pcbase.p);
+            hipLaunchKernelGGL(k_plan_fill, dim3(kGrid), dim3(256), 0, st, dcand, ncap, dcount, v_len,
+                               (const int32_t *)sc->pspan.p, (const int32_t *)sc->pcidx.p, (const int32_t *)sc->pcbase.p,
+                               (int32_t *)sc->tw.p, (int32_t *)sc->to.p, (int4 *)sc->tck.p, (int32_t *)sc->pcand.p,
+                               (const int64_t *)d_slots);
+        }
         HIP_TRY(hipGetLastError());
         KParams p{};
         p.codes = codes;

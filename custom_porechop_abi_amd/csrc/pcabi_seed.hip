@@ -87,6 +87,7 @@ constexpr int kBandGrid = 4096;    // band / cands launches whose count is on th
 // (bands touching a read end, from the region's end), then the two overflow flags
 constexpr int kCnt = 2 * kCls + 2;
 constexpr int kFlag = 2 * kCls;
+constexpr int kVer = kCnt;          // the verified-seed counter, after the task counters and flags
 constexpr int kPinMaxE = 8;        // the pinned band is built for E <= kPinMaxE
 
 struct ScanArgs {
@@ -102,7 +103,7 @@ struct ScanArgs {
                                 // K = 8 is the merged table: every 8-mer extending a probe of any K
     int32_t min_k;              // shortest probe
     int32_t rank_off, estart_off, ent_off;   // dword offsets of the other sections
-                                             // (entries: adapter << 9 | band class << 8 | offset)
+                                             // (entries: adapter << 12 | (K - 4) << 9 | band class << 8 | offset)
     uint4 *raw;                 // per scan block a slab of raw hits (read, position | kSlowBit,
                                 // 8-mer code | valid run << 16, 0): the expansion reads no read bytes
     int32_t slab;
@@ -116,12 +117,40 @@ struct ScanArgs {
     int32_t ent2_off;           // dword offset of the entries' inside limits (lo | hi << 16): a task
                                 // is inside when q >= lo and (read length - q) > hi
     int32_t pin_cls[kCls];      // class c's inside tasks run the pinned band: records (read,
-                                // adapter << 8 | o, the probe's byte offset in codes: lo, hi)
+                                // adapter << 11 | (K - 4) << 8 | o, the probe's byte offset in codes: lo, hi)
     const int64_t *seg_cum;     // n + 1 entries: segments (kSeg positions) before each read, the total last
 };
 
 __device__ __forceinline__ int64_t dev_count(const int32_t *n_dev, int64_t n) {
     return n_dev ? min((int64_t)*n_dev, n) : n;
+}
+
+// Verified seeds (the device rounds' candidate windows): every band task whose bound
+// reaches its adapter's T is recorded as (read, adapter | E << 24, the diagonal's codes offset
+// v_off[read] + d0 as lo / hi): an alignment scoring >= T has an exact piece, so its task is among
+// these, and its end cell lies within the band's reach of the diagonal. list == nullptr: off.
+struct VerOut {
+    int4 *list;
+    int32_t *cnt;
+    int32_t *flag;              // set when the list overflowed (the round reruns with a larger one)
+    int64_t cap;
+};
+// Every lane of the wave that reaches this call takes part (one atomic per wave).
+__device__ __forceinline__ void put_verified(const VerOut &vo, bool want, int32_t read, int32_t a, int E, int64_t dabs) {
+    const uint64_t m = __ballot(want);
+    if (!m) return;
+    const int lane = (int)(threadIdx.x & 63);
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    int b0 = 0;
+    if (lane == leader) b0 = atomicAdd(vo.cnt, __popcll(m));
+    b0 = __shfl(b0, leader);
+    if (want) {
+        const int64_t slot = (int64_t)b0 + __popcll(m & ((1ull << lane) - 1));
+        if (slot < vo.cap)
+            vo.list[slot] = make_int4(read, a | (E << 24), (int)(uint32_t)(uint64_t)dabs, (int)(uint32_t)((uint64_t)dabs >> 32));
+        else
+            atomicOr(vo.flag, 1);
+    }
 }
 
 // Segments (kSeg positions) of read r of a round: 0 past the round's read count.
@@ -368,7 +397,7 @@ __device__ __forceinline__ TaskCount expand_hit(const ScanArgs &a, const uint32_
         const int rr = rank[dw] + __popc(word & (bit - 1));
         const int e = estart[rr + 1];
         for (int b = estart[rr]; b < e; ++b) {
-            const int en = ent[b];                       // adapter << 9 | class << 8 | offset
+            const int en = ent[b];                       // adapter << 12 | (K - 4) << 9 | class << 8 | offset
             const uint32_t lim = ent2[b];
             const bool inside = q >= (int)(lim & 0xFFFFu) && dist > (int)(lim >> 16);
             const int cls = (en >> 8) & 1;
@@ -381,15 +410,15 @@ __device__ __forceinline__ TaskCount expand_hit(const ScanArgs &a, const uint32_
                     at.in += one;
                     if (g < a.cap) {
                         if (a.pin_cls[cls])
-                            region[g] = make_int4((int)rd, ((en >> 9) << 8) | (en & 255), (int)(uint32_t)probe0,
+                            region[g] = make_int4((int)rd, ((en >> 12) << 11) | (((en >> 9) & 7) << 8) | (en & 255), (int)(uint32_t)probe0,
                                                   (int)(uint32_t)((uint64_t)probe0 >> 32));
                         else
-                            region[g] = make_int4((int)rd, en >> 9, q - (en & 255), en & 255);
+                            region[g] = make_int4((int)rd, en >> 12, q - (en & 255), en & 255);
                     }
                 } else {
                     const long long g = (at.edge >> sh) & 0xFFFFFFFFll;
                     at.edge += one;
-                    if (g < a.ecap) region[a.cap + g] = make_int4((int)rd, en >> 9, q - (en & 255), en & 255);
+                    if (g < a.ecap) region[a.cap + g] = make_int4((int)rd, en >> 12, q - (en & 255), en & 255);
                 }
             } else {
                 if (inside) c.in += one;
@@ -582,7 +611,7 @@ __global__ __launch_bounds__(256) void k_seed_band(const int4 *task, const int32
                                                    const uint8_t *codes, const int64_t *v_off, const int32_t *v_len,
                                                    const uint8_t *adp, int32_t adp_lds, const int32_t *adp_off,
                                                    const int32_t *adp_len, pcabi::Scoring sc, const int32_t *thr,
-                                                   int32_t *bound, int64_t n) {
+                                                   int32_t *bound, int64_t n, VerOut vo) {
     extern __shared__ uint32_t lds_adp[];
     const uint8_t *ad = adp;
     if (adp_lds > 0) {
@@ -603,6 +632,7 @@ __global__ __launch_bounds__(256) void k_seed_band(const int4 *task, const int32
         const int best = inside ? band_best<E, false>(rd, len, ac, L, d0, sc, T, codes)
                                 : band_best<E, true>(rd, len, ac, L, d0, sc, T, codes);
         atomicMax(&bound[(int64_t)tk.y * n + tk.x], best);
+        if (vo.list) put_verified(vo, best >= T, tk.x, tk.y, E, v_off[tk.x] + d0);
     }
 }
 
@@ -626,7 +656,7 @@ __global__ __launch_bounds__(256) void k_seed_band(const int4 *task, const int32
 // are never computed. Early exit as band_best: the running maximum plus best_sub per remaining row
 // plus the other half's bound (best_sub per row before it is known).
 //
-// Inside tasks (expand, pinned classes) carry (read, adapter << 8 | o, the probe's byte offset in
+// Inside tasks (expand, pinned classes) carry (read, adapter << 11 | (K - 4) << 8 | o, the probe's byte offset in
 // codes): the read bytes of the whole band, [probe - o - E, probe - o + L + E), are one range. Per
 // lane the range of the NEXT task is loaded (uint4 loads) while the current task computes, then
 // copied to the lane's LDS slot (NC4 x 16 bytes), where the rows read their one new byte each: the
@@ -635,11 +665,11 @@ template <int E, int NC4>
 __global__ __launch_bounds__(256) void k_seed_band_pin(const int4 *task, const int32_t *n_task, int64_t cap,
                                                        const uint8_t *codes, const uint8_t *adp, int32_t adp_dw,
                                                        const int32_t *adp_off, const int32_t *adp_meta, int32_t n_adp,
-                                                       pcabi::Scoring sc, int32_t *bound, int64_t n) {
+                                                       pcabi::Scoring sc, int32_t *bound, int64_t n, VerOut vo) {
     constexpr int W = 2 * E + 1;
     extern __shared__ uint4 lds4[];
     uint32_t *lds = reinterpret_cast<uint32_t *>(lds4);
-    // LDS: the flat adapters (adp_dw dwords), their offsets, their meta (L | K << 8 | T << 12), then
+    // LDS: the flat adapters (adp_dw dwords), their offsets, their meta (L | T << 12), then
     // per lane NC4 uint4 of read bytes
     for (int i = threadIdx.x; i < adp_dw; i += 256) lds[i] = reinterpret_cast<const uint32_t *>(adp)[i];
     for (int i = threadIdx.x; i < n_adp; i += 256) {
@@ -659,7 +689,7 @@ __global__ __launch_bounds__(256) void k_seed_band_pin(const int4 *task, const i
     const uintptr_t lo_addr = (uintptr_t)codes & ~(uintptr_t)15;
     // the range of a task: [cb, cb + 16 * nld) with cb = (probe - o - E) & ~15
     auto range_of = [&](const int4 &rc, uintptr_t &cb, int &nld) {
-        const int a = rc.y >> 8, o = rc.y & 255;
+        const int a = rc.y >> 11, o = rc.y & 255;
         const int L = (int)((uint32_t)ameta[a] & 255u);
         const uintptr_t pa = (uintptr_t)codes + (uintptr_t)(((uint64_t)(uint32_t)rc.w << 32) | (uint32_t)rc.z);
         const uintptr_t lo = pa - (uintptr_t)(o + E), hi = pa - (uintptr_t)o + (uintptr_t)(L + E);
@@ -701,9 +731,9 @@ __global__ __launch_bounds__(256) void k_seed_band_pin(const int4 *task, const i
             t += stride;
         }
         // ---- this task
-        const int a = rc.y >> 8, o = rc.y & 255;
+        const int a = rc.y >> 11, o = rc.y & 255, K = kMinK + ((rc.y >> 8) & 7);
         const uint32_t meta = (uint32_t)ameta[a];
-        const int L = (int)(meta & 255u), K = (int)((meta >> 8) & 15u), T = (int)(meta >> 12);
+        const int L = (int)(meta & 255u), T = (int)(meta >> 12);
         const int aoff = aoffs[a];
         const int64_t bidx = (int64_t)a * n + rc.x;
         const uintptr_t pa = (uintptr_t)codes + (uintptr_t)(((uint64_t)(uint32_t)rc.w << 32) | (uint32_t)rc.z);
@@ -735,15 +765,21 @@ __global__ __launch_bounds__(256) void k_seed_band_pin(const int4 *task, const i
             apos = aoff + o - 1;
             adir = -1;
         };
+        // the task's diagonal as a codes offset (probe - o): the verified-seed record
+        const int64_t dabs = (int64_t)(((uint64_t)(uint32_t)rc.w << 32) | (uint32_t)rc.z) - o;
+        bool ver = false;
         if (active && rows == 0) {                    // the run ends the adapter: Q = 0
             if (o == 0) {
                 atomicMax(&bound[bidx], pin);
+                ver = pin >= T;
                 active = false;
             } else {
                 begin_prefix();
             }
         }
+        if (vo.list) put_verified(vo, ver, rc.x, a, E, dabs);
         while (__any(active)) {
+            ver = false;
             if (active) {
                 const int ab = ad[apos];
                 apos += adir;
@@ -776,18 +812,23 @@ __global__ __launch_bounds__(256) void k_seed_band_pin(const int4 *task, const i
                         begin_prefix();
                     } else {
                         atomicMax(&bound[bidx], mx + other);
+                        ver = mx + other >= T;
                         active = false;
                     }
                 }
             }
+            if (vo.list) put_verified(vo, ver, rc.x, a, E, dabs);
         }
     }
 }
 
 // The pairs whose bound reaches their adapter's threshold T[a], as (a << 32 | read) keys
 // (unordered; one atomic per wave), grid-stride over the n_dev x n_adp bounds (row stride n).
+// pmap != nullptr (the device rounds; pmap may be `bound` itself): a candidate pair's entry becomes its
+// index in the list, which its verified seeds' windows look up.
 __global__ __launch_bounds__(256) void k_cands(const int32_t *bound, int64_t n, const int32_t *n_dev, int32_t n_adp,
-                                               const int32_t *T, int64_t *out, int64_t cap, unsigned long long *cnt) {
+                                               const int32_t *T, int64_t *out, int64_t cap, unsigned long long *cnt,
+                                               int32_t *pmap) {
     const int64_t nr = dev_count(n_dev, n);
     const int64_t total = nr * n_adp;
     const int lane = threadIdx.x & 63;
@@ -803,7 +844,10 @@ __global__ __launch_bounds__(256) void k_cands(const int32_t *bound, int64_t n, 
         b0 = __shfl(b0, leader);
         if (want) {
             const unsigned long long slot = b0 + __popcll(m & ((1ull << lane) - 1));
-            if ((int64_t)slot < cap) out[slot] = (a << 32) | r;
+            if ((int64_t)slot < cap) {
+                out[slot] = (a << 32) | r;
+                if (pmap) pmap[a * n + r] = (int32_t)slot;
+            }
         }
     }
 }
@@ -876,6 +920,9 @@ struct State {
     int scan_blocks = 0;                          // resident k_seed_scan blocks
     int expand_blocks = 0;                        // resident k_seed_expand blocks
     int pin_blocks[kCls] = {0, 0};                // resident k_seed_band_pin blocks per class
+    Buf vseed;                                    // verified seeds (device rounds)
+    int64_t vcap = 0;
+    VerOut ver{nullptr, nullptr, nullptr, 0};     // the band launches' record target (list nullptr: off)
 };
 
 State *create() { return new State(); }
@@ -891,14 +938,14 @@ int plan(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hl
          const std::vector<int> &fb_rows, const pcabi::Scoring &sc, double threshold) {
     s->planned = true;
     s->ok = false;
-    if (!(threshold > 0.0) || sc.go >= 0 || sc.ge >= 0 || n_adp >= (1 << 22)) return 0;
+    if (!(threshold > 0.0) || sc.go >= 0 || sc.ge >= 0 || n_adp >= (1 << 19)) return 0;
     // band_best's early exit bounds the rows still to come by best_sub per row: sound only when no
     // row step can gain more (every gap step costs, checked above, and best_sub > 0 > go, ge)
     if (pcabi::best_sub(sc) <= 0) return 0;
     const double th = (threshold - 1e-5) / 100.0;
     if (th <= 0.0 || th > 1.0) return 0;
     std::vector<std::vector<std::vector<int32_t>>> lists(kNK);
-    std::vector<int32_t> es((size_t)n_adp, -1), pk((size_t)n_adp, 0);
+    std::vector<int32_t> es((size_t)n_adp, -1);
     std::vector<int32_t> thr((size_t)n_adp, INT32_MAX);   // not under the filter: the caller adds them
     double filt = 0.0, seed = kScanPos;
     int e_lo = kMaxE + 1, e_hi = -1;
@@ -912,22 +959,25 @@ int plan(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hl
         if (T <= pcabi::sf::NEG16 || T <= 0) return 0;   // no usable bound: the filter / cross product
         const int e = (int)std::floor((double)L * (1.0 - th) / th + 1e-9);
         if (e > kMaxE) return 0;
-        const int plen = L / (e + 1);
-        const int K = std::min(kMaxK, plen);
-        if (K < kMinK) return 0;
+        // e + 1 disjoint pieces covering the adapter, lengths L / (e + 1) or one more (the longer
+        // first): any cut works for the seed argument, and an even one gives the longest probes
+        // (a random position matches a K-probe with probability 4^-K; r02 cut L / (e + 1) bases
+        // per piece and left the remainder out, so 27 bp at e = 3 had four 6-mers instead of 7, 7,
+        // 7 and a 6-mer)
+        const int plen = L / (e + 1), extra = L % (e + 1);
+        if (std::min(kMaxK, plen) < kMinK) return 0;
         es[a] = e;
-        pk[a] = K;
         thr[a] = T;
         e_lo = std::min(e_lo, e);
         e_hi = std::max(e_hi, e);
         filt += kFilterCell * fb_rows[a];
-        auto &lk = lists[K - kMinK];
-        if (lk.empty()) lk.resize((size_t)1 << (2 * K));
-        for (int p = 0; p <= e; ++p) {
-            const int o = p * plen;
+        for (int p = 0, o = 0; p <= e; o += plen + (p < extra ? 1 : 0), ++p) {
+            const int K = std::min(kMaxK, plen + (p < extra ? 1 : 0));
+            auto &lk = lists[K - kMinK];
+            if (lk.empty()) lk.resize((size_t)1 << (2 * K));
             uint32_t code = 0;
             for (int t = 0; t < K; ++t) code = (code << 2) | hcodes[hoff[a] + o + t];
-            lk[code].push_back((a << 9) | o);   // the class bit (8) is set below
+            lk[code].push_back((a << 12) | ((K - kMinK) << 9) | o);   // the class bit (8) is set below
         }
     }
     if (e_hi < 0) return 0;
@@ -969,7 +1019,7 @@ int plan(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hl
             bits[A.bits_off[kk] + c / 32] |= 1u << (c % 32);
             estart.push_back((uint16_t)ent.size());
             for (int32_t x : lists[kk][c]) {
-                const int a = x >> 9;
+                const int a = x >> 12;
                 ent.push_back(x | (cls[a] << 8));
                 if (kk == kNK - 1)                     // the merged table: each random hit costs a band
                     seed += kBandCell * (double)hlen[a] * (2.0 * s->band[cls[a]] + 1.0) / (double)((size_t)1 << (2 * K));
@@ -1000,7 +1050,7 @@ int plan(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hl
     // per entry the inside-band limits of its tasks (k_seed_band: d0 - E >= 1, d0 + E + L + 1 < len)
     A.ent2_off = (int32_t)img.size();
     for (int32_t x : ent) {
-        const int a = x >> 9, o = x & 255, E = s->band[(x >> 8) & 1];
+        const int a = x >> 12, o = x & 255, E = s->band[(x >> 8) & 1];
         img.push_back((uint32_t)(o + E + 1) | ((uint32_t)(hlen[a] - o + E + 1) << 16));
     }
     A.tab_dw = (int32_t)img.size();
@@ -1022,16 +1072,16 @@ int plan(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hl
     if (int rc = s->adp.ensure(flat.size())) return rc;
     if (int rc = s->adp_off.ensure(4 * aoff.size())) return rc;
     if (int rc = s->adp_len.ensure(4 * alen.size())) return rc;
-    if (int rc = s->cnt.ensure(4 * kCnt)) return rc;
+    if (int rc = s->cnt.ensure(4 * (kCnt + 1))) return rc;
     if (int rc = s->thr.ensure(4 * thr.size())) return rc;
-    // the pinned band: adapters and their (offset, meta) in LDS, meta = L | K << 8 | T << 12
+    // the pinned band: adapters and their (offset, meta) in LDS, meta = L | T << 12 (a task carries its K)
     {
         std::vector<int32_t> meta((size_t)n_adp, 0);
         bool fits = s->adp_bytes <= kAdpLds && (size_t)n_adp * 8 <= (size_t)kAdpLds;
         for (int32_t a = 0; a < n_adp && fits; ++a)
             if (es[a] >= 0) {
                 if (thr[a] >= (1 << 19)) fits = false;
-                meta[a] = alen[a] | (pk[a] << 8) | (thr[a] << 12);
+                meta[a] = alen[a] | (thr[a] << 12);
             }
         const char *e = std::getenv("PCABI_SEED_PIN");
         const bool on = fits && !(e && e[0] == '0');
@@ -1086,7 +1136,7 @@ int launch_pin(State *s, int c, const int4 *task, const uint8_t *codes, const pc
     hipLaunchKernelGGL((k_seed_band_pin<E, NC4>), dim3((unsigned)blocks), dim3(256), lds, st, task,
                        (const int32_t *)s->cnt.p + c, s->cap, codes, (const uint8_t *)s->adp.p, s->adp_bytes / 4,
                        (const int32_t *)s->adp_off.p, (const int32_t *)s->adp_meta.p, s->n_adp, sc,
-                       (int32_t *)s->bound.p, n);
+                       (int32_t *)s->bound.p, n, s->ver);
     return 0;
 }
 
@@ -1135,11 +1185,11 @@ int launch_band(State *s, int E, int c, const uint8_t *codes, const int64_t *v_o
         if (n_in != 0)                                                                                          \
             hipLaunchKernelGGL(k_seed_band<X>, dim3(grid_of(n_in, kBandGrid)), dim3(256), (size_t)lds, st, task,  \
                                cnt + c, s->cap, codes, v_off, v_len, adp, lds, aoff, alen, sc,                  \
-                               (const int32_t *)s->thr.p, bound, n);                                            \
+                               (const int32_t *)s->thr.p, bound, n, s->ver);                                    \
         if (n_edge != 0)                                                                                        \
             hipLaunchKernelGGL(k_seed_band<X>, dim3(grid_of(n_edge, 512)), dim3(256), (size_t)lds, st_edge,      \
                                task + s->cap, cnt + kCls + c, s->ecap, codes, v_off, v_len, adp, lds, aoff,     \
-                               alen, sc, (const int32_t *)s->thr.p, bound, n);                                  \
+                               alen, sc, (const int32_t *)s->thr.p, bound, n, s->ver);                          \
         break;
         C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8) C(9) C(10) C(11) C(12) C(13) C(14) C(15)
 #undef C
@@ -1202,7 +1252,7 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
     if (int rc = s->raw.ensure(sizeof(uint4) * (size_t)s->raw_cap)) return rc;
     if (int rc = s->rawcnt.ensure(4 * (size_t)grid)) return rc;
     if (int rc = s->task.ensure(sizeof(int4) * kCls * (size_t)(s->cap + s->ecap))) return rc;
-    if (int rc = s->cnt.ensure(4 * kCnt)) return rc;
+    if (int rc = s->cnt.ensure(4 * (kCnt + 1))) return rc;
     if (int rc = s->bound.ensure(sizeof(int32_t) * (size_t)n * n_adp)) return rc;
     ScanArgs A = s->a;
     A.codes = codes;
@@ -1233,7 +1283,7 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
         A.seg_cum = (const int64_t *)s->segcum.p;
     }
     hipLaunchKernelGGL(k_bound_reset, dim3(1024), dim3(256), 0, st, (int32_t *)s->bound.p, n, n_dev, n_adp, A.cnt,
-                       kCnt, (unsigned long long *)s->ccnt.p);
+                       kCnt + 1, (unsigned long long *)s->ccnt.p);
     hipLaunchKernelGGL(k_seed_scan, dim3(grid), dim3(256), 4 * (size_t)A.bits_dw + 4, st, A);
     hipLaunchKernelGGL(k_seed_expand, dim3(s->expand_blocks), dim3(256), s->lds_bytes, st, A);
     SD_TRY(hipGetLastError());
@@ -1259,6 +1309,7 @@ bool grow(State *s, const int32_t (&c)[kCnt]) {
         for (int k = 0; k < kCls; ++k) most = std::max<int64_t>(most, std::max<int64_t>(c[k], 4 * (int64_t)c[kCls + k]));
         if (most > (1ll << 30)) return false;
         s->cap = std::max<int64_t>(2 * s->cap, most + most / 4);   // ecap follows (cap / 4)
+        if (s->vcap) s->vcap *= 2;                   // the verified-seed list shares the flag
     }
     return true;
 }
@@ -1306,6 +1357,7 @@ int bounds(State *s, const void *adps_key, const uint8_t *hcodes, const int32_t 
            std::vector<int64_t> *cands, const int64_t **dcands, int64_t *n_dcands, hipStream_t st) {
     if (mode <= 0 || n <= 0) return 0;
     (void)adps_key;
+    s->ver = VerOut{nullptr, nullptr, nullptr, 0};   // no verified seeds on this path
     if (int rc = check_plan(s, hcodes, hoff, hlen, n_adp, fb_rows, sc, threshold, st)) return rc;
     if (!s->ok) return 0;
     if (mode == 1 && !(s->cost_seed < 0.5 * s->cost_filter)) return 0;
@@ -1341,7 +1393,7 @@ int bounds(State *s, const void *adps_key, const uint8_t *hcodes, const int32_t 
     SD_TRY(hipMemsetAsync(s->ccnt.p, 0, 8, st));
     hipLaunchKernelGGL(k_cands, dim3((unsigned)std::min<int64_t>((tot + 255) / 256, kBandGrid)), dim3(256), 0, st,
                        (const int32_t *)s->bound.p, n, nullptr, n_adp, (const int32_t *)s->thr.p, (int64_t *)s->cands.p,
-                       s->ccap, (unsigned long long *)s->ccnt.p);
+                       s->ccap, (unsigned long long *)s->ccnt.p, nullptr);
     SD_TRY(hipGetLastError());
     unsigned long long nc = 0;
     SD_TRY(hipMemcpyAsync(&nc, s->ccnt.p, 8, hipMemcpyDeviceToHost, st));
@@ -1368,11 +1420,23 @@ int bounds(State *s, const void *adps_key, const uint8_t *hcodes, const int32_t 
 // expansion, both band classes (grid-stride over the device task counts) and k_cands; the keys
 // (a << 32 | read, unordered) land in *dcands, their count in *dcount (device uint64), and
 // *flags (device int32[2]) is set when a buffer overflowed (the caller reruns the round after
-// grow_after_overflow()).
+// grow_after_overflow()). vlist != nullptr (candidate windows): the band kernels also record the
+// verified seeds (*vlist, their count *vcount on the device: int4 (read, adapter | E << 24, diagonal
+// codes offset lo, hi)) and *pmap (n_adp x n, row stride n) maps a candidate pair to its index in
+// *dcands.
 int bounds_dev(State *s, const uint8_t *codes, const int64_t *v_off, const int32_t *v_len, int64_t n,
                const int32_t *n_dev, int32_t n_adp, const pcabi::Scoring &sc, const int64_t **dcands,
-               const unsigned long long **dcount, const int32_t **flags, hipStream_t st) {
+               const unsigned long long **dcount, const int32_t **flags, const int4 **vlist, const int32_t **vcount,
+               const int32_t **pmap, int64_t *vcap, hipStream_t st) {
+    const bool win = vlist != nullptr;
     if (!s->ok) return fail(PCABI_E_ARG, "seed plan not ready");
+    s->ver = VerOut{nullptr, nullptr, nullptr, 0};
+    if (win) {
+        if (s->vcap == 0) s->vcap = std::max<int64_t>(1 << 16, n);
+        if (int rc = s->vseed.ensure(sizeof(int4) * (size_t)s->vcap)) return rc;
+        if (int rc = s->cnt.ensure(4 * (kCnt + 1))) return rc;
+        s->ver = VerOut{(int4 *)s->vseed.p, (int32_t *)s->cnt.p + kVer, (int32_t *)s->cnt.p + kFlag + 1, s->vcap};
+    }
     if (int rc = enqueue_seeds(s, codes, v_off, v_len, n, n_dev, n_adp, sc, nullptr, st)) return rc;
     const int64_t tot = n * (int64_t)n_adp;
     if (s->ccap < tot) s->ccap = tot;
@@ -1380,11 +1444,18 @@ int bounds_dev(State *s, const uint8_t *codes, const int64_t *v_off, const int32
     // (ccnt zeroed by k_bound_reset)
     hipLaunchKernelGGL(k_cands, dim3((unsigned)std::min<int64_t>((tot + 255) / 256, kBandGrid)), dim3(256), 0, st,
                        (const int32_t *)s->bound.p, n, n_dev, n_adp, (const int32_t *)s->thr.p, (int64_t *)s->cands.p,
-                       s->ccap, (unsigned long long *)s->ccnt.p);
+                       s->ccap, (unsigned long long *)s->ccnt.p, win ? (int32_t *)s->bound.p : nullptr);
     SD_TRY(hipGetLastError());
     *dcands = (const int64_t *)s->cands.p;
     *dcount = (const unsigned long long *)s->ccnt.p;
     *flags = (const int32_t *)s->cnt.p + kFlag;
+    if (win) {
+        *vlist = (const int4 *)s->vseed.p;
+        *vcount = (const int32_t *)s->cnt.p + kVer;
+        *pmap = (const int32_t *)s->bound.p;
+        *vcap = s->vcap;
+    }
+    s->ver = VerOut{nullptr, nullptr, nullptr, 0};
     g_runs.fetch_add(1);
     return 0;
 }

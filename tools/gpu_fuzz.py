@@ -58,6 +58,7 @@ def main():
     fails = 0
     it = 0
     stats = {'alignments': 0, 'middle_reads': 0}
+    t_last = time.time()
     while time.time() < t_end:
         seed = seed0 * 1000003 + it
         it += 1
@@ -108,7 +109,8 @@ def main():
                 print('MIDDLE MISMATCH seed %d scheme %s threshold %s mode %s: got %d hits, exp %d' %
                       (seed, sc, th, mode, got.shape[1], exp.shape[1]), flush=True)
                 fails += 1
-        if it % 20 == 0:
+        if time.time() - t_last >= 20.0:             # a line at least every ~20 s (gpurun's hang check)
+            t_last = time.time()
             print('iteration %d: %d failing cases, %s' % (it, fails, stats), flush=True)
     print('done: %d iterations, %d failing cases, %s' % (it, fails, stats), flush=True)
     return min(fails, 100)
