@@ -280,31 +280,26 @@ __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
             d[8] = q2[0];
             d[9] = q2[1];
         };
-        int64_t b = lo;
-        advance(b);
-        int64_t nrd = 0, noff = 0;
-        int np = 0, nlen = 0;
-        uint32_t nd[10];
-#pragma unroll
-        for (int t = 0; t < 10; ++t) nd[t] = 0x04040404u;
-        bool nact = map(b, nrd, np, noff, nlen);
-        if (nact) fetch(noff, np, nlen, nd);
-        while (b < hi) {                               // wave-uniform
-            const int64_t crd = nrd, coff = noff;
-            const int cp = np, clen = nlen;
-            const bool cact = nact;
+        // Two segments in flight: while one is looked up, the next one's 40 bytes load (ping-pong
+        // buffers, so no register copies between steps)
+        struct Seg {
             uint32_t d[10];
-#pragma unroll
-            for (int t = 0; t < 10; ++t) d[t] = nd[t];
-            const int64_t bn = b + 64;
-            nact = false;
-            if (bn < hi) {
-                advance(bn);
-                nact = map(bn, nrd, np, noff, nlen);
-                if (nact) fetch(noff, np, nlen, nd);
-            }
-            b = bn;
-            if (!cact) continue;
+            int64_t rd, off;
+            int p, len;
+            bool act;
+        };
+        auto issue = [&](int64_t bb, Seg &g) {
+            g.act = false;
+            if (bb >= hi) return;
+            advance(bb);
+            g.act = map(bb, g.rd, g.p, g.off, g.len);
+            if (g.act) fetch(g.off, g.p, g.len, g.d);
+        };
+        auto process = [&](const Seg &g) {
+            if (!g.act) return;
+            const uint32_t (&d)[10] = g.d;
+            const int64_t crd = g.rd, coff = g.off;
+            const int cp = g.p, clen = g.len;
             // ---- the segment's 32 positions ----
             auto byte = [&](int j) -> uint32_t {
                 return (j & 3) == 3 ? d[j >> 2] >> 24 : (d[j >> 2] >> (8 * (j & 3))) & 0xFFu;
@@ -336,12 +331,19 @@ __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
                 hits &= full8;
                 if (a.min_k < kMaxK) slow = ~(uint32_t)(t2 | (t2 >> (a.min_k - kMinK))) & ~full8;
             }
-            const uint32_t any = hits | slow;
-            if (any) {                                 // ~15 % of the lanes: append to the block's slab
-                int slot = atomicAdd(&s_cnt, __popc(any));
-                uint32_t left = any;
-                const uint8_t *seg = a.codes + coff + cp;
-                while (left) {
+            // ~15 % of the lanes hold a hit: appended to the block's slab one hit per lane and pass
+            // (passes = the most hits of a lane, usually 1), one LDS atomic per pass
+            uint32_t left = hits | slow;
+            const uint8_t *seg = a.codes + coff + cp;
+            while (__any(left != 0)) {                 // wave-uniform
+                const bool has = left != 0;
+                const uint64_t m = __ballot(has);
+                const int leader = __ffsll((unsigned long long)m) - 1;
+                int base = 0;
+                if (lane == leader) base = atomicAdd(&s_cnt, __popcll(m));
+                base = __shfl(base, leader);
+                if (has) {
+                    const int slot = base + __popcll(m & ((1ull << lane) - 1));
                     const int i = __builtin_ctz(left);
                     left &= left - 1;
                     // the position's 8-mer from the (cached) read bytes, its valid run
@@ -352,9 +354,25 @@ __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
                     if (slot < a.slab)
                         slab[slot] = make_uint4((uint32_t)crd, (uint32_t)(cp + i) | ((slow >> i) & 1u ? kSlowBit : 0u),
                                                 c8 | (run << 16), (uint32_t)(clen - (cp + i)));
-                    ++slot;
                 }
             }
+        };
+        Seg sa, sb;
+#pragma unroll
+        for (int t = 0; t < 10; ++t) sa.d[t] = sb.d[t] = 0x04040404u;
+        sb.rd = sb.off = 0;
+        sb.p = sb.len = 0;
+        sb.act = false;
+        int64_t b = lo;
+        issue(b, sa);
+        while (b < hi) {                               // wave-uniform
+            issue(b + 64, sb);
+            process(sa);
+            b += 64;
+            if (b >= hi) break;
+            issue(b + 64, sa);
+            process(sb);
+            b += 64;
         }
     }
     __syncthreads();
