@@ -82,6 +82,8 @@ def parse():
                     help='drivers: reads whose decisions are compared with the same drivers over the oracle')
     ap.add_argument('--check-phase-check', type=int, default=400,
                     help='check_phase: check reads whose device reduction is compared with the oracle')
+    ap.add_argument('--rest-overlap', type=int, default=1,
+                    help='headline: both sides\' smaller buckets after both dominant launches (0: after each side)')
     ap.add_argument('--only-subs', default='', help='comma-separated sub-record names to run (default: all)')
     ap.add_argument('--sub', type=int, default=1,
                     help='endtrim at N=1: also time the middle workload (configs[2]) and the host-buffer path '
@@ -247,7 +249,21 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
         _lib.check(L.pcabi_event_create(ctypes.byref(e)), 'event')
         ev.append(e)
 
-    def align_side(sd, e0=None, e1=None, fused=False):
+    # the headline schedule's second caller stream: the two sides' smaller buckets run side by side
+    # after both dominant launches (each side's own call forks them over the library's side streams)
+    stream2 = vp()
+    _lib.check(L.pcabi_stream_create(ctypes.byref(stream2)), 'stream')
+    ev_fork, ev_join = vp(), vp()
+    _lib.check(L.pcabi_event_create(ctypes.byref(ev_fork)), 'event')
+    _lib.check(L.pcabi_event_create(ctypes.byref(ev_join)), 'event')
+
+    def align_rest(sd, st):
+        tab, cnt = sd['rest']
+        if cnt:
+            _lib.check(L.pcabi_align_cross_dev(sd['d_tiles'], sd['d_toff'], sd['d_len'], n, int(sd['lens'].max()), tab,
+                                               *sc, sd['d_res_rest'], sd['stride'], st), 'align')
+
+    def align_side(sd, e0=None, e1=None, fused=False, rest=True):
         _lib.check(L.pcabi_tile_windows_dev(d_codes, sd['d_off'], sd['d_len'], n, sd['d_toff'], sd['mq'],
                                             sd['d_tiles'], stream), 'tile')
         mx = int(sd['lens'].max())
@@ -263,7 +279,7 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
         # kernel itself, the roofline), then the other buckets side by side
         for key, d_res in (('dom', sd['d_res']), ('rest', sd['d_res_rest'])):
             tab, cnt = sd[key]
-            if not cnt:
+            if not cnt or (key == 'rest' and not rest):
                 continue
             if key == 'dom' and e0 is not None:
                 L.pcabi_event_record(e0, stream)
@@ -297,12 +313,24 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
     timed_fused = not headline
 
     def step(k=None, fused=False):
-        if k is None:
-            align_side(sides[0], fused=fused)
-            align_side(sides[1], fused=fused)
+        fused = fused if k is None else timed_fused
+        e = (None,) * 4 if k is None else tuple(ev[4 * k + i] for i in range(4))
+        if fused or not args.rest_overlap:
+            align_side(sides[0], e[0], e[1], fused=fused)
+            align_side(sides[1], e[2], e[3], fused=fused)
         else:
-            align_side(sides[0], ev[4 * k], ev[4 * k + 1], fused=timed_fused)
-            align_side(sides[1], ev[4 * k + 2], ev[4 * k + 3], fused=timed_fused)
+            # headline schedule: each side's dominant launch alone (its events are the kernel's own
+            # time), then both sides' smaller buckets together -- the start side's on `stream`, the
+            # end side's on stream2 -- so the latency-bound single-adapter buckets (50 bp, 1.6 k
+            # waves) overlap the other side's instead of leaving the GPU idle behind them
+            align_side(sides[0], e[0], e[1], rest=False)
+            align_side(sides[1], e[2], e[3], rest=False)
+            L.pcabi_event_record(ev_fork, stream)
+            L.pcabi_stream_wait_event(stream2, ev_fork)
+            align_rest(sides[0], stream)
+            align_rest(sides[1], stream2)
+            L.pcabi_event_record(ev_join, stream2)
+            L.pcabi_stream_wait_event(stream, ev_join)
         epilogue()
 
     for _ in range(args.warmup):

@@ -61,6 +61,7 @@ def lib():
         'pcabi_event_create': ([ctypes.POINTER(c_p)], c_int),
         'pcabi_event_destroy': ([c_p], c_int),
         'pcabi_event_record': ([c_p, c_p], c_int),
+        'pcabi_stream_wait_event': ([c_p, c_p], c_int),
         'pcabi_event_elapsed_ms': ([ctypes.POINTER(ctypes.c_float), c_p, c_p], c_int),
         'pcabi_adapters_create': ([c_p, c_p, c_p, ctypes.c_int32, ctypes.POINTER(c_p)], c_int),
         'pcabi_adapters_create_scored': ([c_p, c_p, c_p, ctypes.c_int32, c_int, c_int, c_int, c_int,
@@ -119,7 +120,7 @@ def exported_symbols():
             'pcabi_dev_malloc', 'pcabi_dev_free', 'pcabi_dev_h2d', 'pcabi_dev_d2h',
             'pcabi_dev_memset', 'pcabi_dev_sync', 'pcabi_dev_copy_async', 'pcabi_stream_create', 'pcabi_stream_destroy',
             'pcabi_stream_sync', 'pcabi_event_create', 'pcabi_event_destroy', 'pcabi_event_record',
-            'pcabi_event_elapsed_ms', 'pcabi_adapters_create', 'pcabi_adapters_create_scored', 'pcabi_adapters_destroy',
+            'pcabi_stream_wait_event', 'pcabi_event_elapsed_ms', 'pcabi_adapters_create', 'pcabi_adapters_create_scored', 'pcabi_adapters_destroy',
             'pcabi_tile_layout', 'pcabi_tile_windows_dev', 'pcabi_align_cross_dev', 'pcabi_align_cross_dev_marked',
             'pcabi_end_trim_dev',
             'pcabi_best_full_identity_dev', 'pcabi_first_hits_host', 'pcabi_first_hit_dev', 'pcabi_scan_create',

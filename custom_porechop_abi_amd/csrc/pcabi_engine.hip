@@ -1660,6 +1660,10 @@ int pcabi_event_create(void **ev) {
 }
 int pcabi_event_destroy(void *ev) { HIP_TRY(hipEventDestroy((hipEvent_t)ev)); return 0; }
 int pcabi_event_record(void *ev, void *stream) { HIP_TRY(hipEventRecord((hipEvent_t)ev, (hipStream_t)stream)); return 0; }
+int pcabi_stream_wait_event(void *stream, void *ev) {
+    HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)ev, 0));
+    return 0;
+}
 int pcabi_event_elapsed_ms(float *ms, void *start, void *stop) {
     HIP_TRY(hipEventSynchronize((hipEvent_t)stop));
     HIP_TRY(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop));

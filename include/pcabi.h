@@ -123,6 +123,8 @@ int pcabi_stream_sync(void *stream);
 int pcabi_event_create(void **ev);
 int pcabi_event_destroy(void *ev);
 int pcabi_event_record(void *ev, void *stream);
+/* later work on `stream` waits for `ev` (recorded on another stream): fork / join of caller streams */
+int pcabi_stream_wait_event(void *stream, void *ev);
 int pcabi_event_elapsed_ms(float *ms, void *start, void *stop);
 
 /*
