@@ -83,7 +83,10 @@ def parse():
     ap.add_argument('--check-phase-check', type=int, default=400,
                     help='check_phase: check reads whose device reduction is compared with the oracle')
     ap.add_argument('--rest-overlap', type=int, default=1,
-                    help='headline: both sides\' smaller buckets after both dominant launches (0: after each side)')
+                    help='headline: 2 = after both dominant launches, both sides\' smaller buckets each on its own '
+                         'stream; 1 = the two sides\' calls side by side; 0 = after each side\'s dominant launch')
+    ap.add_argument('--hw-queues', type=int, default=8,
+                    help='GPU_MAX_HW_QUEUES for this process when the environment does not set it (0: HIP default)')
     ap.add_argument('--only-subs', default='', help='comma-separated sub-record names to run (default: all)')
     ap.add_argument('--sub', type=int, default=1,
                     help='endtrim at N=1: also time the middle workload (configs[2]) and the host-buffer path '
@@ -95,6 +98,10 @@ def parse():
 
 def main():
     args = parse()
+    if args.hw_queues > 0 and 'GPU_MAX_HW_QUEUES' not in os.environ:
+        # hardware queues per process (HIP's default 4): the headline's smaller buckets run on one
+        # stream each (--rest-overlap 2), and streams beyond the queue count share queues
+        os.environ['GPU_MAX_HW_QUEUES'] = str(min(args.hw_queues, 32))
     rank = int(os.environ.get('RANK', '0'))
     world = int(os.environ.get('WORLD_SIZE', '1'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
@@ -177,8 +184,11 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
     dom = lambda x: 20 < len(x) <= 24
     start_sets = [a for a in sets if a.start_sequence]
     end_sets = [a for a in sets if a.end_sequence]
-    order_s = sorted(range(len(start_sets)), key=lambda k: not dom(start_sets[k].start_sequence[1]))
-    order_e = sorted(range(len(end_sets)), key=lambda k: not dom(end_sets[k].end_sequence[1]))
+    # the other adapters grouped by register bucket (rows = length rounded up to 4), so each bucket is
+    # one contiguous table (the headline's per-bucket streams)
+    rank_of = lambda x: (not dom(x), 0 if dom(x) else (len(x) + 3) // 4)
+    order_s = sorted(range(len(start_sets)), key=lambda k: rank_of(start_sets[k].start_sequence[1]))
+    order_e = sorted(range(len(end_sets)), key=lambda k: rank_of(end_sets[k].end_sequence[1]))
     start_adps = [start_sets[k].start_sequence[1] for k in order_s]
     end_adps = [end_sets[k].end_sequence[1] for k in order_e]
     pos_s, pos_e = np.argsort(order_s).astype(np.int32), np.argsort(order_e).astype(np.int32)
@@ -239,9 +249,18 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
         if nd < 0:
             raise _lib.PcabiError('tile layout failed')
         n_dom = sum(1 for x in adps if dom(x))
+        groups = []                                 # (table, result rows) per register bucket of the rest
+        k0 = n_dom
+        while k0 < len(adps):
+            k1 = k0
+            while k1 < len(adps) and (len(adps[k1]) + 3) // 4 == (len(adps[k0]) + 3) // 4:
+                k1 += 1
+            groups.append((table(adps[k0:k1]), vp(d_res.value + 4 * k0 * n)))
+            k0 = k1
         sides.append(dict(lens=lens, d_off=d_off, d_len=d_len, d_toff=h2d(toff), d_tiles=dalloc(4 * nd),
                           mq=int(np.diff(toff).max() // 256), dom=table(adps[:n_dom]), rest=table(adps[n_dom:]),
-                          all=table(adps), d_res=d_res, d_res_rest=vp(d_res.value + 4 * n_dom * n), stride=stride))
+                          all=table(adps), d_res=d_res, d_res_rest=vp(d_res.value + 4 * n_dom * n), stride=stride,
+                          groups=groups))
 
     ev = []
     for _ in range(4 * args.steps + 4):
@@ -256,6 +275,31 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
     ev_fork, ev_join = vp(), vp()
     _lib.check(L.pcabi_event_create(ctypes.byref(ev_fork)), 'event')
     _lib.check(L.pcabi_event_create(ctypes.byref(ev_join)), 'event')
+
+    n_groups = sum(len(sd['groups']) for sd in sides)
+    g_streams, g_join = [], []
+    for _ in range(n_groups):
+        gs, ge = vp(), vp()
+        _lib.check(L.pcabi_stream_create(ctypes.byref(gs)), 'stream')
+        _lib.check(L.pcabi_event_create(ctypes.byref(ge)), 'event')
+        g_streams.append(gs)
+        g_join.append(ge)
+
+    def align_groups():
+        # every smaller bucket of both sides on its own stream, after both dominant launches
+        L.pcabi_event_record(ev_fork, stream)
+        j = 0
+        for sd in sides:
+            mx = int(sd['lens'].max())
+            for (tab, cnt), d_res in sd['groups']:
+                gs = g_streams[j]
+                L.pcabi_stream_wait_event(gs, ev_fork)
+                _lib.check(L.pcabi_align_cross_dev(sd['d_tiles'], sd['d_toff'], sd['d_len'], n, mx, tab, *sc, d_res,
+                                                   sd['stride'], gs), 'align')
+                L.pcabi_event_record(g_join[j], gs)
+                j += 1
+        for e in g_join:
+            L.pcabi_stream_wait_event(stream, e)
 
     def align_rest(sd, st):
         tab, cnt = sd['rest']
@@ -325,6 +369,10 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
             # waves) overlap the other side's instead of leaving the GPU idle behind them
             align_side(sides[0], e[0], e[1], rest=False)
             align_side(sides[1], e[2], e[3], rest=False)
+            if args.rest_overlap == 2:
+                align_groups()
+                epilogue()
+                return
             L.pcabi_event_record(ev_fork, stream)
             L.pcabi_stream_wait_event(stream2, ev_fork)
             align_rest(sides[0], stream)
