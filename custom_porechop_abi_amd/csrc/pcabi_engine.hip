@@ -108,9 +108,10 @@ bool middle_devplan_on() {
     return !(e && e[0] == '0');
 }
 
-// Queued rounds run the candidate DP over the verified seeds' windows instead of whole reads
-// (PCABI_MIDDLE_WINDOWS=1; off by default: a window's best is the whole read's only when no
-// alignment without an exact piece can outscore it -- work in progress).
+// Queued rounds run the candidate DP over the verified seeds' windows, with the whole read only for
+// the candidates whose window winner is a hit the certificate cannot vouch for (k_certify)
+// (PCABI_MIDDLE_WINDOWS=1). Off by default: the second plan's launches cost more than the windows
+// save on 8 kb reads (2.77 -> 2.96 ms per middle step), while 20 kb reads gain (4.31 -> 3.95 ms).
 bool middle_windows_on() {
     const char *e = std::getenv("PCABI_MIDDLE_WINDOWS");
     return e && e[0] == '1';
@@ -359,13 +360,13 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
 // nc_dev != nullptr: the candidate count is on the device (at most nc); the blocks stride.
 __global__ __launch_bounds__(256) void k_plan_count(const int64_t *cand, int64_t nc, const unsigned long long *nc_dev,
                                                     const int32_t *v_len, const int32_t *start, const int32_t *span,
-                                                    int32_t *adp_tasks) {
+                                                    int32_t *adp_tasks, const int32_t *cmask) {
     const int64_t ncl = nc_dev ? min((int64_t)*nc_dev, nc) : nc;
     const int lane = threadIdx.x & 63;
     for (int64_t b0 = (int64_t)blockIdx.x * 256; b0 < ncl; b0 += (int64_t)gridDim.x * 256) {   // uniform
         const int64_t i = b0 + threadIdx.x;
         const int64_t key = i < ncl ? cand[i] : 0;
-        const bool active = i < ncl && plan_valid(key, v_len, start);
+        const bool active = i < ncl && plan_valid(key, v_len, start) && (!cmask || cmask[i]);
         const int32_t a = active ? (int32_t)(key >> 32) : -1;
         int nt[kPlanC] = {0, 0, 0, 0};
         if (active) {
@@ -396,14 +397,14 @@ __global__ __launch_bounds__(256) void k_plan_place(const int64_t *cand, int64_t
                                                     const int32_t *v_len, const int32_t *start, const int32_t *span,
                                                     const int32_t *cidx, const int64_t *wave_off, int32_t *fill,
                                                     int32_t *tw, int32_t *to, int4 *tck, int32_t *tcand,
-                                                    const int64_t *slots_dev, int32_t *cbase_out) {
+                                                    const int64_t *slots_dev, int32_t *cbase_out, const int32_t *cmask) {
     const int64_t ncl = nc_dev ? min((int64_t)*nc_dev, nc) : nc;
     const int64_t slots = slots_dev ? *slots_dev : INT64_MAX;
     const int lane = threadIdx.x & 63;
     for (int64_t b0 = (int64_t)blockIdx.x * 256; b0 < ncl; b0 += (int64_t)gridDim.x * 256) {   // uniform
         const int64_t i = b0 + threadIdx.x;
         const int64_t key = i < ncl ? cand[i] : 0;
-        const bool active = i < ncl && plan_valid(key, v_len, start);
+        const bool active = i < ncl && plan_valid(key, v_len, start) && (!cmask || cmask[i]);
         const int32_t a = active ? (int32_t)(key >> 32) : -1, k = (int32_t)(key & 0xFFFFFFFF);
         int n = 0, D = -1, c = 0, nt = 0;
         if (active) {
@@ -595,17 +596,52 @@ __global__ __launch_bounds__(256) void k_merge_best(const int32_t *tw, const int
     }
 }
 
+// The candidate windows' certificate, per window slot that holds its candidate's best (k_merge_best):
+// only a winner that is a hit (full identity not below the threshold) needs one. If the whole
+// read's best alignment A* were a hit, it would have an exact piece and stay in its band, so it
+// would be in a window and be the windows' winner; so a winner that is no hit proves the pair has
+// no hit. A winner that is a hit is the whole read's best when its score is above U[a] (pcabi_seed
+// cert_bounds: every alignment without an exact piece, or with more gap columns than the band
+// allows, scores at most U[a]; U[a] >= T - 1). Otherwise the candidate is flagged (cmask 1, its
+// window best dropped) and its whole read runs in chunks. Block 0 also clears the plan counters for
+// that second plan.
+__global__ __launch_bounds__(256) void k_certify(const int64_t *cand, const int32_t *tw, const int4 *tck,
+                                                 const int32_t *tcand, const int32_t *res, int64_t slots,
+                                                 const int64_t *slots_dev, double thr, const int32_t *U,
+                                                 unsigned long long *best, int32_t *cmask, int32_t *adp_tasks,
+                                                 int32_t *fill, int32_t n_adp) {
+    if (blockIdx.x == 0) {
+        for (int i = threadIdx.x; i < n_adp * kPlanC; i += 256) adp_tasks[i] = 0;
+        for (int i = threadIdx.x; i < n_adp; i += 256) fill[i] = 0;
+    }
+    const int64_t ns = *slots_dev;
+    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < ns; q += (int64_t)gridDim.x * 256) {
+        if (tw[q] < 0) continue;
+        const int32_t ci = tcand[q];
+        const int32_t score = res[4 * slots + q];
+        if ((unsigned long long)merge_key(score, tck[q]) != best[ci]) continue;
+        const int rs = res[0 * slots + q];
+        const double full = rs == -1 ? 0.0 : pcabi::pid6(res[5 * slots + q], res[7 * slots + q]);
+        if (full < thr) continue;                    // no hit: the pair has none (NaN is a hit, as k_merge_hit)
+        if (score > U[(int32_t)(cand[ci] >> 32)]) continue;
+        cmask[ci] = 1;
+        best[ci] = 0ull;
+    }
+}
+
 // pass 0: per window the smallest adapter whose winning chunk reaches the threshold (atomicMin);
 // pass 1: that candidate writes the window's hit (rs / re back to whole-window offsets).
 // slots: the result rows' stride; slots_dev: the live slots (nullptr: all).
 __global__ __launch_bounds__(256) void k_merge_hit(const int64_t *cand, const int32_t *tw, const int4 *tck,
                                                    const int32_t *tcand, const int32_t *res, int64_t slots,
                                                    const int64_t *slots_dev, const unsigned long long *best, double thr,
-                                                   int pass, int32_t *hit_a, int32_t *hb, int64_t n) {
+                                                   int pass, int32_t *hit_a, int32_t *hb, int64_t n,
+                                                   const int32_t *cmask, int want) {
     const int64_t ns = slots_dev ? *slots_dev : slots;
     for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < ns; q += (int64_t)gridDim.x * 256) {
         if (tw[q] < 0) continue;
         const int32_t ci = tcand[q];
+        if (cmask && cmask[ci] != want) continue;    // (candidate windows: this plan does not decide it)
         const int4 ck = tck[q];
         const int32_t st = ck.x;
         if ((unsigned long long)merge_key(res[4 * slots + q], ck) != best[ci]) continue;
@@ -668,9 +704,13 @@ __global__ __launch_bounds__(256) void k_round_views(const int64_t *win_off, con
 // Before the merges: the candidates' best keys zeroed (k < *n_cand), the round's per-window hit
 // adapter (INT32_MAX) and hit table row 0 (-1) reset (k < *n_dev).
 __global__ __launch_bounds__(256) void k_merge_reset(unsigned long long *best, const unsigned long long *n_cand, int64_t cap,
-                                                     int32_t *hit_a, int32_t *hb, const int32_t *n_dev) {
+                                                     int32_t *hit_a, int32_t *hb, const int32_t *n_dev,
+                                                     int32_t *cmask) {
     const int64_t nc = min((int64_t)*n_cand, cap), nr = *n_dev;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nc; i += (int64_t)gridDim.x * 256) best[i] = 0ull;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nc; i += (int64_t)gridDim.x * 256) {
+        best[i] = 0ull;
+        if (cmask) cmask[i] = 0;
+    }
     for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < nr; k += (int64_t)gridDim.x * 256) {
         hit_a[k] = INT32_MAX;
         hb[k] = -1;
@@ -1081,6 +1121,7 @@ int bounds_dev(State *s, const uint8_t *codes, const int64_t *v_off, const int32
                const unsigned long long **dcount, const int32_t **flags, const int4 **vlist, const int32_t **vcount,
                const int32_t **pmap, int64_t *vcap, hipStream_t st);
 bool grow_after_overflow(State *s, int raw_overflow, int task_overflow);
+void cert_bounds(State *s, std::vector<int32_t> &U);
 int debug_counts(State *s, int64_t (&out)[5], hipStream_t st);
 }  // namespace pcabi_seed
 
@@ -1089,6 +1130,7 @@ struct pcabi_scan {
     DeviceBuf tiles, toff, res, hits, idx, start, soff, slen, mwin, ms, me;
     DeviceBuf s16, tw, to, wa, pres, tck;   // score filter + candidate pairs (chunks)
     DeviceBuf pspan, ptasks, pfill, pwoff, pcidx, pcand, pbest, phit, phb, plist, pcnt, plen;   // device planning
+    DeviceBuf tw2, to2, tck2, pcand2, wa2, pres2, pcert, pucert, q_bk2, q_misc2;   // candidate windows' second plan
     pcabi_seed::State *seed = nullptr; // seeded round-1 bounds (pcabi_seed.hip)
     // queued rounds (middle_device_rounds): per round slot the reads, their start adapters and the
     // hit list; round counts and flags; the plan's bucket tables and scratch
@@ -1096,6 +1138,7 @@ struct pcabi_scan {
     int32_t *h_stage = nullptr;                     // pinned host staging of the queued rounds' hit lists
     size_t h_stage_cap = 0;                         // (int32 elements)
     int64_t q_slots_cap = 0;
+    std::vector<int32_t> h_ucert;                   // the certificate bounds last uploaded to pucert
 };
 
 namespace {
@@ -1896,7 +1939,8 @@ void pcabi_scan_destroy(pcabi_scan *s) {
                          &s->mwin, &s->ms, &s->me, &s->s16, &s->tw, &s->to, &s->wa, &s->pres, &s->tck,
                          &s->pspan, &s->ptasks, &s->pfill, &s->pwoff, &s->pcidx, &s->pcand, &s->pbest, &s->phit, &s->phb,
                          &s->plist, &s->pcnt, &s->q_cur, &s->q_start, &s->q_list, &s->q_n, &s->q_flags,
-                         &s->q_bk, &s->q_wave, &s->q_misc, &s->pcbase})
+                         &s->q_bk, &s->q_wave, &s->q_misc, &s->pcbase, &s->plen, &s->tw2, &s->to2, &s->tck2,
+                         &s->pcand2, &s->wa2, &s->pres2, &s->pcert, &s->pucert, &s->q_bk2, &s->q_misc2})
         if (b->p) (void)hipFree(b->p);
     if (s->h_stage) (void)hipHostFree(s->h_stage);
     if (s->seed) pcabi_seed::destroy(s->seed);
@@ -1962,7 +2006,7 @@ int device_plan_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_off,
     HIP_TRY(hipMemsetAsync(sc->ptasks.p, 0, sizeof(int32_t) * n_adp * kPlanC, st));
     const unsigned gc = (unsigned)((nc + 255) / 256);
     hipLaunchKernelGGL(k_plan_count, dim3(gc), dim3(256), 0, st, dcand, nc, nullptr, v_len, d_start,
-                       (const int32_t *)sc->pspan.p, (int32_t *)sc->ptasks.p);
+                       (const int32_t *)sc->pspan.p, (int32_t *)sc->ptasks.p, nullptr);
     HIP_TRY(hipGetLastError());
     std::vector<int32_t> tasks((size_t)n_adp * kPlanC);
     HIP_TRY(hipMemcpyAsync(tasks.data(), sc->ptasks.p, sizeof(int32_t) * tasks.size(), hipMemcpyDeviceToHost, st));
@@ -2036,7 +2080,7 @@ int device_plan_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_off,
                        (const int32_t *)sc->pspan.p, (const int32_t *)sc->pcidx.p, (const int64_t *)sc->pwoff.p,
                        (int32_t *)sc->pfill.p,
                        (int32_t *)sc->tw.p, (int32_t *)sc->to.p, (int4 *)sc->tck.p, (int32_t *)sc->pcand.p, nullptr,
-                       nullptr);
+                       nullptr, nullptr);
     HIP_TRY(hipGetLastError());
     KParams p{};
     p.codes = codes;
@@ -2090,7 +2134,7 @@ int device_plan_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_off,
     for (int pass = 0; pass < 2; ++pass)
         hipLaunchKernelGGL(k_merge_hit, dim3(gs), dim3(256), 0, st, dcand, tw, tck, tcand, res, slots, nullptr,
                            (const unsigned long long *)sc->pbest.p, threshold, pass, (int32_t *)sc->phit.p,
-                           (int32_t *)sc->phb.p, n);
+                           (int32_t *)sc->phb.p, n, nullptr, 0);
     hipLaunchKernelGGL(k_hits_compact, dim3(gn), dim3(256), 0, st, (const int32_t *)sc->phb.p, n,
                        (int32_t *)sc->plist.p, (unsigned int *)sc->pcnt.p);
     HIP_TRY(hipGetLastError());
@@ -2480,6 +2524,11 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
     if (int rc = sc->pcbase.ensure(sizeof(int32_t) * n * n_adp)) return rc;
     if (int rc = sc->q_bk.ensure(4 * (bk_first.size() + 2 * bk_adp.size() + 2 * (size_t)n_bk + 16))) return rc;
     if (int rc = sc->q_misc.ensure(64)) return rc;   // [0] slots (int64), [8] need (int64), [16] plan flag
+    if (int rc = sc->q_misc2.ensure(64)) return rc;  // the second plan's slots and need
+    if (int rc = sc->q_bk2.ensure(4 * (2 * (size_t)n_bk + 16))) return rc;
+    if (int rc = sc->pcert.ensure(sizeof(int32_t) * n * n_adp)) return rc;
+    if (sc->pucert.cap < sizeof(int32_t) * (size_t)n_adp) sc->h_ucert.clear();   // (re)allocated below
+    if (int rc = sc->pucert.ensure(sizeof(int32_t) * n_adp)) return rc;
     int32_t *d_bk_first = (int32_t *)sc->q_bk.p, *d_bk_adp = d_bk_first + bk_first.size();
     int32_t *d_bk_local = d_bk_adp + bk_adp.size(), *d_bk_waves = d_bk_local + bk_adp.size();
     std::vector<int32_t> bk_host(bk_first);
@@ -2489,6 +2538,16 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
     HIP_TRY(hipMemcpyAsync(sc->pspan.p, span.data(), 4 * (size_t)n_adp, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(sc->plen.p, adps->hlen.data(), 4 * (size_t)n_adp, hipMemcpyHostToDevice, st));
     const bool windows = middle_windows_on();
+    if (windows) {
+        std::vector<int32_t> U;
+        pcabi_seed::cert_bounds(sc->seed, U);
+        if (U != sc->h_ucert) {                       // a new plan: its bounds up once (pageable: staged)
+            HIP_TRY(hipMemcpyAsync(sc->pucert.p, U.data(), 4 * (size_t)n_adp, hipMemcpyHostToDevice, st));
+            sc->h_ucert = U;
+        }
+    }
+    int32_t *d_bk_waves2 = (int32_t *)sc->q_bk2.p;
+    int64_t *d_slots2 = (int64_t *)sc->q_misc2.p, *d_need2 = d_slots2 + 1;
     int64_t *d_slots = (int64_t *)sc->q_misc.p, *d_need = d_slots + 1;
     int32_t *d_pflag = (int32_t *)(d_slots + 2);
     int32_t *d_n = (int32_t *)sc->q_n.p, *d_rflag = (int32_t *)sc->q_flags.p;
@@ -2496,11 +2555,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
     auto start_of = [&](int slot) { return (int32_t *)sc->q_start.p + (int64_t)slot * n; };
     auto list_of = [&](int slot) { return (int32_t *)sc->q_list.p + (int64_t)slot * 8 * n; };
     // round 1: every window (in window order: a round's results do not depend on its order)
-    {
-        const int32_t n32 = (int32_t)n;
-        HIP_TRY(hipMemcpyAsync(d_n, &n32, 4, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipStreamSynchronize(st));           // n32 leaves scope
-    }
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)d_n, (int)n, 1, st));   // (no host buffer to wait for)
     if (sc->q_slots_cap == 0) sc->q_slots_cap = std::max<int64_t>(1 << 20, 4 * n);
     const int64_t target = middle_plan_waves();
     const unsigned gn = (unsigned)std::min<int64_t>((n + 255) / 256, kGrid);
@@ -2536,45 +2591,59 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
                                             windows ? &vlist : nullptr, &vcount, &pmap, &vcap, st))
             return rc;
         const int64_t ncap = n * (int64_t)n_adp;
-        if (windows)
-            hipLaunchKernelGGL(k_wplan_count, dim3(kGrid), dim3(256), 0, st, vlist, vcount, vcap, v_len, start,
-                               (int32_t *)sc->ptasks.p);
-        else
-            hipLaunchKernelGGL(k_plan_count, dim3(kGrid), dim3(256), 0, st, dcand, ncap, dcount, v_len, start,
-                               (const int32_t *)sc->pspan.p, (int32_t *)sc->ptasks.p);
-        hipLaunchKernelGGL(k_plan_layout, dim3(1), dim3(256), 0, st, (const int32_t *)sc->ptasks.p, n_bk, d_bk_first,
-                           d_bk_adp, d_bk_local, target, slots_cap, (int32_t *)sc->pcidx.p, (int64_t *)sc->pwoff.p,
-                           (int32_t *)sc->wa.p, (int32_t *)sc->tw.p, d_bk_waves, d_slots, d_pflag, d_need);
-        if (windows) {
-            hipLaunchKernelGGL(k_wplan_place, dim3(kGrid), dim3(256), 0, st, vlist, vcount, vcap, v_off, v_len, start,
-                               (const int32_t *)sc->plen.p, (const int32_t *)sc->pspan.p, pmap, n,
-                               (const int64_t *)sc->pwoff.p, (int32_t *)sc->pfill.p, (int32_t *)sc->tw.p,
-                               (int32_t *)sc->to.p, (int4 *)sc->tck.p, (int32_t *)sc->pcand.p, (const int64_t *)d_slots);
-        } else {
-            hipLaunchKernelGGL(k_plan_place, dim3(kGrid), dim3(256), 0, st, dcand, ncap, dcount, v_len, start,
-                               (const int32_t *)sc->pspan.p, (const int32_t *)sc->pcidx.p, (const int64_t *)sc->pwoff.p,
-                               (int32_t *)sc->pfill.p, (int32_t *)sc->tw.p, (int32_t *)sc->to.p, (int4 *)sc->tck.p,
-                               (int32_t *)sc->pcand.p, (const int64_t *)d_slots, (int32_t *)sc->pcbase.p);
-            hipLaunchKernelGGL(k_plan_fill, dim3(kGrid), dim3(256), 0, st, dcand, ncap, dcount, v_len,
-                               (const int32_t *)sc->pspan.p, (const int32_t *)sc->pcidx.p, (const int32_t *)sc->pcbase.p,
-                               (int32_t *)sc->tw.p, (int32_t *)sc->to.p, (int4 *)sc->tck.p, (int32_t *)sc->pcand.p,
-                               (const int64_t *)d_slots);
-        }
-        HIP_TRY(hipGetLastError());
-        KParams p{};
-        p.codes = codes;
-        p.win_off = v_off;
-        p.win_len = v_len;
-        p.n_win = n;
-        p.out = (int32_t *)sc->pres.p;
-        p.out_stride = slots_cap;
-        p.sc = scr;
-        p.task_win = (const int32_t *)sc->tw.p;
-        p.task_out = (const int32_t *)sc->to.p;
-        p.wave_adp = (const int32_t *)sc->wa.p;
-        p.task_chunk = (const int4 *)sc->tck.p;
-        p.n_waves = kGrid;
-        {
+        // one candidate-DP plan into a set of task slots: WIN = the verified seeds' windows, else the
+        // candidates' whole-read chunks (cmask != nullptr: only the candidates it flags)
+        struct Plan {
+            DeviceBuf *tw, *to, *tck, *cand, *wa, *res;
+            int32_t *bk_waves;
+            int64_t *slots, *need;
+        };
+        auto run_plan = [&](const Plan &pl, bool win, const int32_t *cmask) -> int {
+            if (int rc = pl.tw->ensure(sizeof(int32_t) * slots_cap)) return rc;
+            if (int rc = pl.to->ensure(sizeof(int32_t) * slots_cap)) return rc;
+            if (int rc = pl.tck->ensure(sizeof(int4) * slots_cap)) return rc;
+            if (int rc = pl.cand->ensure(sizeof(int32_t) * slots_cap)) return rc;
+            if (int rc = pl.wa->ensure(sizeof(int32_t) * (slots_cap / 64 + 1))) return rc;
+            if (int rc = pl.res->ensure(sizeof(int32_t) * PCABI_NFIELDS * (size_t)slots_cap)) return rc;
+            if (win)
+                hipLaunchKernelGGL(k_wplan_count, dim3(kGrid), dim3(256), 0, st, vlist, vcount, vcap, v_len, start,
+                                   (int32_t *)sc->ptasks.p);
+            else
+                hipLaunchKernelGGL(k_plan_count, dim3(kGrid), dim3(256), 0, st, dcand, ncap, dcount, v_len, start,
+                                   (const int32_t *)sc->pspan.p, (int32_t *)sc->ptasks.p, cmask);
+            hipLaunchKernelGGL(k_plan_layout, dim3(1), dim3(256), 0, st, (const int32_t *)sc->ptasks.p, n_bk, d_bk_first,
+                               d_bk_adp, d_bk_local, target, slots_cap, (int32_t *)sc->pcidx.p, (int64_t *)sc->pwoff.p,
+                               (int32_t *)pl.wa->p, (int32_t *)pl.tw->p, pl.bk_waves, pl.slots, d_pflag, pl.need);
+            if (win) {
+                hipLaunchKernelGGL(k_wplan_place, dim3(kGrid), dim3(256), 0, st, vlist, vcount, vcap, v_off, v_len, start,
+                                   (const int32_t *)sc->plen.p, (const int32_t *)sc->pspan.p, pmap, n,
+                                   (const int64_t *)sc->pwoff.p, (int32_t *)sc->pfill.p, (int32_t *)pl.tw->p,
+                                   (int32_t *)pl.to->p, (int4 *)pl.tck->p, (int32_t *)pl.cand->p, (const int64_t *)pl.slots);
+            } else {
+                hipLaunchKernelGGL(k_plan_place, dim3(kGrid), dim3(256), 0, st, dcand, ncap, dcount, v_len, start,
+                                   (const int32_t *)sc->pspan.p, (const int32_t *)sc->pcidx.p,
+                                   (const int64_t *)sc->pwoff.p, (int32_t *)sc->pfill.p, (int32_t *)pl.tw->p,
+                                   (int32_t *)pl.to->p, (int4 *)pl.tck->p, (int32_t *)pl.cand->p,
+                                   (const int64_t *)pl.slots, (int32_t *)sc->pcbase.p, cmask);
+                hipLaunchKernelGGL(k_plan_fill, dim3(kGrid), dim3(256), 0, st, dcand, ncap, dcount, v_len,
+                                   (const int32_t *)sc->pspan.p, (const int32_t *)sc->pcidx.p,
+                                   (const int32_t *)sc->pcbase.p, (int32_t *)pl.tw->p, (int32_t *)pl.to->p,
+                                   (int4 *)pl.tck->p, (int32_t *)pl.cand->p, (const int64_t *)pl.slots);
+            }
+            HIP_TRY(hipGetLastError());
+            KParams p{};
+            p.codes = codes;
+            p.win_off = v_off;
+            p.win_len = v_len;
+            p.n_win = n;
+            p.out = (int32_t *)pl.res->p;
+            p.out_stride = slots_cap;
+            p.sc = scr;
+            p.task_win = (const int32_t *)pl.tw->p;
+            p.task_out = (const int32_t *)pl.to->p;
+            p.wave_adp = (const int32_t *)pl.wa->p;
+            p.task_chunk = (const int4 *)pl.tck->p;
+            p.n_waves = kGrid;
             ForkJoin fj;
             if (int rc = fj.begin(st, used.size())) return rc;
             for (int k = 0; k < n_bk; ++k) {
@@ -2584,26 +2653,57 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
                 p.adp_id = adps->id[b];
                 p.n_adp = adps->count[b];
                 p.rt = adps->rt[b];
-                p.dev_waves = d_bk_waves + 2 * k;
+                p.dev_waves = pl.bk_waves + 2 * k;
                 if (int rc = dispatch_chunk(b, p, scr.go != scr.ge, fj.at(k))) {
                     (void)fj.end();
                     return rc;
                 }
             }
             if (int rc = fj.end()) return rc;
+            HIP_TRY(hipGetLastError());
+            return 0;
+        };
+        const Plan pw{&sc->tw, &sc->to, &sc->tck, &sc->pcand, &sc->wa, &sc->pres, d_bk_waves, d_slots, d_need};
+        const Plan pf{&sc->tw2, &sc->to2, &sc->tck2, &sc->pcand2, &sc->wa2, &sc->pres2, d_bk_waves2, d_slots2, d_need2};
+        auto merge_best = [&](const Plan &pl) {
+            hipLaunchKernelGGL(k_merge_best, dim3(kGrid), dim3(256), 0, st, (const int32_t *)pl.tw->p,
+                               (const int4 *)pl.tck->p, (const int32_t *)pl.cand->p, (const int32_t *)pl.res->p,
+                               slots_cap, (const int64_t *)pl.slots, (unsigned long long *)sc->pbest.p);
+        };
+        auto merge_hit = [&](const Plan &pl, int pass, const int32_t *cmask, int want) {
+            hipLaunchKernelGGL(k_merge_hit, dim3(kGrid), dim3(256), 0, st, dcand, (const int32_t *)pl.tw->p,
+                               (const int4 *)pl.tck->p, (const int32_t *)pl.cand->p, (const int32_t *)pl.res->p,
+                               slots_cap, (const int64_t *)pl.slots, (const unsigned long long *)sc->pbest.p,
+                               threshold, pass, (int32_t *)sc->phit.p, (int32_t *)sc->phb.p, n, cmask, want);
+        };
+        if (!windows) {
+            if (int rc = run_plan(pw, false, nullptr)) return rc;
+            hipLaunchKernelGGL(k_merge_reset, dim3(kGrid), dim3(256), 0, st, (unsigned long long *)sc->pbest.p, dcount,
+                               ncap, (int32_t *)sc->phit.p, (int32_t *)sc->phb.p, nr, nullptr);
+            merge_best(pw);
+            for (int pass = 0; pass < 2; ++pass) merge_hit(pw, pass, nullptr, 0);
+        } else {
+            // the windows; then per candidate the certificate (k_certify): its best window score is the
+            // whole read's when it lies above every score an alignment without an exact piece, or
+            // with more gap columns than the band, can reach; the other candidates (flagged) run
+            // their whole reads in chunks, into the same merge
+            if (int rc = run_plan(pw, true, nullptr)) return rc;
+            hipLaunchKernelGGL(k_merge_reset, dim3(kGrid), dim3(256), 0, st, (unsigned long long *)sc->pbest.p, dcount,
+                               ncap, (int32_t *)sc->phit.p, (int32_t *)sc->phb.p, nr, (int32_t *)sc->pcert.p);
+            merge_best(pw);
+            hipLaunchKernelGGL(k_certify, dim3(kGrid), dim3(256), 0, st, dcand, (const int32_t *)pw.tw->p,
+                               (const int4 *)pw.tck->p, (const int32_t *)pw.cand->p, (const int32_t *)pw.res->p,
+                               slots_cap, (const int64_t *)pw.slots, threshold, (const int32_t *)sc->pucert.p,
+                               (unsigned long long *)sc->pbest.p, (int32_t *)sc->pcert.p, (int32_t *)sc->ptasks.p,
+                               (int32_t *)sc->pfill.p, n_adp);
+            const int32_t *flagged = (const int32_t *)sc->pcert.p;
+            if (int rc = run_plan(pf, false, flagged)) return rc;
+            merge_best(pf);
+            for (int pass = 0; pass < 2; ++pass) {
+                merge_hit(pw, pass, flagged, 0);      // certified candidates: their windows
+                merge_hit(pf, pass, nullptr, 0);      // flagged candidates: their whole reads
+            }
         }
-        HIP_TRY(hipGetLastError());
-        const int32_t *tw = (const int32_t *)sc->tw.p, *tcand = (const int32_t *)sc->pcand.p;
-        const int4 *tck = (const int4 *)sc->tck.p;
-        const int32_t *res = (const int32_t *)sc->pres.p;
-        hipLaunchKernelGGL(k_merge_reset, dim3(kGrid), dim3(256), 0, st, (unsigned long long *)sc->pbest.p, dcount, ncap,
-                           (int32_t *)sc->phit.p, (int32_t *)sc->phb.p, nr);
-        hipLaunchKernelGGL(k_merge_best, dim3(kGrid), dim3(256), 0, st, tw, tck, tcand, res, slots_cap,
-                           (const int64_t *)d_slots, (unsigned long long *)sc->pbest.p);
-        for (int pass = 0; pass < 2; ++pass)
-            hipLaunchKernelGGL(k_merge_hit, dim3(kGrid), dim3(256), 0, st, dcand, tw, tck, tcand, res, slots_cap,
-                               (const int64_t *)d_slots, (const unsigned long long *)sc->pbest.p, threshold, pass,
-                               (int32_t *)sc->phit.p, (int32_t *)sc->phb.p, n);
         hipLaunchKernelGGL(k_round_hits, dim3(gn), dim3(256), 0, st, (const int32_t *)sc->phb.p, n, nr, cur,
                            list_of(r), d_n + r + 1, cur_of(r + 1), start_of(r + 1), sflags, d_pflag, d_rflag + r);
         hipLaunchKernelGGL(k_mask_list, dim3(1024), dim3(256), 0, st, codes, win_off, list_of(r), d_n + r + 1);
@@ -2623,7 +2723,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
         return 0;
     };
     std::vector<int32_t> h_n(kSlots + 2), h_flag(kSlots + 2);
-    int64_t need = 0;
+    int64_t need = 0, need2 = 0;
     for (int guard = 0;; ++guard) {
         if (guard > 10000) return fail(PCABI_E_DEVICE, "middle scan: rounds did not settle");
         // queue up to kBatch rounds from `slot`
@@ -2634,6 +2734,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
         HIP_TRY(hipMemcpyAsync(h_n.data(), d_n, 4 * (size_t)(queued_to + 1), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipMemcpyAsync(h_flag.data(), d_rflag, 4 * (size_t)queued_to, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipMemcpyAsync(&need, d_need, 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(&need2, d_need2, 8, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         // the first flagged round (nothing of it or after it was kept): grow, queue it again
         int bad = -1;
@@ -2672,7 +2773,10 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
         if (bad >= 0) {
             if ((h_flag[bad] & 3) && !pcabi_seed::grow_after_overflow(sc->seed, h_flag[bad] & 1, (h_flag[bad] >> 1) & 1))
                 return fail(PCABI_E_DEVICE, "middle scan: seed buffers past their limits");
-            if (h_flag[bad] & 4) sc->q_slots_cap = std::max<int64_t>(2 * sc->q_slots_cap, need + need / 4);
+            if (h_flag[bad] & 4) {
+                const int64_t most = std::max(need, need2);
+                sc->q_slots_cap = std::max<int64_t>(2 * sc->q_slots_cap, most + most / 4);
+            }
             HIP_TRY(hipStreamSynchronize(st));
             slot = bad;
             continue;

@@ -939,6 +939,7 @@ struct State {
     int expand_blocks = 0;                        // resident k_seed_expand blocks
     int pin_blocks[kCls] = {0, 0};                // resident k_seed_band_pin blocks per class
     Buf vseed;                                    // verified seeds (device rounds)
+    std::vector<int32_t> ucert;                   // per adapter: the candidate windows' certificate bound
     int64_t vcap = 0;
     VerOut ver{nullptr, nullptr, nullptr, 0};     // the band launches' record target (list nullptr: off)
 };
@@ -1017,6 +1018,24 @@ int plan(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hl
     s->band[1] = std::max(s->band[0], e_hi);
     std::vector<int32_t> cls((size_t)n_adp, 0);
     for (int32_t a = 0; a < n_adp; ++a) cls[a] = es[a] > s->band[0] ? 1 : 0;
+    // The candidate windows' certificate (engine k_certify): a window best above U[a] is the whole
+    // read's. Every alignment scoring above U[a] has an exact piece and at most E gap columns, so its
+    // band task (E = its class's half-width) bounds it and is verified, and its end lies in that
+    // task's window. Relative to the ideal L * match, an alignment with no exact piece loses in every
+    // piece at least lam = min(match - mismatch, match + min|gap| (a deletion per touched piece),
+    // |gap_open| (an insertion run inside it)), except that the two end pieces may instead hang off a
+    // read end (match per hanging base); more than E gap columns cost at least min(|go| + E |ge|,
+    // (E + 1) |go|). Schemes where a mismatch scores at least a match certify nothing.
+    s->ucert.assign((size_t)n_adp, INT32_MAX);
+    for (int32_t a = 0; a < n_adp; ++a) {
+        if (es[a] < 0 || sc.mi >= sc.ma) continue;
+        const long long L = hlen[a], ma = sc.ma, E = s->band[cls[a]], np = es[a] + 1, plen = L / np;
+        const long long lam = std::min<long long>({ma - sc.mi, ma + std::min(-sc.go, -sc.ge), -sc.go});
+        const long long loss = np >= 2 ? (np - 2) * std::min(lam, ma * plen) + 2 * std::min(lam, ma) : std::min(lam, ma);
+        const long long gaps = std::min<long long>(-sc.go + E * -(long long)sc.ge, (E + 1) * -(long long)sc.go);
+        const long long u = std::max<long long>({ma * L - loss, ma * L - gaps, (long long)thr[a] - 1});
+        s->ucert[a] = (int32_t)std::min<long long>(u, INT32_MAX);
+    }
     // LDS image: bitmaps of the present K, per-dword rank (probes before the dword), the probe
     // entry ranges, the entries
     std::vector<uint32_t> bits;
@@ -1477,6 +1496,9 @@ int bounds_dev(State *s, const uint8_t *codes, const int64_t *v_off, const int32
     g_runs.fetch_add(1);
     return 0;
 }
+
+// The candidate windows' certificate bounds per adapter (plan(): INT32_MAX = never certified).
+void cert_bounds(State *s, std::vector<int32_t> &U) { U = s->ucert; }
 
 // After a device-resident run reported an overflow (flags from bounds_dev, read by the caller):
 // larger buffers for the rerun. Returns false past the limits.
