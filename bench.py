@@ -276,7 +276,7 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
     _lib.check(L.pcabi_event_create(ctypes.byref(ev_fork)), 'event')
     _lib.check(L.pcabi_event_create(ctypes.byref(ev_join)), 'event')
 
-    n_groups = sum(len(sd['groups']) for sd in sides)
+    n_groups = sum(len(sd['groups']) for sd in sides) if args.rest_overlap == 2 else 0
     g_streams, g_join = [], []
     for _ in range(n_groups):
         gs, ge = vp(), vp()
@@ -469,6 +469,11 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
                                   '(pcabi_align_cross_dev_marked): register buckets side by side with the dominant one'}
         subs['host_path'] = run_host_path(args, L, _lib, buf, s_off, s_len, e_off, e_len, sides, d_sres, d_eres, d_st,
                                           d_et, n, n_sa, n_ea, stream, start_adps, end_adps)
+
+    # the headline's extra streams go before the other configurations run (idle streams still take
+    # hardware queues from the ones the library creates later)
+    for st_ in [stream2] + g_streams:
+        L.pcabi_stream_destroy(st_)
 
     if rank == 0:
         value = world * n * args.steps / elapsed

@@ -2547,8 +2547,9 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
         }
     }
     int32_t *d_bk_waves2 = (int32_t *)sc->q_bk2.p;
-    int64_t *d_slots2 = (int64_t *)sc->q_misc2.p, *d_need2 = d_slots2 + 1;
-    int64_t *d_slots = (int64_t *)sc->q_misc.p, *d_need = d_slots + 1;
+    // q_misc: [0] slots, [1] need, [2] plan flag (int32), [3] the second plan's need (read with need)
+    int64_t *d_slots2 = (int64_t *)sc->q_misc2.p;
+    int64_t *d_slots = (int64_t *)sc->q_misc.p, *d_need = d_slots + 1, *d_need2 = d_slots + 3;
     int32_t *d_pflag = (int32_t *)(d_slots + 2);
     int32_t *d_n = (int32_t *)sc->q_n.p, *d_rflag = (int32_t *)sc->q_flags.p;
     auto cur_of = [&](int slot) { return (int32_t *)sc->q_cur.p + (int64_t)slot * n; };
@@ -2733,9 +2734,11 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
         queued_to = upto;
         HIP_TRY(hipMemcpyAsync(h_n.data(), d_n, 4 * (size_t)(queued_to + 1), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipMemcpyAsync(h_flag.data(), d_rflag, 4 * (size_t)queued_to, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipMemcpyAsync(&need, d_need, 8, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipMemcpyAsync(&need2, d_need2, 8, hipMemcpyDeviceToHost, st));
+        int64_t nd[3];                                // need, flag word, need2: one copy
+        HIP_TRY(hipMemcpyAsync(nd, d_need, sizeof(nd), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
+        need = nd[0];
+        need2 = nd[2];
         // the first flagged round (nothing of it or after it was kept): grow, queue it again
         int bad = -1;
         for (int r = slot; r < queued_to && bad < 0; ++r)
