@@ -253,9 +253,15 @@ def _end_decisions(reads, starts, ends, end_size, extra, thr, scoring_scheme_val
         part = np.where(failed, 0.0, engine.pid6(m, l1))
         re_x = np.where(failed, 0, re_ + 1)
         full, part, rs, re_x = (np.repeat(x, rep)[order] for x in (full, part, rs, re_x))
-        for i, k, f, p, a, b in zip(read[order].tolist(), set_k[order].tolist(), full.tolist(), part.tolist(),
-                                    rs.tolist(), re_x.tolist()):
-            getattr(reads[i], attr).append((sets[k], f, p, a, b))
+        # the tuples in one pass, then one extend per read (not one append per alignment)
+        rows = list(zip(map(sets.__getitem__, set_k[order].tolist()), full.tolist(), part.tolist(), rs.tolist(),
+                        re_x.tolist()))
+        rd = read[order]
+        cut = np.flatnonzero(np.diff(rd)) + 1
+        lo = np.concatenate([[0], cut]).tolist()
+        hi = np.concatenate([cut, [len(rd)]]).tolist()
+        for i, a, b in zip(rd[lo].tolist() if len(rd) else [], lo, hi):
+            getattr(reads[i], attr).extend(rows[a:b])
     if bc_full is not None:
         j0 = 0
         for side, sets in ((0, starts), (1, ends)):
