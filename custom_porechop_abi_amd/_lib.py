@@ -44,6 +44,7 @@ def lib():
         'pcabi_max_adapter_len': ([], c_int),
         'pcabi_max_window_len': ([], c_int),
         'pcabi_encode_dna5': ([c_p, c_p, c_i64], None),
+        'pcabi_encode_dna5_gather': ([c_p, c_p, c_p, c_i64, c_p, c_i64], None),
         'pcabi_pid6_host': ([c_p, c_p, c_i64, c_p], None),
         'pcabi_align_host': ([c_int, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_p, ctypes.c_int32,
                               c_p, c_p, c_i64, c_int, c_int, c_int, c_int, c_p], c_int),
@@ -116,7 +117,7 @@ def exported_symbols():
     lib()
     return ['adapterAlignment', 'freeCString', 'pcabi_last_error', 'pcabi_version',
             'pcabi_device_count', 'pcabi_max_adapter_len', 'pcabi_max_window_len',
-            'pcabi_encode_dna5', 'pcabi_pid6_host', 'pcabi_align_host', 'pcabi_dev_set',
+            'pcabi_encode_dna5', 'pcabi_encode_dna5_gather', 'pcabi_pid6_host', 'pcabi_align_host', 'pcabi_dev_set',
             'pcabi_dev_malloc', 'pcabi_dev_free', 'pcabi_dev_h2d', 'pcabi_dev_d2h',
             'pcabi_dev_memset', 'pcabi_dev_sync', 'pcabi_dev_copy_async', 'pcabi_stream_create', 'pcabi_stream_destroy',
             'pcabi_stream_sync', 'pcabi_event_create', 'pcabi_event_destroy', 'pcabi_event_record',

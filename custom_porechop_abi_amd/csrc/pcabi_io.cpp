@@ -700,6 +700,50 @@ void pcabi_gather_host(const uint8_t *src, const int64_t *src_off, const int32_t
         if (len[i] > 0) std::memcpy(dst + dst_off[i], src + src_off[i], (size_t)len[i]);
 }
 
+void pcabi_encode_dna5_gather(const uint64_t *src, const int64_t *len, const int64_t *dst_off, int64_t n,
+                              uint8_t *codes, int64_t codes_len) {
+    static const struct Tab {
+        uint8_t t[256];
+        Tab() {
+            for (int c = 0; c < 256; ++c) t[c] = 4;
+            t['A'] = t['a'] = 0;
+            t['C'] = t['c'] = 1;
+            t['G'] = t['g'] = 2;
+            t['T'] = t['t'] = t['U'] = t['u'] = 3;
+        }
+    } tab;
+    // segments [lo, hi) and the N gap after each (up to the next segment / codes_len)
+    auto run = [&](int64_t lo, int64_t hi) {
+        if (lo == 0 && n > 0) std::memset(codes, 4, (size_t)dst_off[0]);
+        for (int64_t i = lo; i < hi; ++i) {
+            const uint8_t *s = reinterpret_cast<const uint8_t *>(src[i]);
+            uint8_t *d = codes + dst_off[i];
+            for (int64_t k = 0; k < len[i]; ++k) d[k] = tab.t[s[k]];
+            const int64_t end = i + 1 < n ? dst_off[i + 1] : codes_len;
+            const int64_t gap = end - dst_off[i] - len[i];
+            if (gap > 0) std::memset(d + len[i], 4, (size_t)gap);
+        }
+    };
+    if (n <= 0) {
+        if (codes_len > 0) std::memset(codes, 4, (size_t)codes_len);
+        return;
+    }
+    // split by bytes, not by segments: chunk k starts at the first segment at or past k/nt of the total
+    const int nt = (int)std::min<int64_t>(16, std::max<int64_t>(1, codes_len / (4 << 20)));
+    if (nt <= 1) {
+        run(0, n);
+        return;
+    }
+    std::vector<int64_t> cut(nt + 1, n);
+    cut[0] = 0;
+    for (int k = 1; k < nt; ++k)
+        cut[k] = std::lower_bound(dst_off, dst_off + n, codes_len * k / nt) - dst_off;
+    std::vector<std::thread> th;
+    for (int k = 0; k < nt; ++k)
+        if (cut[k] < cut[k + 1]) th.emplace_back(run, cut[k], cut[k + 1]);
+    for (auto &t : th) t.join();
+}
+
 int64_t pcabi_reads_count(const pcabi_reads *b) { return b ? b->n : 0; }
 int pcabi_reads_type(const pcabi_reads *b) { return b ? b->type : -1; }
 

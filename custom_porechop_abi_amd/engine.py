@@ -24,6 +24,18 @@ for _c, _v in (('A', 0), ('C', 1), ('G', 2), ('T', 3), ('U', 3)):
 PAD = 16
 
 
+_AS_UTF8 = None
+
+
+def _as_utf8():
+    global _AS_UTF8
+    if _AS_UTF8 is None:
+        f = ctypes.pythonapi.PyUnicode_AsUTF8
+        f.restype, f.argtypes = ctypes.c_void_p, [ctypes.py_object]
+        _AS_UTF8 = f
+    return _AS_UTF8
+
+
 def _ptr(a):
     return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
 
@@ -81,6 +93,37 @@ class SeqPack(object):
         offs = np.zeros(len(seqs), dtype=np.int64)
         np.cumsum((lens + pads)[:-1], out=offs[1:])
         return joined.encode('ascii'), offs, lens.astype(np.int32)
+
+    @classmethod
+    def windows(cls, seqs, starts, lengths, index=None):
+        """The pack of [seqs[k][a:a + l] for k, a, l in zip(index, starts, lengths)] (index
+        defaults to every sequence once; same layout as SeqPack of those slices) without making
+        them: for ASCII str the codes are gathered from the strs' own buffers by
+        pcabi_encode_dna5_gather (one byte per base, so character positions are byte positions).
+        `starts` / `lengths` must lie inside each sequence."""
+        starts = np.asarray(starts, np.int64)
+        lengths = np.asarray(lengths, np.int64)
+        idx = np.arange(len(seqs)) if index is None else np.asarray(index, np.int64)
+        n = len(idx)
+        try:
+            ascii_str = n > 0 and all(map(str.isascii, seqs))
+        except TypeError:                              # bytes / arrays: the slicing path
+            ascii_str = False
+        if not ascii_str:
+            return cls([seqs[k][a:a + l] for k, a, l in zip(idx.tolist(), starts.tolist(), lengths.tolist())])
+        # CPython keeps an ASCII str's bytes inside the object: PyUnicode_AsUTF8 is their address
+        # (no copy), valid while `seqs` holds the strs -- i.e. for this call
+        base = np.fromiter(map(_as_utf8(), seqs), np.uint64, len(seqs))
+        addr = base[idx] + starts.astype(np.uint64)
+        offs = np.zeros(n, np.int64)
+        np.cumsum((lengths + ((-lengths) & 3))[:-1], out=offs[1:])
+        total = int(offs[-1] + lengths[-1] + ((-lengths[-1]) & 3)) + PAD
+        self = cls.__new__(cls)
+        self.codes = np.empty(total, np.uint8)
+        lib().pcabi_encode_dna5_gather(_ptr(addr), _ptr(lengths), _ptr(offs), n, _ptr(self.codes), total)
+        self.offsets = offs
+        self.lengths = lengths.astype(np.int32)
+        return self
 
     def __len__(self):
         return len(self.lengths)

@@ -14,6 +14,8 @@ every read against every adapter on the unmasked read; for each read the first a
 list order) with a hit is final for all adapters before it; the hit is masked and the read
 re-enters the next round from that adapter on. Rounds repeat until no read has a hit.
 """
+import contextlib
+import gc
 import sys
 
 import numpy as np
@@ -211,12 +213,37 @@ def end_windows_pack(reads, end_size):
     them (nanopore_read.py:181, 203), packed into one Dna5 buffer: (codes, start views, end views)
     -- only the 2 x end_size bases per read travel, not the whole reads."""
     n = len(reads)
-    pack = SeqPack([r.seq[:end_size] for r in reads] + [r.seq[-end_size:] for r in reads])
+    seqs = [r.seq for r in reads]
+    ln = np.fromiter(map(len, seqs), np.int64, n)
+    e = int(end_size)
+    s_len = np.clip(ln + e if e < 0 else np.minimum(ln, e), 0, None)      # seq[:e]
+    e_start = np.zeros(n, np.int64) if e == 0 else (np.maximum(ln - e, 0) if e > 0 else np.minimum(-e, ln))
+    pack = SeqPack.windows(seqs, np.concatenate([np.zeros(n, np.int64), e_start]),
+                           np.concatenate([s_len, ln - e_start]), index=np.tile(np.arange(n), 2))   # seq[-e:]
     return pack.codes, (pack.offsets[:n], pack.lengths[:n]), (pack.offsets[n:], pack.lengths[n:])
 
 
-def _end_decisions(reads, starts, ends, end_size, extra, thr, scoring_scheme_vals, min_trim, check_barcodes,
-                   fwd_rev):
+@contextlib.contextmanager
+def _gc_paused():
+    """The cyclic collector off while a driver makes its ~10^5 result tuples / lists: each
+    generation-2 pass would walk every NanoporeRead of the batch (a third of the end-trim
+    driver's host time at 100k reads). Nothing made here is cyclic garbage."""
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
+
+
+def _end_decisions(*args):
+    with _gc_paused():
+        _end_decisions_batch(*args)
+
+
+def _end_decisions_batch(reads, starts, ends, end_size, extra, thr, scoring_scheme_vals, min_trim, check_barcodes,
+                         fwd_rev):
     """The decisions of find_start_trim / find_end_trim (nanopore_read.py:175-217) for every read at
     once, on the device (engine.end_decisions: k_end_trim, then only the recorded alignments and --
     with -b -- the barcode identities come back): trim amounts, the start / end alignment lists in
@@ -239,13 +266,16 @@ def _end_decisions(reads, starts, ends, end_size, extra, thr, scoring_scheme_val
                                  (ends, e_idx, e_list, 'end_adapter_alignments')):
         if not sets or not lst.shape[1]:
             continue
-        # distinct sequence -> the sets holding it (set order)
-        members = {}
-        for k, u in enumerate(idx.tolist()):
-            members.setdefault(u, []).append(k)
+        # distinct sequence -> the sets holding it (set order), as index arrays: `mem` lists the
+        # sets grouped by distinct sequence, `first` / `cnt` each sequence's slice of it
+        idx = np.asarray(idx, np.int64)
+        cnt = np.bincount(idx, minlength=int(idx.max()) + 1)
+        mem = np.argsort(idx, kind='stable')
+        first = np.cumsum(cnt) - cnt
         read, u, rs, re_, m, l1, l2 = lst
-        rep = np.array([len(members[x]) for x in u.tolist()], np.int64)
-        set_k = np.concatenate([np.array(members[x], np.int64) for x in u.tolist()])
+        rep = cnt[u]
+        within = np.arange(int(rep.sum())) - np.repeat(np.cumsum(rep) - rep, rep)
+        set_k = mem[np.repeat(first[u], rep) + within]
         read = np.repeat(read, rep)
         order = np.lexsort((set_k, read))           # read-major, set order within a read
         failed = rs == -1
@@ -313,12 +343,27 @@ def middle_adapter_list(matching_sets):
     return adapters, start_names, end_names
 
 
-def scan_middles(seqs, adapter_seqs, middle_threshold, scoring_scheme_vals, device=0):
+def trimmed_bounds(reads):
+    """(start, length) of get_seq_with_start_end_adapters_trimmed() inside each read's seq, with
+    Python's slice rules for seq[s:len(seq) - e] (a negative stop counts from the end, both ends
+    clipped) -- the trimmed reads as views of the untrimmed ones, no copy."""
+    n = np.fromiter((len(r.seq) for r in reads), np.int64, len(reads))
+    s = np.fromiter((r.start_trim_amount for r in reads), np.int64, len(reads))
+    e = np.fromiter((r.end_trim_amount for r in reads), np.int64, len(reads))
+    a = np.minimum(s, n)
+    b = n - e
+    b = np.clip(np.where(b < 0, b + n, b), 0, n)
+    return a, np.maximum(b - a, 0)
+
+
+def scan_middles(seqs, adapter_seqs, middle_threshold, scoring_scheme_vals, device=0, bounds=None):
     """Exact batched equivalent of the reference's masked re-alignment loop
     (porechop_abi/nanopore_read.py:219-252), run on the GPU in rounds (engine.middle_scan,
     pcabi_middle_scan_host): round 1 keeps each read's first adapter over the threshold, later
     rounds re-align only the reads that just hit -- masked with '-' (Dna5 N) -- from that adapter
-    onwards.
+    onwards. `bounds` = (start, length) arrays scans those windows of `seqs` (in the sequences,
+    as trimmed_bounds gives them) instead of the whole sequences; positions are relative to the
+    window start.
 
     Returns, per read, the ordered list of hits (adapter_index, full_identity, read_start,
     read_end) that nanopore_read.find_middle_adapters would record."""
@@ -326,7 +371,7 @@ def scan_middles(seqs, adapter_seqs, middle_threshold, scoring_scheme_vals, devi
     hits = [[] for _ in range(n)]
     if n == 0 or not adapter_seqs:
         return hits
-    pack = SeqPack(seqs)
+    pack = SeqPack(seqs) if bounds is None else SeqPack.windows(seqs, *bounds)
     views = pack.views(np.zeros(n, np.int64), pack.lengths)
     h = engine.middle_scan(views, adapter_seqs, scoring_scheme_vals, middle_threshold, device=device)
     full = engine.pid6(h[4], h[5])
@@ -347,8 +392,10 @@ def find_adapters_in_read_middles(reads, matching_sets, verbosity, middle_thresh
     read_count = len(reads)
     if verbosity == 1:
         output_progress_line(0, read_count, print_dest)
-    seqs = [r.get_seq_with_start_end_adapters_trimmed() for r in reads]
-    all_hits = scan_middles(seqs, [a[1] for a in adapters], middle_threshold, scoring_scheme_vals)
+    # the trimmed reads packed straight from the untrimmed strs (SeqPack.windows), no slices
+    with _gc_paused():
+        all_hits = scan_middles([r.seq for r in reads], [a[1] for a in adapters], middle_threshold,
+                                scoring_scheme_vals, bounds=trimmed_bounds(reads))
     for r, hits in zip(reads, all_hits):
         for a, full, s0, e0 in hits:
             r._apply_middle_hit(adapters[a][0], full, s0, e0, extra_trim_good_side, extra_trim_bad_side,

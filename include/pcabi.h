@@ -80,6 +80,14 @@ int pcabi_max_window_len(void);          /* longest window / read the kernels ac
 
 /* ASCII -> Dna5 codes (host, table lookup). n bytes. */
 void pcabi_encode_dna5(const char *ascii, uint8_t *codes, int64_t n);
+/* Gathered ASCII -> Dna5 (host, up to 16 threads): codes[dst_off[i] .. + len[i]) = the codes of
+ * the len[i] bytes at address src[i]; every byte of codes[0 .. codes_len) outside those segments
+ * is set to N (4). dst_off ascending, segments disjoint. The Python drivers pass the addresses of
+ * the reads' own str buffers, so windows of 10^5 reads are packed without a slice, a join or an
+ * encode (replaces the per-read seq[:end_size] / seq[-end_size:] / trimmed-read slices that
+ * nanopore_read.py:181, 203 and porechop_abi.py:495 hand to SeqAn's marshalling). */
+void pcabi_encode_dna5_gather(const uint64_t *src, const int64_t *len, const int64_t *dst_off, int64_t n,
+                              uint8_t *codes, int64_t codes_len);
 
 /* Identity exactly as Python holds it after the reference's text round trip
  * (alignment.cpp:118-119 "%f", nanopore_read.py:497-498 float()): out[k] = pid6(m[k], l[k]),

@@ -95,3 +95,41 @@ def test_window_views_match_python_slices():
                 got = codes[off[k]:off[k] + ln[k]]
                 assert off[k] + ln[k] + 16 <= len(codes)      # the ABI's tail padding
                 assert np.array_equal(got, engine.encode_seq(sl))
+
+
+def test_gathered_windows_equal_packed_slices():
+    """SeqPack.windows (pcabi_encode_dna5_gather from the strs' own buffers) lays out exactly what
+    SeqPack of the slices does: codes byte for byte, N padding included; non-ASCII input takes
+    the slicing path. Covers the drivers' end windows and trimmed reads (porechop_abi.py)."""
+    import random
+    from custom_porechop_abi_amd import engine, porechop_abi as P
+    from custom_porechop_abi_amd.nanopore_read import NanoporeRead
+    rng = random.Random(7)
+    seqs = [''.join(rng.choice('ACGTNacgu-xyz') for _ in range(rng.randint(0, 3000))) for _ in range(700)]
+    seqs += ['', 'A', 'GATTACA' * 5000]
+    st = [rng.randint(0, len(s)) for s in seqs]
+    ln = [rng.randint(0, len(s) - a) for s, a in zip(seqs, st)]
+    want = engine.SeqPack([s[a:a + l] for s, a, l in zip(seqs, st, ln)])
+    for mixed in (False, True):
+        q = seqs + (['ACGTé'] if mixed else [])
+        got = engine.SeqPack.windows(q, st + [1] * mixed, ln + [3] * mixed)
+        ref = want if not mixed else engine.SeqPack([s[a:a + l] for s, a, l in zip(q, st + [1], ln + [3])])
+        assert np.array_equal(got.codes, ref.codes) and np.array_equal(got.offsets, ref.offsets)
+        assert np.array_equal(got.lengths, ref.lengths)
+    # 22 MB: the byte-balanced thread split (each thread starts at a segment boundary)
+    big = engine.SeqPack.windows(['ACGT' * 3000000, 'TTGCA' * 2000000], [5, 17], [12000000 - 5, 9999983 - 17])
+    assert np.array_equal(big.codes, engine.SeqPack([('ACGT' * 3000000)[5:], ('TTGCA' * 2000000)[17:9999983]]).codes)
+    # the drivers' end windows for every sign of end_size, and the trimmed reads
+    reads = [NanoporeRead('r%d' % i, s, '') for i, s in enumerate(seqs[:200])]
+    for E in (150, 1, 0, -3, 5000):
+        codes, (so, sl), (eo, el) = P.end_windows_pack(reads, E)
+        ref = engine.SeqPack([r.seq[:E] for r in reads] + [r.seq[-E:] for r in reads])
+        assert np.array_equal(codes, ref.codes)
+        assert np.array_equal(np.concatenate([so, eo]), ref.offsets)
+        assert np.array_equal(np.concatenate([sl, el]), ref.lengths)
+    for r in reads:
+        r.start_trim_amount, r.end_trim_amount = rng.randint(0, 400), rng.randint(0, 4000)
+    a, l = P.trimmed_bounds(reads)
+    got = engine.SeqPack.windows([r.seq for r in reads], a, l)
+    ref = engine.SeqPack([r.get_seq_with_start_end_adapters_trimmed() for r in reads])
+    assert np.array_equal(got.codes, ref.codes) and np.array_equal(got.lengths, ref.lengths)
