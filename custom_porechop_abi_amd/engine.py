@@ -113,6 +113,10 @@ class SeqPack(object):
             return cls([seqs[k][a:a + l] for k, a, l in zip(idx.tolist(), starts.tolist(), lengths.tolist())])
         # CPython keeps an ASCII str's bytes inside the object: PyUnicode_AsUTF8 is their address
         # (no copy), valid while `seqs` holds the strs -- i.e. for this call
+        have = np.fromiter(map(len, seqs), np.int64, len(seqs))[idx]
+        if len(starts) != n or len(lengths) != n or (starts < 0).any() or (lengths < 0).any() or \
+                (starts + lengths > have).any():
+            raise ValueError('SeqPack.windows: a window lies outside its sequence')
         base = np.fromiter(map(_as_utf8(), seqs), np.uint64, len(seqs))
         addr = base[idx] + starts.astype(np.uint64)
         offs = np.zeros(n, np.int64)

@@ -133,3 +133,10 @@ def test_gathered_windows_equal_packed_slices():
     got = engine.SeqPack.windows([r.seq for r in reads], a, l)
     ref = engine.SeqPack([r.get_seq_with_start_end_adapters_trimmed() for r in reads])
     assert np.array_equal(got.codes, ref.codes) and np.array_equal(got.lengths, ref.lengths)
+
+
+def test_gathered_windows_reject_out_of_range():
+    from custom_porechop_abi_amd import engine
+    for st, ln in (([0], [5]), ([-1], [1]), ([2], [-1]), ([0, 0], [1, 1])):
+        with pytest.raises(ValueError):
+            engine.SeqPack.windows(['ACGT'], st, ln)
