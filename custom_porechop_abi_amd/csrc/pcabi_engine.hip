@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <atomic>
 #include <cstdio>
 #include <memory>
 #include <cstdlib>
@@ -1121,6 +1122,7 @@ int bounds_dev(State *s, const uint8_t *codes, const int64_t *v_off, const int32
                const unsigned long long **dcount, const int32_t **flags, const int4 **vlist, const int32_t **vcount,
                const int32_t **pmap, int64_t *vcap, hipStream_t st);
 bool grow_after_overflow(State *s, int raw_overflow, int task_overflow);
+void shrink_next(State *s, int bits);
 void cert_bounds(State *s, std::vector<int32_t> &U);
 int debug_counts(State *s, int64_t (&out)[5], hipStream_t st);
 }  // namespace pcabi_seed
@@ -2448,6 +2450,28 @@ bool middle_devrounds_on() {
     return !(e && e[0] == '0');
 }
 
+// Overflow recovery of the queued rounds, counted for the tests (pcabi_middle_requeues).
+std::atomic<int64_t> g_requeues{0};
+std::atomic<int32_t> g_requeue_flags{0};
+
+// Tests: PCABI_MIDDLE_FAULT="round:bits[,round:bits...]" makes the first run of that round (0 =
+// round 1 of a call) overflow for real -- its raw-hit slabs (1), inside-task regions (2) and / or
+// candidate-DP task slots (4) shrunk to nothing -- so its kernels flag it, nothing of it is kept and
+// it is queued again (without growing: the real capacities were enough).
+std::vector<std::pair<int64_t, int>> middle_faults() {
+    std::vector<std::pair<int64_t, int>> f;
+    const char *e = std::getenv("PCABI_MIDDLE_FAULT");
+    while (e && *e) {
+        long long r = 0;
+        int bits = 0, used = 0;
+        if (std::sscanf(e, "%lld:%d%n", &r, &bits, &used) < 2 || used <= 0) break;
+        f.emplace_back((int64_t)r, bits & 7);
+        e += used;
+        if (*e == ',') ++e;
+    }
+    return f;
+}
+
 // The whole seeded middle scan as QUEUED rounds: no host synchronisation between the end trim and
 // the scan's result. Every round runs the seeded plan's steps with its counts on the device -- the
 // reads of the round (round 1: all windows, longest first by a device radix sort; later: those
@@ -2557,7 +2581,15 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
     auto list_of = [&](int slot) { return (int32_t *)sc->q_list.p + (int64_t)slot * 8 * n; };
     // round 1: every window (in window order: a round's results do not depend on its order)
     HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)d_n, (int)n, 1, st));   // (no host buffer to wait for)
-    if (sc->q_slots_cap == 0) sc->q_slots_cap = std::max<int64_t>(1 << 20, 4 * n);
+    if (sc->q_slots_cap == 0) {
+        sc->q_slots_cap = std::max<int64_t>(1 << 20, 4 * n);
+        long long raw = 0, task = 0, slots = 0;     // tests: PCABI_MIDDLE_INIT_CAPS="raw,task,slots"
+        if (const char *e = std::getenv("PCABI_MIDDLE_INIT_CAPS"))
+            if (std::sscanf(e, "%lld,%lld,%lld", &raw, &task, &slots) == 3 && slots > 0) sc->q_slots_cap = slots;
+    }
+    const std::vector<std::pair<int64_t, int>> faults = middle_faults();
+    std::vector<char> fired(faults.size(), 0);
+    int injected[kSlots + 1] = {};                  // per slot: the faults its last queueing injected
     const int64_t target = middle_plan_waves();
     const unsigned gn = (unsigned)std::min<int64_t>((n + 255) / 256, kGrid);
     std::vector<int32_t> out;                       // (round, 8 ints) of finished slots
@@ -2566,7 +2598,15 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
     int slot = 0;                                   // next round to queue (slot index)
     int queued_to = 0;                              // rounds [0, queued_to) are queued
     auto queue_round = [&](int r) -> int {
-        const int64_t slots_cap = sc->q_slots_cap;
+        int fault = 0;
+        for (size_t k = 0; k < faults.size(); ++k)
+            if (!fired[k] && faults[k].first == round_base + r) {
+                fault |= faults[k].second;
+                fired[k] = 1;
+            }
+        injected[r] = fault;
+        if (fault & 3) pcabi_seed::shrink_next(sc->seed, fault & 3);
+        const int64_t slots_cap = (fault & 4) ? 64 : sc->q_slots_cap;
         if (int rc = sc->tw.ensure(sizeof(int32_t) * slots_cap)) return rc;
         if (int rc = sc->to.ensure(sizeof(int32_t) * slots_cap)) return rc;
         if (int rc = sc->tck.ensure(sizeof(int4) * slots_cap)) return rc;
@@ -2774,9 +2814,18 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
                 std::fprintf(stderr, "[pcabi] middle queued round %lld: %d reads, %d hits, flag %d\n",
                              (long long)(round_base + r), h_n[r], h_n[r + 1], h_flag[r]);
         if (bad >= 0) {
-            if ((h_flag[bad] & 3) && !pcabi_seed::grow_after_overflow(sc->seed, h_flag[bad] & 1, (h_flag[bad] >> 1) & 1))
+            g_requeues.fetch_add(1);
+            g_requeue_flags.fetch_or(h_flag[bad] & 7);
+            // the rounds queued behind it ran on no reads: their injected faults fire again
+            for (size_t k = 0; k < faults.size(); ++k)
+                if (faults[k].first > round_base + bad) fired[k] = 0;
+            if (injected[bad]) {
+                // an injected overflow (tests): the real buffers were large enough, queue it again
+            } else if ((h_flag[bad] & 3) &&
+                       !pcabi_seed::grow_after_overflow(sc->seed, h_flag[bad] & 1, (h_flag[bad] >> 1) & 1)) {
                 return fail(PCABI_E_DEVICE, "middle scan: seed buffers past their limits");
-            if (h_flag[bad] & 4) {
+            }
+            if ((h_flag[bad] & 4) && !injected[bad]) {
                 const int64_t most = std::max(need, need2);
                 sc->q_slots_cap = std::max<int64_t>(2 * sc->q_slots_cap, most + most / 4);
             }
@@ -2818,6 +2867,11 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
 }  // namespace
 
 extern "C" {
+
+int64_t pcabi_middle_requeues(int32_t *flags_seen) {
+    if (flags_seen) *flags_seen = g_requeue_flags.load();
+    return g_requeues.load();
+}
 
 int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win_off, const int32_t *win_len,
                               const int32_t *h_win_len, int64_t n_win, int match, int mismatch, int gap_open,

@@ -941,6 +941,8 @@ struct State {
     Buf vseed;                                    // verified seeds (device rounds)
     std::vector<int32_t> ucert;                   // per adapter: the candidate windows' certificate bound
     int64_t vcap = 0;
+    int shrink = 0;                               // tests: the next seeding runs with 1 raw-hit slab entry (1)
+                                                  // and / or 1 inside task per class (2), see shrink_next()
     VerOut ver{nullptr, nullptr, nullptr, 0};     // the band launches' record target (list nullptr: off)
 };
 
@@ -1283,9 +1285,29 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
         s->expand_blocks = std::min(s->scan_blocks, std::max(1, cus * std::max(1, per_cu)));
     }
     const int grid = s->scan_blocks;
-    if (s->raw_cap == 0) s->raw_cap = (int64_t)grid * 4096;
-    if (s->cap == 0) s->cap = 1 << 22;
+    if (s->raw_cap == 0 || s->cap == 0) {
+        // first sizing; PCABI_MIDDLE_INIT_CAPS="raw,task[,slots]" (tests: small buffers that overflow
+        // and grow) overrides the defaults, 0 keeps one
+        int64_t raw = 0, task = 0;
+        if (const char *e = std::getenv("PCABI_MIDDLE_INIT_CAPS"))
+            if (std::sscanf(e, "%lld,%lld", (long long *)&raw, (long long *)&task) < 1) raw = task = 0;
+        if (s->raw_cap == 0) s->raw_cap = raw > 0 ? std::max<int64_t>(raw, grid) : (int64_t)grid * 4096;
+        if (s->cap == 0) s->cap = task > 0 ? task : 1 << 22;
+    }
+    // tests (shrink_next): this seeding's buffers shrunk to nothing, restored when it is queued
+    const int64_t cap_keep = s->cap;
+    const int shrink = s->shrink;
+    s->shrink = 0;
+    if (shrink & 2) s->cap = 1;
     s->ecap = std::max<int64_t>(s->cap / 4, 1 << 16);
+    struct Restore {
+        State *s;
+        int64_t cap;
+        ~Restore() {
+            s->cap = cap;
+            s->ecap = std::max<int64_t>(cap / 4, 1 << 16);
+        }
+    } restore{s, cap_keep};
     if (int rc = s->raw.ensure(sizeof(uint4) * (size_t)s->raw_cap)) return rc;
     if (int rc = s->rawcnt.ensure(4 * (size_t)grid)) return rc;
     if (int rc = s->task.ensure(sizeof(int4) * kCls * (size_t)(s->cap + s->ecap))) return rc;
@@ -1299,7 +1321,7 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
     A.n_dev = n_dev;
     A.raw = (uint4 *)s->raw.p;
     A.n_slab = grid;
-    A.slab = (int32_t)std::min<int64_t>(s->raw_cap / grid, INT32_MAX);
+    A.slab = (shrink & 1) ? 1 : (int32_t)std::min<int64_t>(s->raw_cap / grid, INT32_MAX);
     A.raw_cnt = (int32_t *)s->rawcnt.p;
     A.cnt = (int32_t *)s->cnt.p;
     A.flags = A.cnt + kFlag;
@@ -1496,6 +1518,11 @@ int bounds_dev(State *s, const uint8_t *codes, const int64_t *v_off, const int32
     g_runs.fetch_add(1);
     return 0;
 }
+
+// Tests (the engine's PCABI_MIDDLE_FAULT): the next queued seeding runs with its raw-hit slabs
+// (bits & 1) and / or its inside-task regions (bits & 2) shrunk to one entry, so its kernels overflow
+// for real and flag the round; the buffers keep their sizes.
+void shrink_next(State *s, int bits) { s->shrink = bits & 3; }
 
 // The candidate windows' certificate bounds per adapter (plan(): INT32_MAX = never certified).
 void cert_bounds(State *s, std::vector<int32_t> &U) { U = s->ucert; }

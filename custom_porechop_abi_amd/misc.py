@@ -289,6 +289,22 @@ def load_fasta_or_fastq(filename):
     return recs, 'FASTQ'
 
 
+# Terminal formatting of the verbose output (misc.py:270-316): the same escape codes.
+END_FORMATTING = '\033[0m'
+BOLD = '\033[1m'
+UNDERLINE = '\033[4m'
+RED = '\033[31m'
+YELLOW = '\033[93m'
+
+
+def red(text):
+    return RED + text + END_FORMATTING
+
+
+def yellow(text):
+    return YELLOW + text + END_FORMATTING
+
+
 def add_line_breaks_to_sequence(sequence, line_length):
     """misc.py:327-338."""
     if not sequence:

@@ -15,9 +15,12 @@ the trimming logic.
 
 Trimmed output (get_fasta / get_fastq / get_split_read_parts, :66-156) is mirrored for the
 per-read interface; the batched path writes through the native writer (misc.write_reads,
-pcabi_reads_write). Colourised verbose windows are not mirrored.
+pcabi_reads_write). The verbose views the drivers print at verbosity 2 and 3
+(formatted_start_seq ... middle_adapter_results, :254-406) give the reference's text, colour codes
+included (tests/golden/g6_verbose.json.gz).
 """
 from .cpp_function_wrappers import adapter_alignment
+from .misc import END_FORMATTING, RED, YELLOW, red, yellow
 
 
 class NanoporeRead(object):
@@ -182,6 +185,115 @@ class NanoporeRead(object):
         trim_start = read_start - (bad_side if adapter_name in start_sequence_names else good_side)
         trim_end = read_end + (bad_side if adapter_name in end_sequence_names else good_side)
         self.middle_trim_positions.update(range(trim_start, trim_end))
+
+    # --- verbose views (porechop_abi/nanopore_read.py:254-406) ----------------------------------
+    # The drivers print these at verbosity 2 (formatted_start_and_end_seq, middle_adapter_results)
+    # and 3 (full_start_end_output). Red = the trimmed adapter bases, yellow = the extra trim.
+    def formatted_start_seq(self, end_size, extra_trim_size):
+        window = self.seq[:end_size]
+        if not self.start_trim_amount:
+            return window
+        n_red = self.start_trim_amount - extra_trim_size
+        head = red(window[:n_red]) if n_red else ''
+        return head + yellow(window[n_red:n_red + extra_trim_size]) + window[n_red + extra_trim_size:]
+
+    def formatted_end_seq(self, end_size, extra_trim_size):
+        window = self.seq[-end_size:]
+        if not self.end_trim_amount:
+            return window
+        n_red = self.end_trim_amount - extra_trim_size
+        tail = red(window[-n_red:]) if n_red else ''
+        # slices as the reference takes them (n_red == 0 makes the yellow slice [-extra:0], empty)
+        return window[:-(n_red + extra_trim_size)] + yellow(window[-(n_red + extra_trim_size):-n_red]) + tail
+
+    def formatted_whole_seq(self, extra_trim_size):
+        if not self.start_trim_amount and not self.end_trim_amount:
+            return self.seq
+        n_start = self.start_trim_amount - extra_trim_size if self.start_trim_amount else 0
+        n_end = self.end_trim_amount - extra_trim_size if self.end_trim_amount else 0
+        if n_start + n_end >= len(self.seq):
+            return red(self.seq)
+        head = red(self.seq[:n_start]) if self.start_trim_amount else ''
+        tail = red(self.seq[-n_end:]) if self.end_trim_amount else ''
+        mid = self.seq[n_start:len(self.seq) - n_end]
+        if len(mid) <= 2 * extra_trim_size:
+            mid = yellow(mid)
+        else:
+            if self.start_trim_amount:
+                mid = yellow(mid[:extra_trim_size]) + mid[extra_trim_size:]
+            if self.end_trim_amount:
+                mid = mid[:-extra_trim_size] + yellow(mid[-extra_trim_size:])
+        return head + mid + tail
+
+    def formatted_start_and_end_seq(self, end_size, extra_trim_size, check_barcodes):
+        out = ''
+        if check_barcodes:
+            out += 'start: %s (%.1f%%), end: %s (%.1f%%), barcode call: %s   ' % (
+                self.best_start_barcode[0], self.best_start_barcode[1], self.best_end_barcode[0],
+                self.best_end_barcode[1], self.barcode_call)
+        if len(self.seq) <= 2 * end_size:
+            return out + self.formatted_whole_seq(extra_trim_size)
+        return out + self.formatted_start_seq(end_size, extra_trim_size) + '...' + \
+            self.formatted_end_seq(end_size, extra_trim_size)
+
+    @staticmethod
+    def get_alignment_string(aln):
+        """One recorded alignment (adapter, full, partial, read_start, read_end) as
+        full_start_end_output lists it (nanopore_read.py:331-333)."""
+        return '%s, full score=%s, partial score=%s, read position: %s-%s' % (
+            aln[0].name, str(aln[1]), str(aln[2]), str(aln[3]), str(aln[4]))
+
+    def full_start_end_output(self, end_size, extra_trim_size, check_barcodes):
+        lines = [self.name, '  start: ' + self.formatted_start_seq(end_size, extra_trim_size) + '...']
+        if self.start_adapter_alignments:
+            lines.append('    start alignments:')
+            lines += ['      ' + self.get_alignment_string(a) for a in self.start_adapter_alignments]
+        lines.append('  end:   ...' + self.formatted_end_seq(end_size, extra_trim_size))
+        if self.end_adapter_alignments:
+            lines.append('    end alignments:')
+            lines += ['      ' + self.get_alignment_string(a) for a in self.end_adapter_alignments]
+        if check_barcodes:
+            def listing(scores):
+                return ', '.join('%s (%.1f%%)' % (k, v) for k, v in scores.items())
+            lines += ['  Barcodes:',
+                      '    start barcodes:        ' + listing(self.start_barcode_scores),
+                      '    end barcodes:          ' + listing(self.end_barcode_scores),
+                      '    best start barcode:    %s (%.1f%%)' % self.best_start_barcode,
+                      '    best end barcode:      %s (%.1f%%)' % self.best_end_barcode]
+            if self.albacore_barcode_call is not None:
+                lines.append('    albacore barcode call: ' + self.albacore_barcode_call)
+            lines.append('    final barcode call:    ' + self.barcode_call)
+        return '\n'.join(lines) + '\n'
+
+    def formatted_middle_seq(self):
+        """The trimmed read around its middle hits (100 bases either side of the trim positions):
+        adapter bases red, the extra middle trim yellow; None without middle hits."""
+        if not self.middle_adapter_positions:
+            return None
+        seq = self.get_seq_with_start_end_adapters_trimmed()
+        lo = max(0, min(self.middle_trim_positions) - 100)
+        hi = min(len(seq), max(self.middle_trim_positions) + 100)
+        out = [] if lo == 0 else ['(%d bp)...' % lo]
+        last = None
+        for i in range(lo, hi):
+            c = RED if i in self.middle_adapter_positions else (YELLOW if i in self.middle_trim_positions else None)
+            if c != last:
+                out.append(END_FORMATTING + (c or ''))
+                last = c
+            out.append(seq[i])
+        if last is not None:
+            out.append(END_FORMATTING)
+        if hi != len(seq):
+            out.append('...(%d bp)' % (len(seq) - hi))
+        return ''.join(out)
+
+    def middle_adapter_results(self, verbosity):
+        if not self.middle_adapter_positions:
+            return ''
+        out = self.name + '\n' + self.middle_hit_str
+        if verbosity > 1:
+            out += self.formatted_middle_seq() + '\n'
+        return out
 
     def determine_barcode(self, barcode_threshold, barcode_diff, require_two_barcodes):
         """Barcode call from the start/end full-adapter identities (stable sorts: ties keep

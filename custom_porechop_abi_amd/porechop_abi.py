@@ -25,6 +25,7 @@ from .adapters import make_full_native_barcode_adapter, make_new_full_rapid_barc
     make_old_full_rapid_barcode_adapter
 from . import engine
 from .engine import SeqPack
+from .misc import red
 
 END_FORMATTING = '\033[0m'
 BOLD = '\033[1m'
@@ -46,6 +47,14 @@ def output_progress_line(completed, total, print_dest, end_newline=False, step=1
     pct = 100.0 * completed / total if total > 0 else 0.0
     line = '\r%s / %s (%.1f%%)' % (int_to_str(completed), int_to_str(total), pct)
     print(line, end='\n' if end_newline else '', flush=True, file=print_dest)
+
+
+def _replay_progress(read_count, print_dest, plus_one=False):
+    """The progress lines the reference's per-read loop prints after each read (every 10th and the
+    last, output_progress_line's step), emitted after the batch. plus_one: the middle phase's
+    thread-pool loop reports finished_count + 1 (porechop_abi.py:513-515)."""
+    for k in range(1, read_count + 1):
+        output_progress_line(k + 1 if plus_one else k, read_count, print_dest)
 
 
 def _unique(seqs):
@@ -76,6 +85,7 @@ def find_matching_adapter_sets(check_reads, verbosity, end_size, scoring_scheme_
         maxima = set_search_maxima(check_reads, end_size, scoring_scheme_vals, search)
         apply_set_maxima(search, maxima)
     if verbosity > 0:
+        _replay_progress(read_count, print_dest)
         output_progress_line(read_count, read_count, print_dest, end_newline=True)
     return [a for a in search if a.best_start_or_end_score() >= adapter_threshold]
 
@@ -188,8 +198,7 @@ def find_adapters_at_read_ends(reads, matching_sets, verbosity, end_size, extra_
         for s in matching_sets:
             for seq in (s.start_sequence, s.end_sequence):
                 if seq:
-                    print('  ' + seq[0].rjust(name_len) + ': ' + '\033[31m' + seq[1] + END_FORMATTING,
-                          file=print_dest)
+                    print('  ' + seq[0].rjust(name_len) + ': ' + red(seq[1]), file=print_dest)
         print('', file=print_dest)
     read_count = len(reads)
     if verbosity == 1:
@@ -202,6 +211,15 @@ def find_adapters_at_read_ends(reads, matching_sets, verbosity, end_size, extra_
         if check_barcodes:
             for r in reads:
                 r.determine_barcode(barcode_threshold, barcode_diff, require_two_barcodes)
+    # per read, in read order, what the reference's loop prints after each read (:395-402, 426-432)
+    if verbosity == 1:
+        _replay_progress(read_count, print_dest)
+    elif verbosity == 2:
+        for r in reads:
+            print(r.formatted_start_and_end_seq(end_size, extra_trim_size, check_barcodes), file=print_dest)
+    elif verbosity > 2:
+        for r in reads:
+            print(r.full_start_end_output(end_size, extra_trim_size, check_barcodes), file=print_dest)
     if verbosity == 1:
         output_progress_line(read_count, read_count, print_dest, end_newline=True)
     if verbosity > 0:
@@ -401,8 +419,10 @@ def find_adapters_in_read_middles(reads, matching_sets, verbosity, middle_thresh
             r._apply_middle_hit(adapters[a][0], full, s0, e0, extra_trim_good_side, extra_trim_bad_side,
                                 start_names, end_names)
         if r.middle_adapter_positions and verbosity > 1:
-            print(r.name + '\n' + r.middle_hit_str, file=print_dest, flush=True)
+            print(r.middle_adapter_results(verbosity), file=print_dest, flush=True)
     if verbosity == 1:
+        # the single-thread loop reports each read, the thread pool's loop one ahead (:492-493, 513-515)
+        _replay_progress(read_count, print_dest, plus_one=threads != 1)
         output_progress_line(read_count, read_count, print_dest, end_newline=True)
         print('', flush=True, file=print_dest)
 

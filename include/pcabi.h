@@ -272,10 +272,14 @@ int pcabi_first_hit_dev(const int32_t *res, int64_t stride, int64_t n_win, int32
 /*
  * The whole middle-adapter scan (porechop_abi/nanopore_read.py:219-252, the masked re-alignment
  * loop of find_middle_adapters) for a batch of end-trimmed reads, in rounds on the device:
- * round 1 aligns every read against every adapter and keeps each read's first hit
- * (k_first_hit); every later round masks the new hits in place (codes -> N, the reference's
- * '-') and re-aligns only the reads that just hit, from the adapter that hit onwards, until no
- * read hits. Hits are written to `hits` (HOST int32, 6 rows x cap: read, adapter, read_start,
+ * round 1 finds each read's first adapter whose best alignment reaches the threshold -- the pairs
+ * that can hit are found first, by exact k-mer seeds (pcabi_seed.hip: seed scan, expansion, banded
+ * bounds) or, where seeds do not apply, by a score-only filter, and only those candidates get the
+ * attribute DP (in owned-column chunks, planned on the device); every later round masks the new
+ * hits in place (codes -> N, the reference's '-') and re-aligns only the reads that just hit, from
+ * the adapter that hit onwards, until no read hits (DESIGN.md §4 "Middle scan"). Pairs where
+ * neither way applies run the full cross product with k_first_hit. Hits are written to `hits`
+ * (HOST int32, 6 rows x cap: read, adapter, read_start,
  * read_end (exclusive), m, l2 -- full identity = pid6(m, l2)) in discovery order, which per read
  * is the reference's order. Returns the number of hits (may exceed cap: only the first cap are
  * written) or a negative error. threshold must be > 0 (the reference never terminates otherwise).
@@ -291,6 +295,12 @@ int pcabi_first_hit_dev(const int32_t *res, int64_t stride, int64_t n_win, int32
  *                                 (pcabi_seed.hip) instead of the score filter, process-wide.
  *                                 PCABI_MIDDLE_SEEDS=0 / 1 (default, cost model) / 2 (always when
  *                                 the seeds apply) selects; the hits are the same either way.
+ *   pcabi_middle_requeues       : queued rounds that overflowed a buffer (raw-hit slabs, band task
+ *                                 regions, candidate-DP task slots), were dropped and queued again,
+ *                                 process-wide; *flags_seen (optional) = the OR of their flags
+ *                                 (1 raw hits, 2 band tasks, 4 task slots). Test knobs:
+ *                                 PCABI_MIDDLE_INIT_CAPS="raw,task,slots" sizes a new scan's buffers,
+ *                                 PCABI_MIDDLE_FAULT="round:bits,..." shrinks one round's buffers.
  */
 typedef struct pcabi_scan pcabi_scan;
 int pcabi_scan_create(const pcabi_adapters *adps, pcabi_scan **out);
@@ -306,6 +316,7 @@ int64_t pcabi_middle_scan_host(int device, const uint8_t *codes, int64_t codes_l
                                int gap_open, int gap_extend, double threshold, int32_t *hits,
                                int64_t cap);
 int64_t pcabi_middle_seed_runs(void);
+int64_t pcabi_middle_requeues(int32_t *flags_seen);
 
 /*
  * Adapter-set discovery reduction (porechop_abi/nanopore_read.py:158-173): for each adapter a
