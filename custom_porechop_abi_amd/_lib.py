@@ -134,7 +134,7 @@ def exported_symbols():
             'pcabi_reads_free', 'pcabi_reads_write', 'check_compatibility', 'pcabi_compat_host',
             'pcabi_compat_all_vs_all_host', 'pcabi_kmer_count_host', 'pcabi_kmer_top_host', 'pcabi_gather_host',
             'pcabi_kmer_approx_host', 'pcabi_io_release_cache', 'pcabi_best_full_identity_host',
-            'pcabi_middle_cuts_dev', 'pcabi_middle_cuts_host', 'pcabi_fastx_record_start', 'pcabi_fastx_set_range',
+            'pcabi_middle_cuts_dev', 'pcabi_middle_cuts_host', 'pcabi_fastx_record_start', 'pcabi_fastx_set_range', 'pcabi_fastx_next_text',
             'pcabi_end_decisions_host', 'pcabi_flag_list_dev', 'pcabi_trim_views_dev']
 
 

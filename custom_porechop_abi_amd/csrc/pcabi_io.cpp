@@ -82,12 +82,14 @@ struct pcabi_fastx {
     size_t pin = (size_t)-1;       // refills keep the bytes from here on (a batch's records)
     size_t pos = 0, end = 0;
     bool eof = false;
+    bool err = false;              // a read error (e.g. a truncated gzip stream): the next call fails
     int64_t line_no = 0;
     bool raw = false;              // keep the file's text (misc.load_fasta_or_fastq tuples)
     size_t size_hint = 0;          // decoded bytes expected (file size; x4 for gzip)
     // FASTA state that crosses batch boundaries
     bool fa_have_name = false;     // a header was seen (its name may be empty)
     std::string fa_name, fa_seq;
+    int txt_named = -1;            // pcabi_fastx_next_text: the last header had a name (1), none (0), no header (-1)
 };
 
 // Large batch buffers (>= 64 MB) come from anonymous mappings with transparent huge pages and
@@ -256,10 +258,13 @@ bool next_line(pcabi_fastx *r, const char **p, size_t *n) {
         if (r->buf.size() - r->end < (1u << 20)) r->buf.resize(std::max<size_t>(r->buf.size() * 2, 4u << 20));
         r->base = r->buf.data();
         const int got = gzread(r->f, r->buf.data() + r->end, (unsigned)std::min<size_t>(r->buf.size() - r->end, 1u << 30));
-        if (got < 0) {
-            int e = 0;
-            const char *m = gzerror(r->f, &e);
-            fail(PCABI_E_ARG, std::string("read error: ") + (m ? m : "?"));
+        int zerr = Z_OK;
+        const char *zmsg = got < 0 || got == 0 ? gzerror(r->f, &zerr) : nullptr;
+        if (got < 0 || (got == 0 && zerr != Z_OK && zerr != Z_STREAM_END)) {
+            // a damaged or truncated gzip stream: the reference's gzip module raises too
+            // (EOFError "Compressed file ended before the end-of-stream marker was reached")
+            fail(PCABI_E_PARSE, std::string("read error: ") + (zmsg ? zmsg : "?"));
+            r->err = true;
             r->eof = true;
             r->end = r->pos;   // drop the partial data
             return false;
@@ -671,12 +676,52 @@ int64_t pcabi_fastx_next(pcabi_fastx *r, int64_t max_reads, int64_t max_bases, p
             }
         }
     }
-    if (r->eof && r->pos >= r->end && r->type == PCABI_FASTQ) {
-        // nothing more
+    if (r->err) {
+        delete b;
+        return PCABI_E_PARSE;   // the message is pcabi_last_error()'s (next_line)
     }
     finish_batch(b);
     *out = b;
     return b->n;
+}
+
+// The next span of the decoded text holding whole records, cut where a reader starting afresh
+// parses the same records as the continuous read: FASTQ after a record whose successor's line
+// starts with '@'; FASTA before a header with a name whose preceding header had one (an empty
+// header's sequence runs on into the next record). At least max_bytes unless the input ends first
+// (one record may overshoot). *text stays valid until the next call on r. Returns 1, 0 at the end.
+int pcabi_fastx_next_text(pcabi_fastx *r, int64_t max_bytes, const char **text, int64_t *len) {
+    if (!r || !text || !len || max_bytes <= 0) return fail(PCABI_E_ARG, "bad arguments");
+    r->pin = r->pos;
+    const char *p;
+    size_t n;
+    for (;;) {
+        const size_t ls = r->pos - r->pin;           // this line's start, relative to the pin
+        if (!next_line(r, &p, &n)) break;
+        if (r->type == PCABI_FASTQ) {
+            bool whole = true;
+            for (int k = 0; k < 3 && whole; ++k) whole = next_line(r, &p, &n);
+            if (!whole) break;                        // truncated: the chunk's reader reports it
+            if ((int64_t)(r->pos - r->pin) >= max_bytes && r->pos < r->end && r->base[r->pos] == '@') break;
+        } else {
+            const char *q = p;
+            size_t m = n;
+            strip(&q, &m);
+            if (m > 0 && q[0] == '>') {
+                const int named = m > 1 ? 1 : 0;
+                if ((int64_t)ls >= max_bytes && p[0] == '>' && named && r->txt_named == 1) {
+                    r->pos = r->pin + ls;             // unread: the next span starts with this header
+                    break;
+                }
+                r->txt_named = named;
+            }
+        }
+    }
+    *text = r->base + r->pin;
+    *len = (int64_t)(r->pos - r->pin);
+    r->pin = (size_t)-1;
+    if (r->err) return PCABI_E_PARSE;
+    return *len > 0 ? 1 : 0;
 }
 
 int pcabi_fastx_load(const char *path, int raw, pcabi_reads **out) {

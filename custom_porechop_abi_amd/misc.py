@@ -49,6 +49,7 @@ def _declare(L):
         'pcabi_reads_write': ([P, ctypes.c_char_p, c_int, c_int, c_int, P, P, P, P, c_int, c_int, c_int, P], c_int),
         'pcabi_fastx_record_start': ([P, i64], i64),
         'pcabi_fastx_set_range': ([P, i64, i64], c_int),
+        'pcabi_fastx_next_text': ([P, i64, ctypes.POINTER(P), ctypes.POINTER(i64)], c_int),
     }
     for name, (a, r) in sig.items():
         f = getattr(L, name)
@@ -238,6 +239,28 @@ def read_batches(path, max_reads=100000, max_bases=1 << 30, raw=False, byte_rang
                 L.pcabi_reads_free(b)
                 return
             yield ReadBatch(b)
+    finally:
+        L.pcabi_fastx_close(h)
+
+
+def text_chunks(path, chunk_bytes):
+    """Stream a FASTA / FASTQ(.gz) file as spans of its decoded text holding whole records, cut
+    where a fresh reader parses the same records (pcabi_fastx_next_text): yields memoryviews of at
+    least chunk_bytes (the last may be shorter), each valid until the next one is requested."""
+    L = _declare(lib())
+    h = ctypes.c_void_p()
+    rc = L.pcabi_fastx_open(os.fsencode(path), 0, ctypes.byref(h))
+    if rc != 0:
+        raise ValueError(_open_error(path))
+    try:
+        while True:
+            p, n = ctypes.c_void_p(), ctypes.c_int64()
+            rc = L.pcabi_fastx_next_text(h, int(chunk_bytes), ctypes.byref(p), ctypes.byref(n))
+            if rc < 0:
+                raise ValueError(_open_error(path))
+            if rc == 0:
+                return
+            yield memoryview((ctypes.c_char * int(n.value)).from_address(p.value)).cast('B')
     finally:
         L.pcabi_fastx_close(h)
 

@@ -222,7 +222,7 @@ class FileTrimmer(object):
         return np.where(calls == want, calls, -1).astype(np.int32)
 
     def trim_file(self, in_path, out_path, out_format='fastq', max_reads=200000, byte_range=None, batch_filter=None,
-                  segments=None):
+                  segments=None, source=None):
         """Trim a FASTA / FASTQ(.gz) file -- or an Albacore output directory, its *.fastq(.gz) files
         in sorted order as load_reads reads them (porechop_abi.py:133-187), each batch carrying
         its file's barcode for the -b cross-check -- batch by batch into out_path. Returns read
@@ -230,7 +230,9 @@ class FileTrimmer(object):
 
         Shards (shards.trim_file_sharded): byte_range = (begin, end) record starts of a plain file
         reads only that range; batch_filter(k) False skips batch k (parsed, not trimmed or
-        written); segments, a list, receives (k, begin, end) byte spans of out_path per written batch.
+        written); segments, a list, receives (k, begin, end) byte spans of out_path per written batch;
+        source, an iterable of (key, ReadBatch, albacore barcode), replaces reading in_path (the
+        spooled chunks of shards.spool_batches; key is what segments record).
 
         Three stages overlap across batches: a reader thread parses the next batch, this thread
         runs the device work, a writer thread writes the previous batch (in file order). The
@@ -266,7 +268,8 @@ class FileTrimmer(object):
 
         def produce():
             try:
-                for k, (b, alb) in enumerate(batches()):
+                items = source if source is not None else ((k, b, alb) for k, (b, alb) in enumerate(batches()))
+                for k, b, alb in items:
                     if batch_filter is not None and not batch_filter(k):
                         continue
                     if not put_parsed((k, b, alb)):

@@ -56,14 +56,21 @@ def _device_tensor(values, group):
 
 def rank_device(device=None):
     """The GPU of this rank: `device` if given, else LOCAL_RANK (torch.distributed.run sets it),
-    else 0 -- one process per GPU, each rank on its own card."""
+    else the rank in the default group (launchers that set RANK only: one process per GPU of a
+    single node), else 0. A local rank past the node's GPU count is an error, not a shared card."""
     import os
     if device is not None:
         return int(device)
-    dev = int(os.environ.get('LOCAL_RANK', '0'))
+    if 'LOCAL_RANK' in os.environ:
+        dev = int(os.environ['LOCAL_RANK'])
+    else:
+        dist = _dist()
+        dev = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
     import torch
     n = torch.cuda.device_count()   # counting does not initialise the GPU
-    return dev % n if n > 0 else dev
+    if n > 0 and dev >= n:
+        raise RuntimeError('rank device %d but this node has %d GPU(s): one process per GPU' % (dev, n))
+    return dev
 
 
 def find_matching_adapter_sets(check_reads, verbosity, end_size, scoring_scheme_vals, print_dest,
@@ -167,12 +174,102 @@ def gather_trims(reads, bounds, group=None):
     return rows[:, 0].astype(np.int64), rows[:, 1].astype(np.int64)
 
 
+# ---- spooled input: gzip files and Albacore directories ----------------------------------------
+# A gzip stream cannot be entered mid-way, so one reader (rank 0's distributor thread) inflates it
+# once, cut into spans of whole records (misc.text_chunks), and writes span c to a spool file that
+# rank c % world parses and trims as soon as it is there. Every rank, rank 0's own trimming
+# included, consumes its spans in order; at most SPOOL_DEPTH spans per rank wait on disk (the
+# distributor blocks until the rank has deleted one), so no full-size scratch copy is made and
+# nobody waits for the whole inflate. A failure of the distributor leaves an .error marker that
+# makes every consumer raise instead of waiting. The spool directory must be visible to every rank
+# (the output directory by default; /dev/shm only when all ranks share a node).
+SPOOL_CHUNK_BYTES = 128 << 20
+SPOOL_DEPTH = 2
+
+
+def _spool_prefix(spool, job):
+    import os
+    return os.path.join(spool, '.pcabi_spool_%s_' % job)
+
+
+def spool_distribute(in_path, spool, job, world, chunk_bytes=None, depth=SPOOL_DEPTH, stop=None):
+    """Rank 0's distributor (run in a thread): every input file in load_reads' order
+    (misc.input_files), cut into record-aligned spans of ~chunk_bytes, span c written to
+    <spool>/.pcabi_spool_<job>_<c>_<albacore>.fq for rank c % world; then an .end marker holding
+    the span count, or an .error marker holding the failure."""
+    import os
+    import time
+    from . import misc
+    pre = _spool_prefix(spool, job)
+    chunk_bytes = int(chunk_bytes or SPOOL_CHUNK_BYTES)
+    pending = [[] for _ in range(world)]
+    c = 0
+    try:
+        for f, alb in misc.input_files(in_path):
+            for mv in misc.text_chunks(f, chunk_bytes):
+                r = c % world
+                while True:
+                    pending[r] = [x for x in pending[r] if os.path.exists(x)]
+                    if len(pending[r]) < depth:
+                        break
+                    if (stop is not None and stop.is_set()) or os.path.exists(pre + 'error'):
+                        return                 # this rank or another one gave up
+                    time.sleep(0.005)
+                path = '%s%d_%s.fq' % (pre, c, alb if alb is not None else '-')
+                with open(path + '.tmp', 'wb') as fo:
+                    fo.write(mv)
+                os.replace(path + '.tmp', path)
+                pending[r].append(path)
+                c += 1
+        with open(pre + 'end.tmp', 'w') as fo:
+            fo.write(str(c))
+        os.replace(pre + 'end.tmp', pre + 'end')
+    except BaseException as ex:   # every consumer raises it instead of waiting
+        with open(pre + 'error', 'w') as fo:
+            fo.write('%s: %s' % (type(ex).__name__, ex))
+
+
+def spool_batches(spool, job, rank, world, max_reads, poll=0.005):
+    """This rank's spans from the distributor, parsed: yields ((c, j), ReadBatch, albacore) for
+    batch j of span c = rank, rank + world, ... in order, deleting each span file once parsed."""
+    import os
+    import time
+    from . import misc
+    pre = _spool_prefix(spool, job)
+    d, base = os.path.split(pre)
+    c = rank
+    while True:
+        while True:
+            if os.path.exists(pre + 'error'):
+                with open(pre + 'error') as f:
+                    raise RuntimeError('input distributor failed: ' + f.read())
+            mine = [x for x in os.listdir(d) if x.startswith('%s%d_' % (base, c)) and x.endswith('.fq')]
+            if mine:
+                break
+            if os.path.exists(pre + 'end'):
+                with open(pre + 'end') as f:
+                    if c >= int(f.read()):
+                        return
+                continue                       # the marker came after the span: look again
+            time.sleep(poll)
+        path = os.path.join(d, mine[0])
+        alb = mine[0][len(base) + len(str(c)) + 1:-3]
+        alb = None if alb == '-' else alb
+        try:
+            for j, b in enumerate(misc.read_batches(path, max_reads=max_reads)):
+                yield (c, j), b, alb
+        finally:
+            os.remove(path)
+        c += world
+
+
 def trim_file_sharded(in_path, out_path, out_format='fastq', scoring_scheme_vals=(3, -6, -5, -2), end_size=150,
                       end_threshold=75.0, extra_end_trim=2, min_trim_size=4, middle_threshold=90.0,
                       extra_middle_trim_good_side=10, extra_middle_trim_bad_side=100, min_split_read_size=1000,
                       check_reads=10000, adapter_threshold=90.0, max_reads=100000, group=None, device=None,
                       trimmer_factory=None, barcode_dir=None, barcode_threshold=75.0, barcode_diff=5.0,
-                      require_two_barcodes=False, untrimmed=False, discard_unassigned=False, inflate_dir=None):
+                      require_two_barcodes=False, untrimmed=False, discard_unassigned=False, inflate_dir=None,
+                      spool_chunk_bytes=None):
     """The CLI's file-to-file path (porechop_abi.py:41-131: adapter-set search on the first
     check_reads records, end trim, middle scan, the fork's filter, trimmed output) on every rank of
     `group`, one GPU each:
@@ -183,12 +280,13 @@ def trim_file_sharded(in_path, out_path, out_format='fastq', scoring_scheme_vals
       * trimming: a plain file is split into contiguous record ranges of about equal bytes (so
         bases), cut at record starts (misc.record_boundaries); each rank trims its range with a
         pipeline.FileTrimmer into its own part file, in order. A gzip file cannot be entered
-        mid-stream: rank 0 alone inflates it (one zlib stream per job, not one per rank) into a
-        plain file next to the output (inflate_dir overrides, e.g. /dev/shm), and every rank then
-        takes its record range of that file as above. An Albacore directory is streamed by every
-        rank, which trims every world-th batch and records the byte span of each batch it writes;
+        mid-stream, and an Albacore directory is many files: rank 0's distributor thread inflates
+        the input once, in record-aligned spans handed round-robin to the ranks through spool files
+        in inflate_dir (default: the output directory; it must be visible to every rank), at most
+        SPOOL_DEPTH waiting per rank -- the ranks trim while it inflates (spool_distribute /
+        spool_batches), recording the byte span of each batch they write;
       * output: rank 0 concatenates the parts in record order (the reference's output order) --
-        the only other exchange is the span lists (gzip input) and the read counts.
+        the only other exchange is the span lists (spooled input), the job id and the read counts.
 
     With barcode_dir (-b) every rank writes its bins into a private directory, recording the
     byte span of each bin write, and rank 0 stitches every bin in record order; the barcoding
@@ -230,30 +328,45 @@ def trim_file_sharded(in_path, out_path, out_format='fastq', scoring_scheme_vals
     ft = trimmer_factory(matching, **opts)
     d, base = os.path.split(os.path.abspath(out_path))
     part = lambda r: os.path.join(d, '.pcabi_part%d_%s' % (r, base))
-    src = in_path
-    inflated = None
-    if world > 1 and os.path.isfile(in_path) and misc.get_compression_type(in_path) == 'gz':
-        # one inflater per job: rank 0 writes the plain text once, every rank maps its range of it
-        inflated = os.path.join(inflate_dir or d, '.pcabi_inflated_%s' % base)
-        if rank == 0:
-            import gzip
-            with gzip.open(in_path, 'rb') as fi, open(inflated + '.tmp', 'wb') as fo:
-                shutil.copyfileobj(fi, fo, 1 << 24)
-            os.replace(inflated + '.tmp', inflated)
-        dist.barrier(group=group)
-        src = inflated
-    bounds = misc.record_boundaries(src, world)
+    spooled = world > 1 and (os.path.isdir(in_path) or misc.get_compression_type(in_path) == 'gz')
+    bounds = None if spooled else misc.record_boundaries(in_path, world)
     segments = None if (bounds is not None and barcode_dir is None) else []
+    job = spool = distributor = None
+    stop = None
+    if spooled:
+        import threading
+        import uuid
+        ids = [uuid.uuid4().hex if rank == 0 else None]
+        dist.broadcast_object_list(ids, src=0, group=group)   # one spool namespace per job
+        job, spool = ids[0], inflate_dir or d
+        os.makedirs(spool, exist_ok=True)
+        if rank == 0:
+            stop = threading.Event()
+            distributor = threading.Thread(target=spool_distribute, args=(in_path, spool, job, world),
+                                           kwargs={'stop': stop, 'chunk_bytes': spool_chunk_bytes}, daemon=True)
+            distributor.start()
     try:
-        if bounds is not None:
-            counts = ft.trim_file(src, part(rank), out_format, max_reads, byte_range=(bounds[rank], bounds[rank + 1]),
-                                  segments=segments)
+        if spooled:
+            counts = ft.trim_file(None, part(rank), out_format, max_reads, segments=segments,
+                                  source=spool_batches(spool, job, rank, world, max_reads))
+        elif bounds is not None:
+            counts = ft.trim_file(in_path, part(rank), out_format, max_reads,
+                                  byte_range=(bounds[rank], bounds[rank + 1]), segments=segments)
         else:
-            counts = ft.trim_file(src, part(rank), out_format, max_reads,
-                                  batch_filter=lambda k: k % world == rank, segments=segments)
+            counts = ft.trim_file(in_path, part(rank), out_format, max_reads, segments=segments)
+    except BaseException as ex:
+        if spooled:                           # the other ranks stop waiting for spans and raise too
+            pre = _spool_prefix(spool, job)
+            if not os.path.exists(pre + 'error'):
+                with open(pre + 'error', 'w') as fo:
+                    fo.write('rank %d: %s: %s' % (rank, type(ex).__name__, ex))
+        raise
     finally:
         if hasattr(ft, 'close'):
             ft.close()
+        if distributor is not None:
+            stop.set()
+            distributor.join()
     if world > 1:
         spans = [None] * world
         dist.all_gather_object(spans, (segments, {k: v for k, v in counts.items() if k != 'bins'}), group=group)
@@ -298,9 +411,14 @@ def trim_file_sharded(in_path, out_path, out_format='fastq', scoring_scheme_vals
                 os.remove(part(r))
     if world > 1:
         dist.barrier(group=group)
-    if inflated is not None and rank == 0 and os.path.exists(inflated):
-        os.remove(inflated)
+    if spooled and rank == 0:                 # markers (and anything a failed run left behind)
+        pre = _spool_prefix(spool, job)
+        sd, sb = os.path.split(pre)
+        for f in os.listdir(sd):
+            if f.startswith(sb):
+                os.remove(os.path.join(sd, f))
     out = {k: sum(c[k] for _, c in spans) for k in ('reads_in', 'reads_kept')}
+    out['reads_in_per_rank'] = [c['reads_in'] for _, c in spans]
     if barcode_dir is not None:
         out['bins'] = sorted(set(nm for segs, _ in spans for _, nm, _, _ in segs))
     return out

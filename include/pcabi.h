@@ -493,6 +493,13 @@ int pcabi_fastx_type(const pcabi_fastx *r);
  *       file size); a fresh reader (no record read yet). */
 int64_t pcabi_fastx_record_start(const pcabi_fastx *r, int64_t byte);
 int pcabi_fastx_set_range(pcabi_fastx *r, int64_t begin, int64_t end);
+/* Streaming split of any input (gzip included) into spans of decoded text holding whole records,
+ * for a distributor that hands spans to other readers (shards.trim_file_sharded): the next span,
+ * at least max_bytes long unless the input ends (one record may overshoot), cut where a fresh
+ * reader parses the same records as the continuous read -- FASTQ after a record whose successor's
+ * first line starts with '@', FASTA before a header with a name whose preceding header has one.
+ * *text is valid until the next call on r. Returns 1, 0 at the end of the input, or < 0. */
+int pcabi_fastx_next_text(pcabi_fastx *r, int64_t max_bytes, const char **text, int64_t *len);
 int64_t pcabi_fastx_next(pcabi_fastx *r, int64_t max_reads, int64_t max_bases, pcabi_reads **out);
 void pcabi_fastx_close(pcabi_fastx *r);
 int pcabi_fastx_load(const char *path, int raw, pcabi_reads **out);

@@ -206,3 +206,37 @@ def test_byte_range_shards_cover_every_record_once(tmp_path):
                 got += _batches_text(path, (b[k], b[k + 1]))
             assert got == whole, (path, parts)
     assert misc.record_boundaries(os.path.join(GOLDEN_IO, 'plain_mixed.fastq.gz'), 2) is None
+
+
+def test_text_chunks_reparse_to_the_same_records(tmp_path):
+    """misc.text_chunks (pcabi_fastx_next_text, the sharded pipeline's distributor): for every
+    fixture, plain and gzip, and chunk sizes from one byte up, each span written to its own file and
+    parsed afresh gives, concatenated, exactly the whole file's records (CRLF / lone-CR endings,
+    blank and whitespace lines, empty FASTA headers whose sequence runs on, '@'-leading qualities)."""
+    import random
+    from custom_porechop_abi_amd import misc
+    files = [os.path.join(GOLDEN_IO, f) for f in sorted(os.listdir(GOLDEN_IO))]
+    rng = random.Random(9)
+    q = str(tmp_path / 'at_quals.fastq.gz')
+    with gzip.open(q, 'wt') as f:
+        for k in range(60):
+            s = ''.join(rng.choice('ACGT') for _ in range(rng.randint(0, 40)))
+            f.write('@r%d x\n%s\n+\n%s\n' % (k, s, '@' * len(s) if k % 2 else ''.join(rng.choice('@+!#I') for _ in s)))
+    a = str(tmp_path / 'empty_headers.fasta.gz')
+    with gzip.open(a, 'wt') as f:
+        for k in range(40):
+            f.write('>%s\n%s\n\n%s\n' % ('' if k % 4 == 1 else 'r%d' % k, 'ACGT' * (k % 5), 'GG' * (k % 3)))
+    files += [q, a]
+    for path in files:
+        whole = _batches_text(path, max_reads=1 << 20)
+        for size in (1, 7, 64, 500, 1 << 20):
+            got, n_chunks = [], 0
+            for k, mv in enumerate(misc.text_chunks(path, size)):
+                part = str(tmp_path / ('chunk%d' % k))
+                with open(part, 'wb') as f:
+                    f.write(mv)
+                got += _batches_text(part, max_reads=1 << 20)
+                n_chunks += 1
+            assert got == whole, (path, size)
+            if size == 1:
+                assert n_chunks > 1 or len(whole) <= 1, path

@@ -189,7 +189,7 @@ class _OracleTrimmer(object):
         return st, et, cut_off, np.array(flat, np.int64), None, keep
 
 
-def _file_worker(rank, world, port, case_name, in_path, out_path, res_path, bins=None):
+def _file_worker(rank, world, port, case_name, in_path, out_path, res_path, bins=None, chunk=None):
     import torch.distributed as dist
     from custom_porechop_abi_amd import engine, shards
     from tests import oracle_lib
@@ -207,7 +207,7 @@ def _file_worker(rank, world, port, case_name, in_path, out_path, res_path, bins
                                           check_reads=o.get('check_reads', 10000),
                                           adapter_threshold=o['adapter_threshold'], max_reads=3 if bins else 7,
                                           trimmer_factory=_OracleTrimmer, barcode_dir=bins,
-                                          require_two_barcodes=bool(o.get('require_two')))
+                                          require_two_barcodes=bool(o.get('require_two')), spool_chunk_bytes=chunk)
         with open(res_path % rank, 'w') as f:
             json.dump(counts, f)
     finally:
@@ -243,8 +243,60 @@ def test_sharded_file_pipeline_matches_reference(case_name, gz, tmp_path):
     counts = [json.load(open(res_path % r)) for r in range(2)]
     assert counts[0] == counts[1] and counts[0]['reads_in'] == len(records)
     assert open(out_path).read() == _expected(case, records)
-    # gzip input: rank 0 inflated it once into a plain file both ranks took record ranges of
-    assert not [f for f in os.listdir(str(tmp_path)) if f.startswith('.pcabi_part') or f.startswith('.pcabi_inflated')]
+    # no part or spool file is left behind
+    assert not [f for f in os.listdir(str(tmp_path)) if f.startswith('.pcabi_part') or f.startswith('.pcabi_spool')]
+
+
+@pytest.mark.parametrize('fasta', [False, True])
+@pytest.mark.parametrize('chunk', [1, 3000])
+def test_sharded_gzip_spool_many_spans(chunk, fasta, tmp_path):
+    """gzip input through the spool (shards.spool_distribute / spool_batches) in many small
+    record-aligned spans, handed round-robin to the two ranks while rank 0 still inflates: both
+    ranks trim spans, the stitched output == the reference's (G2), no spool file is left."""
+    import gzip
+    import torch.multiprocessing as mp
+    from tests.test_pipeline import _expected
+    case = next(c for c in G2['cases'] if c['case'] == 'synthetic_default')
+    records = [tuple(x) for x in G2['synthetic_reads']]
+    if fasta:
+        text = ''.join('>%s\n%s\n' % (n, '\n'.join(s[k:k + 60] for k in range(0, len(s), 60))) for n, s, _ in records)
+    else:
+        text = ''.join('@%s\n%s\n+\n%s\n' % r for r in records)
+    in_path = str(tmp_path / ('in.fasta.gz' if fasta else 'in.fastq.gz'))
+    with gzip.open(in_path, 'wt') as f:
+        f.write(text)
+    out_path = str(tmp_path / 'out.fastq')
+    res_path = str(tmp_path / 'counts%d.json')
+    mp.spawn(_file_worker, args=(2, _free_port(), 'synthetic_default', in_path, out_path, res_path, None, chunk),
+             nprocs=2, join=True)
+    counts = [json.load(open(res_path % r)) for r in range(2)]
+    assert counts[0]['reads_in'] == len(records)
+    assert min(counts[0]['reads_in_per_rank']) > 0
+    exp = _expected(case, [(n, s, '' if fasta else q) for n, s, q in records])
+    if fasta:   # FASTA reads carry no qualities: compare the written sequences and names
+        got = open(out_path).read().split('\n')[0::4]
+        assert got == exp.split('\n')[0::4]
+    else:
+        assert open(out_path).read() == exp
+    assert not [f for f in os.listdir(str(tmp_path)) if f.startswith('.pcabi_spool') or f.startswith('.pcabi_part')]
+
+
+def test_sharded_gzip_spool_failure_raises_on_every_rank(tmp_path):
+    """A truncated gzip input (the reference's gzip module raises EOFError): the distributor's
+    error reaches both ranks, which raise instead of waiting for spans that never come."""
+    import gzip
+    import torch.multiprocessing as mp
+    # ~6 MB of text, cut at 90 %: the check reads (50, 'synthetic_endsize') come from the intact
+    # first decode buffer, the spans run into the damage while both ranks trim
+    records = [('%s_%d' % (n, k), s, q) for k in range(8) for n, s, q in G2['synthetic_reads']]
+    data = gzip.compress(''.join('@%s\n%s\n+\n%s\n' % r for r in records).encode())
+    in_path = str(tmp_path / 'in.fastq.gz')
+    with open(in_path, 'wb') as f:
+        f.write(data[:len(data) * 9 // 10])
+    with pytest.raises(Exception) as ei:
+        mp.spawn(_file_worker, args=(2, _free_port(), 'synthetic_endsize', in_path, str(tmp_path / 'o.fastq'),
+                                     str(tmp_path / 'c%d.json'), None, 200000), nprocs=2, join=True)
+    assert 'unexpected end of file' in str(ei.value) or 'distributor failed' in str(ei.value)
 
 
 @pytest.mark.parametrize('gz', [False, True])
