@@ -551,6 +551,10 @@ def run_other_configs(args, ctx):
         ('check_phase', lambda: run_check_phase(sub(), rank, 1, None, torch, L, _lib, A, synth, encode_adapters)),
         # the reference-API path (porechop_abi.py's three drivers on 100k NanoporeRead objects)
         ('drivers', lambda: run_drivers(sub(steps=2), rank, 1, None, torch, L, _lib, A, synth, encode_adapters)),
+        # the reference's own job shape: set search on the first 10k reads x 119 sets, then end trim
+        # and middle scan of 100k reads with only the sets it keeps (porechop_abi.py:41-131)
+        ('reference_job', lambda: run_reference_job(sub(), rank, 1, None, torch, L, _lib, A, synth,
+                                                    encode_adapters)),
         # configs[2]: end trim + middle scan, 100k x 8 kb per GPU
         ('middle', lambda: run_middle(sub(workload='middle'), rank, 1, None, torch, L, _lib, A, synth,
                                       encode_adapters)),
@@ -752,6 +756,223 @@ def run_check_phase(args, rank, world, dist, torch, L, _lib, A, synth, encode_ad
                 'gcups_rank0': round(cells / (step_ms * 1e-3) / 1e9, 1),
                 'ranks_agree': agree, 'parity_spot_check': checked}
     return None
+
+
+def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapters, n_check=10000):
+    """The reference's job as its main() runs it (porechop_abi/porechop_abi.py:41-131), on 100k
+    synthetic reads of mean 8 kb per GPU, inputs resident in HBM. One step:
+      adapter-set search: the first 10k reads' start / end windows x the 119 sets' distinct
+          sequences (k_align cross products -> k_best_full_id -> the maxima to the host)  (:200-245)
+      host: sets with best start-or-end identity >= 90, fix_up_1d2_sets, add_full_barcode_adapter_sets
+      end trim of every read with only the kept sets (k_align -> k_end_trim)          (:359-438)
+      trimmed views + middle scan with the kept sets' middle list (queued device rounds) (:457-522)
+    The kept sets' adapter tables and the scan's scratch are made on the first step and reused (a
+    job makes them once). Events time each phase; the roofline is the step's dominant launch (the
+    set search's largest register bucket). Parity: the set search's maxima == the oracle's on the
+    first 400 check reads, the kept end windows == the oracle on the first 256 reads, the middle hits
+    == the oracle's masked loop on the first 1000 reads."""
+    from custom_porechop_abi_amd import porechop_abi as P
+    from custom_porechop_abi_amd.engine import pid6
+    vp = ctypes.c_void_p
+    n, E, sc = args.reads, args.end_size, SCORING
+    search = [a for a in A.fresh_adapters() if '(full sequence)' not in a.name]
+    starts_u, _ = P._unique([a.start_sequence[1] for a in search if a.start_sequence])
+    ends_u, _ = P._unique([a.end_sequence[1] for a in search if a.end_sequence])
+    n_u = len(starts_u) + len(ends_u)
+    t0 = time.time()
+    reads = synth.make_reads(n, args.mean_len, seed=12345 + rank)
+    lens = np.array([len(r) for r in reads], np.int64)
+    offs = np.zeros(n, np.int64)
+    offs[1:] = np.cumsum((lens + 3) & ~3)[:-1]
+    pack = np.full(int(offs[-1] + lens[-1]) + 64, 4, np.uint8)
+    for k, r in enumerate(reads):
+        pack[offs[k]:offs[k] + lens[k]] = r
+    s_len = np.minimum(lens, E).astype(np.int32)
+    e_len = s_len.copy()
+    s_off, e_off = offs.copy(), offs + lens - e_len
+    gen_s = time.time() - t0
+    n_chk = min(n_check, n)
+
+    def dalloc(nbytes):
+        p = vp()
+        _lib.check(L.pcabi_dev_malloc(ctypes.byref(p), max(int(nbytes), 16)), 'malloc')
+        return p
+
+    def h2d(arr):
+        arr = np.ascontiguousarray(arr)
+        p = dalloc(arr.nbytes)
+        _lib.check(L.pcabi_dev_h2d(p, arr.ctypes.data_as(vp), arr.nbytes), 'h2d')
+        return p
+
+    def table(lst):
+        c, o, l = encode_adapters(lst)
+        t = vp()
+        _lib.check(L.pcabi_adapters_create_scored(c.ctypes.data_as(vp), o.ctypes.data_as(vp), l.ctypes.data_as(vp),
+                                                  len(lst), *sc, ctypes.byref(t)), 'adapters_create')
+        return t
+
+    d_pristine = h2d(pack)
+    d_work = dalloc(pack.nbytes)
+    d_offs, d_lens = h2d(offs), h2d(lens.astype(np.int32))
+    d_st, d_et = dalloc(4 * n), dalloc(4 * n)
+    d_toff_mid, d_tlen_mid = dalloc(8 * n), dalloc(4 * n)
+    d_best = dalloc(8 * n_u)
+    stream = vp()
+    _lib.check(L.pcabi_stream_create(ctypes.byref(stream)), 'stream')
+    sides = []
+    for w_off, w_len, u in ((s_off, s_len, starts_u), (e_off, e_len, ends_u)):
+        toff = np.zeros((n + 255) // 256 + 1, np.int64)
+        nd = L.pcabi_tile_layout(w_len.ctypes.data_as(vp), n, toff.ctypes.data_as(vp))
+        sides.append(dict(d_off=h2d(w_off), d_len=h2d(w_len), d_toff=h2d(toff), d_tiles=dalloc(4 * nd),
+                          mq=int(np.diff(toff).max() // 256), mx=int(w_len.max()), mx_chk=int(w_len[:n_chk].max()),
+                          search=table(u), n_u=len(u), d_chk=dalloc(4 * 8 * len(u) * n_chk)))
+    ev = [vp() for _ in range(10)]
+    for e in ev:
+        _lib.check(L.pcabi_event_create(ctypes.byref(e)), 'event')
+    kept_cache = {}
+    cap = max(4096, n)
+    hits = np.zeros((6, cap), np.int32)
+    stats = {'kept': None, 'hits': 0}
+    acc = {}
+
+    def kept_state(names, matching):
+        if names not in kept_cache:
+            st_ = [a.start_sequence[1] for a in matching if a.start_sequence]
+            en_ = [a.end_sequence[1] for a in matching if a.end_sequence]
+            mid = [x[1] for x in P.middle_adapter_list(matching)[0]]
+            ks = dict(start=st_, end=en_, mid=mid, tabs=[table(x) if x else None for x in (st_, en_, mid)],
+                      d_res=[dalloc(4 * 8 * max(1, len(x)) * n) for x in (st_, en_)], scan=vp())
+            if mid:
+                _lib.check(L.pcabi_scan_create(ks['tabs'][2], ctypes.byref(ks['scan'])), 'scan_create')
+            kept_cache[names] = ks
+        return kept_cache[names]
+
+    def step():
+        _lib.check(L.pcabi_dev_copy_async(d_work, d_pristine, pack.nbytes, 2, stream), 'copy')
+        L.pcabi_event_record(ev[0], stream)
+        _lib.check(L.pcabi_dev_memset(d_best, 0, 8 * n_u), 'memset')
+        b0 = 0
+        for k, sd in enumerate(sides):
+            _lib.check(L.pcabi_tile_windows_dev(d_work, sd['d_off'], sd['d_len'], n, sd['d_toff'], sd['mq'],
+                                                sd['d_tiles'], stream), 'tile')
+            # the check reads are the first n_check reads: their windows are the first tiles
+            _lib.check(L.pcabi_align_cross_dev_marked(sd['d_tiles'], sd['d_toff'], sd['d_len'], n_chk, sd['mx_chk'],
+                                                      sd['search'], *sc, sd['d_chk'], sd['n_u'] * n_chk, stream,
+                                                      ev[2 + 2 * k], ev[3 + 2 * k]), 'align')
+            _lib.check(L.pcabi_best_full_identity_dev(sd['d_chk'], sd['n_u'] * n_chk, n_chk, sd['n_u'],
+                                                      vp(d_best.value + 8 * b0), stream), 'best')
+            b0 += sd['n_u']
+        maxima = np.empty(n_u, np.float64)
+        _lib.check(L.pcabi_dev_copy_async(maxima.ctypes.data_as(vp), d_best, 8 * n_u, 1, stream), 'd2h')
+        _lib.check(L.pcabi_stream_sync(stream), 'sync')
+        th = time.perf_counter()
+        sets_ = A.fresh_adapters()
+        srch = [a for a in sets_ if '(full sequence)' not in a.name]
+        P.apply_set_maxima(srch, maxima)
+        matching = [a for a in srch if a.best_start_or_end_score() >= 90.0]
+        matching = P.add_full_barcode_adapter_sets(P.fix_up_1d2_sets(matching))
+        ks = kept_state(tuple(a.name for a in matching), matching)
+        acc['host_ms'] = acc.get('host_ms', 0.0) + 1e3 * (time.perf_counter() - th)
+        stats['kept'] = [a.name for a in matching]
+        L.pcabi_event_record(ev[1], stream)
+        for k, sd in enumerate(sides):
+            adps = ks['start'] if k == 0 else ks['end']
+            if adps:
+                _lib.check(L.pcabi_align_cross_dev(sd['d_tiles'], sd['d_toff'], sd['d_len'], n, sd['mx'], ks['tabs'][k],
+                                                   *sc, ks['d_res'][k], len(adps) * n, stream), 'align')
+        n_sa, n_ea = len(ks['start']), len(ks['end'])
+        _lib.check(L.pcabi_end_trim_dev(ks['d_res'][0], n_sa * n, n_sa, ks['d_res'][1], n_ea * n, n_ea, n, E, 2, 75.0, 4,
+                                        d_st, d_et, None, None, stream), 'end_trim')
+        L.pcabi_event_record(ev[6], stream)
+        nh = 0
+        if ks['mid']:
+            _lib.check(L.pcabi_trim_views_dev(d_offs, d_lens, d_st, d_et, n, d_toff_mid, d_tlen_mid, stream), 'views')
+            nh = L.pcabi_middle_scan_dev(ks['scan'], d_work, d_toff_mid, d_tlen_mid, None, n, *sc, 90.0,
+                                         hits.ctypes.data_as(vp), cap, stream)
+            if nh < 0:
+                _lib.check(int(nh), 'middle_scan')
+        L.pcabi_event_record(ev[7], stream)
+        _lib.check(L.pcabi_stream_sync(stream), 'sync')
+        stats['hits'] = int(nh)
+        for key, a, b in (('check_ms', 0, 1), ('end_trim_ms', 1, 6), ('middle_ms', 6, 7), ('check_dom_start_ms', 2, 3),
+                          ('check_dom_end_ms', 4, 5)):
+            ms = ctypes.c_float()
+            _lib.check(L.pcabi_event_elapsed_ms(ctypes.byref(ms), ev[a], ev[b]), 'elapsed')
+            acc[key] = acc.get(key, 0.0) + ms.value
+        return matching
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    acc.clear()
+    torch.cuda.synchronize() if torch.cuda.is_available() else None
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        matching = step()
+    elapsed = time.perf_counter() - t0
+    step_ms = 1e3 * elapsed / args.steps
+    per = {k: round(v / args.steps, 4) for k, v in acc.items()}
+    ks = kept_state(tuple(a.name for a in matching), matching)
+    # the dominant launch: the set search's largest register bucket (start and end launches averaged)
+    dom_ms = 0.5 * (per['check_dom_start_ms'] + per['check_dom_end_ms'])
+    dom_cells = []
+    for k, (w_len, u) in enumerate(((s_len, starts_u), (e_len, ends_u))):
+        from collections import Counter
+        rows = Counter((len(x) + 3) // 4 * 4 for x in u)
+        big = max(rows, key=lambda r: rows[r] * r)   # the table's largest bucket by adapters x rows
+        dom_cells.append(int(w_len[:n_chk].astype(np.int64).sum()) * sum(len(x) for x in u if (len(x) + 3) // 4 * 4 == big))
+    tops = float(np.mean(dom_cells)) * OPS_PER_CELL / (dom_ms * 1e-3) / 1e12
+    # end trim with the kept sets: cells and rate (the few-adapter launches)
+    end_cells = int(s_len.astype(np.int64).sum() * sum(map(len, ks['start'])) +
+                    e_len.astype(np.int64).sum() * sum(map(len, ks['end'])))
+    chk_cells = int(s_len[:n_chk].astype(np.int64).sum() * sum(map(len, starts_u)) +
+                    e_len[:n_chk].astype(np.int64).sum() * sum(map(len, ends_u)))
+    checked = None
+    if args.check and rank == 0:
+        from tests import oracle_lib
+        # set search maxima over the first 400 check reads vs the oracle's
+        k = min(400, n_chk)
+        heads = [synth.codes_to_str(r[:E]) for r in reads[:k]]
+        tails = [synth.codes_to_str(r[-E:]) for r in reads[:k]]
+        exp = np.zeros(n_u)
+        for wins, u, b0 in ((heads, starts_u, 0), (tails, ends_u, len(starts_u))):
+            r_ = oracle_lib.align_many(wins, u, (np.tile(np.arange(k), len(u)), np.repeat(np.arange(len(u)), k)), sc)
+            full = np.where(r_[0] == -1, 0.0, pid6(r_[5], r_[7])).reshape(len(u), k)
+            exp[b0:b0 + len(u)] = full.max(axis=1)
+        got = np.zeros(n_u)
+        for j, sd in enumerate(sides):
+            res = np.empty((8, sd['n_u'] * n_chk), np.int32)
+            _lib.check(L.pcabi_dev_d2h(res.ctypes.data_as(vp), sd['d_chk'], res.nbytes), 'd2h')
+            res = res.reshape(8, sd['n_u'], n_chk)[:, :, :k].reshape(8, -1)
+            full = np.where(res[0] == -1, 0.0, pid6(res[5], res[7])).reshape(sd['n_u'], k)
+            got[(0 if j == 0 else len(starts_u)):][:sd['n_u']] = full.max(axis=1)
+        trims = np.zeros((2, n), np.int32)
+        _lib.check(L.pcabi_dev_d2h(trims[0].ctypes.data_as(vp), d_st, 4 * n), 'd2h')
+        _lib.check(L.pcabi_dev_d2h(trims[1].ctypes.data_as(vp), d_et, 4 * n), 'd2h')
+        ends_chk = spot_check(L, _lib, ks['d_res'][0], ks['d_res'][1], d_st, d_et, len(ks['start']) * n,
+                              len(ks['end']) * n, n, len(ks['start']), len(ks['end']), reads, ks['start'], ks['end'],
+                              E, min(256, n), sc)
+        mid_chk = middle_spot_check(reads, trims, hits, stats['hits'], ks['mid'], sc, 90.0, min(1000, n)) \
+            if ks['mid'] else None
+        checked = {'set_search_maxima_identical_400_reads': bool(np.array_equal(got, exp)),
+                   'end_windows': ends_chk, 'middle': mid_chk}
+    return {'metric': 'reads/sec through the reference job (set search on 10k reads x 119 sets, then end trim + '
+                      'middle scan with the kept sets)',
+            'value': round(n * args.steps / elapsed, 1), 'unit': 'reads/s', 'steps': args.steps,
+            'ms_per_step': round(step_ms, 3), 'ms_per_phase': per, 'kept_sets': stats['kept'],
+            'kept_adapters': {'start': len(ks['start']), 'end': len(ks['end']), 'middle': len(ks['mid'])},
+            'middle_hits_per_step': stats['hits'],
+            'cells_per_step': {'set_search': chk_cells, 'end_trim': end_cells},
+            'end_trim_gcups': round(end_cells / (per['end_trim_ms'] * 1e-3) / 1e9, 1),
+            'roofline': {'bound': 'valu', 'kernel': 'the set search\'s largest register bucket (k_align<24, true, 6>)',
+                         'achieved': round(tops, 3), 'peak': round(VALU_PEAK_TOPS, 1), 'unit': 'Tops/s (int32 lane-ops)',
+                         'frac': round(tops / VALU_PEAK_TOPS, 4), 'launch_ms': round(dom_ms, 4),
+                         'cells_per_launch': int(np.mean(dom_cells)), 'ops_per_cell': OPS_PER_CELL},
+            'dtype': 'int32', 'data': 'synthetic (seeded ONT-like reads, mean %d bp)' % args.mean_len,
+            'config': {'workload': 'reference job: set search (%d check reads x %d sets, %d + %d distinct sequences), '
+                                   'end trim + middle scan of %d reads/GPU with the kept sets' % (
+                                       n_chk, len(search), len(starts_u), len(ends_u), n),
+                       'reads_per_gpu': n},
+            'parity_spot_check': checked, 'setup_s': round(gen_s, 2)}
 
 
 def run_drivers(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapters):

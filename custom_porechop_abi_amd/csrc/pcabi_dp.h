@@ -1382,6 +1382,266 @@ PCABI_HD Result align_lane_packed_long(ReadFn &rd0, ReadFn &rd1, int n, const Ta
 }
 
 // ==========================================================================================
+// Row-split packed core (k_align_split: launches too small to fill the chip). One
+// adapter over 100k end windows is 1.5 waves per SIMD, and a lane's DP over its 150 columns is a
+// dependency chain the SIMD cannot hide with so few waves. Here K lanes share a window, lane l
+// holding the bucket's rows r0 + 1 .. r0 + R (r0 = l R, K R = RPL), and the lanes form a systolic
+// pipeline: at step t lane l computes column j = t - l from row r0's G and V keys at column j,
+// which lane l - 1 computed at step t - 1 (lane 0 takes row 0). The inner columns' row-L scout is
+// the last lane's. The last column runs in K phases, lane p in phase p, passing down the running
+// first maximum over the column's rows (B2) and the V-run state; the last lane merges B2 into its
+// row-L best -- the reference's visit order: the last row, then the last column top down, strict
+// '>' (S/align/dp_scout.h:175) -- and finishes. Same keys, maxes and tie rules as LanePacked, so
+// the results are identical. The steps are member functions: the kernel runs the K lanes of a
+// window side by side (a lane shift per exchanged value), the host model in lockstep.
+// ==========================================================================================
+struct SplitIn {   // lane l - 1's state after its part of the last column
+    int32_t gup, vup;             // its bottom row's G and V keys
+    int slt, vt, vp;              // the V-run state there
+    int score, bi, lt, trail, prec;   // the running first maximum of the column's rows (B2)
+    uint32_t attr;
+};
+
+template <int R, bool AFFINE, typename LAY>
+struct LaneSplit {
+    using Y = LAY;
+    int32_t G[R + 1];     // S keys with tb cleared + gap open (LanePacked's G)
+    int32_t HK[R + 1];    // H keys (affine)
+    int r0, off, L;
+    bool last;            // this lane holds row RPL (adapter row L)
+    int32_t k_go, k_ge, k_gex, k_vo, k_gev, k_geh, neg2;
+    int32_t gdiag;        // row r0's G key at the previous column (the first row's diagonal source)
+    int32_t bkey;         // last lane: row-L scout of the inner columns (LanePacked::column_tail)
+    int bj;
+    int bscore, bi, blt, btrail, bprec;
+    uint32_t battr;
+    int slt_last, ht_last, hp_last;
+    int32_t gbot, vbot;   // bottom row keys of the last column computed (sent to lane l + 1)
+    SplitIn out;          // after the last column: what lane l + 1 needs
+
+    PCABI_HD void init(int lane, int K, int L_, int RPL, const Scoring &sc) {
+        r0 = lane * R;
+        off = RPL - L_;
+        L = L_;
+        last = lane == K - 1;
+        const int32_t neg = Y::sc(pk::neg_score(sc));
+        k_go = Y::sc(sc.go);
+        k_ge = Y::sc(sc.ge);
+        k_gev = Y::sc(sc.ge) - Y::sc(sc.go) + Y::TB2;
+        k_geh = Y::sc(sc.ge) - Y::sc(sc.go) + Y::TB1;
+        k_gex = Y::sc(sc.ge) + (Y::TAGGED ? Y::TB1 : 0);
+        k_vo = Y::TAGGED ? Y::TB2 : 0;
+#pragma unroll
+        for (int s = 1; s <= R; ++s) {
+            G[s] = Y::start(off - (r0 + s)) + k_go;   // padded (s, 0) reaches real (0, off - s)
+            HK[s] = Y::TAGGED ? neg : (neg | Y::TB1);
+        }
+        neg2 = neg | Y::TB2;
+        gdiag = Y::start(off - r0) + k_go;            // row r0 at column 0 (row 0 for lane 0)
+        bkey = Y::start(-L_);                         // the (L, 0) seed
+        bj = 0;
+        gbot = G[R];
+        vbot = neg2;
+    }
+
+    PCABI_HD int32_t row0_g(int j) const { return Y::start(j + off) + k_go; }   // G(0, j)
+
+    // one row's candidates (LanePacked::column's recurrences)
+    PCABI_HD void cell(int s, int32_t diag, int32_t gup, int32_t vup, int32_t &hn, int32_t &vn2, int32_t &sn,
+                       bool &hext, bool &vext) const {
+        if (AFFINE && Y::TAGGED) {
+            const int32_t hx = HK[s] + k_gex, ho = G[s];
+            hn = hx > ho ? hx : ho;
+            const int32_t vx = vup + k_gex, vo = gup + k_vo;
+            vn2 = vx > vo ? vx : vo;
+            hext = Y::tb(hn) != 0;
+            vext = Y::tb(vn2) > (Y::TB2 >> Y::TB_SH);
+        } else if (AFFINE) {
+            const int32_t hx = HK[s] + k_ge, ho = G[s];
+            hn = hx > ho ? hx : ho;
+            const int32_t vx = vup + k_ge, vo = gup;
+            const int32_t vn = vx > vo ? vx : vo;
+            vn2 = vn | Y::TB2;
+            hext = Y::tb(hn) == 1;
+            vext = Y::tb(vn) == 2;
+        } else {
+            vn2 = gup + k_gev;
+            hn = G[s] + k_geh;
+            hext = vext = false;
+        }
+        sn = max3i(diag, vn2, hn);
+    }
+
+    // inner column j (1 <= j < n); gup / vup: row r0's G / V keys at column j
+    template <typename TabRow>
+    PCABI_HD void inner(const TabRow &tab, int j, int32_t gup, int32_t vup) {
+        const int32_t g_in = gup;
+        int32_t diag = gdiag + tab(1);
+        int32_t lv = 0, ls = 0;
+#pragma unroll
+        for (int s = 1; s <= R; ++s) {
+            int32_t diag_nx = 0;
+            if (s < R) diag_nx = G[s] + tab(s + 1);
+            int32_t hn, vn2, sn;
+            bool hext, vext;
+            cell(s, diag, gup, vup, hn, vn2, sn, hext, vext);
+            if (s == R) { lv = vn2; ls = sn; }
+            G[s] = (sn & ~Y::TBM) + k_go;
+            if (AFFINE) HK[s] = Y::TAGGED ? hn : (hn | Y::TB1);
+            gup = G[s];
+            vup = vn2;
+            diag = diag_nx;
+        }
+        gdiag = g_in;
+        gbot = G[R];
+        vbot = vup;
+        // row-L scout (meaningful in the last lane only): LanePacked::column_tail
+        int32_t corr;
+        if (AFFINE && Y::TAGGED) corr = std::max(lv, ls & ~Y::TBM);
+        else if (AFFINE) corr = std::max(lv | Y::TB3, ls & ~Y::TBM);
+        else corr = ls;
+        const bool upd = corr > (bkey | ((1 << Y::SC_SH) - 1));
+        bkey = upd ? corr : bkey;
+        bj = upd ? j : bj;
+    }
+
+    // the last column (j = n) of this lane's rows, after lane l - 1's part of it (`in`; lane 0:
+    // row 0 -- empty_in())
+    PCABI_HD SplitIn empty_in(int n) const {
+        SplitIn e;
+        e.gup = row0_g(n);
+        e.vup = neg2;
+        e.slt = LT_NONE;
+        e.vt = e.vp = 0;
+        e.score = (int)0x80000000;
+        e.bi = e.lt = e.trail = e.prec = 0;
+        e.attr = 0;
+        return e;
+    }
+
+    template <typename TabRow>
+    PCABI_HD void last_col(const TabRow &tab, int n, const SplitIn &in) {
+        if (last) {
+            // the row-L best of the inner columns (LanePacked::materialize), then B2
+            const int t = Y::tb(bkey);
+            int lt;
+            if (bj == 0) lt = LT_NONE;
+            else if (AFFINE) lt = (Y::TAGGED ? t != 0 : t == 3) ? LT_V : LT_D;
+            else lt = t == 3 ? LT_D : (t == 2 ? LT_V : LT_H);
+            bscore = Y::score(bkey);
+            bi = L;
+            battr = Y::attr(bkey);
+            blt = lt;
+            btrail = 0;
+            bprec = 0;
+            slt_last = LT_NONE;
+            ht_last = 0;
+            hp_last = 0;
+            if (in.score > bscore) {
+                bscore = in.score; bi = in.bi; bj = n; battr = in.attr; blt = in.lt; btrail = in.trail; bprec = in.prec;
+            }
+        } else {
+            bscore = in.score; bi = in.bi; bj = n; battr = in.attr; blt = in.lt; btrail = in.trail; bprec = in.prec;
+        }
+        int32_t gup = in.gup, vup = in.vup;
+        int slt_up = in.slt, vt_up = in.vt, vp_up = in.vp;
+        int32_t diag = gdiag + tab(1);
+        int32_t lv = 0, lh = 0, ls = 0;
+        int lslt = LT_D;
+        bool lhext = false;
+#pragma unroll
+        for (int s = 1; s <= R; ++s) {
+            int32_t diag_nx = 0;
+            if (s < R) diag_nx = G[s] + tab(s + 1);
+            int32_t hn, vn2, sn;
+            bool hext, vext;
+            cell(s, diag, gup, vup, hn, vn2, sn, hext, vext);
+            const int t = Y::tb(sn);
+            const int slt = Y::TAGGED ? (t == (Y::TBM >> Y::TB_SH) ? LT_D : (t >= (Y::TB2 >> Y::TB_SH) ? LT_V : LT_H))
+                                      : (t == 3 ? LT_D : (t == 2 ? LT_V : LT_H));
+            const bool cont = AFFINE ? (vext || slt_up == LT_V) : (slt_up == LT_V);
+            const int vt = cont ? vt_up + 1 : 1;
+            const int vp = cont ? vp_up : (slt_up == LT_D ? 1 : 0);
+            if (s < R || !last) {
+                // a column-n row above row L: the scout, strict '>'
+                const int sc_s = Y::score(sn);
+                if (sc_s > bscore) {
+                    bscore = sc_s;
+                    bi = r0 + s - off;
+                    bj = n;
+                    if (AFFINE) {
+                        const bool isv = Y::score(vn2) == sc_s, ish = !isv && Y::score(hn) == sc_s;
+                        battr = Y::attr(isv ? vn2 : (ish ? hn : sn));
+                        blt = isv ? LT_V : (ish ? LT_H : LT_D);
+                        btrail = isv ? vt : 0;
+                        bprec = isv ? vp : 0;
+                    } else {
+                        battr = Y::attr(sn);
+                        blt = slt;
+                        btrail = (slt == LT_V) ? vt : 0;
+                        bprec = (slt == LT_V) ? vp : 0;
+                    }
+                }
+                if (AFFINE) { vt_up = vt; vp_up = vp; }
+                else { vt_up = (slt == LT_V) ? vt : 0; vp_up = (slt == LT_V) ? vp : 0; }
+                slt_up = slt;
+            } else {
+                // row L (last lane): its cell is scouted below with the trailing runs
+                lv = vn2; lh = hn; ls = sn; lslt = slt; lhext = hext;
+                vt_up = vt;
+                vp_up = vp;
+            }
+            G[s] = (sn & ~Y::TBM) + k_go;
+            if (AFFINE) HK[s] = Y::TAGGED ? hn : (hn | Y::TB1);
+            gup = G[s];
+            vup = vn2;
+            diag = diag_nx;
+        }
+        out.gup = gup; out.vup = vup;
+        out.slt = slt_up; out.vt = vt_up; out.vp = vp_up;
+        out.score = bscore; out.bi = bi; out.lt = blt; out.trail = btrail; out.prec = bprec; out.attr = battr;
+        if (!last) return;
+        // ---- row L, last column (LanePacked::column's tail) ----
+        const bool hcont = AFFINE ? (lhext || slt_last == LT_H) : (slt_last == LT_H);
+        const int ht = hcont ? ht_last + 1 : 1;
+        const int hp = hcont ? hp_last : (slt_last == LT_D ? 1 : 0);
+        const int lsc = Y::score(ls);
+        const bool upd = lsc > bscore;
+        int clt, ctrail, cprec;
+        uint32_t cattr;
+        if (AFFINE) {
+            const bool isv = Y::score(lv) == lsc, ish = !isv && Y::score(lh) == lsc;
+            cattr = Y::attr(isv ? lv : (ish ? lh : ls));
+            clt = isv ? LT_V : (ish ? LT_H : LT_D);
+            ctrail = isv ? vt_up : (ish ? ht : 0);
+            cprec = isv ? vp_up : (ish ? hp : 0);
+        } else {
+            cattr = Y::attr(ls);
+            clt = lslt;
+            ctrail = (lslt == LT_V) ? vt_up : (lslt == LT_H ? ht : 0);
+            cprec = (lslt == LT_V) ? vp_up : (lslt == LT_H ? hp : 0);
+        }
+        bscore = upd ? lsc : bscore;
+        bi = upd ? L : bi;
+        bj = upd ? n : bj;
+        battr = upd ? cattr : battr;
+        blt = upd ? clt : blt;
+        btrail = upd ? ctrail : btrail;
+        bprec = upd ? cprec : bprec;
+    }
+
+    PCABI_HD Result result(int n) const {
+        Best b;
+        b.score = bscore; b.bi = bi; b.bj = bj; b.attr = Y::to_std(battr, bj);
+        b.ltype = blt; b.trail = btrail; b.precd = bprec;
+        return finish(b, L, n);
+    }
+};
+
+// Range conditions: a split bucket runs the packed (or run-tagged) layout of its RPL rows.
+PCABI_HD bool split_ok(int rpl, int K) { return K >= 2 && rpl % K == 0 && rpl / K >= 2 && rpl <= 64; }
+
+// ==========================================================================================
 // Score-only filter for the middle-adapter scan.
 //
 // The scan only needs the alignments whose full-adapter identity reaches the threshold, and

@@ -937,6 +937,18 @@ bool chunkable(int b, bool packed) {
            kBuckets[b].kind == STRIPED || (kBuckets[b].kind == FAST && packed);
 }
 
+// Lanes per window of the row-split core (k_align_split) for a cross-mode launch of `waves`
+// waves: 1 (the one-lane core) once the launch fills 4 waves per SIMD, else 2 or 4 -- the fewest
+// that reach it (at least 2 rows per lane). PCABI_SPLIT=0 turns the split off, 2 / 4 force it.
+int split_lanes(int rpl, int64_t waves) {
+    const char *e = std::getenv("PCABI_SPLIT");
+    const int forced = (e && e[0]) ? std::atoi(e) : -1;
+    int K = 1;
+    if (forced >= 0) K = forced;
+    else if (waves < 4096) K = (2 * waves >= 4096 || rpl < 16) ? 2 : 4;
+    return (K == 2 || K == 4) && pcabi::split_ok(rpl, K) ? K : 1;
+}
+
 // packed: bucket_pack_mode (0 untagged cores off, 1 packed key layout, 2 run-tagged layout)
 int dispatch(int b, const KParams &p, bool affine, hipStream_t st, int packed) {
     if (kBuckets[b].kind == STRIPED) return launch_striped(p, affine, st);
@@ -944,6 +956,11 @@ int dispatch(int b, const KParams &p, bool affine, hipStream_t st, int packed) {
     dim3 grid = p.task_win ? dim3((unsigned)((p.n_waves + 3) / 4))
                            : dim3((unsigned)(tiles8 * p.n_adp));
     const BucketDef d = kBuckets[b];
+    if (!p.task_win && !p.compat && packed && d.kind == FAST && d.rpl <= 64) {
+        // a launch too small to fill the chip: K lanes per window (pcabi_dp.h LaneSplit)
+        const int K = split_lanes(d.rpl, (p.n_win + 255) / 256 * 4 * (int64_t)p.n_adp);
+        if (K > 1 && dispatch_split(d.rpl, K, p, affine, packed == 2, st)) return 0;
+    }
     if (d.kind == LONG || d.kind == WIDE || (d.kind == FAST && packed && d.rpl > 32))
         dispatch_packed_large(d.rpl, d.kind == LONG, p, affine, grid, st);
     else if (d.kind == FAST && packed)
@@ -3499,10 +3516,13 @@ extern "C" int pcabi_end_decisions_host(
     HIP_TRY(hipStreamSynchronize(st));
     n_hits[0] = (int64_t)cnt[0];
     n_hits[1] = (int64_t)cnt[1];
-    // the lists: compact (int16 fields, per-read counts) when every field fits 16 bits
-    int32_t max_win = 0;
+    // the lists: compact (int16 fields, per-read counts) when every field fits 16 bits -- the
+    // alignment lengths l1 / l2 reach the window plus the adapter
+    int32_t max_win = 0, max_adp = 0;
     for (size_t w = 0; w < n; ++w) max_win = std::max(max_win, std::max(s_len[w], e_len[w]));
-    const bool compact = max_win < 32768 && n_sa < 32768 && n_ea < 32768;
+    for (int32_t a = 0; a < n_sa; ++a) max_adp = std::max(max_adp, sa_len[a]);
+    for (int32_t a = 0; a < n_ea; ++a) max_adp = std::max(max_adp, ea_len[a]);
+    const bool compact = (int64_t)max_win + max_adp < 32768 && n_sa < 32768 && n_ea < 32768;
     const size_t half = (n + 1) / 2;                // count dwords per side
     if (compact) {
         size_t words = 0;

@@ -9,6 +9,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <string>
+#include <type_traits>
 
 #include "../../include/pcabi.h"
 #include "pcabi_dp.h"
@@ -103,6 +104,7 @@ struct WindowReader {
     int64_t stride;      // dwords between consecutive chunks
     int a8;
     uint32_t lo, hi, nx;
+    __device__ __forceinline__ WindowReader() : q(nullptr), stride(0), a8(0), lo(0), hi(0), nx(0) {}   // no window
     __device__ __forceinline__ WindowReader(const uint32_t *base, int64_t stride_, int a8_)
         : q(base), stride(stride_), a8(a8_) {
         lo = q[0]; hi = q[stride]; nx = q[2 * stride];
@@ -500,6 +502,86 @@ __global__ __launch_bounds__(256) void k_align_striped(KParams p) {
     }
 }
 
+// ---- row-split cross mode (pcabi_dp.h LaneSplit): launches too small to fill the chip ---------
+// K consecutive lanes share one window, lane l holding rows l R + 1 .. (l + 1) R (R = RPL / K):
+// block = (tile of 256 windows, one of its K sub-ranges of 256 / K windows, adapter), in the
+// XCD-aware order of k_align (the K blocks of a tile on one XCD). The lanes run as a systolic
+// pipeline: at step t lane l computes column t - l from what lane l - 1 computed at step t - 1,
+// received by one DPP row shift (row_shr:1: lane i reads lane i - 1; a group of K lanes never
+// straddles a row of 16); lane 0 takes row 0 instead. The last column runs in K phases. Packed and
+// run-tagged layouts (the end-window buckets), affine and linear gaps.
+__device__ __forceinline__ int32_t lane_from_below(int32_t v) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
+}
+
+template <int RPL, int K, bool AFFINE, int KIND>
+__global__ __launch_bounds__(256, PCABI_WAVES) void k_align_split(KParams p) {
+    constexpr int R = RPL / K;
+    static_assert(RPL % K == 0 && 16 % K == 0 && R >= 2, "split geometry");
+    using Y = typename std::conditional<KIND == TAGGED, pcabi::pk::LayT<RPL>, pcabi::pk::Lay<RPL>>::type;
+    __shared__ __attribute__((aligned(16))) int32_t tab[4 * kTabW * RPL];
+    int32_t *wave_tab = tab + (threadIdx.x >> 6) * (kTabW * RPL);
+    const int64_t b = blockIdx.x;
+    const int64_t k = b >> 3;
+    const int a_local = (int)(k % p.n_adp);
+    const int64_t q = k / p.n_adp;
+    const int64_t tile = (q / K) * 8 + (b & 7);
+    const int l = (int)(threadIdx.x % K);
+    const int64_t w = tile * 256 + (q % K) * (256 / K) + threadIdx.x / K;
+    const int L = __builtin_amdgcn_readfirstlane(p.adp_len[a_local]);
+    fill_wave_tab<RPL, Y>(p, a_local, L, wave_tab);
+    const bool live = w < p.n_win;
+    const int n = live ? p.win_len[w] : 0;
+    int nmax = n;                                        // the wave's step count: its longest window
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) nmax = max(nmax, __shfl_xor(nmax, o));
+    WindowReader rd;
+    if (n > 0) rd = WindowReader(p.tiles + p.tile_off[tile] + (w & 255), 256, 0);
+    pcabi::LaneSplit<R, AFFINE, Y> st;
+    st.init(l, K, L, RPL, p.sc);
+    int32_t sg = st.gbot, sv = st.vbot;
+    const int steps = nmax - 1 + K - 1;
+#pragma unroll 1
+    for (int t = 1; t <= steps; ++t) {
+        int32_t rg = lane_from_below(sg), rv = lane_from_below(sv);
+        if (l == 0) {
+            rg = st.row0_g(t);
+            rv = st.neg2;
+        }
+        const int j = t - l;
+        if (j >= 1 && j < n) {
+            const int c = rd(j);
+            st.inner(LdsRow{wave_tab + c * RPL + st.r0}, j, rg, rv);
+            sg = st.gbot;
+            sv = st.vbot;
+        }
+    }
+    // the last column, lane by lane
+    st.out = pcabi::SplitIn{};
+#pragma unroll
+    for (int ph = 0; ph < K; ++ph) {
+        pcabi::SplitIn in;
+        in.gup = lane_from_below(st.out.gup);
+        in.vup = lane_from_below(st.out.vup);
+        in.slt = lane_from_below(st.out.slt);
+        in.vt = lane_from_below(st.out.vt);
+        in.vp = lane_from_below(st.out.vp);
+        in.score = lane_from_below(st.out.score);
+        in.bi = lane_from_below(st.out.bi);
+        in.lt = lane_from_below(st.out.lt);
+        in.trail = lane_from_below(st.out.trail);
+        in.prec = lane_from_below(st.out.prec);
+        in.attr = (uint32_t)lane_from_below((int32_t)st.out.attr);
+        if (l == ph && n > 0) {
+            if (l == 0) in = st.empty_in(n);
+            const int c = rd(n);
+            st.last_col(LdsRow{wave_tab + c * RPL + st.r0}, n, in);
+        }
+    }
+    if (l == K - 1 && live)
+        store_result(p.out, p.out_stride, (int64_t)p.adp_id[a_local] * p.n_win + w, n > 0 ? st.result(n) : empty_result());
+}
+
 template <int RPL, int KIND>
 void launch(const KParams &p, bool affine, dim3 grid, hipStream_t st) {
     if (affine) hipLaunchKernelGGL((k_align<RPL, true, KIND>), grid, dim3(256), 0, st, p);
@@ -518,6 +600,8 @@ void dispatch_fast(int rpl, bool generic, const KParams &p, bool affine, dim3 gr
 int dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st);
 // k_score_filter launches
 void dispatch_filter(int rpl, const FParams &p, bool affine, hipStream_t st);
+// k_align_split launches (cross mode; grid = padded tiles x adapters x K); false: no such kernel
+bool dispatch_split(int rpl, int K, const KParams &p, bool affine, bool tagged, hipStream_t st);
 // the striped bucket (k_align_striped): p.rt, p.max_cols set by the caller
 int launch_striped(KParams p, bool affine, hipStream_t st);
 

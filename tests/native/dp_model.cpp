@@ -423,3 +423,79 @@ extern "C" int pcabi_model_align_long(const char *read, int n, const char *adp, 
     else run_long<128>(read, n, adp, L, sc, out);
     return 0;
 }
+
+// row-split packed core (pcabi::LaneSplit, k_align_split): the K lanes of one window stepped in
+// lockstep as the kernel runs them -- at step t every lane first takes what its upper neighbour
+// sent at step t - 1 (the lane shift), then lane l computes column t - l; the last column in K
+// phases. tagged != 0: the run-tagged layout (affine, <= 32 rows), else the packed layout.
+template <int RPL, int K, bool AFFINE, typename Y>
+static void run_split(const char *read, int n, const char *adp, int L, pcabi::Scoring sc, int *out) {
+    constexpr int R = RPL / K;
+    const int off = RPL - L;
+    auto ad = [&](int s) { return s <= off ? pcabi::PAD_CODE : dna5((unsigned char)adp[s - off - 1]); };
+    int32_t tab[pcabi::pk::TAB_W * RPL];
+    for (int c = 0; c < pcabi::pk::TAB_W; ++c)
+        for (int s = 1; s <= RPL; ++s) tab[c * RPL + s - 1] = pcabi::pk::sub_key<RPL, decltype(ad), Y>(s, c, ad, off, sc);
+    struct Row {
+        const int32_t *p;
+        int32_t operator()(int s) const { return p[s - 1]; }
+    };
+    auto code = [&](int j) { return dna5((unsigned char)read[j - 1]); };
+    pcabi::LaneSplit<R, AFFINE, Y> st[K];
+    int32_t sg[K], sv[K];
+    for (int l = 0; l < K; ++l) {
+        st[l].init(l, K, L, RPL, sc);
+        sg[l] = st[l].gbot;
+        sv[l] = st[l].vbot;
+    }
+    for (int t = 1; t <= n - 1 + K - 1; ++t) {
+        int32_t rg[K], rv[K];
+        for (int l = 0; l < K; ++l) {
+            rg[l] = l ? sg[l - 1] : st[0].row0_g(t);
+            rv[l] = l ? sv[l - 1] : st[0].neg2;
+        }
+        for (int l = 0; l < K; ++l) {
+            const int j = t - l;
+            if (j >= 1 && j < n) {
+                st[l].inner(Row{tab + code(j) * RPL + st[l].r0}, j, rg[l], rv[l]);
+                sg[l] = st[l].gbot;
+                sv[l] = st[l].vbot;
+            }
+        }
+    }
+    for (int p = 0; p < K; ++p)
+        st[p].last_col(Row{tab + code(n) * RPL + st[p].r0}, n, p ? st[p - 1].out : st[0].empty_in(n));
+    const pcabi::Result r = st[K - 1].result(n);
+    out[0] = r.rs; out[1] = r.re; out[2] = r.as; out[3] = r.ae;
+    out[4] = r.score; out[5] = r.m; out[6] = r.l1; out[7] = r.l2;
+}
+
+template <int RPL, int K>
+static int run_split_any(const char *read, int n, const char *adp, int L, int tagged, pcabi::Scoring sc, int *out) {
+    if (tagged) {
+        if constexpr (RPL <= 32) {
+            if (!pcabi::layt_ok(L, RPL, sc)) return -3;
+            run_split<RPL, K, true, pcabi::pk::LayT<RPL>>(read, n, adp, L, sc, out);
+            return 0;
+        }
+        return -2;
+    }
+    if (!pcabi::packed_ok(L, RPL, sc)) return -3;
+    if (sc.go != sc.ge) run_split<RPL, K, true, pcabi::pk::Lay<RPL>>(read, n, adp, L, sc, out);
+    else run_split<RPL, K, false, pcabi::pk::Lay<RPL>>(read, n, adp, L, sc, out);
+    return 0;
+}
+
+extern "C" int pcabi_model_align_split(const char *read, int n, const char *adp, int L, int rpl, int K, int tagged,
+                                       int ma, int mi, int go, int ge, int *out) {
+    pcabi::Scoring sc{ma, mi, go, ge};
+    if (L <= 0 || n <= 0) return -1;
+    if (!pcabi::split_ok(rpl, K)) return -2;
+#define C(R) case R: return K == 2 ? run_split_any<R, 2>(read, n, adp, L, tagged, sc, out) \
+                                   : (K == 4 ? run_split_any<R, 4>(read, n, adp, L, tagged, sc, out) : -2);
+    switch (rpl) {
+    C(8) C(12) C(16) C(20) C(24) C(28) C(32) C(36) C(40) C(44) C(48) C(52) C(56) C(60) C(64)
+    default: return -2;
+    }
+#undef C
+}

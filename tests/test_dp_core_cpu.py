@@ -601,3 +601,76 @@ def test_cores_free_gap_schemes_golden(model):
         n_str += 1
         n_long += len(r) >= 32768
     assert n_gen >= 1500 and n_str >= 1800 and n_long >= 30
+
+
+def test_row_split_core(model):
+    """The row-split packed core (pcabi_dp.h LaneSplit, k_align_split: K lanes per window, each
+    holding RPL / K rows, the lanes a systolic pipeline with the last column in K phases), run by
+    the host model in lockstep: == the oracle for the run-tagged and packed layouts, K = 2 and 4,
+    every bucket, tie-heavy alphabets, long gap runs, extra padding rows (whole padding lanes
+    included), windows of 1 column and the reference's golden rows."""
+    model.pcabi_model_align_split.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int] + \
+        [ctypes.c_int] * 7 + [ctypes.c_void_p]
+
+    def split(r, a, rpl, K, tagged, sc):
+        out = (ctypes.c_int * 8)()
+        rc = model.pcabi_model_align_split(r.encode(), len(r), a.encode(), len(a), rpl, K, tagged, *sc, out)
+        return rc, list(out)
+
+    rng = random.Random(77)
+    schemes = [(3, -6, -5, -2), (2, -1, -1, -1), (1, -1, -3, -1), (3, -6, -2, -5), (5, -4, -8, -6), (2, -3, -5, -1),
+               (1, 3, -5, -2)]
+    n_checked = {(t, K): 0 for t in (0, 1) for K in (2, 4)}
+    for k in range(8000):
+        sc = schemes[k % len(schemes)]
+        tagged = k % 2
+        K = rng.choice([2, 4])
+        al = rng.choice(['A', 'AT', 'ACGT', 'ACGTN'])
+        L = rng.randint(1, 31 if tagged else 64)
+        rpl = rng.choice([r for r in range(8, (33 if tagged else 65), 4) if r >= L and r % K == 0 and r // K >= 2])
+        a = ''.join(rng.choice(al) for _ in range(L))
+        if k % 3 == 0:
+            b = list(a)
+            for _ in range(rng.randint(0, 3)):
+                p = rng.randint(0, len(b))
+                if rng.random() < 0.5:
+                    b[p:p] = [rng.choice(al) for _ in range(rng.randint(1, 30))]
+                else:
+                    del b[p:p + rng.randint(1, 8)]
+            r = ''.join(rng.choice(al) for _ in range(rng.randint(0, 60))) + ''.join(b) + \
+                ''.join(rng.choice(al) for _ in range(rng.randint(0, 60)))
+            r = r or 'A'
+        else:
+            r = ''.join(rng.choice(al) for _ in range(rng.choice([1, 2, 3, rng.randint(1, 260)])))
+        rc, res = split(r, a, rpl, K, tagged, sc)
+        if rc == -3:
+            continue
+        assert rc == 0 and res == oracle_lib.align(r, a, sc), (sc, r, a, rpl, K, tagged)
+        n_checked[(tagged, K)] += 1
+    assert min(n_checked.values()) > 800, n_checked
+    for sc in schemes:                                # the longest gap runs
+        for L in (1, 8, 17, 24, 28, 31):
+            for n in (1, 60, 150, 400):
+                for K in (2, 4):
+                    for tagged in (0, 1):
+                        rpl = max(8, (L + 3) & ~3)
+                        rpl += (-rpl) % (4 * K // 2)
+                        rc, res = split('A' * n, 'C' * L, rpl, K, tagged, sc)
+                        if rc == 0:
+                            assert res == oracle_lib.align('A' * n, 'C' * L, sc), (sc, L, n, K, tagged)
+    n_gold = 0
+    for sc, r, a, exp in golden_lib.g1_rows():
+        if not r or not a or len(a) > 64:
+            continue
+        rpl = max(8, (len(a) + 3) & ~3)
+        for K in (2, 4):
+            if rpl % K or rpl // K < 2:
+                continue
+            rc, res = split(r, a, rpl, K, int(len(a) <= 31), sc)
+            if rc == -3 or (rc == -2 and len(a) <= 31):
+                rc, res = split(r, a, rpl, K, 0, sc)
+            if rc != 0:
+                continue
+            assert _fmt(res) == exp, (sc, r, a, exp, res, K)
+            n_gold += 1
+    assert n_gold > 2000

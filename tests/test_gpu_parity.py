@@ -469,3 +469,41 @@ def test_middle_scan_seed_plan_follows_adapters(gpu_lib, monkeypatch):
         order_g = np.lexsort((np.arange(got.shape[1]), got[0]))
         order_e = np.lexsort((np.arange(exp.shape[1]), exp[0]))
         assert np.array_equal(got[:, order_g], exp[:, order_e]), trial
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('split', ['2', '4', ''])
+@pytest.mark.parametrize('scheme', [(3, -6, -5, -2), (2, -1, -1, -1), (1, -1, -3, -1), (1, 3, -5, -2)])
+def test_row_split_cross_product(gpu_lib, monkeypatch, split, scheme):
+    """Cross products of a few adapters over thousands of windows -- the launches the row-split
+    core (k_align_split: K lanes per window, DPP row shifts, the last column in K phases) takes
+    (PCABI_SPLIT unset: by wave count; 2 / 4 forced) -- vs the oracle on every field: run-tagged
+    and packed buckets of 8..64 rows, adapters padded into larger buckets, ragged, empty and
+    1-column windows, tie-heavy alphabets, planted mutated copies."""
+    from custom_porechop_abi_amd import engine
+    monkeypatch.setenv('PCABI_SPLIT', split)
+    rng = random.Random(sum(scheme) * 31 + len(split))
+    adps = ['AATGTACTTCGTTCAGTTACGTATTGCT', 'GCAATACGTAACTGAACGAAGT', 'CTTCGTTCAGTTACGTATTGCTGGCGTCTGCTT',
+            _rand_seq(rng, 7, 'ACGT'), _rand_seq(rng, 45, 'ACGT'), _rand_seq(rng, 63, 'ACGT')]
+    reads = []
+    for k in range(3000):
+        n = rng.choice([0, 1, 2, 150, 150, 150, rng.randint(3, 400)])
+        r = _rand_seq(rng, n, rng.choice(['ACGT', 'ACGT', 'AT', 'ACGTN']))
+        if n > 40 and rng.random() < 0.6:
+            a = _mutate(rng, rng.choice(adps), rng.choice([0.0, 0.05, 0.15]))
+            p = rng.randint(0, n)
+            r = (r[:p] + a + r[p:])[:max(n, len(a))]
+        reads.append(r)
+    pack = engine.SeqPack(reads)
+    views = pack.views(np.zeros(len(reads), np.int64), pack.lengths)
+    n = len(reads)
+    for group in ([0], [1], [2], [3], [4], [5], [0, 1], [1, 2, 4]):
+        sel = [adps[i] for i in group]
+        got = engine.align(views, sel, scheme)
+        k = 700                                    # the oracle on the first k windows of every adapter
+        exp = oracle_lib.align_many(reads[:k], sel, (np.tile(np.arange(k), len(sel)), np.repeat(np.arange(len(sel)), k)),
+                                    scheme)
+        g = got.reshape(8, len(sel), n)[:, :, :k].reshape(8, -1)
+        ok = exp[0] != -1
+        assert np.array_equal(g[0], exp[0])
+        assert np.array_equal(g[:, ok], exp[:, ok]), (group, _first_diff(g, exp, reads[:k], sel, k))
