@@ -110,12 +110,18 @@ bool middle_devplan_on() {
 }
 
 // Queued rounds run the candidate DP over the verified seeds' windows, with the whole read only for
-// the candidates whose window winner is a hit the certificate cannot vouch for (k_certify)
-// (PCABI_MIDDLE_WINDOWS=1). Off by default: the second plan's launches cost more than the windows
-// save on 8 kb reads (2.77 -> 2.96 ms per middle step), while 20 kb reads gain (4.31 -> 3.95 ms).
-bool middle_windows_on() {
+// the candidates whose window winner is a hit the certificate cannot vouch for (k_certify). The
+// windows pay on long reads only: the second plan's launches cost more than they save at 8 kb
+// (2.90 -> 2.86 ms), break even at 12 kb and win 10-12 % from 16 kb (20 kb: 4.21 -> 3.70 ms,
+// profiles/r03/final/windows_sweep/). So they run when the batch's mean read length reaches
+// kWindowsMeanLen -- from the host lengths when the caller passes them, else from the previous
+// call's round-1 segment total (pcabi_scan::last_mean). PCABI_MIDDLE_WINDOWS=1 / 0 forces them.
+constexpr double kWindowsMeanLen = 14000.0;
+bool middle_windows_on(double mean_len) {
     const char *e = std::getenv("PCABI_MIDDLE_WINDOWS");
-    return e && e[0] == '1';
+    if (e && e[0] == '1') return true;
+    if (e && e[0] == '0') return false;
+    return mean_len >= kWindowsMeanLen;
 }
 
 // Device planning aims at this many waves per candidate-DP round (4 per SIMD): the chunk length
@@ -1140,6 +1146,8 @@ int bounds_dev(State *s, const uint8_t *codes, const int64_t *v_off, const int32
                const int32_t **pmap, int64_t *vcap, hipStream_t st);
 bool grow_after_overflow(State *s, int raw_overflow, int task_overflow);
 void shrink_next(State *s, int bits);
+const int64_t *seg_cum_dev(State *s);
+int seg_positions();
 void cert_bounds(State *s, std::vector<int32_t> &U);
 int debug_counts(State *s, int64_t (&out)[5], hipStream_t st);
 }  // namespace pcabi_seed
@@ -1156,6 +1164,9 @@ struct pcabi_scan {
     DeviceBuf q_cur, q_start, q_list, q_n, q_flags, q_bk, q_wave, q_misc, pcbase;
     int32_t *h_stage = nullptr;                     // pinned host staging of the queued rounds' hit lists
     size_t h_stage_cap = 0;                         // (int32 elements)
+    int32_t *h_ctl = nullptr;                       // pinned: round counts, flags, plan needs of a batch
+    int64_t spec_hits = 4096;                       // hits per round copied with the counts (grows to fit)
+    double last_mean = 0.0;                         // the previous call's mean read length (round 1)
     int64_t q_slots_cap = 0;
     std::vector<int32_t> h_ucert;                   // the certificate bounds last uploaded to pucert
 };
@@ -1962,6 +1973,7 @@ void pcabi_scan_destroy(pcabi_scan *s) {
                          &s->pcand2, &s->wa2, &s->pres2, &s->pcert, &s->pucert, &s->q_bk2, &s->q_misc2})
         if (b->p) (void)hipFree(b->p);
     if (s->h_stage) (void)hipHostFree(s->h_stage);
+    if (s->h_ctl) (void)hipHostFree(s->h_ctl);
     if (s->seed) pcabi_seed::destroy(s->seed);
     delete s;
 }
@@ -2502,8 +2514,8 @@ std::vector<std::pair<int64_t, int>> middle_faults() {
 // Returns the hit count (> 0, <= 0 on error as pcabi_middle_scan_dev); applied = false when the
 // seeded plan does not cover this table and scoring (the caller runs the host-driven loop).
 int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_off, const int32_t *win_len,
-                             int64_t n_win, const pcabi::Scoring &scr, double threshold, int32_t *hits, int64_t cap,
-                             hipStream_t st, bool &applied) {
+                             const int32_t *h_win_len, int64_t n_win, const pcabi::Scoring &scr, double threshold,
+                             int32_t *hits, int64_t cap, hipStream_t st, bool &applied) {
     applied = false;
     const pcabi_adapters *adps = sc->adps;
     const int32_t n_adp = adps->n_adp;
@@ -2578,7 +2590,13 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
     HIP_TRY(hipMemcpyAsync(sc->q_bk.p, bk_host.data(), 4 * bk_host.size(), hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(sc->pspan.p, span.data(), 4 * (size_t)n_adp, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(sc->plen.p, adps->hlen.data(), 4 * (size_t)n_adp, hipMemcpyHostToDevice, st));
-    const bool windows = middle_windows_on();
+    double mean_len = sc->last_mean;
+    if (h_win_len) {
+        double tot = 0.0;
+        for (int64_t k = 0; k < n; ++k) tot += h_win_len[k];
+        mean_len = n ? tot / (double)n : 0.0;
+    }
+    const bool windows = middle_windows_on(mean_len);
     if (windows) {
         std::vector<int32_t> U;
         pcabi_seed::cert_bounds(sc->seed, U);
@@ -2780,51 +2798,64 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
         }
         return 0;
     };
-    std::vector<int32_t> h_n(kSlots + 2), h_flag(kSlots + 2);
-    int64_t need = 0, need2 = 0;
+    // pinned control block: round counts [kSlots + 2], flags [kSlots + 2], need / flag word / need2
+    if (!sc->h_ctl) HIP_TRY(hipHostMalloc((void **)&sc->h_ctl, 4 * (2 * (kSlots + 2) + 8), hipHostMallocDefault));
+    int32_t *h_n = sc->h_ctl, *h_flag = sc->h_ctl + (kSlots + 2);
+    int64_t *h_nd = (int64_t *)(sc->h_ctl + 2 * (kSlots + 2));   // [0..2] need, flag word, need2; [3] round 1's segments
+    h_nd[3] = -1;
+    // every queued round's first spec entries come back with the counts (one synchronisation per
+    // batch of rounds instead of two); a round with more hits fetches the rest after
+    const int64_t spec = std::min<int64_t>(sc->spec_hits, n);
+    {
+        const size_t want = 8 * (size_t)spec * kBatch;
+        if (want > sc->h_stage_cap) {
+            if (sc->h_stage) HIP_TRY(hipHostFree(sc->h_stage));
+            sc->h_stage = nullptr;
+            sc->h_stage_cap = 0;
+            HIP_TRY(hipHostMalloc((void **)&sc->h_stage, 4 * want, hipHostMallocDefault));
+            sc->h_stage_cap = want;
+        }
+    }
+    int64_t need = 0, need2 = 0, most_hits = 0;
     for (int guard = 0;; ++guard) {
         if (guard > 10000) return fail(PCABI_E_DEVICE, "middle scan: rounds did not settle");
         // queue up to kBatch rounds from `slot`
         const int upto = std::min(slot + kBatch, kSlots);
-        for (int r = slot; r < upto; ++r)
+        for (int r = slot; r < upto; ++r) {
             if (int rc = queue_round(r)) return rc;
+            if (r == 0 && round_base == 0)        // round 1's segment total (the next call's mean length)
+                HIP_TRY(hipMemcpyAsync(h_nd + 3, pcabi_seed::seg_cum_dev(sc->seed) + n, sizeof(int64_t),
+                                       hipMemcpyDeviceToHost, st));
+        }
         queued_to = upto;
-        HIP_TRY(hipMemcpyAsync(h_n.data(), d_n, 4 * (size_t)(queued_to + 1), hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipMemcpyAsync(h_flag.data(), d_rflag, 4 * (size_t)queued_to, hipMemcpyDeviceToHost, st));
-        int64_t nd[3];                                // need, flag word, need2: one copy
-        HIP_TRY(hipMemcpyAsync(nd, d_need, sizeof(nd), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(h_n, d_n, 4 * (size_t)(queued_to + 1), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(h_flag, d_rflag, 4 * (size_t)queued_to, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(h_nd, d_need, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, st));   // need, flags, need2
+        for (int r = slot; r < queued_to; ++r)
+            HIP_TRY(hipMemcpyAsync(sc->h_stage + 8 * (size_t)spec * (r - slot), list_of(r), 32 * (size_t)spec,
+                                   hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
-        need = nd[0];
-        need2 = nd[2];
+        need = h_nd[0];
+        need2 = h_nd[2];
         // the first flagged round (nothing of it or after it was kept): grow, queue it again
         int bad = -1;
         for (int r = slot; r < queued_to && bad < 0; ++r)
             if (h_flag[r]) bad = r;
         int done_to = bad >= 0 ? bad : queued_to;    // rounds [slot, done_to) are final
-        {
-            // the finished rounds' lists, through pinned staging (one synchronisation)
-            size_t want = 0;
-            for (int r = slot; r < done_to; ++r) want += 8 * (size_t)h_n[r + 1];
-            if (want > sc->h_stage_cap) {
-                if (sc->h_stage) HIP_TRY(hipHostFree(sc->h_stage));
-                sc->h_stage = nullptr;
-                sc->h_stage_cap = 0;
-                const size_t cap2 = std::max<size_t>(want, 1 << 16);
-                HIP_TRY(hipHostMalloc((void **)&sc->h_stage, 4 * cap2, hipHostMallocDefault));
-                sc->h_stage_cap = cap2;
+        // the finished rounds' lists: the staged part, then (rarely) the rest
+        for (int r = slot; r < done_to; ++r) {
+            const int64_t nh = h_n[r + 1];
+            if (!nh) continue;
+            most_hits = std::max(most_hits, nh);
+            const int32_t *st_r = sc->h_stage + 8 * (size_t)spec * (r - slot);
+            out.insert(out.end(), st_r, st_r + 8 * (size_t)std::min(nh, spec));
+            if (nh > spec) {
+                const size_t old = out.size();
+                out.resize(old + 8 * (size_t)(nh - spec));
+                HIP_TRY(hipMemcpy(out.data() + old, list_of(r) + 8 * spec, 32 * (size_t)(nh - spec),
+                                  hipMemcpyDeviceToHost));
             }
-            size_t at = 0;
-            for (int r = slot; r < done_to; ++r) {
-                const int32_t nh = h_n[r + 1];
-                if (!nh) continue;
-                HIP_TRY(hipMemcpyAsync(sc->h_stage + at, list_of(r), 32 * (size_t)nh, hipMemcpyDeviceToHost, st));
-                at += 8 * (size_t)nh;
-                out_round.insert(out_round.end(), (size_t)nh, round_base + r);
-            }
-            if (at) {
-                HIP_TRY(hipStreamSynchronize(st));
-                out.insert(out.end(), sc->h_stage, sc->h_stage + at);
-            }
+            out_round.insert(out_round.end(), (size_t)nh, round_base + r);
         }
         if (g_debug)
             for (int r = slot; r < queued_to; ++r)
@@ -2861,6 +2892,10 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
         }
     }
     HIP_TRY(hipStreamSynchronize(st));
+    // the next call stages as many hits per round as this one's busiest round had (+ 25 %), and
+    // takes its mean read length from this call's round-1 segments
+    sc->spec_hits = std::max<int64_t>(4096, most_hits + most_hits / 4);
+    if (h_nd[3] >= 0 && n > 0) sc->last_mean = (double)h_nd[3] * pcabi_seed::seg_positions() / (double)n;
     // (round, read) order: per read the reference's discovery order
     const int64_t total = (int64_t)out_round.size();
     std::vector<int64_t> ord((size_t)total);
@@ -2931,7 +2966,8 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
     }
     {
         bool applied = false;
-        const int64_t r = middle_device_rounds(sc, codes, win_off, win_len, n_win, scoring, threshold, hits, cap, st, applied);
+        const int64_t r = middle_device_rounds(sc, codes, win_off, win_len, h_win_len, n_win, scoring, threshold, hits,
+                                               cap, st, applied);
         if (applied || r < 0) return r;
     }
     if (int rc = host_lengths()) return rc;

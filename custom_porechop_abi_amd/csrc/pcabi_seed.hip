@@ -1519,6 +1519,11 @@ int bounds_dev(State *s, const uint8_t *codes, const int64_t *v_off, const int32
     return 0;
 }
 
+// The last seeding's segment scan (kSeg positions per segment, n + 1 entries, the total last):
+// the engine reads round 1's total to size its next call (candidate windows on long reads).
+const int64_t *seg_cum_dev(State *s) { return (const int64_t *)s->segcum.p; }
+int seg_positions() { return kSeg; }
+
 // Tests (the engine's PCABI_MIDDLE_FAULT): the next queued seeding runs with its raw-hit slabs
 // (bits & 1) and / or its inside-task regions (bits & 2) shrunk to one entry, so its kernels overflow
 // for real and flag the round; the buffers keep their sizes.
