@@ -2139,7 +2139,7 @@ int device_plan_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_off,
             p.max_cols = nb_maxcols[k];
             int rc;
             if (bchunk[b]) {
-                rc = dispatch_chunk(b, p, scr.go != scr.ge, fj.at(k));
+                rc = dispatch_chunk(b, p, scr.go != scr.ge, fj.at(k), bucket_pack_mode(b, adps->lens[b], scr) == 2);
             } else {
                 p.task_chunk = nullptr;   // whole windows
                 rc = dispatch(b, p, scr.go != scr.ge, fj.at(k), bucket_pack_mode(b, adps->lens[b], scr));
@@ -2430,7 +2430,7 @@ int filtered_first_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_o
             p.max_cols = nb_maxcols[k];
             int rc;
             if (nb_chunked[k]) {
-                rc = dispatch_chunk(b, p, scr.go != scr.ge, fj.at(k));
+                rc = dispatch_chunk(b, p, scr.go != scr.ge, fj.at(k), bucket_pack_mode(b, adps->lens[b], scr) == 2);
             } else {
                 p.task_chunk = nullptr;   // whole windows
                 rc = dispatch(b, p, scr.go != scr.ge, fj.at(k), bucket_pack_mode(b, adps->lens[b], scr));
@@ -2730,7 +2730,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
                 p.n_adp = adps->count[b];
                 p.rt = adps->rt[b];
                 p.dev_waves = pl.bk_waves + 2 * k;
-                if (int rc = dispatch_chunk(b, p, scr.go != scr.ge, fj.at(k))) {
+                if (int rc = dispatch_chunk(b, p, scr.go != scr.ge, fj.at(k), bucket_pack_mode(b, adps->lens[b], scr) == 2)) {
                     (void)fj.end();
                     return rc;
                 }

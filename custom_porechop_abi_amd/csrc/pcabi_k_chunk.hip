@@ -4,10 +4,18 @@
 
 namespace pcabi_eng {
 
-int dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st) {
+int dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st, bool tagged) {
     // planned on the device: n_waves is the grid (blocks striding over the device wave count)
     const dim3 grid((unsigned)(p.dev_waves ? p.n_waves : (p.n_waves + 3) / 4));
     if (kBuckets[b].kind == STRIPED) return launch_striped(p, affine, st);
+    if (tagged && affine && kBuckets[b].kind == FAST && kBuckets[b].rpl <= 32) {
+        // the run-tagged layout (9 VALU ops per cell instead of 10), as the end-window buckets
+        switch (kBuckets[b].rpl) {
+#define C(R) case R: hipLaunchKernelGGL((k_align_chunk<R, true, TAGGED>), grid, dim3(256), 0, st, p); return 0;
+        C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32)
+#undef C
+        }
+    }
     if (kBuckets[b].kind == GENERIC) {
         switch (kBuckets[b].rpl) {
 #define C(R)                                                                                            \

@@ -350,6 +350,7 @@ __device__ __forceinline__ void chunk_wave(const KParams &p, int64_t wave, bool 
     const int a_local = __builtin_amdgcn_readfirstlane(p.wave_adp[wave]);
     const int L = __builtin_amdgcn_readfirstlane(p.adp_len[a_local]);
     if constexpr (KIND == PACKED) fill_wave_tab<RPL>(p, a_local, L, wave_tab);
+    if constexpr (KIND == TAGGED) fill_wave_tab<RPL, pcabi::pk::LayT<RPL>>(p, a_local, L, wave_tab);
     if constexpr (KIND == LONG) fill_wave_tab_long<RPL>(p, a_local, L, wave_tab);
     const int32_t tw = live ? p.task_win[slot] : -1;
     if (tw < 0) return;
@@ -361,6 +362,10 @@ __device__ __forceinline__ void chunk_wave(const KParams &p, int64_t wave, bool 
     if constexpr (KIND == PACKED) {
         auto tabfn = [&](int rc) { return LdsRow{wave_tab + rc * RPL}; };
         r = pcabi::align_lane_packed<RPL, AFFINE, true>(rd, ck.y, tabfn, L, p.sc, ck.z, ck.w);
+    } else if constexpr (KIND == TAGGED) {
+        static_assert(RPL <= 32 && AFFINE, "run-tagged layout: affine buckets of <= 32 rows");
+        auto tabfn = [&](int rc) { return LdsRow{wave_tab + rc * RPL}; };
+        r = pcabi::align_lane_packed<RPL, true, true, pcabi::pk::LayT<RPL>>(rd, ck.y, tabfn, L, p.sc, ck.z, ck.w);
     } else if constexpr (KIND == LONG) {
         WindowReader rd1 = rd;
         auto tab0 = [&](int rc) { return LdsRow{wave_tab + rc * RPL}; };
@@ -596,8 +601,9 @@ void dispatch_packed_small(int rpl, const KParams &p, bool affine, dim3 grid, hi
 void dispatch_packed_large(int rpl, bool long_kind, const KParams &p, bool affine, dim3 grid,
                            hipStream_t st);                                                   // PACKED 36..88, LONG
 void dispatch_fast(int rpl, bool generic, const KParams &p, bool affine, dim3 grid, hipStream_t st);
-// k_align_chunk launches (middle-scan candidates in owned-column chunks), striped bucket included
-int dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st);
+// k_align_chunk launches (middle-scan candidates in owned-column chunks), striped bucket included;
+// tagged: the bucket runs the run-tagged layout (bucket_pack_mode 2)
+int dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st, bool tagged = false);
 // k_score_filter launches
 void dispatch_filter(int rpl, const FParams &p, bool affine, hipStream_t st);
 // k_align_split launches (cross mode; grid = padded tiles x adapters x K); false: no such kernel

@@ -3,6 +3,7 @@
 // per-lane algorithm the HIP kernels execute can be checked exhaustively without a GPU.
 #include "../../custom_porechop_abi_amd/csrc/pcabi_dp.h"
 #include <cstring>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -270,15 +271,17 @@ extern "C" int pcabi_model_compat(const char *s1, const char *s2) {
 // chunks of C owned columns for threshold score T, each aligned alone, merged in read order (first
 // largest score), read offsets added back. Returns the number of chunks, -3 if out of range, -4
 // if chunking does not apply (chunk_span < 0).
-template <int RPL>
+template <int RPL, bool TAGGED_LAY = false>
 static void run_packed_chunk(const char *read, int n, const char *adp, int L, pcabi::Scoring sc, int own_lo,
                              int own_hi, int *out) {
+    using Y = typename std::conditional<TAGGED_LAY && RPL <= 32, pcabi::pk::LayT<(RPL <= 32 ? RPL : 32)>,
+                                        pcabi::pk::Lay<RPL>>::type;
     const int off = RPL - L;
     auto rd = [&](int j) { return j <= n ? dna5((unsigned char)read[j - 1]) : 4; };
     auto ad = [&](int s) { return s <= off ? pcabi::PAD_CODE : dna5((unsigned char)adp[s - off - 1]); };
     int32_t tab[pcabi::pk::TAB_W * RPL];
     for (int c = 0; c < pcabi::pk::TAB_W; ++c)
-        for (int s = 1; s <= RPL; ++s) tab[c * RPL + s - 1] = pcabi::pk::sub_key<RPL>(s, c, ad, off, sc);
+        for (int s = 1; s <= RPL; ++s) tab[c * RPL + s - 1] = pcabi::pk::sub_key<RPL, decltype(ad), Y>(s, c, ad, off, sc);
     struct Row {
         const int32_t *p;
         int32_t operator()(int s) const { return p[s - 1]; }
@@ -286,8 +289,8 @@ static void run_packed_chunk(const char *read, int n, const char *adp, int L, pc
     };
     auto tabfn = [&](int rc) { return Row{tab + rc * RPL}; };
     pcabi::Result r = (sc.go != sc.ge)
-        ? pcabi::align_lane_packed<RPL, true, true>(rd, n, tabfn, L, sc, own_lo, own_hi)
-        : pcabi::align_lane_packed<RPL, false, true>(rd, n, tabfn, L, sc, own_lo, own_hi);
+        ? pcabi::align_lane_packed<RPL, true, true, Y>(rd, n, tabfn, L, sc, own_lo, own_hi)
+        : pcabi::align_lane_packed<RPL, false, true, Y>(rd, n, tabfn, L, sc, own_lo, own_hi);
     out[0] = r.rs; out[1] = r.re; out[2] = r.as; out[3] = r.ae;
     out[4] = r.score; out[5] = r.m; out[6] = r.l1; out[7] = r.l2;
 }
@@ -305,12 +308,15 @@ static void run_generic_chunk(const char *read, int n, const char *adp, int L, p
     out[4] = r.score; out[5] = r.m; out[6] = r.l1; out[7] = r.l2;
 }
 
-// generic != 0: the generic core (long adapters) instead of the packed one
+// generic: 0 the packed core, 1 the generic core (long adapters), 2 the run-tagged layout
 extern "C" int pcabi_model_align_chunked(const char *read, int n, const char *adp, int L, int ma, int mi, int go,
                                          int ge, int T, int C, int generic, int *out) {
     pcabi::Scoring sc{ma, mi, go, ge};
     if (L <= 0 || n <= 0 || C <= 0) return -1;
     const int rpl = (L + 3) & ~3;
+    const bool tagged = generic == 2;
+    if (tagged) generic = 0;
+    if (tagged && !pcabi::layt_ok(L, rpl, sc)) return -3;
     if (!generic && !pcabi::packed_ok(L, rpl, sc)) return -3;
     if (generic && L > 128) return -3;
     const int D = pcabi::sf::chunk_span(L, T, sc);
@@ -321,6 +327,10 @@ extern "C" int pcabi_model_align_chunked(const char *read, int n, const char *ad
         if (generic) {
             if (L <= 64) run_generic_chunk<64>(read + ck.start, ck.len, adp, L, sc, ck.own_lo, ck.own_hi, got);
             else run_generic_chunk<128>(read + ck.start, ck.len, adp, L, sc, ck.own_lo, ck.own_hi, got);
+        } else if (tagged) switch (rpl) {
+#define C_(R) case R: run_packed_chunk<R, true>(read + ck.start, ck.len, adp, L, sc, ck.own_lo, ck.own_hi, got); break;
+        C_(4) C_(8) C_(12) C_(16) C_(20) C_(24) C_(28) C_(32)
+#undef C_
         } else switch (rpl) {
 #define C_(R) case R: run_packed_chunk<R>(read + ck.start, ck.len, adp, L, sc, ck.own_lo, ck.own_hi, got); break;
         C_(4) C_(8) C_(12) C_(16) C_(20) C_(24) C_(28) C_(32) C_(36) C_(40) C_(44) C_(48) C_(52) C_(56) C_(60)

@@ -377,7 +377,7 @@ def test_score_filter_threshold_is_a_lower_bound(model):
     assert checked > 500
 
 
-@pytest.mark.parametrize('core', ['packed', 'generic'])
+@pytest.mark.parametrize('core', ['packed', 'generic', 'tagged'])
 @pytest.mark.parametrize('sc', [(3, -6, -5, -2), (2, -1, -1, -1), (1, -1, -3, -1), (5, -4, -8, -6), (1, 2, -4, -2)])
 def test_chunked_candidate_dp(model, sc, core):
     """The middle scan's chunked candidate DP (pcabi_dp.h sf::chunk_plan + align_lane_packed with
@@ -392,7 +392,11 @@ def test_chunked_candidate_dp(model, sc, core):
             ''.join(rng.choice('ACGT') for _ in range(40)), ''.join(rng.choice('ACGT') for _ in range(64))]
     if core == 'generic':   # long adapters (the 102 / 111 bp full rapid sequences) too
         adps += [''.join(rng.choice('ACGT') for _ in range(L)) for L in (102, 111)]
-    for it in range(1500 if core == 'packed' else 300):
+    if core == 'tagged':    # the run-tagged chunk kernels (k_align_chunk<.., TAGGED>): <= 31 bp
+        adps = [x for x in adps if len(x) <= 31] + [''.join(rng.choice('ACGT') for _ in range(31))]
+        if sc[2] == sc[3]:
+            pytest.skip('the run-tagged layout is affine only')
+    for it in range(1500 if core != 'generic' else 300):
         a = rng.choice(adps)
         n = rng.choice([rng.randint(1, 60), rng.randint(60, 600), rng.randint(600, 2500)])
         r = ''.join(rng.choice('ACGT') for _ in range(n))
@@ -416,7 +420,10 @@ def test_chunked_candidate_dp(model, sc, core):
             C = rng.choice([1, 3, 17, 64, 200, 1000])
             out = (ctypes.c_int * 8)()
             rb, ab = r.encode(), a.encode()
-            nc = model.pcabi_model_align_chunked(rb, len(rb), ab, len(ab), *sc, T, C, int(core == 'generic'), out)
+            nc = model.pcabi_model_align_chunked(rb, len(rb), ab, len(ab), *sc, T, C,
+                                                 {'packed': 0, 'generic': 1, 'tagged': 2}[core], out)
+            if nc == -3 and core == 'tagged':
+                continue
             assert nc > 0, (nc, sc, T, C)
             got = list(out)
             if whole[4] >= T:
