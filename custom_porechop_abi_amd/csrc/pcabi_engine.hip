@@ -124,6 +124,16 @@ bool middle_windows_on(double mean_len) {
     return mean_len >= kWindowsMeanLen;
 }
 
+// Queued rounds from this index on (0 = round 1) launch their band classes and candidate-DP
+// buckets one after the other on the scan's stream: by the third round only the reads that hit
+// twice are left, their launches last a few microseconds, and each fork / join over side streams
+// costs ~15-20 us of event latency (profiles/r03/final/kernel_trace_middle_8kb.csv).
+// PCABI_MIDDLE_SERIAL_FROM overrides (a large value keeps every round side by side).
+int middle_serial_from() {
+    const char *e = std::getenv("PCABI_MIDDLE_SERIAL_FROM");
+    return (e && e[0]) ? std::atoi(e) : 2;
+}
+
 // Device planning aims at this many waves per candidate-DP round (4 per SIMD): the chunk length
 // is the longest of 512, 256, 128, 64 owned columns that still reaches it.
 int64_t middle_plan_waves() {
@@ -1146,6 +1156,7 @@ int bounds_dev(State *s, const uint8_t *codes, const int64_t *v_off, const int32
                const int32_t **pmap, int64_t *vcap, hipStream_t st);
 bool grow_after_overflow(State *s, int raw_overflow, int task_overflow);
 void shrink_next(State *s, int bits);
+void serial_next(State *s);
 const int64_t *seg_cum_dev(State *s);
 int seg_positions();
 void cert_bounds(State *s, std::vector<int32_t> &U);
@@ -2623,6 +2634,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
             if (std::sscanf(e, "%lld,%lld,%lld", &raw, &task, &slots) == 3 && slots > 0) sc->q_slots_cap = slots;
     }
     const std::vector<std::pair<int64_t, int>> faults = middle_faults();
+    const int serial_from = middle_serial_from();
     std::vector<char> fired(faults.size(), 0);
     int injected[kSlots + 1] = {};                  // per slot: the faults its last queueing injected
     const int64_t target = middle_plan_waves();
@@ -2641,6 +2653,8 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
             }
         injected[r] = fault;
         if (fault & 3) pcabi_seed::shrink_next(sc->seed, fault & 3);
+        const bool serial = round_base + r >= serial_from;
+        if (serial) pcabi_seed::serial_next(sc->seed);
         const int64_t slots_cap = (fault & 4) ? 64 : sc->q_slots_cap;
         if (int rc = sc->tw.ensure(sizeof(int32_t) * slots_cap)) return rc;
         if (int rc = sc->to.ensure(sizeof(int32_t) * slots_cap)) return rc;
@@ -2721,7 +2735,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
             p.task_chunk = (const int4 *)pl.tck->p;
             p.n_waves = kGrid;
             ForkJoin fj;
-            if (int rc = fj.begin(st, used.size())) return rc;
+            if (int rc = fj.begin(st, serial ? 1 : used.size())) return rc;
             for (int k = 0; k < n_bk; ++k) {
                 const int b = used[k];
                 p.adp_pad = adps->pad[b];

@@ -943,6 +943,7 @@ struct State {
     int64_t vcap = 0;
     int shrink = 0;                               // tests: the next seeding runs with 1 raw-hit slab entry (1)
                                                   // and / or 1 inside task per class (2), see shrink_next()
+    bool serial = false;                          // the next seeding's band launches all on the caller's stream
     VerOut ver{nullptr, nullptr, nullptr, 0};     // the band launches' record target (list nullptr: off)
 };
 
@@ -1250,6 +1251,13 @@ int launch_bands(State *s, const uint8_t *codes, const int64_t *v_off, const int
         SD_TRY(hipEventCreateWithFlags(&s->join, hipEventDisableTiming));
         SD_TRY(hipEventCreateWithFlags(&s->join2, hipEventDisableTiming));
     }
+    if (s->serial) {
+        // a small round (serial_next): the fork / join events cost more than the side streams gain
+        s->serial = false;
+        for (int k = 0; k < kCls; ++k)
+            if (int rc = launch_band(s, s->band[k], k, codes, v_off, v_len, sc, n, in_of(k), edge_of(k), st, st)) return rc;
+        return 0;
+    }
     // class 0's inside tasks on `st`, class 1's on a side stream, the (few, latency-bound) edge tasks
     // of both on a second side stream: the three run side by side (atomicMax into one bound array)
     SD_TRY(hipEventRecord(s->fork, st));
@@ -1528,6 +1536,9 @@ int seg_positions() { return kSeg; }
 // (bits & 1) and / or its inside-task regions (bits & 2) shrunk to one entry, so its kernels overflow
 // for real and flag the round; the buffers keep their sizes.
 void shrink_next(State *s, int bits) { s->shrink = bits & 3; }
+
+// The next queued seeding launches its band classes one after the other on the caller's stream.
+void serial_next(State *s) { s->serial = true; }
 
 // The candidate windows' certificate bounds per adapter (plan(): INT32_MAX = never certified).
 void cert_bounds(State *s, std::vector<int32_t> &U) { U = s->ucert; }
