@@ -1275,6 +1275,20 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
     _lib.check(L.pcabi_dev_copy_async(t_len.ctypes.data_as(vp), d_tlen_mid, 4 * n, 1, stream), 'd2h')
     _lib.check(L.pcabi_stream_sync(stream), 'sync')
 
+    # one more step (untimed) with the scan's per-phase profile on: every queued round synchronised
+    # on its own, events around its phases, the units they processed -> per-kernel roofline
+    phases = None
+    if rank == 0:
+        prof = np.zeros(15, np.float64)
+        timed = dict(stats)
+        rc = int(L.pcabi_scan_profile(scan, 1, None, 0))
+        if rc >= 0:
+            step()
+            rc = int(L.pcabi_scan_profile(scan, 0, prof.ctypes.data_as(vp), 15))
+        if rc < 0:
+            _lib.check(rc, 'profile')
+        stats.update(timed)
+        phases = middle_phase_roofline(prof)
     checked = None
     if args.check and rank == 0:
         checked = middle_spot_check(reads, trims, hits, stats['hits'], mid_adps, sc, args.middle_threshold,
@@ -1310,10 +1324,45 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
             'cpu_baseline': cpu,
             'gpu_vs_cpu': round(value / cpu['value'], 1) if cpu else None,
             'parity_spot_check': checked,
+            'middle_phases': phases,
             'setup_s': round(gen_s, 2),
         }
         return out
     return None
+
+
+def middle_phase_roofline(prof):
+    """pcabi_scan_profile's table (include/pcabi.h) -> per-phase time and, for the kernels with an
+    algorithmic unit, their roofline (one profiled step: every queued round synchronised on its own):
+      k_seed_scan   HBM: every base of the round's reads once (u8 codes) + 16 B per raw seed hit written;
+      k_seed_expand HBM: 16 B per raw hit read + 16 B per band task written;
+      candidate DP  VALU: cells (chunk columns x adapter rows) x OPS_PER_CELL int32 lane-ops.
+    The band classes exit early per task (data-dependent work): time and tasks only; k_cands, the
+    plan kernels and the rest (views, merges, masks: latency-bound launches): time only."""
+    names = ['k_seed_scan', 'k_seed_expand', 'bands', 'k_cands', 'plan', 'candidate_dp', 'rest']
+    ms = {k: float(prof[i]) for i, k in enumerate(names)}
+    rounds, reads, bases, raw, b_in, b_edge, dp_tasks, dp_cells = (int(x) for x in prof[7:15])
+    out = {'ms': {k: round(v, 4) for k, v in ms.items()}, 'rounds': rounds, 'reads_scanned': reads,
+           'bases_scanned': bases, 'raw_seed_hits': raw, 'band_tasks': {'inside': b_in, 'edge': b_edge},
+           'dp_tasks': dp_tasks, 'dp_cells': dp_cells, 'roofline': {}}
+
+    def hbm(nbytes, t_ms, per_unit):
+        if t_ms <= 0:
+            return None
+        gbs = nbytes / (t_ms * 1e-3) / 1e9
+        return {'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                'frac': round(gbs / HBM_PEAK_GBS, 4), 'algorithmic_bytes': int(nbytes), 'per_unit': per_unit}
+    out['roofline']['k_seed_scan'] = hbm(bases + 16 * raw, ms['k_seed_scan'],
+                                         '1 B per base scanned + 16 B per raw hit written')
+    out['roofline']['k_seed_expand'] = hbm(16 * raw + 16 * (b_in + b_edge), ms['k_seed_expand'],
+                                           '16 B per raw hit read + 16 B per band task written')
+    if ms['candidate_dp'] > 0:
+        tops = dp_cells * OPS_PER_CELL / (ms['candidate_dp'] * 1e-3) / 1e12
+        out['roofline']['candidate_dp'] = {'bound': 'valu', 'achieved': round(tops, 3),
+                                           'peak': round(VALU_PEAK_TOPS, 1), 'unit': 'T int32 lane-ops/s',
+                                           'frac': round(tops / VALU_PEAK_TOPS, 4),
+                                           'per_unit': '%d ops per cell (SURVEY.md §8d)' % OPS_PER_CELL}
+    return out
 
 
 def run_compat(args, rank, world, dist, torch, L, _lib):

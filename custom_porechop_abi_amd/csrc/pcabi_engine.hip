@@ -29,6 +29,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 #include "../../include/pcabi.h"
@@ -734,6 +735,41 @@ __global__ __launch_bounds__(256) void k_merge_reset(unsigned long long *best, c
     }
 }
 
+// Profile counters (pcabi_scan_profile): a round's reads and bases, and a plan's tasks and DP cells
+// (columns x adapter rows; a whole-window task, chunk (0, 0, 0, 0), computes its window).
+__global__ __launch_bounds__(256) void k_prof_round(const int32_t *v_len, const int32_t *n_dev, unsigned long long *out) {
+    const int64_t n = *n_dev;
+    unsigned long long b = 0;
+    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256) b += (uint32_t)v_len[k];
+    for (int d = 32; d > 0; d >>= 1) b += __shfl_xor(b, d);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&out[1], b);
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&out[0], (unsigned long long)n);
+}
+
+__global__ __launch_bounds__(256) void k_prof_cells(const int32_t *tw, const int4 *tck, const int32_t *tcand,
+                                                    const int64_t *cand, const int32_t *v_len, const int32_t *alen,
+                                                    const int64_t *slots_dev, unsigned long long *out) {
+    const int64_t ns = *slots_dev;
+    unsigned long long t = 0, c = 0;
+    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < ns; q += (int64_t)gridDim.x * 256) {
+        const int32_t k = tw[q];
+        if (k < 0) continue;
+        const int4 ck = tck[q];
+        const int32_t a = (int32_t)(cand[tcand[q]] >> 32);
+        const int cols = (ck.x | ck.y | ck.z | ck.w) ? ck.y : v_len[k];
+        t += 1;
+        c += (unsigned long long)cols * (uint32_t)alen[a];
+    }
+    for (int d = 32; d > 0; d >>= 1) {
+        t += __shfl_xor(t, d);
+        c += __shfl_xor(c, d);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&out[2], t);
+        atomicAdd(&out[3], c);
+    }
+}
+
 // The device plan's layout (device_plan_hits' host part, on the device, one block): per bucket
 // the longest chunk length whose waves reach `target` (else the shortest), every adapter's wave
 // offset (buckets in order, a bucket's adapters in order, one adapter per wave), the wave ->
@@ -1161,7 +1197,33 @@ const int64_t *seg_cum_dev(State *s);
 int seg_positions();
 void cert_bounds(State *s, std::vector<int32_t> &U);
 int debug_counts(State *s, int64_t (&out)[5], hipStream_t st);
+void profile_events(State *s, hipEvent_t *ev);
+int profile_counts(State *s, int64_t (&out)[3], hipStream_t st);
 }  // namespace pcabi_seed
+
+// Per-phase profile of the device-resident middle scan (pcabi_scan_profile): events around the
+// phases of every queued round, which is then synchronised on its own (a diagnostic pass, never
+// the timed one), and the algorithmic units the rounds processed (profile kernels, counters).
+enum MidPhase { kPhScan, kPhExpand, kPhBands, kPhCands, kPhPlan, kPhDp, kPhOther, kPhases };
+struct MidProf {
+    bool on = false;
+    std::vector<hipEvent_t> pool;
+    size_t used = 0;
+    std::vector<std::tuple<int, hipEvent_t, hipEvent_t>> spans;   // this round's (phase, from, to)
+    double ms[kPhases] = {};
+    int64_t rounds = 0, reads = 0, bases = 0, raw = 0, band_in = 0, band_edge = 0, dp_tasks = 0, dp_cells = 0;
+    hipEvent_t get() {
+        if (used == pool.size()) {
+            hipEvent_t e = nullptr;
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            pool.push_back(e);
+        }
+        return pool[used++];
+    }
+    ~MidProf() {
+        for (hipEvent_t e : pool) (void)hipEventDestroy(e);
+    }
+};
 
 struct pcabi_scan {
     const pcabi_adapters *adps = nullptr;
@@ -1180,6 +1242,8 @@ struct pcabi_scan {
     double last_mean = 0.0;                         // the previous call's mean read length (round 1)
     int64_t q_slots_cap = 0;
     std::vector<int32_t> h_ucert;                   // the certificate bounds last uploaded to pucert
+    MidProf prof;                                   // pcabi_scan_profile
+    DeviceBuf pprof;                                // its device counters (4 x u64)
 };
 
 namespace {
@@ -1981,7 +2045,7 @@ void pcabi_scan_destroy(pcabi_scan *s) {
                          &s->pspan, &s->ptasks, &s->pfill, &s->pwoff, &s->pcidx, &s->pcand, &s->pbest, &s->phit, &s->phb,
                          &s->plist, &s->pcnt, &s->q_cur, &s->q_start, &s->q_list, &s->q_n, &s->q_flags,
                          &s->q_bk, &s->q_wave, &s->q_misc, &s->pcbase, &s->plen, &s->tw2, &s->to2, &s->tck2,
-                         &s->pcand2, &s->wa2, &s->pres2, &s->pcert, &s->pucert, &s->q_bk2, &s->q_misc2})
+                         &s->pcand2, &s->wa2, &s->pres2, &s->pcert, &s->pucert, &s->q_bk2, &s->q_misc2, &s->pprof})
         if (b->p) (void)hipFree(b->p);
     if (s->h_stage) (void)hipHostFree(s->h_stage);
     if (s->h_ctl) (void)hipHostFree(s->h_ctl);
@@ -2666,6 +2730,30 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
         const bool first = r == 0 && round_base == 0;  // round 1: the windows themselves
         const int32_t *start = first ? nullptr : start_of(r);
         const int32_t *cur = first ? nullptr : cur_of(r);
+        MidProf &pf_ = sc->prof;                       // pcabi_scan_profile: marks of this round
+        hipEvent_t pr_begin = nullptr, pr_seed[4] = {};
+        if (pf_.on) {
+            pf_.used = 0;
+            pf_.spans.clear();
+            if (int rc = sc->pprof.ensure(64)) return rc;
+            HIP_TRY(hipMemsetAsync(sc->pprof.p, 0, 32, st));
+            pr_begin = pf_.get();
+            for (auto &e : pr_seed) e = pf_.get();
+            if (!pr_begin || !pr_seed[3]) return fail(PCABI_E_DEVICE, "profile events");
+            HIP_TRY(hipEventRecord(pr_begin, st));
+            pcabi_seed::profile_events(sc->seed, pr_seed);
+        }
+        struct SeedMarksOff {                          // the seed state never keeps this frame's events
+            pcabi_seed::State *s;
+            ~SeedMarksOff() { pcabi_seed::profile_events(s, nullptr); }
+        } seed_marks_off{sc->seed};
+        auto pmark = [&](int phase, hipEvent_t from) -> hipEvent_t {   // a span from `from` to now
+            if (!pf_.on) return nullptr;
+            hipEvent_t e = pf_.get();
+            if (!e || hipEventRecord(e, st) != hipSuccess) return nullptr;
+            if (phase >= 0 && from) pf_.spans.emplace_back(phase, from, e);
+            return e;
+        };
         hipLaunchKernelGGL(k_round_views, dim3(first ? 1 : gn), dim3(256), 0, st, win_off, win_len, cur, nr,
                            (int64_t *)sc->soff.p, (int32_t *)sc->slen.p, d_n + r + 1, d_pflag, (int32_t *)sc->ptasks.p,
                            (int32_t *)sc->pfill.p, n_adp);
@@ -2680,6 +2768,14 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
         if (int rc = pcabi_seed::bounds_dev(sc->seed, codes, v_off, v_len, n, nr, n_adp, scr, &dcand, &dcount, &sflags,
                                             windows ? &vlist : nullptr, &vcount, &pmap, &vcap, st))
             return rc;
+        if (pf_.on) {
+            pf_.spans.emplace_back(kPhScan, pr_seed[0], pr_seed[1]);
+            pf_.spans.emplace_back(kPhExpand, pr_seed[1], pr_seed[2]);
+            pf_.spans.emplace_back(kPhBands, pr_seed[2], pr_seed[3]);
+            (void)pmark(kPhCands, pr_seed[3]);
+            hipLaunchKernelGGL(k_prof_round, dim3(64), dim3(256), 0, st, v_len, nr,
+                               (unsigned long long *)sc->pprof.p);
+        }
         const int64_t ncap = n * (int64_t)n_adp;
         // one candidate-DP plan into a set of task slots: WIN = the verified seeds' windows, else the
         // candidates' whole-read chunks (cmask != nullptr: only the candidates it flags)
@@ -2695,6 +2791,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
             if (int rc = pl.cand->ensure(sizeof(int32_t) * slots_cap)) return rc;
             if (int rc = pl.wa->ensure(sizeof(int32_t) * (slots_cap / 64 + 1))) return rc;
             if (int rc = pl.res->ensure(sizeof(int32_t) * PCABI_NFIELDS * (size_t)slots_cap)) return rc;
+            const hipEvent_t pr_plan = pmark(-1, nullptr);
             if (win)
                 hipLaunchKernelGGL(k_wplan_count, dim3(kGrid), dim3(256), 0, st, vlist, vcount, vcap, v_len, start,
                                    (int32_t *)sc->ptasks.p);
@@ -2721,6 +2818,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
                                    (int4 *)pl.tck->p, (int32_t *)pl.cand->p, (const int64_t *)pl.slots);
             }
             HIP_TRY(hipGetLastError());
+            const hipEvent_t pr_dp = pmark(kPhPlan, pr_plan);
             KParams p{};
             p.codes = codes;
             p.win_off = v_off;
@@ -2751,6 +2849,14 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
             }
             if (int rc = fj.end()) return rc;
             HIP_TRY(hipGetLastError());
+            if (pf_.on) {
+                (void)pmark(kPhDp, pr_dp);
+                hipLaunchKernelGGL(k_prof_cells, dim3(256), dim3(256), 0, st, (const int32_t *)pl.tw->p,
+                                   (const int4 *)pl.tck->p, (const int32_t *)pl.cand->p, dcand, v_len,
+                                   (const int32_t *)sc->plen.p, (const int64_t *)pl.slots,
+                                   (unsigned long long *)sc->pprof.p);
+                HIP_TRY(hipGetLastError());
+            }
             return 0;
         };
         const Plan pw{&sc->tw, &sc->to, &sc->tck, &sc->pcand, &sc->wa, &sc->pres, d_bk_waves, d_slots, d_need};
@@ -2809,6 +2915,31 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
                          "%lld candidates, %lld task slots, %d hits\n", (long long)(round_base + r), rn[0],
                          (long long)c[0], (long long)c[1], (long long)c[2], (long long)c[3], (long long)c[4],
                          (long long)sl, rn[1]);
+        }
+        if (pf_.on) {                                // the round on its own: its spans and counters
+            const hipEvent_t pr_end = pmark(-1, nullptr);
+            int64_t cnt[3] = {};
+            if (int rc = pcabi_seed::profile_counts(sc->seed, cnt, st)) return rc;   // (synchronises st)
+            unsigned long long u[4] = {};
+            HIP_TRY(hipMemcpy(u, sc->pprof.p, sizeof(u), hipMemcpyDeviceToHost));
+            float tot = 0.f;
+            HIP_TRY(hipEventElapsedTime(&tot, pr_begin, pr_end));
+            double named = 0.0;
+            for (const auto &sp : pf_.spans) {
+                float ms = 0.f;
+                HIP_TRY(hipEventElapsedTime(&ms, std::get<1>(sp), std::get<2>(sp)));
+                pf_.ms[std::get<0>(sp)] += ms;
+                named += ms;
+            }
+            pf_.ms[kPhOther] += std::max(0.0, (double)tot - named);
+            pf_.rounds += 1;
+            pf_.reads += (int64_t)u[0];
+            pf_.bases += (int64_t)u[1];
+            pf_.dp_tasks += (int64_t)u[2];
+            pf_.dp_cells += (int64_t)u[3];
+            pf_.raw += cnt[0];
+            pf_.band_in += cnt[1];
+            pf_.band_edge += cnt[2];
         }
         return 0;
     };
@@ -2933,6 +3064,22 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
 }  // namespace
 
 extern "C" {
+
+int32_t pcabi_scan_profile(pcabi_scan *s, int32_t mode, double *out, int32_t n_out) {
+    if (!s || mode < 0 || mode > 2 || n_out < 0 || (n_out && !out)) return fail(PCABI_E_ARG, "bad arguments");
+    MidProf &p = s->prof;
+    if (mode == 1) {
+        std::fill(p.ms, p.ms + kPhases, 0.0);
+        p.rounds = p.reads = p.bases = p.raw = p.band_in = p.band_edge = p.dp_tasks = p.dp_cells = 0;
+    }
+    if (mode != 2) p.on = mode == 1;
+    const double v[kPhases + 8] = {p.ms[0], p.ms[1], p.ms[2], p.ms[3], p.ms[4], p.ms[5], p.ms[6],
+                                   (double)p.rounds, (double)p.reads, (double)p.bases, (double)p.raw,
+                                   (double)p.band_in, (double)p.band_edge, (double)p.dp_tasks, (double)p.dp_cells};
+    const int32_t k = std::min<int32_t>(n_out, kPhases + 8);
+    for (int32_t i = 0; i < k; ++i) out[i] = v[i];
+    return kPhases + 8;
+}
 
 int64_t pcabi_middle_requeues(int32_t *flags_seen) {
     if (flags_seen) *flags_seen = g_requeue_flags.load();

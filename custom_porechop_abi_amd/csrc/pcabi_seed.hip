@@ -944,6 +944,7 @@ struct State {
     int shrink = 0;                               // tests: the next seeding runs with 1 raw-hit slab entry (1)
                                                   // and / or 1 inside task per class (2), see shrink_next()
     bool serial = false;                          // the next seeding's band launches all on the caller's stream
+    hipEvent_t *pev = nullptr;                    // profile (profile_events): 4 marks recorded on the caller's stream
     VerOut ver{nullptr, nullptr, nullptr, 0};     // the band launches' record target (list nullptr: off)
 };
 
@@ -1351,8 +1352,11 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
     }
     hipLaunchKernelGGL(k_bound_reset, dim3(1024), dim3(256), 0, st, (int32_t *)s->bound.p, n, n_dev, n_adp, A.cnt,
                        kCnt + 1, (unsigned long long *)s->ccnt.p);
+    if (s->pev) SD_TRY(hipEventRecord(s->pev[0], st));
     hipLaunchKernelGGL(k_seed_scan, dim3(grid), dim3(256), 4 * (size_t)A.bits_dw + 4, st, A);
+    if (s->pev) SD_TRY(hipEventRecord(s->pev[1], st));
     hipLaunchKernelGGL(k_seed_expand, dim3(s->expand_blocks), dim3(256), s->lds_bytes, st, A);
+    if (s->pev) SD_TRY(hipEventRecord(s->pev[2], st));
     SD_TRY(hipGetLastError());
     if (tasks) return 0;                                // the caller launches the bands (host counts)
     return launch_bands(s, codes, v_off, v_len, sc, n, nullptr, st);
@@ -1505,6 +1509,7 @@ int bounds_dev(State *s, const uint8_t *codes, const int64_t *v_off, const int32
         s->ver = VerOut{(int4 *)s->vseed.p, (int32_t *)s->cnt.p + kVer, (int32_t *)s->cnt.p + kFlag + 1, s->vcap};
     }
     if (int rc = enqueue_seeds(s, codes, v_off, v_len, n, n_dev, n_adp, sc, nullptr, st)) return rc;
+    if (s->pev) SD_TRY(hipEventRecord(s->pev[3], st));   // the band classes joined
     const int64_t tot = n * (int64_t)n_adp;
     if (s->ccap < tot) s->ccap = tot;
     if (int rc = s->cands.ensure(sizeof(int64_t) * (size_t)s->ccap)) return rc;
@@ -1539,6 +1544,24 @@ void shrink_next(State *s, int bits) { s->shrink = bits & 3; }
 
 // The next queued seeding launches its band classes one after the other on the caller's stream.
 void serial_next(State *s) { s->serial = true; }
+
+// Profiling (pcabi_scan_profile): the next seedings record ev[0] before k_seed_scan, ev[1] after it,
+// ev[2] after k_seed_expand and ev[3] after the band classes (nullptr: off).
+void profile_events(State *s, hipEvent_t *ev) { s->pev = ev; }
+
+// Profiling: the last seeding's raw hits (slabs, clamped), inside and edge band tasks (synchronises `st`).
+int profile_counts(State *s, int64_t (&out)[3], hipStream_t st) {
+    std::vector<int32_t> raw((size_t)std::max(1, s->scan_blocks));
+    int32_t c[kCnt] = {};
+    SD_TRY(hipMemcpyAsync(raw.data(), s->rawcnt.p, 4 * raw.size(), hipMemcpyDeviceToHost, st));
+    SD_TRY(hipMemcpyAsync(c, s->cnt.p, sizeof(c), hipMemcpyDeviceToHost, st));
+    SD_TRY(hipStreamSynchronize(st));
+    out[0] = 0;
+    for (int32_t x : raw) out[0] += x;
+    out[1] = (int64_t)std::min<int64_t>(c[0], s->cap) + std::min<int64_t>(c[1], s->cap);
+    out[2] = (int64_t)std::min<int64_t>(c[kCls], s->ecap) + std::min<int64_t>(c[kCls + 1], s->ecap);
+    return 0;
+}
 
 // The candidate windows' certificate bounds per adapter (plan(): INT32_MAX = never certified).
 void cert_bounds(State *s, std::vector<int32_t> &U) { U = s->ucert; }

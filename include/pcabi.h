@@ -301,6 +301,13 @@ int pcabi_first_hit_dev(const int32_t *res, int64_t stride, int64_t n_win, int32
  *                                 (1 raw hits, 2 band tasks, 4 task slots). Test knobs:
  *                                 PCABI_MIDDLE_INIT_CAPS="raw,task,slots" sizes a new scan's buffers,
  *                                 PCABI_MIDDLE_FAULT="round:bits,..." shrinks one round's buffers.
+ *   pcabi_scan_profile          : per-phase profile of this scan's device rounds (a diagnostic: with
+ *                                 it on, every queued round is synchronised on its own). mode 1 =
+ *                                 reset and on, 0 = off, 2 = read only; out[0..14] (n_out values at
+ *                                 most): ms of k_seed_scan, k_seed_expand, the band classes, k_cands,
+ *                                 the plan kernels, the candidate DP, the rest; then rounds, reads,
+ *                                 bases scanned, raw seed hits, inside / edge band tasks, candidate-DP
+ *                                 tasks and cells (columns x adapter rows). Returns 15 or < 0.
  */
 typedef struct pcabi_scan pcabi_scan;
 int pcabi_scan_create(const pcabi_adapters *adps, pcabi_scan **out);
@@ -317,6 +324,7 @@ int64_t pcabi_middle_scan_host(int device, const uint8_t *codes, int64_t codes_l
                                int64_t cap);
 int64_t pcabi_middle_seed_runs(void);
 int64_t pcabi_middle_requeues(int32_t *flags_seen);
+int32_t pcabi_scan_profile(pcabi_scan *s, int32_t mode, double *out, int32_t n_out);
 
 /*
  * Adapter-set discovery reduction (porechop_abi/nanopore_read.py:158-173): for each adapter a

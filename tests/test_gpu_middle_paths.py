@@ -201,7 +201,8 @@ def _pid6(m, l):
 @pytest.mark.parametrize('require_two', [False, True])
 def test_barcode_call_96_sets_random_scores(gpu_lib, require_two):
     """SQK-NSK007 + 96 forward barcode sets + a few reverse ones (ignored by the call) and repeated
-    names: 100+ slots per side, tie-heavy identities drawn from few (m, l2) values."""
+    names (104 adapters per side, 96 slots: a repeated name's slot takes its last position),
+    tie-heavy identities drawn from few (m, l2) values."""
     from custom_porechop_abi_amd import adapters as A, engine
     from custom_porechop_abi_amd.nanopore_read import NanoporeRead
     from custom_porechop_abi_amd.porechop_abi import barcode_slots
@@ -217,15 +218,23 @@ def test_barcode_call_96_sets_random_scores(gpu_lib, require_two):
         for _ in range(2):
             sets = nsk + fwd + rev + rng.sample(fwd, 3)          # 104 slots, three names twice
             rng.shuffle(sets)
-            ms = [rng.randint(10, 24) for _ in range(5)]
+            ms = [rng.randint(10, 21) for _ in range(5)]
             res = np.zeros((8, len(sets) * n_read), np.int32)
             res[0] = np.where(np.array([rng.random() for _ in range(res.shape[1])]) < 0.05, -1, 3)
             res[5] = np.array([rng.choice(ms) for _ in range(res.shape[1])], np.int32)
             res[7] = 24
+            for r in range(n_read):                                  # most reads: one clear best slot
+                if rng.random() < 0.7:
+                    k = rng.randrange(len(sets)) * n_read + r
+                    res[0, k], res[5, k] = 3, 24
             sides.append((sets, res))
         ids = {}
         slots = [barcode_slots(s, 'forward', ids) for s, _ in sides]
-        assert len(slots[0][0]) >= 99 and len(slots[1][0]) >= 99
+        assert len(slots[0][0]) == 96 and len(slots[1][0]) == 96
+        for (sets, _), (adp, _) in zip(sides, slots):           # repeated names -> their later table index
+            last = {a.get_barcode_name(): k for k, a in enumerate(sets)
+                    if a.is_barcode() and a.barcode_direction() == 'forward'}
+            assert sorted(adp.tolist()) == sorted(last.values())
         names = {v: k for k, v in ids.items()}
         thr, diff = rng.choice([50.0, 75.0]), rng.choice([0.0, 5.0])
         call = engine.barcode_call(sides[0][1], sides[1][1], slots[0], slots[1], n_read, thr, diff, require_two)
