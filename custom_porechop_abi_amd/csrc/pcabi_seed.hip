@@ -211,7 +211,7 @@ __device__ __forceinline__ ReadMeta read_meta(const ScanArgs &a, int64_t r, int6
 // disturbs the codes of windows that contain it, and those are masked.)
 // Hits are appended to the block's slab as before: (read, position | kSlowBit, its clean 8-mer |
 // valid run << 16, read length - position).
-__global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
+__global__ __launch_bounds__(256) void k_seed_scan_bits(ScanArgs a) {
     // dynamic LDS: the bitmaps from byte 0 (so a word's address is one mask away from the code),
     // then the slab counter
     extern __shared__ uint32_t lds[];
@@ -361,6 +361,208 @@ __global__ __launch_bounds__(256) void k_seed_scan(ScanArgs a) {
 #pragma unroll
         for (int t = 0; t < 10; ++t) sa.d[t] = sb.d[t] = 0x04040404u;
         sb.rd = sb.off = 0;
+        sb.p = sb.len = 0;
+        sb.act = false;
+        int64_t b = lo;
+        issue(b, sa);
+        while (b < hi) {                               // wave-uniform
+            issue(b + 64, sb);
+            process(sa);
+            b += 64;
+            if (b >= hi) break;
+            issue(b + 64, sa);
+            process(sb);
+            b += 64;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        a.raw_cnt[blockIdx.x] = min(s_cnt, a.slab);
+        if (s_cnt > a.slab) atomicOr(&a.flags[0], 1);
+    }
+}
+
+// k_seed_scan (r04): the same segment walk, hit masks and slab records as k_seed_scan_bits (the
+// r03 kernel, PCABI_SEED_BYTEMAP=0), with the per-position work cut from 6 VALU instructions to 2:
+//   * the merged 8-mer bitmap is expanded into a BYTE map in LDS (64 KiB: byte c = bit c), so a
+//     position's lookup is one ds_read_u8 at its 8-mer code, and the byte shifts straight into the
+//     hit mask (no word address, no bit shift);
+//   * a lane's 40 bytes are packed once into 2-bit codes, base 0 in the top bits (P0 = bases 0-15,
+//     Q0 = 8-23, P1 = 16-31, Q1 = 24-39): position i's code is one bit-field extract of one of them;
+//   * a hit's 8-mer comes from the same packed words (no re-read of the read bytes).
+// 512-thread blocks: two blocks (16 waves) per CU share the CU's LDS between their byte maps.
+constexpr int kScanThreads = 512;
+constexpr int kByteMap = 1 << 16;            // bytes: one per 8-mer code
+constexpr int kScanLds = kByteMap + 16;      // + the slab counter
+
+__device__ __forceinline__ uint32_t lds_byte(uint32_t byte_addr) {
+    return *reinterpret_cast<const __attribute__((address_space(3))) uint8_t *>((size_t)byte_addr);
+}
+
+// 4 bytes (base codes in their low 2 bits) -> 8 bits, byte 0's base in the top two: in the low byte
+__device__ __forceinline__ uint32_t pack4(uint32_t d) {
+    const uint32_t t = d & 0x03030303u;
+    const uint32_t v = (t << 2) | (t >> 8);          // byte 0: b0 b1, byte 2: b2 b3
+    return (v << 4) | (v >> 16);                     // byte 0: b0 b1 b2 b3
+}
+// four packed bytes (low bytes of x0..x3) -> one word, x0 in the top byte
+__device__ __forceinline__ uint32_t pack16(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
+    const uint32_t hi = __builtin_amdgcn_perm(x0, x1, 0x0C0C0400u);   // byte 1: x0, byte 0: x1
+    const uint32_t lo = __builtin_amdgcn_perm(x2, x3, 0x0C0C0400u);
+    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_seed_scan(ScanArgs a) {
+    // dynamic LDS: the byte map from byte 0 (a position's code is its address), then the slab counter
+    extern __shared__ uint32_t lds[];
+    int &s_cnt = *reinterpret_cast<int *>(lds + kByteMap / 4);
+    for (int w = threadIdx.x; w < kByteMap / 32; w += kScanThreads) {    // bitmap word w -> 8 map dwords
+        const uint32_t word = a.tabs[w];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) lds[w * 8 + k] = (((word >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
+    }
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    const int64_t nr = dev_count(a.n_dev, a.n);
+    const int64_t S = rfl64(a.seg_cum[nr]);
+    const int lane = (int)(threadIdx.x & 63);
+    constexpr int kW = kScanThreads / 64;
+    const int64_t nw = (int64_t)gridDim.x * kW;
+    const int64_t gw = (int64_t)blockIdx.x * kW + (threadIdx.x >> 6);
+    const int64_t lo = S * gw / nw, hi = S * (gw + 1) / nw;
+    uint4 *slab = a.raw + (int64_t)blockIdx.x * a.slab;
+    if (lo < hi) {
+        int64_t ra = 0, rb = nr;
+        while (rb - ra > 1) {
+            const int64_t step = (rb - ra + 63) / 64;
+            const int64_t idx = ra + (int64_t)lane * step;
+            const bool le = idx < rb && a.seg_cum[idx] <= lo;
+            const int c = __popcll(__ballot(le));
+            ra = rfl64(ra + (int64_t)(c - 1) * step);
+            rb = rfl64(min(rb, ra + step));
+        }
+        int64_t rc = ra, s0c = rfl64(a.seg_cum[ra]);
+        ReadMeta mc = read_meta(a, rc, nr, S), mn = read_meta(a, rc + 1, nr, S);
+        auto advance = [&](int64_t b) {
+            while (b >= mc.s1) {
+                ++rc;
+                s0c = mc.s1;
+                mc = mn;
+                mn = read_meta(a, rc + 1, nr, S);
+            }
+        };
+        auto map = [&](int64_t b, int64_t &r, int &p, int64_t &off, int &len) -> bool {
+            const int64_t sg = b + lane;
+            if (sg >= hi) return false;
+            if (sg < mc.s1) {
+                r = rc; p = (int)(sg - s0c) * kSeg; off = mc.off; len = mc.len;
+            } else if (sg < mn.s1) {
+                r = rc + 1; p = (int)(sg - mc.s1) * kSeg; off = mn.off; len = mn.len;
+            } else {
+                r = rc + 2;
+                int64_t e = a.seg_cum[r + 1];
+                while (e <= sg) e = a.seg_cum[++r + 1];
+                p = (int)(sg - a.seg_cum[r]) * kSeg;
+                off = a.v_off[r];
+                len = a.v_len[r];
+            }
+            return true;
+        };
+        auto fetch = [&](int64_t off, int p, int len, uint32_t (&d)[10]) {
+            const uint32_t *q = reinterpret_cast<const uint32_t *>(a.codes + off + p);
+            const uint32_t *q1 = p + 16 <= len ? q + 4 : q;
+            const uint32_t *q2 = p + 24 <= len ? q + 8 : q;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) d[t] = q[t];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) d[4 + t] = q1[t];
+            d[8] = q2[0];
+            d[9] = q2[1];
+        };
+        struct Seg {
+            uint32_t d[10];
+            int64_t rd;
+            int p, len;
+            bool act;
+        };
+        auto issue = [&](int64_t bb, Seg &g) {
+            g.act = false;
+            if (bb >= hi) return;
+            advance(bb);
+            int64_t off = 0;
+            g.act = map(bb, g.rd, g.p, off, g.len);
+            if (g.act) fetch(off, g.p, g.len, g.d);
+        };
+        auto process = [&](const Seg &g) {
+            if (!g.act) return;
+            const uint32_t (&d)[10] = g.d;
+            const int64_t crd = g.rd;
+            const int cp = g.p, clen = g.len;
+            // ---- the segment's 32 positions: packed codes, one extract + one byte-map read each ----
+            const uint32_t P0 = pack16(pack4(d[0]), pack4(d[1]), pack4(d[2]), pack4(d[3]));
+            const uint32_t P1 = pack16(pack4(d[4]), pack4(d[5]), pack4(d[6]), pack4(d[7]));
+            const uint32_t P2 = __builtin_amdgcn_perm(pack4(d[8]), pack4(d[9]), 0x04000C0Cu);   // bases 32-39 on top
+            const uint32_t Q0 = __builtin_amdgcn_alignbit(P0, P1, 16);   // bases 8-23
+            const uint32_t Q1 = __builtin_amdgcn_alignbit(P1, P2, 16);   // bases 24-39
+            // (the reads of 16 positions issued together: LDS latency, not issue, is the risk at the
+            // 4 waves per SIMD the two byte maps leave)
+            uint32_t hits = 0;
+#pragma unroll
+            for (int h = 0; h < kSeg; h += 16) {
+                uint32_t m[16];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const int i = h + j;
+                    const uint32_t src = i < 8 ? P0 : i < 16 ? Q0 : i < 24 ? P1 : Q1;
+                    m[j] = lds_byte((src >> (16 - 2 * (i & 7))) & 0xFFFFu);
+                }
+#pragma unroll
+                for (int j = 0; j < 16; ++j) hits |= m[j] << (h + j);
+            }
+            // ---- validity: N bytes and the read end (as k_seed_scan_bits) ----
+            const int rem = clen - cp;
+            uint32_t nor = 0;
+#pragma unroll
+            for (int t = 0; t < 10; ++t) nor |= d[t];
+            uint64_t inv = 0;
+            uint32_t slow = 0;
+            if ((nor & 0x04040404u) || rem < 40) {
+#pragma unroll
+                for (int t = 0; t < 10; ++t)
+                    inv |= (uint64_t)((((d[t] >> 2) & 0x01010101u) * 0x10204080u) >> 28) << (4 * t);
+                if (rem < 64) inv |= ~0ull << rem;
+                const uint64_t t1 = inv | (inv >> 1), t2 = t1 | (t1 >> 2), t3 = t2 | (t2 >> 4);
+                const uint32_t full8 = ~(uint32_t)t3;
+                hits &= full8;
+                if (a.min_k < kMaxK) slow = ~(uint32_t)(t2 | (t2 >> (a.min_k - kMinK))) & ~full8;
+            }
+            uint32_t left = hits | slow;
+            while (__any(left != 0)) {                 // wave-uniform
+                const bool has = left != 0;
+                const uint64_t m = __ballot(has);
+                const int leader = __ffsll((unsigned long long)m) - 1;
+                int base = 0;
+                if (lane == leader) base = atomicAdd(&s_cnt, __popcll(m));
+                base = __shfl(base, leader);
+                if (has) {
+                    const int slot = base + __popcll(m & ((1ull << lane) - 1));
+                    const int i = __builtin_ctz(left);
+                    left &= left - 1;
+                    // the position's 8-mer from the packed words (N bytes read as code 0, as the
+                    // bytes' low bits; bases past a short run are not used by the expansion)
+                    const uint32_t src = i < 8 ? P0 : i < 16 ? Q0 : i < 24 ? P1 : Q1;
+                    const uint32_t c8 = (src >> (16 - 2 * (i & 7))) & 0xFFFFu;
+                    const uint32_t run = (slow >> i) & 1u ? (uint32_t)min(8, __builtin_ctzll(inv >> i)) : 8u;
+                    if (slot < a.slab)
+                        slab[slot] = make_uint4((uint32_t)crd, (uint32_t)(cp + i) | ((slow >> i) & 1u ? kSlowBit : 0u),
+                                                c8 | (run << 16), (uint32_t)(clen - (cp + i)));
+                }
+            }
+        };
+        Seg sa, sb;
+#pragma unroll
+        for (int t = 0; t < 10; ++t) sa.d[t] = sb.d[t] = 0x04040404u;
+        sb.rd = 0;
         sb.p = sb.len = 0;
         sb.act = false;
         int64_t b = lo;
@@ -936,6 +1138,7 @@ struct State {
     int32_t n_adp = 0;
     int64_t cap = 0, ecap = 0, ccap = 0, raw_cap = 0;
     int scan_blocks = 0;                          // resident k_seed_scan blocks
+    bool bytemap = true;                          // k_seed_scan (byte map) or k_seed_scan_bits (r03)
     int expand_blocks = 0;                        // resident k_seed_expand blocks
     int pin_blocks[kCls] = {0, 0};                // resident k_seed_band_pin blocks per class
     Buf vseed;                                    // verified seeds (device rounds)
@@ -1287,7 +1490,16 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
         int dev = 0, cus = 0, per_cu = 0;
         SD_TRY(hipGetDevice(&dev));
         SD_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_scan, 256, 4 * (size_t)s->a.bits_dw + 4));
+        const char *e = std::getenv("PCABI_SEED_BYTEMAP");   // 0: the r03 bitmap scan (A/B)
+        s->bytemap = !(e && e[0] == '0');
+        if (s->bytemap) {
+            SD_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_seed_scan),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, kScanLds));
+            SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_scan, kScanThreads, kScanLds));
+        } else {
+            SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_scan_bits, 256,
+                                                                4 * (size_t)s->a.bits_dw + 4));
+        }
         s->scan_blocks = std::max(1, cus * std::max(1, per_cu));
         per_cu = 0;
         SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_expand, 256, s->lds_bytes));
@@ -1300,7 +1512,8 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
         int64_t raw = 0, task = 0;
         if (const char *e = std::getenv("PCABI_MIDDLE_INIT_CAPS"))
             if (std::sscanf(e, "%lld,%lld", (long long *)&raw, (long long *)&task) < 1) raw = task = 0;
-        if (s->raw_cap == 0) s->raw_cap = raw > 0 ? std::max<int64_t>(raw, grid) : (int64_t)grid * 4096;
+        // (the byte-map scan's blocks are twice as wide and about a third as many: 3x the slab)
+        if (s->raw_cap == 0) s->raw_cap = raw > 0 ? std::max<int64_t>(raw, grid) : (int64_t)grid * (s->bytemap ? 12288 : 4096);
         if (s->cap == 0) s->cap = task > 0 ? task : 1 << 22;
     }
     // tests (shrink_next): this seeding's buffers shrunk to nothing, restored when it is queued
@@ -1353,7 +1566,10 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
     hipLaunchKernelGGL(k_bound_reset, dim3(1024), dim3(256), 0, st, (int32_t *)s->bound.p, n, n_dev, n_adp, A.cnt,
                        kCnt + 1, (unsigned long long *)s->ccnt.p);
     if (s->pev) SD_TRY(hipEventRecord(s->pev[0], st));
-    hipLaunchKernelGGL(k_seed_scan, dim3(grid), dim3(256), 4 * (size_t)A.bits_dw + 4, st, A);
+    if (s->bytemap)
+        hipLaunchKernelGGL(k_seed_scan, dim3(grid), dim3(kScanThreads), kScanLds, st, A);
+    else
+        hipLaunchKernelGGL(k_seed_scan_bits, dim3(grid), dim3(256), 4 * (size_t)A.bits_dw + 4, st, A);
     if (s->pev) SD_TRY(hipEventRecord(s->pev[1], st));
     hipLaunchKernelGGL(k_seed_expand, dim3(s->expand_blocks), dim3(256), s->lds_bytes, st, A);
     if (s->pev) SD_TRY(hipEventRecord(s->pev[2], st));

@@ -72,9 +72,10 @@ def _sorted(h):
     return h[:, np.lexsort((np.arange(h.shape[1]), h[0]))]
 
 
-def _dev_scan(L, views, adps, sc, thr):
+def _dev_scan(L, views, adps, sc, thr, profile=None):
     """A FRESH scan through the device ABI (pcabi_adapters_create_scored, pcabi_scan_create,
-    pcabi_middle_scan_dev): its buffers are sized on this first use (PCABI_MIDDLE_INIT_CAPS)."""
+    pcabi_middle_scan_dev): its buffers are sized on this first use (PCABI_MIDDLE_INIT_CAPS).
+    profile: a float64 array of 15 that receives pcabi_scan_profile's table of the call."""
     from custom_porechop_abi_amd import _lib, engine
     vp = ctypes.c_void_p
     codes, offs, lens = views
@@ -98,12 +99,16 @@ def _dev_scan(L, views, adps, sc, thr):
         cap = 8 * len(lens) + 1024
         hits = np.zeros((6, cap), np.int32)
         h_len = np.ascontiguousarray(lens, np.int32)
+        if profile is not None:
+            assert L.pcabi_scan_profile(scan, 1, None, 0) == 15
         nh = L.pcabi_middle_scan_dev(scan, d_codes, d_off, d_len, h_len.ctypes.data_as(vp), len(lens), *sc,
                                      float(thr), hits.ctypes.data_as(vp), cap, None)
         if nh < 0:
             _lib.check(int(nh), 'pcabi_middle_scan_dev')
         assert nh <= cap
         _lib.check(L.pcabi_dev_sync(), 'sync')
+        if profile is not None:
+            assert L.pcabi_scan_profile(scan, 0, profile.ctypes.data_as(vp), 15) == 15
         return hits[:, :nh].copy()
     finally:
         if scan.value:
@@ -189,6 +194,39 @@ def test_candidate_windows_at_the_certificate_bound(gpu_lib, monkeypatch, mean_l
         monkeypatch.setenv('PCABI_MIDDLE_WINDOWS', w)
         got = engine.middle_scan(views, ADPS, SC, thr)
         assert np.array_equal(_sorted(got), exp), 'windows=%s' % w
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('thr', [90.0, 85.0])
+def test_seed_scan_bytemap_equals_bitmap_scan(gpu_lib, monkeypatch, thr):
+    """k_seed_scan (r04: the byte map, packed codes) vs k_seed_scan_bits (r03, PCABI_SEED_BYTEMAP=0)
+    on reads with N bases, reads shorter than a segment and ragged ends, at 90 % (8-mers only) and
+    85 % (probes of 5-6 bases: the short-run path): the same raw hits, band tasks and candidate-DP
+    cells per round (pcabi_scan_profile's counters) and the oracle's hits."""
+    from custom_porechop_abi_amd import engine
+    rng = random.Random(int(thr))
+    reads = _reads(31 + int(thr), 90, 3000, thr)
+    for k in range(0, len(reads), 3):                 # N runs and single Ns
+        r = list(reads[k])
+        for _ in range(rng.randint(1, 6)):
+            p = rng.randrange(len(r))
+            for q in range(p, min(len(r), p + rng.choice([1, 1, 2, 9]))):
+                r[q] = 'N'
+        reads[k] = ''.join(r)
+    reads += [a[:n] + _rand_seq(rng, m) for a in ADPS for n, m in ((len(a), 0), (len(a), 3), (len(a) - 2, 9))]
+    reads += [_rand_seq(rng, n) for n in (1, 5, 8, 31, 32, 33, 39, 40, 41)]
+    pack = engine.SeqPack(reads)
+    views = pack.views(np.zeros(len(reads), np.int64), pack.lengths)
+    exp = _sorted(oracle_lib.middle_scan_threaded(views, ADPS, SC, thr))
+    monkeypatch.setenv('PCABI_MIDDLE_SEEDS', '2')
+    prof = {}
+    for mode in ('1', '0'):
+        monkeypatch.setenv('PCABI_SEED_BYTEMAP', mode)
+        prof[mode] = np.zeros(15, np.float64)
+        got = _dev_scan(gpu_lib, views, ADPS, SC, thr, profile=prof[mode])
+        assert np.array_equal(_sorted(got), exp), 'bytemap=%s' % mode
+    assert prof['1'][10] > 0
+    assert np.array_equal(prof['1'][7:15], prof['0'][7:15]), (prof['1'][7:15], prof['0'][7:15])
 
 
 # ---- k_barcode_call at the configs[3] width ---------------------------------------------------
