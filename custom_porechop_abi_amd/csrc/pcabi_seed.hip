@@ -431,6 +431,7 @@ __global__ __launch_bounds__(kScanThreads) void k_seed_scan(ScanArgs a) {
     const int64_t gw = (int64_t)blockIdx.x * kW + (threadIdx.x >> 6);
     const int64_t lo = S * gw / nw, hi = S * (gw + 1) / nw;
     uint4 *slab = a.raw + (int64_t)blockIdx.x * a.slab;
+    const uint64_t lt_mask = (1ull << lane) - 1;
     if (lo < hi) {
         int64_t ra = 0, rb = nr;
         while (rb - ra > 1) {
@@ -536,16 +537,22 @@ __global__ __launch_bounds__(kScanThreads) void k_seed_scan(ScanArgs a) {
                 hits &= full8;
                 if (a.min_k < kMaxK) slow = ~(uint32_t)(t2 | (t2 >> (a.min_k - kMinK))) & ~full8;
             }
+            // the lane's hits go to consecutive slab slots: a wave prefix of the hit counts (one ballot
+            // per count bit that any lane has), one LDS atomic per wave and segment, then each lane
+            // writes its own (a loop of the wave's most hits per lane, usually 1-2)
             uint32_t left = hits | slow;
-            while (__any(left != 0)) {                 // wave-uniform
-                const bool has = left != 0;
-                const uint64_t m = __ballot(has);
-                const int leader = __ffsll((unsigned long long)m) - 1;
-                int base = 0;
-                if (lane == leader) base = atomicAdd(&s_cnt, __popcll(m));
-                base = __shfl(base, leader);
-                if (has) {
-                    const int slot = base + __popcll(m & ((1ull << lane) - 1));
+            const int cnt = __popc(left);
+            if (__any(cnt != 0)) {                     // wave-uniform
+                int excl = 0;
+                for (int bit = 0; bit < 6; ++bit) {    // wave-uniform
+                    if (!__any((cnt >> bit) != 0)) break;
+                    excl += __popcll(__ballot((cnt >> bit) & 1) & lt_mask) << bit;
+                }
+                const int total = __builtin_amdgcn_readlane(excl + cnt, 63);
+                int b0 = 0;
+                if (lane == 0) b0 = atomicAdd(&s_cnt, total);
+                int slot = __builtin_amdgcn_readlane(b0, 0) + excl;
+                while (left) {
                     const int i = __builtin_ctz(left);
                     left &= left - 1;
                     // the position's 8-mer from the packed words (N bytes read as code 0, as the
@@ -556,6 +563,7 @@ __global__ __launch_bounds__(kScanThreads) void k_seed_scan(ScanArgs a) {
                     if (slot < a.slab)
                         slab[slot] = make_uint4((uint32_t)crd, (uint32_t)(cp + i) | ((slow >> i) & 1u ? kSlowBit : 0u),
                                                 c8 | (run << 16), (uint32_t)(clen - (cp + i)));
+                    ++slot;
                 }
             }
         };
