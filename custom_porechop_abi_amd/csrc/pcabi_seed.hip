@@ -393,11 +393,6 @@ __global__ __launch_bounds__(256) void k_seed_scan_bits(ScanArgs a) {
 // 512-thread blocks: two blocks (16 waves) per CU share the CU's LDS between their byte maps.
 constexpr int kScanThreads = 512;
 constexpr int kByteMap = 1 << 16;            // bytes: one per 8-mer code
-constexpr int kScanLds = kByteMap + 16;      // + the slab counter
-
-__device__ __forceinline__ uint32_t lds_byte(uint32_t byte_addr) {
-    return *reinterpret_cast<const __attribute__((address_space(3))) uint8_t *>((size_t)byte_addr);
-}
 
 // 4 bytes (base codes in their low 2 bits) -> 8 bits, byte 0's base in the top two: in the low byte
 __device__ __forceinline__ uint32_t pack4(uint32_t d) {
@@ -413,14 +408,16 @@ __device__ __forceinline__ uint32_t pack16(uint32_t x0, uint32_t x1, uint32_t x2
 }
 
 __global__ __launch_bounds__(kScanThreads) void k_seed_scan(ScanArgs a) {
-    // dynamic LDS: the byte map from byte 0 (a position's code is its address), then the slab counter
-    extern __shared__ uint32_t lds[];
-    int &s_cnt = *reinterpret_cast<int *>(lds + kByteMap / 4);
+    // static LDS (a workgroup may hold more than 64 KiB of it on gfx950): the byte map -- a position's
+    // code plus the map's constant LDS address is its read address -- and the slab counter
+    __shared__ __attribute__((aligned(16))) uint32_t bmap[kByteMap / 4];
+    __shared__ int s_cnt;
     for (int w = threadIdx.x; w < kByteMap / 32; w += kScanThreads) {    // bitmap word w -> 8 map dwords
         const uint32_t word = a.tabs[w];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) lds[w * 8 + k] = (((word >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
+        for (int k = 0; k < 8; ++k) bmap[w * 8 + k] = (((word >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
     }
+    const uint8_t *bytes = reinterpret_cast<const uint8_t *>(bmap);
     if (threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
     const int64_t nr = dev_count(a.n_dev, a.n);
@@ -494,8 +491,9 @@ __global__ __launch_bounds__(kScanThreads) void k_seed_scan(ScanArgs a) {
             g.act = map(bb, g.rd, g.p, off, g.len);
             if (g.act) fetch(off, g.p, g.len, g.d);
         };
+        // every lane of the wave takes part (the hit slots are reserved with wave-wide ballots and
+        // lane 63's prefix); a lane without a segment contributes no hit
         auto process = [&](const Seg &g) {
-            if (!g.act) return;
             const uint32_t (&d)[10] = g.d;
             const int64_t crd = g.rd;
             const int cp = g.p, clen = g.len;
@@ -515,7 +513,7 @@ __global__ __launch_bounds__(kScanThreads) void k_seed_scan(ScanArgs a) {
                 for (int j = 0; j < 16; ++j) {
                     const int i = h + j;
                     const uint32_t src = i < 8 ? P0 : i < 16 ? Q0 : i < 24 ? P1 : Q1;
-                    m[j] = lds_byte((src >> (16 - 2 * (i & 7))) & 0xFFFFu);
+                    m[j] = bytes[(src >> (16 - 2 * (i & 7))) & 0xFFFFu];
                 }
 #pragma unroll
                 for (int j = 0; j < 16; ++j) hits |= m[j] << (h + j);
@@ -540,7 +538,7 @@ __global__ __launch_bounds__(kScanThreads) void k_seed_scan(ScanArgs a) {
             // the lane's hits go to consecutive slab slots: a wave prefix of the hit counts (one ballot
             // per count bit that any lane has), one LDS atomic per wave and segment, then each lane
             // writes its own (a loop of the wave's most hits per lane, usually 1-2)
-            uint32_t left = hits | slow;
+            uint32_t left = g.act ? hits | slow : 0u;
             const int cnt = __popc(left);
             if (__any(cnt != 0)) {                     // wave-uniform
                 int excl = 0;
@@ -1501,9 +1499,7 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
         const char *e = std::getenv("PCABI_SEED_BYTEMAP");   // 0: the r03 bitmap scan (A/B)
         s->bytemap = !(e && e[0] == '0');
         if (s->bytemap) {
-            SD_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_seed_scan),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, kScanLds));
-            SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_scan, kScanThreads, kScanLds));
+            SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_scan, kScanThreads, 0));
         } else {
             SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_scan_bits, 256,
                                                                 4 * (size_t)s->a.bits_dw + 4));
@@ -1575,7 +1571,7 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
                        kCnt + 1, (unsigned long long *)s->ccnt.p);
     if (s->pev) SD_TRY(hipEventRecord(s->pev[0], st));
     if (s->bytemap)
-        hipLaunchKernelGGL(k_seed_scan, dim3(grid), dim3(kScanThreads), kScanLds, st, A);
+        hipLaunchKernelGGL(k_seed_scan, dim3(grid), dim3(kScanThreads), 0, st, A);
     else
         hipLaunchKernelGGL(k_seed_scan_bits, dim3(grid), dim3(256), 4 * (size_t)A.bits_dw + 4, st, A);
     if (s->pev) SD_TRY(hipEventRecord(s->pev[1], st));

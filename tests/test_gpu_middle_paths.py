@@ -219,12 +219,13 @@ def test_seed_scan_bytemap_equals_bitmap_scan(gpu_lib, monkeypatch, thr):
     views = pack.views(np.zeros(len(reads), np.int64), pack.lengths)
     exp = _sorted(oracle_lib.middle_scan_threaded(views, ADPS, SC, thr))
     monkeypatch.setenv('PCABI_MIDDLE_SEEDS', '2')
-    prof = {}
+    prof, got = {}, {}
     for mode in ('1', '0'):
         monkeypatch.setenv('PCABI_SEED_BYTEMAP', mode)
         prof[mode] = np.zeros(15, np.float64)
-        got = _dev_scan(gpu_lib, views, ADPS, SC, thr, profile=prof[mode])
-        assert np.array_equal(_sorted(got), exp), 'bytemap=%s' % mode
+        got[mode] = _dev_scan(gpu_lib, views, ADPS, SC, thr, profile=prof[mode])
+    for mode in ('0', '1'):
+        assert np.array_equal(_sorted(got[mode]), exp), ('bytemap=%s' % mode, prof[mode][7:15], prof['0'][7:15])
     assert prof['1'][10] > 0
     assert np.array_equal(prof['1'][7:15], prof['0'][7:15]), (prof['1'][7:15], prof['0'][7:15])
 
