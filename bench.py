@@ -1279,12 +1279,12 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
     # on its own, events around its phases, the units they processed -> per-kernel roofline
     phases = None
     if rank == 0:
-        prof = np.zeros(15, np.float64)
+        prof = np.zeros(16, np.float64)
         timed = dict(stats)
         rc = int(L.pcabi_scan_profile(scan, 1, None, 0))
         if rc >= 0:
             step()
-            rc = int(L.pcabi_scan_profile(scan, 0, prof.ctypes.data_as(vp), 15))
+            rc = int(L.pcabi_scan_profile(scan, 0, prof.ctypes.data_as(vp), 16))
         if rc < 0:
             _lib.check(rc, 'profile')
         stats.update(timed)
@@ -1342,7 +1342,8 @@ def middle_phase_roofline(prof):
     names = ['k_seed_scan', 'k_seed_expand', 'bands', 'k_cands', 'plan', 'candidate_dp', 'rest']
     ms = {k: float(prof[i]) for i, k in enumerate(names)}
     rounds, reads, bases, raw, b_in, b_edge, dp_tasks, dp_cells = (int(x) for x in prof[7:15])
-    out = {'ms': {k: round(v, 4) for k, v in ms.items()}, 'rounds': rounds, 'reads_scanned': reads,
+    out = {'ms': {k: round(v, 4) for k, v in ms.items()}, 'round1_ms': round(float(prof[15]), 4),
+           'rounds': rounds, 'reads_scanned': reads,
            'bases_scanned': bases, 'raw_seed_hits': raw, 'band_tasks': {'inside': b_in, 'edge': b_edge},
            'dp_tasks': dp_tasks, 'dp_cells': dp_cells, 'roofline': {}}
 

@@ -1212,6 +1212,7 @@ struct MidProf {
     std::vector<std::tuple<int, hipEvent_t, hipEvent_t>> spans;   // this round's (phase, from, to)
     double ms[kPhases] = {};
     int64_t rounds = 0, reads = 0, bases = 0, raw = 0, band_in = 0, band_edge = 0, dp_tasks = 0, dp_cells = 0;
+    double round1_ms = 0.0;                                        // round 1's runs (whole rounds)
     hipEvent_t get() {
         if (used == pool.size()) {
             hipEvent_t e = nullptr;
@@ -2932,6 +2933,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
                 named += ms;
             }
             pf_.ms[kPhOther] += std::max(0.0, (double)tot - named);
+            if (first) pf_.round1_ms += tot;
             pf_.rounds += 1;
             pf_.reads += (int64_t)u[0];
             pf_.bases += (int64_t)u[1];
@@ -3071,14 +3073,16 @@ int32_t pcabi_scan_profile(pcabi_scan *s, int32_t mode, double *out, int32_t n_o
     if (mode == 1) {
         std::fill(p.ms, p.ms + kPhases, 0.0);
         p.rounds = p.reads = p.bases = p.raw = p.band_in = p.band_edge = p.dp_tasks = p.dp_cells = 0;
+        p.round1_ms = 0.0;
     }
     if (mode != 2) p.on = mode == 1;
-    const double v[kPhases + 8] = {p.ms[0], p.ms[1], p.ms[2], p.ms[3], p.ms[4], p.ms[5], p.ms[6],
+    const double v[kPhases + 9] = {p.ms[0], p.ms[1], p.ms[2], p.ms[3], p.ms[4], p.ms[5], p.ms[6],
                                    (double)p.rounds, (double)p.reads, (double)p.bases, (double)p.raw,
-                                   (double)p.band_in, (double)p.band_edge, (double)p.dp_tasks, (double)p.dp_cells};
-    const int32_t k = std::min<int32_t>(n_out, kPhases + 8);
+                                   (double)p.band_in, (double)p.band_edge, (double)p.dp_tasks, (double)p.dp_cells,
+                                   p.round1_ms};
+    const int32_t k = std::min<int32_t>(n_out, kPhases + 9);
     for (int32_t i = 0; i < k; ++i) out[i] = v[i];
-    return kPhases + 8;
+    return kPhases + 9;
 }
 
 int64_t pcabi_middle_requeues(int32_t *flags_seen) {

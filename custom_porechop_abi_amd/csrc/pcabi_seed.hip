@@ -409,16 +409,14 @@ __device__ __forceinline__ uint32_t pack16(uint32_t x0, uint32_t x1, uint32_t x2
 
 __global__ __launch_bounds__(kScanThreads) void k_seed_scan(ScanArgs a) {
     // static LDS (a workgroup may hold more than 64 KiB of it on gfx950): the byte map -- a position's
-    // code plus the map's constant LDS address is its read address -- and the slab counter
+    // code plus the map's constant LDS address is its read address
     __shared__ __attribute__((aligned(16))) uint32_t bmap[kByteMap / 4];
-    __shared__ int s_cnt;
     for (int w = threadIdx.x; w < kByteMap / 32; w += kScanThreads) {    // bitmap word w -> 8 map dwords
         const uint32_t word = a.tabs[w];
 #pragma unroll
         for (int k = 0; k < 8; ++k) bmap[w * 8 + k] = (((word >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
     }
     const uint8_t *bytes = reinterpret_cast<const uint8_t *>(bmap);
-    if (threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
     const int64_t nr = dev_count(a.n_dev, a.n);
     const int64_t S = rfl64(a.seg_cum[nr]);
@@ -427,7 +425,10 @@ __global__ __launch_bounds__(kScanThreads) void k_seed_scan(ScanArgs a) {
     const int64_t nw = (int64_t)gridDim.x * kW;
     const int64_t gw = (int64_t)blockIdx.x * kW + (threadIdx.x >> 6);
     const int64_t lo = S * gw / nw, hi = S * (gw + 1) / nw;
-    uint4 *slab = a.raw + (int64_t)blockIdx.x * a.slab;
+    // one slab per WAVE (its own running count: no LDS atomic), so the expansion has 8x the slabs
+    // to spread over its blocks
+    uint4 *slab = a.raw + gw * a.slab;
+    int wcnt = 0;
     const uint64_t lt_mask = (1ull << lane) - 1;
     if (lo < hi) {
         int64_t ra = 0, rb = nr;
@@ -547,9 +548,8 @@ __global__ __launch_bounds__(kScanThreads) void k_seed_scan(ScanArgs a) {
                     excl += __popcll(__ballot((cnt >> bit) & 1) & lt_mask) << bit;
                 }
                 const int total = __builtin_amdgcn_readlane(excl + cnt, 63);
-                int b0 = 0;
-                if (lane == 0) b0 = atomicAdd(&s_cnt, total);
-                int slot = __builtin_amdgcn_readlane(b0, 0) + excl;
+                int slot = wcnt + excl;
+                wcnt += total;
                 while (left) {
                     const int i = __builtin_ctz(left);
                     left &= left - 1;
@@ -583,10 +583,9 @@ __global__ __launch_bounds__(kScanThreads) void k_seed_scan(ScanArgs a) {
             b += 64;
         }
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        a.raw_cnt[blockIdx.x] = min(s_cnt, a.slab);
-        if (s_cnt > a.slab) atomicOr(&a.flags[0], 1);
+    if (lane == 0) {
+        a.raw_cnt[gw] = min(wcnt, a.slab);
+        if (wcnt > a.slab) atomicOr(&a.flags[0], 1);
     }
 }
 
@@ -1144,6 +1143,7 @@ struct State {
     int32_t n_adp = 0;
     int64_t cap = 0, ecap = 0, ccap = 0, raw_cap = 0;
     int scan_blocks = 0;                          // resident k_seed_scan blocks
+    int n_slab = 0;                               // raw-hit slabs: one per byte-map scan wave (r03 scan: per block)
     bool bytemap = true;                          // k_seed_scan (byte map) or k_seed_scan_bits (r03)
     int expand_blocks = 0;                        // resident k_seed_expand blocks
     int pin_blocks[kCls] = {0, 0};                // resident k_seed_band_pin blocks per class
@@ -1505,9 +1505,10 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
                                                                 4 * (size_t)s->a.bits_dw + 4));
         }
         s->scan_blocks = std::max(1, cus * std::max(1, per_cu));
+        s->n_slab = s->bytemap ? s->scan_blocks * (kScanThreads / 64) : s->scan_blocks;   // per wave / per block
         per_cu = 0;
         SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_expand, 256, s->lds_bytes));
-        s->expand_blocks = std::min(s->scan_blocks, std::max(1, cus * std::max(1, per_cu)));
+        s->expand_blocks = std::min(s->n_slab, std::max(1, cus * std::max(1, per_cu)));
     }
     const int grid = s->scan_blocks;
     if (s->raw_cap == 0 || s->cap == 0) {
@@ -1516,8 +1517,8 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
         int64_t raw = 0, task = 0;
         if (const char *e = std::getenv("PCABI_MIDDLE_INIT_CAPS"))
             if (std::sscanf(e, "%lld,%lld", (long long *)&raw, (long long *)&task) < 1) raw = task = 0;
-        // (the byte-map scan's blocks are twice as wide and about a third as many: 3x the slab)
-        if (s->raw_cap == 0) s->raw_cap = raw > 0 ? std::max<int64_t>(raw, grid) : (int64_t)grid * (s->bytemap ? 12288 : 4096);
+        // (4096 raw hits per r03 scan block: the same total for the byte-map scan's wave slabs)
+        if (s->raw_cap == 0) s->raw_cap = raw > 0 ? std::max<int64_t>(raw, s->n_slab) : (int64_t)std::max(grid * 4096, 1536 * 4096);
         if (s->cap == 0) s->cap = task > 0 ? task : 1 << 22;
     }
     // tests (shrink_next): this seeding's buffers shrunk to nothing, restored when it is queued
@@ -1535,7 +1536,7 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
         }
     } restore{s, cap_keep};
     if (int rc = s->raw.ensure(sizeof(uint4) * (size_t)s->raw_cap)) return rc;
-    if (int rc = s->rawcnt.ensure(4 * (size_t)grid)) return rc;
+    if (int rc = s->rawcnt.ensure(4 * (size_t)s->n_slab)) return rc;
     if (int rc = s->task.ensure(sizeof(int4) * kCls * (size_t)(s->cap + s->ecap))) return rc;
     if (int rc = s->cnt.ensure(4 * (kCnt + 1))) return rc;
     if (int rc = s->bound.ensure(sizeof(int32_t) * (size_t)n * n_adp)) return rc;
@@ -1546,8 +1547,8 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
     A.n = n;
     A.n_dev = n_dev;
     A.raw = (uint4 *)s->raw.p;
-    A.n_slab = grid;
-    A.slab = (shrink & 1) ? 1 : (int32_t)std::min<int64_t>(s->raw_cap / grid, INT32_MAX);
+    A.n_slab = s->n_slab;
+    A.slab = (shrink & 1) ? 1 : (int32_t)std::min<int64_t>(s->raw_cap / s->n_slab, INT32_MAX);
     A.raw_cnt = (int32_t *)s->rawcnt.p;
     A.cnt = (int32_t *)s->cnt.p;
     A.flags = A.cnt + kFlag;
@@ -1771,7 +1772,7 @@ void profile_events(State *s, hipEvent_t *ev) { s->pev = ev; }
 
 // Profiling: the last seeding's raw hits (slabs, clamped), inside and edge band tasks (synchronises `st`).
 int profile_counts(State *s, int64_t (&out)[3], hipStream_t st) {
-    std::vector<int32_t> raw((size_t)std::max(1, s->scan_blocks));
+    std::vector<int32_t> raw((size_t)std::max(1, s->n_slab));
     int32_t c[kCnt] = {};
     SD_TRY(hipMemcpyAsync(raw.data(), s->rawcnt.p, 4 * raw.size(), hipMemcpyDeviceToHost, st));
     SD_TRY(hipMemcpyAsync(c, s->cnt.p, sizeof(c), hipMemcpyDeviceToHost, st));

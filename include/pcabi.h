@@ -307,7 +307,8 @@ int pcabi_first_hit_dev(const int32_t *res, int64_t stride, int64_t n_win, int32
  *                                 most): ms of k_seed_scan, k_seed_expand, the band classes, k_cands,
  *                                 the plan kernels, the candidate DP, the rest; then rounds, reads,
  *                                 bases scanned, raw seed hits, inside / edge band tasks, candidate-DP
- *                                 tasks and cells (columns x adapter rows). Returns 15 or < 0.
+ *                                 tasks and cells (columns x adapter rows); out[15] = ms of round 1
+ *                                 (its runs, whole). Returns 16 or < 0.
  */
 typedef struct pcabi_scan pcabi_scan;
 int pcabi_scan_create(const pcabi_adapters *adps, pcabi_scan **out);

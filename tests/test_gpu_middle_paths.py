@@ -75,7 +75,7 @@ def _sorted(h):
 def _dev_scan(L, views, adps, sc, thr, profile=None):
     """A FRESH scan through the device ABI (pcabi_adapters_create_scored, pcabi_scan_create,
     pcabi_middle_scan_dev): its buffers are sized on this first use (PCABI_MIDDLE_INIT_CAPS).
-    profile: a float64 array of 15 that receives pcabi_scan_profile's table of the call."""
+    profile: a float64 array of 16 that receives pcabi_scan_profile's table of the call."""
     from custom_porechop_abi_amd import _lib, engine
     vp = ctypes.c_void_p
     codes, offs, lens = views
@@ -100,7 +100,7 @@ def _dev_scan(L, views, adps, sc, thr, profile=None):
         hits = np.zeros((6, cap), np.int32)
         h_len = np.ascontiguousarray(lens, np.int32)
         if profile is not None:
-            assert L.pcabi_scan_profile(scan, 1, None, 0) == 15
+            assert L.pcabi_scan_profile(scan, 1, None, 0) == 16
         nh = L.pcabi_middle_scan_dev(scan, d_codes, d_off, d_len, h_len.ctypes.data_as(vp), len(lens), *sc,
                                      float(thr), hits.ctypes.data_as(vp), cap, None)
         if nh < 0:
@@ -108,7 +108,7 @@ def _dev_scan(L, views, adps, sc, thr, profile=None):
         assert nh <= cap
         _lib.check(L.pcabi_dev_sync(), 'sync')
         if profile is not None:
-            assert L.pcabi_scan_profile(scan, 0, profile.ctypes.data_as(vp), 15) == 15
+            assert L.pcabi_scan_profile(scan, 0, profile.ctypes.data_as(vp), 16) == 16
         return hits[:, :nh].copy()
     finally:
         if scan.value:
@@ -222,7 +222,7 @@ def test_seed_scan_bytemap_equals_bitmap_scan(gpu_lib, monkeypatch, thr):
     prof, got = {}, {}
     for mode in ('1', '0'):
         monkeypatch.setenv('PCABI_SEED_BYTEMAP', mode)
-        prof[mode] = np.zeros(15, np.float64)
+        prof[mode] = np.zeros(16, np.float64)
         got[mode] = _dev_scan(gpu_lib, views, ADPS, SC, thr, profile=prof[mode])
     for mode in ('0', '1'):
         assert np.array_equal(_sorted(got[mode]), exp), ('bytemap=%s' % mode, prof[mode][7:15], prof['0'][7:15])
