@@ -990,14 +990,19 @@ bool chunkable(int b, bool packed) {
 }
 
 // Lanes per window of the row-split core (k_align_split) for a cross-mode launch of `waves`
-// waves: 1 (the one-lane core) once the launch fills 4 waves per SIMD, else 2 or 4 -- the fewest
-// that reach it (at least 2 rows per lane). PCABI_SPLIT=0 turns the split off, 2 / 4 force it.
+// waves: 4 (2 under 16 rows) for launches under 1024 waves, else 1 (the one-lane core).
+// PCABI_SPLIT=0 turns the split off, 2 / 4 force it. The split costs ~1.3-1.7x the VALU work per
+// cell (the per-step exchange and bookkeeping over R / K rows), so it pays only where a launch is
+// latency-bound on its own: r04 A/B (profiles/r04/split_ab/), a threshold of 4096 waves split the
+// headline's one-adapter buckets (1,564 waves), which run beside the other side's buckets anyway:
+// 7.78 -> 7.98 ms per step; the set search of 10k reads (156 waves per adapter) gained 2.79 ->
+// 2.53 ms.
 int split_lanes(int rpl, int64_t waves) {
     const char *e = std::getenv("PCABI_SPLIT");
     const int forced = (e && e[0]) ? std::atoi(e) : -1;
     int K = 1;
     if (forced >= 0) K = forced;
-    else if (waves < 4096) K = (2 * waves >= 4096 || rpl < 16) ? 2 : 4;
+    else if (waves < 1024) K = rpl < 16 ? 2 : 4;
     return (K == 2 || K == 4) && pcabi::split_ok(rpl, K) ? K : 1;
 }
 
