@@ -144,17 +144,22 @@ int64_t middle_plan_waves() {
 
 // ---- decision epilogues --------------------------------------------------------------------
 
+// One block per 64 reads: wave w takes adapters w, w + 4, ... of both sides (lane = read: the
+// loads of one adapter's field are 256-B coalesced), the four partial maxima meet in LDS. (r03: one
+// thread per read looped over every adapter -- 391 blocks for 100k reads, latency-bound.)
 __global__ __launch_bounds__(256) void k_end_trim(const int32_t *sres, int64_t sstride, int32_t n_sa,
                                                   const int32_t *eres, int64_t estride, int32_t n_ea,
                                                   int64_t n_read, int end_size, int extra,
                                                   double thr, int min_trim,
                                                   int32_t *start_trim, int32_t *end_trim,
                                                   uint8_t *shit, uint8_t *ehit) {
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= n_read) return;
+    __shared__ int s_st[4][64], s_et[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t r = (int64_t)blockIdx.x * 64 + lane;
+    const bool live = r < n_read;
     // find_start_trim (nanopore_read.py:175-195)
     int st = 0;
-    for (int a = 0; a < n_sa; ++a) {
+    for (int a = w; live && a < n_sa; a += 4) {
         const int64_t i = (int64_t)a * n_read + r;
         const int rs = sres[0 * sstride + i];
         int re1, hit = 0;
@@ -169,7 +174,7 @@ __global__ __launch_bounds__(256) void k_end_trim(const int32_t *sres, int64_t s
     }
     // find_end_trim (nanopore_read.py:197-217)
     int et = 0;
-    for (int a = 0; a < n_ea; ++a) {
+    for (int a = w; live && a < n_ea; a += 4) {
         const int64_t i = (int64_t)a * n_read + r;
         const int rs = eres[0 * estride + i];
         int re1, hit = 0;
@@ -182,8 +187,13 @@ __global__ __launch_bounds__(256) void k_end_trim(const int32_t *sres, int64_t s
         }
         if (ehit) ehit[i] = (uint8_t)hit;
     }
-    start_trim[r] = st;
-    end_trim[r] = et;
+    s_st[w][lane] = st;
+    s_et[w][lane] = et;
+    __syncthreads();
+    if (w == 0 && live) {
+        start_trim[r] = max(max(s_st[0][lane], s_st[1][lane]), max(s_st[2][lane], s_st[3][lane]));
+        end_trim[r] = max(max(s_et[0][lane], s_et[1][lane]), max(s_et[2][lane], s_et[3][lane]));
+    }
 }
 
 // best[a] = max(best[a], max_w pid2): one block per adapter, uint64 ordering of non-negative
@@ -3350,7 +3360,7 @@ int pcabi_end_trim_dev(const int32_t *start_res, int64_t start_stride, int32_t n
                        int32_t *start_trim, int32_t *end_trim, uint8_t *start_hit, uint8_t *end_hit,
                        void *stream) {
     if (n_read <= 0) return 0;
-    const unsigned blocks = (unsigned)((n_read + 255) / 256);
+    const unsigned blocks = (unsigned)((n_read + 63) / 64);
     hipLaunchKernelGGL(k_end_trim, dim3(blocks), dim3(256), 0, (hipStream_t)stream, start_res, start_stride,
                        n_sa, end_res, end_stride, n_ea, n_read, end_size, extra_trim, end_threshold,
                        min_trim_size, start_trim, end_trim, start_hit, end_hit);
