@@ -411,10 +411,17 @@ __global__ __launch_bounds__(kScanThreads) void k_seed_scan(ScanArgs a) {
     // static LDS (a workgroup may hold more than 64 KiB of it on gfx950): the byte map -- a position's
     // code plus the map's constant LDS address is its read address
     __shared__ __attribute__((aligned(16))) uint32_t bmap[kByteMap / 4];
-    for (int w = threadIdx.x; w < kByteMap / 32; w += kScanThreads) {    // bitmap word w -> 8 map dwords
-        const uint32_t word = a.tabs[w];
+    {   // bitmap word w -> 8 map dwords; a thread's four words loaded together
+        static_assert(kByteMap / 32 == 4 * kScanThreads, "four bitmap words per thread");
+        uint32_t word[4];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) bmap[w * 8 + k] = (((word >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
+        for (int q = 0; q < 4; ++q) word[q] = a.tabs[threadIdx.x + q * kScanThreads];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int w = threadIdx.x + q * kScanThreads;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) bmap[w * 8 + k] = (((word[q] >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
+        }
     }
     const uint8_t *bytes = reinterpret_cast<const uint8_t *>(bmap);
     __syncthreads();
@@ -655,11 +662,26 @@ __device__ __forceinline__ TaskCount expand_hit(const ScanArgs &a, const uint32_
 }
 
 __global__ __launch_bounds__(256) void k_seed_expand(ScanArgs a) {
-    extern __shared__ uint32_t lds[];
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     typedef hipcub::BlockScan<long long, 256> Scan;
     __shared__ typename Scan::TempStorage scan_tmp;
     __shared__ long long s_base[2];                      // inside / edge bases, classes packed 32 | 32
-    for (int i = threadIdx.x; i < a.tab_dw; i += 256) lds[i] = a.tabs[i];
+    {   // the probe image (up to ~60 KB): 16-B loads, four in flight per thread (a dword loop waited
+        // out one load latency per dword: ~50 us of fixed cost per launch, most of a small round's)
+        const int n4 = a.tab_dw / 4;
+        const uint4 *src = reinterpret_cast<const uint4 *>(a.tabs);
+        uint4 *dst = reinterpret_cast<uint4 *>(lds);
+        for (int i = threadIdx.x; i < n4; i += 4 * 256) {
+            uint4 v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (i + k * 256 < n4) v[k] = src[i + k * 256];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (i + k * 256 < n4) dst[i + k * 256] = v[k];
+        }
+        for (int i = 4 * n4 + (int)threadIdx.x; i < a.tab_dw; i += 256) lds[i] = a.tabs[i];
+    }
     __syncthreads();
     const uint16_t *rank = reinterpret_cast<const uint16_t *>(lds + a.rank_off);
     const uint16_t *estart = reinterpret_cast<const uint16_t *>(lds + a.estart_off);
@@ -763,12 +785,15 @@ struct ByteStream {
 // Banded score DP of one task: rows i = 1..L of the adapter, per row the 2E+1 cells of the
 // diagonals d0 - E .. d0 + E (cell x <-> read column j = i + d0 + x - E), free end gaps as the
 // full DP: S(0, j) = 0, S(i, 0) = 0, ends in row L (j < len) or in the last column (j = len).
-// CHECK: the band touches column 0 or the last column, or leaves the read.
-// Early exit (inside bands, T > 0, best_sub > 0 -- plan() requires both): no path gains more
-// than best_sub per remaining row (gaps cost), and an inside band holds no column-0 restart and
-// no last-column end, so once every cell of row i satisfies S + best_sub (L - i) < T the pair
-// cannot reach T: the DP stops and returns that bound (below T, which is all the caller
-// compares). Random probe hits -- most tasks -- stop early.
+// CHECK: the band touches column 0 or the last column, or leaves the read. Only the rows whose
+// columns reach 0 or len take the checked cells (r04: every row did, 20 k edge tasks cost ~75 us
+// per round, a tail behind the pinned bands); the other rows of an edge band are inside rows.
+// Early exit: no path gains more than best_sub per remaining row (gaps cost), so once every cell
+// of row i satisfies S + best_sub (L - i) < T -- and no later row can restart in column 0 or end in
+// the last column (always so for inside bands; for an edge band once its columns are past 0 and
+// its last row ends before len), and no last-column end so far reached T -- the pair cannot reach
+// T: the DP stops and returns a bound below T, which is all the caller compares. Random probe hits
+// -- most tasks -- stop early.
 template <int E, bool CHECK>
 __device__ __forceinline__ int band_best(const uint8_t *rd, int len, const uint8_t *ac, int L, int d0,
                                          const pcabi::Scoring &sc, int T, const uint8_t *codes) {
@@ -787,24 +812,38 @@ __device__ __forceinline__ int band_best(const uint8_t *rd, int len, const uint8
         R[x] = CHECK ? ((j1 >= 1 && j1 <= len) ? v : 7) : v;
     }
     int best = 0;                                            // S(L, 0) = 0 is always scouted
+    // an edge band: no restart after row E - d0, no last-column end when its last row stops short
+    const bool tail_inside = !CHECK || L + d0 + E < len;
     for (int i = 1; i <= L; ++i) {
         const int ab = ac[i - 1];
         int h = kNeg, sl = kNeg;                             // H, S of the cell to the left
+        const bool edge_row = CHECK && (i + d0 - E <= 0 || i + d0 + E >= len);
+        if (edge_row) {
 #pragma unroll
-        for (int x = 0; x < W; ++x) {
-            const int dg = S[x] + ((R[x] == ab) ? sc.ma : sc.mi);
-            const int vu = (x + 1 < W) ? max(V[x + 1] + sc.ge, S[x + 1] + sc.go) : kNeg;
-            h = max(h + sc.ge, sl + sc.go);
-            int s = max(dg, max(vu, h)), v = vu;
-            if (CHECK) {
+            for (int x = 0; x < W; ++x) {
+                const int dg = S[x] + ((R[x] == ab) ? sc.ma : sc.mi);
+                const int vu = (x + 1 < W) ? max(V[x + 1] + sc.ge, S[x + 1] + sc.go) : kNeg;
+                h = max(h + sc.ge, sl + sc.go);
+                int s = max(dg, max(vu, h)), v = vu;
                 const int j = i + d0 + x - E;
                 if (j == 0) { s = 0; v = kNeg; h = kNeg; }              // the adapter head hangs off
                 else if (j < 0 || j > len) { s = kNeg; v = kNeg; h = kNeg; }
                 if (j == len) best = max(best, s);                      // last column
+                S[x] = s;
+                V[x] = v;
+                sl = s;
             }
-            S[x] = s;
-            V[x] = v;
-            sl = s;
+        } else {
+#pragma unroll
+            for (int x = 0; x < W; ++x) {
+                const int dg = S[x] + ((R[x] == ab) ? sc.ma : sc.mi);
+                const int vu = (x + 1 < W) ? max(V[x + 1] + sc.ge, S[x + 1] + sc.go) : kNeg;
+                h = max(h + sc.ge, sl + sc.go);
+                const int s = max(dg, max(vu, h));
+                S[x] = s;
+                V[x] = vu;
+                sl = s;
+            }
         }
 #pragma unroll
         for (int x = 0; x + 1 < W; ++x) R[x] = R[x + 1];
@@ -813,12 +852,12 @@ __device__ __forceinline__ int band_best(const uint8_t *rd, int len, const uint8
             const int v = bs.next();
             R[W - 1] = CHECK ? ((jn >= 1 && jn <= len) ? v : 7) : v;
         }
-        if (!CHECK && (i % PCABI_BAND_EXIT) == 0) {
+        if ((i % PCABI_BAND_EXIT) == 0 && tail_inside && (!CHECK || i + d0 - E >= 0)) {
             int mx = S[0];
 #pragma unroll
             for (int x = 1; x < W; ++x) mx = max(mx, S[x]);
             const int ub = mx + pcabi::best_sub(sc) * (L - i);
-            if (ub < T) return ub;
+            if (ub < T && best < T) return max(ub, best);
         }
     }
 #pragma unroll
