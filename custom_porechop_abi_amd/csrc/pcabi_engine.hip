@@ -1264,11 +1264,16 @@ struct pcabi_scan {
 
 namespace {
 
-// Side streams of a device for the fork / join of pcabi_align_cross_dev's bucket launches.
+// Side streams of a device for the fork / join of pcabi_align_cross_dev's bucket launches. A fork
+// region takes its side streams from a rotating start, so two regions queued back to back (the
+// headline's two sides, each a cross product on its own caller stream) use different side streams
+// and their launches overlap (r04 trace: with 3 shared side streams the end side's small buckets
+// queued behind the start side's).
 struct SideStreams {
-    static constexpr int N = 3;
+    static constexpr int N = 6;
     std::mutex mu;               // one fork / join region at a time per device
     bool init = false;
+    int next = 0;                // the next region's first side stream
     hipStream_t s[N] = {};
     hipEvent_t fork = nullptr, join[N] = {};
 };
@@ -1292,13 +1297,15 @@ int side_streams(int dev, SideStreams **out) {
 }
 
 // Fork / join of independent launches: launch k runs on the caller's stream (k == 0) or on side
-// stream (k - 1) % N, each side stream first waiting for the work already queued on the caller's
-// stream; end() makes the caller's stream wait for every side stream used.
+// stream (first + k - 1) % N, each side stream first waiting for the work already queued on the
+// caller's stream; end() makes the caller's stream wait for every side stream used.
 struct ForkJoin {
     hipStream_t main = nullptr;
     SideStreams *ss = nullptr;
     std::unique_lock<std::mutex> lock;
-    int used = 0;
+    int first = 0;
+    unsigned used = 0;           // bit i: side stream i took a launch of this region
+    int n_side = 0;              // side launches of this region
     int begin(hipStream_t m, size_t n_launch) {
         main = m;
         if (n_launch <= 1) return 0;
@@ -1306,22 +1313,27 @@ struct ForkJoin {
         HIP_TRY(hipGetDevice(&dev));
         if (int rc = side_streams(dev, &ss)) return rc;
         lock = std::unique_lock<std::mutex>(ss->mu);
+        first = ss->next;
         HIP_TRY(hipEventRecord(ss->fork, main));
         return 0;
     }
     hipStream_t at(size_t k) {
         if (k == 0 || !ss) return main;
-        const int i = (int)((k - 1) % SideStreams::N);
-        if (k - 1 < (size_t)SideStreams::N) (void)hipStreamWaitEvent(ss->s[i], ss->fork, 0);
-        used = std::max(used, i + 1);
+        const int i = (int)((first + k - 1) % SideStreams::N);
+        if (!(used & (1u << i))) (void)hipStreamWaitEvent(ss->s[i], ss->fork, 0);
+        used |= 1u << i;
+        n_side = std::max(n_side, (int)k);
         return ss->s[i];
     }
     int end() {
-        for (int i = 0; i < used; ++i) {
+        for (int i = 0; i < SideStreams::N; ++i) {
+            if (!(used & (1u << i))) continue;
             HIP_TRY(hipEventRecord(ss->join[i], ss->s[i]));
             HIP_TRY(hipStreamWaitEvent(main, ss->join[i], 0));
         }
+        if (ss && n_side) ss->next = (first + n_side) % SideStreams::N;
         used = 0;
+        n_side = 0;
         if (lock.owns_lock()) lock.unlock();
         return 0;
     }
