@@ -709,14 +709,17 @@ __global__ __launch_bounds__(256) void k_hits_compact(const int32_t *hb, int64_t
 // Start of a round: views of its windows (sub[k] = window cur[k], k < n_dev; cur == nullptr: none,
 // round 1 reads the windows themselves) and the round's counters zeroed -- the next round's read
 // count, the plan flag, the plan's per-adapter task counts (n_adp x kPlanC) and fill counters.
+// n_first != nullptr (round 1): its read count, n_first_val, is written too.
 __global__ __launch_bounds__(256) void k_round_views(const int64_t *win_off, const int32_t *win_len, const int32_t *cur,
                                                      const int32_t *n_dev, int64_t *sub_off, int32_t *sub_len,
                                                      int32_t *n_next, int32_t *plan_flag, int32_t *ptasks,
-                                                     int32_t *pfill, int32_t n_adp) {
+                                                     int32_t *pfill, int32_t n_adp, int32_t *n_first,
+                                                     int32_t n_first_val) {
     if (blockIdx.x == 0) {
         if (threadIdx.x == 0) {
             *n_next = 0;
             *plan_flag = 0;
+            if (n_first) *n_first = n_first_val;
         }
         for (int i = threadIdx.x; i < n_adp * kPlanC; i += 256) ptasks[i] = 0;
         for (int i = threadIdx.x; i < n_adp; i += 256) pfill[i] = 0;
@@ -1258,6 +1261,8 @@ struct pcabi_scan {
     double last_mean = 0.0;                         // the previous call's mean read length (round 1)
     int64_t q_slots_cap = 0;
     std::vector<int32_t> h_ucert;                   // the certificate bounds last uploaded to pucert
+    std::vector<int32_t> h_up;                      // bucket tables | spans | lengths last uploaded
+    const void *up_at[3] = {nullptr, nullptr, nullptr};   // ... into these buffers
     MidProf prof;                                   // pcabi_scan_profile
     DeviceBuf pprof;                                // its device counters (4 x u64)
 };
@@ -2690,9 +2695,20 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
     std::vector<int32_t> bk_host(bk_first);
     bk_host.insert(bk_host.end(), bk_adp.begin(), bk_adp.end());
     bk_host.insert(bk_host.end(), bk_local.begin(), bk_local.end());
-    HIP_TRY(hipMemcpyAsync(sc->q_bk.p, bk_host.data(), 4 * bk_host.size(), hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(sc->pspan.p, span.data(), 4 * (size_t)n_adp, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(sc->plen.p, adps->hlen.data(), 4 * (size_t)n_adp, hipMemcpyHostToDevice, st));
+    {   // the bucket tables, spans and lengths depend on the table and scoring only: up once per
+        // change (three pageable copies cost ~20 us of every call otherwise)
+        std::vector<int32_t> key(bk_host);
+        key.insert(key.end(), span.begin(), span.end());
+        key.insert(key.end(), adps->hlen.begin(), adps->hlen.end());
+        const void *where[3] = {sc->q_bk.p, sc->pspan.p, sc->plen.p};
+        if (key != sc->h_up || std::memcmp(where, sc->up_at, sizeof(where)) != 0) {
+            HIP_TRY(hipMemcpyAsync(sc->q_bk.p, bk_host.data(), 4 * bk_host.size(), hipMemcpyHostToDevice, st));
+            HIP_TRY(hipMemcpyAsync(sc->pspan.p, span.data(), 4 * (size_t)n_adp, hipMemcpyHostToDevice, st));
+            HIP_TRY(hipMemcpyAsync(sc->plen.p, adps->hlen.data(), 4 * (size_t)n_adp, hipMemcpyHostToDevice, st));
+            sc->h_up.swap(key);
+            std::memcpy(sc->up_at, where, sizeof(where));
+        }
+    }
     double mean_len = sc->last_mean;
     if (h_win_len) {
         double tot = 0.0;
@@ -2717,8 +2733,8 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
     auto cur_of = [&](int slot) { return (int32_t *)sc->q_cur.p + (int64_t)slot * n; };
     auto start_of = [&](int slot) { return (int32_t *)sc->q_start.p + (int64_t)slot * n; };
     auto list_of = [&](int slot) { return (int32_t *)sc->q_list.p + (int64_t)slot * 8 * n; };
-    // round 1: every window (in window order: a round's results do not depend on its order)
-    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)d_n, (int)n, 1, st));   // (no host buffer to wait for)
+    // round 1: every window (in window order: a round's results do not depend on its order); its
+    // read count d_n[0] = n is written by its k_round_views
     if (sc->q_slots_cap == 0) {
         sc->q_slots_cap = std::max<int64_t>(1 << 20, 4 * n);
         long long raw = 0, task = 0, slots = 0;     // tests: PCABI_MIDDLE_INIT_CAPS="raw,task,slots"
@@ -2784,7 +2800,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
         };
         hipLaunchKernelGGL(k_round_views, dim3(first ? 1 : gn), dim3(256), 0, st, win_off, win_len, cur, nr,
                            (int64_t *)sc->soff.p, (int32_t *)sc->slen.p, d_n + r + 1, d_pflag, (int32_t *)sc->ptasks.p,
-                           (int32_t *)sc->pfill.p, n_adp);
+                           (int32_t *)sc->pfill.p, n_adp, first ? d_n : nullptr, (int32_t)n);
         const int64_t *dcand = nullptr;
         const unsigned long long *dcount = nullptr;
         const int32_t *sflags = nullptr;
