@@ -2669,8 +2669,10 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
     if (int rc = sc->q_cur.ensure(4 * (size_t)n * (kSlots + 1))) return rc;
     if (int rc = sc->q_start.ensure(4 * (size_t)n * (kSlots + 1))) return rc;
     if (int rc = sc->q_list.ensure(4 * 8 * (size_t)n * kSlots)) return rc;
-    if (int rc = sc->q_n.ensure(4 * (kSlots + 2))) return rc;
-    if (int rc = sc->q_flags.ensure(4 * (kSlots + 2))) return rc;
+    // the control block, laid out as its pinned host copy (one D2H per batch of rounds): round
+    // counts [kSlots + 2], round flags [kSlots + 2], then int64 [slots, need, plan flag, need2]
+    constexpr size_t kCtlBytes = 4 * 2 * (kSlots + 2) + 8 * 4;
+    if (int rc = sc->q_n.ensure(kCtlBytes)) return rc;
     if (int rc = sc->soff.ensure(sizeof(int64_t) * n)) return rc;
     if (int rc = sc->slen.ensure(sizeof(int32_t) * n)) return rc;
     if (int rc = sc->pspan.ensure(sizeof(int32_t) * n_adp)) return rc;
@@ -2684,7 +2686,6 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
     if (int rc = sc->pbest.ensure(sizeof(unsigned long long) * n * n_adp)) return rc;
     if (int rc = sc->pcbase.ensure(sizeof(int32_t) * n * n_adp)) return rc;
     if (int rc = sc->q_bk.ensure(4 * (bk_first.size() + 2 * bk_adp.size() + 2 * (size_t)n_bk + 16))) return rc;
-    if (int rc = sc->q_misc.ensure(64)) return rc;   // [0] slots (int64), [8] need (int64), [16] plan flag
     if (int rc = sc->q_misc2.ensure(64)) return rc;  // the second plan's slots and need
     if (int rc = sc->q_bk2.ensure(4 * (2 * (size_t)n_bk + 16))) return rc;
     if (int rc = sc->pcert.ensure(sizeof(int32_t) * n * n_adp)) return rc;
@@ -2727,9 +2728,9 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
     int32_t *d_bk_waves2 = (int32_t *)sc->q_bk2.p;
     // q_misc: [0] slots, [1] need, [2] plan flag (int32), [3] the second plan's need (read with need)
     int64_t *d_slots2 = (int64_t *)sc->q_misc2.p;
-    int64_t *d_slots = (int64_t *)sc->q_misc.p, *d_need = d_slots + 1, *d_need2 = d_slots + 3;
+    int64_t *d_slots = (int64_t *)((int32_t *)sc->q_n.p + 2 * (kSlots + 2)), *d_need = d_slots + 1, *d_need2 = d_slots + 3;
     int32_t *d_pflag = (int32_t *)(d_slots + 2);
-    int32_t *d_n = (int32_t *)sc->q_n.p, *d_rflag = (int32_t *)sc->q_flags.p;
+    int32_t *d_n = (int32_t *)sc->q_n.p, *d_rflag = d_n + (kSlots + 2);
     auto cur_of = [&](int slot) { return (int32_t *)sc->q_cur.p + (int64_t)slot * n; };
     auto start_of = [&](int slot) { return (int32_t *)sc->q_start.p + (int64_t)slot * n; };
     auto list_of = [&](int slot) { return (int32_t *)sc->q_list.p + (int64_t)slot * 8 * n; };
@@ -2989,10 +2990,10 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
         return 0;
     };
     // pinned control block: round counts [kSlots + 2], flags [kSlots + 2], need / flag word / need2
-    if (!sc->h_ctl) HIP_TRY(hipHostMalloc((void **)&sc->h_ctl, 4 * (2 * (kSlots + 2) + 8), hipHostMallocDefault));
+    if (!sc->h_ctl) HIP_TRY(hipHostMalloc((void **)&sc->h_ctl, kCtlBytes + 8, hipHostMallocDefault));
     int32_t *h_n = sc->h_ctl, *h_flag = sc->h_ctl + (kSlots + 2);
-    int64_t *h_nd = (int64_t *)(sc->h_ctl + 2 * (kSlots + 2));   // [0..2] need, flag word, need2; [3] round 1's segments
-    h_nd[3] = -1;
+    int64_t *h_nd = (int64_t *)(sc->h_ctl + 2 * (kSlots + 2));   // [0..3] as the device's; [4] round 1's segments
+    h_nd[4] = -1;
     // every queued round's first spec entries come back with the counts (one synchronisation per
     // batch of rounds instead of two); a round with more hits fetches the rest after
     const int64_t spec = std::min<int64_t>(sc->spec_hits, n);
@@ -3014,19 +3015,17 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
         for (int r = slot; r < upto; ++r) {
             if (int rc = queue_round(r)) return rc;
             if (r == 0 && round_base == 0)        // round 1's segment total (the next call's mean length)
-                HIP_TRY(hipMemcpyAsync(h_nd + 3, pcabi_seed::seg_cum_dev(sc->seed) + n, sizeof(int64_t),
+                HIP_TRY(hipMemcpyAsync(h_nd + 4, pcabi_seed::seg_cum_dev(sc->seed) + n, sizeof(int64_t),
                                        hipMemcpyDeviceToHost, st));
         }
         queued_to = upto;
-        HIP_TRY(hipMemcpyAsync(h_n, d_n, 4 * (size_t)(queued_to + 1), hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipMemcpyAsync(h_flag, d_rflag, 4 * (size_t)queued_to, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipMemcpyAsync(h_nd, d_need, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, st));   // need, flags, need2
+        HIP_TRY(hipMemcpyAsync(sc->h_ctl, d_n, kCtlBytes, hipMemcpyDeviceToHost, st));   // counts, flags, needs
         for (int r = slot; r < queued_to; ++r)
             HIP_TRY(hipMemcpyAsync(sc->h_stage + 8 * (size_t)spec * (r - slot), list_of(r), 32 * (size_t)spec,
                                    hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
-        need = h_nd[0];
-        need2 = h_nd[2];
+        need = h_nd[1];
+        need2 = h_nd[3];
         // the first flagged round (nothing of it or after it was kept): grow, queue it again
         int bad = -1;
         for (int r = slot; r < queued_to && bad < 0; ++r)
@@ -3085,7 +3084,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
     // the next call stages as many hits per round as this one's busiest round had (+ 25 %), and
     // takes its mean read length from this call's round-1 segments
     sc->spec_hits = std::max<int64_t>(4096, most_hits + most_hits / 4);
-    if (h_nd[3] >= 0 && n > 0) sc->last_mean = (double)h_nd[3] * pcabi_seed::seg_positions() / (double)n;
+    if (h_nd[4] >= 0 && n > 0) sc->last_mean = (double)h_nd[4] * pcabi_seed::seg_positions() / (double)n;
     // (round, read) order: per read the reference's discovery order
     const int64_t total = (int64_t)out_round.size();
     std::vector<int64_t> ord((size_t)total);
