@@ -789,11 +789,12 @@ struct ByteStream {
 // columns reach 0 or len take the checked cells (r04: every row did, 20 k edge tasks cost ~75 us
 // per round, a tail behind the pinned bands); the other rows of an edge band are inside rows.
 // Early exit: no path gains more than best_sub per remaining row (gaps cost), so once every cell
-// of row i satisfies S + best_sub (L - i) < T -- and no later row can restart in column 0 or end in
-// the last column (always so for inside bands; for an edge band once its columns are past 0 and
-// its last row ends before len), and no last-column end so far reached T -- the pair cannot reach
+// of row i satisfies S + best_sub (L - i) < T, every cell of the later rows does too -- row L and
+// the last column's cells alike -- unless a later row restarts in column 0 (an edge band whose
+// columns are not yet past 0). Then, if no last-column end so far reached T, the pair cannot reach
 // T: the DP stops and returns a bound below T, which is all the caller compares. Random probe hits
-// -- most tasks -- stop early.
+// -- most tasks, edge tasks included (r04: an edge band never exited, and its last rows are all
+// checked cells: ~75 us per launch, the band phase's critical path) -- stop early.
 template <int E, bool CHECK>
 __device__ __forceinline__ int band_best(const uint8_t *rd, int len, const uint8_t *ac, int L, int d0,
                                          const pcabi::Scoring &sc, int T, const uint8_t *codes) {
@@ -812,8 +813,6 @@ __device__ __forceinline__ int band_best(const uint8_t *rd, int len, const uint8
         R[x] = CHECK ? ((j1 >= 1 && j1 <= len) ? v : 7) : v;
     }
     int best = 0;                                            // S(L, 0) = 0 is always scouted
-    // an edge band: no restart after row E - d0, no last-column end when its last row stops short
-    const bool tail_inside = !CHECK || L + d0 + E < len;
     for (int i = 1; i <= L; ++i) {
         const int ab = ac[i - 1];
         int h = kNeg, sl = kNeg;                             // H, S of the cell to the left
@@ -852,7 +851,7 @@ __device__ __forceinline__ int band_best(const uint8_t *rd, int len, const uint8
             const int v = bs.next();
             R[W - 1] = CHECK ? ((jn >= 1 && jn <= len) ? v : 7) : v;
         }
-        if ((i % PCABI_BAND_EXIT) == 0 && tail_inside && (!CHECK || i + d0 - E >= 0)) {
+        if ((i % PCABI_BAND_EXIT) == 0 && (!CHECK || i + d0 - E >= 0)) {   // (no restart after row E - d0)
             int mx = S[0];
 #pragma unroll
             for (int x = 1; x < W; ++x) mx = max(mx, S[x]);
