@@ -1547,6 +1547,8 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
         per_cu = 0;
         SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_expand, 256, s->lds_bytes));
         s->expand_blocks = std::min(s->n_slab, std::max(1, cus * std::max(1, per_cu)));
+        if (const char *eb = std::getenv("PCABI_EXPAND_BLOCKS"))   // experiments: the expansion's grid
+            if (std::atoi(eb) > 0) s->expand_blocks = std::min(s->n_slab, std::atoi(eb));
     }
     const int grid = s->scan_blocks;
     if (s->raw_cap == 0 || s->cap == 0) {
