@@ -1,0 +1,26 @@
+#!/bin/bash
+# GPU-box script (r04): PMC passes on the seed band kernels of the 8 kb middle step (why an edge-band
+# launch of a few thousand tasks takes ~55 us).
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/r04f
+mkdir -p $OUT
+export TMPDIR=/tmp
+cd /tmp
+i=0
+for pmc in "SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM" "SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE"; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --pmc $pmc --kernel-include-regex "k_seed_band|k_seed_expand" --output-format csv -d $OUT/pmc$i -o run -- python3 $R/bench.py --workload middle --steps 2 --warmup 1 --cpu-sample 0 --check 0 > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; tail -5 $OUT/pmc$i.log; exit 1; }
+  echo "pmc pass $i ok"
+done
+python3 - $OUT <<'PY'
+import csv, sys, os, glob, collections
+for f in sorted(glob.glob(os.path.join(sys.argv[1], 'pmc*', '*counter_collection.csv'))):
+    rows = list(csv.DictReader(open(f)))
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for r in rows:
+        agg[r['Kernel_Name'][:40]][r['Counter_Name']].append(float(r['Counter_Value']))
+    print('==', f)
+    for k, d in agg.items():
+        print(k, {c: round(sum(v) / len(v), 1) for c, v in d.items()})
+PY
