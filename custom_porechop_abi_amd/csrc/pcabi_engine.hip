@@ -878,30 +878,61 @@ __global__ __launch_bounds__(256) void k_plan_layout(const int32_t *tasks, int32
 // each: read, adapter, rs, re, m, l2, position, 0), the next round's reads (those that hit, from
 // the adapter that hit) and their count. A round whose seed / plan buffers overflowed keeps nothing
 // (no hits, no next round, no masking): the host sees rflag and reruns it with larger buffers.
+// (r04) The list is an ORDERED compaction -- a round's hits in the order of its reads, which round
+// 1 takes in read order -- so every round's list is sorted by read and the host concatenates the
+// rounds without sorting (an indirect std::sort of ~5 k hits cost ~0.1-0.4 ms of host time per
+// call). k_round_count counts each 256-entry chunk's hits; a chunk's base is the sum of the counts
+// before it (summed by the block: a few hundred chunks), its hits' places a block scan.
+__global__ __launch_bounds__(256) void k_round_count(const int32_t *hb, const int32_t *n_dev, const int32_t *seed_flags,
+                                                     const int32_t *plan_flag, int32_t *counts) {
+    if (seed_flags[0] || seed_flags[1] || *plan_flag) return;
+    const int64_t nr = *n_dev, nch = (nr + 255) / 256;
+    for (int64_t c = blockIdx.x; c < nch; c += gridDim.x) {   // block-uniform
+        const int64_t k = c * 256 + threadIdx.x;
+        const int cnt = __syncthreads_count(k < nr && hb[k] >= 0);
+        if (threadIdx.x == 0) counts[c] = cnt;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_round_hits(const int32_t *hb, int64_t n, const int32_t *n_dev, const int32_t *cur,
-                                                    int32_t *list, int32_t *n_next, int32_t *cur_next,
-                                                    int32_t *start_next, const int32_t *seed_flags,
+                                                    const int32_t *counts, int32_t *list, int32_t *n_next,
+                                                    int32_t *cur_next, int32_t *start_next, const int32_t *seed_flags,
                                                     const int32_t *plan_flag, int32_t *rflag) {
+    typedef hipcub::BlockScan<int, 256> Scan;
+    __shared__ typename Scan::TempStorage scan_tmp;
+    __shared__ int s_part[4];
     const int32_t f = (seed_flags[0] ? 1 : 0) | (seed_flags[1] ? 2 : 0) | (*plan_flag ? 4 : 0);
     if (blockIdx.x == 0 && threadIdx.x == 0) *rflag = f;
     if (f) return;
-    const int64_t nr = *n_dev;
-    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < nr; k += (int64_t)gridDim.x * 256) {
-        const int32_t a = hb[k];
-        if (a < 0) continue;
-        const int32_t j = atomicAdd(n_next, 1);
-        const int32_t r = cur ? cur[k] : (int32_t)k;
-        int32_t *o = list + 8 * (int64_t)j;
-        o[0] = r;
-        o[1] = a;
-        o[2] = hb[1 * n + k];
-        o[3] = hb[2 * n + k];
-        o[4] = hb[3 * n + k];
-        o[5] = hb[4 * n + k];
-        o[6] = (int32_t)k;
-        o[7] = 0;
-        cur_next[j] = r;
-        start_next[j] = a;
+    const int64_t nr = *n_dev, nch = (nr + 255) / 256;
+    for (int64_t c = blockIdx.x; c < nch; c += gridDim.x) {   // block-uniform
+        int part = 0;                                          // hits of the chunks before c
+        for (int64_t i = threadIdx.x; i < c; i += 256) part += counts[i];
+        for (int d = 32; d > 0; d >>= 1) part += __shfl_xor(part, d);
+        if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = part;
+        __syncthreads();
+        const int base = s_part[0] + s_part[1] + s_part[2] + s_part[3];
+        const int64_t k = c * 256 + threadIdx.x;
+        const int32_t a = k < nr ? hb[k] : -1;
+        int pos = 0, tot = 0;
+        Scan(scan_tmp).ExclusiveSum(a >= 0 ? 1 : 0, pos, tot);
+        if (a >= 0) {
+            const int32_t j = base + pos;
+            const int32_t r = cur ? cur[k] : (int32_t)k;
+            int32_t *o = list + 8 * (int64_t)j;
+            o[0] = r;
+            o[1] = a;
+            o[2] = hb[1 * n + k];
+            o[3] = hb[2 * n + k];
+            o[4] = hb[3 * n + k];
+            o[5] = hb[4 * n + k];
+            o[6] = (int32_t)k;
+            o[7] = 0;
+            cur_next[j] = r;
+            start_next[j] = a;
+        }
+        if (c == nch - 1 && threadIdx.x == 0) *n_next = base + tot;
+        __syncthreads();                                       // s_part, scan_tmp reused
     }
 }
 
@@ -1263,6 +1294,7 @@ struct pcabi_scan {
     std::vector<int32_t> h_ucert;                   // the certificate bounds last uploaded to pucert
     std::vector<int32_t> h_up;                      // bucket tables | spans | lengths last uploaded
     const void *up_at[3] = {nullptr, nullptr, nullptr};   // ... into these buffers
+    DeviceBuf pcount;                               // k_round_count's per-chunk hit counts
     MidProf prof;                                   // pcabi_scan_profile
     DeviceBuf pprof;                                // its device counters (4 x u64)
 };
@@ -2078,7 +2110,7 @@ void pcabi_scan_destroy(pcabi_scan *s) {
                          &s->pspan, &s->ptasks, &s->pfill, &s->pwoff, &s->pcidx, &s->pcand, &s->pbest, &s->phit, &s->phb,
                          &s->plist, &s->pcnt, &s->q_cur, &s->q_start, &s->q_list, &s->q_n, &s->q_flags,
                          &s->q_bk, &s->q_wave, &s->q_misc, &s->pcbase, &s->plen, &s->tw2, &s->to2, &s->tck2,
-                         &s->pcand2, &s->wa2, &s->pres2, &s->pcert, &s->pucert, &s->q_bk2, &s->q_misc2, &s->pprof})
+                         &s->pcand2, &s->wa2, &s->pres2, &s->pcert, &s->pucert, &s->q_bk2, &s->q_misc2, &s->pprof, &s->pcount})
         if (b->p) (void)hipFree(b->p);
     if (s->h_stage) (void)hipHostFree(s->h_stage);
     if (s->h_ctl) (void)hipHostFree(s->h_ctl);
@@ -2685,6 +2717,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
     if (int rc = sc->phb.ensure(sizeof(int32_t) * 5 * n)) return rc;
     if (int rc = sc->pbest.ensure(sizeof(unsigned long long) * n * n_adp)) return rc;
     if (int rc = sc->pcbase.ensure(sizeof(int32_t) * n * n_adp)) return rc;
+    if (int rc = sc->pcount.ensure(sizeof(int32_t) * ((size_t)n / 256 + 2))) return rc;
     if (int rc = sc->q_bk.ensure(4 * (bk_first.size() + 2 * bk_adp.size() + 2 * (size_t)n_bk + 16))) return rc;
     if (int rc = sc->q_misc2.ensure(64)) return rc;  // the second plan's slots and need
     if (int rc = sc->q_bk2.ensure(4 * (2 * (size_t)n_bk + 16))) return rc;
@@ -2945,8 +2978,11 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
                 merge_hit(pf, pass, nullptr, 0);      // flagged candidates: their whole reads
             }
         }
+        hipLaunchKernelGGL(k_round_count, dim3(gn), dim3(256), 0, st, (const int32_t *)sc->phb.p, nr, sflags, d_pflag,
+                           (int32_t *)sc->pcount.p);
         hipLaunchKernelGGL(k_round_hits, dim3(gn), dim3(256), 0, st, (const int32_t *)sc->phb.p, n, nr, cur,
-                           list_of(r), d_n + r + 1, cur_of(r + 1), start_of(r + 1), sflags, d_pflag, d_rflag + r);
+                           (const int32_t *)sc->pcount.p, list_of(r), d_n + r + 1, cur_of(r + 1), start_of(r + 1),
+                           sflags, d_pflag, d_rflag + r);
         hipLaunchKernelGGL(k_mask_list, dim3(1024), dim3(256), 0, st, codes, win_off, list_of(r), d_n + r + 1);
         HIP_TRY(hipGetLastError());
         if (g_debug) {                               // debugging only: a synchronisation per round
@@ -3085,16 +3121,14 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
     // takes its mean read length from this call's round-1 segments
     sc->spec_hits = std::max<int64_t>(4096, most_hits + most_hits / 4);
     if (h_nd[4] >= 0 && n > 0) sc->last_mean = (double)h_nd[4] * pcabi_seed::seg_positions() / (double)n;
-    // (round, read) order: per read the reference's discovery order
+    // (round, read) order: per read the reference's discovery order. The rounds come in order and
+    // each round's list in read order (k_round_hits' ordered compaction): only checked here
     const int64_t total = (int64_t)out_round.size();
-    std::vector<int64_t> ord((size_t)total);
-    for (int64_t j = 0; j < total; ++j) ord[j] = j;
-    std::sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) {
-        if (out_round[x] != out_round[y]) return out_round[x] < out_round[y];
-        return out[8 * x] < out[8 * y];
-    });
+    for (int64_t j = 1; j < total; ++j)
+        if (out_round[j] == out_round[j - 1] && out[8 * j] <= out[8 * (j - 1)])
+            return fail(PCABI_E_DEVICE, "middle scan: a round's hit list is out of read order");
     for (int64_t q = 0; q < total && q < cap; ++q) {
-        const int32_t *o = out.data() + 8 * ord[q];
+        const int32_t *o = out.data() + 8 * q;
         hits[0 * cap + q] = o[0];
         hits[1 * cap + q] = o[1];
         hits[2 * cap + q] = o[2];
