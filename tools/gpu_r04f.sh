@@ -17,7 +17,7 @@ cd /tmp
 i=0
 for pmc in "SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM" "SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $pmc --kernel-include-regex "k_seed_band|k_seed_expand" --output-format csv -d $OUT/pmc$i -o run -- python3 $R/bench.py --workload middle --steps 2 --warmup 1 --cpu-sample 0 --check 0 > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; tail -5 $OUT/pmc$i.log; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc $pmc --kernel-include-regex "k_seed_band|k_seed_expand|k_align_chunk|k_seed_scan" --output-format csv -d $OUT/pmc$i -o run -- python3 $R/bench.py --workload middle --steps 2 --warmup 1 --cpu-sample 0 --check 0 > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; tail -5 $OUT/pmc$i.log; exit 1; }
   echo "pmc pass $i ok"
 done
 python3 - $OUT <<'PY'
