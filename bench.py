@@ -817,8 +817,9 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
     d_st, d_et = dalloc(4 * n), dalloc(4 * n)
     d_toff_mid, d_tlen_mid = dalloc(8 * n), dalloc(4 * n)
     d_best = dalloc(8 * n_u)
-    stream = vp()
+    stream, stream2 = vp(), vp()
     _lib.check(L.pcabi_stream_create(ctypes.byref(stream)), 'stream')
+    _lib.check(L.pcabi_stream_create(ctypes.byref(stream2)), 'stream')
     sides = []
     for w_off, w_len, u in ((s_off, s_len, starts_u), (e_off, e_len, ends_u)):
         toff = np.zeros((n + 255) // 256 + 1, np.int64)
@@ -826,7 +827,7 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
         sides.append(dict(d_off=h2d(w_off), d_len=h2d(w_len), d_toff=h2d(toff), d_tiles=dalloc(4 * nd),
                           mq=int(np.diff(toff).max() // 256), mx=int(w_len.max()), mx_chk=int(w_len[:n_chk].max()),
                           search=table(u), n_u=len(u), d_chk=dalloc(4 * 8 * len(u) * n_chk)))
-    ev = [vp() for _ in range(10)]
+    ev = [vp() for _ in range(11)]
     for e in ev:
         _lib.check(L.pcabi_event_create(ctypes.byref(e)), 'event')
     kept_cache = {}
@@ -875,11 +876,18 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
         acc['host_ms'] = acc.get('host_ms', 0.0) + 1e3 * (time.perf_counter() - th)
         stats['kept'] = [a.name for a in matching]
         L.pcabi_event_record(ev[1], stream)
+        # the two sides' few-adapter cross products side by side (start on `stream`, end on stream2):
+        # with the kept sets each bucket holds one adapter (1,564 waves), too few to fill the chip alone
+        L.pcabi_stream_wait_event(stream2, ev[1])
         for k, sd in enumerate(sides):
             adps = ks['start'] if k == 0 else ks['end']
             if adps:
                 _lib.check(L.pcabi_align_cross_dev(sd['d_tiles'], sd['d_toff'], sd['d_len'], n, sd['mx'], ks['tabs'][k],
-                                                   *sc, ks['d_res'][k], len(adps) * n, stream), 'align')
+                                                   *sc, ks['d_res'][k], len(adps) * n, stream if k == 0 else stream2),
+                           'align')
+        L.pcabi_event_record(ev[8], stream2)
+        L.pcabi_stream_wait_event(stream, ev[8])
+        L.pcabi_event_record(ev[10], stream)
         n_sa, n_ea = len(ks['start']), len(ks['end'])
         _lib.check(L.pcabi_end_trim_dev(ks['d_res'][0], n_sa * n, n_sa, ks['d_res'][1], n_ea * n, n_ea, n, E, 2, 75.0, 4,
                                         d_st, d_et, None, None, stream), 'end_trim')
@@ -895,7 +903,7 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
         _lib.check(L.pcabi_stream_sync(stream), 'sync')
         stats['hits'] = int(nh)
         for key, a, b in (('check_ms', 0, 1), ('end_trim_ms', 1, 6), ('middle_ms', 6, 7), ('check_dom_start_ms', 2, 3),
-                          ('check_dom_end_ms', 4, 5)):
+                          ('check_dom_end_ms', 4, 5), ('end_trim_align_ms', 1, 10)):
             ms = ctypes.c_float()
             _lib.check(L.pcabi_event_elapsed_ms(ctypes.byref(ms), ev[a], ev[b]), 'elapsed')
             acc[key] = acc.get(key, 0.0) + ms.value
@@ -963,6 +971,13 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
             'middle_hits_per_step': stats['hits'],
             'cells_per_step': {'set_search': chk_cells, 'end_trim': end_cells},
             'end_trim_gcups': round(end_cells / (per['end_trim_ms'] * 1e-3) / 1e9, 1),
+            # the kept sets' one-adapter launches (both sides side by side, events around them)
+            'single_adapter_launches': {
+                'bound': 'valu', 'cells': end_cells, 'ms': per['end_trim_align_ms'],
+                'achieved': round(end_cells * OPS_PER_CELL / (per['end_trim_align_ms'] * 1e-3) / 1e12, 3),
+                'peak': round(VALU_PEAK_TOPS, 1), 'unit': 'Tops/s (int32 lane-ops)',
+                'frac': round(end_cells * OPS_PER_CELL / (per['end_trim_align_ms'] * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4),
+                'launches': 'one per register bucket and side, %d + %d adapters' % (len(ks['start']), len(ks['end']))},
             'roofline': {'bound': 'valu', 'kernel': 'the set search\'s largest register bucket (k_align<24, true, 6>)',
                          'achieved': round(tops, 3), 'peak': round(VALU_PEAK_TOPS, 1), 'unit': 'Tops/s (int32 lane-ops)',
                          'frac': round(tops / VALU_PEAK_TOPS, 4), 'launch_ms': round(dom_ms, 4),
