@@ -1107,6 +1107,13 @@ struct BucketHost {
 // side (the caller's stream + SideStreams::N), and a bucket of one or two adapters is too small
 // a grid to fill the GPU on its own.
 constexpr int kMaxFastBuckets = 4;
+int max_fast_buckets() {   // PCABI_MAX_FAST_BUCKETS (A/B runs) overrides kMaxFastBuckets
+    static const int v = [] {
+        const char *e = std::getenv("PCABI_MAX_FAST_BUCKETS");
+        return (e && std::atoi(e) > 0) ? std::atoi(e) : kMaxFastBuckets;
+    }();
+    return v;
+}
 
 // Bucket of every adapter: its own register bucket, then the cheapest merges of a FAST bucket
 // into the next larger non-empty one (cost = adapters x added padding rows) until at most
@@ -1133,7 +1140,7 @@ std::vector<int> assign_buckets(const int32_t *adp_len, int32_t n_adp, const pca
         std::vector<int> fast;
         for (int b = 0; b < kNumBuckets; ++b)
             if (count[b] && kBuckets[b].kind == FAST) fast.push_back(b);
-        if ((int)fast.size() <= kMaxFastBuckets) break;
+        if ((int)fast.size() <= max_fast_buckets()) break;
         int best = -1;
         int64_t best_cost = 0;
         for (size_t k = 0; k + 1 < fast.size(); ++k) {
