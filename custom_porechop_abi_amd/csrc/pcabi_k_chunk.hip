@@ -1,5 +1,7 @@
 // pcabi_k_chunk.hip -- k_align_chunk instantiations: the middle scan's candidate DP over
 // owned-column chunks of long reads (pcabi_dp.h sf::chunk_plan), every core.
+#include <cstdlib>
+
 #include "pcabi_kern.h"
 
 namespace pcabi_eng {
@@ -10,6 +12,18 @@ int dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st, bool ta
     if (kBuckets[b].kind == STRIPED) return launch_striped(p, affine, st);
     if (tagged && affine && kBuckets[b].kind == FAST && kBuckets[b].rpl <= 32) {
         // the run-tagged layout (9 VALU ops per cell instead of 10), as the end-window buckets
+        static const bool w6 = [] {
+            const char *e = std::getenv("PCABI_CHUNK_WAVES");
+            return e && std::atoi(e) == 6;
+        }();
+        if (w6 && kBuckets[b].rpl == 24) {
+            hipLaunchKernelGGL((k_align_chunk<24, true, TAGGED, 6>), grid, dim3(256), 0, st, p);
+            return 0;
+        }
+        if (w6 && kBuckets[b].rpl == 28) {
+            hipLaunchKernelGGL((k_align_chunk<28, true, TAGGED, 6>), grid, dim3(256), 0, st, p);
+            return 0;
+        }
         switch (kBuckets[b].rpl) {
 #define C(R) case R: hipLaunchKernelGGL((k_align_chunk<R, true, TAGGED>), grid, dim3(256), 0, st, p); return 0;
         C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32)

@@ -379,8 +379,11 @@ __device__ __forceinline__ void chunk_wave(const KParams &p, int64_t wave, bool 
     store_result(p.out, p.out_stride, p.task_out[slot], r);
 }
 
-template <int RPL, bool AFFINE, int KIND>
-__global__ __launch_bounds__(256, PCABI_WAVES) void k_align_chunk(KParams p) {
+// W: the launch's minimum waves per SIMD (amdgpu_waves_per_eu; 1 = no bound): the run-tagged
+// <= 28-row chunk kernels also come with W = 6 (80 VGPRs instead of 89: 6 waves per SIMD instead of
+// 5), chosen by PCABI_CHUNK_WAVES=6 at dispatch (A/B).
+template <int RPL, bool AFFINE, int KIND, int W = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k_align_chunk(KParams p) {
     __shared__ __attribute__((aligned(16))) int32_t tab[4 * wave_tab_ints<KIND, RPL>()];
     int32_t *wave_tab = tab + (threadIdx.x >> 6) * wave_tab_ints<KIND, RPL>();
     if (!p.dev_waves) {
