@@ -82,6 +82,9 @@ def parse():
                     help='drivers: reads whose decisions are compared with the same drivers over the oracle')
     ap.add_argument('--check-phase-check', type=int, default=400,
                     help='check_phase: check reads whose device reduction is compared with the oracle')
+    ap.add_argument('--rj-check-overlap', type=int, default=0,
+                    help='reference_job: 1 = the set search\'s two sides side by side (stream2); 0 = one after the '
+                         'other (each side\'s dominant launch then has the GPU to itself, the roofline\'s events)')
     ap.add_argument('--rest-overlap', type=int, default=1,
                     help='headline: 2 = after both dominant launches, both sides\' smaller buckets each on its own '
                          'stream; 1 = the two sides\' calls side by side; 0 = after each side\'s dominant launch')
@@ -856,13 +859,21 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
         for k, sd in enumerate(sides):
             _lib.check(L.pcabi_tile_windows_dev(d_work, sd['d_off'], sd['d_len'], n, sd['d_toff'], sd['mq'],
                                                 sd['d_tiles'], stream), 'tile')
+        if args.rj_check_overlap:
+            L.pcabi_event_record(ev[9], stream)
+            L.pcabi_stream_wait_event(stream2, ev[9])
+        for k, sd in enumerate(sides):
+            st_k = stream2 if (args.rj_check_overlap and k == 1) else stream
             # the check reads are the first n_check reads: their windows are the first tiles
             _lib.check(L.pcabi_align_cross_dev_marked(sd['d_tiles'], sd['d_toff'], sd['d_len'], n_chk, sd['mx_chk'],
-                                                      sd['search'], *sc, sd['d_chk'], sd['n_u'] * n_chk, stream,
+                                                      sd['search'], *sc, sd['d_chk'], sd['n_u'] * n_chk, st_k,
                                                       ev[2 + 2 * k], ev[3 + 2 * k]), 'align')
             _lib.check(L.pcabi_best_full_identity_dev(sd['d_chk'], sd['n_u'] * n_chk, n_chk, sd['n_u'],
-                                                      vp(d_best.value + 8 * b0), stream), 'best')
+                                                      vp(d_best.value + 8 * b0), st_k), 'best')
             b0 += sd['n_u']
+        if args.rj_check_overlap:
+            L.pcabi_event_record(ev[9], stream2)
+            L.pcabi_stream_wait_event(stream, ev[9])
         maxima = np.empty(n_u, np.float64)
         _lib.check(L.pcabi_dev_copy_async(maxima.ctypes.data_as(vp), d_best, 8 * n_u, 1, stream), 'd2h')
         _lib.check(L.pcabi_stream_sync(stream), 'sync')

@@ -20,3 +20,7 @@ for W in 1 6; do
   PCABI_CHUNK_WAVES=$W timeout -k 10 300 python bench.py --workload middle --steps 8 --warmup 2 --cpu-sample 0 > $OUT/mid_w$W.json 2> $OUT/mid_w$W.err || { echo "mid w$W failed rc=$?"; tail -20 $OUT/mid_w$W.err; exit 1; }
   python -c "import json; d=json.load(open('$OUT/mid_w$W.json')); print('mid chunkwaves=$W', d['middle_ms_per_step'], json.dumps(d['middle_phases']['ms']), d['parity_spot_check']['identical'])"
 done
+for O in 0 1 0 1; do
+  GPU_MAX_HW_QUEUES=8 timeout -k 10 300 python bench.py --only-subs reference_job --rj-check-overlap $O --steps 6 --warmup 2 --cpu-sample 0 --check 0 > $OUT/rj_o$O.json 2> $OUT/rj_o$O.err || { echo "rj o$O failed rc=$?"; tail -20 $OUT/rj_o$O.err; exit 1; }
+  python -c "import json; d=json.load(open('$OUT/rj_o$O.json'))['reference_job']; print('rj q8 overlap=$O', d['ms_per_step'], d['ms_per_phase']['check_ms'], d['ms_per_phase']['end_trim_align_ms'], d['single_adapter_launches']['frac'])"
+done
