@@ -661,9 +661,14 @@ __device__ __forceinline__ TaskCount expand_hit(const ScanArgs &a, const uint32_
     return c;
 }
 
-__global__ __launch_bounds__(256) void k_seed_expand(ScanArgs a) {
+// 1024-thread blocks (r04): the probe image takes ~60 KB of LDS, so two blocks fit a CU; with
+// quarter-size blocks that was 8 waves per CU and the expansion waited on its loads and barriers
+// (PMC: waves waiting ~88 % of their lifetime) over ~3.5 generations of blocks
+constexpr int kExpandThreads = 1024;
+
+__global__ __launch_bounds__(kExpandThreads) void k_seed_expand(ScanArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    typedef hipcub::BlockScan<long long, 256> Scan;
+    typedef hipcub::BlockScan<long long, kExpandThreads> Scan;
     __shared__ typename Scan::TempStorage scan_tmp;
     __shared__ long long s_base[2];                      // inside / edge bases, classes packed 32 | 32
     {   // the probe image (up to ~60 KB): 16-B loads, four in flight per thread (a dword loop waited
@@ -671,16 +676,17 @@ __global__ __launch_bounds__(256) void k_seed_expand(ScanArgs a) {
         const int n4 = a.tab_dw / 4;
         const uint4 *src = reinterpret_cast<const uint4 *>(a.tabs);
         uint4 *dst = reinterpret_cast<uint4 *>(lds);
-        for (int i = threadIdx.x; i < n4; i += 4 * 256) {
-            uint4 v[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (i + k * 256 < n4) v[k] = src[i + k * 256];
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (i + k * 256 < n4) dst[i + k * 256] = v[k];
+        constexpr int T = kExpandThreads;
+        for (int i = threadIdx.x; i < n4; i += 4 * T) {
+            const bool f1 = i + T < n4, f2 = i + 2 * T < n4, f3 = i + 3 * T < n4;
+            const uint4 v0 = src[i];
+            const uint4 v1 = src[f1 ? i + T : i], v2 = src[f2 ? i + 2 * T : i], v3 = src[f3 ? i + 3 * T : i];
+            dst[i] = v0;
+            if (f1) dst[i + T] = v1;
+            if (f2) dst[i + 2 * T] = v2;
+            if (f3) dst[i + 3 * T] = v3;
         }
-        for (int i = 4 * n4 + (int)threadIdx.x; i < a.tab_dw; i += 256) lds[i] = a.tabs[i];
+        for (int i = 4 * n4 + (int)threadIdx.x; i < a.tab_dw; i += T) lds[i] = a.tabs[i];
     }
     __syncthreads();
     const uint16_t *rank = reinterpret_cast<const uint16_t *>(lds + a.rank_off);
@@ -692,7 +698,7 @@ __global__ __launch_bounds__(256) void k_seed_expand(ScanArgs a) {
     for (int sl = blockIdx.x; sl < a.n_slab; sl += gridDim.x) {
         const uint4 *slab = a.raw + (int64_t)sl * a.slab;
         const int cnt = a.raw_cnt[sl];
-        for (int i = threadIdx.x; i < cnt; i += 256) {
+        for (int i = threadIdx.x; i < cnt; i += kExpandThreads) {
             const TaskCount c = expand_hit<false>(a, lds, rank, estart, ent, ent2, slab[i], TaskCount{0, 0});
             mine.in += c.in;
             mine.edge += c.edge;
@@ -720,11 +726,11 @@ __global__ __launch_bounds__(256) void k_seed_expand(ScanArgs a) {
         }
         __syncthreads();
     }
-    // 2. the tasks, 256 hits at a time
+    // 2. the tasks, a block's worth of hits at a time
     for (int sl = blockIdx.x; sl < a.n_slab; sl += gridDim.x) {      // block-uniform
         const uint4 *slab = a.raw + (int64_t)sl * a.slab;
         const int cnt = a.raw_cnt[sl];
-        for (int base = 0; base < cnt; base += 256) {
+        for (int base = 0; base < cnt; base += kExpandThreads) {
             const int i = base + (int)threadIdx.x;
             const uint4 r = i < cnt ? slab[i] : make_uint4(0u, 0u, 0u, 0u);
             const TaskCount c = i < cnt ? expand_hit<false>(a, lds, rank, estart, ent, ent2, r, TaskCount{0, 0})
@@ -1545,7 +1551,7 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
         s->scan_blocks = std::max(1, cus * std::max(1, per_cu));
         s->n_slab = s->bytemap ? s->scan_blocks * (kScanThreads / 64) : s->scan_blocks;   // per wave / per block
         per_cu = 0;
-        SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_expand, 256, s->lds_bytes));
+        SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_expand, kExpandThreads, s->lds_bytes));
         s->expand_blocks = std::min(s->n_slab, std::max(1, cus * std::max(1, per_cu)));
         if (const char *eb = std::getenv("PCABI_EXPAND_BLOCKS"))   // experiments: the expansion's grid
             if (std::atoi(eb) > 0) s->expand_blocks = std::min(s->n_slab, std::atoi(eb));
@@ -1616,7 +1622,7 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
     else
         hipLaunchKernelGGL(k_seed_scan_bits, dim3(grid), dim3(256), 4 * (size_t)A.bits_dw + 4, st, A);
     if (s->pev) SD_TRY(hipEventRecord(s->pev[1], st));
-    hipLaunchKernelGGL(k_seed_expand, dim3(s->expand_blocks), dim3(256), s->lds_bytes, st, A);
+    hipLaunchKernelGGL(k_seed_expand, dim3(s->expand_blocks), dim3(kExpandThreads), s->lds_bytes, st, A);
     if (s->pev) SD_TRY(hipEventRecord(s->pev[2], st));
     SD_TRY(hipGetLastError());
     if (tasks) return 0;                                // the caller launches the bands (host counts)

@@ -6,6 +6,8 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/r04k
 mkdir -p $OUT
 cd $R
+timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_gpu_middle_paths.py tests/test_gpu_parity.py -k "middle or seed or windows or overflow or scan" > $OUT/pytest_mid.log 2>&1 || { echo "pytest failed rc=$?"; grep -E "FAILED|Error" $OUT/pytest_mid.log | head -20; tail -30 $OUT/pytest_mid.log; exit 1; }
+tail -2 $OUT/pytest_mid.log
 for Q in 4 8 4 8; do
   GPU_MAX_HW_QUEUES=$Q timeout -k 10 300 python bench.py --sub 0 --steps 20 --warmup 3 --cpu-sample 0 --check 0 > $OUT/head_q$Q.json 2> $OUT/head_q$Q.err || { echo "head $Q failed rc=$?"; tail -20 $OUT/head_q$Q.err; exit 1; }
   python -c "import json; d=json.load(open('$OUT/head_q$Q.json')); print('head q=$Q', d['value'], d['ms_per_step'], d['roofline']['launch_ms'])"
