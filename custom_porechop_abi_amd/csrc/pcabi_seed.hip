@@ -596,6 +596,27 @@ __global__ __launch_bounds__(kScanThreads) void k_seed_scan(ScanArgs a) {
     }
 }
 
+// The round's segment space in one block: each thread sums a contiguous run of reads' segment
+// counts, a block scan places the runs, the threads write their prefixes (reads past n_dev: none).
+constexpr int kSegCumThreads = 1024;
+__global__ __launch_bounds__(kSegCumThreads) void k_seg_cum(const int32_t *v_len, const int32_t *n_dev, int64_t n,
+                                                            int64_t *seg_cum) {
+    typedef hipcub::BlockScan<long long, kSegCumThreads> Scan;
+    __shared__ typename Scan::TempStorage tmp;
+    const int64_t nr = dev_count(n_dev, n);
+    const int64_t per = (nr + kSegCumThreads - 1) / kSegCumThreads;
+    const int64_t lo = min((int64_t)threadIdx.x * per, nr), hi = min(lo + per, nr);
+    long long sum = 0;
+    for (int64_t k = lo; k < hi; ++k) sum += ((int64_t)max(v_len[k], 0) + kSeg - 1) / kSeg;
+    long long ex = 0, total = 0;
+    Scan(tmp).ExclusiveSum(sum, ex, total);
+    for (int64_t k = lo; k < hi; ++k) {
+        seg_cum[k] = ex;
+        ex += ((int64_t)max(v_len[k], 0) + kSeg - 1) / kSeg;
+    }
+    if (threadIdx.x == 0) seg_cum[nr] = total;
+}
+
 // Resident blocks striding over the slabs: the probe entries of the slabs' raw hits become tasks.
 // The raw hits carry their 8-mer and valid run, so nothing here touches the reads: the slabs, the
 // LDS image and the task stores. A block first counts its tasks per class (all its slabs) and
@@ -1602,18 +1623,22 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
     A.cap = s->cap;
     A.ecap = s->ecap;
     if (int rc = s->ccnt.ensure(8)) return rc;
-    // the scan's segment space: seg_cum[r] = segments before read r, seg_cum[n_dev] = all
-    {
+    // the scan's segment space: seg_cum[r] = segments before read r, seg_cum[n_dev] = all -- one
+    // block up to 256 k reads (hipcub's device scan takes two launches, ~20 us a round), else
+    // hipcub's (its entries past n_dev repeat the total)
+    if (int rc = s->segcum.ensure(sizeof(int64_t) * (size_t)(n + 1))) return rc;
+    if (n <= (int64_t)kSegCumThreads * 256) {
+        hipLaunchKernelGGL(k_seg_cum, dim3(1), dim3(kSegCumThreads), 0, st, v_len, n_dev, n, (int64_t *)s->segcum.p);
+    } else {
         hipcub::CountingInputIterator<int64_t> idx(0);
         hipcub::TransformInputIterator<int64_t, SegCount, hipcub::CountingInputIterator<int64_t>> segs(
             idx, SegCount{v_len, n_dev, n});
         size_t tmp = 0;
         SD_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, segs, (int64_t *)nullptr, n + 1, st));
         if (int rc = s->scantmp.ensure(tmp)) return rc;
-        if (int rc = s->segcum.ensure(sizeof(int64_t) * (size_t)(n + 1))) return rc;
         SD_TRY(hipcub::DeviceScan::ExclusiveSum(s->scantmp.p, tmp, segs, (int64_t *)s->segcum.p, n + 1, st));
-        A.seg_cum = (const int64_t *)s->segcum.p;
     }
+    A.seg_cum = (const int64_t *)s->segcum.p;
     hipLaunchKernelGGL(k_bound_reset, dim3(1024), dim3(256), 0, st, (int32_t *)s->bound.p, n, n_dev, n_adp, A.cnt,
                        kCnt + 1, (unsigned long long *)s->ccnt.p);
     if (s->pev) SD_TRY(hipEventRecord(s->pev[0], st));
