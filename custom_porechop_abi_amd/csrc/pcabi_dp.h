@@ -1472,9 +1472,10 @@ struct LaneSplit {
         sn = max3i(diag, vn2, hn);
     }
 
-    // inner column j (1 <= j < n); gup / vup: row r0's G / V keys at column j
+    // inner column j (1 <= j < n); gup / vup: row r0's G / V keys at column j. owned == false (a
+    // chunk's lead-in columns, LanePacked::column's GATE): the column cannot become the row-L best
     template <typename TabRow>
-    PCABI_HD void inner(const TabRow &tab, int j, int32_t gup, int32_t vup) {
+    PCABI_HD void inner(const TabRow &tab, int j, int32_t gup, int32_t vup, bool owned = true) {
         const int32_t g_in = gup;
         int32_t diag = gdiag + tab(1);
         int32_t lv = 0, ls = 0;
@@ -1500,9 +1501,26 @@ struct LaneSplit {
         if (AFFINE && Y::TAGGED) corr = std::max(lv, ls & ~Y::TBM);
         else if (AFFINE) corr = std::max(lv | Y::TB3, ls & ~Y::TBM);
         else corr = ls;
-        const bool upd = corr > (bkey | ((1 << Y::SC_SH) - 1));
+        const bool upd = owned && corr > (bkey | ((1 << Y::SC_SH) - 1));
         bkey = upd ? corr : bkey;
         bj = upd ? j : bj;
+    }
+
+    // A chunk that ends before the read end (its last column ran as an inner column): the last
+    // lane's row-L best from the scout (LanePacked::materialize); result(n + 1) then reports it.
+    PCABI_HD void materialize() {
+        if (!last) return;
+        const int t = Y::tb(bkey);
+        int lt;
+        if (bj == 0) lt = LT_NONE;
+        else if (AFFINE) lt = (Y::TAGGED ? t != 0 : t == 3) ? LT_V : LT_D;
+        else lt = t == 3 ? LT_D : (t == 2 ? LT_V : LT_H);
+        bscore = Y::score(bkey);
+        bi = L;
+        battr = Y::attr(bkey);
+        blt = lt;
+        btrail = 0;
+        bprec = 0;
     }
 
     // the last column (j = n) of this lane's rows, after lane l - 1's part of it (`in`; lane 0:

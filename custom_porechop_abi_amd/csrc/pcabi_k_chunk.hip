@@ -10,12 +10,18 @@ int dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st, bool ta
     // planned on the device: n_waves is the grid (blocks striding over the device wave count)
     const dim3 grid((unsigned)(p.dev_waves ? p.n_waves : (p.n_waves + 3) / 4));
     if (kBuckets[b].kind == STRIPED) return launch_striped(p, affine, st);
+    {   // PCABI_CHUNK_SPLIT=2|4: the row-split core, K lanes per chunk task (A/B)
+        const char *e = std::getenv("PCABI_CHUNK_SPLIT");   // (read per launch: tests switch it)
+        const int ks = e ? std::atoi(e) : 0;
+        if ((ks == 2 || ks == 4) && kBuckets[b].kind == FAST && kBuckets[b].rpl <= 64 &&
+            pcabi::split_ok(kBuckets[b].rpl, ks) &&
+            dispatch_split_chunk(kBuckets[b].rpl, ks, p, affine, tagged && affine && kBuckets[b].rpl <= 32, st))
+            return 0;
+    }
     if (tagged && affine && kBuckets[b].kind == FAST && kBuckets[b].rpl <= 32) {
         // the run-tagged layout (9 VALU ops per cell instead of 10), as the end-window buckets
-        static const bool w6 = [] {
-            const char *e = std::getenv("PCABI_CHUNK_WAVES");
-            return e && std::atoi(e) == 6;
-        }();
+        const char *ew = std::getenv("PCABI_CHUNK_WAVES");
+        const bool w6 = ew && std::atoi(ew) == 6;
         if (w6 && kBuckets[b].rpl == 24) {
             hipLaunchKernelGGL((k_align_chunk<24, true, TAGGED, 6>), grid, dim3(256), 0, st, p);
             return 0;

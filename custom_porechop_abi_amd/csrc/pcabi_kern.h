@@ -590,6 +590,101 @@ __global__ __launch_bounds__(256, PCABI_WAVES) void k_align_split(KParams p) {
         store_result(p.out, p.out_stride, (int64_t)p.adp_id[a_local] * p.n_win + w, n > 0 ? st.result(n) : empty_result());
 }
 
+// ---- row-split chunk mode: the middle scan's candidate DP with K lanes per chunk task ----------
+// The device plan's wave w (64 task slots, one adapter) runs as K sub-waves: sub-wave k takes slots
+// w * 64 + k * (64 / K) .. + 64 / K, K consecutive lanes per slot (LaneSplit as k_align_split). Inner
+// columns gated by the owned range; the read's last chunk (own_hi < 0) ends with the K-phase last
+// column, an inner chunk runs its last column as an inner one and materializes (packed_best's CHUNK
+// rules, host model: tests/native/dp_model.cpp run_split_chunk). K x the waves of k_align_chunk
+// for the same chunks: the plan's ~4,096 waves per bucket leave the one-lane kernel at ~3 waves
+// per SIMD.
+template <int RPL, int K, bool AFFINE, int KIND>
+__device__ __forceinline__ void split_chunk_wave(const KParams &p, int64_t pw, int sub, bool live, int32_t *wave_tab) {
+    constexpr int R = RPL / K;
+    using Y = typename std::conditional<KIND == TAGGED, pcabi::pk::LayT<RPL>, pcabi::pk::Lay<RPL>>::type;
+    const int lane = threadIdx.x & 63, l = lane % K;
+    const int64_t slot = pw * 64 + sub * (64 / K) + lane / K;
+    const int a_local = __builtin_amdgcn_readfirstlane(p.wave_adp[pw]);
+    const int L = __builtin_amdgcn_readfirstlane(p.adp_len[a_local]);
+    fill_wave_tab<RPL, Y>(p, a_local, L, wave_tab);
+    const int32_t tw = live ? p.task_win[slot] : -1;
+    int4 ck = make_int4(0, 0, 1, 0);
+    if (tw >= 0) ck = p.task_chunk[slot];
+    const int n = tw >= 0 ? ck.y : 0;
+    const bool at_end = ck.w < 0;
+    const int hi = at_end ? n + 1 : ck.w;
+    const int n_in = at_end ? n - 1 : n;
+    int nmax = n_in;                                      // the sub-wave's step count
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) nmax = max(nmax, __shfl_xor(nmax, o));
+    WindowReader rd;
+    if (n > 0) {
+        const uint8_t *b = p.codes + p.win_off[tw] + ck.x;
+        const int a0 = (int)((uintptr_t)b & 3);
+        rd = WindowReader(reinterpret_cast<const uint32_t *>(b - a0), 1, 8 * a0);
+    }
+    pcabi::LaneSplit<R, AFFINE, Y> st;
+    st.init(l, K, L, RPL, p.sc);
+    int32_t sg = st.gbot, sv = st.vbot;
+    const int steps = nmax + K - 1;
+#pragma unroll 1
+    for (int t = 1; t <= steps; ++t) {
+        int32_t rg = lane_from_below(sg), rv = lane_from_below(sv);
+        if (l == 0) {
+            rg = st.row0_g(t);
+            rv = st.neg2;
+        }
+        const int j = t - l;
+        if (j >= 1 && j <= n_in) {
+            const int c = rd(j);
+            st.inner(LdsRow{wave_tab + c * RPL + st.r0}, j, rg, rv, j >= ck.z && j < hi);
+            sg = st.gbot;
+            sv = st.vbot;
+        }
+    }
+    // the read's last chunk: its last column, lane by lane; an inner chunk: the scout's best
+    st.out = pcabi::SplitIn{};
+#pragma unroll
+    for (int ph = 0; ph < K; ++ph) {
+        pcabi::SplitIn in;
+        in.gup = lane_from_below(st.out.gup);
+        in.vup = lane_from_below(st.out.vup);
+        in.slt = lane_from_below(st.out.slt);
+        in.vt = lane_from_below(st.out.vt);
+        in.vp = lane_from_below(st.out.vp);
+        in.score = lane_from_below(st.out.score);
+        in.bi = lane_from_below(st.out.bi);
+        in.lt = lane_from_below(st.out.lt);
+        in.trail = lane_from_below(st.out.trail);
+        in.prec = lane_from_below(st.out.prec);
+        in.attr = (uint32_t)lane_from_below((int32_t)st.out.attr);
+        if (l == ph && n > 0 && at_end) {
+            if (l == 0) in = st.empty_in(n);
+            const int c = rd(n);
+            st.last_col(LdsRow{wave_tab + c * RPL + st.r0}, n, in);
+        }
+    }
+    if (!at_end) st.materialize();
+    if (l == K - 1 && tw >= 0)
+        store_result(p.out, p.out_stride, p.task_out[slot], n > 0 ? st.result(at_end ? n : n + 1) : empty_result());
+}
+
+template <int RPL, int K, bool AFFINE, int KIND>
+__global__ __launch_bounds__(256) void k_align_split_chunk(KParams p) {
+    static_assert(RPL % K == 0 && 16 % K == 0 && RPL / K >= 2, "split geometry");
+    __shared__ __attribute__((aligned(16))) int32_t tab[4 * kTabW * RPL];
+    int32_t *wave_tab = tab + (threadIdx.x >> 6) * (kTabW * RPL);
+    // planned on the device: the bucket's waves from dev_waves, K sub-waves each, the blocks
+    // striding over them (block-uniform trip count: every wave joins every table barrier)
+    const int64_t w0 = p.dev_waves[0], nsub = (int64_t)p.dev_waves[1] * K;
+    for (int64_t wb = blockIdx.x; wb * 4 < nsub; wb += gridDim.x) {
+        int64_t sw = wb * 4 + (threadIdx.x >> 6);
+        const bool live = sw < nsub;
+        if (!live) sw = nsub - 1;
+        split_chunk_wave<RPL, K, AFFINE, KIND>(p, w0 + sw / K, (int)(sw % K), live, wave_tab);
+    }
+}
+
 template <int RPL, int KIND>
 void launch(const KParams &p, bool affine, dim3 grid, hipStream_t st) {
     if (affine) hipLaunchKernelGGL((k_align<RPL, true, KIND>), grid, dim3(256), 0, st, p);
@@ -611,6 +706,8 @@ int dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st, bool ta
 void dispatch_filter(int rpl, const FParams &p, bool affine, hipStream_t st);
 // k_align_split launches (cross mode; grid = padded tiles x adapters x K); false: no such kernel
 bool dispatch_split(int rpl, int K, const KParams &p, bool affine, bool tagged, hipStream_t st);
+// k_align_split_chunk launches (device-planned chunk tasks, K lanes each); false: no such kernel
+bool dispatch_split_chunk(int rpl, int K, const KParams &p, bool affine, bool tagged, hipStream_t st);
 // the striped bucket (k_align_striped): p.rt, p.max_cols set by the caller
 int launch_striped(KParams p, bool affine, hipStream_t st);
 

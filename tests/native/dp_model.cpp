@@ -480,6 +480,94 @@ static void run_split(const char *read, int n, const char *adp, int L, pcabi::Sc
     out[4] = r.score; out[5] = r.m; out[6] = r.l1; out[7] = r.l2;
 }
 
+// the row-split core on one chunk (k_align_split_chunk): inner columns 1 .. n_in gated by the owned
+// range, then the K-phase last column (the read's last chunk, own_hi < 0) or the last lane's
+// materialize (an inner chunk: its last column is an inner read column) -- and the one-lane chunk
+// core on the same chunk, for a field-by-field comparison
+template <int RPL, int K, bool AFFINE, typename Y>
+static void run_split_chunk(const char *read, int n, const char *adp, int L, pcabi::Scoring sc, int own_lo, int own_hi,
+                            int *out) {
+    constexpr int R = RPL / K;
+    const int off = RPL - L;
+    auto ad = [&](int s) { return s <= off ? pcabi::PAD_CODE : dna5((unsigned char)adp[s - off - 1]); };
+    int32_t tab[pcabi::pk::TAB_W * RPL];
+    for (int c = 0; c < pcabi::pk::TAB_W; ++c)
+        for (int s = 1; s <= RPL; ++s) tab[c * RPL + s - 1] = pcabi::pk::sub_key<RPL, decltype(ad), Y>(s, c, ad, off, sc);
+    struct Row {
+        const int32_t *p;
+        int32_t operator()(int s) const { return p[s - 1]; }
+    };
+    auto code = [&](int j) { return dna5((unsigned char)read[j - 1]); };
+    const bool at_end = own_hi < 0;
+    const int hi = at_end ? n + 1 : own_hi;
+    const int n_in = at_end ? n - 1 : n;
+    pcabi::LaneSplit<R, AFFINE, Y> st[K];
+    int32_t sg[K], sv[K];
+    for (int l = 0; l < K; ++l) {
+        st[l].init(l, K, L, RPL, sc);
+        sg[l] = st[l].gbot;
+        sv[l] = st[l].vbot;
+    }
+    for (int t = 1; t <= n_in + K - 1; ++t) {
+        int32_t rg[K], rv[K];
+        for (int l = 0; l < K; ++l) {
+            rg[l] = l ? sg[l - 1] : st[0].row0_g(t);
+            rv[l] = l ? sv[l - 1] : st[0].neg2;
+        }
+        for (int l = 0; l < K; ++l) {
+            const int j = t - l;
+            if (j >= 1 && j <= n_in) {
+                st[l].inner(Row{tab + code(j) * RPL + st[l].r0}, j, rg[l], rv[l], j >= own_lo && j < hi);
+                sg[l] = st[l].gbot;
+                sv[l] = st[l].vbot;
+            }
+        }
+    }
+    if (at_end) {
+        for (int p = 0; p < K; ++p)
+            st[p].last_col(Row{tab + code(n) * RPL + st[p].r0}, n, p ? st[p - 1].out : st[0].empty_in(n));
+    } else {
+        st[K - 1].materialize();
+    }
+    const pcabi::Result r = st[K - 1].result(at_end ? n : n + 1);
+    out[0] = r.rs; out[1] = r.re; out[2] = r.as; out[3] = r.ae;
+    out[4] = r.score; out[5] = r.m; out[6] = r.l1; out[7] = r.l2;
+}
+
+template <int RPL, int K>
+static int run_split_chunk_any(const char *read, int n, const char *adp, int L, int tagged, pcabi::Scoring sc,
+                               int own_lo, int own_hi, int *out_split, int *out_lane) {
+    if (tagged) {
+        if constexpr (RPL <= 32) {
+            if (!pcabi::layt_ok(L, RPL, sc)) return -3;
+            run_split_chunk<RPL, K, true, pcabi::pk::LayT<RPL>>(read, n, adp, L, sc, own_lo, own_hi, out_split);
+            run_packed_chunk<RPL, true>(read, n, adp, L, sc, own_lo, own_hi, out_lane);
+            return 0;
+        }
+        return -2;
+    }
+    if (!pcabi::packed_ok(L, RPL, sc)) return -3;
+    if (sc.go != sc.ge) run_split_chunk<RPL, K, true, pcabi::pk::Lay<RPL>>(read, n, adp, L, sc, own_lo, own_hi, out_split);
+    else run_split_chunk<RPL, K, false, pcabi::pk::Lay<RPL>>(read, n, adp, L, sc, own_lo, own_hi, out_split);
+    run_packed_chunk<RPL>(read, n, adp, L, sc, own_lo, own_hi, out_lane);
+    return 0;
+}
+
+extern "C" int pcabi_model_split_chunk(const char *read, int n, const char *adp, int L, int rpl, int K, int tagged,
+                                       int ma, int mi, int go, int ge, int own_lo, int own_hi, int *out_split,
+                                       int *out_lane) {
+    pcabi::Scoring sc{ma, mi, go, ge};
+    if (L <= 0 || n <= 0) return -1;
+    if (!pcabi::split_ok(rpl, K)) return -2;
+#define C(R) case R: return K == 2 ? run_split_chunk_any<R, 2>(read, n, adp, L, tagged, sc, own_lo, own_hi, out_split, out_lane) \
+                                   : (K == 4 ? run_split_chunk_any<R, 4>(read, n, adp, L, tagged, sc, own_lo, own_hi, out_split, out_lane) : -2);
+    switch (rpl) {
+    C(8) C(12) C(16) C(20) C(24) C(28) C(32) C(36) C(40) C(44) C(48) C(52) C(56) C(60) C(64)
+    default: return -2;
+    }
+#undef C
+}
+
 template <int RPL, int K>
 static int run_split_any(const char *read, int n, const char *adp, int L, int tagged, pcabi::Scoring sc, int *out) {
     if (tagged) {

@@ -681,3 +681,48 @@ def test_row_split_core(model):
             assert _fmt(res) == exp, (sc, r, a, exp, res, K)
             n_gold += 1
     assert n_gold > 2000
+
+
+def test_row_split_chunk_core(model):
+    """The row-split core in chunk mode (k_align_split_chunk: the middle scan's candidate DP with K
+    lanes per chunk task): inner columns gated by the owned range (the lead-in columns cannot be
+    the row-L best), then the K-phase last column for a read's last chunk (own_hi < 0) or the last
+    lane's materialize for an inner chunk (reported as not at the read end). Field for field equal
+    to the one-lane chunk core (align_lane_packed with CHUNK) on the same chunk, both layouts,
+    K = 2 and 4, every bucket, owned ranges anywhere in the chunk (empty ones included)."""
+    model.pcabi_model_split_chunk.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int] + \
+        [ctypes.c_int] * 9 + [ctypes.c_void_p, ctypes.c_void_p]
+    rng = random.Random(91)
+    schemes = [(3, -6, -5, -2), (2, -1, -1, -1), (1, -1, -3, -1), (3, -6, -2, -5), (5, -4, -8, -6), (2, -3, -5, -1)]
+    n_checked = {(t, K, e): 0 for t in (0, 1) for K in (2, 4) for e in (0, 1)}
+    for k in range(6000):
+        sc = schemes[k % len(schemes)]
+        tagged = k % 2
+        K = rng.choice([2, 4])
+        al = rng.choice(['AT', 'ACGT', 'ACGTN'])
+        L = rng.randint(1, 31 if tagged else 64)
+        rpl = rng.choice([r for r in range(8, (33 if tagged else 65), 4) if r >= L and r % K == 0 and r // K >= 2])
+        a = ''.join(rng.choice(al) for _ in range(L))
+        b = list(a)
+        for _ in range(rng.randint(0, 2)):
+            p = rng.randint(0, len(b))
+            if rng.random() < 0.5:
+                b[p:p] = [rng.choice(al) for _ in range(rng.randint(1, 6))]
+            else:
+                del b[p:p + rng.randint(1, 4)]
+        r = ''.join(rng.choice(al) for _ in range(rng.randint(0, 80))) + ''.join(b) + \
+            ''.join(rng.choice(al) for _ in range(rng.randint(0, 80)))
+        r = r or 'A'
+        n = len(r)
+        at_end = rng.random() < 0.4
+        own_lo = rng.randint(1, n + 1)
+        own_hi = -1 if at_end else rng.randint(own_lo, n + 1)
+        o_split, o_lane = (ctypes.c_int * 8)(), (ctypes.c_int * 8)()
+        rc = model.pcabi_model_split_chunk(r.encode(), n, a.encode(), L, rpl, K, tagged, *sc, own_lo, own_hi,
+                                           o_split, o_lane)
+        if rc == -3:
+            continue
+        assert rc == 0 and list(o_split) == list(o_lane), (sc, r, a, rpl, K, tagged, own_lo, own_hi,
+                                                             list(o_split), list(o_lane))
+        n_checked[(tagged, K, int(at_end))] += 1
+    assert min(n_checked.values()) > 300, n_checked

@@ -230,6 +230,25 @@ def test_seed_scan_bytemap_equals_bitmap_scan(gpu_lib, monkeypatch, thr):
     assert np.array_equal(prof['1'][7:15], prof['0'][7:15]), (prof['1'][7:15], prof['0'][7:15])
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize('split', ['2', '4'])
+@pytest.mark.parametrize('windows', ['0', '1'])
+def test_chunk_dp_row_split(gpu_lib, monkeypatch, reads_8kb, split, windows):
+    """PCABI_CHUNK_SPLIT=2|4: the candidate DP's chunk tasks on the row-split core (K lanes per task,
+    k_align_split_chunk; host model: test_dp_core_cpu.py::test_row_split_chunk_core) -- the scan
+    equals the oracle, whole-read chunks and candidate windows alike, and at 90 % on shorter copies
+    with the 85 % threshold's longer probes."""
+    from custom_porechop_abi_amd import engine
+    views, exp = reads_8kb
+    monkeypatch.setenv('PCABI_MIDDLE_SEEDS', '2')
+    monkeypatch.setenv('PCABI_MIDDLE_WINDOWS', windows)
+    monkeypatch.setenv('PCABI_CHUNK_SPLIT', split)
+    got = _dev_scan(gpu_lib, views, ADPS, SC, 90.0)      # a fresh scan: the switch is read per process
+    assert np.array_equal(_sorted(got), exp)
+    got2 = engine.middle_scan(views, ADPS, SC, 90.0)
+    assert np.array_equal(_sorted(got2), exp)
+
+
 # ---- k_barcode_call at the configs[3] width ---------------------------------------------------
 
 def _pid6(m, l):
