@@ -614,13 +614,29 @@ __device__ __forceinline__ uint64_t merge_key(int32_t score, int4 ck) {
     return ((uint64_t)((uint32_t)score ^ 0x80000000u) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)(ck.x + ck.z));
 }
 
+// A candidate's chunk tasks sit in consecutive slots, so a wave's lanes mostly share a few
+// candidates: a segmented max over each run of equal candidates (shuffles) leaves one atomic per
+// run instead of one per task (64 same-address atomics per wave serialised: ~48 us of round 1).
 __global__ __launch_bounds__(256) void k_merge_best(const int32_t *tw, const int4 *tck, const int32_t *tcand,
                                                     const int32_t *res, int64_t slots, const int64_t *slots_dev,
                                                     unsigned long long *best) {
     const int64_t ns = slots_dev ? *slots_dev : slots;
-    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < ns; q += (int64_t)gridDim.x * 256) {
-        if (tw[q] < 0) continue;
-        atomicMax(&best[tcand[q]], (unsigned long long)merge_key(res[4 * slots + q], tck[q]));
+    const int lane = threadIdx.x & 63;
+    for (int64_t b0 = (int64_t)blockIdx.x * 256; b0 < ns; b0 += (int64_t)gridDim.x * 256) {   // block-uniform
+        const int64_t q = b0 + threadIdx.x;
+        const bool live = q < ns && tw[q] >= 0;
+        const int32_t cand = live ? tcand[q] : -1 - lane;           // idle lanes: runs of their own
+        unsigned long long key = live ? (unsigned long long)merge_key(res[4 * slots + q], tck[q]) : 0ull;
+        const int32_t prev = __shfl_up(cand, 1);
+        const uint64_t heads = __ballot(lane == 0 || prev != cand);
+        const int start = 63 - __clzll(heads & ((2ull << lane) - 1ull));   // this lane's run head
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const unsigned long long o = __shfl_up(key, d);
+            if (lane - d >= start) key = key > o ? key : o;
+        }
+        const bool tail = lane == 63 || ((heads >> (lane + 1)) & 1ull);
+        if (live && tail) atomicMax(&best[cand], key);
     }
 }
 
