@@ -687,10 +687,38 @@ __device__ __forceinline__ TaskCount expand_hit(const ScanArgs &a, const uint32_
 // (PMC: waves waiting ~88 % of their lifetime) over ~3.5 generations of blocks
 constexpr int kExpandThreads = 1024;
 
+// Exclusive block sum over kExpandThreads threads in ~200 B of static LDS (hipcub's BlockScan takes
+// 8.4 KB at this width, which with a ~60 KB probe image passes the 64 KB a workgroup's LDS may hold
+// without an attribute): a wave scan by shuffles, then the 16 wave totals. Every thread calls it.
+__device__ __forceinline__ long long expand_excl_sum(long long v, long long &total, long long *s_w) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    long long x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const long long t = __shfl_up(x, d);
+        if (lane >= d) x += t;
+    }
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    if (w == 0) {
+        long long y = lane < kExpandThreads / 64 ? s_w[lane] : 0;
+#pragma unroll
+        for (int d = 1; d < kExpandThreads / 64; d <<= 1) {
+            const long long t = __shfl_up(y, d);
+            if (lane >= d) y += t;
+        }
+        if (lane < kExpandThreads / 64) s_w[lane] = y;   // inclusive wave prefixes
+    }
+    __syncthreads();
+    total = s_w[kExpandThreads / 64 - 1];
+    const long long ex = x - v + (w ? s_w[w - 1] : 0);
+    __syncthreads();                                     // s_w is reused by the next call
+    return ex;
+}
+
 __global__ __launch_bounds__(kExpandThreads) void k_seed_expand(ScanArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    typedef hipcub::BlockScan<long long, kExpandThreads> Scan;
-    __shared__ typename Scan::TempStorage scan_tmp;
+    __shared__ long long s_w[kExpandThreads / 64];
     __shared__ long long s_base[2];                      // inside / edge bases, classes packed 32 | 32
     {   // the probe image (up to ~60 KB): 16-B loads, four in flight per thread (a dword loop waited
         // out one load latency per dword: ~50 us of fixed cost per launch, most of a small round's)
@@ -726,10 +754,9 @@ __global__ __launch_bounds__(kExpandThreads) void k_seed_expand(ScanArgs a) {
         }
     }
     {
-        long long ex, tin, tedge;
-        Scan(scan_tmp).ExclusiveSum(mine.in, ex, tin);
-        __syncthreads();
-        Scan(scan_tmp).ExclusiveSum(mine.edge, ex, tedge);
+        long long tin, tedge;
+        (void)expand_excl_sum(mine.in, tin, s_w);
+        (void)expand_excl_sum(mine.edge, tedge, s_w);
         if (threadIdx.x == 0) {
             long long b[2] = {0, 0};
             bool over = false;
@@ -756,12 +783,11 @@ __global__ __launch_bounds__(kExpandThreads) void k_seed_expand(ScanArgs a) {
             const uint4 r = i < cnt ? slab[i] : make_uint4(0u, 0u, 0u, 0u);
             const TaskCount c = i < cnt ? expand_hit<false>(a, lds, rank, estart, ent, ent2, r, TaskCount{0, 0})
                                         : TaskCount{0, 0};
-            long long exi, exe, ti, te;
-            Scan(scan_tmp).ExclusiveSum(c.in, exi, ti);
-            __syncthreads();
-            Scan(scan_tmp).ExclusiveSum(c.edge, exe, te);
+            long long ti, te;
+            const long long exi = expand_excl_sum(c.in, ti, s_w);
+            const long long exe = expand_excl_sum(c.edge, te, s_w);
             if (i < cnt) expand_hit<true>(a, lds, rank, estart, ent, ent2, r, TaskCount{s_base[0] + exi, s_base[1] + exe});
-            __syncthreads();                           // scan_tmp reused; s_base advanced
+            __syncthreads();                           // s_base advanced after every read of it
             if (threadIdx.x == 0) {
                 s_base[0] += ti;
                 s_base[1] += te;
