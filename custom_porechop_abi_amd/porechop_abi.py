@@ -361,11 +361,12 @@ def middle_adapter_list(matching_sets):
     return adapters, start_names, end_names
 
 
-def trimmed_bounds(reads):
+def trimmed_bounds(reads, seqs=None):
     """(start, length) of get_seq_with_start_end_adapters_trimmed() inside each read's seq, with
     Python's slice rules for seq[s:len(seq) - e] (a negative stop counts from the end, both ends
-    clipped) -- the trimmed reads as views of the untrimmed ones, no copy."""
-    n = np.fromiter((len(r.seq) for r in reads), np.int64, len(reads))
+    clipped) -- the trimmed reads as views of the untrimmed ones, no copy. `seqs`: the reads'
+    seq strings when the caller has them already."""
+    n = np.fromiter(map(len, [r.seq for r in reads] if seqs is None else seqs), np.int64, len(reads))
     s = np.fromiter((r.start_trim_amount for r in reads), np.int64, len(reads))
     e = np.fromiter((r.end_trim_amount for r in reads), np.int64, len(reads))
     a = np.minimum(s, n)
@@ -385,18 +386,32 @@ def scan_middles(seqs, adapter_seqs, middle_threshold, scoring_scheme_vals, devi
 
     Returns, per read, the ordered list of hits (adapter_index, full_identity, read_start,
     read_end) that nanopore_read.find_middle_adapters would record."""
+    hits = [[] for _ in range(len(seqs))]
+    for r, lst in _middle_hits_by_read(seqs, adapter_seqs, middle_threshold, scoring_scheme_vals, device, bounds):
+        hits[r] = lst
+    return hits
+
+
+def _middle_hits_by_read(seqs, adapter_seqs, middle_threshold, scoring_scheme_vals, device=0, bounds=None):
+    """scan_middles' hits as (read index, ordered hit list) for the reads that have any, in read
+    order: the drivers then touch only those reads (a few percent of a batch), not every read."""
     n = len(seqs)
-    hits = [[] for _ in range(n)]
     if n == 0 or not adapter_seqs:
-        return hits
+        return []
     pack = SeqPack(seqs) if bounds is None else SeqPack.windows(seqs, *bounds)
     views = pack.views(np.zeros(n, np.int64), pack.lengths)
     h = engine.middle_scan(views, adapter_seqs, scoring_scheme_vals, middle_threshold, device=device)
+    if not h.shape[1]:
+        return []
     full = engine.pid6(h[4], h[5])
     full[h[2] == -1] = 0.0
-    for r, a, s0, e0, f in zip(h[0].tolist(), h[1].tolist(), h[2].tolist(), h[3].tolist(), full.tolist()):
-        hits[r].append((a, f, s0, e0))
-    return hits
+    # a read's hits keep their discovery order (rounds come back round-major): stable sort by read
+    order = np.argsort(h[0], kind='stable')
+    rd = h[0][order]
+    rows = list(zip(h[1][order].tolist(), full[order].tolist(), h[2][order].tolist(), h[3][order].tolist()))
+    cut = (np.flatnonzero(np.diff(rd)) + 1).tolist()
+    lo, hi = [0] + cut, cut + [len(rows)]
+    return [(r, rows[a:b]) for r, a, b in zip(rd[lo].tolist(), lo, hi)]
 
 
 def find_adapters_in_read_middles(reads, matching_sets, verbosity, middle_threshold,
@@ -412,9 +427,14 @@ def find_adapters_in_read_middles(reads, matching_sets, verbosity, middle_thresh
         output_progress_line(0, read_count, print_dest)
     # the trimmed reads packed straight from the untrimmed strs (SeqPack.windows), no slices
     with _gc_paused():
-        all_hits = scan_middles([r.seq for r in reads], [a[1] for a in adapters], middle_threshold,
-                                scoring_scheme_vals, bounds=trimmed_bounds(reads))
-    for r, hits in zip(reads, all_hits):
+        seqs = [r.seq for r in reads]
+        by_read = _middle_hits_by_read(seqs, [a[1] for a in adapters], middle_threshold, scoring_scheme_vals,
+                                       bounds=trimmed_bounds(reads, seqs))
+    # only reads with hits change; at verbosity > 1 every read is visited in order, since a read
+    # with positions from an earlier call prints too (the reference's per-read loop, porechop_abi.py:487-495)
+    visit = [(i, h.get(i, ())) for h in (dict(by_read),) for i in range(read_count)] if verbosity > 1 else by_read
+    for i, hits in visit:
+        r = reads[i]
         for a, full, s0, e0 in hits:
             r._apply_middle_hit(adapters[a][0], full, s0, e0, extra_trim_good_side, extra_trim_bad_side,
                                 start_names, end_names)
