@@ -101,6 +101,7 @@ def parse():
 
 def main():
     args = parse()
+    print('GPU_MAX_HW_QUEUES in the environment: %s' % os.environ.get('GPU_MAX_HW_QUEUES', 'unset'), file=sys.stderr)
     if args.hw_queues > 0 and 'GPU_MAX_HW_QUEUES' not in os.environ:
         # hardware queues per process (HIP's default 4): the headline's smaller buckets run on one
         # stream each (--rest-overlap 2), and streams beyond the queue count share queues
@@ -510,7 +511,8 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
                                     'start+end windows of %d bp, + per-read trim decisions'
                                     % (n, len(sets), n_sa, n_ea, args.end_size)),
                        'reads_per_gpu': n, 'adapter_sets': len(sets), 'end_size': args.end_size,
-                       'scoring': list(sc), 'parallelism': 'dp%d (read shards)' % world},
+                       'scoring': list(sc), 'parallelism': 'dp%d (read shards)' % world,
+                       'hw_queues': os.environ.get('GPU_MAX_HW_QUEUES', 'HIP default')},
             'roofline': {'bound': 'valu', 'achieved': round(tops, 3), 'peak': round(VALU_PEAK_TOPS, 1),
                          'unit': 'Tops/s (int32 lane-ops)', 'frac': round(tops / VALU_PEAK_TOPS, 4),
                          'traffic': prof.get('traffic_bytes_per_launch') if prof and headline else None,
