@@ -716,27 +716,72 @@ __device__ __forceinline__ long long expand_excl_sum(long long v, long long &tot
     return ex;
 }
 
+// The probe image (up to ~60 KB) into LDS: 16-B loads, four in flight per thread (a dword loop
+// waited out one load latency per dword: ~50 us of fixed cost per launch, most of a small round's).
+__device__ __forceinline__ void expand_load_image(const ScanArgs &a, uint32_t *lds) {
+    const int n4 = a.tab_dw / 4;
+    const uint4 *src = reinterpret_cast<const uint4 *>(a.tabs);
+    uint4 *dst = reinterpret_cast<uint4 *>(lds);
+    constexpr int T = kExpandThreads;
+    for (int i = threadIdx.x; i < n4; i += 4 * T) {
+        const bool f1 = i + T < n4, f2 = i + 2 * T < n4, f3 = i + 3 * T < n4;
+        const uint4 v0 = src[i];
+        const uint4 v1 = src[f1 ? i + T : i], v2 = src[f2 ? i + 2 * T : i], v3 = src[f3 ? i + 3 * T : i];
+        dst[i] = v0;
+        if (f1) dst[i + T] = v1;
+        if (f2) dst[i + 2 * T] = v2;
+        if (f3) dst[i + 3 * T] = v3;
+    }
+    for (int i = 4 * n4 + (int)threadIdx.x; i < a.tab_dw; i += T) lds[i] = a.tabs[i];
+}
+
+// Two exclusive block sums at once (one set of barriers): s_w holds 2 x kExpandThreads / 64.
+__device__ __forceinline__ void expand_excl_sum2(long long v0, long long v1, long long &ex0, long long &ex1,
+                                                 long long &t0, long long &t1, long long *s_w) {
+    constexpr int NW = kExpandThreads / 64;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    long long x0 = v0, x1 = v1;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const long long y0 = __shfl_up(x0, d), y1 = __shfl_up(x1, d);
+        if (lane >= d) {
+            x0 += y0;
+            x1 += y1;
+        }
+    }
+    if (lane == 63) {
+        s_w[w] = x0;
+        s_w[NW + w] = x1;
+    }
+    __syncthreads();
+    if (w == 0) {
+        long long y0 = lane < NW ? s_w[lane] : 0, y1 = lane < NW ? s_w[NW + lane] : 0;
+#pragma unroll
+        for (int d = 1; d < NW; d <<= 1) {
+            const long long z0 = __shfl_up(y0, d), z1 = __shfl_up(y1, d);
+            if (lane >= d) {
+                y0 += z0;
+                y1 += z1;
+            }
+        }
+        if (lane < NW) {
+            s_w[lane] = y0;
+            s_w[NW + lane] = y1;
+        }
+    }
+    __syncthreads();
+    t0 = s_w[NW - 1];
+    t1 = s_w[2 * NW - 1];
+    ex0 = x0 - v0 + (w ? s_w[w - 1] : 0);
+    ex1 = x1 - v1 + (w ? s_w[NW + w - 1] : 0);
+    __syncthreads();                                     // s_w is reused by the next call
+}
+
 __global__ __launch_bounds__(kExpandThreads) void k_seed_expand(ScanArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     __shared__ long long s_w[kExpandThreads / 64];
     __shared__ long long s_base[2];                      // inside / edge bases, classes packed 32 | 32
-    {   // the probe image (up to ~60 KB): 16-B loads, four in flight per thread (a dword loop waited
-        // out one load latency per dword: ~50 us of fixed cost per launch, most of a small round's)
-        const int n4 = a.tab_dw / 4;
-        const uint4 *src = reinterpret_cast<const uint4 *>(a.tabs);
-        uint4 *dst = reinterpret_cast<uint4 *>(lds);
-        constexpr int T = kExpandThreads;
-        for (int i = threadIdx.x; i < n4; i += 4 * T) {
-            const bool f1 = i + T < n4, f2 = i + 2 * T < n4, f3 = i + 3 * T < n4;
-            const uint4 v0 = src[i];
-            const uint4 v1 = src[f1 ? i + T : i], v2 = src[f2 ? i + 2 * T : i], v3 = src[f3 ? i + 3 * T : i];
-            dst[i] = v0;
-            if (f1) dst[i + T] = v1;
-            if (f2) dst[i + 2 * T] = v2;
-            if (f3) dst[i + 3 * T] = v3;
-        }
-        for (int i = 4 * n4 + (int)threadIdx.x; i < a.tab_dw; i += T) lds[i] = a.tabs[i];
-    }
+    expand_load_image(a, lds);
     __syncthreads();
     const uint16_t *rank = reinterpret_cast<const uint16_t *>(lds + a.rank_off);
     const uint16_t *estart = reinterpret_cast<const uint16_t *>(lds + a.estart_off);
@@ -794,6 +839,100 @@ __global__ __launch_bounds__(kExpandThreads) void k_seed_expand(ScanArgs a) {
             }
             __syncthreads();
         }
+    }
+}
+
+// One-pass expansion (r04, PCABI_EXPAND_PASSES=1): a block's slabs (blockIdx.x + k * gridDim.x) in
+// groups of kExpandGroup are one flat run of hits (a prefix of their counts in LDS), taken
+// kExpandHits per thread at a time: each hit's probe walk counts its tasks (kept in registers), a
+// block scan places them, one atomic per class and pass takes the block's place, and the second
+// walk writes. The two-pass kernel walks every hit three times and runs a slab at a time (~1.1 k
+// hits per slab in round 1 of 8 kb reads: a 1024-thread pass half idle, two scans per slab).
+constexpr int kExpandHits = 2;                 // 4 needs 74 VGPRs: one block per CU instead of two
+constexpr int kExpandGroup = 64;
+__global__ __launch_bounds__(kExpandThreads) void k_seed_expand1(ScanArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    __shared__ long long s_w[2 * (kExpandThreads / 64)];
+    __shared__ long long s_base[2];
+    __shared__ int s_pre[kExpandGroup + 1];
+    expand_load_image(a, lds);
+    __syncthreads();
+    const uint16_t *rank = reinterpret_cast<const uint16_t *>(lds + a.rank_off);
+    const uint16_t *estart = reinterpret_cast<const uint16_t *>(lds + a.estart_off);
+    const int32_t *ent = reinterpret_cast<const int32_t *>(lds + a.ent_off);
+    const uint32_t *ent2 = lds + a.ent2_off;
+    const int G = (int)gridDim.x, b = (int)blockIdx.x;
+    const int mine = b < a.n_slab ? (a.n_slab - b + G - 1) / G : 0;     // block-uniform
+    for (int g0 = 0; g0 < mine; g0 += kExpandGroup) {
+        const int ng = min(kExpandGroup, mine - g0);
+        if (threadIdx.x < 64) {                          // wave 0: inclusive prefix of the group's counts
+            const int l = (int)threadIdx.x;
+            int x = l < ng ? a.raw_cnt[b + (g0 + l) * G] : 0;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int y = __shfl_up(x, d);
+                if (l >= d) x += y;
+            }
+            s_pre[l + 1] = x;
+            if (l == 0) s_pre[0] = 0;
+        }
+        __syncthreads();
+        const int total = s_pre[ng];
+        for (int base = 0; base < total; base += kExpandHits * kExpandThreads) {
+            uint4 r[kExpandHits];
+            uint64_t pc[kExpandHits];                    // a hit's four counts in 16 bits each (a hit
+                                                         // has fewer tasks than the table has entries)
+            long long si = 0, se = 0;
+#pragma unroll
+            for (int j = 0; j < kExpandHits; ++j) {
+                const int f = base + j * kExpandThreads + (int)threadIdx.x;
+                pc[j] = 0;
+                r[j] = make_uint4(0u, 0u, 0u, 0u);
+                if (f < total) {
+                    int lo = 0, hi = ng - 1;             // the slab k holding f: s_pre[k] <= f < s_pre[k + 1]
+                    while (lo < hi) {
+                        const int m = (lo + hi + 1) >> 1;
+                        if (s_pre[m] <= f) lo = m;
+                        else hi = m - 1;
+                    }
+                    r[j] = a.raw[(int64_t)(b + (g0 + lo) * G) * a.slab + (f - s_pre[lo])];
+                    const TaskCount c = expand_hit<false>(a, lds, rank, estart, ent, ent2, r[j], TaskCount{0, 0});
+                    si += c.in;
+                    se += c.edge;
+                    pc[j] = (uint64_t)(c.in & 0xFFFF) | (uint64_t)((c.in >> 32) & 0xFFFF) << 16 |
+                            (uint64_t)(c.edge & 0xFFFF) << 32 | (uint64_t)((c.edge >> 32) & 0xFFFF) << 48;
+                }
+            }
+            long long exi, exe, ti, te;
+            expand_excl_sum2(si, se, exi, exe, ti, te, s_w);
+            if (threadIdx.x == 0) {
+                long long bb[2] = {0, 0};
+                bool over = false;
+                for (int cl = 0; cl < kCls; ++cl) {
+                    const long long xi = (ti >> (32 * cl)) & 0xFFFFFFFFll, xe = (te >> (32 * cl)) & 0xFFFFFFFFll;
+                    const long long bi = xi ? atomicAdd(&a.cnt[cl], (int)xi) : 0;
+                    const long long be = xe ? atomicAdd(&a.cnt[kCls + cl], (int)xe) : 0;
+                    bb[0] |= bi << (32 * cl);
+                    bb[1] |= be << (32 * cl);
+                    over |= bi + xi > a.cap || be + xe > a.ecap;
+                }
+                s_base[0] = bb[0];
+                s_base[1] = bb[1];
+                if (over) atomicOr(&a.flags[1], 1);
+            }
+            __syncthreads();
+            TaskCount at{s_base[0] + exi, s_base[1] + exe};
+#pragma unroll
+            for (int j = 0; j < kExpandHits; ++j) {
+                if (pc[j]) {                             // hits without tasks write nothing
+                    expand_hit<true>(a, lds, rank, estart, ent, ent2, r[j], at);
+                    at.in += (long long)(pc[j] & 0xFFFF) | (long long)((pc[j] >> 16) & 0xFFFF) << 32;
+                    at.edge += (long long)((pc[j] >> 32) & 0xFFFF) | (long long)(pc[j] >> 48) << 32;
+                }
+            }
+            __syncthreads();                             // s_base is rewritten by the next pass
+        }
+        __syncthreads();                                 // s_pre likewise
     }
 }
 
@@ -1673,7 +1812,13 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
     else
         hipLaunchKernelGGL(k_seed_scan_bits, dim3(grid), dim3(256), 4 * (size_t)A.bits_dw + 4, st, A);
     if (s->pev) SD_TRY(hipEventRecord(s->pev[1], st));
-    hipLaunchKernelGGL(k_seed_expand, dim3(s->expand_blocks), dim3(kExpandThreads), s->lds_bytes, st, A);
+    {   // PCABI_EXPAND_PASSES=1: the one-pass expansion (read per launch: tests switch it)
+        const char *ep = std::getenv("PCABI_EXPAND_PASSES");
+        if (ep && ep[0] == '1')
+            hipLaunchKernelGGL(k_seed_expand1, dim3(s->expand_blocks), dim3(kExpandThreads), s->lds_bytes, st, A);
+        else
+            hipLaunchKernelGGL(k_seed_expand, dim3(s->expand_blocks), dim3(kExpandThreads), s->lds_bytes, st, A);
+    }
     if (s->pev) SD_TRY(hipEventRecord(s->pev[2], st));
     SD_TRY(hipGetLastError());
     if (tasks) return 0;                                // the caller launches the bands (host counts)

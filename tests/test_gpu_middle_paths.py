@@ -231,6 +231,44 @@ def test_seed_scan_bytemap_equals_bitmap_scan(gpu_lib, monkeypatch, thr):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('thr', [90.0, 85.0])
+def test_seed_expand_one_pass(gpu_lib, monkeypatch, thr):
+    """k_seed_expand1 (PCABI_EXPAND_PASSES=1: a block's slabs as one flat run of hits, two per
+    thread and pass, one walk to count and one to write) vs the two-pass k_seed_expand: the same
+    raw hits, band tasks and candidate-DP cells per scan (pcabi_scan_profile) and the oracle's hits,
+    on reads with N runs and ragged ends; then with task regions far too small (every pass flags
+    the overflow, the round grows them and reruns)."""
+    from custom_porechop_abi_amd import engine
+    rng = random.Random(7 + int(thr))
+    reads = _reads(57 + int(thr), 120, 3000, thr)
+    for k in range(0, len(reads), 4):
+        r = list(reads[k])
+        p = rng.randrange(len(r))
+        r[p:p + 5] = 'NNNNN'
+        reads[k] = ''.join(r)[:len(reads[k])]
+    reads += [_rand_seq(rng, n) for n in (1, 7, 8, 33, 41)]
+    pack = engine.SeqPack(reads)
+    views = pack.views(np.zeros(len(reads), np.int64), pack.lengths)
+    exp = _sorted(oracle_lib.middle_scan_threaded(views, ADPS, SC, thr))
+    monkeypatch.setenv('PCABI_MIDDLE_SEEDS', '2')
+    prof = {}
+    for mode in ('0', '1'):
+        monkeypatch.setenv('PCABI_EXPAND_PASSES', mode)
+        prof[mode] = np.zeros(16, np.float64)
+        got = _dev_scan(gpu_lib, views, ADPS, SC, thr, profile=prof[mode])
+        assert np.array_equal(_sorted(got), exp), 'passes=%s' % mode
+    assert prof['1'][11] > 0
+    assert np.array_equal(prof['1'][7:15], prof['0'][7:15]), (prof['1'][7:15], prof['0'][7:15])
+    monkeypatch.setenv('PCABI_EXPAND_PASSES', '1')
+    monkeypatch.setenv('PCABI_MIDDLE_INIT_CAPS', '0,64,0')
+    n0, _ = _requeues(gpu_lib)
+    got = _dev_scan(gpu_lib, views, ADPS, SC, thr)
+    n1, flags = _requeues(gpu_lib)
+    assert n1 > n0 and flags & 2, (n1 - n0, flags)
+    assert np.array_equal(_sorted(got), exp)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('split', ['2', '4'])
 @pytest.mark.parametrize('windows', ['0', '1'])
 def test_chunk_dp_row_split(gpu_lib, monkeypatch, reads_8kb, split, windows):

@@ -9,8 +9,8 @@ mkdir -p $OUT
 cd $R
 timeout -k 10 700 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_gpu_middle_paths.py tests/test_gpu_parity.py -k "middle or seed or windows or overflow or scan or split" > $OUT/pytest_mid.log 2>&1 || { echo "pytest failed rc=$?"; grep -E "FAILED|Error" $OUT/pytest_mid.log | head -20; tail -30 $OUT/pytest_mid.log; exit 1; }
 tail -2 $OUT/pytest_mid.log
-for V in base w6 s2 s4 base s2; do
-  case $V in base) E="PCABI_NOOP=1";; w6) E="PCABI_CHUNK_WAVES=6";; s2) E="PCABI_CHUNK_SPLIT=2";; s4) E="PCABI_CHUNK_SPLIT=4";; esac
+for V in base e1 w6 s2 s4 base e1 s2; do
+  case $V in base) E="PCABI_NOOP=1";; e1) E="PCABI_EXPAND_PASSES=1";; w6) E="PCABI_CHUNK_WAVES=6";; s2) E="PCABI_CHUNK_SPLIT=2";; s4) E="PCABI_CHUNK_SPLIT=4";; esac
   env $E timeout -k 10 300 python bench.py --workload middle --steps 8 --warmup 2 --cpu-sample 0 > $OUT/mid_$V.json 2> $OUT/mid_$V.err || { echo "mid $V failed rc=$?"; tail -20 $OUT/mid_$V.err; exit 1; }
   python -c "import json; d=json.load(open('$OUT/mid_$V.json')); print('mid $V', d['middle_ms_per_step'], json.dumps(d['middle_phases']['ms']), d['parity_spot_check']['identical'])"
 done
