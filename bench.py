@@ -82,14 +82,16 @@ def parse():
                     help='drivers: reads whose decisions are compared with the same drivers over the oracle')
     ap.add_argument('--check-phase-check', type=int, default=400,
                     help='check_phase: check reads whose device reduction is compared with the oracle')
-    ap.add_argument('--rj-check-overlap', type=int, default=0,
-                    help='reference_job: 1 = the set search\'s two sides side by side (stream2); 0 = one after the '
-                         'other (each side\'s dominant launch then has the GPU to itself, the roofline\'s events)')
+    ap.add_argument('--rj-check-overlap', type=int, default=1,
+                    help='reference_job: 1 = the set search\'s two sides side by side (stream2; r04 A/B: 5.13 vs '
+                         '5.23 ms per step); 0 = one after the other (each side\'s dominant launch then has the GPU '
+                         'to itself, the roofline\'s events)')
     ap.add_argument('--rest-overlap', type=int, default=1,
                     help='headline: 2 = after both dominant launches, both sides\' smaller buckets each on its own '
                          'stream; 1 = the two sides\' calls side by side; 0 = after each side\'s dominant launch')
-    ap.add_argument('--hw-queues', type=int, default=8,
-                    help='GPU_MAX_HW_QUEUES for this process when the environment does not set it (0: HIP default)')
+    ap.add_argument('--hw-queues', type=int, default=0,
+                    help='GPU_MAX_HW_QUEUES for this process when the environment does not set it (0: HIP default, '
+                         '4; r04 A/B with 8: headline 8.05 vs 7.61 ms, reference job 5.85 vs 5.23 ms)')
     ap.add_argument('--only-subs', default='', help='comma-separated sub-record names to run (default: all)')
     ap.add_argument('--sub', type=int, default=1,
                     help='endtrim at N=1: also time the middle workload (configs[2]) and the host-buffer path '
@@ -994,7 +996,9 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
             'roofline': {'bound': 'valu', 'kernel': 'the set search\'s largest register bucket (k_align<24, true, 6>)',
                          'achieved': round(tops, 3), 'peak': round(VALU_PEAK_TOPS, 1), 'unit': 'Tops/s (int32 lane-ops)',
                          'frac': round(tops / VALU_PEAK_TOPS, 4), 'launch_ms': round(dom_ms, 4),
-                         'cells_per_launch': int(np.mean(dom_cells)), 'ops_per_cell': OPS_PER_CELL},
+                         'cells_per_launch': int(np.mean(dom_cells)), 'ops_per_cell': OPS_PER_CELL,
+                         'schedule': ('both sides\' cross products side by side: the launch shares the GPU'
+                                      if args.rj_check_overlap else 'each side\'s cross product alone')},
             'dtype': 'int32', 'data': 'synthetic (seeded ONT-like reads, mean %d bp)' % args.mean_len,
             'config': {'workload': 'reference job: set search (%d check reads x %d sets, %d + %d distinct sequences), '
                                    'end trim + middle scan of %d reads/GPU with the kept sets' % (

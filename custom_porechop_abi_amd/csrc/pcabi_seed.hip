@@ -596,25 +596,50 @@ __global__ __launch_bounds__(kScanThreads) void k_seed_scan(ScanArgs a) {
     }
 }
 
-// The round's segment space in one block: each thread sums a contiguous run of reads' segment
-// counts, a block scan places the runs, the threads write their prefixes (reads past n_dev: none).
+// The round's segment space in one block, in tiles of kSegCumThreads x kSegCumItems reads: each
+// thread takes kSegCumItems consecutive reads of the tile (their loads all in flight, the next
+// tile's issued before this one's scan), a block scan places the threads' sums, a carry runs
+// across tiles (reads past n_dev: none). r04 first summed one contiguous run per thread with one
+// load at a time: ~100 dependent load latencies for 100 k reads, ~0.1 ms.
 constexpr int kSegCumThreads = 1024;
+constexpr int kSegCumItems = 16;
+__device__ __forceinline__ void seg_cum_load(const int32_t *v_len, int64_t nr, int64_t t0, int (&x)[kSegCumItems]) {
+    const int64_t b = t0 + (int64_t)threadIdx.x * kSegCumItems;
+#pragma unroll
+    for (int i = 0; i < kSegCumItems; ++i) x[i] = b + i < nr ? max(v_len[b + i], 0) : 0;
+}
 __global__ __launch_bounds__(kSegCumThreads) void k_seg_cum(const int32_t *v_len, const int32_t *n_dev, int64_t n,
                                                             int64_t *seg_cum) {
     typedef hipcub::BlockScan<long long, kSegCumThreads> Scan;
     __shared__ typename Scan::TempStorage tmp;
+    constexpr int64_t kTile = (int64_t)kSegCumThreads * kSegCumItems;
     const int64_t nr = dev_count(n_dev, n);
-    const int64_t per = (nr + kSegCumThreads - 1) / kSegCumThreads;
-    const int64_t lo = min((int64_t)threadIdx.x * per, nr), hi = min(lo + per, nr);
-    long long sum = 0;
-    for (int64_t k = lo; k < hi; ++k) sum += ((int64_t)max(v_len[k], 0) + kSeg - 1) / kSeg;
-    long long ex = 0, total = 0;
-    Scan(tmp).ExclusiveSum(sum, ex, total);
-    for (int64_t k = lo; k < hi; ++k) {
-        seg_cum[k] = ex;
-        ex += ((int64_t)max(v_len[k], 0) + kSeg - 1) / kSeg;
+    int cur[kSegCumItems], nxt[kSegCumItems];
+    seg_cum_load(v_len, nr, 0, cur);
+    long long carry = 0;
+    for (int64_t t0 = 0; t0 < nr; t0 += kTile) {
+        if (t0 + kTile < nr) seg_cum_load(v_len, nr, t0 + kTile, nxt);
+        long long sum = 0;
+#pragma unroll
+        for (int i = 0; i < kSegCumItems; ++i) {
+            cur[i] = (cur[i] + kSeg - 1) / kSeg;
+            sum += cur[i];
+        }
+        long long ex = 0, total = 0;
+        Scan(tmp).ExclusiveSum(sum, ex, total);
+        ex += carry;
+        const int64_t b = t0 + (int64_t)threadIdx.x * kSegCumItems;
+#pragma unroll
+        for (int i = 0; i < kSegCumItems; ++i) {
+            if (b + i < nr) seg_cum[b + i] = ex;
+            ex += cur[i];
+        }
+        carry += total;
+        __syncthreads();                                 // tmp is reused by the next tile's scan
+#pragma unroll
+        for (int i = 0; i < kSegCumItems; ++i) cur[i] = nxt[i];
     }
-    if (threadIdx.x == 0) seg_cum[nr] = total;
+    if (threadIdx.x == 0) seg_cum[nr] = carry;
 }
 
 // Resident blocks striding over the slabs: the probe entries of the slabs' raw hits become tasks.
