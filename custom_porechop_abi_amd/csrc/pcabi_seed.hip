@@ -596,52 +596,6 @@ __global__ __launch_bounds__(kScanThreads) void k_seed_scan(ScanArgs a) {
     }
 }
 
-// The round's segment space in one block, in tiles of kSegCumThreads x kSegCumItems reads: each
-// thread takes kSegCumItems consecutive reads of the tile (their loads all in flight, the next
-// tile's issued before this one's scan), a block scan places the threads' sums, a carry runs
-// across tiles (reads past n_dev: none). r04 first summed one contiguous run per thread with one
-// load at a time: ~100 dependent load latencies for 100 k reads, ~0.1 ms.
-constexpr int kSegCumThreads = 1024;
-constexpr int kSegCumItems = 16;
-__device__ __forceinline__ void seg_cum_load(const int32_t *v_len, int64_t nr, int64_t t0, int (&x)[kSegCumItems]) {
-    const int64_t b = t0 + (int64_t)threadIdx.x * kSegCumItems;
-#pragma unroll
-    for (int i = 0; i < kSegCumItems; ++i) x[i] = b + i < nr ? max(v_len[b + i], 0) : 0;
-}
-__global__ __launch_bounds__(kSegCumThreads) void k_seg_cum(const int32_t *v_len, const int32_t *n_dev, int64_t n,
-                                                            int64_t *seg_cum) {
-    typedef hipcub::BlockScan<long long, kSegCumThreads> Scan;
-    __shared__ typename Scan::TempStorage tmp;
-    constexpr int64_t kTile = (int64_t)kSegCumThreads * kSegCumItems;
-    const int64_t nr = dev_count(n_dev, n);
-    int cur[kSegCumItems], nxt[kSegCumItems];
-    seg_cum_load(v_len, nr, 0, cur);
-    long long carry = 0;
-    for (int64_t t0 = 0; t0 < nr; t0 += kTile) {
-        if (t0 + kTile < nr) seg_cum_load(v_len, nr, t0 + kTile, nxt);
-        long long sum = 0;
-#pragma unroll
-        for (int i = 0; i < kSegCumItems; ++i) {
-            cur[i] = (cur[i] + kSeg - 1) / kSeg;
-            sum += cur[i];
-        }
-        long long ex = 0, total = 0;
-        Scan(tmp).ExclusiveSum(sum, ex, total);
-        ex += carry;
-        const int64_t b = t0 + (int64_t)threadIdx.x * kSegCumItems;
-#pragma unroll
-        for (int i = 0; i < kSegCumItems; ++i) {
-            if (b + i < nr) seg_cum[b + i] = ex;
-            ex += cur[i];
-        }
-        carry += total;
-        __syncthreads();                                 // tmp is reused by the next tile's scan
-#pragma unroll
-        for (int i = 0; i < kSegCumItems; ++i) cur[i] = nxt[i];
-    }
-    if (threadIdx.x == 0) seg_cum[nr] = carry;
-}
-
 // Resident blocks striding over the slabs: the probe entries of the slabs' raw hits become tasks.
 // The raw hits carry their 8-mer and valid run, so nothing here touches the reads: the slabs, the
 // LDS image and the task stores. A block first counts its tasks per class (all its slabs) and
@@ -867,7 +821,7 @@ __global__ __launch_bounds__(kExpandThreads) void k_seed_expand(ScanArgs a) {
     }
 }
 
-// One-pass expansion (r04, PCABI_EXPAND_PASSES=1): a block's slabs (blockIdx.x + k * gridDim.x) in
+// One-pass expansion (r04, the default): a block's slabs (blockIdx.x + k * gridDim.x) in
 // groups of kExpandGroup are one flat run of hits (a prefix of their counts in LDS), taken
 // kExpandHits per thread at a time: each hit's probe walk counts its tasks (kept in registers), a
 // block scan places them, one atomic per class and pass takes the block's place, and the second
@@ -1813,13 +1767,11 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
     A.cap = s->cap;
     A.ecap = s->ecap;
     if (int rc = s->ccnt.ensure(8)) return rc;
-    // the scan's segment space: seg_cum[r] = segments before read r, seg_cum[n_dev] = all -- one
-    // block up to 256 k reads (hipcub's device scan takes two launches, ~20 us a round), else
-    // hipcub's (its entries past n_dev repeat the total)
+    // the scan's segment space: seg_cum[r] = segments before read r, seg_cum[n_dev] = all (entries
+    // past n_dev repeat the total). r04 measured one-block scans against hipcub's device scan (two
+    // launches): 40 us per round against ~11-23, so hipcub's stays.
     if (int rc = s->segcum.ensure(sizeof(int64_t) * (size_t)(n + 1))) return rc;
-    if (n <= (int64_t)kSegCumThreads * 256) {
-        hipLaunchKernelGGL(k_seg_cum, dim3(1), dim3(kSegCumThreads), 0, st, v_len, n_dev, n, (int64_t *)s->segcum.p);
-    } else {
+    {
         hipcub::CountingInputIterator<int64_t> idx(0);
         hipcub::TransformInputIterator<int64_t, SegCount, hipcub::CountingInputIterator<int64_t>> segs(
             idx, SegCount{v_len, n_dev, n});
@@ -1837,12 +1789,13 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
     else
         hipLaunchKernelGGL(k_seed_scan_bits, dim3(grid), dim3(256), 4 * (size_t)A.bits_dw + 4, st, A);
     if (s->pev) SD_TRY(hipEventRecord(s->pev[1], st));
-    {   // PCABI_EXPAND_PASSES=1: the one-pass expansion (read per launch: tests switch it)
+    {   // the one-pass expansion (r04: 0.25 -> 0.18 ms at 8 kb); PCABI_EXPAND_PASSES=2 runs the
+        // two-pass kernel (read per launch: tests switch it)
         const char *ep = std::getenv("PCABI_EXPAND_PASSES");
-        if (ep && ep[0] == '1')
-            hipLaunchKernelGGL(k_seed_expand1, dim3(s->expand_blocks), dim3(kExpandThreads), s->lds_bytes, st, A);
-        else
+        if (ep && ep[0] == '2')
             hipLaunchKernelGGL(k_seed_expand, dim3(s->expand_blocks), dim3(kExpandThreads), s->lds_bytes, st, A);
+        else
+            hipLaunchKernelGGL(k_seed_expand1, dim3(s->expand_blocks), dim3(kExpandThreads), s->lds_bytes, st, A);
     }
     if (s->pev) SD_TRY(hipEventRecord(s->pev[2], st));
     SD_TRY(hipGetLastError());

@@ -233,8 +233,8 @@ def test_seed_scan_bytemap_equals_bitmap_scan(gpu_lib, monkeypatch, thr):
 @pytest.mark.gpu
 @pytest.mark.parametrize('thr', [90.0, 85.0])
 def test_seed_expand_one_pass(gpu_lib, monkeypatch, thr):
-    """k_seed_expand1 (PCABI_EXPAND_PASSES=1: a block's slabs as one flat run of hits, two per
-    thread and pass, one walk to count and one to write) vs the two-pass k_seed_expand: the same
+    """k_seed_expand1 (the default: a block's slabs as one flat run of hits, two per thread and
+    pass, one walk to count and one to write) vs the two-pass k_seed_expand (PCABI_EXPAND_PASSES=2): the same
     raw hits, band tasks and candidate-DP cells per scan (pcabi_scan_profile) and the oracle's hits,
     on reads with N runs and ragged ends; then with task regions far too small (every pass flags
     the overflow, the round grows them and reruns)."""
@@ -252,13 +252,13 @@ def test_seed_expand_one_pass(gpu_lib, monkeypatch, thr):
     exp = _sorted(oracle_lib.middle_scan_threaded(views, ADPS, SC, thr))
     monkeypatch.setenv('PCABI_MIDDLE_SEEDS', '2')
     prof = {}
-    for mode in ('0', '1'):
+    for mode in ('2', '1'):
         monkeypatch.setenv('PCABI_EXPAND_PASSES', mode)
         prof[mode] = np.zeros(16, np.float64)
         got = _dev_scan(gpu_lib, views, ADPS, SC, thr, profile=prof[mode])
         assert np.array_equal(_sorted(got), exp), 'passes=%s' % mode
     assert prof['1'][11] > 0
-    assert np.array_equal(prof['1'][7:15], prof['0'][7:15]), (prof['1'][7:15], prof['0'][7:15])
+    assert np.array_equal(prof['1'][7:15], prof['2'][7:15]), (prof['1'][7:15], prof['2'][7:15])
     monkeypatch.setenv('PCABI_EXPAND_PASSES', '1')
     monkeypatch.setenv('PCABI_MIDDLE_INIT_CAPS', '0,64,0')
     n0, _ = _requeues(gpu_lib)
