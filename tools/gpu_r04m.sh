@@ -8,6 +8,8 @@ mkdir -p $OUT
 cd $R
 timeout -k 10 60 tools/launch_bench > $OUT/launch_bench.txt 2>&1 || { echo "launch_bench failed rc=$?"; cat $OUT/launch_bench.txt; exit 1; }
 cat $OUT/launch_bench.txt
+timeout -k 10 60 tools/queue_probe > $OUT/queue_probe.txt 2>&1 || { echo "queue_probe failed rc=$?"; cat $OUT/queue_probe.txt; exit 1; }
+cat $OUT/queue_probe.txt
 for W in 0 1 0 1; do
   PCABI_MIDDLE_WINDOWS=$W timeout -k 10 300 python bench.py --only-subs reference_job --steps 6 --warmup 2 --cpu-sample 0 > $OUT/rj_w$W.json 2> $OUT/rj_w$W.err || { echo "rj w$W failed rc=$?"; tail -20 $OUT/rj_w$W.err; exit 1; }
   python -c "import json; d=json.load(open('$OUT/rj_w$W.json'))['reference_job']; print('rj windows=$W', d['ms_per_step'], json.dumps(d['ms_per_phase']), d['parity_spot_check']['middle'])"
