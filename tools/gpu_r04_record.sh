@@ -5,7 +5,7 @@
 # stopping at the first failure.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$R/gpurun_out/r04
+OUT=$R/gpurun_out/${TAG:-r04}
 mkdir -p $OUT
 cd $R
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
