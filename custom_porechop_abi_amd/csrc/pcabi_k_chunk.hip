@@ -18,6 +18,25 @@ int dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st, bool ta
             dispatch_split_chunk(kBuckets[b].rpl, ks, p, affine, tagged && affine && kBuckets[b].rpl <= 32, st))
             return 0;
     }
+    // PCABI_CHUNK_WPB=1 (A/B): one-wave blocks for the device-planned run-tagged / packed buckets,
+    // 4x the blocks (the same wave slots)
+    const char *ewpb = std::getenv("PCABI_CHUNK_WPB");
+    const bool wpb1 = p.dev_waves && ewpb && ewpb[0] == '1' && kBuckets[b].kind == FAST && affine;
+    const dim3 grid1(grid.x * 4);
+    if (wpb1 && tagged && kBuckets[b].rpl <= 32) {
+        switch (kBuckets[b].rpl) {
+#define C(R) case R: hipLaunchKernelGGL((k_align_chunk<R, true, TAGGED, 1, 1>), grid1, dim3(64), 0, st, p); return 0;
+        C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32)
+#undef C
+        }
+    }
+    if (wpb1 && !tagged) {
+        switch (kBuckets[b].rpl) {
+#define C(R) case R: hipLaunchKernelGGL((k_align_chunk<R, true, PACKED, 1, 1>), grid1, dim3(64), 0, st, p); return 0;
+        C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32) C(36) C(40) C(44) C(48) C(52) C(56) C(60) C(64)
+#undef C
+        }
+    }
     if (tagged && affine && kBuckets[b].kind == FAST && kBuckets[b].rpl <= 32) {
         // the run-tagged layout (9 VALU ops per cell instead of 10), as the end-window buckets
         const char *ew = std::getenv("PCABI_CHUNK_WAVES");

@@ -381,13 +381,15 @@ __device__ __forceinline__ void chunk_wave(const KParams &p, int64_t wave, bool 
 
 // W: the launch's minimum waves per SIMD (amdgpu_waves_per_eu; 1 = no bound): the run-tagged
 // <= 28-row chunk kernels also come with W = 6 (80 VGPRs instead of 89: 6 waves per SIMD instead of
-// 5), chosen by PCABI_CHUNK_WAVES=6 at dispatch (A/B).
-template <int RPL, bool AFFINE, int KIND, int W = 1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k_align_chunk(KParams p) {
-    __shared__ __attribute__((aligned(16))) int32_t tab[4 * wave_tab_ints<KIND, RPL>()];
+// 5), chosen by PCABI_CHUNK_WAVES=6 at dispatch (A/B). WPB: waves per block -- with 4, a block's
+// waves meet at every table barrier and the block holds its CU slot until its slowest wave (the
+// longest chunk of its 4 x 64 tasks) ends; with 1 (PCABI_CHUNK_WPB=1, A/B) every wave retires alone.
+template <int RPL, bool AFFINE, int KIND, int W = 1, int WPB = 4>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(W))) void k_align_chunk(KParams p) {
+    __shared__ __attribute__((aligned(16))) int32_t tab[WPB * wave_tab_ints<KIND, RPL>()];
     int32_t *wave_tab = tab + (threadIdx.x >> 6) * wave_tab_ints<KIND, RPL>();
     if (!p.dev_waves) {
-        int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+        int64_t wave = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
         const bool live = wave < p.n_waves;        // dead waves still join the table barrier
         if (!live) wave = p.n_waves - 1;
         chunk_wave<RPL, AFFINE, KIND>(p, wave, live, wave_tab);
@@ -397,8 +399,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
     // (block-uniform trip count: every wave joins every table barrier); a wave rewrites only its
     // own table, after its own reads of the previous one
     const int64_t w0 = p.dev_waves[0], nw = p.dev_waves[1];
-    for (int64_t wb = blockIdx.x; wb * 4 < nw; wb += gridDim.x) {
-        int64_t wave = wb * 4 + (threadIdx.x >> 6);
+    for (int64_t wb = blockIdx.x; wb * WPB < nw; wb += gridDim.x) {
+        int64_t wave = wb * WPB + (threadIdx.x >> 6);
         const bool live = wave < nw;
         if (!live) wave = nw - 1;
         chunk_wave<RPL, AFFINE, KIND>(p, w0 + wave, live, wave_tab);

@@ -287,6 +287,20 @@ def test_chunk_dp_row_split(gpu_lib, monkeypatch, reads_8kb, split, windows):
     assert np.array_equal(_sorted(got2), exp)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize('windows', ['0', '1'])
+def test_chunk_dp_one_wave_blocks(gpu_lib, monkeypatch, reads_8kb, windows):
+    """PCABI_CHUNK_WPB=1: the device-planned chunk launches in one-wave blocks (no table barrier
+    shared by four waves) -- the scan equals the oracle, whole-read chunks and candidate windows."""
+    from custom_porechop_abi_amd import engine
+    views, exp = reads_8kb
+    monkeypatch.setenv('PCABI_MIDDLE_SEEDS', '2')
+    monkeypatch.setenv('PCABI_MIDDLE_WINDOWS', windows)
+    monkeypatch.setenv('PCABI_CHUNK_WPB', '1')
+    got = engine.middle_scan(views, ADPS, SC, 90.0)
+    assert np.array_equal(_sorted(got), exp)
+
+
 # ---- k_barcode_call at the configs[3] width ---------------------------------------------------
 
 def _pid6(m, l):
