@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU-box script (r04): one-wave chunk blocks (PCABI_CHUNK_WPB=1) parity and A/B on the middle step,
-# then the full record (tools/gpu_r04_record.sh, TAG=r04final).
+# and the reference job with it.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/r04n
@@ -15,4 +15,3 @@ for V in base wpb1 base wpb1; do
 done
 env PCABI_CHUNK_WPB=1 timeout -k 10 300 python bench.py --only-subs reference_job --steps 6 --warmup 2 --cpu-sample 0 > $OUT/rj_wpb1.json 2> $OUT/rj_wpb1.err || { echo "rj wpb1 failed rc=$?"; tail -20 $OUT/rj_wpb1.err; exit 1; }
 python -c "import json; d=json.load(open('$OUT/rj_wpb1.json'))['reference_job']; print('rj wpb1', d['ms_per_step'], json.dumps(d['ms_per_phase']))"
-TAG=r04final bash tools/gpu_r04_record.sh
