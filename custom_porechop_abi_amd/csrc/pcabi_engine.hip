@@ -16,6 +16,7 @@
 //   k_first_hit                 middle-scan round 1: first adapter over the threshold per read
 //                               (nanopore_read.py:219-252).
 //   k_tile_windows              window list -> tile layout (coalesced cross-mode reads).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -1345,8 +1346,23 @@ int side_streams(int dev, SideStreams **out) {
     std::lock_guard<std::mutex> g(g_side_mu);
     SideStreams &ss = g_side[dev];
     if (!ss.init) {
+        // PCABI_SIDE_CUMASK=1 (A/B): side streams with a CU mask of every CU, each on a hardware
+        // queue of its own (a plain stream shares one of the process's GPU_MAX_HW_QUEUES, and two
+        // regions' small buckets landing on one queue run one after the other: r04 trace of the
+        // reference job's end trim)
+        const char *cm = std::getenv("PCABI_SIDE_CUMASK");
+        std::vector<uint32_t> mask;
+        if (cm && cm[0] == '1') {
+            int cus = 0;
+            HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+            mask.assign((size_t)(cus + 31) / 32, 0u);
+            for (int c = 0; c < cus; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
+        }
         for (int i = 0; i < SideStreams::N; ++i) {
-            HIP_TRY(hipStreamCreateWithFlags(&ss.s[i], hipStreamNonBlocking));
+            if (mask.empty())
+                HIP_TRY(hipStreamCreateWithFlags(&ss.s[i], hipStreamNonBlocking));
+            else
+                HIP_TRY(hipExtStreamCreateWithCUMask(&ss.s[i], (uint32_t)mask.size(), mask.data()));
             HIP_TRY(hipEventCreateWithFlags(&ss.join[i], hipEventDisableTiming));
         }
         HIP_TRY(hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming));

@@ -1,6 +1,7 @@
 #!/bin/bash
 # GPU-box script (r04): one-wave chunk blocks (PCABI_CHUNK_WPB=1) parity and A/B on the middle step,
-# and the reference job with it.
+# and the reference job with it; CU-masked side streams (PCABI_SIDE_CUMASK=1) on the headline and the
+# reference job.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/r04n
@@ -15,3 +16,10 @@ for V in base wpb1 base wpb1; do
 done
 env PCABI_CHUNK_WPB=1 timeout -k 10 300 python bench.py --only-subs reference_job --steps 6 --warmup 2 --cpu-sample 0 > $OUT/rj_wpb1.json 2> $OUT/rj_wpb1.err || { echo "rj wpb1 failed rc=$?"; tail -20 $OUT/rj_wpb1.err; exit 1; }
 python -c "import json; d=json.load(open('$OUT/rj_wpb1.json'))['reference_job']; print('rj wpb1', d['ms_per_step'], json.dumps(d['ms_per_phase']))"
+for V in base cm base cm; do
+  case $V in base) E="PCABI_NOOP=1";; cm) E="PCABI_SIDE_CUMASK=1";; esac
+  env $E timeout -k 10 300 python bench.py --sub 0 --steps 20 --warmup 3 --cpu-sample 0 --check 0 > $OUT/head_$V.json 2> $OUT/head_$V.err || { echo "head $V failed rc=$?"; tail -20 $OUT/head_$V.err; exit 1; }
+  python -c "import json; d=json.load(open('$OUT/head_$V.json')); print('head $V', d['value'], d['ms_per_step'], d['roofline']['launch_ms'])"
+  env $E timeout -k 10 300 python bench.py --only-subs reference_job --steps 6 --warmup 2 --cpu-sample 0 --check 0 > $OUT/rj_$V.json 2> $OUT/rj_$V.err || { echo "rj $V failed rc=$?"; tail -20 $OUT/rj_$V.err; exit 1; }
+  python -c "import json; d=json.load(open('$OUT/rj_$V.json'))['reference_job']; print('rj $V', d['ms_per_step'], json.dumps(d['ms_per_phase']), d['single_adapter_launches']['frac'])"
+done
