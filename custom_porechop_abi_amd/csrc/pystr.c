@@ -1,0 +1,215 @@
+/* _pystr -- host-side helpers for the Python drivers (CPython C API, no GPU code).
+ *
+ * The drivers hand batches of ~10^5 Python objects to the engine: NanoporeRead objects and their
+ * seq strs. Each Python-level pass over such a batch (a list comprehension, map(len, ...), one
+ * ctypes call per str for its buffer address) costs 20-60 ms per 100k objects, mostly cache
+ * misses on the scattered objects plus the interpreter's per-item overhead; the end-trim driver
+ * made five such passes before its GPU call. These helpers make one C pass each:
+ *
+ *   ascii_buffers(strs, addr, lens) -> bool
+ *       For a list of str: addr[k] = the address of strs[k]'s characters (a compact ASCII str
+ *       keeps its bytes inside the object: PyUnicode_AsUTF8 is that address, no copy), lens[k] =
+ *       its length. addr: writable uint64 buffer, lens: writable int64 buffer, len(strs) entries
+ *       each. Returns False (buffers partly filled) at the first item that is not an ASCII str:
+ *       the caller takes its slicing path. The addresses are valid while the strs live.
+ *   attr_list(objs, name) -> list
+ *       [getattr(o, name) for o in objs].
+ *   append_rows(reads, name, objs, read, obj, f1, f2, i1, i2)
+ *       Alignment tuples appended to each read's list attribute (below).
+ *   raise_trims(reads, start, end)
+ *       For each read k: read.start_trim_amount = max(read.start_trim_amount, start[k]), the same
+ *       for end_trim_amount (start / end: int32 buffers) -- the end-trim driver's update of the
+ *       reference's NanoporeRead fields (nanopore_read.py:175-217, find_start_trim /
+ *       find_end_trim keep the largest trim).
+ */
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+#include <stdint.h>
+
+static PyObject *ascii_buffers(PyObject *self, PyObject *args) {
+    PyObject *seq;
+    Py_buffer ab, lb;
+    if (!PyArg_ParseTuple(args, "Ow*w*", &seq, &ab, &lb)) return NULL;
+    PyObject *fast = PySequence_Fast(seq, "ascii_buffers: a sequence of str");
+    PyObject *ret = NULL;
+    if (!fast) goto done;
+    const Py_ssize_t n = PySequence_Fast_GET_SIZE(fast);
+    if (ab.len < n * (Py_ssize_t)sizeof(uint64_t) || lb.len < n * (Py_ssize_t)sizeof(int64_t)) {
+        PyErr_SetString(PyExc_ValueError, "ascii_buffers: buffers too small");
+        goto done;
+    }
+    uint64_t *addr = (uint64_t *)ab.buf;
+    int64_t *lens = (int64_t *)lb.buf;
+    PyObject **items = PySequence_Fast_ITEMS(fast);
+    int ok = 1;
+    for (Py_ssize_t k = 0; k < n; ++k) {
+        PyObject *s = items[k];
+        if (!PyUnicode_Check(s) || PyUnicode_READY(s) != 0 || !PyUnicode_IS_ASCII(s)) {
+            PyErr_Clear();
+            ok = 0;
+            break;
+        }
+        const char *p = PyUnicode_AsUTF8(s);   /* compact ASCII: the object's own bytes */
+        if (!p) {
+            PyErr_Clear();
+            ok = 0;
+            break;
+        }
+        addr[k] = (uint64_t)(uintptr_t)p;
+        lens[k] = (int64_t)PyUnicode_GET_LENGTH(s);
+    }
+    ret = PyBool_FromLong(ok);
+done:
+    Py_XDECREF(fast);
+    PyBuffer_Release(&ab);
+    PyBuffer_Release(&lb);
+    return ret;
+}
+
+static PyObject *attr_list(PyObject *self, PyObject *args) {
+    PyObject *seq, *name;
+    if (!PyArg_ParseTuple(args, "OU", &seq, &name)) return NULL;
+    PyObject *fast = PySequence_Fast(seq, "attr_list: a sequence");
+    if (!fast) return NULL;
+    const Py_ssize_t n = PySequence_Fast_GET_SIZE(fast);
+    PyObject **items = PySequence_Fast_ITEMS(fast);
+    PyObject *out = PyList_New(n);
+    if (!out) {
+        Py_DECREF(fast);
+        return NULL;
+    }
+    for (Py_ssize_t k = 0; k < n; ++k) {
+        PyObject *v = PyObject_GetAttr(items[k], name);
+        if (!v) {
+            Py_DECREF(out);
+            Py_DECREF(fast);
+            return NULL;
+        }
+        PyList_SET_ITEM(out, k, v);
+    }
+    Py_DECREF(fast);
+    return out;
+}
+
+static int raise_field(PyObject *o, PyObject *name, long v) {
+    PyObject *cur = PyObject_GetAttr(o, name);
+    if (!cur) return -1;
+    int gt = 0;
+    PyObject *nv = PyLong_FromLong(v);
+    if (!nv) {
+        Py_DECREF(cur);
+        return -1;
+    }
+    gt = PyObject_RichCompareBool(nv, cur, Py_GT);   /* v > current, as the driver's `if a > r.x` */
+    Py_DECREF(cur);
+    int rc = gt < 0 ? -1 : 0;
+    if (gt > 0) rc = PyObject_SetAttr(o, name, nv);
+    Py_DECREF(nv);
+    return rc;
+}
+
+static PyObject *raise_trims(PyObject *self, PyObject *args) {
+    PyObject *seq;
+    Py_buffer sb, eb;
+    if (!PyArg_ParseTuple(args, "Oy*y*", &seq, &sb, &eb)) return NULL;
+    PyObject *ret = NULL, *fast = NULL;
+    PyObject *ns = PyUnicode_InternFromString("start_trim_amount");
+    PyObject *ne = PyUnicode_InternFromString("end_trim_amount");
+    if (!ns || !ne) goto done;
+    fast = PySequence_Fast(seq, "raise_trims: a sequence of reads");
+    if (!fast) goto done;
+    const Py_ssize_t n = PySequence_Fast_GET_SIZE(fast);
+    if (sb.len < n * 4 || eb.len < n * 4) {
+        PyErr_SetString(PyExc_ValueError, "raise_trims: buffers too small");
+        goto done;
+    }
+    const int32_t *st = (const int32_t *)sb.buf, *et = (const int32_t *)eb.buf;
+    PyObject **items = PySequence_Fast_ITEMS(fast);
+    for (Py_ssize_t k = 0; k < n; ++k)
+        if (raise_field(items[k], ns, st[k]) < 0 || raise_field(items[k], ne, et[k]) < 0) goto done;
+    Py_INCREF(Py_None);
+    ret = Py_None;
+done:
+    Py_XDECREF(fast);
+    Py_XDECREF(ns);
+    Py_XDECREF(ne);
+    PyBuffer_Release(&sb);
+    PyBuffer_Release(&eb);
+    return ret;
+}
+
+/* append_rows(reads, name, objs, read, obj, f1, f2, i1, i2): for every row k (rows grouped by read,
+ * in the order they are to be appended), getattr(reads[read[k]], name).append(
+ * (objs[obj[k]], f1[k], f2[k], i1[k], i2[k])) -- the end-trim driver's alignment lists
+ * (nanopore_read.py:186-188, 208-210: (adapter, full identity, partial identity, read start,
+ * read end)). read / obj / i1 / i2: int64 buffers, f1 / f2: float64 buffers. */
+static PyObject *append_rows(PyObject *self, PyObject *args) {
+    PyObject *reads, *name, *objs;
+    Py_buffer rb, ob, f1b, f2b, i1b, i2b;
+    if (!PyArg_ParseTuple(args, "OUOy*y*y*y*y*y*", &reads, &name, &objs, &rb, &ob, &f1b, &f2b, &i1b, &i2b))
+        return NULL;
+    PyObject *ret = NULL, *fr = NULL, *fo = NULL, *lst = NULL;
+    fr = PySequence_Fast(reads, "append_rows: a sequence of reads");
+    fo = fr ? PySequence_Fast(objs, "append_rows: a sequence of objects") : NULL;
+    if (!fo) goto done;
+    const Py_ssize_t m = rb.len / 8;
+    if (ob.len / 8 < m || f1b.len / 8 < m || f2b.len / 8 < m || i1b.len / 8 < m || i2b.len / 8 < m) {
+        PyErr_SetString(PyExc_ValueError, "append_rows: buffers of different lengths");
+        goto done;
+    }
+    const int64_t *rd = (const int64_t *)rb.buf, *oi = (const int64_t *)ob.buf;
+    const double *f1 = (const double *)f1b.buf, *f2 = (const double *)f2b.buf;
+    const int64_t *i1 = (const int64_t *)i1b.buf, *i2 = (const int64_t *)i2b.buf;
+    const Py_ssize_t nr = PySequence_Fast_GET_SIZE(fr), no = PySequence_Fast_GET_SIZE(fo);
+    PyObject **ri = PySequence_Fast_ITEMS(fr), **oo = PySequence_Fast_ITEMS(fo);
+    int64_t cur = -1;
+    for (Py_ssize_t k = 0; k < m; ++k) {
+        if (rd[k] < 0 || rd[k] >= nr || oi[k] < 0 || oi[k] >= no) {
+            PyErr_SetString(PyExc_IndexError, "append_rows: index out of range");
+            goto done;
+        }
+        if (rd[k] != cur) {
+            Py_XDECREF(lst);
+            lst = PyObject_GetAttr(ri[rd[k]], name);
+            if (!lst) goto done;
+            cur = rd[k];
+        }
+        PyObject *t = Py_BuildValue("(Oddll)", oo[oi[k]], f1[k], f2[k], (long)i1[k], (long)i2[k]);
+        if (!t) goto done;
+        const int rc = PyList_Check(lst) ? PyList_Append(lst, t) : -1;
+        if (rc < 0 && !PyErr_Occurred()) {
+            PyObject *r = PyObject_CallMethod(lst, "append", "O", t);   /* not a list: its append */
+            Py_DECREF(t);
+            if (!r) goto done;
+            Py_DECREF(r);
+            continue;
+        }
+        Py_DECREF(t);
+        if (rc < 0) goto done;
+    }
+    Py_INCREF(Py_None);
+    ret = Py_None;
+done:
+    Py_XDECREF(lst);
+    Py_XDECREF(fr);
+    Py_XDECREF(fo);
+    PyBuffer_Release(&rb);
+    PyBuffer_Release(&ob);
+    PyBuffer_Release(&f1b);
+    PyBuffer_Release(&f2b);
+    PyBuffer_Release(&i1b);
+    PyBuffer_Release(&i2b);
+    return ret;
+}
+
+static PyMethodDef methods[] = {
+    {"append_rows", append_rows, METH_VARARGS, "append alignment tuples to the reads' lists"},
+    {"ascii_buffers", ascii_buffers, METH_VARARGS, "addresses and lengths of ASCII strs"},
+    {"attr_list", attr_list, METH_VARARGS, "[getattr(o, name) for o in objs]"},
+    {"raise_trims", raise_trims, METH_VARARGS, "raise the reads' trim amounts to the given ones"},
+    {NULL, NULL, 0, NULL}};
+
+static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_pystr", NULL, -1, methods,
+                                    NULL, NULL, NULL, NULL};
+
+PyMODINIT_FUNC PyInit__pystr(void) { return PyModule_Create(&module); }

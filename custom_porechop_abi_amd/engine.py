@@ -27,6 +27,31 @@ PAD = 16
 _AS_UTF8 = None
 
 
+try:
+    from . import _pystr   # the drivers' host helpers (csrc/pystr.c, built by __graft_entry__.build)
+except ImportError:        # not built: the same results through Python-level passes
+    _pystr = None
+
+
+def str_buffers(seqs):
+    """(character addresses uint64[n], lengths int64[n]) of a list of ASCII strs in one native
+    pass (_pystr.ascii_buffers), or None when an item is not an ASCII str. The addresses are
+    valid while the strs live."""
+    n = len(seqs)
+    if n == 0:
+        return None
+    if _pystr is None:
+        try:
+            if not all(map(str.isascii, seqs)):
+                return None
+        except TypeError:
+            return None
+        return (np.fromiter(map(_as_utf8(), seqs), np.uint64, n), np.fromiter(map(len, seqs), np.int64, n))
+    addr = np.empty(n, np.uint64)
+    lens = np.empty(n, np.int64)
+    return (addr, lens) if _pystr.ascii_buffers(seqs, addr, lens) else None
+
+
 def _as_utf8():
     global _AS_UTF8
     if _AS_UTF8 is None:
@@ -95,30 +120,28 @@ class SeqPack(object):
         return joined.encode('ascii'), offs, lens.astype(np.int32)
 
     @classmethod
-    def windows(cls, seqs, starts, lengths, index=None):
+    def windows(cls, seqs, starts, lengths, index=None, bufs=None):
         """The pack of [seqs[k][a:a + l] for k, a, l in zip(index, starts, lengths)] (index
         defaults to every sequence once; same layout as SeqPack of those slices) without making
         them: for ASCII str the codes are gathered from the strs' own buffers by
         pcabi_encode_dna5_gather (one byte per base, so character positions are byte positions).
-        `starts` / `lengths` must lie inside each sequence."""
+        `starts` / `lengths` must lie inside each sequence. bufs: str_buffers(seqs) when the caller
+        has it already."""
         starts = np.asarray(starts, np.int64)
         lengths = np.asarray(lengths, np.int64)
         idx = np.arange(len(seqs)) if index is None else np.asarray(index, np.int64)
         n = len(idx)
-        try:
-            ascii_str = n > 0 and all(map(str.isascii, seqs))
-        except TypeError:                              # bytes / arrays: the slicing path
-            ascii_str = False
-        if not ascii_str:
-            return cls([seqs[k][a:a + l] for k, a, l in zip(idx.tolist(), starts.tolist(), lengths.tolist())])
         # CPython keeps an ASCII str's bytes inside the object: PyUnicode_AsUTF8 is their address
         # (no copy), valid while `seqs` holds the strs -- i.e. for this call
-        have = np.fromiter(map(len, seqs), np.int64, len(seqs))[idx]
+        if bufs is None and n > 0:
+            bufs = str_buffers(seqs)
+        if n == 0 or bufs is None:                     # bytes / arrays / non-ASCII: the slicing path
+            return cls([seqs[k][a:a + l] for k, a, l in zip(idx.tolist(), starts.tolist(), lengths.tolist())])
+        have = bufs[1][idx]
         if len(starts) != n or len(lengths) != n or (starts < 0).any() or (lengths < 0).any() or \
                 (starts + lengths > have).any():
             raise ValueError('SeqPack.windows: a window lies outside its sequence')
-        base = np.fromiter(map(_as_utf8(), seqs), np.uint64, len(seqs))
-        addr = base[idx] + starts.astype(np.uint64)
+        addr = bufs[0][idx] + starts.astype(np.uint64)
         offs = np.zeros(n, np.int64)
         np.cumsum((lengths + ((-lengths) & 3))[:-1], out=offs[1:])
         total = int(offs[-1] + lengths[-1] + ((-lengths[-1]) & 3)) + PAD

@@ -231,13 +231,15 @@ def end_windows_pack(reads, end_size):
     them (nanopore_read.py:181, 203), packed into one Dna5 buffer: (codes, start views, end views)
     -- only the 2 x end_size bases per read travel, not the whole reads."""
     n = len(reads)
-    seqs = [r.seq for r in reads]
-    ln = np.fromiter(map(len, seqs), np.int64, n)
+    seqs = _attrs(reads, 'seq')
+    bufs = engine.str_buffers(seqs)
+    ln = bufs[1] if bufs is not None else np.fromiter(map(len, seqs), np.int64, n)
     e = int(end_size)
     s_len = np.clip(ln + e if e < 0 else np.minimum(ln, e), 0, None)      # seq[:e]
     e_start = np.zeros(n, np.int64) if e == 0 else (np.maximum(ln - e, 0) if e > 0 else np.minimum(-e, ln))
     pack = SeqPack.windows(seqs, np.concatenate([np.zeros(n, np.int64), e_start]),
-                           np.concatenate([s_len, ln - e_start]), index=np.tile(np.arange(n), 2))   # seq[-e:]
+                           np.concatenate([s_len, ln - e_start]), index=np.tile(np.arange(n), 2),
+                           bufs=bufs)   # seq[-e:]
     return pack.codes, (pack.offsets[:n], pack.lengths[:n]), (pack.offsets[n:], pack.lengths[n:])
 
 
@@ -253,6 +255,13 @@ def _gc_paused():
         yield
     finally:
         gc.unfreeze()
+
+
+def _attrs(objs, name):
+    """[getattr(o, name) for o in objs], in one native pass when the host helpers are built."""
+    if engine._pystr is not None:
+        return engine._pystr.attr_list(objs, name)
+    return [getattr(o, name) for o in objs]
 
 
 def _end_decisions(*args):
@@ -275,11 +284,14 @@ def _end_decisions_batch(reads, starts, ends, end_size, extra, thr, scoring_sche
     st, et, s_list, e_list, bc_full = engine.end_decisions(
         codes, sw, ew, s_u, e_u, scoring_scheme_vals, end_size, extra, thr, min_trim,
         bc_start=s_idx[bc[0]] if bc[0] else None, bc_end=e_idx[bc[1]] if bc[1] else None)
-    for r, a, b in zip(reads, st.tolist(), et.tolist()):
-        if a > r.start_trim_amount:
-            r.start_trim_amount = a
-        if b > r.end_trim_amount:
-            r.end_trim_amount = b
+    if engine._pystr is not None:                 # one native pass: the same max-updates
+        engine._pystr.raise_trims(reads, np.ascontiguousarray(st, np.int32), np.ascontiguousarray(et, np.int32))
+    else:
+        for r, a, b in zip(reads, st.tolist(), et.tolist()):
+            if a > r.start_trim_amount:
+                r.start_trim_amount = a
+            if b > r.end_trim_amount:
+                r.end_trim_amount = b
     for sets, idx, lst, attr in ((starts, s_idx, s_list, 'start_adapter_alignments'),
                                  (ends, e_idx, e_list, 'end_adapter_alignments')):
         if not sets or not lst.shape[1]:
@@ -301,10 +313,15 @@ def _end_decisions_batch(reads, starts, ends, end_size, extra, thr, scoring_sche
         part = np.where(failed, 0.0, engine.pid6(m, l1))
         re_x = np.where(failed, 0, re_ + 1)
         full, part, rs, re_x = (np.repeat(x, rep)[order] for x in (full, part, rs, re_x))
+        rd = read[order]
+        if engine._pystr is not None:             # the tuples made and appended in one native pass
+            engine._pystr.append_rows(reads, attr, sets, rd.astype(np.int64), set_k[order].astype(np.int64),
+                                      full.astype(np.float64), part.astype(np.float64), rs.astype(np.int64),
+                                      re_x.astype(np.int64))
+            continue
         # the tuples in one pass, then one extend per read (not one append per alignment)
         rows = list(zip(map(sets.__getitem__, set_k[order].tolist()), full.tolist(), part.tolist(), rs.tolist(),
                         re_x.tolist()))
-        rd = read[order]
         cut = np.flatnonzero(np.diff(rd)) + 1
         lo = np.concatenate([[0], cut]).tolist()
         hi = np.concatenate([cut, [len(rd)]]).tolist()
@@ -361,14 +378,15 @@ def middle_adapter_list(matching_sets):
     return adapters, start_names, end_names
 
 
-def trimmed_bounds(reads, seqs=None):
+def trimmed_bounds(reads, seq_lens=None):
     """(start, length) of get_seq_with_start_end_adapters_trimmed() inside each read's seq, with
     Python's slice rules for seq[s:len(seq) - e] (a negative stop counts from the end, both ends
-    clipped) -- the trimmed reads as views of the untrimmed ones, no copy. `seqs`: the reads'
-    seq strings when the caller has them already."""
-    n = np.fromiter(map(len, [r.seq for r in reads] if seqs is None else seqs), np.int64, len(reads))
-    s = np.fromiter((r.start_trim_amount for r in reads), np.int64, len(reads))
-    e = np.fromiter((r.end_trim_amount for r in reads), np.int64, len(reads))
+    clipped) -- the trimmed reads as views of the untrimmed ones, no copy. `seq_lens`: the reads'
+    seq lengths when the caller has them already."""
+    n = np.fromiter(map(len, _attrs(reads, 'seq')), np.int64, len(reads)) if seq_lens is None else \
+        np.asarray(seq_lens, np.int64)
+    s = np.array(_attrs(reads, 'start_trim_amount'), np.int64).reshape(-1)
+    e = np.array(_attrs(reads, 'end_trim_amount'), np.int64).reshape(-1)
     a = np.minimum(s, n)
     b = n - e
     b = np.clip(np.where(b < 0, b + n, b), 0, n)
@@ -392,13 +410,15 @@ def scan_middles(seqs, adapter_seqs, middle_threshold, scoring_scheme_vals, devi
     return hits
 
 
-def _middle_hits_by_read(seqs, adapter_seqs, middle_threshold, scoring_scheme_vals, device=0, bounds=None):
+def _middle_hits_by_read(seqs, adapter_seqs, middle_threshold, scoring_scheme_vals, device=0, bounds=None,
+                         bufs=None):
     """scan_middles' hits as (read index, ordered hit list) for the reads that have any, in read
-    order: the drivers then touch only those reads (a few percent of a batch), not every read."""
+    order: the drivers then touch only those reads (a few percent of a batch), not every read.
+    bufs: engine.str_buffers(seqs) when the caller has it."""
     n = len(seqs)
     if n == 0 or not adapter_seqs:
         return []
-    pack = SeqPack(seqs) if bounds is None else SeqPack.windows(seqs, *bounds)
+    pack = SeqPack(seqs) if bounds is None else SeqPack.windows(seqs, *bounds, bufs=bufs)
     views = pack.views(np.zeros(n, np.int64), pack.lengths)
     h = engine.middle_scan(views, adapter_seqs, scoring_scheme_vals, middle_threshold, device=device)
     if not h.shape[1]:
@@ -427,9 +447,10 @@ def find_adapters_in_read_middles(reads, matching_sets, verbosity, middle_thresh
         output_progress_line(0, read_count, print_dest)
     # the trimmed reads packed straight from the untrimmed strs (SeqPack.windows), no slices
     with _gc_paused():
-        seqs = [r.seq for r in reads]
+        seqs = _attrs(reads, 'seq')
+        bufs = engine.str_buffers(seqs)
         by_read = _middle_hits_by_read(seqs, [a[1] for a in adapters], middle_threshold, scoring_scheme_vals,
-                                       bounds=trimmed_bounds(reads, seqs))
+                                       bounds=trimmed_bounds(reads, None if bufs is None else bufs[1]), bufs=bufs)
     # only reads with hits change; at verbosity > 1 every read is visited in order, since a read
     # with positions from an earlier call prints too (the reference's per-read loop, porechop_abi.py:487-495)
     visit = [(i, h.get(i, ())) for h in (dict(by_read),) for i in range(read_count)] if verbosity > 1 else by_read
