@@ -18,10 +18,11 @@ int dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st, bool ta
             dispatch_split_chunk(kBuckets[b].rpl, ks, p, affine, tagged && affine && kBuckets[b].rpl <= 32, st))
             return 0;
     }
-    // PCABI_CHUNK_WPB=1 (A/B): one-wave blocks for the device-planned run-tagged / packed buckets,
-    // 4x the blocks (the same wave slots)
+    // one-wave blocks for the device-planned run-tagged / packed buckets, 4x the blocks (the same
+    // wave slots): r04n, candidate DP 0.68 -> 0.62 ms per 8 kb step, the reference job's middle
+    // 1.57-1.59 -> 1.52 ms. PCABI_CHUNK_WPB=4 keeps four-wave blocks (A/B).
     const char *ewpb = std::getenv("PCABI_CHUNK_WPB");
-    const bool wpb1 = p.dev_waves && ewpb && ewpb[0] == '1' && kBuckets[b].kind == FAST && affine;
+    const bool wpb1 = p.dev_waves && !(ewpb && ewpb[0] == '4') && kBuckets[b].kind == FAST && affine;
     const dim3 grid1(grid.x * 4);
     if (wpb1 && tagged && kBuckets[b].rpl <= 32) {
         switch (kBuckets[b].rpl) {

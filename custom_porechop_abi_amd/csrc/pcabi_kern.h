@@ -383,7 +383,7 @@ __device__ __forceinline__ void chunk_wave(const KParams &p, int64_t wave, bool 
 // <= 28-row chunk kernels also come with W = 6 (80 VGPRs instead of 89: 6 waves per SIMD instead of
 // 5), chosen by PCABI_CHUNK_WAVES=6 at dispatch (A/B). WPB: waves per block -- with 4, a block's
 // waves meet at every table barrier and the block holds its CU slot until its slowest wave (the
-// longest chunk of its 4 x 64 tasks) ends; with 1 (PCABI_CHUNK_WPB=1, A/B) every wave retires alone.
+// longest chunk of its 4 x 64 tasks) ends; with 1 (the device-planned default) every wave retires alone.
 template <int RPL, bool AFFINE, int KIND, int W = 1, int WPB = 4>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(W))) void k_align_chunk(KParams p) {
     __shared__ __attribute__((aligned(16))) int32_t tab[WPB * wave_tab_ints<KIND, RPL>()];

@@ -289,14 +289,16 @@ def test_chunk_dp_row_split(gpu_lib, monkeypatch, reads_8kb, split, windows):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('windows', ['0', '1'])
-def test_chunk_dp_one_wave_blocks(gpu_lib, monkeypatch, reads_8kb, windows):
-    """PCABI_CHUNK_WPB=1: the device-planned chunk launches in one-wave blocks (no table barrier
-    shared by four waves) -- the scan equals the oracle, whole-read chunks and candidate windows."""
+@pytest.mark.parametrize('wpb', ['1', '4'])
+def test_chunk_dp_one_wave_blocks(gpu_lib, monkeypatch, reads_8kb, windows, wpb):
+    """The device-planned chunk launches in one-wave blocks (the default: no table barrier shared
+    by four waves) and in four-wave blocks (PCABI_CHUNK_WPB=4) -- the scan equals the oracle,
+    whole-read chunks and candidate windows."""
     from custom_porechop_abi_amd import engine
     views, exp = reads_8kb
     monkeypatch.setenv('PCABI_MIDDLE_SEEDS', '2')
     monkeypatch.setenv('PCABI_MIDDLE_WINDOWS', windows)
-    monkeypatch.setenv('PCABI_CHUNK_WPB', '1')
+    monkeypatch.setenv('PCABI_CHUNK_WPB', wpb)
     got = engine.middle_scan(views, ADPS, SC, 90.0)
     assert np.array_equal(_sorted(got), exp)
 
