@@ -1153,11 +1153,16 @@ std::vector<int> assign_buckets(const int32_t *adp_len, int32_t n_adp, const pca
                 return false;
         return true;
     };
+    // PCABI_SMALL_TABLE_BUCKETS=N (A/B): tables of at most 4 adapters keep at most N FAST buckets
+    // (the reference job's kept sets: one launch per side instead of two one-adapter launches)
+    int max_fast = max_fast_buckets();
+    if (const char *e = std::getenv("PCABI_SMALL_TABLE_BUCKETS"))
+        if (std::atoi(e) > 0 && n_adp <= 4) max_fast = std::min(max_fast, std::atoi(e));
     while (merge) {
         std::vector<int> fast;
         for (int b = 0; b < kNumBuckets; ++b)
             if (count[b] && kBuckets[b].kind == FAST) fast.push_back(b);
-        if ((int)fast.size() <= max_fast_buckets()) break;
+        if ((int)fast.size() <= max_fast) break;
         int best = -1;
         int64_t best_cost = 0;
         for (size_t k = 0; k + 1 < fast.size(); ++k) {
