@@ -16,3 +16,4 @@ for Q in 2 4 3 1 2 4; do
   GPU_MAX_HW_QUEUES=$Q timeout -k 10 300 python bench.py --workload middle --steps 8 --warmup 2 --cpu-sample 0 --check 0 > $OUT/mid_q$Q.json 2> $OUT/mid_q$Q.err || { echo "mid $Q failed rc=$?"; tail -20 $OUT/mid_q$Q.err; exit 1; }
   python -c "import json; d=json.load(open('$OUT/mid_q$Q.json')); print('mid q=$Q', d['value'], d['ms_per_step'], d['middle_ms_per_step'])"
 done
+bash tools/gpu_r04p.sh
