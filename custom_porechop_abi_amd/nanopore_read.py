@@ -23,12 +23,19 @@ from .cpp_function_wrappers import adapter_alignment
 from .misc import END_FORMATTING, RED, YELLOW, red, yellow
 
 
+_LOWER = 'abcdefghijklmnopqrstuvwxyz'   # what str.upper changes in an ASCII str
+
+
 class NanoporeRead(object):
 
     def __init__(self, name, seq, quals):
         self.name = name
-        seq_u = seq.upper()
-        self.rna = seq_u.count('U') > seq_u.count('T')
+        # seq.upper(), and the RNA test count('U') > count('T') (nanopore_read.py:35-40): the same
+        # values with memchr-speed membership scans where they decide it -- an ASCII read with no
+        # lower-case letter is its own upper case, and a read without a U is not RNA (an 8 kb read:
+        # ~35 -> ~5 us, most of building a batch of reads)
+        seq_u = seq if seq.isascii() and not any(c in seq for c in _LOWER) else seq.upper()
+        self.rna = 'U' in seq_u and seq_u.count('U') > seq_u.count('T')
         self.seq = seq_u.replace('U', 'T') if self.rna else seq_u
         self.quals = quals if len(quals) >= len(seq) else quals + '+' * (len(seq) - len(quals))
 

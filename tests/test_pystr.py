@@ -75,3 +75,16 @@ def test_append_rows_matches_python_tuples():
     with pytest.raises(IndexError):
         engine._pystr.append_rows(reads, 'start_adapter_alignments', objs, np.array([99], np.int64),
                                   ob[:1], f1[:1], f2[:1], i1[:1], i2[:1])
+
+
+def test_nanopore_read_init_fast_paths_match_reference_rules():
+    """NanoporeRead.__init__'s upper-case and RNA shortcuts against the reference's rules
+    (nanopore_read.py:35-40: seq.upper(), RNA when count('U') > count('T'), then U -> T)."""
+    rng = random.Random(5)
+    alpha = 'ACGTNUacgtnu-xyzé'
+    for _ in range(5000):
+        s = ''.join(rng.choice(alpha[:rng.randint(1, len(alpha))]) for _ in range(rng.randint(0, 30)))
+        r = NanoporeRead('n', s, '')
+        su = s.upper()
+        rna = su.count('U') > su.count('T')
+        assert r.rna == rna and r.seq == (su.replace('U', 'T') if rna else su), s
