@@ -17,3 +17,4 @@ for Q in 2 4 3 1 2 4; do
   python -c "import json; d=json.load(open('$OUT/mid_q$Q.json')); print('mid q=$Q', d['value'], d['ms_per_step'], d['middle_ms_per_step'])"
 done
 bash tools/gpu_r04p.sh
+bash tools/gpu_r04q.sh
