@@ -25,6 +25,7 @@
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 #include <stdint.h>
+#include <string.h>
 
 static PyObject *ascii_buffers(PyObject *self, PyObject *args) {
     PyObject *seq;
@@ -149,6 +150,14 @@ static PyObject *append_rows(PyObject *self, PyObject *args) {
     if (!PyArg_ParseTuple(args, "OUOy*y*y*y*y*y*", &reads, &name, &objs, &rb, &ob, &f1b, &f2b, &i1b, &i2b))
         return NULL;
     PyObject *ret = NULL, *fr = NULL, *fo = NULL, *lst = NULL;
+    /* the identities are pid6 values of small (matches, length) pairs: a few hundred distinct
+     * doubles over 10^5 rows, so their float objects are shared through a small cache (direct
+     * mapped on the value's bits) instead of two allocations per row */
+    enum { kFC = 4096 };
+    PyObject *fcache[kFC];
+    uint64_t fkey[kFC];
+    memset(fcache, 0, sizeof(fcache));
+    memset(fkey, 0, sizeof(fkey));
     fr = PySequence_Fast(reads, "append_rows: a sequence of reads");
     fo = fr ? PySequence_Fast(objs, "append_rows: a sequence of objects") : NULL;
     if (!fo) goto done;
@@ -162,6 +171,21 @@ static PyObject *append_rows(PyObject *self, PyObject *args) {
     const int64_t *i1 = (const int64_t *)i1b.buf, *i2 = (const int64_t *)i2b.buf;
     const Py_ssize_t nr = PySequence_Fast_GET_SIZE(fr), no = PySequence_Fast_GET_SIZE(fo);
     PyObject **ri = PySequence_Fast_ITEMS(fr), **oo = PySequence_Fast_ITEMS(fo);
+#define CACHED_FLOAT(dst, val)                                                           \
+    do {                                                                                 \
+        uint64_t b_;                                                                     \
+        const double v_ = (val);                                                         \
+        memcpy(&b_, &v_, 8);                                                             \
+        const unsigned h_ = (unsigned)((b_ * 0x9E3779B97F4A7C15ull) >> 52) & (kFC - 1);  \
+        if (!fcache[h_] || fkey[h_] != b_) {                                             \
+            PyObject *f_ = PyFloat_FromDouble(v_);                                       \
+            if (!f_) goto done;                                                          \
+            Py_XDECREF(fcache[h_]);                                                      \
+            fcache[h_] = f_;                                                             \
+            fkey[h_] = b_;                                                               \
+        }                                                                                \
+        (dst) = fcache[h_];                                                              \
+    } while (0)
     int64_t cur = -1;
     for (Py_ssize_t k = 0; k < m; ++k) {
         if (rd[k] < 0 || rd[k] >= nr || oi[k] < 0 || oi[k] >= no) {
@@ -174,8 +198,26 @@ static PyObject *append_rows(PyObject *self, PyObject *args) {
             if (!lst) goto done;
             cur = rd[k];
         }
-        PyObject *t = Py_BuildValue("(Oddll)", oo[oi[k]], f1[k], f2[k], (long)i1[k], (long)i2[k]);
+        PyObject *a1, *a2;
+        CACHED_FLOAT(a1, f1[k]);
+        CACHED_FLOAT(a2, f2[k]);
+        PyObject *t = PyTuple_New(5);
         if (!t) goto done;
+        PyObject *x1 = PyLong_FromLongLong(i1[k]), *x2 = PyLong_FromLongLong(i2[k]);
+        if (!x1 || !x2) {
+            Py_XDECREF(x1);
+            Py_XDECREF(x2);
+            Py_DECREF(t);
+            goto done;
+        }
+        Py_INCREF(oo[oi[k]]);
+        Py_INCREF(a1);
+        Py_INCREF(a2);
+        PyTuple_SET_ITEM(t, 0, oo[oi[k]]);
+        PyTuple_SET_ITEM(t, 1, a1);
+        PyTuple_SET_ITEM(t, 2, a2);
+        PyTuple_SET_ITEM(t, 3, x1);
+        PyTuple_SET_ITEM(t, 4, x2);
         const int rc = PyList_Check(lst) ? PyList_Append(lst, t) : -1;
         if (rc < 0 && !PyErr_Occurred()) {
             PyObject *r = PyObject_CallMethod(lst, "append", "O", t);   /* not a list: its append */
@@ -190,6 +232,8 @@ static PyObject *append_rows(PyObject *self, PyObject *args) {
     Py_INCREF(Py_None);
     ret = Py_None;
 done:
+    for (int h = 0; h < kFC; ++h) Py_XDECREF(fcache[h]);
+#undef CACHED_FLOAT
     Py_XDECREF(lst);
     Py_XDECREF(fr);
     Py_XDECREF(fo);
