@@ -1390,6 +1390,10 @@ struct ForkJoin {
     int begin(hipStream_t m, size_t n_launch) {
         main = m;
         if (n_launch <= 1) return 0;
+        {   // PCABI_FORK=0 (A/B): every launch of the region on the caller's stream, in order
+            const char *e = std::getenv("PCABI_FORK");
+            if (e && e[0] == '0') return 0;
+        }
         int dev = 0;
         HIP_TRY(hipGetDevice(&dev));
         if (int rc = side_streams(dev, &ss)) return rc;
