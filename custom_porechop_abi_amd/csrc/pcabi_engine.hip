@@ -1377,6 +1377,21 @@ int side_streams(int dev, SideStreams **out) {
     return 0;
 }
 
+// pcabi_set_side_streams: whether fork / join regions use the side streams (initially PCABI_FORK,
+// default kSideStreamsDefault)
+constexpr int kSideStreamsDefault = 1;
+std::atomic<int> g_side_on{-1};
+bool side_streams_on() {
+    int v = g_side_on.load(std::memory_order_relaxed);
+    if (v < 0) {
+        const char *e = std::getenv("PCABI_FORK");
+        v = (e && (e[0] == '0' || e[0] == '1')) ? e[0] - '0' : kSideStreamsDefault;
+        int expect = -1;
+        if (!g_side_on.compare_exchange_strong(expect, v)) v = expect;
+    }
+    return v != 0;
+}
+
 // Fork / join of independent launches: launch k runs on the caller's stream (k == 0) or on side
 // stream (first + k - 1) % N, each side stream first waiting for the work already queued on the
 // caller's stream; end() makes the caller's stream wait for every side stream used.
@@ -1389,11 +1404,7 @@ struct ForkJoin {
     int n_side = 0;              // side launches of this region
     int begin(hipStream_t m, size_t n_launch) {
         main = m;
-        if (n_launch <= 1) return 0;
-        {   // PCABI_FORK=0 (A/B): every launch of the region on the caller's stream, in order
-            const char *e = std::getenv("PCABI_FORK");
-            if (e && e[0] == '0') return 0;
-        }
+        if (n_launch <= 1 || !side_streams_on()) return 0;   // off: every launch on the caller's stream
         int dev = 0;
         HIP_TRY(hipGetDevice(&dev));
         if (int rc = side_streams(dev, &ss)) return rc;
@@ -3190,6 +3201,12 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
 }  // namespace
 
 extern "C" {
+
+int pcabi_set_side_streams(int on) {
+    const int prev = side_streams_on() ? 1 : 0;
+    if (on >= 0) g_side_on.store(on ? 1 : 0);
+    return prev;
+}
 
 int32_t pcabi_scan_profile(pcabi_scan *s, int32_t mode, double *out, int32_t n_out) {
     if (!s || mode < 0 || mode > 2 || n_out < 0 || (n_out && !out)) return fail(PCABI_E_ARG, "bad arguments");

@@ -188,6 +188,16 @@ int pcabi_align_cross_dev_marked(const uint32_t *tiles, const int64_t *tile_off,
                                  int match, int mismatch, int gap_open, int gap_extend,
                                  int32_t *out, int64_t out_stride, void *stream, void *ev_begin,
                                  void *ev_end);
+/* Side streams (process-wide): with on = 1 a cross product (and a middle-scan round) runs its
+ * largest register bucket on the caller's stream and the others beside it on the device's side
+ * streams; with on = 0 every bucket runs on the caller's stream, one after the other. Side by side
+ * pays for ONE cross product at a time (the largest bucket's tail fills with the small ones);
+ * callers that run cross products on several streams at once should turn it off: HIP maps the
+ * process's streams onto GPU_MAX_HW_QUEUES hardware queues, and a side stream on the queue of
+ * another caller stream's large launch waits for it (r04r: the reference job 4.95 -> 4.66 ms
+ * off). The initial setting is PCABI_FORK (0 or 1; unset: see DESIGN.md §5). Returns the previous
+ * setting; on < 0 only reads it. */
+int pcabi_set_side_streams(int on);
 
 /*
  * End-trim decision epilogue (porechop_abi/nanopore_read.py:175-217), device pointers:
