@@ -86,6 +86,12 @@ def parse():
                     help='reference_job: 1 = the set search\'s two sides side by side (stream2; r04 A/B: 5.13 vs '
                          '5.23 ms per step); 0 = one after the other (each side\'s dominant launch then has the GPU '
                          'to itself, the roofline\'s events)')
+    ap.add_argument('--rj-side-streams', type=int, default=0,
+                    help='reference_job: the library\'s side streams (pcabi_set_side_streams) during the job; 0 '
+                         '(default: it runs two caller streams at once) or 1')
+    ap.add_argument('--head-side-streams', type=int, default=0,
+                    help='headline schedule: the library\'s side streams while both sides\' smaller buckets run on two '
+                         'caller streams at once; 0 (default, r04r: 7.61 vs 7.68 ms) or 1')
     ap.add_argument('--rest-overlap', type=int, default=1,
                     help='headline: 2 = after both dominant launches, both sides\' smaller buckets each on its own '
                          'stream; 1 = the two sides\' calls side by side; 0 = after each side\'s dominant launch')
@@ -387,6 +393,11 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
             L.pcabi_stream_wait_event(stream, ev_join)
         epilogue()
 
+    # the headline schedule runs both sides' smaller buckets on two caller streams at once: the
+    # library's side streams go off for it (pcabi_set_side_streams; one cross product at a time,
+    # as the production schedule, keeps them on)
+    two_streams = not timed_fused and args.rest_overlap == 1
+    side_prev = L.pcabi_set_side_streams(args.head_side_streams if two_streams else -1)
     for _ in range(args.warmup):
         step(fused=timed_fused)
     _lib.check(L.pcabi_stream_sync(stream), 'sync')
@@ -404,6 +415,7 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
     L.pcabi_stream_sync(stream)
     barrier()
     elapsed = time.perf_counter() - t0
+    side_timed = L.pcabi_set_side_streams(side_prev)
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device='cuda' if args.dist_backend == 'nccl' else 'cpu')
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -462,6 +474,7 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
         # the same step in the production schedule: one cross product per side, the small buckets
         # overlapping the dominant launch (faster as a whole; the dominant launch then shares the
         # GPU, so the headline keeps it alone for the roofline)
+        fused_prev = L.pcabi_set_side_streams(1)   # one cross product at a time: side by side pays
         for _ in range(2):
             step(fused=True)
         L.pcabi_stream_sync(stream)
@@ -470,9 +483,11 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
             step(fused=True)
         L.pcabi_stream_sync(stream)
         dt = (time.perf_counter() - t0) / args.steps
+        L.pcabi_set_side_streams(fused_prev)
         subs['fused_schedule'] = {'value': round(n / dt, 1), 'unit': 'reads/s', 'ms_per_step': round(1e3 * dt, 4),
                                   'steps': args.steps, 'what': 'the headline step with one cross product per side '
-                                  '(pcabi_align_cross_dev_marked): register buckets side by side with the dominant one'}
+                                  '(pcabi_align_cross_dev_marked): register buckets side by side with the dominant one '
+                                  '(side streams on)'}
         subs['host_path'] = run_host_path(args, L, _lib, buf, s_off, s_len, e_off, e_len, sides, d_sres, d_eres, d_st,
                                           d_et, n, n_sa, n_ea, stream, start_adps, end_adps)
 
@@ -514,7 +529,8 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
                                     % (n, len(sets), n_sa, n_ea, args.end_size)),
                        'reads_per_gpu': n, 'adapter_sets': len(sets), 'end_size': args.end_size,
                        'scoring': list(sc), 'parallelism': 'dp%d (read shards)' % world,
-                       'hw_queues': os.environ.get('GPU_MAX_HW_QUEUES', 'HIP default')},
+                       'hw_queues': os.environ.get('GPU_MAX_HW_QUEUES', 'HIP default'),
+                       'side_streams': side_timed},
             'roofline': {'bound': 'valu', 'achieved': round(tops, 3), 'peak': round(VALU_PEAK_TOPS, 1),
                          'unit': 'Tops/s (int32 lane-ops)', 'frac': round(tops / VALU_PEAK_TOPS, 4),
                          'traffic': prof.get('traffic_bytes_per_launch') if prof and headline else None,
@@ -924,14 +940,22 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
             acc[key] = acc.get(key, 0.0) + ms.value
         return matching
 
-    for _ in range(max(1, args.warmup)):
-        step()
-    acc.clear()
-    torch.cuda.synchronize() if torch.cuda.is_available() else None
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        matching = step()
-    elapsed = time.perf_counter() - t0
+    # the job runs cross products on two caller streams at once (set search and end trim: both
+    # sides side by side), so the library's side streams go off (pcabi_set_side_streams, r04r:
+    # 4.95 -> 4.66 ms per step): a side stream on the other caller stream's hardware queue waits
+    # for its large launch
+    side_prev = L.pcabi_set_side_streams(0 if args.rj_side_streams == 0 else 1)
+    try:
+        for _ in range(max(1, args.warmup)):
+            step()
+        acc.clear()
+        torch.cuda.synchronize() if torch.cuda.is_available() else None
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            matching = step()
+        elapsed = time.perf_counter() - t0
+    finally:
+        L.pcabi_set_side_streams(side_prev)
     step_ms = 1e3 * elapsed / args.steps
     per = {k: round(v / args.steps, 4) for k, v in acc.items()}
     ks = kept_state(tuple(a.name for a in matching), matching)
