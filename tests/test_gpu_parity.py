@@ -155,16 +155,27 @@ def test_long_reads_middle_shape(gpu_lib):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('side', [1, 0])
 @pytest.mark.parametrize('scored', [False, True])
 @pytest.mark.parametrize('scheme', [(3, -6, -5, -2), (2, -1, -1, -1)])
-def test_device_abi_tiled_cross(gpu_lib, scheme, scored):
+def test_device_abi_tiled_cross(gpu_lib, scheme, scored, side):
     """Device-pointer ABI: pcabi_tile_layout -> pcabi_tile_windows_dev -> pcabi_align_cross_dev,
     with ragged windows (empty, 1 bp, several kb) and more than one tile. scored: the table is
     built for the scoring, so small register buckets are merged (extra padding rows), and the
     call goes through pcabi_align_cross_dev_marked on a stream of its own (events around the
-    largest bucket)."""
+    largest bucket). side: the buckets side by side on the side streams (1) or one after the
+    other on the caller's stream (0, pcabi_set_side_streams)."""
     from custom_porechop_abi_amd import _lib, engine
     L, vp = gpu_lib, ctypes.c_void_p
+    side_prev = L.pcabi_set_side_streams(side)
+    try:
+        _tiled_cross_case(L, _lib, engine, vp, scheme, scored)
+    finally:
+        L.pcabi_set_side_streams(side_prev)
+    assert L.pcabi_set_side_streams(-1) == side_prev
+
+
+def _tiled_cross_case(L, _lib, engine, vp, scheme, scored):
     reads, adps = _case_set(31, 700, 7, 3000, 64)
     adps = adps + ['ACGTTGCA' * k for k in (1, 2, 3, 4, 5, 6, 7)] + ['GATTACA' * 5 + 'G', 'TTAGGC' * 9]
     # wide register buckets (65..88 bp, packed-key core, pk::Lay<RPL > 64>) and past them (generic)
