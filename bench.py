@@ -93,8 +93,9 @@ def parse():
                     help='headline schedule: the library\'s side streams while both sides\' smaller buckets run on two '
                          'caller streams at once; 0 (default, r04r: 7.61 vs 7.68 ms) or 1')
     ap.add_argument('--rest-overlap', type=int, default=1,
-                    help='headline: 2 = after both dominant launches, both sides\' smaller buckets each on its own '
-                         'stream; 1 = the two sides\' calls side by side; 0 = after each side\'s dominant launch')
+                    help='headline: 3 = after both dominant launches, both sides\' smaller buckets dealt onto the two '
+                         'caller streams by cost; 2 = each on its own stream; 1 = the two sides\' calls side by side; '
+                         '0 = after each side\'s dominant launch')
     ap.add_argument('--hw-queues', type=int, default=0,
                     help='GPU_MAX_HW_QUEUES for this process when the environment does not set it (0: HIP default, '
                          '4; r04 A/B with 8: headline 8.05 vs 7.61 ms, reference job 5.85 vs 5.23 ms)')
@@ -261,18 +262,19 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
         if nd < 0:
             raise _lib.PcabiError('tile layout failed')
         n_dom = sum(1 for x in adps if dom(x))
-        groups = []                                 # (table, result rows) per register bucket of the rest
+        groups, group_first = [], []                # (table, result rows) per register bucket of the rest
         k0 = n_dom
         while k0 < len(adps):
             k1 = k0
             while k1 < len(adps) and (len(adps[k1]) + 3) // 4 == (len(adps[k0]) + 3) // 4:
                 k1 += 1
             groups.append((table(adps[k0:k1]), vp(d_res.value + 4 * k0 * n)))
+            group_first.append(k0)
             k0 = k1
         sides.append(dict(lens=lens, d_off=d_off, d_len=d_len, d_toff=h2d(toff), d_tiles=dalloc(4 * nd),
                           mq=int(np.diff(toff).max() // 256), dom=table(adps[:n_dom]), rest=table(adps[n_dom:]),
                           all=table(adps), d_res=d_res, d_res_rest=vp(d_res.value + 4 * n_dom * n), stride=stride,
-                          groups=groups))
+                          groups=groups, group_first=group_first, adps=adps))
 
     ev = []
     for _ in range(4 * args.steps + 4):
@@ -312,6 +314,32 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
                 j += 1
         for e in g_join:
             L.pcabi_stream_wait_event(stream, e)
+
+    # --rest-overlap 3: both sides' smaller buckets dealt onto the two caller streams, largest first
+    # onto the less loaded one (cost = adapters x rows), so neither stream ends long after the other
+    balanced = [[], []]
+    if args.rest_overlap == 3:
+        jobs = []
+        for i, sd in enumerate(sides):
+            for ((tab, cnt), d_res), k0 in zip(sd['groups'], sd['group_first']):
+                jobs.append((cnt * ((len(sd['adps'][k0]) + 3) // 4 * 4), i, tab, d_res))
+        jobs.sort(key=lambda x: -x[0])
+        load = [0, 0]
+        for cost, i, tab, d_res in jobs:
+            j = 0 if load[0] <= load[1] else 1
+            load[j] += cost
+            balanced[j].append((i, tab, d_res))
+
+    def align_balanced():
+        L.pcabi_event_record(ev_fork, stream)
+        L.pcabi_stream_wait_event(stream2, ev_fork)
+        for st, lst in ((stream, balanced[0]), (stream2, balanced[1])):
+            for i, tab, d_res in lst:
+                sd = sides[i]
+                _lib.check(L.pcabi_align_cross_dev(sd['d_tiles'], sd['d_toff'], sd['d_len'], n, int(sd['lens'].max()),
+                                                   tab, *sc, d_res, sd['stride'], st), 'align')
+        L.pcabi_event_record(ev_join, stream2)
+        L.pcabi_stream_wait_event(stream, ev_join)
 
     def align_rest(sd, st):
         tab, cnt = sd['rest']
@@ -385,6 +413,10 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
                 align_groups()
                 epilogue()
                 return
+            if args.rest_overlap == 3:
+                align_balanced()
+                epilogue()
+                return
             L.pcabi_event_record(ev_fork, stream)
             L.pcabi_stream_wait_event(stream2, ev_fork)
             align_rest(sides[0], stream)
@@ -396,7 +428,7 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
     # the headline schedule runs both sides' smaller buckets on two caller streams at once: the
     # library's side streams go off for it (pcabi_set_side_streams; one cross product at a time,
     # as the production schedule, keeps them on)
-    two_streams = not timed_fused and args.rest_overlap == 1
+    two_streams = not timed_fused and args.rest_overlap in (1, 3)
     side_prev = L.pcabi_set_side_streams(args.head_side_streams if two_streams else -1)
     for _ in range(args.warmup):
         step(fused=timed_fused)
