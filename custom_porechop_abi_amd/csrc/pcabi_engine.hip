@@ -1065,7 +1065,7 @@ int split_lanes(int rpl, int64_t waves) {
     if (forced >= 0) K = forced;
     else if (waves < 1024) K = rpl < 16 ? 2 : 4;
     else if (rpl >= 36 && waves < 4096) {
-        // PCABI_SPLIT_WIDE=1 (A/B): the >= 36-row packed buckets (2 waves per SIMD) of a few
+        // PCABI_SPLIT_WIDE=1 (A/B): the >= 36-row packed buckets (3-5 waves per SIMD) of a few
         // adapters in 2 lanes per window
         const char *w = std::getenv("PCABI_SPLIT_WIDE");
         if (w && w[0] == '1') K = 2;
