@@ -259,7 +259,14 @@ def test_seed_expand_one_pass(gpu_lib, monkeypatch, thr):
         assert np.array_equal(_sorted(got), exp), 'passes=%s' % mode
     assert prof['1'][11] > 0
     assert np.array_equal(prof['1'][7:15], prof['2'][7:15]), (prof['1'][7:15], prof['2'][7:15])
+    # a grid of 8 blocks: hundreds of slabs per block, in several groups of kExpandGroup
     monkeypatch.setenv('PCABI_EXPAND_PASSES', '1')
+    monkeypatch.setenv('PCABI_EXPAND_BLOCKS', '8')
+    prof['g'] = np.zeros(16, np.float64)
+    got = _dev_scan(gpu_lib, views, ADPS, SC, thr, profile=prof['g'])
+    assert np.array_equal(_sorted(got), exp), 'passes=1, 8 blocks'
+    assert np.array_equal(prof['g'][7:15], prof['2'][7:15]), (prof['g'][7:15], prof['2'][7:15])
+    monkeypatch.delenv('PCABI_EXPAND_BLOCKS')
     monkeypatch.setenv('PCABI_MIDDLE_INIT_CAPS', '0,64,0')
     n0, _ = _requeues(gpu_lib)
     got = _dev_scan(gpu_lib, views, ADPS, SC, thr)

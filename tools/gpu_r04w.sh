@@ -1,0 +1,9 @@
+#!/bin/bash
+# GPU-box script (r04): the middle-path and parity tests after the last r04 changes.
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/r04w
+mkdir -p $OUT
+cd $R
+timeout -k 10 700 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_gpu_middle_paths.py tests/test_gpu_parity.py tests/test_drivers.py > $OUT/pytest.log 2>&1 || { echo "pytest failed rc=$?"; grep -E "FAILED|Error" $OUT/pytest.log | head -20; tail -30 $OUT/pytest.log; exit 1; }
+tail -2 $OUT/pytest.log
