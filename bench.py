@@ -86,6 +86,8 @@ def parse():
                     help='reference_job: 1 = the set search\'s two sides side by side (stream2; r04 A/B: 5.13 vs '
                          '5.23 ms per step); 0 = one after the other (each side\'s dominant launch then has the GPU '
                          'to itself, the roofline\'s events)')
+    ap.add_argument('--rj-end-streams', type=int, default=0,
+                    help='reference_job: 1 = each kept adapter\'s end-trim cross product on a stream of its own (A/B)')
     ap.add_argument('--rj-side-streams', type=int, default=0,
                     help='reference_job: the library\'s side streams (pcabi_set_side_streams) during the job; 0 '
                          '(default: it runs two caller streams at once) or 1')
@@ -875,6 +877,14 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
     stream, stream2 = vp(), vp()
     _lib.check(L.pcabi_stream_create(ctypes.byref(stream)), 'stream')
     _lib.check(L.pcabi_stream_create(ctypes.byref(stream2)), 'stream')
+    # --rj-end-streams 1: each kept adapter's end-trim cross product on a stream of its own
+    x_streams, x_join = [], []
+    for _ in range(6 if args.rj_end_streams else 0):
+        xs, xe = vp(), vp()
+        _lib.check(L.pcabi_stream_create(ctypes.byref(xs)), 'stream')
+        _lib.check(L.pcabi_event_create(ctypes.byref(xe)), 'event')
+        x_streams.append(xs)
+        x_join.append(xe)
     sides = []
     for w_off, w_len, u in ((s_off, s_len, starts_u), (e_off, e_len, ends_u)):
         toff = np.zeros((n + 255) // 256 + 1, np.int64)
@@ -897,7 +907,8 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
             en_ = [a.end_sequence[1] for a in matching if a.end_sequence]
             mid = [x[1] for x in P.middle_adapter_list(matching)[0]]
             ks = dict(start=st_, end=en_, mid=mid, tabs=[table(x) if x else None for x in (st_, en_, mid)],
-                      d_res=[dalloc(4 * 8 * max(1, len(x)) * n) for x in (st_, en_)], scan=vp())
+                      d_res=[dalloc(4 * 8 * max(1, len(x)) * n) for x in (st_, en_)], scan=vp(),
+                      one=[[table([a]) for a in x] if args.rj_end_streams else [] for x in (st_, en_)])
             if mid:
                 _lib.check(L.pcabi_scan_create(ks['tabs'][2], ctypes.byref(ks['scan'])), 'scan_create')
             kept_cache[names] = ks
@@ -942,12 +953,25 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
         # the two sides' few-adapter cross products side by side (start on `stream`, end on stream2):
         # with the kept sets each bucket holds one adapter (1,564 waves), too few to fill the chip alone
         L.pcabi_stream_wait_event(stream2, ev[1])
-        for k, sd in enumerate(sides):
-            adps = ks['start'] if k == 0 else ks['end']
-            if adps:
-                _lib.check(L.pcabi_align_cross_dev(sd['d_tiles'], sd['d_toff'], sd['d_len'], n, sd['mx'], ks['tabs'][k],
-                                                   *sc, ks['d_res'][k], len(adps) * n, stream if k == 0 else stream2),
-                           'align')
+        if args.rj_end_streams:
+            j = 0
+            for k, sd in enumerate(sides):
+                adps = ks['start'] if k == 0 else ks['end']
+                for a, tab in enumerate(ks['one'][k]):
+                    xs = x_streams[j % len(x_streams)]
+                    L.pcabi_stream_wait_event(xs, ev[1])
+                    _lib.check(L.pcabi_align_cross_dev(sd['d_tiles'], sd['d_toff'], sd['d_len'], n, sd['mx'], tab, *sc,
+                                                       vp(ks['d_res'][k].value + 4 * a * n), len(adps) * n, xs), 'align')
+                    L.pcabi_event_record(x_join[j % len(x_join)], xs)
+                    L.pcabi_stream_wait_event(stream, x_join[j % len(x_join)])
+                    j += 1
+        else:
+            for k, sd in enumerate(sides):
+                adps = ks['start'] if k == 0 else ks['end']
+                if adps:
+                    _lib.check(L.pcabi_align_cross_dev(sd['d_tiles'], sd['d_toff'], sd['d_len'], n, sd['mx'],
+                                                       ks['tabs'][k], *sc, ks['d_res'][k], len(adps) * n,
+                                                       stream if k == 0 else stream2), 'align')
         L.pcabi_event_record(ev[8], stream2)
         L.pcabi_stream_wait_event(stream, ev[8])
         L.pcabi_event_record(ev[10], stream)
