@@ -86,8 +86,9 @@ def parse():
                     help='reference_job: 1 = the set search\'s two sides side by side (stream2; r04 A/B: 5.13 vs '
                          '5.23 ms per step); 0 = one after the other (each side\'s dominant launch then has the GPU '
                          'to itself, the roofline\'s events)')
-    ap.add_argument('--rj-end-streams', type=int, default=0,
-                    help='reference_job: 1 = each kept adapter\'s end-trim cross product on a stream of its own (A/B)')
+    ap.add_argument('--rj-end-streams', type=int, default=1,
+                    help='reference_job: 1 = each kept adapter\'s end-trim cross product on a stream of its own '
+                         '(r04x: 4.69-4.71 vs 4.78-4.84 ms per step); 0 = each side\'s table on one stream')
     ap.add_argument('--rj-side-streams', type=int, default=0,
                     help='reference_job: the library\'s side streams (pcabi_set_side_streams) during the job; 0 '
                          '(default: it runs two caller streams at once) or 1')
