@@ -286,7 +286,8 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
         ev.append(e)
 
     # the headline schedule's second caller stream: the two sides' smaller buckets run side by side
-    # after both dominant launches (each side's own call forks them over the library's side streams)
+    # after both dominant launches (each side's own call on its stream; the library's side streams are
+    # off while the two streams run: see two_streams below)
     stream2 = vp()
     _lib.check(L.pcabi_stream_create(ctypes.byref(stream2)), 'stream')
     ev_fork, ev_join = vp(), vp()
