@@ -86,10 +86,6 @@ def parse():
                     help='reference_job: 1 = the set search\'s two sides side by side (stream2; r04 A/B: 5.13 vs '
                          '5.23 ms per step); 0 = one after the other (each side\'s dominant launch then has the GPU '
                          'to itself, the roofline\'s events)')
-    ap.add_argument('--stage-inputs', type=int, default=1,
-                    help='middle / reference job: 1 = one staged copy of the read pack per timed step, made before '
-                         'the timed region (the scan masks hits in place); 0 = a device copy from the pristine pack '
-                         'inside every step (r04 and earlier)')
     ap.add_argument('--rj-end-streams', type=int, default=1,
                     help='reference_job: 1 = each kept adapter\'s end-trim cross product on a stream of its own '
                          '(r04x: 4.69-4.71 vs 4.78-4.84 ms per step); 0 = each side\'s table on one stream')
@@ -874,8 +870,7 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
                                                   len(lst), *sc, ctypes.byref(t)), 'adapters_create')
         return t
 
-    d_pristine = h2d(pack)
-    d_work = dalloc(pack.nbytes)
+    d_pack = h2d(pack)               # resident for every step (the middle scan leaves it intact)
     d_offs, d_lens = h2d(offs), h2d(lens.astype(np.int32))
     d_st, d_et = dalloc(4 * n), dalloc(4 * n)
     d_toff_mid, d_tlen_mid = dalloc(8 * n), dalloc(4 * n)
@@ -920,12 +915,8 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
             kept_cache[names] = ks
         return kept_cache[names]
 
-    def step(work=None):
-        # work: a staged copy of the reads (the middle scan masks its hits in place); None: restore
-        # the working copy from the pristine pack first (warm-up steps)
-        if work is None:
-            _lib.check(L.pcabi_dev_copy_async(d_work, d_pristine, pack.nbytes, 2, stream), 'copy')
-            work = d_work
+    def step():
+        work = d_pack
         L.pcabi_event_record(ev[0], stream)
         _lib.check(L.pcabi_dev_memset(d_best, 0, 8 * n_u), 'memset')
         b0 = 0
@@ -1011,27 +1002,18 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
     # 4.95 -> 4.66 ms per step): a side stream on the other caller stream's hardware queue waits
     # for its large launch
     side_prev = L.pcabi_set_side_streams(0 if args.rj_side_streams == 0 else 1)
-    staged = []
     try:
         for _ in range(max(1, args.warmup)):
             step()
-        # the timed steps' reads resident before the timed region (one staged copy per step, as
-        # run_middle; --stage-inputs 0: the per-step device copy)
-        if args.stage_inputs:
-            for _ in range(args.steps):
-                staged.append(dalloc(pack.nbytes))
-                _lib.check(L.pcabi_dev_copy_async(staged[-1], d_pristine, pack.nbytes, 2, stream), 'copy')
         _lib.check(L.pcabi_stream_sync(stream), 'sync')
         acc.clear()
         torch.cuda.synchronize() if torch.cuda.is_available() else None
         t0 = time.perf_counter()
         for k in range(args.steps):
-            matching = step(staged[k] if staged else None)
+            matching = step()
         elapsed = time.perf_counter() - t0
     finally:
         L.pcabi_set_side_streams(side_prev)
-        for p_ in staged:
-            L.pcabi_dev_free(p_)
     step_ms = 1e3 * elapsed / args.steps
     per = {k: round(v / args.steps, 4) for k, v in acc.items()}
     ks = kept_state(tuple(a.name for a in matching), matching)
@@ -1077,7 +1059,7 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
         mid_chk = middle_spot_check(reads, trims, hits, stats['hits'], ks['mid'], sc, 90.0, min(1000, n)) \
             if ks['mid'] else None
         checked = {'set_search_maxima_identical_400_reads': bool(np.array_equal(got, exp)),
-                   'end_windows': ends_chk, 'middle': mid_chk}
+                   'end_windows': ends_chk, 'middle': mid_chk, 'input_pack_intact': pack_intact(L, _lib, d_pack, pack)}
     return {'metric': 'reads/sec through the reference job (set search on 10k reads x 119 sets, then end trim + '
                       'middle scan with the kept sets)',
             'value': round(n * args.steps / elapsed, 1), 'unit': 'reads/s', 'steps': args.steps,
@@ -1104,8 +1086,7 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
                                    'end trim + middle scan of %d reads/GPU with the kept sets' % (
                                        n_chk, len(search), len(starts_u), len(ends_u), n),
                        'reads_per_gpu': n,
-                       'inputs': ('one staged copy of the read pack per timed step, resident before the timed region'
-                                  if args.stage_inputs else 'a device copy from the pristine pack inside every step')},
+                       'inputs': 'one read pack resident in HBM for every step (the scan leaves it intact)'},
             'parity_spot_check': checked, 'setup_s': round(gen_s, 2)}
 
 
@@ -1333,8 +1314,9 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
                                                   len(lst), *SCORING, ctypes.byref(t)), 'adapters_create')
         return t
 
-    d_pristine = h2d(pack)
-    d_work = dalloc(pack.nbytes)
+    # the reads, resident in HBM for every step: the middle scan leaves them intact (it masks copies
+    # of the reads that hit, as the reference masks a copy, nanopore_read.py:225,234)
+    d_pack = h2d(pack)
     d_offs, d_lens = h2d(offs), h2d(lens.astype(np.int32))
     n_sa, n_ea = len(start_adps), len(end_adps)
     d_sres, d_eres = dalloc(4 * 8 * n_sa * n), dalloc(4 * 8 * n_ea * n)
@@ -1362,12 +1344,8 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
     t_len = np.zeros(n, np.int32)
     stats = {}
 
-    def step(work=None):
-        # work: a staged copy of the reads for this step (the scan masks its hits in place); None:
-        # restore the working copy from the pristine pack first (warm-up and profiled steps)
-        if work is None:
-            _lib.check(L.pcabi_dev_copy_async(d_work, d_pristine, pack.nbytes, 2, stream), 'copy')
-            work = d_work
+    def step():
+        work = d_pack
         for sd in sides:
             _lib.check(L.pcabi_tile_windows_dev(work, sd['d_off'], sd['d_len'], n, sd['d_toff'], sd['mq'],
                                                 sd['d_tiles'], stream), 'tile')
@@ -1391,14 +1369,6 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
 
     for _ in range(args.warmup):
         step()
-    # the timed steps' inputs resident in HBM before the timed region: one staged copy of the read
-    # pack per step (the scan masks hits in place; a real batch arrives fresh), --stage-inputs 0:
-    # one device copy from the pristine pack inside every step instead
-    staged = []
-    if args.stage_inputs:
-        for _ in range(args.steps):
-            staged.append(dalloc(pack.nbytes))
-            _lib.check(L.pcabi_dev_copy_async(staged[-1], d_pristine, pack.nbytes, 2, stream), 'copy')
     _lib.check(L.pcabi_stream_sync(stream), 'sync')
     stats['middle_s'] = 0.0
     if dist is not None:
@@ -1406,10 +1376,8 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
     torch.cuda.synchronize() if torch.cuda.is_available() else None
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(staged[k] if staged else None)
+        step()
     L.pcabi_stream_sync(stream)
-    for p_ in staged:
-        L.pcabi_dev_free(p_)
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -1441,6 +1409,7 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
     if args.check and rank == 0:
         checked = middle_spot_check(reads, trims, hits, stats['hits'], mid_adps, sc, args.middle_threshold,
                                     min(args.middle_check, n))
+        checked['input_pack_intact'] = pack_intact(L, _lib, d_pack, pack)
     Lm = np.array([len(x) for x in mid_adps], np.int64)
     cells_mid = int(t_len.astype(np.int64).sum() * Lm.sum())
     cells_end = int(s_len.astype(np.int64).sum() * sum(map(len, start_adps)) +
@@ -1463,9 +1432,7 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
                                    % (n, args.mean_len, len(sets), n_sa, n_ea, len(mid_adps), args.middle_threshold),
                        'reads_per_gpu': n, 'adapter_sets': len(sets), 'scoring': list(sc),
                        'parallelism': 'dp%d (read shards)' % world,
-                       'inputs': ('one staged copy of the read pack per timed step, resident before the timed region '
-                                  '(the scan masks hits in place)' if args.stage_inputs else
-                                  'a device copy from the pristine pack inside every step')},
+                       'inputs': 'one read pack resident in HBM for every step (the scan leaves it intact)'},
             'middle_ms_per_step': round(1e3 * stats['middle_s'] / args.steps, 3),
             'middle_hits_per_step': stats['hits'],
             # the middle scan computes only the seeded band cells and its candidates' chunks, not
@@ -1828,6 +1795,14 @@ def run_e2e(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapters):
         }
         return out
     return None
+
+
+def pack_intact(L, _lib, d_pack, pack):
+    """The read pack on the device after the timed steps is byte-identical to the one uploaded:
+    the middle scan masks copies, not the caller's reads (nanopore_read.py:225,234)."""
+    back = np.empty_like(pack)
+    _lib.check(L.pcabi_dev_d2h(back.ctypes.data_as(ctypes.c_void_p), d_pack, pack.nbytes), 'd2h')
+    return bool(np.array_equal(back, pack))
 
 
 def middle_spot_check(reads, trims, hits, n_hits, mid_adps, sc, thr, k):

@@ -339,13 +339,83 @@ __global__ __launch_bounds__(256) void k_gather_views(const int64_t *win_off, co
     sub_len[k] = win_len[idx[k]];
 }
 
-// Masking of a middle hit (nanopore_read.py:245: the hit's read span becomes '-', Dna5 N):
-// one block per hit, codes[win_off[w] + s .. win_off[w] + e) = 4.
-__global__ __launch_bounds__(256) void k_mask(uint8_t *codes, const int64_t *win_off, const int32_t *mwin,
-                                              const int32_t *ms, const int32_t *me) {
-    const int64_t h = blockIdx.x;
-    const int64_t base = win_off[mwin[h]];
-    for (int64_t i = ms[h] + threadIdx.x; i < me[h]; i += 256) codes[base + i] = 4;
+// ---- input-preserving masking (r05) ------------------------------------------------------------
+// The reference masks a COPY of the read (nanopore_read.py:225 masked_seq = the trimmed read, :234
+// rebuilt with '-'), so the caller's sequence is never touched. The scan does the same on the
+// device: the caller's codes are read-only, and a read's first hit copies the whole window into a
+// shadow arena owned by the scan (16-byte aligned, zero tail padding for the window readers'
+// look-ahead), with the hit's span masked as it is copied; from then on the read's effective offset
+// eoff[w] (an offset from `codes`, like win_off) points at the copy, which later hits mask in place.
+// Only reads that hit are ever copied (round 1: ~4.5 % of a batch); every round after round 1 runs
+// on reads that hit in round 1 only.
+__device__ __forceinline__ int64_t shadow_bytes(int32_t len) { return ((int64_t)max(len, 0) + 16 + 15) & ~(int64_t)15; }
+
+// Masking of a round's hits (nanopore_read.py:245, the span becomes '-', Dna5 N): the blocks stride
+// over the list (8 int32 per hit, k_round_hits' layout), a block's threads over the read. o[7] > 0:
+// the read's first hit, shadow at arena byte (o[7] - 1) * 16 (k_round_hits' allocation): the window
+// is copied from the caller's codes with the span masked, and eoff redirected; o[7] == 0: the read
+// already has its copy (eoff), the span is masked there. *bump > cap (the round's allocations did
+// not fit): nothing is copied or masked, the round is flagged (rflag bit 8) and holds no next round,
+// so the host grows the arena and queues it again.
+__global__ __launch_bounds__(256) void k_mask_list(const uint8_t *codes, const int64_t *win_off, int64_t *eoff,
+                                                   const int32_t *win_len, const int32_t *list, int32_t *n_dev,
+                                                   uint8_t *arena, int64_t arena_rel, int64_t cap,
+                                                   const unsigned long long *bump, int32_t *rflag) {
+    if ((int64_t)*bump > cap) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            if (rflag) *rflag |= 8;
+            *n_dev = 0;
+        }
+        return;
+    }
+    const int64_t nh = *n_dev;
+    for (int64_t j = blockIdx.x; j < nh; j += gridDim.x) {
+        const int32_t *o = list + 8 * j;
+        const int32_t w = o[0], rs = o[2], rend = rs == -1 ? 0 : o[3] + 1;
+        if (o[7] > 0) {
+            // 16 bytes per thread and pass: the source's aligned dwords (those holding a byte of the
+            // window: the caller's padding is not assumed), shifted into place, the span masked,
+            // bytes past the window zero, one 16-byte store
+            const int64_t at = (int64_t)(o[7] - 1) * 16;
+            const int32_t len = win_len[w];
+            const int64_t nb = shadow_bytes(len);
+            const uintptr_t sa = (uintptr_t)(codes + win_off[w]);
+            const uint32_t *s4 = reinterpret_cast<const uint32_t *>(sa & ~(uintptr_t)3);
+            const int a0 = (int)(sa & 3), sh = 8 * a0;
+            const int64_t lim = (int64_t)len + a0;      // source dword k holds window bytes iff 4k < lim
+            uint4 *dst = reinterpret_cast<uint4 *>(arena + at);
+            for (int64_t c = threadIdx.x; c * 16 < nb; c += 256) {
+                uint32_t d[5];
+#pragma unroll
+                for (int k = 0; k < 5; ++k) d[k] = (4 * (4 * c + k) < lim) ? s4[4 * c + k] : 0u;
+                uint32_t v[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    uint32_t x = sh ? __builtin_amdgcn_alignbit(d[i + 1], d[i], sh) : d[i];
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        const int64_t pos = 16 * c + 4 * i + b;
+                        const uint32_t m = 0xFFu << (8 * b);
+                        if (pos >= len) x &= ~m;
+                        else if (pos >= rs && pos < rend) x = (x & ~m) | (4u << (8 * b));
+                    }
+                    v[i] = x;
+                }
+                dst[c] = make_uint4(v[0], v[1], v[2], v[3]);
+            }
+            if (threadIdx.x == 0) eoff[w] = arena_rel + at;
+        } else {
+            // the copy already exists: eoff[w] lies in the arena
+            uint8_t *dst = arena + (eoff[w] - arena_rel);
+            for (int64_t i = rs + threadIdx.x; i < rend; i += 256) dst[i] = 4;
+        }
+    }
+}
+
+// The arena moved (grown): every redirected offset follows it.
+__global__ __launch_bounds__(256) void k_shadow_rebase(const int64_t *win_off, int64_t *eoff, int64_t n, int64_t delta) {
+    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256)
+        if (eoff[k] != win_off[k]) eoff[k] += delta;
 }
 
 // ---- device-planned candidate DP (middle scan, seeded rounds) --------------------------------
@@ -911,12 +981,19 @@ __global__ __launch_bounds__(256) void k_round_count(const int32_t *hb, const in
     }
 }
 
+// (r05) A read's first masked hit also takes its shadow-arena space here (k_mask_list copies it):
+// one atomic per block over the block's scanned sizes; o[7] = 1 + the 16-byte unit it starts at.
 __global__ __launch_bounds__(256) void k_round_hits(const int32_t *hb, int64_t n, const int32_t *n_dev, const int32_t *cur,
                                                     const int32_t *counts, int32_t *list, int32_t *n_next,
                                                     int32_t *cur_next, int32_t *start_next, const int32_t *seed_flags,
-                                                    const int32_t *plan_flag, int32_t *rflag) {
+                                                    const int32_t *plan_flag, int32_t *rflag, const int64_t *win_off,
+                                                    const int64_t *eoff, const int32_t *win_len,
+                                                    unsigned long long *bump) {
     typedef hipcub::BlockScan<int, 256> Scan;
+    typedef hipcub::BlockScan<long long, 256> Scan64;
     __shared__ typename Scan::TempStorage scan_tmp;
+    __shared__ typename Scan64::TempStorage scan64_tmp;
+    __shared__ unsigned long long s_at;
     __shared__ int s_part[4];
     const int32_t f = (seed_flags[0] ? 1 : 0) | (seed_flags[1] ? 2 : 0) | (*plan_flag ? 4 : 0);
     if (blockIdx.x == 0 && threadIdx.x == 0) *rflag = f;
@@ -933,36 +1010,32 @@ __global__ __launch_bounds__(256) void k_round_hits(const int32_t *hb, int64_t n
         const int32_t a = k < nr ? hb[k] : -1;
         int pos = 0, tot = 0;
         Scan(scan_tmp).ExclusiveSum(a >= 0 ? 1 : 0, pos, tot);
+        const int32_t r = a >= 0 ? (cur ? cur[k] : (int32_t)k) : 0;
+        const int32_t rs = a >= 0 ? hb[1 * n + k] : -1, re = a >= 0 ? hb[2 * n + k] : 0;
+        // shadow space (16-byte units) of a first masked hit
+        long long units = 0;
+        if (a >= 0 && rs != -1 && re + 1 > rs && eoff[r] == win_off[r]) units = shadow_bytes(win_len[r]) / 16;
+        long long uex = 0, utot = 0;
+        Scan64(scan64_tmp).ExclusiveSum(units, uex, utot);
+        if (threadIdx.x == 0) s_at = utot ? atomicAdd(bump, (unsigned long long)utot * 16ull) : 0ull;
+        __syncthreads();
         if (a >= 0) {
             const int32_t j = base + pos;
-            const int32_t r = cur ? cur[k] : (int32_t)k;
             int32_t *o = list + 8 * (int64_t)j;
             o[0] = r;
             o[1] = a;
-            o[2] = hb[1 * n + k];
-            o[3] = hb[2 * n + k];
+            o[2] = rs;
+            o[3] = re;
             o[4] = hb[3 * n + k];
             o[5] = hb[4 * n + k];
             o[6] = (int32_t)k;
-            o[7] = 0;
+            const long long at = (long long)(s_at / 16ull) + uex;   // a unit index; < 2^31 (checked by the host's cap)
+            o[7] = units ? (int32_t)min(at + 1, (long long)INT32_MAX) : 0;
             cur_next[j] = r;
             start_next[j] = a;
         }
         if (c == nch - 1 && threadIdx.x == 0) *n_next = base + tot;
         __syncthreads();                                       // s_part, scan_tmp reused
-    }
-}
-
-// Masking of a round's hits (nanopore_read.py:245, the span becomes '-', Dna5 N): the blocks stride
-// over the list, a block's threads over the span.
-__global__ __launch_bounds__(256) void k_mask_list(uint8_t *codes, const int64_t *win_off, const int32_t *list,
-                                                   const int32_t *n_dev) {
-    const int64_t nh = *n_dev;
-    for (int64_t j = blockIdx.x; j < nh; j += gridDim.x) {
-        const int32_t *o = list + 8 * j;
-        const int32_t rs = o[2], rend = rs == -1 ? 0 : o[3] + 1;
-        const int64_t base = win_off[o[0]];
-        for (int64_t i = rs + threadIdx.x; i < rend; i += 256) codes[base + i] = 4;
     }
 }
 
@@ -1312,7 +1385,7 @@ struct MidProf {
 
 struct pcabi_scan {
     const pcabi_adapters *adps = nullptr;
-    DeviceBuf tiles, toff, res, hits, idx, start, soff, slen, mwin, ms, me;
+    DeviceBuf tiles, toff, res, hits, idx, start, soff, slen, mwin;
     DeviceBuf s16, tw, to, wa, pres, tck;   // score filter + candidate pairs (chunks)
     DeviceBuf pspan, ptasks, pfill, pwoff, pcidx, pcand, pbest, phit, phb, plist, pcnt, plen;   // device planning
     DeviceBuf tw2, to2, tck2, pcand2, wa2, pres2, pcert, pucert, q_bk2, q_misc2;   // candidate windows' second plan
@@ -1330,6 +1403,10 @@ struct pcabi_scan {
     std::vector<int32_t> h_up;                      // bucket tables | spans | lengths last uploaded
     const void *up_at[3] = {nullptr, nullptr, nullptr};   // ... into these buffers
     DeviceBuf pcount;                               // k_round_count's per-chunk hit counts
+    // (r05) input-preserving masking: the reads' effective offsets and the shadow arena of the
+    // masked copies (shadow_cap: its usable bytes), a zeroed bump for the host-driven loop
+    DeviceBuf eoff, shadow, shadow_zero;
+    int64_t shadow_cap = 0;
     MidProf prof;                                   // pcabi_scan_profile
     DeviceBuf pprof;                                // its device counters (4 x u64)
 };
@@ -2171,7 +2248,7 @@ int pcabi_scan_create(const pcabi_adapters *adps, pcabi_scan **out) {
 void pcabi_scan_destroy(pcabi_scan *s) {
     if (!s) return;
     for (DeviceBuf *b : {&s->tiles, &s->toff, &s->res, &s->hits, &s->idx, &s->start, &s->soff, &s->slen,
-                         &s->mwin, &s->ms, &s->me, &s->s16, &s->tw, &s->to, &s->wa, &s->pres, &s->tck,
+                         &s->mwin, &s->eoff, &s->shadow, &s->shadow_zero, &s->s16, &s->tw, &s->to, &s->wa, &s->pres, &s->tck,
                          &s->pspan, &s->ptasks, &s->pfill, &s->pwoff, &s->pcidx, &s->pcand, &s->pbest, &s->phit, &s->phb,
                          &s->plist, &s->pcnt, &s->q_cur, &s->q_start, &s->q_list, &s->q_n, &s->q_flags,
                          &s->q_bk, &s->q_wave, &s->q_misc, &s->pcbase, &s->plen, &s->tw2, &s->to2, &s->tck2,
@@ -2684,6 +2761,60 @@ bool middle_devrounds_on() {
     return !(e && e[0] == '0');
 }
 
+// ---- the shadow arena of the input-preserving masking (k_round_hits, k_mask_list) ----------------
+// eoff values are offsets from the caller's `codes`, so a copy in the arena is addressed as
+// codes + eoff like any window (a flat device address space).
+int64_t shadow_rel(const pcabi_scan *sc, const uint8_t *codes) {
+    return (int64_t)((intptr_t)sc->shadow.p - (intptr_t)codes);
+}
+constexpr int64_t kShadowMax = (int64_t)INT32_MAX * 16;   // k_round_hits' 16-byte unit index is an int32
+constexpr int64_t kShadowLead = 256;                      // arena bytes before the first copy
+
+// The arena's first size: 1/8 of the batch's bases (about 3x the ~4.5 % of reads a round 1 hits at
+// the default threshold), at least 16 MB; tests set it with the 4th PCABI_MIDDLE_INIT_CAPS value.
+int shadow_reserve(pcabi_scan *sc, const int32_t *h_win_len, int64_t n) {
+    if (sc->shadow_cap > 0) return 0;
+    int64_t want = 16ll << 20;
+    if (h_win_len) {
+        int64_t bases = 0;
+        for (int64_t k = 0; k < n; ++k) bases += std::max(h_win_len[k], 0);
+        want = std::max(want, bases / 8);
+    }
+    long long raw = 0, task = 0, slots = 0, arena = 0;
+    if (const char *e = std::getenv("PCABI_MIDDLE_INIT_CAPS"))
+        if (std::sscanf(e, "%lld,%lld,%lld,%lld", &raw, &task, &slots, &arena) == 4 && arena > 0) want = arena;
+    want = std::min(std::max(want, kShadowLead), kShadowMax);
+    if (int rc = sc->shadow.ensure((size_t)want)) return rc;
+    sc->shadow_cap = want;
+    return 0;
+}
+
+// A larger arena (the round that ran out flagged itself and is queued again): the copies move with
+// it (eoff rebased), and the bump goes on from the old end. taken: the bytes the rounds asked for.
+int shadow_grow(pcabi_scan *sc, const uint8_t *codes, const int64_t *win_off, int64_t *eoff, int64_t n, int64_t taken,
+                unsigned long long *d_bump, hipStream_t st) {
+    (void)codes;
+    const int64_t old_cap = sc->shadow_cap;
+    const int64_t want = std::min<int64_t>(std::max<int64_t>(2 * std::max(old_cap, taken), 1ll << 20), kShadowMax);
+    if (want <= old_cap || want < taken - old_cap) return fail(PCABI_E_NOMEM, "middle scan: shadow arena past its limit");
+    void *np = nullptr;
+    if (hipMalloc(&np, (size_t)want) != hipSuccess) return fail(PCABI_E_NOMEM, "hipMalloc failed (shadow arena)");
+    if (sc->shadow.p && old_cap > 0) HIP_TRY(hipMemcpyAsync(np, sc->shadow.p, (size_t)old_cap, hipMemcpyDeviceToDevice, st));
+    const int64_t delta = (int64_t)((intptr_t)np - (intptr_t)sc->shadow.p);
+    if (sc->shadow.p && n > 0)
+        hipLaunchKernelGGL(k_shadow_rebase, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 2048)), dim3(256), 0, st,
+                           win_off, eoff, n, delta);
+    HIP_TRY(hipGetLastError());
+    const unsigned long long at = (unsigned long long)old_cap;
+    if (d_bump) HIP_TRY(hipMemcpyAsync(d_bump, &at, sizeof(at), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (sc->shadow.p) HIP_TRY(hipFree(sc->shadow.p));
+    sc->shadow.p = np;
+    sc->shadow.cap = (size_t)want;
+    sc->shadow_cap = want;
+    return 0;
+}
+
 // Overflow recovery of the queued rounds, counted for the tests (pcabi_middle_requeues).
 std::atomic<int64_t> g_requeues{0};
 std::atomic<int32_t> g_requeue_flags{0};
@@ -2699,7 +2830,7 @@ std::vector<std::pair<int64_t, int>> middle_faults() {
         long long r = 0;
         int bits = 0, used = 0;
         if (std::sscanf(e, "%lld:%d%n", &r, &bits, &used) < 2 || used <= 0) break;
-        f.emplace_back((int64_t)r, bits & 7);
+        f.emplace_back((int64_t)r, bits & 15);
         e += used;
         if (*e == ',') ++e;
     }
@@ -2718,7 +2849,7 @@ std::vector<std::pair<int64_t, int>> middle_faults() {
 // by (round, read): per read the reference's discovery order.
 // Returns the hit count (> 0, <= 0 on error as pcabi_middle_scan_dev); applied = false when the
 // seeded plan does not cover this table and scoring (the caller runs the host-driven loop).
-int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_off, const int32_t *win_len,
+int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t *win_off, const int32_t *win_len,
                              const int32_t *h_win_len, int64_t n_win, const pcabi::Scoring &scr, double threshold,
                              int32_t *hits, int64_t cap, hipStream_t st, bool &applied) {
     applied = false;
@@ -2767,9 +2898,12 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
     if (int rc = sc->q_start.ensure(4 * (size_t)n * (kSlots + 1))) return rc;
     if (int rc = sc->q_list.ensure(4 * 8 * (size_t)n * kSlots)) return rc;
     // the control block, laid out as its pinned host copy (one D2H per batch of rounds): round
-    // counts [kSlots + 2], round flags [kSlots + 2], then int64 [slots, need, plan flag, need2]
-    constexpr size_t kCtlBytes = 4 * 2 * (kSlots + 2) + 8 * 4;
+    // counts [kSlots + 2], round flags [kSlots + 2], then int64 [slots, need, plan flag, need2,
+    // shadow-arena bytes taken]
+    constexpr size_t kCtlBytes = 4 * 2 * (kSlots + 2) + 8 * 5;
     if (int rc = sc->q_n.ensure(kCtlBytes)) return rc;
+    if (int rc = sc->eoff.ensure(sizeof(int64_t) * n)) return rc;
+    if (int rc = shadow_reserve(sc, h_win_len, n)) return rc;
     if (int rc = sc->soff.ensure(sizeof(int64_t) * n)) return rc;
     if (int rc = sc->slen.ensure(sizeof(int32_t) * n)) return rc;
     if (int rc = sc->pspan.ensure(sizeof(int32_t) * n_adp)) return rc;
@@ -2827,8 +2961,16 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
     // q_misc: [0] slots, [1] need, [2] plan flag (int32), [3] the second plan's need (read with need)
     int64_t *d_slots2 = (int64_t *)sc->q_misc2.p;
     int64_t *d_slots = (int64_t *)((int32_t *)sc->q_n.p + 2 * (kSlots + 2)), *d_need = d_slots + 1, *d_need2 = d_slots + 3;
+    unsigned long long *d_bump = (unsigned long long *)(d_slots + 4);
     int32_t *d_pflag = (int32_t *)(d_slots + 2);
     int32_t *d_n = (int32_t *)sc->q_n.p, *d_rflag = d_n + (kSlots + 2);
+    // the reads' effective offsets start as the caller's; no shadow taken yet
+    int64_t *eoff = (int64_t *)sc->eoff.p;
+    HIP_TRY(hipMemcpyAsync(eoff, win_off, sizeof(int64_t) * n, hipMemcpyDeviceToDevice, st));
+    // the bump starts past the arena's lead-in (kShadowLead bytes no copy uses: band loads that
+    // reach a little before a read's start stay inside the allocation)
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)d_bump, (int)kShadowLead, 1, st));
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)((int32_t *)d_bump + 1), 0, 1, st));
     auto cur_of = [&](int slot) { return (int32_t *)sc->q_cur.p + (int64_t)slot * n; };
     auto start_of = [&](int slot) { return (int32_t *)sc->q_start.p + (int64_t)slot * n; };
     auto list_of = [&](int slot) { return (int32_t *)sc->q_list.p + (int64_t)slot * 8 * n; };
@@ -2897,13 +3039,13 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
             if (phase >= 0 && from) pf_.spans.emplace_back(phase, from, e);
             return e;
         };
-        hipLaunchKernelGGL(k_round_views, dim3(first ? 1 : gn), dim3(256), 0, st, win_off, win_len, cur, nr,
+        hipLaunchKernelGGL(k_round_views, dim3(first ? 1 : gn), dim3(256), 0, st, eoff, win_len, cur, nr,
                            (int64_t *)sc->soff.p, (int32_t *)sc->slen.p, d_n + r + 1, d_pflag, (int32_t *)sc->ptasks.p,
                            (int32_t *)sc->pfill.p, n_adp, first ? d_n : nullptr, (int32_t)n);
         const int64_t *dcand = nullptr;
         const unsigned long long *dcount = nullptr;
         const int32_t *sflags = nullptr;
-        const int64_t *v_off = first ? win_off : (const int64_t *)sc->soff.p;
+        const int64_t *v_off = first ? eoff : (const int64_t *)sc->soff.p;
         const int32_t *v_len = first ? win_len : (const int32_t *)sc->slen.p;
         const int4 *vlist = nullptr;
         const int32_t *vcount = nullptr, *pmap = nullptr;
@@ -3047,8 +3189,10 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
                            (int32_t *)sc->pcount.p);
         hipLaunchKernelGGL(k_round_hits, dim3(gn), dim3(256), 0, st, (const int32_t *)sc->phb.p, n, nr, cur,
                            (const int32_t *)sc->pcount.p, list_of(r), d_n + r + 1, cur_of(r + 1), start_of(r + 1),
-                           sflags, d_pflag, d_rflag + r);
-        hipLaunchKernelGGL(k_mask_list, dim3(1024), dim3(256), 0, st, codes, win_off, list_of(r), d_n + r + 1);
+                           sflags, d_pflag, d_rflag + r, win_off, (const int64_t *)eoff, win_len, d_bump);
+        hipLaunchKernelGGL(k_mask_list, dim3(1024), dim3(256), 0, st, codes, win_off, eoff, win_len, list_of(r),
+                           d_n + r + 1, (uint8_t *)sc->shadow.p, shadow_rel(sc, codes), (fault & 8) ? (int64_t)-1 : sc->shadow_cap,
+                           (const unsigned long long *)d_bump, d_rflag + r);
         HIP_TRY(hipGetLastError());
         if (g_debug) {                               // debugging only: a synchronisation per round
             int64_t c[5];
@@ -3093,8 +3237,8 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
     // pinned control block: round counts [kSlots + 2], flags [kSlots + 2], need / flag word / need2
     if (!sc->h_ctl) HIP_TRY(hipHostMalloc((void **)&sc->h_ctl, kCtlBytes + 8, hipHostMallocDefault));
     int32_t *h_n = sc->h_ctl, *h_flag = sc->h_ctl + (kSlots + 2);
-    int64_t *h_nd = (int64_t *)(sc->h_ctl + 2 * (kSlots + 2));   // [0..3] as the device's; [4] round 1's segments
-    h_nd[4] = -1;
+    int64_t *h_nd = (int64_t *)(sc->h_ctl + 2 * (kSlots + 2));   // [0..4] as the device's; [5] round 1's segments
+    h_nd[5] = -1;
     // every queued round's first spec entries come back with the counts (one synchronisation per
     // batch of rounds instead of two); a round with more hits fetches the rest after
     const int64_t spec = std::min<int64_t>(sc->spec_hits, n);
@@ -3116,7 +3260,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
         for (int r = slot; r < upto; ++r) {
             if (int rc = queue_round(r)) return rc;
             if (r == 0 && round_base == 0)        // round 1's segment total (the next call's mean length)
-                HIP_TRY(hipMemcpyAsync(h_nd + 4, pcabi_seed::seg_cum_dev(sc->seed) + n, sizeof(int64_t),
+                HIP_TRY(hipMemcpyAsync(h_nd + 5, pcabi_seed::seg_cum_dev(sc->seed) + n, sizeof(int64_t),
                                        hipMemcpyDeviceToHost, st));
         }
         queued_to = upto;
@@ -3153,7 +3297,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
                              (long long)(round_base + r), h_n[r], h_n[r + 1], h_flag[r]);
         if (bad >= 0) {
             g_requeues.fetch_add(1);
-            g_requeue_flags.fetch_or(h_flag[bad] & 7);
+            g_requeue_flags.fetch_or(h_flag[bad] & 15);
             // the rounds queued behind it ran on no reads: their injected faults fire again
             for (size_t k = 0; k < faults.size(); ++k)
                 if (faults[k].first > round_base + bad) fired[k] = 0;
@@ -3167,6 +3311,10 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
                 const int64_t most = std::max(need, need2);
                 sc->q_slots_cap = std::max<int64_t>(2 * sc->q_slots_cap, most + most / 4);
             }
+            // the shadow arena was too small for the round's first hits: a larger one (the copies
+            // made so far move with it), allocations go on past the old end
+            if ((h_flag[bad] & 8) && h_nd[4] > sc->shadow_cap)
+                if (int rc = shadow_grow(sc, codes, win_off, eoff, n, h_nd[4], d_bump, st)) return rc;
             HIP_TRY(hipStreamSynchronize(st));
             slot = bad;
             continue;
@@ -3185,7 +3333,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, uint8_t *codes, const int64_t *win_
     // the next call stages as many hits per round as this one's busiest round had (+ 25 %), and
     // takes its mean read length from this call's round-1 segments
     sc->spec_hits = std::max<int64_t>(4096, most_hits + most_hits / 4);
-    if (h_nd[4] >= 0 && n > 0) sc->last_mean = (double)h_nd[4] * pcabi_seed::seg_positions() / (double)n;
+    if (h_nd[5] >= 0 && n > 0) sc->last_mean = (double)h_nd[5] * pcabi_seed::seg_positions() / (double)n;
     // (round, read) order: per read the reference's discovery order. The rounds come in order and
     // each round's list in read order (k_round_hits' ordered compaction): only checked here
     const int64_t total = (int64_t)out_round.size();
@@ -3237,7 +3385,7 @@ int64_t pcabi_middle_requeues(int32_t *flags_seen) {
     return g_requeues.load();
 }
 
-int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win_off, const int32_t *win_len,
+int64_t pcabi_middle_scan_dev(pcabi_scan *sc, const uint8_t *codes, const int64_t *win_off, const int32_t *win_len,
                               const int32_t *h_win_len, int64_t n_win, int match, int mismatch, int gap_open,
                               int gap_extend, double threshold, int32_t *hits, int64_t cap, void *stream) {
     if (!sc || n_win < 0 || cap < 0) return fail(PCABI_E_ARG, "bad arguments");
@@ -3283,8 +3431,17 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
         if (applied || r < 0) return r;
     }
     if (int rc = host_lengths()) return rc;
+    // input-preserving masking (k_mask_list): effective offsets, shadows allocated on the host here
+    if (int rc = sc->eoff.ensure(sizeof(int64_t) * n_win)) return rc;
+    if (int rc = sc->shadow_zero.ensure(sizeof(unsigned long long))) return rc;
+    if (int rc = shadow_reserve(sc, h_win_len, n_win)) return rc;
+    int64_t *eoff = (int64_t *)sc->eoff.p;
+    HIP_TRY(hipMemcpyAsync(eoff, win_off, sizeof(int64_t) * n_win, hipMemcpyDeviceToDevice, st));
+    HIP_TRY(hipMemsetAsync(sc->shadow_zero.p, 0, sizeof(unsigned long long), st));
+    std::vector<char> shadowed((size_t)n_win, 0);
+    int64_t sh_bump = kShadowLead;                  // arena bytes taken (the lead-in first)
     int64_t n_hits = 0;
-    std::vector<int32_t> cur, nxt, nxt_start, hm_w, hm_s, hm_e, lens;
+    std::vector<int32_t> cur, nxt, nxt_start, hm_list, lens;
     std::vector<int32_t> hb;
     std::vector<int64_t> toff;
     std::vector<int16_t> h16;                       // round-1 filter scores (bounds for later rounds)
@@ -3323,7 +3480,7 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
     }
     for (int round = 0;; ++round) {
         const int64_t n = (int64_t)cur.size();
-        const int64_t *v_off = win_off;
+        const int64_t *v_off = eoff;
         const int32_t *v_len = win_len;
         lens.resize((size_t)n);
         {
@@ -3335,7 +3492,7 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
             HIP_TRY(hipMemcpyAsync(sc->idx.p, cur.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
             if (round > 0)
                 HIP_TRY(hipMemcpyAsync(sc->start.p, nxt_start.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
-            hipLaunchKernelGGL(k_gather_views, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, win_off, win_len,
+            hipLaunchKernelGGL(k_gather_views, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, eoff, win_len,
                                (const int32_t *)sc->idx.p, n, (int64_t *)sc->soff.p, (int32_t *)sc->slen.p);
             v_off = (const int64_t *)sc->soff.p;
             v_len = (const int32_t *)sc->slen.p;
@@ -3396,7 +3553,7 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
             HIP_TRY(hipMemcpyAsync(hb.data(), sc->hits.p, sizeof(int32_t) * 5 * n, hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
         }
-        nxt.clear(); nxt_start.clear(); hm_w.clear(); hm_s.clear(); hm_e.clear();
+        nxt.clear(); nxt_start.clear(); hm_list.clear();
         for (int64_t k = 0; k < n; ++k) {
             const int32_t a = hb[k];
             if (a < 0) continue;
@@ -3414,22 +3571,35 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, uint8_t *codes, const int64_t *win
             ++n_hits;
             nxt.push_back(r);
             nxt_start.push_back(a);
-            if (rend > rs) { hm_w.push_back(r); hm_s.push_back(rs); hm_e.push_back(rend); }
+            if (rend > rs) {                       // k_mask_list's entry; a read's first: its shadow
+                int32_t unit = 0;
+                if (!shadowed[r]) {
+                    shadowed[r] = 1;
+                    unit = (int32_t)(sh_bump / 16) + 1;
+                    sh_bump += (std::max(h_win_len[r], 0) + 16 + 15) & ~(int64_t)15;
+                }
+                const int32_t e[8] = {r, a, rs, re, 0, 0, 0, unit};
+                hm_list.insert(hm_list.end(), e, e + 8);
+            }
         }
         if (g_debug)
             std::fprintf(stderr, "[pcabi] middle host round %d: %lld reads, %zu hits (%s)\n", round, (long long)n,
                          nxt.size(), filt ? "filtered" : "cross product");
         if (nxt.empty()) break;
-        if (!hm_w.empty()) {
-            const size_t m = hm_w.size();
-            if (int rc = sc->mwin.ensure(sizeof(int32_t) * m)) return rc;
-            if (int rc = sc->ms.ensure(sizeof(int32_t) * m)) return rc;
-            if (int rc = sc->me.ensure(sizeof(int32_t) * m)) return rc;
-            HIP_TRY(hipMemcpyAsync(sc->mwin.p, hm_w.data(), sizeof(int32_t) * m, hipMemcpyHostToDevice, st));
-            HIP_TRY(hipMemcpyAsync(sc->ms.p, hm_s.data(), sizeof(int32_t) * m, hipMemcpyHostToDevice, st));
-            HIP_TRY(hipMemcpyAsync(sc->me.p, hm_e.data(), sizeof(int32_t) * m, hipMemcpyHostToDevice, st));
-            hipLaunchKernelGGL(k_mask, dim3((unsigned)m), dim3(256), 0, st, codes, win_off,
-                               (const int32_t *)sc->mwin.p, (const int32_t *)sc->ms.p, (const int32_t *)sc->me.p);
+        if (!hm_list.empty()) {
+            if (sh_bump > sc->shadow_cap) {           // grow first: this round's copies go past the end
+                if (sh_bump > kShadowMax) return fail(PCABI_E_NOMEM, "middle scan: shadow arena past its limit");
+                if (int rc = shadow_grow(sc, codes, win_off, eoff, n_win, sh_bump, nullptr, st)) return rc;
+            }
+            const int32_t m = (int32_t)(hm_list.size() / 8);
+            if (int rc = sc->mwin.ensure(sizeof(int32_t) * (hm_list.size() + 1))) return rc;
+            HIP_TRY(hipMemcpyAsync(sc->mwin.p, hm_list.data(), sizeof(int32_t) * hm_list.size(), hipMemcpyHostToDevice, st));
+            int32_t *d_m = (int32_t *)sc->mwin.p + hm_list.size();
+            HIP_TRY(hipMemcpyAsync(d_m, &m, sizeof(int32_t), hipMemcpyHostToDevice, st));
+            hipLaunchKernelGGL(k_mask_list, dim3((unsigned)std::min<int32_t>(m, 1024)), dim3(256), 0, st, codes, win_off,
+                               eoff, win_len, (const int32_t *)sc->mwin.p, d_m, (uint8_t *)sc->shadow.p,
+                               shadow_rel(sc, codes), sc->shadow_cap, (const unsigned long long *)sc->shadow_zero.p,
+                               (int32_t *)nullptr);
             HIP_TRY(hipGetLastError());
         }
         // host vectors uploaded above must stay intact until the copies ran

@@ -972,8 +972,10 @@ __device__ __forceinline__ int band_best(const uint8_t *rd, int len, const uint8
     constexpr int W = 2 * E + 1;
     int S[W], V[W], R[W];
     // rd[d0 - E] onwards; an edge band's columns outside 1 .. len are masked (7 never matches) and
-    // its loads stay inside [codes, rd + len] (the buffer's start; the read's end)
-    ByteStream<CHECK> bs(rd + (d0 - E), (uintptr_t)codes & ~(uintptr_t)3, ((uintptr_t)(rd + len)) & ~(uintptr_t)3);
+    // its loads stay inside [rd, rd + len] (the read's own start and end, dword-aligned: the read may
+    // lie in the caller's codes or in the scan's shadow arena of masked copies, r05)
+    (void)codes;
+    ByteStream<CHECK> bs(rd + (d0 - E), (uintptr_t)rd & ~(uintptr_t)3, ((uintptr_t)(rd + len)) & ~(uintptr_t)3);
 #pragma unroll
     for (int x = 0; x < W; ++x) {
         const int j0 = d0 + x - E;                           // row 0
@@ -1121,14 +1123,17 @@ __global__ __launch_bounds__(256) void k_seed_band_pin(const int4 *task, const i
     int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int bs = pcabi::best_sub(sc), ma = sc.ma, mi = sc.mi, go = sc.go, ge = sc.ge;
     const uintptr_t lo_addr = (uintptr_t)codes & ~(uintptr_t)15;
-    // the range of a task: [cb, cb + 16 * nld) with cb = (probe - o - E) & ~15
+    // the range of a task: [cb, cb + 16 * nld) with cb = (probe - o - E) & ~15. An inside band lies
+    // within its read, so the range starts inside the read's buffer; the clamp to the start of the
+    // caller's codes is a guard for reads there only (a masked copy in the scan's shadow arena, r05,
+    // may lie below codes; the arena's first 256 bytes are a lead-in no copy uses)
     auto range_of = [&](const int4 &rc, uintptr_t &cb, int &nld) {
         const int a = rc.y >> 11, o = rc.y & 255;
         const int L = (int)((uint32_t)ameta[a] & 255u);
         const uintptr_t pa = (uintptr_t)codes + (uintptr_t)(((uint64_t)(uint32_t)rc.w << 32) | (uint32_t)rc.z);
         const uintptr_t lo = pa - (uintptr_t)(o + E), hi = pa - (uintptr_t)o + (uintptr_t)(L + E);
         cb = lo & ~(uintptr_t)15;
-        if (cb < lo_addr) cb = lo_addr;
+        if (pa >= lo_addr && cb < lo_addr) cb = lo_addr;
         nld = (int)((hi - cb + 15) >> 4);
     };
     // ---- pipeline: recA / chA = the task to copy into the slot next, recB = the one after

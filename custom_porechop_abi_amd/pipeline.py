@@ -200,8 +200,8 @@ class FileTrimmer(object):
                     check(int(nh), 'pcabi_middle_scan_dev')
                 if nh <= cap:
                     break
-                cap = int(nh)                 # the scan masked the codes: re-upload and rerun
-                d_codes = self._h2d('codes', batch.codes)
+                cap = int(nh)                 # the scan leaves the codes intact: rerun, larger
+
             hits = hits[:, :int(nh)]
             # NanoporeRead._apply_middle_hit's trim ranges (nanopore_read.py:242-250) on the device,
             # grouped per read in the writer's cut layout

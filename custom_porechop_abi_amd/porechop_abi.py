@@ -17,6 +17,7 @@ re-enters the next round from that adapter on. Rounds repeat until no read has a
 import contextlib
 import gc
 import sys
+import threading
 
 import numpy as np
 
@@ -243,18 +244,34 @@ def end_windows_pack(reads, end_size):
     return pack.codes, (pack.offsets[:n], pack.lengths[:n]), (pack.offsets[n:], pack.lengths[n:])
 
 
+_gc_lock = threading.Lock()
+_gc_state = {'depth': 0, 'froze': False}
+
+
 @contextlib.contextmanager
 def _gc_paused():
     """While a driver makes its ~10^5 result tuples / lists, every object alive at the start (the
     batch's NanoporeRead objects among them) sits in the collector's permanent generation
     (gc.freeze), so the collections the new objects trigger do not walk the whole batch (a full
     pass over 100k reads cost a third of the end-trim driver's host time). The collector stays on:
-    other threads' cyclic garbage is still collected. gc.unfreeze() hands the objects back."""
-    gc.freeze()
+    other threads' cyclic garbage is still collected. Freezing is process-wide, so it is done only
+    when nothing is frozen yet (an application that froze its own objects, e.g. before a fork, keeps
+    them frozen: the drivers then run without the shortcut), and nested or concurrent drivers share
+    one freeze, undone by the last one out."""
+    with _gc_lock:
+        if _gc_state['depth'] == 0:
+            _gc_state['froze'] = gc.get_freeze_count() == 0
+            if _gc_state['froze']:
+                gc.freeze()
+        _gc_state['depth'] += 1
     try:
         yield
     finally:
-        gc.unfreeze()
+        with _gc_lock:
+            _gc_state['depth'] -= 1
+            if _gc_state['depth'] == 0 and _gc_state['froze']:
+                gc.unfreeze()
+                _gc_state['froze'] = False
 
 
 def _attrs(objs, name):

@@ -55,22 +55,30 @@ def _device_tensor(values, group):
 
 
 def rank_device(device=None):
-    """The GPU of this rank: `device` if given, else LOCAL_RANK (torch.distributed.run sets it),
-    else the rank in the default group (launchers that set RANK only: one process per GPU of a
-    single node), else 0. A local rank past the node's GPU count is an error, not a shared card."""
+    """The GPU of this rank: `device` if given, else LOCAL_RANK (torch.distributed.run sets it; a
+    LOCAL_RANK past the node's GPU count is an error, not a shared card), else the global rank
+    modulo the node's GPU count (launchers that set RANK only, srun / MPI style: one process per GPU
+    on each node), else 0."""
     import os
+    import warnings
+    import torch
     if device is not None:
         return int(device)
+    n = torch.cuda.device_count()   # counting does not initialise the GPU
     if 'LOCAL_RANK' in os.environ:
         dev = int(os.environ['LOCAL_RANK'])
-    else:
-        dist = _dist()
-        dev = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
-    import torch
-    n = torch.cuda.device_count()   # counting does not initialise the GPU
-    if n > 0 and dev >= n:
-        raise RuntimeError('rank device %d but this node has %d GPU(s): one process per GPU' % (dev, n))
-    return dev
+        if n > 0 and dev >= n:
+            raise RuntimeError('LOCAL_RANK %d but this node has %d GPU(s): one process per GPU' % (dev, n))
+        return dev
+    dist = _dist()
+    if not (dist.is_available() and dist.is_initialized()):
+        return 0
+    rank, world = dist.get_rank(), dist.get_world_size()
+    if n > 0 and world > n:
+        warnings.warn('LOCAL_RANK is not set and the world (%d) exceeds this node\'s %d GPU(s): rank %d takes GPU %d '
+                      '(rank mod GPUs, one process per GPU on each node); set LOCAL_RANK on multi-node jobs'
+                      % (world, n, rank, rank % n))
+    return rank % n if n > 0 else rank
 
 
 def find_matching_adapter_sets(check_reads, verbosity, end_size, scoring_scheme_vals, print_dest,
@@ -229,6 +237,44 @@ def spool_distribute(in_path, spool, job, world, chunk_bytes=None, depth=SPOOL_D
             fo.write('%s: %s' % (type(ex).__name__, ex))
 
 
+def spool_fail_cleanup(spool, job, rank, world, wait_s=30.0, poll=0.01):
+    """A failed rank's share of the spool cleanup (the job raised on this rank): its own spans that
+    were never consumed go (span c belongs to rank c % world), then an acknowledgement marker. Rank
+    0 -- which has joined the distributor, so nothing new appears -- removes every file of the job
+    once every rank has acknowledged (or after wait_s); the other ranks wait (bounded) until it has,
+    so a launcher that kills the rest of a job when one process fails
+    (torch.multiprocessing.spawn) cannot cut rank 0's cleanup short."""
+    import os
+    import time
+    pre = _spool_prefix(spool, job)
+    d, base = os.path.split(pre)
+
+    def rm(name):
+        try:
+            os.remove(os.path.join(d, name))
+        except FileNotFoundError:
+            pass
+
+    for f in os.listdir(d):
+        head = f[len(base):].split('_', 1)[0] if f.startswith(base) else ''
+        if head.isdigit() and int(head) % world == rank:
+            rm(f)                                 # a span (or its .tmp) of this rank
+    with open(pre + 'ack%d' % rank, 'w'):
+        pass
+    t_end = time.monotonic() + wait_s
+    while time.monotonic() < t_end:
+        names = set(os.listdir(d))
+        if rank == 0 and all(base + 'ack%d' % r in names for r in range(world)):
+            break
+        if rank != 0 and base + 'ack%d' % rank not in names:
+            return                                # rank 0 has cleaned up
+        time.sleep(poll)
+    if rank == 0:
+        for f in os.listdir(d):
+            if f.startswith(base):
+                rm(f)
+
+
 def spool_batches(spool, job, rank, world, max_reads, poll=0.005):
     """This rank's spans from the distributor, parsed: yields ((c, j), ReadBatch, albacore) for
     batch j of span c = rank, rank + world, ... in order, deleting each span file once parsed."""
@@ -345,6 +391,7 @@ def trim_file_sharded(in_path, out_path, out_format='fastq', scoring_scheme_vals
             distributor = threading.Thread(target=spool_distribute, args=(in_path, spool, job, world),
                                            kwargs={'stop': stop, 'chunk_bytes': spool_chunk_bytes}, daemon=True)
             distributor.start()
+    failed = False
     try:
         if spooled:
             counts = ft.trim_file(None, part(rank), out_format, max_reads, segments=segments,
@@ -355,6 +402,7 @@ def trim_file_sharded(in_path, out_path, out_format='fastq', scoring_scheme_vals
         else:
             counts = ft.trim_file(in_path, part(rank), out_format, max_reads, segments=segments)
     except BaseException as ex:
+        failed = True
         if spooled:                           # the other ranks stop waiting for spans and raise too
             pre = _spool_prefix(spool, job)
             if not os.path.exists(pre + 'error'):
@@ -367,6 +415,8 @@ def trim_file_sharded(in_path, out_path, out_format='fastq', scoring_scheme_vals
         if distributor is not None:
             stop.set()
             distributor.join()
+        if failed and spooled:                # no hidden spool files left in the user's directory
+            spool_fail_cleanup(spool, job, rank, world)
     if world > 1:
         spans = [None] * world
         dist.all_gather_object(spans, (segments, {k: v for k, v in counts.items() if k != 'bins'}), group=group)

@@ -286,16 +286,18 @@ int pcabi_first_hit_dev(const int32_t *res, int64_t stride, int64_t n_win, int32
  * that can hit are found first, by exact k-mer seeds (pcabi_seed.hip: seed scan, expansion, banded
  * bounds) or, where seeds do not apply, by a score-only filter, and only those candidates get the
  * attribute DP (in owned-column chunks, planned on the device); every later round masks the new
- * hits in place (codes -> N, the reference's '-') and re-aligns only the reads that just hit, from
- * the adapter that hit onwards, until no read hits (DESIGN.md §4 "Middle scan"). Pairs where
+ * hits (N, the reference's '-') and re-aligns only the reads that just hit, from the adapter that
+ * hit onwards, until no read hits (DESIGN.md §4 "Middle scan"). As the reference masks a copy
+ * (nanopore_read.py:225,234), the caller's codes are never written: a read's first hit copies it
+ * into a shadow arena the scan owns, and later hits mask that copy. Pairs where
  * neither way applies run the full cross product with k_first_hit. Hits are written to `hits`
  * (HOST int32, 6 rows x cap: read, adapter, read_start,
  * read_end (exclusive), m, l2 -- full identity = pid6(m, l2)) in discovery order, which per read
  * is the reference's order. Returns the number of hits (may exceed cap: only the first cap are
  * written) or a negative error. threshold must be > 0 (the reference never terminates otherwise).
  *   pcabi_scan_create / destroy : scratch for one adapter table (current device).
- *   pcabi_middle_scan_dev       : codes/win_off/win_len are DEVICE pointers (codes are masked in
- *                                 place), h_win_len the host copy of the lengths or NULL (the call
+ *   pcabi_middle_scan_dev       : codes/win_off/win_len are DEVICE pointers (codes are read only:
+ *                                 byte-identical after the call), h_win_len the host copy of the lengths or NULL (the call
  *                                 then copies them: e.g. views from pcabi_trim_views_dev). When the
  *                                 seeded plan covers the table and scoring, the rounds are queued on
  *                                 the device with their counts there (no host round trip between
@@ -308,8 +310,8 @@ int pcabi_first_hit_dev(const int32_t *res, int64_t stride, int64_t n_win, int32
  *   pcabi_middle_requeues       : queued rounds that overflowed a buffer (raw-hit slabs, band task
  *                                 regions, candidate-DP task slots), were dropped and queued again,
  *                                 process-wide; *flags_seen (optional) = the OR of their flags
- *                                 (1 raw hits, 2 band tasks, 4 task slots). Test knobs:
- *                                 PCABI_MIDDLE_INIT_CAPS="raw,task,slots" sizes a new scan's buffers,
+ *                                 (1 raw hits, 2 band tasks, 4 task slots, 8 shadow arena). Test knobs:
+ *                                 PCABI_MIDDLE_INIT_CAPS="raw,task,slots[,arena]" sizes a new scan's buffers,
  *                                 PCABI_MIDDLE_FAULT="round:bits,..." shrinks one round's buffers.
  *   pcabi_scan_profile          : per-phase profile of this scan's device rounds (a diagnostic: with
  *                                 it on, every queued round is synchronised on its own). mode 1 =
@@ -323,7 +325,7 @@ int pcabi_first_hit_dev(const int32_t *res, int64_t stride, int64_t n_win, int32
 typedef struct pcabi_scan pcabi_scan;
 int pcabi_scan_create(const pcabi_adapters *adps, pcabi_scan **out);
 void pcabi_scan_destroy(pcabi_scan *s);
-int64_t pcabi_middle_scan_dev(pcabi_scan *s, uint8_t *codes, const int64_t *win_off,
+int64_t pcabi_middle_scan_dev(pcabi_scan *s, const uint8_t *codes, const int64_t *win_off,
                               const int32_t *win_len, const int32_t *h_win_len, int64_t n_win,
                               int match, int mismatch, int gap_open, int gap_extend,
                               double threshold, int32_t *hits, int64_t cap, void *stream);

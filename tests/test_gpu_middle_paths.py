@@ -72,10 +72,12 @@ def _sorted(h):
     return h[:, np.lexsort((np.arange(h.shape[1]), h[0]))]
 
 
-def _dev_scan(L, views, adps, sc, thr, profile=None):
+def _dev_scan(L, views, adps, sc, thr, profile=None, calls=1, intact=None):
     """A FRESH scan through the device ABI (pcabi_adapters_create_scored, pcabi_scan_create,
     pcabi_middle_scan_dev): its buffers are sized on this first use (PCABI_MIDDLE_INIT_CAPS).
-    profile: a float64 array of 16 that receives pcabi_scan_profile's table of the call."""
+    profile: a float64 array of 16 that receives pcabi_scan_profile's table of the call.
+    calls: scans of the same device pack with the same scan object (every call's hits must agree);
+    intact: a list that receives, per call, whether the device pack is byte-identical afterwards."""
     from custom_porechop_abi_amd import _lib, engine
     vp = ctypes.c_void_p
     codes, offs, lens = views
@@ -101,15 +103,27 @@ def _dev_scan(L, views, adps, sc, thr, profile=None):
         h_len = np.ascontiguousarray(lens, np.int32)
         if profile is not None:
             assert L.pcabi_scan_profile(scan, 1, None, 0) == 16
-        nh = L.pcabi_middle_scan_dev(scan, d_codes, d_off, d_len, h_len.ctypes.data_as(vp), len(lens), *sc,
-                                     float(thr), hits.ctypes.data_as(vp), cap, None)
-        if nh < 0:
-            _lib.check(int(nh), 'pcabi_middle_scan_dev')
-        assert nh <= cap
-        _lib.check(L.pcabi_dev_sync(), 'sync')
+        first = None
+        for _ in range(calls):
+            hits[:] = 0
+            nh = L.pcabi_middle_scan_dev(scan, d_codes, d_off, d_len, h_len.ctypes.data_as(vp), len(lens), *sc,
+                                         float(thr), hits.ctypes.data_as(vp), cap, None)
+            if nh < 0:
+                _lib.check(int(nh), 'pcabi_middle_scan_dev')
+            assert nh <= cap
+            _lib.check(L.pcabi_dev_sync(), 'sync')
+            if intact is not None:
+                back = np.empty_like(codes)
+                _lib.check(L.pcabi_dev_d2h(back.ctypes.data_as(vp), d_codes, back.nbytes), 'd2h')
+                intact.append(bool(np.array_equal(back, codes)))
+            got = hits[:, :nh].copy()
+            if first is None:
+                first = got
+            else:
+                assert np.array_equal(got, first), 'a second scan of the same pack differs'
         if profile is not None:
             assert L.pcabi_scan_profile(scan, 0, profile.ctypes.data_as(vp), 16) == 16
-        return hits[:, :nh].copy()
+        return first
     finally:
         if scan.value:
             L.pcabi_scan_destroy(scan)
@@ -158,11 +172,38 @@ def test_overflow_grows_and_requeues_round1(gpu_lib, monkeypatch, reads_8kb, cap
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('devrounds', ['1', '0'])
+@pytest.mark.parametrize('arena', ['', '0,0,0,4096'])
+def test_scan_leaves_the_callers_reads_intact(gpu_lib, monkeypatch, reads_8kb, devrounds, arena):
+    """The reference masks a copy of the read (nanopore_read.py:225 masked_seq, :234), so the
+    caller's sequence is never touched: after pcabi_middle_scan_dev the device read pack is
+    byte-identical, and scanning the same pack again with the same scan object gives the same hits
+    (the oracle's) -- in the queued device rounds and in the host-driven loop
+    (PCABI_MIDDLE_DEVROUNDS=0), with the default shadow arena and with one of 4 KB that has to grow
+    (flag 8 in the queued rounds; the host loop grows it before the copies)."""
+    views, exp = reads_8kb
+    monkeypatch.setenv('PCABI_MIDDLE_SEEDS', '2')
+    monkeypatch.setenv('PCABI_MIDDLE_DEVROUNDS', devrounds)
+    if arena:
+        monkeypatch.setenv('PCABI_MIDDLE_INIT_CAPS', arena)
+    n0, _ = _requeues(gpu_lib)
+    intact = []
+    got = _dev_scan(gpu_lib, views, ADPS, SC, 90.0, calls=3, intact=intact)
+    n1, flags = _requeues(gpu_lib)
+    assert intact == [True, True, True]
+    assert np.array_equal(_sorted(got), exp)
+    if arena and devrounds == '1':
+        assert n1 > n0 and flags & 8, 'the 4 KB arena did not overflow'
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('windows', ['0', '1'])
-@pytest.mark.parametrize('fault', ['0:1', '0:2', '0:4', '1:1', '1:2', '1:4', '2:7', '0:7,1:4,2:2'])
+@pytest.mark.parametrize('fault', ['0:1', '0:2', '0:4', '1:1', '1:2', '1:4', '2:7', '0:7,1:4,2:2', '0:8', '1:8',
+                                   '2:15'])
 def test_overflow_in_a_round_is_dropped_and_requeued(gpu_lib, monkeypatch, reads_8kb, fault, windows):
     """PCABI_MIDDLE_FAULT: the first run of round k overflows for real (its buffers shrunk to one
-    entry: the seed scan's raw-hit slab, the band tasks, or 64 candidate task slots); nothing of that
+    entry: the seed scan's raw-hit slab, the band tasks, 64 candidate task slots, or (8) a shadow
+    arena of no bytes for the round's masked copies); nothing of that
     round is kept or masked, the rounds queued behind it see no reads, and the rerun gives the same
     hits as the oracle -- in round 1 and in later rounds, with and without candidate windows."""
     from custom_porechop_abi_amd import engine

@@ -283,7 +283,8 @@ def test_sharded_gzip_spool_many_spans(chunk, fasta, tmp_path):
 
 def test_sharded_gzip_spool_failure_raises_on_every_rank(tmp_path):
     """A truncated gzip input (the reference's gzip module raises EOFError): the distributor's
-    error reaches both ranks, which raise instead of waiting for spans that never come."""
+    error reaches both ranks, which raise instead of waiting for spans that never come, and leave
+    no spool file behind in the output directory."""
     import gzip
     import torch.multiprocessing as mp
     # ~6 MB of text, cut at 90 %: the check reads (50, 'synthetic_endsize') come from the intact
@@ -297,6 +298,9 @@ def test_sharded_gzip_spool_failure_raises_on_every_rank(tmp_path):
         mp.spawn(_file_worker, args=(2, _free_port(), 'synthetic_endsize', in_path, str(tmp_path / 'o.fastq'),
                                      str(tmp_path / 'c%d.json'), None, 200000), nprocs=2, join=True)
     assert 'unexpected end of file' in str(ei.value) or 'distributor failed' in str(ei.value)
+    # every rank's unconsumed spans, the markers and the acknowledgements are gone (shards.spool_fail_cleanup)
+    left = [f for f in os.listdir(str(tmp_path)) if f.startswith('.pcabi_spool')]
+    assert left == [], left
 
 
 @pytest.mark.parametrize('gz', [False, True])

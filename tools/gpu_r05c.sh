@@ -1,0 +1,13 @@
+#!/bin/bash
+# r05c: (1) input-preserving middle scan -- middle-path GPU tests, middle / 20 kb / reference-job
+# sub-records; (2) the dominant kernel's replay microbenchmark (tools/replay_k24) by events and under
+# rocprofv3 PMC, next to the same PMC passes of the real kernel in the headline bench.
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/r05c
+mkdir -p $OUT
+cd $R
+timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_gpu_middle_paths.py tests/test_pipeline.py > $OUT/pytest_mid.log 2>&1 || { echo "pytest failed rc=$?"; tail -40 $OUT/pytest_mid.log; exit 1; }
+tail -3 $OUT/pytest_mid.log
+timeout -k 10 600 python bench.py --only-subs middle,middle_20kb,reference_job > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed rc=$?"; tail -20 $OUT/bench.err; exit 1; }
+echo bench ok

@@ -1,0 +1,158 @@
+"""Generate the replay microbenchmark of the dominant kernel's inner column.
+
+Compiles the kernel translation unit that holds k_align<24, true, TAGGED> (the headline's dominant
+launch) to gfx950 assembly, extracts that kernel's inner column loop -- the blocks of the loop with
+the most v_max3_i32, i.e. LanePacked::column over 24 adapter rows, the window reader's look-ahead
+load every 4 columns and the row-L scout -- VERBATIM, and writes:
+
+  profiles/r05/k_align24_inner_column.s   the loop as the compiler emitted it (labels as emitted)
+  tools/replay_k24_body.inc               the same text as C string literals for tools/replay_k24.hip,
+                                          labels renamed, one copy per variant:
+                                            exact   -- the loop as emitted
+                                            nolds   -- the ds_reads and their lgkmcnt waits removed
+                                                       (the destinations keep stale values): the
+                                                       VALU + SALU issue of the same mix alone
+
+Run: python tools/make_replay_k24.py   (hipcc, ~20 s), then build tools/replay_k24.hip.
+"""
+import os
+import re
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNEL = '_ZN9pcabi_eng7k_alignILi24ELb1ELi6EEEvNS_7KParamsE'
+
+
+def device_asm():
+    out = os.path.join(ROOT, 'build', 'replay', 'pcabi_k_packed_small.s')
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    src = os.path.join(ROOT, 'custom_porechop_abi_amd', 'csrc', 'pcabi_k_packed_small.hip')
+    subprocess.check_call(['/opt/rocm/bin/hipcc', '--offload-arch=gfx950', '--cuda-device-only', '-O3', '-std=c++17',
+                           '-S', '-o', out, src])
+    return open(out).read().splitlines()
+
+
+def kernel_lines(lines):
+    start = next(i for i, l in enumerate(lines) if l.startswith(KERNEL + ':'))
+    end = next(i for i in range(start + 1, len(lines)) if lines[i].startswith('.Lfunc_end') or
+               (lines[i].startswith('_Z') and lines[i].rstrip().endswith(':') and i > start + 1))
+    return lines[start:end]
+
+
+def blocks(body):
+    """(label, header-of-loop or None, is_header, lines) per basic block."""
+    out = []
+    cur = None
+    for l in body:
+        m = re.match(r'^(\.LBB\d+_\d+|; %bb\.\d+):?\s*(.*)$', l)
+        if m:
+            lab = m.group(1).replace('; %bb.', '.LBB_bb')
+            note = m.group(2)
+            hdr = re.search(r'Header=BB(\d+_\d+)', note)
+            is_h = 'Inner Loop Header' in note
+            cur = [lab, hdr.group(1) if hdr else None, is_h, [l]]
+            out.append(cur)
+        elif cur is not None:
+            cur[3].append(l)
+    return out
+
+
+def inner_loop(body):
+    """The cross-mode column loop: 24 v_max3_i32 (one per adapter row) and the window reader's
+    look-ahead at a runtime stride (the tile layout's 256 dwords, v_mad_u64_u32). The compiler also
+    emits a copy of the loop for pairs mode (stride 1, the window's own bytes); that one is not the
+    headline's."""
+    bl = blocks(body)
+    found = []
+    for k, b in enumerate(bl):
+        if not b[2]:
+            continue
+        hid = b[0].replace('.LBB', '')
+        members = [x for x in bl if x is b or x[1] == hid]
+        n3 = sum(l.count('v_max3_i32') for x in members for l in x[3])
+        strided = any('v_mad_u64_u32' in l for x in members for l in x[3])
+        if n3 == 24 and strided:
+            found.append((members, hid))
+    if len(found) != 1:
+        raise SystemExit('expected one strided 24-row column loop, found %d' % len(found))
+    return found[0]
+
+
+def main():
+    lines = device_asm()
+    body = kernel_lines(lines)
+    members, hid = inner_loop(body)
+    text = [l for b in members for l in b[3]]
+    prof = os.path.join(ROOT, 'profiles', 'r05')
+    os.makedirs(prof, exist_ok=True)
+    with open(os.path.join(prof, 'k_align24_inner_column.s'), 'w') as f:
+        f.write('; %s: inner column loop (header .LBB%s), gfx950, hipcc -O3, extracted by '
+                'tools/make_replay_k24.py\n' % (KERNEL, hid))
+        f.write('\n'.join(text) + '\n')
+    labels = sorted({b[0] for b in members})
+    exits = sorted({m for l in text for m in re.findall(r'(\.LBB\d+_\d+)', l)} - set(labels))
+    if len(exits) != 1:
+        raise SystemExit('expected one exit label, found %s' % exits)
+    counts = {}
+    for l in text:
+        m = re.match(r'^\s+([a-z][a-z0-9_]*)', l)
+        if m:
+            counts[m.group(1)] = counts.get(m.group(1), 0) + 1
+    vregs = sorted({int(x) for l in text for x in re.findall(r'\bv(\d+)\b', l)} |
+                   {int(a) + i for l in text for a, b in re.findall(r'\bv\[(\d+):(\d+)\]', l)
+                    for i in range(int(b) - int(a) + 1)})
+    sregs = sorted({int(x) for l in text for x in re.findall(r'\bs(\d+)\b', l)} |
+                   {int(a) + i for l in text for a, b in re.findall(r'\bs\[(\d+):(\d+)\]', l)
+                    for i in range(int(b) - int(a) + 1)})
+
+    def variant(tag, nolds):
+        out = []
+        for l in text:
+            s = l.split(';')[0].rstrip()
+            if not s.strip():
+                if l.strip().startswith('; sched_barrier'):
+                    continue
+                continue
+            m = re.match(r'^(\.LBB\d+_\d+|; %bb\.\d+)', l)
+            if m:
+                if m.group(1).startswith('; %bb'):
+                    continue                   # fall-through block: no label needed
+                out.append(m.group(1).replace('.LBB', '.Lrp_%s_' % tag) + ':')
+                continue
+            s = s.replace(exits[0], '.Lrp_%s_exit' % tag)
+            s = re.sub(r'\.LBB(\d+_\d+)', lambda mm: '.Lrp_%s_%s' % (tag, mm.group(1)), s)
+            if nolds and ('ds_read' in s or 'lgkmcnt' in s):
+                continue                       # no LDS read, no wait: the destinations keep old values
+            out.append(s)
+        header = '.Lrp_%s_%s' % (tag, hid)
+        return header, out
+
+    inc = ['// generated by tools/make_replay_k24.py from %s (do not edit)' % KERNEL,
+           '// instruction counts per loop pass: ' + ', '.join('%s %d' % kv for kv in sorted(counts.items())),
+           '#define RP_VREGS_MAX %d' % max(vregs),
+           '#define RP_SREGS_MAX %d' % max(sregs),
+           '#define RP_CLOBBER_V %s' % ', '.join('"v%d"' % v for v in range(0, max(vregs) + 1)),
+           '#define RP_CLOBBER_S %s' % ', '.join('"s%d"' % s for s in sregs),
+           '#define RP_SREGS "%s"' % ' '.join('s%d' % s for s in sregs)]
+    for tag, nolds in (('exact', False), ('nolds', True)):
+        header, out = variant(tag, nolds)
+        inc.append('#define RP_HEADER_%s "%s"' % (tag.upper(), header))
+        inc.append('#define RP_LOOP_%s \\' % tag.upper())
+        for s in out:
+            inc.append('    "%s\\n" \\' % s.replace('\t', ' ').strip())
+        inc.append('    ""')
+    valu = sum(v for k, v in counts.items() if k.startswith('v_'))
+    inc.append('#define RP_VALU_PER_PASS_MAIN %d' % (valu - sum(1 for b in members if b[0].startswith('.LBB_bb')
+                                                               for l in b[3] if re.match(r'^\s+v_', l))))
+    inc.append('#define RP_VALU_PER_PASS_LOAD %d' % sum(1 for b in members if b[0].startswith('.LBB_bb')
+                                                         for l in b[3] if re.match(r'^\s+v_', l)))
+    with open(os.path.join(ROOT, 'tools', 'replay_k24_body.inc'), 'w') as f:
+        f.write('\n'.join(inc) + '\n')
+    print('loop header .LBB%s: %d lines, %d VALU per pass, exits to %s; vregs up to v%d, sregs %s' % (
+        hid, len(text), valu, exits[0], max(vregs), sregs))
+    print(sorted(counts.items()))
+
+
+if __name__ == '__main__':
+    sys.exit(main())
