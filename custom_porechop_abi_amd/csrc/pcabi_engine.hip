@@ -91,6 +91,33 @@ constexpr int kChunkCols = 512;
 constexpr int kChunkColsMin = 64;
 constexpr int64_t kChunkTasks = 65536;
 
+// PCABI_HOSTPROF=1: the middle scan prints its host-side time marks per call to stderr (where the
+// host spends the time between the end trim's kernels and the scan's first launch).
+struct HostMarks {
+    bool on = false;
+    std::vector<std::pair<const char *, std::chrono::steady_clock::time_point>> m;
+    HostMarks() {
+        const char *e = std::getenv("PCABI_HOSTPROF");
+        on = e && e[0] == '1';
+    }
+    void mark(const char *what) {
+        if (on) m.emplace_back(what, std::chrono::steady_clock::now());
+    }
+    ~HostMarks() {
+        if (!on || m.empty()) return;
+        std::string s;
+        for (size_t k = 1; k < m.size(); ++k)
+            s += std::string(" ") + m[k].first + "=" +
+                 std::to_string(std::chrono::duration<double, std::micro>(m[k].second - m[k - 1].second).count());
+        std::fprintf(stderr, "[pcabi hostprof] us:%s\n", s.c_str());
+    }
+};
+
+thread_local HostMarks *g_hm = nullptr;
+inline void hmark(const char *what) {
+    if (g_hm) g_hm->mark(what);
+}
+
 // PCABI_DEBUG=1: the middle scan prints its candidate counts per round to stderr.
 const bool g_debug = [] {
     const char *e = std::getenv("PCABI_DEBUG");
@@ -2882,8 +2909,10 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
         for (int32_t id : adps->ids[b]) rows[id] = kBuckets[b].rpl;
     if (!sc->seed) sc->seed = pcabi_seed::create();
     {
+        hmark("setup");
         const int rc = pcabi_seed::plan_ready(sc->seed, adps->hcodes.data(), adps->hoff.data(), adps->hlen.data(), n_adp,
                                               rows, scr, threshold, middle_seed_mode(), st);
+        hmark("plan");
         if (rc < 0) return rc;
         if (rc == 0) return 0;
     }
@@ -2891,7 +2920,15 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
     const int n_bk = (int)used.size();
     const int64_t n = n_win;
     constexpr int kSlots = 16;                      // round slots held on the device (wrapped past)
-    constexpr int kBatch = 3;                       // rounds queued per host check
+    constexpr int kBatch = 3;                       // rounds queued per host check (later batches)
+    // the first batch's rounds (PCABI_MIDDLE_BATCH1 = 1..3, A/B): with 2, data where round 2 finds
+    // nothing skips a third round's ~35 empty launches, but data with a third round pays a host round
+    // trip for it (r05g: within the run-to-run noise either way, so the default stays 3)
+    const int batch1 = [] {
+        const char *e = std::getenv("PCABI_MIDDLE_BATCH1");
+        const int v = e ? std::atoi(e) : kBatch;
+        return v >= 1 && v <= kBatch ? v : kBatch;
+    }();
     constexpr unsigned kGrid = 2048;                // blocks of the device-counted launches
     // ---- device buffers ----
     if (int rc = sc->q_cur.ensure(4 * (size_t)n * (kSlots + 1))) return rc;
@@ -2948,6 +2985,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
         for (int64_t k = 0; k < n; ++k) tot += h_win_len[k];
         mean_len = n ? tot / (double)n : 0.0;
     }
+    hmark("bufs");
     const bool windows = middle_windows_on(mean_len);
     if (windows) {
         std::vector<int32_t> U;
@@ -3190,7 +3228,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
         hipLaunchKernelGGL(k_round_hits, dim3(gn), dim3(256), 0, st, (const int32_t *)sc->phb.p, n, nr, cur,
                            (const int32_t *)sc->pcount.p, list_of(r), d_n + r + 1, cur_of(r + 1), start_of(r + 1),
                            sflags, d_pflag, d_rflag + r, win_off, (const int64_t *)eoff, win_len, d_bump);
-        hipLaunchKernelGGL(k_mask_list, dim3(1024), dim3(256), 0, st, codes, win_off, eoff, win_len, list_of(r),
+        hipLaunchKernelGGL(k_mask_list, dim3(4096), dim3(256), 0, st, codes, win_off, eoff, win_len, list_of(r),
                            d_n + r + 1, (uint8_t *)sc->shadow.p, shadow_rel(sc, codes), (fault & 8) ? (int64_t)-1 : sc->shadow_cap,
                            (const unsigned long long *)d_bump, d_rflag + r);
         HIP_TRY(hipGetLastError());
@@ -3253,22 +3291,26 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
         }
     }
     int64_t need = 0, need2 = 0, most_hits = 0;
+    hmark("pre");
     for (int guard = 0;; ++guard) {
         if (guard > 10000) return fail(PCABI_E_DEVICE, "middle scan: rounds did not settle");
         // queue up to kBatch rounds from `slot`
-        const int upto = std::min(slot + kBatch, kSlots);
+        const int upto = std::min(slot + (round_base == 0 && slot == 0 ? batch1 : kBatch), kSlots);
         for (int r = slot; r < upto; ++r) {
             if (int rc = queue_round(r)) return rc;
+            hmark("round");
             if (r == 0 && round_base == 0)        // round 1's segment total (the next call's mean length)
                 HIP_TRY(hipMemcpyAsync(h_nd + 5, pcabi_seed::seg_cum_dev(sc->seed) + n, sizeof(int64_t),
                                        hipMemcpyDeviceToHost, st));
         }
         queued_to = upto;
+        hmark("queue");
         HIP_TRY(hipMemcpyAsync(sc->h_ctl, d_n, kCtlBytes, hipMemcpyDeviceToHost, st));   // counts, flags, needs
         for (int r = slot; r < queued_to; ++r)
             HIP_TRY(hipMemcpyAsync(sc->h_stage + 8 * (size_t)spec * (r - slot), list_of(r), 32 * (size_t)spec,
                                    hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
+        hmark("sync");
         need = h_nd[1];
         need2 = h_nd[3];
         // the first flagged round (nothing of it or after it was kept): grow, queue it again
@@ -3332,6 +3374,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
     HIP_TRY(hipStreamSynchronize(st));
     // the next call stages as many hits per round as this one's busiest round had (+ 25 %), and
     // takes its mean read length from this call's round-1 segments
+    hmark("end");
     sc->spec_hits = std::max<int64_t>(4096, most_hits + most_hits / 4);
     if (h_nd[5] >= 0 && n > 0) sc->last_mean = (double)h_nd[5] * pcabi_seed::seg_positions() / (double)n;
     // (round, read) order: per read the reference's discovery order. The rounds come in order and
@@ -3394,6 +3437,12 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *sc, const uint8_t *codes, const int64_
     const hipStream_t st = (hipStream_t)stream;
     const int32_t n_adp = sc->adps->n_adp;
     if (n_win == 0 || n_adp == 0) return 0;
+    HostMarks hm;
+    struct MarksOff {
+        ~MarksOff() { g_hm = nullptr; }
+    } marks_off;
+    g_hm = hm.on ? &hm : nullptr;
+    hmark("entry");
     // the layout of the scan's table that serves this scoring on these reads (adapters_for: any
     // scoring the reference accepts, any read length), for the duration of the call
     struct TableSwap {

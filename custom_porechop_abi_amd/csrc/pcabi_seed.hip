@@ -1097,6 +1097,12 @@ __global__ __launch_bounds__(256) void k_seed_band(const int4 *task, const int32
 // lane the range of the NEXT task is loaded (uint4 loads) while the current task computes, then
 // copied to the lane's LDS slot (NC4 x 16 bytes), where the rows read their one new byte each: the
 // row loop touches no global memory, so no wait of the loop is a memory latency.
+#ifdef PCABI_BAND_STATS
+// (experiments, -DPCABI_BAND_STATS) per band kernel class (E): row iterations x 64 lanes, active
+// lane-rows, tasks, passes -- the lanes a pass leaves idle behind its longest task
+__device__ unsigned long long g_band_stats[2][4];
+#endif
+
 template <int E, int NC4>
 __global__ __launch_bounds__(256) void k_seed_band_pin(const int4 *task, const int32_t *n_task, int64_t cap,
                                                        const uint8_t *codes, const uint8_t *adp, int32_t adp_dw,
@@ -1170,6 +1176,9 @@ __global__ __launch_bounds__(256) void k_seed_band_pin(const int4 *task, const i
             t += stride;
         }
         // ---- this task
+#ifdef PCABI_BAND_STATS
+        const bool vA_was = active;
+#endif
         const int a = rc.y >> 11, o = rc.y & 255, K = kMinK + ((rc.y >> 8) & 7);
         const uint32_t meta = (uint32_t)ameta[a];
         const int L = (int)(meta & 255u), T = (int)(meta >> 12);
@@ -1217,7 +1226,15 @@ __global__ __launch_bounds__(256) void k_seed_band_pin(const int4 *task, const i
             }
         }
         if (vo.list) put_verified(vo, ver, rc.x, a, E, dabs);
+#ifdef PCABI_BAND_STATS
+        unsigned long long st_it = 0, st_act = 0;
+        const unsigned long long st_tasks = __popcll(__ballot(rc.x >= 0 && vA_was));
+#endif
         while (__any(active)) {
+#ifdef PCABI_BAND_STATS
+            st_it += 64;
+            st_act += __popcll(__ballot(active));
+#endif
             ver = false;
             if (active) {
                 const int ab = ad[apos];
@@ -1258,6 +1275,14 @@ __global__ __launch_bounds__(256) void k_seed_band_pin(const int4 *task, const i
             }
             if (vo.list) put_verified(vo, ver, rc.x, a, E, dabs);
         }
+#ifdef PCABI_BAND_STATS
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(&g_band_stats[E > 2][0], st_it);
+            atomicAdd(&g_band_stats[E > 2][1], st_act);
+            atomicAdd(&g_band_stats[E > 2][2], st_tasks);
+            atomicAdd(&g_band_stats[E > 2][3], 1ull);
+        }
+#endif
     }
 }
 
@@ -2051,3 +2076,21 @@ int plan_ready(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32
 }  // namespace pcabi_seed
 
 extern "C" int64_t pcabi_middle_seed_runs(void) { return pcabi_seed::g_runs.load(); }
+
+// Experiments only (not in include/pcabi.h): the band statistics of a -DPCABI_BAND_STATS build,
+// out[2][4] (see g_band_stats); -1 without the flag. reset != 0 zeroes them afterwards.
+extern "C" int pcabi_debug_band_stats(unsigned long long *out, int reset) {
+#ifdef PCABI_BAND_STATS
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pcabi_seed::g_band_stats), sizeof(unsigned long long) * 8) != hipSuccess)
+        return -2;
+    if (reset) {
+        unsigned long long z[8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(pcabi_seed::g_band_stats), z, sizeof(z)) != hipSuccess) return -2;
+    }
+    return 0;
+#else
+    (void)out;
+    (void)reset;
+    return -1;
+#endif
+}
