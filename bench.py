@@ -78,6 +78,8 @@ def parse():
                          'Rapid + RBK004, Barcode 1..12 (forward) + their 111 bp full rapid sequences')
     ap.add_argument('--middle-threshold', type=float, default=90.0)
     ap.add_argument('--middle-check', type=int, default=1000, help='middle: reads checked against the oracle loop')
+    ap.add_argument('--e2e-check', type=int, default=150,
+                    help='e2e: head reads whose written bytes are checked against the oracle-driven reference writer')
     ap.add_argument('--drivers-check', type=int, default=200,
                     help='drivers: reads whose decisions are compared with the same drivers over the oracle')
     ap.add_argument('--check-phase-check', type=int, default=400,
@@ -90,7 +92,7 @@ def parse():
                     help='reference_job: 1 = each kept adapter\'s end-trim cross product on a stream of its own '
                          '(r04x: 4.69-4.71 vs 4.78-4.84 ms per step); 0 = each side\'s table on one stream')
     ap.add_argument('--rj-side-streams', type=int, default=0,
-                    help='reference_job: the library\'s side streams (pcabi_set_side_streams) during the job; 0 '
+                    help='reference_job: the library\'s side streams (pcabi_stream_side_streams on its streams) during the job; 0 '
                          '(default: it runs two caller streams at once) or 1')
     ap.add_argument('--head-side-streams', type=int, default=0,
                     help='headline schedule: the library\'s side streams while both sides\' smaller buckets run on two '
@@ -430,10 +432,13 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
         epilogue()
 
     # the headline schedule runs both sides' smaller buckets on two caller streams at once: the
-    # library's side streams go off for it (pcabi_set_side_streams; one cross product at a time,
+    # library's side streams go off on its two streams (pcabi_stream_side_streams; one cross product at a time,
     # as the production schedule, keeps them on)
     two_streams = not timed_fused and args.rest_overlap in (1, 3)
-    side_prev = L.pcabi_set_side_streams(args.head_side_streams if two_streams else -1)
+    # (per stream, r05: pcabi_stream_side_streams leaves every other caller of the library alone)
+    if two_streams:
+        for s_ in (stream, stream2):
+            L.pcabi_stream_side_streams(s_, args.head_side_streams)
     for _ in range(args.warmup):
         step(fused=timed_fused)
     _lib.check(L.pcabi_stream_sync(stream), 'sync')
@@ -451,7 +456,9 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
     L.pcabi_stream_sync(stream)
     barrier()
     elapsed = time.perf_counter() - t0
-    side_timed = L.pcabi_set_side_streams(side_prev)
+    side_timed = args.head_side_streams if two_streams else L.pcabi_set_side_streams(-1)
+    for s_ in (stream, stream2):
+        L.pcabi_stream_side_streams(s_, -1)
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device='cuda' if args.dist_backend == 'nccl' else 'cpu')
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -510,7 +517,7 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
         # the same step in the production schedule: one cross product per side, the small buckets
         # overlapping the dominant launch (faster as a whole; the dominant launch then shares the
         # GPU, so the headline keeps it alone for the roofline)
-        fused_prev = L.pcabi_set_side_streams(1)   # one cross product at a time: side by side pays
+        L.pcabi_stream_side_streams(stream, 1)     # one cross product at a time: side by side pays
         for _ in range(2):
             step(fused=True)
         L.pcabi_stream_sync(stream)
@@ -519,7 +526,7 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
             step(fused=True)
         L.pcabi_stream_sync(stream)
         dt = (time.perf_counter() - t0) / args.steps
-        L.pcabi_set_side_streams(fused_prev)
+        L.pcabi_stream_side_streams(stream, -1)
         subs['fused_schedule'] = {'value': round(n / dt, 1), 'unit': 'reads/s', 'ms_per_step': round(1e3 * dt, 4),
                                   'steps': args.steps, 'what': 'the headline step with one cross product per side '
                                   '(pcabi_align_cross_dev_marked): register buckets side by side with the dominant one '
@@ -629,7 +636,9 @@ def run_other_configs(args, ctx):
                                                         cpu_sample=args.cpu_sample // 4),
                                                     rank, 1, None, torch, L, _lib, A, synth, encode_adapters)),
         # the CLI path file to file (parse + trim + middle + write), 25k reads
-        ('e2e', lambda: run_e2e(sub(workload='e2e', reads=25000, steps=3, warmup=1), rank, 1, None, torch, L, _lib, A,
+        # 100k reads = 8 batches of 12.5k per step: the parse / device / write pipeline at its
+        # steady state (r04 timed 2 batches per step, which never fills it)
+        ('e2e', lambda: run_e2e(sub(workload='e2e', reads=100000, steps=2, warmup=1), rank, 1, None, torch, L, _lib, A,
                                 synth, encode_adapters)),
         # SURVEY §8(f) 3 and 4
         ('compat', lambda: run_compat(sub(workload='compat', cpu_sample=args.cpu_sample // 4), rank, 1, None, torch,
@@ -998,10 +1007,11 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
         return matching
 
     # the job runs cross products on two caller streams at once (set search and end trim: both
-    # sides side by side), so the library's side streams go off (pcabi_set_side_streams, r04r:
+    # sides side by side), so the library's side streams go off on its streams (pcabi_stream_side_streams, r04r:
     # 4.95 -> 4.66 ms per step): a side stream on the other caller stream's hardware queue waits
     # for its large launch
-    side_prev = L.pcabi_set_side_streams(0 if args.rj_side_streams == 0 else 1)
+    for s_ in [stream, stream2] + x_streams:
+        L.pcabi_stream_side_streams(s_, 0 if args.rj_side_streams == 0 else 1)
     try:
         for _ in range(max(1, args.warmup)):
             step()
@@ -1013,7 +1023,8 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
             matching = step()
         elapsed = time.perf_counter() - t0
     finally:
-        L.pcabi_set_side_streams(side_prev)
+        for s_ in [stream, stream2] + x_streams:
+            L.pcabi_stream_side_streams(s_, -1)
     step_ms = 1e3 * elapsed / args.steps
     per = {k: round(v / args.steps, 4) for k, v in acc.items()}
     ks = kept_state(tuple(a.name for a in matching), matching)
@@ -1745,10 +1756,14 @@ def run_e2e(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapters):
     probe = write_probe(out_path + '.probe', out_bytes, args.steps + args.warmup) if rank == 0 else None
     checked = None
     if args.check and rank == 0:
-        # the written file, read back: every kept read's first part equals the reference's rule
-        # on its own trims (the reads' alignment parity is covered by the other workloads)
+        # the written bytes of the first reads against the reference's output rule on decisions the
+        # ORACLE made: the reference-API drivers (porechop_abi.find_adapters_at_read_ends /
+        # find_adapters_in_read_middles) with the oracle standing in for the kernels, the fork's
+        # filter and NanoporeRead.get_fastq (nanopore_read.py:106-156, porechop_abi.py:535-668)
         got = misc.load_batch(out_path)
         checked = {'records_written': int(got.n), 'reads_in': last['reads_in'], 'reads_kept': last['reads_kept']}
+        checked.update(e2e_output_check(in_path, out_path, sets, sc, E, args.middle_threshold,
+                                        min(args.e2e_check, n)))
     for p in (in_path, out_path):
         try:
             os.remove(p)
@@ -1795,6 +1810,41 @@ def run_e2e(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapters):
         }
         return out
     return None
+
+
+def e2e_output_check(in_path, out_path, sets, sc, end_size, middle_threshold, k):
+    """The first k input reads through the reference's drivers and writer with the oracle as the
+    alignment engine (tests/oracle_lib: CPU restatements pinned to the reference's own build, the
+    kernels swapped out for the duration), against the same reads' records at the head of the
+    pipeline's output file, byte for byte."""
+    import contextlib
+    import io
+    from custom_porechop_abi_amd import engine, misc, porechop_abi as P
+    from custom_porechop_abi_amd.nanopore_read import NanoporeRead
+    from tests import oracle_lib
+    b = misc.load_batch(in_path)
+    reads = [NanoporeRead(b.name(i), b.sequence(i), b.quals(i)) for i in range(min(k, b.n))]
+    swaps = {'align': oracle_lib.align_windows, 'end_decisions': oracle_lib.end_decisions_windows,
+             'first_hits': oracle_lib.first_hits_windows,
+             'middle_scan': lambda w, a, s_, t, device=0: oracle_lib.middle_scan_threaded(w, a, s_, t)}
+    saved = {name: getattr(engine, name) for name in swaps}
+    t0 = time.perf_counter()
+    try:
+        for name, fn in swaps.items():
+            setattr(engine, name, fn)
+        sink = io.StringIO()
+        with contextlib.redirect_stdout(sink):
+            P.find_adapters_at_read_ends(reads, sets, 0, end_size, 2, 75.0, sc, sink, 4, 1, False, 75.0, 5.0, False,
+                                         None)
+            P.find_adapters_in_read_middles(reads, sets, 0, middle_threshold, 10, 100, sc, sink, 1, False)
+    finally:
+        for name, fn in saved.items():
+            setattr(engine, name, fn)
+    want = ''.join(r.get_fastq(1000, False) for r in reads if r.adapters_found()).encode()
+    with open(out_path, 'rb') as f:
+        head = f.read(len(want))
+    return {'oracle_reads_checked': len(reads), 'oracle_bytes_compared': len(want), 'output_identical': head == want,
+            'oracle_s': round(time.perf_counter() - t0, 2)}
 
 
 def pack_intact(L, _lib, d_pack, pack):

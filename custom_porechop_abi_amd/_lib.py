@@ -90,6 +90,7 @@ def lib():
         'pcabi_middle_requeues': ([c_p], c_i64),
         'pcabi_scan_profile': ([c_p, ctypes.c_int32, c_p, ctypes.c_int32], ctypes.c_int32),
         'pcabi_set_side_streams': ([c_int], c_int),
+        'pcabi_stream_side_streams': ([c_p, c_int], c_int),
         'pcabi_io_release_cache': ([], None),
         'pcabi_best_full_identity_host': ([c_int, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_p, ctypes.c_int32, c_int,
                                            c_int, c_int, c_int, c_p, c_int], c_int),
@@ -129,7 +130,7 @@ def exported_symbols():
             'pcabi_end_trim_dev',
             'pcabi_best_full_identity_dev', 'pcabi_first_hits_host', 'pcabi_first_hit_dev', 'pcabi_scan_create',
             'pcabi_scan_destroy', 'pcabi_middle_scan_dev', 'pcabi_middle_scan_host', 'pcabi_middle_seed_runs',
-            'pcabi_middle_requeues', 'pcabi_scan_profile', 'pcabi_set_side_streams',
+            'pcabi_middle_requeues', 'pcabi_scan_profile', 'pcabi_set_side_streams', 'pcabi_stream_side_streams',
             'pcabi_barcode_call_dev',
             'pcabi_barcode_call_host', 'pcabi_fastx_open', 'pcabi_fastx_type', 'pcabi_fastx_next',
             'pcabi_fastx_close', 'pcabi_fastx_load', 'pcabi_reads_count', 'pcabi_reads_type', 'pcabi_reads_views',

@@ -1502,6 +1502,20 @@ bool side_streams_on() {
     return v != 0;
 }
 
+// Per-stream setting (pcabi_stream_side_streams, r05): a caller that runs cross products on several
+// streams at once turns the side streams off for ITS streams only; streams without an entry follow
+// the process-wide default (pcabi_set_side_streams / PCABI_FORK).
+std::mutex g_stream_side_mu;
+std::vector<std::pair<hipStream_t, int>> g_stream_side;   // few entries: a linear scan
+bool side_streams_on(hipStream_t st) {
+    {
+        std::lock_guard<std::mutex> g(g_stream_side_mu);
+        for (const auto &e : g_stream_side)
+            if (e.first == st) return e.second != 0;
+    }
+    return side_streams_on();
+}
+
 // Fork / join of independent launches: launch k runs on the caller's stream (k == 0) or on side
 // stream (first + k - 1) % N, each side stream first waiting for the work already queued on the
 // caller's stream; end() makes the caller's stream wait for every side stream used.
@@ -1514,7 +1528,7 @@ struct ForkJoin {
     int n_side = 0;              // side launches of this region
     int begin(hipStream_t m, size_t n_launch) {
         main = m;
-        if (n_launch <= 1 || !side_streams_on()) return 0;   // off: every launch on the caller's stream
+        if (n_launch <= 1 || !side_streams_on(m)) return 0;  // off: every launch on the caller's stream
         int dev = 0;
         HIP_TRY(hipGetDevice(&dev));
         if (int rc = side_streams(dev, &ss)) return rc;
@@ -3403,6 +3417,20 @@ int pcabi_set_side_streams(int on) {
     const int prev = side_streams_on() ? 1 : 0;
     if (on >= 0) g_side_on.store(on ? 1 : 0);
     return prev;
+}
+
+int pcabi_stream_side_streams(void *stream, int on) {
+    const hipStream_t st = (hipStream_t)stream;
+    std::lock_guard<std::mutex> g(g_stream_side_mu);
+    for (size_t k = 0; k < g_stream_side.size(); ++k)
+        if (g_stream_side[k].first == st) {
+            const int prev = g_stream_side[k].second;
+            if (on < 0) g_stream_side.erase(g_stream_side.begin() + (long)k);
+            else g_stream_side[k].second = on ? 1 : 0;
+            return prev;
+        }
+    if (on >= 0) g_stream_side.emplace_back(st, on ? 1 : 0);
+    return -1;
 }
 
 int32_t pcabi_scan_profile(pcabi_scan *s, int32_t mode, double *out, int32_t n_out) {

@@ -198,6 +198,14 @@ int pcabi_align_cross_dev_marked(const uint32_t *tiles, const int64_t *tile_off,
  * off). The initial setting is PCABI_FORK (0 or 1; unset: see DESIGN.md §5). Returns the previous
  * setting; on < 0 only reads it. */
 int pcabi_set_side_streams(int on);
+/* The same setting for one stream (r05): the cross products and middle-scan rounds queued on `stream`
+ * use the side streams when on = 1 and run every bucket on `stream` when on = 0, whatever the
+ * process-wide setting; on = -1 removes the stream's entry (it follows pcabi_set_side_streams again).
+ * Returns the stream's previous entry (0 / 1) or -1 when it had none. Callers that run cross
+ * products on several streams at once set 0 on those streams (r04r: the reference job 4.95 -> 4.66
+ * ms), and no other caller of the library is affected. Destroying a stream does not remove its entry:
+ * remove it first (a new stream may reuse the handle). */
+int pcabi_stream_side_streams(void *stream, int on);
 
 /*
  * End-trim decision epilogue (porechop_abi/nanopore_read.py:175-217), device pointers:

@@ -175,7 +175,22 @@ def test_device_abi_tiled_cross(gpu_lib, scheme, scored, side):
     assert L.pcabi_set_side_streams(-1) == side_prev
 
 
-def _tiled_cross_case(L, _lib, engine, vp, scheme, scored):
+@pytest.mark.gpu
+@pytest.mark.parametrize('side', [1, 0])
+def test_device_abi_per_stream_side_streams(gpu_lib, side):
+    """pcabi_stream_side_streams (r05): the setting of the call's own stream wins over the
+    process-wide one (set to the opposite here); the entry reports its previous value and -1
+    removes it. Results bit-exact either way."""
+    from custom_porechop_abi_amd import _lib, engine
+    L, vp = gpu_lib, ctypes.c_void_p
+    side_prev = L.pcabi_set_side_streams(1 - side)
+    try:
+        _tiled_cross_case(L, _lib, engine, vp, (3, -6, -5, -2), True, stream_side=side)
+    finally:
+        L.pcabi_set_side_streams(side_prev)
+
+
+def _tiled_cross_case(L, _lib, engine, vp, scheme, scored, stream_side=None):
     reads, adps = _case_set(31, 700, 7, 3000, 64)
     adps = adps + ['ACGTTGCA' * k for k in (1, 2, 3, 4, 5, 6, 7)] + ['GATTACA' * 5 + 'G', 'TTAGGC' * 9]
     # wide register buckets (65..88 bp, packed-key core, pk::Lay<RPL > 64>) and past them (generic)
@@ -226,9 +241,15 @@ def _tiled_cross_case(L, _lib, engine, vp, scheme, scored):
             _lib.check(L.pcabi_stream_create(ctypes.byref(st)), 'stream')
             _lib.check(L.pcabi_event_create(ctypes.byref(e0)), 'event')
             _lib.check(L.pcabi_event_create(ctypes.byref(e1)), 'event')
+            if stream_side is not None:
+                assert L.pcabi_stream_side_streams(st, stream_side) == -1       # no entry before
+                assert L.pcabi_stream_side_streams(st, stream_side) == stream_side
             _lib.check(L.pcabi_align_cross_dev_marked(d_tiles, d_toff, d_len, n, int(lens.max()), tab, *scheme,
                                                       d_out, stride, st, e0, e1), 'align')
             _lib.check(L.pcabi_stream_sync(st), 'sync')
+            if stream_side is not None:
+                assert L.pcabi_stream_side_streams(st, -1) == stream_side       # entry removed
+                assert L.pcabi_stream_side_streams(st, -1) == -1
             ms = ctypes.c_float()
             _lib.check(L.pcabi_event_elapsed_ms(ctypes.byref(ms), e0, e1), 'elapsed')
             assert ms.value > 0.0

@@ -23,7 +23,7 @@ def main():
     L = _lib.lib()
     sets = [a for a in A.fresh_adapters() if '(full sequence)' not in a.name][:50]
     mid = [x[1] for x in middle_adapter_list(sets)[0]]
-    reads = synth.make_reads(20000, mean_len, seed=12345, keep=150)
+    reads = synth.make_reads(20000, mean_len, seed=12345)
     pack = engine.SeqPack([synth.codes_to_str(r) for r in reads])
     views = pack.views(np.zeros(len(reads), np.int64), pack.lengths)
     f = L.pcabi_debug_band_stats
