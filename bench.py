@@ -1164,10 +1164,12 @@ def run_drivers(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
         from tests import oracle_lib
         got = reads[:k]
         sub = [NanoporeRead('r%d' % i, s, '') for i, s in enumerate(seqs[:k])]
-        saved = {f: getattr(engine, f) for f in ('align', 'end_decisions', 'best_full_identity', 'middle_scan')}
+        saved = {f: getattr(engine, f) for f in ('align', 'end_decisions', 'best_full_identity', 'middle_scan',
+                                                 'middle_scan_seqs')}
         engine.align, engine.end_decisions = oracle_lib.align_windows, oracle_lib.end_decisions_windows
         engine.best_full_identity = oracle_lib.best_full_identity_windows
         engine.middle_scan = lambda v, a, s_, t, device=0: oracle_lib.middle_scan_threaded(v, a, s_, t)
+        engine.middle_scan_seqs = oracle_lib.middle_scan_seqs_threaded
         try:
             P.find_adapters_at_read_ends(sub, sets, 0, E, 2, 75.0, sc, sink, 4, 1, False, 75.0, 5.0, False, None)
             P.find_adapters_in_read_middles(sub, sets, 0, 90.0, 10, 100, sc, sink, 1, False)
@@ -1795,10 +1797,16 @@ def run_e2e(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapters):
                                                       args.middle_threshold),
                        'reads_per_gpu': n, 'batch_reads': min(n, args.e2e_batch), 'adapter_sets': len(sets),
                        'scoring': list(sc), 'parallelism': 'dp%d (read shards)' % world},
-            # 'write' is the writer thread's busy time, overlapped with the rest: not in 'other'
+            # 'read' / 'write' are the reader / writer threads' busy times, overlapped with the rest:
+            # not in 'other'
             'breakdown_ms_per_step': dict({k: round(1e3 * v / args.steps, 2) for k, v in acc.items()},
-                                          other=round(1e3 * (step_s - sum(v for k, v in acc.items() if k != 'write')
+                                          other=round(1e3 * (step_s - sum(v for k, v in acc.items()
+                                                                          if k not in ('read', 'write'))
                                                              / args.steps), 2)),
+            # the step against its slowest stage (steady state: the stages overlap fully)
+            'step_vs_slowest_stage': round(step_s / max(1e-9, max(acc.get('read', 0.0), acc.get('write', 0.0),
+                                                                  acc.get('end_trim', 0.0) + acc.get('middle', 0.0))
+                                                        / args.steps), 3),
             'input_MB_per_s': round(in_bytes / step_s / 1e6, 1),
             'output_bytes': out_bytes,
             # the file system's own ceiling for this output: the same byte count from one buffer
@@ -1826,7 +1834,8 @@ def e2e_output_check(in_path, out_path, sets, sc, end_size, middle_threshold, k)
     reads = [NanoporeRead(b.name(i), b.sequence(i), b.quals(i)) for i in range(min(k, b.n))]
     swaps = {'align': oracle_lib.align_windows, 'end_decisions': oracle_lib.end_decisions_windows,
              'first_hits': oracle_lib.first_hits_windows,
-             'middle_scan': lambda w, a, s_, t, device=0: oracle_lib.middle_scan_threaded(w, a, s_, t)}
+             'middle_scan': lambda w, a, s_, t, device=0: oracle_lib.middle_scan_threaded(w, a, s_, t),
+             'middle_scan_seqs': oracle_lib.middle_scan_seqs_threaded}
     saved = {name: getattr(engine, name) for name in swaps}
     t0 = time.perf_counter()
     try:

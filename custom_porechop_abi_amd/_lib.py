@@ -86,6 +86,8 @@ def lib():
                                   c_i64),
         'pcabi_middle_scan_host': ([c_int, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_p, ctypes.c_int32, c_int, c_int,
                                     c_int, c_int, c_d, c_p, c_i64], c_i64),
+        'pcabi_middle_scan_seqs': ([c_int, c_p, c_p, c_i64, c_p, c_p, c_p, ctypes.c_int32, c_int, c_int, c_int, c_int,
+                                    c_d, c_p, c_i64], c_i64),
         'pcabi_middle_seed_runs': ([], c_i64),
         'pcabi_middle_requeues': ([c_p], c_i64),
         'pcabi_scan_profile': ([c_p, ctypes.c_int32, c_p, ctypes.c_int32], ctypes.c_int32),
@@ -129,7 +131,7 @@ def exported_symbols():
             'pcabi_tile_layout', 'pcabi_tile_windows_dev', 'pcabi_align_cross_dev', 'pcabi_align_cross_dev_marked',
             'pcabi_end_trim_dev',
             'pcabi_best_full_identity_dev', 'pcabi_first_hits_host', 'pcabi_first_hit_dev', 'pcabi_scan_create',
-            'pcabi_scan_destroy', 'pcabi_middle_scan_dev', 'pcabi_middle_scan_host', 'pcabi_middle_seed_runs',
+            'pcabi_scan_destroy', 'pcabi_middle_scan_dev', 'pcabi_middle_scan_host', 'pcabi_middle_scan_seqs', 'pcabi_middle_seed_runs',
             'pcabi_middle_requeues', 'pcabi_scan_profile', 'pcabi_set_side_streams', 'pcabi_stream_side_streams',
             'pcabi_barcode_call_dev',
             'pcabi_barcode_call_host', 'pcabi_fastx_open', 'pcabi_fastx_type', 'pcabi_fastx_next',

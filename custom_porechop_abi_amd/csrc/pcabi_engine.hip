@@ -1571,6 +1571,10 @@ struct Engine {
     // pcabi_end_decisions_host: both sides' windows, results, trims, flags and lists; the two
     // sides' prepared adapter tables, kept while the adapters and the scoring stay the same
     DeviceBuf dec[17];
+    // pcabi_middle_scan_seqs: pinned staging slots the host strings are encoded into while the
+    // previous slots' copies run (allocated on first use, kept)
+    uint8_t *stage[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t stage_ev[3] = {nullptr, nullptr, nullptr};
     struct DTab {
         std::vector<uint8_t> codes;
         std::vector<int32_t> lens;
@@ -1888,6 +1892,14 @@ int align_host_impl(int device, const uint8_t *codes, int64_t codes_len, const i
 
 }  // namespace
 
+namespace {
+int64_t middle_scan_resident(Engine &e, const int64_t *win_off, const int32_t *win_len, int64_t n_win,
+                             const uint8_t *adp_codes, const int32_t *adp_off, const int32_t *adp_len, int32_t n_adp,
+                             int match, int mismatch, int gap_open, int gap_extend, double threshold, int32_t *hits,
+                             int64_t cap);
+int stage_seqs(Engine &e, const char *const *seqs, const int32_t *len, const int64_t *off, int64_t n, int64_t total);
+}  // namespace
+
 extern "C" {
 
 int pcabi_align_host(int device, const uint8_t *codes, int64_t codes_len, const int64_t *win_off,
@@ -1946,9 +1958,51 @@ int64_t pcabi_middle_scan_host(int device, const uint8_t *codes, int64_t codes_l
     if (int rc = engine_init(e, device)) return rc;
     HIP_TRY(hipSetDevice(device));
     if (int rc = e.codes.ensure((size_t)codes_len)) return rc;
+    HIP_TRY(hipMemcpyAsync(e.codes.p, codes, (size_t)codes_len, hipMemcpyHostToDevice, e.stream));
+    return middle_scan_resident(e, win_off, win_len, n_win, adp_codes, adp_off, adp_len, n_adp, match, mismatch,
+                                gap_open, gap_extend, threshold, hits, cap);
+}
+
+int64_t pcabi_middle_scan_seqs(int device, const char *const *seqs, const int32_t *seq_len, int64_t n,
+                               const uint8_t *adp_codes, const int32_t *adp_off, const int32_t *adp_len,
+                               int32_t n_adp, int match, int mismatch, int gap_open, int gap_extend,
+                               double threshold, int32_t *hits, int64_t cap) {
+    if (device < 0 || device >= 16) return fail(PCABI_E_ARG, "bad device index");
+    if (n < 0 || n_adp < 0 || cap < 0) return fail(PCABI_E_ARG, "negative count");
+    if (int rc = check_common(adp_len, n_adp)) return rc;
+    // the layout of pcabi_middle_scan_host's buffer (and of the Python SeqPack): windows back to
+    // back from 4-aligned offsets, N between them and 16 N bytes after the last
+    std::vector<int64_t> off((size_t)n);
+    int64_t total = 0;
+    for (int64_t w = 0; w < n; ++w) {
+        if (seq_len[w] < 0 || seq_len[w] > pcabi::MAX_WINDOW_LEN) return fail(PCABI_E_ARG, "window length out of range");
+        if (seq_len[w] > 0 && !seqs[w]) return fail(PCABI_E_ARG, "NULL sequence");
+        off[(size_t)w] = total;
+        total += ((int64_t)seq_len[w] + 3) & ~(int64_t)3;
+    }
+    total += 16;
+    if (n == 0 || n_adp == 0) return 0;
+    Engine &e = g_engines[device];
+    std::lock_guard<std::mutex> lock(e.mu);
+    if (int rc = engine_init(e, device)) return rc;
+    HIP_TRY(hipSetDevice(device));
+    if (int rc = e.codes.ensure((size_t)total)) return rc;
+    if (int rc = stage_seqs(e, seqs, seq_len, off.data(), n, total)) return rc;
+    return middle_scan_resident(e, off.data(), seq_len, n, adp_codes, adp_off, adp_len, n_adp, match, mismatch,
+                                gap_open, gap_extend, threshold, hits, cap);
+}
+
+}  // extern "C"
+
+namespace {
+
+// The middle scan over windows whose codes are in e.codes (being copied there on e.stream).
+int64_t middle_scan_resident(Engine &e, const int64_t *win_off, const int32_t *win_len, int64_t n_win,
+                             const uint8_t *adp_codes, const int32_t *adp_off, const int32_t *adp_len, int32_t n_adp,
+                             int match, int mismatch, int gap_open, int gap_extend, double threshold, int32_t *hits,
+                             int64_t cap) {
     if (int rc = e.woff.ensure(sizeof(int64_t) * (size_t)n_win)) return rc;
     if (int rc = e.wlen.ensure(sizeof(int32_t) * (size_t)n_win)) return rc;
-    HIP_TRY(hipMemcpyAsync(e.codes.p, codes, (size_t)codes_len, hipMemcpyHostToDevice, e.stream));
     HIP_TRY(hipMemcpyAsync(e.woff.p, win_off, sizeof(int64_t) * (size_t)n_win, hipMemcpyHostToDevice, e.stream));
     HIP_TRY(hipMemcpyAsync(e.wlen.p, win_len, sizeof(int32_t) * (size_t)n_win, hipMemcpyHostToDevice, e.stream));
     pcabi_adapters *tab = nullptr;
@@ -1965,6 +2019,102 @@ int64_t pcabi_middle_scan_host(int device, const uint8_t *codes, int64_t codes_l
     pcabi_adapters_destroy(tab);
     return r;
 }
+
+// Host strings -> Dna5 codes in e.codes: the layout's bytes [0, total) in chunks of kStageBytes,
+// each encoded by the worker threads (S/basic/alphabet_residue_tabs.h's table, as
+// pcabi_encode_dna5) into one of three pinned slots and copied to the device on e.stream while
+// the workers encode the next ones. A slot is refilled once its copy has completed. Nothing is
+// written to pageable memory, so the 10^8-byte batches cost neither page faults nor the
+// runtime's staging copy.
+constexpr int64_t kStageBytes = 32 << 20;
+int stage_seqs(Engine &e, const char *const *seqs, const int32_t *len, const int64_t *off, int64_t n, int64_t total) {
+    static const struct Tab {
+        uint8_t t[256];
+        Tab() {
+            for (int c = 0; c < 256; ++c) t[c] = 4;
+            t['A'] = t['a'] = 0;
+            t['C'] = t['c'] = 1;
+            t['G'] = t['g'] = 2;
+            t['T'] = t['t'] = t['U'] = t['u'] = 3;
+        }
+    } tab;
+    for (int k = 0; k < 3; ++k) {
+        if (!e.stage[k]) {
+            HIP_TRY(hipHostMalloc((void **)&e.stage[k], (size_t)kStageBytes, hipHostMallocDefault));
+            HIP_TRY(hipEventCreateWithFlags(&e.stage_ev[k], hipEventDisableTiming));
+        }
+    }
+    // bytes [b0, b1) of the layout into dst
+    auto encode = [&](int64_t b0, int64_t b1, uint8_t *dst) {
+        int64_t w = std::upper_bound(off, off + n, b0) - off - 1;
+        int64_t b = b0;
+        while (b < b1) {
+            const int64_t s = off[w], t = s + len[w], nx = w + 1 < n ? off[w + 1] : total;
+            if (b < t) {
+                const int64_t hi = std::min(t, b1);
+                const uint8_t *src = reinterpret_cast<const uint8_t *>(seqs[w]) + (b - s);
+                uint8_t *d = dst + (b - b0);
+                for (int64_t k = 0, m = hi - b; k < m; ++k) d[k] = tab.t[src[k]];
+                b = hi;
+            }
+            const int64_t hi = std::min(nx, b1);
+            if (b < hi) {
+                std::memset(dst + (b - b0), 4, (size_t)(hi - b));
+                b = hi;
+            }
+            ++w;
+        }
+    };
+    const int64_t n_chunk = (total + kStageBytes - 1) / kStageBytes;
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({16, (int64_t)std::thread::hardware_concurrency(),
+                                                                 total / (1 << 20)}));
+    std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[(size_t)n_chunk]);
+    for (int64_t c = 0; c < n_chunk; ++c) left[c].store(nt);
+    std::atomic<int64_t> free_upto{std::min<int64_t>(3, n_chunk)};   // chunks below it may be encoded
+    std::atomic<bool> stop{false};
+    auto work = [&](int t) {
+        for (int64_t c = 0; c < n_chunk; ++c) {
+            while (free_upto.load(std::memory_order_acquire) <= c && !stop.load(std::memory_order_relaxed))
+                std::this_thread::yield();
+            if (stop.load(std::memory_order_relaxed)) return;
+            const int64_t c0 = c * kStageBytes, c1 = std::min(total, c0 + kStageBytes);
+            const int64_t b0 = c0 + (c1 - c0) * t / nt, b1 = c0 + (c1 - c0) * (t + 1) / nt;
+            if (b0 < b1) encode(b0, b1, e.stage[c % 3] + (b0 - c0));
+            left[c].fetch_sub(1, std::memory_order_release);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
+    int rc = 0;
+    std::string err;
+    // thread 0 is this one: its share of a chunk, then the chunk's copy once every share is in
+    for (int64_t c = 0; c < n_chunk && !rc; ++c) {
+        const int64_t c0 = c * kStageBytes, c1 = std::min(total, c0 + kStageBytes);
+        const int64_t b1 = c0 + (c1 - c0) / nt;
+        if (c0 < b1) encode(c0, b1, e.stage[c % 3]);
+        left[c].fetch_sub(1, std::memory_order_release);
+        while (left[c].load(std::memory_order_acquire) > 0) std::this_thread::yield();
+        hipError_t he = hipMemcpyAsync((uint8_t *)e.codes.p + c0, e.stage[c % 3], (size_t)(c1 - c0),
+                                       hipMemcpyHostToDevice, e.stream);
+        if (he == hipSuccess) he = hipEventRecord(e.stage_ev[c % 3], e.stream);
+        // chunk c + 3 reuses this slot: once this copy is done (the next two chunks encode meanwhile)
+        if (he == hipSuccess && c + 3 < n_chunk) he = hipEventSynchronize(e.stage_ev[c % 3]);
+        if (he != hipSuccess) {
+            rc = PCABI_E_DEVICE;
+            err = std::string("pcabi_middle_scan_seqs: staging copy: ") + hipGetErrorString(he);
+            break;
+        }
+        free_upto.store(std::min<int64_t>(n_chunk, c + 4), std::memory_order_release);
+    }
+    stop.store(true);
+    for (auto &t : th) t.join();
+    if (rc) return fail(rc, err);
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
 
 int pcabi_first_hit_dev(const int32_t *res, int64_t stride, int64_t n_win, int32_t n_adp, double threshold,
                         int32_t *hits, int64_t hit_stride, void *stream) {

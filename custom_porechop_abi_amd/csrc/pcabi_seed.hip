@@ -88,6 +88,7 @@ constexpr int kBandGrid = 4096;    // band / cands launches whose count is on th
 constexpr int kCnt = 2 * kCls + 2;
 constexpr int kFlag = 2 * kCls;
 constexpr int kVer = kCnt;          // the verified-seed counter, after the task counters and flags
+constexpr int kCntAll = kCnt + 1;   // every counter k_bound_reset zeroes
 constexpr int kPinMaxE = 8;        // the pinned band is built for E <= kPinMaxE
 
 struct ScanArgs {
@@ -1286,6 +1287,255 @@ __global__ __launch_bounds__(256) void k_seed_band_pin(const int4 *task, const i
     }
 }
 
+// k_seed_band_pin_sw (r05): the same tasks, bounds and verified seeds as k_seed_band_pin, with the
+// lanes of a wave switching tasks independently and taking them from a shared counter.
+// k_seed_band_pin gives lane l of the persistent grid the tasks l, l + stride, ... (~10 per lane at
+// 20 kb) and runs one task per lane and PASS, a pass as long as its longest task: a random probe
+// hit's band usually exits within a few rows, so half of the lane-rows idle (tools/band_stats.py:
+// 0.47-0.53 active, r05j). Here each block owns a contiguous range of the tasks (~2.5 k at 20 kb,
+// so the blocks' totals differ little) behind an LDS counter; the row loop runs until the block's
+// counter is exhausted; a lane whose task ended starts its next one as soon as kRefill lanes wait
+// (or none runs), and the waiting lanes take new tasks with one LDS atomic per wave (one global
+// counter measured 10x slower: same-address atomics serialise at the L2). Per lane a three-deep
+// pipeline keeps every memory latency off the refill: the next task with its read bytes loaded (A),
+// the one after with its record loaded (B) and an index (C); a grab's answer is read at the next
+// refill.
+constexpr int kRefill = 16;
+
+template <int E, int NC4>
+__global__ __launch_bounds__(256) void k_seed_band_pin_sw(const int4 *task, const int32_t *n_task, int64_t cap,
+                                                          const uint8_t *codes, const uint8_t *adp, int32_t adp_dw,
+                                                          const int32_t *adp_off, const int32_t *adp_meta, int32_t n_adp,
+                                                          pcabi::Scoring sc, int32_t *bound, int64_t n, VerOut vo) {
+    constexpr int W = 2 * E + 1;
+    extern __shared__ uint4 lds4[];
+    __shared__ int32_t s_next;                          // the block's task counter
+    uint32_t *lds = reinterpret_cast<uint32_t *>(lds4);
+    const int64_t nt_all = min((int64_t)*n_task, cap);
+    const int64_t per = (nt_all + gridDim.x - 1) / gridDim.x;
+    const int64_t blo = min(nt_all, (int64_t)blockIdx.x * per);
+    if (threadIdx.x == 0) s_next = (int32_t)blo;
+    int32_t *next = &s_next;
+    for (int i = threadIdx.x; i < adp_dw; i += 256) lds[i] = reinterpret_cast<const uint32_t *>(adp)[i];
+    for (int i = threadIdx.x; i < n_adp; i += 256) {
+        lds[adp_dw + i] = (uint32_t)adp_off[i];
+        lds[adp_dw + n_adp + i] = (uint32_t)adp_meta[i];
+    }
+    __syncthreads();
+    const uint8_t *ad = reinterpret_cast<const uint8_t *>(lds);
+    const int32_t *aoffs = reinterpret_cast<const int32_t *>(lds + adp_dw);
+    const int32_t *ameta = aoffs + n_adp;
+    uint4 *slot4 = lds4 + ((adp_dw + 2 * n_adp + 3) >> 2) + (int)threadIdx.x * NC4;
+    const uint8_t *slot = reinterpret_cast<const uint8_t *>(slot4);
+    const int64_t nt = min(nt_all, blo + per);         // the end of the block's range
+    const int lane = (int)(threadIdx.x & 63);
+    const uint64_t lt = (1ull << lane) - 1;
+    const int bs = pcabi::best_sub(sc), ma = sc.ma, mi = sc.mi, go = sc.go, ge = sc.ge;
+    const uintptr_t lo_addr = (uintptr_t)codes & ~(uintptr_t)15;
+    auto range_of = [&](const int4 &rc, uintptr_t &cb, int &nld) {   // as k_seed_band_pin
+        const int a = rc.y >> 11, o = rc.y & 255;
+        const int L = (int)((uint32_t)ameta[a] & 255u);
+        const uintptr_t pa = (uintptr_t)codes + (uintptr_t)(((uint64_t)(uint32_t)rc.w << 32) | (uint32_t)rc.z);
+        const uintptr_t lo = pa - (uintptr_t)(o + E), hi = pa - (uintptr_t)o + (uintptr_t)(L + E);
+        cb = lo & ~(uintptr_t)15;
+        if (pa >= lo_addr && cb < lo_addr) cb = lo_addr;
+        nld = (int)((hi - cb + 15) >> 4);
+    };
+    int4 recA = make_int4(0, 0, 0, 0), recB = recA;
+    bool vA = false, vB = false, vC = false;
+    int32_t idxC = 0;
+    uint4 chA[NC4];
+    uintptr_t cbA = lo_addr;
+    auto load_range = [&]() {
+        int nld = 0;
+        range_of(recA, cbA, nld);
+#pragma unroll
+        for (int k = 0; k < NC4; ++k)
+            chA[k] = k < nld ? *reinterpret_cast<const uint4 *>(cbA + 16 * (uintptr_t)k) : make_uint4(0u, 0u, 0u, 0u);
+    };
+    // the wave's outstanding grab: the leader lane's atomic answer, read at the next refill by the
+    // lanes it was for (pend = member, pre = the lane's place among them)
+    int32_t pendB0 = 0;
+    int pendLeader = -1;
+    bool pend = false;
+    int pre = 0;
+    auto grab_now = [&]() -> int32_t {                 // every lane: one index each (start-up)
+        int32_t b0 = 0;
+        if (lane == 0) b0 = atomicAdd(next, 64);
+        return __shfl(b0, 0) + lane;
+    };
+    {
+        const int32_t ia = grab_now(), ib = grab_now(), ic = grab_now();
+        vA = ia < nt;
+        if (vA) {
+            recA = task[ia];
+            load_range();
+        }
+        vB = ib < nt;
+        if (vB) recB = task[ib];
+        vC = ic < nt;
+        idxC = ic;
+    }
+    auto pin_start = [&](int x) -> int { return x == E ? 0 : (x > E ? go + (x - E - 1) * ge : kNeg); };
+    bool active = false;
+    int4 rc = make_int4(0, 0, 0, 0);
+    int a = 0, o = 0, T = 0, aoff = 0, base = 0, pin = 0;
+    int64_t bidx = 0, dabs = 0;
+    int S[W], V[W], R[W];
+#pragma unroll
+    for (int x = 0; x < W; ++x) S[x] = V[x] = R[x] = 0;
+    int phase = 0, rows = 0, other = 0, mx = 0, apos = 0, adir = 1, bpos = 0, bdir = 1;
+#ifdef PCABI_BAND_STATS
+    unsigned long long st_it = 0, st_act = 0, st_tasks = 0, st_refill = 0;
+#endif
+    auto begin_prefix = [&]() {                        // rows o .. 1 backwards, mirrored band
+        phase = 1;
+        rows = o;
+        other = pin + mx;
+        mx = 0;
+#pragma unroll
+        for (int x = 0; x < W; ++x) {
+            S[x] = pin_start(x);
+            V[x] = kNeg;
+            R[x] = slot[base - 1 + E - x];
+        }
+        bpos = base - 2 - E;
+        bdir = -1;
+        apos = aoff + o - 1;
+        adir = -1;
+    };
+    for (;;) {                                         // wave-uniform exits
+        const uint64_t can = __ballot(!active && vA);
+        const uint64_t run = __ballot(active);
+        if (!can && !run) break;
+        bool ver = false;
+        if (can && (!run || __popcll(can) >= kRefill)) {
+#ifdef PCABI_BAND_STATS
+            st_refill += 1;
+            st_tasks += __popcll(can);
+#endif
+            // the previous grab's answer, to the lanes it was for
+            if (pendLeader >= 0) {
+                const int32_t b0 = __shfl(pendB0, pendLeader);
+                if (pend) {
+                    idxC = b0 + pre;
+                    vC = idxC < nt;
+                    pend = false;
+                }
+            }
+            const bool me = !active && vA;
+            if (me) {                                  // this lane starts task A; A <- B <- C
+#pragma unroll
+                for (int k = 0; k < NC4; ++k) slot4[k] = chA[k];
+                rc = recA;
+                const uintptr_t cb = cbA;
+                vA = vB;
+                recA = recB;
+                if (vA) load_range();
+                vB = vC;
+                if (vB) recB = task[idxC];
+                vC = false;
+                a = rc.y >> 11;
+                o = rc.y & 255;
+                const int K = kMinK + ((rc.y >> 8) & 7);
+                const uint32_t meta = (uint32_t)ameta[a];
+                const int L = (int)(meta & 255u);
+                T = (int)(meta >> 12);
+                aoff = aoffs[a];
+                bidx = (int64_t)a * n + rc.x;
+                const uintptr_t pa = (uintptr_t)codes + (uintptr_t)(((uint64_t)(uint32_t)rc.w << 32) | (uint32_t)rc.z);
+                base = (int)(pa - cb);
+                pin = ma * K;
+                phase = 0;
+                rows = L - o - K;
+                other = pin + bs * o;
+                mx = 0;
+                apos = aoff + o + K;
+                adir = 1;
+                bpos = base + K + E + 1;
+                bdir = 1;
+#pragma unroll
+                for (int x = 0; x < W; ++x) {
+                    S[x] = pin_start(x);
+                    V[x] = kNeg;
+                    R[x] = slot[base + K + x - E];
+                }
+                dabs = (int64_t)(((uint64_t)(uint32_t)rc.w << 32) | (uint32_t)rc.z) - o;
+                active = true;
+                if (rows == 0) {                       // the run ends the adapter: Q = 0
+                    if (o == 0) {
+                        atomicMax(&bound[bidx], pin);
+                        ver = pin >= T;
+                        active = false;
+                    } else {
+                        begin_prefix();
+                    }
+                }
+            }
+            // a new index for every lane that used its C (read at the next refill)
+            const uint64_t want = __ballot(me);
+            pendLeader = -1;
+            if (want) {
+                const int leader = __ffsll((unsigned long long)want) - 1;
+                if (lane == leader) pendB0 = atomicAdd(next, __popcll(want));
+                pendLeader = leader;
+                pend = me;
+                pre = __popcll(want & lt);
+            }
+        }
+#ifdef PCABI_BAND_STATS
+        st_it += 64;
+        st_act += __popcll(__ballot(active));
+#endif
+        if (active) {
+            const int ab = ad[apos];
+            apos += adir;
+            const int nb = slot[bpos];
+            bpos += bdir;
+            int h = kNeg, sl = kNeg;
+#pragma unroll
+            for (int x = 0; x < W; ++x) {
+                const int dg = S[x] + (R[x] == ab ? ma : mi);
+                const int vu = (x + 1 < W) ? max(V[x + 1] + ge, S[x + 1] + go) : kNeg;
+                h = max(h + ge, sl + go);
+                const int sv = max(dg, max(vu, h));
+                S[x] = sv;
+                V[x] = vu;
+                sl = sv;
+            }
+#pragma unroll
+            for (int x = 0; x + 1 < W; ++x) R[x] = R[x + 1];
+            R[W - 1] = nb;
+            --rows;
+            mx = S[0];
+#pragma unroll
+            for (int x = 1; x < W; ++x) mx = max(mx, S[x]);
+            const int ub = mx + bs * rows + other;
+            if (ub < T) {
+                atomicMax(&bound[bidx], ub);
+                active = false;
+            } else if (rows == 0) {
+                if (phase == 0 && o > 0) {
+                    begin_prefix();
+                } else {
+                    atomicMax(&bound[bidx], mx + other);
+                    ver = mx + other >= T;
+                    active = false;
+                }
+            }
+        }
+        if (vo.list) put_verified(vo, ver, rc.x, a, E, dabs);
+    }
+#ifdef PCABI_BAND_STATS
+    if (lane == 0) {
+        atomicAdd(&g_band_stats[E > 2][0], st_it);
+        atomicAdd(&g_band_stats[E > 2][1], st_act);
+        atomicAdd(&g_band_stats[E > 2][2], st_tasks);
+        atomicAdd(&g_band_stats[E > 2][3], st_refill);
+    }
+#endif
+}
+
 // The pairs whose bound reaches their adapter's threshold T[a], as (a << 32 | read) keys
 // (unordered; one atomic per wave), grid-stride over the n_dev x n_adp bounds (row stride n).
 // pmap != nullptr (the device rounds; pmap may be `bound` itself): a candidate pair's entry becomes its
@@ -1561,7 +1811,7 @@ int plan(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hl
     if (int rc = s->adp.ensure(flat.size())) return rc;
     if (int rc = s->adp_off.ensure(4 * aoff.size())) return rc;
     if (int rc = s->adp_len.ensure(4 * alen.size())) return rc;
-    if (int rc = s->cnt.ensure(4 * (kCnt + 1))) return rc;
+    if (int rc = s->cnt.ensure(4 * kCntAll)) return rc;
     if (int rc = s->thr.ensure(4 * thr.size())) return rc;
     // the pinned band: adapters and their (offset, meta) in LDS, meta = L | T << 12 (a task carries its K)
     {
@@ -1613,19 +1863,31 @@ template <int E, int NC4>
 int launch_pin(State *s, int c, const int4 *task, const uint8_t *codes, const pcabi::Scoring &sc, int64_t n,
                int64_t n_in, hipStream_t st) {
     const size_t lds = 16 * (((size_t)s->adp_bytes / 4 + 2 * (size_t)s->n_adp + 3) / 4) + 16 * 256 * (size_t)NC4;
+    // PCABI_BAND_SWITCH=1: lanes switch tasks alone (k_seed_band_pin_sw, an A/B: no faster, r05j)
+    static const bool sw = [] {
+        const char *e = std::getenv("PCABI_BAND_SWITCH");
+        return e && e[0] == '1';
+    }();
     if (!s->pin_blocks[c]) {
         int dev = 0, cus = 0, per_cu = 0;
         SD_TRY(hipGetDevice(&dev));
         SD_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_band_pin<E, NC4>, 256, lds));
+        if (sw) SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_band_pin_sw<E, NC4>, 256, lds));
+        else SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_band_pin<E, NC4>, 256, lds));
         s->pin_blocks[c] = std::max(1, cus * std::max(1, per_cu));
     }
     const int64_t blocks = n_in >= 0 ? std::max<int64_t>(1, std::min<int64_t>((n_in + 255) / 256, s->pin_blocks[c]))
                                      : s->pin_blocks[c];
-    hipLaunchKernelGGL((k_seed_band_pin<E, NC4>), dim3((unsigned)blocks), dim3(256), lds, st, task,
-                       (const int32_t *)s->cnt.p + c, s->cap, codes, (const uint8_t *)s->adp.p, s->adp_bytes / 4,
-                       (const int32_t *)s->adp_off.p, (const int32_t *)s->adp_meta.p, s->n_adp, sc,
-                       (int32_t *)s->bound.p, n, s->ver);
+    if (sw)
+        hipLaunchKernelGGL((k_seed_band_pin_sw<E, NC4>), dim3((unsigned)blocks), dim3(256), lds, st, task,
+                           (const int32_t *)s->cnt.p + c, s->cap, codes, (const uint8_t *)s->adp.p, s->adp_bytes / 4,
+                           (const int32_t *)s->adp_off.p, (const int32_t *)s->adp_meta.p, s->n_adp, sc,
+                           (int32_t *)s->bound.p, n, s->ver);
+    else
+        hipLaunchKernelGGL((k_seed_band_pin<E, NC4>), dim3((unsigned)blocks), dim3(256), lds, st, task,
+                           (const int32_t *)s->cnt.p + c, s->cap, codes, (const uint8_t *)s->adp.p, s->adp_bytes / 4,
+                           (const int32_t *)s->adp_off.p, (const int32_t *)s->adp_meta.p, s->n_adp, sc,
+                           (int32_t *)s->bound.p, n, s->ver);
     return 0;
 }
 
@@ -1779,7 +2041,7 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
     if (int rc = s->raw.ensure(sizeof(uint4) * (size_t)s->raw_cap)) return rc;
     if (int rc = s->rawcnt.ensure(4 * (size_t)s->n_slab)) return rc;
     if (int rc = s->task.ensure(sizeof(int4) * kCls * (size_t)(s->cap + s->ecap))) return rc;
-    if (int rc = s->cnt.ensure(4 * (kCnt + 1))) return rc;
+    if (int rc = s->cnt.ensure(4 * kCntAll)) return rc;
     if (int rc = s->bound.ensure(sizeof(int32_t) * (size_t)n * n_adp)) return rc;
     ScanArgs A = s->a;
     A.codes = codes;
@@ -1812,7 +2074,7 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
     }
     A.seg_cum = (const int64_t *)s->segcum.p;
     hipLaunchKernelGGL(k_bound_reset, dim3(1024), dim3(256), 0, st, (int32_t *)s->bound.p, n, n_dev, n_adp, A.cnt,
-                       kCnt + 1, (unsigned long long *)s->ccnt.p);
+                       kCntAll, (unsigned long long *)s->ccnt.p);
     if (s->pev) SD_TRY(hipEventRecord(s->pev[0], st));
     if (s->bytemap)
         hipLaunchKernelGGL(k_seed_scan, dim3(grid), dim3(kScanThreads), 0, st, A);
@@ -1976,7 +2238,7 @@ int bounds_dev(State *s, const uint8_t *codes, const int64_t *v_off, const int32
     if (win) {
         if (s->vcap == 0) s->vcap = std::max<int64_t>(1 << 16, n);
         if (int rc = s->vseed.ensure(sizeof(int4) * (size_t)s->vcap)) return rc;
-        if (int rc = s->cnt.ensure(4 * (kCnt + 1))) return rc;
+        if (int rc = s->cnt.ensure(4 * kCntAll)) return rc;
         s->ver = VerOut{(int4 *)s->vseed.p, (int32_t *)s->cnt.p + kVer, (int32_t *)s->cnt.p + kFlag + 1, s->vcap};
     }
     if (int rc = enqueue_seeds(s, codes, v_off, v_len, n, n_dev, n_adp, sc, nullptr, st)) return rc;

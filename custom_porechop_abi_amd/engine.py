@@ -273,6 +273,31 @@ def middle_scan(windows, adapter_seqs, scoring_scheme_vals, threshold, device=0)
         cap = int(n)
 
 
+def middle_scan_seqs(addr, lens, adapter_seqs, scoring_scheme_vals, threshold, device=0):
+    """middle_scan over windows given as host string addresses (pcabi_middle_scan_seqs): addr
+    uint64[n] the address of each window's first character (an ASCII str's own bytes, see
+    str_buffers), lens its length; the library encodes them into pinned staging buffers while the
+    earlier chunks copy to the device -- no Dna5 pack in pageable memory. Same result as
+    middle_scan over the packed windows."""
+    addr = np.ascontiguousarray(addr, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.int32)
+    acodes, aoffs, alens = encode_adapters(adapter_seqs)
+    n_win = len(lens)
+    if n_win == 0 or not len(alens):
+        return np.zeros((6, 0), np.int32)
+    m, mm, go, ge = (int(x) for x in scoring_scheme_vals[:4])
+    cap = max(1024, n_win // 4)
+    while True:
+        out = np.zeros((6, cap), dtype=np.int32)
+        n = lib().pcabi_middle_scan_seqs(device, _ptr(addr), _ptr(lens), n_win, _ptr(acodes), _ptr(aoffs),
+                                         _ptr(alens), len(alens), m, mm, go, ge, float(threshold), _ptr(out), cap)
+        if n < 0:
+            check(int(n), 'pcabi_middle_scan_seqs')
+        if n <= cap:
+            return out[:, :n]
+        cap = int(n)
+
+
 def best_full_identity(windows, adapter_seqs, scoring_scheme_vals, best=None, device=0, best_device_ptr=None):
     """Adapter-set search reduction on the GPU (pcabi_best_full_identity_host,
     porechop_abi/nanopore_read.py:158-173): best[a] = max(best[a], max over windows of the full

@@ -237,7 +237,7 @@ class FileTrimmer(object):
         Three stages overlap across batches: a reader thread parses the next batch, this thread
         runs the device work, a writer thread writes the previous batch (in file order). The
         library's parse, alignment and write calls release the GIL. times: 'parse' / 'write_wait'
-        are this thread's waits, 'write' the writer's own busy time (overlapped)."""
+        are this thread's waits, 'read' / 'write' the reader's / writer's own busy time (overlapped)."""
         counts = {'reads_in': 0, 'reads_kept': 0}
         bins = {}                             # barcode name -> (path, reads selected for it)
         if self.barcode_dir is not None:
@@ -268,8 +268,16 @@ class FileTrimmer(object):
 
         def produce():
             try:
-                items = source if source is not None else ((k, b, alb) for k, (b, alb) in enumerate(batches()))
-                for k, b, alb in items:
+                items = iter(source if source is not None else
+                             ((k, b, alb) for k, (b, alb) in enumerate(batches())))
+                while True:
+                    t0 = time.perf_counter()
+                    item = next(items, None)
+                    # the reader's own busy time (parse; overlapped like 'write')
+                    self.times['read'] = self.times.get('read', 0.0) + time.perf_counter() - t0
+                    if item is None:
+                        break
+                    k, b, alb = item
                     if batch_filter is not None and not batch_filter(k):
                         continue
                     if not put_parsed((k, b, alb)):

@@ -437,9 +437,22 @@ def _middle_hits_by_read(seqs, adapter_seqs, middle_threshold, scoring_scheme_va
     n = len(seqs)
     if n == 0 or not adapter_seqs:
         return []
-    pack = SeqPack(seqs) if bounds is None else SeqPack.windows(seqs, *bounds, bufs=bufs)
-    views = pack.views(np.zeros(n, np.int64), pack.lengths)
-    h = engine.middle_scan(views, adapter_seqs, scoring_scheme_vals, middle_threshold, device=device)
+    if bufs is None:
+        bufs = engine.str_buffers(seqs)
+    if bufs is not None:
+        # ASCII strs: the windows go to the library as addresses into the strs' own bytes, encoded
+        # there into pinned staging buffers while earlier chunks copy (no pack in pageable memory)
+        starts, lengths = (np.zeros(n, np.int64), bufs[1]) if bounds is None else \
+            (np.asarray(bounds[0], np.int64), np.asarray(bounds[1], np.int64))
+        if len(starts) != n or len(lengths) != n or (starts < 0).any() or (lengths < 0).any() or \
+                (starts + lengths > bufs[1]).any():
+            raise ValueError('middle scan: a window lies outside its sequence')
+        h = engine.middle_scan_seqs(bufs[0] + starts.astype(np.uint64), lengths, adapter_seqs, scoring_scheme_vals,
+                                    middle_threshold, device=device)
+    else:
+        pack = SeqPack(seqs) if bounds is None else SeqPack.windows(seqs, *bounds, bufs=bufs)
+        views = pack.views(np.zeros(n, np.int64), pack.lengths)
+        h = engine.middle_scan(views, adapter_seqs, scoring_scheme_vals, middle_threshold, device=device)
     if not h.shape[1]:
         return []
     full = engine.pid6(h[4], h[5])

@@ -311,6 +311,12 @@ int pcabi_first_hit_dev(const int32_t *res, int64_t stride, int64_t n_win, int32
  *                                 the device with their counts there (no host round trip between
  *                                 rounds; PCABI_MIDDLE_DEVROUNDS=0 keeps the host-driven loop).
  *   pcabi_middle_scan_host      : host buffers (as pcabi_align_host), copies in, scans.
+ *   pcabi_middle_scan_seqs      : the windows as host strings, seqs[w] its first character and
+ *                                 seq_len[w] its length (the char * the reference's ctypes wrapper
+ *                                 passes per call, porechop_abi/cpp_function_wrappers.py:42-63):
+ *                                 encoded (the Dna5 table of pcabi_encode_dna5) by host threads into
+ *                                 pinned staging buffers while earlier chunks copy to the device,
+ *                                 then scanned as pcabi_middle_scan_host. Same hits, same returns.
  *   pcabi_middle_seed_runs      : how many round-1 scans took their bounds from exact k-mer seeds
  *                                 (pcabi_seed.hip) instead of the score filter, process-wide.
  *                                 PCABI_MIDDLE_SEEDS=0 / 1 (default, cost model) / 2 (always when
@@ -339,6 +345,11 @@ int64_t pcabi_middle_scan_dev(pcabi_scan *s, const uint8_t *codes, const int64_t
                               double threshold, int32_t *hits, int64_t cap, void *stream);
 int64_t pcabi_middle_scan_host(int device, const uint8_t *codes, int64_t codes_len,
                                const int64_t *win_off, const int32_t *win_len, int64_t n_win,
+                               const uint8_t *adp_codes, const int32_t *adp_off,
+                               const int32_t *adp_len, int32_t n_adp, int match, int mismatch,
+                               int gap_open, int gap_extend, double threshold, int32_t *hits,
+                               int64_t cap);
+int64_t pcabi_middle_scan_seqs(int device, const char *const *seqs, const int32_t *seq_len, int64_t n,
                                const uint8_t *adp_codes, const int32_t *adp_off,
                                const int32_t *adp_len, int32_t n_adp, int match, int mismatch,
                                int gap_open, int gap_extend, double threshold, int32_t *hits,

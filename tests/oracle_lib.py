@@ -170,6 +170,33 @@ def middle_scan_threaded(windows, adapter_seqs, scoring, threshold, threads=None
         cap = int(nh)
 
 
+def seqs_windows(addr, lens):
+    """The windows engine.middle_scan_seqs takes (host character addresses, lengths) as the packed
+    (codes, offsets, lengths) the windowed checkers take: the bytes read back with ctypes, encoded
+    with the Dna5 table, 4-aligned offsets as SeqPack lays them out."""
+    from custom_porechop_abi_amd.engine import DNA5, PAD
+    lens = np.asarray(lens, np.int64)
+    offs = np.zeros(len(lens), np.int64)
+    if len(lens) > 1:
+        offs[1:] = np.cumsum((lens + 3) & ~3)[:-1]
+    total = int(offs[-1] + ((lens[-1] + 3) & ~3)) + PAD if len(lens) else PAD
+    codes = np.full(total, 4, np.uint8)
+    for a, o, l in zip(np.asarray(addr, np.uint64).tolist(), offs.tolist(), lens.tolist()):
+        if l:
+            codes[o:o + l] = DNA5[np.frombuffer(ctypes.string_at(a, l), np.uint8)]
+    return codes, offs, lens.astype(np.int32)
+
+
+def middle_scan_seqs_windows(addr, lens, adapter_seqs, scoring, threshold, device=0):
+    """Drop-in for custom_porechop_abi_amd.engine.middle_scan_seqs computed by the oracle (CPU)."""
+    return middle_scan_windows(seqs_windows(addr, lens), adapter_seqs, scoring, threshold)
+
+
+def middle_scan_seqs_threaded(addr, lens, adapter_seqs, scoring, threshold, device=0):
+    """middle_scan_seqs_windows on the C loop (middle_scan_threaded)."""
+    return middle_scan_threaded(seqs_windows(addr, lens), adapter_seqs, scoring, threshold)
+
+
 def best_full_identity_windows(windows, adapter_seqs, scoring, best=None, device=0, best_device_ptr=None):
     """Drop-in for custom_porechop_abi_amd.engine.best_full_identity computed by the oracle (CPU)."""
     from custom_porechop_abi_amd.engine import pid6

@@ -135,6 +135,23 @@ def test_gathered_windows_equal_packed_slices():
     assert np.array_equal(got.codes, ref.codes) and np.array_equal(got.lengths, ref.lengths)
 
 
+def test_host_string_windows_checker_layout():
+    """oracle_lib.seqs_windows -- how the checkers read the windows engine.middle_scan_seqs takes
+    (host character addresses + lengths) -- gives SeqPack's layout of the same slices."""
+    import random
+    from custom_porechop_abi_amd import engine
+    from tests import oracle_lib
+    rng = random.Random(5)
+    seqs = [''.join(rng.choice('ACGTNacgu-xyz') for _ in range(rng.randint(0, 900))) for _ in range(300)] + ['']
+    st = [rng.randint(0, len(s)) for s in seqs]
+    ln = [rng.randint(0, len(s) - a) for s, a in zip(seqs, st)]
+    addr, have = engine.str_buffers(seqs)
+    codes, offs, lens = oracle_lib.seqs_windows(addr + np.array(st, np.uint64), ln)
+    ref = engine.SeqPack([s[a:a + l] for s, a, l in zip(seqs, st, ln)])
+    assert np.array_equal(codes, ref.codes) and np.array_equal(offs, ref.offsets)
+    assert np.array_equal(lens, ref.lengths)
+
+
 def test_gathered_windows_reject_out_of_range():
     from custom_porechop_abi_amd import engine
     for st, ln in (([0], [5]), ([-1], [1]), ([2], [-1]), ([0, 0], [1, 1])):

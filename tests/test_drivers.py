@@ -87,6 +87,7 @@ def test_drivers_match_reference_with_oracle_backend(case_name, monkeypatch):
     monkeypatch.setattr(engine, 'best_full_identity', oracle_lib.best_full_identity_windows)
     monkeypatch.setattr(engine, 'first_hits', oracle_lib.first_hits_windows)
     monkeypatch.setattr(engine, 'middle_scan', oracle_lib.middle_scan_windows)
+    monkeypatch.setattr(engine, 'middle_scan_seqs', oracle_lib.middle_scan_seqs_windows)
     check_case([c for c in G2['cases'] if c['case'] == case_name][0])
 
 
@@ -105,6 +106,7 @@ def test_reference_test_expectations_one_adapter_set(monkeypatch):
     monkeypatch.setattr(engine, 'best_full_identity', oracle_lib.best_full_identity_windows)
     monkeypatch.setattr(engine, 'first_hits', oracle_lib.first_hits_windows)
     monkeypatch.setattr(engine, 'middle_scan', oracle_lib.middle_scan_windows)
+    monkeypatch.setattr(engine, 'middle_scan_seqs', oracle_lib.middle_scan_seqs_windows)
     case = [c for c in G2['cases'] if c['case'] == 'one_adapter_set'][0]
     _, _, _, reads = run_pipeline(case)
     assert sum(1 for r in reads if r.start_trim_amount) == 4

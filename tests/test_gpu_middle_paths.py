@@ -197,6 +197,36 @@ def test_scan_leaves_the_callers_reads_intact(gpu_lib, monkeypatch, reads_8kb, d
 
 
 @pytest.mark.gpu
+def test_host_string_scan_equals_packed_scan(gpu_lib):
+    """pcabi_middle_scan_seqs (the windows as host string addresses, encoded by host threads into
+    three pinned 32 MB staging slots while earlier chunks copy) returns what
+    pcabi_middle_scan_host returns for the SeqPack of the same windows: ~110 MB of windows (four
+    chunks, a slot refilled), odd window starts, lower-case / N / other bytes, empty windows; and
+    the first reads against the oracle loop."""
+    from custom_porechop_abi_amd import engine
+    rng = random.Random(3)
+    base = _reads(11, 120, 8000, 90.0)
+    base[0] = base[0][:3000].lower() + base[0][3000:]
+    base[1] = base[1][:2000] + 'NNNNRYKM' + base[1][2000:]
+    seqs, total = [], 0
+    while total < 110 * 10 ** 6:
+        seqs.append(base[rng.randrange(len(base))])
+        total += len(seqs[-1])
+    st = np.array([rng.randint(0, 60) for _ in seqs], np.int64)
+    ln = np.array([max(0, len(s) - a - rng.randint(0, 60)) for s, a in zip(seqs, st)], np.int64)
+    ln[5] = 0
+    addr, have = engine.str_buffers(seqs)
+    got = engine.middle_scan_seqs(addr + st.astype(np.uint64), ln, ADPS, SC, 90.0)
+    pack = engine.SeqPack.windows(seqs, st, ln)
+    exp = engine.middle_scan(pack.views(np.zeros(len(seqs), np.int64), pack.lengths), ADPS, SC, 90.0)
+    assert got.shape[1] > 1000
+    assert np.array_equal(got, exp)
+    k = 150
+    ora = oracle_lib.middle_scan_seqs_threaded(addr[:k] + st[:k].astype(np.uint64), ln[:k], ADPS, SC, 90.0)
+    assert np.array_equal(_sorted(got[:, got[0] < k]), _sorted(ora))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('windows', ['0', '1'])
 @pytest.mark.parametrize('fault', ['0:1', '0:2', '0:4', '1:1', '1:2', '1:4', '2:7', '0:7,1:4,2:2', '0:8', '1:8',
                                    '2:15'])

@@ -53,6 +53,7 @@ def _worker(rank, world, port, case_name, out_dir):
     engine.best_full_identity = oracle_lib.best_full_identity_windows
     engine.first_hits = oracle_lib.first_hits_windows
     engine.middle_scan = oracle_lib.middle_scan_windows
+    engine.middle_scan_seqs = oracle_lib.middle_scan_seqs_windows
     dist.init_process_group('gloo', init_method='tcp://127.0.0.1:%d' % port, rank=rank, world_size=world)
     try:
         case = next(c for c in G2['cases'] if c['case'] == case_name)
@@ -198,6 +199,7 @@ def _file_worker(rank, world, port, case_name, in_path, out_path, res_path, bins
     engine.best_full_identity = oracle_lib.best_full_identity_windows
     engine.first_hits = oracle_lib.first_hits_windows
     engine.middle_scan = oracle_lib.middle_scan_windows
+    engine.middle_scan_seqs = oracle_lib.middle_scan_seqs_windows
     dist.init_process_group('gloo', init_method='tcp://127.0.0.1:%d' % port, rank=rank, world_size=world)
     try:
         case = next(c for c in G2['cases'] if c['case'] == case_name)
@@ -342,6 +344,7 @@ def _albacore_worker(rank, world, port, bins, check, out_path, res_path):
     engine.best_full_identity = oracle_lib.best_full_identity_windows
     engine.first_hits = oracle_lib.first_hits_windows
     engine.middle_scan = oracle_lib.middle_scan_windows
+    engine.middle_scan_seqs = oracle_lib.middle_scan_seqs_windows
     dist.init_process_group('gloo', init_method='tcp://127.0.0.1:%d' % port, rank=rank, world_size=world)
     try:
         counts = shards.trim_file_sharded(ALBACORE, out_path, 'fastq', check_reads=check, max_reads=3,

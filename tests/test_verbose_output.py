@@ -74,6 +74,7 @@ def _oracle_backend(monkeypatch):
     monkeypatch.setattr(engine, 'best_full_identity', oracle_lib.best_full_identity_windows)
     monkeypatch.setattr(engine, 'first_hits', oracle_lib.first_hits_windows)
     monkeypatch.setattr(engine, 'middle_scan', oracle_lib.middle_scan_windows)
+    monkeypatch.setattr(engine, 'middle_scan_seqs', oracle_lib.middle_scan_seqs_windows)
 
 
 @pytest.mark.parametrize('case_name,verbosity,threads', RUNS)
