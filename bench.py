@@ -1408,12 +1408,12 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
     # on its own, events around its phases, the units they processed -> per-kernel roofline
     phases = None
     if rank == 0:
-        prof = np.zeros(16, np.float64)
+        prof = np.zeros(26, np.float64)
         timed = dict(stats)
         rc = int(L.pcabi_scan_profile(scan, 1, None, 0))
         if rc >= 0:
             step()
-            rc = int(L.pcabi_scan_profile(scan, 0, prof.ctypes.data_as(vp), 16))
+            rc = int(L.pcabi_scan_profile(scan, 0, prof.ctypes.data_as(vp), 26))
         if rc < 0:
             _lib.check(rc, 'profile')
         stats.update(timed)
@@ -1467,9 +1467,12 @@ def middle_phase_roofline(prof):
     algorithmic unit, their roofline (one profiled step: every queued round synchronised on its own):
       k_seed_scan   HBM: every base of the round's reads once (u8 codes) + 16 B per raw seed hit written;
       k_seed_expand HBM: 16 B per raw hit read + 16 B per band task written;
-      candidate DP  VALU: cells (chunk columns x adapter rows) x OPS_PER_CELL int32 lane-ops.
-    The band classes exit early per task (data-dependent work): time and tasks only; k_cands, the
-    plan kernels and the rest (views, merges, masks: latency-bound launches): time only."""
+      candidate DP  VALU: cells (chunk columns x adapter rows) x OPS_PER_CELL int32 lane-ops;
+      bands         VALU: the pinned classes' band cells (active lane-rows x (2E + 1), counted by the
+                    profiled launches) x OPS_PER_CELL over the phase's time (which also holds the
+                    edge tasks' band_best launches beside them: a lower bound on the pinned kernels'
+                    own rate), and the lanes the passes kept busy.
+    k_cands, the plan kernels and the rest (views, merges, masks: latency-bound launches): time only."""
     names = ['k_seed_scan', 'k_seed_expand', 'bands', 'k_cands', 'plan', 'candidate_dp', 'rest']
     ms = {k: float(prof[i]) for i, k in enumerate(names)}
     rounds, reads, bases, raw, b_in, b_edge, dp_tasks, dp_cells = (int(x) for x in prof[7:15])
@@ -1488,6 +1491,19 @@ def middle_phase_roofline(prof):
                                          '1 B per base scanned + 16 B per raw hit written')
     out['roofline']['k_seed_expand'] = hbm(16 * raw + 16 * (b_in + b_edge), ms['k_seed_expand'],
                                            '16 B per raw hit read + 16 B per band task written')
+    if len(prof) >= 26 and ms['bands'] > 0:
+        band = [int(x) for x in prof[16:24]]
+        es = [int(x) for x in prof[24:26]]
+        cells = sum(band[4 * c + 1] * (2 * es[c] + 1) for c in range(2))
+        tops = cells * OPS_PER_CELL / (ms['bands'] * 1e-3) / 1e12
+        out['roofline']['bands'] = {
+            'bound': 'valu', 'achieved': round(tops, 3), 'peak': round(VALU_PEAK_TOPS, 1),
+            'unit': 'T int32 lane-ops/s', 'frac': round(tops / VALU_PEAK_TOPS, 4), 'band_cells': cells,
+            'per_unit': '%d ops per band cell; cells = active lane-rows x (2E + 1)' % OPS_PER_CELL,
+            'classes': [{'E': es[c], 'lane_rows_issued': band[4 * c], 'lane_rows_active': band[4 * c + 1],
+                         'lanes_busy': round(band[4 * c + 1] / max(1, band[4 * c]), 3), 'tasks': band[4 * c + 2],
+                         'rows_per_task': round(band[4 * c + 1] / max(1, band[4 * c + 2]), 2),
+                         'passes': band[4 * c + 3]} for c in range(2)]}
     if ms['candidate_dp'] > 0:
         tops = dp_cells * OPS_PER_CELL / (ms['candidate_dp'] * 1e-3) / 1e12
         out['roofline']['candidate_dp'] = {'bound': 'valu', 'achieved': round(tops, 3),

@@ -452,11 +452,12 @@ __global__ __launch_bounds__(256) void k_shadow_rebase(const int64_t *win_off, i
 // writes the task slots, the DP runs per bucket, and k_merge_* pick per candidate the first chunk
 // (read order) with the largest score, then per window the first adapter (list order) whose
 // full identity is not below the threshold -- the host path's rules (filtered_first_hits).
-constexpr int kPlanC = 4;   // chunk lengths 64 << c, c = 0..3
+constexpr int kPlanC = 5;     // chunk lengths kPlanMin << c, c = 0..4
+constexpr int kPlanMin = 32;  // (r05: 32-column chunks for the few whole reads a round certifies)
 
 __device__ __forceinline__ int plan_tasks(int len, int span, int c) {
     if (span < 0) return 1;                          // whole windows
-    const int C = 64 << c;
+    const int C = kPlanMin << c;
     return (len + C - 1) / C;                        // sf::chunk_plan's chunk count
 }
 
@@ -494,7 +495,7 @@ __global__ __launch_bounds__(256) void k_plan_count(const int64_t *cand, int64_t
         const int64_t key = i < ncl ? cand[i] : 0;
         const bool active = i < ncl && plan_valid(key, v_len, start) && (!cmask || cmask[i]);
         const int32_t a = active ? (int32_t)(key >> 32) : -1;
-        int nt[kPlanC] = {0, 0, 0, 0};
+        int nt[kPlanC] = {};
         if (active) {
             const int32_t k = (int32_t)(key & 0xFFFFFFFF);
 #pragma unroll
@@ -517,7 +518,7 @@ __global__ __launch_bounds__(256) void k_plan_count(const int64_t *cand, int64_t
 
 // Task slots: adapter a's tasks fill slots [wave_off[a] * 64, ...) in any order (a slot's result
 // depends only on its own task); idle slots keep task_win = -1. cidx[a]: the chunk length of a's
-// bucket (64 << cidx). nc_dev / slots_dev (device counts, nullptr: host values): the candidate
+// bucket (kPlanMin << cidx). nc_dev / slots_dev (device counts, nullptr: host values): the candidate
 // count, and the slots the layout holds (a task past them is not written: the layout overflowed).
 __global__ __launch_bounds__(256) void k_plan_place(const int64_t *cand, int64_t nc, const unsigned long long *nc_dev,
                                                     const int32_t *v_len, const int32_t *start, const int32_t *span,
@@ -559,7 +560,7 @@ __global__ __launch_bounds__(256) void k_plan_place(const int64_t *cand, int64_t
             continue;
         }
         if (!active) continue;
-        const int C = 64 << c;
+        const int C = kPlanMin << c;
         for (int t = 0; t < nt; ++t) {
             const int64_t q = base + t;
             if (q >= slots) break;
@@ -593,7 +594,7 @@ __global__ __launch_bounds__(256) void k_plan_fill(const int64_t *cand, int64_t 
         const int64_t key = cand[i];
         const int32_t a = (int32_t)(key >> 32), k = (int32_t)(key & 0xFFFFFFFF);
         const int n = v_len[k], D = span[a], c = cidx[a];
-        const int nt = plan_tasks(n, D, c), C = 64 << c;
+        const int nt = plan_tasks(n, D, c), C = kPlanMin << c;
         for (int t = lane; t < nt; t += 64) {
             const int64_t q = (int64_t)base + t;
             if (q >= slots) break;
@@ -1383,6 +1384,9 @@ void cert_bounds(State *s, std::vector<int32_t> &U);
 int debug_counts(State *s, int64_t (&out)[5], hipStream_t st);
 void profile_events(State *s, hipEvent_t *ev);
 int profile_counts(State *s, int64_t (&out)[3], hipStream_t st);
+int profile_band_stats(State *s, bool on);
+int band_stats(State *s, unsigned long long (&out)[8]);
+int band_e(State *s, int c);
 }  // namespace pcabi_seed
 
 // Per-phase profile of the device-resident middle scan (pcabi_scan_profile): events around the
@@ -1397,6 +1401,8 @@ struct MidProf {
     double ms[kPhases] = {};
     int64_t rounds = 0, reads = 0, bases = 0, raw = 0, band_in = 0, band_edge = 0, dp_tasks = 0, dp_cells = 0;
     double round1_ms = 0.0;                                        // round 1's runs (whole rounds)
+    // the pinned band classes' work: per class lane-rows issued, active lane-rows, tasks, passes
+    unsigned long long band[8] = {};
     hipEvent_t get() {
         if (used == pool.size()) {
             hipEvent_t e = nullptr;
@@ -2550,7 +2556,7 @@ int device_plan_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_off,
         }
         if (wa.size() == w_before) continue;
         nb_used.push_back(b);
-        nb_maxcols.push_back(bchunk[b] ? std::min<int32_t>(max_len, (64 << bc[b]) + bspan[b] + 1) : max_len);
+        nb_maxcols.push_back(bchunk[b] ? std::min<int32_t>(max_len, (kPlanMin << bc[b]) + bspan[b] + 1) : max_len);
         wave0.push_back((int64_t)w_before);
     }
     wave0.push_back((int64_t)wa.size());
@@ -2559,7 +2565,7 @@ int device_plan_hits(pcabi_scan *sc, const uint8_t *codes, const int64_t *v_off,
         std::string d;
         for (size_t k = 0; k < nb_used.size(); ++k)
             d += " rpl" + std::to_string(kBuckets[nb_used[k]].rpl) + ":" + std::to_string(wave0[k + 1] - wave0[k]) +
-                 "w/c" + std::to_string(64 << bc[nb_used[k]]);
+                 "w/c" + std::to_string(kPlanMin << bc[nb_used[k]]);
         std::fprintf(stderr, "[pcabi] middle device plan: %lld candidates, waves per bucket:%s\n", (long long)nc,
                      d.c_str());
     }
@@ -3229,10 +3235,14 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
             if (!pr_begin || !pr_seed[3]) return fail(PCABI_E_DEVICE, "profile events");
             HIP_TRY(hipEventRecord(pr_begin, st));
             pcabi_seed::profile_events(sc->seed, pr_seed);
+            if (int rc = pcabi_seed::profile_band_stats(sc->seed, true)) return rc;
         }
         struct SeedMarksOff {                          // the seed state never keeps this frame's events
             pcabi_seed::State *s;
-            ~SeedMarksOff() { pcabi_seed::profile_events(s, nullptr); }
+            ~SeedMarksOff() {
+                pcabi_seed::profile_events(s, nullptr);
+                (void)pcabi_seed::profile_band_stats(s, false);
+            }
         } seed_marks_off{sc->seed};
         auto pmark = [&](int phase, hipEvent_t from) -> hipEvent_t {   // a span from `from` to now
             if (!pf_.on) return nullptr;
@@ -3285,8 +3295,12 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
             else
                 hipLaunchKernelGGL(k_plan_count, dim3(kGrid), dim3(256), 0, st, dcand, ncap, dcount, v_len, start,
                                    (const int32_t *)sc->pspan.p, (int32_t *)sc->ptasks.p, cmask);
+            // the flagged candidates' whole reads (cmask): half the wave target, so their chunks are
+            // 64 columns rather than 32 at a few hundred reads -- the lead-in (the adapter's span) is
+            // recomputed per chunk (r05q: 20 kb 3.21-3.27 -> 3.13-3.22 ms; 8 kb keeps 4096)
             hipLaunchKernelGGL(k_plan_layout, dim3(1), dim3(256), 0, st, (const int32_t *)sc->ptasks.p, n_bk, d_bk_first,
-                               d_bk_adp, d_bk_local, target, slots_cap, (int32_t *)sc->pcidx.p, (int64_t *)sc->pwoff.p,
+                               d_bk_adp, d_bk_local, cmask ? std::max<int64_t>(1, target / 2) : target, slots_cap,
+                               (int32_t *)sc->pcidx.p, (int64_t *)sc->pwoff.p,
                                (int32_t *)pl.wa->p, (int32_t *)pl.tw->p, pl.bk_waves, pl.slots, d_pflag, pl.need);
             if (win) {
                 hipLaunchKernelGGL(k_wplan_place, dim3(kGrid), dim3(256), 0, st, vlist, vcount, vcap, v_off, v_len, start,
@@ -3407,11 +3421,31 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
                          "%lld candidates, %lld task slots, %d hits\n", (long long)(round_base + r), rn[0],
                          (long long)c[0], (long long)c[1], (long long)c[2], (long long)c[3], (long long)c[4],
                          (long long)sl, rn[1]);
+            if (windows) {                           // the certificate's flagged candidates, their plan
+                std::vector<int32_t> fl((size_t)std::max<int64_t>(1, std::min<int64_t>(c[4], ncap)));
+                HIP_TRY(hipMemcpy(fl.data(), sc->pcert.p, 4 * fl.size(), hipMemcpyDeviceToHost));
+                int64_t nf = 0, sl2 = 0;
+                for (int32_t x : fl) nf += x != 0;
+                HIP_TRY(hipMemcpy(&sl2, d_slots2, 8, hipMemcpyDeviceToHost));
+                std::vector<int32_t> bw(2 * (size_t)n_bk), bw2(2 * (size_t)n_bk);
+                HIP_TRY(hipMemcpy(bw.data(), d_bk_waves, 4 * bw.size(), hipMemcpyDeviceToHost));
+                HIP_TRY(hipMemcpy(bw2.data(), d_bk_waves2, 4 * bw2.size(), hipMemcpyDeviceToHost));
+                std::string w1, w2;
+                for (int b = 0; b < n_bk; ++b) {
+                    w1 += " " + std::to_string(bw[2 * b + 1]);
+                    w2 += " " + std::to_string(bw2[2 * b + 1]);
+                }
+                std::fprintf(stderr, "[pcabi]   windows plan waves per bucket:%s; %lld flagged, whole-read plan %lld slots, "
+                             "waves per bucket:%s\n", w1.c_str(), (long long)nf, (long long)sl2, w2.c_str());
+            }
         }
         if (pf_.on) {                                // the round on its own: its spans and counters
             const hipEvent_t pr_end = pmark(-1, nullptr);
             int64_t cnt[3] = {};
             if (int rc = pcabi_seed::profile_counts(sc->seed, cnt, st)) return rc;   // (synchronises st)
+            unsigned long long bst[8];
+            if (int rc = pcabi_seed::band_stats(sc->seed, bst)) return rc;
+            for (int i = 0; i < 8; ++i) pf_.band[i] += bst[i];
             unsigned long long u[4] = {};
             HIP_TRY(hipMemcpy(u, sc->pprof.p, sizeof(u), hipMemcpyDeviceToHost));
             float tot = 0.f;
@@ -3590,15 +3624,21 @@ int32_t pcabi_scan_profile(pcabi_scan *s, int32_t mode, double *out, int32_t n_o
         std::fill(p.ms, p.ms + kPhases, 0.0);
         p.rounds = p.reads = p.bases = p.raw = p.band_in = p.band_edge = p.dp_tasks = p.dp_cells = 0;
         p.round1_ms = 0.0;
+        std::fill(p.band, p.band + 8, 0ull);
     }
     if (mode != 2) p.on = mode == 1;
-    const double v[kPhases + 9] = {p.ms[0], p.ms[1], p.ms[2], p.ms[3], p.ms[4], p.ms[5], p.ms[6],
-                                   (double)p.rounds, (double)p.reads, (double)p.bases, (double)p.raw,
-                                   (double)p.band_in, (double)p.band_edge, (double)p.dp_tasks, (double)p.dp_cells,
-                                   p.round1_ms};
-    const int32_t k = std::min<int32_t>(n_out, kPhases + 9);
+    const int32_t nv = kPhases + 9 + 8 + 2;
+    const double v[nv] = {p.ms[0], p.ms[1], p.ms[2], p.ms[3], p.ms[4], p.ms[5], p.ms[6],
+                          (double)p.rounds, (double)p.reads, (double)p.bases, (double)p.raw,
+                          (double)p.band_in, (double)p.band_edge, (double)p.dp_tasks, (double)p.dp_cells,
+                          p.round1_ms,
+                          (double)p.band[0], (double)p.band[1], (double)p.band[2], (double)p.band[3],
+                          (double)p.band[4], (double)p.band[5], (double)p.band[6], (double)p.band[7],
+                          (double)(s->seed ? pcabi_seed::band_e(s->seed, 0) : 0),
+                          (double)(s->seed ? pcabi_seed::band_e(s->seed, 1) : 0)};
+    const int32_t k = std::min<int32_t>(n_out, nv);
     for (int32_t i = 0; i < k; ++i) out[i] = v[i];
-    return kPhases + 9;
+    return nv;
 }
 
 int64_t pcabi_middle_requeues(int32_t *flags_seen) {

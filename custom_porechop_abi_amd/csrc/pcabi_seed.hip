@@ -90,6 +90,7 @@ constexpr int kFlag = 2 * kCls;
 constexpr int kVer = kCnt;          // the verified-seed counter, after the task counters and flags
 constexpr int kCntAll = kCnt + 1;   // every counter k_bound_reset zeroes
 constexpr int kPinMaxE = 8;        // the pinned band is built for E <= kPinMaxE
+constexpr int kStatBlocks = 8192;  // profiled band launches: per-wave counter slots for this many blocks
 
 struct ScanArgs {
     const uint8_t *codes;
@@ -1098,17 +1099,18 @@ __global__ __launch_bounds__(256) void k_seed_band(const int4 *task, const int32
 // lane the range of the NEXT task is loaded (uint4 loads) while the current task computes, then
 // copied to the lane's LDS slot (NC4 x 16 bytes), where the rows read their one new byte each: the
 // row loop touches no global memory, so no wait of the loop is a memory latency.
-#ifdef PCABI_BAND_STATS
-// (experiments, -DPCABI_BAND_STATS) per band kernel class (E): row iterations x 64 lanes, active
-// lane-rows, tasks, passes -- the lanes a pass leaves idle behind its longest task
-__device__ unsigned long long g_band_stats[2][4];
-#endif
-
-template <int E, int NC4>
+//
+// STATS (the profiled launches of pcabi_scan_profile only): per wave, row iterations x 64 lanes,
+// active lane-rows (the band cells computed: x (2E + 1)), tasks and passes, added to the wave's own
+// four counters stats[4 * (block * 4 + wave) ..] at its end (plain stores: same-address atomics from
+// every pass serialise at the L2 and cost more than the bands, r05l) -- the roofline's work and the
+// lanes a pass leaves idle behind its longest task.
+template <int E, int NC4, bool STATS>
 __global__ __launch_bounds__(256) void k_seed_band_pin(const int4 *task, const int32_t *n_task, int64_t cap,
                                                        const uint8_t *codes, const uint8_t *adp, int32_t adp_dw,
                                                        const int32_t *adp_off, const int32_t *adp_meta, int32_t n_adp,
-                                                       pcabi::Scoring sc, int32_t *bound, int64_t n, VerOut vo) {
+                                                       pcabi::Scoring sc, int32_t *bound, int64_t n, VerOut vo,
+                                                       unsigned long long *stats) {
     constexpr int W = 2 * E + 1;
     extern __shared__ uint4 lds4[];
     uint32_t *lds = reinterpret_cast<uint32_t *>(lds4);
@@ -1159,6 +1161,7 @@ __global__ __launch_bounds__(256) void k_seed_band_pin(const int4 *task, const i
     if (vA) load_range();
     if (t < nt) { recB = task[t]; vB = true; t += stride; }
     auto pin_start = [&](int x) -> int { return x == E ? 0 : (x > E ? go + (x - E - 1) * ge : kNeg); };
+    unsigned long long st_it = 0, st_act = 0, st_tasks = 0, st_pass = 0;
     while (__any(vA)) {                               // one task per lane and pass
         bool active = vA;
         int4 rc = recA;
@@ -1177,9 +1180,7 @@ __global__ __launch_bounds__(256) void k_seed_band_pin(const int4 *task, const i
             t += stride;
         }
         // ---- this task
-#ifdef PCABI_BAND_STATS
         const bool vA_was = active;
-#endif
         const int a = rc.y >> 11, o = rc.y & 255, K = kMinK + ((rc.y >> 8) & 7);
         const uint32_t meta = (uint32_t)ameta[a];
         const int L = (int)(meta & 255u), T = (int)(meta >> 12);
@@ -1227,15 +1228,15 @@ __global__ __launch_bounds__(256) void k_seed_band_pin(const int4 *task, const i
             }
         }
         if (vo.list) put_verified(vo, ver, rc.x, a, E, dabs);
-#ifdef PCABI_BAND_STATS
-        unsigned long long st_it = 0, st_act = 0;
-        const unsigned long long st_tasks = __popcll(__ballot(rc.x >= 0 && vA_was));
-#endif
+        if constexpr (STATS) {
+            st_tasks += __popcll(__ballot(vA_was));
+            st_pass += 1;
+        }
         while (__any(active)) {
-#ifdef PCABI_BAND_STATS
-            st_it += 64;
-            st_act += __popcll(__ballot(active));
-#endif
+            if constexpr (STATS) {
+                st_it += 64;
+                st_act += __popcll(__ballot(active));
+            }
             ver = false;
             if (active) {
                 const int ab = ad[apos];
@@ -1276,264 +1277,16 @@ __global__ __launch_bounds__(256) void k_seed_band_pin(const int4 *task, const i
             }
             if (vo.list) put_verified(vo, ver, rc.x, a, E, dabs);
         }
-#ifdef PCABI_BAND_STATS
+    }
+    if constexpr (STATS) {
         if ((threadIdx.x & 63) == 0) {
-            atomicAdd(&g_band_stats[E > 2][0], st_it);
-            atomicAdd(&g_band_stats[E > 2][1], st_act);
-            atomicAdd(&g_band_stats[E > 2][2], st_tasks);
-            atomicAdd(&g_band_stats[E > 2][3], 1ull);
+            unsigned long long *w = stats + 4 * ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6));
+            w[0] += st_it;
+            w[1] += st_act;
+            w[2] += st_tasks;
+            w[3] += st_pass;
         }
-#endif
     }
-}
-
-// k_seed_band_pin_sw (r05): the same tasks, bounds and verified seeds as k_seed_band_pin, with the
-// lanes of a wave switching tasks independently and taking them from a shared counter.
-// k_seed_band_pin gives lane l of the persistent grid the tasks l, l + stride, ... (~10 per lane at
-// 20 kb) and runs one task per lane and PASS, a pass as long as its longest task: a random probe
-// hit's band usually exits within a few rows, so half of the lane-rows idle (tools/band_stats.py:
-// 0.47-0.53 active, r05j). Here each block owns a contiguous range of the tasks (~2.5 k at 20 kb,
-// so the blocks' totals differ little) behind an LDS counter; the row loop runs until the block's
-// counter is exhausted; a lane whose task ended starts its next one as soon as kRefill lanes wait
-// (or none runs), and the waiting lanes take new tasks with one LDS atomic per wave (one global
-// counter measured 10x slower: same-address atomics serialise at the L2). Per lane a three-deep
-// pipeline keeps every memory latency off the refill: the next task with its read bytes loaded (A),
-// the one after with its record loaded (B) and an index (C); a grab's answer is read at the next
-// refill.
-constexpr int kRefill = 16;
-
-template <int E, int NC4>
-__global__ __launch_bounds__(256) void k_seed_band_pin_sw(const int4 *task, const int32_t *n_task, int64_t cap,
-                                                          const uint8_t *codes, const uint8_t *adp, int32_t adp_dw,
-                                                          const int32_t *adp_off, const int32_t *adp_meta, int32_t n_adp,
-                                                          pcabi::Scoring sc, int32_t *bound, int64_t n, VerOut vo) {
-    constexpr int W = 2 * E + 1;
-    extern __shared__ uint4 lds4[];
-    __shared__ int32_t s_next;                          // the block's task counter
-    uint32_t *lds = reinterpret_cast<uint32_t *>(lds4);
-    const int64_t nt_all = min((int64_t)*n_task, cap);
-    const int64_t per = (nt_all + gridDim.x - 1) / gridDim.x;
-    const int64_t blo = min(nt_all, (int64_t)blockIdx.x * per);
-    if (threadIdx.x == 0) s_next = (int32_t)blo;
-    int32_t *next = &s_next;
-    for (int i = threadIdx.x; i < adp_dw; i += 256) lds[i] = reinterpret_cast<const uint32_t *>(adp)[i];
-    for (int i = threadIdx.x; i < n_adp; i += 256) {
-        lds[adp_dw + i] = (uint32_t)adp_off[i];
-        lds[adp_dw + n_adp + i] = (uint32_t)adp_meta[i];
-    }
-    __syncthreads();
-    const uint8_t *ad = reinterpret_cast<const uint8_t *>(lds);
-    const int32_t *aoffs = reinterpret_cast<const int32_t *>(lds + adp_dw);
-    const int32_t *ameta = aoffs + n_adp;
-    uint4 *slot4 = lds4 + ((adp_dw + 2 * n_adp + 3) >> 2) + (int)threadIdx.x * NC4;
-    const uint8_t *slot = reinterpret_cast<const uint8_t *>(slot4);
-    const int64_t nt = min(nt_all, blo + per);         // the end of the block's range
-    const int lane = (int)(threadIdx.x & 63);
-    const uint64_t lt = (1ull << lane) - 1;
-    const int bs = pcabi::best_sub(sc), ma = sc.ma, mi = sc.mi, go = sc.go, ge = sc.ge;
-    const uintptr_t lo_addr = (uintptr_t)codes & ~(uintptr_t)15;
-    auto range_of = [&](const int4 &rc, uintptr_t &cb, int &nld) {   // as k_seed_band_pin
-        const int a = rc.y >> 11, o = rc.y & 255;
-        const int L = (int)((uint32_t)ameta[a] & 255u);
-        const uintptr_t pa = (uintptr_t)codes + (uintptr_t)(((uint64_t)(uint32_t)rc.w << 32) | (uint32_t)rc.z);
-        const uintptr_t lo = pa - (uintptr_t)(o + E), hi = pa - (uintptr_t)o + (uintptr_t)(L + E);
-        cb = lo & ~(uintptr_t)15;
-        if (pa >= lo_addr && cb < lo_addr) cb = lo_addr;
-        nld = (int)((hi - cb + 15) >> 4);
-    };
-    int4 recA = make_int4(0, 0, 0, 0), recB = recA;
-    bool vA = false, vB = false, vC = false;
-    int32_t idxC = 0;
-    uint4 chA[NC4];
-    uintptr_t cbA = lo_addr;
-    auto load_range = [&]() {
-        int nld = 0;
-        range_of(recA, cbA, nld);
-#pragma unroll
-        for (int k = 0; k < NC4; ++k)
-            chA[k] = k < nld ? *reinterpret_cast<const uint4 *>(cbA + 16 * (uintptr_t)k) : make_uint4(0u, 0u, 0u, 0u);
-    };
-    // the wave's outstanding grab: the leader lane's atomic answer, read at the next refill by the
-    // lanes it was for (pend = member, pre = the lane's place among them)
-    int32_t pendB0 = 0;
-    int pendLeader = -1;
-    bool pend = false;
-    int pre = 0;
-    auto grab_now = [&]() -> int32_t {                 // every lane: one index each (start-up)
-        int32_t b0 = 0;
-        if (lane == 0) b0 = atomicAdd(next, 64);
-        return __shfl(b0, 0) + lane;
-    };
-    {
-        const int32_t ia = grab_now(), ib = grab_now(), ic = grab_now();
-        vA = ia < nt;
-        if (vA) {
-            recA = task[ia];
-            load_range();
-        }
-        vB = ib < nt;
-        if (vB) recB = task[ib];
-        vC = ic < nt;
-        idxC = ic;
-    }
-    auto pin_start = [&](int x) -> int { return x == E ? 0 : (x > E ? go + (x - E - 1) * ge : kNeg); };
-    bool active = false;
-    int4 rc = make_int4(0, 0, 0, 0);
-    int a = 0, o = 0, T = 0, aoff = 0, base = 0, pin = 0;
-    int64_t bidx = 0, dabs = 0;
-    int S[W], V[W], R[W];
-#pragma unroll
-    for (int x = 0; x < W; ++x) S[x] = V[x] = R[x] = 0;
-    int phase = 0, rows = 0, other = 0, mx = 0, apos = 0, adir = 1, bpos = 0, bdir = 1;
-#ifdef PCABI_BAND_STATS
-    unsigned long long st_it = 0, st_act = 0, st_tasks = 0, st_refill = 0;
-#endif
-    auto begin_prefix = [&]() {                        // rows o .. 1 backwards, mirrored band
-        phase = 1;
-        rows = o;
-        other = pin + mx;
-        mx = 0;
-#pragma unroll
-        for (int x = 0; x < W; ++x) {
-            S[x] = pin_start(x);
-            V[x] = kNeg;
-            R[x] = slot[base - 1 + E - x];
-        }
-        bpos = base - 2 - E;
-        bdir = -1;
-        apos = aoff + o - 1;
-        adir = -1;
-    };
-    for (;;) {                                         // wave-uniform exits
-        const uint64_t can = __ballot(!active && vA);
-        const uint64_t run = __ballot(active);
-        if (!can && !run) break;
-        bool ver = false;
-        if (can && (!run || __popcll(can) >= kRefill)) {
-#ifdef PCABI_BAND_STATS
-            st_refill += 1;
-            st_tasks += __popcll(can);
-#endif
-            // the previous grab's answer, to the lanes it was for
-            if (pendLeader >= 0) {
-                const int32_t b0 = __shfl(pendB0, pendLeader);
-                if (pend) {
-                    idxC = b0 + pre;
-                    vC = idxC < nt;
-                    pend = false;
-                }
-            }
-            const bool me = !active && vA;
-            if (me) {                                  // this lane starts task A; A <- B <- C
-#pragma unroll
-                for (int k = 0; k < NC4; ++k) slot4[k] = chA[k];
-                rc = recA;
-                const uintptr_t cb = cbA;
-                vA = vB;
-                recA = recB;
-                if (vA) load_range();
-                vB = vC;
-                if (vB) recB = task[idxC];
-                vC = false;
-                a = rc.y >> 11;
-                o = rc.y & 255;
-                const int K = kMinK + ((rc.y >> 8) & 7);
-                const uint32_t meta = (uint32_t)ameta[a];
-                const int L = (int)(meta & 255u);
-                T = (int)(meta >> 12);
-                aoff = aoffs[a];
-                bidx = (int64_t)a * n + rc.x;
-                const uintptr_t pa = (uintptr_t)codes + (uintptr_t)(((uint64_t)(uint32_t)rc.w << 32) | (uint32_t)rc.z);
-                base = (int)(pa - cb);
-                pin = ma * K;
-                phase = 0;
-                rows = L - o - K;
-                other = pin + bs * o;
-                mx = 0;
-                apos = aoff + o + K;
-                adir = 1;
-                bpos = base + K + E + 1;
-                bdir = 1;
-#pragma unroll
-                for (int x = 0; x < W; ++x) {
-                    S[x] = pin_start(x);
-                    V[x] = kNeg;
-                    R[x] = slot[base + K + x - E];
-                }
-                dabs = (int64_t)(((uint64_t)(uint32_t)rc.w << 32) | (uint32_t)rc.z) - o;
-                active = true;
-                if (rows == 0) {                       // the run ends the adapter: Q = 0
-                    if (o == 0) {
-                        atomicMax(&bound[bidx], pin);
-                        ver = pin >= T;
-                        active = false;
-                    } else {
-                        begin_prefix();
-                    }
-                }
-            }
-            // a new index for every lane that used its C (read at the next refill)
-            const uint64_t want = __ballot(me);
-            pendLeader = -1;
-            if (want) {
-                const int leader = __ffsll((unsigned long long)want) - 1;
-                if (lane == leader) pendB0 = atomicAdd(next, __popcll(want));
-                pendLeader = leader;
-                pend = me;
-                pre = __popcll(want & lt);
-            }
-        }
-#ifdef PCABI_BAND_STATS
-        st_it += 64;
-        st_act += __popcll(__ballot(active));
-#endif
-        if (active) {
-            const int ab = ad[apos];
-            apos += adir;
-            const int nb = slot[bpos];
-            bpos += bdir;
-            int h = kNeg, sl = kNeg;
-#pragma unroll
-            for (int x = 0; x < W; ++x) {
-                const int dg = S[x] + (R[x] == ab ? ma : mi);
-                const int vu = (x + 1 < W) ? max(V[x + 1] + ge, S[x + 1] + go) : kNeg;
-                h = max(h + ge, sl + go);
-                const int sv = max(dg, max(vu, h));
-                S[x] = sv;
-                V[x] = vu;
-                sl = sv;
-            }
-#pragma unroll
-            for (int x = 0; x + 1 < W; ++x) R[x] = R[x + 1];
-            R[W - 1] = nb;
-            --rows;
-            mx = S[0];
-#pragma unroll
-            for (int x = 1; x < W; ++x) mx = max(mx, S[x]);
-            const int ub = mx + bs * rows + other;
-            if (ub < T) {
-                atomicMax(&bound[bidx], ub);
-                active = false;
-            } else if (rows == 0) {
-                if (phase == 0 && o > 0) {
-                    begin_prefix();
-                } else {
-                    atomicMax(&bound[bidx], mx + other);
-                    ver = mx + other >= T;
-                    active = false;
-                }
-            }
-        }
-        if (vo.list) put_verified(vo, ver, rc.x, a, E, dabs);
-    }
-#ifdef PCABI_BAND_STATS
-    if (lane == 0) {
-        atomicAdd(&g_band_stats[E > 2][0], st_it);
-        atomicAdd(&g_band_stats[E > 2][1], st_act);
-        atomicAdd(&g_band_stats[E > 2][2], st_tasks);
-        atomicAdd(&g_band_stats[E > 2][3], st_refill);
-    }
-#endif
 }
 
 // The pairs whose bound reaches their adapter's threshold T[a], as (a << 32 | read) keys
@@ -1643,6 +1396,8 @@ struct State {
                                                   // and / or 1 inside task per class (2), see shrink_next()
     bool serial = false;                          // the next seeding's band launches all on the caller's stream
     hipEvent_t *pev = nullptr;                    // profile (profile_events): 4 marks recorded on the caller's stream
+    bool bstats_on = false;                       // profile (profile_band_stats): the pinned bands count their work
+    Buf bstats;                                   //   into 2 classes x (lane-rows issued, active, tasks, passes)
     VerOut ver{nullptr, nullptr, nullptr, 0};     // the band launches' record target (list nullptr: off)
 };
 
@@ -1863,31 +1618,26 @@ template <int E, int NC4>
 int launch_pin(State *s, int c, const int4 *task, const uint8_t *codes, const pcabi::Scoring &sc, int64_t n,
                int64_t n_in, hipStream_t st) {
     const size_t lds = 16 * (((size_t)s->adp_bytes / 4 + 2 * (size_t)s->n_adp + 3) / 4) + 16 * 256 * (size_t)NC4;
-    // PCABI_BAND_SWITCH=1: lanes switch tasks alone (k_seed_band_pin_sw, an A/B: no faster, r05j)
-    static const bool sw = [] {
-        const char *e = std::getenv("PCABI_BAND_SWITCH");
-        return e && e[0] == '1';
-    }();
     if (!s->pin_blocks[c]) {
         int dev = 0, cus = 0, per_cu = 0;
         SD_TRY(hipGetDevice(&dev));
         SD_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        if (sw) SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_band_pin_sw<E, NC4>, 256, lds));
-        else SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_band_pin<E, NC4>, 256, lds));
+        SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_band_pin<E, NC4, false>, 256, lds));
         s->pin_blocks[c] = std::max(1, cus * std::max(1, per_cu));
     }
     const int64_t blocks = n_in >= 0 ? std::max<int64_t>(1, std::min<int64_t>((n_in + 255) / 256, s->pin_blocks[c]))
                                      : s->pin_blocks[c];
-    if (sw)
-        hipLaunchKernelGGL((k_seed_band_pin_sw<E, NC4>), dim3((unsigned)blocks), dim3(256), lds, st, task,
+    if (s->bstats_on && blocks <= kStatBlocks)       // a profiled round (pcabi_scan_profile)
+        hipLaunchKernelGGL((k_seed_band_pin<E, NC4, true>), dim3((unsigned)blocks), dim3(256), lds, st, task,
                            (const int32_t *)s->cnt.p + c, s->cap, codes, (const uint8_t *)s->adp.p, s->adp_bytes / 4,
                            (const int32_t *)s->adp_off.p, (const int32_t *)s->adp_meta.p, s->n_adp, sc,
-                           (int32_t *)s->bound.p, n, s->ver);
+                           (int32_t *)s->bound.p, n, s->ver,
+                           (unsigned long long *)s->bstats.p + (size_t)c * 4 * 4 * kStatBlocks);
     else
-        hipLaunchKernelGGL((k_seed_band_pin<E, NC4>), dim3((unsigned)blocks), dim3(256), lds, st, task,
+        hipLaunchKernelGGL((k_seed_band_pin<E, NC4, false>), dim3((unsigned)blocks), dim3(256), lds, st, task,
                            (const int32_t *)s->cnt.p + c, s->cap, codes, (const uint8_t *)s->adp.p, s->adp_bytes / 4,
                            (const int32_t *)s->adp_off.p, (const int32_t *)s->adp_meta.p, s->n_adp, sc,
-                           (int32_t *)s->bound.p, n, s->ver);
+                           (int32_t *)s->bound.p, n, s->ver, nullptr);
     return 0;
 }
 
@@ -2282,6 +2032,30 @@ void serial_next(State *s) { s->serial = true; }
 // ev[2] after k_seed_expand and ev[3] after the band classes (nullptr: off).
 void profile_events(State *s, hipEvent_t *ev) { s->pev = ev; }
 
+// Profiling: the pinned band classes count their work while on (k_seed_band_pin<..., true>); on
+// zeroes the counters. band_stats reads them: per class lane-rows issued, active, tasks, passes.
+int profile_band_stats(State *s, bool on) {
+    s->bstats_on = false;
+    if (!on) return 0;
+    const size_t bytes = sizeof(unsigned long long) * kCls * 4 * 4 * kStatBlocks;
+    if (int rc = s->bstats.ensure(bytes)) return rc;
+    SD_TRY(hipMemset(s->bstats.p, 0, bytes));
+    s->bstats_on = true;
+    return 0;
+}
+
+// The band half-width E of class c (0 before a plan).
+int band_e(State *s, int c) { return (c >= 0 && c < kCls) ? s->band[c] : 0; }
+
+int band_stats(State *s, unsigned long long (&out)[8]) {
+    std::fill(out, out + 8, 0ull);
+    if (!s->bstats.p) return 0;
+    std::vector<unsigned long long> w((size_t)kCls * 4 * 4 * kStatBlocks);
+    SD_TRY(hipMemcpy(w.data(), s->bstats.p, 8 * w.size(), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < w.size(); ++i) out[4 * (i / (4 * 4 * kStatBlocks)) + i % 4] += w[i];
+    return 0;
+}
+
 // Profiling: the last seeding's raw hits (slabs, clamped), inside and edge band tasks (synchronises `st`).
 int profile_counts(State *s, int64_t (&out)[3], hipStream_t st) {
     std::vector<int32_t> raw((size_t)std::max(1, s->n_slab));
@@ -2339,20 +2113,3 @@ int plan_ready(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32
 
 extern "C" int64_t pcabi_middle_seed_runs(void) { return pcabi_seed::g_runs.load(); }
 
-// Experiments only (not in include/pcabi.h): the band statistics of a -DPCABI_BAND_STATS build,
-// out[2][4] (see g_band_stats); -1 without the flag. reset != 0 zeroes them afterwards.
-extern "C" int pcabi_debug_band_stats(unsigned long long *out, int reset) {
-#ifdef PCABI_BAND_STATS
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pcabi_seed::g_band_stats), sizeof(unsigned long long) * 8) != hipSuccess)
-        return -2;
-    if (reset) {
-        unsigned long long z[8] = {};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(pcabi_seed::g_band_stats), z, sizeof(z)) != hipSuccess) return -2;
-    }
-    return 0;
-#else
-    (void)out;
-    (void)reset;
-    return -1;
-#endif
-}

@@ -243,8 +243,10 @@ class FileTrimmer(object):
         if self.barcode_dir is not None:
             os.makedirs(self.barcode_dir, exist_ok=True)
             counts['bins'] = bins
-        pq = queue.Queue(maxsize=2)
-        wq = queue.Queue(maxsize=2)
+        # batches parsed ahead / trimmed and waiting for the writer (PCABI_PIPE_DEPTH, default 2)
+        depth = max(1, int(os.environ.get('PCABI_PIPE_DEPTH', '2')))
+        pq = queue.Queue(maxsize=depth)
+        wq = queue.Queue(maxsize=depth)
         errors = []
         stop = threading.Event()          # set when this thread leaves: the reader stops putting
 

@@ -334,7 +334,10 @@ int pcabi_first_hit_dev(const int32_t *res, int64_t stride, int64_t n_win, int32
  *                                 the plan kernels, the candidate DP, the rest; then rounds, reads,
  *                                 bases scanned, raw seed hits, inside / edge band tasks, candidate-DP
  *                                 tasks and cells (columns x adapter rows); out[15] = ms of round 1
- *                                 (its runs, whole). Returns 16 or < 0.
+ *                                 (its runs, whole); out[16..23] per band class (2) the pinned bands'
+ *                                 lane-rows issued, active lane-rows (x (2E + 1) = band cells), tasks
+ *                                 and passes (counted by the profiled launches only); out[24..25]
+ *                                 the classes' E. Returns 26 or < 0.
  */
 typedef struct pcabi_scan pcabi_scan;
 int pcabi_scan_create(const pcabi_adapters *adps, pcabi_scan **out);

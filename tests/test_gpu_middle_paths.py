@@ -75,7 +75,7 @@ def _sorted(h):
 def _dev_scan(L, views, adps, sc, thr, profile=None, calls=1, intact=None):
     """A FRESH scan through the device ABI (pcabi_adapters_create_scored, pcabi_scan_create,
     pcabi_middle_scan_dev): its buffers are sized on this first use (PCABI_MIDDLE_INIT_CAPS).
-    profile: a float64 array of 16 that receives pcabi_scan_profile's table of the call.
+    profile: a float64 array of 26 that receives pcabi_scan_profile's table of the call.
     calls: scans of the same device pack with the same scan object (every call's hits must agree);
     intact: a list that receives, per call, whether the device pack is byte-identical afterwards."""
     from custom_porechop_abi_amd import _lib, engine
@@ -102,7 +102,7 @@ def _dev_scan(L, views, adps, sc, thr, profile=None, calls=1, intact=None):
         hits = np.zeros((6, cap), np.int32)
         h_len = np.ascontiguousarray(lens, np.int32)
         if profile is not None:
-            assert L.pcabi_scan_profile(scan, 1, None, 0) == 16
+            assert L.pcabi_scan_profile(scan, 1, None, 0) == 26
         first = None
         for _ in range(calls):
             hits[:] = 0
@@ -122,7 +122,7 @@ def _dev_scan(L, views, adps, sc, thr, profile=None, calls=1, intact=None):
             else:
                 assert np.array_equal(got, first), 'a second scan of the same pack differs'
         if profile is not None:
-            assert L.pcabi_scan_profile(scan, 0, profile.ctypes.data_as(vp), 16) == 16
+            assert L.pcabi_scan_profile(scan, 0, profile.ctypes.data_as(vp), 26) == 26
         return first
     finally:
         if scan.value:
@@ -293,7 +293,7 @@ def test_seed_scan_bytemap_equals_bitmap_scan(gpu_lib, monkeypatch, thr):
     prof, got = {}, {}
     for mode in ('1', '0'):
         monkeypatch.setenv('PCABI_SEED_BYTEMAP', mode)
-        prof[mode] = np.zeros(16, np.float64)
+        prof[mode] = np.zeros(26, np.float64)
         got[mode] = _dev_scan(gpu_lib, views, ADPS, SC, thr, profile=prof[mode])
     for mode in ('0', '1'):
         assert np.array_equal(_sorted(got[mode]), exp), ('bytemap=%s' % mode, prof[mode][7:15], prof['0'][7:15])
@@ -325,7 +325,7 @@ def test_seed_expand_one_pass(gpu_lib, monkeypatch, thr):
     prof = {}
     for mode in ('2', '1'):
         monkeypatch.setenv('PCABI_EXPAND_PASSES', mode)
-        prof[mode] = np.zeros(16, np.float64)
+        prof[mode] = np.zeros(26, np.float64)
         got = _dev_scan(gpu_lib, views, ADPS, SC, thr, profile=prof[mode])
         assert np.array_equal(_sorted(got), exp), 'passes=%s' % mode
     assert prof['1'][11] > 0
@@ -333,7 +333,7 @@ def test_seed_expand_one_pass(gpu_lib, monkeypatch, thr):
     # a grid of 8 blocks: hundreds of slabs per block, in several groups of kExpandGroup
     monkeypatch.setenv('PCABI_EXPAND_PASSES', '1')
     monkeypatch.setenv('PCABI_EXPAND_BLOCKS', '8')
-    prof['g'] = np.zeros(16, np.float64)
+    prof['g'] = np.zeros(26, np.float64)
     got = _dev_scan(gpu_lib, views, ADPS, SC, thr, profile=prof['g'])
     assert np.array_equal(_sorted(got), exp), 'passes=1, 8 blocks'
     assert np.array_equal(prof['g'][7:15], prof['2'][7:15]), (prof['g'][7:15], prof['2'][7:15])
