@@ -1675,14 +1675,16 @@ def run_kmer(args, rank, world, dist, torch, L, _lib, synth):
 def write_probe(path, nbytes, repeat):
     """The output file system's write ceiling for the e2e output: nbytes from one contiguous,
     already faulted-in buffer through write() calls of 256 MB (the page-cache copy the trimmed-read
-    writer also pays). 'burst': one file of nbytes, best of three; 'sustained': `repeat` files of
-    nbytes back to back, each truncating the last as the timed e2e steps do (dirty-page writeback
-    and throttling included). The e2e writer's busy time is compared against these."""
+    writer also pays). 'burst': one fresh file of nbytes, best of three; 'sustained': `repeat` fresh
+    files of nbytes back to back, as the timed e2e steps write them (dirty-page writeback and
+    throttling included); 'rewrite': `repeat` writes of one path, each truncating the last (what the
+    steps did through r05's first records: the truncation frees the previous file's cached pages).
+    The e2e writer's busy time is compared against these."""
     buf = np.full(min(nbytes, 256 << 20), 65, np.uint8)
     mv = memoryview(buf)
 
-    def one():
-        fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    def one(p):
+        fd = os.open(p, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
         left = nbytes
         while left > 0:
             left -= os.write(fd, mv[:min(left, len(buf))])
@@ -1691,18 +1693,25 @@ def write_probe(path, nbytes, repeat):
     best = None
     for _ in range(3):
         t0 = time.perf_counter()
-        one()
+        one(path)
         dt = time.perf_counter() - t0
         best = dt if best is None else min(best, dt)
         os.remove(path)
     t0 = time.perf_counter()
-    for _ in range(repeat):
-        one()
+    for k in range(repeat):
+        one('%s.%d' % (path, k))
     sus = (time.perf_counter() - t0) / repeat
+    for k in range(repeat):
+        os.remove('%s.%d' % (path, k))
+    t0 = time.perf_counter()
+    for _ in range(repeat):
+        one(path)
+    rew = (time.perf_counter() - t0) / repeat
     os.remove(path)
     return {'bytes': int(nbytes), 'burst_ms': round(1e3 * best, 2), 'burst_GB_per_s': round(nbytes / best / 1e9, 2),
             'sustained_ms': round(1e3 * sus, 2), 'sustained_GB_per_s': round(nbytes / sus / 1e9, 2),
-            'sustained_files': repeat}
+            'sustained_files': repeat, 'rewrite_ms': round(1e3 * rew, 2),
+            'rewrite_GB_per_s': round(nbytes / rew / 1e9, 2)}
 
 
 def write_fastq(path, reads, seed):
@@ -1750,14 +1759,28 @@ def run_e2e(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapters):
     n_sa, n_ea = len(start_adps), len(end_adps)
     ft = FileTrimmer(sets, sc, E, 75.0, 2, 4, args.middle_threshold, 10, 100, 1000, device=args.local_device)
     last = {}
+    outs, done_outs = [], []
 
     def step():
+        # every step writes a fresh output file, as a CLI run does: re-truncating one 1.4 GB file
+        # each step made the writer also free the previous step's ~350 k cached pages (~150 ms per
+        # step on the GPU box: bench write_probe, r04-r05 'sustained' vs 'burst'); the files are
+        # removed after the timed steps
         ft.times = {}
-        last.update(ft.trim_file(in_path, out_path, 'fastq', max_reads=min(n, args.e2e_batch)))
+        outs.append('%s.%d' % (out_path, len(done_outs) + len(outs)))
+        last.update(ft.trim_file(in_path, outs[-1], 'fastq', max_reads=min(n, args.e2e_batch)))
+        if getattr(ft, 'trace', None):
+            t0 = min(x[2] for x in ft.trace)
+            last['timeline'] = [[s_, k_, round(1e3 * (a_ - t0), 2), round(1e3 * (b_ - t0), 2)]
+                                for s_, k_, a_, b_ in ft.trace]
         return dict(ft.times)
 
     for _ in range(args.warmup):
         step()
+    for p in outs:                        # the warm-up's output, before the timed steps
+        os.remove(p)
+    done_outs += outs
+    del outs[:]
     if dist is not None:
         dist.barrier()
     acc = {}
@@ -1770,7 +1793,10 @@ def run_e2e(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapters):
         tt = torch.tensor([elapsed], dtype=torch.float64, device='cuda' if args.dist_backend == 'nccl' else 'cpu')
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+    out_path = outs[-1]
     out_bytes = os.path.getsize(out_path)
+    for p in outs[:-1]:
+        os.remove(p)
     probe = write_probe(out_path + '.probe', out_bytes, args.steps + args.warmup) if rank == 0 else None
     checked = None
     if args.check and rank == 0:
@@ -1832,6 +1858,8 @@ def run_e2e(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapters):
             'parity_spot_check': checked,
             'setup_s': round(gen_s, 2),
         }
+        if 'timeline' in last:            # PCABI_PIPE_TRACE=1: the last step's (stage, batch, ms, ms)
+            out['timeline'] = last['timeline']
         return out
     return None
 

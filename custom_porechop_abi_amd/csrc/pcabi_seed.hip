@@ -1069,7 +1069,9 @@ __global__ __launch_bounds__(256) void k_seed_band(const int4 *task, const int32
         const int T = thr[tk.y];
         const int best = inside ? band_best<E, false>(rd, len, ac, L, d0, sc, T, codes)
                                 : band_best<E, true>(rd, len, ac, L, d0, sc, T, codes);
-        atomicMax(&bound[(int64_t)tk.y * n + tk.x], best);
+        // only a bound that reaches T is ever read (k_cands, the host's >= T): lower ones stay
+        // unwritten, so random probe hits -- most tasks -- cost no atomic
+        if (best >= T) atomicMax(&bound[(int64_t)tk.y * n + tk.x], best);
         if (vo.list) put_verified(vo, best >= T, tk.x, tk.y, E, v_off[tk.x] + d0);
     }
 }
@@ -1220,7 +1222,7 @@ __global__ __launch_bounds__(256) void k_seed_band_pin(const int4 *task, const i
         bool ver = false;
         if (active && rows == 0) {                    // the run ends the adapter: Q = 0
             if (o == 0) {
-                atomicMax(&bound[bidx], pin);
+                if (pin >= T) atomicMax(&bound[bidx], pin);
                 ver = pin >= T;
                 active = false;
             } else {
@@ -1262,15 +1264,14 @@ __global__ __launch_bounds__(256) void k_seed_band_pin(const int4 *task, const i
 #pragma unroll
                 for (int x = 1; x < W; ++x) mx = max(mx, S[x]);
                 const int ub = mx + bs * rows + other;
-                if (ub < T) {
-                    atomicMax(&bound[bidx], ub);
+                if (ub < T) {                         // below T: nothing to record (k_seed_band)
                     active = false;
                 } else if (rows == 0) {
                     if (phase == 0 && o > 0) {
                         begin_prefix();
                     } else {
-                        atomicMax(&bound[bidx], mx + other);
                         ver = mx + other >= T;
+                        if (ver) atomicMax(&bound[bidx], mx + other);
                         active = false;
                     }
                 }

@@ -16,6 +16,9 @@
  *       [getattr(o, name) for o in objs].
  *   append_rows(reads, name, objs, read, obj, f1, f2, i1, i2)
  *       Alignment tuples appended to each read's list attribute (below).
+ *   int_attrs(objs, name, out)
+ *       out[k] = getattr(objs[k], name) for int attributes (out: writable int64 buffer) -- the
+ *       middle driver's trim amounts without a list of ints and its numpy conversion.
  *   raise_trims(reads, start, end)
  *       For each read k: read.start_trim_amount = max(read.start_trim_amount, start[k]), the same
  *       for end_trim_amount (start / end: int32 buffers) -- the end-trim driver's update of the
@@ -90,6 +93,36 @@ static PyObject *attr_list(PyObject *self, PyObject *args) {
     }
     Py_DECREF(fast);
     return out;
+}
+
+static PyObject *int_attrs(PyObject *self, PyObject *args) {
+    PyObject *seq, *name;
+    Py_buffer ob;
+    if (!PyArg_ParseTuple(args, "OUw*", &seq, &name, &ob)) return NULL;
+    PyObject *ret = NULL;
+    PyObject *fast = PySequence_Fast(seq, "int_attrs: a sequence");
+    if (!fast) goto done;
+    const Py_ssize_t n = PySequence_Fast_GET_SIZE(fast);
+    if (ob.len < n * (Py_ssize_t)sizeof(int64_t)) {
+        PyErr_SetString(PyExc_ValueError, "int_attrs: buffer too small");
+        goto done;
+    }
+    int64_t *out = (int64_t *)ob.buf;
+    PyObject **items = PySequence_Fast_ITEMS(fast);
+    for (Py_ssize_t k = 0; k < n; ++k) {
+        PyObject *v = PyObject_GetAttr(items[k], name);
+        if (!v) goto done;
+        const long long x = PyLong_AsLongLong(v);   /* an int (or __index__): as int(...) would */
+        Py_DECREF(v);
+        if (x == -1 && PyErr_Occurred()) goto done;
+        out[k] = (int64_t)x;
+    }
+    Py_INCREF(Py_None);
+    ret = Py_None;
+done:
+    Py_XDECREF(fast);
+    PyBuffer_Release(&ob);
+    return ret;
 }
 
 static int raise_field(PyObject *o, PyObject *name, long v) {
@@ -260,6 +293,7 @@ static PyMethodDef methods[] = {
     {"append_rows", append_rows, METH_VARARGS, "append alignment tuples to the reads' lists"},
     {"ascii_buffers", ascii_buffers, METH_VARARGS, "addresses and lengths of ASCII strs"},
     {"attr_list", attr_list, METH_VARARGS, "[getattr(o, name) for o in objs]"},
+    {"int_attrs", int_attrs, METH_VARARGS, "int attributes of objs into an int64 buffer"},
     {"raise_trims", raise_trims, METH_VARARGS, "raise the reads' trim amounts to the given ones"},
     {NULL, NULL, 0, NULL}};
 

@@ -239,6 +239,9 @@ class FileTrimmer(object):
         library's parse, alignment and write calls release the GIL. times: 'parse' / 'write_wait'
         are this thread's waits, 'read' / 'write' the reader's / writer's own busy time (overlapped)."""
         counts = {'reads_in': 0, 'reads_kept': 0}
+        # PCABI_PIPE_TRACE=1: (stage, batch, begin, end) per stage and batch in self.trace (the
+        # pipeline's timeline: which stage holds the others up)
+        trace = self.trace = [] if os.environ.get('PCABI_PIPE_TRACE') == '1' else None
         bins = {}                             # barcode name -> (path, reads selected for it)
         if self.barcode_dir is not None:
             os.makedirs(self.barcode_dir, exist_ok=True)
@@ -276,7 +279,10 @@ class FileTrimmer(object):
                     t0 = time.perf_counter()
                     item = next(items, None)
                     # the reader's own busy time (parse; overlapped like 'write')
-                    self.times['read'] = self.times.get('read', 0.0) + time.perf_counter() - t0
+                    t1 = time.perf_counter()
+                    self.times['read'] = self.times.get('read', 0.0) + t1 - t0
+                    if trace is not None:
+                        trace.append(('read', item[0] if item is not None else -1, t0, t1))
                     if item is None:
                         break
                     k, b, alb = item
@@ -312,7 +318,10 @@ class FileTrimmer(object):
                 first = False
                 counts['reads_in'] += b.n
                 counts['reads_kept'] += int(keep.sum()) if keep is not None else b.n
-                self.times['write'] = self.times.get('write', 0.0) + time.perf_counter() - t0
+                t1 = time.perf_counter()
+                self.times['write'] = self.times.get('write', 0.0) + t1 - t0
+                if trace is not None:
+                    trace.append(('write', k, t0, t1))
             if first and not errors and self.barcode_dir is None:   # empty input: still create the output
                 open(out_path, 'wb').close()
 
@@ -330,11 +339,17 @@ class FileTrimmer(object):
                 if isinstance(b, BaseException):
                     raise b
                 k, b, alb = b
+                t0 = t
                 st, et, co, cu, _, keep = self.trim(b) if alb is None else self.trim(b, albacore=alb)
                 calls = self.last_calls if self.barcode_dir is not None else None
+                t1 = time.perf_counter()
                 wq.put((k, b, st, et, co, cu, keep, calls))   # the writer drains even after a failure
                 del b
                 t = time.perf_counter()
+                self.times['put_wait'] = self.times.get('put_wait', 0.0) + t - t1
+                if trace is not None:
+                    trace.append(('trim', k, t0, t1))
+                    trace.append(('put', k, t1, t))
         finally:
             # on every exit (errors included) the reader's pending put times out on `stop`, so
             # joining it cannot block on a full queue

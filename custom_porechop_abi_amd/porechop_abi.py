@@ -404,8 +404,13 @@ def trimmed_bounds(reads, seq_lens=None):
     seq lengths when the caller has them already."""
     n = np.fromiter(map(len, _attrs(reads, 'seq')), np.int64, len(reads)) if seq_lens is None else \
         np.asarray(seq_lens, np.int64)
-    s = np.array(_attrs(reads, 'start_trim_amount'), np.int64).reshape(-1)
-    e = np.array(_attrs(reads, 'end_trim_amount'), np.int64).reshape(-1)
+    if engine._pystr is not None:                 # one native pass per field, straight into int64
+        s, e = np.empty(len(reads), np.int64), np.empty(len(reads), np.int64)
+        engine._pystr.int_attrs(reads, 'start_trim_amount', s)
+        engine._pystr.int_attrs(reads, 'end_trim_amount', e)
+    else:
+        s = np.array(_attrs(reads, 'start_trim_amount'), np.int64).reshape(-1)
+        e = np.array(_attrs(reads, 'end_trim_amount'), np.int64).reshape(-1)
     a = np.minimum(s, n)
     b = n - e
     b = np.clip(np.where(b < 0, b + n, b), 0, n)
