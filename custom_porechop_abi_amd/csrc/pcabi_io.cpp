@@ -86,6 +86,7 @@ struct pcabi_fastx {
     int64_t line_no = 0;
     bool raw = false;              // keep the file's text (misc.load_fasta_or_fastq tuples)
     size_t size_hint = 0;          // decoded bytes expected (file size; x4 for gzip)
+    size_t released = 0;           // mapped file bytes before this have had their page mappings dropped
     // FASTA state that crosses batch boundaries
     bool fa_have_name = false;     // a header was seen (its name may be empty)
     std::string fa_name, fa_seq;
@@ -387,6 +388,13 @@ void fill_fastq(pcabi_reads *b, const char *T, const std::vector<Span> &rec, boo
         b->len[n0 + i] = (int32_t)r.sn;
         code_end += (int64_t)((r.sn + 3) & ~(size_t)3);
     }
+    // exact sizes, known from the record scan (finish_batch's 16 bytes of padding included): the
+    // blocks of one batch then match the next batch's, and the block cache hands them back already
+    // faulted in (a file-sized reservation per batch made every free an unmapping, r05)
+    b->names.reserve((size_t)b->name_off[n0 + n]);
+    b->seq.reserve((size_t)b->seq_off[n0 + n]);
+    b->qual.reserve((size_t)b->qual_off[n0 + n]);
+    b->codes.reserve((size_t)code_end + 16);
     b->names.resize((size_t)b->name_off[n0 + n]);
     b->seq.resize((size_t)b->seq_off[n0 + n]);
     b->qual.resize((size_t)b->qual_off[n0 + n]);
@@ -460,10 +468,10 @@ int pcabi_fastx_open(const char *path, int raw, pcabi_fastx **out) {
         const int fd = ::open(path, O_RDONLY);
         struct stat st;
         if (fd >= 0 && fstat(fd, &st) == 0 && st.st_size > 0) {
-            // MAP_POPULATE: the pages of a cached file are mapped in one pass, not fault by fault
-            // (files past 8 GB are mapped lazily: a range reader touches only its own part)
-            const int pop = st.st_size <= (8ll << 30) ? MAP_POPULATE : 0;
-            void *m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE | pop, fd, 0);
+            // mapped lazily (r05): the record scan faults its batch in as it goes (fault-around maps
+            // 16 pages a fault); MAP_POPULATE mapped the whole file before the first batch could be
+            // parsed (~80 ms of a 1.6 GB file's first batch, nothing else overlapping it)
+            void *m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
             if (m != MAP_FAILED) {
                 madvise(m, (size_t)st.st_size, MADV_SEQUENTIAL);
                 r->map = m;
@@ -577,6 +585,7 @@ int pcabi_fastx_set_range(pcabi_fastx *r, int64_t begin, int64_t end) {
     if (begin < 0 || end < begin || (size_t)end > r->map_len) return fail(PCABI_E_ARG, "byte range outside the file");
     r->pos = (size_t)begin;
     r->end = (size_t)end;
+    r->released = (size_t)begin & ~(size_t)4095;
     const size_t pg = (size_t)begin & ~(size_t)4095;
     if (end > begin) madvise((char *)r->map + pg, (size_t)end - pg, MADV_WILLNEED);
     r->eof = true;
@@ -602,12 +611,12 @@ int64_t pcabi_fastx_next(pcabi_fastx *r, int64_t max_reads, int64_t max_bases, p
     if (!r || !out || max_reads <= 0) return fail(PCABI_E_ARG, "bad arguments");
     pcabi_reads *b = new pcabi_reads();
     b->type = r->type;
-    {
-        // sequence and qualities are about half the decoded bytes each
+    if (r->type != PCABI_FASTQ) {
+        // FASTA appends record by record: sequence about the decoded bytes (FASTQ sizes its
+        // buffers exactly from the record scan, fill_fastq)
         const size_t want = std::min<size_t>(r->size_hint / 2 + 4096, (size_t)std::min<int64_t>(max_bases, 1LL << 40));
         b->seq.reserve(want);
         b->codes.reserve(want + 4096);
-        if (r->type == PCABI_FASTQ) b->qual.reserve(want);
     }
     int64_t bases = 0;
     const char *p;
@@ -679,6 +688,18 @@ int64_t pcabi_fastx_next(pcabi_fastx *r, int64_t max_reads, int64_t max_bases, p
     if (r->err) {
         delete b;
         return PCABI_E_PARSE;   // the message is pcabi_last_error()'s (next_line)
+    }
+    if (r->map) {
+        // the batch holds copies of its records: the page mappings of the file bytes it consumed
+        // are dropped as the reader goes (madvise takes the address space's lock shared), so the
+        // final munmap has nothing left to tear down -- a whole-file teardown held the lock
+        // exclusively for ~50 ms and stalled every other thread's page faults (r05 e2e timeline).
+        // The bytes stay in the page cache; a later read of them faults them back in.
+        const size_t upto = r->pos & ~(size_t)4095;
+        if (upto >= r->released + (32u << 20)) {
+            madvise((char *)r->map + r->released, upto - r->released, MADV_DONTNEED);
+            r->released = upto;
+        }
     }
     finish_batch(b);
     *out = b;
