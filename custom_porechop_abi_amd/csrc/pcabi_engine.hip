@@ -1343,11 +1343,18 @@ struct pcabi_adapters {
 
 namespace {
 
+}  // namespace
+// Bumped by every device (re)allocation of the engine's and the seeds' scratch and by every new
+// seed plan: a captured round graph (middle_device_rounds) holds their addresses and launch
+// arguments, and is replayed only while the generation it was captured at holds.
+std::atomic<uint64_t> g_buf_gen{0};
+namespace {
 struct DeviceBuf {
     void *p = nullptr;
     size_t cap = 0;
     int ensure(size_t bytes) {
         if (bytes <= cap) return 0;
+        g_buf_gen.fetch_add(1);
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
@@ -1442,6 +1449,13 @@ struct pcabi_scan {
     int64_t shadow_cap = 0;
     MidProf prof;                                   // pcabi_scan_profile
     DeviceBuf pprof;                                // its device counters (4 x u64)
+    // (r05) later rounds replayed from captured graphs, one per round slot: the key is everything
+    // a round's launches take by value or address (middle_device_rounds, RoundKey)
+    struct RoundGraph {
+        std::vector<int64_t> key;
+        hipGraphExec_t exec = nullptr;
+    };
+    RoundGraph graphs[32];
 };
 
 namespace {
@@ -2453,6 +2467,8 @@ void pcabi_scan_destroy(pcabi_scan *s) {
         if (b->p) (void)hipFree(b->p);
     if (s->h_stage) (void)hipHostFree(s->h_stage);
     if (s->h_ctl) (void)hipHostFree(s->h_ctl);
+    for (auto &g : s->graphs)
+        if (g.exec) (void)hipGraphExecDestroy(g.exec);
     if (s->seed) pcabi_seed::destroy(s->seed);
     delete s;
 }
@@ -3470,6 +3486,63 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
         }
         return 0;
     };
+    // A round other than a call's first one is ~40 small launches and fork / join events whose
+    // arguments depend only on the slot, the call's inputs and the scratch addresses: it is captured
+    // once into a graph and replayed (r05: one host call instead of ~40 launches and ~10 event
+    // operations, and the graph's ~1.6 us per kernel instead of ~2.7 back to back, tools/
+    // launch_bench.hip). Not for rounds that inject faults (tests), profile, debug, serial rounds or
+    // the legacy stream; PCABI_MIDDLE_GRAPHS=0 queues every round directly (A/B).
+    const bool graphs_on = [] {
+        const char *e = std::getenv("PCABI_MIDDLE_GRAPHS");
+        return !(e && e[0] == '0');
+    }() && st != nullptr && faults.empty() && !g_debug && !sc->prof.on;
+    auto run_round = [&](int r) -> int {
+        const bool first = r == 0 && round_base == 0;
+        if (!graphs_on || first || round_base + r >= serial_from) return queue_round(r);
+        std::vector<int64_t> key = {(int64_t)round_base, (int64_t)(intptr_t)codes, (int64_t)(intptr_t)win_off,
+                                    (int64_t)(intptr_t)win_len, n, windows ? 1 : 0, (int64_t)(threshold * 1e6),
+                                    scr.ma, scr.mi, scr.go, scr.ge, (int64_t)(intptr_t)adps, sc->q_slots_cap,
+                                    sc->shadow_cap, (int64_t)(intptr_t)sc->shadow.p, target,
+                                    (int64_t)g_buf_gen.load()};
+        auto &g = sc->graphs[r & 31];
+        if (g.exec && g.key == key) {
+            HIP_TRY(hipGraphLaunch(g.exec, st));
+            return 0;
+        }
+        if (g.exec) {
+            (void)hipGraphExecDestroy(g.exec);
+            g.exec = nullptr;
+        }
+        // the round's buffers exist after round 1 of this call; a reallocation while capturing would
+        // change the generation: the graph is then dropped and the round queued directly
+        if (hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed) != hipSuccess) {
+            (void)hipGetLastError();
+            return queue_round(r);
+        }
+        const uint64_t gen0 = g_buf_gen.load();
+        const int rc = queue_round(r);
+        hipGraph_t graph = nullptr;
+        const hipError_t ec = hipStreamEndCapture(st, &graph);
+        if (rc) {
+            if (graph) (void)hipGraphDestroy(graph);
+            return rc;
+        }
+        hipGraphExec_t exec = nullptr;
+        const bool ok = ec == hipSuccess && graph && g_buf_gen.load() == gen0 &&
+                        hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0) == hipSuccess;
+        if (graph) (void)hipGraphDestroy(graph);
+        if (!ok) {                                   // nothing of the round ran: queue it directly
+            (void)hipGetLastError();
+            if (exec) (void)hipGraphExecDestroy(exec);
+            return queue_round(r);
+        }
+        g.exec = exec;
+        g.key = key;
+        key[16] = (int64_t)g_buf_gen.load();
+        g.key = key;
+        HIP_TRY(hipGraphLaunch(g.exec, st));
+        return 0;
+    };
     // pinned control block: round counts [kSlots + 2], flags [kSlots + 2], need / flag word / need2
     if (!sc->h_ctl) HIP_TRY(hipHostMalloc((void **)&sc->h_ctl, kCtlBytes + 8, hipHostMallocDefault));
     int32_t *h_n = sc->h_ctl, *h_flag = sc->h_ctl + (kSlots + 2);
@@ -3495,7 +3568,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
         // queue up to kBatch rounds from `slot`
         const int upto = std::min(slot + (round_base == 0 && slot == 0 ? batch1 : kBatch), kSlots);
         for (int r = slot; r < upto; ++r) {
-            if (int rc = queue_round(r)) return rc;
+            if (int rc = run_round(r)) return rc;
             hmark("round");
             if (r == 0 && round_base == 0)        // round 1's segment total (the next call's mean length)
                 HIP_TRY(hipMemcpyAsync(h_nd + 5, pcabi_seed::seg_cum_dev(sc->seed) + n, sizeof(int64_t),

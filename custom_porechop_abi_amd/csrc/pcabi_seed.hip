@@ -56,6 +56,9 @@
 namespace pcabi_internal {
 int fail(int code, const std::string &msg);
 }
+// pcabi_engine.hip: the scratch generation its captured round graphs are keyed on (a reallocation,
+// a new plan or new capacities here change addresses or launch arguments those graphs hold)
+extern std::atomic<uint64_t> g_buf_gen;
 using pcabi_internal::fail;
 
 #define SD_TRY(expr)                                                                                          \
@@ -386,9 +389,9 @@ __global__ __launch_bounds__(256) void k_seed_scan_bits(ScanArgs a) {
 
 // k_seed_scan (r04): the same segment walk, hit masks and slab records as k_seed_scan_bits (the
 // r03 kernel, PCABI_SEED_BYTEMAP=0), with the per-position work cut from 6 VALU instructions to 2:
-//   * the merged 8-mer bitmap is expanded into a BYTE map in LDS (64 KiB: byte c = bit c), so a
-//     position's lookup is one ds_read_u8 at its 8-mer code, and the byte shifts straight into the
-//     hit mask (no word address, no bit shift);
+//   * the merged 8-mer bitmap is expanded into a BYTE map in LDS (64 KiB), so a lookup is one
+//     ds_read_u8 at an 8-mer code; r05: a PAIR map -- byte c holds the membership of c and, per next
+//     base j, of the 8-mer that follows (c << 2 | j), so one read serves two positions;
 //   * a lane's 40 bytes are packed once into 2-bit codes, base 0 in the top bits (P0 = bases 0-15,
 //     Q0 = 8-23, P1 = 16-31, Q1 = 24-39): position i's code is one bit-field extract of one of them;
 //   * a hit's 8-mer comes from the same packed words (no re-read of the read bytes).
@@ -413,16 +416,33 @@ __global__ __launch_bounds__(kScanThreads) void k_seed_scan(ScanArgs a) {
     // static LDS (a workgroup may hold more than 64 KiB of it on gfx950): the byte map -- a position's
     // code plus the map's constant LDS address is its read address
     __shared__ __attribute__((aligned(16))) uint32_t bmap[kByteMap / 4];
-    {   // bitmap word w -> 8 map dwords; a thread's four words loaded together
+    {   // the pair map from the bitmap B (2048 words, bit c of the merged table = word c >> 5, bit
+        // c & 31): byte c holds, for each next base j, bits 2j = B[c] and 2j + 1 = B[(4c + j) & 0xFFFF]
+        // -- the membership of the 8-mers at positions i and i + 1 of a 9-mer c.j. Map dword m (codes
+        // 4m .. 4m + 3): the first bits from nibble m & 7 of word m >> 3, the second ones from the
+        // 16-bit half m & 1 of word (m >> 1) & 2047 (bits 16m + 4j' .. + 3 for byte j'). Bitmap word w
+        // covers map dwords 8w .. 8w + 7; a thread's words loaded together.
         static_assert(kByteMap / 32 == 4 * kScanThreads, "four bitmap words per thread");
-        uint32_t word[4];
+        uint32_t word[4], half[4][4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) word[q] = a.tabs[threadIdx.x + q * kScanThreads];
+        for (int q = 0; q < 4; ++q) {
+            const int w = threadIdx.x + q * kScanThreads;
+            word[q] = a.tabs[w];
+#pragma unroll
+            for (int h = 0; h < 4; ++h) half[q][h] = a.tabs[(4 * w + h) & 2047];
+        }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int w = threadIdx.x + q * kScanThreads;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) bmap[w * 8 + k] = (((word[q] >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t first = ((((word[q] >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u) * 0x55u;
+                const uint32_t hs = (half[q][k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+                const uint32_t d = (hs & 0xFu) | ((hs & 0xF0u) << 4) | ((hs & 0xF00u) << 8) | ((hs & 0xF000u) << 12);
+                const uint32_t second = ((d & 0x01010101u) << 1) | ((d & 0x02020202u) << 2) | ((d & 0x04040404u) << 3) |
+                                        ((d & 0x08080808u) << 4);
+                bmap[w * 8 + k] = first | second;
+            }
         }
     }
     const uint8_t *bytes = reinterpret_cast<const uint8_t *>(bmap);
@@ -515,18 +535,28 @@ __global__ __launch_bounds__(kScanThreads) void k_seed_scan(ScanArgs a) {
             const uint32_t Q1 = __builtin_amdgcn_alignbit(P1, P2, 16);   // bases 24-39
             // (the reads of 16 positions issued together: LDS latency, not issue, is the risk at the
             // 4 waves per SIMD the two byte maps leave)
+            // one pair-map read per two positions: the byte of the 8-mer at even i, then the 2-bit
+            // field of the base at i + 8 -- (hit at i, hit at i + 1) -- straight into the mask (r05:
+            // half the LDS reads and bank-conflict cycles, ~58 % of the LDS array's time before; the
+            // scan's time did not move, r05u / r05v: it is not LDS-bound, nor load-depth-bound -- a
+            // third segment in flight per lane was measured neutral too)
             uint32_t hits = 0;
 #pragma unroll
             for (int h = 0; h < kSeg; h += 16) {
-                uint32_t m[16];
+                uint32_t m[8];
 #pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    const int i = h + j;
+                for (int j = 0; j < 8; ++j) {
+                    const int i = h + 2 * j;
                     const uint32_t src = i < 8 ? P0 : i < 16 ? Q0 : i < 24 ? P1 : Q1;
                     m[j] = bytes[(src >> (16 - 2 * (i & 7))) & 0xFFFFu];
                 }
 #pragma unroll
-                for (int j = 0; j < 16; ++j) hits |= m[j] << (h + j);
+                for (int j = 0; j < 8; ++j) {
+                    const int i = h + 2 * j;
+                    const uint32_t src = i < 8 ? P0 : i < 16 ? Q0 : i < 24 ? P1 : Q1;
+                    const uint32_t b2 = (src >> (13 - 2 * (i & 7))) & 6u;    // 2 x the base at i + 8
+                    hits |= ((m[j] >> b2) & 3u) << i;
+                }
             }
             // ---- validity: N bytes and the read end (as k_seed_scan_bits) ----
             const int rem = clen - cp;
@@ -1350,6 +1380,7 @@ struct Buf {
         p = nullptr;
         cap = 0;
         const size_t want = std::max<size_t>(bytes, 1 << 16);
+        g_buf_gen.fetch_add(1);
         if (hipMalloc(&p, want) != hipSuccess) return fail(PCABI_E_NOMEM, "hipMalloc failed (seeds)");
         cap = want;
         return 0;
@@ -1855,6 +1886,7 @@ int read_counts(State *s, int32_t (&out)[kCnt], hipStream_t st) {
 
 // Larger buffers after an overflow; false when they would pass sane limits.
 bool grow(State *s, const int32_t (&c)[kCnt]) {
+    g_buf_gen.fetch_add(1);           // new capacities: launch arguments of captured rounds change
     if (c[kFlag]) {
         if (s->raw_cap > (1ll << 31)) return false;
         s->raw_cap *= 2;
@@ -1882,6 +1914,7 @@ int check_plan(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32
     if (!same) {
         // a new plan: the old tables may still be read by work queued on `st`
         SD_TRY(hipStreamSynchronize(st));
+        g_buf_gen.fetch_add(1);
         s->key_len.assign(hlen, hlen + n_adp);
         s->key_rows = fb_rows;
         s->key_codes.clear();

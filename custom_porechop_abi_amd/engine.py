@@ -385,11 +385,25 @@ def middle_cuts(hits, n_reads, bad_start, bad_end, good_side, bad_side, device=0
     return cut_off, cuts
 
 
+_PID6_TAB = []
+
+
 def pid6(m, l):
     """float('%f' % (100*m/l)) elementwise (NaN where l == 0), the reference's identity text
-    round trip (porechop_abi/src/alignment.cpp:118-119, porechop_abi/nanopore_read.py:497-498)."""
+    round trip (porechop_abi/src/alignment.cpp:118-119, porechop_abi/nanopore_read.py:497-498).
+    Pairs with 0 <= m, l < 256 (every end-window alignment) come from a table the library filled
+    once (pcabi_pid6_host over all 65,536 pairs): the drivers convert ~10^6 pairs per batch."""
     m = np.ascontiguousarray(m, dtype=np.int32)
     l = np.ascontiguousarray(l, dtype=np.int32)
+    if m.size > 4096 and m.shape == l.shape:
+        small = ((m | l) & ~255) == 0
+        if small.all():
+            if not _PID6_TAB:
+                mm, ll = np.divmod(np.arange(65536, dtype=np.int32), 256)
+                tab = np.empty(65536, dtype=np.float64)
+                lib().pcabi_pid6_host(_ptr(np.ascontiguousarray(mm)), _ptr(np.ascontiguousarray(ll)), 65536, _ptr(tab))
+                _PID6_TAB.append(tab)
+            return _PID6_TAB[0][(m << 8) | l]
     out = np.empty(m.shape, dtype=np.float64)
     lib().pcabi_pid6_host(_ptr(m), _ptr(l), m.size, _ptr(out))
     return out

@@ -347,11 +347,12 @@ def test_seed_expand_one_pass(gpu_lib, monkeypatch, thr):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('split', ['2', '4'])
+@pytest.mark.parametrize('split', ['0', '2', '4'])
 @pytest.mark.parametrize('windows', ['0', '1'])
 def test_chunk_dp_row_split(gpu_lib, monkeypatch, reads_8kb, split, windows):
-    """PCABI_CHUNK_SPLIT=2|4: the candidate DP's chunk tasks on the row-split core (K lanes per task,
-    k_align_split_chunk; host model: test_dp_core_cpu.py::test_row_split_chunk_core) -- the scan
+    """PCABI_CHUNK_SPLIT=0|2|4: the candidate DP's chunk tasks one lane per task, or on the row-split
+    core (K lanes per task, k_align_split_chunk, K = 2 the default since r05; host model:
+    test_dp_core_cpu.py::test_row_split_chunk_core) -- the scan
     equals the oracle, whole-read chunks and candidate windows alike, and at 90 % on shorter copies
     with the 85 % threshold's longer probes."""
     from custom_porechop_abi_amd import engine
