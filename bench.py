@@ -105,6 +105,9 @@ def parse():
                     help='GPU_MAX_HW_QUEUES for this process when the environment does not set it (0: HIP default, '
                          '4; r04 A/B with 8: headline 8.05 vs 7.61 ms, reference job 5.85 vs 5.23 ms)')
     ap.add_argument('--only-subs', default='', help='comma-separated sub-record names to run (default: all)')
+    ap.add_argument('--ab', default='',
+                    help='middle workloads: NAME=v0,v1 alternates an environment switch of the library between '
+                         'timed steps and reports the middle scan time per value (A/B within one process)')
     ap.add_argument('--sub', type=int, default=1,
                     help='endtrim at N=1: also time the middle workload (configs[2]) and the host-buffer path '
                          '(H2D + kernels + D2H) as sub-records of the same JSON line')
@@ -1356,6 +1359,7 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
     trims = np.zeros((2, n), np.int32)
     t_len = np.zeros(n, np.int32)
     stats = {}
+    ab_name, ab_vals = (args.ab.split('=', 1)[0], args.ab.split('=', 1)[1].split(',')) if args.ab else ('', [])
 
     def step():
         work = d_pack
@@ -1379,6 +1383,8 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
         _lib.check(L.pcabi_event_elapsed_ms(ctypes.byref(ms), ev[0], ev[1]), 'elapsed')
         stats['hits'] = int(nh)
         stats['middle_s'] = stats.get('middle_s', 0.0) + 1e-3 * ms.value
+        if ab_name:
+            stats.setdefault('ab', {}).setdefault(os.environ.get(ab_name, ''), []).append(round(ms.value, 4))
 
     for _ in range(args.warmup):
         step()
@@ -1389,6 +1395,8 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
     torch.cuda.synchronize() if torch.cuda.is_available() else None
     t0 = time.perf_counter()
     for k in range(args.steps):
+        if ab_name:                        # --ab: the switch alternates between the timed steps
+            os.environ[ab_name] = ab_vals[k % 2]
         step()
     L.pcabi_stream_sync(stream)
     if dist is not None:
@@ -1448,6 +1456,9 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
                        'inputs': 'one read pack resident in HBM for every step (the scan leaves it intact)'},
             'middle_ms_per_step': round(1e3 * stats['middle_s'] / args.steps, 3),
             'middle_hits_per_step': stats['hits'],
+            # --ab: the middle scan's event time per value of the alternated switch (median, all)
+            'ab': {ab_name: {v: {'median_ms': float(np.median(x)), 'ms': x} for v, x in stats.get('ab', {}).items()}}
+                  if ab_name else None,
             # the middle scan computes only the seeded band cells and its candidates' chunks, not
             # the whole-read cross product: only the end windows' cells are counted as computed
             'cells_per_step': {'end_windows': cells_end, 'middle_cross_product_not_computed': cells_mid},

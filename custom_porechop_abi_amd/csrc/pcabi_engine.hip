@@ -1318,8 +1318,12 @@ int fail(int code, const std::string &msg) { return pcabi_eng::fail(code, msg); 
 }  // namespace pcabi_internal
 
 // ---- prepared adapter tables (device) ---------------------------------------------------------
+std::atomic<uint64_t> g_table_serial{0};
 struct pcabi_adapters {
     int32_t n_adp = 0;
+    // a process-unique number (a new table may reuse a freed one's address): what the middle scan's
+    // captured round graphs are keyed on, since they hold the table's device pointers
+    uint64_t serial = g_table_serial.fetch_add(1) + 1;
     int rt[kNumBuckets] = {};        // striped bucket: table rows per adapter
     bool padded[kNumBuckets] = {};
     int max_off[kNumBuckets] = {};   // most padding rows above an adapter (> 3: packed core only)
@@ -1456,6 +1460,8 @@ struct pcabi_scan {
         hipGraphExec_t exec = nullptr;
     };
     RoundGraph graphs[32];
+    int rounds_hint = 3;                            // rounds the last call needed (the first batch's size)
+    uint64_t last_table = 0;                        // the adapter table (serial) of the last call
 };
 
 namespace {
@@ -3107,12 +3113,14 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
     const int64_t n = n_win;
     constexpr int kSlots = 16;                      // round slots held on the device (wrapped past)
     constexpr int kBatch = 3;                       // rounds queued per host check (later batches)
-    // the first batch's rounds (PCABI_MIDDLE_BATCH1 = 1..3, A/B): with 2, data where round 2 finds
-    // nothing skips a third round's ~35 empty launches, but data with a third round pays a host round
-    // trip for it (r05g: within the run-to-run noise either way, so the default stays 3)
-    const int batch1 = [] {
+    // the first batch's rounds: as many as the previous call needed (its rounds up to the first one
+    // that found nothing), 2 to 3. Data where round 2 finds nothing then skips a third round of ~35
+    // empty launches, data with a third round pays no extra host round trip for it (r05y, in-process
+    // A/B: the 20 kb scan 2.86 ms with 3 against 2.72 with 2, the 8 kb one 2.01 with 3 against 2.19
+    // with 2). PCABI_MIDDLE_BATCH1 = 1..3 fixes it (A/B).
+    const int batch1 = [&] {
         const char *e = std::getenv("PCABI_MIDDLE_BATCH1");
-        const int v = e ? std::atoi(e) : kBatch;
+        const int v = e ? std::atoi(e) : std::min(kBatch, std::max(2, sc->rounds_hint));
         return v >= 1 && v <= kBatch ? v : kBatch;
     }();
     constexpr unsigned kGrid = 2048;                // blocks of the device-counted launches
@@ -3349,6 +3357,11 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
             p.wave_adp = (const int32_t *)pl.wa->p;
             p.task_chunk = (const int4 *)pl.tck->p;
             p.n_waves = kGrid;
+            // two lanes per chunk task in the candidate-window rounds (long reads: the windows and the
+            // certified-out candidates' whole reads), one lane in the whole-read rounds of shorter reads
+            // (r05y / r05z in-process A/B: two lanes everywhere made the 20 kb scan 0.13 ms faster --
+            // most of it the whole reads' 32-column chunks -- and the 8 kb one 0.08-0.09 ms slower)
+            p.chunk_split = windows ? 2 : 0;
             ForkJoin fj;
             if (int rc = fj.begin(st, serial ? 1 : used.size())) return rc;
             for (int k = 0; k < n_bk; ++k) {
@@ -3495,13 +3508,16 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
     const bool graphs_on = [] {
         const char *e = std::getenv("PCABI_MIDDLE_GRAPHS");
         return !(e && e[0] == '0');
-    }() && st != nullptr && faults.empty() && !g_debug && !sc->prof.on;
+    }() && st != nullptr && faults.empty() && !g_debug && !sc->prof.on && sc->last_table == adps->serial;
+    // (a table new to this scan -- e.g. the host API's per-call tables -- runs its rounds directly:
+    // a capture pays only for a table the next call uses again)
+    sc->last_table = adps->serial;
     auto run_round = [&](int r) -> int {
         const bool first = r == 0 && round_base == 0;
         if (!graphs_on || first || round_base + r >= serial_from) return queue_round(r);
         std::vector<int64_t> key = {(int64_t)round_base, (int64_t)(intptr_t)codes, (int64_t)(intptr_t)win_off,
                                     (int64_t)(intptr_t)win_len, n, windows ? 1 : 0, (int64_t)(threshold * 1e6),
-                                    scr.ma, scr.mi, scr.go, scr.ge, (int64_t)(intptr_t)adps, sc->q_slots_cap,
+                                    scr.ma, scr.mi, scr.go, scr.ge, (int64_t)adps->serial, sc->q_slots_cap,
                                     sc->shadow_cap, (int64_t)(intptr_t)sc->shadow.p, target,
                                     (int64_t)g_buf_gen.load()};
         auto &g = sc->graphs[r & 31];
@@ -3632,7 +3648,17 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
             slot = bad;
             continue;
         }
-        if (h_n[queued_to] == 0) break;              // the last queued round found no hit
+        if (h_n[queued_to] == 0) {                   // the last queued round found no hit
+            // the rounds this call needed: up to the first that found nothing (the next call's first batch)
+            int need_r = queued_to;
+            for (int r = slot; r < queued_to; ++r)
+                if (h_n[r + 1] == 0) {
+                    need_r = r + 1;
+                    break;
+                }
+            sc->rounds_hint = (int)std::min<int64_t>(round_base + need_r, 64);
+            break;
+        }
         slot = queued_to;
         if (slot == kSlots) {                        // wrap: the next round's reads to slot 0
             HIP_TRY(hipMemcpyAsync(cur_of(0), cur_of(kSlots), 4 * (size_t)h_n[kSlots], hipMemcpyDeviceToDevice, st));

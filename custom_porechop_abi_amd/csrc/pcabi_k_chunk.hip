@@ -10,12 +10,11 @@ int dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st, bool ta
     // planned on the device: n_waves is the grid (blocks striding over the device wave count)
     const dim3 grid((unsigned)(p.dev_waves ? p.n_waves : (p.n_waves + 3) / 4));
     if (kBuckets[b].kind == STRIPED) return launch_striped(p, affine, st);
-    {   // the row-split core, K = 2 lanes per chunk task (r05 default: the 20 kb scan's certified-out
-        // whole reads, 32-column chunks behind a ~60-column lead-in, ran latency-bound one lane per
-        // chunk: candidate DP 0.71-0.73 -> 0.59 ms per 20 kb step, 0.66 -> 0.64 at 8 kb, r05w).
-        // PCABI_CHUNK_SPLIT=0 (one lane per task) | 2 | 4 (A/B)
+    {   // the row-split core, K lanes per chunk task: p.chunk_split, the caller's choice (r05: 2 for
+        // the middle scan's certified-out whole reads, whose 32-column chunks behind a ~60-column
+        // lead-in ran latency-bound one lane per chunk). PCABI_CHUNK_SPLIT=0 | 2 | 4 overrides (A/B)
         const char *e = std::getenv("PCABI_CHUNK_SPLIT");   // (read per launch: tests switch it)
-        const int ks = e ? std::atoi(e) : 2;
+        const int ks = (e && e[0] >= '0' && e[0] <= '9') ? std::atoi(e) : p.chunk_split;
         if ((ks == 2 || ks == 4) && kBuckets[b].kind == FAST && kBuckets[b].rpl <= 64 &&
             pcabi::split_ok(kBuckets[b].rpl, ks) &&
             dispatch_split_chunk(kBuckets[b].rpl, ks, p, affine, tagged && affine && kBuckets[b].rpl <= 32, st))

@@ -81,6 +81,7 @@ struct KParams {
     int64_t out_stride;
     pcabi::Scoring sc;
     int32_t *compat;           // != nullptr: write check_compatibility flags instead of results
+    int32_t chunk_split;       // k_align_chunk: lanes per chunk task (0 / 1: one; 2, 4: the row-split core)
     const int4 *task_chunk;    // k_align_chunk: per task slot (read offset, columns, owned lo, hi)
     // striped bucket (k_align_striped)
     int32_t rt;                // table rows per adapter (multiple of kStripeTab)
