@@ -1363,7 +1363,12 @@ struct DeviceBuf {
         p = nullptr;
         cap = 0;
         size_t want = std::max<size_t>(bytes, 1 << 16);
-        if (hipMalloc(&p, want) != hipSuccess) return fail(PCABI_E_NOMEM, "hipMalloc failed");
+        const hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            p = nullptr;
+            return fail(PCABI_E_NOMEM, "hipMalloc failed (" + std::to_string(want) + " bytes): " + hipGetErrorString(e));
+        }
         cap = want;
         return 0;
     }
@@ -3196,6 +3201,9 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
     unsigned long long *d_bump = (unsigned long long *)(d_slots + 4);
     int32_t *d_pflag = (int32_t *)(d_slots + 2);
     int32_t *d_n = (int32_t *)sc->q_n.p, *d_rflag = d_n + (kSlots + 2);
+    // the plans' slot counts and needs start at 0 (q_n is uninitialised device memory: a round that
+    // overflowed read a need its plan never wrote -- r05aa, a 10^18-byte growth request)
+    HIP_TRY(hipMemsetAsync(d_slots, 0, 4 * sizeof(int64_t), st));
     // the reads' effective offsets start as the caller's; no shadow taken yet
     int64_t *eoff = (int64_t *)sc->eoff.p;
     HIP_TRY(hipMemcpyAsync(eoff, win_off, sizeof(int64_t) * n, hipMemcpyDeviceToDevice, st));
@@ -3637,7 +3645,8 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
                 return fail(PCABI_E_DEVICE, "middle scan: seed buffers past their limits");
             }
             if ((h_flag[bad] & 4) && !injected[bad]) {
-                const int64_t most = std::max(need, need2);
+                // need2: the whole-read plan's slots, written only by the window rounds' second plan
+                const int64_t most = std::max(need, windows ? need2 : (int64_t)0);
                 sc->q_slots_cap = std::max<int64_t>(2 * sc->q_slots_cap, most + most / 4);
             }
             // the shadow arena was too small for the round's first hits: a larger one (the copies

@@ -1381,7 +1381,12 @@ struct Buf {
         cap = 0;
         const size_t want = std::max<size_t>(bytes, 1 << 16);
         g_buf_gen.fetch_add(1);
-        if (hipMalloc(&p, want) != hipSuccess) return fail(PCABI_E_NOMEM, "hipMalloc failed (seeds)");
+        const hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            p = nullptr;
+            return fail(PCABI_E_NOMEM, "hipMalloc failed (seeds, " + std::to_string(want) + " bytes): " + hipGetErrorString(e));
+        }
         cap = want;
         return 0;
     }
