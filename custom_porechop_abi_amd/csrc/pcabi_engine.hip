@@ -145,7 +145,8 @@ bool middle_devplan_on() {
 // profiles/r03/final/windows_sweep/). So they run when the batch's mean read length reaches
 // kWindowsMeanLen -- from the host lengths when the caller passes them, else from the previous
 // call's round-1 segment total (pcabi_scan::last_mean). PCABI_MIDDLE_WINDOWS=1 / 0 forces them.
-constexpr double kWindowsMeanLen = 14000.0;
+constexpr double kWindowsMeanLen = 10000.0;   // r05ac in-process A/B (graphs off): off 1.99 / on 2.03 ms at
+                                              // 8 kb, off 2.50 / on 2.29 at 14 kb, off 3.21 / on 2.74 at 20 kb
 bool middle_windows_on(double mean_len) {
     const char *e = std::getenv("PCABI_MIDDLE_WINDOWS");
     if (e && e[0] == '1') return true;
@@ -1461,7 +1462,7 @@ struct pcabi_scan {
     // (r05) later rounds replayed from captured graphs, one per round slot: the key is everything
     // a round's launches take by value or address (middle_device_rounds, RoundKey)
     struct RoundGraph {
-        std::vector<int64_t> key;
+        std::vector<int64_t> key, seen;     // the captured graph's key; the last key queued directly
         hipGraphExec_t exec = nullptr;
     };
     RoundGraph graphs[32];
@@ -3536,6 +3537,12 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
         if (g.exec) {
             (void)hipGraphExecDestroy(g.exec);
             g.exec = nullptr;
+        }
+        // captured on the second sight of a key: a caller alternating inputs (or switches) keeps
+        // queueing directly instead of paying a capture per call
+        if (g.seen != key) {
+            g.seen = key;
+            return queue_round(r);
         }
         // the round's buffers exist after round 1 of this call; a reallocation while capturing would
         // change the generation: the graph is then dropped and the round queued directly

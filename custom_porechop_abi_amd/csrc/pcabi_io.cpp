@@ -108,13 +108,14 @@ struct pcabi_fastx {
     int txt_named = -1;            // pcabi_fastx_next_text: the last header had a name (1), none (0), no header (-1)
 };
 
-// Large batch buffers (>= 64 MB) come from anonymous mappings with transparent huge pages and
+// Large batch buffers (>= 8 MB, r05) come from anonymous mappings with transparent huge pages and
 // go back to a small process-wide cache when a batch is freed, so the next batch reuses pages
 // that are already faulted in: first-touch faults and the unmapping of gigabyte buffers cost
 // about as much as the parse itself (4 KB pages: ~400 k faults per 1.6 GB batch).
 namespace {
 namespace bigmem {
-constexpr size_t kBig = 64ull << 20;
+constexpr size_t kBig = 8ull << 20;   // r05: 64 MB left the buffers of 6 k-read batches to malloc, which
+                                      // maps and unmaps them per batch (e2e 3.5x slower at that size)
 // Free blocks kept for reuse: PCABI_IO_CACHE_MB, default min(4 GB, physical memory / 8) -- enough
 // for the batches a pipeline keeps in flight; pcabi_io_release_cache() returns them all.
 size_t cache_max() {

@@ -396,7 +396,7 @@ __global__ __launch_bounds__(256) void k_seed_scan_bits(ScanArgs a) {
 //     Q0 = 8-23, P1 = 16-31, Q1 = 24-39): position i's code is one bit-field extract of one of them;
 //   * a hit's 8-mer comes from the same packed words (no re-read of the read bytes).
 // 512-thread blocks: two blocks (16 waves) per CU share the CU's LDS between their byte maps.
-constexpr int kScanThreads = 512;
+constexpr int kScanThreads = 1024;
 constexpr int kByteMap = 1 << 16;            // bytes: one per 8-mer code
 
 // 4 bytes (base codes in their low 2 bits) -> 8 bits, byte 0's base in the top two: in the low byte
@@ -412,7 +412,10 @@ __device__ __forceinline__ uint32_t pack16(uint32_t x0, uint32_t x1, uint32_t x2
     return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
 }
 
-__global__ __launch_bounds__(kScanThreads) void k_seed_scan(ScanArgs a) {
+// TPB: threads per block (r05: 1024 -- two blocks per CU, each holding the 64 KiB map, run 32 waves
+// per CU instead of 16; PCABI_SCAN_THREADS=512 keeps the r04 blocks, A/B)
+template <int TPB>
+__global__ __launch_bounds__(TPB) void k_seed_scan(ScanArgs a) {
     // static LDS (a workgroup may hold more than 64 KiB of it on gfx950): the byte map -- a position's
     // code plus the map's constant LDS address is its read address
     __shared__ __attribute__((aligned(16))) uint32_t bmap[kByteMap / 4];
@@ -422,18 +425,19 @@ __global__ __launch_bounds__(kScanThreads) void k_seed_scan(ScanArgs a) {
         // 4m .. 4m + 3): the first bits from nibble m & 7 of word m >> 3, the second ones from the
         // 16-bit half m & 1 of word (m >> 1) & 2047 (bits 16m + 4j' .. + 3 for byte j'). Bitmap word w
         // covers map dwords 8w .. 8w + 7; a thread's words loaded together.
-        static_assert(kByteMap / 32 == 4 * kScanThreads, "four bitmap words per thread");
-        uint32_t word[4], half[4][4];
+        constexpr int kWpt = (kByteMap / 32) / TPB;        // bitmap words per thread
+        static_assert(kWpt * TPB == kByteMap / 32, "whole bitmap words per thread");
+        uint32_t word[kWpt], half[kWpt][4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int w = threadIdx.x + q * kScanThreads;
+        for (int q = 0; q < kWpt; ++q) {
+            const int w = threadIdx.x + q * TPB;
             word[q] = a.tabs[w];
 #pragma unroll
             for (int h = 0; h < 4; ++h) half[q][h] = a.tabs[(4 * w + h) & 2047];
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int w = threadIdx.x + q * kScanThreads;
+        for (int q = 0; q < kWpt; ++q) {
+            const int w = threadIdx.x + q * TPB;
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const uint32_t first = ((((word[q] >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u) * 0x55u;
@@ -450,7 +454,7 @@ __global__ __launch_bounds__(kScanThreads) void k_seed_scan(ScanArgs a) {
     const int64_t nr = dev_count(a.n_dev, a.n);
     const int64_t S = rfl64(a.seg_cum[nr]);
     const int lane = (int)(threadIdx.x & 63);
-    constexpr int kW = kScanThreads / 64;
+    constexpr int kW = TPB / 64;
     const int64_t nw = (int64_t)gridDim.x * kW;
     const int64_t gw = (int64_t)blockIdx.x * kW + (threadIdx.x >> 6);
     const int64_t lo = S * gw / nw, hi = S * (gw + 1) / nw;
@@ -1422,6 +1426,7 @@ struct State {
     int32_t n_adp = 0;
     int64_t cap = 0, ecap = 0, ccap = 0, raw_cap = 0;
     int scan_blocks = 0;                          // resident k_seed_scan blocks
+    int scan_tpb = kScanThreads;                  // their threads (PCABI_SCAN_THREADS=512: the r04 blocks)
     int n_slab = 0;                               // raw-hit slabs: one per byte-map scan wave (r03 scan: per block)
     bool bytemap = true;                          // k_seed_scan (byte map) or k_seed_scan_bits (r03)
     int expand_blocks = 0;                        // resident k_seed_expand blocks
@@ -1787,13 +1792,18 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
         const char *e = std::getenv("PCABI_SEED_BYTEMAP");   // 0: the r03 bitmap scan (A/B)
         s->bytemap = !(e && e[0] == '0');
         if (s->bytemap) {
-            SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_scan, kScanThreads, 0));
+            const char *et = std::getenv("PCABI_SCAN_THREADS");
+            s->scan_tpb = (et && std::atoi(et) == 512) ? 512 : kScanThreads;
+            if (s->scan_tpb == 512)
+                SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_scan<512>, 512, 0));
+            else
+                SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_scan<kScanThreads>, kScanThreads, 0));
         } else {
             SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_scan_bits, 256,
                                                                 4 * (size_t)s->a.bits_dw + 4));
         }
         s->scan_blocks = std::max(1, cus * std::max(1, per_cu));
-        s->n_slab = s->bytemap ? s->scan_blocks * (kScanThreads / 64) : s->scan_blocks;   // per wave / per block
+        s->n_slab = s->bytemap ? s->scan_blocks * (s->scan_tpb / 64) : s->scan_blocks;   // per wave / per block
         per_cu = 0;
         SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_expand, kExpandThreads, s->lds_bytes));
         s->expand_blocks = std::min(s->n_slab, std::max(1, cus * std::max(1, per_cu)));
@@ -1863,8 +1873,10 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
     hipLaunchKernelGGL(k_bound_reset, dim3(1024), dim3(256), 0, st, (int32_t *)s->bound.p, n, n_dev, n_adp, A.cnt,
                        kCntAll, (unsigned long long *)s->ccnt.p);
     if (s->pev) SD_TRY(hipEventRecord(s->pev[0], st));
-    if (s->bytemap)
-        hipLaunchKernelGGL(k_seed_scan, dim3(grid), dim3(kScanThreads), 0, st, A);
+    if (s->bytemap && s->scan_tpb == 512)
+        hipLaunchKernelGGL(k_seed_scan<512>, dim3(grid), dim3(512), 0, st, A);
+    else if (s->bytemap)
+        hipLaunchKernelGGL(k_seed_scan<kScanThreads>, dim3(grid), dim3(kScanThreads), 0, st, A);
     else
         hipLaunchKernelGGL(k_seed_scan_bits, dim3(grid), dim3(256), 4 * (size_t)A.bits_dw + 4, st, A);
     if (s->pev) SD_TRY(hipEventRecord(s->pev[1], st));

@@ -218,9 +218,11 @@ def record_boundaries(path, parts):
         L.pcabi_fastx_close(h)
 
 
-def read_batches(path, max_reads=100000, max_bases=1 << 30, raw=False, byte_range=None):
+def read_batches(path, max_reads=100000, max_bases=1 << 30, raw=False, byte_range=None, first_reads=None):
     """Stream a FASTA / FASTQ(.gz) file as ReadBatch objects (pcabi_fastx_next); byte_range =
-    (begin, end) record starts of a plain file (record_boundaries) reads only that range."""
+    (begin, end) record starts of a plain file (record_boundaries) reads only that range;
+    first_reads: the first batch's size, if other than max_reads (a pipeline starts its later
+    stages sooner on a small first batch)."""
     L = _declare(lib())
     h = ctypes.c_void_p()
     rc = L.pcabi_fastx_open(os.fsencode(path), int(raw), ctypes.byref(h))
@@ -230,9 +232,11 @@ def read_batches(path, max_reads=100000, max_bases=1 << 30, raw=False, byte_rang
         L.pcabi_fastx_close(h)
         raise ValueError(_open_error(path))
     try:
+        want = int(first_reads) if first_reads else int(max_reads)
         while True:
             b = ctypes.c_void_p()
-            n = L.pcabi_fastx_next(h, int(max_reads), int(max_bases), ctypes.byref(b))
+            n = L.pcabi_fastx_next(h, want, int(max_bases), ctypes.byref(b))
+            want = int(max_reads)
             if n < 0:
                 raise ValueError(_open_error(path))
             if n == 0:

@@ -103,6 +103,9 @@ class FileTrimmer(object):
         nbytes = max(int(nbytes), 16)
         if key not in self.dev or self.dev[key][1] < nbytes:
             if key in self.dev:
+                # grown with headroom: batches of varying size do not reallocate (a free waits for
+                # the device) every time one is a little larger than the last
+                nbytes = max(nbytes, self.dev[key][1] + self.dev[key][1] // 4)
                 self.L.pcabi_dev_free(self.dev[key][0])
             p = VP()
             check(self.L.pcabi_dev_malloc(ctypes.byref(p), nbytes), 'pcabi_dev_malloc')
