@@ -72,12 +72,14 @@ def _sorted(h):
     return h[:, np.lexsort((np.arange(h.shape[1]), h[0]))]
 
 
-def _dev_scan(L, views, adps, sc, thr, profile=None, calls=1, intact=None):
+def _dev_scan(L, views, adps, sc, thr, profile=None, calls=1, intact=None, stream=False):
     """A FRESH scan through the device ABI (pcabi_adapters_create_scored, pcabi_scan_create,
     pcabi_middle_scan_dev): its buffers are sized on this first use (PCABI_MIDDLE_INIT_CAPS).
     profile: a float64 array of 26 that receives pcabi_scan_profile's table of the call.
     calls: scans of the same device pack with the same scan object (every call's hits must agree);
-    intact: a list that receives, per call, whether the device pack is byte-identical afterwards."""
+    intact: a list that receives, per call, whether the device pack is byte-identical afterwards;
+    stream: on a library stream instead of the legacy one (rounds after a call's first are then
+    captured into graphs on the third call and replayed from the fourth)."""
     from custom_porechop_abi_amd import _lib, engine
     vp = ctypes.c_void_p
     codes, offs, lens = views
@@ -93,9 +95,11 @@ def _dev_scan(L, views, adps, sc, thr, profile=None, calls=1, intact=None):
 
     d_codes, d_off, d_len = h2d(codes), h2d(offs.astype(np.int64)), h2d(lens.astype(np.int32))
     c, o, ln = engine.encode_adapters(adps)
-    tab, scan = vp(), vp()
+    tab, scan, st = vp(), vp(), vp()
     _lib.check(L.pcabi_adapters_create_scored(c.ctypes.data_as(vp), o.ctypes.data_as(vp), ln.ctypes.data_as(vp),
                                               len(adps), *sc, ctypes.byref(tab)), 'adapters')
+    if stream:
+        _lib.check(L.pcabi_stream_create(ctypes.byref(st)), 'stream')
     try:
         _lib.check(L.pcabi_scan_create(tab, ctypes.byref(scan)), 'scan_create')
         cap = 8 * len(lens) + 1024
@@ -107,7 +111,7 @@ def _dev_scan(L, views, adps, sc, thr, profile=None, calls=1, intact=None):
         for _ in range(calls):
             hits[:] = 0
             nh = L.pcabi_middle_scan_dev(scan, d_codes, d_off, d_len, h_len.ctypes.data_as(vp), len(lens), *sc,
-                                         float(thr), hits.ctypes.data_as(vp), cap, None)
+                                         float(thr), hits.ctypes.data_as(vp), cap, st if stream else None)
             if nh < 0:
                 _lib.check(int(nh), 'pcabi_middle_scan_dev')
             assert nh <= cap
@@ -128,6 +132,8 @@ def _dev_scan(L, views, adps, sc, thr, profile=None, calls=1, intact=None):
         if scan.value:
             L.pcabi_scan_destroy(scan)
         L.pcabi_adapters_destroy(tab)
+        if st.value:
+            L.pcabi_stream_destroy(st)
         for p in held:
             L.pcabi_dev_free(p)
 
@@ -344,6 +350,22 @@ def test_seed_expand_one_pass(gpu_lib, monkeypatch, thr):
     n1, flags = _requeues(gpu_lib)
     assert n1 > n0 and flags & 2, (n1 - n0, flags)
     assert np.array_equal(_sorted(got), exp)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('windows', ['0', '1'])
+def test_round_graphs_replay(gpu_lib, monkeypatch, reads_8kb, windows):
+    """Rounds after a call's first, captured into graphs (the third call of a key) and replayed (the
+    fourth and fifth), on a library stream: every call equals the oracle, with and without candidate
+    windows, and equals the same scans with graphs off (PCABI_MIDDLE_GRAPHS=0)."""
+    views, exp = reads_8kb
+    monkeypatch.setenv('PCABI_MIDDLE_SEEDS', '2')
+    monkeypatch.setenv('PCABI_MIDDLE_WINDOWS', windows)
+    got = _dev_scan(gpu_lib, views, ADPS, SC, 90.0, calls=5, stream=True)
+    assert np.array_equal(_sorted(got), exp)
+    monkeypatch.setenv('PCABI_MIDDLE_GRAPHS', '0')
+    off = _dev_scan(gpu_lib, views, ADPS, SC, 90.0, calls=2, stream=True)
+    assert np.array_equal(got, off)
 
 
 @pytest.mark.gpu
