@@ -147,7 +147,9 @@ void *get(size_t bytes) {
         cache.erase(cache.begin() + (long)bi);
         return p;
     }
-    const size_t m = round2m(bytes);
+    // 1/8 headroom: the next batch's buffers, sized exactly and a little larger or smaller than
+    // these, still fit a cached block (already faulted in) instead of a fresh mapping
+    const size_t m = round2m(bytes + bytes / 8);
     void *p = mmap(nullptr, m, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
     if (p == MAP_FAILED) throw std::bad_alloc();
 #ifdef MADV_HUGEPAGE
@@ -410,7 +412,10 @@ void populate_ahead(pcabi_fastx *r, size_t at, size_t end) {
     volatile unsigned sink = 0;
     const char *m = (const char *)r->map;
     while (!r->ahead_stop.load(std::memory_order_relaxed) && at < end) {
-        const size_t lim = r->reader_at.load(std::memory_order_relaxed) + kAhead;
+        const size_t rd = r->reader_at.load(std::memory_order_relaxed);
+        at = std::max(at, rd & ~(size_t)4095);        // never behind the reader (its pages are mapped)
+        if (at >= end) break;
+        const size_t lim = rd + kAhead;
         if (at >= lim) {
             std::this_thread::sleep_for(std::chrono::microseconds(200));
             continue;
@@ -699,6 +704,12 @@ int64_t pcabi_fastx_next(pcabi_fastx *r, int64_t max_reads, int64_t max_bases, p
     int64_t bases = 0;
     const char *p;
     size_t n;
+    // PCABI_IOPROF=1: per batch, the record scan's and the fill's milliseconds on stderr
+    static const bool ioprof = [] {
+        const char *e = std::getenv("PCABI_IOPROF");
+        return e && e[0] == '1';
+    }();
+    const auto t_scan = std::chrono::steady_clock::now();
     if (r->type == PCABI_FASTQ) {
         std::vector<Span> rec;
         r->pin = r->pos;                 // the batch's bytes survive refills (shifted with the pin)
@@ -734,7 +745,14 @@ int64_t pcabi_fastx_next(pcabi_fastx *r, int64_t max_reads, int64_t max_bases, p
             rec.push_back(sp);
             bases += (int64_t)sp.sn;
         }
+        const auto t_fill = std::chrono::steady_clock::now();
         fill_fastq(b, r->base + r->pin, rec, r->raw);
+        if (ioprof) {
+            const auto t_end = std::chrono::steady_clock::now();
+            std::fprintf(stderr, "[pcabi io] batch %zu reads: scan %.2f ms, fill %.2f ms\n", rec.size(),
+                         std::chrono::duration<double, std::milli>(t_fill - t_scan).count(),
+                         std::chrono::duration<double, std::milli>(t_end - t_fill).count());
+        }
         r->pin = (size_t)-1;
     } else {
         while (b->n < max_reads && bases < max_bases) {
