@@ -1125,8 +1125,20 @@ def run_drivers(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
     d2h = {}
     real = engine.end_decisions
 
+    eng_t = {}
+    real_mid = engine.middle_scan_seqs
+
+    def timed_mid(*a, **kw):                # the middle driver's library call (staging + scan)
+        t = time.perf_counter()
+        try:
+            return real_mid(*a, **kw)
+        finally:
+            eng_t['middle_scan_seqs'] = eng_t.get('middle_scan_seqs', 0.0) + time.perf_counter() - t
+
     def counted(*a, **kw):                  # the end-trim driver's device -> host bytes
+        t = time.perf_counter()
         st, et, sl, el, bcf = real(*a, **kw)
+        eng_t['end_decisions'] = eng_t.get('end_decisions', 0.0) + time.perf_counter() - t
         # pcabi_end_decisions_host's transfer (windows < 32 k, < 32 k adapters): the trims, the two
         # alignment counts, per side 12 B per alignment (six int16 fields) + 2 B per read (counts),
         # the barcode identities
@@ -1147,8 +1159,10 @@ def run_drivers(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
             times[k] = times.get(k, 0.0) + v
 
     engine.end_decisions = counted
+    engine.middle_scan_seqs = timed_mid
     try:
         drivers([NanoporeRead('r%d' % i, s, '') for i, s in enumerate(seqs[:2000])], {})   # warm-up
+        eng_t.clear()
         times = {}
         build = 0.0
         for _ in range(args.steps):
@@ -1158,6 +1172,7 @@ def run_drivers(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
             drivers(reads, times)
     finally:
         engine.end_decisions = real
+        engine.middle_scan_seqs = real_mid
     total = sum(times.values()) / args.steps
     checked = None
     k = min(args.drivers_check, n)
@@ -1193,6 +1208,9 @@ def run_drivers(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
             'value': round(n / total, 1), 'unit': 'reads/s', 'steps': args.steps, 'ms_per_step': round(1e3 * total, 2),
             'ms_per_driver': {k: round(1e3 * v / args.steps, 2) for k, v in times.items()},
             'nanopore_read_objects_ms': round(1e3 * build / args.steps, 1),
+            # inside the drivers: the library calls (engine.end_decisions -- window pack excluded --
+            # and engine.middle_scan_seqs: host staging, PCIe and the scan)
+            'library_call_ms': {k: round(1e3 * v / args.steps, 2) for k, v in eng_t.items()},
             'end_trim_d2h_bytes_per_100k_reads': int(d2h.get('bytes', 0) * 100000 / max(n, 1)),
             'dtype': 'int32', 'data': 'synthetic (seeded ONT-like reads, mean %d bp)' % args.mean_len,
             'config': {'workload': 'porechop_abi.find_matching_adapter_sets (first 10k reads x %d sets) + '

@@ -1605,8 +1605,8 @@ struct Engine {
     DeviceBuf dec[17];
     // pcabi_middle_scan_seqs: pinned staging slots the host strings are encoded into while the
     // previous slots' copies run (allocated on first use, kept)
-    uint8_t *stage[3] = {nullptr, nullptr, nullptr};
-    hipEvent_t stage_ev[3] = {nullptr, nullptr, nullptr};
+    uint8_t *stage[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t stage_ev[4] = {nullptr, nullptr, nullptr, nullptr};
     struct DTab {
         std::vector<uint8_t> codes;
         std::vector<int32_t> lens;
@@ -2054,7 +2054,7 @@ int64_t middle_scan_resident(Engine &e, const int64_t *win_off, const int32_t *w
 
 // Host strings -> Dna5 codes in e.codes: the layout's bytes [0, total) in chunks of kStageBytes,
 // each encoded by the worker threads (S/basic/alphabet_residue_tabs.h's table, as
-// pcabi_encode_dna5) into one of three pinned slots and copied to the device on e.stream while
+// pcabi_encode_dna5) into one of four pinned slots and copied to the device on e.stream while
 // the workers encode the next ones. A slot is refilled once its copy has completed. Nothing is
 // written to pageable memory, so the 10^8-byte batches cost neither page faults nor the
 // runtime's staging copy.
@@ -2070,11 +2070,14 @@ int stage_seqs(Engine &e, const char *const *seqs, const int32_t *len, const int
             t['T'] = t['t'] = t['U'] = t['u'] = 3;
         }
     } tab;
-    for (int k = 0; k < 3; ++k) {
+    constexpr int kSlots = 4;
+    for (int k = 0; k < kSlots; ++k) {
         if (!e.stage[k]) {
             HIP_TRY(hipHostMalloc((void **)&e.stage[k], (size_t)kStageBytes, hipHostMallocDefault));
             HIP_TRY(hipEventCreateWithFlags(&e.stage_ev[k], hipEventDisableTiming));
         }
+        // a call that failed after staging may have left copies out of a slot in flight
+        HIP_TRY(hipEventSynchronize(e.stage_ev[k]));
     }
     // bytes [b0, b1) of the layout into dst
     auto encode = [&](int64_t b0, int64_t b1, uint8_t *dst) {
@@ -2097,12 +2100,15 @@ int stage_seqs(Engine &e, const char *const *seqs, const int32_t *len, const int
             ++w;
         }
     };
+    // r05: the workers encode, this thread only queues the copies, and a slot is waited for only
+    // when a worker needs it again (kSlots - 1 chunks later): the copies run back to back. (r04:
+    // this thread encoded a share too and waited out each chunk's copy before encoding the next.)
     const int64_t n_chunk = (total + kStageBytes - 1) / kStageBytes;
     const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({16, (int64_t)std::thread::hardware_concurrency(),
                                                                  total / (1 << 20)}));
     std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[(size_t)n_chunk]);
     for (int64_t c = 0; c < n_chunk; ++c) left[c].store(nt);
-    std::atomic<int64_t> free_upto{std::min<int64_t>(3, n_chunk)};   // chunks below it may be encoded
+    std::atomic<int64_t> free_upto{std::min<int64_t>(kSlots, n_chunk)};   // chunks below it may be encoded
     std::atomic<bool> stop{false};
     auto work = [&](int t) {
         for (int64_t c = 0; c < n_chunk; ++c) {
@@ -2111,32 +2117,36 @@ int stage_seqs(Engine &e, const char *const *seqs, const int32_t *len, const int
             if (stop.load(std::memory_order_relaxed)) return;
             const int64_t c0 = c * kStageBytes, c1 = std::min(total, c0 + kStageBytes);
             const int64_t b0 = c0 + (c1 - c0) * t / nt, b1 = c0 + (c1 - c0) * (t + 1) / nt;
-            if (b0 < b1) encode(b0, b1, e.stage[c % 3] + (b0 - c0));
+            if (b0 < b1) encode(b0, b1, e.stage[c % kSlots] + (b0 - c0));
             left[c].fetch_sub(1, std::memory_order_release);
         }
     };
     std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
+    for (int t = 0; t < nt; ++t) th.emplace_back(work, t);
     int rc = 0;
     std::string err;
-    // thread 0 is this one: its share of a chunk, then the chunk's copy once every share is in
+    int64_t freed = std::min<int64_t>(kSlots, n_chunk);   // chunks [0, freed) have a slot
     for (int64_t c = 0; c < n_chunk && !rc; ++c) {
-        const int64_t c0 = c * kStageBytes, c1 = std::min(total, c0 + kStageBytes);
-        const int64_t b1 = c0 + (c1 - c0) / nt;
-        if (c0 < b1) encode(c0, b1, e.stage[c % 3]);
-        left[c].fetch_sub(1, std::memory_order_release);
         while (left[c].load(std::memory_order_acquire) > 0) std::this_thread::yield();
-        hipError_t he = hipMemcpyAsync((uint8_t *)e.codes.p + c0, e.stage[c % 3], (size_t)(c1 - c0),
+        const int64_t c0 = c * kStageBytes, c1 = std::min(total, c0 + kStageBytes);
+        hipError_t he = hipMemcpyAsync((uint8_t *)e.codes.p + c0, e.stage[c % kSlots], (size_t)(c1 - c0),
                                        hipMemcpyHostToDevice, e.stream);
-        if (he == hipSuccess) he = hipEventRecord(e.stage_ev[c % 3], e.stream);
-        // chunk c + 3 reuses this slot: once this copy is done (the next two chunks encode meanwhile)
-        if (he == hipSuccess && c + 3 < n_chunk) he = hipEventSynchronize(e.stage_ev[c % 3]);
+        if (he == hipSuccess) he = hipEventRecord(e.stage_ev[c % kSlots], e.stream);
+        // hand the workers the slot of the oldest copy still queued once it has landed, keeping
+        // kSlots - 1 chunks queued or being encoded behind it
+        const int64_t oldest = c - (kSlots - 2);
+        if (he == hipSuccess && oldest >= 0 && freed < n_chunk) {
+            he = hipEventSynchronize(e.stage_ev[oldest % kSlots]);
+            if (he == hipSuccess) {
+                freed = std::min<int64_t>(n_chunk, oldest + kSlots);
+                free_upto.store(freed, std::memory_order_release);
+            }
+        }
         if (he != hipSuccess) {
             rc = PCABI_E_DEVICE;
             err = std::string("pcabi_middle_scan_seqs: staging copy: ") + hipGetErrorString(he);
             break;
         }
-        free_upto.store(std::min<int64_t>(n_chunk, c + 4), std::memory_order_release);
     }
     stop.store(true);
     for (auto &t : th) t.join();

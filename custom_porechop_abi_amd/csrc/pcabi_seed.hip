@@ -405,6 +405,10 @@ __device__ __forceinline__ uint32_t pack4(uint32_t d) {
     const uint32_t v = (t << 2) | (t >> 8);          // byte 0: b0 b1, byte 2: b2 b3
     return (v << 4) | (v >> 16);                     // byte 0: b0 b1 b2 b3
 }
+// the same byte with one dot product: byte k's code times 64 >> 2k (the N code's bit 2 masked first)
+__device__ __forceinline__ uint32_t pack4_dot(uint32_t d) {
+    return __builtin_amdgcn_udot4(d & 0x03030303u, 0x01041040u, 0u, false);
+}
 // four packed bytes (low bytes of x0..x3) -> one word, x0 in the top byte
 __device__ __forceinline__ uint32_t pack16(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
     const uint32_t hi = __builtin_amdgcn_perm(x0, x1, 0x0C0C0400u);   // byte 1: x0, byte 0: x1
@@ -415,7 +419,7 @@ __device__ __forceinline__ uint32_t pack16(uint32_t x0, uint32_t x1, uint32_t x2
 // TPB: threads per block (r05: 1024 -- two blocks per CU, each holding the 64 KiB map, run 32 waves
 // per CU instead of 16; PCABI_SCAN_THREADS=512 keeps the r04 blocks, A/B)
 template <int TPB>
-__global__ __launch_bounds__(TPB) void k_seed_scan(ScanArgs a) {
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB == 1024 ? 8 : 4))) void k_seed_scan(ScanArgs a) {
     // static LDS (a workgroup may hold more than 64 KiB of it on gfx950): the byte map -- a position's
     // code plus the map's constant LDS address is its read address
     __shared__ __attribute__((aligned(16))) uint32_t bmap[kByteMap / 4];
@@ -456,8 +460,10 @@ __global__ __launch_bounds__(TPB) void k_seed_scan(ScanArgs a) {
     const int lane = (int)(threadIdx.x & 63);
     constexpr int kW = TPB / 64;
     const int64_t nw = (int64_t)gridDim.x * kW;
-    const int64_t gw = (int64_t)blockIdx.x * kW + (threadIdx.x >> 6);
-    const int64_t lo = S * gw / nw, hi = S * (gw + 1) / nw;
+    // the wave's index, read as wave-uniform so its bounds and slab live in SGPRs (r05: as a lane
+    // value they cost a 64-bit division per lane and, at 64 VGPRs, two spilled registers)
+    const int64_t gw = (int64_t)blockIdx.x * kW + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t lo = rfl64(S * gw / nw), hi = rfl64(S * (gw + 1) / nw);
     // one slab per WAVE (its own running count: no LDS atomic), so the expansion has 8x the slabs
     // to spread over its blocks
     uint4 *slab = a.raw + gw * a.slab;
@@ -483,20 +489,21 @@ __global__ __launch_bounds__(TPB) void k_seed_scan(ScanArgs a) {
                 mn = read_meta(a, rc + 1, nr, S);
             }
         };
-        auto map = [&](int64_t b, int64_t &r, int &p, int64_t &off, int &len) -> bool {
+        auto map = [&](int64_t b, int32_t &r, int &p, int64_t &off, int &len) -> bool {
             const int64_t sg = b + lane;
             if (sg >= hi) return false;
             if (sg < mc.s1) {
-                r = rc; p = (int)(sg - s0c) * kSeg; off = mc.off; len = mc.len;
+                r = (int32_t)rc; p = (int)(sg - s0c) * kSeg; off = mc.off; len = mc.len;
             } else if (sg < mn.s1) {
-                r = rc + 1; p = (int)(sg - mc.s1) * kSeg; off = mn.off; len = mn.len;
+                r = (int32_t)rc + 1; p = (int)(sg - mc.s1) * kSeg; off = mn.off; len = mn.len;
             } else {
-                r = rc + 2;
-                int64_t e = a.seg_cum[r + 1];
-                while (e <= sg) e = a.seg_cum[++r + 1];
-                p = (int)(sg - a.seg_cum[r]) * kSeg;
-                off = a.v_off[r];
-                len = a.v_len[r];
+                int64_t rr = rc + 2;
+                int64_t e = a.seg_cum[rr + 1];
+                while (e <= sg) e = a.seg_cum[++rr + 1];
+                r = (int32_t)rr;
+                p = (int)(sg - a.seg_cum[rr]) * kSeg;
+                off = a.v_off[rr];
+                len = a.v_len[rr];
             }
             return true;
         };
@@ -513,7 +520,7 @@ __global__ __launch_bounds__(TPB) void k_seed_scan(ScanArgs a) {
         };
         struct Seg {
             uint32_t d[10];
-            int64_t rd;
+            int32_t rd;                                // the round's read (< 2^31 reads a round)
             int p, len;
             bool act;
         };
@@ -529,12 +536,17 @@ __global__ __launch_bounds__(TPB) void k_seed_scan(ScanArgs a) {
         // lane 63's prefix); a lane without a segment contributes no hit
         auto process = [&](const Seg &g) {
             const uint32_t (&d)[10] = g.d;
-            const int64_t crd = g.rd;
+            const int32_t crd = g.rd;
             const int cp = g.p, clen = g.len;
             // ---- the segment's 32 positions: packed codes, one extract + one byte-map read each ----
-            const uint32_t P0 = pack16(pack4(d[0]), pack4(d[1]), pack4(d[2]), pack4(d[3]));
-            const uint32_t P1 = pack16(pack4(d[4]), pack4(d[5]), pack4(d[6]), pack4(d[7]));
-            const uint32_t P2 = __builtin_amdgcn_perm(pack4(d[8]), pack4(d[9]), 0x04000C0Cu);   // bases 32-39 on top
+            // (r05: 4 bases -> a byte with one v_dot4_u32_u8 of the masked codes against 64/16/4/1 --
+            // 2 VALU per dword instead of 5)
+            uint32_t v[10];
+#pragma unroll
+            for (int t = 0; t < 10; ++t) v[t] = pack4_dot(d[t]);
+            const uint32_t P0 = (((v[0] << 8) | v[1]) << 16) | (v[2] << 8) | v[3];
+            const uint32_t P1 = (((v[4] << 8) | v[5]) << 16) | (v[6] << 8) | v[7];
+            const uint32_t P2 = ((v[8] << 8) | v[9]) << 16;                  // bases 32-39 on top
             const uint32_t Q0 = __builtin_amdgcn_alignbit(P0, P1, 16);   // bases 8-23
             const uint32_t Q1 = __builtin_amdgcn_alignbit(P1, P2, 16);   // bases 24-39
             // (the reads of 16 positions issued together: LDS latency, not issue, is the risk at the
@@ -544,6 +556,11 @@ __global__ __launch_bounds__(TPB) void k_seed_scan(ScanArgs a) {
             // half the LDS reads and bank-conflict cycles, ~58 % of the LDS array's time before; the
             // scan's time did not move, r05u / r05v: it is not LDS-bound, nor load-depth-bound -- a
             // third segment in flight per lane was measured neutral too)
+            // r05: the selecting bases (i + 8 for even i = bases 8, 10, .., 38) doubled in place,
+            // one per nibble of X0 (bases 8-22) / X1 (24-38), base 8 on top: pair k's field offset
+            // is X >> (28 - 4 (k & 7)), whose low 5 bits -- all v_bfe_u32 reads of an offset -- are
+            // the nibble and a zero bit. 3 VALU per pair (shift, bfe, shift-or) instead of ~5.5.
+            const uint32_t X0 = (Q0 >> 1) & 0x66666666u, X1 = (Q1 >> 1) & 0x66666666u;
             uint32_t hits = 0;
 #pragma unroll
             for (int h = 0; h < kSeg; h += 16) {
@@ -557,9 +574,8 @@ __global__ __launch_bounds__(TPB) void k_seed_scan(ScanArgs a) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const int i = h + 2 * j;
-                    const uint32_t src = i < 8 ? P0 : i < 16 ? Q0 : i < 24 ? P1 : Q1;
-                    const uint32_t b2 = (src >> (13 - 2 * (i & 7))) & 6u;    // 2 x the base at i + 8
-                    hits |= ((m[j] >> b2) & 3u) << i;
+                    const uint32_t x = h < 16 ? X0 : X1;
+                    hits |= __builtin_amdgcn_ubfe(m[j], x >> (28 - 4 * j), 2u) << i;
                 }
             }
             // ---- validity: N bytes and the read end (as k_seed_scan_bits) ----
