@@ -1208,7 +1208,7 @@ def run_drivers(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
             'value': round(n / total, 1), 'unit': 'reads/s', 'steps': args.steps, 'ms_per_step': round(1e3 * total, 2),
             'ms_per_driver': {k: round(1e3 * v / args.steps, 2) for k, v in times.items()},
             'nanopore_read_objects_ms': round(1e3 * build / args.steps, 1),
-            # inside the drivers: the library calls (engine.end_decisions -- window pack excluded --
+            # inside the drivers: the library calls (engine.end_decisions -- the windows gathered there --
             # and engine.middle_scan_seqs: host staging, PCIe and the scan)
             'library_call_ms': {k: round(1e3 * v / args.steps, 2) for k, v in eng_t.items()},
             'end_trim_d2h_bytes_per_100k_reads': int(d2h.get('bytes', 0) * 100000 / max(n, 1)),

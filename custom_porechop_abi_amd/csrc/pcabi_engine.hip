@@ -1929,7 +1929,8 @@ int64_t middle_scan_resident(Engine &e, const int64_t *win_off, const int32_t *w
                              const uint8_t *adp_codes, const int32_t *adp_off, const int32_t *adp_len, int32_t n_adp,
                              int match, int mismatch, int gap_open, int gap_extend, double threshold, int32_t *hits,
                              int64_t cap);
-int stage_seqs(Engine &e, const char *const *seqs, const int32_t *len, const int64_t *off, int64_t n, int64_t total);
+int stage_seqs(Engine &e, uint8_t *dst, const char *const *seqs, const int32_t *len, const int64_t *off, int64_t n,
+               int64_t total);
 }  // namespace
 
 extern "C" {
@@ -2019,7 +2020,7 @@ int64_t pcabi_middle_scan_seqs(int device, const char *const *seqs, const int32_
     if (int rc = engine_init(e, device)) return rc;
     HIP_TRY(hipSetDevice(device));
     if (int rc = e.codes.ensure((size_t)total)) return rc;
-    if (int rc = stage_seqs(e, seqs, seq_len, off.data(), n, total)) return rc;
+    if (int rc = stage_seqs(e, (uint8_t *)e.codes.p, seqs, seq_len, off.data(), n, total)) return rc;
     return middle_scan_resident(e, off.data(), seq_len, n, adp_codes, adp_off, adp_len, n_adp, match, mismatch,
                                 gap_open, gap_extend, threshold, hits, cap);
 }
@@ -2052,14 +2053,15 @@ int64_t middle_scan_resident(Engine &e, const int64_t *win_off, const int32_t *w
     return r;
 }
 
-// Host strings -> Dna5 codes in e.codes: the layout's bytes [0, total) in chunks of kStageBytes,
+// Host strings -> Dna5 codes at dst (device): the layout's bytes [0, total) in chunks of kStageBytes,
 // each encoded by the worker threads (S/basic/alphabet_residue_tabs.h's table, as
 // pcabi_encode_dna5) into one of four pinned slots and copied to the device on e.stream while
 // the workers encode the next ones. A slot is refilled once its copy has completed. Nothing is
 // written to pageable memory, so the 10^8-byte batches cost neither page faults nor the
 // runtime's staging copy.
 constexpr int64_t kStageBytes = 32 << 20;
-int stage_seqs(Engine &e, const char *const *seqs, const int32_t *len, const int64_t *off, int64_t n, int64_t total) {
+int stage_seqs(Engine &e, uint8_t *dst, const char *const *seqs, const int32_t *len, const int64_t *off, int64_t n,
+               int64_t total) {
     static const struct Tab {
         uint8_t t[256];
         Tab() {
@@ -2129,7 +2131,7 @@ int stage_seqs(Engine &e, const char *const *seqs, const int32_t *len, const int
     for (int64_t c = 0; c < n_chunk && !rc; ++c) {
         while (left[c].load(std::memory_order_acquire) > 0) std::this_thread::yield();
         const int64_t c0 = c * kStageBytes, c1 = std::min(total, c0 + kStageBytes);
-        hipError_t he = hipMemcpyAsync((uint8_t *)e.codes.p + c0, e.stage[c % kSlots], (size_t)(c1 - c0),
+        hipError_t he = hipMemcpyAsync(dst + c0, e.stage[c % kSlots], (size_t)(c1 - c0),
                                        hipMemcpyHostToDevice, e.stream);
         if (he == hipSuccess) he = hipEventRecord(e.stage_ev[c % kSlots], e.stream);
         // hand the workers the slot of the oldest copy still queued once it has landed, keeping
@@ -4307,14 +4309,18 @@ int side_table(Engine::DTab &c, const uint8_t *codes, const int32_t *off, const 
 
 }  // namespace
 
-extern "C" int pcabi_end_decisions_host(
-    int device, const uint8_t *codes, int64_t codes_len, const int64_t *s_off, const int32_t *s_len,
-    const int64_t *e_off, const int32_t *e_len, int64_t n_read, const uint8_t *sa_codes, const int32_t *sa_off,
-    const int32_t *sa_len, int32_t n_sa, const uint8_t *ea_codes, const int32_t *ea_off, const int32_t *ea_len,
-    int32_t n_ea, int match, int mismatch, int gap_open, int gap_extend, int end_size, int extra_trim,
-    double end_threshold, int min_trim_size, int32_t *start_trim, int32_t *end_trim, int32_t *start_hits,
-    int32_t *end_hits, int64_t cap, int64_t *n_hits, const int32_t *bc_s, int32_t n_bc_s, const int32_t *bc_e,
-    int32_t n_bc_e, double *bc_full) {
+namespace {
+// pcabi_end_decisions_host / _seqs: the windows' codes come from `codes` (a host Dna5 buffer) or,
+// when `win` is set, from the 2 n_read window strings (start windows, then end windows), encoded
+// straight into pinned staging buffers while earlier chunks copy (stage_seqs)
+int end_decisions_impl(
+    int device, const uint8_t *codes, const char *const *win, const int32_t *win_len, int64_t codes_len,
+    const int64_t *s_off, const int32_t *s_len, const int64_t *e_off, const int32_t *e_len, int64_t n_read,
+    const uint8_t *sa_codes, const int32_t *sa_off, const int32_t *sa_len, int32_t n_sa, const uint8_t *ea_codes,
+    const int32_t *ea_off, const int32_t *ea_len, int32_t n_ea, int match, int mismatch, int gap_open, int gap_extend,
+    int end_size, int extra_trim, double end_threshold, int min_trim_size, int32_t *start_trim, int32_t *end_trim,
+    int32_t *start_hits, int32_t *end_hits, int64_t cap, int64_t *n_hits, const int32_t *bc_s, int32_t n_bc_s,
+    const int32_t *bc_e, int32_t n_bc_e, double *bc_full) {
     if (device < 0 || device >= 16) return fail(PCABI_E_ARG, "bad device index");
     if (n_read < 0 || n_sa < 0 || n_ea < 0 || cap < 0 || n_bc_s < 0 || n_bc_e < 0) return fail(PCABI_E_ARG, "negative count");
     if (int rc = check_common(sa_len, n_sa)) return rc;
@@ -4334,6 +4340,14 @@ extern "C" int pcabi_end_decisions_host(
         if (bc_e[j] < 0 || bc_e[j] >= n_ea) return fail(PCABI_E_ARG, "end barcode adapter out of range");
     n_hits[0] = n_hits[1] = 0;
     if (n_read == 0) return 0;
+    // PCABI_END_PROF=1: the call's host / device phases on stderr
+    static const bool prof = [] { const char *v = std::getenv("PCABI_END_PROF"); return v && v[0] == '1'; }();
+    const auto t0 = std::chrono::steady_clock::now();
+    auto mark = [&](const char *what) {
+        if (prof)
+            std::fprintf(stderr, "pcabi_end_decisions: %-10s %.3f ms\n", what,
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    };
     Engine &e = g_engines[device];
     std::lock_guard<std::mutex> lock(e.mu);
     if (int rc = engine_init(e, device)) return rc;
@@ -4345,7 +4359,15 @@ extern "C" int pcabi_end_decisions_host(
     // buffers: 0 codes; per side (base 1 + 6 side): offsets, lengths, tile offsets, tiles, results, flags;
     // 13 trims (2 x n); 14 lists (2 sides x 7 x n_read x n_adp bound); 15 counts + barcode identities
     if (int rc = e.dec[0].ensure((size_t)codes_len)) return rc;
-    HIP_TRY(hipMemcpyAsync(e.dec[0].p, codes, (size_t)codes_len, hipMemcpyHostToDevice, st));
+    if (win) {
+        std::vector<int64_t> off(2 * n);
+        std::copy(s_off, s_off + n, off.begin());
+        std::copy(e_off, e_off + n, off.begin() + (int64_t)n);
+        if (int rc = stage_seqs(e, (uint8_t *)e.dec[0].p, win, win_len, off.data(), 2 * n_read, codes_len)) return rc;
+    } else {
+        HIP_TRY(hipMemcpyAsync(e.dec[0].p, codes, (size_t)codes_len, hipMemcpyHostToDevice, st));
+    }
+    mark("staged");
     if (int rc = e.dec[13].ensure(8 * n)) return rc;
     int32_t *d_st = (int32_t *)e.dec[13].p, *d_et = d_st + n;
     std::vector<int64_t> toff[2];
@@ -4391,7 +4413,7 @@ extern "C" int pcabi_end_decisions_host(
     if (int rc = e.dec[14].ensure(4 * 7 * (dcap[0] + dcap[1]) + 16)) return rc;
     int32_t *d_list[2] = {(int32_t *)e.dec[14].p, (int32_t *)e.dec[14].p + 7 * dcap[0]};
     const size_t nbc = (size_t)n_bc_s + (size_t)n_bc_e;
-    if (int rc = e.dec[15].ensure(64 + 4 * nbc + 8 * nbc * n)) return rc;
+    if (int rc = e.dec[15].ensure(64 + ((4 * nbc + 7) & ~(size_t)7) + 8 * nbc * n)) return rc;   // d_full below
     unsigned long long *d_cnt = (unsigned long long *)e.dec[15].p;
     int32_t *d_sel = (int32_t *)((char *)e.dec[15].p + 16);
     double *d_full = (double *)((char *)e.dec[15].p + 64 + ((4 * nbc + 7) & ~(size_t)7));
@@ -4422,8 +4444,10 @@ extern "C" int pcabi_end_decisions_host(
     unsigned long long cnt[2] = {0, 0};
     HIP_TRY(hipMemcpyAsync(start_trim, d_st, 4 * n, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(end_trim, d_et, 4 * n, hipMemcpyDeviceToHost, st));
+    mark("queued");
     HIP_TRY(hipMemcpyAsync(cnt, d_cnt, 16, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    mark("device");
     n_hits[0] = (int64_t)cnt[0];
     n_hits[1] = (int64_t)cnt[1];
     // the lists: compact (int16 fields, per-read counts) when every field fits 16 bits -- the
@@ -4455,6 +4479,7 @@ extern "C" int pcabi_end_decisions_host(
         HIP_TRY(hipGetLastError());
         if (words) HIP_TRY(hipMemcpyAsync(h.data(), e.dec[16].p, 4 * words, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
+        mark("lists d2h");
         for (int side = 0; side < 2; ++side) {
             int32_t *dst = side ? end_hits : start_hits;
             const int64_t k = (int64_t)cnt[side];
@@ -4467,6 +4492,7 @@ extern "C" int pcabi_end_decisions_host(
             for (int f = 0; f < 6; ++f)
                 for (int64_t q = 0; q < k; ++q) dst[(f + 1) * cap + q] = f16[f * k + q];
         }
+        mark("unpacked");
         return 0;
     }
     for (int side = 0; side < 2; ++side) {
@@ -4478,4 +4504,47 @@ extern "C" int pcabi_end_decisions_host(
     }
     HIP_TRY(hipStreamSynchronize(st));
     return 0;
+}
+}  // namespace
+
+extern "C" int pcabi_end_decisions_host(
+    int device, const uint8_t *codes, int64_t codes_len, const int64_t *s_off, const int32_t *s_len,
+    const int64_t *e_off, const int32_t *e_len, int64_t n_read, const uint8_t *sa_codes, const int32_t *sa_off,
+    const int32_t *sa_len, int32_t n_sa, const uint8_t *ea_codes, const int32_t *ea_off, const int32_t *ea_len,
+    int32_t n_ea, int match, int mismatch, int gap_open, int gap_extend, int end_size, int extra_trim,
+    double end_threshold, int min_trim_size, int32_t *start_trim, int32_t *end_trim, int32_t *start_hits,
+    int32_t *end_hits, int64_t cap, int64_t *n_hits, const int32_t *bc_s, int32_t n_bc_s, const int32_t *bc_e,
+    int32_t n_bc_e, double *bc_full) {
+    return end_decisions_impl(device, codes, nullptr, nullptr, codes_len, s_off, s_len, e_off, e_len, n_read, sa_codes,
+                              sa_off, sa_len, n_sa, ea_codes, ea_off, ea_len, n_ea, match, mismatch, gap_open,
+                              gap_extend, end_size, extra_trim, end_threshold, min_trim_size, start_trim, end_trim,
+                              start_hits, end_hits, cap, n_hits, bc_s, n_bc_s, bc_e, n_bc_e, bc_full);
+}
+
+// pcabi_end_decisions_host over window strings: win / win_len hold the n_read start windows, then
+// the n_read end windows (addresses of their first characters -- ASCII, one byte per base -- and
+// lengths); the library lays them out as the host entry's buffer and encodes them itself.
+extern "C" int pcabi_end_decisions_seqs(
+    int device, const char *const *win, const int32_t *win_len, int64_t n_read, const uint8_t *sa_codes,
+    const int32_t *sa_off, const int32_t *sa_len, int32_t n_sa, const uint8_t *ea_codes, const int32_t *ea_off,
+    const int32_t *ea_len, int32_t n_ea, int match, int mismatch, int gap_open, int gap_extend, int end_size,
+    int extra_trim, double end_threshold, int min_trim_size, int32_t *start_trim, int32_t *end_trim,
+    int32_t *start_hits, int32_t *end_hits, int64_t cap, int64_t *n_hits, const int32_t *bc_s, int32_t n_bc_s,
+    const int32_t *bc_e, int32_t n_bc_e, double *bc_full) {
+    if (n_read < 0) return fail(PCABI_E_ARG, "negative count");
+    const int64_t nw = 2 * n_read;
+    std::vector<int64_t> off((size_t)nw);
+    int64_t total = 0;
+    for (int64_t w = 0; w < nw; ++w) {
+        if (win_len[w] < 0 || win_len[w] > pcabi::MAX_WINDOW_LEN) return fail(PCABI_E_ARG, "window length out of range");
+        if (win_len[w] > 0 && !win[w]) return fail(PCABI_E_ARG, "NULL sequence");
+        off[(size_t)w] = total;
+        total += ((int64_t)win_len[w] + 3) & ~(int64_t)3;
+    }
+    total += 16;
+    return end_decisions_impl(device, nullptr, win, win_len, total, off.data(), win_len, off.data() + n_read,
+                              win_len + n_read, n_read, sa_codes, sa_off, sa_len, n_sa, ea_codes, ea_off, ea_len, n_ea,
+                              match, mismatch, gap_open, gap_extend, end_size, extra_trim, end_threshold, min_trim_size,
+                              start_trim, end_trim, start_hits, end_hits, cap, n_hits, bc_s, n_bc_s, bc_e, n_bc_e,
+                              bc_full);
 }

@@ -120,13 +120,13 @@ class SeqPack(object):
         return joined.encode('ascii'), offs, lens.astype(np.int32)
 
     @classmethod
-    def windows(cls, seqs, starts, lengths, index=None, bufs=None):
+    def windows(cls, seqs, starts, lengths, index=None, bufs=None, lazy=False):
         """The pack of [seqs[k][a:a + l] for k, a, l in zip(index, starts, lengths)] (index
         defaults to every sequence once; same layout as SeqPack of those slices) without making
         them: for ASCII str the codes are gathered from the strs' own buffers by
         pcabi_encode_dna5_gather (one byte per base, so character positions are byte positions).
         `starts` / `lengths` must lie inside each sequence. bufs: str_buffers(seqs) when the caller
-        has it already."""
+        has it already. lazy: for ASCII str, a StrWindows (the same layout, not yet gathered) instead."""
         starts = np.asarray(starts, np.int64)
         lengths = np.asarray(lengths, np.int64)
         idx = np.arange(len(seqs)) if index is None else np.asarray(index, np.int64)
@@ -145,6 +145,8 @@ class SeqPack(object):
         offs = np.zeros(n, np.int64)
         np.cumsum((lengths + ((-lengths) & 3))[:-1], out=offs[1:])
         total = int(offs[-1] + lengths[-1] + ((-lengths[-1]) & 3)) + PAD
+        if lazy:
+            return StrWindows(seqs, addr, lengths, offs, total)
         self = cls.__new__(cls)
         self.codes = np.empty(total, np.uint8)
         lib().pcabi_encode_dna5_gather(_ptr(addr), _ptr(lengths), _ptr(offs), n, _ptr(self.codes), total)
@@ -162,6 +164,32 @@ class SeqPack(object):
         starts = np.asarray(starts, dtype=np.int64)
         lengths = np.asarray(lengths, dtype=np.int32)
         return self.codes, self.offsets[idx] + starts, lengths
+
+
+class StrWindows(object):
+    """A window pack not made yet: the windows as addresses into ASCII strs (str_buffers) and
+    lengths, at SeqPack.windows' offsets. engine.end_decisions hands the addresses to the library,
+    which gathers and encodes them into pinned staging buffers itself (pcabi_end_decisions_seqs);
+    np.asarray(w) makes the Dna5 pack for anything that needs the bytes. `codes` is the object
+    itself, so it stands where a SeqPack's codes buffer goes; it keeps `seqs` (the strs) alive."""
+
+    def __init__(self, seqs, addr, lengths, offsets, total):
+        self.seqs = seqs
+        self.addr = np.ascontiguousarray(addr, np.uint64)
+        self._lens64 = np.ascontiguousarray(lengths, np.int64)
+        self.lengths = self._lens64.astype(np.int32)
+        self.offsets = np.ascontiguousarray(offsets, np.int64)
+        self.size = int(total)
+        self.codes = self
+
+    def __len__(self):
+        return self.size
+
+    def __array__(self, dtype=None, copy=None):
+        codes = np.empty(self.size, np.uint8)
+        lib().pcabi_encode_dna5_gather(_ptr(self.addr), _ptr(self._lens64), _ptr(self.offsets), len(self.lengths),
+                                       _ptr(codes), self.size)
+        return codes if dtype is None else codes.astype(dtype, copy=False)
 
 
 def start_end_windows(pack, end_size):
@@ -330,17 +358,24 @@ def end_decisions(codes, start_windows, end_windows, start_seqs, end_seqs, scori
     """find_start_trim / find_end_trim for a batch of reads on the GPU (pcabi_end_decisions_host,
     porechop_abi/nanopore_read.py:175-217): only the decisions come back, never the result matrix.
 
-    codes: one Dna5 buffer holding both window sets; start_windows / end_windows: (offsets int64,
-    lengths int32). Returns (start_trim int32[n], end_trim int32[n], start_list, end_list,
+    codes: one Dna5 buffer holding both window sets, or the StrWindows they are views of (start
+    windows, then end windows: pcabi_end_decisions_seqs); start_windows / end_windows: (offsets
+    int64, lengths int32). Returns (start_trim int32[n], end_trim int32[n], start_list, end_list,
     bc_full): each list is int32 (7, k) -- read, adapter, rs, re (inclusive), m, l1, l2 -- of the
     alignments the reference records, read-major in adapter order; bc_full is float64
     (len(bc_start) + len(bc_end), n) full identities of the listed adapters (None without them)."""
-    codes = np.ascontiguousarray(codes, dtype=np.uint8)
     s_off = np.ascontiguousarray(start_windows[0], dtype=np.int64)
     s_len = np.ascontiguousarray(start_windows[1], dtype=np.int32)
     e_off = np.ascontiguousarray(end_windows[0], dtype=np.int64)
     e_len = np.ascontiguousarray(end_windows[1], dtype=np.int32)
     n = len(s_len)
+    # window strings (StrWindows: start windows then end windows, the views its own) go to the
+    # library as addresses; anything else as a Dna5 buffer
+    strs = isinstance(codes, StrWindows) and len(codes.lengths) == 2 * n and \
+        np.array_equal(codes.offsets, np.concatenate([s_off, e_off])) and \
+        np.array_equal(codes.lengths, np.concatenate([s_len, e_len]))
+    if not strs:
+        codes = np.ascontiguousarray(codes, dtype=np.uint8)
     sa, so, sl = encode_adapters(start_seqs)
     ea, eo, el = encode_adapters(end_seqs)
     bs = np.ascontiguousarray(bc_start if bc_start is not None else [], dtype=np.int32)
@@ -355,13 +390,21 @@ def end_decisions(codes, start_windows, end_windows, start_seqs, end_seqs, scori
         sh = np.zeros((7, cap), np.int32)
         eh = np.zeros((7, cap), np.int32)
         cnt = np.zeros(2, np.int64)
-        rc = lib().pcabi_end_decisions_host(device, _ptr(codes), codes.size, _ptr(s_off), _ptr(s_len), _ptr(e_off),
-                                            _ptr(e_len), n, _ptr(sa), _ptr(so), _ptr(sl), len(sl), _ptr(ea), _ptr(eo),
-                                            _ptr(el), len(el), m, mm, go, ge, int(end_size), int(extra_trim),
-                                            float(end_threshold), int(min_trim_size), _ptr(st), _ptr(et), _ptr(sh),
-                                            _ptr(eh), cap, _ptr(cnt), _ptr(bs), len(bs), _ptr(be), len(be),
-                                            _ptr(bc_full))
-        check(rc, 'pcabi_end_decisions_host')
+        if strs:
+            rc = lib().pcabi_end_decisions_seqs(device, _ptr(codes.addr), _ptr(codes.lengths), n, _ptr(sa), _ptr(so),
+                                                _ptr(sl), len(sl), _ptr(ea), _ptr(eo), _ptr(el), len(el), m, mm, go, ge,
+                                                int(end_size), int(extra_trim), float(end_threshold),
+                                                int(min_trim_size), _ptr(st), _ptr(et), _ptr(sh), _ptr(eh), cap,
+                                                _ptr(cnt), _ptr(bs), len(bs), _ptr(be), len(be), _ptr(bc_full))
+            check(rc, 'pcabi_end_decisions_seqs')
+        else:
+            rc = lib().pcabi_end_decisions_host(device, _ptr(codes), codes.size, _ptr(s_off), _ptr(s_len),
+                                                _ptr(e_off), _ptr(e_len), n, _ptr(sa), _ptr(so), _ptr(sl), len(sl),
+                                                _ptr(ea), _ptr(eo), _ptr(el), len(el), m, mm, go, ge, int(end_size),
+                                                int(extra_trim), float(end_threshold), int(min_trim_size), _ptr(st),
+                                                _ptr(et), _ptr(sh), _ptr(eh), cap, _ptr(cnt), _ptr(bs), len(bs),
+                                                _ptr(be), len(be), _ptr(bc_full))
+            check(rc, 'pcabi_end_decisions_host')
         if cnt.max() <= cap:
             return st, et, sh[:, :cnt[0]], eh[:, :cnt[1]], bc_full
         cap = int(cnt.max())

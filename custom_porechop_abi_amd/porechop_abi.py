@@ -227,10 +227,11 @@ def find_adapters_at_read_ends(reads, matching_sets, verbosity, end_size, extra_
         print('', file=print_dest)
 
 
-def end_windows_pack(reads, end_size):
+def end_windows_pack(reads, end_size, lazy=False):
     """The reads' start and end windows, seq[:end_size] and seq[-end_size:] as the reference slices
     them (nanopore_read.py:181, 203), packed into one Dna5 buffer: (codes, start views, end views)
-    -- only the 2 x end_size bases per read travel, not the whole reads."""
+    -- only the 2 x end_size bases per read travel, not the whole reads. lazy: `codes` may be an
+    engine.StrWindows (the windows as addresses into the reads' strs; the library encodes them)."""
     n = len(reads)
     seqs = _attrs(reads, 'seq')
     bufs = engine.str_buffers(seqs)
@@ -240,7 +241,7 @@ def end_windows_pack(reads, end_size):
     e_start = np.zeros(n, np.int64) if e == 0 else (np.maximum(ln - e, 0) if e > 0 else np.minimum(-e, ln))
     pack = SeqPack.windows(seqs, np.concatenate([np.zeros(n, np.int64), e_start]),
                            np.concatenate([s_len, ln - e_start]), index=np.tile(np.arange(n), 2),
-                           bufs=bufs)   # seq[-e:]
+                           bufs=bufs, lazy=lazy)   # seq[-e:]
     return pack.codes, (pack.offsets[:n], pack.lengths[:n]), (pack.offsets[n:], pack.lengths[n:])
 
 
@@ -293,7 +294,7 @@ def _end_decisions_batch(reads, starts, ends, end_size, extra, thr, scoring_sche
     with -b -- the barcode identities come back): trim amounts, the start / end alignment lists in
     the reference's order (read, then set order) and the barcode dicts. Distinct sequences are
     aligned once; a list entry is made for every set holding the sequence."""
-    codes, sw, ew = end_windows_pack(reads, end_size)
+    codes, sw, ew = end_windows_pack(reads, end_size, lazy=True)
     s_u, s_idx = _unique([a.start_sequence[1] for a in starts])
     e_u, e_idx = _unique([a.end_sequence[1] for a in ends])
     bc = [[k for k, a in enumerate(sets) if check_barcodes and a.is_barcode() and a.barcode_direction() == fwd_rev]

@@ -264,6 +264,21 @@ int pcabi_end_decisions_host(int device, const uint8_t *codes, int64_t codes_len
                              int32_t *start_hits, int32_t *end_hits, int64_t cap, int64_t *n_hits,
                              const int32_t *bc_s, int32_t n_bc_s, const int32_t *bc_e, int32_t n_bc_e,
                              double *bc_full);
+/*
+ * pcabi_end_decisions_seqs: the same decisions from the window STRINGS (the reference's
+ * seq[:end_size] / seq[-end_size:] slices, nanopore_read.py:181, 203, never made): win[2 n_read]
+ * the address of each window's first character (ASCII, one byte per base -- start windows, then
+ * end windows), win_len[2 n_read] its length. The library lays them out as pcabi_end_decisions_host's
+ * buffer and encodes them itself into pinned staging buffers while earlier chunks copy.
+ */
+int pcabi_end_decisions_seqs(int device, const char *const *win, const int32_t *win_len, int64_t n_read,
+                             const uint8_t *sa_codes, const int32_t *sa_off, const int32_t *sa_len, int32_t n_sa,
+                             const uint8_t *ea_codes, const int32_t *ea_off, const int32_t *ea_len, int32_t n_ea,
+                             int match, int mismatch, int gap_open, int gap_extend, int end_size, int extra_trim,
+                             double end_threshold, int min_trim_size, int32_t *start_trim, int32_t *end_trim,
+                             int32_t *start_hits, int32_t *end_hits, int64_t cap, int64_t *n_hits,
+                             const int32_t *bc_s, int32_t n_bc_s, const int32_t *bc_e, int32_t n_bc_e,
+                             double *bc_full);
 int pcabi_flag_list_dev(const uint8_t *flag, int32_t n_adp, int64_t n_read, const int32_t *res, int64_t stride,
                         int32_t *out, int64_t cap, unsigned long long *n_out, void *stream);
 

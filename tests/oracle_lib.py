@@ -217,6 +217,7 @@ def end_decisions_windows(codes, start_windows, end_windows, start_seqs, end_seq
     restated over them, the recorded alignments as (read, adapter, rs, re, m, l1, l2) lists in the
     reference's order, and the listed adapters' full identities."""
     from custom_porechop_abi_amd.engine import pid6
+    codes = np.asarray(codes, np.uint8)             # an engine.StrWindows is gathered here
     n = len(start_windows[1])
     trims, lists, fulls = [], [], []
     for side, (win, seqs, sel) in enumerate(((start_windows, start_seqs, bc_start), (end_windows, end_seqs, bc_end))):

@@ -151,6 +151,71 @@ def test_per_read_methods_on_gpu(gpu_lib, case_name):
         assert r.middle_hit_str == exp['middle_hit_str']
 
 
+def _edge_reads(seed=7, n=3000):
+    """Random reads with the window edge cases: empty reads, reads shorter than the window, N /
+    lowercase / U bases, adapters planted at both ends."""
+    import random
+    from custom_porechop_abi_amd import adapters as A
+    rng = random.Random(seed)
+    ad = [a for a in A.fresh_adapters() if '(full sequence)' not in a.name][:8]
+    out = []
+    for i in range(n):
+        k = rng.choice([0, 1, 3, 40, 149, 150, 151, 300, 2000])
+        s = ''.join(rng.choice('ACGTACGTNacgtU') for _ in range(k))
+        if k >= 150 and rng.random() < 0.5:
+            a = rng.choice(ad)
+            s = (a.start_sequence[1] if a.start_sequence else '') + s + (a.end_sequence[1] if a.end_sequence else '')
+        out.append(s)
+    return out, ad
+
+
+def test_lazy_end_windows_match_pack():
+    """engine.StrWindows (the window strings as addresses, pcabi_end_decisions_seqs' input) lays
+    the windows out as the eager pack does, and np.asarray of it gathers the same bytes."""
+    import numpy as np
+    from custom_porechop_abi_amd import engine, porechop_abi as P
+    from custom_porechop_abi_amd.nanopore_read import NanoporeRead
+    seqs, _ = _edge_reads(n=500)
+    reads = [NanoporeRead('r%d' % i, s, '') for i, s in enumerate(seqs)]
+    for e in (150, 40, 0, -20):
+        codes, sw, ew = P.end_windows_pack(reads, e)
+        lz, lsw, lew = P.end_windows_pack(reads, e, lazy=True)
+        assert isinstance(lz, engine.StrWindows)
+        for a, b in zip(sw + ew, lsw + lew):
+            assert np.array_equal(a, b)
+        assert np.array_equal(np.asarray(lz), codes)
+
+
+@pytest.mark.gpu
+def test_end_decisions_from_strings_on_gpu(gpu_lib):
+    """pcabi_end_decisions_seqs (window strings, encoded by the library into pinned staging) ==
+    pcabi_end_decisions_host (the packed Dna5 buffer) field for field, on reads with the window
+    edge cases, and both == the CPU oracle on a slice."""
+    import numpy as np
+    from custom_porechop_abi_amd import engine, porechop_abi as P
+    from custom_porechop_abi_amd.nanopore_read import NanoporeRead
+    seqs, ad = _edge_reads()
+    reads = [NanoporeRead('r%d' % i, s, '') for i, s in enumerate(seqs)]
+    starts = [a.start_sequence[1] for a in ad if a.start_sequence]
+    ends = [a.end_sequence[1] for a in ad if a.end_sequence]
+    sc = [3, -6, -5, -2]
+    for e in (150, 40):
+        lz, sw, ew = P.end_windows_pack(reads, e, lazy=True)
+        codes = np.asarray(lz)
+        args = (sw, ew, starts, ends, sc, e, 2, 75.0, 4)
+        got = engine.end_decisions(lz, *args, bc_start=np.arange(2), bc_end=np.arange(1))
+        exp = engine.end_decisions(codes, *args, bc_start=np.arange(2), bc_end=np.arange(1))
+        for g, x in zip(got, exp):
+            assert np.array_equal(g, x)
+        k = 300
+        sub = [NanoporeRead('r%d' % i, s, '') for i, s in enumerate(seqs[:k])]
+        lz2, sw2, ew2 = P.end_windows_pack(sub, e, lazy=True)
+        ora = oracle_lib.end_decisions_windows(lz2, sw2, ew2, starts, ends, sc, e, 2, 75.0, 4)
+        gpu = engine.end_decisions(lz2, sw2, ew2, starts, ends, sc, e, 2, 75.0, 4)
+        for g, x in zip(gpu[:4], ora[:4]):
+            assert np.array_equal(np.asarray(g, np.int64), np.asarray(x, np.int64))
+
+
 @pytest.mark.gpu
 def test_middle_cut_ranges_on_device(gpu_lib):
     """pcabi_middle_cuts (the device epilogue of the middle scan) == NanoporeRead._apply_middle_hit's
