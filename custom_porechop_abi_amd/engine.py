@@ -353,6 +353,9 @@ def best_full_identity(windows, adapter_seqs, scoring_scheme_vals, best=None, de
     return out
 
 
+_END_LIST_RATIO = [4.0]
+
+
 def end_decisions(codes, start_windows, end_windows, start_seqs, end_seqs, scoring_scheme_vals, end_size, extra_trim,
                   end_threshold, min_trim_size, bc_start=None, bc_end=None, device=0):
     """find_start_trim / find_end_trim for a batch of reads on the GPU (pcabi_end_decisions_host,
@@ -384,11 +387,14 @@ def end_decisions(codes, start_windows, end_windows, start_seqs, end_seqs, scori
     et = np.zeros(n, np.int32)
     nb = len(bs) + len(be)
     bc_full = np.zeros((nb, n), np.float64) if nb else None
-    cap = 2 * n + 1024
+    # list capacity from the most alignments per read seen so far (a call whose lists overflow runs
+    # again -- the whole decision, ~half the driver's library time, r05); the lists are np.empty:
+    # only the columns written are ever touched, so headroom costs address space, not time
+    cap = int(n * _END_LIST_RATIO[0] * 1.25) + 1024
     m, mm, go, ge = (int(x) for x in scoring_scheme_vals[:4])
     while True:
-        sh = np.zeros((7, cap), np.int32)
-        eh = np.zeros((7, cap), np.int32)
+        sh = np.empty((7, cap), np.int32)
+        eh = np.empty((7, cap), np.int32)
         cnt = np.zeros(2, np.int64)
         if strs:
             rc = lib().pcabi_end_decisions_seqs(device, _ptr(codes.addr), _ptr(codes.lengths), n, _ptr(sa), _ptr(so),
@@ -405,6 +411,8 @@ def end_decisions(codes, start_windows, end_windows, start_seqs, end_seqs, scori
                                                 _ptr(et), _ptr(sh), _ptr(eh), cap, _ptr(cnt), _ptr(bs), len(bs),
                                                 _ptr(be), len(be), _ptr(bc_full))
             check(rc, 'pcabi_end_decisions_host')
+        if n:
+            _END_LIST_RATIO[0] = max(_END_LIST_RATIO[0], float(cnt.max()) / n)
         if cnt.max() <= cap:
             return st, et, sh[:, :cnt[0]], eh[:, :cnt[1]], bc_full
         cap = int(cnt.max())
