@@ -107,6 +107,7 @@ def lib():
                                       c_p, c_p, c_p, ctypes.c_int32, c_int, c_int, c_int, c_int, c_int, c_int, c_d,
                                       c_int, c_p, c_p, c_p, c_p, c_i64, c_p, c_p, ctypes.c_int32, c_p,
                                       ctypes.c_int32, c_p], c_int),
+        'pcabi_stage_seqs_host': ([c_int, c_p, c_p, c_i64, c_p, c_i64], c_int),
         'pcabi_end_decisions_seqs': ([c_int, c_p, c_p, c_i64, c_p, c_p, c_p, ctypes.c_int32, c_p, c_p, c_p,
                                       ctypes.c_int32, c_int, c_int, c_int, c_int, c_int, c_int, c_d, c_int, c_p, c_p,
                                       c_p, c_p, c_i64, c_p, c_p, ctypes.c_int32, c_p, ctypes.c_int32, c_p], c_int),
@@ -143,7 +144,7 @@ def exported_symbols():
             'pcabi_compat_all_vs_all_host', 'pcabi_kmer_count_host', 'pcabi_kmer_top_host', 'pcabi_gather_host',
             'pcabi_kmer_approx_host', 'pcabi_io_release_cache', 'pcabi_best_full_identity_host',
             'pcabi_middle_cuts_dev', 'pcabi_middle_cuts_host', 'pcabi_fastx_record_start', 'pcabi_fastx_set_range', 'pcabi_fastx_next_text',
-            'pcabi_end_decisions_host', 'pcabi_end_decisions_seqs', 'pcabi_flag_list_dev', 'pcabi_trim_views_dev']
+            'pcabi_end_decisions_host', 'pcabi_end_decisions_seqs', 'pcabi_stage_seqs_host', 'pcabi_flag_list_dev', 'pcabi_trim_views_dev']
 
 
 def check(rc, what):

@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <immintrin.h>
+
 #include <algorithm>
 #include <chrono>
 #include <atomic>
@@ -1607,6 +1609,7 @@ struct Engine {
     // previous slots' copies run (allocated on first use, kept)
     uint8_t *stage[4] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t stage_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    DeviceBuf stage_dev;          // the slots' device copies (2-bit codes + N masks), unpacked into place
     struct DTab {
         std::vector<uint8_t> codes;
         std::vector<int32_t> lens;
@@ -1996,6 +1999,31 @@ int64_t pcabi_middle_scan_host(int device, const uint8_t *codes, int64_t codes_l
                                 gap_open, gap_extend, threshold, hits, cap);
 }
 
+int pcabi_stage_seqs_host(int device, const char *const *seqs, const int32_t *seq_len, int64_t n, uint8_t *out,
+                          int64_t out_len) {
+    if (device < 0 || device >= 16) return fail(PCABI_E_ARG, "bad device index");
+    if (n < 0) return fail(PCABI_E_ARG, "negative count");
+    int64_t total = 0;
+    std::vector<int64_t> off((size_t)n);
+    for (int64_t w = 0; w < n; ++w) {
+        if (seq_len[w] < 0 || seq_len[w] > pcabi::MAX_WINDOW_LEN) return fail(PCABI_E_ARG, "window length out of range");
+        if (seq_len[w] > 0 && !seqs[w]) return fail(PCABI_E_ARG, "NULL sequence");
+        off[(size_t)w] = total;
+        total += ((int64_t)seq_len[w] + 3) & ~(int64_t)3;
+    }
+    total += 16;
+    if (out_len < total) return fail(PCABI_E_ARG, "output buffer smaller than the layout");
+    Engine &e = g_engines[device];
+    std::lock_guard<std::mutex> lock(e.mu);
+    if (int rc = engine_init(e, device)) return rc;
+    HIP_TRY(hipSetDevice(device));
+    if (int rc = e.codes.ensure((size_t)total)) return rc;
+    if (int rc = stage_seqs(e, (uint8_t *)e.codes.p, seqs, seq_len, off.data(), n, total)) return rc;
+    HIP_TRY(hipMemcpyAsync(out, e.codes.p, (size_t)total, hipMemcpyDeviceToHost, e.stream));
+    HIP_TRY(hipStreamSynchronize(e.stream));
+    return 0;
+}
+
 int64_t pcabi_middle_scan_seqs(int device, const char *const *seqs, const int32_t *seq_len, int64_t n,
                                const uint8_t *adp_codes, const int32_t *adp_off, const int32_t *adp_len,
                                int32_t n_adp, int match, int mismatch, int gap_open, int gap_extend,
@@ -2053,58 +2081,123 @@ int64_t middle_scan_resident(Engine &e, const int64_t *win_off, const int32_t *w
     return r;
 }
 
-// Host strings -> Dna5 codes at dst (device): the layout's bytes [0, total) in chunks of kStageBytes,
-// each encoded by the worker threads (S/basic/alphabet_residue_tabs.h's table, as
-// pcabi_encode_dna5) into one of four pinned slots and copied to the device on e.stream while
-// the workers encode the next ones. A slot is refilled once its copy has completed. Nothing is
-// written to pageable memory, so the 10^8-byte batches cost neither page faults nor the
-// runtime's staging copy.
+// Host strings -> Dna5 codes at dst (device): the layout's bytes [0, total) in chunks of kStageBytes.
+// r05: what crosses PCIe is 3 bits a base, not 8 -- each chunk travels as 2-bit codes (base j of
+// a 32-base block at bits 2j of its 8 bytes) plus a 1-bit "not A/C/G/T/U" mask (bit j of the
+// block's 32-bit word), k_unpack_codes writes the Dna5 bytes (S/basic/alphabet_residue_tabs.h's
+// table, as pcabi_encode_dna5: A/a 0, C/c 1, G/g 2, T/t/U/u 3, anything else N = 4) into dst.
+// The worker threads gather their share of a chunk's characters (the windows' own bytes, N
+// between them) into a thread-local block and encode it with AVX2 (a scalar loop without it) into
+// one of four pinned slots; this thread queues each chunk's two copies and its unpack on e.stream
+// and waits for a slot only when a worker needs it again. Nothing is written to pageable memory.
 constexpr int64_t kStageBytes = 32 << 20;
+constexpr int64_t kStageCodes = kStageBytes / 4, kStageMask = kStageBytes / 8, kStageSlot = kStageCodes + kStageMask;
+
+__global__ __launch_bounds__(256) void k_unpack_codes(const uint32_t *__restrict__ codes, const uint32_t *__restrict__ mask,
+                                                      uint8_t *__restrict__ dst, int64_t n) {
+    // 16 bases a thread: one dword of codes, half a mask word, one 16-byte store
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t b = 16 * q;
+    if (b >= n) return;
+    const uint32_t c = codes[q];
+    const uint32_t m = (mask[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int i = 4 * k + j;
+            const uint32_t v = (m >> i) & 1u ? 4u : (c >> (2 * i)) & 3u;
+            x |= v << (8 * j);
+        }
+        w[k] = x;
+    }
+    if (b + 16 <= n) {
+        *reinterpret_cast<uint4 *>(dst + b) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+        for (int64_t i = b; i < n; ++i) dst[i] = (uint8_t)(w[(i - b) >> 2] >> (8 * ((i - b) & 3)));
+    }
+}
+
+// 32 characters -> 8 bytes of 2-bit codes + the 32-bit N mask (the scalar and AVX2 forms agree)
+inline void pack32_scalar(const uint8_t *s, uint8_t *codes, uint32_t *mask) {
+    uint64_t c = 0;
+    uint32_t m = 0;
+    for (int j = 0; j < 32; ++j) {
+        const uint8_t u = s[j] & 0xDF;
+        uint32_t v = 4;
+        if (u == 'A') v = 0;
+        else if (u == 'C') v = 1;
+        else if (u == 'G') v = 2;
+        else if (u == 'T' || u == 'U') v = 3;
+        if (v == 4) m |= 1u << j;
+        else c |= (uint64_t)v << (2 * j);
+    }
+    std::memcpy(codes, &c, 8);
+    *mask = m;
+}
+__attribute__((target("avx2"))) void pack_avx2(const uint8_t *s, int64_t nblk, uint8_t *codes, uint32_t *mask) {
+    const __m256i df = _mm256_set1_epi8((char)0xDF);
+    const __m256i kA = _mm256_set1_epi8('A'), kC = _mm256_set1_epi8('C'), kG = _mm256_set1_epi8('G');
+    const __m256i kT = _mm256_set1_epi8('T'), kU = _mm256_set1_epi8('U');
+    const __m256i one = _mm256_set1_epi8(1), two = _mm256_set1_epi8(2), three = _mm256_set1_epi8(3);
+    const __m256i m14 = _mm256_set1_epi16(0x0401);             // bytes (1, 4): c0 + 4 c1
+    const __m256i m116 = _mm256_set1_epi32(0x00100001);        // words (1, 16)
+    const __m256i sh = _mm256_setr_epi8(0, 4, 8, 12, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1,
+                                        0, 4, 8, 12, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1);
+    const __m256i perm = _mm256_setr_epi32(0, 4, 1, 1, 1, 1, 1, 1);
+    for (int64_t b = 0; b < nblk; ++b) {
+        const __m256i u = _mm256_and_si256(_mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + 32 * b)), df);
+        const __m256i eA = _mm256_cmpeq_epi8(u, kA), eC = _mm256_cmpeq_epi8(u, kC), eG = _mm256_cmpeq_epi8(u, kG);
+        const __m256i eT = _mm256_or_si256(_mm256_cmpeq_epi8(u, kT), _mm256_cmpeq_epi8(u, kU));
+        const __m256i code = _mm256_or_si256(_mm256_or_si256(_mm256_and_si256(eC, one), _mm256_and_si256(eG, two)),
+                                             _mm256_and_si256(eT, three));
+        const __m256i ok = _mm256_or_si256(_mm256_or_si256(eA, eC), _mm256_or_si256(eG, eT));
+        mask[b] = ~(uint32_t)_mm256_movemask_epi8(ok);
+        const __m256i p2 = _mm256_maddubs_epi16(code, m14);      // per 16 bits: c0 | c1 << 2
+        const __m256i p4 = _mm256_madd_epi16(p2, m116);          // per 32 bits: c0 .. c3 in the low byte
+        const __m256i g = _mm256_permutevar8x32_epi32(_mm256_shuffle_epi8(p4, sh), perm);
+        _mm_storel_epi64(reinterpret_cast<__m128i *>(codes + 8 * b), _mm256_castsi256_si128(g));
+    }
+}
+
 int stage_seqs(Engine &e, uint8_t *dst, const char *const *seqs, const int32_t *len, const int64_t *off, int64_t n,
                int64_t total) {
-    static const struct Tab {
-        uint8_t t[256];
-        Tab() {
-            for (int c = 0; c < 256; ++c) t[c] = 4;
-            t['A'] = t['a'] = 0;
-            t['C'] = t['c'] = 1;
-            t['G'] = t['g'] = 2;
-            t['T'] = t['t'] = t['U'] = t['u'] = 3;
-        }
-    } tab;
     constexpr int kSlots = 4;
     for (int k = 0; k < kSlots; ++k) {
         if (!e.stage[k]) {
-            HIP_TRY(hipHostMalloc((void **)&e.stage[k], (size_t)kStageBytes, hipHostMallocDefault));
+            HIP_TRY(hipHostMalloc((void **)&e.stage[k], (size_t)kStageSlot, hipHostMallocDefault));
             HIP_TRY(hipEventCreateWithFlags(&e.stage_ev[k], hipEventDisableTiming));
         }
         // a call that failed after staging may have left copies out of a slot in flight
         HIP_TRY(hipEventSynchronize(e.stage_ev[k]));
     }
-    // bytes [b0, b1) of the layout into dst
-    auto encode = [&](int64_t b0, int64_t b1, uint8_t *dst) {
+    if (int rc = e.stage_dev.ensure((size_t)(kSlots * kStageSlot))) return rc;
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    // characters [b0, b1) of the layout into raw (windows' bytes, 'N' between them)
+    auto gather = [&](int64_t b0, int64_t b1, uint8_t *raw) {
         int64_t w = std::upper_bound(off, off + n, b0) - off - 1;
         int64_t b = b0;
         while (b < b1) {
+            if (w >= n) {
+                std::memset(raw + (b - b0), 'N', (size_t)(b1 - b));
+                break;
+            }
             const int64_t s = off[w], t = s + len[w], nx = w + 1 < n ? off[w + 1] : total;
             if (b < t) {
                 const int64_t hi = std::min(t, b1);
-                const uint8_t *src = reinterpret_cast<const uint8_t *>(seqs[w]) + (b - s);
-                uint8_t *d = dst + (b - b0);
-                for (int64_t k = 0, m = hi - b; k < m; ++k) d[k] = tab.t[src[k]];
+                std::memcpy(raw + (b - b0), seqs[w] + (b - s), (size_t)(hi - b));
                 b = hi;
             }
             const int64_t hi = std::min(nx, b1);
             if (b < hi) {
-                std::memset(dst + (b - b0), 4, (size_t)(hi - b));
+                std::memset(raw + (b - b0), 'N', (size_t)(hi - b));
                 b = hi;
             }
             ++w;
         }
     };
-    // r05: the workers encode, this thread only queues the copies, and a slot is waited for only
-    // when a worker needs it again (kSlots - 1 chunks later): the copies run back to back. (r04:
-    // this thread encoded a share too and waited out each chunk's copy before encoding the next.)
     const int64_t n_chunk = (total + kStageBytes - 1) / kStageBytes;
     const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({16, (int64_t)std::thread::hardware_concurrency(),
                                                                  total / (1 << 20)}));
@@ -2113,13 +2206,28 @@ int stage_seqs(Engine &e, uint8_t *dst, const char *const *seqs, const int32_t *
     std::atomic<int64_t> free_upto{std::min<int64_t>(kSlots, n_chunk)};   // chunks below it may be encoded
     std::atomic<bool> stop{false};
     auto work = [&](int t) {
+        constexpr int64_t kBlk = 256 << 10;                    // characters gathered at a time (L2-resident)
+        std::unique_ptr<uint8_t[]> raw(new uint8_t[kBlk + 32]);
         for (int64_t c = 0; c < n_chunk; ++c) {
             while (free_upto.load(std::memory_order_acquire) <= c && !stop.load(std::memory_order_relaxed))
                 std::this_thread::yield();
             if (stop.load(std::memory_order_relaxed)) return;
             const int64_t c0 = c * kStageBytes, c1 = std::min(total, c0 + kStageBytes);
-            const int64_t b0 = c0 + (c1 - c0) * t / nt, b1 = c0 + (c1 - c0) * (t + 1) / nt;
-            if (b0 < b1) encode(b0, b1, e.stage[c % kSlots] + (b0 - c0));
+            // the thread's share: 32-base blocks of the chunk (the last one may run past c1: 'N')
+            const int64_t nb = (c1 - c0 + 31) / 32;
+            const int64_t k0 = nb * t / nt, k1 = nb * (t + 1) / nt;
+            uint8_t *slot = e.stage[c % kSlots];
+            for (int64_t k = k0; k < k1; k += kBlk / 32) {
+                const int64_t ke = std::min(k1, k + kBlk / 32);
+                const int64_t b0 = c0 + 32 * k, b1 = std::min(c1, c0 + 32 * ke);
+                gather(b0, b1, raw.get());
+                if (b1 - b0 < 32 * (ke - k)) std::memset(raw.get() + (b1 - b0), 'N', (size_t)(32 * (ke - k) - (b1 - b0)));
+                uint8_t *codes = slot + 8 * k;
+                uint32_t *mask = reinterpret_cast<uint32_t *>(slot + kStageCodes) + k;
+                if (avx2) pack_avx2(raw.get(), ke - k, codes, mask);
+                else
+                    for (int64_t q = 0; q < ke - k; ++q) pack32_scalar(raw.get() + 32 * q, codes + 8 * q, mask + q);
+            }
             left[c].fetch_sub(1, std::memory_order_release);
         }
     };
@@ -2131,11 +2239,23 @@ int stage_seqs(Engine &e, uint8_t *dst, const char *const *seqs, const int32_t *
     for (int64_t c = 0; c < n_chunk && !rc; ++c) {
         while (left[c].load(std::memory_order_acquire) > 0) std::this_thread::yield();
         const int64_t c0 = c * kStageBytes, c1 = std::min(total, c0 + kStageBytes);
-        hipError_t he = hipMemcpyAsync(dst + c0, e.stage[c % kSlots], (size_t)(c1 - c0),
-                                       hipMemcpyHostToDevice, e.stream);
-        if (he == hipSuccess) he = hipEventRecord(e.stage_ev[c % kSlots], e.stream);
+        const int64_t nb = (c1 - c0 + 31) / 32;
+        const int s = (int)(c % kSlots);
+        uint8_t *dslot = (uint8_t *)e.stage_dev.p + s * kStageSlot;
+        hipError_t he = hipMemcpyAsync(dslot, e.stage[s], (size_t)(8 * nb), hipMemcpyHostToDevice, e.stream);
+        if (he == hipSuccess)
+            he = hipMemcpyAsync(dslot + kStageCodes, e.stage[s] + kStageCodes, (size_t)(4 * nb), hipMemcpyHostToDevice,
+                                e.stream);
+        if (he == hipSuccess) he = hipEventRecord(e.stage_ev[s], e.stream);
+        if (he == hipSuccess) {
+            const int64_t nq = (c1 - c0 + 15) / 16;
+            hipLaunchKernelGGL(k_unpack_codes, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, e.stream,
+                               (const uint32_t *)dslot, (const uint32_t *)(dslot + kStageCodes), dst + c0, c1 - c0);
+            he = hipGetLastError();
+        }
         // hand the workers the slot of the oldest copy still queued once it has landed, keeping
-        // kSlots - 1 chunks queued or being encoded behind it
+        // kSlots - 1 chunks queued or being encoded behind it (the device slot is reused in stream
+        // order: its next copy follows this chunk's unpack)
         const int64_t oldest = c - (kSlots - 2);
         if (he == hipSuccess && oldest >= 0 && freed < n_chunk) {
             he = hipEventSynchronize(e.stage_ev[oldest % kSlots]);
@@ -2146,7 +2266,7 @@ int stage_seqs(Engine &e, uint8_t *dst, const char *const *seqs, const int32_t *
         }
         if (he != hipSuccess) {
             rc = PCABI_E_DEVICE;
-            err = std::string("pcabi_middle_scan_seqs: staging copy: ") + hipGetErrorString(he);
+            err = std::string("staging copy: ") + hipGetErrorString(he);
             break;
         }
     }

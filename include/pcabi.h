@@ -367,6 +367,14 @@ int64_t pcabi_middle_scan_host(int device, const uint8_t *codes, int64_t codes_l
                                const int32_t *adp_len, int32_t n_adp, int match, int mismatch,
                                int gap_open, int gap_extend, double threshold, int32_t *hits,
                                int64_t cap);
+/*
+ * pcabi_stage_seqs_host: the staging the *_seqs entry points use, on its own -- the n strings
+ * (addresses of their first characters, lengths) laid out as SeqPack does (4-aligned starts, N
+ * between, 16 N after), carried to the device as 2-bit codes plus an N mask and unpacked there
+ * into Dna5 bytes, then copied to out[out_len >= the layout's size] (a check of the staging).
+ */
+int pcabi_stage_seqs_host(int device, const char *const *seqs, const int32_t *seq_len, int64_t n, uint8_t *out,
+                          int64_t out_len);
 int64_t pcabi_middle_scan_seqs(int device, const char *const *seqs, const int32_t *seq_len, int64_t n,
                                const uint8_t *adp_codes, const int32_t *adp_off,
                                const int32_t *adp_len, int32_t n_adp, int match, int mismatch,

@@ -233,6 +233,40 @@ def test_host_string_scan_equals_packed_scan(gpu_lib):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('mb', [1, 70])
+def test_staging_codec_is_byte_exact(gpu_lib, mb):
+    """pcabi_stage_seqs_host: windows of a random byte buffer (every byte value, odd starts and
+    lengths, empty windows; 70 MB = three 32 MB chunks, the last partial) carried as 2-bit codes
+    + N masks and unpacked on the device == the Dna5 table applied on the host to SeqPack's
+    layout, byte for byte (pads and the 16-byte tail N)."""
+    import ctypes
+    from custom_porechop_abi_amd import engine
+    rng = np.random.default_rng(mb)
+    buf = rng.integers(0, 256, size=mb * 10 ** 6 + 100, dtype=np.uint8)
+    acgt = np.frombuffer(b'ACGTacgtUuN', np.uint8)
+    buf[:] = np.where(rng.random(buf.size) < 0.95, acgt[rng.integers(0, len(acgt), size=buf.size)], buf)
+    starts, lens, at = [], [], 0
+    while at < buf.size - 20000:
+        ln = int(rng.integers(0, 20000)) if rng.random() > 0.05 else 0
+        starts.append(at)
+        lens.append(ln)
+        at += ln + int(rng.integers(0, 7))
+    starts, lens = np.array(starts, np.uint64), np.array(lens, np.int32)
+    addr = np.uint64(buf.ctypes.data) + starts
+    offs = np.zeros(len(lens), np.int64)
+    np.cumsum(((lens.astype(np.int64) + 3) & ~3)[:-1], out=offs[1:])
+    total = int(offs[-1] + ((int(lens[-1]) + 3) & ~3)) + 16
+    exp = np.full(total, 4, np.uint8)
+    for o, s0, ln in zip(offs.tolist(), starts.tolist(), lens.tolist()):
+        exp[o:o + ln] = engine.DNA5[buf[s0:s0 + ln]]
+    got = np.zeros(total, np.uint8)
+    rc = engine.lib().pcabi_stage_seqs_host(0, addr.ctypes.data_as(ctypes.c_void_p), lens.ctypes.data_as(ctypes.c_void_p),
+                                            len(lens), got.ctypes.data_as(ctypes.c_void_p), total)
+    engine.check(rc, 'pcabi_stage_seqs_host')
+    assert np.array_equal(got, exp)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('windows', ['0', '1'])
 @pytest.mark.parametrize('fault', ['0:1', '0:2', '0:4', '1:1', '1:2', '1:4', '2:7', '0:7,1:4,2:2', '0:8', '1:8',
                                    '2:15'])
