@@ -2174,7 +2174,9 @@ int stage_seqs(Engine &e, uint8_t *dst, const char *const *seqs, const int32_t *
         HIP_TRY(hipEventSynchronize(e.stage_ev[k]));
     }
     if (int rc = e.stage_dev.ensure((size_t)(kSlots * kStageSlot))) return rc;
-    static const bool avx2 = __builtin_cpu_supports("avx2");
+    // PCABI_STAGE_SCALAR=1: the scalar encoder (the form used without AVX2), for its test
+    const char *sc_env = std::getenv("PCABI_STAGE_SCALAR");
+    const bool avx2 = __builtin_cpu_supports("avx2") && !(sc_env && sc_env[0] == '1');
     // characters [b0, b1) of the layout into raw (windows' bytes, 'N' between them)
     auto gather = [&](int64_t b0, int64_t b1, uint8_t *raw) {
         int64_t w = std::upper_bound(off, off + n, b0) - off - 1;

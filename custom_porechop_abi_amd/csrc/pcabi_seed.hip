@@ -1269,6 +1269,8 @@ __global__ __launch_bounds__(256) void k_seed_band_pin(const int4 *task, const i
         };
         // the task's diagonal as a codes offset (probe - o): the verified-seed record
         const int64_t dabs = (int64_t)(((uint64_t)(uint32_t)rc.w << 32) | (uint32_t)rc.z) - o;
+        // the task's verified flag (set once, where its lane finishes): one record call per task
+        // after the row loop, not a ballot per row (r05)
         bool ver = false;
         if (active && rows == 0) {                    // the run ends the adapter: Q = 0
             if (o == 0) {
@@ -1279,7 +1281,6 @@ __global__ __launch_bounds__(256) void k_seed_band_pin(const int4 *task, const i
                 begin_prefix();
             }
         }
-        if (vo.list) put_verified(vo, ver, rc.x, a, E, dabs);
         if constexpr (STATS) {
             st_tasks += __popcll(__ballot(vA_was));
             st_pass += 1;
@@ -1289,7 +1290,6 @@ __global__ __launch_bounds__(256) void k_seed_band_pin(const int4 *task, const i
                 st_it += 64;
                 st_act += __popcll(__ballot(active));
             }
-            ver = false;
             if (active) {
                 const int ab = ad[apos];
                 apos += adir;
@@ -1326,8 +1326,8 @@ __global__ __launch_bounds__(256) void k_seed_band_pin(const int4 *task, const i
                     }
                 }
             }
-            if (vo.list) put_verified(vo, ver, rc.x, a, E, dabs);
         }
+        if (vo.list) put_verified(vo, ver, rc.x, a, E, dabs);
     }
     if constexpr (STATS) {
         if ((threadIdx.x & 63) == 0) {

@@ -233,13 +233,14 @@ def test_host_string_scan_equals_packed_scan(gpu_lib):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('mb', [1, 70])
-def test_staging_codec_is_byte_exact(gpu_lib, mb):
+@pytest.mark.parametrize('mb,scalar', [(1, '0'), (70, '0'), (3, '1')])
+def test_staging_codec_is_byte_exact(gpu_lib, monkeypatch, mb, scalar):
     """pcabi_stage_seqs_host: windows of a random byte buffer (every byte value, odd starts and
     lengths, empty windows; 70 MB = three 32 MB chunks, the last partial) carried as 2-bit codes
     + N masks and unpacked on the device == the Dna5 table applied on the host to SeqPack's
-    layout, byte for byte (pads and the 16-byte tail N)."""
+    layout, byte for byte (pads and the 16-byte tail N). scalar '1': the encoder used without AVX2."""
     import ctypes
+    monkeypatch.setenv('PCABI_STAGE_SCALAR', scalar)
     from custom_porechop_abi_amd import engine
     rng = np.random.default_rng(mb)
     buf = rng.integers(0, 256, size=mb * 10 ** 6 + 100, dtype=np.uint8)
