@@ -157,13 +157,16 @@ bool middle_windows_on(double mean_len) {
 }
 
 // Queued rounds from this index on (0 = round 1) launch their band classes and candidate-DP
-// buckets one after the other on the scan's stream: by the third round only the reads that hit
-// twice are left, their launches last a few microseconds, and each fork / join over side streams
-// costs ~15-20 us of event latency (profiles/r03/final/kernel_trace_middle_8kb.csv).
-// PCABI_MIDDLE_SERIAL_FROM overrides (a large value keeps every round side by side).
+// buckets one after the other on the scan's stream: after round 1 only the reads that hit are
+// left, their launches last a few microseconds, and each fork / join over side streams costs
+// ~15-20 us of event latency (profiles/r03/final/kernel_trace_middle_8kb.csv). r05at (in-process
+// A/B, profiles/r05/at/): from round 2 on (1) 1.93 ms at 8 kb / 2.53 at 20 kb, against 1.96-1.99 /
+// 2.65-2.69 from round 3 on (2, the r03-r05 default, round 2 replayed from a graph) and 2.02 /
+// 2.51 with round 1 serial too (0). PCABI_MIDDLE_SERIAL_FROM overrides (a large value keeps every
+// round side by side).
 int middle_serial_from() {
     const char *e = std::getenv("PCABI_MIDDLE_SERIAL_FROM");
-    return (e && e[0]) ? std::atoi(e) : 2;
+    return (e && e[0]) ? std::atoi(e) : 1;
 }
 
 // Device planning aims at this many waves per candidate-DP round (4 per SIMD): the chunk length
