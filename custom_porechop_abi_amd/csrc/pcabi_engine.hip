@@ -3649,8 +3649,9 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
     // arguments depend only on the slot, the call's inputs and the scratch addresses: it is captured
     // once into a graph and replayed (r05: one host call instead of ~40 launches and ~10 event
     // operations, and the graph's ~1.6 us per kernel instead of ~2.7 back to back, tools/
-    // launch_bench.hip). Not for rounds that inject faults (tests), profile, debug, serial rounds or
-    // the legacy stream; PCABI_MIDDLE_GRAPHS=0 queues every round directly (A/B).
+    // launch_bench.hip; r05au: serial rounds too, the fork setting in the key). Not for rounds that
+    // inject faults (tests), profile, debug or the legacy stream; PCABI_MIDDLE_GRAPHS=0 queues every
+    // round directly (A/B).
     const bool graphs_on = [] {
         const char *e = std::getenv("PCABI_MIDDLE_GRAPHS");
         return !(e && e[0] == '0');
@@ -3660,12 +3661,12 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
     sc->last_table = adps->serial;
     auto run_round = [&](int r) -> int {
         const bool first = r == 0 && round_base == 0;
-        if (!graphs_on || first || round_base + r >= serial_from) return queue_round(r);
+        if (!graphs_on || first) return queue_round(r);
         std::vector<int64_t> key = {(int64_t)round_base, (int64_t)(intptr_t)codes, (int64_t)(intptr_t)win_off,
                                     (int64_t)(intptr_t)win_len, n, windows ? 1 : 0, (int64_t)(threshold * 1e6),
                                     scr.ma, scr.mi, scr.go, scr.ge, (int64_t)adps->serial, sc->q_slots_cap,
                                     sc->shadow_cap, (int64_t)(intptr_t)sc->shadow.p, target,
-                                    (int64_t)g_buf_gen.load()};
+                                    (int64_t)g_buf_gen.load(), (int64_t)serial_from};
         auto &g = sc->graphs[r & 31];
         if (g.exec && g.key == key) {
             HIP_TRY(hipGraphLaunch(g.exec, st));
