@@ -3362,6 +3362,13 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
     }
     const std::vector<std::pair<int64_t, int>> faults = middle_faults();
     const int serial_from = middle_serial_from();
+    // the candidate-DP buckets' own threshold: in the window rounds (long reads) round 1's buckets
+    // run serial too (r05aw in-process A/B, 20 kb: 2.512 -> 2.491 ms; 8 kb whole-read rounds keep
+    // them side by side: 1.933 against 1.999 serial); PCABI_MIDDLE_DP_SERIAL_FROM overrides
+    const int dp_serial_from = [&] {
+        const char *e = std::getenv("PCABI_MIDDLE_DP_SERIAL_FROM");
+        return (e && e[0]) ? std::atoi(e) : (windows ? 0 : serial_from);
+    }();
     std::vector<char> fired(faults.size(), 0);
     int injected[kSlots + 1] = {};                  // per slot: the faults its last queueing injected
     const int64_t target = middle_plan_waves();
@@ -3509,7 +3516,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
             // most of it the whole reads' 32-column chunks -- and the 8 kb one 0.08-0.09 ms slower)
             p.chunk_split = windows ? 2 : 0;
             ForkJoin fj;
-            if (int rc = fj.begin(st, serial ? 1 : used.size())) return rc;
+            if (int rc = fj.begin(st, round_base + r >= dp_serial_from ? 1 : used.size())) return rc;
             for (int k = 0; k < n_bk; ++k) {
                 const int b = used[k];
                 p.adp_pad = adps->pad[b];
@@ -3666,7 +3673,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
                                     (int64_t)(intptr_t)win_len, n, windows ? 1 : 0, (int64_t)(threshold * 1e6),
                                     scr.ma, scr.mi, scr.go, scr.ge, (int64_t)adps->serial, sc->q_slots_cap,
                                     sc->shadow_cap, (int64_t)(intptr_t)sc->shadow.p, target,
-                                    (int64_t)g_buf_gen.load(), (int64_t)serial_from};
+                                    (int64_t)g_buf_gen.load(), (int64_t)serial_from, (int64_t)dp_serial_from};
         auto &g = sc->graphs[r & 31];
         if (g.exec && g.key == key) {
             HIP_TRY(hipGraphLaunch(g.exec, st));
