@@ -321,26 +321,41 @@ def _end_decisions_batch(reads, starts, ends, end_size, extra, thr, scoring_sche
         mem = np.argsort(idx, kind='stable')
         first = np.cumsum(cnt) - cnt
         read, u, rs, re_, m, l1, l2 = lst
-        rep = cnt[u]
-        within = np.arange(int(rep.sum())) - np.repeat(np.cumsum(rep) - rep, rep)
-        set_k = mem[np.repeat(first[u], rep) + within]
-        read = np.repeat(read, rep)
-        # read-major, set order within a read: one stable sort of a combined key (the rows come
-        # read-major already, so the sort's runs are long: ~6x faster than lexsort on 500 k rows)
-        order = np.argsort(read.astype(np.int64) * max(1, len(sets)) + set_k, kind='stable')
         failed = rs == -1
         full = np.where(failed, 0.0, engine.pid6(m, l2))
         part = np.where(failed, 0.0, engine.pid6(m, l1))
         re_x = np.where(failed, 0, re_ + 1)
-        full, part, rs, re_x = (np.repeat(x, rep)[order] for x in (full, part, rs, re_x))
-        rd = read[order]
+        if int(cnt.max()) == 1:
+            # every distinct sequence in one set (the usual table): a row per alignment, and the
+            # device's read-major lists are in set order within a read whenever the distinct
+            # sequences are numbered in set order -- then nothing is expanded or sorted (r05)
+            set_k = mem[u]
+            key = read.astype(np.int64) * max(1, len(sets)) + set_k
+            if key.size < 2 or bool(np.all(key[1:] > key[:-1])):
+                order = None
+            else:
+                order = np.argsort(key, kind='stable')
+            rd = read if order is None else read[order]
+            if order is not None:
+                set_k, full, part, rs, re_x = (x[order] for x in (set_k, full, part, rs, re_x))
+        else:
+            rep = cnt[u]
+            within = np.arange(int(rep.sum())) - np.repeat(np.cumsum(rep) - rep, rep)
+            set_k = mem[np.repeat(first[u], rep) + within]
+            read = np.repeat(read, rep)
+            # read-major, set order within a read: one stable sort of a combined key (the rows come
+            # read-major already, so the sort's runs are long: ~6x faster than lexsort on 500 k rows)
+            order = np.argsort(read.astype(np.int64) * max(1, len(sets)) + set_k, kind='stable')
+            full, part, rs, re_x = (np.repeat(x, rep)[order] for x in (full, part, rs, re_x))
+            rd = read[order]
+            set_k = set_k[order]
         if engine._pystr is not None:             # the tuples made and appended in one native pass
-            engine._pystr.append_rows(reads, attr, sets, rd.astype(np.int64), set_k[order].astype(np.int64),
+            engine._pystr.append_rows(reads, attr, sets, rd.astype(np.int64), set_k.astype(np.int64),
                                       full.astype(np.float64), part.astype(np.float64), rs.astype(np.int64),
                                       re_x.astype(np.int64))
             continue
         # the tuples in one pass, then one extend per read (not one append per alignment)
-        rows = list(zip(map(sets.__getitem__, set_k[order].tolist()), full.tolist(), part.tolist(), rs.tolist(),
+        rows = list(zip(map(sets.__getitem__, set_k.tolist()), full.tolist(), part.tolist(), rs.tolist(),
                         re_x.tolist()))
         cut = np.flatnonzero(np.diff(rd)) + 1
         lo = np.concatenate([[0], cut]).tolist()
