@@ -54,6 +54,70 @@ def test_attr_list_and_raise_trims():
     assert all(type(r.start_trim_amount) is int for r in reads)
 
 
+class _Slotted(object):
+    __slots__ = ('name', 'seq', 'start_trim_amount', 'end_trim_amount')
+
+    def __init__(self, i):
+        self.name, self.seq, self.start_trim_amount, self.end_trim_amount = 'r%d' % i, 'ACGT' * (i % 5), i % 7, i % 3
+
+
+class _Prop(object):
+    """Attributes behind a property and a class attribute (no instance-dict value to prefetch)."""
+    end_trim_amount = 2
+
+    def __init__(self, i):
+        self._s = i % 11
+        self.seq = 'A' * (i % 9)
+        self.name = 'p%d' % i
+
+    @property
+    def start_trim_amount(self):
+        return self._s
+
+    @start_trim_amount.setter
+    def start_trim_amount(self, v):
+        self._s = v
+
+
+def _mixed_objects(n=300, seed=5):
+    """NanoporeReads (shared-key instance dicts), reads whose dicts were unshared by attributes set
+    in another order, __slots__ objects and property-backed ones, interleaved: the helpers'
+    prefetching (object, instance dict, its value array, the value) must follow each kind."""
+    rng = random.Random(seed)
+    out = []
+    for i in range(n):
+        k = rng.randrange(4)
+        if k == 0:
+            out.append(NanoporeRead('r%d' % i, 'ACGT' * (i % 6), ''))
+        elif k == 1:
+            r = NanoporeRead('u%d' % i, 'GATT' * (i % 4), '')
+            r.__dict__ = dict(reversed(list(r.__dict__.items())))   # a combined (unshared) table
+            r.extra = i
+            out.append(r)
+        elif k == 2:
+            out.append(_Slotted(i))
+        else:
+            out.append(_Prop(i))
+    return out
+
+
+def test_helpers_on_every_object_layout():
+    rng = random.Random(6)
+    objs = _mixed_objects()
+    for name in ('seq', 'name', 'start_trim_amount', 'end_trim_amount'):
+        assert engine._pystr.attr_list(objs, name) == [getattr(o, name) for o in objs]
+    out = np.empty(len(objs), np.int64)
+    engine._pystr.int_attrs(objs, 'start_trim_amount', out)
+    assert out.tolist() == [o.start_trim_amount for o in objs]
+    st = np.array([rng.randint(0, 12) for _ in objs], np.int32)
+    et = np.zeros(len(objs), np.int32)           # never above: end trims stay (the class attribute too)
+    want = [(max(o.start_trim_amount, int(a)), o.end_trim_amount) for o, a in zip(objs, st)]
+    engine._pystr.raise_trims(objs, st, et)
+    assert [(o.start_trim_amount, o.end_trim_amount) for o in objs] == want
+    with pytest.raises(AttributeError):
+        engine._pystr.attr_list(objs + [object()], 'seq')
+
+
 def test_append_rows_matches_python_tuples():
     rng = random.Random(4)
     reads = [NanoporeRead('r%d' % i, 'ACGT', '') for i in range(50)]
