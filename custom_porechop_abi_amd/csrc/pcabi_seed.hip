@@ -879,9 +879,16 @@ __global__ __launch_bounds__(kExpandThreads) void k_seed_expand(ScanArgs a) {
 // block scan places them, one atomic per class and pass takes the block's place, and the second
 // walk writes. The two-pass kernel walks every hit three times and runs a slab at a time (~1.1 k
 // hits per slab in round 1 of 8 kb reads: a 1024-thread pass half idle, two scans per slab).
-constexpr int kExpandHits = 2;                 // 4 needs 74 VGPRs: one block per CU instead of two
+int expand_hits() {
+    const char *e = std::getenv("PCABI_EXPAND_HITS");
+    return (e && e[0] == '2') ? 2 : 3;
+}
+// kExpandHits hits per thread and pass (r05bb: 3 fits 64 VGPRs under amdgpu_waves_per_eu(8), two
+// blocks per CU, and beats 2 in-process: 1.938 -> 1.924 ms at 8 kb, 2.495 -> 2.462 at 20 kb; 4
+// spills there; PCABI_EXPAND_HITS=2 selects the r04 form, A/B)
 constexpr int kExpandGroup = 64;
-__global__ __launch_bounds__(kExpandThreads) void k_seed_expand1(ScanArgs a) {
+template <int kExpandHits>
+__global__ __launch_bounds__(kExpandThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_seed_expand1(ScanArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     __shared__ long long s_w[2 * (kExpandThreads / 64)];
     __shared__ long long s_base[2];
@@ -1902,7 +1909,10 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
         if (ep && ep[0] == '2')
             hipLaunchKernelGGL(k_seed_expand, dim3(s->expand_blocks), dim3(kExpandThreads), s->lds_bytes, st, A);
         else
-            hipLaunchKernelGGL(k_seed_expand1, dim3(s->expand_blocks), dim3(kExpandThreads), s->lds_bytes, st, A);
+            if (expand_hits() == 3)
+                hipLaunchKernelGGL(k_seed_expand1<3>, dim3(s->expand_blocks), dim3(kExpandThreads), s->lds_bytes, st, A);
+            else
+                hipLaunchKernelGGL(k_seed_expand1<2>, dim3(s->expand_blocks), dim3(kExpandThreads), s->lds_bytes, st, A);
     }
     if (s->pev) SD_TRY(hipEventRecord(s->pev[2], st));
     SD_TRY(hipGetLastError());
