@@ -57,6 +57,7 @@ extern "C" int pcabi_middle_cuts_dev(const int32_t *hits, int64_t hit_stride, in
     const size_t tmp = std::max(sort_tmp, scan_tmp);
     char *buf = nullptr;
     HIP_TRY(hipMallocAsync((void **)&buf, 4 * a4 + a8 + tmp + 256, st));
+    pcabi_poison_async(buf, 4 * a4 + a8 + tmp + 256, st);
     uint32_t *key = (uint32_t *)buf, *idx = (uint32_t *)(buf + a4), *key2 = (uint32_t *)(buf + 2 * a4),
              *order = (uint32_t *)(buf + 3 * a4);
     unsigned long long *count = (unsigned long long *)(buf + 4 * a4);

@@ -65,6 +65,7 @@ extern "C" int pcabi_flag_list_dev(const uint8_t *flag, int32_t n_adp, int64_t n
     const size_t a8 = (8 * (nr + 1) + 255) & ~(size_t)255;
     char *buf = nullptr;
     HIP_TRY(hipMallocAsync((void **)&buf, 2 * a8 + scan_tmp + 256, st));
+    pcabi_poison_async(buf, 2 * a8 + scan_tmp + 256, st);
     unsigned long long *count = (unsigned long long *)buf, *off = (unsigned long long *)(buf + a8);
     void *t = buf + 2 * a8;
     int rc = 0;

@@ -659,6 +659,18 @@ namespace pcabi {
 // ------------------------------------------------------------------------------------------
 constexpr uint32_t INC_PAD = 1u << ATTR_CSH;   // padding diagonal: start column + 1
 
+// gfx950 issues a VOP2 instruction that reads an SGPR at half rate: 4.4 cycles per wave64
+// instruction against 2.45 for the same op on VGPRs or a literal (tools/replay_k24.hip rate probes,
+// profiles/r06/replay). A core's per-call constants (gap extend / open keys) are uniform, so the
+// compiler keeps them in SGPRs and every cell's adds pay that; vreg() pins such a value in a VGPR
+// (an empty asm the compiler cannot see through) so the cell's adds read VGPRs only.
+PCABI_HD int32_t vreg(int32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(x));
+#endif
+    return x;
+}
+
 PCABI_HD int max3i(int a, int b, int c) {   // one v_max3_i32 on gfx950
     const int ab = a > b ? a : b;
     return ab > c ? ab : c;
@@ -1327,6 +1339,10 @@ PCABI_HD Best packed_best(ReadFn &rd, int n, const TabFn &tabfn, int L, const Sc
     st.k_geh = Y::sc(sc.ge) - Y::sc(sc.go) + Y::TB1;
     st.k_gex = Y::sc(sc.ge) + (Y::TAGGED ? Y::TB1 : 0);
     st.k_vo = Y::TAGGED ? Y::TB2 : 0;
+    // the cell's adds read these: VGPR operands, not SGPR (vreg)
+    st.k_ge = vreg(st.k_ge);
+    st.k_go = vreg(st.k_go);
+    st.k_gex = vreg(st.k_gex);
 #pragma unroll
     for (int s = 1; s <= RPL; ++s) {
         st.G[s] = Y::start(off - s) + st.k_go;    // padded (s, 0) reaches real (0, off - s)

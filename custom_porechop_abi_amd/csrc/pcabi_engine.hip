@@ -1358,6 +1358,26 @@ namespace {
 // seed plan: a captured round graph (middle_device_rounds) holds their addresses and launch
 // arguments, and is replayed only while the generation it was captured at holds.
 std::atomic<uint64_t> g_buf_gen{0};
+
+// Debug switch PCABI_POISON=1: every fresh scratch allocation and every growth (DeviceBuf, the
+// seeds' Buf, the shadow arena) is filled with 0xFF bytes before use, so a kernel that reads
+// scratch nothing wrote sees garbage instead of the zeros fresh hipMalloc memory usually holds
+// (the r05 `need2` read went unnoticed for that reason).
+bool pcabi_poison_on() {
+    static const bool on = [] {
+        const char *e = std::getenv("PCABI_POISON");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+void pcabi_poison(void *p, size_t bytes) {
+    if (!pcabi_poison_on() || !p || !bytes) return;
+    (void)hipMemset(p, 0xFF, bytes);
+    (void)hipDeviceSynchronize();
+}
+void pcabi_poison_async(void *p, size_t bytes, hipStream_t st) {
+    if (pcabi_poison_on() && p && bytes) (void)hipMemsetAsync(p, 0xFF, bytes, st);
+}
 namespace {
 struct DeviceBuf {
     void *p = nullptr;
@@ -1376,6 +1396,7 @@ struct DeviceBuf {
             return fail(PCABI_E_NOMEM, "hipMalloc failed (" + std::to_string(want) + " bytes): " + hipGetErrorString(e));
         }
         cap = want;
+        pcabi_poison(p, want);
         return 0;
     }
 };
@@ -3161,6 +3182,7 @@ int shadow_grow(pcabi_scan *sc, const uint8_t *codes, const int64_t *win_off, in
     if (want <= old_cap || want < taken - old_cap) return fail(PCABI_E_NOMEM, "middle scan: shadow arena past its limit");
     void *np = nullptr;
     if (hipMalloc(&np, (size_t)want) != hipSuccess) return fail(PCABI_E_NOMEM, "hipMalloc failed (shadow arena)");
+    pcabi_poison(np, (size_t)want);
     if (sc->shadow.p && old_cap > 0) HIP_TRY(hipMemcpyAsync(np, sc->shadow.p, (size_t)old_cap, hipMemcpyDeviceToDevice, st));
     const int64_t delta = (int64_t)((intptr_t)np - (intptr_t)sc->shadow.p);
     if (sc->shadow.p && n > 0)

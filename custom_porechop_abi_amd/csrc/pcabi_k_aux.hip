@@ -41,6 +41,7 @@ int launch_striped(KParams p, bool affine, hipStream_t st) {
     void *scr = nullptr;
     // slots past the last item never touch their scratch
     HIP_TRY(hipMallocAsync(&scr, (size_t)(std::min(slots, p.n_items) * per_slot), st));
+    pcabi_poison_async(scr, (size_t)(std::min(slots, p.n_items) * per_slot), st);
     p.scratch = (int32_t *)scr;
     p.max_cols = std::max<int32_t>(1, p.max_cols);
     const dim3 grid((unsigned)(slots / 4));

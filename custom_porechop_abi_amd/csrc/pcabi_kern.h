@@ -18,6 +18,11 @@
 #define PCABI_WAVES 1
 #endif
 
+// PCABI_POISON=1 (debug, pcabi_engine.hip): fresh device scratch is filled with 0xFF bytes, on the
+// host's behalf (pcabi_poison) or stream-ordered for hipMallocAsync scratch (pcabi_poison_async)
+void pcabi_poison(void *p, size_t bytes);
+void pcabi_poison_async(void *p, size_t bytes, hipStream_t st);
+
 namespace pcabi_eng {
 
 // thread-local error message (pcabi_last_error), defined in pcabi_engine.hip

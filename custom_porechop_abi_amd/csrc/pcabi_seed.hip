@@ -59,6 +59,7 @@ int fail(int code, const std::string &msg);
 // pcabi_engine.hip: the scratch generation its captured round graphs are keyed on (a reallocation,
 // a new plan or new capacities here change addresses or launch arguments those graphs hold)
 extern std::atomic<uint64_t> g_buf_gen;
+void pcabi_poison(void *p, size_t bytes);   // pcabi_engine.hip: PCABI_POISON=1 fills fresh scratch
 using pcabi_internal::fail;
 
 #define SD_TRY(expr)                                                                                          \
@@ -1415,6 +1416,7 @@ struct Buf {
             return fail(PCABI_E_NOMEM, "hipMalloc failed (seeds, " + std::to_string(want) + " bytes): " + hipGetErrorString(e));
         }
         cap = want;
+        pcabi_poison(p, want);
         return 0;
     }
     ~Buf() {

@@ -14,7 +14,10 @@ oracle's masked loop (the reference's find_middle_adapters, porechop_abi/nanopor
     vs NanoporeRead.determine_barcode (nanopore_read.py:408-482).
 """
 import ctypes
+import os
 import random
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -547,3 +550,18 @@ def test_barcode_call_96_sets_on_barcoded_reads(gpu_lib):
             exp.append(read.barcode_call)
         assert got == exp
         assert sum(x != 'none' for x in exp) > n // 2
+
+
+@pytest.mark.gpu
+def test_poisoned_scratch(gpu_lib):
+    """PCABI_POISON=1 (a child process: the switch is read once per process): every fresh device
+    scratch buffer and every growth starts as 0xFF bytes, and the overflow / requeue, shadow-arena,
+    candidate-window and end-trim cases of tests/poisoned_middle.py still equal the oracle -- a path
+    that reads scratch nothing wrote (r05: the plans' need2) no longer hides behind zeroed memory."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PCABI_POISON='1')
+    r = subprocess.run([sys.executable, '-u', os.path.join(root, 'tests', 'poisoned_middle.py')], env=env,
+                       capture_output=True, text=True, timeout=400)
+    print(r.stdout)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    assert 'all cases ok' in r.stdout

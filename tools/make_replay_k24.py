@@ -84,9 +84,11 @@ def main():
     body = kernel_lines(lines)
     members, hid = inner_loop(body)
     text = [l for b in members for l in b[3]]
-    prof = os.path.join(ROOT, 'profiles', 'r05')
-    os.makedirs(prof, exist_ok=True)
-    with open(os.path.join(prof, 'k_align24_inner_column.s'), 'w') as f:
+    # REPLAY_S: where the extracted loop goes (r05: profiles/r05/k_align24_inner_column.s, the loop the
+    # replay harness's register setup is written for)
+    out_s = os.environ.get('REPLAY_S', os.path.join(ROOT, 'profiles', 'r05', 'k_align24_inner_column.s'))
+    os.makedirs(os.path.dirname(out_s), exist_ok=True)
+    with open(out_s, 'w') as f:
         f.write('; %s: inner column loop (header .LBB%s), gfx950, hipcc -O3, extracted by '
                 'tools/make_replay_k24.py\n' % (KERNEL, hid))
         f.write('\n'.join(text) + '\n')
@@ -106,13 +108,35 @@ def main():
                    {int(a) + i for l in text for a, b in re.findall(r'\bs\[(\d+):(\d+)\]', l)
                     for i in range(int(b) - int(a) + 1)})
 
-    def variant(tag, nolds):
+    nv = max(vregs) + 1                        # the interleaved copy's registers start here
+    lits = {}                                  # VOP2 literal -> SGPR (variant sgprlit)
+
+    def rename(s, k):
+        """Copy B of a vector instruction: every VGPR vN -> v(N + k)."""
+        s = re.sub(r'\bv\[(\d+):(\d+)\]', lambda m: 'v[%d:%d]' % (int(m.group(1)) + k, int(m.group(2)) + k), s)
+        return re.sub(r'\bv(\d+)\b', lambda m: 'v%d' % (int(m.group(1)) + k), s)
+
+    def split3(s, op):
+        """v_max3_i32 d, a, b, c -> two VOP2 `op`s (src1 a VGPR; d may alias one source)."""
+        m = re.match(r'^\s*v_max3_i32\s+(\S+),\s*(\S+),\s*(\S+),\s*(\S+)$', s)
+        d, a, b, c = m.groups()
+        srcs = [a, b, c]
+        z = next((x for x in srcs if x.startswith('s') and x != d), None) or next(x for x in reversed(srcs) if x != d)
+        rest = list(srcs)
+        rest.remove(z)
+        x, y = rest if rest[1].startswith('v') else (rest[1], rest[0])
+        return ['%s %s, %s, %s' % (op, d, x, y), '%s %s, %s, %s' % (op, d, z, d)]
+
+    def variant(tag, mode):
+        """mode: exact | nolds (ds_reads and their waits dropped) | nowait (ds_reads kept, waits
+        dropped) | sgprlit (VOP2 literals from SGPRs: half the bytes) | max3split (each v_max3_i32
+        as two v_max_i32) | maxadd (every max as full-rate v_add_u32s: same chains, no max) |
+        inter2 (a second copy of every vector instruction on registers v+NV, interleaved one by
+        one: two independent columns per lane, the loop control shared)"""
         out = []
         for l in text:
             s = l.split(';')[0].rstrip()
             if not s.strip():
-                if l.strip().startswith('; sched_barrier'):
-                    continue
                 continue
             m = re.match(r'^(\.LBB\d+_\d+|; %bb\.\d+)', l)
             if m:
@@ -122,31 +146,84 @@ def main():
                 continue
             s = s.replace(exits[0], '.Lrp_%s_exit' % tag)
             s = re.sub(r'\.LBB(\d+_\d+)', lambda mm: '.Lrp_%s_%s' % (tag, mm.group(1)), s)
-            if nolds and ('ds_read' in s or 'lgkmcnt' in s):
+            s = s.strip()
+            if mode == 'nolds' and ('ds_read' in s or 'lgkmcnt' in s):
                 continue                       # no LDS read, no wait: the destinations keep old values
+            if mode == 'nowait' and 'lgkmcnt' in s:
+                continue
+            if mode == 'sgprlit' and s.startswith('v_') and '_e32' in s:
+                mm = re.search(r',\s*(0x[0-9a-f]+),', s)
+                if mm:
+                    reg = lits.setdefault(mm.group(1), 's%d' % (61 + len(lits)))
+                    s = s.replace(mm.group(1), reg, 1)
+            if mode in ('max3split', 'maxadd') and s.startswith('v_max3_i32'):
+                out += split3(s, 'v_max_i32_e32' if mode == 'max3split' else 'v_add_u32_e32')
+                continue
+            if mode == 'vgconst':               # the cell's SGPR constants read from VGPRs v72 / v73
+                s = re.sub(r'^(v_\w+_e32 v\d+), s16,', r'\1, v72,', s)
+                s = re.sub(r'^(v_\w+_e32 v\d+), s28,', r'\1, v73,', s)
+            if mode == 'maxadd' and s.startswith('v_max_i32'):
+                s = s.replace('v_max_i32', 'v_add_u32')
             out.append(s)
+            if mode == 'inter2' and re.match(r'^(v_|ds_|global_)', s):
+                out.append(rename(s, nv))
         header = '.Lrp_%s_%s' % (tag, hid)
         return header, out
+
+    def half_rate(s):
+        """Issue classes measured by tools/replay_k24.hip's rate probes: VOP3 forms and the 32-bit
+        maxes take two full-rate issue slots (4 cycles per wave64 instruction)."""
+        op = s.split()[0]
+        return op.startswith('v_max') or (op.startswith('v_') and not op.endswith(('_e32', '_e64')) and
+                                           not op.startswith(('v_mov_b32', 'v_cndmask', 'v_cmp')))
 
     inc = ['// generated by tools/make_replay_k24.py from %s (do not edit)' % KERNEL,
            '// instruction counts per loop pass: ' + ', '.join('%s %d' % kv for kv in sorted(counts.items())),
            '#define RP_VREGS_MAX %d' % max(vregs),
+           '#define RP_NV %d' % nv,
            '#define RP_SREGS_MAX %d' % max(sregs),
-           '#define RP_CLOBBER_V %s' % ', '.join('"v%d"' % v for v in range(0, max(vregs) + 1)),
+           '#define RP_CLOBBER_V %s' % ', '.join('"v%d"' % v for v in range(0, nv)),
+           '#define RP_CLOBBER_V2 %s' % ', '.join('"v%d"' % v for v in range(nv, 2 * nv)),
            '#define RP_CLOBBER_S %s' % ', '.join('"s%d"' % s for s in sregs),
            '#define RP_SREGS "%s"' % ' '.join('s%d' % s for s in sregs)]
-    for tag, nolds in (('exact', False), ('nolds', True)):
-        header, out = variant(tag, nolds)
+    load_labels = {b[0].replace('.LBB', '') for b in members if b[0].startswith('.LBB_bb')}
+    # the *4 copies run at the other 4-byte code phase (same instructions, own labels)
+    for tag, mode in (('exact', 'exact'), ('nolds', 'nolds'), ('nowait', 'nowait'), ('sgprlit', 'sgprlit'),
+                      ('max3split', 'max3split'), ('maxadd', 'maxadd'), ('inter2', 'inter2'), ('exact4', 'exact'),
+                      ('nolds4', 'nolds'), ('vgconst', 'vgconst')):
+        header, out = variant(tag, mode)
         inc.append('#define RP_HEADER_%s "%s"' % (tag.upper(), header))
+        inc.append('#define RP_EXIT_%s ".Lrp_%s_exit:\\n"' % (tag.upper(), tag))
         inc.append('#define RP_LOOP_%s \\' % tag.upper())
         for s in out:
             inc.append('    "%s\\n" \\' % s.replace('\t', ' ').strip())
         inc.append('    ""')
+        # per pass: VALU of the main blocks, VALU of the look-ahead block (every 4th pass), and
+        # how many of the main blocks' VALU are half rate
+        main, load, half = 0, 0, 0
+        in_load = False
+        for s in out:
+            if s.endswith(':'):
+                continue
+            if s.startswith('s_lshr_b32'):     # the look-ahead block's first instruction
+                in_load = True
+            if s.startswith('s_branch') and in_load:
+                in_load = False
+                continue
+            if s.startswith('v_'):
+                if in_load:
+                    load += 1
+                else:
+                    main += 1
+                    half += half_rate(s)
+        inc.append('#define RP_VALU_MAIN_%s %d' % (tag.upper(), main))
+        inc.append('#define RP_VALU_LOAD_%s %d' % (tag.upper(), load))
+        inc.append('#define RP_VALU_HALF_%s %d' % (tag.upper(), half))
+    inc.append('#define RP_SGPRLIT_SETUP "%s"' % ''.join('s_mov_b32 %s, %s\\n' % (r, v) for v, r in lits.items()))
+    inc.append('#define RP_CLOBBER_LIT %s' % ', '.join('"%s"' % r for r in lits.values()))
     valu = sum(v for k, v in counts.items() if k.startswith('v_'))
-    inc.append('#define RP_VALU_PER_PASS_MAIN %d' % (valu - sum(1 for b in members if b[0].startswith('.LBB_bb')
-                                                               for l in b[3] if re.match(r'^\s+v_', l))))
-    inc.append('#define RP_VALU_PER_PASS_LOAD %d' % sum(1 for b in members if b[0].startswith('.LBB_bb')
-                                                         for l in b[3] if re.match(r'^\s+v_', l)))
+    if os.environ.get('REPLAY_NO_INC') == '1':    # extraction only (ISA of the current source)
+        return 0
     with open(os.path.join(ROOT, 'tools', 'replay_k24_body.inc'), 'w') as f:
         f.write('\n'.join(inc) + '\n')
     print('loop header .LBB%s: %d lines, %d VALU per pass, exits to %s; vregs up to v%d, sregs %s' % (
