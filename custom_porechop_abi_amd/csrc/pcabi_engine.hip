@@ -1359,24 +1359,28 @@ namespace {
 // arguments, and is replayed only while the generation it was captured at holds.
 std::atomic<uint64_t> g_buf_gen{0};
 
-// Debug switch PCABI_POISON=1: every fresh scratch allocation and every growth (DeviceBuf, the
-// seeds' Buf, the shadow arena) is filled with 0xFF bytes before use, so a kernel that reads
-// scratch nothing wrote sees garbage instead of the zeros fresh hipMalloc memory usually holds
-// (the r05 `need2` read went unnoticed for that reason).
-bool pcabi_poison_on() {
-    static const bool on = [] {
+// Debug switch PCABI_POISON: every fresh scratch allocation and every growth (DeviceBuf, the
+// seeds' Buf, the shadow arena, the stream-ordered scratch of the epilogues and the striped core)
+// is filled with one byte before use, so a kernel or host path that reads scratch nothing wrote
+// sees garbage instead of the zeros fresh hipMalloc memory usually holds (the
+// r05 `need2` read went unnoticed for that reason). "1" fills 0xFF (every int -1); a hex byte such
+// as "0x7f" fills that byte (0x7f: every int32 / int64 a huge positive count).
+int pcabi_poison_byte() {
+    static const int b = [] {
         const char *e = std::getenv("PCABI_POISON");
-        return e && e[0] == '1';
+        if (!e || !e[0] || (e[0] == '0' && !e[1])) return -1;
+        if (e[0] == '1' && !e[1]) return 0xFF;
+        return (int)(std::strtol(e, nullptr, 0) & 0xFF);
     }();
-    return on;
+    return b;
 }
 void pcabi_poison(void *p, size_t bytes) {
-    if (!pcabi_poison_on() || !p || !bytes) return;
-    (void)hipMemset(p, 0xFF, bytes);
+    if (pcabi_poison_byte() < 0 || !p || !bytes) return;
+    (void)hipMemset(p, pcabi_poison_byte(), bytes);
     (void)hipDeviceSynchronize();
 }
 void pcabi_poison_async(void *p, size_t bytes, hipStream_t st) {
-    if (pcabi_poison_on() && p && bytes) (void)hipMemsetAsync(p, 0xFF, bytes, st);
+    if (pcabi_poison_byte() >= 0 && p && bytes) (void)hipMemsetAsync(p, pcabi_poison_byte(), bytes, st);
 }
 namespace {
 struct DeviceBuf {

@@ -1,6 +1,6 @@
 """Test infrastructure (run by tests/test_gpu_middle_paths.py::test_poisoned_scratch, in a child
-process started with PCABI_POISON=1): every device scratch buffer this process
-allocates starts as 0xFF bytes instead of the zeros fresh hipMalloc memory usually holds, and the
+process started with PCABI_POISON=1 or =0x7f): every device scratch buffer this
+process allocates starts as 0xFF (every int -1) or 0x7F bytes (every int a huge count) instead of the zeros fresh hipMalloc memory usually holds, and the
 middle scan's product paths and an end-trim cross product must still equal the oracle:
 
   * round-1 overflow, growth and requeue from tiny initial buffers (PCABI_MIDDLE_INIT_CAPS);
@@ -38,7 +38,7 @@ def setenv(**kw):
 
 
 def main():
-    assert os.environ.get('PCABI_POISON') == '1', 'run with PCABI_POISON=1'
+    assert os.environ.get('PCABI_POISON', '0') != '0', 'run with PCABI_POISON=1 (0xFF) or a hex byte'
     L = _lib.lib()
     assert L.pcabi_device_count() >= 1
     os.environ['PCABI_MIDDLE_SEEDS'] = '2'

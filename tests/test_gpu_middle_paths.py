@@ -553,13 +553,15 @@ def test_barcode_call_96_sets_on_barcoded_reads(gpu_lib):
 
 
 @pytest.mark.gpu
-def test_poisoned_scratch(gpu_lib):
-    """PCABI_POISON=1 (a child process: the switch is read once per process): every fresh device
-    scratch buffer and every growth starts as 0xFF bytes, and the overflow / requeue, shadow-arena,
-    candidate-window and end-trim cases of tests/poisoned_middle.py still equal the oracle -- a path
-    that reads scratch nothing wrote (r05: the plans' need2) no longer hides behind zeroed memory."""
+@pytest.mark.parametrize('byte', ['1', '0x7f'])
+def test_poisoned_scratch(gpu_lib, byte):
+    """PCABI_POISON (a child process: the switch is read once per process): every fresh device
+    scratch buffer and every growth starts as 0xFF bytes (every int -1) or 0x7F bytes (every int a
+    huge count), and the overflow / requeue, shadow-arena, candidate-window and end-trim cases of
+    tests/poisoned_middle.py still equal the oracle -- a path that reads scratch nothing wrote (r05:
+    the plans' need2) no longer hides behind zeroed memory."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, PCABI_POISON='1')
+    env = dict(os.environ, PCABI_POISON=byte)
     r = subprocess.run([sys.executable, '-u', os.path.join(root, 'tests', 'poisoned_middle.py')], env=env,
                        capture_output=True, text=True, timeout=400)
     print(r.stdout)

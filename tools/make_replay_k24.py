@@ -149,6 +149,17 @@ def main():
             s = s.strip()
             if mode == 'nolds' and ('ds_read' in s or 'lgkmcnt' in s):
                 continue                       # no LDS read, no wait: the destinations keep old values
+            if mode == 'nolds_mov' and 'lgkmcnt' in s:
+                continue
+            if mode == 'nolds_mov' and s.startswith('ds_read'):
+                # a fresh value from a register no recent VALU wrote (v70 / v71: the quad read's
+                # destinations, never written in this variant): exact's dependency pattern, no LDS
+                m2 = re.match(r'^ds_read_b(32|64)\s+(v\d+|v\[\d+:\d+\]),', s)
+                dst = m2.group(2)
+                if m2.group(1) == '64':
+                    continue
+                out.append('v_mov_b32_e32 %s, v71' % dst)
+                continue
             if mode == 'nowait' and 'lgkmcnt' in s:
                 continue
             if mode == 'sgprlit' and s.startswith('v_') and '_e32' in s:
@@ -190,7 +201,7 @@ def main():
     # the *4 copies run at the other 4-byte code phase (same instructions, own labels)
     for tag, mode in (('exact', 'exact'), ('nolds', 'nolds'), ('nowait', 'nowait'), ('sgprlit', 'sgprlit'),
                       ('max3split', 'max3split'), ('maxadd', 'maxadd'), ('inter2', 'inter2'), ('exact4', 'exact'),
-                      ('nolds4', 'nolds'), ('vgconst', 'vgconst')):
+                      ('nolds4', 'nolds'), ('vgconst', 'vgconst'), ('nolds_mov', 'nolds_mov')):
         header, out = variant(tag, mode)
         inc.append('#define RP_HEADER_%s "%s"' % (tag.upper(), header))
         inc.append('#define RP_EXIT_%s ".Lrp_%s_exit:\\n"' % (tag.upper(), tag))
@@ -224,6 +235,11 @@ def main():
     valu = sum(v for k, v in counts.items() if k.startswith('v_'))
     if os.environ.get('REPLAY_NO_INC') == '1':    # extraction only (ISA of the current source)
         return 0
+    # tools/replay_k24.hip's register setup (RP_SETUP) is written for the r05 loop (the source at
+    # faa8f29): LDS row stride in s57, table base in v16, constants in s16 / s28. Refuse another.
+    if not any('v_mad_u32_u24 v0, v0, s57, v16' in l for l in text):
+        raise SystemExit('this loop is not the r05 one the replay setup is written for: build it from the r05 '
+                         'source (git show faa8f29:custom_porechop_abi_amd/csrc/pcabi_dp.h) or use REPLAY_NO_INC=1')
     with open(os.path.join(ROOT, 'tools', 'replay_k24_body.inc'), 'w') as f:
         f.write('\n'.join(inc) + '\n')
     print('loop header .LBB%s: %d lines, %d VALU per pass, exits to %s; vregs up to v%d, sregs %s' % (

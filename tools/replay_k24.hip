@@ -140,6 +140,7 @@ RP_KERNEL(k_sgprlit, SGPRLIT, RP_SGPRLIT_SETUP, PAD0, RP_CLOBBER_V, RP_CLOBBER_S
 RP_KERNEL(k_max3split, MAX3SPLIT, "", PAD0, RP_CLOBBER_V, RP_CLOBBER_S)
 RP_KERNEL(k_maxadd, MAXADD, "", PAD0, RP_CLOBBER_V, RP_CLOBBER_S)
 RP_KERNEL(k_inter2, INTER2, RP_SETUP_INTER2, PAD0, RP_CLOBBER_V, RP_CLOBBER_V2, RP_CLOBBER_S)
+RP_KERNEL(k_nolds_mov, NOLDS_MOV, "", PAD0, RP_CLOBBER_V, RP_CLOBBER_S)
 RP_KERNEL(k_vgconst, VGCONST, "v_mov_b32 v72, s16\n v_mov_b32 v73, s28\n", PAD0, RP_CLOBBER_V, "v72", "v73",
           RP_CLOBBER_S)
 
@@ -251,6 +252,7 @@ int main(int argc, char **argv) {
         {"max3split", k_max3split, RP_VALU_MAIN_MAX3SPLIT, RP_VALU_LOAD_MAX3SPLIT, RP_VALU_HALF_MAX3SPLIT, 1},
         {"maxadd", k_maxadd, RP_VALU_MAIN_MAXADD, RP_VALU_LOAD_MAXADD, RP_VALU_HALF_MAXADD, 1},
         {"inter2", k_inter2, RP_VALU_MAIN_INTER2, RP_VALU_LOAD_INTER2, RP_VALU_HALF_INTER2, 2},
+        {"nolds_mov", k_nolds_mov, RP_VALU_MAIN_NOLDS_MOV, RP_VALU_LOAD_NOLDS_MOV, RP_VALU_HALF_NOLDS_MOV, 1},
         {"vgconst", k_vgconst, RP_VALU_MAIN_VGCONST, RP_VALU_LOAD_VGCONST, RP_VALU_HALF_VGCONST, 1},
     };
     // waves per SIMD: 0 = as many as the registers allow; else capped through dynamic LDS (a block
@@ -262,7 +264,7 @@ int main(int argc, char **argv) {
     std::vector<Run> runs;
     for (int v = 0; v < (int)(sizeof(vs) / sizeof(vs[0])); ++v) runs.push_back({v, 0});
     for (int w : {3, 4, 5, 6}) runs.push_back({0, w});
-    runs.push_back({9, 5});
+    runs.push_back({10, 5});
     for (const Run &r : runs) {
         const Variant &v = vs[r.v];
         const int lds = lds_for(r.waves);
