@@ -656,6 +656,11 @@ int64_t pcabi_fastx_record_start(const pcabi_fastx *r, int64_t byte) {
     return (int64_t)n;
 }
 
+int64_t pcabi_fastx_remaining(const pcabi_fastx *r) {
+    if (!r || !r->map) return -1;
+    return r->end > r->pos ? (int64_t)(r->end - r->pos) : 0;
+}
+
 int pcabi_fastx_set_range(pcabi_fastx *r, int64_t begin, int64_t end) {
     if (!r || !r->map) return fail(PCABI_E_ARG, "byte ranges need a plain (memory-mapped) file");
     if (begin < 0 || end < begin || (size_t)end > r->map_len) return fail(PCABI_E_ARG, "byte range outside the file");

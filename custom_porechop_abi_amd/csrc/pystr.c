@@ -39,13 +39,20 @@ static inline void pf_attrs(PyObject *o, int stage) {
         __builtin_prefetch(o);
         return;
     }
+#if PY_VERSION_HEX >= 0x030B0000
+    /* 3.11+: objects with managed / inline-values dicts have no dict until one is asked for, and
+     * _PyObject_GetDictPtr would create it from the inline values -- an allocation per object
+     * ahead of the cursor that also turns off the inline-values fast path. Only the
+     * object itself is prefetched there. */
+    (void)o;
+    return;
+#else
     PyObject **dp = _PyObject_GetDictPtr(o);
     if (!dp || !*dp) return;
     if (stage == 1) {
         __builtin_prefetch(*dp);
         return;
     }
-#if PY_VERSION_HEX < 0x030B0000
     PyDictObject *d = (PyDictObject *)*dp;
     if (d->ma_values) {
         __builtin_prefetch(d->ma_values);

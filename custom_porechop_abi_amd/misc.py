@@ -49,6 +49,7 @@ def _declare(L):
         'pcabi_reads_write': ([P, ctypes.c_char_p, c_int, c_int, c_int, P, P, P, P, c_int, c_int, c_int, P], c_int),
         'pcabi_fastx_record_start': ([P, i64], i64),
         'pcabi_fastx_set_range': ([P, i64, i64], c_int),
+        'pcabi_fastx_remaining': ([P], i64),
         'pcabi_fastx_next_text': ([P, i64, ctypes.POINTER(P), ctypes.POINTER(i64)], c_int),
     }
     for name, (a, r) in sig.items():
@@ -218,11 +219,27 @@ def record_boundaries(path, parts):
         L.pcabi_fastx_close(h)
 
 
-def read_batches(path, max_reads=100000, max_bases=1 << 30, raw=False, byte_range=None, first_reads=None):
+def ramp_sizes(max_reads, remaining_reads=None, done=0):
+    """The next batch's read count for a pipeline's ramp (misc.read_batches ramp=True): batches
+    grow from max_reads / 8 by doubling (the later stages start after a small first parse) and,
+    once fewer than 1.5 x max_reads reads remain (remaining_reads, estimated from the bytes left),
+    take half of what remains, down to max_reads / 8 (the last write is a small one, overlapped by
+    the trims before it). done: batches already read."""
+    lo = max(1, max_reads // 8)
+    want = min(max_reads, lo << done)
+    if remaining_reads is not None and remaining_reads < 1.5 * max_reads:
+        want = min(want, remaining_reads if remaining_reads <= 2 * lo else (remaining_reads + 1) // 2)
+    return max(1, int(want))
+
+
+def read_batches(path, max_reads=100000, max_bases=1 << 30, raw=False, byte_range=None, first_reads=None,
+                 ramp=False):
     """Stream a FASTA / FASTQ(.gz) file as ReadBatch objects (pcabi_fastx_next); byte_range =
     (begin, end) record starts of a plain file (record_boundaries) reads only that range;
     first_reads: the first batch's size, if other than max_reads (a pipeline starts its later
-    stages sooner on a small first batch)."""
+    stages sooner on a small first batch); ramp: batch sizes from ramp_sizes (a plain file's last
+    batches shrink too, from the bytes left and the bytes per read so far). Batching never changes
+    what is read or written, only when."""
     L = _declare(lib())
     h = ctypes.c_void_p()
     rc = L.pcabi_fastx_open(os.fsencode(path), int(raw), ctypes.byref(h))
@@ -232,16 +249,27 @@ def read_batches(path, max_reads=100000, max_bases=1 << 30, raw=False, byte_rang
         L.pcabi_fastx_close(h)
         raise ValueError(_open_error(path))
     try:
-        want = int(first_reads) if first_reads else int(max_reads)
+        want = int(first_reads) if first_reads else (ramp_sizes(int(max_reads)) if ramp else int(max_reads))
+        left0 = L.pcabi_fastx_remaining(h)
+        n_done, b_done, k = 0, 0, 0
         while True:
             b = ctypes.c_void_p()
             n = L.pcabi_fastx_next(h, want, int(max_bases), ctypes.byref(b))
-            want = int(max_reads)
             if n < 0:
                 raise ValueError(_open_error(path))
             if n == 0:
                 L.pcabi_reads_free(b)
                 return
+            k += 1
+            want = int(max_reads)
+            if ramp:
+                left = L.pcabi_fastx_remaining(h)
+                n_done += n
+                est = None
+                if left >= 0 and left0 > 0:
+                    b_done = left0 - left
+                    est = int(left * n_done / max(1, b_done))
+                want = ramp_sizes(int(max_reads), est, k)
             yield ReadBatch(b)
     finally:
         L.pcabi_fastx_close(h)

@@ -271,7 +271,9 @@ class FileTrimmer(object):
                 if byte_range is not None:
                     raise ValueError('byte ranges apply to a single plain file, not to a directory')
             for f, alb in files:
-                for b in misc.read_batches(f, max_reads=max_reads, byte_range=byte_range):
+                # batch sizes ramp up at the start and down at the end (misc.ramp_sizes): the first
+                # parse and the last write are small, so they overlap the other stages
+                for b in misc.read_batches(f, max_reads=max_reads, byte_range=byte_range, ramp=True):
                     yield b, alb
 
         def produce():

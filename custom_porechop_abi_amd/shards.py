@@ -55,29 +55,37 @@ def _device_tensor(values, group):
 
 
 def rank_device(device=None):
-    """The GPU of this rank: `device` if given, else LOCAL_RANK (torch.distributed.run sets it; a
-    LOCAL_RANK past the node's GPU count is an error, not a shared card), else the global rank
-    modulo the node's GPU count (launchers that set RANK only, srun / MPI style: one process per GPU
-    on each node), else 0."""
+    """The GPU of this rank: `device` if given, else the node-local rank a launcher publishes
+    (LOCAL_RANK from torch.distributed.run, or Open MPI's / MVAPICH's / Slurm's / Intel MPI's; one
+    past the node's GPU count is an error, not a shared card), else the global rank when the world
+    fits the node's GPUs; a larger world without a local rank is an error unless PCABI_SHARE_GPUS=1
+    (rank mod GPUs). 0 outside torch.distributed."""
     import os
     import warnings
-    import torch
     if device is not None:
         return int(device)
+    import torch
     n = torch.cuda.device_count()   # counting does not initialise the GPU
-    if 'LOCAL_RANK' in os.environ:
-        dev = int(os.environ['LOCAL_RANK'])
-        if n > 0 and dev >= n:
-            raise RuntimeError('LOCAL_RANK %d but this node has %d GPU(s): one process per GPU' % (dev, n))
-        return dev
+    # the node-local rank as torchrun, Open MPI, MVAPICH, Slurm or Intel MPI publish it
+    for var in ('LOCAL_RANK', 'OMPI_COMM_WORLD_LOCAL_RANK', 'MV2_COMM_WORLD_LOCAL_RANK', 'SLURM_LOCALID',
+                'MPI_LOCALRANKID'):
+        if var in os.environ:
+            dev = int(os.environ[var])
+            if n > 0 and dev >= n:
+                raise RuntimeError('%s %d but this node has %d GPU(s): one process per GPU' % (var, dev, n))
+            return dev
     dist = _dist()
     if not (dist.is_available() and dist.is_initialized()):
         return 0
     rank, world = dist.get_rank(), dist.get_world_size()
     if n > 0 and world > n:
-        warnings.warn('LOCAL_RANK is not set and the world (%d) exceeds this node\'s %d GPU(s): rank %d takes GPU %d '
-                      '(rank mod GPUs, one process per GPU on each node); set LOCAL_RANK on multi-node jobs'
-                      % (world, n, rank, rank % n))
+        # no node-local rank: one node oversubscribed, or a launcher that publishes none. Sharing
+        # cards (rank mod GPUs) is opt-in (PCABI_SHARE_GPUS=1), not a silent fallback.
+        if os.environ.get('PCABI_SHARE_GPUS') != '1':
+            raise RuntimeError('the world (%d ranks) exceeds this node\'s %d GPU(s) and no node-local rank is set '
+                               '(LOCAL_RANK, OMPI_COMM_WORLD_LOCAL_RANK, SLURM_LOCALID, ...): one process per GPU; '
+                               'PCABI_SHARE_GPUS=1 lets rank r take GPU r mod %d' % (world, n, n))
+        warnings.warn('PCABI_SHARE_GPUS=1: rank %d takes GPU %d of %d' % (rank, rank % n, n))
     return rank % n if n > 0 else rank
 
 
@@ -212,22 +220,33 @@ def spool_distribute(in_path, spool, job, world, chunk_bytes=None, depth=SPOOL_D
     chunk_bytes = int(chunk_bytes or SPOOL_CHUNK_BYTES)
     pending = [[] for _ in range(world)]
     c = 0
+
+    def beat():                               # liveness for the consumers' bounded wait
+        with open(pre + 'beat', 'w'):
+            pass
+
     try:
+        beat()
         for f, alb in misc.input_files(in_path):
             for mv in misc.text_chunks(f, chunk_bytes):
                 r = c % world
+                t_beat = time.monotonic()
                 while True:
                     pending[r] = [x for x in pending[r] if os.path.exists(x)]
                     if len(pending[r]) < depth:
                         break
                     if (stop is not None and stop.is_set()) or os.path.exists(pre + 'error'):
                         return                 # this rank or another one gave up
+                    if time.monotonic() - t_beat > 1.0:
+                        beat()
+                        t_beat = time.monotonic()
                     time.sleep(0.005)
                 path = '%s%d_%s.fq' % (pre, c, alb if alb is not None else '-')
                 with open(path + '.tmp', 'wb') as fo:
                     fo.write(mv)
                 os.replace(path + '.tmp', path)
                 pending[r].append(path)
+                beat()
                 c += 1
         with open(pre + 'end.tmp', 'w') as fo:
             fo.write(str(c))
@@ -241,9 +260,12 @@ def spool_fail_cleanup(spool, job, rank, world, wait_s=30.0, poll=0.01):
     """A failed rank's share of the spool cleanup (the job raised on this rank): its own spans that
     were never consumed go (span c belongs to rank c % world), then an acknowledgement marker. Rank
     0 -- which has joined the distributor, so nothing new appears -- removes every file of the job
-    once every rank has acknowledged (or after wait_s); the other ranks wait (bounded) until it has,
-    so a launcher that kills the rest of a job when one process fails
-    (torch.multiprocessing.spawn) cannot cut rank 0's cleanup short."""
+    once every rank has acknowledged; the other ranks wait (bounded) until it has, so a launcher that
+    kills the rest of a job when one process fails (torch.multiprocessing.spawn) cannot cut rank 0's
+    cleanup short. If some rank has not acknowledged within wait_s (it is still trimming a span and
+    has not seen the failure yet), rank 0 removes the spans but leaves the .error / .end markers and
+    the acknowledgements, plus a .left marker: the late rank still finds the error and raises
+    instead of polling for spans forever, and the last rank to acknowledge removes what is left."""
     import os
     import time
     pre = _spool_prefix(spool, job)
@@ -261,23 +283,47 @@ def spool_fail_cleanup(spool, job, rank, world, wait_s=30.0, poll=0.01):
             rm(f)                                 # a span (or its .tmp) of this rank
     with open(pre + 'ack%d' % rank, 'w'):
         pass
-    t_end = time.monotonic() + wait_s
-    while time.monotonic() < t_end:
-        names = set(os.listdir(d))
-        if rank == 0 and all(base + 'ack%d' % r in names for r in range(world)):
-            break
-        if rank != 0 and base + 'ack%d' % rank not in names:
-            return                                # rank 0 has cleaned up
-        time.sleep(poll)
-    if rank == 0:
+
+    def all_acked(names):
+        return all(base + 'ack%d' % r in names for r in range(world))
+
+    def rm_all():
         for f in os.listdir(d):
             if f.startswith(base):
                 rm(f)
 
+    t_end = time.monotonic() + wait_s
+    while time.monotonic() < t_end:
+        names = set(os.listdir(d))
+        if rank == 0 and all_acked(names):
+            rm_all()
+            return
+        if rank != 0:
+            if base + 'ack%d' % rank not in names:
+                return                            # rank 0 has cleaned up
+            if base + 'left' in names and all_acked(names):
+                rm_all()                          # rank 0 left first: the last rank cleans up
+                return
+        time.sleep(poll)
+    if rank == 0:
+        # a rank has not seen the failure yet: everything but the markers it needs to raise
+        keep = {base + x for x in ('error', 'end', 'left')} | {base + 'ack%d' % r for r in range(world)}
+        for f in os.listdir(d):
+            if f.startswith(base) and f not in keep:
+                rm(f)
+        with open(pre + 'left', 'w'):
+            pass
+        if all_acked(set(os.listdir(d))):         # it acknowledged meanwhile
+            rm_all()
 
-def spool_batches(spool, job, rank, world, max_reads, poll=0.005):
+
+def spool_batches(spool, job, rank, world, max_reads, poll=0.005, stale_s=600.0):
     """This rank's spans from the distributor, parsed: yields ((c, j), ReadBatch, albacore) for
-    batch j of span c = rank, rank + world, ... in order, deleting each span file once parsed."""
+    batch j of span c = rank, rank + world, ... in order, deleting each span file once parsed.
+    The wait for a span is bounded: the distributor touches a .beat marker while it runs (each span
+    written, and every second it waits for a slow rank); if neither a span, the .end marker nor the
+    .error marker appears while the beat is older than stale_s seconds (the distributor's process
+    died without leaving .error), this rank raises instead of polling forever."""
     import os
     import time
     from . import misc
@@ -285,6 +331,7 @@ def spool_batches(spool, job, rank, world, max_reads, poll=0.005):
     d, base = os.path.split(pre)
     c = rank
     while True:
+        t_wait = time.time()
         while True:
             if os.path.exists(pre + 'error'):
                 with open(pre + 'error') as f:
@@ -297,6 +344,14 @@ def spool_batches(spool, job, rank, world, max_reads, poll=0.005):
                     if c >= int(f.read()):
                         return
                 continue                       # the marker came after the span: look again
+            if time.time() - t_wait > stale_s:
+                try:
+                    beat = os.path.getmtime(pre + 'beat')
+                except OSError:
+                    beat = t_wait
+                if time.time() - beat > stale_s:
+                    raise RuntimeError('input distributor silent for %.0f s (span %d of job %s never came)'
+                                       % (time.time() - beat, c, job))
             time.sleep(poll)
         path = os.path.join(d, mine[0])
         alb = mine[0][len(base) + len(str(c)) + 1:-3]

@@ -559,6 +559,10 @@ int pcabi_fastx_type(const pcabi_fastx *r);
  *       file size); a fresh reader (no record read yet). */
 int64_t pcabi_fastx_record_start(const pcabi_fastx *r, int64_t byte);
 int pcabi_fastx_set_range(pcabi_fastx *r, int64_t begin, int64_t end);
+/* Bytes of a plain file (or of its set range) not yet parsed; -1 for a gzip input, whose decoded
+ * size is unknown. misc.read_batches sizes a pipeline's last batches from it (a ramp-down, so the
+ * final write overlaps the trims before it). */
+int64_t pcabi_fastx_remaining(const pcabi_fastx *r);
 /* Streaming split of any input (gzip included) into spans of decoded text holding whole records,
  * for a distributor that hands spans to other readers (shards.trim_file_sharded): the next span,
  * at least max_bytes long unless the input ends (one record may overshoot), cut where a fresh

@@ -381,3 +381,93 @@ def test_sharded_albacore_directory_matches_reference(run, tmp_path):
             assert open(os.path.join(bdir, name)).read() == txt, name
     else:
         assert open(out_path).read() == exp['output']
+
+
+def test_spool_failure_reaches_a_late_rank(tmp_path):
+    """rank 0 fails, acknowledges and waits wait_s for the others; rank 1 is still busy
+    past wait_s. Rank 0 must leave the .error marker (and the acknowledgements) behind, so that
+    rank 1, reaching spool_batches later, raises instead of polling for spans forever -- and rank 1,
+    the last to acknowledge, removes every file of the job."""
+    import threading
+    import time
+    from custom_porechop_abi_amd import shards
+    spool, job, world = str(tmp_path), 'jlate', 2
+    pre = shards._spool_prefix(spool, job)
+    for c in (0, 1, 2):                      # spans never consumed (c % world is the owner)
+        with open('%s%d_-.fq' % (pre, c), 'w') as f:
+            f.write('@r\nACGT\n+\n!!!!\n')
+    with open(pre + 'error', 'w') as f:      # what trim_file_sharded writes when a rank raises
+        f.write('rank 0: RuntimeError: boom')
+    out = {}
+
+    def rank0():
+        shards.spool_fail_cleanup(spool, job, 0, world, wait_s=0.3)
+        out['r0'] = True
+
+    def rank1():
+        time.sleep(0.8)                      # past rank 0's wait
+        try:
+            for _ in shards.spool_batches(spool, job, 1, world, 100, stale_s=5.0):
+                pass
+        except RuntimeError as ex:
+            out['r1_raised'] = str(ex)
+        shards.spool_fail_cleanup(spool, job, 1, world, wait_s=0.3)
+
+    ts = [threading.Thread(target=rank0, daemon=True), threading.Thread(target=rank1, daemon=True)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=20)
+    assert not any(t.is_alive() for t in ts), 'a rank hung'
+    assert out.get('r0') and 'input distributor failed' in out.get('r1_raised', '')
+    assert not [x for x in os.listdir(spool) if x.startswith(os.path.basename(pre))], os.listdir(spool)
+
+
+def test_spool_wait_is_bounded_without_a_distributor(tmp_path):
+    """A distributor that died without an .error marker (its process killed) stops beating:
+    spool_batches raises once its beat is older than stale_s instead of waiting forever."""
+    import time
+    from custom_porechop_abi_amd import shards
+    spool, job = str(tmp_path), 'jdead'
+    pre = shards._spool_prefix(spool, job)
+    with open(pre + 'beat', 'w'):
+        pass
+    old = time.time() - 100
+    os.utime(pre + 'beat', (old, old))
+    t0 = time.monotonic()
+    with pytest.raises(RuntimeError, match='silent'):
+        for _ in shards.spool_batches(spool, job, 0, 2, 100, stale_s=0.3):
+            pass
+    assert time.monotonic() - t0 < 10
+
+
+def test_rank_device_rules(monkeypatch):
+    """an explicit device needs no torch query; a node-local rank from any common
+    launcher wins; a world larger than the node's GPUs without one is an error unless sharing is
+    asked for (PCABI_SHARE_GPUS=1)."""
+    import types
+    import torch
+    from custom_porechop_abi_amd import shards
+    for v in ('LOCAL_RANK', 'OMPI_COMM_WORLD_LOCAL_RANK', 'MV2_COMM_WORLD_LOCAL_RANK', 'SLURM_LOCALID',
+              'MPI_LOCALRANKID', 'PCABI_SHARE_GPUS'):
+        monkeypatch.delenv(v, raising=False)
+    assert shards.rank_device(3) == 3
+    monkeypatch.setattr(torch.cuda, 'device_count', lambda: 8)
+    monkeypatch.setenv('SLURM_LOCALID', '5')
+    assert shards.rank_device() == 5
+    monkeypatch.setenv('SLURM_LOCALID', '9')
+    with pytest.raises(RuntimeError, match='one process per GPU'):
+        shards.rank_device()
+    monkeypatch.delenv('SLURM_LOCALID')
+    fake = types.SimpleNamespace(is_available=lambda: True, is_initialized=lambda: True, get_rank=lambda: 11,
+                                 get_world_size=lambda: 16)
+    monkeypatch.setattr(shards, '_dist', lambda: fake)
+    with pytest.raises(RuntimeError, match='PCABI_SHARE_GPUS'):
+        shards.rank_device()
+    monkeypatch.setenv('PCABI_SHARE_GPUS', '1')
+    with pytest.warns(UserWarning):
+        assert shards.rank_device() == 3
+    fake.get_world_size = lambda: 8
+    fake.get_rank = lambda: 6
+    monkeypatch.delenv('PCABI_SHARE_GPUS')
+    assert shards.rank_device() == 6

@@ -56,6 +56,11 @@ PY
         PCABI_POISON=$b PCABI_LIB=$R/perf_variants/r05bug.so timeout -k 10 400 python -u tests/poisoned_middle.py > $OUT/poison_r05bug_$b.log 2>&1
         echo "r05bug variant, poison $b: rc=$? (nonzero expected for 0x7f)"; tail -3 $OUT/poison_r05bug_$b.log
       done ;;
+    trace)
+      # kernel trace (per-dispatch begin / end) of the headline bench (TRACE_ARGS), for timelines
+      export TMPDIR=/tmp
+      ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace -o run -- python3 $R/bench.py --sub 0 --steps 3 --warmup 1 --cpu-sample 0 --check 0 ${TRACE_ARGS:-} > $OUT/trace.json 2> $OUT/trace.err ) || { echo "trace failed rc=$?"; tail -5 $OUT/trace.err; exit 1; }
+      ls $OUT/trace ;;
     *) echo "unknown stage $st"; exit 2 ;;
   esac
 done
