@@ -61,6 +61,17 @@ PY
       export TMPDIR=/tmp
       ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace -o run -- python3 $R/bench.py --sub 0 --steps 3 --warmup 1 --cpu-sample 0 --check 0 ${TRACE_ARGS:-} > $OUT/trace.json 2> $OUT/trace.err ) || { echo "trace failed rc=$?"; tail -5 $OUT/trace.err; exit 1; }
       ls $OUT/trace ;;
+    midab)
+      # in-process A/B of a library switch over the middle workloads: AB="NAME=v0,v1"
+      for L in 8000 20000; do
+        timeout -k 10 300 python bench.py --workload middle --mean-len $L --steps ${AB_STEPS:-20} --warmup 2 --ab "$AB" ${MID_ARGS:-} > $OUT/midab_$L.json 2> $OUT/midab_$L.err || { echo "midab $L failed rc=$?"; tail -20 $OUT/midab_$L.err; exit 1; }
+        python -c "import json,sys; d=json.load(open(sys.argv[1])); print($L, d.get('middle_ms_per_step'), {k: {v: x['median_ms'] for v, x in y.items()} for k, y in (d.get('ab') or {}).items()}, d.get('parity_spot_check'))" $OUT/midab_$L.json
+      done ;;
+    e2e)
+      for th in ${E2E_THREADS:-16}; do
+        PCABI_PIPE_TRACE=1 PCABI_IO_THREADS=$th timeout -k 10 300 python bench.py --workload e2e --reads 100000 --steps 2 --warmup 1 ${E2E_ARGS:-} > $OUT/e2e_t$th.json 2> $OUT/e2e_t$th.err || { echo "e2e failed rc=$?"; tail -20 $OUT/e2e_t$th.err; exit 1; }
+        python -c "import json,sys; d=json.load(open(sys.argv[1])); print('io threads $th', d['ms_per_step'], d['step_vs_slowest_stage'], d['breakdown_ms_per_step'], d['parity_spot_check']['output_identical'])" $OUT/e2e_t$th.json
+      done ;;
     *) echo "unknown stage $st"; exit 2 ;;
   esac
 done

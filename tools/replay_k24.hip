@@ -161,9 +161,15 @@ RP_KERNEL(k_vgconst, VGCONST, "v_mov_b32 v72, s16\n v_mov_b32 v73, s28\n", PAD0,
 #define I_MINI(i) "v_min_i32 %" #i ", %" #i ", %8\n"
 #define I_MAXF(i) "v_max_f32 %" #i ", %" #i ", %8\n"
 #define I_CELL(i) I_ADD(i) I_MAX(i) I_ADD(i) I_ANDLIT(i) I_MAX(i) I_ADD(i) I_MAX3(i) I_ANDLIT(i) I_ADD(i)
+#define I_CMPCND(i) "v_cmp_eq_u32 vcc, %" #i ", %8\n v_cndmask_b32 %" #i ", %9, %8, vcc\n"
+#define I_CND64(i) "v_cndmask_b32_e64 %" #i ", %" #i ", %8, %11\n"
+#define I_BFE(i) "v_bfe_u32 %" #i ", %8, %" #i ", 4\n"
+#define I_CMPS(i) "v_cmp_gt_i32 %11, %" #i ", %8\n"
+#define I_XORMIN(i) "v_xor_b32 %" #i ", %" #i ", %8\n v_min_u32 %" #i ", 1, %" #i "\n"
 
 template <int OP>
 __global__ __launch_bounds__(256) void k_rate(int *out, int seed, int iters, unsigned long long *clk) {
+    const unsigned long long m64 = __builtin_amdgcn_read_exec() & 0x5555555555555555ull;
     int a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
     int b = seed, c = ~seed;
     const int sg = __builtin_amdgcn_readfirstlane(seed * 3);
@@ -172,7 +178,7 @@ __global__ __launch_bounds__(256) void k_rate(int *out, int seed, int iters, uns
     for (int i = 0; i < iters; ++i) {
 #define RATE_CASE(K, BODY) \
         if (OP == K) asm volatile(P8(BODY) P8(BODY) : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), \
-                                  "+v"(a6), "+v"(a7) : "v"(b), "v"(c), "s"(sg) : "vcc");
+                                  "+v"(a6), "+v"(a7) : "v"(b), "v"(c), "s"(sg), "s"(m64) : "vcc");
         RATE_CASE(0, I_ADD)
         RATE_CASE(1, I_ANDLIT)
         RATE_CASE(2, I_ANDSG)
@@ -188,6 +194,10 @@ __global__ __launch_bounds__(256) void k_rate(int *out, int seed, int iters, uns
         RATE_CASE(12, I_MINI)
         RATE_CASE(13, I_MAXF)
         RATE_CASE(14, I_CELL)
+        RATE_CASE(15, I_CMPCND)
+        RATE_CASE(16, I_CND64)
+        RATE_CASE(17, I_BFE)
+        RATE_CASE(18, I_XORMIN)
     }
     const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     if ((threadIdx.x & 63) == 0) {
@@ -305,13 +315,17 @@ int main(int argc, char **argv) {
     CHECK(hipMalloc(&d_rclk, (size_t)rblocks * 4 * 16));
     const char *names[] = {"v_add_u32", "v_and_b32 literal", "v_and_b32 sgpr", "v_max_i32", "v_max3_i32",
                            "v_max_u32", "v_max_i16", "v_pk_max_i16", "v_cndmask_b32", "v_add3_u32",
-                           "v_med3_i32", "v_subrev_u32", "v_min_i32", "v_max_f32", "tagged cell (6 full + 3 max)"};
+                           "v_med3_i32", "v_subrev_u32", "v_min_i32", "v_max_f32", "tagged cell (6 full + 3 max)",
+                           "v_cmp_eq + v_cndmask (vcc) pair", "v_cndmask_b32_e64 (sgpr-pair mask)", "v_bfe_u32",
+                           "v_xor + v_min_u32 pair"};
     void (*rk[])(int *, int, int, unsigned long long *) = {k_rate<0>, k_rate<1>, k_rate<2>, k_rate<3>, k_rate<4>,
                                                             k_rate<5>, k_rate<6>, k_rate<7>, k_rate<8>, k_rate<9>,
                                                             k_rate<10>, k_rate<11>, k_rate<12>, k_rate<13>,
-                                                            k_rate<14>};
-    for (int op = 0; op < 15; ++op) {
-        const int per_iter = op == 14 ? 9 * 16 : 16;   // wave-instructions per chain-set pass, x 8 chains
+                                                            k_rate<14>, k_rate<15>, k_rate<16>, k_rate<17>,
+                                                            k_rate<18>};
+    for (int op = 0; op < 19; ++op) {
+        // wave-instructions per asm statement (8 chains x 2 copies x instructions per chain step)
+        const int per_iter = op == 14 ? 9 * 16 : ((op == 15 || op == 18) ? 2 * 16 : 16);
         auto launch = [&]() { hipLaunchKernelGGL(rk[op], dim3(rblocks), dim3(256), 0, 0, d_out, 3, iters, d_rclk); };
         launch();
         CHECK(hipGetLastError());
