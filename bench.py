@@ -88,6 +88,10 @@ def parse():
                     help='reference_job: 1 = the set search\'s two sides side by side (stream2; r04 A/B: 5.13 vs '
                          '5.23 ms per step); 0 = one after the other (each side\'s dominant launch then has the GPU '
                          'to itself, the roofline\'s events)')
+    ap.add_argument('--rj-multi', type=int, default=1,
+                    help='reference_job: 1 (default, r06) = the set search of both read ends in one '
+                         'pcabi_align_cross_multi_dev call, and the kept-set end trim likewise (grouped launches); 0 = '
+                         'per-side calls as --rj-check-overlap / --rj-end-streams say (r05)')
     ap.add_argument('--rj-end-streams', type=int, default=1,
                     help='reference_job: 1 = each kept adapter\'s end-trim cross product on a stream of its own '
                          '(r04x: 4.69-4.71 vs 4.78-4.84 ms per step); 0 = each side\'s table on one stream')
@@ -97,10 +101,13 @@ def parse():
     ap.add_argument('--head-side-streams', type=int, default=0,
                     help='headline schedule: the library\'s side streams while both sides\' smaller buckets run on two '
                          'caller streams at once; 0 (default, r04r: 7.61 vs 7.68 ms) or 1')
-    ap.add_argument('--rest-overlap', type=int, default=1,
-                    help='headline: 3 = after both dominant launches, both sides\' smaller buckets dealt onto the two '
-                         'caller streams by cost; 2 = each on its own stream; 1 = the two sides\' calls side by side; '
-                         '0 = after each side\'s dominant launch')
+    ap.add_argument('--rest-overlap', type=int, default=5,
+                    help='headline schedule: 5 (default, r06) = both read ends in ONE pcabi_align_cross_multi_dev call '
+                         '(every run-tagged bucket of both sides in one grouped launch, the packed ones in another '
+                         'beside it); 4 = each side\'s dominant launch alone, then both sides\' smaller buckets in one '
+                         'multi call; 3 = after both dominant launches, both sides\' smaller buckets dealt onto the two '
+                         'caller streams by cost; 2 = each on its own stream; 1 = the two sides\' calls side by side '
+                         '(r05); 0 = after each side\'s dominant launch')
     ap.add_argument('--hw-queues', type=int, default=0,
                     help='GPU_MAX_HW_QUEUES for this process when the environment does not set it (0: HIP default, '
                          '4; r04 A/B with 8: headline 8.05 vs 7.61 ms, reference job 5.85 vs 5.23 ms)')
@@ -299,6 +306,15 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
     _lib.check(L.pcabi_event_create(ctypes.byref(ev_fork)), 'event')
     _lib.check(L.pcabi_event_create(ctypes.byref(ev_join)), 'event')
 
+    # --rest-overlap 4: both sides' smaller buckets in ONE pcabi_align_cross_multi_dev call (grouped
+    # launches per core family); 5: both sides' whole tables in one call (the dominant buckets grouped
+    # with the other run-tagged ones: one launch for both read ends, its events the roofline's)
+    def regions(key, res_key):
+        return _lib.cross_regions([(sd['d_tiles'], sd['d_toff'], sd['d_len'], n, int(sd['lens'].max()), sd[key][0],
+                                    sd[res_key], sd['stride']) for sd in sides if sd[key][1]])
+    rest_regions = regions('rest', 'd_res_rest') if args.rest_overlap == 4 else None
+    all_regions = regions('all', 'd_res') if args.rest_overlap == 5 else None
+
     n_groups = sum(len(sd['groups']) for sd in sides) if args.rest_overlap == 2 else 0
     g_streams, g_join = [], []
     for _ in range(n_groups):
@@ -408,6 +424,18 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
     def step(k=None, fused=False):
         fused = fused if k is None else timed_fused
         e = (None,) * 4 if k is None else tuple(ev[4 * k + i] for i in range(4))
+        if not fused and args.rest_overlap == 5:
+            for sd in sides:
+                _lib.check(L.pcabi_tile_windows_dev(d_codes, sd['d_off'], sd['d_len'], n, sd['d_toff'], sd['mq'],
+                                                    sd['d_tiles'], stream), 'tile')
+            # e0 / e1: the grouped run-tagged launch (the roofline's kernel); e2 / e3: the whole call
+            if e[2] is not None:
+                L.pcabi_event_record(e[2], stream)
+            _lib.check(L.pcabi_align_cross_multi_dev(all_regions, len(all_regions), *sc, stream, e[0], e[1]), 'align')
+            if e[3] is not None:
+                L.pcabi_event_record(e[3], stream)
+            epilogue()
+            return
         if fused or not args.rest_overlap:
             align_side(sides[0], e[0], e[1], fused=fused)
             align_side(sides[1], e[2], e[3], fused=fused)
@@ -426,6 +454,11 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
                 align_balanced()
                 epilogue()
                 return
+            if args.rest_overlap == 4:
+                _lib.check(L.pcabi_align_cross_multi_dev(rest_regions, len(rest_regions), *sc, stream, None, None),
+                           'align')
+                epilogue()
+                return
             L.pcabi_event_record(ev_fork, stream)
             L.pcabi_stream_wait_event(stream2, ev_fork)
             align_rest(sides[0], stream)
@@ -438,6 +471,8 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
     # library's side streams go off on its two streams (pcabi_stream_side_streams; one cross product at a time,
     # as the production schedule, keeps them on)
     two_streams = not timed_fused and args.rest_overlap in (1, 3)
+    if not timed_fused and args.rest_overlap in (4, 5):
+        L.pcabi_stream_side_streams(stream, 1)     # one (grouped) call at a time: its launches side by side
     # (per stream, r05: pcabi_stream_side_streams leaves every other caller of the library alone)
     if two_streams:
         for s_ in (stream, stream2):
@@ -475,6 +510,10 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
             _lib.check(L.pcabi_event_elapsed_ms(ctypes.byref(ms), ev[4 * k + 2 * side], ev[4 * k + 2 * side + 1]),
                        'elapsed')
             dom_ms[side].append(ms.value)
+    phase_ms = None
+    if args.rest_overlap == 5 and not timed_fused:
+        phase_ms = float(np.mean(dom_ms[1]))      # the whole multi call (both grouped launches)
+        dom_ms = [dom_ms[0], dom_ms[0]]           # one grouped launch for both sides
     dom_ms = [float(np.mean(x)) for x in dom_ms]
 
     # ---- algorithmic work (per GPU) ----
@@ -490,6 +529,23 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
     launch_ms = float(np.mean(dom_ms))
     launch_cells = float(np.mean(dom_cells))
     launch_bytes = float(np.mean(dom_bytes))
+    dom_kernel = DOM_KERNEL
+    phase = None
+    if args.rest_overlap == 5 and not timed_fused:
+        # the grouped run-tagged launch: every <= 32-row bucket of both sides
+        grp = lambda x: (len(x) + 3) // 4 * 4 <= 32
+        launch_cells = float(s_len64.sum() * La[[grp(x) for x in start_adps]].sum() +
+                             e_len64.sum() * Le[[grp(x) for x in end_adps]].sum())
+        launch_bytes = float(s_len64.sum() + e_len64.sum() + 32 * n * (sum(map(grp, start_adps)) + sum(map(grp, end_adps))))
+        launch_ms = dom_ms[0]
+        dom_kernel = 'k_align_group<0> (run-tagged core, every <= 32-row bucket of both read ends in one launch)'
+        # the align phase as a whole: both grouped launches (k_align_group<1>, the 36-52-row packed
+        # buckets, runs beside <0> and inside its span), every cell of the step over the call's time
+        phase = {'ms': round(phase_ms, 4), 'cells': cells,
+                 'achieved': round(cells * OPS_PER_CELL / (phase_ms * 1e-3) / 1e12, 3),
+                 'frac': round(cells * OPS_PER_CELL / (phase_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4),
+                 'what': 'pcabi_align_cross_multi_dev over both read ends: k_align_group<0> and <1> (events around '
+                         'the call)'}
     tops = launch_cells * OPS_PER_CELL / (launch_ms * 1e-3) / 1e12
     gbs = launch_bytes / (launch_ms * 1e-3) / 1e9
     step_ms = 1e3 * elapsed / args.steps
@@ -530,10 +586,11 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
         L.pcabi_stream_sync(stream)
         dt = (time.perf_counter() - t0) / args.steps
         L.pcabi_stream_side_streams(stream, -1)
-        subs['fused_schedule'] = {'value': round(n / dt, 1), 'unit': 'reads/s', 'ms_per_step': round(1e3 * dt, 4),
-                                  'steps': args.steps, 'what': 'the headline step with one cross product per side '
-                                  '(pcabi_align_cross_dev_marked): register buckets side by side with the dominant one '
-                                  '(side streams on)'}
+        subs['per_side_schedule'] = {'value': round(n / dt, 1), 'unit': 'reads/s', 'ms_per_step': round(1e3 * dt, 4),
+                                     'steps': args.steps, 'what': 'the headline step with one cross product per side '
+                                     '(pcabi_align_cross_dev_marked, the r05 production schedule): register buckets side '
+                                     'by side with the dominant one (side streams on); r06 production (the library\'s '
+                                     'end decisions, pipeline.FileTrimmer) is the headline\'s multi call'}
         subs['host_path'] = run_host_path(args, L, _lib, buf, s_off, s_len, e_off, e_len, sides, d_sres, d_eres, d_st,
                                           d_et, n, n_sa, n_ea, stream, start_adps, end_adps)
 
@@ -545,7 +602,7 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
     if rank == 0:
         value = world * n * args.steps / elapsed
         prof = load_traffic()   # the PMC traffic record: the headline configuration's dominant launch
-        if prof and not DOM_KERNEL.startswith(str(prof.get('kernel'))):
+        if prof and not dom_kernel.startswith(str(prof.get('kernel'))):
             prof = None         # recorded for another layout of the dominant bucket
         out = {
             'metric': ('reads/sec trimmed + demultiplexed (ONT reads x %d barcode sets)' % (len(sets) - kit_n)
@@ -580,15 +637,18 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
             'roofline': {'bound': 'valu', 'achieved': round(tops, 3), 'peak': round(VALU_PEAK_TOPS, 1),
                          'unit': 'Tops/s (int32 lane-ops)', 'frac': round(tops / VALU_PEAK_TOPS, 4),
                          'traffic': prof.get('traffic_bytes_per_launch') if prof and headline else None,
-                         'kernel': DOM_KERNEL,
+                         'kernel': dom_kernel,
                          'launch_ms': round(launch_ms, 4), 'cells_per_launch': int(launch_cells),
                          'schedule': ('production: one cross product per side, the dominant launch shares the GPU '
-                                      'with the small buckets' if timed_fused else 'dominant launch alone'),
+                                      'with the small buckets' if timed_fused else
+                                      'both read ends in one multi call: the grouped run-tagged launch, the grouped '
+                                      'packed launch beside it' if args.rest_overlap == 5 else 'dominant launch alone'),
                          'ops_per_cell': OPS_PER_CELL,
-                         'traffic_source': prof.get('source') if prof and headline else None},
+                         'traffic_source': prof.get('source') if prof and headline else None,
+                         'align_phase': phase},
             'hbm': {'achieved': round(gbs, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                     'frac': round(gbs / HBM_PEAK_GBS, 5), 'algorithmic_bytes_per_launch': int(launch_bytes),
-                    'kernel': DOM_KERNEL},
+                    'kernel': dom_kernel},
             'gcups_step': round(cells / (step_ms * 1e-3) / 1e9, 1),
             'cells_per_step': cells,
             'cpu_baseline': cpu,
@@ -905,6 +965,8 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
         sides.append(dict(d_off=h2d(w_off), d_len=h2d(w_len), d_toff=h2d(toff), d_tiles=dalloc(4 * nd),
                           mq=int(np.diff(toff).max() // 256), mx=int(w_len.max()), mx_chk=int(w_len[:n_chk].max()),
                           search=table(u), n_u=len(u), d_chk=dalloc(4 * 8 * len(u) * n_chk)))
+    search_regions = _lib.cross_regions([(sd['d_tiles'], sd['d_toff'], sd['d_len'], n_chk, sd['mx_chk'], sd['search'],
+                                          sd['d_chk'], sd['n_u'] * n_chk) for sd in sides])
     ev = [vp() for _ in range(11)]
     for e in ev:
         _lib.check(L.pcabi_event_create(ctypes.byref(e)), 'event')
@@ -924,6 +986,9 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
                       one=[[table([a]) for a in x] if args.rj_end_streams else [] for x in (st_, en_)])
             if mid:
                 _lib.check(L.pcabi_scan_create(ks['tabs'][2], ctypes.byref(ks['scan'])), 'scan_create')
+            ks['regions'] = _lib.cross_regions([(sd['d_tiles'], sd['d_toff'], sd['d_len'], n, sd['mx'], ks['tabs'][k],
+                                                  ks['d_res'][k], len(x) * n)
+                                                 for k, (sd, x) in enumerate(zip(sides, (st_, en_))) if x])
             kept_cache[names] = ks
         return kept_cache[names]
 
@@ -935,10 +1000,21 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
         for k, sd in enumerate(sides):
             _lib.check(L.pcabi_tile_windows_dev(work, sd['d_off'], sd['d_len'], n, sd['d_toff'], sd['mq'],
                                                 sd['d_tiles'], stream), 'tile')
-        if args.rj_check_overlap:
+        if args.rj_multi:
+            # both read ends' set search in one call; events around the whole call (ev[2] / ev[3])
+            L.pcabi_event_record(ev[2], stream)
+            _lib.check(L.pcabi_align_cross_multi_dev(search_regions, len(search_regions), *sc, stream, None, None),
+                       'align')
+            L.pcabi_event_record(ev[3], stream)
+            for k, sd in enumerate(sides):
+                L.pcabi_event_record(ev[4 + k], stream)
+                _lib.check(L.pcabi_best_full_identity_dev(sd['d_chk'], sd['n_u'] * n_chk, n_chk, sd['n_u'],
+                                                          vp(d_best.value + 8 * b0), stream), 'best')
+                b0 += sd['n_u']
+        if args.rj_check_overlap and not args.rj_multi:
             L.pcabi_event_record(ev[9], stream)
             L.pcabi_stream_wait_event(stream2, ev[9])
-        for k, sd in enumerate(sides):
+        for k, sd in enumerate(sides if not args.rj_multi else []):
             st_k = stream2 if (args.rj_check_overlap and k == 1) else stream
             # the check reads are the first n_check reads: their windows are the first tiles
             _lib.check(L.pcabi_align_cross_dev_marked(sd['d_tiles'], sd['d_toff'], sd['d_len'], n_chk, sd['mx_chk'],
@@ -947,7 +1023,7 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
             _lib.check(L.pcabi_best_full_identity_dev(sd['d_chk'], sd['n_u'] * n_chk, n_chk, sd['n_u'],
                                                       vp(d_best.value + 8 * b0), st_k), 'best')
             b0 += sd['n_u']
-        if args.rj_check_overlap:
+        if args.rj_check_overlap and not args.rj_multi:
             L.pcabi_event_record(ev[9], stream2)
             L.pcabi_stream_wait_event(stream, ev[9])
         maxima = np.empty(n_u, np.float64)
@@ -966,7 +1042,11 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
         # the two sides' few-adapter cross products side by side (start on `stream`, end on stream2):
         # with the kept sets each bucket holds one adapter (1,564 waves), too few to fill the chip alone
         L.pcabi_stream_wait_event(stream2, ev[1])
-        if args.rj_end_streams:
+        if args.rj_multi:
+            if len(ks['regions']):
+                _lib.check(L.pcabi_align_cross_multi_dev(ks['regions'], len(ks['regions']), *sc, stream, None, None),
+                           'align')
+        elif args.rj_end_streams:
             j = 0
             for k, sd in enumerate(sides):
                 adps = ks['start'] if k == 0 else ks['end']
@@ -1015,6 +1095,9 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
     # for its large launch
     for s_ in [stream, stream2] + x_streams:
         L.pcabi_stream_side_streams(s_, 0 if args.rj_side_streams == 0 else 1)
+    if args.rj_multi:
+        # one (multi) call at a time on `stream`: its grouped launches side by side
+        L.pcabi_stream_side_streams(stream, 1)
     try:
         for _ in range(max(1, args.warmup)):
             step()
@@ -1031,20 +1114,23 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
     step_ms = 1e3 * elapsed / args.steps
     per = {k: round(v / args.steps, 4) for k, v in acc.items()}
     ks = kept_state(tuple(a.name for a in matching), matching)
-    # the dominant launch: the set search's largest register bucket (start and end launches averaged)
-    dom_ms = 0.5 * (per['check_dom_start_ms'] + per['check_dom_end_ms'])
+    # the dominant launch: the set search's largest register bucket (start and end launches averaged);
+    # --rj-multi: the set search's whole multi call (both read ends, every grouped launch)
+    dom_ms = per['check_dom_start_ms'] if args.rj_multi else 0.5 * (per['check_dom_start_ms'] + per['check_dom_end_ms'])
     dom_cells = []
     for k, (w_len, u) in enumerate(((s_len, starts_u), (e_len, ends_u))):
         from collections import Counter
         rows = Counter((len(x) + 3) // 4 * 4 for x in u)
         big = max(rows, key=lambda r: rows[r] * r)   # the table's largest bucket by adapters x rows
         dom_cells.append(int(w_len[:n_chk].astype(np.int64).sum()) * sum(len(x) for x in u if (len(x) + 3) // 4 * 4 == big))
-    tops = float(np.mean(dom_cells)) * OPS_PER_CELL / (dom_ms * 1e-3) / 1e12
     # end trim with the kept sets: cells and rate (the few-adapter launches)
     end_cells = int(s_len.astype(np.int64).sum() * sum(map(len, ks['start'])) +
                     e_len.astype(np.int64).sum() * sum(map(len, ks['end'])))
     chk_cells = int(s_len[:n_chk].astype(np.int64).sum() * sum(map(len, starts_u)) +
                     e_len[:n_chk].astype(np.int64).sum() * sum(map(len, ends_u)))
+    if args.rj_multi:
+        dom_cells = [chk_cells, chk_cells]
+    tops = float(np.mean(dom_cells)) * OPS_PER_CELL / (dom_ms * 1e-3) / 1e12
     checked = None
     if args.check and rank == 0:
         from tests import oracle_lib
@@ -1088,12 +1174,17 @@ def run_reference_job(args, rank, world, dist, torch, L, _lib, A, synth, encode_
                 'achieved': round(end_cells * OPS_PER_CELL / (per['end_trim_align_ms'] * 1e-3) / 1e12, 3),
                 'peak': round(VALU_PEAK_TOPS, 1), 'unit': 'Tops/s (int32 lane-ops)',
                 'frac': round(end_cells * OPS_PER_CELL / (per['end_trim_align_ms'] * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4),
-                'launches': 'one per register bucket and side, %d + %d adapters' % (len(ks['start']), len(ks['end']))},
-            'roofline': {'bound': 'valu', 'kernel': 'the set search\'s largest register bucket (k_align<24, true, 6>)',
+                'launches': ('both sides\' kept adapters in one pcabi_align_cross_multi_dev call (grouped launches), '
+                             '%d + %d adapters' if args.rj_multi else 'one per register bucket and side, %d + %d adapters')
+                            % (len(ks['start']), len(ks['end']))},
+            'roofline': {'bound': 'valu', 'kernel': ('the set search\'s multi call (both read ends, every grouped launch; '
+                                                     'events around the call)' if args.rj_multi else
+                                                     'the set search\'s largest register bucket (k_align<24, true, 6>)'),
                          'achieved': round(tops, 3), 'peak': round(VALU_PEAK_TOPS, 1), 'unit': 'Tops/s (int32 lane-ops)',
                          'frac': round(tops / VALU_PEAK_TOPS, 4), 'launch_ms': round(dom_ms, 4),
                          'cells_per_launch': int(np.mean(dom_cells)), 'ops_per_cell': OPS_PER_CELL,
-                         'schedule': ('both sides\' cross products side by side: the launch shares the GPU'
+                         'schedule': ('one multi call for both read ends' if args.rj_multi else
+                                      'both sides\' cross products side by side: the launch shares the GPU'
                                       if args.rj_check_overlap else 'each side\'s cross product alone')},
             'dtype': 'int32', 'data': 'synthetic (seeded ONT-like reads, mean %d bp)' % args.mean_len,
             'config': {'workload': 'reference job: set search (%d check reads x %d sets, %d + %d distinct sequences), '

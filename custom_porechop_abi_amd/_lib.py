@@ -74,6 +74,7 @@ def lib():
                                    c_p, c_i64, c_p], c_int),
         'pcabi_align_cross_dev_marked': ([c_p, c_p, c_p, c_i64, ctypes.c_int32, c_p, c_int, c_int, c_int, c_int,
                                           c_p, c_i64, c_p, c_p, c_p], c_int),
+        'pcabi_align_cross_multi_dev': ([c_p, ctypes.c_int32, c_int, c_int, c_int, c_int, c_p, c_p, c_p], c_int),
         'pcabi_end_trim_dev': ([c_p, c_i64, ctypes.c_int32, c_p, c_i64, ctypes.c_int32, c_i64, c_int,
                                 c_int, c_d, c_int, c_p, c_p, c_p, c_p, c_p], c_int),
         'pcabi_best_full_identity_dev': ([c_p, c_i64, c_i64, ctypes.c_int32, c_p, c_p], c_int),
@@ -133,18 +134,35 @@ def exported_symbols():
             'pcabi_stream_sync', 'pcabi_event_create', 'pcabi_event_destroy', 'pcabi_event_record',
             'pcabi_stream_wait_event', 'pcabi_event_elapsed_ms', 'pcabi_adapters_create', 'pcabi_adapters_create_scored', 'pcabi_adapters_destroy',
             'pcabi_tile_layout', 'pcabi_tile_windows_dev', 'pcabi_align_cross_dev', 'pcabi_align_cross_dev_marked',
-            'pcabi_end_trim_dev',
+            'pcabi_align_cross_multi_dev', 'pcabi_end_trim_dev',
             'pcabi_best_full_identity_dev', 'pcabi_first_hits_host', 'pcabi_first_hit_dev', 'pcabi_scan_create',
             'pcabi_scan_destroy', 'pcabi_middle_scan_dev', 'pcabi_middle_scan_host', 'pcabi_middle_scan_seqs', 'pcabi_middle_seed_runs',
             'pcabi_middle_requeues', 'pcabi_scan_profile', 'pcabi_set_side_streams', 'pcabi_stream_side_streams',
             'pcabi_barcode_call_dev',
             'pcabi_barcode_call_host', 'pcabi_fastx_open', 'pcabi_fastx_type', 'pcabi_fastx_next',
-            'pcabi_fastx_close', 'pcabi_fastx_load', 'pcabi_reads_count', 'pcabi_reads_type', 'pcabi_reads_views',
+            'pcabi_fastx_close', 'pcabi_fastx_remaining', 'pcabi_fastx_load', 'pcabi_reads_count', 'pcabi_reads_type', 'pcabi_reads_views',
             'pcabi_reads_free', 'pcabi_reads_write', 'check_compatibility', 'pcabi_compat_host',
             'pcabi_compat_all_vs_all_host', 'pcabi_kmer_count_host', 'pcabi_kmer_top_host', 'pcabi_gather_host',
             'pcabi_kmer_approx_host', 'pcabi_io_release_cache', 'pcabi_best_full_identity_host',
             'pcabi_middle_cuts_dev', 'pcabi_middle_cuts_host', 'pcabi_fastx_record_start', 'pcabi_fastx_set_range', 'pcabi_fastx_next_text',
             'pcabi_end_decisions_host', 'pcabi_end_decisions_seqs', 'pcabi_stage_seqs_host', 'pcabi_flag_list_dev', 'pcabi_trim_views_dev']
+
+
+class CrossRegion(ctypes.Structure):
+    """include/pcabi.h pcabi_cross_region: one cross product of pcabi_align_cross_multi_dev."""
+    _fields_ = [('tiles', ctypes.c_void_p), ('tile_off', ctypes.c_void_p), ('win_len', ctypes.c_void_p),
+                ('n_win', ctypes.c_int64), ('max_win_len', ctypes.c_int32), ('adps', ctypes.c_void_p),
+                ('out', ctypes.c_void_p), ('out_stride', ctypes.c_int64)]
+
+
+def cross_regions(regions):
+    """A ctypes array of CrossRegion from (tiles, tile_off, win_len, n_win, max_win_len, adps, out,
+    out_stride) tuples (device pointers as ints or c_void_p)."""
+    arr = (CrossRegion * len(regions))()
+    for k, r in enumerate(regions):
+        vals = [x.value if isinstance(x, ctypes.c_void_p) else x for x in r]
+        arr[k] = CrossRegion(*vals)
+    return arr
 
 
 def check(rc, what):

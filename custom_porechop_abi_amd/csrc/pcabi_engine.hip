@@ -2617,6 +2617,124 @@ int pcabi_align_cross_dev_marked(const uint32_t *tiles, const int64_t *tile_off,
     return 0;
 }
 
+int pcabi_align_cross_multi_dev(const pcabi_cross_region *regions, int32_t n_regions, int match, int mismatch,
+                                int gap_open, int gap_extend, void *stream, void *ev_begin, void *ev_end) {
+    if (n_regions < 0 || (n_regions > 0 && !regions)) return fail(PCABI_E_ARG, "bad arguments");
+    const pcabi::Scoring sc{match, mismatch, gap_open, gap_extend};
+    const bool affine = gap_open != gap_extend;
+    // the units: (region, bucket) with its launch class (-1: a launch of its own)
+    struct Unit {
+        int cls, b, pack;
+        KParams p;
+        int64_t blocks, cost;
+    };
+    std::vector<Unit> units;
+    for (int32_t r = 0; r < n_regions; ++r) {
+        const pcabi_cross_region &g = regions[r];
+        if (!g.adps || g.n_win < 0 || (g.n_win > 0 && (!g.tiles || !g.tile_off || !g.win_len || !g.out)))
+            return fail(PCABI_E_ARG, "bad region " + std::to_string(r));
+        if (g.n_win == 0) continue;
+        const pcabi_adapters *adps = nullptr;
+        if (int rc = adapters_for(g.adps, sc, g.max_win_len, &adps)) return rc;
+        for (int b = 0; b < kNumBuckets; ++b) {
+            if (!adps->count[b]) continue;
+            Unit u{};
+            u.b = b;
+            u.pack = bucket_pack_mode(b, adps->lens[b], sc);
+            u.cls = kBuckets[b].kind == FAST ? group_class(kBuckets[b].rpl, u.pack, affine) : -1;
+            KParams &p = u.p;
+            p.tiles = g.tiles;
+            p.tile_off = g.tile_off;
+            p.win_len = g.win_len;
+            p.n_win = g.n_win;
+            p.out = g.out;
+            p.out_stride = g.out_stride;
+            p.sc = sc;
+            p.max_cols = g.max_win_len;
+            p.adp_pad = adps->pad[b];
+            p.adp_len = adps->len[b];
+            p.adp_id = adps->id[b];
+            p.n_adp = adps->count[b];
+            p.rt = adps->rt[b];
+            u.blocks = (g.n_win + 8 * 256 - 1) / (8 * 256) * 8 * (int64_t)p.n_adp;
+            u.cost = (g.n_win + 255) / 256 * (int64_t)p.n_adp * kBuckets[b].rpl;
+            units.push_back(u);
+        }
+    }
+    if (units.empty()) return 0;
+    // the launches: per class, its units longest rows first in segments of at most kMaxGroupSegs;
+    // a class of one unit launches it on its own (k_align, the row split where that applies)
+    struct Launch {
+        int cls;                 // -1: units[unit] alone
+        size_t unit;
+        GroupParams gp;
+        int64_t blocks, cost;
+    };
+    std::vector<Launch> launches;
+    for (int c = 0; c < kGroupClasses; ++c) {
+        std::vector<size_t> mine;
+        for (size_t k = 0; k < units.size(); ++k)
+            if (units[k].cls == c) mine.push_back(k);
+        if (mine.size() == 1) units[mine[0]].cls = -1;
+        if (mine.size() <= 1) continue;
+        std::stable_sort(mine.begin(), mine.end(),
+                         [&](size_t x, size_t y) { return kBuckets[units[x].b].rpl > kBuckets[units[y].b].rpl; });
+        for (size_t k0 = 0; k0 < mine.size(); k0 += kMaxGroupSegs) {
+            Launch l{};
+            l.cls = c;
+            l.gp.sc = sc;
+            for (size_t k = k0; k < std::min(mine.size(), k0 + kMaxGroupSegs); ++k) {
+                const Unit &u = units[mine[k]];
+                GroupSeg &s = l.gp.seg[l.gp.n_seg++];
+                s.tiles = u.p.tiles;
+                s.tile_off = u.p.tile_off;
+                s.win_len = u.p.win_len;
+                s.n_win = u.p.n_win;
+                s.adp_pad = u.p.adp_pad;
+                s.adp_len = u.p.adp_len;
+                s.adp_id = u.p.adp_id;
+                s.n_adp = u.p.n_adp;
+                s.out = u.p.out;
+                s.out_stride = u.p.out_stride;
+                s.rpl = kBuckets[u.b].rpl;
+                s.block0 = l.blocks;
+                l.blocks += u.blocks;
+                l.cost += u.cost;
+            }
+            launches.push_back(l);
+        }
+    }
+    for (size_t k = 0; k < units.size(); ++k)
+        if (units[k].cls < 0) {
+            Launch l{};
+            l.cls = -1;
+            l.unit = k;
+            l.cost = units[k].cost;
+            launches.push_back(l);
+        }
+    std::stable_sort(launches.begin(), launches.end(), [](const Launch &x, const Launch &y) { return x.cost > y.cost; });
+    ForkJoin fj;
+    if (int rc = fj.begin((hipStream_t)stream, launches.size())) return rc;
+    for (size_t k = 0; k < launches.size(); ++k) {
+        const Launch &l = launches[k];
+        const hipStream_t st = fj.at(k);
+        if (k == 0 && ev_begin) HIP_TRY(hipEventRecord((hipEvent_t)ev_begin, st));
+        if (l.cls >= 0) {
+            dispatch_group(l.cls, l.gp, l.blocks, st);
+        } else {
+            const Unit &u = units[l.unit];
+            if (int rc = dispatch(u.b, u.p, affine, st, u.pack)) {
+                (void)fj.end();
+                return rc;
+            }
+        }
+        if (k == 0 && ev_end) HIP_TRY(hipEventRecord((hipEvent_t)ev_end, st));
+    }
+    if (int rc = fj.end()) return rc;
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
 }  // extern "C"
 
 
@@ -4532,6 +4650,8 @@ int end_decisions_impl(
     std::vector<int64_t> toff[2];
     const int32_t *res[2] = {nullptr, nullptr};
     uint8_t *flag[2] = {nullptr, nullptr};
+    pcabi_cross_region reg[2];
+    int32_t n_reg = 0;
     for (int side = 0; side < 2; ++side) {
         const int64_t *off = side ? e_off : s_off;
         const int32_t *len = side ? e_len : s_len;
@@ -4559,11 +4679,12 @@ int end_decisions_impl(
             return rc;
         launch_tiles((const uint8_t *)e.dec[0].p, (const int64_t *)b[0].p, (const int32_t *)b[1].p, n_read,
                      (const int64_t *)b[2].p, max_nq, (uint32_t *)b[3].p, st);
-        if (int rc = pcabi_align_cross_dev((const uint32_t *)b[3].p, (const int64_t *)b[2].p, (const int32_t *)b[1].p,
-                                           n_read, max_len, tab, match, mismatch, gap_open, gap_extend, (int32_t *)b[4].p,
-                                           (int64_t)n_adp[side] * n_read, st))
-            return rc;
+        reg[n_reg++] = pcabi_cross_region{(const uint32_t *)b[3].p, (const int64_t *)b[2].p, (const int32_t *)b[1].p,
+                                          n_read, max_len, tab, (int32_t *)b[4].p, (int64_t)n_adp[side] * n_read};
     }
+    // both read ends in one call: the register buckets of both sides in grouped launches (r06)
+    if (int rc = pcabi_align_cross_multi_dev(reg, n_reg, match, mismatch, gap_open, gap_extend, st, nullptr, nullptr))
+        return rc;
     if (int rc = pcabi_end_trim_dev(res[0], (int64_t)n_sa * n_read, n_sa, res[1], (int64_t)n_ea * n_read, n_ea, n_read,
                                     end_size, extra_trim, end_threshold, min_trim_size, d_st, d_et, flag[0], flag[1], st))
         return rc;

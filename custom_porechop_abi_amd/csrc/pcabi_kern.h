@@ -256,23 +256,27 @@ constexpr int wave_tab_ints() {
     return (KIND == PACKED || KIND == TAGGED) ? kTabW * RPL : (KIND == LONG ? 2 * kTabW * RPL : 1);
 }
 
+// Cross mode, block b of a (window tiles x adapters) grid. XCD-aware order: workgroups are dealt to
+// the 8 XCDs round-robin, so block b runs on XCD b % 8. Each XCD takes every 8th tile of 256 windows
+// and runs ALL adapters of a tile back to back, so a tile is fetched into one L2 once instead of once
+// per adapter. (The grid is the tiles padded to a multiple of 8, times the adapters.)
+template <int RPL, bool AFFINE, int KIND>
+__device__ __forceinline__ void cross_block(const KParams &p, int64_t b, int32_t *wave_tab) {
+    const int64_t k = b >> 3;
+    const int a_local = (int)(k % p.n_adp);
+    const int64_t tile = (k / p.n_adp) * 8 + (b & 7);
+    const int64_t w = tile * 256 + threadIdx.x;
+    const int a_glob = p.adp_id[a_local];
+    const int64_t toff = w < p.n_win ? p.tile_off[tile] : 0;
+    run_lane<RPL, AFFINE, KIND>(p, a_local, w < p.n_win ? w : -1, (int64_t)a_glob * p.n_win + w, wave_tab, toff);
+}
+
 template <int RPL, bool AFFINE, int KIND>
 __global__ __launch_bounds__(256, PCABI_WAVES) void k_align(KParams p) {
     __shared__ __attribute__((aligned(16))) int32_t tab[4 * wave_tab_ints<KIND, RPL>()];
     int32_t *wave_tab = tab + (threadIdx.x >> 6) * wave_tab_ints<KIND, RPL>();
     if (p.task_win == nullptr) {
-        // XCD-aware order: workgroups are dealt to the 8 XCDs round-robin, so block b runs on
-        // XCD b % 8. Each XCD takes every 8th tile of 256 windows and runs ALL adapters of a
-        // tile back to back, so a tile is fetched into one L2 once instead of once per adapter.
-        const int64_t b = blockIdx.x;
-        const int64_t k = b >> 3;
-        const int a_local = (int)(k % p.n_adp);
-        const int64_t tile = (k / p.n_adp) * 8 + (b & 7);
-        const int64_t w = tile * 256 + threadIdx.x;
-        const int a_glob = p.adp_id[a_local];
-        const int64_t toff = w < p.n_win ? p.tile_off[tile] : 0;
-        run_lane<RPL, AFFINE, KIND>(p, a_local, w < p.n_win ? w : -1, (int64_t)a_glob * p.n_win + w, wave_tab,
-                                    toff);
+        cross_block<RPL, AFFINE, KIND>(p, blockIdx.x, wave_tab);
     } else {
         int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
         const bool live = wave < p.n_waves;            // dead waves still join the table barrier
@@ -698,6 +702,45 @@ void launch(const KParams &p, bool affine, dim3 grid, hipStream_t st) {
     if (affine) hipLaunchKernelGGL((k_align<RPL, true, KIND>), grid, dim3(256), 0, st, p);
     else hipLaunchKernelGGL((k_align<RPL, false, KIND>), grid, dim3(256), 0, st, p);
 }
+
+// ---- grouped cross launches (pcabi_k_group.hip) ---------------------------------------------
+// Several (window set, register bucket) units of one core family in ONE launch: a unit is the cross
+// product of one region's windows (tile layout) with one register bucket of its adapter table, as a
+// k_align launch would run it; the launch's blocks are the units' grids back to back (each a
+// multiple of 8 blocks, so block b of a unit keeps k_align's XCD order), longest rows first. A
+// bucket of one or two adapters is a grid of ~400 blocks (1.5 waves per SIMD for 100k windows):
+// alone it is latency-bound; grouped, its waves share the SIMDs with the other units'.
+//   class 0: the run-tagged core (affine, 4..32 rows)    class 1: the packed core (affine, 36..64 rows)
+constexpr int kMaxGroupSegs = 16;
+constexpr int kGroupClasses = 2;
+struct GroupSeg {
+    const uint32_t *tiles;
+    const int64_t *tile_off;
+    const int32_t *win_len;
+    int64_t n_win;
+    const uint32_t *adp_pad;
+    const int32_t *adp_len;
+    const int32_t *adp_id;
+    int32_t *out;
+    int64_t out_stride;
+    int64_t block0;            // the unit's first block in the launch
+    int32_t n_adp;
+    int32_t rpl;
+};
+struct GroupParams {
+    GroupSeg seg[kMaxGroupSegs];
+    int32_t n_seg;
+    pcabi::Scoring sc;
+};
+constexpr int group_max_rpl(int cls) { return cls == 0 ? 32 : 64; }
+// the class a cross-mode unit belongs to, -1: launched on its own (bucket_pack_mode: 1 packed, 2 tagged)
+inline int group_class(int rpl, int pack_mode, bool affine) {
+    if (!affine) return -1;
+    if (pack_mode == 2 && rpl <= 32) return 0;
+    if (pack_mode == 1 && rpl >= 36 && rpl <= 64) return 1;
+    return -1;
+}
+void dispatch_group(int cls, const GroupParams &p, int64_t blocks, hipStream_t st);
 
 // ---- kernel translation units (pcabi_k_*.hip) ----------------------------------------------
 // k_align launches by core, grid as k_align expects (cross: XCD-ordered tiles x adapters;

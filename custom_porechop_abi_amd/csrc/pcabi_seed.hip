@@ -1348,201 +1348,6 @@ __global__ __launch_bounds__(256) void k_seed_band_pin(const int4 *task, const i
     }
 }
 
-// r06 form of k_seed_band_pin (PCABI_BAND_V2 A/B): the next row's adapter byte prefetched, the row
-// straight-line on every lane, the rare phase events under a wave-uniform test.
-template <int E, int NC4, bool STATS>
-__global__ __launch_bounds__(256) void k_seed_band_pin2(const int4 *task, const int32_t *n_task, int64_t cap,
-                                                       const uint8_t *codes, const uint8_t *adp, int32_t adp_dw,
-                                                       const int32_t *adp_off, const int32_t *adp_meta, int32_t n_adp,
-                                                       pcabi::Scoring sc, int32_t *bound, int64_t n, VerOut vo,
-                                                       unsigned long long *stats) {
-    constexpr int W = 2 * E + 1;
-    extern __shared__ uint4 lds4[];
-    uint32_t *lds = reinterpret_cast<uint32_t *>(lds4);
-    // LDS: the flat adapters (adp_dw dwords), their offsets, their meta (L | T << 12), then
-    // per lane NC4 uint4 of read bytes
-    for (int i = threadIdx.x; i < adp_dw; i += 256) lds[i] = reinterpret_cast<const uint32_t *>(adp)[i];
-    for (int i = threadIdx.x; i < n_adp; i += 256) {
-        lds[adp_dw + i] = (uint32_t)adp_off[i];
-        lds[adp_dw + n_adp + i] = (uint32_t)adp_meta[i];
-    }
-    __syncthreads();
-    const uint8_t *ad = reinterpret_cast<const uint8_t *>(lds);
-    const int32_t *aoffs = reinterpret_cast<const int32_t *>(lds + adp_dw);
-    const int32_t *ameta = aoffs + n_adp;
-    uint4 *slot4 = lds4 + ((adp_dw + 2 * n_adp + 3) >> 2) + (int)threadIdx.x * NC4;
-    const uint8_t *slot = reinterpret_cast<const uint8_t *>(slot4);
-    const int64_t nt = min((int64_t)*n_task, cap);
-    const int64_t stride = (int64_t)gridDim.x * 256;
-    int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int bs = pcabi::best_sub(sc), ma = sc.ma, mi = sc.mi, go = sc.go, ge = sc.ge;
-    const uintptr_t lo_addr = (uintptr_t)codes & ~(uintptr_t)15;
-    // the range of a task: [cb, cb + 16 * nld) with cb = (probe - o - E) & ~15. An inside band lies
-    // within its read, so the range starts inside the read's buffer; the clamp to the start of the
-    // caller's codes is a guard for reads there only (a masked copy in the scan's shadow arena, r05,
-    // may lie below codes; the arena's first 256 bytes are a lead-in no copy uses)
-    auto range_of = [&](const int4 &rc, uintptr_t &cb, int &nld) {
-        const int a = rc.y >> 11, o = rc.y & 255;
-        const int L = (int)((uint32_t)ameta[a] & 255u);
-        const uintptr_t pa = (uintptr_t)codes + (uintptr_t)(((uint64_t)(uint32_t)rc.w << 32) | (uint32_t)rc.z);
-        const uintptr_t lo = pa - (uintptr_t)(o + E), hi = pa - (uintptr_t)o + (uintptr_t)(L + E);
-        cb = lo & ~(uintptr_t)15;
-        if (pa >= lo_addr && cb < lo_addr) cb = lo_addr;
-        nld = (int)((hi - cb + 15) >> 4);
-    };
-    // ---- pipeline: recA / chA = the task to copy into the slot next, recB = the one after
-    int4 recA = make_int4(0, 0, 0, 0), recB = recA;
-    bool vA = false, vB = false;
-    uint4 chA[NC4];
-    uintptr_t cbA = lo_addr;
-    auto load_range = [&]() {                         // chA := recA's range (recA has arrived)
-        int nld = 0;
-        range_of(recA, cbA, nld);
-#pragma unroll
-        for (int k = 0; k < NC4; ++k)
-            chA[k] = k < nld ? *reinterpret_cast<const uint4 *>(cbA + 16 * (uintptr_t)k) : make_uint4(0u, 0u, 0u, 0u);
-    };
-    if (t < nt) { recA = task[t]; vA = true; t += stride; }
-    if (vA) load_range();
-    if (t < nt) { recB = task[t]; vB = true; t += stride; }
-    auto pin_start = [&](int x) -> int { return x == E ? 0 : (x > E ? go + (x - E - 1) * ge : kNeg); };
-    unsigned long long st_it = 0, st_act = 0, st_tasks = 0, st_pass = 0;
-    while (__any(vA)) {                               // one task per lane and pass
-        bool active = vA;
-        int4 rc = recA;
-        uintptr_t cb = cbA;
-        if (vA) {
-#pragma unroll
-            for (int k = 0; k < NC4; ++k) slot4[k] = chA[k];
-        }
-        // the pipeline moves on: B's range loads while this task computes
-        vA = vB;
-        recA = recB;
-        if (vA) load_range();
-        vB = t < nt;
-        if (vB) {
-            recB = task[t];
-            t += stride;
-        }
-        // ---- this task
-        const bool vA_was = active;
-        const int a = rc.y >> 11, o = rc.y & 255, K = kMinK + ((rc.y >> 8) & 7);
-        const uint32_t meta = (uint32_t)ameta[a];
-        const int L = (int)(meta & 255u), T = (int)(meta >> 12);
-        const int aoff = aoffs[a];
-        const int64_t bidx = (int64_t)a * n + rc.x;
-        const uintptr_t pa = (uintptr_t)codes + (uintptr_t)(((uint64_t)(uint32_t)rc.w << 32) | (uint32_t)rc.z);
-        const int base = (int)(pa - cb);              // the probe's byte in the slot
-        const int pin = ma * K;
-        int S[W], V[W], R[W];
-        int phase = 0, rows = L - o - K, other = pin + bs * o, mx = 0;
-        int apos = aoff + o + K, adir = 1;
-        int bpos = base + K + E + 1, bdir = 1;          // the slot byte entering the next row
-#pragma unroll
-        for (int x = 0; x < W; ++x) {
-            S[x] = pin_start(x);
-            V[x] = kNeg;
-            R[x] = active ? slot[base + K + x - E] : 0;   // row o + K + 1: read q + K + x - E
-        }
-        auto begin_prefix = [&]() {                   // rows o .. 1 backwards, mirrored band
-            phase = 1;
-            rows = o;
-            other = pin + mx;                         // K * match + Q
-            mx = 0;
-#pragma unroll
-            for (int x = 0; x < W; ++x) {
-                S[x] = pin_start(x);
-                V[x] = kNeg;
-                R[x] = slot[base - 1 + E - x];        // read q - 1 + E - x
-            }
-            bpos = base - 2 - E;
-            bdir = -1;
-            apos = aoff + o - 1;
-            adir = -1;
-        };
-        // the task's diagonal as a codes offset (probe - o): the verified-seed record
-        const int64_t dabs = (int64_t)(((uint64_t)(uint32_t)rc.w << 32) | (uint32_t)rc.z) - o;
-        // the task's verified flag (set once, where its lane finishes): one record call per task
-        // after the row loop, not a ballot per row (r05)
-        bool ver = false;
-        if (active && rows == 0) {                    // the run ends the adapter: Q = 0
-            if (o == 0) {
-                if (pin >= T) atomicMax(&bound[bidx], pin);
-                ver = pin >= T;
-                active = false;
-            } else {
-                begin_prefix();
-            }
-        }
-        if constexpr (STATS) {
-            st_tasks += __popcll(__ballot(vA_was));
-            st_pass += 1;
-        }
-        // the first row's adapter byte; every row loads the next row's while it computes (r06: the
-        // row no longer waits out an LDS round trip before its first cell)
-        int abn = ad[max(apos, 0)];
-        while (__any(active)) {
-            if constexpr (STATS) {
-                st_it += 64;
-                st_act += __popcll(__ballot(active));
-            }
-            // every lane runs the row, finished ones on stale state (their results are dropped):
-            // the row is straight-line code, no exec-mask branches around it (r06)
-            {
-                const int ab = abn;
-                apos += adir;
-                abn = ad[max(apos, 0)];
-                const int nb = slot[max(bpos, 0)];
-                bpos += bdir;
-                int h = kNeg, sl = kNeg;
-#pragma unroll
-                for (int x = 0; x < W; ++x) {
-                    const int dg = S[x] + (R[x] == ab ? ma : mi);
-                    const int vu = (x + 1 < W) ? max(V[x + 1] + ge, S[x + 1] + go) : kNeg;
-                    h = max(h + ge, sl + go);
-                    const int sv = max(dg, max(vu, h));
-                    S[x] = sv;
-                    V[x] = vu;
-                    sl = sv;
-                }
-#pragma unroll
-                for (int x = 0; x + 1 < W; ++x) R[x] = R[x + 1];
-                R[W - 1] = nb;
-                --rows;
-                mx = S[0];
-#pragma unroll
-                for (int x = 1; x < W; ++x) mx = max(mx, S[x]);
-                // below T: nothing to record (k_seed_band)
-                active = active && mx + bs * rows + other >= T;
-            }
-            // a phase ends (rare): the prefix starts, or the task finishes and records its bound
-            const bool ev = active && rows == 0;
-            if (__any(ev)) {
-                if (ev) {
-                    if (phase == 0 && o > 0) {
-                        begin_prefix();
-                        abn = ad[max(apos, 0)];
-                    } else {
-                        ver = mx + other >= T;
-                        if (ver) atomicMax(&bound[bidx], mx + other);
-                        active = false;
-                    }
-                }
-            }
-        }
-        if (vo.list) put_verified(vo, ver, rc.x, a, E, dabs);
-    }
-    if constexpr (STATS) {
-        if ((threadIdx.x & 63) == 0) {
-            unsigned long long *w = stats + 4 * ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6));
-            w[0] += st_it;
-            w[1] += st_act;
-            w[2] += st_tasks;
-            w[3] += st_pass;
-        }
-    }
-}
-
 // The pairs whose bound reaches their adapter's threshold T[a], as (a << 32 | read) keys
 // (unordered; one atomic per wave), grid-stride over the n_dev x n_adp bounds (row stride n).
 // pmap != nullptr (the device rounds; pmap may be `bound` itself): a candidate pair's entry becomes its
@@ -1889,23 +1694,6 @@ int launch_pin(State *s, int c, const int4 *task, const uint8_t *codes, const pc
     }
     const int64_t blocks = n_in >= 0 ? std::max<int64_t>(1, std::min<int64_t>((n_in + 255) / 256, s->pin_blocks[c]))
                                      : s->pin_blocks[c];
-    {   // (A/B, read per launch)
-        const char *e = std::getenv("PCABI_BAND_V2");
-        if (e && e[0] == '1') {
-            if (s->bstats_on && blocks <= kStatBlocks)
-                hipLaunchKernelGGL((k_seed_band_pin2<E, NC4, true>), dim3((unsigned)blocks), dim3(256), lds, st, task,
-                                   (const int32_t *)s->cnt.p + c, s->cap, codes, (const uint8_t *)s->adp.p,
-                                   s->adp_bytes / 4, (const int32_t *)s->adp_off.p, (const int32_t *)s->adp_meta.p,
-                                   s->n_adp, sc, (int32_t *)s->bound.p, n, s->ver,
-                                   (unsigned long long *)s->bstats.p + (size_t)c * 4 * 4 * kStatBlocks);
-            else
-                hipLaunchKernelGGL((k_seed_band_pin2<E, NC4, false>), dim3((unsigned)blocks), dim3(256), lds, st, task,
-                                   (const int32_t *)s->cnt.p + c, s->cap, codes, (const uint8_t *)s->adp.p,
-                                   s->adp_bytes / 4, (const int32_t *)s->adp_off.p, (const int32_t *)s->adp_meta.p,
-                                   s->n_adp, sc, (int32_t *)s->bound.p, n, s->ver, nullptr);
-            return 0;
-        }
-    }
     if (s->bstats_on && blocks <= kStatBlocks)       // a profiled round (pcabi_scan_profile)
         hipLaunchKernelGGL((k_seed_band_pin<E, NC4, true>), dim3((unsigned)blocks), dim3(256), lds, st, task,
                            (const int32_t *)s->cnt.p + c, s->cap, codes, (const uint8_t *)s->adp.p, s->adp_bytes / 4,

@@ -22,7 +22,7 @@ import time
 import numpy as np
 
 from . import misc
-from ._lib import check, lib
+from ._lib import check, cross_regions, lib
 from .engine import encode_adapters, middle_cuts
 from .porechop_abi import middle_adapter_list
 
@@ -143,6 +143,7 @@ class FileTrimmer(object):
         d_codes = self._h2d('codes', batch.codes)
         trims = np.zeros((2, nb), np.int32)
         res = [None, None]
+        regions = []
         n_ad = (len(self.start_adps), len(self.end_adps))
         for side, (w_off, w_len) in enumerate(((batch.code_off, s_len), (batch.code_off + e_start, e_len))):
             res[side] = self._buf('res%d' % side, 4 * 8 * max(1, n_ad[side]) * nb)
@@ -155,8 +156,11 @@ class FileTrimmer(object):
             d_tiles = self._buf('tiles%d' % side, 4 * nd)
             check(L.pcabi_tile_windows_dev(d_codes, d_off, d_len, nb, d_toff, int(np.diff(toff).max() // 256), d_tiles,
                                            self.stream), 'tile')
-            check(L.pcabi_align_cross_dev(d_tiles, d_toff, d_len, nb, int(w_len.max()), self.tabs[side], *sc,
-                                          res[side], n_ad[side] * nb, self.stream), 'align')
+            regions.append((d_tiles, d_toff, d_len, nb, int(w_len.max()), self.tabs[side], res[side], n_ad[side] * nb))
+        if regions:
+            # both read ends in one call: their register buckets in grouped launches (r06)
+            arr = cross_regions(regions)
+            check(L.pcabi_align_cross_multi_dev(arr, len(regions), *sc, self.stream, None, None), 'align')
         if nb:
             d_st, d_et = self._buf('st', 4 * nb), self._buf('et', 4 * nb)
             check(L.pcabi_end_trim_dev(res[0], n_ad[0] * nb, n_ad[0], res[1], n_ad[1] * nb, n_ad[1], nb, E, self.extra,

@@ -188,6 +188,28 @@ int pcabi_align_cross_dev_marked(const uint32_t *tiles, const int64_t *tile_off,
                                  int match, int mismatch, int gap_open, int gap_extend,
                                  int32_t *out, int64_t out_stride, void *stream, void *ev_begin,
                                  void *ev_end);
+/* Several cross products in one call (r06): region k = (tiles, tile_off, win_len, n_win,
+ * max_win_len, adps, out, out_stride) is aligned exactly as pcabi_align_cross_dev would align it
+ * (same results, same layout), but the register buckets of ALL regions run as grouped launches: the
+ * buckets of one core family -- the run-tagged core (affine, <= 32 rows) and the packed core (affine,
+ * 36..64 rows) -- across every region share one launch each (pcabi_kern.h "grouped cross
+ * launches"), the other buckets launch on their own. A bucket of one or two adapters (a 400-block
+ * grid for 100k windows) is latency-bound alone; grouped with the others its waves fill the SIMDs.
+ * The largest launch runs on `stream` (ev_begin / ev_end, either may be NULL, are recorded around
+ * it), the others beside it on the side streams when they are on for `stream`. Replaces the
+ * per-side calls of porechop_abi.py:359-438's end trim (both read ends in one call). */
+typedef struct pcabi_cross_region {
+    const uint32_t *tiles;
+    const int64_t *tile_off;
+    const int32_t *win_len;
+    int64_t n_win;
+    int32_t max_win_len;
+    const pcabi_adapters *adps;
+    int32_t *out;
+    int64_t out_stride;
+} pcabi_cross_region;
+int pcabi_align_cross_multi_dev(const pcabi_cross_region *regions, int32_t n_regions, int match, int mismatch,
+                                int gap_open, int gap_extend, void *stream, void *ev_begin, void *ev_end);
 /* Side streams (process-wide): with on = 1 a cross product (and a middle-scan round) runs its
  * largest register bucket on the caller's stream and the others beside it on the device's side
  * streams; with on = 0 every bucket runs on the caller's stream, one after the other. Side by side

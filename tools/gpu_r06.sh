@@ -29,7 +29,7 @@ for st in ${STAGES:-replay}; do
 import json, sys
 d = json.load(open(sys.argv[1]))
 print(json.dumps({k: d.get(k) for k in ('value', 'ms_per_step', 'roofline')}))
-for k in ('reference_job', 'middle', 'middle_20kb', 'fused_schedule', 'barcodes', 'config2_10k_119sets', 'drivers', 'check_phase', 'e2e'):
+for k in ('reference_job', 'middle', 'middle_20kb', 'per_side_schedule', 'barcodes', 'config2_10k_119sets', 'drivers', 'check_phase', 'e2e'):
     v = d.get(k) or {}
     print(k, json.dumps({x: v.get(x) for x in ('value', 'ms_per_step', 'middle_ms_per_step', 'ms_per_phase', 'error', 'parity_spot_check', 'step_vs_slowest_stage')})[:900])
 PY
