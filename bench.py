@@ -42,10 +42,8 @@ VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # int32 lane-ops/s: 256 CU x 4 SI
 HBM_PEAK_GBS = 8000.0
 OPS_PER_CELL = 10                               # algorithmic int ops per cell
 SCORING = (3, -6, -5, -2)                       # reference default (arg_parser.py:178-180)
-# the default scheme's 21-24 bp bucket runs the run-tagged layout (pcabi_dp.h pk::LayT, KIND 6);
-# PCABI_TAGGED=0 keeps the untagged packed layout (KIND 2) for A/B runs
-DOM_KERNEL = ('k_align<24, true, 2> (packed core, 21-24 bp adapters, affine)' if os.environ.get('PCABI_TAGGED') == '0'
-              else 'k_align<24, true, 6> (run-tagged packed core, 21-24 bp adapters, affine)')
+# the default scheme's 21-24 bp bucket runs the run-tagged layout (pcabi_dp.h pk::LayT, KIND 6)
+DOM_KERNEL = 'k_align<24, true, 6> (run-tagged packed core, 21-24 bp adapters, affine)'
 
 
 def parse():

@@ -162,12 +162,10 @@ bool middle_windows_on(double mean_len) {
 // ~15-20 us of event latency (profiles/r03/final/kernel_trace_middle_8kb.csv). r05at (in-process
 // A/B, profiles/r05/at/): from round 2 on (1) 1.93 ms at 8 kb / 2.53 at 20 kb, against 1.96-1.99 /
 // 2.65-2.69 from round 3 on (2, the r03-r05 default, round 2 replayed from a graph) and 2.02 /
-// 2.51 with round 1 serial too (0). PCABI_MIDDLE_SERIAL_FROM overrides (a large value keeps every
-// round side by side).
-int middle_serial_from() {
-    const char *e = std::getenv("PCABI_MIDDLE_SERIAL_FROM");
-    return (e && e[0]) ? std::atoi(e) : 1;
-}
+// 2.51 with round 1 serial too (0).
+// round side by side). Captured round graphs (run_round) hold only serial rounds: a capture never
+// records another caller's work on the shared side streams.
+constexpr int kMiddleSerialFrom = 1;
 
 // Device planning aims at this many waves per candidate-DP round (4 per SIMD): the chunk length
 // is the longest of 512, 256, 128, 64 owned columns that still reaches it.
@@ -1159,7 +1157,7 @@ bool chunkable(int b, bool packed) {
 
 // Lanes per window of the row-split core (k_align_split) for a cross-mode launch of `waves`
 // waves: 4 (2 under 16 rows) for launches under 1024 waves, else 1 (the one-lane core).
-// PCABI_SPLIT=0 turns the split off, 2 / 4 force it. The split costs ~1.3-1.7x the VALU work per
+// PCABI_SPLIT=0 turns the split off, 2 / 4 force it (tests: the split core on any launch). The split costs ~1.3-1.7x the VALU work per
 // cell (the per-step exchange and bookkeeping over R / K rows), so it pays only where a launch is
 // latency-bound on its own: r04 A/B (profiles/r04/split_ab/), a threshold of 4096 waves split the
 // headline's one-adapter buckets (1,564 waves), which run beside the other side's buckets anyway:
@@ -1171,12 +1169,6 @@ int split_lanes(int rpl, int64_t waves) {
     int K = 1;
     if (forced >= 0) K = forced;
     else if (waves < 1024) K = rpl < 16 ? 2 : 4;
-    else if (rpl >= 36 && waves < 4096) {
-        // PCABI_SPLIT_WIDE=1 (A/B): the >= 36-row packed buckets (3-5 waves per SIMD) of a few
-        // adapters in 2 lanes per window
-        const char *w = std::getenv("PCABI_SPLIT_WIDE");
-        if (w && w[0] == '1') K = 2;
-    }
     return (K == 2 || K == 4) && pcabi::split_ok(rpl, K) ? K : 1;
 }
 
@@ -1213,14 +1205,10 @@ bool bucket_packed_ok(int b, const std::vector<int32_t> &lens, const pcabi::Scor
 
 // How k_align serves a bucket: 0 = not packed (fast / generic cores), 1 = packed key layout,
 // 2 = the run-tagged layout (pcabi_dp.h pk::LayT: affine buckets of <= 32 rows whose adapters all
-// pass layt_ok; one VALU op per cell less). PCABI_TAGGED=0 keeps the untagged layout (A/B runs).
+// pass layt_ok; one VALU op per cell less).
 int bucket_pack_mode(int b, const std::vector<int32_t> &lens, const pcabi::Scoring &sc) {
     if (!bucket_packed_ok(b, lens, sc)) return 0;
-    static const bool tagged_on = [] {
-        const char *e = std::getenv("PCABI_TAGGED");
-        return !(e && e[0] == '0');
-    }();
-    if (!tagged_on || kBuckets[b].kind != FAST || kBuckets[b].rpl > 32) return 1;
+    if (kBuckets[b].kind != FAST || kBuckets[b].rpl > 32) return 1;
     for (int32_t L : lens)
         if (!pcabi::layt_ok(L, kBuckets[b].rpl, sc)) return 1;
     return 2;
@@ -1237,13 +1225,6 @@ struct BucketHost {
 // side (the caller's stream + SideStreams::N), and a bucket of one or two adapters is too small
 // a grid to fill the GPU on its own.
 constexpr int kMaxFastBuckets = 4;
-int max_fast_buckets() {   // PCABI_MAX_FAST_BUCKETS (A/B runs) overrides kMaxFastBuckets
-    static const int v = [] {
-        const char *e = std::getenv("PCABI_MAX_FAST_BUCKETS");
-        return (e && std::atoi(e) > 0) ? std::atoi(e) : kMaxFastBuckets;
-    }();
-    return v;
-}
 
 // Bucket of every adapter: its own register bucket, then the cheapest merges of a FAST bucket
 // into the next larger non-empty one (cost = adapters x added padding rows) until at most
@@ -1266,11 +1247,7 @@ std::vector<int> assign_buckets(const int32_t *adp_len, int32_t n_adp, const pca
                 return false;
         return true;
     };
-    // PCABI_SMALL_TABLE_BUCKETS=N (A/B): tables of at most 4 adapters keep at most N FAST buckets
-    // (the reference job's kept sets: one launch per side instead of two one-adapter launches)
-    int max_fast = max_fast_buckets();
-    if (const char *e = std::getenv("PCABI_SMALL_TABLE_BUCKETS"))
-        if (std::atoi(e) > 0 && n_adp <= 4) max_fast = std::min(max_fast, std::atoi(e));
+    const int max_fast = kMaxFastBuckets;
     while (merge) {
         std::vector<int> fast;
         for (int b = 0; b < kNumBuckets; ++b)
@@ -1523,23 +1500,10 @@ int side_streams(int dev, SideStreams **out) {
     std::lock_guard<std::mutex> g(g_side_mu);
     SideStreams &ss = g_side[dev];
     if (!ss.init) {
-        // PCABI_SIDE_CUMASK=1 (A/B): side streams with a CU mask of every CU, each on a hardware
-        // queue of its own (a plain stream shares one of the process's GPU_MAX_HW_QUEUES, and two
-        // regions' small buckets landing on one queue run one after the other: r04 trace of the
-        // reference job's end trim)
-        const char *cm = std::getenv("PCABI_SIDE_CUMASK");
-        std::vector<uint32_t> mask;
-        if (cm && cm[0] == '1') {
-            int cus = 0;
-            HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-            mask.assign((size_t)(cus + 31) / 32, 0u);
-            for (int c = 0; c < cus; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
-        }
+        // plain streams on the process's GPU_MAX_HW_QUEUES (side streams with a CU mask, a hardware
+        // queue each, measured slower in r04n)
         for (int i = 0; i < SideStreams::N; ++i) {
-            if (mask.empty())
-                HIP_TRY(hipStreamCreateWithFlags(&ss.s[i], hipStreamNonBlocking));
-            else
-                HIP_TRY(hipExtStreamCreateWithCUMask(&ss.s[i], (uint32_t)mask.size(), mask.data()));
+            HIP_TRY(hipStreamCreateWithFlags(&ss.s[i], hipStreamNonBlocking));
             HIP_TRY(hipEventCreateWithFlags(&ss.join[i], hipEventDisableTiming));
         }
         HIP_TRY(hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming));
@@ -1549,24 +1513,14 @@ int side_streams(int dev, SideStreams **out) {
     return 0;
 }
 
-// pcabi_set_side_streams: whether fork / join regions use the side streams (initially PCABI_FORK,
-// default kSideStreamsDefault)
+// pcabi_set_side_streams: whether fork / join regions use the side streams (initially on)
 constexpr int kSideStreamsDefault = 1;
-std::atomic<int> g_side_on{-1};
-bool side_streams_on() {
-    int v = g_side_on.load(std::memory_order_relaxed);
-    if (v < 0) {
-        const char *e = std::getenv("PCABI_FORK");
-        v = (e && (e[0] == '0' || e[0] == '1')) ? e[0] - '0' : kSideStreamsDefault;
-        int expect = -1;
-        if (!g_side_on.compare_exchange_strong(expect, v)) v = expect;
-    }
-    return v != 0;
-}
+std::atomic<int> g_side_on{kSideStreamsDefault};
+bool side_streams_on() { return g_side_on.load(std::memory_order_relaxed) != 0; }
 
 // Per-stream setting (pcabi_stream_side_streams, r05): a caller that runs cross products on several
 // streams at once turns the side streams off for ITS streams only; streams without an entry follow
-// the process-wide default (pcabi_set_side_streams / PCABI_FORK).
+// the process-wide default (pcabi_set_side_streams).
 std::mutex g_stream_side_mu;
 std::vector<std::pair<hipStream_t, int>> g_stream_side;   // few entries: a linear scan
 bool side_streams_on(hipStream_t st) {
@@ -3404,12 +3358,8 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
     // that found nothing), 2 to 3. Data where round 2 finds nothing then skips a third round of ~35
     // empty launches, data with a third round pays no extra host round trip for it (r05y, in-process
     // A/B: the 20 kb scan 2.86 ms with 3 against 2.72 with 2, the 8 kb one 2.01 with 3 against 2.19
-    // with 2). PCABI_MIDDLE_BATCH1 = 1..3 fixes it (A/B).
-    const int batch1 = [&] {
-        const char *e = std::getenv("PCABI_MIDDLE_BATCH1");
-        const int v = e ? std::atoi(e) : std::min(kBatch, std::max(2, sc->rounds_hint));
-        return v >= 1 && v <= kBatch ? v : kBatch;
-    }();
+    // with 2).
+    const int batch1 = std::min(kBatch, std::max(2, sc->rounds_hint));
     constexpr unsigned kGrid = 2048;                // blocks of the device-counted launches
     // ---- device buffers ----
     if (int rc = sc->q_cur.ensure(4 * (size_t)n * (kSlots + 1))) return rc;
@@ -3505,14 +3455,11 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
             if (std::sscanf(e, "%lld,%lld,%lld", &raw, &task, &slots) == 3 && slots > 0) sc->q_slots_cap = slots;
     }
     const std::vector<std::pair<int64_t, int>> faults = middle_faults();
-    const int serial_from = middle_serial_from();
+    const int serial_from = kMiddleSerialFrom;
     // the candidate-DP buckets' own threshold: in the window rounds (long reads) round 1's buckets
     // run serial too (r05aw in-process A/B, 20 kb: 2.512 -> 2.491 ms; 8 kb whole-read rounds keep
-    // them side by side: 1.933 against 1.999 serial); PCABI_MIDDLE_DP_SERIAL_FROM overrides
-    const int dp_serial_from = [&] {
-        const char *e = std::getenv("PCABI_MIDDLE_DP_SERIAL_FROM");
-        return (e && e[0]) ? std::atoi(e) : (windows ? 0 : serial_from);
-    }();
+    // them side by side: 1.933 against 1.999 serial)
+    const int dp_serial_from = windows ? 0 : serial_from;
     std::vector<char> fired(faults.size(), 0);
     int injected[kSlots + 1] = {};                  // per slot: the faults its last queueing injected
     const int64_t target = middle_plan_waves();
@@ -3801,23 +3748,21 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
     // once into a graph and replayed (r05: one host call instead of ~40 launches and ~10 event
     // operations, and the graph's ~1.6 us per kernel instead of ~2.7 back to back, tools/
     // launch_bench.hip; r05au: serial rounds too, the fork setting in the key). Not for rounds that
-    // inject faults (tests), profile, debug or the legacy stream; PCABI_MIDDLE_GRAPHS=0 queues every
-    // round directly (A/B).
-    const bool graphs_on = [] {
-        const char *e = std::getenv("PCABI_MIDDLE_GRAPHS");
-        return !(e && e[0] == '0');
-    }() && st != nullptr && faults.empty() && !g_debug && !sc->prof.on && sc->last_table == adps->serial;
+    // inject faults (tests), profile, debug or the legacy stream, and only rounds that run serial
+    // (a capture would record another caller's launches on the shared side streams).
+    const bool graphs_on = st != nullptr && faults.empty() && !g_debug && !sc->prof.on && sc->last_table == adps->serial;
     // (a table new to this scan -- e.g. the host API's per-call tables -- runs its rounds directly:
     // a capture pays only for a table the next call uses again)
     sc->last_table = adps->serial;
     auto run_round = [&](int r) -> int {
         const bool first = r == 0 && round_base == 0;
-        if (!graphs_on || first) return queue_round(r);
+        const bool serial = round_base + r >= serial_from && round_base + r >= dp_serial_from;
+        if (!graphs_on || first || !serial) return queue_round(r);
         std::vector<int64_t> key = {(int64_t)round_base, (int64_t)(intptr_t)codes, (int64_t)(intptr_t)win_off,
                                     (int64_t)(intptr_t)win_len, n, windows ? 1 : 0, (int64_t)(threshold * 1e6),
                                     scr.ma, scr.mi, scr.go, scr.ge, (int64_t)adps->serial, sc->q_slots_cap,
                                     sc->shadow_cap, (int64_t)(intptr_t)sc->shadow.p, target,
-                                    (int64_t)g_buf_gen.load(), (int64_t)serial_from, (int64_t)dp_serial_from};
+                                    (int64_t)g_buf_gen.load()};
         auto &g = sc->graphs[r & 31];
         if (g.exec && g.key == key) {
             HIP_TRY(hipGraphLaunch(g.exec, st));

@@ -1,7 +1,5 @@
 // pcabi_k_chunk.hip -- k_align_chunk instantiations: the middle scan's candidate DP over
 // owned-column chunks of long reads (pcabi_dp.h sf::chunk_plan), every core.
-#include <cstdlib>
-
 #include "pcabi_kern.h"
 
 namespace pcabi_eng {
@@ -12,9 +10,8 @@ int dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st, bool ta
     if (kBuckets[b].kind == STRIPED) return launch_striped(p, affine, st);
     {   // the row-split core, K lanes per chunk task: p.chunk_split, the caller's choice (r05: 2 for
         // the middle scan's certified-out whole reads, whose 32-column chunks behind a ~60-column
-        // lead-in ran latency-bound one lane per chunk). PCABI_CHUNK_SPLIT=0 | 2 | 4 overrides (A/B)
-        const char *e = std::getenv("PCABI_CHUNK_SPLIT");   // (read per launch: tests switch it)
-        const int ks = (e && e[0] >= '0' && e[0] <= '9') ? std::atoi(e) : p.chunk_split;
+        // lead-in ran latency-bound one lane per chunk)
+        const int ks = p.chunk_split;
         if ((ks == 2 || ks == 4) && kBuckets[b].kind == FAST && kBuckets[b].rpl <= 64 &&
             pcabi::split_ok(kBuckets[b].rpl, ks) &&
             dispatch_split_chunk(kBuckets[b].rpl, ks, p, affine, tagged && affine && kBuckets[b].rpl <= 32, st))
@@ -22,9 +19,8 @@ int dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st, bool ta
     }
     // one-wave blocks for the device-planned run-tagged / packed buckets, 4x the blocks (the same
     // wave slots): r04n, candidate DP 0.68 -> 0.62 ms per 8 kb step, the reference job's middle
-    // 1.57-1.59 -> 1.52 ms. PCABI_CHUNK_WPB=4 keeps four-wave blocks (A/B).
-    const char *ewpb = std::getenv("PCABI_CHUNK_WPB");
-    const bool wpb1 = p.dev_waves && !(ewpb && ewpb[0] == '4') && kBuckets[b].kind == FAST && affine;
+    // 1.57-1.59 -> 1.52 ms.
+    const bool wpb1 = p.dev_waves && kBuckets[b].kind == FAST && affine;
     const dim3 grid1(grid.x * 4);
     if (wpb1 && tagged && kBuckets[b].rpl <= 32) {
         switch (kBuckets[b].rpl) {
@@ -42,16 +38,6 @@ int dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st, bool ta
     }
     if (tagged && affine && kBuckets[b].kind == FAST && kBuckets[b].rpl <= 32) {
         // the run-tagged layout (9 VALU ops per cell instead of 10), as the end-window buckets
-        const char *ew = std::getenv("PCABI_CHUNK_WAVES");
-        const bool w6 = ew && std::atoi(ew) == 6;
-        if (w6 && kBuckets[b].rpl == 24) {
-            hipLaunchKernelGGL((k_align_chunk<24, true, TAGGED, 6>), grid, dim3(256), 0, st, p);
-            return 0;
-        }
-        if (w6 && kBuckets[b].rpl == 28) {
-            hipLaunchKernelGGL((k_align_chunk<28, true, TAGGED, 6>), grid, dim3(256), 0, st, p);
-            return 0;
-        }
         switch (kBuckets[b].rpl) {
 #define C(R) case R: hipLaunchKernelGGL((k_align_chunk<R, true, TAGGED>), grid, dim3(256), 0, st, p); return 0;
         C(4) C(8) C(12) C(16) C(20) C(24) C(28) C(32)

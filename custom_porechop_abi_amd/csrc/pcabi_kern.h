@@ -389,9 +389,8 @@ __device__ __forceinline__ void chunk_wave(const KParams &p, int64_t wave, bool 
     store_result(p.out, p.out_stride, p.task_out[slot], r);
 }
 
-// W: the launch's minimum waves per SIMD (amdgpu_waves_per_eu; 1 = no bound): the run-tagged
-// <= 28-row chunk kernels also come with W = 6 (80 VGPRs instead of 89: 6 waves per SIMD instead of
-// 5), chosen by PCABI_CHUNK_WAVES=6 at dispatch (A/B). WPB: waves per block -- with 4, a block's
+// W: the launch's minimum waves per SIMD (amdgpu_waves_per_eu; 1 = no bound). WPB: waves per block
+// -- with 4, a block's
 // waves meet at every table barrier and the block holds its CU slot until its slowest wave (the
 // longest chunk of its 4 x 64 tasks) ends; with 1 (the device-planned default) every wave retires alone.
 template <int RPL, bool AFFINE, int KIND, int W = 1, int WPB = 4>

@@ -22,13 +22,13 @@
 //     largest S_b. Pairs with a bound >= T go to the full attribute DP exactly as after the
 //     filter. The engine re-seeds every later round on the masked reads (N never matches).
 // Kernels (integer work, no MFMA), r03 layout: the streaming part and the irregular part apart.
-//   k_seed_scan   the read bytes stream through (grid-stride over reads, 8 positions per lane and
-//                 sub-step): 2-bit codes by SWAR, one LDS bitmap word per position (the merged
-//                 8-mer table; positions whose valid run is shorter than 8 flagged for the short
-//                 tables). Only the bitmaps sit in LDS. A position that hits is appended as a raw
-//                 hit (read, position) to the block's own slab in global memory (an LDS counter,
-//                 no global atomics, no barriers inside the loop);
-//   k_seed_expand one block per slab: the probe entries of every raw hit (rank / entry tables in
+//   k_seed_scan   the read bytes stream through (every wave an equal range of 32-position segments):
+//                 2-bit codes packed once per lane, one LDS byte-map read per two positions (the
+//                 merged 8-mer table; positions whose valid run is shorter than 8 flagged for the
+//                 short tables). A position that hits is appended as a raw hit (read, position, its
+//                 8-mer) to the wave's own slab in global memory (no global atomics, no barriers
+//                 inside the loop);
+//   k_seed_expand resident blocks over the slabs: the probe entries of every raw hit (rank / entry tables in
 //                 LDS) become (read, adapter, diagonal) tasks per band class -- a block scan of the
 //                 per-hit counts, one global atomic per class and 256 hits;
 //   k_seed_band   grid-stride over a class's tasks: the banded Gotoh score DP (2E+1 cells per
@@ -199,7 +199,7 @@ __device__ __forceinline__ ReadMeta read_meta(const ScanArgs &a, int64_t r, int6
     return m;
 }
 
-// k_seed_scan (r03 rewrite): the reads' positions are cut into segments of kSeg = 32 (seg_cum, an
+// The segment walk (r03): the reads' positions are cut into segments of kSeg = 32 (seg_cum, an
 // exclusive scan of ceil(len / 32) over the round's reads), and every WAVE takes an equal,
 // contiguous range of segments -- no read-length imbalance between waves, and no idle lanes at
 // a read's end beyond its last segment (r02 / early r03: blocks took whole reads in steps of
@@ -217,186 +217,15 @@ __device__ __forceinline__ ReadMeta read_meta(const ScanArgs &a, int64_t r, int6
 // disturbs the codes of windows that contain it, and those are masked.)
 // Hits are appended to the block's slab as before: (read, position | kSlowBit, its clean 8-mer |
 // valid run << 16, read length - position).
-__global__ __launch_bounds__(256) void k_seed_scan_bits(ScanArgs a) {
-    // dynamic LDS: the bitmaps from byte 0 (so a word's address is one mask away from the code),
-    // then the slab counter
-    extern __shared__ uint32_t lds[];
-    int &s_cnt = *reinterpret_cast<int *>(lds + a.bits_dw);
-    for (int i = threadIdx.x; i < a.bits_dw; i += 256) lds[i] = a.tabs[i];
-    if (threadIdx.x == 0) s_cnt = 0;
-    __syncthreads();
-    const int64_t nr = dev_count(a.n_dev, a.n);
-    const int64_t S = rfl64(a.seg_cum[nr]);
-    const int lane = (int)(threadIdx.x & 63);
-    const int64_t nw = (int64_t)gridDim.x * 4;
-    const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int64_t lo = S * gw / nw, hi = S * (gw + 1) / nw;
-    uint4 *slab = a.raw + (int64_t)blockIdx.x * a.slab;
-    if (lo < hi) {
-        // the read holding segment lo: a 64-ary search over seg_cum (seg_cum[ra] <= lo < seg_cum[rb])
-        int64_t ra = 0, rb = nr;
-        while (rb - ra > 1) {
-            const int64_t step = (rb - ra + 63) / 64;
-            const int64_t idx = ra + (int64_t)lane * step;
-            const bool le = idx < rb && a.seg_cum[idx] <= lo;
-            const int c = __popcll(__ballot(le));
-            ra = rfl64(ra + (int64_t)(c - 1) * step);
-            rb = rfl64(min(rb, ra + step));
-        }
-        int64_t rc = ra, s0c = rfl64(a.seg_cum[ra]);
-        ReadMeta mc = read_meta(a, rc, nr, S), mn = read_meta(a, rc + 1, nr, S);
-        // the wave's window moves to the read holding segment b (b < hi <= S: terminates)
-        auto advance = [&](int64_t b) {
-            while (b >= mc.s1) {
-                ++rc;
-                s0c = mc.s1;
-                mc = mn;
-                mn = read_meta(a, rc + 1, nr, S);
-            }
-        };
-        // lane's segment b + lane -> read, position, code offset, length; false past the range
-        auto map = [&](int64_t b, int64_t &r, int &p, int64_t &off, int &len) -> bool {
-            const int64_t sg = b + lane;
-            if (sg >= hi) return false;
-            if (sg < mc.s1) {
-                r = rc; p = (int)(sg - s0c) * kSeg; off = mc.off; len = mc.len;
-            } else if (sg < mn.s1) {
-                r = rc + 1; p = (int)(sg - mc.s1) * kSeg; off = mn.off; len = mn.len;
-            } else {                                   // a read past the next one (short reads)
-                r = rc + 2;
-                int64_t e = a.seg_cum[r + 1];
-                while (e <= sg) e = a.seg_cum[++r + 1];
-                p = (int)(sg - a.seg_cum[r]) * kSeg;
-                off = a.v_off[r];
-                len = a.v_len[r];
-            }
-            return true;
-        };
-        // a lane's 40 bytes: dwords 0-3 always inside the buffer (p < len, >= 16 B of padding past
-        // every view), 4-7 and 8-9 only when they start inside that reach -- otherwise re-read from
-        // the segment start (those bytes lie past the read and are masked)
-        auto fetch = [&](int64_t off, int p, int len, uint32_t (&d)[10]) {
-            const uint32_t *q = reinterpret_cast<const uint32_t *>(a.codes + off + p);
-            const uint32_t *q1 = p + 16 <= len ? q + 4 : q;
-            const uint32_t *q2 = p + 24 <= len ? q + 8 : q;
-#pragma unroll
-            for (int t = 0; t < 4; ++t) d[t] = q[t];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) d[4 + t] = q1[t];
-            d[8] = q2[0];
-            d[9] = q2[1];
-        };
-        // Two segments in flight: while one is looked up, the next one's 40 bytes load (ping-pong
-        // buffers, so no register copies between steps)
-        struct Seg {
-            uint32_t d[10];
-            int64_t rd, off;
-            int p, len;
-            bool act;
-        };
-        auto issue = [&](int64_t bb, Seg &g) {
-            g.act = false;
-            if (bb >= hi) return;
-            advance(bb);
-            g.act = map(bb, g.rd, g.p, g.off, g.len);
-            if (g.act) fetch(g.off, g.p, g.len, g.d);
-        };
-        auto process = [&](const Seg &g) {
-            if (!g.act) return;
-            const uint32_t (&d)[10] = g.d;
-            const int64_t crd = g.rd, coff = g.off;
-            const int cp = g.p, clen = g.len;
-            // ---- the segment's 32 positions ----
-            auto byte = [&](int j) -> uint32_t {
-                return (j & 3) == 3 ? d[j >> 2] >> 24 : (d[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-            };
-            uint32_t c = 0;
-#pragma unroll
-            for (int j = 0; j < 7; ++j) c = (c << 2) | byte(j);
-            uint32_t hits = 0;
-#pragma unroll
-            for (int i = 0; i < kSeg; ++i) {
-                c = (c << 2) | byte(i + 7);
-                const uint32_t word = lds_at((c >> 3) & 0x1FFCu);
-                hits = __builtin_amdgcn_alignbit(word >> (c & 31u), hits, 1);
-            }
-            // ---- validity: N bytes and the read end ----
-            const int rem = clen - cp;                 // >= 1
-            uint32_t nor = 0;
-#pragma unroll
-            for (int t = 0; t < 10; ++t) nor |= d[t];
-            uint64_t inv = 0;
-            uint32_t slow = 0;
-            if ((nor & 0x04040404u) || rem < 40) {
-#pragma unroll
-                for (int t = 0; t < 10; ++t)
-                    inv |= (uint64_t)((((d[t] >> 2) & 0x01010101u) * 0x10204080u) >> 28) << (4 * t);
-                if (rem < 64) inv |= ~0ull << rem;
-                const uint64_t t1 = inv | (inv >> 1), t2 = t1 | (t1 >> 2), t3 = t2 | (t2 >> 4);
-                const uint32_t full8 = ~(uint32_t)t3;
-                hits &= full8;
-                if (a.min_k < kMaxK) slow = ~(uint32_t)(t2 | (t2 >> (a.min_k - kMinK))) & ~full8;
-            }
-            // ~15 % of the lanes hold a hit: appended to the block's slab one hit per lane and pass
-            // (passes = the most hits of a lane, usually 1), one LDS atomic per pass
-            uint32_t left = hits | slow;
-            const uint8_t *seg = a.codes + coff + cp;
-            while (__any(left != 0)) {                 // wave-uniform
-                const bool has = left != 0;
-                const uint64_t m = __ballot(has);
-                const int leader = __ffsll((unsigned long long)m) - 1;
-                int base = 0;
-                if (lane == leader) base = atomicAdd(&s_cnt, __popcll(m));
-                base = __shfl(base, leader);
-                if (has) {
-                    const int slot = base + __popcll(m & ((1ull << lane) - 1));
-                    const int i = __builtin_ctz(left);
-                    left &= left - 1;
-                    // the position's 8-mer from the (cached) read bytes, its valid run
-                    uint32_t c8 = 0;
-#pragma unroll
-                    for (int t = 0; t < 8; ++t) c8 = (c8 << 2) | (seg[i + t] & 3u);
-                    const uint32_t run = (slow >> i) & 1u ? (uint32_t)min(8, __builtin_ctzll(inv >> i)) : 8u;
-                    if (slot < a.slab)
-                        slab[slot] = make_uint4((uint32_t)crd, (uint32_t)(cp + i) | ((slow >> i) & 1u ? kSlowBit : 0u),
-                                                c8 | (run << 16), (uint32_t)(clen - (cp + i)));
-                }
-            }
-        };
-        Seg sa, sb;
-#pragma unroll
-        for (int t = 0; t < 10; ++t) sa.d[t] = sb.d[t] = 0x04040404u;
-        sb.rd = sb.off = 0;
-        sb.p = sb.len = 0;
-        sb.act = false;
-        int64_t b = lo;
-        issue(b, sa);
-        while (b < hi) {                               // wave-uniform
-            issue(b + 64, sb);
-            process(sa);
-            b += 64;
-            if (b >= hi) break;
-            issue(b + 64, sa);
-            process(sb);
-            b += 64;
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        a.raw_cnt[blockIdx.x] = min(s_cnt, a.slab);
-        if (s_cnt > a.slab) atomicOr(&a.flags[0], 1);
-    }
-}
-
-// k_seed_scan (r04): the same segment walk, hit masks and slab records as k_seed_scan_bits (the
-// r03 kernel, PCABI_SEED_BYTEMAP=0), with the per-position work cut from 6 VALU instructions to 2:
+// k_seed_scan (r04): that segment walk, with the per-position work cut from the r03 kernel's 6 VALU
+// instructions (an LDS bitmap word per position) to 2:
 //   * the merged 8-mer bitmap is expanded into a BYTE map in LDS (64 KiB), so a lookup is one
 //     ds_read_u8 at an 8-mer code; r05: a PAIR map -- byte c holds the membership of c and, per next
 //     base j, of the 8-mer that follows (c << 2 | j), so one read serves two positions;
 //   * a lane's 40 bytes are packed once into 2-bit codes, base 0 in the top bits (P0 = bases 0-15,
 //     Q0 = 8-23, P1 = 16-31, Q1 = 24-39): position i's code is one bit-field extract of one of them;
 //   * a hit's 8-mer comes from the same packed words (no re-read of the read bytes).
-// 512-thread blocks: two blocks (16 waves) per CU share the CU's LDS between their byte maps.
+// Two blocks per CU share the CU's LDS between their byte maps.
 constexpr int kScanThreads = 1024;
 constexpr int kByteMap = 1 << 16;            // bytes: one per 8-mer code
 
@@ -418,7 +247,7 @@ __device__ __forceinline__ uint32_t pack16(uint32_t x0, uint32_t x1, uint32_t x2
 }
 
 // TPB: threads per block (r05: 1024 -- two blocks per CU, each holding the 64 KiB map, run 32 waves
-// per CU instead of 16; PCABI_SCAN_THREADS=512 keeps the r04 blocks, A/B)
+// per CU instead of the r04 blocks' 16; measured neutral, kept)
 template <int TPB>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB == 1024 ? 8 : 4))) void k_seed_scan(ScanArgs a) {
     // static LDS (a workgroup may hold more than 64 KiB of it on gfx950): the byte map -- a position's
@@ -579,7 +408,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB == 1024
                     hits |= __builtin_amdgcn_ubfe(m[j], x >> (28 - 4 * j), 2u) << i;
                 }
             }
-            // ---- validity: N bytes and the read end (as k_seed_scan_bits) ----
+            // ---- validity: N bytes and the read end (doubling ORs of the invalid-byte mask) ----
             const int rem = clen - cp;
             uint32_t nor = 0;
 #pragma unroll
@@ -719,35 +548,6 @@ __device__ __forceinline__ TaskCount expand_hit(const ScanArgs &a, const uint32_
 // (PMC: waves waiting ~88 % of their lifetime) over ~3.5 generations of blocks
 constexpr int kExpandThreads = 1024;
 
-// Exclusive block sum over kExpandThreads threads in ~200 B of static LDS (hipcub's BlockScan takes
-// 8.4 KB at this width, which with a ~60 KB probe image passes the 64 KB a workgroup's LDS may hold
-// without an attribute): a wave scan by shuffles, then the 16 wave totals. Every thread calls it.
-__device__ __forceinline__ long long expand_excl_sum(long long v, long long &total, long long *s_w) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    long long x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const long long t = __shfl_up(x, d);
-        if (lane >= d) x += t;
-    }
-    if (lane == 63) s_w[w] = x;
-    __syncthreads();
-    if (w == 0) {
-        long long y = lane < kExpandThreads / 64 ? s_w[lane] : 0;
-#pragma unroll
-        for (int d = 1; d < kExpandThreads / 64; d <<= 1) {
-            const long long t = __shfl_up(y, d);
-            if (lane >= d) y += t;
-        }
-        if (lane < kExpandThreads / 64) s_w[lane] = y;   // inclusive wave prefixes
-    }
-    __syncthreads();
-    total = s_w[kExpandThreads / 64 - 1];
-    const long long ex = x - v + (w ? s_w[w - 1] : 0);
-    __syncthreads();                                     // s_w is reused by the next call
-    return ex;
-}
-
 // The probe image (up to ~60 KB) into LDS: 16-B loads, four in flight per thread (a dword loop
 // waited out one load latency per dword: ~50 us of fixed cost per launch, most of a small round's).
 __device__ __forceinline__ void expand_load_image(const ScanArgs &a, uint32_t *lds) {
@@ -809,86 +609,19 @@ __device__ __forceinline__ void expand_excl_sum2(long long v0, long long v1, lon
     __syncthreads();                                     // s_w is reused by the next call
 }
 
-__global__ __launch_bounds__(kExpandThreads) void k_seed_expand(ScanArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    __shared__ long long s_w[kExpandThreads / 64];
-    __shared__ long long s_base[2];                      // inside / edge bases, classes packed 32 | 32
-    expand_load_image(a, lds);
-    __syncthreads();
-    const uint16_t *rank = reinterpret_cast<const uint16_t *>(lds + a.rank_off);
-    const uint16_t *estart = reinterpret_cast<const uint16_t *>(lds + a.estart_off);
-    const int32_t *ent = reinterpret_cast<const int32_t *>(lds + a.ent_off);
-    const uint32_t *ent2 = lds + a.ent2_off;
-    // 1. the block's task counts and its places (one atomic per counter and block)
-    TaskCount mine{0, 0};
-    for (int sl = blockIdx.x; sl < a.n_slab; sl += gridDim.x) {
-        const uint4 *slab = a.raw + (int64_t)sl * a.slab;
-        const int cnt = a.raw_cnt[sl];
-        for (int i = threadIdx.x; i < cnt; i += kExpandThreads) {
-            const TaskCount c = expand_hit<false>(a, lds, rank, estart, ent, ent2, slab[i], TaskCount{0, 0});
-            mine.in += c.in;
-            mine.edge += c.edge;
-        }
-    }
-    {
-        long long tin, tedge;
-        (void)expand_excl_sum(mine.in, tin, s_w);
-        (void)expand_excl_sum(mine.edge, tedge, s_w);
-        if (threadIdx.x == 0) {
-            long long b[2] = {0, 0};
-            bool over = false;
-            for (int c = 0; c < kCls; ++c) {
-                const long long ti = (tin >> (32 * c)) & 0xFFFFFFFFll, te = (tedge >> (32 * c)) & 0xFFFFFFFFll;
-                const long long bi = ti ? atomicAdd(&a.cnt[c], (int)ti) : 0;
-                const long long be = te ? atomicAdd(&a.cnt[kCls + c], (int)te) : 0;
-                b[0] |= bi << (32 * c);
-                b[1] |= be << (32 * c);
-                over |= bi + ti > a.cap || be + te > a.ecap;
-            }
-            s_base[0] = b[0];
-            s_base[1] = b[1];
-            if (over) atomicOr(&a.flags[1], 1);
-        }
-        __syncthreads();
-    }
-    // 2. the tasks, a block's worth of hits at a time
-    for (int sl = blockIdx.x; sl < a.n_slab; sl += gridDim.x) {      // block-uniform
-        const uint4 *slab = a.raw + (int64_t)sl * a.slab;
-        const int cnt = a.raw_cnt[sl];
-        for (int base = 0; base < cnt; base += kExpandThreads) {
-            const int i = base + (int)threadIdx.x;
-            const uint4 r = i < cnt ? slab[i] : make_uint4(0u, 0u, 0u, 0u);
-            const TaskCount c = i < cnt ? expand_hit<false>(a, lds, rank, estart, ent, ent2, r, TaskCount{0, 0})
-                                        : TaskCount{0, 0};
-            long long ti, te;
-            const long long exi = expand_excl_sum(c.in, ti, s_w);
-            const long long exe = expand_excl_sum(c.edge, te, s_w);
-            if (i < cnt) expand_hit<true>(a, lds, rank, estart, ent, ent2, r, TaskCount{s_base[0] + exi, s_base[1] + exe});
-            __syncthreads();                           // s_base advanced after every read of it
-            if (threadIdx.x == 0) {
-                s_base[0] += ti;
-                s_base[1] += te;
-            }
-            __syncthreads();
-        }
-    }
-}
-
 // One-pass expansion (r04, the default): a block's slabs (blockIdx.x + k * gridDim.x) in
 // groups of kExpandGroup are one flat run of hits (a prefix of their counts in LDS), taken
 // kExpandHits per thread at a time: each hit's probe walk counts its tasks (kept in registers), a
 // block scan places them, one atomic per class and pass takes the block's place, and the second
 // walk writes. The two-pass kernel walks every hit three times and runs a slab at a time (~1.1 k
-// hits per slab in round 1 of 8 kb reads: a 1024-thread pass half idle, two scans per slab).
-int expand_hits() {
-    const char *e = std::getenv("PCABI_EXPAND_HITS");
-    return (e && e[0] == '2') ? 2 : 3;
-}
+// hits per slab in round 1 of 8 kb reads: a 1024-thread pass half idle, two scans per slab; r04:
+// 0.25 -> 0.18 ms per 8 kb step, profiles/r04/r04l/).
 // kExpandHits hits per thread and pass (r05bb: 3 fits 64 VGPRs under amdgpu_waves_per_eu(8), two
 // blocks per CU, and beats 2 in-process: 1.938 -> 1.924 ms at 8 kb, 2.495 -> 2.462 at 20 kb; 4
-// spills there; PCABI_EXPAND_HITS=2 selects the r04 form, A/B)
+// spills there)
 constexpr int kExpandGroup = 64;
-template <int kExpandHits>
+constexpr int kExpandHits = 3;
+template <int HITS>
 __global__ __launch_bounds__(kExpandThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_seed_expand1(ScanArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     __shared__ long long s_w[2 * (kExpandThreads / 64)];
@@ -917,13 +650,13 @@ __global__ __launch_bounds__(kExpandThreads) __attribute__((amdgpu_waves_per_eu(
         }
         __syncthreads();
         const int total = s_pre[ng];
-        for (int base = 0; base < total; base += kExpandHits * kExpandThreads) {
-            uint4 r[kExpandHits];
-            uint64_t pc[kExpandHits];                    // a hit's four counts in 16 bits each (a hit
+        for (int base = 0; base < total; base += HITS * kExpandThreads) {
+            uint4 r[HITS];
+            uint64_t pc[HITS];                    // a hit's four counts in 16 bits each (a hit
                                                          // has fewer tasks than the table has entries)
             long long si = 0, se = 0;
 #pragma unroll
-            for (int j = 0; j < kExpandHits; ++j) {
+            for (int j = 0; j < HITS; ++j) {
                 const int f = base + j * kExpandThreads + (int)threadIdx.x;
                 pc[j] = 0;
                 r[j] = make_uint4(0u, 0u, 0u, 0u);
@@ -962,7 +695,7 @@ __global__ __launch_bounds__(kExpandThreads) __attribute__((amdgpu_waves_per_eu(
             __syncthreads();
             TaskCount at{s_base[0] + exi, s_base[1] + exe};
 #pragma unroll
-            for (int j = 0; j < kExpandHits; ++j) {
+            for (int j = 0; j < HITS; ++j) {
                 if (pc[j]) {                             // hits without tasks write nothing
                     expand_hit<true>(a, lds, rank, estart, ent, ent2, r[j], at);
                     at.in += (long long)(pc[j] & 0xFFFF) | (long long)((pc[j] >> 16) & 0xFFFF) << 32;
@@ -1443,7 +1176,7 @@ struct State {
     bool planned = false, ok = false;
     double cost_seed = 0.0, cost_filter = 0.0;    // per read position (model units)
     int band[kCls] = {0, 0};                      // E of each class
-    size_t lds_bytes = 0;                         // the whole probe image (k_seed_expand)
+    size_t lds_bytes = 0;                         // the whole probe image (k_seed_expand1)
     int32_t adp_bytes = 0;                        // flat adapter table, dword-rounded
     ScanArgs a{};
     Buf tabs, adp, adp_off, adp_len, adp_meta, task, cnt, bound, thr, cands, ccnt, raw, rawcnt, segcum, scantmp;
@@ -1451,10 +1184,8 @@ struct State {
     int32_t n_adp = 0;
     int64_t cap = 0, ecap = 0, ccap = 0, raw_cap = 0;
     int scan_blocks = 0;                          // resident k_seed_scan blocks
-    int scan_tpb = kScanThreads;                  // their threads (PCABI_SCAN_THREADS=512: the r04 blocks)
-    int n_slab = 0;                               // raw-hit slabs: one per byte-map scan wave (r03 scan: per block)
-    bool bytemap = true;                          // k_seed_scan (byte map) or k_seed_scan_bits (r03)
-    int expand_blocks = 0;                        // resident k_seed_expand blocks
+    int n_slab = 0;                               // raw-hit slabs: one per scan wave
+    int expand_blocks = 0;                        // resident k_seed_expand1 blocks
     int pin_blocks[kCls] = {0, 0};                // resident k_seed_band_pin blocks per class
     Buf vseed;                                    // verified seeds (device rounds)
     std::vector<int32_t> ucert;                   // per adapter: the candidate windows' certificate bound
@@ -1644,8 +1375,7 @@ int plan(State *s, const uint8_t *hcodes, const int32_t *hoff, const int32_t *hl
                 if (thr[a] >= (1 << 19)) fits = false;
                 meta[a] = alen[a] | (thr[a] << 12);
             }
-        const char *e = std::getenv("PCABI_SEED_PIN");
-        const bool on = fits && !(e && e[0] == '0');
+        const bool on = fits;
         s->n_adp = n_adp;
         for (int c = 0; c < kCls; ++c) {
             // the slot holds the band's read range: L + 2E bytes from a 16-byte boundary, one more
@@ -1814,26 +1544,13 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
         int dev = 0, cus = 0, per_cu = 0;
         SD_TRY(hipGetDevice(&dev));
         SD_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        const char *e = std::getenv("PCABI_SEED_BYTEMAP");   // 0: the r03 bitmap scan (A/B)
-        s->bytemap = !(e && e[0] == '0');
-        if (s->bytemap) {
-            const char *et = std::getenv("PCABI_SCAN_THREADS");
-            s->scan_tpb = (et && std::atoi(et) == 512) ? 512 : kScanThreads;
-            if (s->scan_tpb == 512)
-                SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_scan<512>, 512, 0));
-            else
-                SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_scan<kScanThreads>, kScanThreads, 0));
-        } else {
-            SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_scan_bits, 256,
-                                                                4 * (size_t)s->a.bits_dw + 4));
-        }
+        SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_scan<kScanThreads>, kScanThreads, 0));
         s->scan_blocks = std::max(1, cus * std::max(1, per_cu));
-        s->n_slab = s->bytemap ? s->scan_blocks * (s->scan_tpb / 64) : s->scan_blocks;   // per wave / per block
+        s->n_slab = s->scan_blocks * (kScanThreads / 64);   // one slab per scan wave
         per_cu = 0;
-        SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_expand, kExpandThreads, s->lds_bytes));
+        SD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_seed_expand1<kExpandHits>, kExpandThreads,
+                                                            s->lds_bytes));
         s->expand_blocks = std::min(s->n_slab, std::max(1, cus * std::max(1, per_cu)));
-        if (const char *eb = std::getenv("PCABI_EXPAND_BLOCKS"))   // experiments: the expansion's grid
-            if (std::atoi(eb) > 0) s->expand_blocks = std::min(s->n_slab, std::atoi(eb));
     }
     const int grid = s->scan_blocks;
     if (s->raw_cap == 0 || s->cap == 0) {
@@ -1898,24 +1615,9 @@ int enqueue_seeds(State *s, const uint8_t *codes, const int64_t *v_off, const in
     hipLaunchKernelGGL(k_bound_reset, dim3(1024), dim3(256), 0, st, (int32_t *)s->bound.p, n, n_dev, n_adp, A.cnt,
                        kCntAll, (unsigned long long *)s->ccnt.p);
     if (s->pev) SD_TRY(hipEventRecord(s->pev[0], st));
-    if (s->bytemap && s->scan_tpb == 512)
-        hipLaunchKernelGGL(k_seed_scan<512>, dim3(grid), dim3(512), 0, st, A);
-    else if (s->bytemap)
-        hipLaunchKernelGGL(k_seed_scan<kScanThreads>, dim3(grid), dim3(kScanThreads), 0, st, A);
-    else
-        hipLaunchKernelGGL(k_seed_scan_bits, dim3(grid), dim3(256), 4 * (size_t)A.bits_dw + 4, st, A);
+    hipLaunchKernelGGL(k_seed_scan<kScanThreads>, dim3(grid), dim3(kScanThreads), 0, st, A);
     if (s->pev) SD_TRY(hipEventRecord(s->pev[1], st));
-    {   // the one-pass expansion (r04: 0.25 -> 0.18 ms at 8 kb); PCABI_EXPAND_PASSES=2 runs the
-        // two-pass kernel (read per launch: tests switch it)
-        const char *ep = std::getenv("PCABI_EXPAND_PASSES");
-        if (ep && ep[0] == '2')
-            hipLaunchKernelGGL(k_seed_expand, dim3(s->expand_blocks), dim3(kExpandThreads), s->lds_bytes, st, A);
-        else
-            if (expand_hits() == 3)
-                hipLaunchKernelGGL(k_seed_expand1<3>, dim3(s->expand_blocks), dim3(kExpandThreads), s->lds_bytes, st, A);
-            else
-                hipLaunchKernelGGL(k_seed_expand1<2>, dim3(s->expand_blocks), dim3(kExpandThreads), s->lds_bytes, st, A);
-    }
+    hipLaunchKernelGGL(k_seed_expand1<kExpandHits>, dim3(s->expand_blocks), dim3(kExpandThreads), s->lds_bytes, st, A);
     if (s->pev) SD_TRY(hipEventRecord(s->pev[2], st));
     SD_TRY(hipGetLastError());
     if (tasks) return 0;                                // the caller launches the bands (host counts)

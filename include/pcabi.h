@@ -217,8 +217,7 @@ int pcabi_align_cross_multi_dev(const pcabi_cross_region *regions, int32_t n_reg
  * callers that run cross products on several streams at once should turn it off: HIP maps the
  * process's streams onto GPU_MAX_HW_QUEUES hardware queues, and a side stream on the queue of
  * another caller stream's large launch waits for it (r04r: the reference job 4.95 -> 4.66 ms
- * off). The initial setting is PCABI_FORK (0 or 1; unset: see DESIGN.md §5). Returns the previous
- * setting; on < 0 only reads it. */
+ * off). Initially on. Returns the previous setting; on < 0 only reads it. */
 int pcabi_set_side_streams(int on);
 /* The same setting for one stream (r05): the cross products and middle-scan rounds queued on `stream`
  * use the side streams when on = 1 and run every bucket on `stream` when on = 0, whatever the

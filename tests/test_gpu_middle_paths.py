@@ -313,11 +313,11 @@ def test_candidate_windows_at_the_certificate_bound(gpu_lib, monkeypatch, mean_l
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('thr', [90.0, 85.0])
-def test_seed_scan_bytemap_equals_bitmap_scan(gpu_lib, monkeypatch, thr):
-    """k_seed_scan (r04: the byte map, packed codes) vs k_seed_scan_bits (r03, PCABI_SEED_BYTEMAP=0)
-    on reads with N bases, reads shorter than a segment and ragged ends, at 90 % (8-mers only) and
-    85 % (probes of 5-6 bases: the short-run path): the same raw hits, band tasks and candidate-DP
-    cells per round (pcabi_scan_profile's counters) and the oracle's hits."""
+def test_seed_scan_n_runs_and_short_reads(gpu_lib, monkeypatch, thr):
+    """k_seed_scan (the pair byte map over packed codes) on reads with N bases, reads shorter than a
+    segment and ragged ends, at 90 % (8-mers only) and 85 % (probes of 5-6 bases: the short-run
+    path): the oracle's hits, and raw hits / band tasks counted (pcabi_scan_profile). (r03-r05 also
+    ran the r03 bitmap scan beside it and compared the counters; that kernel is retired.)"""
     from custom_porechop_abi_amd import engine
     rng = random.Random(int(thr))
     reads = _reads(31 + int(thr), 90, 3000, thr)
@@ -334,25 +334,18 @@ def test_seed_scan_bytemap_equals_bitmap_scan(gpu_lib, monkeypatch, thr):
     views = pack.views(np.zeros(len(reads), np.int64), pack.lengths)
     exp = _sorted(oracle_lib.middle_scan_threaded(views, ADPS, SC, thr))
     monkeypatch.setenv('PCABI_MIDDLE_SEEDS', '2')
-    prof, got = {}, {}
-    for mode in ('1', '0'):
-        monkeypatch.setenv('PCABI_SEED_BYTEMAP', mode)
-        prof[mode] = np.zeros(26, np.float64)
-        got[mode] = _dev_scan(gpu_lib, views, ADPS, SC, thr, profile=prof[mode])
-    for mode in ('0', '1'):
-        assert np.array_equal(_sorted(got[mode]), exp), ('bytemap=%s' % mode, prof[mode][7:15], prof['0'][7:15])
-    assert prof['1'][10] > 0
-    assert np.array_equal(prof['1'][7:15], prof['0'][7:15]), (prof['1'][7:15], prof['0'][7:15])
+    prof = np.zeros(26, np.float64)
+    got = _dev_scan(gpu_lib, views, ADPS, SC, thr, profile=prof)
+    assert np.array_equal(_sorted(got), exp), prof[7:15]
+    assert prof[10] > 0
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('thr', [90.0, 85.0])
 def test_seed_expand_one_pass(gpu_lib, monkeypatch, thr):
-    """k_seed_expand1 (the default: a block's slabs as one flat run of hits, two per thread and
-    pass, one walk to count and one to write) vs the two-pass k_seed_expand (PCABI_EXPAND_PASSES=2): the same
-    raw hits, band tasks and candidate-DP cells per scan (pcabi_scan_profile) and the oracle's hits,
-    on reads with N runs and ragged ends; then with task regions far too small (every pass flags
-    the overflow, the round grows them and reruns)."""
+    """k_seed_expand1 (a block's slabs as one flat run of hits, three per thread and pass, one walk
+    to count and one to write) on reads with N runs and ragged ends: the oracle's hits; then with
+    task regions far too small (every pass flags the overflow, the round grows them and reruns)."""
     from custom_porechop_abi_amd import engine
     rng = random.Random(7 + int(thr))
     reads = _reads(57 + int(thr), 120, 3000, thr)
@@ -366,22 +359,10 @@ def test_seed_expand_one_pass(gpu_lib, monkeypatch, thr):
     views = pack.views(np.zeros(len(reads), np.int64), pack.lengths)
     exp = _sorted(oracle_lib.middle_scan_threaded(views, ADPS, SC, thr))
     monkeypatch.setenv('PCABI_MIDDLE_SEEDS', '2')
-    prof = {}
-    for mode in ('2', '1'):
-        monkeypatch.setenv('PCABI_EXPAND_PASSES', mode)
-        prof[mode] = np.zeros(26, np.float64)
-        got = _dev_scan(gpu_lib, views, ADPS, SC, thr, profile=prof[mode])
-        assert np.array_equal(_sorted(got), exp), 'passes=%s' % mode
-    assert prof['1'][11] > 0
-    assert np.array_equal(prof['1'][7:15], prof['2'][7:15]), (prof['1'][7:15], prof['2'][7:15])
-    # a grid of 8 blocks: hundreds of slabs per block, in several groups of kExpandGroup
-    monkeypatch.setenv('PCABI_EXPAND_PASSES', '1')
-    monkeypatch.setenv('PCABI_EXPAND_BLOCKS', '8')
-    prof['g'] = np.zeros(26, np.float64)
-    got = _dev_scan(gpu_lib, views, ADPS, SC, thr, profile=prof['g'])
-    assert np.array_equal(_sorted(got), exp), 'passes=1, 8 blocks'
-    assert np.array_equal(prof['g'][7:15], prof['2'][7:15]), (prof['g'][7:15], prof['2'][7:15])
-    monkeypatch.delenv('PCABI_EXPAND_BLOCKS')
+    prof = np.zeros(26, np.float64)
+    got = _dev_scan(gpu_lib, views, ADPS, SC, thr, profile=prof)
+    assert np.array_equal(_sorted(got), exp)
+    assert prof[11] > 0
     monkeypatch.setenv('PCABI_MIDDLE_INIT_CAPS', '0,64,0')
     n0, _ = _requeues(gpu_lib)
     got = _dev_scan(gpu_lib, views, ADPS, SC, thr)
@@ -395,49 +376,28 @@ def test_seed_expand_one_pass(gpu_lib, monkeypatch, thr):
 def test_round_graphs_replay(gpu_lib, monkeypatch, reads_8kb, windows):
     """Rounds after a call's first, captured into graphs (the third call of a key) and replayed (the
     fourth and fifth), on a library stream: every call equals the oracle, with and without candidate
-    windows, and equals the same scans with graphs off (PCABI_MIDDLE_GRAPHS=0)."""
+    windows (the whole-read rounds' chunk tasks one lane each, the window rounds' on the row-split
+    core, two lanes per task), and equals a fresh scan's first call (rounds queued directly)."""
     views, exp = reads_8kb
     monkeypatch.setenv('PCABI_MIDDLE_SEEDS', '2')
     monkeypatch.setenv('PCABI_MIDDLE_WINDOWS', windows)
     got = _dev_scan(gpu_lib, views, ADPS, SC, 90.0, calls=5, stream=True)
     assert np.array_equal(_sorted(got), exp)
-    monkeypatch.setenv('PCABI_MIDDLE_GRAPHS', '0')
-    off = _dev_scan(gpu_lib, views, ADPS, SC, 90.0, calls=2, stream=True)
-    assert np.array_equal(got, off)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize('split', ['0', '2', '4'])
-@pytest.mark.parametrize('windows', ['0', '1'])
-def test_chunk_dp_row_split(gpu_lib, monkeypatch, reads_8kb, split, windows):
-    """PCABI_CHUNK_SPLIT=0|2|4: the candidate DP's chunk tasks one lane per task, or on the row-split
-    core (K lanes per task, k_align_split_chunk, K = 2 the default since r05; host model:
-    test_dp_core_cpu.py::test_row_split_chunk_core) -- the scan
-    equals the oracle, whole-read chunks and candidate windows alike, and at 90 % on shorter copies
-    with the 85 % threshold's longer probes."""
-    from custom_porechop_abi_amd import engine
-    views, exp = reads_8kb
-    monkeypatch.setenv('PCABI_MIDDLE_SEEDS', '2')
-    monkeypatch.setenv('PCABI_MIDDLE_WINDOWS', windows)
-    monkeypatch.setenv('PCABI_CHUNK_SPLIT', split)
-    got = _dev_scan(gpu_lib, views, ADPS, SC, 90.0)      # a fresh scan: the switch is read per process
-    assert np.array_equal(_sorted(got), exp)
-    got2 = engine.middle_scan(views, ADPS, SC, 90.0)
-    assert np.array_equal(_sorted(got2), exp)
+    direct = _dev_scan(gpu_lib, views, ADPS, SC, 90.0, calls=1, stream=True)
+    assert np.array_equal(got, direct)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('windows', ['0', '1'])
-@pytest.mark.parametrize('wpb', ['1', '4'])
-def test_chunk_dp_one_wave_blocks(gpu_lib, monkeypatch, reads_8kb, windows, wpb):
-    """The device-planned chunk launches in one-wave blocks (the default: no table barrier shared
-    by four waves) and in four-wave blocks (PCABI_CHUNK_WPB=4) -- the scan equals the oracle,
-    whole-read chunks and candidate windows."""
+def test_chunk_dp_host_api(gpu_lib, monkeypatch, reads_8kb, windows):
+    """The candidate DP's chunk tasks through the host API (engine.middle_scan: per-call tables,
+    rounds queued directly) -- one lane per task in the whole-read rounds, two (k_align_split_chunk,
+    host model: test_dp_core_cpu.py::test_row_split_chunk_core) in the candidate-window rounds --
+    equal the oracle."""
     from custom_porechop_abi_amd import engine
     views, exp = reads_8kb
     monkeypatch.setenv('PCABI_MIDDLE_SEEDS', '2')
     monkeypatch.setenv('PCABI_MIDDLE_WINDOWS', windows)
-    monkeypatch.setenv('PCABI_CHUNK_WPB', wpb)
     got = engine.middle_scan(views, ADPS, SC, 90.0)
     assert np.array_equal(_sorted(got), exp)
 
