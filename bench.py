@@ -106,6 +106,10 @@ def parse():
                          'multi call; 3 = after both dominant launches, both sides\' smaller buckets dealt onto the two '
                          'caller streams by cost; 2 = each on its own stream; 1 = the two sides\' calls side by side '
                          '(r05); 0 = after each side\'s dominant launch')
+    ap.add_argument('--group-side', type=int, default=1,
+                    help='headline schedule 5: the multi call\'s grouped launches side by side on the library\'s side '
+                         'streams (1, default) or one after the other on the caller\'s stream (0: the dominant launch '
+                         'then has the GPU to itself)')
     ap.add_argument('--hw-queues', type=int, default=0,
                     help='GPU_MAX_HW_QUEUES for this process when the environment does not set it (0: HIP default, '
                          '4; r04 A/B with 8: headline 8.05 vs 7.61 ms, reference job 5.85 vs 5.23 ms)')
@@ -470,7 +474,8 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
     # as the production schedule, keeps them on)
     two_streams = not timed_fused and args.rest_overlap in (1, 3)
     if not timed_fused and args.rest_overlap in (4, 5):
-        L.pcabi_stream_side_streams(stream, 1)     # one (grouped) call at a time: its launches side by side
+        # one (grouped) call at a time: its launches side by side (or, --group-side 0, one after the other)
+        L.pcabi_stream_side_streams(stream, 1 if args.rest_overlap == 4 or args.group_side else 0)
     # (per stream, r05: pcabi_stream_side_streams leaves every other caller of the library alone)
     if two_streams:
         for s_ in (stream, stream2):
