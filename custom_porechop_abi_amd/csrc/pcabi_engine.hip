@@ -178,7 +178,17 @@ int64_t middle_plan_waves() {
 
 // One block per 64 reads: wave w takes adapters w, w + 4, ... of both sides (lane = read: the
 // loads of one adapter's field are 256-B coalesced), the four partial maxima meet in LDS. (r03: one
-// thread per read looped over every adapter -- 391 blocks for 100k reads, latency-bound.)
+// thread per read looped over every adapter -- 391 blocks for 100k reads, latency-bound.) r06: the
+// four fields a decision reads (rs, re, m, l1: 16 of the result's 32 bytes) are loaded
+// unconditionally, four adapters at a time, so a wave keeps 16 independent loads in flight instead
+// of a dependent pair per adapter (the kernel reads 149 MB per headline step: HBM-bound, 42 us in r05).
+struct EndFields {
+    int rs, re, m, l1;
+};
+__device__ __forceinline__ EndFields end_fields(const int32_t *res, int64_t stride, int64_t i) {
+    return EndFields{res[0 * stride + i], res[1 * stride + i], res[5 * stride + i], res[6 * stride + i]};
+}
+
 __global__ __launch_bounds__(256) void k_end_trim(const int32_t *sres, int64_t sstride, int32_t n_sa,
                                                   const int32_t *eres, int64_t estride, int32_t n_ea,
                                                   int64_t n_read, int end_size, int extra,
@@ -189,35 +199,60 @@ __global__ __launch_bounds__(256) void k_end_trim(const int32_t *sres, int64_t s
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t r = (int64_t)blockIdx.x * 64 + lane;
     const bool live = r < n_read;
+    constexpr int U = 4;                              // adapters in flight per wave
     // find_start_trim (nanopore_read.py:175-195)
     int st = 0;
-    for (int a = w; live && a < n_sa; a += 4) {
-        const int64_t i = (int64_t)a * n_read + r;
-        const int rs = sres[0 * sstride + i];
-        int re1, hit = 0;
-        double partial;
-        if (rs == -1) { re1 = 0; partial = 0.0; }
-        else { re1 = sres[1 * sstride + i] + 1; partial = pcabi::pid6(sres[5 * sstride + i], sres[6 * sstride + i]); }
-        if (partial > thr && re1 != end_size && re1 - rs >= min_trim) {
-            st = max(st, re1 + extra);
-            hit = 1;
+    for (int a0 = w; live && a0 < n_sa; a0 += 4 * U) {
+        EndFields f[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int a = a0 + 4 * u;
+            f[u] = a < n_sa ? end_fields(sres, sstride, (int64_t)a * n_read + r) : EndFields{-1, 0, 0, 0};
         }
-        if (shit) shit[i] = (uint8_t)hit;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int a = a0 + 4 * u;
+            if (a >= n_sa) break;
+            const int rs = f[u].rs;
+            int re1 = 0, hit = 0;
+            double partial = 0.0;
+            if (rs != -1) {
+                re1 = f[u].re + 1;
+                partial = pcabi::pid6(f[u].m, f[u].l1);
+            }
+            if (partial > thr && re1 != end_size && re1 - rs >= min_trim) {
+                st = max(st, re1 + extra);
+                hit = 1;
+            }
+            if (shit) shit[(int64_t)a * n_read + r] = (uint8_t)hit;
+        }
     }
     // find_end_trim (nanopore_read.py:197-217)
     int et = 0;
-    for (int a = w; live && a < n_ea; a += 4) {
-        const int64_t i = (int64_t)a * n_read + r;
-        const int rs = eres[0 * estride + i];
-        int re1, hit = 0;
-        double partial;
-        if (rs == -1) { re1 = 0; partial = 0.0; }
-        else { re1 = eres[1 * estride + i] + 1; partial = pcabi::pid6(eres[5 * estride + i], eres[6 * estride + i]); }
-        if (partial > thr && rs != 0 && re1 - rs >= min_trim) {
-            et = max(et, (end_size - rs) + extra);
-            hit = 1;
+    for (int a0 = w; live && a0 < n_ea; a0 += 4 * U) {
+        EndFields f[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int a = a0 + 4 * u;
+            f[u] = a < n_ea ? end_fields(eres, estride, (int64_t)a * n_read + r) : EndFields{-1, 0, 0, 0};
         }
-        if (ehit) ehit[i] = (uint8_t)hit;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int a = a0 + 4 * u;
+            if (a >= n_ea) break;
+            const int rs = f[u].rs;
+            int re1 = 0, hit = 0;
+            double partial = 0.0;
+            if (rs != -1) {
+                re1 = f[u].re + 1;
+                partial = pcabi::pid6(f[u].m, f[u].l1);
+            }
+            if (partial > thr && rs != 0 && re1 - rs >= min_trim) {
+                et = max(et, (end_size - rs) + extra);
+                hit = 1;
+            }
+            if (ehit) ehit[(int64_t)a * n_read + r] = (uint8_t)hit;
+        }
     }
     s_st[w][lane] = st;
     s_et[w][lane] = et;
@@ -1088,39 +1123,42 @@ __global__ __launch_bounds__(256) void k_trim_views(const int64_t *read_off, con
 
 // Tile layout of a window list (cross mode): windows [256t, 256t + 256) form tile t; dword
 // (t, q, lane) = codes 4q..4q+3 of window 256t + lane, at tiles[tile_off[t] + 256q + lane].
-// Zero past each window's end. One block transposes 256 windows x 16 chunks through LDS: reads
-// are 64-byte runs of each window (any offset), writes are 1 KB rows.
+// Zero past each window's end. Thread = window: it loads its window's 64-byte slab (17 dwords,
+// independent loads, any offset: a byte funnel shift) and writes its 16 dwords down the tile's
+// rows, so every row store of a wave is 256 contiguous bytes. (r01-r05: 16 threads per window and
+// an LDS transpose, each thread 16 dependent load chains in turn: 25 us per 100k 150-bp windows.)
 // grid (n_tiles, <= 1024): blockIdx.y strides over 16-chunk slabs.
 __global__ __launch_bounds__(256) void k_tile_windows(const uint8_t *codes, const int64_t *win_off,
                                                       const int32_t *win_len, int64_t n_win,
                                                       const int64_t *tile_off, uint32_t *tiles) {
-    __shared__ uint32_t sh[256][17];
     const int64_t t = blockIdx.x;
     const int64_t base = tile_off[t];
     const int64_t nq = (tile_off[t + 1] - base) / 256;
+    const int64_t w = t * 256 + threadIdx.x;
+    int64_t n = 0;
+    const uint8_t *wb = codes;
+    if (w < n_win) {
+        n = max(win_len[w], 0);
+        wb = codes + win_off[w];
+    }
     for (int64_t q0 = (int64_t)blockIdx.y * 16; q0 < nq; q0 += (int64_t)gridDim.y * 16) {
-        for (int k = threadIdx.x; k < 256 * 16; k += 256) {
-            const int wl = k >> 4, qq = k & 15;
-            const int64_t w = t * 256 + wl;
-            const int64_t c0 = 4 * (q0 + qq);
-            uint32_t v = 0;
-            if (w < n_win) {
-                const int n = win_len[w];
-                if (c0 < n) {
-                    // any window offset: two aligned dwords and a byte funnel shift
-                    const uint8_t *b = codes + win_off[w] + c0;
-                    const int sh = (int)((uintptr_t)b & 3);
-                    const uint32_t *q = reinterpret_cast<const uint32_t *>(b - sh);
-                    v = sh ? __builtin_amdgcn_alignbyte(q[1], q[0], sh) : q[0];
-                    if (n - c0 < 4) v &= (1u << (8 * (n - c0))) - 1u;
-                }
-            }
-            sh[wl][qq] = v;
-        }
-        __syncthreads();
+        const int64_t c0 = 4 * q0;
+        const int64_t avail = n - c0;                 // window bytes from column c0 on
+        const uint8_t *b = wb + c0;
+        const int sh = (int)((uintptr_t)b & 3);
+        const uint32_t *q = reinterpret_cast<const uint32_t *>(b - sh);
+        uint32_t d[17];
+#pragma unroll
+        for (int k = 0; k < 17; ++k) d[k] = (avail > 0 && 4 * k < avail + sh) ? q[k] : 0u;   // dwords holding window bytes
         const int nqq = (int)std::min<int64_t>(16, nq - q0);
-        for (int qq = 0; qq < nqq; ++qq) tiles[base + (q0 + qq) * 256 + threadIdx.x] = sh[threadIdx.x][qq];
-        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if (k >= nqq) break;
+            uint32_t v = sh ? __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh) : d[k];
+            const int64_t rem = avail - 4 * k;
+            v = rem >= 4 ? v : (rem > 0 ? v & ((1u << (8 * rem)) - 1u) : 0u);
+            tiles[base + (q0 + k) * 256 + threadIdx.x] = v;
+        }
     }
 }
 
