@@ -1379,7 +1379,8 @@ std::atomic<uint64_t> g_buf_gen{0};
 // is filled with one byte before use, so a kernel or host path that reads scratch nothing wrote
 // sees garbage instead of the zeros fresh hipMalloc memory usually holds (the
 // r05 `need2` read went unnoticed for that reason). "1" fills 0xFF (every int -1); a hex byte such
-// as "0x7f" fills that byte (0x7f: every int32 / int64 a huge positive count).
+// as "0x3f" fills that byte (0x3f: every int32 / int64 a huge positive count whose growth arithmetic
+// -- need + need / 4 -- does not overflow; 0x7f wrapped there and hid the r05 need2 read).
 int pcabi_poison_byte() {
     static const int b = [] {
         const char *e = std::getenv("PCABI_POISON");

@@ -1,6 +1,8 @@
 """Test infrastructure (run by tests/test_gpu_middle_paths.py::test_poisoned_scratch, in a child
-process started with PCABI_POISON=1 or =0x7f): every device scratch buffer this
-process allocates starts as 0xFF (every int -1) or 0x7F bytes (every int a huge count) instead of the zeros fresh hipMalloc memory usually holds, and the
+process started with PCABI_POISON=1 or =0x3f): every device scratch buffer this
+process allocates starts as 0xFF (every int -1) or 0x3F bytes (every int32 / int64 a huge positive count,
+small enough that a quarter more does not overflow int64: 0x7F bytes did, and hid the r05 bug)
+instead of the zeros fresh hipMalloc memory usually holds, and the
 middle scan's product paths and an end-trim cross product must still equal the oracle:
 
   * round-1 overflow, growth and requeue from tiny initial buffers (PCABI_MIDDLE_INIT_CAPS);

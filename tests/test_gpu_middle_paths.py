@@ -513,10 +513,10 @@ def test_barcode_call_96_sets_on_barcoded_reads(gpu_lib):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('byte', ['1', '0x7f'])
+@pytest.mark.parametrize('byte', ['1', '0x3f'])
 def test_poisoned_scratch(gpu_lib, byte):
     """PCABI_POISON (a child process: the switch is read once per process): every fresh device
-    scratch buffer and every growth starts as 0xFF bytes (every int -1) or 0x7F bytes (every int a
+    scratch buffer and every growth starts as 0xFF bytes (every int -1) or 0x3F bytes (every int a
     huge count), and the overflow / requeue, shadow-arena, candidate-window and end-trim cases of
     tests/poisoned_middle.py still equal the oracle -- a path that reads scratch nothing wrote (r05:
     the plans' need2) no longer hides behind zeroed memory."""

@@ -51,8 +51,8 @@ PY
       timeout -k 10 400 python -u -m pytest -x -v --timeout 400 --timeout-method thread -m gpu tests/test_gpu_middle_paths.py -k poisoned > $OUT/poison.log 2>&1 || { echo "poisoned test failed rc=$?"; tail -30 $OUT/poison.log; exit 1; }
       tail -2 $OUT/poison.log
       # the same cases against a library with c1b7048's fix reverted (perf_variants/r05bug.so): the
-      # 0x7f poison is expected to fail it
-      for b in 1 0x7f; do
+      # 0x3f poison is expected to fail it
+      for b in 1 0x3f; do
         PCABI_POISON=$b PCABI_LIB=$R/perf_variants/r05bug.so timeout -k 10 400 python -u tests/poisoned_middle.py > $OUT/poison_r05bug_$b.log 2>&1
         echo "r05bug variant, poison $b: rc=$? (nonzero expected for 0x7f)"; tail -3 $OUT/poison_r05bug_$b.log
       done ;;

@@ -1,13 +1,13 @@
 #!/bin/bash
 # r06: (1) the poisoned-scratch guard against a library with the r05 memset fix reverted
-# (perf_variants/r05bug.so, tools/make_r05bug.sh: the 0x7F poison is expected to fail it, 0xFF to pass);
+# (perf_variants/r05bug.so, tools/make_r05bug.sh: the 0x3F poison is expected to fail it, 0xFF to pass);
 # (2) the device plan's wave target A/B on the middle workloads (MID_AB)
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/${TAG:-r06misc}
 mkdir -p $OUT
 cd $R
-for b in 1 0x7f; do
+for b in 1 0x3f; do
   PCABI_POISON=$b PCABI_LIB=$R/perf_variants/r05bug.so timeout -k 10 300 python -u tests/poisoned_middle.py > $OUT/r05bug_$b.log 2>&1; rc=$?
   echo "r05bug library, poison $b: rc=$rc"; tail -3 $OUT/r05bug_$b.log
   if [ $rc -ge 124 ]; then echo "stopping: rc $rc"; exit 1; fi
