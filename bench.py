@@ -1463,6 +1463,10 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
         sides.append(dict(d_off=h2d(w_off), d_len=h2d(w_len), d_toff=h2d(toff), d_tiles=dalloc(4 * nd),
                           mq=int(np.diff(toff).max() // 256), mx=int(w_len.max()), tab=table(adps), d_res=d_res,
                           stride=len(adps) * n))
+    # both read ends' end-trim cross products in one pcabi_align_cross_multi_dev call (grouped
+    # launches, as the headline's default schedule); --rest-overlap 0..4: one call per side
+    end_regions = _lib.cross_regions([(sd['d_tiles'], sd['d_toff'], sd['d_len'], n, sd['mx'], sd['tab'], sd['d_res'],
+                                       sd['stride']) for sd in sides]) if args.rest_overlap == 5 else None
     mid_tab = table(mid_adps)
     scan = vp()
     _lib.check(L.pcabi_scan_create(mid_tab, ctypes.byref(scan)), 'scan_create')
@@ -1478,8 +1482,11 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
         for sd in sides:
             _lib.check(L.pcabi_tile_windows_dev(work, sd['d_off'], sd['d_len'], n, sd['d_toff'], sd['mq'],
                                                 sd['d_tiles'], stream), 'tile')
-            _lib.check(L.pcabi_align_cross_dev(sd['d_tiles'], sd['d_toff'], sd['d_len'], n, sd['mx'], sd['tab'], *sc,
-                                               sd['d_res'], sd['stride'], stream), 'align')
+            if end_regions is None:
+                _lib.check(L.pcabi_align_cross_dev(sd['d_tiles'], sd['d_toff'], sd['d_len'], n, sd['mx'], sd['tab'],
+                                                   *sc, sd['d_res'], sd['stride'], stream), 'align')
+        if end_regions is not None:
+            _lib.check(L.pcabi_align_cross_multi_dev(end_regions, len(end_regions), *sc, stream, None, None), 'align')
         _lib.check(L.pcabi_end_trim_dev(d_sres, n_sa * n, n_sa, d_eres, n_ea * n, n_ea, n, E, 2, 75.0, 4, d_st, d_et,
                                         None, None, stream), 'end_trim')
         _lib.check(L.pcabi_event_record(ev[0], stream), 'event')
@@ -1565,6 +1572,8 @@ def run_middle(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapter
                                    % (n, args.mean_len, len(sets), n_sa, n_ea, len(mid_adps), args.middle_threshold),
                        'reads_per_gpu': n, 'adapter_sets': len(sets), 'scoring': list(sc),
                        'parallelism': 'dp%d (read shards)' % world,
+                       'end_trim': ('both read ends in one pcabi_align_cross_multi_dev call' if end_regions is not None
+                                    else 'one pcabi_align_cross_dev call per read end'),
                        'inputs': 'one read pack resident in HBM for every step (the scan leaves it intact)'},
             'middle_ms_per_step': round(1e3 * stats['middle_s'] / args.steps, 3),
             'middle_hits_per_step': stats['hits'],

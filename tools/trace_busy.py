@@ -3,7 +3,10 @@ START (a kernel-name substring, default k_end_trim) to the end of the trace, wit
 duration, and the device's idle gaps (no kernel running on any queue) between them -- where a
 step's wall time goes beyond its kernels (launch latency, fork / join events, host round trips).
 
-    python tools/trace_busy.py run_kernel_trace.csv [START] [--all]"""
+    python tools/trace_busy.py run_kernel_trace.csv [START] [--all] [--prev]
+
+--prev: the step before the last (from the second-to-last START to the last one) -- the last step of
+a bench run with a per-phase profile step after the timed ones is that profile step."""
 import csv
 import sys
 
@@ -17,7 +20,10 @@ def main():
     if not idx:
         print('no kernel matching', start_pat)
         return
-    sel = rows[idx[-1]:]
+    if '--prev' in sys.argv and len(idx) > 1:
+        sel = rows[idx[-2]:idx[-1]]
+    else:
+        sel = rows[idx[-1]:]
     t0 = int(sel[0]['Start_Timestamp'])
     busy_end = t0
     idle = 0
