@@ -110,6 +110,11 @@ def parse():
                     help='headline schedule 5: the multi call\'s grouped launches side by side on the library\'s side '
                          'streams (1, default) or one after the other on the caller\'s stream (0: the dominant launch '
                          'then has the GPU to itself)')
+    ap.add_argument('--overlap-steps', type=int, default=1,
+                    help='headline schedule 5: 1 (default, r06) = consecutive steps overlap their memory-bound '
+                         'prologue and epilogue with the align phase: step k+1\'s tile transposes and step k\'s end '
+                         'trim run on a second stream (double-buffered tiles and results) while the main stream '
+                         'aligns; every step still does all of its own work. 0 = one step after the other')
     ap.add_argument('--hw-queues', type=int, default=0,
                     help='GPU_MAX_HW_QUEUES for this process when the environment does not set it (0: HIP default, '
                          '4; r04 A/B with 8: headline 8.05 vs 7.61 ms, reference job 5.85 vs 5.23 ms)')
@@ -423,7 +428,77 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
     headline = not barcodes and n == 100000 and len(sets) == 50 and args.end_size == 150
     timed_fused = not headline
 
-    def step(k=None, fused=False):
+    # --overlap-steps (schedule 5, headline): two buffer sets (tiles and results) so that step k+1's
+    # tile transposes and step k's end trim run on `aux` while `stream` runs the align phase. Events:
+    # tile_done[s] (set s's tiles written), align_done[s] (its align read them and wrote its results),
+    # trim_done[s] (its end trim read the results).
+    pipelined = args.overlap_steps and args.rest_overlap == 5 and headline
+    pipe = None
+    if pipelined:
+        for sd in sides:
+            sd['d_tiles2'] = dalloc(4 * int(L.pcabi_tile_layout(sd['lens'].ctypes.data_as(vp), n,
+                                                                   np.zeros((n + 255) // 256 + 1, np.int64).ctypes.data_as(vp))))
+            sd['d_res2'] = dalloc(4 * 8 * sd['stride'])
+        pipe = dict(set=0, ahead=False, aux=vp(), regions=[all_regions, _lib.cross_regions(
+            [(sd['d_tiles2'], sd['d_toff'], sd['d_len'], n, int(sd['lens'].max()), sd['all'][0], sd['d_res2'],
+              sd['stride']) for sd in sides if sd['all'][1]])],
+                    res=[(d_sres, d_eres), (sides[0]['d_res2'], sides[1]['d_res2'])],
+                    tiles=[[sd['d_tiles'] for sd in sides], [sd['d_tiles2'] for sd in sides]],
+                    ev={k: [vp(), vp()] for k in ('tile', 'align', 'trim')}, used={k: [False, False] for k in ('tile', 'align', 'trim')})
+        _lib.check(L.pcabi_stream_create(ctypes.byref(pipe['aux'])), 'stream')
+        for k in pipe['ev']:
+            for e_ in pipe['ev'][k]:
+                _lib.check(L.pcabi_event_create(ctypes.byref(e_)), 'event')
+
+    def pipe_record(kind, s_, st):
+        L.pcabi_event_record(pipe['ev'][kind][s_], st)
+        pipe['used'][kind][s_] = True
+
+    def pipe_wait(st, kind, s_):
+        if pipe['used'][kind][s_]:
+            L.pcabi_stream_wait_event(st, pipe['ev'][kind][s_])
+
+    def pipe_tiles(s_):
+        # set s_'s tiles on aux, once the align that last read them is done
+        pipe_wait(pipe['aux'], 'align', s_)
+        for sd, d_t in zip(sides, pipe['tiles'][s_]):
+            _lib.check(L.pcabi_tile_windows_dev(d_codes, sd['d_off'], sd['d_len'], n, sd['d_toff'], sd['mq'], d_t,
+                                                pipe['aux']), 'tile')
+        pipe_record('tile', s_, pipe['aux'])
+
+    def step_pipelined(e, last):
+        s_ = pipe['set']
+        if not pipe['ahead']:
+            pipe_tiles(s_)
+        pipe_wait(stream, 'tile', s_)
+        pipe_wait(stream, 'trim', s_)                # set s_'s results: read by the end trim two steps ago
+        if e[2] is not None:
+            L.pcabi_event_record(e[2], stream)
+        _lib.check(L.pcabi_align_cross_multi_dev(pipe['regions'][s_], len(pipe['regions'][s_]), *sc, stream, e[0], e[1]),
+                   'align')
+        if e[3] is not None:
+            L.pcabi_event_record(e[3], stream)
+        pipe_record('align', s_, stream)
+        # the next step's tiles beside this align, then this step's end trim after it
+        pipe['ahead'] = not last
+        if not last:
+            pipe_tiles(1 - s_)
+        pipe_wait(pipe['aux'], 'align', s_)
+        sres, eres = pipe['res'][s_]
+        _lib.check(L.pcabi_end_trim_dev(sres, s_stride, n_sa, eres, e_stride, n_ea, n, args.end_size,
+                                        2, 75.0, 4, d_st, d_et, None, None, pipe['aux']), 'end_trim')
+        pipe_record('trim', s_, pipe['aux'])
+        pipe['set'] = 1 - s_
+
+    def pipe_sync():
+        if pipe is not None:
+            L.pcabi_stream_sync(pipe['aux'])
+            L.pcabi_stream_sync(stream)
+
+    def step(k=None, fused=False, last=True):
+        if pipe is not None and not fused and (k is not None or not timed_fused):
+            step_pipelined((None,) * 4 if k is None else tuple(ev[4 * k + i] for i in range(4)), last)
+            return
         fused = fused if k is None else timed_fused
         e = (None,) * 4 if k is None else tuple(ev[4 * k + i] for i in range(4))
         if not fused and args.rest_overlap == 5:
@@ -480,9 +555,10 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
     if two_streams:
         for s_ in (stream, stream2):
             L.pcabi_stream_side_streams(s_, args.head_side_streams)
-    for _ in range(args.warmup):
-        step(fused=timed_fused)
+    for w_ in range(args.warmup):
+        step(fused=timed_fused, last=w_ == args.warmup - 1)
     _lib.check(L.pcabi_stream_sync(stream), 'sync')
+    pipe_sync()
 
     def barrier():
         if dist is not None:
@@ -493,8 +569,9 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
     barrier()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(k)
+        step(k, last=k == args.steps - 1)
     L.pcabi_stream_sync(stream)
+    pipe_sync()
     barrier()
     elapsed = time.perf_counter() - t0
     side_timed = args.head_side_streams if two_streams else L.pcabi_set_side_streams(-1)
@@ -599,7 +676,7 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
 
     # the headline's extra streams go before the other configurations run (idle streams still take
     # hardware queues from the ones the library creates later)
-    for st_ in [stream2] + g_streams:
+    for st_ in [stream2] + g_streams + ([pipe['aux']] if pipe is not None else []):
         L.pcabi_stream_destroy(st_)
 
     if rank == 0:
@@ -636,7 +713,10 @@ def run_endtrim(args, rank, world, dist, torch, L, _lib, A, synth, encode_adapte
                        'reads_per_gpu': n, 'adapter_sets': len(sets), 'end_size': args.end_size,
                        'scoring': list(sc), 'parallelism': 'dp%d (read shards)' % world,
                        'hw_queues': os.environ.get('GPU_MAX_HW_QUEUES', 'HIP default'),
-                       'side_streams': side_timed},
+                       'side_streams': side_timed,
+                       'steps_overlap': ('each step\'s tile transposes and end trim on a second stream beside the '
+                                         'neighbouring steps\' align phase (double-buffered tiles and results)'
+                                         if pipe is not None else None)},
             'roofline': {'bound': 'valu', 'achieved': round(tops, 3), 'peak': round(VALU_PEAK_TOPS, 1),
                          'unit': 'Tops/s (int32 lane-ops)', 'frac': round(tops / VALU_PEAK_TOPS, 4),
                          'traffic': prof.get('traffic_bytes_per_launch') if prof and headline else None,
