@@ -173,6 +173,11 @@ int64_t middle_plan_waves() {
     const char *e = std::getenv("PCABI_MIDDLE_PLAN_WAVES");
     return (e && e[0]) ? std::max<int64_t>(1, std::atoll(e)) : 4096;
 }
+// PCABI_CHUNK_GROUP=0 / 1 (A/B): the candidate DP's run-tagged buckets as one grouped launch
+int middle_chunk_group() {
+    const char *e = std::getenv("PCABI_CHUNK_GROUP");
+    return (e && e[0] == '0') ? 0 : 1;
+}
 
 // ---- decision epilogues --------------------------------------------------------------------
 
@@ -3502,6 +3507,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
     std::vector<char> fired(faults.size(), 0);
     int injected[kSlots + 1] = {};                  // per slot: the faults its last queueing injected
     const int64_t target = middle_plan_waves();
+    const int chunk_group = middle_chunk_group();
     const unsigned gn = (unsigned)std::min<int64_t>((n + 255) / 256, kGrid);
     std::vector<int32_t> out;                       // (round, 8 ints) of finished slots
     std::vector<int64_t> out_round;
@@ -3645,9 +3651,42 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
             // (r05y / r05z in-process A/B: two lanes everywhere made the 20 kb scan 0.13 ms faster --
             // most of it the whole reads' 32-column chunks -- and the 8 kb one 0.08-0.09 ms slower)
             p.chunk_split = windows ? 2 : 0;
+            // the run-tagged buckets (<= 28 rows) as one grouped launch (k_align_chunk_group), longest
+            // rows first; the other buckets (and a lone run-tagged one) launch on their own
+            const bool affine_dp = scr.go != scr.ge;
+            ChunkGroupParams cg{};
+            std::vector<int> singles;
+            for (int k = n_bk - 1; k >= 0; --k) {
+                const int b = used[k];
+                const bool tg = bucket_pack_mode(b, adps->lens[b], scr) == 2;
+                if (chunk_group && p.chunk_split == 0 && affine_dp && tg && kBuckets[b].kind == FAST &&
+                    kBuckets[b].rpl <= kChunkGroupRpl && cg.n_seg < kMaxChunkSegs) {
+                    ChunkSeg &sg = cg.seg[cg.n_seg++];
+                    sg.adp_pad = adps->pad[b];
+                    sg.adp_len = adps->len[b];
+                    sg.adp_id = adps->id[b];
+                    sg.dev_waves = pl.bk_waves + 2 * k;
+                    sg.n_adp = adps->count[b];
+                    sg.rpl = kBuckets[b].rpl;
+                } else {
+                    singles.push_back(k);
+                }
+            }
+            if (cg.n_seg == 1) {                         // a lone bucket: its own launch, as before
+                for (int k = 0; k < n_bk; ++k)
+                    if (pl.bk_waves + 2 * k == cg.seg[0].dev_waves) singles.push_back(k);
+                cg.n_seg = 0;
+            }
+            std::sort(singles.begin(), singles.end());
+            const size_t n_launch = singles.size() + (cg.n_seg ? 1 : 0);
             ForkJoin fj;
-            if (int rc = fj.begin(st, round_base + r >= dp_serial_from ? 1 : used.size())) return rc;
-            for (int k = 0; k < n_bk; ++k) {
+            if (int rc = fj.begin(st, round_base + r >= dp_serial_from ? 1 : n_launch)) return rc;
+            size_t li = 0;
+            if (cg.n_seg) {
+                cg.p = p;
+                dispatch_chunk_group(cg, 4 * (unsigned)p.n_waves, fj.at(li++));
+            }
+            for (int k : singles) {
                 const int b = used[k];
                 p.adp_pad = adps->pad[b];
                 p.adp_len = adps->len[b];
@@ -3655,7 +3694,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
                 p.n_adp = adps->count[b];
                 p.rt = adps->rt[b];
                 p.dev_waves = pl.bk_waves + 2 * k;
-                if (int rc = dispatch_chunk(b, p, scr.go != scr.ge, fj.at(k), bucket_pack_mode(b, adps->lens[b], scr) == 2)) {
+                if (int rc = dispatch_chunk(b, p, affine_dp, fj.at(li++), bucket_pack_mode(b, adps->lens[b], scr) == 2)) {
                     (void)fj.end();
                     return rc;
                 }
@@ -3800,7 +3839,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
         std::vector<int64_t> key = {(int64_t)round_base, (int64_t)(intptr_t)codes, (int64_t)(intptr_t)win_off,
                                     (int64_t)(intptr_t)win_len, n, windows ? 1 : 0, (int64_t)(threshold * 1e6),
                                     scr.ma, scr.mi, scr.go, scr.ge, (int64_t)adps->serial, sc->q_slots_cap,
-                                    sc->shadow_cap, (int64_t)(intptr_t)sc->shadow.p, target,
+                                    sc->shadow_cap, (int64_t)(intptr_t)sc->shadow.p, target, chunk_group,
                                     (int64_t)g_buf_gen.load()};
         auto &g = sc->graphs[r & 31];
         if (g.exec && g.key == key) {

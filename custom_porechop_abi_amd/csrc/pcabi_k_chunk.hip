@@ -4,6 +4,41 @@
 
 namespace pcabi_eng {
 
+// pcabi_kern.h "grouped candidate-DP launches". PCABI_CG_WAVES (build macro, A/B variants): the
+// launch's minimum waves per SIMD (5: <= 96 VGPRs, a few dwords spilled outside the column loop)
+#ifndef PCABI_CG_WAVES
+#define PCABI_CG_WAVES 5
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PCABI_CG_WAVES))) void k_align_chunk_group(ChunkGroupParams gp) {
+    __shared__ __attribute__((aligned(16))) int32_t tab[wave_tab_ints<TAGGED, kChunkGroupRpl>()];
+    for (int64_t g = blockIdx.x;; g += gridDim.x) {     // block-uniform (one wave per block)
+        int s = 0;
+        int64_t base = 0;
+        for (; s < gp.n_seg; ++s) {
+            const int64_t nw = gp.seg[s].dev_waves[1];
+            if (g < base + nw) break;
+            base += nw;
+        }
+        if (s == gp.n_seg) return;
+        const ChunkSeg &sg = gp.seg[s];
+        KParams p = gp.p;
+        p.adp_pad = sg.adp_pad;
+        p.adp_len = sg.adp_len;
+        p.adp_id = sg.adp_id;
+        p.n_adp = sg.n_adp;
+        const int64_t wave = sg.dev_waves[0] + (g - base);
+        switch (sg.rpl) {
+#define C(R) case R: chunk_wave<R, true, TAGGED>(p, wave, true, tab); break;
+        C(4) C(8) C(12) C(16) C(20) C(24) C(28)
+#undef C
+        }
+    }
+}
+
+void dispatch_chunk_group(const ChunkGroupParams &gp, unsigned blocks, hipStream_t st) {
+    if (gp.n_seg > 0) hipLaunchKernelGGL(k_align_chunk_group, dim3(blocks), dim3(64), 0, st, gp);
+}
+
 int dispatch_chunk(int b, const KParams &p, bool affine, hipStream_t st, bool tagged) {
     // planned on the device: n_waves is the grid (blocks striding over the device wave count)
     const dim3 grid((unsigned)(p.dev_waves ? p.n_waves : (p.n_waves + 3) / 4));

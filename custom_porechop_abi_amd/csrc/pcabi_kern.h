@@ -741,6 +741,30 @@ inline int group_class(int rpl, int pack_mode, bool affine) {
 }
 void dispatch_group(int cls, const GroupParams &p, int64_t blocks, hipStream_t st);
 
+// ---- grouped candidate-DP launches (pcabi_k_chunk.hip) ----------------------------------------
+// The run-tagged chunk buckets (<= 28 rows: the 32-row case alone sets 101 VGPRs, 4 waves per SIMD;
+// up to 28 the group holds 5) of one device plan in ONE launch: one-wave blocks
+// stride over the buckets' device-planned waves back to back (each bucket's (first wave, waves) on
+// the device), the bucket found by a scalar walk, its core by a wave-uniform switch -- so the
+// buckets' waves share the SIMDs instead of running as separate launches (side by side in round 1,
+// one after the other in the serial later rounds). The common task arrays stay in `p`.
+constexpr int kMaxChunkSegs = 8;
+constexpr int kChunkGroupRpl = 28;
+struct ChunkSeg {
+    const uint32_t *adp_pad;
+    const int32_t *adp_len;
+    const int32_t *adp_id;
+    const int32_t *dev_waves;  // the bucket's (first wave, waves) from the device plan
+    int32_t n_adp;
+    int32_t rpl;
+};
+struct ChunkGroupParams {
+    KParams p;
+    ChunkSeg seg[kMaxChunkSegs];
+    int32_t n_seg;
+};
+void dispatch_chunk_group(const ChunkGroupParams &gp, unsigned blocks, hipStream_t st);
+
 // ---- kernel translation units (pcabi_k_*.hip) ----------------------------------------------
 // k_align launches by core, grid as k_align expects (cross: XCD-ordered tiles x adapters;
 // pairs: ceil(waves / 4) blocks).
