@@ -173,11 +173,7 @@ int64_t middle_plan_waves() {
     const char *e = std::getenv("PCABI_MIDDLE_PLAN_WAVES");
     return (e && e[0]) ? std::max<int64_t>(1, std::atoll(e)) : 4096;
 }
-// PCABI_CHUNK_GROUP=0 / 1 (A/B): the candidate DP's run-tagged buckets as one grouped launch
-int middle_chunk_group() {
-    const char *e = std::getenv("PCABI_CHUNK_GROUP");
-    return (e && e[0] == '0') ? 0 : 1;
-}
+
 
 // ---- decision epilogues --------------------------------------------------------------------
 
@@ -3507,7 +3503,6 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
     std::vector<char> fired(faults.size(), 0);
     int injected[kSlots + 1] = {};                  // per slot: the faults its last queueing injected
     const int64_t target = middle_plan_waves();
-    const int chunk_group = middle_chunk_group();
     const unsigned gn = (unsigned)std::min<int64_t>((n + 255) / 256, kGrid);
     std::vector<int32_t> out;                       // (round, 8 ints) of finished slots
     std::vector<int64_t> out_round;
@@ -3659,7 +3654,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
             for (int k = n_bk - 1; k >= 0; --k) {
                 const int b = used[k];
                 const bool tg = bucket_pack_mode(b, adps->lens[b], scr) == 2;
-                if (chunk_group && p.chunk_split == 0 && affine_dp && tg && kBuckets[b].kind == FAST &&
+                if (p.chunk_split == 0 && affine_dp && tg && kBuckets[b].kind == FAST &&
                     kBuckets[b].rpl <= kChunkGroupRpl && cg.n_seg < kMaxChunkSegs) {
                     ChunkSeg &sg = cg.seg[cg.n_seg++];
                     sg.adp_pad = adps->pad[b];
@@ -3839,7 +3834,7 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
         std::vector<int64_t> key = {(int64_t)round_base, (int64_t)(intptr_t)codes, (int64_t)(intptr_t)win_off,
                                     (int64_t)(intptr_t)win_len, n, windows ? 1 : 0, (int64_t)(threshold * 1e6),
                                     scr.ma, scr.mi, scr.go, scr.ge, (int64_t)adps->serial, sc->q_slots_cap,
-                                    sc->shadow_cap, (int64_t)(intptr_t)sc->shadow.p, target, chunk_group,
+                                    sc->shadow_cap, (int64_t)(intptr_t)sc->shadow.p, target,
                                     (int64_t)g_buf_gen.load()};
         auto &g = sc->graphs[r & 31];
         if (g.exec && g.key == key) {
