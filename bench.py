@@ -784,7 +784,7 @@ def run_other_configs(args, ctx):
         # the CLI path file to file (parse + trim + middle + write), 25k reads
         # 100k reads = 8 batches of 12.5k per step: the parse / device / write pipeline at its
         # steady state (r04 timed 2 batches per step, which never fills it)
-        ('e2e', lambda: run_e2e(sub(workload='e2e', reads=100000, steps=2, warmup=1), rank, 1, None, torch, L, _lib, A,
+        ('e2e', lambda: run_e2e(sub(workload='e2e', reads=100000, steps=4, warmup=1), rank, 1, None, torch, L, _lib, A,
                                 synth, encode_adapters)),
         # SURVEY §8(f) 3 and 4
         ('compat', lambda: run_compat(sub(workload='compat', cpu_sample=args.cpu_sample // 4), rank, 1, None, torch,
