@@ -3689,9 +3689,18 @@ int64_t middle_device_rounds(pcabi_scan *sc, const uint8_t *codes, const int64_t
                 p.n_adp = adps->count[b];
                 p.rt = adps->rt[b];
                 p.dev_waves = pl.bk_waves + 2 * k;
-                if (int rc = dispatch_chunk(b, p, affine_dp, fj.at(li++), bucket_pack_mode(b, adps->lens[b], scr) == 2)) {
+                // the packed buckets (36+ rows) of the whole-read rounds on the row-split core, two
+                // lanes per chunk task (r06: 8 kb middle scan 1.74-1.86 -> 1.71-1.75 ms; their
+                // one-lane waves hold 109-132 VGPRs, 3-4 waves per SIMD)
+                const int split_keep = p.chunk_split;
+                if (p.chunk_split == 0 && bucket_pack_mode(b, adps->lens[b], scr) != 2 && kBuckets[b].kind == FAST &&
+                    kBuckets[b].rpl >= 36)
+                    p.chunk_split = 2;
+                const int rc_d = dispatch_chunk(b, p, affine_dp, fj.at(li++), bucket_pack_mode(b, adps->lens[b], scr) == 2);
+                p.chunk_split = split_keep;
+                if (rc_d) {
                     (void)fj.end();
-                    return rc;
+                    return rc_d;
                 }
             }
             if (int rc = fj.end()) return rc;
